@@ -1,0 +1,189 @@
+"""Server aggregation rules / robust defenses on the gathered update matrix ``U [N, P]``.
+
+Each rule returns ``AggResult(params [P] | None, ok, info)``.  Rows are in client-index order;
+``sizes [N]`` are the clients' reported sample counts; ``attackers [N]`` the oracle attacker flags
+(only GMM uses them, as the reference does).  Reference sites:
+
+* fedavg        ``server.py:751-775``      size-weighted mean (fp64 accumulation)
+* trimmed_mean  ``src/Utils.py:267-302``   coordinate-wise, trim int(0.1·N) per side
+* median        ``src/Utils.py:344-357``   coordinate-wise lower median (``torch.median``)
+* krum          ``server.py:373-389``, ``src/Utils.py:326-342``  f = int(N·0.0) (A-11)
+* shieldfl      ``server.py:306-350``      cosine-to-mean inverse-deviation weights
+* gmm           ``server.py:352-372``, ``src/Utils.py:250-323``  (crashes in the reference, A-8;
+  here: 2-component GMM in the rank-(N-1) principal subspace = low-rank Mahalanobis)
+* scionfl       ``server.py:436-492``, ``src/Utils.py:371-387``  1-bit stochastic quantisation +
+  norm clip + cosine filter + FedAvg of the kept originals
+* fltracer      ``src/Utils.py:359-369`` (dormant in the reference)  PCA(1) + MAD z-score
+* byzantine     ``src/Utils.py:218-248`` (dead code in the reference) cosine ≥ 0.9 to model 0
+FLTrust and the hypernetwork live in ``fl/server.py`` (they need training).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..utils.log import print_with_color
+
+
+@dataclass
+class AggResult:
+    params: Optional[torch.Tensor]
+    ok: bool = True
+    info: Dict = field(default_factory=dict)
+
+
+def fedavg(U: torch.Tensor, sizes: torch.Tensor, **_) -> AggResult:
+    if U.shape[0] == 0:
+        return AggResult(None, True, {"n": 0})
+    return AggResult(ops.fedavg(U, sizes), True, {"n": int(U.shape[0])})
+
+
+def mean_of(U: torch.Tensor) -> torch.Tensor:
+    w = torch.full((U.shape[0],), 1.0 / U.shape[0], dtype=torch.float64)
+    return ops.weighted_rows(U, w)
+
+
+def trimmed_mean(U: torch.Tensor, sizes=None, trim_ratio: float = 0.1, **_) -> AggResult:
+    n = U.shape[0]
+    k = int(n * trim_ratio)
+    if 2 * k >= n:
+        raise ValueError("Too few clients for the chosen trim_ratio.")
+    return AggResult(ops.trimmed_mean(U, k), True, {"trim_k": k})
+
+
+def median(U: torch.Tensor, sizes=None, **_) -> AggResult:
+    return AggResult(ops.coord_median(U), True, {})
+
+
+def krum(U: torch.Tensor, sizes=None, f_rate: float = 0.0, **_) -> AggResult:
+    n = U.shape[0]
+    f = int(n * f_rate)
+    d2 = ops.pairwise_sqdist(U).double().cpu()
+    m = n - f - 2
+    scores = []
+    for i in range(n):
+        row = torch.cat([d2[i, :i], d2[i, i + 1:]])
+        closest = torch.sort(row).values[:max(m, 0)]
+        scores.append(float(closest.sum().item()))
+    sel = int(np.argmin(scores))
+    return AggResult(U[sel].clone(), True, {"selected": sel, "f": f, "scores": scores})
+
+
+def shieldfl(U: torch.Tensor, sizes=None, **_) -> AggResult:
+    norms = ops.row_norms(U).to(U.device)
+    Un = U / (norms.to(U.dtype)[:, None] + 1e-8)
+    ref = mean_of(Un)
+    cos = ops.cosine_to(Un, ref, eps=1e-8).float().cpu()
+    dev = 1.0 - cos
+    w = 1.0 / (dev + 1e-6)
+    w = w / w.sum()
+    return AggResult(ops.weighted_rows(U, w.double()), True, {"weights": w.tolist(), "cos": cos.tolist()})
+
+
+def _pca_project(U: torch.Tensor, r: int) -> np.ndarray:
+    X = U.double()
+    Xc = X - X.mean(dim=0, keepdim=True)
+    # thin SVD through the N x N Gram (N <= a few hundred): never forms a P x P matrix
+    Gm = (Xc @ Xc.t()).cpu().numpy()
+    evals, evecs = np.linalg.eigh(Gm)
+    order = np.argsort(evals)[::-1][:r]
+    evals = np.clip(evals[order], 1e-30, None)
+    # scores = Xc V = U_svd * S  ->  evecs * sqrt(evals)
+    return evecs[:, order] * np.sqrt(evals)[None, :]
+
+
+def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, seed: int = 0, **_) -> AggResult:
+    """Low-rank GMM filter (reference intent; the reference itself crashes, A-8)."""
+    from sklearn.mixture import GaussianMixture
+
+    n = U.shape[0]
+    att = attackers.bool().cpu().numpy() if attackers is not None else np.zeros(n, bool)
+    r = max(1, min(n - 1, 8))
+    Z = _pca_project(U, r)
+    benign = Z[~att]
+    mal = Z[att]
+    allz = np.vstack([benign, mal]) if len(mal) else benign
+    ncomp = 2 if allz.shape[0] >= 2 else 1
+    g = GaussianMixture(n_components=ncomp, covariance_type="full", random_state=seed, reg_covar=1e-6).fit(allz)
+
+    def md(x, k):
+        d = x - g.means_[k]
+        return float(np.sqrt(d @ np.linalg.inv(g.covariances_[k]) @ d))
+
+    thr = 3 * np.std([md(x, 0) for x in benign]) if len(benign) else np.inf
+    keep = []
+    for i in range(n):
+        k = int(np.argmax(g.predict_proba(Z[i:i + 1])[0]))
+        if md(Z[i], k) <= thr:
+            keep.append(i)
+    if not keep:
+        return AggResult(None, False, {"kept": []})
+    return AggResult(mean_of(U[keep]), True, {"kept": keep, "threshold": float(thr)})
+
+
+def scionfl(U: torch.Tensor, sizes: torch.Tensor, seed: int = 0, **_) -> AggResult:
+    n = U.shape[0]
+    sigma, smin, smax = ops.stochastic_quantize(U, seed)
+    smin = smin.double().cpu()
+    smax = smax.double().cpu()
+    ones = sigma.double().sum(dim=1).cpu()
+    zeros = U.shape[1] - ones
+    l2 = torch.sqrt(zeros * smin ** 2 + ones * smax ** 2)
+    l2_avg = float(l2.mean())
+    MU, TOPK = 3.0, 0.5
+    for i in range(n):
+        if l2[i] > MU * l2_avg:
+            f = (MU * l2_avg) / float(l2[i])
+            smin[i] *= f
+            smax[i] *= f
+    deq = smin.to(U.device)[:, None].to(U.dtype) + sigma * (smax - smin).to(U.device)[:, None].to(U.dtype)
+    agg = mean_of(deq)
+    cosd = (1.0 - ops.cosine_to(deq, agg, eps=1e-8)).cpu()
+    scores = cosd.tolist()
+    thr = sorted(scores, reverse=True)[int(TOPK * n)] if n > 0 else 0.0
+    keep = [i for i, s in enumerate(scores) if s > thr]
+    if not keep:
+        print_with_color("[Warning] ScionFL kept no client (reference would crash); using all clients", "yellow")
+        keep = list(range(n))
+    kept_sizes = sizes[keep]
+    return AggResult(ops.fedavg(U[keep], kept_sizes), True, {"kept": keep, "scores": scores, "threshold": thr})
+
+
+def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) -> AggResult:
+    from scipy.stats import median_abs_deviation
+
+    z = _pca_project(U, 1)[:, 0]
+    mad = median_abs_deviation(z)
+    med = np.median(z)
+    scores = np.abs(z - med) / (1.4826 * mad + 1e-6)
+    bad = set(np.where(scores > threshold)[0].tolist())
+    keep = [i for i in range(U.shape[0]) if i not in bad]
+    if not keep:
+        keep = list(range(U.shape[0]))
+    return AggResult(ops.fedavg(U[keep], sizes[keep]), True, {"anomalies": sorted(bad)})
+
+
+def byzantine(U: torch.Tensor, sizes=None, threshold: float = 0.9, **_) -> AggResult:
+    cos = ops.cosine_to(U, U[0], eps=1e-8).cpu()
+    keep = [i for i in range(U.shape[0]) if float(cos[i]) >= threshold]
+    if not keep:
+        print_with_color("[Warning] No model passed the similarity threshold. Using fallback.", "yellow")
+        keep = list(range(U.shape[0]))
+    return AggResult(mean_of(U[keep]), True, {"kept": keep})
+
+
+AGGREGATORS = {
+    "fedavg": fedavg,
+    "trimmed_mean": trimmed_mean,
+    "median": median,
+    "krum": krum,
+    "shieldfl": shieldfl,
+    "gmm": gmm,
+    "scionfl": scionfl,
+    "fltracer": fltracer,
+    "byzantine": byzantine,
+}

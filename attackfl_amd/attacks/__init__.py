@@ -1,0 +1,253 @@
+"""Model-poisoning attacks on flat update matrices.
+
+All attacks take the attacker's received genuine models as ONE matrix ``G [K, P]`` (rows in the
+order the server sampled them) plus the attacker's own current model ``own [P]`` and return
+``(ok, malicious [P])``.  Reference semantics (``src/Utils.py:30-214``,
+dispatch ``src/RpcClient.py:119-145``) are kept, including the quirks that define the
+effective attack:
+
+* A-6  distances are ``sum_k ||Δ_k||_2`` per state_dict tensor with the *spectral* norm for 2-D
+  tensors (``torch.linalg.norm(ord=2)``).  ``distance='flat'`` switches to the whole-vector L2
+  (the Gram-matrix form).  For ≥3-D tensors (CNN convs, where the reference raises) the
+  spectral mode uses the ``[out, in*k]`` matricisation — flagged in ``DEVIATIONS``.
+* A-7  candidates are written into ``G[0]`` (alias), so the acceptance test sees a zero
+  self-distance for row 0, and the bisection returns the *last tried* candidate.
+* unbiased std (``torch.std`` default); ``K <= 1`` returns the attacker's own model for the
+  bisection attacks, while LIE with ``K == 1`` yields NaN exactly like the reference.
+
+The bisection itself (``_bisect``) only needs, per iteration, the K distances of one
+candidate.  In flat mode every distance is ``sqrt(A_j - 2γB_j + γ²C)`` with coefficients from
+one pass over ``[K, P]`` (``ops.attack_coeffs``, a HIP kernel on GPU), so the loop is host
+scalar math.  In spectral mode vector-shaped tensors use the same closed form per tensor and
+matrix-shaped tensors use a batched σ_max (``ops.batched_spectral_norm``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..models import ParamLayout
+from ..utils.log import print_with_color
+from .. import ops
+
+DEVIATIONS = {
+    "spectral_3d": "reference torch.linalg.norm(ord=2) raises on 3-D conv weights (A-6); we matricise to [out, -1]",
+}
+
+
+@dataclass
+class ColumnStats:
+    mean: torch.Tensor
+    std: torch.Tensor
+    sign: torch.Tensor
+
+
+def column_stats(G: torch.Tensor) -> ColumnStats:
+    """Per-coordinate mean, unbiased std and sign(mean) over the K genuine rows."""
+    mean, std = ops.column_mean_std(G)
+    return ColumnStats(mean, std, torch.sign(mean))
+
+
+# ----------------------------------------------------------------------------------------------
+# distances
+# ----------------------------------------------------------------------------------------------
+
+class DistanceEngine:
+    """Sum over tensors of per-tensor norms of (x - G_j), batched over rows j."""
+
+    def __init__(self, layout: ParamLayout, mode: str = "spectral"):
+        if mode not in ("spectral", "flat"):
+            raise ValueError(mode)
+        self.layout = layout
+        self.mode = mode
+        self.vec_slots = [s for s in layout.slots if len(s.shape) <= 1] if mode == "spectral" else []
+        self.mat_slots = [s for s in layout.slots if len(s.shape) >= 2] if mode == "spectral" else []
+
+    # pairwise among rows of G: returns [K, K] distance matrix
+    def pairwise(self, G: torch.Tensor) -> torch.Tensor:
+        K = G.shape[0]
+        if self.mode == "flat":
+            return ops.pairwise_l2(G)
+        D = torch.zeros(K, K, dtype=torch.float64, device=G.device)
+        if K < 2:
+            return D
+        iu = torch.triu_indices(K, K, offset=1, device=G.device)
+        diffs = G[iu[0]] - G[iu[1]]                      # [M, P]
+        d = self.rowwise_norm_sum(diffs)                  # [M]
+        D[iu[0], iu[1]] = d
+        D[iu[1], iu[0]] = d
+        return D
+
+    def rowwise_norm_sum(self, diffs: torch.Tensor) -> torch.Tensor:
+        """sum_k ||diffs[m, slot_k]|| for every row m -> [M] float64."""
+        if self.mode == "flat":
+            return torch.linalg.vector_norm(diffs.double(), dim=1)
+        out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
+        if self.vec_slots:
+            out += ops.segment_l2_sum(diffs, self.vec_slots)
+        for s in self.mat_slots:
+            r = s.shape[0]
+            mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], r, -1)
+            out += ops.batched_spectral_norm(mats).double()
+        return out
+
+    def to_rows(self, x: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
+        return self.rowwise_norm_sum(x[None, :] - G)
+
+
+def compute_distance(sd1: Dict[str, torch.Tensor], sd2: Dict[str, torch.Tensor], p: int = 2) -> float:
+    """Reference ``compute_distance`` on two state_dicts (used by parity tests)."""
+    total = 0.0
+    for k in sd1.keys():
+        if k in sd2:
+            diff = sd1[k] - sd2[k]
+            if diff.dim() >= 3:
+                diff = diff.reshape(diff.shape[0], -1)
+            total += torch.linalg.norm(diff, ord=p).item()
+    return total
+
+
+# ----------------------------------------------------------------------------------------------
+# bisection (Min-Max / Min-Sum / Opt-Fang)
+# ----------------------------------------------------------------------------------------------
+
+class _CandidateDistances:
+    """d(c(γ), G_j) for c(γ) = mean - γ·dev, j = 0..K-1 (row 0 aliased to the candidate)."""
+
+    def __init__(self, engine: DistanceEngine, G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor):
+        self.engine = engine
+        self.G = G
+        self.mean = mean
+        self.dev = dev
+        K = G.shape[0]
+        if engine.mode == "flat":
+            # ||m - g_j - γ d||^2 = A_j - 2γ B_j + γ^2 C  (all rows at once, one pass over [K, P])
+            self.A, self.B, self.C = ops.attack_coeffs(G, mean, dev)
+        else:
+            self.vec = engine.vec_slots
+            if self.vec:
+                self.A, self.B, self.C = ops.attack_coeffs_segments(G, mean, dev, self.vec)  # [K,S],[K,S],[S]
+
+    def __call__(self, gamma: float) -> torch.Tensor:
+        K = self.G.shape[0]
+        if self.engine.mode == "flat":
+            q = (self.A - 2.0 * gamma * self.B + gamma * gamma * self.C).clamp_min(0.0)
+            d = torch.sqrt(q)
+        else:
+            d = torch.zeros(K, dtype=torch.float64, device=self.G.device)
+            if self.vec:
+                q = (self.A - 2.0 * gamma * self.B + gamma * gamma * self.C[None, :]).clamp_min(0.0)
+                d = d + torch.sqrt(q).sum(dim=1)
+            if self.engine.mat_slots and K > 1:
+                cand = self.mean - gamma * self.dev
+                diffs = cand[None, :] - self.G[1:]
+                dm = torch.zeros(K, dtype=torch.float64, device=self.G.device)
+                for s in self.engine.mat_slots:
+                    mats = diffs[:, s.offset:s.offset + s.numel].reshape(K - 1, s.shape[0], -1)
+                    dm[1:] += ops.batched_spectral_norm(mats).double()
+                d = d + dm
+        d = d.clone()
+        d[0] = 0.0  # A-7: row 0 *is* the candidate
+        return d
+
+
+def _bisect(accept: Callable[[float], bool], gamma: float = 50.0, tau: float = 1.0) -> Tuple[float, int, float]:
+    """Reference bisection: returns (last tried γ, iterations, last accepted γ)."""
+    step = gamma
+    gamma_succ = 0.0
+    last = gamma
+    it = 0
+    while abs(gamma_succ - gamma) > tau:
+        last = gamma
+        it += 1
+        if accept(gamma):
+            gamma_succ = gamma
+            gamma = gamma + step / 2
+        else:
+            gamma = gamma - step / 2
+        step = step / 2
+    return last, it, gamma_succ
+
+
+@dataclass
+class AttackResult:
+    ok: bool
+    params: Optional[torch.Tensor]
+    info: Dict[str, float]
+
+
+def _minmax_family(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine, kind: str, gamma: float = 50.0,
+                   tau: float = 1.0) -> AttackResult:
+    K = G.shape[0]
+    if K <= 1:
+        return AttackResult(True, own.clone(), {"gamma": 0.0, "iters": 0})
+    st = column_stats(G)
+    dev = st.sign if kind == "fang" else st.std
+    D = engine.pairwise(G)
+    if kind == "sum":
+        threshold = float((D ** 2).sum(dim=1).max().item())
+    else:
+        threshold = float(D.max().item())
+    cand_d = _CandidateDistances(engine, G, st.mean, dev)
+
+    def accept(g: float) -> bool:
+        d = cand_d(g)
+        if kind == "sum":
+            return float((d ** 2).sum().item()) < threshold
+        return float(d.max().item()) < threshold
+
+    last, iters, succ = _bisect(accept, gamma, tau)
+    mal = st.mean - last * dev
+    return AttackResult(True, mal, {"gamma": last, "gamma_succ": succ, "iters": iters, "threshold": threshold})
+
+
+def min_max(G, own, engine, **kw) -> AttackResult:
+    return _minmax_family(G, own, engine, "max", **kw)
+
+
+def min_sum(G, own, engine, **kw) -> AttackResult:
+    return _minmax_family(G, own, engine, "sum", **kw)
+
+
+def opt_fang(G, own, engine, **kw) -> AttackResult:
+    return _minmax_family(G, own, engine, "fang", **kw)
+
+
+def lie(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine = None, scaling_factor: float = 0.74) -> AttackResult:
+    """Little-Is-Enough: mean + z·std (reference ``create_LIE_state_dict``)."""
+    return AttackResult(True, ops.lie_candidate(G, float(scaling_factor)), {"z": float(scaling_factor)})
+
+
+def random_noise(own: torch.Tensor, perturbation: float, generator: Optional[torch.Generator] = None) -> AttackResult:
+    """Random: own + N(0,1)·σ (reference ``create_random_base_model``)."""
+    noise = torch.randn(own.shape, generator=generator, device=own.device, dtype=own.dtype) if generator is not None \
+        else torch.randn_like(own)
+    return AttackResult(True, own + noise * float(perturbation), {"sigma": float(perturbation)})
+
+
+def run_attack(mode: str, args: Sequence[float], own: torch.Tensor, G: Optional[torch.Tensor], engine: DistanceEngine,
+               generator: Optional[torch.Generator] = None) -> AttackResult:
+    """Dispatch by the reference's ``--attack_mode`` names."""
+    if mode == "Random":
+        sigma = args[0] if args else 1e6
+        return random_noise(own, sigma, generator)
+    if G is None or G.shape[0] == 0:
+        raise ValueError("attack needs genuine models")
+    if mode == "Min-Max":
+        return min_max(G, own, engine)
+    if mode == "Min-Sum":
+        return min_sum(G, own, engine)
+    if mode == "Opt-Fang":
+        return opt_fang(G, own, engine)
+    if mode == "LIE":
+        z = args[0] if args else 0.74
+        if G.shape[0] == 1:
+            print_with_color("[Warning] LIE with a single genuine model: unbiased std is NaN (reference behaviour)",
+                             "yellow")
+        return lie(G, own, engine, z)
+    raise ValueError(f"Attack client not contain '{mode}' algorithm.")
+
+
+ATTACKS = ("Random", "Min-Max", "Min-Sum", "Opt-Fang", "LIE")

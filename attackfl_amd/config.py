@@ -1,0 +1,231 @@
+"""Typed ``config.yaml`` schema.
+
+Same keys and defaults as the reference ``config.yaml:1-38`` (read at ``server.py:55-89``,
+``client.py:42-48``).  Every reference key is accepted unchanged; the ``rabbit:`` section is
+parsed and ignored (there is no broker: transport is RCCL / gloo, see ``parallel/comm.py``).
+
+Extensions (all optional, defaults keep reference behaviour):
+
+``comm:``
+  backend: auto | nccl | gloo | loopback
+  clients-per-rank: int (packed launcher; 0 = clients / world)
+  one-shot-allgather: bool  (IPC xGMI all-gather for small updates on a single node)
+  timeout-s: collective timeout (failure detection)
+  attackers: {client_index: {mode, round, args}}  (launcher-side attack assignment)
+``data:``
+  synthetic: auto | true | false   (auto = use the reference pickles when present)
+  train-size / test-size / seed / har-train-size / har-test-size
+``engine:``
+  trainer: auto | fused | eager     (fused = HIP persistent training kernel)
+  distance: spectral | flat         (attack distance; spectral = reference ``torch.linalg.norm(ord=2)``)
+  seed: int                         (torch / client RNG seed; the reference seeds only ``random``)
+  metrics: path of the JSONL metrics file ('' disables)
+  checkpoint-dir: where ``*.pth`` files go (reference: CWD)
+  compat-hyper-resume: bool         (True = reproduce reference A-5: a loaded hyper checkpoint is discarded)
+"""
+from __future__ import annotations
+
+import copy
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import yaml
+
+SERVER_MODES = ("fedavg", "hyper", "FLTrust", "trimmed_mean", "shieldfl", "gmm", "krum", "median", "scionfl",
+                "fltracer", "byzantine")
+ATTACK_MODES = ("Random", "Min-Max", "Min-Sum", "Opt-Fang", "LIE")
+MODEL_NAMES = ("CNNModel", "RNNModel", "TransformerModel", "TransformerClassifier")
+DATA_NAMES = ("ICU", "HAR", "CIFAR10")
+
+REFERENCE_DEFAULTS: Dict[str, Any] = {
+    "name": "Federated Learning poisoning attack testbed",
+    "server": {
+        "num-round": 30,
+        "clients": 3,
+        "mode": "hyper",
+        "hyper-detection": {"enable": False, "cosine-search": 10, "n_components": 3, "eps": 0.007,
+                            "min_samples": 3},
+        "model": "TransformerModel",
+        "data-name": "ICU",
+        "parameters": {"load": False},
+        "validation": True,
+        "data-distribution": {"num-data-range": [12000, 15000]},
+        "genuine-rate": 0.5,
+        "random-seed": 1,
+    },
+    "rabbit": {"address": "192.0.0.1", "username": "admin", "password": "admin"},
+    "log_path": ".",
+    "learning": {"epoch": 5, "learning-rate": 0.004, "hyper-lr": 0.001, "momentum": 0.5, "batch-size": 128,
+                 "clip-grad-norm": 1.0},
+}
+
+EXTENSION_DEFAULTS: Dict[str, Any] = {
+    "comm": {"backend": "auto", "clients-per-rank": 0, "one-shot-allgather": False, "timeout-s": 600,
+             "attackers": {}},
+    "data": {"synthetic": "auto", "train-size": 60000, "test-size": 10000, "seed": 1234,
+             "har-train-size": 2048, "har-test-size": 512, "root": "."},
+    "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
+               "compat-hyper-resume": False},
+}
+
+
+def _deep_merge(base: Dict[str, Any], over: Dict[str, Any]) -> Dict[str, Any]:
+    out = copy.deepcopy(base)
+    for k, v in (over or {}).items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = _deep_merge(out[k], v)
+        else:
+            out[k] = copy.deepcopy(v)
+    return out
+
+
+@dataclass
+class AttackSpec:
+    mode: str
+    round: int
+    args: List[float] = field(default_factory=list)
+
+    def __post_init__(self):
+        if self.mode not in ATTACK_MODES:
+            raise ValueError(f"Attack mode '{self.mode}' is not valid (choose from {ATTACK_MODES}).")
+        self.round = int(self.round)
+        self.args = [float(a) for a in (self.args or [])]
+
+
+@dataclass
+class Config:
+    raw: Dict[str, Any]
+
+    # ---- server ----
+    @property
+    def num_round(self) -> int:
+        return int(self.raw["server"]["num-round"])
+
+    @property
+    def clients(self) -> int:
+        return int(self.raw["server"]["clients"])
+
+    @property
+    def mode(self) -> str:
+        return str(self.raw["server"]["mode"])
+
+    @property
+    def model(self) -> str:
+        return str(self.raw["server"]["model"])
+
+    @property
+    def data_name(self) -> str:
+        return str(self.raw["server"]["data-name"])
+
+    @property
+    def load_parameters(self) -> bool:
+        return bool(self.raw["server"]["parameters"]["load"])
+
+    @property
+    def validation(self) -> bool:
+        return bool(self.raw["server"]["validation"])
+
+    @property
+    def data_range(self) -> List[int]:
+        r = self.raw["server"]["data-distribution"]["num-data-range"]
+        return [int(r[0]), int(r[1])]
+
+    @property
+    def genuine_rate(self) -> float:
+        return float(self.raw["server"]["genuine-rate"])
+
+    @property
+    def random_seed(self):
+        return self.raw["server"]["random-seed"]
+
+    @property
+    def hyper_detection(self) -> Dict[str, Any]:
+        return self.raw["server"]["hyper-detection"]
+
+    # ---- learning ----
+    @property
+    def epoch(self) -> int:
+        return int(self.raw["learning"]["epoch"])
+
+    @property
+    def batch_size(self) -> int:
+        return int(self.raw["learning"]["batch-size"])
+
+    @property
+    def lr(self) -> float:
+        return float(self.raw["learning"]["learning-rate"])
+
+    @property
+    def hyper_lr(self) -> float:
+        return float(self.raw["learning"]["hyper-lr"])
+
+    @property
+    def momentum(self) -> float:
+        return float(self.raw["learning"]["momentum"])
+
+    @property
+    def clip_grad_norm(self) -> float:
+        return float(self.raw["learning"].get("clip-grad-norm", 0.0))
+
+    @property
+    def log_path(self) -> str:
+        return str(self.raw["log_path"])
+
+    # ---- extensions ----
+    @property
+    def comm(self) -> Dict[str, Any]:
+        return self.raw["comm"]
+
+    @property
+    def data(self) -> Dict[str, Any]:
+        return self.raw["data"]
+
+    @property
+    def engine(self) -> Dict[str, Any]:
+        return self.raw["engine"]
+
+    def attackers(self) -> Dict[int, AttackSpec]:
+        out: Dict[int, AttackSpec] = {}
+        for k, v in (self.raw["comm"].get("attackers") or {}).items():
+            out[int(k)] = AttackSpec(v["mode"], v.get("round", 1), v.get("args", []))
+        return out
+
+    def validate(self) -> "Config":
+        if self.mode not in SERVER_MODES:
+            raise ValueError(f"Server mode '{self.mode}' is not valid.")
+        if self.model not in MODEL_NAMES:
+            raise ValueError(f"Model name '{self.model}' is not valid.")
+        if self.data_name not in DATA_NAMES:
+            raise ValueError(f"Data name '{self.data_name}' is not valid.")
+        lo, hi = self.data_range
+        if lo > hi or lo < 0:
+            raise ValueError(f"num-data-range {self.data_range} is invalid")
+        if self.clients < 1:
+            raise ValueError("server.clients must be >= 1")
+        if self.engine["distance"] not in ("spectral", "flat"):
+            raise ValueError("engine.distance must be 'spectral' or 'flat'")
+        return self
+
+    def to_dict(self) -> Dict[str, Any]:
+        return copy.deepcopy(self.raw)
+
+
+def from_dict(d: Optional[Dict[str, Any]] = None) -> Config:
+    raw = _deep_merge(REFERENCE_DEFAULTS, {})
+    raw = _deep_merge(raw, EXTENSION_DEFAULTS)
+    raw = _deep_merge(raw, d or {})
+    return Config(raw).validate()
+
+
+def load_config(path: str = "config.yaml", overrides: Optional[Dict[str, Any]] = None) -> Config:
+    """Load ``config.yaml`` (reference schema + optional extensions)."""
+    d: Dict[str, Any] = {}
+    if path and os.path.exists(path):
+        with open(path, "r") as fh:
+            d = yaml.safe_load(fh) or {}
+    elif path and path != "config.yaml":
+        raise FileNotFoundError(path)
+    if overrides:
+        d = _deep_merge(d, overrides)
+    return from_dict(d)

@@ -1,0 +1,96 @@
+"""Server-side validation (reference ``src/Validation.py:19-214``).
+
+ICU: ROC-AUC over the whole test set (``ROC_AUC: x.xxxx`` in ``app.log``); NaN outputs fail the
+round.  HAR: accuracy.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
+model before one ROC-AUC, like ``test_hyper_icu``.  The test set stays resident on the device
+and is evaluated in one pass (eval mode is batch-size independent); TransformerModel uses the
+fused HIP forward kernel on GPU.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..data import DeviceTable, HARData, ICUData, resolve_dataset
+from ..models import ParamLayout, build_model
+from ..utils.log import print_with_color
+
+EVAL_CHUNK = 65536
+
+
+class Validation:
+    def __init__(self, model_name: str, data_name: str, logger, device="cpu", data_cfg: Optional[dict] = None,
+                 dataset=None, verbose: bool = True):
+        self.model_name = model_name
+        self.data_name = data_name
+        self.logger = logger
+        self.device = torch.device(device)
+        self.verbose = verbose
+        self.model = build_model(model_name, seed=0).to(self.device).eval()
+        self.layout = ParamLayout.from_state_dict(self.model.state_dict())
+        if data_name == "CIFAR10":
+            raise ValueError("CIFAR10 validation needs torchvision downloads, which this framework does not do")
+        ds = dataset if dataset is not None else resolve_dataset(data_name, "test", data_cfg, verbose=verbose)
+        self.table = DeviceTable(ds, self.device)
+        self.last_metric: float = float("nan")
+
+    # -- forward over the whole test set ------------------------------------------------------
+    @torch.no_grad()
+    def _outputs(self, flat: torch.Tensor) -> torch.Tensor:
+        flat = flat.to(self.device, torch.float32)
+        if self.data_name == "ICU" and self.model_name == "TransformerModel" and self.device.type == "cuda":
+            from ..ops.transformer import eval_forward
+
+            return eval_forward(flat, self.table.rows)
+        sd = self.layout.unflatten(flat, clone=False)
+        self.model.load_state_dict(sd, strict=True)
+        outs = []
+        for a in range(0, self.table.n, EVAL_CHUNK):
+            idx = torch.arange(a, min(a + EVAL_CHUNK, self.table.n), device=self.device)
+            if self.data_name == "ICU":
+                v, l, _ = self.table.icu_batch(idx)
+                outs.append(self.model(v, l).reshape(-1))
+            else:
+                x, _ = self.table.har_batch(idx)
+                outs.append(self.model(x))
+        return torch.cat(outs, dim=0)
+
+    def _labels(self) -> torch.Tensor:
+        return self.table.rows[:, -1] if self.data_name == "ICU" else self.table.y
+
+    def _finish_icu(self, outputs: torch.Tensor, labels: torch.Tensor) -> Tuple[bool, float]:
+        if bool(torch.isnan(outputs).any()):
+            print_with_color("NaN detected in output, training false", "yellow")
+            self.last_metric = float("nan")
+            return False, float("nan")
+        auc = ops.roc_auc(outputs, labels)
+        if self.verbose:
+            print(f"ROC_AUC: {auc:.4f}")
+        self.logger.log_info(f"ROC_AUC: {auc:.4f}")
+        self.last_metric = auc
+        return True, auc
+
+    def test(self, flat: torch.Tensor) -> Tuple[bool, float]:
+        out = self._outputs(flat)
+        if self.data_name == "ICU":
+            return self._finish_icu(out, self._labels())
+        pred = out.argmax(dim=1)
+        acc = float((pred == self._labels()).float().mean().item())
+        if self.verbose:
+            print(f"Test Accuracy: {acc:.4f}")
+        self.logger.log_info(f"Test Accuracy: {acc:.4f}")
+        self.last_metric = acc
+        return True, acc
+
+    def test_hyper(self, hnet, num_client: int) -> Tuple[bool, float]:
+        if self.data_name != "ICU":
+            raise ValueError(f"Not found test function for data name {self.data_name}")
+        outs, labs = [], []
+        for i in range(num_client):
+            flat = hnet.generate(i)
+            outs.append(self._outputs(flat).reshape(-1))
+            labs.append(self._labels())
+        return self._finish_icu(torch.cat(outs), torch.cat(labs))

@@ -1,0 +1,459 @@
+"""SPMD federated-learning round engine.
+
+Replaces the reference's broker-driven state machines — server ``on_request`` /
+``process_consumer`` / ``notify_clients`` (``server.py:205-624``) and client
+``RpcClient.response_message`` (``src/RpcClient.py:64-172``) — with one synchronous loop that
+every rank runs:
+
+  START  (replicated decisions: per-client parameters, attackers' genuine-model sample)
+  LOCAL  (this rank's clients: fused training kernel for all genuine clients at once, attacks)
+  GATHER (one all-gather of fixed-layout ``[slots, P+4]`` blocks  == the UPDATE messages)
+  SERVER (replicated aggregation/defense/hypernetwork update — deterministic kernels)
+  LEADER (validation, hyper-detection decision, checkpoint, app.log) -> control broadcast
+  NEXT   (retry the same round on failure, exactly like the reference's ``round`` counter)
+
+Server state is replicated on every rank instead of living in one process, so the only
+traffic per round is the update all-gather plus a few-byte control broadcast.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..agg import AGGREGATORS, AggResult
+from ..attacks import DistanceEngine, run_attack
+from ..config import AttackSpec, Config
+from ..data import DeviceTable, resolve_dataset
+from ..detect import HyperDetector
+from ..eval import Validation
+from ..models import ParamLayout, build_model
+from ..parallel.comm import Comm, LoopbackComm
+from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
+from .hyper_server import HyperServer
+from .trainers import Plan, make_plan, make_trainer
+
+META = 4  # valid, result, size, is_attacker
+
+
+@dataclass
+class ClientInfo:
+    index: int
+    uuid: str
+    owner: int
+    attack: Optional[AttackSpec] = None
+
+
+@dataclass
+class LocalClient:
+    info: ClientInfo
+    rng: random.Random
+    seed: int
+    training_round: int = 0
+    has_model: bool = False
+    genuine: Optional[torch.Tensor] = None     # last received genuine models [K, P]
+
+
+def build_client_table(cfg: Config, world: int, attackers: Optional[Dict[int, AttackSpec]] = None,
+                       clients_per_rank: int = 0) -> List[ClientInfo]:
+    """Packed placement: client c lives on rank c // ceil(N / world) (contiguous blocks)."""
+    n = cfg.clients
+    cpr = clients_per_rank or -(-n // world)
+    atk = attackers if attackers is not None else cfg.attackers()
+    seed = int(cfg.engine.get("seed", 0))
+    table = []
+    for c in range(n):
+        owner = min(c // cpr, world - 1)
+        uid = str(uuid.UUID(int=(seed * 1000003 + c + 1) & ((1 << 128) - 1), version=4))
+        table.append(ClientInfo(c, uid, owner, atk.get(c)))
+    return table
+
+
+class FLEngine:
+    def __init__(self, cfg: Config, comm: Optional[Comm] = None, table: Optional[List[ClientInfo]] = None,
+                 device=None, leader: Optional[bool] = None, verbose: bool = True, train_dataset=None,
+                 test_dataset=None):
+        self.cfg = cfg
+        self.comm = comm or LoopbackComm(device or "cpu")
+        self.device = torch.device(device) if device is not None else self.comm.device
+        self.rank = self.comm.rank
+        self.world = self.comm.world
+        self.leader = (self.rank == 0) if leader is None else leader
+        self.verbose = verbose and self.leader
+        self.table = table if table is not None else build_client_table(cfg, self.world)
+        self.n_clients = len(self.table)
+        self.mode = cfg.mode
+        self.model_name = cfg.model
+        self.data_name = cfg.data_name
+        self.seed = int(cfg.engine.get("seed", 0))
+        self.ckpt_dir = cfg.engine.get("checkpoint-dir", ".")
+        self.max_retries = int(cfg.engine.get("max-retries", 50))
+        self.layout = ParamLayout.for_model(self.model_name)
+        self.P = self.layout.P
+        self.dist = DistanceEngine(self.layout, cfg.engine.get("distance", "spectral"))
+
+        # ---- logging (leader only, like the reference's single server process) ----
+        if self.leader:
+            os.makedirs(cfg.log_path, exist_ok=True)
+            self.logger = Logger(os.path.join(cfg.log_path, "app.log"))
+            self.metrics = MetricsWriter(cfg.engine.get("metrics") or None)
+        else:
+            self.logger = NullLogger()
+            self.metrics = MetricsWriter(None)
+
+        # ---- data (train set shared by all clients, resident on this rank's device) ----
+        self.local = [LocalClient(ci, random.Random(self.seed * 7919 + ci.index), self.seed * 104729 + ci.index)
+                      for ci in self.table if ci.owner == self.rank]
+        need_train = len(self.local) > 0 or self.mode == "FLTrust"
+        self.train_table = None
+        if need_train:
+            ds = train_dataset if train_dataset is not None else resolve_dataset(self.data_name, "train", cfg.data,
+                                                                                 verbose=self.verbose)
+            self.train_table = DeviceTable(ds, self.device)
+        self.trainer = make_trainer(cfg.engine.get("trainer", "auto"), self.model_name, self.data_name,
+                                    self.train_table, self.device) if self.train_table is not None else None
+        self.validation = None
+        if cfg.validation and self.leader:
+            self.validation = Validation(self.model_name, self.data_name, self.logger, self.device, cfg.data,
+                                         dataset=test_dataset, verbose=self.verbose)
+        self.slots = max(sum(1 for ci in self.table if ci.owner == r) for r in range(self.world))
+        # persistent per-client models (the reference's ``RpcClient.model``), own random init (A-16)
+        self.local_params = torch.zeros(max(1, len(self.local)), self.P, dtype=torch.float32, device=self.device)
+        for j, lc in enumerate(self.local):
+            m = build_model(self.model_name, seed=lc.seed)
+            self.local_params[j].copy_(self.layout.flatten(m.state_dict(), device=self.device))
+
+        # ---- server state (replicated) ----
+        self.server_rng = random.Random(cfg.random_seed) if cfg.random_seed else random.Random()
+        self.global_params: Optional[torch.Tensor] = None
+        self.selected: List[int] = []
+        self.genuine_pool: Optional[torch.Tensor] = None
+        self.hyper: Optional[HyperServer] = None
+        self.fltrust_model: Optional[torch.Tensor] = None
+        self.detector: Optional[HyperDetector] = None
+        self.torch_gen = torch.Generator(device=self.device if self.device.type == "cuda" else "cpu")
+        self.torch_gen.manual_seed(self.seed * 31337 + self.rank)
+        self._init_server()
+        self.round_no = 1
+        self.rounds_left = cfg.num_round
+        self.history: List[dict] = []
+        self.logger.log_info("### Application start ###\n")
+
+    # ------------------------------------------------------------------------------------------
+    # server init / checkpoint
+    # ------------------------------------------------------------------------------------------
+    def _pth(self, hyper: bool = False) -> str:
+        if hyper:
+            return os.path.join(self.ckpt_dir, f"{self.model_name}_hyper_{self.cfg.clients}.pth")
+        return os.path.join(self.ckpt_dir, f"{self.model_name}.pth")
+
+    def _init_server(self):
+        cfg = self.cfg
+        if self.mode == "hyper":
+            net = build_model(self.model_name, seed=self.seed + 99)
+            target_sd = net.state_dict()
+            hyper_ckpt = None
+            if cfg.load_parameters:
+                if os.path.exists(self._pth(True)):
+                    hyper_ckpt = torch.load(self._pth(True), weights_only=True, map_location="cpu")
+                elif os.path.exists(self._pth(False)):
+                    net.load_state_dict(torch.load(self._pth(False), weights_only=True, map_location="cpu"))
+                    target_sd = net.state_dict()
+            self.hyper = HyperServer(target_sd, cfg.clients, cfg.hyper_lr, cfg.clip_grad_norm, self.device,
+                                     seed=self.seed)
+            if hyper_ckpt is not None:
+                if cfg.engine.get("compat-hyper-resume", False):
+                    print_with_color("[compat A-5] hyper checkpoint loaded then discarded", "yellow")
+                else:
+                    self.hyper.hnet.load_state_dict(hyper_ckpt)
+                    print_with_color(f"Load state dict from hyper model: {self._pth(True)}", "yellow")
+            hd = cfg.hyper_detection
+            if hd.get("enable", False) and self.leader:
+                self.detector = HyperDetector(cfg.clients, int(hd.get("n_components", 3)), float(hd.get("eps", 0.007)),
+                                              int(hd.get("min_samples", 3)),
+                                              save_path=os.path.join(self.ckpt_dir, "all_embeddings.npy"))
+        if self.mode == "FLTrust":
+            m = build_model(self.model_name, seed=self.seed + 77)
+            self.fltrust_model = self.layout.flatten(m.state_dict(), device=self.device)
+
+    def save_checkpoint(self):
+        if not self.leader:
+            return
+        os.makedirs(self.ckpt_dir, exist_ok=True)
+        if self.mode == "hyper":
+            torch.save(self.hyper.hnet.state_dict(), self._pth(True))
+        elif self.global_params is not None:
+            torch.save(self.layout.unflatten(self.global_params.detach().cpu()), self._pth(False))
+
+    # ------------------------------------------------------------------------------------------
+    # START
+    # ------------------------------------------------------------------------------------------
+    def client_selection(self):
+        self.selected = list(range(self.n_clients))
+        self.logger.log_info(f"Active with {len(self.selected)} client: {self.selected}")
+
+    def _start_params(self, i: int) -> Optional[torch.Tensor]:
+        if self.mode == "hyper":
+            return self.hyper.generate(i)
+        if self.cfg.load_parameters:
+            p = self._pth(False)
+            if os.path.exists(p):
+                return self.layout.flatten(torch.load(p, weights_only=True, map_location="cpu"), device=self.device)
+            return None
+        return self.global_params
+
+    def _genuine_for_attackers(self) -> Dict[int, Optional[torch.Tensor]]:
+        """Replicated: every rank draws the same sample for every attacker (server RNG in sync)."""
+        out: Dict[int, Optional[torch.Tensor]] = {}
+        pool = self.genuine_pool
+        for i in self.selected:
+            ci = self.table[i]
+            if ci.attack is None:
+                continue
+            if pool is not None and pool.shape[0] > 0:
+                G = pool.shape[0]
+                k = max(int(self.cfg.genuine_rate * G), 1)
+                idx = self.server_rng.sample(range(G), k)
+                out[i] = pool[idx] if ci.owner == self.rank else None
+            else:
+                out[i] = None
+        return out
+
+    # ------------------------------------------------------------------------------------------
+    # LOCAL
+    # ------------------------------------------------------------------------------------------
+    def _local_work(self, genuine: Dict[int, Optional[torch.Tensor]]) -> torch.Tensor:
+        cfg = self.cfg
+        block = torch.zeros(self.slots, self.P + META, dtype=torch.float32, device=self.device)
+        lo, hi = cfg.data_range
+        train_rows, train_nd, train_seeds = [], [], []
+        for j, lc in enumerate(self.local):
+            i = lc.info.index
+            if i not in self.selected:
+                continue
+            lc.training_round += 1
+            p = self._start_params(i)
+            if p is not None:
+                self.local_params[j].copy_(p)
+            g = genuine.get(i)
+            if lc.info.attack is not None and g is not None and g.shape[0] > 0:
+                lc.genuine = g
+            num_data = lc.rng.randrange(lo, hi + 1)
+            block[j, self.P + 0] = 1.0
+            block[j, self.P + 2] = float(num_data)
+            block[j, self.P + 3] = 1.0 if lc.info.attack is not None else 0.0
+            atk = lc.info.attack
+            if atk is not None and lc.training_round >= atk.round and lc.genuine is not None and lc.genuine.shape[0] > 0:
+                gen = torch.Generator(device=self.device if self.device.type == "cuda" else "cpu")
+                gen.manual_seed(lc.seed * 1009 + lc.training_round)
+                res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist, gen)
+                if res.ok and res.params is not None:
+                    block[j, :self.P] = res.params
+                    block[j, self.P + 1] = 1.0
+                self._attack_info = res.info
+                if self.verbose:
+                    print_with_color(f"[===] Client {i} attacks with {atk.mode} {res.info}", "red")
+            else:
+                train_rows.append(j)
+                train_nd.append(num_data)
+                train_seeds.append(lc.seed * 7 + lc.training_round)
+        if train_rows:
+            sel = torch.tensor(train_rows, device=self.device)
+            params = self.local_params.index_select(0, sel).contiguous()
+            plan = make_plan(self.train_table.n, train_nd, cfg.epoch, self._plan_gen(), self.device)
+            oks, losses = self.trainer.train(params, plan, cfg.lr, cfg.batch_size, train_seeds)
+            self.local_params.index_copy_(0, sel, params)
+            block[sel, :self.P] = params
+            block[sel, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=self.device)
+            self._last_losses = losses
+        return block
+
+    def _plan_gen(self) -> torch.Generator:
+        return self.torch_gen
+
+    # ------------------------------------------------------------------------------------------
+    # SERVER
+    # ------------------------------------------------------------------------------------------
+    def _aggregate(self, U: torch.Tensor, sizes: torch.Tensor, attackers: torch.Tensor, round_ok: bool) -> dict:
+        info: dict = {}
+        if not round_ok:
+            return info
+        mode = self.mode
+        if mode == "hyper":
+            ups = {i: U[k] for k, i in enumerate(self.selected)}
+            self.hyper.train(self.selected, ups)
+            info.update(self.hyper.last_info)
+            return info
+        if mode == "FLTrust":
+            self.global_params = self._fltrust(U)
+            return info
+        fn = AGGREGATORS[mode]
+        res: AggResult = fn(U, sizes, attackers=attackers, seed=self.seed * 13 + self.round_no)
+        info.update({k: v for k, v in res.info.items() if k != "scores"})
+        if not res.ok:
+            info["agg_failed"] = True
+        elif res.params is not None:
+            self.global_params = res.params.to(torch.float32)
+        return info
+
+    def _fltrust(self, U: torch.Tensor) -> torch.Tensor:
+        """FLTrust with a server model trained on the first 200 test rows (``server.py:682-743``)."""
+        compat = bool(self.cfg.engine.get("compat-fltrust", False))
+        g0 = self.global_params if self.global_params is not None else self.fltrust_model.clone()
+        root = resolve_dataset(self.data_name, "test", self.cfg.data, verbose=False)
+        from ..data import ICUData
+
+        if isinstance(root, ICUData):
+            root = ICUData(vitals=root.vitals[:200], labs=root.labs[:200], labels=root.labels[:200])
+        table = DeviceTable(root, self.device)
+        trainer = make_trainer(self.cfg.engine.get("trainer", "auto"), self.model_name, self.data_name, table,
+                               self.device)
+        params = g0.clone()[None]
+        nd = min(200, table.n)
+        order = torch.arange(nd, dtype=torch.int32, device=self.device)[None, None, :].expand(1, self.cfg.epoch, nd)
+        plan = Plan(order.contiguous(), torch.tensor([nd], dtype=torch.int32), self.cfg.epoch)
+        trainer.train(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
+        server_new = params[0]
+        g0_delta = server_new - g0
+        if compat and self.global_params is None:
+            g0_delta = torch.zeros_like(g0)  # round-1 alias: state_dict() views were trained in place
+        deltas = U - g0[None, :]
+        if compat:
+            deltas = deltas - g0[None, :]   # A-10: the stored delta is reduced by g_0 a second time
+        norm_g0 = float(torch.linalg.vector_norm(g0_delta.double()))
+        norms = ops.row_norms(deltas).cpu()
+        cos = ops.cosine_to(deltas, g0_delta, eps=1e-8).cpu()
+        trust = torch.clamp(cos, min=0.0)
+        scale = (norm_g0 / (norms + 1e-6)) * trust
+        w = scale / (float(trust.sum()) + 1e-6)
+        agg = ops.weighted_rows(deltas, w.double())
+        self.fltrust_model = server_new.clone()
+        self._trust = trust.tolist()
+        return g0 + agg
+
+    # ------------------------------------------------------------------------------------------
+    # one round
+    # ------------------------------------------------------------------------------------------
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def run_round(self) -> dict:
+        t0 = time.perf_counter()
+        if self.verbose:
+            print_with_color(f"Start training round {self.round_no}", "yellow")
+        self._attack_info = None
+        genuine = self._genuine_for_attackers()
+        block = self._local_work(genuine)
+        self._sync()
+        t1 = time.perf_counter()
+        allb = self.comm.all_gather_rows(block)                        # [world*slots, P+META]
+        rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
+        idx = torch.tensor(rows, device=allb.device, dtype=torch.long)
+        sel = allb.index_select(0, idx)
+        U = sel[:, :self.P].contiguous()
+        meta = sel[:, self.P:].float().cpu()
+        self._sync()
+        t2 = time.perf_counter()
+        results = meta[:, 1] > 0.5
+        sizes = meta[:, 2].clone()
+        attackers = meta[:, 3] > 0.5
+        round_ok = bool(results.all())
+        # stored updates (arrival in client order; the reference stops storing after a failure)
+        stored = len(self.selected)
+        if not round_ok:
+            stored = int(torch.nonzero(~results)[0, 0])
+        snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) else None
+        info = self._aggregate(U, sizes, attackers, round_ok)
+        if info.get("agg_failed"):
+            round_ok = False
+        self._sync()
+        t3 = time.perf_counter()
+
+        # ---- leader: detection + validation; control broadcast ----
+        removed: List[int] = []
+        metric = float("nan")
+        if self.leader:
+            if self.detector is not None:
+                embs = {i: self.hyper.embedding(i).cpu().numpy()[None, :] for i in self.selected}
+                removed = self.detector.step(self.round_no, self.selected, embs)
+            if self.validation is not None and round_ok:
+                if self.mode == "hyper":
+                    round_ok, metric = self.validation.test_hyper(self.hyper.hnet, len(self.selected))
+                else:
+                    if self.global_params is None:
+                        round_ok = False
+                    else:
+                        round_ok, metric = self.validation.test(self.global_params)
+        ctrl = torch.full((2 + self.n_clients,), -1.0, dtype=torch.float64, device=self.device)
+        if self.leader:
+            ctrl[0] = 1.0 if round_ok else 0.0
+            ctrl[1] = float(len(removed))
+            for k, r in enumerate(removed):
+                ctrl[2 + k] = float(r)
+        if self.world > 1:
+            self.comm.broadcast_(ctrl, src=0)
+        ctrl = ctrl.cpu()
+        round_ok = bool(ctrl[0] > 0.5)
+        removed = [int(ctrl[2 + k]) for k in range(int(ctrl[1]))]
+        if removed:
+            for r in removed:
+                print_with_color(f"Removing anomaly {r}, rolling back", "yellow")
+                if r in self.selected:
+                    self.selected.remove(r)
+            self.hyper.restore(snapshot)
+        t4 = time.perf_counter()
+
+        # ---- genuine pool for the next START (non-attacker rows stored this round) ----
+        keep = [k for k in range(stored) if not bool(attackers[k])]
+        self.genuine_pool = U[keep].clone() if keep else None
+
+        if round_ok:
+            self.save_checkpoint()
+            self.rounds_left -= 1
+        elif self.verbose:
+            print_with_color("Training failed!", "yellow")
+        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, "t_local": t1 - t0, "t_gather": t2 - t1,
+               "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
+               "n_selected": len(self.selected), "removed": removed}
+        if self._attack_info:
+            rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
+        rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list))})
+        self.metrics.write(rec)
+        self.history.append(rec)
+        if round_ok:
+            self.round_no += 1
+        return rec
+
+    def _slot_of(self, i: int) -> int:
+        owner = self.table[i].owner
+        return sum(1 for c in self.table[:i] if c.owner == owner)
+
+    def run(self, max_rounds: Optional[int] = None) -> List[dict]:
+        if not self.selected:
+            self.client_selection()
+        fails = 0
+        done = 0
+        while self.rounds_left > 0:
+            rec = self.run_round()
+            done += 1
+            fails = 0 if rec["ok"] else fails + 1
+            if self.max_retries and fails > self.max_retries:
+                raise RuntimeError(f"round {self.round_no} failed {fails} times in a row")
+            if max_rounds is not None and done >= max_rounds:
+                break
+        if self.verbose and self.rounds_left <= 0:
+            print_with_color("Training finished, stopping clients.", "green")
+        return self.history
+
+    def close(self):
+        self.metrics.close()
+        if hasattr(self.logger, "close"):
+            self.logger.close()

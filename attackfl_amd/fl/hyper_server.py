@@ -1,0 +1,106 @@
+"""pFedHN-style hypernetwork aggregator (reference ``Server.train_hyper``, ``server.py:637-678``).
+
+For every selected client, sequentially: ``W_i = hnet(i)``; ``δ = W_i - w_client``; VJP of
+``W_i`` w.r.t. all hnet parameters with cotangent δ; global-norm clip to ``clip-grad-norm``;
+one Adam step (lr ``hyper-lr``).  The hnet is held packed (``PackedHyperNet``): all per-key
+heads form one ``[P, H]`` matrix, so
+
+* ``W_i = W·f + b`` is one GEMV and ``δ`` comes out of the same pass,
+* ``∂L/∂f = Wᵀδ`` is accumulated in that same pass (``ops.hyper_delta_vjp``),
+* the head gradient ``δ ⊗ f`` is never materialised: its norm is ``||δ||·||f||`` and the
+  Adam update of the ``P·H`` head weights computes each gradient element on the fly
+  (``ops.hyper_adam_outer``, one streaming pass),
+* the tiny embedding/MLP part (≈ 20 k params) is back-propagated with plain tensor ops and
+  updated by the flat Adam kernel.
+
+Every rank holds an identical replica (deterministic kernels), so ``hnet(rank's clients)`` is
+computed locally and no scatter is needed.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, Sequence
+
+import torch
+
+from .. import ops
+from ..models import PackedHyperNet
+
+
+class HyperServer:
+    def __init__(self, target_sd: "OrderedDict[str, torch.Tensor]", n_clients: int, hyper_lr: float, clip: float,
+                 device, seed: int = 0, embedding_dim: int = 8, hidden_dim: int = 100, n_hidden: int = 2):
+        g = torch.Generator().manual_seed(int(seed) + 0x5EED)
+        self.hnet = PackedHyperNet(target_sd, n_clients, embedding_dim, hidden_dim, n_hidden, device=device,
+                                   generator=g)
+        self.device = torch.device(device)
+        self.lr = float(hyper_lr)
+        self.clip = float(clip)
+        self.m = torch.zeros_like(self.hnet.arena)
+        self.v = torch.zeros_like(self.hnet.arena)
+        self.step = 0
+        off_W, _ = self.hnet.slots["W"]
+        self.n_small = off_W                      # emb + MLP region [0, off_W)
+        self.last_info: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------------------------------
+    def generate(self, i: int) -> torch.Tensor:
+        return self.hnet.generate(i)
+
+    def embedding(self, i: int) -> torch.Tensor:
+        return self.hnet.emb[i].detach().clone()
+
+    def snapshot(self) -> torch.Tensor:
+        return self.hnet.arena.clone()
+
+    def restore(self, snap: torch.Tensor) -> None:
+        self.hnet.arena.copy_(snap)
+
+    # ------------------------------------------------------------------------------------------
+    def _mlp_backward(self, i: int, acts, dfeat: torch.Tensor) -> torch.Tensor:
+        """Grads of emb + MLP into a flat [n_small] buffer (same layout as the arena prefix)."""
+        h = self.hnet
+        g = torch.zeros(self.n_small, dtype=torch.float32, device=self.device)
+
+        def gslot(name):
+            off, shp = h.slots[name]
+            n = 1
+            for s in shp:
+                n *= s
+            return g[off:off + n].view(shp)
+
+        dz = dfeat
+        L = h.n_hidden + 1
+        for li in reversed(range(L)):
+            Wm, _ = h.mlp(li)
+            a_in = acts[li]
+            gslot(f"mlp{li}.W").copy_(torch.outer(dz, a_in))
+            gslot(f"mlp{li}.b").copy_(dz)
+            da = Wm.t() @ dz
+            if li > 0:
+                dz = da * (acts[li] > 0).to(da.dtype)
+            else:
+                gslot("emb")[i].copy_(da)
+        return g
+
+    def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor]) -> None:
+        h = self.hnet
+        for i in selected:
+            emb, feat, acts = h.features(i)
+            delta, dfeat = ops.hyper_delta_vjp(h.W, h.b, feat, updates[i])   # δ = W f + b - u ; Wᵀδ
+            g_small = self._mlp_backward(i, acts, dfeat)
+            dd = float(torch.dot(delta.double(), delta.double()).item())
+            ff = float(torch.dot(feat.double(), feat.double()).item())
+            total_sq = dd * ff + dd + float(torch.dot(g_small.double(), g_small.double()).item())
+            total = total_sq ** 0.5
+            scale = 1.0
+            if self.clip > 0:
+                coef = self.clip / (total + 1e-6)
+                if coef < 1.0:
+                    scale = coef
+            self.step += 1
+            small = slice(0, self.n_small)
+            ops.adam_step_scaled(h.arena[small], g_small, self.m[small], self.v[small], self.step, self.lr, scale)
+            offW, _ = h.slots["W"]
+            ops.hyper_adam_outer(h.W, h.b, self.m[offW:], self.v[offW:], delta, feat, self.step, self.lr, scale)
+            self.last_info = {"grad_norm": total, "clip_scale": scale}

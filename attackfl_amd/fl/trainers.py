@@ -1,0 +1,172 @@
+"""Client local training.
+
+Semantics follow the reference trainers (``client.py:66-131``):
+* fresh ``Adam(lr)`` (β=(0.9, 0.999), eps 1e-8) every round, ``momentum`` unused (A-19);
+* ICU: ``BCELoss`` on sigmoid outputs, batches of size 1 skipped (A-21), a NaN loss aborts the
+  client's round with ``result=False``; ``clip_grad_norm_`` is called before ``backward`` in the
+  reference and therefore never clips (A-4) — we do not clip either;
+* HAR: ``CrossEntropyLoss``;
+* data: each round the client draws ``num_data`` rows without replacement from the shared
+  train set (A-20) and visits them in a fresh random order each epoch (``DataLoader(shuffle=True)``).
+
+Two implementations share one sampling plan (``make_plan``), so they see identical batches:
+* ``EagerTrainer``  — PyTorch modules + ``torch.optim.Adam`` (the CPU path and the oracle);
+* ``FusedTrainer``  — ONE persistent HIP kernel launch trains all of a rank's clients for all
+  their local epochs (one workgroup per client, weights/activations in LDS, Adam state in
+  registers) — ``ops/transformer.py``.  TransformerModel/ICU on gfx950.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ..data import DeviceTable
+from ..models import ParamLayout, build_model
+from ..utils.log import print_with_color
+
+
+@dataclass
+class Plan:
+    """Visit order of train rows for C clients: ``order [C, E, maxnd]`` int32 (+ ``nd [C]``)."""
+
+    order: torch.Tensor
+    nd: torch.Tensor
+    epochs: int
+
+    def client(self, c: int) -> torch.Tensor:
+        return self.order[c, :, : int(self.nd[c])]
+
+
+def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator: torch.Generator, device) -> Plan:
+    """Random subset (without replacement) per client + a fresh permutation per epoch.
+
+    Everything is generated on ``device`` with two batched argsorts (no per-client loops)."""
+    C = len(num_data)
+    if C == 0:
+        return Plan(torch.zeros(0, epochs, 0, dtype=torch.int32, device=device), torch.zeros(0, dtype=torch.int32),
+                    epochs)
+    maxnd = max(num_data)
+    if maxnd > n_train:
+        raise ValueError(f"num_data {maxnd} exceeds the train set size {n_train}")
+    gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
+    keys = torch.rand(C, n_train, generator=generator, device=gdev)
+    subset = torch.argsort(keys, dim=1)[:, :maxnd]                              # [C, maxnd]
+    ek = torch.rand(C, epochs, maxnd, generator=generator, device=gdev)
+    nd = torch.tensor(list(num_data), dtype=torch.long, device=gdev)
+    pad = torch.arange(maxnd, device=gdev)[None, None, :] >= nd[:, None, None]
+    ek = ek.masked_fill(pad, 2.0)                                               # padding sorts last
+    perm = torch.argsort(ek, dim=2)                                             # [C, E, maxnd]
+    order = torch.gather(subset[:, None, :].expand(C, epochs, maxnd), 2, perm)
+    return Plan(order.to(device=device, dtype=torch.int32).contiguous(), nd.to(torch.int32).cpu(), epochs)
+
+
+def batches(nd: int, batch: int):
+    """(start, end) of each batch of one epoch; size-1 batches are skipped (A-21)."""
+    for a in range(0, nd, batch):
+        b = min(nd, a + batch)
+        if b - a == 1:
+            continue
+        yield a, b
+
+
+def bce_loss(p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """``BCELoss`` (mean, log clamped at -100) without the input-range check, so a NaN output
+    reaches the NaN test (``client.py:100-102``) instead of raising inside the loss."""
+    return -(y * torch.clamp(torch.log(p), min=-100.0) + (1 - y) * torch.clamp(torch.log1p(-p), min=-100.0)).mean()
+
+
+class EagerTrainer:
+    """Reference-semantics trainer on PyTorch modules (CPU oracle / fallback)."""
+
+    kind = "eager"
+
+    def __init__(self, model_name: str, data_name: str, table: DeviceTable, device, verbose: bool = False):
+        self.model_name = model_name
+        self.data_name = data_name
+        self.table = table
+        self.device = torch.device(device)
+        self.model = build_model(model_name, seed=0).to(self.device)
+        self.layout = ParamLayout.from_state_dict(self.model.state_dict())
+        self.verbose = verbose
+
+    def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
+              ) -> Tuple[List[bool], torch.Tensor]:
+        """Train every row of ``params`` [C, P] in place.  Returns (ok per client, losses [C, E])."""
+        C = params.shape[0]
+        losses = torch.zeros(C, plan.epochs, dtype=torch.float64)
+        oks: List[bool] = []
+        for c in range(C):
+            torch.manual_seed(int(seeds[c]))  # dropout masks
+            sd = self.layout.unflatten(params[c].to(self.device), clone=True)
+            self.model.load_state_dict(sd)
+            ok = self._train_one(plan.client(c), lr, batch, losses[c])
+            with torch.no_grad():
+                params[c].copy_(self.layout.flatten(self.model.state_dict(), device=params.device))
+            oks.append(ok)
+        return oks, losses
+
+    def _train_one(self, order: torch.Tensor, lr: float, batch: int, loss_out: torch.Tensor) -> bool:
+        model = self.model
+        model.train()
+        opt = torch.optim.Adam(model.parameters(), lr=lr)
+        crit = bce_loss if self.data_name == "ICU" else torch.nn.CrossEntropyLoss()
+        nd = order.shape[1]
+        nbatches = max(1, (nd + batch - 1) // batch)
+        for e in range(order.shape[0]):
+            total = torch.zeros((), dtype=torch.float64, device=self.device)
+            for a, b in batches(nd, batch):
+                idx = order[e, a:b].long()
+                opt.zero_grad()
+                if self.data_name == "ICU":
+                    v, l, y = self.table.icu_batch(idx)
+                    out = model(v, l)
+                    loss = crit(out, y[:, None])
+                else:
+                    x, y = self.table.har_batch(idx)
+                    loss = crit(model(x), y)
+                if bool(torch.isnan(loss).any()):
+                    print_with_color("NaN detected in loss, stop training", "yellow")
+                    return False
+                total += loss.detach().double()
+                loss.backward()
+                opt.step()
+            loss_out[e] = float(total.item()) / nbatches
+            if self.verbose:
+                print_with_color(f"Loss {float(loss_out[e]):.6f} ", "yellow")
+        return True
+
+
+class FusedTrainer:
+    """All local clients' local training in one persistent HIP kernel (TransformerModel/ICU)."""
+
+    kind = "fused"
+
+    def __init__(self, model_name: str, data_name: str, table: DeviceTable, device, verbose: bool = False):
+        if model_name != "TransformerModel" or data_name != "ICU":
+            raise ValueError("fused trainer supports TransformerModel/ICU")
+        if torch.device(device).type != "cuda":
+            raise ValueError("fused trainer needs a GPU")
+        from ..ops import transformer as T
+
+        self.T = T
+        self.table = table
+        self.device = torch.device(device)
+        self.layout = ParamLayout.for_model(model_name)
+        self.verbose = verbose
+
+    def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
+              ) -> Tuple[List[bool], torch.Tensor]:
+        ok, losses = self.T.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
+                                          seeds)
+        return [bool(x) for x in ok.tolist()], losses
+
+
+def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable, device, verbose=False):
+    dev = torch.device(device)
+    if kind == "auto":
+        kind = "fused" if (dev.type == "cuda" and model_name == "TransformerModel" and data_name == "ICU") else "eager"
+    if kind == "fused":
+        return FusedTrainer(model_name, data_name, table, device, verbose)
+    return EagerTrainer(model_name, data_name, table, device, verbose)

@@ -1,0 +1,227 @@
+"""Op dispatch: HIP kernels for device tensors, PyTorch composites for CPU tensors.
+
+Rule: a CUDA (ROCm) tensor ALWAYS goes to the native gfx950 kernel in ``attackfl_amd/_C.so``;
+if that extension is missing on a GPU box the call raises (no silent eager fallback).  CPU
+tensors run the composites in ``ops/composite.py``, which double as the numerical oracles in
+the test-suite.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Sequence, Tuple
+
+import torch
+
+from . import composite
+
+_NATIVE = None
+
+
+def native():
+    """Return the loaded native extension or raise with build instructions."""
+    global _NATIVE
+    if _NATIVE is None:
+        try:
+            from .. import _C  # noqa: F401
+
+            _NATIVE = _C
+        except Exception as e:  # pragma: no cover - depends on build state
+            _NATIVE = e
+    if isinstance(_NATIVE, Exception):
+        raise RuntimeError("attackfl_amd native extension (_C.so) is not built/loadable; run "
+                           "`python -m attackfl_amd._build`: " + repr(_NATIVE))
+    return _NATIVE
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _dev(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _tiles(slots, P: int, tile: int = 4096):
+    """Split [0, P) into tiles that never cross a slot boundary -> int32 [T, 3] (seg, start, end)."""
+    rows = []
+    for si, s in enumerate(slots):
+        a, b = s.offset, s.offset + s.numel
+        while a < b:
+            e = min(b, a + tile)
+            rows.append((si, a, e))
+            a = e
+    return torch.tensor(rows, dtype=torch.int32)
+
+
+_TILE_CACHE = {}
+
+
+def _tile_table(slots, P: int, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    key = (tuple((s.offset, s.numel) for s in slots), P, str(device))
+    if key not in _TILE_CACHE:
+        t = _tiles(slots, P)
+        # segment -> [first tile, last tile) ranges for the deterministic second pass
+        seg_first = torch.zeros(len(slots) + 1, dtype=torch.int32)
+        for i in range(t.shape[0]):
+            seg_first[int(t[i, 0]) + 1] = i + 1
+        for si in range(1, len(slots) + 1):
+            seg_first[si] = max(int(seg_first[si]), int(seg_first[si - 1]))
+        _TILE_CACHE[key] = (t.to(device), seg_first.to(device))
+    return _TILE_CACHE[key]
+
+
+class _WholeSlot:
+    def __init__(self, P):
+        self.offset, self.numel, self.shape = 0, P, (P,)
+
+
+# ---------------------------------------------------------------- column statistics / attacks
+def column_mean_std(G: torch.Tensor):
+    if _dev(G):
+        out = native().colstats(G.contiguous(), 0, 0.0)
+        return out[0], out[1]
+    return composite.column_mean_std(G)
+
+
+def lie_candidate(G: torch.Tensor, z: float) -> torch.Tensor:
+    if _dev(G):
+        return native().colstats(G.contiguous(), 1, float(z))[2]
+    return composite.lie_candidate(G, z)
+
+
+def pairwise_l2(G: torch.Tensor) -> torch.Tensor:
+    if _dev(G):
+        return native().pairwise_sqdist(G.contiguous()).clamp_min(0.0).sqrt()
+    return composite.pairwise_l2(G)
+
+
+def pairwise_sqdist(G: torch.Tensor) -> torch.Tensor:
+    if _dev(G):
+        return native().pairwise_sqdist(G.contiguous())
+    return composite.pairwise_l2(G) ** 2
+
+
+def segment_l2_sum(diffs: torch.Tensor, slots) -> torch.Tensor:
+    if _dev(diffs):
+        tiles, segf = _tile_table(slots, diffs.shape[1], diffs.device)
+        sq = native().segment_sqsum(diffs.contiguous(), tiles, segf, len(slots))  # [M, S] fp64
+        return sq.clamp_min(0.0).sqrt().sum(dim=1)
+    return composite.segment_l2_sum(diffs, slots)
+
+
+def batched_spectral_norm(mats: torch.Tensor) -> torch.Tensor:
+    if _dev(mats):
+        return native().spectral_norm(mats.contiguous())
+    return composite.batched_spectral_norm(mats)
+
+
+def attack_coeffs(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor):
+    if _dev(G):
+        A, B, C = attack_coeffs_segments(G, mean, dev, [_WholeSlot(G.shape[1])])
+        return A[:, 0], B[:, 0], C[0]
+    return composite.attack_coeffs(G, mean, dev)
+
+
+def attack_coeffs_segments(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor, slots):
+    if _dev(G):
+        tiles, segf = _tile_table(slots, G.shape[1], G.device)
+        A, B, C = native().attack_coeffs(G.contiguous(), mean.contiguous(), dev.contiguous(), tiles, segf, len(slots))
+        return A, B, C
+    return composite.attack_coeffs_segments(G, mean, dev, slots)
+
+
+# ---------------------------------------------------------------- aggregation
+def weighted_rows(U: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if _dev(U):
+        return native().weighted_rows(U.contiguous(), w.to(device=U.device, dtype=torch.float64).contiguous())
+    return composite.weighted_rows(U, w)
+
+
+def fedavg(U: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+    s = sizes.to(torch.float64)
+    if _dev(U):
+        return weighted_rows(U, s / s.sum())
+    return composite.fedavg(U, sizes)
+
+
+def coord_median(U: torch.Tensor) -> torch.Tensor:
+    if _dev(U):
+        return native().coord_select(U.contiguous(), 0, 0)
+    return composite.coord_median(U)
+
+
+def trimmed_mean(U: torch.Tensor, trim_k: int) -> torch.Tensor:
+    if _dev(U):
+        return native().coord_select(U.contiguous(), 1, int(trim_k))
+    return composite.trimmed_mean(U, trim_k)
+
+
+def row_norms(U: torch.Tensor) -> torch.Tensor:
+    if _dev(U):
+        return native().row_dots(U.contiguous(), U.new_zeros(0), 0)[:, 0].clamp_min(0).sqrt()
+    return composite.row_norms(U)
+
+
+def cosine_to(U: torch.Tensor, ref: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
+    if _dev(U):
+        d = native().row_dots(U.contiguous(), ref.contiguous(), 1)  # [N, 3]: <u,u>, <u,r>, <r,r>
+        den = torch.clamp(d[:, 0].sqrt() * d[:, 2].sqrt(), min=eps)
+        return d[:, 1] / den
+    return composite.cosine_to(U, ref, eps)
+
+
+def stochastic_quantize(U: torch.Tensor, seed: int):
+    if _dev(U):
+        sigma, smin, smax = native().stoch_quant(U.contiguous(), int(seed) & 0x7FFFFFFFFFFFFFFF)
+        return sigma, smin, smax
+    g = torch.Generator(device="cpu")
+    g.manual_seed(int(seed))
+    return composite.stochastic_quantize(U, g)
+
+
+# ---------------------------------------------------------------- optimizer
+def adam_step(p, g, m, v, step: int, lr: float, beta1=0.9, beta2=0.999, eps=1e-8) -> None:
+    if _dev(p):
+        native().adam_flat(p, g, m, v, int(step), float(lr), float(beta1), float(beta2), float(eps), 1.0)
+        return
+    composite.adam_step(p, g, m, v, step, lr, beta1, beta2, eps)
+
+
+# ---------------------------------------------------------------- metrics
+def roc_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
+    if _dev(scores):
+        return float(native().roc_auc(scores.reshape(-1).float().contiguous(), labels.reshape(-1).float().contiguous()))
+    return composite.roc_auc(scores, labels)
+
+
+def adam_step_scaled(p, g, m, v, step: int, lr: float, scale: float, beta1=0.9, beta2=0.999, eps=1e-8) -> None:
+    if _dev(p):
+        native().adam_flat(p, g, m, v, int(step), float(lr), float(beta1), float(beta2), float(eps), float(scale))
+        return
+    composite.adam_step_scaled(p, g, m, v, step, lr, scale, beta1, beta2, eps)
+
+
+# ---------------------------------------------------------------- hypernetwork
+def hyper_delta_vjp(W: torch.Tensor, b: torch.Tensor, feat: torch.Tensor, u: torch.Tensor):
+    if _dev(W):
+        out = native().hyper_delta_vjp(W, b, feat.contiguous(), u.contiguous())
+        return out[0], out[1]
+    return composite.hyper_delta_vjp(W, b, feat, u)
+
+
+def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale: float) -> None:
+    if _dev(W):
+        native().hyper_adam_outer(W, b, m_wb, v_wb, delta.contiguous(), feat.contiguous(), int(step), float(lr),
+                                  0.9, 0.999, 1e-8, float(scale))
+        return
+    composite.hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step, lr, scale)
+
+
+def hyper_generate(W: torch.Tensor, b: torch.Tensor, feat: torch.Tensor) -> torch.Tensor:
+    if _dev(W):
+        return native().hyper_generate(W, b, feat.contiguous())
+    return torch.addmv(b, W, feat)

@@ -1,0 +1,166 @@
+"""Plain-PyTorch composites of every native op.
+
+These are the CPU implementations *and* the numerical oracles that the HIP kernels in
+``csrc/kernels`` are tested against (fp32/fp64 PyTorch references of the same op).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+
+# ---------------------------------------------------------------- column statistics / attacks
+def column_mean_std(G: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    mean = G.mean(dim=0)
+    std = G.std(dim=0) if G.shape[0] > 1 else torch.full_like(mean, float("nan"))
+    return mean, std
+
+
+def lie_candidate(G: torch.Tensor, z: float) -> torch.Tensor:
+    mean, std = column_mean_std(G)
+    return mean + z * std
+
+
+def pairwise_l2(G: torch.Tensor) -> torch.Tensor:
+    Gd = G.double()
+    sq = (Gd * Gd).sum(dim=1)
+    gram = Gd @ Gd.t()
+    d2 = (sq[:, None] + sq[None, :] - 2.0 * gram).clamp_min(0.0)
+    d2.fill_diagonal_(0.0)
+    return d2.sqrt()
+
+
+def gram(G: torch.Tensor) -> torch.Tensor:
+    Gd = G.double()
+    return Gd @ Gd.t()
+
+
+def segment_l2_sum(diffs: torch.Tensor, slots) -> torch.Tensor:
+    out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
+    for s in slots:
+        seg = diffs[:, s.offset:s.offset + s.numel].double()
+        out += torch.linalg.vector_norm(seg, dim=1)
+    return out
+
+
+def batched_spectral_norm(mats: torch.Tensor) -> torch.Tensor:
+    return torch.linalg.matrix_norm(mats.double(), ord=2).to(torch.float64)
+
+
+def attack_coeffs(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor):
+    Gd, md, dd = G.double(), mean.double(), dev.double()
+    r = md[None, :] - Gd
+    A = (r * r).sum(dim=1)
+    B = (r * dd[None, :]).sum(dim=1)
+    C = (dd * dd).sum()
+    return A, B, C
+
+
+def attack_coeffs_segments(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor, slots):
+    K = G.shape[0]
+    S = len(slots)
+    A = torch.zeros(K, S, dtype=torch.float64, device=G.device)
+    B = torch.zeros(K, S, dtype=torch.float64, device=G.device)
+    C = torch.zeros(S, dtype=torch.float64, device=G.device)
+    for i, s in enumerate(slots):
+        sl = slice(s.offset, s.offset + s.numel)
+        a, b, c = attack_coeffs(G[:, sl], mean[sl], dev[sl])
+        A[:, i], B[:, i], C[i] = a, b, c
+    return A, B, C
+
+
+# ---------------------------------------------------------------- aggregation
+def weighted_rows(U: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """sum_i w_i U_i  (w already normalised by the caller)."""
+    return (w.to(U.dtype)[:, None] * U).sum(dim=0)
+
+
+def fedavg(U: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
+    s = sizes.to(torch.float64)
+    return ((s[:, None] * U.double()).sum(dim=0) / s.sum()).to(U.dtype)
+
+
+def coord_median(U: torch.Tensor) -> torch.Tensor:
+    return torch.median(U, dim=0).values
+
+
+def trimmed_mean(U: torch.Tensor, trim_k: int) -> torch.Tensor:
+    n = U.shape[0]
+    s, _ = torch.sort(U, dim=0)
+    return s[trim_k:n - trim_k].mean(dim=0)
+
+
+def row_norms(U: torch.Tensor) -> torch.Tensor:
+    return torch.linalg.vector_norm(U.double(), dim=1)
+
+
+def cosine_to(U: torch.Tensor, ref: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
+    Ud, rd = U.double(), ref.double()
+    num = Ud @ rd
+    den = torch.clamp(torch.linalg.vector_norm(Ud, dim=1) * torch.linalg.vector_norm(rd), min=eps)
+    return num / den
+
+
+def stochastic_quantize(U: torch.Tensor, generator: torch.Generator = None):
+    """ScionFL 1-bit quantisation per row: returns (sigma [N,P] {0,1}, smin [N], smax [N])."""
+    smin = U.min(dim=1).values
+    smax = U.max(dim=1).values
+    probs = (U - smin[:, None]) / (smax - smin + 1e-6)[:, None]
+    u = torch.rand(U.shape, generator=generator, device=U.device, dtype=U.dtype) if generator is not None \
+        else torch.rand_like(U)
+    sigma = (u < probs).to(U.dtype)
+    return sigma, smin, smax
+
+
+# ---------------------------------------------------------------- optimizer
+def adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+              beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8) -> None:
+    """In-place Adam (torch.optim.Adam default, non-foreach math)."""
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+# ---------------------------------------------------------------- metrics
+def roc_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
+    """ROC-AUC with sklearn's tie handling (trapezoid over distinct thresholds)."""
+    s = scores.reshape(-1).double()
+    y = labels.reshape(-1).double()
+    order = torch.argsort(s, descending=True, stable=True)
+    s, y = s[order], y[order]
+    tps = torch.cumsum(y, 0)
+    fps = torch.cumsum(1 - y, 0)
+    # keep the last index of every run of equal scores
+    last = torch.ones_like(s, dtype=torch.bool)
+    last[:-1] = s[1:] != s[:-1]
+    tps, fps = tps[last], fps[last]
+    P, N = tps[-1], fps[-1]
+    if P <= 0 or N <= 0:
+        return float("nan")
+    tpr = torch.cat([tps.new_zeros(1), tps / P])
+    fpr = torch.cat([fps.new_zeros(1), fps / N])
+    return float(torch.trapz(tpr, fpr).item())
+
+
+def adam_step_scaled(p, g, m, v, step: int, lr: float, scale: float, beta1=0.9, beta2=0.999, eps=1e-8) -> None:
+    adam_step(p, g * scale, m, v, step, lr, beta1, beta2, eps)
+
+
+# ---------------------------------------------------------------- hypernetwork
+def hyper_delta_vjp(W: torch.Tensor, b: torch.Tensor, feat: torch.Tensor, u: torch.Tensor):
+    """delta = W f + b - u  and  W^T delta (one pass over W in the native kernel)."""
+    delta = torch.addmv(b, W, feat) - u
+    return delta, W.t() @ delta
+
+
+def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale: float, beta1=0.9, beta2=0.999,
+                     eps=1e-8) -> None:
+    """Adam on the packed heads with grad(W) = scale·δ⊗f, grad(b) = scale·δ (never materialised natively)."""
+    P, H = W.shape
+    gW = torch.outer(delta, feat) * scale
+    adam_step(W.view(-1), gW.view(-1), m_wb[:P * H], v_wb[:P * H], step, lr, beta1, beta2, eps)
+    adam_step(b, delta * scale, m_wb[P * H:P * H + P], v_wb[P * H:P * H + P], step, lr, beta1, beta2, eps)
