@@ -71,7 +71,7 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     dev_flags = common + [f"--offload-arch={ARCH}", "-ffast-math", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
     dev_flags = [f for f in dev_flags if f != "-ffast-math"]  # keep IEEE semantics (NaN checks in kernels)
     host_flags = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM",
-                           "-I" + py_inc] + ["-I" + p for p in inc] + ["-x", "c++"]
+                           "-I" + py_inc, "-I" + os.path.join(ROCM, "include")] + ["-I" + p for p in inc] + ["-x", "c++"]
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
     hosts = sorted(glob.glob(os.path.join(ROOT, "csrc", "*.cpp")) + glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))

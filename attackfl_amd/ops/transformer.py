@@ -1,0 +1,182 @@
+"""Fused TransformerModel/ICU training and evaluation (HIP kernels in ``csrc/kernels/transformer.hip``).
+
+``train_clients`` runs ONE persistent kernel launch that trains every row of ``params [C, P]``
+for all local epochs (one 512-thread workgroup per client).  ``reference_train`` is the plain
+PyTorch fp32 oracle of exactly the same computation — same batches, same hash-generated dropout
+masks, Adam (or the SGD test mode) — used by the numerics tests to check the kernel.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+NPARAM = 47693
+M32 = 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------------------- device entry points
+def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
+                  lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Train all clients in place. Returns (ok [C] int32 on host, losses [C, E] fp32 on host)."""
+    dev = params.device
+    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
+    seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
+    ok, losses = native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
+                                   int(batch), float(lr), int(opt_mode))
+    return ok.cpu(), losses.cpu()
+
+
+def eval_forward(params: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """Sigmoid outputs of TransformerModel (eval mode) for every row of ``rows [N, 24]``."""
+    return native().tf_eval(params.contiguous(), rows.contiguous())
+
+
+# ------------------------------------------------------------------------------- hash dropout (host mirror)
+def _u32(x):
+    return np.asarray(x, dtype=np.uint64) & M32
+
+
+def hash32(a: int, b: int) -> int:
+    a &= M32
+    b &= M32
+    x = ((a * 0x9E3779B1) & M32) ^ ((b + 0x7F4A7C15 + ((a << 6) & M32) + (a >> 2)) & M32)
+    x ^= x >> 16
+    x = (x * 0x21F0AAAD) & M32
+    x ^= x >> 15
+    x = (x * 0x735A2D97) & M32
+    x ^= x >> 15
+    return x
+
+
+def keep_mask(key: int, layer: int, n_rows: int, n_cols: int, p: float) -> torch.Tensor:
+    """Vectorised mirror of ``tf::keep`` -> bool [n_rows, n_cols]."""
+    r = np.arange(n_rows, dtype=np.uint64)[:, None]
+    c = np.arange(n_cols, dtype=np.uint64)[None, :]
+    x = (np.uint64(key) ^ ((np.uint64(layer) * np.uint64(0x9E3779B9)) & np.uint64(M32))
+         ^ ((r * np.uint64(0x85EBCA6B)) & np.uint64(M32)) ^ ((c * np.uint64(0xC2B2AE35)) & np.uint64(M32)))
+    x &= np.uint64(M32)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & np.uint64(M32)
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & np.uint64(M32)
+    x ^= x >> np.uint64(16)
+    thr = {0.1: 1677722, 0.3: 5033165}[p]
+    return torch.from_numpy(((x >> np.uint64(8)) >= np.uint64(thr)))
+
+
+# ------------------------------------------------------------------------------- fp32 oracle
+def _views(p: torch.Tensor) -> Dict[str, torch.Tensor]:
+    from ..models import ParamLayout
+
+    lay = ParamLayout.for_model("TransformerModel")
+    return lay.unflatten(p, clone=False)
+
+
+def reference_forward(sd: Dict[str, torch.Tensor], xv: torch.Tensor, xl: torch.Tensor, masks=None) -> torch.Tensor:
+    """Functional TransformerModel forward with explicit dropout masks (None = eval)."""
+    outs = []
+    for bi, (br, x) in enumerate((("vitals", xv), ("labs", xl))):
+        pre = f"{br}_transformer."
+        h0 = F.gelu(F.linear(x, sd[f"{br}_dense.weight"], sd[f"{br}_dense.bias"]))
+        W = sd[pre + "attention.in_proj_weight"]
+        b = sd[pre + "attention.in_proj_bias"]
+        v = F.linear(h0, W[128:], b[128:])
+        if masks is not None:
+            v = v * masks[(bi, "att")].repeat_interleave(16, dim=1) / 0.9
+        o = F.linear(v, sd[pre + "attention.out_proj.weight"], sd[pre + "attention.out_proj.bias"])
+        if masks is not None:
+            o = o * masks[(bi, "d1")] / 0.9
+        x1 = F.layer_norm(h0 + o, (64,), sd[pre + "attention_norm.weight"], sd[pre + "attention_norm.bias"], 1e-5)
+        f = F.gelu(F.linear(x1, sd[pre + "ffn.0.weight"], sd[pre + "ffn.0.bias"]))
+        if masks is not None:
+            f = f * masks[(bi, "df")] / 0.9
+        f3 = F.linear(f, sd[pre + "ffn.3.weight"], sd[pre + "ffn.3.bias"])
+        if masks is not None:
+            f3 = f3 * masks[(bi, "d2")] / 0.9
+        x2 = F.layer_norm(x1 + f3, (64,), sd[pre + "ffn_norm.weight"], sd[pre + "ffn_norm.bias"], 1e-5)
+        outs.append(F.layer_norm(x2, (64,), sd[f"{br}_bn.weight"], sd[f"{br}_bn.bias"], 1e-5))
+    h = torch.cat(outs, dim=1)
+    h = F.gelu(F.linear(h, sd["fc1.weight"], sd["fc1.bias"]))
+    if masks is not None:
+        h = h * masks["head"] / 0.7
+    h = F.gelu(F.linear(h, sd["fc2.weight"], sd["fc2.bias"]))
+    return torch.sigmoid(F.linear(h, sd["output.weight"], sd["output.bias"]))
+
+
+def step_masks(seed: int, step: int, n: int) -> dict:
+    key = hash32(seed, step)
+    m = {}
+    for bi in (0, 1):
+        m[(bi, "att")] = keep_mask(key, 8 * bi + 0, n, 4, 0.1).float()
+        m[(bi, "d1")] = keep_mask(key, 8 * bi + 1, n, 64, 0.1).float()
+        m[(bi, "df")] = keep_mask(key, 8 * bi + 2, n, 6, 0.1).float()
+        m[(bi, "d2")] = keep_mask(key, 8 * bi + 3, n, 64, 0.1).float()
+    m["head"] = keep_mask(key, 16, n, 64, 0.3).float()
+    return m
+
+
+def reference_train(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
+                    lr: float, seeds: Sequence[int], opt_mode: int = 0, max_steps: int = -1):
+    """fp32 PyTorch oracle of ``train_clients`` (CPU).  Returns (ok [C], losses [C, E])."""
+    from .composite import adam_step
+
+    C = params.shape[0]
+    oks, losses = [], torch.zeros(C, epochs)
+    skip = ("in_proj_weight", "in_proj_bias")
+    for ci in range(C):
+        p = params[ci].clone()
+        sd = _views(p)
+        train_keys = [k for k in sd]
+        m = {k: torch.zeros_like(v) for k, v in sd.items()}
+        vv = {k: torch.zeros_like(v) for k, v in sd.items()}
+        n = int(nd[ci])
+        step = 0
+        ok = True
+        nbt = max(1, (n + batch - 1) // batch)
+        for e in range(epochs):
+            tot = 0.0
+            for b0 in range(0, n, batch):
+                Bn = min(batch, n - b0)
+                if Bn == 1:
+                    continue
+                if 0 <= max_steps <= step:
+                    break
+                step += 1
+                idx = order[ci, e, b0:b0 + Bn].long()
+                r = rows[idx]
+                leaf = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+                out = reference_forward(leaf, r[:, :7], r[:, 7:23], step_masks(int(seeds[ci]) & 0x7FFFFFFF, step, Bn))
+                y = r[:, 23:24]
+                loss = -(y * torch.clamp(torch.log(out), min=-100) + (1 - y) * torch.clamp(torch.log1p(-out), min=-100)).mean()
+                if torch.isnan(loss):
+                    ok = False
+                    break
+                tot += float(loss.detach())
+                loss.backward()
+                with torch.no_grad():
+                    for k in train_keys:
+                        g = leaf[k].grad
+                        if g is None:
+                            continue
+                        if k.endswith(skip):
+                            # q/k rows get exactly zero gradient at seq_len 1 (only v rows train)
+                            g = g.clone()
+                            g[:128] = 0
+                        if opt_mode == 1:
+                            sd[k].sub_(lr * g)
+                        elif k.endswith(skip):
+                            sl = slice(128, 192)
+                            adam_step(sd[k][sl], g[sl], m[k][sl], vv[k][sl], step, lr)
+                        else:
+                            adam_step(sd[k], g, m[k], vv[k], step, lr)
+            if not ok:
+                break
+            losses[ci, e] = tot / nbt
+        params[ci].copy_(p)
+        oks.append(ok)
+    return torch.tensor(oks, dtype=torch.int32), losses

@@ -1,0 +1,297 @@
+// torch bindings of the gfx950 kernels (attackfl_amd._C).  Host side only: shape checks, output
+// allocation on the caching allocator, launch on the current HIP stream.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
+
+// surface launch-configuration errors at the call that caused them
+#define AFL_CHECK_LAUNCH()                                                              \
+  do {                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                 \
+    TORCH_CHECK(e_ == hipSuccess, "HIP launch failed: ", hipGetErrorString(e_));       \
+  } while (0)
+
+void check_dev(const torch::Tensor& t, const char* name, c10::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+std::vector<torch::Tensor> colstats(torch::Tensor G, int64_t mode, double z) {
+  check_dev(G, "G", torch::kFloat32);
+  TORCH_CHECK(G.dim() == 2 && G.size(0) >= 1, "G must be [K, P]");
+  const int K = G.size(0);
+  const long P = G.size(1);
+  auto mean = torch::empty({P}, G.options());
+  auto stdv = torch::empty({P}, G.options());
+  auto out = mode == 1 ? torch::empty({P}, G.options()) : torch::empty({0}, G.options());
+  afl_colstats(G.data_ptr<float>(), K, P, mean.data_ptr<float>(), stdv.data_ptr<float>(),
+               mode == 1 ? out.data_ptr<float>() : nullptr, (float)z, (int)mode, cur());
+  AFL_CHECK_LAUNCH();
+  return {mean, stdv, out};
+}
+
+torch::Tensor pairwise_sqdist(torch::Tensor G) {
+  check_dev(G, "G", torch::kFloat32);
+  const int K = G.size(0);
+  const long P = G.size(1);
+  auto D = torch::zeros({K, K}, G.options().dtype(torch::kFloat64));
+  if (K < 2) return D;
+  TORCH_CHECK(K <= 128, "pairwise_sqdist supports K <= 128 rows");
+  const int M = K * (K - 1) / 2;
+  auto partial = torch::empty({(long)afl_pair_sqdist_nblocks(P) * M}, D.options());
+  afl_pair_sqdist(G.data_ptr<float>(), K, P, partial.data_ptr<double>(), D.data_ptr<double>(), cur());
+  AFL_CHECK_LAUNCH();
+  return D;
+}
+
+torch::Tensor segment_sqsum(torch::Tensor X, torch::Tensor tiles, torch::Tensor segf, int64_t S) {
+  check_dev(X, "X", torch::kFloat32);
+  check_dev(tiles, "tiles", torch::kInt32);
+  check_dev(segf, "segf", torch::kInt32);
+  const int rows = X.size(0);
+  const long P = X.size(1);
+  const int T = tiles.size(0);
+  auto out = torch::empty({rows, S}, X.options().dtype(torch::kFloat64));
+  auto partial = torch::empty({(long)T * rows * 2}, out.options());
+  afl_seg_reduce(0, X.data_ptr<float>(), P, rows, nullptr, nullptr, tiles.data_ptr<int>(), T, segf.data_ptr<int>(),
+                 (int)S, partial.data_ptr<double>(), out.data_ptr<double>(), nullptr, cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+std::vector<torch::Tensor> attack_coeffs(torch::Tensor G, torch::Tensor mean, torch::Tensor dev, torch::Tensor tiles,
+                                         torch::Tensor segf, int64_t S) {
+  check_dev(G, "G", torch::kFloat32);
+  check_dev(mean, "mean", torch::kFloat32);
+  check_dev(dev, "dev", torch::kFloat32);
+  const int K = G.size(0);
+  const long P = G.size(1);
+  const int rows = K + 1;
+  const int T = tiles.size(0);
+  auto o0 = torch::empty({rows, S}, G.options().dtype(torch::kFloat64));
+  auto o1 = torch::empty({rows, S}, o0.options());
+  auto partial = torch::empty({(long)T * rows * 2}, o0.options());
+  afl_seg_reduce(1, G.data_ptr<float>(), P, rows, mean.data_ptr<float>(), dev.data_ptr<float>(), tiles.data_ptr<int>(),
+                 T, segf.data_ptr<int>(), (int)S, partial.data_ptr<double>(), o0.data_ptr<double>(),
+                 o1.data_ptr<double>(), cur());
+  AFL_CHECK_LAUNCH();
+  return {o0.narrow(0, 0, K), o1.narrow(0, 0, K), o0[K]};
+}
+
+torch::Tensor spectral_norm(torch::Tensor X) {
+  check_dev(X, "X", torch::kFloat32);
+  TORCH_CHECK(X.dim() == 3, "X must be [B, r, c]");
+  const int B = X.size(0), r = X.size(1), c = X.size(2);
+  auto out = torch::empty({B}, X.options().dtype(torch::kFloat64));
+  if (B == 0) return out;
+  const int n = r <= c ? r : c;
+  if (n > 128) {
+    // rare (no model tensor has both dims > 128): exact batched SVD through the library
+    return at::linalg_matrix_norm(X.to(torch::kFloat64), 2).contiguous();
+  }
+  auto scratch = torch::empty({(long)B * afl_spectral_scratch(r, c)}, X.options());
+  TORCH_CHECK(afl_spectral(X.data_ptr<float>(), B, r, c, scratch.data_ptr<float>(), out.data_ptr<double>(), cur()) == 0,
+              "spectral_norm launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+torch::Tensor weighted_rows(torch::Tensor U, torch::Tensor w) {
+  check_dev(U, "U", torch::kFloat32);
+  check_dev(w, "w", torch::kFloat64);
+  const int N = U.size(0);
+  const long P = U.size(1);
+  TORCH_CHECK(w.numel() == N, "w must have N entries");
+  auto out = torch::empty({P}, U.options());
+  afl_weighted_rows(U.data_ptr<float>(), w.data_ptr<double>(), N, P, out.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+torch::Tensor coord_select(torch::Tensor U, int64_t mode, int64_t trim) {
+  check_dev(U, "U", torch::kFloat32);
+  const int N = U.size(0);
+  const long P = U.size(1);
+  TORCH_CHECK(N >= 1 && N <= 64, "coord_select supports 1..64 rows");
+  TORCH_CHECK(mode == 0 || 2 * trim < N, "trim too large");
+  auto out = torch::empty({P}, U.options());
+  afl_coord_select(U.data_ptr<float>(), N, P, (int)mode, (int)trim, out.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+torch::Tensor row_dots(torch::Tensor U, torch::Tensor ref, int64_t mode) {
+  check_dev(U, "U", torch::kFloat32);
+  const int N = U.size(0);
+  const long P = U.size(1);
+  if (mode) {
+    check_dev(ref, "ref", torch::kFloat32);
+    TORCH_CHECK(ref.numel() == P, "ref must have P entries");
+  }
+  auto out = torch::empty({N, 3}, U.options().dtype(torch::kFloat64));
+  auto partial = torch::empty({(long)N * afl_row_dots_nchunks(P) * 3}, out.options());
+  afl_row_dots(U.data_ptr<float>(), mode ? ref.data_ptr<float>() : nullptr, N, P, (int)mode,
+               partial.data_ptr<double>(), out.data_ptr<double>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+std::vector<torch::Tensor> stoch_quant(torch::Tensor U, int64_t seed) {
+  check_dev(U, "U", torch::kFloat32);
+  const int N = U.size(0);
+  const long P = U.size(1);
+  auto sigma = torch::empty_like(U);
+  auto smin = torch::empty({N}, U.options());
+  auto smax = torch::empty({N}, U.options());
+  afl_stoch_quant(U.data_ptr<float>(), N, P, (uint64_t)seed, sigma.data_ptr<float>(), smin.data_ptr<float>(),
+                  smax.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return {sigma, smin, smax};
+}
+
+void adam_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, int64_t step, double lr, double b1,
+               double b2, double eps, double scale) {
+  for (auto* t : {&p, &g, &m, &v}) check_dev(*t, "adam tensor", torch::kFloat32);
+  const long n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  afl_adam_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), n, (int)step,
+                (float)lr, (float)b1, (float)b2, (float)eps, (float)scale, cur());
+  AFL_CHECK_LAUNCH();
+}
+
+double roc_auc(torch::Tensor scores, torch::Tensor labels) {
+  check_dev(scores, "scores", torch::kFloat32);
+  check_dev(labels, "labels", torch::kFloat32);
+  const int n = scores.numel();
+  auto sorted = scores.sort(/*stable=*/true, /*dim=*/0, /*descending=*/true);
+  auto s = std::get<0>(sorted).contiguous();
+  auto y = labels.index_select(0, std::get<1>(sorted)).contiguous();
+  auto out = torch::empty({1}, scores.options().dtype(torch::kFloat64));
+  afl_roc_auc_sorted(s.data_ptr<float>(), y.data_ptr<float>(), n, out.data_ptr<double>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out.item<double>();
+}
+
+std::vector<torch::Tensor> hyper_delta_vjp(torch::Tensor W, torch::Tensor b, torch::Tensor f, torch::Tensor u) {
+  check_dev(W, "W", torch::kFloat32);
+  check_dev(b, "b", torch::kFloat32);
+  check_dev(f, "f", torch::kFloat32);
+  check_dev(u, "u", torch::kFloat32);
+  const long P = W.size(0);
+  const int H = W.size(1);
+  TORCH_CHECK(H <= 128, "hidden size must be <= 128");
+  auto delta = torch::empty({P}, W.options());
+  auto dfeat = torch::empty({H}, W.options());
+  auto partial = torch::empty({(long)afl_hyper_nblocks(P) * H}, W.options());
+  afl_hyper_rows(W.data_ptr<float>(), b.data_ptr<float>(), f.data_ptr<float>(), u.data_ptr<float>(), P, H,
+                 delta.data_ptr<float>(), partial.data_ptr<float>(), dfeat.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return {delta, dfeat};
+}
+
+torch::Tensor hyper_generate(torch::Tensor W, torch::Tensor b, torch::Tensor f) {
+  check_dev(W, "W", torch::kFloat32);
+  const long P = W.size(0);
+  const int H = W.size(1);
+  TORCH_CHECK(H <= 128, "hidden size must be <= 128");
+  auto out = torch::empty({P}, W.options());
+  afl_hyper_rows(W.data_ptr<float>(), b.data_ptr<float>(), f.data_ptr<float>(), nullptr, P, H, out.data_ptr<float>(),
+                 nullptr, nullptr, cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+void hyper_adam_outer(torch::Tensor W, torch::Tensor b, torch::Tensor m, torch::Tensor v, torch::Tensor delta,
+                      torch::Tensor f, int64_t step, double lr, double b1, double b2, double eps, double scale) {
+  TORCH_CHECK(W.is_cuda() && W.is_contiguous(), "W");
+  const long P = W.size(0);
+  const int H = W.size(1);
+  TORCH_CHECK(m.numel() >= P * H + P && v.numel() >= P * H + P, "moment buffers too small");
+  afl_hyper_adam(W.data_ptr<float>(), b.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                 delta.data_ptr<float>(), f.data_ptr<float>(), P, H, (int)step, (float)lr, (float)b1, (float)b2,
+                 (float)eps, (float)scale, cur());
+  AFL_CHECK_LAUNCH();
+}
+
+std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
+                                    torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
+                                    int64_t opt_mode) {
+  check_dev(params, "params", torch::kFloat32);
+  check_dev(rows, "rows", torch::kFloat32);
+  check_dev(order, "order", torch::kInt32);
+  check_dev(nd, "nd", torch::kInt32);
+  check_dev(seeds, "seeds", torch::kInt32);
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == afl_tf_param_count(), "params must be [C, 47693]");
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 24, "rows must be [N, 24]");
+  const int C = params.size(0);
+  TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
+  TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
+  const long stride = ((afl_tf_ws_floats() + 63) / 64) * 64;
+  auto ws = torch::empty({(long)C * stride}, params.options());
+  auto ok = torch::zeros({C}, order.options());
+  auto losses = torch::zeros({C, epochs}, params.options());
+  if (C == 0) return {ok, losses};
+  AflTfTrainArgs a;
+  a.params = params.data_ptr<float>();
+  a.rows = rows.data_ptr<float>();
+  a.order = order.data_ptr<int>();
+  a.nd = nd.data_ptr<int>();
+  a.seeds = (const uint32_t*)seeds.data_ptr<int>();
+  a.ws = ws.data_ptr<float>();
+  a.ws_stride = stride;
+  a.ok = ok.data_ptr<int>();
+  a.losses = losses.data_ptr<float>();
+  a.C = C;
+  a.E = (int)epochs;
+  a.maxnd = order.size(2);
+  a.batch = (int)batch;
+  a.lr = (float)lr;
+  a.opt_mode = (int)opt_mode;
+  TORCH_CHECK(afl_tf_train(&a, cur()) == 0, "tf_train launch failed");
+  AFL_CHECK_LAUNCH();
+  return {ok, losses};
+}
+
+torch::Tensor tf_eval(torch::Tensor params, torch::Tensor rows) {
+  check_dev(params, "params", torch::kFloat32);
+  check_dev(rows, "rows", torch::kFloat32);
+  TORCH_CHECK(params.numel() == afl_tf_param_count(), "params must have 47693 entries");
+  const int n = rows.size(0);
+  auto out = torch::empty({n}, rows.options());
+  auto bf = torch::empty({(long)(afl_tf_bf_ushorts() + 1) / 2}, params.options());
+  if (n == 0) return out;
+  afl_tf_eval_bf(params.data_ptr<float>(), (unsigned short*)bf.data_ptr<float>(), rows.data_ptr<float>(), n,
+                 out.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "attackfl_amd native gfx950 kernels";
+  m.def("colstats", &colstats);
+  m.def("pairwise_sqdist", &pairwise_sqdist);
+  m.def("segment_sqsum", &segment_sqsum);
+  m.def("attack_coeffs", &attack_coeffs);
+  m.def("spectral_norm", &spectral_norm);
+  m.def("weighted_rows", &weighted_rows);
+  m.def("coord_select", &coord_select);
+  m.def("row_dots", &row_dots);
+  m.def("stoch_quant", &stoch_quant);
+  m.def("adam_flat", &adam_flat);
+  m.def("roc_auc", &roc_auc);
+  m.def("hyper_delta_vjp", &hyper_delta_vjp);
+  m.def("hyper_generate", &hyper_generate);
+  m.def("hyper_adam_outer", &hyper_adam_outer);
+  m.def("tf_train", &tf_train);
+  m.def("tf_eval", &tf_eval);
+  m.def("tf_param_count", &afl_tf_param_count);
+  m.def("tf_ws_floats", &afl_tf_ws_floats);
+}

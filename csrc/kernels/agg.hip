@@ -1,0 +1,330 @@
+// Aggregation / attack kernels on the gathered client-update matrix U[N, P] (fp32, row-major).
+//
+//   colstats        column mean / unbiased std (+ LIE candidate mean + z*std)      K-G2/K-G3
+//   weighted_rows   out = sum_i w_i U_i (fp64 weights, fp64 accumulate)            K-G1 FedAvg
+//   pair_sqdist     D2[i][j] = ||U_i - U_j||^2 (difference form, no cancellation)   K-G4b / Krum
+//   seg_reduce      per-(row, state_dict tensor) partial sums over tiles             K-G4a / K-G5
+//   coord_select    coordinate-wise lower median / trimmed mean (register sort)      K-G6
+//   row_dots        <u,u>, <u,r>, <r,r> per row                                      K-G8
+//   stoch_quant     ScionFL 1-bit stochastic quantisation                            K-G9
+//   adam_flat       Adam over a flat arena (optional grad scale = clip coefficient)  K-O1
+//
+// Every reduction is two-pass with a fixed summation order (no float atomics), so results are
+// bit-identical across ranks: the replicated server state on each rank stays in lock-step.
+#include "common.h"
+#include "kernels.h"
+
+// ============================================================================ colstats
+__global__ void __launch_bounds__(256) k_colstats(const float* __restrict__ G, int K, long P, float* __restrict__ mean,
+                                                  float* __restrict__ stdv, float* __restrict__ out, float z, int mode) {
+  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P) return;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) s += (double)G[(long)k * P + c];
+  double m = s / K;
+  double ss = 0.0;
+  for (int k = 0; k < K; ++k) {
+    double d = (double)G[(long)k * P + c] - m;
+    ss += d * d;
+  }
+  float mf = (float)m;
+  float sf = K > 1 ? (float)sqrt(ss / (K - 1)) : __int_as_float(0x7fc00000);
+  mean[c] = mf;
+  stdv[c] = sf;
+  if (mode == 1) out[c] = mf + z * sf;
+}
+
+void afl_colstats(const float* G, int K, long P, float* mean, float* stdv, float* out, float z, int mode,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_colstats, dim3(afl_cdiv(P, 256)), dim3(256), 0, s, G, K, P, mean, stdv, out, z, mode);
+}
+
+// ============================================================================ weighted rows
+__global__ void __launch_bounds__(256) k_weighted_rows(const float* __restrict__ U, const double* __restrict__ w, int N,
+                                                       long P, float* __restrict__ out) {
+  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P) return;
+  double acc = 0.0;
+  for (int i = 0; i < N; ++i) acc += w[i] * (double)U[(long)i * P + c];
+  out[c] = (float)acc;
+}
+
+void afl_weighted_rows(const float* U, const double* w, int N, long P, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_weighted_rows, dim3(afl_cdiv(P, 256)), dim3(256), 0, s, U, w, N, P, out);
+}
+
+// ============================================================================ pairwise sq-dist
+// Block b stages a [K][CH] column chunk in LDS (row stride CH+1: conflict-free column reads),
+// then threads loop over pairs; partial[b][pair] (fp64) is reduced by k_pair_reduce.
+constexpr int PD_CH = 256;
+__global__ void __launch_bounds__(256) k_pair_sqdist(const float* __restrict__ G, int K, long P,
+                                                     double* __restrict__ partial) {
+  extern __shared__ float lds[];  // K * (PD_CH + 1)
+  const long c0 = (long)blockIdx.x * PD_CH;
+  const int ncol = (int)min((long)PD_CH, P - c0);
+  for (int k = 0; k < K; ++k)
+    for (int j = threadIdx.x; j < PD_CH; j += blockDim.x)
+      lds[k * (PD_CH + 1) + j] = j < ncol ? G[(long)k * P + c0 + j] : 0.f;
+  __syncthreads();
+  const int M = K * (K - 1) / 2;
+  for (int pr = threadIdx.x; pr < M; pr += blockDim.x) {
+    // pair index -> (i, j), i < j
+    int i = 0, rem = pr;
+    while (rem >= K - 1 - i) { rem -= K - 1 - i; ++i; }
+    int j = i + 1 + rem;
+    const float* a = lds + i * (PD_CH + 1);
+    const float* b = lds + j * (PD_CH + 1);
+    double acc = 0.0;
+    for (int t = 0; t < ncol; ++t) {
+      float d = a[t] - b[t];
+      acc += (double)(d * d);
+    }
+    partial[(long)blockIdx.x * M + pr] = acc;
+  }
+}
+
+__global__ void k_pair_reduce(const double* __restrict__ partial, int nb, int K, double* __restrict__ D) {
+  const int M = K * (K - 1) / 2;
+  int pr = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pr >= M) return;
+  double acc = 0.0;
+  for (int b = 0; b < nb; ++b) acc += partial[(long)b * M + pr];
+  int i = 0, rem = pr;
+  while (rem >= K - 1 - i) { rem -= K - 1 - i; ++i; }
+  int j = i + 1 + rem;
+  D[i * K + j] = acc;
+  D[j * K + i] = acc;
+}
+
+int afl_pair_sqdist_nblocks(long P) { return afl_cdiv(P, PD_CH); }
+
+void afl_pair_sqdist(const float* G, int K, long P, double* partial, double* D, hipStream_t s) {
+  int nb = afl_cdiv(P, PD_CH);
+  size_t lds = (size_t)K * (PD_CH + 1) * sizeof(float);
+  hipLaunchKernelGGL(k_pair_sqdist, dim3(nb), dim3(256), lds, s, G, K, P, partial);
+  int M = K * (K - 1) / 2;
+  if (M > 0) hipLaunchKernelGGL(k_pair_reduce, dim3(afl_cdiv(M, 256)), dim3(256), 0, s, partial, nb, K, D);
+}
+
+// ============================================================================ segmented reductions
+// tiles[t] = (segment, start, end).  Pass 1: block (t, row) -> partial[t][row][q].  Pass 2:
+// per (row, segment) sum of its tiles in order.
+//   mode 0 (sqsum):   q0 = sum x^2                       X = diffs [M, P]
+//   mode 1 (coeffs):  row < K: q0 = sum (m-g)^2, q1 = sum (m-g)*d ; row == K: q0 = sum d^2
+__global__ void __launch_bounds__(256) k_seg_pass1(int mode, const float* __restrict__ X, long P, int rows,
+                                                   const float* __restrict__ mean, const float* __restrict__ dev,
+                                                   const int* __restrict__ tiles, double* __restrict__ partial) {
+  __shared__ double scratch[8];
+  const int t = blockIdx.x, r = blockIdx.y;
+  const int st = tiles[3 * t + 1], en = tiles[3 * t + 2];
+  double q0 = 0.0, q1 = 0.0;
+  if (mode == 0) {
+    const float* x = X + (long)r * P;
+    for (int c = st + threadIdx.x; c < en; c += blockDim.x) {
+      float v = x[c];
+      q0 += (double)v * v;
+    }
+  } else if (r < rows - 1) {
+    const float* g = X + (long)r * P;
+    for (int c = st + threadIdx.x; c < en; c += blockDim.x) {
+      double a = (double)mean[c] - (double)g[c];
+      q0 += a * a;
+      q1 += a * (double)dev[c];
+    }
+  } else {
+    for (int c = st + threadIdx.x; c < en; c += blockDim.x) {
+      double d = dev[c];
+      q0 += d * d;
+    }
+  }
+  q0 = block_sum(q0, scratch);
+  q1 = block_sum(q1, scratch);
+  if (threadIdx.x == 0) {
+    partial[((long)t * rows + r) * 2 + 0] = q0;
+    partial[((long)t * rows + r) * 2 + 1] = q1;
+  }
+}
+
+__global__ void k_seg_pass2(const double* __restrict__ partial, const int* __restrict__ segf, int rows, int S,
+                            double* __restrict__ out0, double* __restrict__ out1) {
+  int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= rows * S) return;
+  int r = id / S, sg = id % S;
+  double a = 0.0, b = 0.0;
+  for (int t = segf[sg]; t < segf[sg + 1]; ++t) {
+    a += partial[((long)t * rows + r) * 2 + 0];
+    b += partial[((long)t * rows + r) * 2 + 1];
+  }
+  out0[(long)r * S + sg] = a;
+  if (out1) out1[(long)r * S + sg] = b;
+}
+
+void afl_seg_reduce(int mode, const float* X, long P, int rows, const float* mean, const float* dev, const int* tiles,
+                    int T, const int* segf, int S, double* partial, double* out0, double* out1, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_pass1, dim3(T, rows), dim3(256), 0, s, mode, X, P, rows, mean, dev, tiles, partial);
+  hipLaunchKernelGGL(k_seg_pass2, dim3(afl_cdiv((long)rows * S, 256)), dim3(256), 0, s, partial, segf, rows, S, out0,
+                     out1);
+}
+
+// ============================================================================ coordinate select
+// Each thread owns one column: N values in registers, odd-even transposition sort network with
+// compile-time indices (NMAX template; padding +inf), then lower-median or trimmed mean.
+template <int NMAX>
+__global__ void __launch_bounds__(256) k_coord_select(const float* __restrict__ U, int N, long P, int mode, int trim,
+                                                      float* __restrict__ out) {
+  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P) return;
+  float v[NMAX];
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) v[i] = i < N ? U[(long)i * P + c] : __int_as_float(0x7f800000);
+#pragma unroll
+  for (int r = 0; r < NMAX; ++r) {
+#pragma unroll
+    for (int i = (r & 1); i + 1 < NMAX; i += 2) {
+      float a = v[i], b = v[i + 1];
+      // NaN-aware: torch.sort/median place NaN last (treated as largest)
+      bool sw = (a > b) || (a != a && b == b);
+      v[i] = sw ? b : a;
+      v[i + 1] = sw ? a : b;
+    }
+  }
+  float r = 0.f;
+  if (mode == 0) {
+    const int mid = (N - 1) / 2;
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i) r = (i == mid) ? v[i] : r;
+  } else {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i) acc += (i >= trim && i < N - trim) ? v[i] : 0.f;
+    r = acc / (float)(N - 2 * trim);
+  }
+  out[c] = r;
+}
+
+void afl_coord_select(const float* U, int N, long P, int mode, int trim, float* out, hipStream_t s) {
+  dim3 g(afl_cdiv(P, 256)), b(256);
+  if (N <= 8) hipLaunchKernelGGL(k_coord_select<8>, g, b, 0, s, U, N, P, mode, trim, out);
+  else if (N <= 16) hipLaunchKernelGGL(k_coord_select<16>, g, b, 0, s, U, N, P, mode, trim, out);
+  else if (N <= 32) hipLaunchKernelGGL(k_coord_select<32>, g, b, 0, s, U, N, P, mode, trim, out);
+  else hipLaunchKernelGGL(k_coord_select<64>, g, b, 0, s, U, N, P, mode, trim, out);
+}
+
+// ============================================================================ row dots
+constexpr int RD_CH = 8192;
+__global__ void __launch_bounds__(256) k_row_dots(const float* __restrict__ U, const float* __restrict__ ref, long P,
+                                                  int mode, double* __restrict__ partial) {
+  __shared__ double scratch[8];
+  const int ch = blockIdx.x, r = blockIdx.y;
+  const long st = (long)ch * RD_CH, en = min(P, st + RD_CH);
+  const float* u = U + (long)r * P;
+  double uu = 0, ur = 0, rr = 0;
+  for (long c = st + threadIdx.x; c < en; c += blockDim.x) {
+    double a = u[c];
+    uu += a * a;
+    if (mode) {
+      double b = ref[c];
+      ur += a * b;
+      rr += b * b;
+    }
+  }
+  uu = block_sum(uu, scratch);
+  ur = block_sum(ur, scratch);
+  rr = block_sum(rr, scratch);
+  if (threadIdx.x == 0) {
+    double* p = partial + ((long)r * gridDim.x + ch) * 3;
+    p[0] = uu;
+    p[1] = ur;
+    p[2] = rr;
+  }
+}
+
+__global__ void k_row_dots_reduce(const double* __restrict__ partial, int N, int nch, double* __restrict__ out) {
+  int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= N * 3) return;
+  int r = id / 3, q = id % 3;
+  double a = 0;
+  for (int c = 0; c < nch; ++c) a += partial[((long)r * nch + c) * 3 + q];
+  out[r * 3 + q] = a;
+}
+
+int afl_row_dots_nchunks(long P) { return afl_cdiv(P, RD_CH); }
+
+void afl_row_dots(const float* U, const float* ref, int N, long P, int mode, double* partial, double* out,
+                  hipStream_t s) {
+  int nch = afl_cdiv(P, RD_CH);
+  hipLaunchKernelGGL(k_row_dots, dim3(nch, N), dim3(256), 0, s, U, ref, P, mode, partial);
+  hipLaunchKernelGGL(k_row_dots_reduce, dim3(afl_cdiv(N * 3, 256)), dim3(256), 0, s, partial, N, nch, out);
+}
+
+// ============================================================================ ScionFL quantisation
+__global__ void __launch_bounds__(256) k_row_minmax(const float* __restrict__ U, long P, float* __restrict__ smin,
+                                                    float* __restrict__ smax) {
+  __shared__ float smn[4], smx[4];
+  const float* u = U + (long)blockIdx.x * P;
+  float mn = __int_as_float(0x7f800000), mx = -mn;
+  for (long c = threadIdx.x; c < P; c += blockDim.x) {
+    float a = u[c];
+    mn = fminf(mn, a);
+    mx = fmaxf(mx, a);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    smn[w] = mn;
+    smx[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      mn = fminf(mn, smn[i]);
+      mx = fmaxf(mx, smx[i]);
+    }
+    mn = fminf(mn, smn[0]);
+    mx = fmaxf(mx, smx[0]);
+    smin[blockIdx.x] = mn;
+    smax[blockIdx.x] = mx;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_stoch_quant(const float* __restrict__ U, long P, long total,
+                                                     const float* __restrict__ smin, const float* __restrict__ smax,
+                                                     uint64_t seed, float* __restrict__ sigma) {
+  long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= total) return;
+  long r = id / P;
+  float lo = smin[r], hi = smax[r];
+  float p = (U[id] - lo) / (hi - lo + 1e-6f);
+  sigma[id] = afl_uniform(seed, (uint64_t)id) < p ? 1.f : 0.f;
+}
+
+void afl_stoch_quant(const float* U, int N, long P, uint64_t seed, float* sigma, float* smin, float* smax,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_row_minmax, dim3(N), dim3(256), 0, s, U, P, smin, smax);
+  long total = (long)N * P;
+  hipLaunchKernelGGL(k_stoch_quant, dim3(afl_cdiv(total, 256)), dim3(256), 0, s, U, P, total, smin, smax, seed, sigma);
+}
+
+// ============================================================================ Adam (flat)
+// torch.optim.Adam (foreach=False) math: m <- m + (1-b1)(g-m); v <- b2 v + (1-b2) g^2;
+// p <- p - (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps).  `gscale` folds in a clip coefficient.
+__global__ void __launch_bounds__(256) k_adam_flat(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n, float lr_bc1,
+                                                   float rsqrt_bc2, float b1, float b2, float eps, float gscale) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = g[i] * gscale;
+  float mi = m[i] + (1.f - b1) * (gi - m[i]);
+  float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  p[i] -= lr_bc1 * mi / (sqrtf(vi) * rsqrt_bc2 + eps);
+}
+
+void afl_adam_flat(float* p, const float* g, float* m, float* v, long n, int step, float lr, float b1, float b2,
+                   float eps, float gscale, hipStream_t s) {
+  double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+  hipLaunchKernelGGL(k_adam_flat, dim3(afl_cdiv(n, 256)), dim3(256), 0, s, p, g, m, v, n, (float)(lr / bc1),
+                     (float)(1.0 / sqrt(bc2)), b1, b2, eps, gscale);
+}

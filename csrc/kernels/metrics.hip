@@ -1,0 +1,106 @@
+// ROC-AUC over scores sorted in descending order (sort done by the binding), with sklearn's tie
+// handling: one ROC point per distinct threshold, trapezoidal area.
+// Single workgroup of 1024 threads; chunked inclusive scans in LDS with carries between chunks.
+#include "common.h"
+#include "kernels.h"
+
+constexpr int AUC_T = 1024;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_incl_max(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o, 64);
+    if (lane >= o) v = v > t ? v : t;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(AUC_T) k_roc_auc(const float* __restrict__ s, const float* __restrict__ y, int n,
+                                                   double* __restrict__ out) {
+  __shared__ int wsum[16], wmax[16];
+  __shared__ int tp_l[AUC_T];
+  __shared__ double dred[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int carry_tp = 0;           // positives before this chunk
+  int carry_end = -1;         // global index of the last tie-group end before this chunk
+  int carry_end_tp = 0;       // tp at that end
+  double area = 0.0;          // sum of trapezoids * 2 (in count units)
+  for (int base = 0; base < n; base += AUC_T) {
+    const int i = base + tid;
+    const bool valid = i < n;
+    const float si = valid ? s[i] : 0.f;
+    const int yi = valid ? (y[i] > 0.5f ? 1 : 0) : 0;
+    const bool end = valid && (i == n - 1 || s[i + 1] != si);
+    // inclusive scan of y
+    int sc = wave_incl_scan(yi);
+    if (lane == 63) wsum[w] = sc;
+    // inclusive max-scan of end indices
+    int me = wave_incl_max(end ? i : -1);
+    if (lane == 63) wmax[w] = me;
+    __syncthreads();
+    int off = 0, pm = -1;
+    for (int k = 0; k < w; ++k) {
+      off += wsum[k];
+      pm = pm > wmax[k] ? pm : wmax[k];
+    }
+    const int tp = carry_tp + off + sc;
+    tp_l[tid] = tp;
+    // exclusive max of ends = previous end strictly before i
+    int prev_in_wave = __shfl_up(me, 1, 64);
+    if (lane == 0) prev_in_wave = -1;
+    int prev = prev_in_wave > pm ? prev_in_wave : pm;
+    __syncthreads();
+    if (end) {
+      int tp_prev, fp_prev;
+      if (prev >= base) {
+        tp_prev = tp_l[prev - base];
+        fp_prev = prev + 1 - tp_prev;
+      } else if (carry_end >= 0) {
+        tp_prev = carry_end_tp;
+        fp_prev = carry_end + 1 - carry_end_tp;
+      } else {
+        tp_prev = 0;
+        fp_prev = 0;
+      }
+      const int fp = i + 1 - tp;
+      area += (double)(fp - fp_prev) * (double)(tp + tp_prev);
+    }
+    // carries for the next chunk
+    int last_end = pm;
+    int tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      tot += wsum[k];
+      last_end = last_end > wmax[k] ? last_end : wmax[k];
+    }
+    if (last_end >= base) {
+      carry_end_tp = tp_l[last_end - base];
+      carry_end = last_end;
+    }
+    carry_tp += tot;
+    __syncthreads();
+  }
+  area = wave_sum(area);
+  if (lane == 0) dred[w] = area;
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0;
+    for (int k = 0; k < 16; ++k) a += dred[k];
+    double P = (double)carry_tp, N = (double)n - P;
+    out[0] = (P > 0 && N > 0) ? a * 0.5 / (P * N) : __longlong_as_double(0x7ff8000000000000ll);
+  }
+}
+
+void afl_roc_auc_sorted(const float* s, const float* y, int n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_roc_auc, dim3(1), dim3(AUC_T), 0, st, s, y, n, out);
+}

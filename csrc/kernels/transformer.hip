@@ -1,0 +1,977 @@
+// Fused TransformerModel/ICU local training — ONE persistent launch trains every client of a rank
+// for all its local epochs (reference training loop client.py:75-111, model src/Model.py:166-246).
+//
+// Grid = one 512-thread workgroup (8 waves) per client.  Per optimizer step (batch <= 128 rows):
+//   forward  : 2 branches (dense->GELU -> L=1 MHA (== out_proj(dropout_head(v_proj))) -> +res LN ->
+//              FFN(64->6->64, GELU) -> +res LN -> LN) -> head (128->64 GELU drop0.3 ->32 GELU ->1 sigmoid)
+//   loss     : BCE (log clamped at -100); NaN -> client result False (client.py:100-102)
+//   backward : hand-written VJPs of every op; weight gradients never leave the MFMA accumulators:
+//              the dW GEMM epilogue applies Adam directly (torch.optim.Adam math, fresh per round)
+//
+// GEMMs run on v_mfma_f32_16x16x32_bf16 (bf16 operands, fp32 accumulate):
+//   X.W^T and dY.W  : activation fragments from LDS (ds_read_b128), weight fragments from
+//                     bf16 copies in global memory (row and transposed layouts, rewritten by Adam)
+//   dW = dY^T.X     : both operands from LDS through the gfx950 transposed read ds_read_b64_tr_b16
+// Elementwise work (bias, exact-erf GELU, dropout, residual, LayerNorm fwd/bwd, BCE) runs in fp32
+// in a row-per-4-lanes layout between GEMM phases.  Master weights, Adam moments and activations
+// saved for the backward pass are fp32 in a per-client global workspace (L2 resident).
+//
+// Attention at seq_len 1: softmax over one key is exactly 1, so the output is
+// out_proj(dropout(v_proj(x))) with the dropout mask per (row, head) (SDPA math path), and the
+// q/k projections receive exactly zero gradient (softmax backward at L=1 is 0) — Adam leaves
+// them unchanged, so they are skipped here bit-for-bit.
+// Dropout masks come from a stateless hash of (client seed, step, layer, row, col), regenerated in
+// backward; bitwise parity with torch's Philox stream is impossible by construction.
+#include "common.h"
+#include "kernels.h"
+#include "tf_common.h"
+
+using namespace tf;
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+
+
+
+namespace {
+
+constexpr int NT = 512;
+constexpr int BM = 128;  // max rows per batch
+// LDS map (bytes)
+constexpr int LD64 = 72, LD32 = 40, LD128 = 136, LDACC = 68;
+constexpr int S_ACC = 0;
+constexpr int S_XIN = S_ACC + BM * LDACC * 4;     // 34816 ; XIN / DF0  [128][40] bf16
+constexpr int S_TA = S_XIN + BM * LD32 * 2;       // 45056
+constexpr int S_TB = S_TA + BM * LD64 * 2;        // 63488
+constexpr int S_TC = S_TB + BM * LD64 * 2;        // 81920
+constexpr int S_CAT = S_TC + BM * LD64 * 2;       // 100352 ; CAT [128][136] / TD [128][72]
+constexpr int S_F2 = S_CAT + BM * LD128 * 2;      // 135168 ; F2 / T32 [128][40]
+constexpr int S_CS = S_F2 + BM * LD32 * 2;        // 145408 ; CS fp32 [6][8][64]
+constexpr int S_LAB = S_CS + 6 * 8 * 64 * 4;      // 157696
+constexpr int S_DY3 = S_LAB + BM * 4;             // 158208
+constexpr int S_RED = S_DY3 + BM * 4;             // 158720
+constexpr int S_TOTAL = S_RED + 16 * 4;           // 158784
+static_assert(S_TOTAL <= 160 * 1024, "LDS budget");
+
+// ---- workspace layout (float units) ----
+constexpr long W_M = 0, W_V = NPARAM;
+constexpr long W_BF = ((2L * NPARAM + 63) / 64) * 64;  // bf16 region (16-B aligned)
+// bf16 weight copies (ushort offsets inside the bf16 region), per branch then head
+struct BrW { int WFd, WFv, WTv, WFo, WTo, WF1, WT1, WF2, WT2; };
+__host__ __device__ constexpr BrW brw(int base) {
+  BrW w{};
+  int p = base;
+  w.WFd = p; p += 64 * 32;
+  w.WFv = p; p += 64 * 64;
+  w.WTv = p; p += 64 * 64;
+  w.WFo = p; p += 64 * 64;
+  w.WTo = p; p += 64 * 64;
+  w.WF1 = p; p += 16 * 64;
+  w.WT1 = p; p += 64 * 32;
+  w.WF2 = p; p += 64 * 32;
+  w.WT2 = p; p += 16 * 64;
+  return w;
+}
+constexpr int BRW_SIZE = 64 * 32 + 4 * 64 * 64 + 16 * 64 + 64 * 32 + 64 * 32 + 16 * 64;  // 24576
+constexpr BrW WBV = brw(0);
+constexpr BrW WBL = brw(BRW_SIZE);
+constexpr int WFF1 = 2 * BRW_SIZE, WTF1 = WFF1 + 64 * 128, WFF2 = WTF1 + 128 * 64, WTF2 = WFF2 + 32 * 64;
+constexpr int BF_TOTAL = WTF2 + 64 * 32;  // ushorts
+// saved activations (float offsets from W_ACT)
+constexpr long W_ACT = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
+struct BrS { long H0F, H0B, XH1, R1, X1F, F0, XH2, R2, XH3, R3, DX1F, DH0F; };
+__host__ __device__ constexpr BrS brs(long base) {
+  BrS s{};
+  long p = base;
+  s.H0F = p; p += BM * 64;
+  s.H0B = p; p += BM * 64 / 2;
+  s.XH1 = p; p += BM * 64;
+  s.R1 = p; p += BM;
+  s.X1F = p; p += BM * 64;
+  s.F0 = p; p += BM * 8;
+  s.XH2 = p; p += BM * 64;
+  s.R2 = p; p += BM;
+  s.XH3 = p; p += BM * 64;
+  s.R3 = p; p += BM;
+  s.DX1F = p; p += BM * 64;
+  s.DH0F = p; p += BM * 64;
+  return s;
+}
+constexpr long BRS_SIZE = 8L * BM * 64 + BM * 32 + BM * 8 + 3 * BM;
+constexpr BrS SV = brs(W_ACT);
+constexpr BrS SL = brs(W_ACT + BRS_SIZE);
+constexpr long W_Y1 = W_ACT + 2 * BRS_SIZE, W_Y2 = W_Y1 + BM * 64, W_DX3V = W_Y2 + BM * 32;
+constexpr long WS_FLOATS = W_DX3V + BM * 64;
+
+struct AdamK {
+  float lr_bc1, rsqrt_bc2;
+  float sgd_lr;  // > 0: test mode, plain SGD p -= sgd_lr * g (exposes raw gradients to the tests)
+};
+constexpr float B1 = 0.9f, B2 = 0.999f, EPS = 1e-8f;
+
+__device__ __forceinline__ float adam(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int idx,
+                                      float g, AdamK k) {
+  if (k.sgd_lr > 0.f) {
+    float pn = p[idx] - k.sgd_lr * g;
+    p[idx] = pn;
+    return pn;
+  }
+  float mi = m[idx] + (1.f - B1) * (g - m[idx]);
+  float vi = B2 * v[idx] + (1.f - B2) * g * g;
+  m[idx] = mi;
+  v[idx] = vi;
+  float pn = p[idx] - k.lr_bc1 * mi / (sqrtf(vi) * k.rsqrt_bc2 + EPS);
+  p[idx] = pn;
+  return pn;
+}
+
+struct Ctx {
+  unsigned char* smem;
+  float* P;          // master params of this client
+  float* M;
+  float* V;
+  unsigned short* BF;  // bf16 weight copies
+  float* ws;
+  int tid, lane, wave;
+
+  __device__ float* acc() const { return (float*)(smem + S_ACC); }
+  __device__ unsigned short* u16(int off) const { return (unsigned short*)(smem + off); }
+  __device__ float* cs(int v) const { return (float*)(smem + S_CS) + v * 8 * 64; }
+  __device__ float* wsf(long off) const { return ws + off; }
+};
+
+// ---------------------------------------------------------------- fragments
+__device__ __forceinline__ s8v lds_row_frag(const unsigned short* base, int ld, int r0, int k0, int lane) {
+  const unsigned short* p = base + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4);
+  return *(const LDS_AS s8v*)p;
+}
+// A[m][k] = S[k][m] (S row-major [k rows][m cols]); two transposed 4x16 reads per 16-lane group
+__device__ __forceinline__ s8v lds_col_frag(const unsigned short* S, int ld, int k0, int m0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const unsigned short* a1 = S + (k0 + 8 * g + q) * ld + m0 + 4 * p;
+  const unsigned short* a2 = a1 + 4 * ld;
+  s4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a1);
+  s4v r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a2);
+  s8v r;
+  r[0] = r1[0]; r[1] = r1[1]; r[2] = r1[2]; r[3] = r1[3];
+  r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
+  return r;
+}
+__device__ __forceinline__ s8v glb_frag(const unsigned short* W, int ldk, int n0, int k0, int lane) {
+  return *(const s8v*)(W + (n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+}
+__device__ __forceinline__ f4v mfma(s8v a, s8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+// ACC[128][N] = A[128][K] (LDS bf16, ld lda) x W^T, W = global bf16 [N][K] row-major
+template <int N, int K>
+__device__ __forceinline__ void gemm_xw(const Ctx& c, const unsigned short* A, int lda, const unsigned short* W) {
+  constexpr int NTL = N / 16;
+  f4v acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int r0 = 16 * c.wave;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    s8v a = lds_row_frag(A, lda, r0, k0, c.lane);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, glb_frag(W, K, 16 * t, k0, c.lane), acc[t]);
+  }
+  float* out = c.acc();
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
+}
+
+// Matrix weight descriptor for the dW+Adam epilogue
+struct MatW {
+  int off;      // param offset of W[n][k]
+  int n_real, k_real;
+  int wf, wf_ld;  // bf16 WF [n][k] copy (ushort offset in BF region, row stride)
+  int wt, wt_ld;  // bf16 WT [k][n] copy (-1 = none)
+};
+
+// dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows, then Adam on the real entries
+template <int MT, int NTL>
+__device__ __forceinline__ void gemm_dw_adam(const Ctx& c, const unsigned short* DY, int ldy, const unsigned short* X,
+                                             int ldx, MatW mw, AdamK k) {
+  for (int t = c.wave; t < MT * NTL; t += 8) {
+    const int mt = t / NTL, nt = t % NTL;
+    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b0 = 0; b0 < BM; b0 += 32)
+      acc = mfma(lds_col_frag(DY, ldy, b0, 16 * mt, c.lane), lds_col_frag(X, ldx, b0, 16 * nt, c.lane), acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 16 * mt + 4 * (c.lane >> 4) + i, kk = 16 * nt + (c.lane & 15);
+      if (n < mw.n_real && kk < mw.k_real) {
+        float pn = adam(c.P, c.M, c.V, mw.off + n * mw.k_real + kk, acc[i], k);
+        unsigned short h = f2bf(pn);
+        c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+        if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
+      }
+    }
+  }
+}
+
+// column partial sums of 16 values per thread (row-per-4-lanes layout, 64-wide rows):
+// lanes sharing (lane & 3) are reduced -> CS[v][wave][q*16 + j]
+__device__ __forceinline__ void colsum16(const Ctx& c, int v, const float (&x)[16]) {
+  float s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    float a = x[j];
+    a += __shfl_xor(a, 4, 64);
+    a += __shfl_xor(a, 8, 64);
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    s[j] = a;
+  }
+  if (c.lane < 4) {
+    float* d = c.cs(v) + c.wave * 64 + c.lane * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = s[j];
+  }
+}
+template <int W>
+__device__ __forceinline__ void colsumW(const Ctx& c, int v, const float (&x)[W], int colbase) {
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    float a = x[j];
+    a += __shfl_xor(a, 4, 64);
+    a += __shfl_xor(a, 8, 64);
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    if (c.lane < 4) c.cs(v)[c.wave * 64 + colbase + j] = a;
+  }
+}
+__device__ __forceinline__ float cs_total(const Ctx& c, int v, int col) {
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) s += c.cs(v)[w * 64 + col];
+  return s;
+}
+
+// row-wise sum over the 4 lanes of a row
+__device__ __forceinline__ float rsum4(float a) {
+  a += __shfl_xor(a, 1, 64);
+  a += __shfl_xor(a, 2, 64);
+  return a;
+}
+
+// LayerNorm forward on 16 values/lane (64-wide row): returns xhat in place, rstd
+__device__ __forceinline__ float ln_fwd(float (&x)[16]) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += x[j];
+  const float mean = rsum4(s) * (1.f / 64.f);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    x[j] -= mean;
+    ss += x[j] * x[j];
+  }
+  const float var = rsum4(ss) * (1.f / 64.f);
+  const float rstd = 1.f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] *= rstd;
+  return rstd;
+}
+// LayerNorm backward: dy -> dx given xhat, rstd, gamma (per column)
+__device__ __forceinline__ void ln_bwd(float (&dx)[16], const float (&dy)[16], const float (&xh)[16], float rstd,
+                                       const float* gamma, int c0) {
+  float a = 0.f, b = 0.f, g[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    g[j] = dy[j] * gamma[c0 + j];
+    a += g[j];
+    b += g[j] * xh[j];
+  }
+  a = rsum4(a) * (1.f / 64.f);
+  b = rsum4(b) * (1.f / 64.f);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dx[j] = rstd * (g[j] - a - xh[j] * b);
+}
+
+__device__ __forceinline__ void load16(float (&x)[16], const float* p) {
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) {
+    float4 v = *(const float4*)(p + j);
+    x[j] = v.x; x[j + 1] = v.y; x[j + 2] = v.z; x[j + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void store16(float* p, const float (&x)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) *(float4*)(p + j) = make_float4(x[j], x[j + 1], x[j + 2], x[j + 3]);
+}
+__device__ __forceinline__ void store16bf(unsigned short* p, const float (&x)[16]) {
+  s8v a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (short)f2bf(x[j]);
+    b[j] = (short)f2bf(x[j + 8]);
+  }
+  *(LDS_AS s8v*)p = a;
+  *(LDS_AS s8v*)(p + 8) = b;
+}
+
+// write the bf16 copies of one matrix from the master params
+__device__ void init_copies(const Ctx& c, MatW mw) {
+  for (int e = c.tid; e < mw.n_real * mw.k_real; e += NT) {
+    const int n = e / mw.k_real, kk = e % mw.k_real;
+    unsigned short h = f2bf(c.P[mw.off + e]);
+    c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+    if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
+  }
+}
+
+struct Branch {
+  BrOff o;
+  BrW w;
+  BrS s;
+  int din, xoff, br;
+  __device__ MatW dense() const { return MatW{o.dense_w, 64, din, w.WFd, 32, -1, 0}; }
+  __device__ MatW vproj() const { return MatW{o.inproj_w + 128 * 64, 64, 64, w.WFv, 64, w.WTv, 64}; }
+  __device__ MatW oproj() const { return MatW{o.out_w, 64, 64, w.WFo, 64, w.WTo, 64}; }
+  __device__ MatW ff0() const { return MatW{o.ff0_w, 6, 64, w.WF1, 64, w.WT1, 32}; }
+  __device__ MatW ff3() const { return MatW{o.ff3_w, 64, 6, w.WF2, 32, w.WT2, 64}; }
+};
+
+__device__ __forceinline__ Branch branch(int br) {
+  Branch b;
+  b.o = br == 0 ? OV : OL;
+  b.w = br == 0 ? WBV : WBL;
+  b.s = br == 0 ? SV : SL;
+  b.din = br == 0 ? D_V : D_L;
+  b.xoff = br == 0 ? 0 : D_V;
+  b.br = br;
+  return b;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int cid = blockIdx.x;
+  Ctx c;
+  c.smem = smem;
+  c.P = a.params + (long)cid * NPARAM;
+  c.ws = a.ws + (long)cid * a.ws_stride;
+  c.M = c.ws + W_M;
+  c.V = c.ws + W_V;
+  c.BF = (unsigned short*)(c.ws + W_BF);
+  c.tid = threadIdx.x;
+  c.lane = threadIdx.x & 63;
+  c.wave = threadIdx.x >> 6;
+  const int tid = c.tid;
+  const int r = tid >> 2, q = tid & 3;  // row-per-4-lanes layout
+
+  // ---- init: zero Adam moments, bf16 weight copies (padding zeroed first) ----
+  for (int i = tid; i < NPARAM; i += NT) {
+    c.M[i] = 0.f;
+    c.V[i] = 0.f;
+  }
+  for (int i = tid; i < BF_TOTAL; i += NT) c.BF[i] = 0;
+  __syncthreads();
+  for (int br = 0; br < 2; ++br) {
+    Branch B = branch(br);
+    init_copies(c, B.dense());
+    init_copies(c, B.vproj());
+    init_copies(c, B.oproj());
+    init_copies(c, B.ff0());
+    init_copies(c, B.ff3());
+  }
+  init_copies(c, MatW{FC1_W, 64, 128, WFF1, 128, WTF1, 64});
+  init_copies(c, MatW{FC2_W, 32, 64, WFF2, 64, WTF2, 32});
+  // zero LDS once (padding columns of operand buffers must be finite)
+  for (int i = tid; i < S_TOTAL / 4; i += NT) ((float*)smem)[i] = 0.f;
+  __syncthreads();
+
+  const int nd = a.nd[cid];
+  const int BS = a.batch;
+  const int nb_total = (nd + BS - 1) / BS;
+  const uint32_t seed = a.seeds[cid];
+  double b1t = 1.0, b2t = 1.0;
+  int step = 0;
+  bool failed = false;
+  const float* rows = a.rows;
+  float* LAB = (float*)(smem + S_LAB);
+  float* DY3 = (float*)(smem + S_DY3);
+  float* RED = (float*)(smem + S_RED);
+  unsigned short* XIN = c.u16(S_XIN);
+  unsigned short* TA = c.u16(S_TA);
+  unsigned short* TB = c.u16(S_TB);
+  unsigned short* TC = c.u16(S_TC);
+  unsigned short* CAT = c.u16(S_CAT);
+  unsigned short* F2 = c.u16(S_F2);
+  float* ACC = c.acc();
+  const MatW mfc1{FC1_W, 64, 128, WFF1, 128, WTF1, 64};
+  const MatW mfc2{FC2_W, 32, 64, WFF2, 64, WTF2, 32};
+
+  for (int e = 0; e < a.E && !failed; ++e) {
+    const int* ord = a.order + ((long)cid * a.E + e) * a.maxnd;
+    float epoch_loss = 0.f;
+    for (int b0 = 0; b0 < nd; b0 += BS) {
+      const int Bn = min(BS, nd - b0);
+      if (Bn == 1) continue;  // reference skips size-1 batches (client.py:86-87)
+      ++step;
+      b1t *= (double)B1;
+      b2t *= (double)B2;
+      const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+      const uint32_t key = afl_hash32(seed, (uint32_t)step);
+      const bool valid = r < Bn;
+      const int ridx = valid ? ord[b0 + r] : 0;
+
+      // =============================== forward ===============================
+      for (int br = 0; br < 2; ++br) {
+        const Branch B = branch(br);
+        // P0: gather inputs
+        {
+          s8v v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            float x = (valid && col < B.din) ? rows[(long)ridx * ROW + B.xoff + col] : 0.f;
+            v[j] = (short)f2bf(x);
+          }
+          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
+          if (br == 0 && q == 0) LAB[r] = valid ? rows[(long)ridx * ROW + ROW - 1] : 0.f;
+        }
+        __syncthreads();
+        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WFd);
+        __syncthreads();
+        // E1: h0 = gelu(z0)
+        {
+          float h[16];
+          const int c0 = q * 16;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + c.P[B.o.dense_b + c0 + j]);
+          store16bf(TA + r * LD64 + c0, h);
+          store16(c.wsf(B.s.H0F) + r * 64 + c0, h);
+          unsigned short* hb = (unsigned short*)c.wsf(B.s.H0B) + r * 64 + c0;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) hb[j] = f2bf(h[j]);
+        }
+        __syncthreads();
+        gemm_xw<64, 64>(c, TA, LD64, c.BF + B.w.WFv);
+        __syncthreads();
+        // E2: a = head_dropout(v)
+        {
+          float x[16];
+          const int c0 = q * 16;
+          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;  // head = c0/16 = q
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B.o.inproj_b + 128 + c0 + j]) * m;
+          store16bf(TB + r * LD64 + c0, x);
+        }
+        __syncthreads();
+        gemm_xw<64, 64>(c, TB, LD64, c.BF + B.w.WFo);
+        __syncthreads();
+        // E3: r1 = h0 + drop(o); x1 = LN1(r1)
+        {
+          float x[16], h[16];
+          const int c0 = q * 16;
+          load16(h, c.wsf(B.s.H0F) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float o = ACC[r * LDACC + c0 + j] + c.P[B.o.out_b + c0 + j];
+            x[j] = h[j] + (keep(key, 8 * br + L_D1, r, c0 + j, THR_P01) ? o * INV_K01 : 0.f);
+          }
+          const float rstd = ln_fwd(x);
+          store16(c.wsf(B.s.XH1) + r * 64 + c0, x);
+          if (q == 0) c.wsf(B.s.R1)[r] = rstd;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.ln1_w + c0 + j] + c.P[B.o.ln1_b + c0 + j];
+          store16(c.wsf(B.s.X1F) + r * 64 + c0, x);
+          store16bf(TC + r * LD64 + c0, x);
+        }
+        __syncthreads();
+        gemm_xw<16, 64>(c, TC, LD64, c.BF + B.w.WF1);
+        __syncthreads();
+        // E4: f0 -> f2 = drop(gelu(f0)) (cols 0..5; rest of the K=32 operand zeroed)
+        {
+          s8v v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            float f2 = 0.f;
+            if (col < FF) {
+              const float f0 = ACC[r * LDACC + col] + c.P[B.o.ff0_b + col];
+              c.wsf(B.s.F0)[r * 8 + col] = f0;
+              f2 = keep(key, 8 * br + L_DF, r, col, THR_P01) ? gelu(f0) * INV_K01 : 0.f;
+            }
+            v[j] = (short)f2bf(f2);
+          }
+          *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
+        }
+        __syncthreads();
+        gemm_xw<64, 32>(c, F2, LD32, c.BF + B.w.WF2);
+        __syncthreads();
+        // E5: r2 = x1 + drop(f3); x2 = LN2(r2); x3 = LN3(x2) -> CAT
+        {
+          float x[16], x1[16];
+          const int c0 = q * 16;
+          load16(x1, c.wsf(B.s.X1F) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float f3 = ACC[r * LDACC + c0 + j] + c.P[B.o.ff3_b + c0 + j];
+            x[j] = x1[j] + (keep(key, 8 * br + L_D2, r, c0 + j, THR_P01) ? f3 * INV_K01 : 0.f);
+          }
+          float rstd = ln_fwd(x);
+          store16(c.wsf(B.s.XH2) + r * 64 + c0, x);
+          if (q == 0) c.wsf(B.s.R2)[r] = rstd;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.ln2_w + c0 + j] + c.P[B.o.ln2_b + c0 + j];
+          rstd = ln_fwd(x);
+          store16(c.wsf(B.s.XH3) + r * 64 + c0, x);
+          if (q == 0) c.wsf(B.s.R3)[r] = rstd;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.bn_w + c0 + j] + c.P[B.o.bn_b + c0 + j];
+          store16bf(CAT + r * LD128 + br * 64 + c0, x);
+        }
+        __syncthreads();
+      }
+      // =============================== head forward + loss ===============================
+      gemm_xw<64, 128>(c, CAT, LD128, c.BF + WFF1);
+      __syncthreads();
+      {  // E6: y1 -> d1 = drop0.3(gelu(y1))
+        float x[16], y[16];
+        const int c0 = q * 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          y[j] = ACC[r * LDACC + c0 + j] + c.P[FC1_B + c0 + j];
+          x[j] = keep(key, L_HEAD, r, c0 + j, THR_P03) ? gelu(y[j]) * INV_K03 : 0.f;
+        }
+        store16(c.wsf(W_Y1) + r * 64 + c0, y);
+        store16bf(TA + r * LD64 + c0, x);
+      }
+      __syncthreads();
+      gemm_xw<32, 64>(c, TA, LD64, c.BF + WFF2);
+      __syncthreads();
+      {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
+        float y2[8], g2[8], dot = 0.f;
+        const int c0 = q * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          y2[j] = ACC[r * LDACC + c0 + j] + c.P[FC2_B + c0 + j];
+          g2[j] = gelu(y2[j]);
+          dot += g2[j] * c.P[OUT_W + c0 + j];
+        }
+        const float y3 = rsum4(dot) + c.P[OUT_B];
+        const float p = sigmoidf_(y3);
+        const float lab = LAB[r];
+        float lrow = 0.f, dy3 = 0.f;
+        if (valid) {
+          // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
+          const float lg = logf(p), lg1 = log1pf(-p);
+          const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
+          lrow = -(lab * lp + (1.f - lab) * l1p);
+          const float pq = p * (1.f - p);
+          dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
+        }
+        if (q == 0) DY3[r] = dy3;
+        float gw[8], dy2[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          gw[j] = dy3 * g2[j];
+          dy2[j] = dy3 * c.P[OUT_W + c0 + j] * gelu_grad(y2[j]);
+        }
+        s8v v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(dy2[j]);
+        *(LDS_AS s8v*)(F2 + r * LD32 + c0) = v;  // T32 aliases F2
+        colsumW<8>(c, 0, gw, c0);
+        colsumW<8>(c, 1, dy2, c0);
+        // loss reduction (q == 0 lanes carry the row loss)
+        float lsum = wave_sum(q == 0 ? lrow : 0.f);
+        if (c.lane == 0) RED[c.wave] = lsum;
+      }
+      __syncthreads();
+      {
+        float tot = 0.f;
+        for (int w = 0; w < 8; ++w) tot += RED[w];
+        const float loss = tot / (float)Bn;
+        if (loss != loss) {
+          failed = true;  // uniform across the workgroup
+        } else {
+          epoch_loss += loss;
+        }
+      }
+      if (failed) break;
+      // =============================== head backward ===============================
+      // A7: Adam output.weight / output.bias / fc2.bias
+      if (tid < 32) {
+        adam(c.P, c.M, c.V, OUT_W + tid, cs_total(c, 0, tid), K);
+      } else if (tid < 64) {
+        adam(c.P, c.M, c.V, FC2_B + tid - 32, cs_total(c, 1, tid - 32), K);
+      } else if (tid == 64) {
+        float s = 0.f;
+        for (int i = 0; i < BM; ++i) s += DY3[i];
+        adam(c.P, c.M, c.V, OUT_B, s, K);
+      }
+      gemm_xw<64, 32>(c, F2, LD32, c.BF + WTF2);  // dd1 = dy2 . Wf2
+      __syncthreads();
+      {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
+        float d[16], y[16];
+        const int c0 = q * 16;
+        load16(y, c.wsf(W_Y1) + r * 64 + c0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float g = keep(key, L_HEAD, r, c0 + j, THR_P03) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
+          d[j] = g * gelu_grad(y[j]);
+        }
+        store16bf(TB + r * LD64 + c0, d);
+        colsum16(c, 2, d);
+      }
+      __syncthreads();
+      gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, mfc2, K);  // dWf2 = dy2^T d1
+      if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
+      __syncthreads();
+      gemm_xw<64, 64>(c, TB, LD64, c.BF + WTF1);  // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
+      __syncthreads();
+      for (int i = tid; i < BM * 64; i += NT) c.wsf(W_DX3V)[i] = ACC[(i >> 6) * LDACC + (i & 63)];
+      __syncthreads();
+      gemm_xw<64, 64>(c, TB, LD64, c.BF + WTF1 + 64 * 64);  // dcat[:, 64:128] (kept in ACC for branch 1)
+      __syncthreads();
+      gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, mfc1, K);  // dWf1 = dy1^T cat
+      __syncthreads();
+
+      // =============================== branch backward (labs first, dx3 in ACC) ===============================
+      for (int br = 1; br >= 0; --br) {
+        const Branch B = branch(br);
+        {  // E10: LN3 bwd, LN2 bwd, df3 ; colsums g3 (v0), b3 (v1), g2 (v2), be2 (v3), b2 (v4)
+          float dy[16], xh[16], dx[16];
+          const int c0 = q * 16;
+          if (br == 1) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
+          } else {
+            load16(dy, c.wsf(W_DX3V) + r * 64 + c0);
+          }
+          load16(xh, c.wsf(B.s.XH3) + r * 64 + c0);
+          float t[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
+          colsum16(c, 0, t);
+          colsum16(c, 1, dy);
+          ln_bwd(dx, dy, xh, c.wsf(B.s.R3)[r], c.P + B.o.bn_w, c0);
+          load16(xh, c.wsf(B.s.XH2) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+          colsum16(c, 2, t);
+          colsum16(c, 3, dx);
+          ln_bwd(dy, dx, xh, c.wsf(B.s.R2)[r], c.P + B.o.ln2_w, c0);  // dy := dr2
+          store16(c.wsf(B.s.DX1F) + r * 64 + c0, dy);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = keep(key, 8 * br + L_D2, r, c0 + j, THR_P01) ? dy[j] * INV_K01 : 0.f;
+          store16bf(TA + r * LD64 + c0, t);
+          colsum16(c, 4, t);
+        }
+        __syncthreads();
+        // A10 (LN/bias vectors) + G11 (df2 = df3 . W2)
+        if (tid < 64) {
+          adam(c.P, c.M, c.V, B.o.bn_w + tid, cs_total(c, 0, tid), K);
+          adam(c.P, c.M, c.V, B.o.bn_b + tid, cs_total(c, 1, tid), K);
+          adam(c.P, c.M, c.V, B.o.ln2_w + tid, cs_total(c, 2, tid), K);
+          adam(c.P, c.M, c.V, B.o.ln2_b + tid, cs_total(c, 3, tid), K);
+          adam(c.P, c.M, c.V, B.o.ff3_b + tid, cs_total(c, 4, tid), K);
+        }
+        gemm_xw<16, 64>(c, TA, LD64, c.BF + B.w.WT2);
+        __syncthreads();
+        {  // E11: df0 (-> DF0 = XIN region), recompute f2 (-> F2); colsum b1 (v5)
+          s8v vd, vf;
+          float db[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            float d0 = 0.f, f2 = 0.f;
+            if (col < FF) {
+              const float f0 = c.wsf(B.s.F0)[r * 8 + col];
+              const bool kp = keep(key, 8 * br + L_DF, r, col, THR_P01);
+              d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
+              f2 = kp ? gelu(f0) * INV_K01 : 0.f;
+            }
+            db[j] = d0;
+            vd[j] = (short)f2bf(d0);
+            vf[j] = (short)f2bf(f2);
+          }
+          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = vd;
+          *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = vf;
+          colsumW<8>(c, 5, db, q * 8);
+        }
+        __syncthreads();
+        gemm_dw_adam<4, 1>(c, TA, LD64, F2, LD32, B.ff3(), K);  // dW2 = df3^T f2
+        if (tid < FF) adam(c.P, c.M, c.V, B.o.ff0_b + tid, cs_total(c, 5, tid), K);
+        __syncthreads();
+        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WT1);  // dx1 = df0 . W1
+        __syncthreads();
+        {  // E12: dx1 += DX1F ; LN1 bwd ; do ; x1 recompute ; colsums g1 (v0), be1 (v1), bo (v2)
+          float dx[16], xh[16], t[16], d[16];
+          const int c0 = q * 16;
+          load16(t, c.wsf(B.s.DX1F) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) dx[j] = ACC[r * LDACC + c0 + j] + t[j];
+          load16(xh, c.wsf(B.s.XH1) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+          colsum16(c, 0, t);
+          colsum16(c, 1, dx);
+          ln_bwd(d, dx, xh, c.wsf(B.s.R1)[r], c.P + B.o.ln1_w, c0);  // d = dr1
+          store16(c.wsf(B.s.DH0F) + r * 64 + c0, d);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = keep(key, 8 * br + L_D1, r, c0 + j, THR_P01) ? d[j] * INV_K01 : 0.f;
+          store16bf(TB + r * LD64 + c0, t);
+          colsum16(c, 2, t);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = xh[j] * c.P[B.o.ln1_w + c0 + j] + c.P[B.o.ln1_b + c0 + j];
+          store16bf(TC + r * LD64 + c0, t);
+        }
+        __syncthreads();
+        gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B.ff0(), K);  // dW1 = df0^T x1
+        if (tid < 64) {
+          adam(c.P, c.M, c.V, B.o.ln1_w + tid, cs_total(c, 0, tid), K);
+          adam(c.P, c.M, c.V, B.o.ln1_b + tid, cs_total(c, 1, tid), K);
+          adam(c.P, c.M, c.V, B.o.out_b + tid, cs_total(c, 2, tid), K);
+        }
+        __syncthreads();
+        gemm_xw<64, 64>(c, TB, LD64, c.BF + B.w.WTo);  // da = do . Wo
+        __syncthreads();
+        {  // E13: dv ; reload h0 ; colsum bv (v3)
+          float d[16];
+          const int c0 = q * 16;
+          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) d[j] = ACC[r * LDACC + c0 + j] * m;
+          store16bf(TC + r * LD64 + c0, d);
+          colsum16(c, 3, d);
+          const unsigned short* hb = (const unsigned short*)c.wsf(B.s.H0B) + r * 64 + c0;
+          s8v h0a = *(const s8v*)hb, h0b = *(const s8v*)(hb + 8);
+          *(LDS_AS s8v*)(TA + r * LD64 + c0) = h0a;
+          *(LDS_AS s8v*)(TA + r * LD64 + c0 + 8) = h0b;
+        }
+        __syncthreads();
+        gemm_xw<64, 64>(c, TA, LD64, c.BF + B.w.WFv);  // v recompute
+        __syncthreads();
+        {  // E13b: a = head_dropout(v) -> TD (CAT region, ld 72)
+          float x[16];
+          const int c0 = q * 16;
+          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B.o.inproj_b + 128 + c0 + j]) * m;
+          store16bf(CAT + r * LD64 + c0, x);
+        }
+        __syncthreads();
+        gemm_xw<64, 64>(c, TC, LD64, c.BF + B.w.WTv);  // dh0 part = dv . Wv
+        gemm_dw_adam<4, 4>(c, TB, LD64, CAT, LD64, B.oproj(), K);  // dWo = do^T a  (WTo not read here)
+        if (tid < 64) adam(c.P, c.M, c.V, B.o.inproj_b + 128 + tid, cs_total(c, 3, tid), K);
+        __syncthreads();
+        {  // E14: DH0F += ACC ; gather x for z0 recompute
+          float t[16];
+          const int c0 = q * 16;
+          load16(t, c.wsf(B.s.DH0F) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] += ACC[r * LDACC + c0 + j];
+          store16(c.wsf(B.s.DH0F) + r * 64 + c0, t);
+          s8v v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            float x = (valid && col < B.din) ? rows[(long)ridx * ROW + B.xoff + col] : 0.f;
+            v[j] = (short)f2bf(x);
+          }
+          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
+        }
+        __syncthreads();
+        gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B.vproj(), K);  // dWv = dv^T h0 (after WFv/WTv reads)
+        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WFd);             // z0 recompute
+        __syncthreads();
+        {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
+          float t[16], d[16];
+          const int c0 = q * 16;
+          load16(t, c.wsf(B.s.DH0F) + r * 64 + c0);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) d[j] = t[j] * gelu_grad(ACC[r * LDACC + c0 + j] + c.P[B.o.dense_b + c0 + j]);
+          store16bf(TB + r * LD64 + c0, d);
+          colsum16(c, 4, d);
+        }
+        __syncthreads();
+        gemm_dw_adam<4, 1>(c, TB, LD64, XIN, LD32, B.dense(), K);  // dWd = dz0^T x
+        if (tid < 64) adam(c.P, c.M, c.V, B.o.dense_b + tid, cs_total(c, 4, tid), K);
+        __syncthreads();
+      }
+    }
+    if (tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
+  }
+  if (tid == 0) a.ok[cid] = failed ? 0 : 1;
+}
+
+// ================================================================================================
+// eval forward: one 512-thread workgroup per 128-row tile of the test set, weights read directly
+// from the fp32 params (converted to bf16 copies in LDS once per tile would not pay: reuse is 1).
+// ================================================================================================
+__global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, const unsigned short* __restrict__ BF,
+                                                const float* __restrict__ rows, int n, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Ctx c;
+  c.smem = smem;
+  c.tid = threadIdx.x;
+  c.lane = threadIdx.x & 63;
+  c.wave = threadIdx.x >> 6;
+  c.P = (float*)P;
+  const int tid = c.tid, r = tid >> 2, q = tid & 3;
+  const int row0 = blockIdx.x * BM;
+  const bool valid = row0 + r < n;
+  const long ridx = valid ? row0 + r : 0;
+  unsigned short* XIN = c.u16(S_XIN);
+  unsigned short* TA = c.u16(S_TA);
+  unsigned short* TB = c.u16(S_TB);
+  unsigned short* CAT = c.u16(S_CAT);
+  unsigned short* F2 = c.u16(S_F2);
+  float* ACC = c.acc();
+  for (int br = 0; br < 2; ++br) {
+    const Branch B = branch(br);
+    {
+      s8v v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = q * 8 + j;
+        float x = (valid && col < B.din) ? rows[ridx * ROW + B.xoff + col] : 0.f;
+        v[j] = (short)f2bf(x);
+      }
+      *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
+    }
+    __syncthreads();
+    gemm_xw<64, 32>(c, XIN, LD32, BF + B.w.WFd);
+    __syncthreads();
+    float h[16];
+    {
+      const int c0 = q * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + P[B.o.dense_b + c0 + j]);
+      store16bf(TA + r * LD64 + c0, h);
+    }
+    __syncthreads();
+    gemm_xw<64, 64>(c, TA, LD64, BF + B.w.WFv);
+    __syncthreads();
+    {
+      float x[16];
+      const int c0 = q * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = ACC[r * LDACC + c0 + j] + P[B.o.inproj_b + 128 + c0 + j];
+      store16bf(TB + r * LD64 + c0, x);
+    }
+    __syncthreads();
+    gemm_xw<64, 64>(c, TB, LD64, BF + B.w.WFo);
+    __syncthreads();
+    float x1[16];
+    {
+      const int c0 = q * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x1[j] = h[j] + ACC[r * LDACC + c0 + j] + P[B.o.out_b + c0 + j];
+      ln_fwd(x1);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x1[j] = x1[j] * P[B.o.ln1_w + c0 + j] + P[B.o.ln1_b + c0 + j];
+      store16bf(TA + r * LD64 + c0, x1);
+    }
+    __syncthreads();
+    gemm_xw<16, 64>(c, TA, LD64, BF + B.w.WF1);
+    __syncthreads();
+    {
+      s8v v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = q * 8 + j;
+        v[j] = (short)f2bf(col < FF ? gelu(ACC[r * LDACC + col] + P[B.o.ff0_b + col]) : 0.f);
+      }
+      *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
+    }
+    __syncthreads();
+    gemm_xw<64, 32>(c, F2, LD32, BF + B.w.WF2);
+    __syncthreads();
+    {
+      float x[16];
+      const int c0 = q * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = x1[j] + ACC[r * LDACC + c0 + j] + P[B.o.ff3_b + c0 + j];
+      ln_fwd(x);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B.o.ln2_w + c0 + j] + P[B.o.ln2_b + c0 + j];
+      ln_fwd(x);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B.o.bn_w + c0 + j] + P[B.o.bn_b + c0 + j];
+      store16bf(CAT + r * LD128 + br * 64 + c0, x);
+    }
+    __syncthreads();
+  }
+  gemm_xw<64, 128>(c, CAT, LD128, BF + WFF1);
+  __syncthreads();
+  {
+    float x[16];
+    const int c0 = q * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = gelu(ACC[r * LDACC + c0 + j] + P[FC1_B + c0 + j]);
+    store16bf(TA + r * LD64 + c0, x);
+  }
+  __syncthreads();
+  gemm_xw<32, 64>(c, TA, LD64, BF + WFF2);
+  __syncthreads();
+  {
+    float dot = 0.f;
+    const int c0 = q * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dot += gelu(ACC[r * LDACC + c0 + j] + P[FC2_B + c0 + j]) * P[OUT_W + c0 + j];
+    const float y3 = rsum4(dot) + P[OUT_B];
+    if (valid && q == 0) out[row0 + r] = sigmoidf_(y3);
+  }
+}
+
+// bf16 weight copies for eval (same layout as the training workspace's BF region)
+__global__ void k_tf_copies(const float* __restrict__ P, unsigned short* __restrict__ BF) {
+  Ctx c;
+  c.tid = blockIdx.x * blockDim.x + threadIdx.x;
+  c.P = (float*)P;
+  c.BF = BF;
+  // a grid-stride variant of init_copies
+  auto put = [&](MatW mw) {
+    for (int e = c.tid; e < mw.n_real * mw.k_real; e += gridDim.x * blockDim.x) {
+      const int nn = e / mw.k_real, kk = e % mw.k_real;
+      unsigned short h = f2bf(P[mw.off + e]);
+      BF[mw.wf + nn * mw.wf_ld + kk] = h;
+      if (mw.wt >= 0) BF[mw.wt + kk * mw.wt_ld + nn] = h;
+    }
+  };
+  for (int br = 0; br < 2; ++br) {
+    Branch B = branch(br);
+    put(B.dense());
+    put(B.vproj());
+    put(B.oproj());
+    put(B.ff0());
+    put(B.ff3());
+  }
+  put(MatW{FC1_W, 64, 128, WFF1, 128, WTF1, 64});
+  put(MatW{FC2_W, 32, 64, WFF2, 64, WTF2, 32});
+}
+
+long afl_tf_ws_floats() { return WS_FLOATS; }
+int afl_tf_bf_ushorts() { return BF_TOTAL; }
+int afl_tf_param_count() { return NPARAM; }
+
+int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
+  if (a->batch > BM || a->batch < 1) return -1;
+  hipFuncSetAttribute((const void*)k_tf_train, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL);
+  hipLaunchKernelGGL(k_tf_train, dim3(a->C), dim3(NT), S_TOTAL, s, *a);
+  return 0;
+}
+
+int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s) {
+  hipMemsetAsync(bf, 0, (size_t)BF_TOTAL * 2, s);
+  hipLaunchKernelGGL(k_tf_copies, dim3(32), dim3(256), 0, s, params, bf);
+  hipFuncSetAttribute((const void*)k_tf_eval, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL);
+  hipLaunchKernelGGL(k_tf_eval, dim3((n + BM - 1) / BM), dim3(NT), S_TOTAL, s, params, bf, rows, n, out);
+  return 0;
+}

@@ -1,0 +1,127 @@
+"""Every native aggregation / attack / metric kernel vs its fp32/fp64 PyTorch composite."""
+import pytest
+import torch
+
+from attackfl_amd import ops
+from attackfl_amd.ops import composite as C
+from attackfl_amd.models import ParamLayout
+
+pytestmark = pytest.mark.gpu
+
+
+def _U(n=8, p=47693, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, p, generator=g) * 0.1 + torch.randn(1, p, generator=g)
+
+
+def test_colstats_lie(gpu):
+    U = _U(5)
+    m, s = ops.column_mean_std(U.to(gpu))
+    mr, sr = C.column_mean_std(U)
+    assert torch.allclose(m.cpu(), mr, atol=1e-6) and torch.allclose(s.cpu(), sr, atol=1e-5)
+    assert torch.allclose(ops.lie_candidate(U.to(gpu), 0.74).cpu(), C.lie_candidate(U, 0.74), atol=1e-5)
+    one = ops.column_mean_std(U[:1].to(gpu))[1]
+    assert torch.isnan(one).all()
+
+
+def test_weighted_rows_fedavg(gpu):
+    U = _U(8)
+    sizes = torch.tensor([12000., 13000, 15000, 14000, 12500, 12001, 14999, 13333])
+    assert torch.allclose(ops.fedavg(U.to(gpu), sizes).cpu(), C.fedavg(U, sizes), atol=1e-6)
+
+
+@pytest.mark.parametrize("n", [3, 8, 11, 33])
+def test_median_trimmed(gpu, n):
+    U = _U(n, 5000, seed=n)
+    assert torch.equal(ops.coord_median(U.to(gpu)).cpu(), C.coord_median(U))
+    k = max(1, int(n * 0.1))
+    assert torch.allclose(ops.trimmed_mean(U.to(gpu), k).cpu(), C.trimmed_mean(U, k), atol=1e-5)
+
+
+def test_pairwise(gpu):
+    U = _U(9, 20000)
+    d = ops.pairwise_l2(U.to(gpu)).cpu()
+    assert torch.allclose(d, C.pairwise_l2(U), rtol=1e-6, atol=1e-6)
+
+
+def test_row_dots_cosine(gpu):
+    U = _U(6, 30000)
+    r = U.mean(0)
+    assert torch.allclose(ops.cosine_to(U.to(gpu), r.to(gpu)).cpu(), C.cosine_to(U, r), atol=1e-9)
+    assert torch.allclose(ops.row_norms(U.to(gpu)).cpu(), C.row_norms(U), rtol=1e-9)
+
+
+def test_segments_and_coeffs(gpu):
+    lay = ParamLayout.for_model("TransformerModel")
+    G = _U(4)
+    mean, std = C.column_mean_std(G)
+    vec = [s for s in lay.slots if len(s.shape) == 1]
+    A, B, Cc = ops.attack_coeffs_segments(G.to(gpu), mean.to(gpu), std.to(gpu), vec)
+    Ar, Br, Cr = C.attack_coeffs_segments(G, mean, std, vec)
+    assert torch.allclose(A.cpu(), Ar, rtol=1e-9) and torch.allclose(B.cpu(), Br, rtol=1e-7, atol=1e-9)
+    assert torch.allclose(Cc.cpu(), Cr, rtol=1e-9)
+    diffs = G[1:] - G[:1]
+    assert torch.allclose(ops.segment_l2_sum(diffs.to(gpu), vec).cpu(), C.segment_l2_sum(diffs, vec), rtol=1e-9)
+
+
+@pytest.mark.parametrize("shape", [(192, 64), (64, 64), (64, 7), (6, 64), (1, 32), (128, 1024), (96, 32)])
+def test_spectral_norm(gpu, shape):
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(5, *shape, generator=g)
+    got = ops.batched_spectral_norm(X.to(gpu)).cpu()
+    ref = C.batched_spectral_norm(X)
+    assert torch.allclose(got, ref, rtol=2e-5), (got, ref)
+
+
+def test_spectral_degenerate(gpu):
+    X = torch.zeros(3, 16, 16)
+    X[0] = torch.eye(16) * 2.0          # repeated top singular value
+    X[2, 0, 0] = 1e-3
+    got = ops.batched_spectral_norm(X.to(gpu)).cpu()
+    assert torch.allclose(got, torch.tensor([2.0, 0.0, 1e-3], dtype=torch.float64), rtol=1e-5)
+
+
+def test_roc_auc(gpu):
+    from sklearn.metrics import roc_auc_score
+
+    g = torch.Generator().manual_seed(0)
+    for n in (10, 1000, 5000, 80000):
+        y = (torch.rand(n, generator=g) < 0.3).float()
+        s = torch.rand(n, generator=g) + y * 0.3
+        s = (s * 50).round() / 50  # many ties
+        a = ops.roc_auc(s.to(gpu), y.to(gpu))
+        assert abs(a - roc_auc_score(y.numpy(), s.numpy())) < 1e-9
+
+
+def test_adam_flat(gpu):
+    g = torch.Generator().manual_seed(0)
+    p, gr = torch.randn(1000, generator=g), torch.randn(1000, generator=g)
+    m, v = torch.zeros(1000), torch.zeros(1000)
+    pd, md, vd = p.clone().to(gpu), m.clone().to(gpu), v.clone().to(gpu)
+    for step in (1, 2, 3):
+        C.adam_step_scaled(p, gr, m, v, step, 1e-3, 0.5)
+        ops.adam_step_scaled(pd, gr.to(gpu), md, vd, step, 1e-3, 0.5)
+    assert torch.allclose(pd.cpu(), p, atol=1e-6)
+
+
+def test_hyper_kernels(gpu):
+    g = torch.Generator().manual_seed(0)
+    P, H = 47693, 100
+    W, b, f, u = torch.randn(P, H, generator=g) * 0.1, torch.randn(P, generator=g), torch.randn(H, generator=g), torch.randn(P, generator=g)
+    d, df = ops.hyper_delta_vjp(W.to(gpu), b.to(gpu), f.to(gpu), u.to(gpu))
+    dr, dfr = C.hyper_delta_vjp(W, b, f, u)
+    assert torch.allclose(d.cpu(), dr, atol=1e-4) and torch.allclose(df.cpu(), dfr, rtol=1e-4, atol=1e-2)
+    assert torch.allclose(ops.hyper_generate(W.to(gpu), b.to(gpu), f.to(gpu)).cpu(), torch.addmv(b, W, f), atol=1e-4)
+    m, v = torch.zeros(P * H + P), torch.zeros(P * H + P)
+    Wd, bd, md, vd = W.clone().to(gpu), b.clone().to(gpu), m.clone().to(gpu), v.clone().to(gpu)
+    C.hyper_adam_outer(W, b, m, v, dr, f, 1, 1e-3, 0.3)
+    ops.hyper_adam_outer(Wd, bd, md, vd, dr.to(gpu), f.to(gpu), 1, 1e-3, 0.3)
+    assert torch.allclose(Wd.cpu(), W, atol=1e-6) and torch.allclose(bd.cpu(), b, atol=1e-6)
+
+
+def test_stoch_quant(gpu):
+    U = _U(4, 100000)
+    sigma, smin, smax = ops.stochastic_quantize(U.to(gpu), 123)
+    assert torch.allclose(smin.cpu(), U.min(1).values) and torch.allclose(smax.cpu(), U.max(1).values)
+    probs = (U - U.min(1, keepdim=True).values) / (U.max(1, keepdim=True).values - U.min(1, keepdim=True).values + 1e-6)
+    assert abs(sigma.cpu().mean().item() - probs.mean().item()) < 5e-3
