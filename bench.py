@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FL rounds/sec for the whole node (+ test ROC-AUC), TransformerModel/ICU, 8 clients.
+
+Metric and config come from BASELINE.json ("FL rounds/sec (whole node) + test-acc, TransformerModel/ICU,
+8 clients"); the workload is the reference ``config.yaml`` learning setup (5 local epochs, batch 128,
+Adam lr 0.004, 12000-15000 rows per client per round) with ``mode: fedavg`` and no attacker.  A "step"
+is one complete FL round: every client's local training, the update all-gather, FedAvg, server-side
+ROC-AUC validation on the 10k-row test set and the ``TransformerModel.pth`` checkpoint write.
+
+The 8 clients are spread over the N ranks (8/N clients per GPU, one process per GPU, RCCL over xGMI):
+total work is fixed as N grows, so scaling is *strong*.  Data are synthetic ICU-shaped rows with a
+planted signal, weights are random-init (no datasets or checkpoints are downloadable here).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_ROUNDS_PER_S = 0.18  # measured proxy of the reference, whole node, 8 clients
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--model", default="TransformerModel")
+    ap.add_argument("--mode", default="fedavg")
+    ap.add_argument("--trainer", default="auto")
+    ap.add_argument("--profile-rounds", action="store_true", help="print per-phase timings to stderr")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from attackfl_amd.config import from_dict
+    from attackfl_amd.fl.engine import FLEngine, build_client_table
+    from attackfl_amd.parallel.comm import LoopbackComm, TorchComm, init_distributed
+    from attackfl_amd.utils.log import set_quiet
+
+    set_quiet(True)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    if world > 1:
+        backend, device = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+        comm = TorchComm(device)
+    else:
+        device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        if device.type == "cuda":
+            torch.cuda.set_device(device)
+        comm = LoopbackComm(device)
+    rank = comm.rank
+    tmp = tempfile.mkdtemp(prefix=f"attackfl_bench_r{rank}_")
+    cfg = from_dict({
+        "server": {"num-round": args.warmup + args.steps + 1, "clients": args.clients, "mode": args.mode,
+                   "model": args.model, "data-name": "ICU", "validation": True,
+                   "data-distribution": {"num-data-range": [12000, 15000]}},
+        "learning": {"epoch": 5, "batch-size": 128, "learning-rate": 0.004},
+        "data": {"synthetic": True, "train-size": 60000, "test-size": 10000},
+        "engine": {"trainer": args.trainer, "checkpoint-dir": tmp, "seed": 1},
+        "log_path": tmp,
+    })
+    table = build_client_table(cfg, comm.world)
+    eng = FLEngine(cfg, comm=comm, table=table, device=device, verbose=False)
+    eng.client_selection()
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if comm.world > 1:
+            comm.barrier()
+
+    for _ in range(args.warmup):
+        eng.run_round()
+    sync()
+    t0 = time.perf_counter()
+    recs = []
+    for _ in range(args.steps):
+        recs.append(eng.run_round())
+    sync()
+    elapsed = time.perf_counter() - t0
+    if comm.world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if args.profile_rounds and rank == 0:
+        for r in recs:
+            print(json.dumps({k: r[k] for k in ("round", "ok", "t_local", "t_gather", "t_aggregate", "t_validate",
+                                                "t_round", "metric")}), file=sys.stderr)
+    value = args.steps / elapsed
+    if rank == 0:
+        aucs = [r["metric"] for r in recs if r["metric"] == r["metric"]]
+        out = {
+            "metric": "FL rounds/sec (whole node) + test-acc, TransformerModel/ICU, 8 clients",
+            "value": round(value, 4),
+            "unit": "rounds/s",
+            "n_gpus": comm.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_ROUNDS_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic ICU-shaped rows (planted signal), random-init weights",
+            "config": {"model": args.model, "global_batch": 128 * args.clients, "seq_len": 1,
+                       "parallelism": f"fl{args.clients}-clients-over-{comm.world}-ranks",
+                       "clients": args.clients, "local_epochs": 5, "rows_per_client": "12000-15000",
+                       "mode": args.mode, "trainer": eng.trainer.kind if eng.trainer else None},
+            "test_roc_auc": round(aucs[-1], 4) if aucs else None,
+            "rounds_ok": sum(1 for r in recs if r["ok"]),
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
