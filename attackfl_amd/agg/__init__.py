@@ -102,8 +102,10 @@ def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, s
 
     n = U.shape[0]
     att = attackers.bool().cpu().numpy() if attackers is not None else np.zeros(n, bool)
-    r = max(1, min(n - 1, 8))
+    # subspace rank small enough that each of the 2 components has well-conditioned covariance
+    r = max(1, min(4, n // 2 - 1))
     Z = _pca_project(U, r)
+    Z = Z / max(float(np.abs(Z).max()), 1e-30)
     benign = Z[~att]
     mal = Z[att]
     allz = np.vstack([benign, mal]) if len(mal) else benign

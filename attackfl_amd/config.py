@@ -61,8 +61,8 @@ REFERENCE_DEFAULTS: Dict[str, Any] = {
 }
 
 EXTENSION_DEFAULTS: Dict[str, Any] = {
-    "comm": {"backend": "auto", "clients-per-rank": 0, "one-shot-allgather": False, "timeout-s": 600,
-             "attackers": {}},
+    "comm": {"backend": "auto", "address": "", "port": 29517, "clients-per-rank": 0, "one-shot-allgather": False,
+             "timeout-s": 600, "attackers": {}},
     "data": {"synthetic": "auto", "train-size": 60000, "test-size": 10000, "seed": 1234,
              "har-train-size": 2048, "har-test-size": 512, "root": "."},
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",

@@ -134,6 +134,7 @@ class FLEngine:
         self.server_rng = random.Random(cfg.random_seed) if cfg.random_seed else random.Random()
         self.global_params: Optional[torch.Tensor] = None
         self.selected: List[int] = []
+        self._selection_done = False
         self.genuine_pool: Optional[torch.Tensor] = None
         self.hyper: Optional[HyperServer] = None
         self.fltrust_model: Optional[torch.Tensor] = None
@@ -196,6 +197,7 @@ class FLEngine:
     # START
     # ------------------------------------------------------------------------------------------
     def client_selection(self):
+        self._selection_done = True
         self.selected = list(range(self.n_clients))
         self.logger.log_info(f"Active with {len(self.selected)} client: {self.selected}")
 
@@ -267,16 +269,14 @@ class FLEngine:
         if train_rows:
             sel = torch.tensor(train_rows, device=self.device)
             params = self.local_params.index_select(0, sel).contiguous()
-            plan = make_plan(self.train_table.n, train_nd, cfg.epoch, self._plan_gen(), self.device)
+            plan = make_plan(self.train_table.n, train_nd, cfg.epoch, [sd * 1000003 + 17 for sd in train_seeds],
+                             self.device)
             oks, losses = self.trainer.train(params, plan, cfg.lr, cfg.batch_size, train_seeds)
             self.local_params.index_copy_(0, sel, params)
             block[sel, :self.P] = params
             block[sel, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=self.device)
             self._last_losses = losses
         return block
-
-    def _plan_gen(self) -> torch.Generator:
-        return self.torch_gen
 
     # ------------------------------------------------------------------------------------------
     # SERVER
@@ -346,6 +346,8 @@ class FLEngine:
             torch.cuda.synchronize(self.device)
 
     def run_round(self) -> dict:
+        if not self._selection_done:
+            self.client_selection()
         t0 = time.perf_counter()
         if self.verbose:
             print_with_color(f"Start training round {self.round_no}", "yellow")

@@ -39,10 +39,12 @@ class Plan:
         return self.order[c, :, : int(self.nd[c])]
 
 
-def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator: torch.Generator, device) -> Plan:
+def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, device) -> Plan:
     """Random subset (without replacement) per client + a fresh permutation per epoch.
 
-    Everything is generated on ``device`` with two batched argsorts (no per-client loops)."""
+    ``generator`` is one ``torch.Generator`` shared by all rows, or a list of per-client integer seeds
+    (placement-independent: a client draws the same batches whichever rank hosts it).  The random keys
+    are drawn on ``device`` and sorted with two batched argsorts (no per-client sort loops)."""
     C = len(num_data)
     if C == 0:
         return Plan(torch.zeros(0, epochs, 0, dtype=torch.int32, device=device), torch.zeros(0, dtype=torch.int32),
@@ -50,10 +52,21 @@ def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator: tor
     maxnd = max(num_data)
     if maxnd > n_train:
         raise ValueError(f"num_data {maxnd} exceeds the train set size {n_train}")
-    gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
-    keys = torch.rand(C, n_train, generator=generator, device=gdev)
+    if isinstance(generator, (list, tuple)):
+        gdev = torch.device(device)
+        keys, ek = [], []
+        for s in generator:
+            g = torch.Generator(device=gdev).manual_seed(int(s) & 0x7FFFFFFFFFFFFFFF)
+            keys.append(torch.rand(n_train, generator=g, device=gdev))
+            ek.append(torch.rand(epochs, maxnd, generator=g, device=gdev))
+        keys, ek = torch.stack(keys), torch.stack(ek)
+    else:
+        gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
+        keys = torch.rand(C, n_train, generator=generator, device=gdev)
+        ek = None
     subset = torch.argsort(keys, dim=1)[:, :maxnd]                              # [C, maxnd]
-    ek = torch.rand(C, epochs, maxnd, generator=generator, device=gdev)
+    if ek is None:
+        ek = torch.rand(C, epochs, maxnd, generator=generator, device=gdev)
     nd = torch.tensor(list(num_data), dtype=torch.long, device=gdev)
     pad = torch.arange(maxnd, device=gdev)[None, None, :] >= nd[:, None, None]
     ek = ek.masked_fill(pad, 2.0)                                               # padding sorts last

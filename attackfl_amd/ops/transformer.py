@@ -21,13 +21,17 @@ M32 = 0xFFFFFFFF
 
 # ------------------------------------------------------------------------------- device entry points
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
-                  lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Train all clients in place. Returns (ok [C] int32 on host, losses [C, E] fp32 on host)."""
+                  lr: float, seeds: Sequence[int], opt_mode: int = 0, stamps: torch.Tensor = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Train all clients in place. Returns (ok [C] int32 on host, losses [C, E] fp32 on host).
+
+    ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
+    workgroup 0, summed over all steps (diagnostics)."""
     dev = params.device
     nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
     seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
     ok, losses = native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
-                                   int(batch), float(lr), int(opt_mode))
+                                   int(batch), float(lr), int(opt_mode), stamps)
     return ok.cpu(), losses.cpu()
 
 

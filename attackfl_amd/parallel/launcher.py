@@ -1,0 +1,101 @@
+"""Process launch / rendezvous (replaces the RabbitMQ REGISTER handshake, ``server.py:205-235``,
+``client.py:134-143``, and the broker queue janitor ``server.py:803-835``).
+
+Two ways to start a run:
+
+* **classic** — ``python server.py`` plus N x ``python client.py [--attack ...]``, exactly like the
+  reference.  The server opens a TCPStore at ``comm.address`` (default: ``rabbit.address``) and waits
+  for ``server.clients`` registrations; every client claims the next rank with an atomic counter and
+  publishes its descriptor (uuid + attack flags).  Registration order defines the client index like
+  the reference's ``list_clients``.  Then all processes join one ``torch.distributed`` group
+  (rank 0 = server, ranks 1..N = clients) and run the SPMD engine.  A fresh store per run plays the
+  role of the queue janitor.
+* **packed** — ``torchrun --nproc-per-node G launch.py`` (or ``bench.py``): one process per GPU, the
+  ``server.clients`` clients packed N/G per rank, server state replicated on every rank.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import time
+import uuid
+from typing import Dict, List, Optional, Tuple
+
+import torch.distributed as dist
+
+from ..config import AttackSpec, Config
+from ..utils.log import print_with_color
+
+PREFIX = "attackfl/"
+
+
+def _host_port(cfg: Config) -> Tuple[str, int]:
+    host = cfg.comm.get("address") or cfg.raw["rabbit"]["address"] or "127.0.0.1"
+    return str(host), int(cfg.comm.get("port", 29517))
+
+
+def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0):
+    """Server side: open the store, wait for ``clients`` registrations, publish the client table.
+
+    Returns (store, world_size, table_json)."""
+    host, port = _host_port(cfg)
+    n = cfg.clients
+    store = dist.TCPStore(host, port, world_size=None, is_master=True, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=timeout_s), use_libuv=False)
+    store.set(PREFIX + "n_clients", str(n))
+    print_with_color(f"Server is waiting for {n} clients.", "green")
+    t0 = time.time()
+    while int(store.add(PREFIX + "next_rank", 0)) < n:
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError("clients did not register in time")
+        time.sleep(0.05)
+    table = []
+    for r in range(1, n + 1):
+        d = json.loads(store.get(PREFIX + f"client/{r}").decode())
+        table.append({"index": r - 1, "uuid": d["uuid"], "owner": r, "attack": d.get("attack")})
+        print_with_color(f"[<<<] Received message from client: {d}", "blue")
+    store.set(PREFIX + "table", json.dumps(table))
+    print_with_color("All clients are connected. Sending notifications.", "green")
+    return store, n + 1, table
+
+
+def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float = 3600.0):
+    """Client side: claim a rank, publish the descriptor, wait for the table.
+
+    Returns (store, rank, world_size, table_json)."""
+    host, port = _host_port(cfg)
+    store = dist.TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s),
+                          use_libuv=False)
+    rank = int(store.add(PREFIX + "next_rank", 1))
+    n = int(store.get(PREFIX + "n_clients").decode())
+    if rank > n:
+        raise RuntimeError(f"server expects {n} clients; this would be client #{rank}")
+    desc = {"uuid": str(uuid.uuid4()), "message": "Hello from Client!",
+            "attack": None if attack is None else {"mode": attack.mode, "round": attack.round, "args": attack.args}}
+    store.set(PREFIX + f"client/{rank}", json.dumps(desc))
+    print_with_color(f"[>>>] Client {desc['uuid']} registered as rank {rank}", "red")
+    store.wait([PREFIX + "table"])
+    table = json.loads(store.get(PREFIX + "table").decode())
+    return store, rank, n + 1, table
+
+
+def table_from_json(table_json: List[Dict]):
+    from ..fl.engine import ClientInfo
+
+    out = []
+    for d in table_json:
+        a = d.get("attack")
+        out.append(ClientInfo(int(d["index"]), str(d["uuid"]), int(d["owner"]),
+                              AttackSpec(a["mode"], a["round"], a.get("args", [])) if a else None))
+    return out
+
+
+def init_group(store, rank: int, world: int, backend: str, timeout_s: int = 600, device_index=None):
+    import torch
+
+    kw = dict(backend=backend, store=dist.PrefixStore(PREFIX + "pg", store), rank=rank, world_size=world,
+              timeout=datetime.timedelta(seconds=timeout_s))
+    if backend == "nccl" and torch.cuda.is_available():
+        torch.cuda.set_device(device_index or 0)
+        kw["device_id"] = torch.device("cuda", device_index or 0)
+    dist.init_process_group(**kw)

@@ -221,7 +221,7 @@ void hyper_adam_outer(torch::Tensor W, torch::Tensor b, torch::Tensor m, torch::
 
 std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
-                                    int64_t opt_mode) {
+                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps) {
   check_dev(params, "params", torch::kFloat32);
   check_dev(rows, "rows", torch::kFloat32);
   check_dev(order, "order", torch::kInt32);
@@ -253,6 +253,12 @@ std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, to
   a.batch = (int)batch;
   a.lr = (float)lr;
   a.opt_mode = (int)opt_mode;
+  a.stamps = nullptr;
+  if (stamps.has_value() && stamps->defined()) {
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == torch::kInt64 && stamps->numel() >= 32,
+                "stamps must be a device int64 tensor with >= 32 entries");
+    a.stamps = (uint64_t*)stamps->data_ptr<int64_t>();
+  }
   TORCH_CHECK(afl_tf_train(&a, cur()) == 0, "tf_train launch failed");
   AFL_CHECK_LAUNCH();
   return {ok, losses};
@@ -290,7 +296,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hyper_delta_vjp", &hyper_delta_vjp);
   m.def("hyper_generate", &hyper_generate);
   m.def("hyper_adam_outer", &hyper_adam_outer);
-  m.def("tf_train", &tf_train);
+  m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
+        py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
+        py::arg("stamps") = py::none());
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);

@@ -49,6 +49,7 @@ struct AflTfTrainArgs {
   int C, E, maxnd, batch;
   float lr;
   int opt_mode;  // 0 = Adam (reference), 1 = SGD (test hook: exposes raw gradients)
+  uint64_t* stamps;  // optional per-phase timers (AFL_TF_STAMPS builds), may be null
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);

@@ -136,6 +136,15 @@ struct Ctx {
   unsigned short* BF;  // bf16 weight copies
   float* ws;
   int tid, lane, wave;
+  int r, q;  // row-per-4-lanes layout: row, quarter
+
+  // barrier + make every base value opaque, so the compiler recomputes addresses per phase instead of
+  // keeping hundreds of CSE'd pointers live across the whole step (which spills to scratch)
+  __device__ __forceinline__ void sync() {
+    __syncthreads();
+    asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
+    asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
+  }
 
   __device__ float* acc() const { return (float*)(smem + S_ACC); }
   __device__ unsigned short* u16(int off) const { return (unsigned short*)(smem + off); }
@@ -330,30 +339,416 @@ __device__ void init_copies(const Ctx& c, MatW mw) {
   }
 }
 
-struct Branch {
-  BrOff o;
-  BrW w;
-  BrS s;
-  int din, xoff, br;
-  __device__ MatW dense() const { return MatW{o.dense_w, 64, din, w.WFd, 32, -1, 0}; }
-  __device__ MatW vproj() const { return MatW{o.inproj_w + 128 * 64, 64, 64, w.WFv, 64, w.WTv, 64}; }
-  __device__ MatW oproj() const { return MatW{o.out_w, 64, 64, w.WFo, 64, w.WTo, 64}; }
-  __device__ MatW ff0() const { return MatW{o.ff0_w, 6, 64, w.WF1, 64, w.WT1, 32}; }
-  __device__ MatW ff3() const { return MatW{o.ff3_w, 64, 6, w.WF2, 32, w.WT2, 64}; }
+template <int BR>
+struct BrC {
+  static constexpr BrOff o = BR == 0 ? OV : OL;
+  static constexpr BrW w = BR == 0 ? WBV : WBL;
+  static constexpr BrS s = BR == 0 ? SV : SL;
+  static constexpr int din = BR == 0 ? D_V : D_L;
+  static constexpr int xoff = BR == 0 ? 0 : D_V;
+  static constexpr MatW dense{o.dense_w, 64, din, w.WFd, 32, -1, 0};
+  static constexpr MatW vproj{o.inproj_w + 128 * 64, 64, 64, w.WFv, 64, w.WTv, 64};
+  static constexpr MatW oproj{o.out_w, 64, 64, w.WFo, 64, w.WTo, 64};
+  static constexpr MatW ff0{o.ff0_w, FF, 64, w.WF1, 64, w.WT1, 32};
+  static constexpr MatW ff3{o.ff3_w, 64, FF, w.WF2, 32, w.WT2, 64};
+};
+constexpr MatW MFC1{FC1_W, 64, 128, WFF1, 128, WTF1, 64};
+constexpr MatW MFC2{FC2_W, 32, 64, WFF2, 64, WTF2, 32};
+
+// ---- weight fragments prefetched into registers before the barrier that precedes their GEMM ----
+template <int N, int K>
+struct WFr {
+  s8v f[N / 16][K / 32];
+};
+template <int N, int K>
+__device__ __forceinline__ void wload(WFr<N, K>& w, const unsigned short* W, int lane) {
+#pragma unroll
+  for (int t = 0; t < N / 16; ++t)
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) w.f[t][kk] = glb_frag(W, K, 16 * t, 32 * kk, lane);
+}
+template <int N, int K>
+__device__ __forceinline__ void gemm_pf(const Ctx& c, const unsigned short* A, int lda, const WFr<N, K>& w) {
+  constexpr int NTL = N / 16;
+  f4v acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int r0 = 16 * c.wave;
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk) {
+    s8v a = lds_row_frag(A, lda, r0, 32 * kk, c.lane);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, w.f[t][kk], acc[t]);
+  }
+  float* out = c.acc();
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
+}
+
+// per-step, per-thread state (row-per-4-lanes layout)
+struct St {
+  int r, q;       // row, quarter
+  bool valid;     // r < Bn
+  int ridx;       // train row index
+  int Bn;
+  uint32_t key;   // dropout key of this step
+  AdamK K;
+  const float* rows;
 };
 
-__device__ __forceinline__ Branch branch(int br) {
-  Branch b;
-  b.o = br == 0 ? OV : OL;
-  b.w = br == 0 ? WBV : WBL;
-  b.s = br == 0 ? SV : SL;
-  b.din = br == 0 ? D_V : D_L;
-  b.xoff = br == 0 ? 0 : D_V;
-  b.br = br;
-  return b;
+// opaque per-phase row offset: keeps the compiler from hoisting dozens of per-thread addresses out of
+// the step loop (they would stay live across the whole loop and spill)
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// per-phase wall-clock stamps (s_memrealtime, 100 MHz) of workgroup 0, accumulated over all steps;
+// only when the caller passes a stamps buffer (diagnostics; one uniform branch per phase otherwise)
+#define STAMP(id)                                                                   \
+  do {                                                                              \
+    if (stamps && blockIdx.x == 0 && threadIdx.x == 0) {                           \
+      uint64_t now_ = __builtin_amdgcn_s_memrealtime();                            \
+      stamps[id] += now_ - t_prev;                                                  \
+      t_prev = now_;                                                                \
+    }                                                                               \
+  } while (0)
+
+template <int BR>
+__device__ __forceinline__ void gather_x(const Ctx& c, const St& s) {
+  using B = BrC<BR>;
+  unsigned short* XIN = c.u16(S_XIN);
+  s8v v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = s.q * 8 + j;
+    float x = (s.valid && col < B::din) ? s.rows[(long)s.ridx * ROW + B::xoff + col] : 0.f;
+    v[j] = (short)f2bf(x);
+  }
+  *(LDS_AS s8v*)(XIN + s.r * LD32 + s.q * 8) = v;
+}
+
+// ============================================================== branch forward
+template <int BR>
+__device__ __forceinline__ void fwd_branch(Ctx& c, const St& s, uint64_t* stamps, uint64_t& t_prev) {
+  using B = BrC<BR>;
+  unsigned short* XIN = c.u16(S_XIN);
+  unsigned short* TA = c.u16(S_TA);
+  unsigned short* TB = c.u16(S_TB);
+  unsigned short* TC = c.u16(S_TC);
+  unsigned short* CAT = c.u16(S_CAT);
+  unsigned short* F2 = c.u16(S_F2);
+  float* ACC = c.acc();
+  int r = c.r, q = c.q, c0 = q * 16;
+  WFr<64, 32> wd;
+  wload(wd, c.BF + B::w.WFd, c.lane);
+  gather_x<BR>(c, s);
+  if (BR == 0 && q == 0) ((float*)(c.smem + S_LAB))[r] = s.valid ? s.rows[(long)s.ridx * ROW + ROW - 1] : 0.f;
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_pf<64, 32>(c, XIN, LD32, wd);
+  WFr<64, 64> wv;
+  wload(wv, c.BF + B::w.WFv, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(0);
+  float h[16];  // h0 stays in registers until the residual (E3)
+  {
+    const int ro = opaque(r * 64 + c0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + c.P[B::o.dense_b + c0 + j]);
+    store16bf(TA + r * LD64 + c0, h);
+    unsigned short* hb = (unsigned short*)c.wsf(B::s.H0B) + ro;
+    s8v a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = (short)f2bf(h[j]);
+      b[j] = (short)f2bf(h[j + 8]);
+    }
+    *(s8v*)hb = a;
+    *(s8v*)(hb + 8) = b;
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_pf<64, 64>(c, TA, LD64, wv);
+  WFr<64, 64> wo;
+  wload(wo, c.BF + B::w.WFo, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(1);
+  {  // E2: a = head_dropout(v)
+    float x[16];
+    const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B::o.inproj_b + 128 + c0 + j]) * m;
+    store16bf(TB + r * LD64 + c0, x);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_pf<64, 64>(c, TB, LD64, wo);
+  WFr<16, 64> w1;
+  wload(w1, c.BF + B::w.WF1, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(2);
+  float x1[16];  // x1 stays in registers until the second residual (E5)
+  {
+    const int ro = opaque(r * 64 + c0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float o = ACC[r * LDACC + c0 + j] + c.P[B::o.out_b + c0 + j];
+      x1[j] = h[j] + (keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? o * INV_K01 : 0.f);
+    }
+    const float rstd = ln_fwd(x1);
+    store16(c.wsf(B::s.XH1) + ro, x1);
+    if (q == 0) c.wsf(B::s.R1)[r] = rstd;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x1[j] = x1[j] * c.P[B::o.ln1_w + c0 + j] + c.P[B::o.ln1_b + c0 + j];
+    store16bf(TC + r * LD64 + c0, x1);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_pf<16, 64>(c, TC, LD64, w1);
+  WFr<64, 32> w2;
+  wload(w2, c.BF + B::w.WF2, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(3);
+  {  // E4: f0 -> f2
+    s8v v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = q * 8 + j;
+      float f2 = 0.f;
+      if (col < FF) {
+        const float f0 = ACC[r * LDACC + col] + c.P[B::o.ff0_b + col];
+        c.wsf(B::s.F0)[opaque(r * 8) + col] = f0;
+        f2 = keep(s.key, 8 * BR + L_DF, r, col, THR_P01) ? gelu(f0) * INV_K01 : 0.f;
+      }
+      v[j] = (short)f2bf(f2);
+    }
+    *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_pf<64, 32>(c, F2, LD32, w2);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(4);
+  {  // E5: r2 = x1 + drop(f3); LN2; LN3 -> CAT
+    const int ro = opaque(r * 64 + c0);
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float f3 = ACC[r * LDACC + c0 + j] + c.P[B::o.ff3_b + c0 + j];
+      x[j] = x1[j] + (keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? f3 * INV_K01 : 0.f);
+    }
+    float rstd = ln_fwd(x);
+    store16(c.wsf(B::s.XH2) + ro, x);
+    if (q == 0) c.wsf(B::s.R2)[r] = rstd;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B::o.ln2_w + c0 + j] + c.P[B::o.ln2_b + c0 + j];
+    rstd = ln_fwd(x);
+    store16(c.wsf(B::s.XH3) + ro, x);
+    if (q == 0) c.wsf(B::s.R3)[r] = rstd;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B::o.bn_w + c0 + j] + c.P[B::o.bn_b + c0 + j];
+    store16bf(CAT + r * LD128 + BR * 64 + c0, x);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(5);
+}
+
+// ============================================================== branch backward
+// on entry: dx3 of this branch in ACC (BR == 1) or in the DX3V workspace (BR == 0)
+template <int BR>
+__device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps, uint64_t& t_prev) {
+  using B = BrC<BR>;
+  unsigned short* XIN = c.u16(S_XIN);  // also DF0
+  unsigned short* TA = c.u16(S_TA);
+  unsigned short* TB = c.u16(S_TB);
+  unsigned short* TC = c.u16(S_TC);
+  unsigned short* TD = c.u16(S_CAT);  // [128][72] alias of CAT (dead after dWf1)
+  unsigned short* F2 = c.u16(S_F2);
+  float* ACC = c.acc();
+  int r = c.r, q = c.q, c0 = q * 16;
+  const AdamK K = s.K;
+  float dr2[16];  // residual gradient into x1, kept in registers until E12
+  WFr<16, 64> wt2;
+  wload(wt2, c.BF + B::w.WT2, c.lane);
+  {  // E10: LN3 bwd, LN2 bwd, df3 ; colsums g3 (v0), b3 (v1), g2 (v2), be2 (v3), b2 (v4)
+    const int ro = opaque(r * 64 + c0);
+    float dy[16], xh[16], dx[16], t[16];
+    if (BR == 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
+    } else {
+      load16(dy, c.wsf(W_DX3V) + ro);
+    }
+    load16(xh, c.wsf(B::s.XH3) + ro);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
+    colsum16(c, 0, t);
+    colsum16(c, 1, dy);
+    ln_bwd(dx, dy, xh, c.wsf(B::s.R3)[r], c.P + B::o.bn_w, c0);
+    load16(xh, c.wsf(B::s.XH2) + ro);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    colsum16(c, 2, t);
+    colsum16(c, 3, dx);
+    ln_bwd(dr2, dx, xh, c.wsf(B::s.R2)[r], c.P + B::o.ln2_w, c0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? dr2[j] * INV_K01 : 0.f;
+    store16bf(TA + r * LD64 + c0, t);
+    colsum16(c, 4, t);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(10);
+  // A10 + G11 (df2 = df3 . W2)
+  if (c.tid < 64) {
+    const int i = c.tid;
+    adam(c.P, c.M, c.V, B::o.bn_w + i, cs_total(c, 0, i), K);
+    adam(c.P, c.M, c.V, B::o.bn_b + i, cs_total(c, 1, i), K);
+    adam(c.P, c.M, c.V, B::o.ln2_w + i, cs_total(c, 2, i), K);
+    adam(c.P, c.M, c.V, B::o.ln2_b + i, cs_total(c, 3, i), K);
+    adam(c.P, c.M, c.V, B::o.ff3_b + i, cs_total(c, 4, i), K);
+  }
+  gemm_pf<16, 64>(c, TA, LD64, wt2);
+  WFr<64, 32> wt1;
+  wload(wt1, c.BF + B::w.WT1, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(11);
+  {  // E11: df0 (-> DF0 = XIN region), recompute f2 (-> F2); colsum b1 (v5)
+    s8v vd, vf;
+    float db[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = q * 8 + j;
+      float d0 = 0.f, f2 = 0.f;
+      if (col < FF) {
+        const float f0 = c.wsf(B::s.F0)[opaque(r * 8) + col];
+        const bool kp = keep(s.key, 8 * BR + L_DF, r, col, THR_P01);
+        d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
+        f2 = kp ? gelu(f0) * INV_K01 : 0.f;
+      }
+      db[j] = d0;
+      vd[j] = (short)f2bf(d0);
+      vf[j] = (short)f2bf(f2);
+    }
+    *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = vd;
+    *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = vf;
+    colsumW<8>(c, 5, db, q * 8);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(12);
+  gemm_pf<64, 32>(c, XIN, LD32, wt1);                 // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
+  gemm_dw_adam<4, 1>(c, TA, LD64, F2, LD32, B::ff3, K);  // dW2 = df3^T f2
+  if (c.tid < FF) adam(c.P, c.M, c.V, B::o.ff0_b + c.tid, cs_total(c, 5, c.tid), K);
+  WFr<64, 64> wto;
+  wload(wto, c.BF + B::w.WTo, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(13);
+  float dh0[16];  // residual gradient into h0, kept in registers until E15
+  {  // E12: dx1 += dr2 ; LN1 bwd ; do ; x1 recompute ; colsums g1 (v0), be1 (v1), bo (v2)
+    const int ro = opaque(r * 64 + c0);
+    float dx[16], xh[16], t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dx[j] = ACC[r * LDACC + c0 + j] + dr2[j];
+    load16(xh, c.wsf(B::s.XH1) + ro);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    colsum16(c, 0, t);
+    colsum16(c, 1, dx);
+    ln_bwd(dh0, dx, xh, c.wsf(B::s.R1)[r], c.P + B::o.ln1_w, c0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? dh0[j] * INV_K01 : 0.f;
+    store16bf(TB + r * LD64 + c0, t);
+    colsum16(c, 2, t);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = xh[j] * c.P[B::o.ln1_w + c0 + j] + c.P[B::o.ln1_b + c0 + j];
+    store16bf(TC + r * LD64 + c0, t);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(14);
+  gemm_pf<64, 64>(c, TB, LD64, wto);                     // da = do . Wo
+  gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B::ff0, K);  // dW1 = df0^T x1
+  if (c.tid < 64) {
+    const int i = c.tid;
+    adam(c.P, c.M, c.V, B::o.ln1_w + i, cs_total(c, 0, i), K);
+    adam(c.P, c.M, c.V, B::o.ln1_b + i, cs_total(c, 1, i), K);
+    adam(c.P, c.M, c.V, B::o.out_b + i, cs_total(c, 2, i), K);
+  }
+  WFr<64, 64> wfv;
+  wload(wfv, c.BF + B::w.WFv, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(15);
+  {  // E13: dv (-> TC) ; reload h0 (-> TA) ; colsum bv (v3)
+    const int ro = opaque(r * 64 + c0);
+    float d[16];
+    const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = ACC[r * LDACC + c0 + j] * m;
+    store16bf(TC + r * LD64 + c0, d);
+    colsum16(c, 3, d);
+    const unsigned short* hb = (const unsigned short*)c.wsf(B::s.H0B) + ro;
+    s8v h0a = *(const s8v*)hb, h0b = *(const s8v*)(hb + 8);
+    *(LDS_AS s8v*)(TA + r * LD64 + c0) = h0a;
+    *(LDS_AS s8v*)(TA + r * LD64 + c0 + 8) = h0b;
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(16);
+  gemm_pf<64, 64>(c, TA, LD64, wfv);  // v recompute (before Wv's Adam)
+  WFr<64, 64> wtv;
+  wload(wtv, c.BF + B::w.WTv, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  {  // E13b: a = head_dropout(v) -> TD
+    float x[16];
+    const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B::o.inproj_b + 128 + c0 + j]) * m;
+    store16bf(TD + r * LD64 + c0, x);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(17);
+  gemm_pf<64, 64>(c, TC, LD64, wtv);                       // dh0 part = dv . Wv
+  gemm_dw_adam<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K);  // dWo = do^T a
+  if (c.tid < 64) adam(c.P, c.M, c.V, B::o.inproj_b + 128 + c.tid, cs_total(c, 3, c.tid), K);
+  WFr<64, 32> wd;
+  wload(wd, c.BF + B::w.WFd, c.lane);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(18);
+  {  // E14: dh0 += ACC ; gather x for the z0 recompute
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dh0[j] += ACC[r * LDACC + c0 + j];
+    gather_x<BR>(c, s);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K);  // dWv = dv^T h0
+  gemm_pf<64, 32>(c, XIN, LD32, wd);                       // z0 recompute
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(19);
+  {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
+    float d[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = dh0[j] * gelu_grad(ACC[r * LDACC + c0 + j] + c.P[B::o.dense_b + c0 + j]);
+    store16bf(TB + r * LD64 + c0, d);
+    colsum16(c, 4, d);
+  }
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  gemm_dw_adam<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K);  // dWd = dz0^T x
+  if (c.tid < 64) adam(c.P, c.M, c.V, B::o.dense_b + c.tid, cs_total(c, 4, c.tid), K);
+  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  STAMP(20);
 }
 
 }  // namespace
+
+__device__ void init_copies_all(const Ctx& c) {
+  init_copies(c, BrC<0>::dense);
+  init_copies(c, BrC<0>::vproj);
+  init_copies(c, BrC<0>::oproj);
+  init_copies(c, BrC<0>::ff0);
+  init_copies(c, BrC<0>::ff3);
+  init_copies(c, BrC<1>::dense);
+  init_copies(c, BrC<1>::vproj);
+  init_copies(c, BrC<1>::oproj);
+  init_copies(c, BrC<1>::ff0);
+  init_copies(c, BrC<1>::ff3);
+  init_copies(c, MFC1);
+  init_copies(c, MFC2);
+}
 
 __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -369,27 +764,19 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   c.lane = threadIdx.x & 63;
   c.wave = threadIdx.x >> 6;
   const int tid = c.tid;
-  const int r = tid >> 2, q = tid & 3;  // row-per-4-lanes layout
+  uint64_t* stamps = a.stamps;
+  uint64_t t_prev = 0;
+  if (stamps && blockIdx.x == 0 && threadIdx.x == 0) t_prev = __builtin_amdgcn_s_memrealtime();
 
-  // ---- init: zero Adam moments, bf16 weight copies (padding zeroed first) ----
+  // ---- init: zero Adam moments, bf16 weight copies (padding zeroed first), LDS ----
   for (int i = tid; i < NPARAM; i += NT) {
     c.M[i] = 0.f;
     c.V[i] = 0.f;
   }
   for (int i = tid; i < BF_TOTAL; i += NT) c.BF[i] = 0;
-  __syncthreads();
-  for (int br = 0; br < 2; ++br) {
-    Branch B = branch(br);
-    init_copies(c, B.dense());
-    init_copies(c, B.vproj());
-    init_copies(c, B.oproj());
-    init_copies(c, B.ff0());
-    init_copies(c, B.ff3());
-  }
-  init_copies(c, MatW{FC1_W, 64, 128, WFF1, 128, WTF1, 64});
-  init_copies(c, MatW{FC2_W, 32, 64, WFF2, 64, WTF2, 32});
-  // zero LDS once (padding columns of operand buffers must be finite)
   for (int i = tid; i < S_TOTAL / 4; i += NT) ((float*)smem)[i] = 0.f;
+  __syncthreads();
+  init_copies_all(c);
   __syncthreads();
 
   const int nd = a.nd[cid];
@@ -399,19 +786,21 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   double b1t = 1.0, b2t = 1.0;
   int step = 0;
   bool failed = false;
-  const float* rows = a.rows;
   float* LAB = (float*)(smem + S_LAB);
   float* DY3 = (float*)(smem + S_DY3);
   float* RED = (float*)(smem + S_RED);
-  unsigned short* XIN = c.u16(S_XIN);
   unsigned short* TA = c.u16(S_TA);
   unsigned short* TB = c.u16(S_TB);
-  unsigned short* TC = c.u16(S_TC);
   unsigned short* CAT = c.u16(S_CAT);
   unsigned short* F2 = c.u16(S_F2);
   float* ACC = c.acc();
-  const MatW mfc1{FC1_W, 64, 128, WFF1, 128, WTF1, 64};
-  const MatW mfc2{FC2_W, 32, 64, WFF2, 64, WTF2, 32};
+  St s;
+  s.r = tid >> 2;
+  s.q = tid & 3;
+  s.rows = a.rows;
+  c.r = s.r;
+  c.q = s.q;
+  int r = c.r, q = c.q;
 
   for (int e = 0; e < a.E && !failed; ++e) {
     const int* ord = a.order + ((long)cid * a.E + e) * a.maxnd;
@@ -422,137 +811,40 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       ++step;
       b1t *= (double)B1;
       b2t *= (double)B2;
-      const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
-      const uint32_t key = afl_hash32(seed, (uint32_t)step);
-      const bool valid = r < Bn;
-      const int ridx = valid ? ord[b0 + r] : 0;
+      s.K = AdamK{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+      s.key = afl_hash32(seed, (uint32_t)step);
+      s.Bn = Bn;
+      s.valid = r < Bn;
+      s.ridx = s.valid ? ord[b0 + r] : 0;
+      const AdamK K = s.K;
 
-      // =============================== forward ===============================
-      for (int br = 0; br < 2; ++br) {
-        const Branch B = branch(br);
-        // P0: gather inputs
-        {
-          s8v v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int col = q * 8 + j;
-            float x = (valid && col < B.din) ? rows[(long)ridx * ROW + B.xoff + col] : 0.f;
-            v[j] = (short)f2bf(x);
-          }
-          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
-          if (br == 0 && q == 0) LAB[r] = valid ? rows[(long)ridx * ROW + ROW - 1] : 0.f;
-        }
-        __syncthreads();
-        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WFd);
-        __syncthreads();
-        // E1: h0 = gelu(z0)
-        {
-          float h[16];
-          const int c0 = q * 16;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + c.P[B.o.dense_b + c0 + j]);
-          store16bf(TA + r * LD64 + c0, h);
-          store16(c.wsf(B.s.H0F) + r * 64 + c0, h);
-          unsigned short* hb = (unsigned short*)c.wsf(B.s.H0B) + r * 64 + c0;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) hb[j] = f2bf(h[j]);
-        }
-        __syncthreads();
-        gemm_xw<64, 64>(c, TA, LD64, c.BF + B.w.WFv);
-        __syncthreads();
-        // E2: a = head_dropout(v)
-        {
-          float x[16];
-          const int c0 = q * 16;
-          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;  // head = c0/16 = q
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B.o.inproj_b + 128 + c0 + j]) * m;
-          store16bf(TB + r * LD64 + c0, x);
-        }
-        __syncthreads();
-        gemm_xw<64, 64>(c, TB, LD64, c.BF + B.w.WFo);
-        __syncthreads();
-        // E3: r1 = h0 + drop(o); x1 = LN1(r1)
-        {
-          float x[16], h[16];
-          const int c0 = q * 16;
-          load16(h, c.wsf(B.s.H0F) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const float o = ACC[r * LDACC + c0 + j] + c.P[B.o.out_b + c0 + j];
-            x[j] = h[j] + (keep(key, 8 * br + L_D1, r, c0 + j, THR_P01) ? o * INV_K01 : 0.f);
-          }
-          const float rstd = ln_fwd(x);
-          store16(c.wsf(B.s.XH1) + r * 64 + c0, x);
-          if (q == 0) c.wsf(B.s.R1)[r] = rstd;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.ln1_w + c0 + j] + c.P[B.o.ln1_b + c0 + j];
-          store16(c.wsf(B.s.X1F) + r * 64 + c0, x);
-          store16bf(TC + r * LD64 + c0, x);
-        }
-        __syncthreads();
-        gemm_xw<16, 64>(c, TC, LD64, c.BF + B.w.WF1);
-        __syncthreads();
-        // E4: f0 -> f2 = drop(gelu(f0)) (cols 0..5; rest of the K=32 operand zeroed)
-        {
-          s8v v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int col = q * 8 + j;
-            float f2 = 0.f;
-            if (col < FF) {
-              const float f0 = ACC[r * LDACC + col] + c.P[B.o.ff0_b + col];
-              c.wsf(B.s.F0)[r * 8 + col] = f0;
-              f2 = keep(key, 8 * br + L_DF, r, col, THR_P01) ? gelu(f0) * INV_K01 : 0.f;
-            }
-            v[j] = (short)f2bf(f2);
-          }
-          *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
-        }
-        __syncthreads();
-        gemm_xw<64, 32>(c, F2, LD32, c.BF + B.w.WF2);
-        __syncthreads();
-        // E5: r2 = x1 + drop(f3); x2 = LN2(r2); x3 = LN3(x2) -> CAT
-        {
-          float x[16], x1[16];
-          const int c0 = q * 16;
-          load16(x1, c.wsf(B.s.X1F) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const float f3 = ACC[r * LDACC + c0 + j] + c.P[B.o.ff3_b + c0 + j];
-            x[j] = x1[j] + (keep(key, 8 * br + L_D2, r, c0 + j, THR_P01) ? f3 * INV_K01 : 0.f);
-          }
-          float rstd = ln_fwd(x);
-          store16(c.wsf(B.s.XH2) + r * 64 + c0, x);
-          if (q == 0) c.wsf(B.s.R2)[r] = rstd;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.ln2_w + c0 + j] + c.P[B.o.ln2_b + c0 + j];
-          rstd = ln_fwd(x);
-          store16(c.wsf(B.s.XH3) + r * 64 + c0, x);
-          if (q == 0) c.wsf(B.s.R3)[r] = rstd;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B.o.bn_w + c0 + j] + c.P[B.o.bn_b + c0 + j];
-          store16bf(CAT + r * LD128 + br * 64 + c0, x);
-        }
-        __syncthreads();
-      }
+      fwd_branch<0>(c, s, stamps, t_prev);
+      fwd_branch<1>(c, s, stamps, t_prev);
       // =============================== head forward + loss ===============================
-      gemm_xw<64, 128>(c, CAT, LD128, c.BF + WFF1);
-      __syncthreads();
-      {  // E6: y1 -> d1 = drop0.3(gelu(y1))
-        float x[16], y[16];
+      WFr<64, 128> wf1;
+      wload(wf1, c.BF + WFF1, c.lane);
+      gemm_pf<64, 128>(c, CAT, LD128, wf1);
+      WFr<32, 64> wf2;
+      wload(wf2, c.BF + WFF2, c.lane);
+      { c.sync(); r = c.r; q = c.q; }
+      STAMP(6);
+      float y1[16];  // kept in registers until E8
+      {              // E6: y1 -> d1 = drop0.3(gelu(y1))
+        float x[16];
         const int c0 = q * 16;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          y[j] = ACC[r * LDACC + c0 + j] + c.P[FC1_B + c0 + j];
-          x[j] = keep(key, L_HEAD, r, c0 + j, THR_P03) ? gelu(y[j]) * INV_K03 : 0.f;
+          y1[j] = ACC[r * LDACC + c0 + j] + c.P[FC1_B + c0 + j];
+          x[j] = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? gelu(y1[j]) * INV_K03 : 0.f;
         }
-        store16(c.wsf(W_Y1) + r * 64 + c0, y);
         store16bf(TA + r * LD64 + c0, x);
       }
-      __syncthreads();
-      gemm_xw<32, 64>(c, TA, LD64, c.BF + WFF2);
-      __syncthreads();
+      { c.sync(); r = c.r; q = c.q; }
+      gemm_pf<32, 64>(c, TA, LD64, wf2);
+      WFr<64, 32> wtf2;
+      wload(wtf2, c.BF + WTF2, c.lane);
+      { c.sync(); r = c.r; q = c.q; }
+      STAMP(7);
       {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
         float y2[8], g2[8], dot = 0.f;
         const int c0 = q * 8;
@@ -566,7 +858,7 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
         const float p = sigmoidf_(y3);
         const float lab = LAB[r];
         float lrow = 0.f, dy3 = 0.f;
-        if (valid) {
+        if (s.valid) {
           // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
           const float lg = logf(p), lg1 = log1pf(-p);
           const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
@@ -587,223 +879,66 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
         *(LDS_AS s8v*)(F2 + r * LD32 + c0) = v;  // T32 aliases F2
         colsumW<8>(c, 0, gw, c0);
         colsumW<8>(c, 1, dy2, c0);
-        // loss reduction (q == 0 lanes carry the row loss)
         float lsum = wave_sum(q == 0 ? lrow : 0.f);
         if (c.lane == 0) RED[c.wave] = lsum;
       }
-      __syncthreads();
+      { c.sync(); r = c.r; q = c.q; }
       {
         float tot = 0.f;
         for (int w = 0; w < 8; ++w) tot += RED[w];
         const float loss = tot / (float)Bn;
-        if (loss != loss) {
-          failed = true;  // uniform across the workgroup
-        } else {
-          epoch_loss += loss;
-        }
+        if (loss != loss) failed = true;  // uniform across the workgroup
+        else epoch_loss += loss;
       }
       if (failed) break;
       // =============================== head backward ===============================
-      // A7: Adam output.weight / output.bias / fc2.bias
       if (tid < 32) {
         adam(c.P, c.M, c.V, OUT_W + tid, cs_total(c, 0, tid), K);
       } else if (tid < 64) {
         adam(c.P, c.M, c.V, FC2_B + tid - 32, cs_total(c, 1, tid - 32), K);
       } else if (tid == 64) {
-        float s = 0.f;
-        for (int i = 0; i < BM; ++i) s += DY3[i];
-        adam(c.P, c.M, c.V, OUT_B, s, K);
+        float sm = 0.f;
+        for (int i = 0; i < BM; ++i) sm += DY3[i];
+        adam(c.P, c.M, c.V, OUT_B, sm, K);
       }
-      gemm_xw<64, 32>(c, F2, LD32, c.BF + WTF2);  // dd1 = dy2 . Wf2
-      __syncthreads();
+      gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
+      WFr<64, 64> wtf1a;
+      wload(wtf1a, c.BF + WTF1, c.lane);
+      { c.sync(); r = c.r; q = c.q; }
+      STAMP(8);
       {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
-        float d[16], y[16];
+        float d[16];
         const int c0 = q * 16;
-        load16(y, c.wsf(W_Y1) + r * 64 + c0);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float g = keep(key, L_HEAD, r, c0 + j, THR_P03) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
-          d[j] = g * gelu_grad(y[j]);
+          const float g = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
+          d[j] = g * gelu_grad(y1[j]);
         }
         store16bf(TB + r * LD64 + c0, d);
         colsum16(c, 2, d);
       }
-      __syncthreads();
-      gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, mfc2, K);  // dWf2 = dy2^T d1
+      { c.sync(); r = c.r; q = c.q; }
+      gemm_pf<64, 64>(c, TB, LD64, wtf1a);                 // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
+      gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
       if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
-      __syncthreads();
-      gemm_xw<64, 64>(c, TB, LD64, c.BF + WTF1);  // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
-      __syncthreads();
-      for (int i = tid; i < BM * 64; i += NT) c.wsf(W_DX3V)[i] = ACC[(i >> 6) * LDACC + (i & 63)];
-      __syncthreads();
-      gemm_xw<64, 64>(c, TB, LD64, c.BF + WTF1 + 64 * 64);  // dcat[:, 64:128] (kept in ACC for branch 1)
-      __syncthreads();
-      gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, mfc1, K);  // dWf1 = dy1^T cat
-      __syncthreads();
-
-      // =============================== branch backward (labs first, dx3 in ACC) ===============================
-      for (int br = 1; br >= 0; --br) {
-        const Branch B = branch(br);
-        {  // E10: LN3 bwd, LN2 bwd, df3 ; colsums g3 (v0), b3 (v1), g2 (v2), be2 (v3), b2 (v4)
-          float dy[16], xh[16], dx[16];
-          const int c0 = q * 16;
-          if (br == 1) {
+      WFr<64, 64> wtf1b;
+      wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
+      { c.sync(); r = c.r; q = c.q; }
+      {
+        float t[16];
+        const int c0 = q * 16;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
-          } else {
-            load16(dy, c.wsf(W_DX3V) + r * 64 + c0);
-          }
-          load16(xh, c.wsf(B.s.XH3) + r * 64 + c0);
-          float t[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
-          colsum16(c, 0, t);
-          colsum16(c, 1, dy);
-          ln_bwd(dx, dy, xh, c.wsf(B.s.R3)[r], c.P + B.o.bn_w, c0);
-          load16(xh, c.wsf(B.s.XH2) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-          colsum16(c, 2, t);
-          colsum16(c, 3, dx);
-          ln_bwd(dy, dx, xh, c.wsf(B.s.R2)[r], c.P + B.o.ln2_w, c0);  // dy := dr2
-          store16(c.wsf(B.s.DX1F) + r * 64 + c0, dy);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = keep(key, 8 * br + L_D2, r, c0 + j, THR_P01) ? dy[j] * INV_K01 : 0.f;
-          store16bf(TA + r * LD64 + c0, t);
-          colsum16(c, 4, t);
-        }
-        __syncthreads();
-        // A10 (LN/bias vectors) + G11 (df2 = df3 . W2)
-        if (tid < 64) {
-          adam(c.P, c.M, c.V, B.o.bn_w + tid, cs_total(c, 0, tid), K);
-          adam(c.P, c.M, c.V, B.o.bn_b + tid, cs_total(c, 1, tid), K);
-          adam(c.P, c.M, c.V, B.o.ln2_w + tid, cs_total(c, 2, tid), K);
-          adam(c.P, c.M, c.V, B.o.ln2_b + tid, cs_total(c, 3, tid), K);
-          adam(c.P, c.M, c.V, B.o.ff3_b + tid, cs_total(c, 4, tid), K);
-        }
-        gemm_xw<16, 64>(c, TA, LD64, c.BF + B.w.WT2);
-        __syncthreads();
-        {  // E11: df0 (-> DF0 = XIN region), recompute f2 (-> F2); colsum b1 (v5)
-          s8v vd, vf;
-          float db[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int col = q * 8 + j;
-            float d0 = 0.f, f2 = 0.f;
-            if (col < FF) {
-              const float f0 = c.wsf(B.s.F0)[r * 8 + col];
-              const bool kp = keep(key, 8 * br + L_DF, r, col, THR_P01);
-              d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
-              f2 = kp ? gelu(f0) * INV_K01 : 0.f;
-            }
-            db[j] = d0;
-            vd[j] = (short)f2bf(d0);
-            vf[j] = (short)f2bf(f2);
-          }
-          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = vd;
-          *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = vf;
-          colsumW<8>(c, 5, db, q * 8);
-        }
-        __syncthreads();
-        gemm_dw_adam<4, 1>(c, TA, LD64, F2, LD32, B.ff3(), K);  // dW2 = df3^T f2
-        if (tid < FF) adam(c.P, c.M, c.V, B.o.ff0_b + tid, cs_total(c, 5, tid), K);
-        __syncthreads();
-        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WT1);  // dx1 = df0 . W1
-        __syncthreads();
-        {  // E12: dx1 += DX1F ; LN1 bwd ; do ; x1 recompute ; colsums g1 (v0), be1 (v1), bo (v2)
-          float dx[16], xh[16], t[16], d[16];
-          const int c0 = q * 16;
-          load16(t, c.wsf(B.s.DX1F) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) dx[j] = ACC[r * LDACC + c0 + j] + t[j];
-          load16(xh, c.wsf(B.s.XH1) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-          colsum16(c, 0, t);
-          colsum16(c, 1, dx);
-          ln_bwd(d, dx, xh, c.wsf(B.s.R1)[r], c.P + B.o.ln1_w, c0);  // d = dr1
-          store16(c.wsf(B.s.DH0F) + r * 64 + c0, d);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = keep(key, 8 * br + L_D1, r, c0 + j, THR_P01) ? d[j] * INV_K01 : 0.f;
-          store16bf(TB + r * LD64 + c0, t);
-          colsum16(c, 2, t);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = xh[j] * c.P[B.o.ln1_w + c0 + j] + c.P[B.o.ln1_b + c0 + j];
-          store16bf(TC + r * LD64 + c0, t);
-        }
-        __syncthreads();
-        gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B.ff0(), K);  // dW1 = df0^T x1
-        if (tid < 64) {
-          adam(c.P, c.M, c.V, B.o.ln1_w + tid, cs_total(c, 0, tid), K);
-          adam(c.P, c.M, c.V, B.o.ln1_b + tid, cs_total(c, 1, tid), K);
-          adam(c.P, c.M, c.V, B.o.out_b + tid, cs_total(c, 2, tid), K);
-        }
-        __syncthreads();
-        gemm_xw<64, 64>(c, TB, LD64, c.BF + B.w.WTo);  // da = do . Wo
-        __syncthreads();
-        {  // E13: dv ; reload h0 ; colsum bv (v3)
-          float d[16];
-          const int c0 = q * 16;
-          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) d[j] = ACC[r * LDACC + c0 + j] * m;
-          store16bf(TC + r * LD64 + c0, d);
-          colsum16(c, 3, d);
-          const unsigned short* hb = (const unsigned short*)c.wsf(B.s.H0B) + r * 64 + c0;
-          s8v h0a = *(const s8v*)hb, h0b = *(const s8v*)(hb + 8);
-          *(LDS_AS s8v*)(TA + r * LD64 + c0) = h0a;
-          *(LDS_AS s8v*)(TA + r * LD64 + c0 + 8) = h0b;
-        }
-        __syncthreads();
-        gemm_xw<64, 64>(c, TA, LD64, c.BF + B.w.WFv);  // v recompute
-        __syncthreads();
-        {  // E13b: a = head_dropout(v) -> TD (CAT region, ld 72)
-          float x[16];
-          const int c0 = q * 16;
-          const float m = keep(key, 8 * br + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B.o.inproj_b + 128 + c0 + j]) * m;
-          store16bf(CAT + r * LD64 + c0, x);
-        }
-        __syncthreads();
-        gemm_xw<64, 64>(c, TC, LD64, c.BF + B.w.WTv);  // dh0 part = dv . Wv
-        gemm_dw_adam<4, 4>(c, TB, LD64, CAT, LD64, B.oproj(), K);  // dWo = do^T a  (WTo not read here)
-        if (tid < 64) adam(c.P, c.M, c.V, B.o.inproj_b + 128 + tid, cs_total(c, 3, tid), K);
-        __syncthreads();
-        {  // E14: DH0F += ACC ; gather x for z0 recompute
-          float t[16];
-          const int c0 = q * 16;
-          load16(t, c.wsf(B.s.DH0F) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] += ACC[r * LDACC + c0 + j];
-          store16(c.wsf(B.s.DH0F) + r * 64 + c0, t);
-          s8v v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int col = q * 8 + j;
-            float x = (valid && col < B.din) ? rows[(long)ridx * ROW + B.xoff + col] : 0.f;
-            v[j] = (short)f2bf(x);
-          }
-          *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
-        }
-        __syncthreads();
-        gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B.vproj(), K);  // dWv = dv^T h0 (after WFv/WTv reads)
-        gemm_xw<64, 32>(c, XIN, LD32, c.BF + B.w.WFd);             // z0 recompute
-        __syncthreads();
-        {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
-          float t[16], d[16];
-          const int c0 = q * 16;
-          load16(t, c.wsf(B.s.DH0F) + r * 64 + c0);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) d[j] = t[j] * gelu_grad(ACC[r * LDACC + c0 + j] + c.P[B.o.dense_b + c0 + j]);
-          store16bf(TB + r * LD64 + c0, d);
-          colsum16(c, 4, d);
-        }
-        __syncthreads();
-        gemm_dw_adam<4, 1>(c, TB, LD64, XIN, LD32, B.dense(), K);  // dWd = dz0^T x
-        if (tid < 64) adam(c.P, c.M, c.V, B.o.dense_b + tid, cs_total(c, 4, tid), K);
-        __syncthreads();
+        for (int j = 0; j < 16; ++j) t[j] = ACC[r * LDACC + c0 + j];
+        store16(c.wsf(W_DX3V) + opaque(r * 64 + c0), t);
       }
+      { c.sync(); r = c.r; q = c.q; }
+      gemm_pf<64, 64>(c, TB, LD64, wtf1b);  // dcat[:, 64:128] (kept in ACC for the labs branch)
+      { c.sync(); r = c.r; q = c.q; }
+      gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, MFC1, K);  // dWf1 = dy1^T cat
+      { c.sync(); r = c.r; q = c.q; }
+      STAMP(9);
+      bwd_branch<1>(c, s, stamps, t_prev);
+      bwd_branch<0>(c, s, stamps, t_prev);
     }
     if (tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
   }
@@ -811,9 +946,86 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
 }
 
 // ================================================================================================
-// eval forward: one 512-thread workgroup per 128-row tile of the test set, weights read directly
-// from the fp32 params (converted to bf16 copies in LDS once per tile would not pay: reuse is 1).
+// eval forward: one 512-thread workgroup per 128-row tile of the test set (dropout off)
 // ================================================================================================
+template <int BR>
+__device__ __forceinline__ void eval_branch(const Ctx& c, const unsigned short* BF, const float* rows, bool valid,
+                                            long ridx) {
+  using B = BrC<BR>;
+  const float* P = c.P;
+  const int tid = c.tid, r = tid >> 2, q = tid & 3, c0 = q * 16;
+  unsigned short* XIN = c.u16(S_XIN);
+  unsigned short* TA = c.u16(S_TA);
+  unsigned short* TB = c.u16(S_TB);
+  unsigned short* CAT = c.u16(S_CAT);
+  unsigned short* F2 = c.u16(S_F2);
+  float* ACC = c.acc();
+  {
+    s8v v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = q * 8 + j;
+      float x = (valid && col < B::din) ? rows[ridx * ROW + B::xoff + col] : 0.f;
+      v[j] = (short)f2bf(x);
+    }
+    *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
+  }
+  __syncthreads();
+  gemm_xw<64, 32>(c, XIN, LD32, BF + B::w.WFd);
+  __syncthreads();
+  float h[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + P[B::o.dense_b + c0 + j]);
+  store16bf(TA + r * LD64 + c0, h);
+  __syncthreads();
+  gemm_xw<64, 64>(c, TA, LD64, BF + B::w.WFv);
+  __syncthreads();
+  {
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = ACC[r * LDACC + c0 + j] + P[B::o.inproj_b + 128 + c0 + j];
+    store16bf(TB + r * LD64 + c0, x);
+  }
+  __syncthreads();
+  gemm_xw<64, 64>(c, TB, LD64, BF + B::w.WFo);
+  __syncthreads();
+  float x1[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x1[j] = h[j] + ACC[r * LDACC + c0 + j] + P[B::o.out_b + c0 + j];
+  ln_fwd(x1);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x1[j] = x1[j] * P[B::o.ln1_w + c0 + j] + P[B::o.ln1_b + c0 + j];
+  store16bf(TA + r * LD64 + c0, x1);
+  __syncthreads();
+  gemm_xw<16, 64>(c, TA, LD64, BF + B::w.WF1);
+  __syncthreads();
+  {
+    s8v v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = q * 8 + j;
+      v[j] = (short)f2bf(col < FF ? gelu(ACC[r * LDACC + col] + P[B::o.ff0_b + col]) : 0.f);
+    }
+    *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
+  }
+  __syncthreads();
+  gemm_xw<64, 32>(c, F2, LD32, BF + B::w.WF2);
+  __syncthreads();
+  {
+    float x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = x1[j] + ACC[r * LDACC + c0 + j] + P[B::o.ff3_b + c0 + j];
+    ln_fwd(x);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B::o.ln2_w + c0 + j] + P[B::o.ln2_b + c0 + j];
+    ln_fwd(x);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B::o.bn_w + c0 + j] + P[B::o.bn_b + c0 + j];
+    store16bf(CAT + r * LD128 + BR * 64 + c0, x);
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, const unsigned short* __restrict__ BF,
                                                 const float* __restrict__ rows, int n, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -827,87 +1039,11 @@ __global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, con
   const int row0 = blockIdx.x * BM;
   const bool valid = row0 + r < n;
   const long ridx = valid ? row0 + r : 0;
-  unsigned short* XIN = c.u16(S_XIN);
   unsigned short* TA = c.u16(S_TA);
-  unsigned short* TB = c.u16(S_TB);
   unsigned short* CAT = c.u16(S_CAT);
-  unsigned short* F2 = c.u16(S_F2);
   float* ACC = c.acc();
-  for (int br = 0; br < 2; ++br) {
-    const Branch B = branch(br);
-    {
-      s8v v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = q * 8 + j;
-        float x = (valid && col < B.din) ? rows[ridx * ROW + B.xoff + col] : 0.f;
-        v[j] = (short)f2bf(x);
-      }
-      *(LDS_AS s8v*)(XIN + r * LD32 + q * 8) = v;
-    }
-    __syncthreads();
-    gemm_xw<64, 32>(c, XIN, LD32, BF + B.w.WFd);
-    __syncthreads();
-    float h[16];
-    {
-      const int c0 = q * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + P[B.o.dense_b + c0 + j]);
-      store16bf(TA + r * LD64 + c0, h);
-    }
-    __syncthreads();
-    gemm_xw<64, 64>(c, TA, LD64, BF + B.w.WFv);
-    __syncthreads();
-    {
-      float x[16];
-      const int c0 = q * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = ACC[r * LDACC + c0 + j] + P[B.o.inproj_b + 128 + c0 + j];
-      store16bf(TB + r * LD64 + c0, x);
-    }
-    __syncthreads();
-    gemm_xw<64, 64>(c, TB, LD64, BF + B.w.WFo);
-    __syncthreads();
-    float x1[16];
-    {
-      const int c0 = q * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x1[j] = h[j] + ACC[r * LDACC + c0 + j] + P[B.o.out_b + c0 + j];
-      ln_fwd(x1);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x1[j] = x1[j] * P[B.o.ln1_w + c0 + j] + P[B.o.ln1_b + c0 + j];
-      store16bf(TA + r * LD64 + c0, x1);
-    }
-    __syncthreads();
-    gemm_xw<16, 64>(c, TA, LD64, BF + B.w.WF1);
-    __syncthreads();
-    {
-      s8v v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = q * 8 + j;
-        v[j] = (short)f2bf(col < FF ? gelu(ACC[r * LDACC + col] + P[B.o.ff0_b + col]) : 0.f);
-      }
-      *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
-    }
-    __syncthreads();
-    gemm_xw<64, 32>(c, F2, LD32, BF + B.w.WF2);
-    __syncthreads();
-    {
-      float x[16];
-      const int c0 = q * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = x1[j] + ACC[r * LDACC + c0 + j] + P[B.o.ff3_b + c0 + j];
-      ln_fwd(x);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B.o.ln2_w + c0 + j] + P[B.o.ln2_b + c0 + j];
-      ln_fwd(x);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = x[j] * P[B.o.bn_w + c0 + j] + P[B.o.bn_b + c0 + j];
-      store16bf(CAT + r * LD128 + br * 64 + c0, x);
-    }
-    __syncthreads();
-  }
+  eval_branch<0>(c, BF, rows, valid, ridx);
+  eval_branch<1>(c, BF, rows, valid, ridx);
   gemm_xw<64, 128>(c, CAT, LD128, BF + WFF1);
   __syncthreads();
   {
@@ -931,30 +1067,27 @@ __global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, con
 }
 
 // bf16 weight copies for eval (same layout as the training workspace's BF region)
-__global__ void k_tf_copies(const float* __restrict__ P, unsigned short* __restrict__ BF) {
-  Ctx c;
-  c.tid = blockIdx.x * blockDim.x + threadIdx.x;
-  c.P = (float*)P;
-  c.BF = BF;
-  // a grid-stride variant of init_copies
-  auto put = [&](MatW mw) {
-    for (int e = c.tid; e < mw.n_real * mw.k_real; e += gridDim.x * blockDim.x) {
-      const int nn = e / mw.k_real, kk = e % mw.k_real;
-      unsigned short h = f2bf(P[mw.off + e]);
-      BF[mw.wf + nn * mw.wf_ld + kk] = h;
-      if (mw.wt >= 0) BF[mw.wt + kk * mw.wt_ld + nn] = h;
-    }
-  };
-  for (int br = 0; br < 2; ++br) {
-    Branch B = branch(br);
-    put(B.dense());
-    put(B.vproj());
-    put(B.oproj());
-    put(B.ff0());
-    put(B.ff3());
+__device__ __forceinline__ void put_copy(const float* P, unsigned short* BF, MatW mw) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < mw.n_real * mw.k_real; e += gridDim.x * blockDim.x) {
+    const int nn = e / mw.k_real, kk = e % mw.k_real;
+    unsigned short h = f2bf(P[mw.off + e]);
+    BF[mw.wf + nn * mw.wf_ld + kk] = h;
+    if (mw.wt >= 0) BF[mw.wt + kk * mw.wt_ld + nn] = h;
   }
-  put(MatW{FC1_W, 64, 128, WFF1, 128, WTF1, 64});
-  put(MatW{FC2_W, 32, 64, WFF2, 64, WTF2, 32});
+}
+__global__ void k_tf_copies(const float* __restrict__ P, unsigned short* __restrict__ BF) {
+  put_copy(P, BF, BrC<0>::dense);
+  put_copy(P, BF, BrC<0>::vproj);
+  put_copy(P, BF, BrC<0>::oproj);
+  put_copy(P, BF, BrC<0>::ff0);
+  put_copy(P, BF, BrC<0>::ff3);
+  put_copy(P, BF, BrC<1>::dense);
+  put_copy(P, BF, BrC<1>::vproj);
+  put_copy(P, BF, BrC<1>::oproj);
+  put_copy(P, BF, BrC<1>::ff0);
+  put_copy(P, BF, BrC<1>::ff3);
+  put_copy(P, BF, MFC1);
+  put_copy(P, BF, MFC2);
 }
 
 long afl_tf_ws_floats() { return WS_FLOATS; }
@@ -963,7 +1096,8 @@ int afl_tf_param_count() { return NPARAM; }
 
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
   if (a->batch > BM || a->batch < 1) return -1;
-  hipFuncSetAttribute((const void*)k_tf_train, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL);
+  if (hipFuncSetAttribute((const void*)k_tf_train, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess)
+    return -2;
   hipLaunchKernelGGL(k_tf_train, dim3(a->C), dim3(NT), S_TOTAL, s, *a);
   return 0;
 }
@@ -971,7 +1105,8 @@ int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s) {
   hipMemsetAsync(bf, 0, (size_t)BF_TOTAL * 2, s);
   hipLaunchKernelGGL(k_tf_copies, dim3(32), dim3(256), 0, s, params, bf);
-  hipFuncSetAttribute((const void*)k_tf_eval, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL);
+  if (hipFuncSetAttribute((const void*)k_tf_eval, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess)
+    return -2;
   hipLaunchKernelGGL(k_tf_eval, dim3((n + BM - 1) / BM), dim3(NT), S_TOTAL, s, params, bf, rows, n, out);
   return 0;
 }

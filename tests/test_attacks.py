@@ -1,0 +1,139 @@
+"""Attack math on flat update matrices vs an independent state_dict-level re-statement of the reference
+semantics (src/Utils.py:30-214): per-tensor spectral distances, unbiased std, aliasing of genuine[0]
+and the bisection that returns the last candidate tried."""
+import copy
+
+import pytest
+import torch
+
+from attackfl_amd import attacks
+from attackfl_amd.attacks import DistanceEngine, compute_distance, run_attack
+from attackfl_amd.models import ParamLayout, build_model
+
+
+# ------------------------------------------------------------------ reference semantics, state_dict level
+def _dist(a, b):
+    return compute_distance(a, b)
+
+
+def _stats(sds):
+    out = {}
+    for k in sds[0]:
+        st = torch.stack([sd[k] for sd in sds])
+        mean = st.mean(0)
+        out[k] = (mean, st.std(0), torch.sign(mean))
+    return out
+
+
+def ref_bisection(genuine, kind, gamma=50.0, tau=1.0):
+    genuine = [copy.deepcopy(g) for g in genuine]
+    stats = _stats(genuine)
+    n = len(genuine)
+    if kind == "sum":
+        thr = max(sum(_dist(genuine[i], genuine[j]) ** 2 for j in range(n) if j != i) for i in range(n))
+    else:
+        thr = max(_dist(genuine[i], genuine[j]) for i in range(n) for j in range(i + 1, n))
+    step, succ, mal, tried = gamma, 0.0, None, []
+    while abs(succ - gamma) > tau:
+        mal = genuine[0]  # alias (A-7)
+        for k, (m, s, sg) in stats.items():
+            mal[k] = m - gamma * (sg if kind == "fang" else s)
+        ds = [_dist(mal, g) for g in genuine]
+        ok = (sum(d ** 2 for d in ds) < thr) if kind == "sum" else (max(ds) < thr)
+        tried.append(gamma)
+        if ok:
+            succ = gamma
+            gamma = gamma + step / 2
+        else:
+            gamma = gamma - step / 2
+        step /= 2
+    return mal, tried[-1]
+
+
+def _genuine(name, K, scale, seed=0):
+    torch.manual_seed(seed)
+    base = build_model(name, seed=seed).state_dict()
+    return [{k: v + scale * torch.randn_like(v) for k, v in base.items()} for _ in range(K)]
+
+
+@pytest.mark.parametrize("kind,fn", [("max", attacks.min_max), ("sum", attacks.min_sum), ("fang", attacks.opt_fang)])
+@pytest.mark.parametrize("scale", [0.05, 0.5])
+def test_bisection_attacks_match_reference(kind, fn, scale):
+    gen = _genuine("TransformerModel", 4, scale, seed=1)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    own = G[0].clone()
+    res = fn(G, own, DistanceEngine(lay, "spectral"))
+    ref_sd, ref_gamma = ref_bisection(gen, kind)
+    assert res.info["gamma"] == pytest.approx(ref_gamma)
+    assert torch.allclose(res.params, lay.flatten(ref_sd), atol=1e-5)
+
+
+def test_bisection_flat_mode_runs_and_is_consistent():
+    gen = _genuine("RNNModel", 3, 0.1, seed=2)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    eng = DistanceEngine(lay, "flat")
+    res = attacks.min_max(G, G[0], eng)
+    # flat mode: accept test on whole-vector L2
+    D = torch.cdist(G.double(), G.double())
+    thr = D.max().item()
+    cand = res.params.double()
+    assert res.info["threshold"] == pytest.approx(thr, rel=1e-9)
+    assert torch.isfinite(cand).all()
+
+
+def test_cnn_spectral_on_3d_does_not_crash():
+    gen = _genuine("CNNModel", 3, 0.05, seed=3)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    res = attacks.min_sum(G, G[0], DistanceEngine(lay, "spectral"))
+    ref_sd, ref_gamma = ref_bisection(gen, "sum")  # compute_distance matricises 3-D (documented deviation)
+    assert res.info["gamma"] == pytest.approx(ref_gamma)
+
+
+def test_lie_matches_reference():
+    gen = _genuine("TransformerModel", 5, 0.1)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    res = run_attack("LIE", [0.74], G[0], G, DistanceEngine(lay))
+    st = _stats(gen)
+    ref = {k: m + 0.74 * s for k, (m, s, _) in st.items()}
+    assert torch.allclose(res.params, lay.flatten(ref), atol=1e-6)
+
+
+def test_lie_single_model_is_nan_like_reference():
+    gen = _genuine("TransformerModel", 1, 0.1)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    res = run_attack("LIE", [0.74], G[0], G, DistanceEngine(lay))
+    assert torch.isnan(res.params).all()
+
+
+def test_bisection_single_genuine_returns_own():
+    gen = _genuine("TransformerModel", 1, 0.1)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    own = torch.randn(lay.P)
+    assert torch.equal(attacks.min_max(G, own, DistanceEngine(lay)).params, own)
+
+
+def test_random_attack_scale():
+    own = torch.zeros(100000)
+    g = torch.Generator().manual_seed(0)
+    res = run_attack("Random", [0.5], own, None, None, g)
+    assert abs(res.params.std().item() - 0.5) < 0.01
+
+
+def test_unknown_attack():
+    with pytest.raises(ValueError):
+        run_attack("Nope", [], torch.zeros(3), torch.zeros(2, 3), None)
+
+
+def test_compute_distance_spectral_vs_frobenius():
+    torch.manual_seed(0)
+    a = {"w": torch.randn(64, 128), "b": torch.randn(64)}
+    b = {"w": torch.zeros(64, 128), "b": torch.zeros(64)}
+    d = compute_distance(a, b)
+    assert d == pytest.approx(torch.linalg.matrix_norm(a["w"], 2).item() + a["b"].norm().item(), rel=1e-5)
+    assert d < a["w"].norm().item()

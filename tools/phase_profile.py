@@ -1,0 +1,61 @@
+"""Per-phase wall-clock breakdown of the fused TransformerModel training kernel (workgroup 0).
+
+Runs one client's local round (default 13500 rows, 5 epochs) with the stamps buffer enabled and prints
+microseconds per phase per step.  Usage: python tools/phase_profile.py [--rows N] [--clients C]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from attackfl_amd.data import synthetic_icu
+from attackfl_amd.fl.trainers import make_plan
+from attackfl_amd.models import ParamLayout, build_model
+from attackfl_amd.ops import transformer as T
+
+NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G4 ffn0+E4", 4: "F:G5 ffn3+E5 LN2/3",
+         5: "F:branch tail", 6: "H:fc1+E6", 7: "H:fc2+E7 loss", 8: "H:bwd fc2 dX+E8", 9: "H:dcat+dWf2+dWf1",
+         10: "B:E10 LN bwd", 11: "B:A10+G11", 12: "B:E11", 13: "B:G12+dW2", 14: "B:E12 LN1 bwd", 15: "B:G13+dW1",
+         16: "B:E13", 17: "B:G13b+E13b", 18: "B:G14+dWo", 19: "B:E14+dWv+z0", 20: "B:E15+dWd"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=13500)
+    ap.add_argument("--clients", type=int, default=1)
+    ap.add_argument("--epochs", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ds = synthetic_icu(60000, seed=3)
+    rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1).to(dev)
+    lay = ParamLayout.for_model("TransformerModel")
+    params = torch.stack([lay.flatten(build_model("TransformerModel", seed=i).state_dict())
+                          for i in range(args.clients)]).to(dev)
+    plan = make_plan(rows.shape[0], [args.rows] * args.clients, args.epochs, torch.Generator().manual_seed(0), "cpu")
+    order = plan.order.to(dev)
+    T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)))
+    torch.cuda.synchronize()
+    stamps = torch.zeros(64, dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
+                    stamps=stamps)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    steps = args.epochs * ((args.rows + 127) // 128)
+    st = stamps.cpu().tolist()
+    tot = sum(st)
+    out = {"wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
+           "us_per_step_stamped": tot * 0.01 / steps, "phases_us_per_step": {}}
+    for i, v in enumerate(st):
+        if v:
+            out["phases_us_per_step"][f"{i:02d} {NAMES.get(i, '?')}"] = round(v * 0.01 / steps, 3)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
