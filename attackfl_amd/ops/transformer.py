@@ -58,9 +58,10 @@ def hash32(a: int, b: int) -> int:
 
 
 def keep_mask(key: int, layer: int, n_rows: int, n_cols: int, p: float) -> torch.Tensor:
-    """Vectorised mirror of ``tf::keep`` -> bool [n_rows, n_cols]."""
+    """Vectorised mirror of ``tf::keep`` -> bool [n_rows, n_cols] (one hash per column pair)."""
     r = np.arange(n_rows, dtype=np.uint64)[:, None]
-    c = np.arange(n_cols, dtype=np.uint64)[None, :]
+    col = np.arange(n_cols, dtype=np.uint64)[None, :]
+    c = col >> np.uint64(1)
     x = (np.uint64(key) ^ ((np.uint64(layer) * np.uint64(0x9E3779B9)) & np.uint64(M32))
          ^ ((r * np.uint64(0x85EBCA6B)) & np.uint64(M32)) ^ ((c * np.uint64(0xC2B2AE35)) & np.uint64(M32)))
     x &= np.uint64(M32)
@@ -69,8 +70,9 @@ def keep_mask(key: int, layer: int, n_rows: int, n_cols: int, p: float) -> torch
     x ^= x >> np.uint64(15)
     x = (x * np.uint64(0x846CA68B)) & np.uint64(M32)
     x ^= x >> np.uint64(16)
-    thr = {0.1: 1677722, 0.3: 5033165}[p]
-    return torch.from_numpy(((x >> np.uint64(8)) >= np.uint64(thr)))
+    u16 = (x >> ((col & np.uint64(1)) << np.uint64(4))) & np.uint64(0xFFFF)
+    thr = {0.1: 6554, 0.3: 19661}[p]
+    return torch.from_numpy(u16 >= np.uint64(thr))
 
 
 # ------------------------------------------------------------------------------- fp32 oracle

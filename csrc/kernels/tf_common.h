@@ -7,7 +7,6 @@
 namespace tf {
 
 constexpr int D_V = 7, D_L = 16, HID = 64, FF = 6, ROW = 24;  // ROW = vitals|labs|label
-constexpr int BR_SIZE_BASE = 17926;                           // branch params excluding dense.weight
 
 // per-branch offsets relative to the branch start (Din = input dim)
 struct BrOff {
@@ -50,25 +49,53 @@ constexpr int NPARAM = OUT_B + 1;
 static_assert(NPARAM == 47693, "TransformerModel parameter count");
 
 // ---------------------------------------------------------------------------------------------
-// math helpers (fp32; exact-erf GELU like F.gelu default; LN eps 1e-5, biased variance)
+// math helpers (fp32, branch-free).  GELU is the exact-erf form of F.gelu; erf comes from the
+// Chebyshev erfc fit of Numerical Recipes (|relative error| < 1.2e-7), whose exp(-x^2/2) is shared
+// with the Gaussian pdf of the GELU derivative.  LN eps 1e-5, biased variance.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+struct GeluPair {
+  float cdf;  // Phi(x) = 0.5 (1 + erf(x / sqrt 2))
+  float pdf;  // phi(x) = exp(-x^2 / 2) / sqrt(2 pi)
+};
+__device__ __forceinline__ GeluPair gelu_parts(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.5f * z);
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = __expf(-z * z);                 // exp(-x^2/2)
+  const float erfc_z = t * e * __expf(p);         // erfc(|x|/sqrt2)
+  const float half_erfc = 0.5f * erfc_z;
+  GeluPair g;
+  g.cdf = x >= 0.f ? 1.f - half_erfc : half_erfc;
+  g.pdf = 0.39894228040143268f * e;
+  return g;
 }
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu(float x) { return x * gelu_parts(x).cdf; }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const GeluPair g = gelu_parts(x);
+  return fmaf(x, g.pdf, g.cdf);
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+// bf16 round-to-nearest-even (hardware v_cvt_pk_bf16_f32, NaN preserving)
+typedef float tf_f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 tf_b2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((tf_f2v){lo, hi}, tf_b2v));
 }
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// dropout keep-test from a stateless hash of (step key, layer, row, col)
+// dropout keep-test from a stateless hash of (step key, layer, row, column pair): one 32-bit hash
+// gives the 16-bit uniforms of two adjacent columns (keep iff u16 >= p * 65536)
 __device__ __forceinline__ uint32_t hash3(uint32_t key, uint32_t layer, uint32_t r, uint32_t c) {
   uint32_t x = key ^ (layer * 0x9E3779B9u) ^ (r * 0x85EBCA6Bu) ^ (c * 0xC2B2AE35u);
   x ^= x >> 16;
@@ -78,13 +105,12 @@ __device__ __forceinline__ uint32_t hash3(uint32_t key, uint32_t layer, uint32_t
   x ^= x >> 16;
   return x;
 }
-// keep with probability 1-p: threshold on 24 bits
-__device__ __forceinline__ bool keep(uint32_t key, uint32_t layer, uint32_t r, uint32_t c, uint32_t thr24) {
-  return (hash3(key, layer, r, c) >> 8) >= thr24;
+__device__ __forceinline__ bool keep(uint32_t key, uint32_t layer, uint32_t r, uint32_t c, uint32_t thr16) {
+  return ((hash3(key, layer, r, c >> 1) >> ((c & 1u) << 4)) & 0xFFFFu) >= thr16;
 }
 
-constexpr uint32_t THR_P01 = 1677722u;   // round(0.1 * 2^24)
-constexpr uint32_t THR_P03 = 5033165u;   // round(0.3 * 2^24)
+constexpr uint32_t THR_P01 = 6554u;    // round(0.1 * 2^16)
+constexpr uint32_t THR_P03 = 19661u;   // round(0.3 * 2^16)
 constexpr float INV_K01 = 1.f / 0.9f;
 constexpr float INV_K03 = 1.f / 0.7f;
 

@@ -9,12 +9,20 @@
 //              the dW GEMM epilogue applies Adam directly (torch.optim.Adam math, fresh per round)
 //
 // GEMMs run on v_mfma_f32_16x16x32_bf16 (bf16 operands, fp32 accumulate):
-//   X.W^T and dY.W  : activation fragments from LDS (ds_read_b128), weight fragments from
-//                     bf16 copies in global memory (row and transposed layouts, rewritten by Adam)
+//   X.W^T and dY.W  : activation fragments from LDS (ds_read_b128), weight fragments from bf16
+//                     copies in global memory (row and transposed layouts, rewritten by Adam),
+//                     prefetched into registers one phase ahead
 //   dW = dY^T.X     : both operands from LDS through the gfx950 transposed read ds_read_b64_tr_b16
 // Elementwise work (bias, exact-erf GELU, dropout, residual, LayerNorm fwd/bwd, BCE) runs in fp32
 // in a row-per-4-lanes layout between GEMM phases.  Master weights, Adam moments and activations
-// saved for the backward pass are fp32 in a per-client global workspace (L2 resident).
+// saved for the backward pass live in a per-client global workspace (L2 resident); residuals that
+// the same lane needs later (h0, x1, y1, dr2, dh0) stay in registers.
+//
+// The kernel is latency bound (one CU per client, ~50 dependent phases per step), so:
+//   * phases are separated by raw LDS barriers (s_waitcnt lgkmcnt(0); s_barrier): global loads stay
+//     in flight across them and global stores are not drained — every global value is re-read only by
+//     the lane that wrote it within a step; one full __syncthreads() per step publishes Adam's writes;
+//   * each phase issues all of its global loads before its first LDS access.
 //
 // Attention at seq_len 1: softmax over one key is exactly 1, so the output is
 // out_proj(dropout(v_proj(x))) with the dropout mask per (row, head) (SDPA math path), and the
@@ -33,8 +41,12 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
-
-
+// Global-memory pointers carry address_space(1) explicitly: they pass through opaque asm at every phase
+// barrier, and a generic pointer would demote every access to FLAT (which waits on vmcnt AND lgkmcnt).
+#define GAS __attribute__((address_space(1)))
+typedef GAS float gf;
+typedef GAS unsigned short gu16;
+typedef GAS int gi32;
 
 namespace {
 
@@ -80,30 +92,24 @@ constexpr BrW WBV = brw(0);
 constexpr BrW WBL = brw(BRW_SIZE);
 constexpr int WFF1 = 2 * BRW_SIZE, WTF1 = WFF1 + 64 * 128, WFF2 = WTF1 + 128 * 64, WTF2 = WFF2 + 32 * 64;
 constexpr int BF_TOTAL = WTF2 + 64 * 32;  // ushorts
-// saved activations (float offsets from W_ACT)
+// saved activations (float offsets); every entry is written and re-read by the same lane
 constexpr long W_ACT = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
-struct BrS { long H0F, H0B, XH1, R1, X1F, F0, XH2, R2, XH3, R3, DX1F, DH0F; };
+struct BrS { long H0B, XH1, XH2, XH3, RS, F0; };
 __host__ __device__ constexpr BrS brs(long base) {
   BrS s{};
   long p = base;
-  s.H0F = p; p += BM * 64;
-  s.H0B = p; p += BM * 64 / 2;
+  s.H0B = p; p += BM * 64 / 2;  // bf16 h0
   s.XH1 = p; p += BM * 64;
-  s.R1 = p; p += BM;
-  s.X1F = p; p += BM * 64;
-  s.F0 = p; p += BM * 8;
   s.XH2 = p; p += BM * 64;
-  s.R2 = p; p += BM;
   s.XH3 = p; p += BM * 64;
-  s.R3 = p; p += BM;
-  s.DX1F = p; p += BM * 64;
-  s.DH0F = p; p += BM * 64;
+  s.RS = p; p += BM * 4 * 4;     // per lane: rstd1, rstd2, rstd3, pad
+  s.F0 = p; p += BM * 8;
   return s;
 }
-constexpr long BRS_SIZE = 8L * BM * 64 + BM * 32 + BM * 8 + 3 * BM;
+constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8;
 constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
-constexpr long W_Y1 = W_ACT + 2 * BRS_SIZE, W_Y2 = W_Y1 + BM * 64, W_DX3V = W_Y2 + BM * 32;
+constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
 constexpr long WS_FLOATS = W_DX3V + BM * 64;
 
 struct AdamK {
@@ -112,35 +118,45 @@ struct AdamK {
 };
 constexpr float B1 = 0.9f, B2 = 0.999f, EPS = 1e-8f;
 
-__device__ __forceinline__ float adam(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int idx,
-                                      float g, AdamK k) {
-  if (k.sgd_lr > 0.f) {
-    float pn = p[idx] - k.sgd_lr * g;
-    p[idx] = pn;
-    return pn;
+// Adam update given already-loaded state; returns the new parameter
+__device__ __forceinline__ float adam_upd(float p, float& m, float& v, float g, AdamK k) {
+  if (k.sgd_lr > 0.f) return p - k.sgd_lr * g;
+  m = m + (1.f - B1) * (g - m);
+  v = B2 * v + (1.f - B2) * g * g;
+  return p - k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_sqrtf(v) * k.rsqrt_bc2 + EPS);
+}
+__device__ __forceinline__ float adam(gf* __restrict__ p, gf* __restrict__ m, gf* __restrict__ v, int idx, float g,
+                                      AdamK k) {
+  float pp = p[idx], mm = m[idx], vv = v[idx];
+  pp = adam_upd(pp, mm, vv, g, k);
+  p[idx] = pp;
+  if (k.sgd_lr <= 0.f) {
+    m[idx] = mm;
+    v[idx] = vv;
   }
-  float mi = m[idx] + (1.f - B1) * (g - m[idx]);
-  float vi = B2 * v[idx] + (1.f - B2) * g * g;
-  m[idx] = mi;
-  v[idx] = vi;
-  float pn = p[idx] - k.lr_bc1 * mi / (sqrtf(vi) * k.rsqrt_bc2 + EPS);
-  p[idx] = pn;
-  return pn;
+  return pp;
 }
 
 struct Ctx {
   unsigned char* smem;
-  float* P;          // master params of this client
-  float* M;
-  float* V;
-  unsigned short* BF;  // bf16 weight copies
-  float* ws;
+  gf* P;     // master params of this client
+  gf* M;
+  gf* V;
+  gu16* BF;  // bf16 weight copies
+  gf* ws;
   int tid, lane, wave;
   int r, q;  // row-per-4-lanes layout: row, quarter
 
-  // barrier + make every base value opaque, so the compiler recomputes addresses per phase instead of
-  // keeping hundreds of CSE'd pointers live across the whole step (which spills to scratch)
-  __device__ __forceinline__ void sync() {
+  // Phase barrier: LDS-only (global loads stay in flight, global stores are not drained), then make
+  // every base value opaque so the compiler recomputes addresses per phase instead of keeping hundreds
+  // of CSE'd pointers live across the whole step (which spills to scratch).
+  __device__ __forceinline__ void bar() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
+    asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
+  }
+  // Full barrier (drains global stores: publishes Adam's writes to every wave)
+  __device__ __forceinline__ void full_sync() {
     __syncthreads();
     asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
     asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
@@ -149,7 +165,7 @@ struct Ctx {
   __device__ float* acc() const { return (float*)(smem + S_ACC); }
   __device__ unsigned short* u16(int off) const { return (unsigned short*)(smem + off); }
   __device__ float* cs(int v) const { return (float*)(smem + S_CS) + v * 8 * 64; }
-  __device__ float* wsf(long off) const { return ws + off; }
+  __device__ gf* wsf(long off) const { return ws + off; }
 };
 
 // ---------------------------------------------------------------- fragments
@@ -169,16 +185,16 @@ __device__ __forceinline__ s8v lds_col_frag(const unsigned short* S, int ld, int
   r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
   return r;
 }
-__device__ __forceinline__ s8v glb_frag(const unsigned short* W, int ldk, int n0, int k0, int lane) {
-  return *(const s8v*)(W + (n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+__device__ __forceinline__ s8v glb_frag(const gu16* W, int ldk, int n0, int k0, int lane) {
+  return *(const GAS s8v*)(W + (n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
 }
 __device__ __forceinline__ f4v mfma(s8v a, s8v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
 }
 
-// ACC[128][N] = A[128][K] (LDS bf16, ld lda) x W^T, W = global bf16 [N][K] row-major
+// ACC[128][N] = A[128][K] (LDS bf16, ld lda) x W^T, W = global bf16 [N][K] row-major (eval path)
 template <int N, int K>
-__device__ __forceinline__ void gemm_xw(const Ctx& c, const unsigned short* A, int lda, const unsigned short* W) {
+__device__ __forceinline__ void gemm_xw(const Ctx& c, const unsigned short* A, int lda, const gu16* W) {
   constexpr int NTL = N / 16;
   f4v acc[NTL];
 #pragma unroll
@@ -197,30 +213,81 @@ __device__ __forceinline__ void gemm_xw(const Ctx& c, const unsigned short* A, i
     for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
 }
 
+// ---- weight fragments prefetched into registers a phase ahead of their GEMM ----
+template <int N, int K>
+struct WFr {
+  s8v f[N / 16][K / 32];
+};
+template <int N, int K>
+__device__ __forceinline__ void wload(WFr<N, K>& w, const gu16* W, int lane) {
+#pragma unroll
+  for (int t = 0; t < N / 16; ++t)
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) w.f[t][kk] = glb_frag(W, K, 16 * t, 32 * kk, lane);
+}
+template <int N, int K>
+__device__ __forceinline__ void gemm_pf(const Ctx& c, const unsigned short* A, int lda, const WFr<N, K>& w) {
+  constexpr int NTL = N / 16;
+  f4v acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int r0 = 16 * c.wave;
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk) {
+    s8v a = lds_row_frag(A, lda, r0, 32 * kk, c.lane);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, w.f[t][kk], acc[t]);
+  }
+  float* out = c.acc();
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
+}
+
 // Matrix weight descriptor for the dW+Adam epilogue
 struct MatW {
-  int off;      // param offset of W[n][k]
+  int off;        // param offset of W[n][k]
   int n_real, k_real;
   int wf, wf_ld;  // bf16 WF [n][k] copy (ushort offset in BF region, row stride)
   int wt, wt_ld;  // bf16 WT [k][n] copy (-1 = none)
 };
 
-// dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows, then Adam on the real entries
+// dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows, then Adam on the real entries.  The Adam state
+// (p, m, v) of each lane's 4 accumulator elements is loaded before the MFMAs so the global latency
+// overlaps the tile's transposed LDS reads and matrix work.
 template <int MT, int NTL>
 __device__ __forceinline__ void gemm_dw_adam(const Ctx& c, const unsigned short* DY, int ldy, const unsigned short* X,
                                              int ldx, MatW mw, AdamK k) {
   for (int t = c.wave; t < MT * NTL; t += 8) {
     const int mt = t / NTL, nt = t % NTL;
+    const int kk = 16 * nt + (c.lane & 15);
+    float pp[4], mm[4], vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 16 * mt + 4 * (c.lane >> 4) + i;
+      const bool ok = n < mw.n_real && kk < mw.k_real;
+      const int idx = ok ? mw.off + n * mw.k_real + kk : mw.off;
+      pp[i] = c.P[idx];
+      mm[i] = c.M[idx];
+      vv[i] = c.V[idx];
+    }
     f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int b0 = 0; b0 < BM; b0 += 32)
       acc = mfma(lds_col_frag(DY, ldy, b0, 16 * mt, c.lane), lds_col_frag(X, ldx, b0, 16 * nt, c.lane), acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int n = 16 * mt + 4 * (c.lane >> 4) + i, kk = 16 * nt + (c.lane & 15);
+      const int n = 16 * mt + 4 * (c.lane >> 4) + i;
       if (n < mw.n_real && kk < mw.k_real) {
-        float pn = adam(c.P, c.M, c.V, mw.off + n * mw.k_real + kk, acc[i], k);
-        unsigned short h = f2bf(pn);
+        const int idx = mw.off + n * mw.k_real + kk;
+        const float pn = adam_upd(pp[i], mm[i], vv[i], acc[i], k);
+        c.P[idx] = pn;
+        if (k.sgd_lr <= 0.f) {
+          c.M[idx] = mm[i];
+          c.V[idx] = vv[i];
+        }
+        const unsigned short h = f2bf(pn);
         c.BF[mw.wf + n * mw.wf_ld + kk] = h;
         if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
       }
@@ -228,35 +295,66 @@ __device__ __forceinline__ void gemm_dw_adam(const Ctx& c, const unsigned short*
   }
 }
 
-// column partial sums of 16 values per thread (row-per-4-lanes layout, 64-wide rows):
-// lanes sharing (lane & 3) are reduced -> CS[v][wave][q*16 + j]
+// ---- cross-lane reductions without LDS ----
+// Element layout: lane l of wave w owns row r = 16w + (l & 15) and quarter q = l >> 4 of that row.
+// A column sum over the wave's 16 rows is a reduction over 16 consecutive lanes: 4 DPP adds
+// (quad_perm xor1, xor2, row_half_mirror, row_mirror).  A row sum over the 4 quarters pairs lanes
+// l, l^16, l^32: gfx950 v_permlane16_swap / v_permlane32_swap.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float a) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum16lanes(float a) {
+  a += dpp<0xB1>(a);   // quad_perm [1,0,3,2]
+  a += dpp<0x4E>(a);   // quad_perm [2,3,0,1]
+  a += dpp<0x141>(a);  // row_half_mirror
+  a += dpp<0x140>(a);  // row_mirror
+  return a;
+}
+__device__ __forceinline__ float xor16(float a) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]) - a;  // = a[l ^ 16]
+}
+__device__ __forceinline__ float xor32(float a) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]) - a;  // = a[l ^ 32]
+}
+
+// level-major over W independent values: the DPP read-after-VALU-write hazard is covered by the other
+// values' instructions instead of s_nop padding
+template <int W>
+__device__ __forceinline__ void sum16lanes_multi(float (&s)[W]) {
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0xB1>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x4E>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x141>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x140>(s[j]);
+}
+
+// column partial sums of 16 values per lane (64-wide rows): CS[v][wave][q*16 + j]
 __device__ __forceinline__ void colsum16(const Ctx& c, int v, const float (&x)[16]) {
   float s[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    float a = x[j];
-    a += __shfl_xor(a, 4, 64);
-    a += __shfl_xor(a, 8, 64);
-    a += __shfl_xor(a, 16, 64);
-    a += __shfl_xor(a, 32, 64);
-    s[j] = a;
-  }
-  if (c.lane < 4) {
-    float* d = c.cs(v) + c.wave * 64 + c.lane * 16;
+  for (int j = 0; j < 16; ++j) s[j] = x[j];
+  sum16lanes_multi(s);
+  if ((c.lane & 15) == 0) {
+    float* d = c.cs(v) + c.wave * 64 + (c.lane >> 4) * 16;
 #pragma unroll
     for (int j = 0; j < 16; ++j) d[j] = s[j];
   }
 }
 template <int W>
 __device__ __forceinline__ void colsumW(const Ctx& c, int v, const float (&x)[W], int colbase) {
+  float s[W];
 #pragma unroll
-  for (int j = 0; j < W; ++j) {
-    float a = x[j];
-    a += __shfl_xor(a, 4, 64);
-    a += __shfl_xor(a, 8, 64);
-    a += __shfl_xor(a, 16, 64);
-    a += __shfl_xor(a, 32, 64);
-    if (c.lane < 4) c.cs(v)[c.wave * 64 + colbase + j] = a;
+  for (int j = 0; j < W; ++j) s[j] = x[j];
+  sum16lanes_multi(s);
+  if ((c.lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) c.cs(v)[c.wave * 64 + colbase + j] = s[j];
   }
 }
 __device__ __forceinline__ float cs_total(const Ctx& c, int v, int col) {
@@ -266,10 +364,10 @@ __device__ __forceinline__ float cs_total(const Ctx& c, int v, int col) {
   return s;
 }
 
-// row-wise sum over the 4 lanes of a row
+// row-wise sum over the 4 lanes (quarters) of a row: lanes l, l^16, l^32, l^48
 __device__ __forceinline__ float rsum4(float a) {
-  a += __shfl_xor(a, 1, 64);
-  a += __shfl_xor(a, 2, 64);
+  a += xor16(a);
+  a += xor32(a);
   return a;
 }
 
@@ -286,18 +384,18 @@ __device__ __forceinline__ float ln_fwd(float (&x)[16]) {
     ss += x[j] * x[j];
   }
   const float var = rsum4(ss) * (1.f / 64.f);
-  const float rstd = 1.f / sqrtf(var + 1e-5f);
+  const float rstd = __builtin_amdgcn_rsqf(var + 1e-5f);
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] *= rstd;
   return rstd;
 }
-// LayerNorm backward: dy -> dx given xhat, rstd, gamma (per column)
+// LayerNorm backward: dy -> dx given xhat, rstd, gamma (per column, 16 values of this lane)
 __device__ __forceinline__ void ln_bwd(float (&dx)[16], const float (&dy)[16], const float (&xh)[16], float rstd,
-                                       const float* gamma, int c0) {
+                                       const float (&gamma)[16]) {
   float a = 0.f, b = 0.f, g[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    g[j] = dy[j] * gamma[c0 + j];
+    g[j] = dy[j] * gamma[j];
     a += g[j];
     b += g[j] * xh[j];
   }
@@ -307,26 +405,34 @@ __device__ __forceinline__ void ln_bwd(float (&dx)[16], const float (&dy)[16], c
   for (int j = 0; j < 16; ++j) dx[j] = rstd * (g[j] - a - xh[j] * b);
 }
 
-__device__ __forceinline__ void load16(float (&x)[16], const float* p) {
+__device__ __forceinline__ void load16(float (&x)[16], const gf* p) {
 #pragma unroll
   for (int j = 0; j < 16; j += 4) {
-    float4 v = *(const float4*)(p + j);
-    x[j] = v.x; x[j + 1] = v.y; x[j + 2] = v.z; x[j + 3] = v.w;
+    f4v v = *(const GAS f4v*)(p + j);
+    x[j] = v[0]; x[j + 1] = v[1]; x[j + 2] = v[2]; x[j + 3] = v[3];
   }
 }
-__device__ __forceinline__ void store16(float* p, const float (&x)[16]) {
+__device__ __forceinline__ void load8(float (&x)[8], const gf* p) {
+  f4v a = *(const GAS f4v*)p, b = *(const GAS f4v*)(p + 4);
+  x[0] = a[0]; x[1] = a[1]; x[2] = a[2]; x[3] = a[3];
+  x[4] = b[0]; x[5] = b[1]; x[6] = b[2]; x[7] = b[3];
+}
+__device__ __forceinline__ void store16(gf* p, const float (&x)[16]) {
 #pragma unroll
-  for (int j = 0; j < 16; j += 4) *(float4*)(p + j) = make_float4(x[j], x[j + 1], x[j + 2], x[j + 3]);
+  for (int j = 0; j < 16; j += 4) *(GAS f4v*)(p + j) = f4v{x[j], x[j + 1], x[j + 2], x[j + 3]};
+}
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s8v pack8bf(const float* x) {
+  u4v u;
+  u[0] = pack_bf2(x[0], x[1]);
+  u[1] = pack_bf2(x[2], x[3]);
+  u[2] = pack_bf2(x[4], x[5]);
+  u[3] = pack_bf2(x[6], x[7]);
+  return __builtin_bit_cast(s8v, u);
 }
 __device__ __forceinline__ void store16bf(unsigned short* p, const float (&x)[16]) {
-  s8v a, b;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    a[j] = (short)f2bf(x[j]);
-    b[j] = (short)f2bf(x[j + 8]);
-  }
-  *(LDS_AS s8v*)p = a;
-  *(LDS_AS s8v*)(p + 8) = b;
+  *(LDS_AS s8v*)p = pack8bf(x);
+  *(LDS_AS s8v*)(p + 8) = pack8bf(x + 8);
 }
 
 // write the bf16 copies of one matrix from the master params
@@ -355,51 +461,17 @@ struct BrC {
 constexpr MatW MFC1{FC1_W, 64, 128, WFF1, 128, WTF1, 64};
 constexpr MatW MFC2{FC2_W, 32, 64, WFF2, 64, WTF2, 32};
 
-// ---- weight fragments prefetched into registers before the barrier that precedes their GEMM ----
-template <int N, int K>
-struct WFr {
-  s8v f[N / 16][K / 32];
-};
-template <int N, int K>
-__device__ __forceinline__ void wload(WFr<N, K>& w, const unsigned short* W, int lane) {
-#pragma unroll
-  for (int t = 0; t < N / 16; ++t)
-#pragma unroll
-    for (int kk = 0; kk < K / 32; ++kk) w.f[t][kk] = glb_frag(W, K, 16 * t, 32 * kk, lane);
-}
-template <int N, int K>
-__device__ __forceinline__ void gemm_pf(const Ctx& c, const unsigned short* A, int lda, const WFr<N, K>& w) {
-  constexpr int NTL = N / 16;
-  f4v acc[NTL];
-#pragma unroll
-  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int r0 = 16 * c.wave;
-#pragma unroll
-  for (int kk = 0; kk < K / 32; ++kk) {
-    s8v a = lds_row_frag(A, lda, r0, 32 * kk, c.lane);
-#pragma unroll
-    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, w.f[t][kk], acc[t]);
-  }
-  float* out = c.acc();
-#pragma unroll
-  for (int t = 0; t < NTL; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
-}
-
 // per-step, per-thread state (row-per-4-lanes layout)
 struct St {
-  int r, q;       // row, quarter
   bool valid;     // r < Bn
   int ridx;       // train row index
   int Bn;
   uint32_t key;   // dropout key of this step
   AdamK K;
-  const float* rows;
+  const gf* rows;
+  float xin[2][8];  // this lane's 8 input columns of both branches (loaded at step start)
 };
 
-// opaque per-phase row offset: keeps the compiler from hoisting dozens of per-thread addresses out of
-// the step loop (they would stay live across the whole loop and spill)
 __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
@@ -416,23 +488,27 @@ __device__ __forceinline__ int opaque(int v) {
     }                                                                               \
   } while (0)
 
+#define BAR()          \
+  do {                 \
+    c.bar();           \
+    r = c.r;           \
+    q = c.q;           \
+    c0 = q * 16;       \
+  } while (0)
+
+// inputs of one branch -> XIN (bf16, K padded to 32)
 template <int BR>
-__device__ __forceinline__ void gather_x(const Ctx& c, const St& s) {
-  using B = BrC<BR>;
+__device__ __forceinline__ void put_x(const Ctx& c, const St& s) {
   unsigned short* XIN = c.u16(S_XIN);
   s8v v;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = s.q * 8 + j;
-    float x = (s.valid && col < B::din) ? s.rows[(long)s.ridx * ROW + B::xoff + col] : 0.f;
-    v[j] = (short)f2bf(x);
-  }
-  *(LDS_AS s8v*)(XIN + s.r * LD32 + s.q * 8) = v;
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(s.xin[BR][j]);
+  *(LDS_AS s8v*)(XIN + c.r * LD32 + c.q * 8) = v;
 }
 
 // ============================================================== branch forward
 template <int BR>
-__device__ __forceinline__ void fwd_branch(Ctx& c, const St& s, uint64_t* stamps, uint64_t& t_prev) {
+__device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);
   unsigned short* TA = c.u16(S_TA);
@@ -444,69 +520,76 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, const St& s, uint64_t* stamps
   int r = c.r, q = c.q, c0 = q * 16;
   WFr<64, 32> wd;
   wload(wd, c.BF + B::w.WFd, c.lane);
-  gather_x<BR>(c, s);
-  if (BR == 0 && q == 0) ((float*)(c.smem + S_LAB))[r] = s.valid ? s.rows[(long)s.ridx * ROW + ROW - 1] : 0.f;
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  put_x<BR>(c, s);
+  BAR();
   gemm_pf<64, 32>(c, XIN, LD32, wd);
   WFr<64, 64> wv;
   wload(wv, c.BF + B::w.WFv, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float bias[16];
+  load16(bias, c.P + B::o.dense_b + c0);
+  BAR();
   STAMP(0);
   float h[16];  // h0 stays in registers until the residual (E3)
   {
-    const int ro = opaque(r * 64 + c0);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + c.P[B::o.dense_b + c0 + j]);
+    for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + bias[j]);
     store16bf(TA + r * LD64 + c0, h);
-    unsigned short* hb = (unsigned short*)c.wsf(B::s.H0B) + ro;
+    gu16* hb = (gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
     s8v a, b;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       a[j] = (short)f2bf(h[j]);
       b[j] = (short)f2bf(h[j + 8]);
     }
-    *(s8v*)hb = a;
-    *(s8v*)(hb + 8) = b;
+    *(GAS s8v*)hb = a;
+    *(GAS s8v*)(hb + 8) = b;
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  load16(bias, c.P + B::o.inproj_b + 128 + c0);
+  BAR();
   gemm_pf<64, 64>(c, TA, LD64, wv);
   WFr<64, 64> wo;
   wload(wo, c.BF + B::w.WFo, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(1);
   {  // E2: a = head_dropout(v)
     float x[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B::o.inproj_b + 128 + c0 + j]) * m;
+    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bias[j]) * m;
     store16bf(TB + r * LD64 + c0, x);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  load16(bias, c.P + B::o.out_b + c0);
+  float g1[16], b1[16];
+  load16(g1, c.P + B::o.ln1_w + c0);
+  load16(b1, c.P + B::o.ln1_b + c0);
+  BAR();
   gemm_pf<64, 64>(c, TB, LD64, wo);
   WFr<16, 64> w1;
   wload(w1, c.BF + B::w.WF1, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(2);
   float x1[16];  // x1 stays in registers until the second residual (E5)
   {
     const int ro = opaque(r * 64 + c0);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float o = ACC[r * LDACC + c0 + j] + c.P[B::o.out_b + c0 + j];
+      const float o = ACC[r * LDACC + c0 + j] + bias[j];
       x1[j] = h[j] + (keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? o * INV_K01 : 0.f);
     }
     const float rstd = ln_fwd(x1);
     store16(c.wsf(B::s.XH1) + ro, x1);
-    if (q == 0) c.wsf(B::s.R1)[r] = rstd;
+    c.wsf(B::s.RS)[opaque(r * 16 + q * 4) + 0] = rstd;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x1[j] = x1[j] * c.P[B::o.ln1_w + c0 + j] + c.P[B::o.ln1_b + c0 + j];
+    for (int j = 0; j < 16; ++j) x1[j] = x1[j] * g1[j] + b1[j];
     store16bf(TC + r * LD64 + c0, x1);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float fb[8];
+  load8(fb, c.P + B::o.ff0_b);  // 6 used (+2 beyond: next tensor, ignored)
+  BAR();
   gemm_pf<16, 64>(c, TC, LD64, w1);
   WFr<64, 32> w2;
   wload(w2, c.BF + B::w.WF2, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(3);
   {  // E4: f0 -> f2
     s8v v;
@@ -515,7 +598,7 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, const St& s, uint64_t* stamps
       const int col = q * 8 + j;
       float f2 = 0.f;
       if (col < FF) {
-        const float f0 = ACC[r * LDACC + col] + c.P[B::o.ff0_b + col];
+        const float f0 = ACC[r * LDACC + col] + fb[j & 7];
         c.wsf(B::s.F0)[opaque(r * 8) + col] = f0;
         f2 = keep(s.key, 8 * BR + L_DF, r, col, THR_P01) ? gelu(f0) * INV_K01 : 0.f;
       }
@@ -523,38 +606,45 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, const St& s, uint64_t* stamps
     }
     *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float g2[16], bb2[16], g3[16], b3[16];
+  load16(bias, c.P + B::o.ff3_b + c0);
+  load16(g2, c.P + B::o.ln2_w + c0);
+  load16(bb2, c.P + B::o.ln2_b + c0);
+  load16(g3, c.P + B::o.bn_w + c0);
+  load16(b3, c.P + B::o.bn_b + c0);
+  BAR();
   gemm_pf<64, 32>(c, F2, LD32, w2);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(4);
   {  // E5: r2 = x1 + drop(f3); LN2; LN3 -> CAT
     const int ro = opaque(r * 64 + c0);
     float x[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float f3 = ACC[r * LDACC + c0 + j] + c.P[B::o.ff3_b + c0 + j];
+      const float f3 = ACC[r * LDACC + c0 + j] + bias[j];
       x[j] = x1[j] + (keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? f3 * INV_K01 : 0.f);
     }
     float rstd = ln_fwd(x);
     store16(c.wsf(B::s.XH2) + ro, x);
-    if (q == 0) c.wsf(B::s.R2)[r] = rstd;
+    gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
+    rs[1] = rstd;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B::o.ln2_w + c0 + j] + c.P[B::o.ln2_b + c0 + j];
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * g2[j] + bb2[j];
     rstd = ln_fwd(x);
     store16(c.wsf(B::s.XH3) + ro, x);
-    if (q == 0) c.wsf(B::s.R3)[r] = rstd;
+    rs[2] = rstd;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = x[j] * c.P[B::o.bn_w + c0 + j] + c.P[B::o.bn_b + c0 + j];
+    for (int j = 0; j < 16; ++j) x[j] = x[j] * g3[j] + b3[j];
     store16bf(CAT + r * LD128 + BR * 64 + c0, x);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(5);
 }
 
 // ============================================================== branch backward
 // on entry: dx3 of this branch in ACC (BR == 1) or in the DX3V workspace (BR == 0)
 template <int BR>
-__device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps, uint64_t& t_prev) {
+__device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);  // also DF0
   unsigned short* TA = c.u16(S_TA);
@@ -570,31 +660,37 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps
   wload(wt2, c.BF + B::w.WT2, c.lane);
   {  // E10: LN3 bwd, LN2 bwd, df3 ; colsums g3 (v0), b3 (v1), g2 (v2), be2 (v3), b2 (v4)
     const int ro = opaque(r * 64 + c0);
-    float dy[16], xh[16], dx[16], t[16];
+    float dy[16], xh3[16], xh2[16], gm3[16], gm2[16], dx[16], t[16];
+    load16(xh3, c.wsf(B::s.XH3) + ro);
+    load16(xh2, c.wsf(B::s.XH2) + ro);
+    load16(gm3, c.P + B::o.bn_w + c0);
+    load16(gm2, c.P + B::o.ln2_w + c0);
+    const gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
+    const float rstd2 = rs[1], rstd3 = rs[2];
     if (BR == 1) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
     } else {
       load16(dy, c.wsf(W_DX3V) + ro);
     }
-    load16(xh, c.wsf(B::s.XH3) + ro);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
+    for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh3[j];
     colsum16(c, 0, t);
     colsum16(c, 1, dy);
-    ln_bwd(dx, dy, xh, c.wsf(B::s.R3)[r], c.P + B::o.bn_w, c0);
-    load16(xh, c.wsf(B::s.XH2) + ro);
+    ln_bwd(dx, dy, xh3, rstd3, gm3);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh2[j];
     colsum16(c, 2, t);
     colsum16(c, 3, dx);
-    ln_bwd(dr2, dx, xh, c.wsf(B::s.R2)[r], c.P + B::o.ln2_w, c0);
+    ln_bwd(dr2, dx, xh2, rstd2, gm2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? dr2[j] * INV_K01 : 0.f;
     store16bf(TA + r * LD64 + c0, t);
     colsum16(c, 4, t);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float f0v[8];
+  load8(f0v, c.wsf(B::s.F0) + opaque(r * 8));
+  BAR();
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2)
   if (c.tid < 64) {
@@ -608,7 +704,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps
   gemm_pf<16, 64>(c, TA, LD64, wt2);
   WFr<64, 32> wt1;
   wload(wt1, c.BF + B::w.WT1, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(11);
   {  // E11: df0 (-> DF0 = XIN region), recompute f2 (-> F2); colsum b1 (v5)
     s8v vd, vf;
@@ -618,7 +714,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps
       const int col = q * 8 + j;
       float d0 = 0.f, f2 = 0.f;
       if (col < FF) {
-        const float f0 = c.wsf(B::s.F0)[opaque(r * 8) + col];
+        const float f0 = f0v[j];
         const bool kp = keep(s.key, 8 * BR + L_DF, r, col, THR_P01);
         d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
         f2 = kp ? gelu(f0) * INV_K01 : 0.f;
@@ -631,38 +727,50 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps
     *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = vf;
     colsumW<8>(c, 5, db, q * 8);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float xh1[16], gm1[16], bt1[16];
+  {
+    const int ro = opaque(r * 64 + c0);
+    load16(xh1, c.wsf(B::s.XH1) + ro);
+    load16(gm1, c.P + B::o.ln1_w + c0);
+    load16(bt1, c.P + B::o.ln1_b + c0);
+  }
+  const float rstd1 = c.wsf(B::s.RS)[opaque(r * 16 + q * 4)];
+  BAR();
   STAMP(12);
-  gemm_pf<64, 32>(c, XIN, LD32, wt1);                 // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
+  gemm_pf<64, 32>(c, XIN, LD32, wt1);                    // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
   gemm_dw_adam<4, 1>(c, TA, LD64, F2, LD32, B::ff3, K);  // dW2 = df3^T f2
   if (c.tid < FF) adam(c.P, c.M, c.V, B::o.ff0_b + c.tid, cs_total(c, 5, c.tid), K);
   WFr<64, 64> wto;
   wload(wto, c.BF + B::w.WTo, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(13);
   float dh0[16];  // residual gradient into h0, kept in registers until E15
   {  // E12: dx1 += dr2 ; LN1 bwd ; do ; x1 recompute ; colsums g1 (v0), be1 (v1), bo (v2)
-    const int ro = opaque(r * 64 + c0);
-    float dx[16], xh[16], t[16];
+    float dx[16], t[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) dx[j] = ACC[r * LDACC + c0 + j] + dr2[j];
-    load16(xh, c.wsf(B::s.XH1) + ro);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh1[j];
     colsum16(c, 0, t);
     colsum16(c, 1, dx);
-    ln_bwd(dh0, dx, xh, c.wsf(B::s.R1)[r], c.P + B::o.ln1_w, c0);
+    ln_bwd(dh0, dx, xh1, rstd1, gm1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? dh0[j] * INV_K01 : 0.f;
     store16bf(TB + r * LD64 + c0, t);
     colsum16(c, 2, t);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = xh[j] * c.P[B::o.ln1_w + c0 + j] + c.P[B::o.ln1_b + c0 + j];
+    for (int j = 0; j < 16; ++j) t[j] = xh1[j] * gm1[j] + bt1[j];
     store16bf(TC + r * LD64 + c0, t);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  s8v h0a, h0b;
+  {
+    const gu16* hb = (const gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
+    h0a = *(const GAS s8v*)hb;
+    h0b = *(const GAS s8v*)(hb + 8);
+  }
+  BAR();
   STAMP(14);
-  gemm_pf<64, 64>(c, TB, LD64, wto);                     // da = do . Wo
+  gemm_pf<64, 64>(c, TB, LD64, wto);                      // da = do . Wo
   gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B::ff0, K);  // dW1 = df0^T x1
   if (c.tid < 64) {
     const int i = c.tid;
@@ -672,64 +780,65 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, const St& s, uint64_t* stamps
   }
   WFr<64, 64> wfv;
   wload(wfv, c.BF + B::w.WFv, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float bv[16];
+  load16(bv, c.P + B::o.inproj_b + 128 + c0);
+  BAR();
   STAMP(15);
-  {  // E13: dv (-> TC) ; reload h0 (-> TA) ; colsum bv (v3)
-    const int ro = opaque(r * 64 + c0);
+  {  // E13: dv (-> TC) ; h0 (-> TA) ; colsum bv (v3)
     float d[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) d[j] = ACC[r * LDACC + c0 + j] * m;
     store16bf(TC + r * LD64 + c0, d);
     colsum16(c, 3, d);
-    const unsigned short* hb = (const unsigned short*)c.wsf(B::s.H0B) + ro;
-    s8v h0a = *(const s8v*)hb, h0b = *(const s8v*)(hb + 8);
     *(LDS_AS s8v*)(TA + r * LD64 + c0) = h0a;
     *(LDS_AS s8v*)(TA + r * LD64 + c0 + 8) = h0b;
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(16);
   gemm_pf<64, 64>(c, TA, LD64, wfv);  // v recompute (before Wv's Adam)
   WFr<64, 64> wtv;
   wload(wtv, c.BF + B::w.WTv, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   {  // E13b: a = head_dropout(v) -> TD
     float x[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + c.P[B::o.inproj_b + 128 + c0 + j]) * m;
+    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bv[j]) * m;
     store16bf(TD + r * LD64 + c0, x);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(17);
   gemm_pf<64, 64>(c, TC, LD64, wtv);                       // dh0 part = dv . Wv
   gemm_dw_adam<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K);  // dWo = do^T a
   if (c.tid < 64) adam(c.P, c.M, c.V, B::o.inproj_b + 128 + c.tid, cs_total(c, 3, c.tid), K);
   WFr<64, 32> wd;
   wload(wd, c.BF + B::w.WFd, c.lane);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  float bd[16];
+  load16(bd, c.P + B::o.dense_b + c0);
+  BAR();
   STAMP(18);
-  {  // E14: dh0 += ACC ; gather x for the z0 recompute
+  {  // E14: dh0 += ACC ; x for the z0 recompute
 #pragma unroll
     for (int j = 0; j < 16; ++j) dh0[j] += ACC[r * LDACC + c0 + j];
-    gather_x<BR>(c, s);
+    put_x<BR>(c, s);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K);  // dWv = dv^T h0
   gemm_pf<64, 32>(c, XIN, LD32, wd);                       // z0 recompute
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(19);
   {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
     float d[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) d[j] = dh0[j] * gelu_grad(ACC[r * LDACC + c0 + j] + c.P[B::o.dense_b + c0 + j]);
+    for (int j = 0; j < 16; ++j) d[j] = dh0[j] * gelu_grad(ACC[r * LDACC + c0 + j] + bd[j]);
     store16bf(TB + r * LD64 + c0, d);
     colsum16(c, 4, d);
   }
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   gemm_dw_adam<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K);  // dWd = dz0^T x
   if (c.tid < 64) adam(c.P, c.M, c.V, B::o.dense_b + c.tid, cs_total(c, 4, c.tid), K);
-  { c.sync(); r = c.r; q = c.q; c0 = q * 16; }
+  BAR();
   STAMP(20);
 }
 
@@ -755,14 +864,16 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   const int cid = blockIdx.x;
   Ctx c;
   c.smem = smem;
-  c.P = a.params + (long)cid * NPARAM;
-  c.ws = a.ws + (long)cid * a.ws_stride;
+  c.P = (gf*)(a.params + (long)cid * NPARAM);
+  c.ws = (gf*)(a.ws + (long)cid * a.ws_stride);
   c.M = c.ws + W_M;
   c.V = c.ws + W_V;
-  c.BF = (unsigned short*)(c.ws + W_BF);
+  c.BF = (gu16*)(c.ws + W_BF);
   c.tid = threadIdx.x;
   c.lane = threadIdx.x & 63;
   c.wave = threadIdx.x >> 6;
+  c.r = 16 * (threadIdx.x >> 6) + (threadIdx.x & 15);  // row: 16 consecutive lanes per quarter
+  c.q = (threadIdx.x >> 4) & 3;                         // quarter of the row (16 columns)
   const int tid = c.tid;
   uint64_t* stamps = a.stamps;
   uint64_t t_prev = 0;
@@ -795,15 +906,11 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   unsigned short* F2 = c.u16(S_F2);
   float* ACC = c.acc();
   St s;
-  s.r = tid >> 2;
-  s.q = tid & 3;
-  s.rows = a.rows;
-  c.r = s.r;
-  c.q = s.q;
-  int r = c.r, q = c.q;
+  s.rows = (const gf*)a.rows;
+  int r = c.r, q = c.q, c0 = q * 16;
 
   for (int e = 0; e < a.E && !failed; ++e) {
-    const int* ord = a.order + ((long)cid * a.E + e) * a.maxnd;
+    const gi32* ord = (const gi32*)(a.order + ((long)cid * a.E + e) * a.maxnd);
     float epoch_loss = 0.f;
     for (int b0 = 0; b0 < nd; b0 += BS) {
       const int Bn = min(BS, nd - b0);
@@ -814,8 +921,20 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       s.K = AdamK{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
       s.key = afl_hash32(seed, (uint32_t)step);
       s.Bn = Bn;
+      r = c.r;
+      q = c.q;
       s.valid = r < Bn;
       s.ridx = s.valid ? ord[b0 + r] : 0;
+      {  // both branches' input columns and the label, loaded once per step
+        const gf* row = s.rows + (long)s.ridx * ROW;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = q * 8 + j;
+          s.xin[0][j] = (s.valid && col < D_V) ? row[col] : 0.f;
+          s.xin[1][j] = (s.valid && col < D_L) ? row[D_V + col] : 0.f;
+        }
+        if (q == 0) LAB[r] = s.valid ? row[ROW - 1] : 0.f;
+      }
       const AdamK K = s.K;
 
       fwd_branch<0>(c, s, stamps, t_prev);
@@ -823,38 +942,43 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       // =============================== head forward + loss ===============================
       WFr<64, 128> wf1;
       wload(wf1, c.BF + WFF1, c.lane);
+      float bias[16];
+      load16(bias, c.P + FC1_B + q * 16);
       gemm_pf<64, 128>(c, CAT, LD128, wf1);
       WFr<32, 64> wf2;
       wload(wf2, c.BF + WFF2, c.lane);
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       STAMP(6);
       float y1[16];  // kept in registers until E8
       {              // E6: y1 -> d1 = drop0.3(gelu(y1))
         float x[16];
-        const int c0 = q * 16;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          y1[j] = ACC[r * LDACC + c0 + j] + c.P[FC1_B + c0 + j];
+          y1[j] = ACC[r * LDACC + c0 + j] + bias[j];
           x[j] = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? gelu(y1[j]) * INV_K03 : 0.f;
         }
         store16bf(TA + r * LD64 + c0, x);
       }
-      { c.sync(); r = c.r; q = c.q; }
+      float b2v[8], wov[8];
+      load8(b2v, c.P + FC2_B + q * 8);
+      load8(wov, c.P + OUT_W + q * 8);
+      const float bout = c.P[OUT_B];
+      BAR();
       gemm_pf<32, 64>(c, TA, LD64, wf2);
       WFr<64, 32> wtf2;
       wload(wtf2, c.BF + WTF2, c.lane);
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       STAMP(7);
       {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
         float y2[8], g2[8], dot = 0.f;
-        const int c0 = q * 8;
+        const int cc = q * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          y2[j] = ACC[r * LDACC + c0 + j] + c.P[FC2_B + c0 + j];
+          y2[j] = ACC[r * LDACC + cc + j] + b2v[j];
           g2[j] = gelu(y2[j]);
-          dot += g2[j] * c.P[OUT_W + c0 + j];
+          dot += g2[j] * wov[j];
         }
-        const float y3 = rsum4(dot) + c.P[OUT_B];
+        const float y3 = rsum4(dot) + bout;
         const float p = sigmoidf_(y3);
         const float lab = LAB[r];
         float lrow = 0.f, dy3 = 0.f;
@@ -871,18 +995,18 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           gw[j] = dy3 * g2[j];
-          dy2[j] = dy3 * c.P[OUT_W + c0 + j] * gelu_grad(y2[j]);
+          dy2[j] = dy3 * wov[j] * gelu_grad(y2[j]);
         }
         s8v v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(dy2[j]);
-        *(LDS_AS s8v*)(F2 + r * LD32 + c0) = v;  // T32 aliases F2
-        colsumW<8>(c, 0, gw, c0);
-        colsumW<8>(c, 1, dy2, c0);
+        *(LDS_AS s8v*)(F2 + r * LD32 + cc) = v;  // T32 aliases F2
+        colsumW<8>(c, 0, gw, cc);
+        colsumW<8>(c, 1, dy2, cc);
         float lsum = wave_sum(q == 0 ? lrow : 0.f);
         if (c.lane == 0) RED[c.wave] = lsum;
       }
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       {
         float tot = 0.f;
         for (int w = 0; w < 8; ++w) tot += RED[w];
@@ -904,11 +1028,10 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
       WFr<64, 64> wtf1a;
       wload(wtf1a, c.BF + WTF1, c.lane);
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       STAMP(8);
       {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
         float d[16];
-        const int c0 = q * 16;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const float g = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
@@ -917,28 +1040,32 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
         store16bf(TB + r * LD64 + c0, d);
         colsum16(c, 2, d);
       }
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1a);                 // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
       gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
       if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       WFr<64, 64> wtf1b;
       wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       {
         float t[16];
-        const int c0 = q * 16;
 #pragma unroll
         for (int j = 0; j < 16; ++j) t[j] = ACC[r * LDACC + c0 + j];
         store16(c.wsf(W_DX3V) + opaque(r * 64 + c0), t);
       }
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1b);  // dcat[:, 64:128] (kept in ACC for the labs branch)
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, MFC1, K);  // dWf1 = dy1^T cat
-      { c.sync(); r = c.r; q = c.q; }
+      BAR();
       STAMP(9);
       bwd_branch<1>(c, s, stamps, t_prev);
       bwd_branch<0>(c, s, stamps, t_prev);
+      // publish this step's Adam writes (bf16 weight copies, params) to every wave of the workgroup
+      c.full_sync();
+      r = c.r;
+      q = c.q;
+      c0 = q * 16;
     }
     if (tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
   }
@@ -948,12 +1075,13 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
 // ================================================================================================
 // eval forward: one 512-thread workgroup per 128-row tile of the test set (dropout off)
 // ================================================================================================
+namespace {
 template <int BR>
-__device__ __forceinline__ void eval_branch(const Ctx& c, const unsigned short* BF, const float* rows, bool valid,
+__device__ __forceinline__ void eval_branch(const Ctx& c, const gu16* BF, const float* rows, bool valid,
                                             long ridx) {
   using B = BrC<BR>;
-  const float* P = c.P;
-  const int tid = c.tid, r = tid >> 2, q = tid & 3, c0 = q * 16;
+  const gf* P = c.P;
+  const int r = 16 * c.wave + (c.lane & 15), q = c.lane >> 4, c0 = q * 16;
   unsigned short* XIN = c.u16(S_XIN);
   unsigned short* TA = c.u16(S_TA);
   unsigned short* TB = c.u16(S_TB);
@@ -1025,8 +1153,9 @@ __device__ __forceinline__ void eval_branch(const Ctx& c, const unsigned short* 
   }
   __syncthreads();
 }
+}  // namespace
 
-__global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, const unsigned short* __restrict__ BF,
+__global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ Pg, const unsigned short* __restrict__ BFg,
                                                 const float* __restrict__ rows, int n, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Ctx c;
@@ -1034,8 +1163,10 @@ __global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ P, con
   c.tid = threadIdx.x;
   c.lane = threadIdx.x & 63;
   c.wave = threadIdx.x >> 6;
-  c.P = (float*)P;
-  const int tid = c.tid, r = tid >> 2, q = tid & 3;
+  c.P = (gf*)Pg;
+  const gf* P = c.P;
+  const gu16* BF = (const gu16*)BFg;
+  const int r = 16 * c.wave + (c.lane & 15), q = c.lane >> 4;
   const int row0 = blockIdx.x * BM;
   const bool valid = row0 + r < n;
   const long ridx = valid ? row0 + r : 0;
