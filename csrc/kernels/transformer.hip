@@ -245,6 +245,8 @@ __device__ __forceinline__ void gemm_pf(const Ctx& c, const unsigned short* A, i
     for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
 }
 
+__device__ __forceinline__ float cs_total(const Ctx& c, int v, int col);
+
 // Matrix weight descriptor for the dW+Adam epilogue
 struct MatW {
   int off;        // param offset of W[n][k]
@@ -292,6 +294,24 @@ __device__ __forceinline__ void gemm_dw_adam(const Ctx& c, const unsigned short*
         if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
       }
     }
+  }
+}
+
+// Adam on up to 512 small-vector elements (biases, LayerNorm affine) in parallel: thread tid handles
+// element tid of the concatenation of the listed vectors; gradient = column sum CS[v] over 8 waves.
+struct VecG {
+  int off, n, csv;  // param offset, length, column-sum slot (-1: value supplied in `g0`)
+};
+template <int NV>
+__device__ __forceinline__ void adam_vecs(const Ctx& c, const VecG (&vs)[NV], AdamK k, float g0 = 0.f) {
+  int e = c.tid;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (e >= 0 && e < vs[i].n) {
+      const float g = vs[i].csv >= 0 ? cs_total(c, vs[i].csv, e) : g0;
+      adam(c.P, c.M, c.V, vs[i].off + e, g, k);
+    }
+    e -= vs[i].n;
   }
 }
 
@@ -693,13 +713,10 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   BAR();
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2)
-  if (c.tid < 64) {
-    const int i = c.tid;
-    adam(c.P, c.M, c.V, B::o.bn_w + i, cs_total(c, 0, i), K);
-    adam(c.P, c.M, c.V, B::o.bn_b + i, cs_total(c, 1, i), K);
-    adam(c.P, c.M, c.V, B::o.ln2_w + i, cs_total(c, 2, i), K);
-    adam(c.P, c.M, c.V, B::o.ln2_b + i, cs_total(c, 3, i), K);
-    adam(c.P, c.M, c.V, B::o.ff3_b + i, cs_total(c, 4, i), K);
+  {
+    const VecG vs[5] = {{B::o.bn_w, 64, 0}, {B::o.bn_b, 64, 1}, {B::o.ln2_w, 64, 2}, {B::o.ln2_b, 64, 3},
+                        {B::o.ff3_b, 64, 4}};
+    adam_vecs(c, vs, K);
   }
   gemm_pf<16, 64>(c, TA, LD64, wt2);
   WFr<64, 32> wt1;
@@ -772,11 +789,9 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   STAMP(14);
   gemm_pf<64, 64>(c, TB, LD64, wto);                      // da = do . Wo
   gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B::ff0, K);  // dW1 = df0^T x1
-  if (c.tid < 64) {
-    const int i = c.tid;
-    adam(c.P, c.M, c.V, B::o.ln1_w + i, cs_total(c, 0, i), K);
-    adam(c.P, c.M, c.V, B::o.ln1_b + i, cs_total(c, 1, i), K);
-    adam(c.P, c.M, c.V, B::o.out_b + i, cs_total(c, 2, i), K);
+  {
+    const VecG vs[3] = {{B::o.ln1_w, 64, 0}, {B::o.ln1_b, 64, 1}, {B::o.out_b, 64, 2}};
+    adam_vecs(c, vs, K);
   }
   WFr<64, 64> wfv;
   wload(wfv, c.BF + B::w.WFv, c.lane);
@@ -1016,14 +1031,12 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       }
       if (failed) break;
       // =============================== head backward ===============================
-      if (tid < 32) {
-        adam(c.P, c.M, c.V, OUT_W + tid, cs_total(c, 0, tid), K);
-      } else if (tid < 64) {
-        adam(c.P, c.M, c.V, FC2_B + tid - 32, cs_total(c, 1, tid - 32), K);
-      } else if (tid == 64) {
+      {
         float sm = 0.f;
-        for (int i = 0; i < BM; ++i) sm += DY3[i];
-        adam(c.P, c.M, c.V, OUT_B, sm, K);
+        if (tid == 64)
+          for (int i = 0; i < BM; ++i) sm += DY3[i];
+        const VecG vs[3] = {{OUT_W, 32, 0}, {FC2_B, 32, 1}, {OUT_B, 1, -1}};
+        adam_vecs(c, vs, K, sm);
       }
       gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
       WFr<64, 64> wtf1a;
