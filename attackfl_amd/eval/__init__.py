@@ -3,8 +3,9 @@
 ICU: ROC-AUC over the whole test set (``ROC_AUC: x.xxxx`` in ``app.log``); NaN outputs fail the
 round.  HAR: accuracy.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
 model before one ROC-AUC, like ``test_hyper_icu``.  The test set stays resident on the device
-and is evaluated in one pass (eval mode is batch-size independent); TransformerModel uses the
-fused HIP forward kernel on GPU.
+and is evaluated in one pass (eval mode is batch-size independent).  On GPU every model runs a
+native forward: TransformerModel the fused HIP eval kernel, CNNModel / RNNModel /
+TransformerClassifier their layer program (``fl/programs.py``) in eval mode.
 """
 from __future__ import annotations
 
@@ -19,6 +20,7 @@ from ..models import ParamLayout, build_model
 from ..utils.log import print_with_color
 
 EVAL_CHUNK = 65536
+PROGRAM_EVAL_BATCH = {"CNNModel": 4096, "RNNModel": 8192, "TransformerClassifier": 256}
 
 
 class Validation:
@@ -36,6 +38,15 @@ class Validation:
         ds = dataset if dataset is not None else resolve_dataset(data_name, "test", data_cfg, verbose=verbose)
         self.table = DeviceTable(ds, self.device)
         self.last_metric: float = float("nan")
+        self._runner = None
+
+    def _program_runner(self):
+        if self._runner is None:
+            from ..fl.programs import ProgramRunner, make_program
+
+            self._runner = ProgramRunner(make_program(self.model_name, 1, PROGRAM_EVAL_BATCH[self.model_name],
+                                                      self.device, train=False))
+        return self._runner
 
     # -- forward over the whole test set ------------------------------------------------------
     @torch.no_grad()
@@ -45,6 +56,9 @@ class Validation:
             from ..ops.transformer import eval_forward
 
             return eval_forward(flat, self.table.rows)
+        if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH:
+            data = self.table.rows if self.data_name == "ICU" else self.table.x
+            return self._program_runner().predict(flat[None], data)[0]
         sd = self.layout.unflatten(flat, clone=False)
         self.model.load_state_dict(sd, strict=True)
         outs = []

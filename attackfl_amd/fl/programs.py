@@ -1,0 +1,450 @@
+"""Explicit client-batched training programs (forward + hand-written backward + Adam) for the models
+without a whole-step fused kernel: ``CNNModel`` / ``RNNModel`` (ICU) and ``TransformerClassifier`` (HAR).
+
+A program is a fixed sequence of layer ops (``attackfl_amd/ops/layers.py``) over ALL of a rank's
+clients at once — tensors are ``[C, rows, cols]`` and weights are views into the flat ``[C, P]``
+parameter arena, so one launch serves every client.  Everything that changes per optimizer step
+(batch rows, batch size, epoch, dropout key, Adam step) lives in device tensors indexed by a device
+step counter, so on a GPU the whole step is captured ONCE into a HIP graph and replayed per step
+(no per-step host work, no host/device syncs).  On CPU the same program runs the composite ops —
+the fp32 oracle the GPU path is tested against.
+
+Semantics mirror the reference trainers (``client.py:66-131``): fresh Adam per round, BCE (ICU) /
+cross-entropy (HAR) mean loss, size-1 batches skipped (A-21), NaN loss aborts the client's round.
+Model math mirrors ``src/Model.py:27-88`` (CNN), ``91-163`` (RNN), ``418-458`` (HAR classifier).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+from ..models import ParamLayout
+from ..ops import layers as Lx
+from ..ops.layers import ACT_RELU, StepCtl
+
+VIT, LAB = 7, 16
+
+
+class _Program:
+    """Shared machinery: parameter views, buffer pool, weight-gradient GEMM helper."""
+
+    model_name = ""
+    loss = "bce"
+
+    def __init__(self, C: int, B: int, device, train: bool = True, dropout: bool = True):
+        self.layout = ParamLayout.for_model(self.model_name)
+        self.P = self.layout.P
+        self.slot = {s.name: s for s in self.layout.slots}
+        self.C, self.B, self.device, self.train = C, B, torch.device(device), train
+        self.drop_on = train and dropout  # dropout=False: deterministic training (gradient tests)
+        self._bufs: Dict[str, torch.Tensor] = {}
+
+    # -- buffers -------------------------------------------------------------------------------
+    def p(self, prob: float) -> float:
+        return prob if self.drop_on else 0.0
+
+    def buf(self, name: str, *shape, dtype=torch.float32) -> torch.Tensor:
+        t = self._bufs.get(name)
+        if t is None:
+            t = torch.zeros(*shape, dtype=dtype, device=self.device)
+            self._bufs[name] = t
+        return t
+
+    def w(self, flat: torch.Tensor, name: str, as2d: Tuple[int, int] = None) -> torch.Tensor:
+        """View of parameter ``name`` across clients: 2-D weights -> [C, N, K], vectors -> [C, N]."""
+        s = self.slot[name]
+        v = flat[:, s.offset:s.offset + s.numel]
+        if as2d is not None:
+            return v.view(flat.shape[0], *as2d)
+        if len(s.shape) == 1:
+            return v
+        if len(s.shape) == 2:
+            return v.view(flat.shape[0], *s.shape)
+        return v.view(flat.shape[0], s.shape[0], -1)
+
+    def dw(self, dY: torch.Tensor, X: torch.Tensor, gW: torch.Tensor) -> None:
+        """``gW [C, N, K] = dY^T X`` over the rows (split-K with atomic accumulation when the tile grid
+        alone would leave the GPU idle; ``grads`` is zeroed at the start of every step)."""
+        M, N, K = dY.shape[1], dY.shape[2], X.shape[2]
+        tiles = math.ceil(N / 64) * math.ceil(K / 64) * dY.shape[0]
+        splitk = max(1, min(M // 256, math.ceil(1024 / tiles))) if dY.is_cuda else 1
+        Lx.bgemm(dY.transpose(1, 2), X.transpose(1, 2), gW, accum=2 if splitk > 1 else 0, splitk=splitk)
+
+    def linear(self, X, params, wname, bname, out, act=0, ctl=None, layer=0, p=0.0):
+        Lx.bgemm(X, self.w(params, wname), out, bias=self.w(params, bname), act=act, ctl=ctl, layer=layer,
+                 p=self.p(p))
+
+    def linear_bwd(self, dY, X, params, grads, wname, bname, dX=None, G=None, gact=0, accum=0, ctl=None, layer=0,
+                   p=0.0):
+        """Weight/bias grads of ``Y = X W^T + b`` and (optionally) ``dX = dY W`` with a fused
+        dropout'/act' epilogue for the layer that produced X."""
+        self.dw(dY, X, self.w(grads, wname))
+        Lx.colsum(dY, self.w(grads, bname))
+        if dX is not None:
+            Lx.bgemm(dY, self.w(params, wname).transpose(1, 2), dX, G=G, gact=gact, accum=accum, ctl=ctl, layer=layer,
+                     p=self.p(p))
+
+    # -- interface -----------------------------------------------------------------------------
+    def inputs(self, table, idx, ctl):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def set_inputs(self, data: torch.Tensor) -> None:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def forward(self, params, ctl):  # -> output buffer
+        raise NotImplementedError
+
+    def backward(self, params, grads, ctl):
+        raise NotImplementedError
+
+    def skip_range(self) -> Tuple[int, int]:
+        return (0, 0)
+
+
+# ============================================================================================ ICU
+class _ICUProgram(_Program):
+    mask_inputs = False
+
+    def inputs(self, table, idx, ctl):
+        C, B = self.C, self.B
+        Lx.gather_icu(table.rows, idx, ctl, self.mask_inputs, self.buf("xv", C, B, VIT), self.buf("xl", C, B, LAB),
+                      self.buf("y", C, B))
+
+    def set_inputs(self, rows: torch.Tensor) -> None:
+        """Eval: the same ``rows [B, 24]`` for every client (zero-padded to B)."""
+        n = rows.shape[0]
+        feat = rows[:, :23]
+        if self.mask_inputs:
+            feat = torch.where(feat == -2.0, torch.zeros_like(feat), feat)
+        xv, xl = self.buf("xv", self.C, self.B, VIT), self.buf("xl", self.C, self.B, LAB)
+        xv.zero_()
+        xl.zero_()
+        xv[:, :n] = feat[None, :, :VIT]
+        xl[:, :n] = feat[None, :, VIT:23]
+
+    def labels(self):
+        return self.buf("y", self.C, self.B)
+
+
+class CNNProgram(_ICUProgram):
+    """CNNModel: Conv1d towers as im2col + MFMA GEMM (bias+ReLU epilogue), pool+dropout, MLP head."""
+
+    model_name = "CNNModel"
+    CH = (1, 32, 64, 128)
+
+    def _tower(self, br, L, params, ctl, bi):
+        C, B = self.C, self.B
+        x = self.buf("xv" if br == "vitals" else "xl", C, B, L).view(C, B * L, 1)
+        for i in (1, 2, 3):
+            cin, cout = self.CH[i - 1], self.CH[i]
+            cols = self.buf(f"{br}_cols{i}", C, B * L, 3 * cin)
+            h = self.buf(f"{br}_h{i}", C, B * L, cout)
+            Lx.im2col3(x, B, L, cols)
+            Lx.bgemm(cols, self.w(params, f"{br}_conv{i}.weight"), h, bias=self.w(params, f"{br}_conv{i}.bias"),
+                     act=ACT_RELU)
+            x = h
+        Lx.pool4_fwd(x, B, L, self.buf("cat", C, B, 1024), 512 * bi, ctl, layer=bi, p=self.p(0.3))
+
+    def forward(self, params, ctl):
+        C, B = self.C, self.B
+        self._tower("vitals", VIT, params, ctl, 0)
+        self._tower("labs", LAB, params, ctl, 1)
+        f1, f2, f3 = self.buf("f1", C, B, 128), self.buf("f2", C, B, 64), self.buf("f3", C, B, 32)
+        z = self.buf("z", C, B, 1)
+        self.linear(self.buf("cat", C, B, 1024), params, "fc1.weight", "fc1.bias", f1, act=ACT_RELU)
+        self.linear(f1, params, "fc2.weight", "fc2.bias", f2, act=ACT_RELU)
+        self.linear(f2, params, "fc3.weight", "fc3.bias", f3, act=ACT_RELU)
+        self.linear(f3, params, "output.weight", "output.bias", z)
+        return z
+
+    def backward(self, params, grads, ctl):
+        C, B = self.C, self.B
+        f1, f2, f3 = self.buf("f1", C, B, 128), self.buf("f2", C, B, 64), self.buf("f3", C, B, 32)
+        dz = self.buf("dz", C, B, 1)
+        d3, d2, d1 = self.buf("d3", C, B, 32), self.buf("d2", C, B, 64), self.buf("d1", C, B, 128)
+        dcat = self.buf("dcat", C, B, 1024)
+        self.linear_bwd(dz, f3, params, grads, "output.weight", "output.bias", d3, G=f3, gact=ACT_RELU)
+        self.linear_bwd(d3, f2, params, grads, "fc3.weight", "fc3.bias", d2, G=f2, gact=ACT_RELU)
+        self.linear_bwd(d2, f1, params, grads, "fc2.weight", "fc2.bias", d1, G=f1, gact=ACT_RELU)
+        self.linear_bwd(d1, self.buf("cat", C, B, 1024), params, grads, "fc1.weight", "fc1.bias", dcat)
+        for bi, (br, L) in enumerate((("vitals", VIT), ("labs", LAB))):
+            dh = self.buf(f"{br}_dh3", C, B * L, 128)
+            Lx.pool4_bwd(dcat, 512 * bi, self.buf(f"{br}_h3", C, B * L, 128), B, L, dh, ctl, layer=bi, p=self.p(0.3))
+            for i in (3, 2, 1):
+                cin = self.CH[i - 1]
+                cols = self.buf(f"{br}_cols{i}", C, B * L, 3 * cin)
+                self.dw(dh, cols, self.w(grads, f"{br}_conv{i}.weight"))
+                Lx.colsum(dh, self.w(grads, f"{br}_conv{i}.bias"))
+                if i > 1:
+                    dcols = self.buf(f"{br}_dcols{i}", C, B * L, 3 * cin)
+                    Lx.bgemm(dh, self.w(params, f"{br}_conv{i}.weight").transpose(1, 2), dcols)
+                    dprev = self.buf(f"{br}_dh{i - 1}", C, B * L, cin)
+                    Lx.col2im3(dcols, B, L, cin, self.buf(f"{br}_h{i - 1}", C, B * L, cin), dprev)
+                    dh = dprev
+
+
+class RNNProgram(_ICUProgram):
+    """RNNModel: 3 stacked bi-GRU layers per branch at seq_len 1 (h0 = 0), LayerNorm + dropout, MLP."""
+
+    model_name = "RNNModel"
+    mask_inputs = True
+    DIRS = ("", "_reverse")
+
+    def forward(self, params, ctl):
+        C, B = self.C, self.B
+        cat = self.buf("cat", C, B, 128)
+        for bi, (br, din) in enumerate((("vitals", VIT), ("labs", LAB))):
+            x = self.buf("xv" if bi == 0 else "xl", C, B, din)
+            for i in (1, 2, 3):
+                h = self.buf(f"{br}_h{i}", C, B, 64)
+                for d, suf in enumerate(self.DIRS):
+                    gi = self.buf(f"{br}_gi{i}{d}", C, B, 96)
+                    pre = f"{br}_gru{i}."
+                    Lx.bgemm(x, self.w(params, pre + "weight_ih_l0" + suf), gi,
+                             bias=self.w(params, pre + "bias_ih_l0" + suf))
+                    Lx.gru_fwd(gi, self.w(params, pre + "bias_hh_l0" + suf), h, 32 * d)
+                x = h
+            Lx.ln_fwd(x, None, None, cat[:, :, 64 * bi:64 * bi + 64], self.buf(f"{br}_st", C, B, 2),
+                      self.w(params, f"{br}_ln.weight"), self.w(params, f"{br}_ln.bias"), ctl,
+                      layer_o=bi, p_o=self.p(0.3))
+        f1, f2, z = self.buf("f1", C, B, 32), self.buf("f2", C, B, 16), self.buf("z", C, B, 1)
+        self.linear(cat, params, "fc1.weight", "fc1.bias", f1, act=ACT_RELU)
+        self.linear(f1, params, "fc2.weight", "fc2.bias", f2, act=ACT_RELU)
+        self.linear(f2, params, "output.weight", "output.bias", z)
+        return z
+
+    def backward(self, params, grads, ctl):
+        C, B = self.C, self.B
+        f1, f2 = self.buf("f1", C, B, 32), self.buf("f2", C, B, 16)
+        dz, d2, d1 = self.buf("dz", C, B, 1), self.buf("d2", C, B, 16), self.buf("d1", C, B, 32)
+        dcat = self.buf("dcat", C, B, 128)
+        self.linear_bwd(dz, f2, params, grads, "output.weight", "output.bias", d2, G=f2, gact=ACT_RELU)
+        self.linear_bwd(d2, f1, params, grads, "fc2.weight", "fc2.bias", d1, G=f1, gact=ACT_RELU)
+        self.linear_bwd(d1, self.buf("cat", C, B, 128), params, grads, "fc1.weight", "fc1.bias", dcat)
+        for bi, (br, din) in enumerate((("vitals", VIT), ("labs", LAB))):
+            dh = self.buf(f"{br}_dh3", C, B, 64)
+            Lx.ln_bwd(dcat[:, :, 64 * bi:64 * bi + 64], self.buf(f"{br}_h3", C, B, 64), self.buf(f"{br}_st", C, B, 2),
+                      self.w(params, f"{br}_ln.weight"), dh, 0, None, self.w(grads, f"{br}_ln.weight"),
+                      self.w(grads, f"{br}_ln.bias"), ctl, layer_o=bi, p_o=self.p(0.3))
+            for i in (3, 2, 1):
+                x = self.buf("xv" if bi == 0 else "xl", C, B, din) if i == 1 else self.buf(f"{br}_h{i - 1}", C, B, 64)
+                dprev = self.buf(f"{br}_dh{i - 1}", C, B, 64) if i > 1 else None
+                for d, suf in enumerate(self.DIRS):
+                    pre = f"{br}_gru{i}."
+                    dgi = self.buf(f"{br}_dgi{d}", C, B, 96)
+                    Lx.gru_bwd(dh, 32 * d, self.buf(f"{br}_gi{i}{d}", C, B, 96),
+                               self.w(params, pre + "bias_hh_l0" + suf), dgi,
+                               self.w(grads, pre + "bias_ih_l0" + suf), self.w(grads, pre + "bias_hh_l0" + suf))
+                    self.dw(dgi, x, self.w(grads, pre + "weight_ih_l0" + suf))
+                    if dprev is not None:
+                        Lx.bgemm(dgi, self.w(params, pre + "weight_ih_l0" + suf).transpose(1, 2), dprev,
+                                 accum=1 if d else 0)
+                if dprev is not None:
+                    dh = dprev
+
+
+# ============================================================================================ HAR
+class HARProgram(_Program):
+    """TransformerClassifier: Conv1d(1->64)+PE stem, 2 post-norm encoder layers (flash attention,
+    fused residual+dropout+LayerNorm, ReLU FFN), mean over L, MLP classifier; cross-entropy."""
+
+    model_name = "TransformerClassifier"
+    loss = "ce"
+    L = 561
+    NL = 2
+
+    def lyr(self, i, name):
+        return f"transformer.layers.{i}.{name}"
+
+    def inputs(self, table, idx, ctl):
+        C, B = self.C, self.B
+        Lx.gather_har(table.x, table.y, idx, ctl, self.buf("x", C, B, self.L),
+                      self.buf("y", C, B, dtype=torch.long))
+
+    def set_inputs(self, x: torch.Tensor) -> None:
+        n = x.shape[0]
+        xb = self.buf("x", self.C, self.B, self.L)
+        xb.zero_()
+        xb[:, :n] = x.reshape(n, -1)[None]
+
+    def labels(self):
+        return self.buf("y", self.C, self.B, dtype=torch.long)
+
+    def skip_range(self):
+        s = self.slot["pe.pe"]
+        return (s.offset, s.offset + s.numel)
+
+    def forward(self, params, ctl):
+        C, B, L = self.C, self.B, self.L
+        R = B * L
+        h = self.buf("h0", C, R, 64)
+        Lx.conv_pe_fwd(self.buf("x", C, B, L), params, self.slot["conv.weight"].offset, self.slot["conv.bias"].offset,
+                       self.slot["pe.pe"].offset, h)
+        for i in range(self.NL):
+            qkv, o, a = self.buf(f"qkv{i}", C, R, 192), self.buf(f"o{i}", C, R, 64), self.buf(f"a{i}", C, R, 64)
+            lse = self.buf(f"lse{i}", C * B * 4, Lx.attn_lp(L))
+            self.linear(h, params, self.lyr(i, "self_attn.in_proj_weight"), self.lyr(i, "self_attn.in_proj_bias"), qkv)
+            Lx.attn_fwd(qkv, o, lse, B, L, ctl, layer=10 * i, p=self.p(0.1))
+            self.linear(o, params, self.lyr(i, "self_attn.out_proj.weight"), self.lyr(i, "self_attn.out_proj.bias"), a)
+            s1, h1 = self.buf(f"s1_{i}", C, R, 64), self.buf(f"h1_{i}", C, R, 64)
+            Lx.ln_fwd(h, a, s1, h1, self.buf(f"st1_{i}", C, R, 2), self.w(params, self.lyr(i, "norm1.weight")),
+                      self.w(params, self.lyr(i, "norm1.bias")), ctl, layer_a=10 * i + 1, p_a=self.p(0.1))
+            f, f2 = self.buf(f"f{i}", C, R, 256), self.buf(f"f2_{i}", C, R, 64)
+            self.linear(h1, params, self.lyr(i, "linear1.weight"), self.lyr(i, "linear1.bias"), f, act=ACT_RELU,
+                        ctl=ctl, layer=10 * i + 2, p=0.1)
+            self.linear(f, params, self.lyr(i, "linear2.weight"), self.lyr(i, "linear2.bias"), f2)
+            s2, h2 = self.buf(f"s2_{i}", C, R, 64), self.buf(f"h{i + 1}", C, R, 64)
+            Lx.ln_fwd(h1, f2, s2, h2, self.buf(f"st2_{i}", C, R, 2), self.w(params, self.lyr(i, "norm2.weight")),
+                      self.w(params, self.lyr(i, "norm2.bias")), ctl, layer_a=10 * i + 3, p_a=self.p(0.1))
+            h = h2
+        pooled, c1, logits = self.buf("pool", C, B, 64), self.buf("c1", C, B, 64), self.buf("logits", C, B, 6)
+        Lx.mean_rows_fwd(h, B, L, pooled)
+        self.linear(pooled, params, "classifier.0.weight", "classifier.0.bias", c1, act=ACT_RELU, ctl=ctl, layer=30,
+                    p=0.3)
+        self.linear(c1, params, "classifier.3.weight", "classifier.3.bias", logits)
+        return logits
+
+    def backward(self, params, grads, ctl):
+        C, B, L = self.C, self.B, self.L
+        R = B * L
+        dlog, dc1, dpool = self.buf("dz", C, B, 6), self.buf("dc1", C, B, 64), self.buf("dpool", C, B, 64)
+        c1 = self.buf("c1", C, B, 64)
+        self.linear_bwd(dlog, c1, params, grads, "classifier.3.weight", "classifier.3.bias", dc1, G=c1,
+                        gact=ACT_RELU, ctl=ctl, layer=30, p=0.3)
+        self.linear_bwd(dc1, self.buf("pool", C, B, 64), params, grads, "classifier.0.weight", "classifier.0.bias",
+                        dpool)
+        dh = self.buf("dhA", C, R, 64)
+        Lx.mean_rows_bwd(dpool, B, L, dh)
+        other = self.buf("dhB", C, R, 64)
+        for i in reversed(range(self.NL)):
+            hin = self.buf(f"h{i}" if i else "h0", C, R, 64)
+            h1 = self.buf(f"h1_{i}", C, R, 64)
+            dh1, df2, df = self.buf("dh1", C, R, 64), self.buf("df2", C, R, 64), self.buf("df", C, R, 256)
+            Lx.ln_bwd(dh, self.buf(f"s2_{i}", C, R, 64), self.buf(f"st2_{i}", C, R, 2),
+                      self.w(params, self.lyr(i, "norm2.weight")), dh1, 0, df2,
+                      self.w(grads, self.lyr(i, "norm2.weight")), self.w(grads, self.lyr(i, "norm2.bias")), ctl,
+                      layer_a=10 * i + 3, p_a=self.p(0.1))
+            self.linear_bwd(df2, self.buf(f"f{i}", C, R, 256), params, grads, self.lyr(i, "linear2.weight"),
+                            self.lyr(i, "linear2.bias"), df, G=self.buf(f"f{i}", C, R, 256), gact=ACT_RELU, ctl=ctl,
+                            layer=10 * i + 2, p=0.1)
+            self.linear_bwd(df, h1, params, grads, self.lyr(i, "linear1.weight"), self.lyr(i, "linear1.bias"), dh1,
+                            accum=1)
+            da, do, dqkv = self.buf("da", C, R, 64), self.buf("do", C, R, 64), self.buf("dqkv", C, R, 192)
+            Lx.ln_bwd(dh1, self.buf(f"s1_{i}", C, R, 64), self.buf(f"st1_{i}", C, R, 2),
+                      self.w(params, self.lyr(i, "norm1.weight")), other, 0, da,
+                      self.w(grads, self.lyr(i, "norm1.weight")), self.w(grads, self.lyr(i, "norm1.bias")), ctl,
+                      layer_a=10 * i + 1, p_a=self.p(0.1))
+            self.linear_bwd(da, self.buf(f"o{i}", C, R, 64), params, grads, self.lyr(i, "self_attn.out_proj.weight"),
+                            self.lyr(i, "self_attn.out_proj.bias"), do)
+            Lx.attn_bwd(self.buf(f"qkv{i}", C, R, 192), self.buf(f"o{i}", C, R, 64),
+                        self.buf(f"lse{i}", C * B * 4, Lx.attn_lp(L)), do, dqkv, B, L, ctl, layer=10 * i, p=self.p(0.1))
+            self.linear_bwd(dqkv, hin, params, grads, self.lyr(i, "self_attn.in_proj_weight"),
+                            self.lyr(i, "self_attn.in_proj_bias"), other, accum=1)
+            dh, other = other, dh
+        Lx.conv_pe_bwd(self.buf("x", C, B, L), dh, grads, self.slot["conv.weight"].offset,
+                       self.slot["conv.bias"].offset)
+
+
+PROGRAMS = {"CNNModel": CNNProgram, "RNNModel": RNNProgram, "TransformerClassifier": HARProgram}
+
+
+# ================================================================================== step tables
+def step_tables(order: torch.Tensor, nd: Sequence[int], epochs: int, B: int, device):
+    """Per-step batch tables from a ``Plan``: ``idx [S, C, B]`` (-1 = padding), ``bsz [S, C]``,
+    ``epoch [S, C]``, ``nb [C]`` (batches per epoch, the loss divisor).  Client c's s-th step is its
+    s-th batch in (epoch, batch) order; steps past its last batch have ``bsz = 0``."""
+    C = order.shape[0]
+    nd = [int(x) for x in nd]
+    nbat = [max(1, math.ceil(n / B)) for n in nd]
+    S = max([epochs * n for n in nbat] + [0])
+    idx = torch.full((S, C, B), -1, dtype=torch.int32)
+    bsz = torch.zeros(S, C, dtype=torch.int32)
+    ep = torch.zeros(S, C, dtype=torch.int32)
+    oc = order.cpu()
+    for c in range(C):
+        s = 0
+        for e in range(epochs):
+            for j in range(nbat[c]):
+                a, b = j * B, min(nd[c], (j + 1) * B)
+                idx[s, c, :b - a] = oc[c, e, a:b]
+                bsz[s, c] = b - a
+                ep[s, c] = e
+                s += 1
+    return (idx.to(device), bsz.to(device), ep.to(device), torch.tensor(nbat, dtype=torch.int32, device=device), S)
+
+
+class ProgramRunner:
+    """Runs a program's optimizer steps for one round: eager on CPU, HIP-graph replay on GPU."""
+
+    def __init__(self, prog: _Program, use_graph: bool = True):
+        self.prog = prog
+        self.use_graph = use_graph and prog.device.type == "cuda"
+
+    def train(self, table, params: torch.Tensor, plan, lr: float, seeds: Sequence[int], sgd_lr: float = 0.0,
+              max_steps: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Train ``params [C, P]`` in place.  Returns (ok [C] bool, losses [C, E])."""
+        pg = self.prog
+        dev = pg.device
+        C, P = params.shape
+        idx, bsz, ep, nb, S = step_tables(plan.order, plan.nd, plan.epochs, pg.B, dev)
+        if max_steps is not None:
+            S = min(S, max_steps)
+        ctl = StepCtl.create(seeds, dev)
+        grads = torch.zeros(C, P, device=dev)
+        m = torch.zeros(C, P, device=dev)
+        v = torch.zeros(C, P, device=dev)
+        tcount = torch.zeros(C, dtype=torch.int32, device=dev)
+        failed = torch.zeros(C, dtype=torch.int32, device=dev)
+        losses = torch.zeros(C, plan.epochs, device=dev)
+        skip = pg.skip_range()
+
+        def step():
+            pg.inputs(table, idx, ctl)
+            out = pg.forward(params, ctl)
+            dz = pg.buf("dz", *out.shape)
+            if pg.loss == "bce":
+                Lx.bce(out, pg.labels(), bsz, ep, nb, ctl, failed, losses, dz)
+            else:
+                Lx.ce(out, pg.labels(), bsz, ep, nb, ctl, failed, losses, dz)
+            grads.zero_()
+            pg.backward(params, grads, ctl)
+            Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr)
+            Lx.step_end(ctl, tcount, bsz, failed)
+
+        if S == 0:
+            return torch.ones(C, dtype=torch.bool), losses.double().cpu()
+        step()  # eager first step: allocates every buffer and sets kernel attributes before capture
+        if S > 1:
+            if self.use_graph:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    step()
+                # capture recorded without executing; the counter still points at step 1
+                for _ in range(S - 1):
+                    g.replay()
+            else:
+                for _ in range(S - 1):
+                    step()
+        return (failed == 0).cpu(), losses.double().cpu()
+
+    @torch.no_grad()
+    def predict(self, params: torch.Tensor, data: torch.Tensor) -> torch.Tensor:
+        """Eval forward of ``params [C, P]`` on ``data`` (ICU rows [N, 24] or HAR x [N, 561]) in chunks
+        of the program's batch -> [C, N] probabilities (ICU) or [C, N, 6] logits (HAR)."""
+        pg = self.prog
+        outs = []
+        for a in range(0, data.shape[0], pg.B):
+            chunk = data[a:a + pg.B]
+            pg.set_inputs(chunk)
+            out = pg.forward(params, None)
+            n = chunk.shape[0]
+            outs.append(torch.sigmoid(out[:, :n, 0]) if pg.loss == "bce" else out[:, :n].clone())
+        return torch.cat(outs, dim=1)
+
+
+def make_program(model_name: str, C: int, B: int, device, train: bool = True, dropout: bool = True) -> _Program:
+    if model_name not in PROGRAMS:
+        raise ValueError(f"no layer program for {model_name}")
+    return PROGRAMS[model_name](C, B, device, train, dropout)

@@ -14,6 +14,8 @@ Two implementations share one sampling plan (``make_plan``), so they see identic
 * ``FusedTrainer``  — ONE persistent HIP kernel launch trains all of a rank's clients for all
   their local epochs (one workgroup per client, weights/activations in LDS, Adam state in
   registers) — ``ops/transformer.py``.  TransformerModel/ICU on gfx950.
+* ``GraphTrainer``  — client-batched layer programs (``fl/programs.py``: CNNModel, RNNModel,
+  TransformerClassifier/HAR) whose optimizer step is captured once into a HIP graph and replayed.
 """
 from __future__ import annotations
 
@@ -176,10 +178,53 @@ class FusedTrainer:
         return [bool(x) for x in ok.tolist()], losses
 
 
+class GraphTrainer:
+    """All local clients batched through a layer program; one HIP-graph replay per optimizer step."""
+
+    kind = "graph"
+
+    def __init__(self, model_name: str, data_name: str, table: DeviceTable, device, verbose: bool = False):
+        from . import programs
+
+        if model_name not in programs.PROGRAMS:
+            raise ValueError(f"graph trainer supports {sorted(programs.PROGRAMS)}")
+        self.programs = programs
+        self.model_name = model_name
+        self.table = table
+        self.device = torch.device(device)
+        self.layout = ParamLayout.for_model(model_name)
+        self.verbose = verbose
+        self._runner = None
+
+    def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
+              ) -> Tuple[List[bool], torch.Tensor]:
+        C = params.shape[0]
+        if self._runner is None or self._runner.prog.C != C or self._runner.prog.B != batch:
+            self._runner = self.programs.ProgramRunner(
+                self.programs.make_program(self.model_name, C, batch, self.device, train=True))
+        ok, losses = self._runner.train(self.table, params, plan, lr, seeds)
+        if self.verbose:
+            for c in range(C):
+                for e in range(plan.epochs):
+                    print_with_color(f"Loss {float(losses[c, e]):.6f} ", "yellow")
+        return [bool(x) for x in ok.tolist()], losses
+
+
 def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable, device, verbose=False):
+    from .programs import PROGRAMS
+
     dev = torch.device(device)
     if kind == "auto":
-        kind = "fused" if (dev.type == "cuda" and model_name == "TransformerModel" and data_name == "ICU") else "eager"
+        if dev.type != "cuda":
+            kind = "eager"
+        elif model_name == "TransformerModel" and data_name == "ICU":
+            kind = "fused"
+        elif model_name in PROGRAMS:
+            kind = "graph"
+        else:
+            kind = "eager"
     if kind == "fused":
         return FusedTrainer(model_name, data_name, table, device, verbose)
+    if kind == "graph":
+        return GraphTrainer(model_name, data_name, table, device, verbose)
     return EagerTrainer(model_name, data_name, table, device, verbose)

@@ -1,0 +1,482 @@
+"""Client-batched layer ops: HIP kernels (``csrc/kernels/layers.hip``, ``attention.hip``) for device
+tensors, PyTorch composites for CPU tensors.
+
+All ops write into caller-provided outputs (the step programs preallocate and graph-capture them).
+Tensors are ``[C clients, rows, cols]``; weights are strided views into the flat ``[C, P]`` arena,
+so ``W.transpose(1, 2)`` is free.  The composites are the fp32 numerical oracles of the kernels and
+regenerate the same hash dropout masks (``ops/masks.py``); the native path uses bf16 MFMA operands
+with fp32 accumulation.
+
+Dropout convention: ``ctl`` carries the per-client seeds and the device step counter; a site is
+identified by ``(layer id, row, column)`` of the tensor it masks.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import masks
+from . import native as _native
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+
+@dataclass
+class StepCtl:
+    """Per-client dropout seeds (int32 [C]) + the device step counter (int32 [1])."""
+
+    seeds: torch.Tensor
+    stepctl: torch.Tensor
+
+    @classmethod
+    def create(cls, seeds, device) -> "StepCtl":
+        s = torch.tensor([int(x) & masks.M32 for x in seeds], dtype=torch.int64)
+        s = torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32)
+        return cls(s.to(device), torch.zeros(1, dtype=torch.int32, device=device))
+
+    # composite helpers
+    def step(self) -> int:
+        return int(self.stepctl[0])
+
+    def key(self, c: int) -> int:
+        return masks.step_key(int(self.seeds[c]) & masks.M32, self.step())
+
+
+def _nat(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _dargs(ctl: Optional[StepCtl], p: float):
+    if p <= 0.0 or ctl is None:
+        return None, None
+    return ctl.seeds, ctl.stepctl
+
+
+def _scale(ctl: StepCtl, c: int, layer: int, rows, cols, p: float) -> torch.Tensor:
+    return masks.keep(ctl.key(c), layer, rows, cols, p).float() / (1.0 - p)
+
+
+def _act(v, act):
+    return F.relu(v) if act == ACT_RELU else (F.gelu(v) if act == ACT_GELU else v)
+
+
+def _actd(g, gact):
+    if gact == ACT_RELU:
+        return (g > 0).float()
+    if gact == ACT_GELU:
+        cdf = 0.5 * (1.0 + torch.erf(g * 0.7071067811865476))
+        return cdf + g * 0.3989422804014327 * torch.exp(-0.5 * g * g)
+    return torch.ones_like(g)
+
+
+def _rc(M, N):
+    return np.arange(M)[:, None], np.arange(N)[None, :]
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+def bgemm(A, B, C, bias=None, Z=None, G=None, act=0, gact=0, accum=0, splitk=1, alpha=1.0,
+          ctl: Optional[StepCtl] = None, layer: int = 0, p: float = 0.0) -> None:
+    """``C (op)= epi(alpha * A @ B^T)``; A [C,M,K], B [C,N,K], C [C,M,N].
+
+    Epilogue order: +bias -> (Z := pre-activation) -> act -> dropout(layer, m, n) -> *act'(G).
+    accum: 0 store, 1 add, 2 atomic add (required when splitk > 1)."""
+    if _nat(A):
+        s, sc = _dargs(ctl, p)
+        _native().bgemm(A, B, C, bias, Z, G, act, gact, accum, splitk, alpha, s, sc, layer, p)
+        return
+    v = alpha * torch.bmm(A, B.transpose(1, 2))
+    if bias is not None:
+        v = v + bias[:, None, :]
+    if Z is not None:
+        Z.copy_(v)
+    v = _act(v, act)
+    if p > 0.0:
+        r, c = _rc(v.shape[1], v.shape[2])
+        v = v * torch.stack([_scale(ctl, ci, layer, r, c, p) for ci in range(v.shape[0])])
+    if G is not None:
+        v = v * _actd(G, gact)
+    if accum == 0:
+        C.copy_(v)
+    else:
+        C.add_(v)
+
+
+def colsum(Y, out) -> None:
+    """``out [C, N] += Y.sum(rows)`` (atomic accumulation on device: zero ``out`` first)."""
+    if _nat(Y):
+        _native().colsum(Y, out)
+        return
+    out.add_(Y.sum(dim=1))
+
+
+# ------------------------------------------------------------------------------------- batches
+def gather_icu(rows, idx, ctl: StepCtl, mask: bool, vit, lab, y) -> None:
+    """Rows ``idx[step]`` ([S, C, B], -1 = padding) of the ICU table -> vitals/labs/labels."""
+    if _nat(rows):
+        _native().gather_icu(rows, idx, ctl.stepctl, int(mask), vit, lab, y)
+        return
+    ix = idx[ctl.step()].long()
+    r = torch.where((ix >= 0)[..., None], rows[ix.clamp_min(0)], torch.zeros((), dtype=rows.dtype))
+    feat = r[..., :23]
+    if mask:
+        feat = torch.where(feat == -2.0, torch.zeros_like(feat), feat)
+    vit.copy_(feat[..., :7].reshape(vit.shape))
+    lab.copy_(feat[..., 7:23].reshape(lab.shape))
+    y.copy_(r[..., 23].reshape(y.shape))
+
+
+def gather_har(x, yl, idx, ctl: StepCtl, ox, oy) -> None:
+    if _nat(x):
+        _native().gather_har(x, yl, idx, ctl.stepctl, ox, oy)
+        return
+    ix = idx[ctl.step()].long()
+    ok = ix >= 0
+    ox.copy_(torch.where(ok[..., None], x[ix.clamp_min(0)], torch.zeros((), dtype=x.dtype)).reshape(ox.shape))
+    oy.copy_(torch.where(ok, yl[ix.clamp_min(0)], torch.zeros((), dtype=yl.dtype)).reshape(oy.shape))
+
+
+# ---------------------------------------------------------------------------------- conv k=3
+def _im2col(x, B, L):
+    C, _, Cin = x.shape
+    xp = F.pad(x.reshape(C, B, L, Cin), (0, 0, 1, 1))
+    cols = torch.stack([xp[:, :, j:j + L, :] for j in range(3)], dim=-1)  # [C, B, L, Cin, 3]
+    return cols.reshape(C, B * L, Cin * 3)
+
+
+def im2col3(x, B: int, L: int, out) -> None:
+    """Conv1d(k=3, pad=1) patches of channels-last ``x [C, B*L, Cin]`` -> ``out [C, B*L, 3*Cin]``
+    (column ``ci*3 + j`` = input position ``l + j - 1``: PyTorch's ``[Cout][Cin][3]`` weight order)."""
+    if _nat(x):
+        _native().im2col3(x, B, L, out)
+        return
+    out.copy_(_im2col(x, B, L).reshape(out.shape))
+
+
+def col2im3(dcols, B: int, L: int, Cin: int, relu_src, dx) -> None:
+    """Adjoint of ``im2col3`` (optionally times relu'(relu_src))."""
+    if _nat(dcols):
+        _native().col2im3(dcols, B, L, Cin, relu_src, dx)
+        return
+    C = dcols.shape[0]
+    x = torch.zeros(C, B * L, Cin, requires_grad=True)
+    with torch.enable_grad():
+        (g,) = torch.autograd.grad(_im2col(x, B, L), x, dcols.reshape(C, B * L, 3 * Cin))
+    if relu_src is not None:
+        g = g * (relu_src > 0).float()
+    dx.copy_(g.reshape(dx.shape))
+
+
+# --------------------------------------------------------------------- AdaptiveAvgPool1d(4)
+def _pool4(h, B, L):
+    C, _, Ch = h.shape
+    return F.adaptive_avg_pool1d(h.reshape(C * B, L, Ch).transpose(1, 2), 4).reshape(C, B, Ch * 4)
+
+
+def pool4_fwd(h, B: int, L: int, out, col0: int, ctl=None, layer=0, p=0.0) -> None:
+    """``out[:, b, col0 + ch*4 + p] = dropout(mean over bin p of h[:, b*L + l, ch])``."""
+    if _nat(h):
+        s, sc = _dargs(ctl, p)
+        _native().pool4_fwd(h, B, L, out, col0, s, sc, layer, p)
+        return
+    v = _pool4(h, B, L)
+    if p > 0.0:
+        r, c = _rc(B, v.shape[2])
+        v = v * torch.stack([_scale(ctl, ci, layer, r, c + col0, p) for ci in range(v.shape[0])])
+    out[:, :, col0:col0 + v.shape[2]] = v
+
+
+def pool4_bwd(dout, col0: int, h, B: int, L: int, dh, ctl=None, layer=0, p=0.0) -> None:
+    """Adjoint of ``pool4_fwd`` times relu'(h)."""
+    if _nat(h):
+        s, sc = _dargs(ctl, p)
+        _native().pool4_bwd(dout, col0, h, B, L, dh, s, sc, layer, p)
+        return
+    C, _, Ch = h.shape
+    g = dout[:, :, col0:col0 + Ch * 4]
+    if p > 0.0:
+        r, c = _rc(B, Ch * 4)
+        g = g * torch.stack([_scale(ctl, ci, layer, r, c + col0, p) for ci in range(C)])
+    x = h.detach().clone().requires_grad_(True)
+    with torch.enable_grad():
+        (d,) = torch.autograd.grad(_pool4(x, B, L), x, g.contiguous())
+    dh.copy_((d * (h > 0).float()).reshape(dh.shape))
+
+
+# ------------------------------------------------------------------------------- LayerNorm(64)
+def ln_fwd(x, a, s, y, stats, gamma, beta, ctl=None, layer_a=0, p_a=0.0, layer_o=0, p_o=0.0) -> None:
+    """``y = dropout_o(LN(x + dropout_a(a)) * gamma + beta)``; stores the pre-norm sum in ``s`` (optional)
+    and (mean, rstd) per row in ``stats [C, rows, 2]``."""
+    if _nat(x):
+        sd, sc = _dargs(ctl, max(p_a, p_o))
+        _native().ln_fwd(x, a, s, y, stats, gamma, beta, sd, sc, layer_a, p_a, layer_o, p_o)
+        return
+    C, R, _ = x.shape
+    v = x.clone()
+    if a is not None:
+        av = a
+        if p_a > 0.0:
+            r, c = _rc(R, 64)
+            av = a * torch.stack([_scale(ctl, ci, layer_a, r, c, p_a) for ci in range(C)])
+        v = v + av
+    if s is not None:
+        s.copy_(v.reshape(s.shape))
+    mean = v.mean(-1, keepdim=True)
+    var = ((v - mean) ** 2).mean(-1, keepdim=True)
+    rstd = torch.rsqrt(var + 1e-5)
+    out = (v - mean) * rstd * gamma[:, None, :] + beta[:, None, :]
+    if p_o > 0.0:
+        r, c = _rc(R, 64)
+        out = out * torch.stack([_scale(ctl, ci, layer_o, r, c, p_o) for ci in range(C)])
+    y.copy_(out)
+    stats.copy_(torch.cat([mean, rstd], dim=-1).reshape(stats.shape))
+
+
+def ln_bwd(dy, s, stats, gamma, dx, dx_accum, da, dgamma, dbeta, ctl=None, layer_a=0, p_a=0.0, layer_o=0,
+           p_o=0.0) -> None:
+    """Backward of ``ln_fwd``: dx (= d pre-norm sum; stored or accumulated), optional ``da =
+    dropout_a'(dx)``, and ``dgamma``/``dbeta`` accumulated (zero them first)."""
+    if _nat(dy):
+        sd, sc = _dargs(ctl, max(p_a, p_o))
+        _native().ln_bwd(dy, s, stats, gamma, dx, int(dx_accum), da, dgamma, dbeta, sd, sc, layer_a, p_a, layer_o,
+                         p_o)
+        return
+    C, R, _ = dy.shape
+    g = dy
+    if p_o > 0.0:
+        r, c = _rc(R, 64)
+        g = dy * torch.stack([_scale(ctl, ci, layer_o, r, c, p_o) for ci in range(C)])
+    sv = s.detach().clone().requires_grad_(True)
+    gm = gamma.detach().clone().requires_grad_(True)
+    bt = torch.zeros_like(gm, requires_grad=True)
+    with torch.enable_grad():
+        out = torch.stack([F.layer_norm(sv[ci], (64,), gm[ci], bt[ci], 1e-5) for ci in range(C)])
+        ds, dgm, dbt = torch.autograd.grad(out, (sv, gm, bt), g.contiguous())
+    if dx_accum:
+        dx.add_(ds)
+    else:
+        dx.copy_(ds)
+    if da is not None:
+        v = ds
+        if p_a > 0.0:
+            r, c = _rc(R, 64)
+            v = ds * torch.stack([_scale(ctl, ci, layer_a, r, c, p_a) for ci in range(C)])
+        da.copy_(v)
+    dgamma.add_(dgm)
+    dbeta.add_(dbt)
+
+
+# ------------------------------------------------------------------------------------- GRU cell
+def _gru(gi, bhh):
+    r = torch.sigmoid(gi[..., :32] + bhh[:, None, :32])
+    z = torch.sigmoid(gi[..., 32:64] + bhh[:, None, 32:64])
+    n = torch.tanh(gi[..., 64:] + r * bhh[:, None, 64:])
+    return (1 - z) * n
+
+
+def gru_fwd(gi, bhh, h, col0: int) -> None:
+    """One GRU direction at seq_len 1 with h0 = 0: ``h[:, :, col0:col0+32] = (1 - z) * n``."""
+    if _nat(gi):
+        _native().gru_fwd(gi, bhh, h, col0)
+        return
+    h[:, :, col0:col0 + 32] = _gru(gi, bhh)
+
+
+def gru_bwd(dh, col0: int, gi, bhh, dgi, dbih, dbhh) -> None:
+    """dgi (= d(x W_ih^T + b_ih)), and the bias gradients (stored)."""
+    if _nat(gi):
+        _native().gru_bwd(dh, col0, gi, bhh, dgi, dbih, dbhh)
+        return
+    g = gi.detach().clone().requires_grad_(True)
+    b = bhh.detach().clone().requires_grad_(True)
+    with torch.enable_grad():
+        dg, db = torch.autograd.grad(_gru(g, b), (g, b), dh[:, :, col0:col0 + 32].contiguous())
+    dgi.copy_(dg)
+    dbih.copy_(dg.sum(1))
+    dbhh.copy_(db)
+
+
+# ------------------------------------------------------------------------------------- losses
+def _active(bsz, failed, s: int, c: int):
+    bs = int(bsz[s, c]) if s < bsz.shape[0] else 0
+    return bs >= 2 and int(failed[c]) == 0, bs
+
+
+def bce(z, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
+    """Mean BCE on sigmoid(z) over the step's real rows, gradient, NaN abort (client.py:95-103)."""
+    if _nat(z):
+        _native().bce(z, y, bsz, epoch, nb, ctl.stepctl, failed, losses, dz)
+        return
+    s = ctl.step()
+    dz.zero_()
+    C, B = y.shape[0], y.shape[1]
+    zz, yy, dd = z.reshape(C, B), y.reshape(C, B), dz.reshape(C, B)
+    for c in range(C):
+        act, bs = _active(bsz, failed, s, c)
+        if not act:
+            continue
+        p = torch.sigmoid(zz[c, :bs])
+        t = yy[c, :bs]
+        lv = -(t * torch.clamp(torch.log(p), min=-100.0) + (1 - t) * torch.clamp(torch.log1p(-p), min=-100.0))
+        loss = lv.mean()
+        if bool(torch.isnan(loss)):
+            failed[c] = 1
+            continue
+        losses[c, int(epoch[s, c])] += loss / int(nb[c])
+        w = p * (1 - p)
+        dd[c, :bs] = (p - t) / torch.clamp(w, min=1e-12) * w / bs
+
+
+def ce(logits, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
+    """Mean softmax cross-entropy (``nn.CrossEntropyLoss``) + gradient + NaN abort."""
+    if _nat(logits):
+        _native().ce(logits, y, bsz, epoch, nb, ctl.stepctl, failed, losses, dz)
+        return
+    s = ctl.step()
+    dz.zero_()
+    for c in range(logits.shape[0]):
+        act, bs = _active(bsz, failed, s, c)
+        if not act:
+            continue
+        x = logits[c, :bs]
+        loss = F.cross_entropy(x, y[c, :bs])
+        if bool(torch.isnan(loss)):
+            failed[c] = 1
+            continue
+        losses[c, int(epoch[s, c])] += loss / int(nb[c])
+        dz[c, :bs] = (torch.softmax(x, -1) - F.one_hot(y[c, :bs], x.shape[-1]).float()) / bs
+
+
+# ---------------------------------------------------------------------------------- optimizer
+def adam_clients(p, g, m, v, tcount, bsz, ctl: StepCtl, failed, lr: float, skip=(0, 0), sgd_lr: float = 0.0) -> None:
+    """``torch.optim.Adam(lr)`` step (β 0.9/0.999, eps 1e-8) of every client active this step;
+    ``skip`` = [lo, hi) of non-trainable entries (buffers); ``sgd_lr > 0`` = plain SGD (test hook)."""
+    if _nat(p):
+        _native().adam_clients(p, g, m, v, tcount, bsz, ctl.stepctl, failed, float(lr), int(skip[0]), int(skip[1]),
+                               float(sgd_lr))
+        return
+    s = ctl.step()
+    keep = torch.ones(p.shape[1], dtype=torch.bool)
+    keep[skip[0]:skip[1]] = False
+    for c in range(p.shape[0]):
+        act, _ = _active(bsz, failed, s, c)
+        if not act:
+            continue
+        gi = g[c][keep]
+        if sgd_lr > 0:
+            p[c][keep] -= sgd_lr * gi
+            continue
+        t = int(tcount[c]) + 1
+        mi = m[c][keep] + 0.1 * (gi - m[c][keep])
+        vi = 0.999 * v[c][keep] + 0.001 * gi * gi
+        m[c][keep] = mi
+        v[c][keep] = vi
+        bc1, bc2 = 1 - 0.9 ** t, 1 - 0.999 ** t
+        p[c][keep] -= (lr / bc1) * mi / (vi.sqrt() / (bc2 ** 0.5) + 1e-8)
+
+
+def step_end(ctl: StepCtl, tcount, bsz, failed) -> None:
+    """Advance the device step counter and every active client's Adam step count."""
+    if _nat(tcount):
+        _native().step_end(ctl.stepctl, tcount, bsz, failed)
+        return
+    s = ctl.step()
+    for c in range(tcount.shape[0]):
+        if _active(bsz, failed, s, c)[0]:
+            tcount[c] += 1
+    ctl.stepctl[0] += 1
+
+
+# ------------------------------------------------------------------------ HAR stem / pooling
+def conv_pe_fwd(x, params, w_off: int, b_off: int, pe_off: int, h) -> None:
+    """Conv1d(1->64, k3, p1) over ``x [C, B, L]`` + positional encoding -> ``h [C, B*L, 64]``."""
+    if _nat(x):
+        _native().conv_pe_fwd(x, params, w_off, b_off, pe_off, h)
+        return
+    C, B, L = x.shape
+    w = params[:, w_off:w_off + 192].reshape(C, 64, 1, 3)
+    b = params[:, b_off:b_off + 64]
+    pe = params[:, pe_off:pe_off + L * 64].reshape(C, L, 64)
+    for c in range(C):
+        o = F.conv1d(x[c][:, None, :], w[c], b[c], padding=1).transpose(1, 2) + pe[c][None]
+        h[c] = o.reshape(B * L, 64)
+
+
+def conv_pe_bwd(x, dh, grads, w_off: int, b_off: int) -> None:
+    """Accumulate the conv weight/bias gradients into the flat ``grads [C, P]``."""
+    if _nat(x):
+        _native().conv_pe_bwd(x, dh, grads, w_off, b_off)
+        return
+    C, B, L = x.shape
+    for c in range(C):
+        w = torch.zeros(64, 1, 3, requires_grad=True)
+        b = torch.zeros(64, requires_grad=True)
+        with torch.enable_grad():
+            o = F.conv1d(x[c][:, None, :], w, b, padding=1).transpose(1, 2)
+            dw, db = torch.autograd.grad(o, (w, b), dh[c].reshape(B, L, 64))
+        grads[c, w_off:w_off + 192] += dw.reshape(-1)
+        grads[c, b_off:b_off + 64] += db
+
+
+def mean_rows_fwd(h, B: int, L: int, out) -> None:
+    if _nat(h):
+        _native().mean_rows_fwd(h, B, L, out)
+        return
+    out.copy_(h.reshape(h.shape[0], B, L, 64).mean(2).reshape(out.shape))
+
+
+def mean_rows_bwd(dout, B: int, L: int, dh) -> None:
+    if _nat(dout):
+        _native().mean_rows_bwd(dout, B, L, dh)
+        return
+    C = dout.shape[0]
+    dh.copy_((dout.reshape(C, B, 1, 64) / L).expand(C, B, L, 64).reshape(dh.shape))
+
+
+# ---------------------------------------------------------------------------------- attention
+def attn_lp(L: int) -> int:
+    return (L + 31) // 32 * 32
+
+
+def _attn_ref(qkv, B, L, ctl, layer, p):
+    """Composite SDPA (4 heads x 16, scale 1/4, dropout on the probabilities) -> (O, lse)."""
+    C = qkv.shape[0]
+    q, k, v = qkv.reshape(C, B, L, 3, 4, 16).permute(3, 0, 1, 4, 2, 5)  # each [C, B, H, L, 16]
+    s = torch.matmul(q, k.transpose(-1, -2)) * 0.25
+    lse = torch.logsumexp(s, dim=-1)
+    pr = torch.softmax(s, dim=-1)
+    if p > 0.0:
+        rows = (np.arange(B * 4)[:, None] * L + np.arange(L)[None, :]).reshape(B, 4, L, 1)
+        cols = np.arange(L).reshape(1, 1, 1, L)
+        pr = pr * torch.stack([_scale(ctl, ci, layer, rows, cols, p) for ci in range(C)])
+    o = torch.matmul(pr, v)  # [C, B, H, L, 16]
+    return o.permute(0, 1, 3, 2, 4).reshape(C, B * L, 64), lse
+
+
+def attn_fwd(qkv, o, lse, B: int, L: int, ctl=None, layer=0, p=0.0) -> None:
+    """Multi-head self-attention of ``qkv [C, B*L, 192]`` -> ``o [C, B*L, 64]``, ``lse [C*B*4, Lp]``."""
+    if _nat(qkv):
+        s, sc = _dargs(ctl, p)
+        _native().attn_fwd(qkv, o, lse, B, L, s, sc, layer, p)
+        return
+    out, ls = _attn_ref(qkv, B, L, ctl, layer, p)
+    o.copy_(out)
+    Lp = attn_lp(L)
+    lv = lse.view(-1, Lp)
+    lv.fill_(float("inf"))
+    lv[:, :L] = ls.reshape(-1, L)
+
+
+def attn_bwd(qkv, o, lse, dout, dqkv, B: int, L: int, ctl=None, layer=0, p=0.0) -> None:
+    if _nat(qkv):
+        s, sc = _dargs(ctl, p)
+        _native().attn_bwd(qkv, o, lse, dout, dqkv, B, L, s, sc, layer, p)
+        return
+    x = qkv.detach().clone().requires_grad_(True)
+    with torch.enable_grad():
+        out, _ = _attn_ref(x, B, L, ctl, layer, p)
+        (g,) = torch.autograd.grad(out, x, dout)
+    dqkv.copy_(g)

@@ -5,6 +5,8 @@
 
 #include "kernels.h"
 
+void afl_register_layers(pybind11::module& m);  // layers_bind.cpp
+
 namespace {
 
 hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
@@ -302,4 +304,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);
+  afl_register_layers(m);
 }

@@ -78,3 +78,22 @@ __device__ __forceinline__ float afl_uniform(uint64_t seed, uint64_t ctr) {
 // launch helpers
 // ---------------------------------------------------------------------------------------------
 static inline int afl_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------------------------
+// dropout keep-test shared by the layer kernels: one 32-bit hash of (step key, layer, row, column
+// pair) gives the 16-bit uniforms of two adjacent columns; keep iff u16 >= round(p * 65536).
+// Step key = afl_hash32(client seed, step).  Mirrored bit-exactly by ops/masks.py.
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t afl_hash4(uint32_t key, uint32_t layer, uint32_t r, uint32_t c) {
+  uint32_t x = key ^ (layer * 0x9E3779B9u) ^ (r * 0x85EBCA6Bu) ^ (c * 0xC2B2AE35u);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ __forceinline__ bool afl_keep(uint32_t key, uint32_t layer, uint32_t r, uint32_t c,
+                                                  uint32_t thr16) {
+  return ((afl_hash4(key, layer, r, c >> 1) >> ((c & 1u) << 4)) & 0xFFFFu) >= thr16;
+}

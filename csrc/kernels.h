@@ -56,3 +56,106 @@ int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, i
 long afl_tf_ws_floats();
 int afl_tf_bf_ushorts();
 int afl_tf_param_count();
+
+// ============================================================================================
+// layers.hip — client-batched layer kernels: the native path of every model without a fused
+// trainer (CNNModel, RNNModel, TransformerClassifier/HAR).  Tensors are [C clients][rows][cols]
+// fp32 with explicit strides; GEMMs stage bf16 tiles in LDS and run v_mfma_f32_16x16x32_bf16.
+// ============================================================================================
+struct AflDrop {          // dropout site; thr16 == 0 disables it
+  const uint32_t* seeds;  // [C] client seeds
+  const int* stepctl;     // device step counter (null: step 0)
+  uint32_t layer, thr16;
+  float inv_keep;
+};
+struct AflGemm {
+  // Cm[c][m][n] (op)= epi( alpha * sum_k A[c][m][k] * B[c][n][k] )
+  const float* A;
+  long sAc, sAm, sAk;
+  const float* B;
+  long sBc, sBn, sBk;
+  float* Cm;
+  long sCc, sCm, sCn;
+  float* Z;            // optional copy of the pre-activation (Cm strides)
+  const float* bias;   // optional bias[c * sbc + n]
+  long sbc;
+  const float* G;      // optional activation-derivative source: out *= act'(G[c][m][n])
+  long sGc, sGm, sGn;
+  int M, N, K, nC;
+  int act;     // 0 none, 1 relu, 2 gelu(erf)
+  int gact;    // 0 none, 1 relu' (G > 0), 2 gelu'(G)
+  int accum;   // 0 store, 1 add (single writer), 2 atomic add (split-K)
+  int splitk;
+  float alpha;
+  AflDrop drop;
+};
+int afl_bgemm(const AflGemm& g, hipStream_t s);
+int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s);
+int afl_gather_icu(const float* rows, const int* idx, const int* stepctl, int C, int B, int mask, float* vit,
+                   float* lab, float* y, hipStream_t s);
+int afl_gather_har(const float* x, const long* y, int F, const int* idx, const int* stepctl, int C, int B, float* ox,
+                   long* oy, hipStream_t s);
+int afl_im2col3(const float* x, long sXc, long sXr, int C, int B, int L, int Cin, float* out, hipStream_t s);
+int afl_col2im3(const float* dcols, int C, int B, int L, int Cin, const float* relu_src, long sRc, long sRr, float* dx,
+                hipStream_t s);
+int afl_pool4_fwd(const float* h, int C, int B, int L, int Ch, float* out, long sOc, long sOr, int col0, AflDrop d,
+                  hipStream_t s);
+int afl_pool4_bwd(const float* dout, long sOc, long sOr, int col0, const float* h, int C, int B, int L, int Ch,
+                  float* dh, AflDrop d, hipStream_t s);
+struct AflLn {
+  // y = LN(x + drop_a(a)) * gamma + beta, then y = drop_o(y); D = 64
+  const float* x; long sXc, sXr;
+  const float* a; long sAc, sAr;  // optional residual branch
+  float* s;                       // optional stored pre-norm sum [C][rows][64] (dense)
+  float* y; long sYc, sYr;
+  float* stats;                   // [C][rows][2] mean, rstd
+  const float* gamma; const float* beta; long sPc;  // params (+ client stride)
+  int rows, nC;
+  AflDrop da, dout;
+};
+int afl_ln_fwd(const AflLn& l, hipStream_t s);
+struct AflLnB {
+  const float* dy; long sDc, sDr;
+  const float* s; long sSc, sSr;  // pre-norm input (dense [C][rows][64] when from AflLn.s)
+  const float* stats;
+  const float* gamma; long sPc;
+  float* dx; long sXc, sXr; int dx_accum;  // d(pre-norm sum)
+  float* da; long sAc, sAr;               // optional: drop_a'(dx) for the residual branch
+  float* dgamma; float* dbeta;            // grad slots (+ sPc), atomically accumulated
+  int rows, nC;
+  AflDrop da_drop, dout;
+};
+int afl_ln_bwd(const AflLnB& l, hipStream_t s);
+int afl_gru_fwd(const float* gi, const float* bhh, long sPc, int C, int B, float* h, long sHc, long sHr, int col0,
+                hipStream_t s);
+int afl_gru_bwd(const float* dh, long sHc, long sHr, int col0, const float* gi, const float* bhh, long sPc, int C,
+                int B, float* dgi, float* dbih, float* dbhh, hipStream_t s);
+int afl_bce(const float* z, const float* y, const int* bsz, const int* epoch, const int* nb, const int* stepctl, int C,
+            int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s);
+int afl_ce(const float* logits, const long* y, int K, const int* bsz, const int* epoch, const int* nb,
+           const int* stepctl, int C, int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s);
+int afl_adam_clients(float* p, const float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
+                     const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi,
+                     float sgd_lr, hipStream_t s);
+int afl_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, int C, int S, hipStream_t s);
+int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off,
+                    int pe_off, float* h, hipStream_t s);
+int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float* grads, long P, int w_off, int b_off,
+                    hipStream_t s);
+int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s);
+int afl_mean_rows_bwd(const float* dout, int C, int B, int L, float* dh, hipStream_t s);
+
+// attention.hip — flash attention (HAR encoder: 4 heads x 16, L <= 640)
+struct AflAttn {
+  const float* qkv;   // [C][B*L][192]
+  float* o;           // [C][B*L][64]  (fwd output; bwd input)
+  float* lse;         // [C*B*4][Lp]
+  const float* dout;  // [C][B*L][64]  (bwd)
+  float* dqkv;        // [C][B*L][192] (bwd output)
+  int C, B, L, Lp;
+  float scale;
+  AflDrop drop;
+};
+int afl_attn_lp(int L);
+int afl_attn_fwd(const AflAttn& a, hipStream_t s);
+int afl_attn_bwd(const AflAttn& a, hipStream_t s);

@@ -1,0 +1,814 @@
+// Client-batched layer kernels for gfx950 — the native training/eval path of every model that has no
+// whole-step fused trainer: CNNModel (reference src/Model.py:27-88), RNNModel (src/Model.py:91-163)
+// and the HAR TransformerClassifier (src/Model.py:418-458).  The training step is a fixed sequence of
+// these launches over all of a rank's clients at once ([C][rows][cols] tensors), captured once into a
+// HIP graph and replayed per optimizer step (attackfl_amd/fl/programs.py); everything that varies per
+// step (batch rows, batch size, epoch, dropout key, Adam step) is read from device memory.
+//
+//   k_bgemm       C (op)= epi(alpha * A.B^T) on v_mfma_f32_16x16x32_bf16 — 64x64 output tile per
+//                 256-thread workgroup (4 waves x 32x32), fp32 operands converted to bf16 while staged
+//                 into LDS, fp32 accumulate; fused epilogue: bias, activation (relu / erf-GELU),
+//                 pre-activation copy, dropout (hash mask), activation-derivative multiply (backward),
+//                 store / accumulate / atomic split-K accumulate.  Any strides: the same kernel runs
+//                 X.W^T (forward), dY.W (input grad) and dY^T.X (weight grad).
+//   k_colsum      bias gradients (column sums over rows)
+//   k_im2col3 / k_col2im3     Conv1d(k=3, pad=1) as GEMM over channels-last activations (+relu')
+//   k_pool4_*     AdaptiveAvgPool1d(4) (overlapping bins for L=7) + dropout, fwd/bwd (+relu')
+//   k_ln_*        residual-add + dropout + LayerNorm(64) fused fwd/bwd (16 lanes per row)
+//   k_gru_*       bidirectional GRU cell at seq_len 1 (h0 = 0 closed form), fwd/bwd
+//   k_bce / k_ce  sigmoid-BCE / softmax-CE mean loss + gradient + NaN abort (client.py:95-103)
+//   k_adam_clients   torch.optim.Adam over the [C][P] flat arena with per-client step counts
+//   k_conv_pe_*, k_mean_rows_*   HAR stem (Conv1d(1->64) + positional encoding) and mean-pool over L
+#include "common.h"
+#include "kernels.h"
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ uint32_t pk_bf2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){lo, hi}, b2v));
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_d(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  return cdf + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+__device__ __forceinline__ float act_f(float v, int act) {
+  return act == 1 ? fmaxf(v, 0.f) : (act == 2 ? gelu_f(v) : v);
+}
+__device__ __forceinline__ float act_d(float g, int gact) {
+  return gact == 1 ? (g > 0.f ? 1.f : 0.f) : (gact == 2 ? gelu_d(g) : 1.f);
+}
+__device__ __forceinline__ int cur_step(const int* stepctl) { return stepctl ? *stepctl : 0; }
+__device__ __forceinline__ uint32_t drop_key(const AflDrop& d, int c) {
+  return afl_hash32(d.seeds[c], (uint32_t)cur_step(d.stepctl));
+}
+__device__ __forceinline__ float drop_scale(const AflDrop& d, uint32_t key, uint32_t r, uint32_t col) {
+  return afl_keep(key, d.layer, r, col, d.thr16) ? d.inv_keep : 0.f;
+}
+
+// ============================================================================ batched GEMM
+constexpr int GT = 64, GK = 32, GLD = 40;  // output tile, k step, LDS row stride (bf16 elements)
+
+// Each thread stages 8 consecutive-k elements of one row of the A tile and of the B tile.  AK / BK
+// pick the thread->element map that keeps global reads coalesced: k-contiguous operands read 8
+// consecutive k per thread, m-contiguous ones (transposed views) read consecutive m across lanes.
+template <bool KC>
+__device__ __forceinline__ void stage_load(const float* __restrict__ X, long sr, long sk, int rows, int r0, int k0,
+                                           int ke, int tid, float (&v)[8]) {
+  const int r = KC ? r0 + (tid >> 2) : r0 + (tid & 63);
+  const int k = KC ? k0 + (tid & 3) * 8 : k0 + (tid >> 6) * 8;
+  const bool rok = r < rows;
+  const float* p = X + (long)r * sr;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (rok && k + j < ke) ? p[(long)(k + j) * sk] : 0.f;
+}
+template <bool KC>
+__device__ __forceinline__ void stage_store(unsigned short* S, int tid, const float (&v)[8]) {
+  const int r = KC ? (tid >> 2) : (tid & 63);
+  const int k = KC ? (tid & 3) * 8 : (tid >> 6) * 8;
+  u4v w;
+  w[0] = pk_bf2(v[0], v[1]);
+  w[1] = pk_bf2(v[2], v[3]);
+  w[2] = pk_bf2(v[4], v[5]);
+  w[3] = pk_bf2(v[6], v[7]);
+  *(u4v*)(S + r * GLD + k) = w;
+}
+__device__ __forceinline__ s8v frag(const unsigned short* S, int r0, int lane) {
+  return *(const s8v*)(S + (r0 + (lane & 15)) * GLD + 8 * (lane >> 4));
+}
+
+template <bool AK, bool BK>
+__global__ void __launch_bounds__(256) k_bgemm(AflGemm g) {
+  __shared__ __attribute__((aligned(16))) unsigned short As[GT * GLD];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[GT * GLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (g.N + GT - 1) / GT;
+  const int m0 = (blockIdx.x / tiles_n) * GT, n0 = (blockIdx.x % tiles_n) * GT;
+  const int c = blockIdx.z;
+  const int kchunk = ((g.K + g.splitk - 1) / g.splitk + GK - 1) / GK * GK;
+  const int kb = blockIdx.y * kchunk, ke = min(g.K, kb + kchunk);
+  if (kb >= ke) return;
+  const float* A = g.A + (long)c * g.sAc;
+  const float* B = g.B + (long)c * g.sBc;
+
+  f4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  float ra[8], rb[8];
+  stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, kb, ke, tid, ra);
+  stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, kb, ke, tid, rb);
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    stage_store<AK>(As, tid, ra);
+    stage_store<BK>(Bs, tid, rb);
+    __syncthreads();
+    if (k0 + GK < ke) {  // next tile's global loads overlap this tile's MFMAs
+      stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, k0 + GK, ke, tid, ra);
+      stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, k0 + GK, ke, tid, rb);
+    }
+    const s8v a0 = frag(As, wm, lane), a1 = frag(As, wm + 16, lane);
+    const s8v b0 = frag(Bs, wn, lane), b1 = frag(Bs, wn + 16, lane);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a0), __builtin_bit_cast(bf8v, b0),
+                                                        acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a0), __builtin_bit_cast(bf8v, b1),
+                                                        acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a1), __builtin_bit_cast(bf8v, b0),
+                                                        acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a1), __builtin_bit_cast(bf8v, b1),
+                                                        acc[1][1], 0, 0, 0);
+    __syncthreads();
+  }
+  // epilogue: lane holds C[4*(lane>>4)+e][lane&15] of each 16x16 tile
+  const bool dr = g.drop.thr16 != 0;
+  const uint32_t key = dr ? drop_key(g.drop, c) : 0u;
+  float* Cc = g.Cm + (long)c * g.sCc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+        const int n = n0 + wn + 16 * j + (lane & 15);
+        if (m >= g.M || n >= g.N) continue;
+        float v = g.alpha * acc[i][j][e];
+        if (g.bias) v += g.bias[(long)c * g.sbc + n];
+        const long off = (long)m * g.sCm + (long)n * g.sCn;
+        if (g.Z) g.Z[(long)c * g.sCc + off] = v;
+        v = act_f(v, g.act);
+        if (dr) v *= drop_scale(g.drop, key, m, n);
+        if (g.G) v *= act_d(g.G[(long)c * g.sGc + (long)m * g.sGm + (long)n * g.sGn], g.gact);
+        if (g.accum == 0)
+          Cc[off] = v;
+        else if (g.accum == 1)
+          Cc[off] += v;
+        else
+          atomicAdd(Cc + off, v);
+      }
+}
+
+// ============================================================================ column sums
+__global__ void __launch_bounds__(256) k_colsum(const float* __restrict__ Y, long sYc, long sYm, int M, int N,
+                                                float* __restrict__ out, long sOc) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.z, col = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * 256;
+  float s = 0.f;
+  if (col < N) {
+    const float* p = Y + (long)c * sYc + col;
+    for (int r = r0 + rg; r < min(M, r0 + 256); r += 4) s += p[(long)r * sYm];
+  }
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && col < N) {
+    s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + (long)c * sOc + col, s);
+  }
+}
+
+// ============================================================================ batch gathers
+__global__ void k_gather_icu(const float* __restrict__ rows, const int* __restrict__ idx, const int* stepctl, int C,
+                             int B, int mask, float* __restrict__ vit, float* __restrict__ lab, float* __restrict__ y) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= C * B * 24) return;
+  const int f = t % 24, cb = t / 24;
+  const int r = idx[(long)cur_step(stepctl) * C * B + cb];
+  float v = r >= 0 ? rows[(long)r * 24 + f] : 0.f;
+  if (mask && f < 23 && v == -2.0f) v = 0.f;  // RNNModel masking (src/Model.py:121-122)
+  if (f < 7)
+    vit[(long)cb * 7 + f] = v;
+  else if (f < 23)
+    lab[(long)cb * 16 + f - 7] = v;
+  else
+    y[cb] = v;
+}
+
+__global__ void k_gather_har(const float* __restrict__ x, const long* __restrict__ y, int F,
+                             const int* __restrict__ idx, const int* stepctl, int C, int B, float* __restrict__ ox,
+                             long* __restrict__ oy) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)C * B * F) return;
+  const int f = (int)(t % F);
+  const long cb = t / F;
+  const int r = idx[(long)cur_step(stepctl) * C * B + cb];
+  ox[t] = r >= 0 ? x[(long)r * F + f] : 0.f;
+  if (f == 0) oy[cb] = r >= 0 ? y[r] : 0;
+}
+
+// ============================================================================ conv1d k=3 pad=1
+__global__ void k_im2col3(const float* __restrict__ x, long sXc, long sXr, int C, int B, int L, int Cin,
+                          float* __restrict__ out) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = 3 * Cin;
+  if (t >= (long)C * B * L * K) return;
+  const int k = (int)(t % K);
+  const long row = (t / K) % ((long)B * L);
+  const int c = (int)(t / ((long)K * B * L));
+  const int ci = k / 3, j = k % 3;
+  const int l = (int)(row % L) + j - 1;
+  out[t] = (l >= 0 && l < L) ? x[(long)c * sXc + (row - (row % L) + l) * sXr + ci] : 0.f;
+}
+
+__global__ void k_col2im3(const float* __restrict__ dcols, int C, int B, int L, int Cin,
+                          const float* __restrict__ relu_src, long sRc, long sRr, float* __restrict__ dx) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)C * B * L * Cin) return;
+  const int ci = (int)(t % Cin);
+  const long row = (t / Cin) % ((long)B * L);
+  const int c = (int)(t / ((long)Cin * B * L));
+  const int l = (int)(row % L);
+  const float* d = dcols + (long)c * B * L * 3 * Cin;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int lo = l - j + 1;  // output position whose tap j reads input l
+    if (lo >= 0 && lo < L) s += d[(row - l + lo) * 3 * Cin + ci * 3 + j];
+  }
+  if (relu_src && !(relu_src[(long)c * sRc + row * sRr + ci] > 0.f)) s = 0.f;
+  dx[t] = s;
+}
+
+// ============================================================================ AdaptiveAvgPool1d(4)
+__device__ __forceinline__ int bin_lo(int p, int L) { return (p * L) / 4; }
+__device__ __forceinline__ int bin_hi(int p, int L) { return ((p + 1) * L + 3) / 4; }
+
+__global__ void k_pool4_fwd(const float* __restrict__ h, int C, int B, int L, int Ch, float* __restrict__ out,
+                            long sOc, long sOr, int col0, AflDrop d) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)C * B * Ch * 4) return;
+  const int p = (int)(t & 3), ch = (int)((t >> 2) % Ch);
+  const int b = (int)((t / (4L * Ch)) % B), c = (int)(t / (4L * Ch * B));
+  const int lo = bin_lo(p, L), hi = bin_hi(p, L);
+  const float* src = h + ((long)c * B * L + (long)b * L) * Ch + ch;
+  float s = 0.f;
+  for (int l = lo; l < hi; ++l) s += src[(long)l * Ch];
+  s /= (float)(hi - lo);
+  const int col = col0 + ch * 4 + p;
+  if (d.thr16) s *= drop_scale(d, drop_key(d, c), b, col);
+  out[(long)c * sOc + (long)b * sOr + col] = s;
+}
+
+__global__ void k_pool4_bwd(const float* __restrict__ dout, long sOc, long sOr, int col0, const float* __restrict__ h,
+                            int C, int B, int L, int Ch, float* __restrict__ dh, AflDrop d) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)C * B * L * Ch) return;
+  const int ch = (int)(t % Ch), l = (int)((t / Ch) % L);
+  const int b = (int)((t / ((long)Ch * L)) % B), c = (int)(t / ((long)Ch * L * B));
+  const uint32_t key = d.thr16 ? drop_key(d, c) : 0u;
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int lo = bin_lo(p, L), hi = bin_hi(p, L);
+    if (l >= lo && l < hi) {
+      const int col = col0 + ch * 4 + p;
+      float g = dout[(long)c * sOc + (long)b * sOr + col] / (float)(hi - lo);
+      if (d.thr16) g *= drop_scale(d, key, b, col);
+      s += g;
+    }
+  }
+  if (!(h[t] > 0.f)) s = 0.f;  // relu' of the conv3 output
+  dh[t] = s;
+}
+
+// ============================================================================ LayerNorm(64)
+// 16 lanes per row, 4 columns per lane; 16 rows per 256-thread block (fwd).
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_ln_fwd(AflLn l) {
+  const int c = blockIdx.y;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (row >= l.rows) return;
+  const int c0 = (threadIdx.x & 15) * 4;
+  const uint32_t ka = l.da.thr16 ? drop_key(l.da, c) : 0u;
+  const uint32_t ko = l.dout.thr16 ? drop_key(l.dout, c) : 0u;
+  float s[4];
+  const float* xp = l.x + (long)c * l.sXc + (long)row * l.sXr + c0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s[j] = xp[j];
+  if (l.a) {
+    const float* ap = l.a + (long)c * l.sAc + (long)row * l.sAr + c0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = ap[j];
+      if (l.da.thr16) a *= drop_scale(l.da, ka, row, c0 + j);
+      s[j] += a;
+    }
+  }
+  if (l.s) {
+    float* sp = l.s + ((long)c * l.rows + row) * 64 + c0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sp[j] = s[j];
+  }
+  const float mean = sum16(s[0] + s[1] + s[2] + s[3]) * (1.f / 64.f);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q += (s[j] - mean) * (s[j] - mean);
+  const float rstd = rsqrtf(sum16(q) * (1.f / 64.f) + 1e-5f);
+  const float* gm = l.gamma + (long)c * l.sPc;
+  const float* bt = l.beta + (long)c * l.sPc;
+  float* yp = l.y + (long)c * l.sYc + (long)row * l.sYr + c0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float y = (s[j] - mean) * rstd * gm[c0 + j] + bt[c0 + j];
+    if (l.dout.thr16) y *= drop_scale(l.dout, ko, row, c0 + j);
+    yp[j] = y;
+  }
+  if ((threadIdx.x & 15) == 0) {
+    float* st = l.stats + ((long)c * l.rows + row) * 2;
+    st[0] = mean;
+    st[1] = rstd;
+  }
+}
+
+constexpr int LNB_ROWS = 256;  // rows per backward block (dgamma/dbeta partials -> 128 atomics)
+
+__global__ void __launch_bounds__(256) k_ln_bwd(AflLnB l) {
+  __shared__ float red[16][129];
+  const int c = blockIdx.y, li = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c0 = li * 4;
+  const uint32_t ka = l.da_drop.thr16 ? drop_key(l.da_drop, c) : 0u;
+  const uint32_t ko = l.dout.thr16 ? drop_key(l.dout, c) : 0u;
+  const float* gm = l.gamma + (long)c * l.sPc;
+  float gam[4], dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) gam[j] = gm[c0 + j];
+  const int rbeg = blockIdx.x * LNB_ROWS;
+  for (int row = rbeg + rg; row < min(l.rows, rbeg + LNB_ROWS); row += 16) {
+    const float* st = l.stats + ((long)c * l.rows + row) * 2;
+    const float mean = st[0], rstd = st[1];
+    const float* dyp = l.dy + (long)c * l.sDc + (long)row * l.sDr + c0;
+    const float* sp = l.s + (long)c * l.sSc + (long)row * l.sSr + c0;
+    float g[4], xh[4], a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g[j] = dyp[j];
+      if (l.dout.thr16) g[j] *= drop_scale(l.dout, ko, row, c0 + j);
+      xh[j] = (sp[j] - mean) * rstd;
+      dg[j] += g[j] * xh[j];
+      db[j] += g[j];
+      const float dxh = g[j] * gam[j];
+      a1 += dxh;
+      a2 += dxh * xh[j];
+    }
+    a1 = sum16(a1) * (1.f / 64.f);
+    a2 = sum16(a2) * (1.f / 64.f);
+    float* dxp = l.dx + (long)c * l.sXc + (long)row * l.sXr + c0;
+    float* dap = l.da ? l.da + (long)c * l.sAc + (long)row * l.sAr + c0 : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float dx = rstd * (g[j] * gam[j] - a1 - xh[j] * a2);
+      if (l.dx_accum)
+        dxp[j] += dx;
+      else
+        dxp[j] = dx;
+      if (dap) dap[j] = l.da_drop.thr16 ? dx * drop_scale(l.da_drop, ka, row, c0 + j) : dx;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[rg][c0 + j] = dg[j];
+    red[rg][64 + c0 + j] = db[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += red[r][threadIdx.x];
+    float* dst = threadIdx.x < 64 ? l.dgamma + (long)c * l.sPc + threadIdx.x
+                                  : l.dbeta + (long)c * l.sPc + threadIdx.x - 64;
+    atomicAdd(dst, s);
+  }
+}
+
+// ============================================================================ GRU cell, seq_len 1, h0 = 0
+// PyTorch gate order (r, z, n): r = s(gi_r + bhh_r), z = s(gi_z + bhh_z), n = tanh(gi_n + r * bhh_n),
+// h = (1 - z) * n.  gi already holds x.W_ih^T + b_ih.  W_hh receives an exactly-zero gradient.
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__global__ void k_gru_fwd(const float* __restrict__ gi, const float* __restrict__ bhh, long sPc, int C, int B,
+                          float* __restrict__ h, long sHc, long sHr, int col0) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= C * B * 32) return;
+  const int j = t & 31, b = (t >> 5) % B, c = t / (32 * B);
+  const float* g = gi + ((long)c * B + b) * 96;
+  const float* bh = bhh + (long)c * sPc;
+  const float r = sigm(g[j] + bh[j]);
+  const float z = sigm(g[32 + j] + bh[32 + j]);
+  const float n = tanhf(g[64 + j] + r * bh[64 + j]);
+  h[(long)c * sHc + (long)b * sHr + col0 + j] = (1.f - z) * n;
+}
+
+__global__ void __launch_bounds__(256) k_gru_bwd(const float* __restrict__ dh, long sHc, long sHr, int col0,
+                                                 const float* __restrict__ gi, const float* __restrict__ bhh, long sPc,
+                                                 int B, float* __restrict__ dgi, float* __restrict__ dbih,
+                                                 float* __restrict__ dbhh) {
+  __shared__ float red[8][32][5];
+  const int c = blockIdx.x, j = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const float* bh = bhh + (long)c * sPc;
+  const float bhr = bh[j], bhz = bh[32 + j], bhn = bh[64 + j];
+  float sr = 0.f, sz = 0.f, sn = 0.f, snh = 0.f;
+  for (int b = rg; b < B; b += 8) {
+    const float* g = gi + ((long)c * B + b) * 96;
+    const float r = sigm(g[j] + bhr);
+    const float z = sigm(g[32 + j] + bhz);
+    const float n = tanhf(g[64 + j] + r * bhn);
+    const float d = dh[(long)c * sHc + (long)b * sHr + col0 + j];
+    const float dan = d * (1.f - z) * (1.f - n * n);
+    const float dar = dan * bhn * r * (1.f - r);
+    const float daz = -d * n * z * (1.f - z);
+    float* o = dgi + ((long)c * B + b) * 96;
+    o[j] = dar;
+    o[32 + j] = daz;
+    o[64 + j] = dan;
+    sr += dar;
+    sz += daz;
+    sn += dan;
+    snh += dan * r;
+  }
+  red[rg][j][0] = sr;
+  red[rg][j][1] = sz;
+  red[rg][j][2] = sn;
+  red[rg][j][3] = snh;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float a = 0.f, bz = 0.f, n = 0.f, nh = 0.f;
+    for (int r = 0; r < 8; ++r) {
+      a += red[r][j][0];
+      bz += red[r][j][1];
+      n += red[r][j][2];
+      nh += red[r][j][3];
+    }
+    float* bi = dbih + (long)c * sPc;
+    float* bhg = dbhh + (long)c * sPc;
+    bi[j] = a;
+    bi[32 + j] = bz;
+    bi[64 + j] = n;
+    bhg[j] = a;
+    bhg[32 + j] = bz;
+    bhg[64 + j] = nh;
+  }
+}
+
+// ============================================================================ losses
+// Per client: rows b < bsz of the current step are real; bsz < 2 (size-1 batch skip A-21, or past
+// the client's last batch) or a previous NaN -> no loss, zero gradient, no Adam update this step.
+__device__ __forceinline__ bool step_active(const int* bsz, const int* stepctl, int C, int S, const int* failed,
+                                            int c, int* bs_out) {
+  const int s = cur_step(stepctl);
+  const int bs = s < S ? bsz[(long)s * C + c] : 0;
+  *bs_out = bs;
+  return bs >= 2 && failed[c] == 0;
+}
+
+__global__ void __launch_bounds__(256) k_bce(const float* __restrict__ z, const float* __restrict__ y,
+                                             const int* bsz, const int* epoch, const int* nb, const int* stepctl,
+                                             int C, int B, int S, int* failed, float* losses, int E,
+                                             float* __restrict__ dz) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  int bs;
+  const bool act = step_active(bsz, stepctl, C, S, failed, c, &bs);
+  float l = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    if (act && b < bs) {
+      const float p = 1.f / (1.f + expf(-z[(long)c * B + b]));
+      const float t = y[(long)c * B + b];
+      l -= t * fmaxf(logf(p), -100.f) + (1.f - t) * fmaxf(log1pf(-p), -100.f);
+      if (p != p) l = p;  // keep NaN (fmaxf would swallow it)
+    }
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+  __syncthreads();
+  const float loss = (red[0] + red[1] + red[2] + red[3]) / (float)max(bs, 1);
+  const bool nan = act && (loss != loss);
+  for (int b = threadIdx.x; b < B; b += 256) {
+    float g = 0.f;
+    if (act && !nan && b < bs) {
+      // torch: BCE'(p) = (p - t) / max(p (1 - p), 1e-12), times sigmoid'(z) = p (1 - p)
+      const float p = 1.f / (1.f + expf(-z[(long)c * B + b]));
+      const float w = p * (1.f - p);
+      g = (p - y[(long)c * B + b]) / fmaxf(w, 1e-12f) * w / (float)bs;
+    }
+    dz[(long)c * B + b] = g;
+  }
+  if (threadIdx.x == 0 && act) {
+    if (nan)
+      failed[c] = 1;
+    else
+      losses[(long)c * E + epoch[(long)cur_step(stepctl) * C + c]] += loss / (float)nb[c];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_ce(const float* __restrict__ logits, const long* __restrict__ y, int K,
+                                            const int* bsz, const int* epoch, const int* nb, const int* stepctl, int C,
+                                            int B, int S, int* failed, float* losses, int E, float* __restrict__ dz) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  int bs;
+  const bool act = step_active(bsz, stepctl, C, S, failed, c, &bs);
+  float l = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    if (act && b < bs) {
+      const float* x = logits + ((long)c * B + b) * K;
+      float mx = x[0];
+      for (int k = 1; k < K; ++k) mx = fmaxf(mx, x[k]);
+      float se = 0.f;
+      for (int k = 0; k < K; ++k) se += expf(x[k] - mx);
+      l += logf(se) + mx - x[y[(long)c * B + b]];
+      if (x[0] != x[0]) l = x[0];
+    }
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+  __syncthreads();
+  const float loss = (red[0] + red[1] + red[2] + red[3]) / (float)max(bs, 1);
+  const bool nan = act && (loss != loss);
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float* x = logits + ((long)c * B + b) * K;
+    float* d = dz + ((long)c * B + b) * K;
+    if (act && !nan && b < bs) {
+      float mx = x[0];
+      for (int k = 1; k < K; ++k) mx = fmaxf(mx, x[k]);
+      float se = 0.f;
+      for (int k = 0; k < K; ++k) se += expf(x[k] - mx);
+      const long t = y[(long)c * B + b];
+      for (int k = 0; k < K; ++k) d[k] = (expf(x[k] - mx) / se - (k == t ? 1.f : 0.f)) / (float)bs;
+    } else {
+      for (int k = 0; k < K; ++k) d[k] = 0.f;
+    }
+  }
+  if (threadIdx.x == 0 && act) {
+    if (nan)
+      failed[c] = 1;
+    else
+      losses[(long)c * E + epoch[(long)cur_step(stepctl) * C + c]] += loss / (float)nb[c];
+  }
+}
+
+// ============================================================================ optimizer
+__global__ void __launch_bounds__(256) k_adam_clients(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v, long P,
+                                                      const int* tcount, const int* bsz, const int* stepctl, int C,
+                                                      int S, const int* failed, float lr, long skip_lo, long skip_hi,
+                                                      float sgd_lr) {
+  const int c = blockIdx.y;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  int bs;
+  if (i >= P || !step_active(bsz, stepctl, C, S, failed, c, &bs)) return;
+  if (i >= skip_lo && i < skip_hi) return;  // buffers (e.g. the positional-encoding table)
+  const long k = (long)c * P + i;
+  const float gi = g[k];
+  if (sgd_lr > 0.f) {
+    p[k] -= sgd_lr * gi;
+    return;
+  }
+  const float t = (float)(tcount[c] + 1);
+  const float bc1 = 1.f - powf(0.9f, t), bc2 = 1.f - powf(0.999f, t);
+  const float mi = m[k] + 0.1f * (gi - m[k]);
+  const float vi = 0.999f * v[k] + 0.001f * gi * gi;
+  m[k] = mi;
+  v[k] = vi;
+  p[k] -= (lr / bc1) * mi / (sqrtf(vi) / sqrtf(bc2) + 1e-8f);
+}
+
+__global__ void k_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, int C, int S) {
+  const int c = threadIdx.x;
+  int bs;
+  const bool act = c < C && step_active(bsz, stepctl, C, S, failed, c, &bs);
+  __syncthreads();
+  if (act) tcount[c] += 1;
+  __syncthreads();
+  if (threadIdx.x == 0) stepctl[0] += 1;
+}
+
+// ============================================================================ HAR stem and pooling
+// h[c][b*L+l][o] = conv_b[o] + sum_j conv_w[o][j] x[c][b][l+j-1] + pe[l][o]   (src/Model.py:431-452)
+__global__ void k_conv_pe_fwd(const float* __restrict__ x, int C, int B, int L, const float* __restrict__ params,
+                              long P, int w_off, int b_off, int pe_off, float* __restrict__ h) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)C * B * L * 64) return;
+  const int o = (int)(t & 63);
+  const long row = t >> 6;
+  const int l = (int)(row % L), b = (int)((row / L) % B), c = (int)(row / ((long)L * B));
+  const float* pp = params + (long)c * P;
+  const float* xr = x + ((long)c * B + b) * L;
+  float s = pp[b_off + o] + pp[pe_off + l * 64 + o];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int li = l + j - 1;
+    if (li >= 0 && li < L) s += pp[w_off + o * 3 + j] * xr[li];
+  }
+  h[t] = s;
+}
+
+__global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x, const float* __restrict__ dh,
+                                                     int C, int B, int L, float* __restrict__ grads, long P,
+                                                     int w_off, int b_off) {
+  __shared__ float red[4][64][4];
+  const int c = blockIdx.y, o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const long nrows = (long)B * L, r0 = (long)blockIdx.x * 1024;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
+  for (long row = r0 + rg; row < min(nrows, r0 + 1024); row += 4) {
+    const int l = (int)(row % L);
+    const float* xr = x + (long)c * nrows + (row - l);
+    const float d = dh[((long)c * nrows + row) * 64 + o];
+    ab += d;
+    if (l >= 1) a0 += d * xr[l - 1];
+    a1 += d * xr[l];
+    if (l + 1 < L) a2 += d * xr[l + 1];
+  }
+  red[rg][o][0] = a0;
+  red[rg][o][1] = a1;
+  red[rg][o][2] = a2;
+  red[rg][o][3] = ab;
+  __syncthreads();
+  if (rg == 0) {
+    float s[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = red[0][o][q] + red[1][o][q] + red[2][o][q] + red[3][o][q];
+    float* gp = grads + (long)c * P;
+    atomicAdd(gp + w_off + o * 3 + 0, s[0]);
+    atomicAdd(gp + w_off + o * 3 + 1, s[1]);
+    atomicAdd(gp + w_off + o * 3 + 2, s[2]);
+    atomicAdd(gp + b_off + o, s[3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_mean_rows_fwd(const float* __restrict__ h, int L, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const long cb = blockIdx.x;  // c * B + b
+  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const float* src = h + cb * L * 64 + o;
+  float s = 0.f;
+  for (int l = rg; l < L; l += 4) s += src[(long)l * 64];
+  red[rg][o] = s;
+  __syncthreads();
+  if (rg == 0) out[cb * 64 + o] = (red[0][o] + red[1][o] + red[2][o] + red[3][o]) / (float)L;
+}
+
+__global__ void k_mean_rows_bwd(const float* __restrict__ dout, long n, int L, float* __restrict__ dh) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int o = (int)(t & 63);
+  const long cb = (t >> 6) / L;
+  dh[t] = dout[cb * 64 + o] / (float)L;
+}
+
+inline int launched() { return (int)hipGetLastError(); }
+inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+// ============================================================================ host launchers
+int afl_bgemm(const AflGemm& g, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
+  if (g.splitk > 1 && g.accum != 2) return (int)hipErrorInvalidValue;
+  const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
+  dim3 grid(tiles, max(1, g.splitk), g.nC);
+  const bool ak = g.sAk == 1, bk = g.sBk == 1;
+  if (ak && bk)
+    hipLaunchKernelGGL((k_bgemm<true, true>), grid, dim3(256), 0, s, g);
+  else if (ak)
+    hipLaunchKernelGGL((k_bgemm<true, false>), grid, dim3(256), 0, s, g);
+  else if (bk)
+    hipLaunchKernelGGL((k_bgemm<false, true>), grid, dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_bgemm<false, false>), grid, dim3(256), 0, s, g);
+  return launched();
+}
+
+int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s) {
+  hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64, (M + 255) / 256, nC), dim3(256), 0, s, Y, sYc, sYm, M, N, out, sOc);
+  return launched();
+}
+
+int afl_gather_icu(const float* rows, const int* idx, const int* stepctl, int C, int B, int mask, float* vit,
+                   float* lab, float* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_icu, dim3(nb256((long)C * B * 24)), dim3(256), 0, s, rows, idx, stepctl, C, B, mask, vit,
+                     lab, y);
+  return launched();
+}
+
+int afl_gather_har(const float* x, const long* y, int F, const int* idx, const int* stepctl, int C, int B, float* ox,
+                   long* oy, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_har, dim3(nb256((long)C * B * F)), dim3(256), 0, s, x, y, F, idx, stepctl, C, B, ox, oy);
+  return launched();
+}
+
+int afl_im2col3(const float* x, long sXc, long sXr, int C, int B, int L, int Cin, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_im2col3, dim3(nb256((long)C * B * L * 3 * Cin)), dim3(256), 0, s, x, sXc, sXr, C, B, L, Cin,
+                     out);
+  return launched();
+}
+
+int afl_col2im3(const float* dcols, int C, int B, int L, int Cin, const float* relu_src, long sRc, long sRr, float* dx,
+                hipStream_t s) {
+  hipLaunchKernelGGL(k_col2im3, dim3(nb256((long)C * B * L * Cin)), dim3(256), 0, s, dcols, C, B, L, Cin, relu_src,
+                     sRc, sRr, dx);
+  return launched();
+}
+
+int afl_pool4_fwd(const float* h, int C, int B, int L, int Ch, float* out, long sOc, long sOr, int col0, AflDrop d,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_pool4_fwd, dim3(nb256((long)C * B * Ch * 4)), dim3(256), 0, s, h, C, B, L, Ch, out, sOc, sOr,
+                     col0, d);
+  return launched();
+}
+
+int afl_pool4_bwd(const float* dout, long sOc, long sOr, int col0, const float* h, int C, int B, int L, int Ch,
+                  float* dh, AflDrop d, hipStream_t s) {
+  hipLaunchKernelGGL(k_pool4_bwd, dim3(nb256((long)C * B * L * Ch)), dim3(256), 0, s, dout, sOc, sOr, col0, h, C, B, L,
+                     Ch, dh, d);
+  return launched();
+}
+
+int afl_ln_fwd(const AflLn& l, hipStream_t s) {
+  hipLaunchKernelGGL(k_ln_fwd, dim3((l.rows + 15) / 16, l.nC), dim3(256), 0, s, l);
+  return launched();
+}
+
+int afl_ln_bwd(const AflLnB& l, hipStream_t s) {
+  hipLaunchKernelGGL(k_ln_bwd, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
+  return launched();
+}
+
+int afl_gru_fwd(const float* gi, const float* bhh, long sPc, int C, int B, float* h, long sHc, long sHr, int col0,
+                hipStream_t s) {
+  hipLaunchKernelGGL(k_gru_fwd, dim3(nb256((long)C * B * 32)), dim3(256), 0, s, gi, bhh, sPc, C, B, h, sHc, sHr, col0);
+  return launched();
+}
+
+int afl_gru_bwd(const float* dh, long sHc, long sHr, int col0, const float* gi, const float* bhh, long sPc, int C,
+                int B, float* dgi, float* dbih, float* dbhh, hipStream_t s) {
+  hipLaunchKernelGGL(k_gru_bwd, dim3(C), dim3(256), 0, s, dh, sHc, sHr, col0, gi, bhh, sPc, B, dgi, dbih, dbhh);
+  return launched();
+}
+
+int afl_bce(const float* z, const float* y, const int* bsz, const int* epoch, const int* nb, const int* stepctl, int C,
+            int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s) {
+  hipLaunchKernelGGL(k_bce, dim3(C), dim3(256), 0, s, z, y, bsz, epoch, nb, stepctl, C, B, S, failed, losses, E, dz);
+  return launched();
+}
+
+int afl_ce(const float* logits, const long* y, int K, const int* bsz, const int* epoch, const int* nb,
+           const int* stepctl, int C, int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s) {
+  hipLaunchKernelGGL(k_ce, dim3(C), dim3(256), 0, s, logits, y, K, bsz, epoch, nb, stepctl, C, B, S, failed, losses, E,
+                     dz);
+  return launched();
+}
+
+int afl_adam_clients(float* p, const float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
+                     const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi, float sgd_lr,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_adam_clients, dim3(nb256(P), C), dim3(256), 0, s, p, g, m, v, P, tcount, bsz, stepctl, C, S,
+                     failed, lr, skip_lo, skip_hi, sgd_lr);
+  return launched();
+}
+
+int afl_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, int C, int S, hipStream_t s) {
+  if (C > 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_step_end, dim3(1), dim3(max(64, (C + 63) / 64 * 64)), 0, s, stepctl, tcount, bsz, failed, C, S);
+  return launched();
+}
+
+int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,
+                    float* h, hipStream_t s) {
+  hipLaunchKernelGGL(k_conv_pe_fwd, dim3(nb256((long)C * B * L * 64)), dim3(256), 0, s, x, C, B, L, params, P, w_off,
+                     b_off, pe_off, h);
+  return launched();
+}
+
+int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float* grads, long P, int w_off, int b_off,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_conv_pe_bwd, dim3((unsigned)(((long)B * L + 1023) / 1024), C), dim3(256), 0, s, x, dh, C, B, L,
+                     grads, P, w_off, b_off);
+  return launched();
+}
+
+int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_mean_rows_fwd, dim3(C * B), dim3(256), 0, s, h, L, out);
+  return launched();
+}
+
+int afl_mean_rows_bwd(const float* dout, int C, int B, int L, float* dh, hipStream_t s) {
+  const long n = (long)C * B * L * 64;
+  hipLaunchKernelGGL(k_mean_rows_bwd, dim3(nb256(n)), dim3(256), 0, s, dout, n, L, dh);
+  return launched();
+}

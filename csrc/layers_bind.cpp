@@ -1,0 +1,430 @@
+// torch bindings of the client-batched layer kernels (layers.hip, attention.hip).
+// Every op writes into caller-provided tensors (no allocation): the per-model step programs
+// (attackfl_amd/fl/programs.py) preallocate their buffers once and capture the launch sequence in a
+// HIP graph.  Strided operands are passed as 3-D views [C][rows][cols]; their strides go to the
+// kernels unchanged (weights are views into the flat [C][P] parameter arena, transposes are free).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <cmath>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
+
+void ok(int e, const char* what) {
+  TORCH_CHECK(e == 0, what, " launch failed: ", hipGetErrorString((hipError_t)e));
+}
+
+void dev(const torch::Tensor& t, const char* n, c10::ScalarType dt = torch::kFloat32) {
+  TORCH_CHECK(t.defined() && t.is_cuda(), n, " must be a device tensor");
+  TORCH_CHECK(t.scalar_type() == dt, n, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+void dense(const torch::Tensor& t, const char* n, c10::ScalarType dt = torch::kFloat32) {
+  dev(t, n, dt);
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+}
+void view3(const torch::Tensor& t, const char* n) {
+  dev(t, n);
+  TORCH_CHECK(t.dim() == 3, n, " must be a 3-D [C, rows, cols] view");
+}
+const float* optp(const c10::optional<torch::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+AflDrop make_drop(const c10::optional<torch::Tensor>& seeds, const c10::optional<torch::Tensor>& stepctl,
+                  int64_t layer, double p) {
+  AflDrop d{};
+  if (p <= 0.0) return d;
+  TORCH_CHECK(seeds.has_value() && seeds->defined(), "dropout needs client seeds");
+  dense(*seeds, "seeds", torch::kInt32);
+  d.seeds = (const uint32_t*)seeds->data_ptr<int>();
+  if (stepctl.has_value() && stepctl->defined()) {
+    dense(*stepctl, "stepctl", torch::kInt32);
+    d.stepctl = stepctl->data_ptr<int>();
+  }
+  d.layer = (uint32_t)layer;
+  d.thr16 = (uint32_t)std::lround(p * 65536.0);
+  d.inv_keep = (float)(1.0 / (1.0 - p));
+  return d;
+}
+
+// C (op)= epi(alpha * A . B^T): A [C, M, K], B [C, N, K], C [C, M, N] (any strides)
+void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<torch::Tensor> bias,
+           c10::optional<torch::Tensor> Z, c10::optional<torch::Tensor> G, int64_t act, int64_t gact, int64_t accum,
+           int64_t splitk, double alpha, c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl,
+           int64_t layer, double p) {
+  view3(A, "A");
+  view3(B, "B");
+  view3(Cm, "C");
+  const long nC = A.size(0), M = A.size(1), K = A.size(2), N = B.size(1);
+  TORCH_CHECK(B.size(0) == nC && B.size(2) == K, "B must be [C, N, K]");
+  TORCH_CHECK(Cm.size(0) == nC && Cm.size(1) == M && Cm.size(2) == N, "C must be [C, M, N]");
+  AflGemm g{};
+  g.A = A.data_ptr<float>();
+  g.sAc = A.stride(0); g.sAm = A.stride(1); g.sAk = A.stride(2);
+  g.B = B.data_ptr<float>();
+  g.sBc = B.stride(0); g.sBn = B.stride(1); g.sBk = B.stride(2);
+  g.Cm = Cm.data_ptr<float>();
+  g.sCc = Cm.stride(0); g.sCm = Cm.stride(1); g.sCn = Cm.stride(2);
+  if (bias.has_value() && bias->defined()) {
+    dev(*bias, "bias");
+    TORCH_CHECK(bias->dim() == 2 && bias->size(0) == nC && bias->size(1) == N && bias->stride(1) == 1,
+                "bias must be a [C, N] view with unit column stride");
+    g.bias = bias->data_ptr<float>();
+    g.sbc = bias->stride(0);
+  }
+  if (Z.has_value() && Z->defined()) {
+    view3(*Z, "Z");
+    TORCH_CHECK(Z->sizes() == Cm.sizes() && Z->strides() == Cm.strides(), "Z must match C's shape and strides");
+    g.Z = Z->data_ptr<float>();
+  }
+  if (G.has_value() && G->defined()) {
+    view3(*G, "G");
+    TORCH_CHECK(G->size(0) == nC && G->size(1) == M && G->size(2) == N, "G must be [C, M, N]");
+    g.G = G->data_ptr<float>();
+    g.sGc = G->stride(0); g.sGm = G->stride(1); g.sGn = G->stride(2);
+  }
+  g.M = M; g.N = N; g.K = K; g.nC = nC;
+  g.act = act; g.gact = gact; g.accum = accum; g.splitk = std::max<int64_t>(1, splitk);
+  g.alpha = (float)alpha;
+  g.drop = make_drop(seeds, stepctl, layer, p);
+  ok(afl_bgemm(g, cur()), "bgemm");
+}
+
+void colsum(torch::Tensor Y, torch::Tensor out) {
+  view3(Y, "Y");
+  dev(out, "out");
+  TORCH_CHECK(Y.stride(2) == 1, "Y columns must be contiguous");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == Y.size(0) && out.size(1) == Y.size(2) && out.stride(1) == 1,
+              "out must be a [C, N] view");
+  ok(afl_colsum(Y.data_ptr<float>(), Y.stride(0), Y.stride(1), Y.size(1), Y.size(2), Y.size(0), out.data_ptr<float>(),
+                out.stride(0), cur()),
+     "colsum");
+}
+
+void gather_icu(torch::Tensor rows, torch::Tensor idx, torch::Tensor stepctl, int64_t mask, torch::Tensor vit,
+                torch::Tensor lab, torch::Tensor y) {
+  dense(rows, "rows");
+  dense(idx, "idx", torch::kInt32);
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(vit, "vit");
+  dense(lab, "lab");
+  dense(y, "y");
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 24 && idx.dim() == 3, "rows [N, 24], idx [S, C, B]");
+  const int C = idx.size(1), B = idx.size(2);
+  TORCH_CHECK(vit.numel() == (long)C * B * 7 && lab.numel() == (long)C * B * 16 && y.numel() == (long)C * B,
+              "output sizes");
+  ok(afl_gather_icu(rows.data_ptr<float>(), idx.data_ptr<int>(), stepctl.data_ptr<int>(), C, B, (int)mask,
+                    vit.data_ptr<float>(), lab.data_ptr<float>(), y.data_ptr<float>(), cur()),
+     "gather_icu");
+}
+
+void gather_har(torch::Tensor x, torch::Tensor y, torch::Tensor idx, torch::Tensor stepctl, torch::Tensor ox,
+                torch::Tensor oy) {
+  dense(x, "x");
+  dense(y, "y", torch::kInt64);
+  dense(idx, "idx", torch::kInt32);
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(ox, "ox");
+  dense(oy, "oy", torch::kInt64);
+  const int C = idx.size(1), B = idx.size(2), F = x.size(1);
+  TORCH_CHECK(ox.numel() == (long)C * B * F && oy.numel() == (long)C * B, "output sizes");
+  ok(afl_gather_har(x.data_ptr<float>(), (const long*)y.data_ptr<int64_t>(), F, idx.data_ptr<int>(),
+                    stepctl.data_ptr<int>(), C, B, ox.data_ptr<float>(), (long*)oy.data_ptr<int64_t>(), cur()),
+     "gather_har");
+}
+
+void im2col3(torch::Tensor x, int64_t B, int64_t L, torch::Tensor out) {
+  view3(x, "x");
+  dense(out, "out");
+  TORCH_CHECK(x.stride(2) == 1 && x.size(1) == B * L, "x must be [C, B*L, Cin] with contiguous channels");
+  const int C = x.size(0), Cin = x.size(2);
+  TORCH_CHECK(out.numel() == (long)C * B * L * 3 * Cin, "out must be [C, B*L, 3*Cin]");
+  ok(afl_im2col3(x.data_ptr<float>(), x.stride(0), x.stride(1), C, B, L, Cin, out.data_ptr<float>(), cur()), "im2col3");
+}
+
+void col2im3(torch::Tensor dcols, int64_t B, int64_t L, int64_t Cin, c10::optional<torch::Tensor> relu_src,
+             torch::Tensor dx) {
+  dense(dcols, "dcols");
+  dense(dx, "dx");
+  const int C = dcols.size(0);
+  TORCH_CHECK(dcols.numel() == (long)C * B * L * 3 * Cin && dx.numel() == (long)C * B * L * Cin, "sizes");
+  long sRc = 0, sRr = 0;
+  if (relu_src.has_value() && relu_src->defined()) {
+    view3(*relu_src, "relu_src");
+    TORCH_CHECK(relu_src->stride(2) == 1, "relu_src channels must be contiguous");
+    sRc = relu_src->stride(0);
+    sRr = relu_src->stride(1);
+  }
+  ok(afl_col2im3(dcols.data_ptr<float>(), C, B, L, Cin, optp(relu_src), sRc, sRr, dx.data_ptr<float>(), cur()),
+     "col2im3");
+}
+
+void pool4_fwd(torch::Tensor h, int64_t B, int64_t L, torch::Tensor out, int64_t col0,
+               c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+  dense(h, "h");
+  view3(out, "out");
+  TORCH_CHECK(out.stride(2) == 1, "out columns must be contiguous");
+  const int C = h.size(0), Ch = h.size(-1);
+  ok(afl_pool4_fwd(h.data_ptr<float>(), C, B, L, Ch, out.data_ptr<float>(), out.stride(0), out.stride(1), col0,
+                   make_drop(seeds, stepctl, layer, p), cur()),
+     "pool4_fwd");
+}
+
+void pool4_bwd(torch::Tensor dout, int64_t col0, torch::Tensor h, int64_t B, int64_t L, torch::Tensor dh,
+               c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+  view3(dout, "dout");
+  dense(h, "h");
+  dense(dh, "dh");
+  TORCH_CHECK(dout.stride(2) == 1, "dout columns must be contiguous");
+  const int C = h.size(0), Ch = h.size(-1);
+  ok(afl_pool4_bwd(dout.data_ptr<float>(), dout.stride(0), dout.stride(1), col0, h.data_ptr<float>(), C, B, L, Ch,
+                   dh.data_ptr<float>(), make_drop(seeds, stepctl, layer, p), cur()),
+     "pool4_bwd");
+}
+
+void ln_fwd(torch::Tensor x, c10::optional<torch::Tensor> a, c10::optional<torch::Tensor> s, torch::Tensor y,
+            torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, c10::optional<torch::Tensor> seeds,
+            c10::optional<torch::Tensor> stepctl, int64_t layer_a, double p_a, int64_t layer_o, double p_o) {
+  view3(x, "x");
+  view3(y, "y");
+  dense(stats, "stats");
+  dev(gamma, "gamma");
+  dev(beta, "beta");
+  TORCH_CHECK(x.size(2) == 64 && x.stride(2) == 1 && y.stride(2) == 1, "LayerNorm rows of 64 contiguous columns");
+  TORCH_CHECK(gamma.dim() == 2 && gamma.stride(1) == 1 && beta.stride(0) == gamma.stride(0), "gamma/beta [C, 64]");
+  AflLn l{};
+  l.x = x.data_ptr<float>(); l.sXc = x.stride(0); l.sXr = x.stride(1);
+  if (a.has_value() && a->defined()) {
+    view3(*a, "a");
+    TORCH_CHECK(a->stride(2) == 1, "a columns must be contiguous");
+    l.a = a->data_ptr<float>(); l.sAc = a->stride(0); l.sAr = a->stride(1);
+  }
+  if (s.has_value() && s->defined()) {
+    dense(*s, "s");
+    TORCH_CHECK(s->numel() == x.size(0) * x.size(1) * 64, "s must be [C, rows, 64]");
+    l.s = s->data_ptr<float>();
+  }
+  l.y = y.data_ptr<float>(); l.sYc = y.stride(0); l.sYr = y.stride(1);
+  l.stats = stats.data_ptr<float>();
+  l.gamma = gamma.data_ptr<float>(); l.beta = beta.data_ptr<float>(); l.sPc = gamma.stride(0);
+  l.rows = x.size(1); l.nC = x.size(0);
+  l.da = make_drop(seeds, stepctl, layer_a, p_a);
+  l.dout = make_drop(seeds, stepctl, layer_o, p_o);
+  ok(afl_ln_fwd(l, cur()), "ln_fwd");
+}
+
+void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor stats, torch::Tensor gamma, torch::Tensor dx,
+            int64_t dx_accum, c10::optional<torch::Tensor> da, torch::Tensor dgamma, torch::Tensor dbeta,
+            c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer_a, double p_a,
+            int64_t layer_o, double p_o) {
+  view3(dy, "dy");
+  view3(s, "s");
+  view3(dx, "dx");
+  dense(stats, "stats");
+  TORCH_CHECK(dy.stride(2) == 1 && s.stride(2) == 1 && dx.stride(2) == 1, "contiguous columns");
+  TORCH_CHECK(dgamma.stride(0) == gamma.stride(0) && dbeta.stride(0) == gamma.stride(0), "param/grad strides");
+  AflLnB l{};
+  l.dy = dy.data_ptr<float>(); l.sDc = dy.stride(0); l.sDr = dy.stride(1);
+  l.s = s.data_ptr<float>(); l.sSc = s.stride(0); l.sSr = s.stride(1);
+  l.stats = stats.data_ptr<float>();
+  l.gamma = gamma.data_ptr<float>(); l.sPc = gamma.stride(0);
+  l.dx = dx.data_ptr<float>(); l.sXc = dx.stride(0); l.sXr = dx.stride(1); l.dx_accum = (int)dx_accum;
+  if (da.has_value() && da->defined()) {
+    view3(*da, "da");
+    l.da = da->data_ptr<float>(); l.sAc = da->stride(0); l.sAr = da->stride(1);
+  }
+  l.dgamma = dgamma.data_ptr<float>(); l.dbeta = dbeta.data_ptr<float>();
+  l.rows = dy.size(1); l.nC = dy.size(0);
+  l.da_drop = make_drop(seeds, stepctl, layer_a, p_a);
+  l.dout = make_drop(seeds, stepctl, layer_o, p_o);
+  ok(afl_ln_bwd(l, cur()), "ln_bwd");
+}
+
+void gru_fwd(torch::Tensor gi, torch::Tensor bhh, torch::Tensor h, int64_t col0) {
+  dense(gi, "gi");
+  dev(bhh, "bhh");
+  view3(h, "h");
+  const int C = gi.size(0), B = gi.size(1);
+  TORCH_CHECK(gi.size(2) == 96 && bhh.stride(1) == 1 && h.stride(2) == 1, "gru shapes");
+  ok(afl_gru_fwd(gi.data_ptr<float>(), bhh.data_ptr<float>(), bhh.stride(0), C, B, h.data_ptr<float>(), h.stride(0),
+                 h.stride(1), col0, cur()),
+     "gru_fwd");
+}
+
+void gru_bwd(torch::Tensor dh, int64_t col0, torch::Tensor gi, torch::Tensor bhh, torch::Tensor dgi,
+             torch::Tensor dbih, torch::Tensor dbhh) {
+  view3(dh, "dh");
+  dense(gi, "gi");
+  dense(dgi, "dgi");
+  TORCH_CHECK(dbih.stride(0) == bhh.stride(0) && dbhh.stride(0) == bhh.stride(0), "grad strides");
+  const int C = gi.size(0), B = gi.size(1);
+  ok(afl_gru_bwd(dh.data_ptr<float>(), dh.stride(0), dh.stride(1), col0, gi.data_ptr<float>(), bhh.data_ptr<float>(),
+                 bhh.stride(0), C, B, dgi.data_ptr<float>(), dbih.data_ptr<float>(), dbhh.data_ptr<float>(), cur()),
+     "gru_bwd");
+}
+
+void bce(torch::Tensor z, torch::Tensor y, torch::Tensor bsz, torch::Tensor epoch, torch::Tensor nb,
+         torch::Tensor stepctl, torch::Tensor failed, torch::Tensor losses, torch::Tensor dz) {
+  dense(z, "z");
+  dense(y, "y");
+  dense(bsz, "bsz", torch::kInt32);
+  dense(epoch, "epoch", torch::kInt32);
+  dense(nb, "nb", torch::kInt32);
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(failed, "failed", torch::kInt32);
+  dense(losses, "losses");
+  dense(dz, "dz");
+  const int S = bsz.size(0), C = bsz.size(1), B = z.numel() / C;
+  ok(afl_bce(z.data_ptr<float>(), y.data_ptr<float>(), bsz.data_ptr<int>(), epoch.data_ptr<int>(), nb.data_ptr<int>(),
+             stepctl.data_ptr<int>(), C, B, S, failed.data_ptr<int>(), losses.data_ptr<float>(), losses.size(1),
+             dz.data_ptr<float>(), cur()),
+     "bce");
+}
+
+void ce(torch::Tensor logits, torch::Tensor y, torch::Tensor bsz, torch::Tensor epoch, torch::Tensor nb,
+        torch::Tensor stepctl, torch::Tensor failed, torch::Tensor losses, torch::Tensor dz) {
+  dense(logits, "logits");
+  dense(y, "y", torch::kInt64);
+  dense(bsz, "bsz", torch::kInt32);
+  dense(epoch, "epoch", torch::kInt32);
+  dense(nb, "nb", torch::kInt32);
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(failed, "failed", torch::kInt32);
+  dense(losses, "losses");
+  dense(dz, "dz");
+  const int S = bsz.size(0), C = bsz.size(1), K = logits.size(-1), B = logits.numel() / ((long)C * K);
+  ok(afl_ce(logits.data_ptr<float>(), (const long*)y.data_ptr<int64_t>(), K, bsz.data_ptr<int>(), epoch.data_ptr<int>(),
+            nb.data_ptr<int>(), stepctl.data_ptr<int>(), C, B, S, failed.data_ptr<int>(), losses.data_ptr<float>(),
+            losses.size(1), dz.data_ptr<float>(), cur()),
+     "ce");
+}
+
+void adam_clients(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor tcount,
+                  torch::Tensor bsz, torch::Tensor stepctl, torch::Tensor failed, double lr, int64_t skip_lo,
+                  int64_t skip_hi, double sgd_lr) {
+  dense(p, "p");
+  dense(g, "g");
+  dense(m, "m");
+  dense(v, "v");
+  dense(tcount, "tcount", torch::kInt32);
+  dense(bsz, "bsz", torch::kInt32);
+  const int C = p.size(0), S = bsz.size(0);
+  ok(afl_adam_clients(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.size(1), C,
+                      tcount.data_ptr<int>(), bsz.data_ptr<int>(), stepctl.data_ptr<int>(), S,
+                      failed.data_ptr<int>(), (float)lr, skip_lo, skip_hi, (float)sgd_lr, cur()),
+     "adam_clients");
+}
+
+void step_end(torch::Tensor stepctl, torch::Tensor tcount, torch::Tensor bsz, torch::Tensor failed) {
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(tcount, "tcount", torch::kInt32);
+  ok(afl_step_end(stepctl.data_ptr<int>(), tcount.data_ptr<int>(), bsz.data_ptr<int>(), failed.data_ptr<int>(),
+                  bsz.size(1), bsz.size(0), cur()),
+     "step_end");
+}
+
+void conv_pe_fwd(torch::Tensor x, torch::Tensor params, int64_t w_off, int64_t b_off, int64_t pe_off, torch::Tensor h) {
+  dense(x, "x");
+  dense(params, "params");
+  dense(h, "h");
+  const int C = x.size(0), B = x.size(1), L = x.size(2);
+  ok(afl_conv_pe_fwd(x.data_ptr<float>(), C, B, L, params.data_ptr<float>(), params.size(1), w_off, b_off, pe_off,
+                     h.data_ptr<float>(), cur()),
+     "conv_pe_fwd");
+}
+
+void conv_pe_bwd(torch::Tensor x, torch::Tensor dh, torch::Tensor grads, int64_t w_off, int64_t b_off) {
+  dense(x, "x");
+  dense(dh, "dh");
+  dense(grads, "grads");
+  const int C = x.size(0), B = x.size(1), L = x.size(2);
+  ok(afl_conv_pe_bwd(x.data_ptr<float>(), dh.data_ptr<float>(), C, B, L, grads.data_ptr<float>(), grads.size(1), w_off,
+                     b_off, cur()),
+     "conv_pe_bwd");
+}
+
+void mean_rows_fwd(torch::Tensor h, int64_t B, int64_t L, torch::Tensor out) {
+  dense(h, "h");
+  dense(out, "out");
+  ok(afl_mean_rows_fwd(h.data_ptr<float>(), h.size(0), B, L, out.data_ptr<float>(), cur()), "mean_rows_fwd");
+}
+
+void mean_rows_bwd(torch::Tensor dout, int64_t B, int64_t L, torch::Tensor dh) {
+  dense(dout, "dout");
+  dense(dh, "dh");
+  ok(afl_mean_rows_bwd(dout.data_ptr<float>(), dout.size(0), B, L, dh.data_ptr<float>(), cur()), "mean_rows_bwd");
+}
+
+AflAttn attn_args(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t B, int64_t L,
+                  c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+  dense(qkv, "qkv");
+  dense(o, "o");
+  dense(lse, "lse");
+  AflAttn a{};
+  a.C = qkv.size(0);
+  a.B = B;
+  a.L = L;
+  a.Lp = afl_attn_lp(L);
+  TORCH_CHECK(qkv.numel() == (long)a.C * B * L * 192 && o.numel() == (long)a.C * B * L * 64, "qkv/o sizes");
+  TORCH_CHECK(lse.numel() == (long)a.C * B * 4 * a.Lp, "lse must hold C*B*4*Lp floats");
+  a.qkv = qkv.data_ptr<float>();
+  a.o = o.data_ptr<float>();
+  a.lse = lse.data_ptr<float>();
+  a.scale = 0.25f;  // 1 / sqrt(head_dim 16)
+  a.drop = make_drop(seeds, stepctl, layer, p);
+  return a;
+}
+
+void attn_fwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, int64_t B, int64_t L,
+              c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+  AflAttn a = attn_args(qkv, o, lse, B, L, seeds, stepctl, layer, p);
+  ok(afl_attn_fwd(a, cur()), "attn_fwd");
+}
+
+void attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, torch::Tensor dout, torch::Tensor dqkv, int64_t B,
+              int64_t L, c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer,
+              double p) {
+  AflAttn a = attn_args(qkv, o, lse, B, L, seeds, stepctl, layer, p);
+  dense(dout, "dout");
+  dense(dqkv, "dqkv");
+  a.dout = dout.data_ptr<float>();
+  a.dqkv = dqkv.data_ptr<float>();
+  ok(afl_attn_bwd(a, cur()), "attn_bwd");
+}
+
+}  // namespace
+
+void afl_register_layers(pybind11::module& m) {
+  namespace py = pybind11;
+  const auto none = py::none();
+  m.def("bgemm", &bgemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias") = none, py::arg("Z") = none,
+        py::arg("G") = none, py::arg("act") = 0, py::arg("gact") = 0, py::arg("accum") = 0, py::arg("splitk") = 1,
+        py::arg("alpha") = 1.0, py::arg("seeds") = none, py::arg("stepctl") = none, py::arg("layer") = 0,
+        py::arg("p") = 0.0);
+  m.def("colsum", &colsum);
+  m.def("gather_icu", &gather_icu);
+  m.def("gather_har", &gather_har);
+  m.def("im2col3", &im2col3);
+  m.def("col2im3", &col2im3);
+  m.def("pool4_fwd", &pool4_fwd);
+  m.def("pool4_bwd", &pool4_bwd);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("gru_fwd", &gru_fwd);
+  m.def("gru_bwd", &gru_bwd);
+  m.def("bce", &bce);
+  m.def("ce", &ce);
+  m.def("adam_clients", &adam_clients);
+  m.def("step_end", &step_end);
+  m.def("conv_pe_fwd", &conv_pe_fwd);
+  m.def("conv_pe_bwd", &conv_pe_bwd);
+  m.def("mean_rows_fwd", &mean_rows_fwd);
+  m.def("mean_rows_bwd", &mean_rows_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_lp", &afl_attn_lp);
+}

@@ -1,0 +1,199 @@
+"""GPU numerics of the client-batched layer kernels and the graph-captured step programs, each
+against the fp32 PyTorch composite of the same op (CPU), with identical hash dropout masks."""
+import pytest
+import torch
+
+from attackfl_amd.data import DeviceTable, synthetic_har, synthetic_icu
+from attackfl_amd.fl.programs import ProgramRunner, make_program
+from attackfl_amd.fl.trainers import Plan
+from attackfl_amd.models import ParamLayout, build_model
+from attackfl_amd.ops import layers as Lx
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, rel=2e-2, name=""):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= rel * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _ctl(C):
+    return Lx.StepCtl.create([7 + 3 * c for c in range(C)], DEV), Lx.StepCtl.create([7 + 3 * c for c in range(C)],
+                                                                                       "cpu")
+
+
+@pytest.mark.parametrize("act,gact,p", [(0, 0, 0.0), (1, 0, 0.1), (2, 0, 0.3), (0, 1, 0.1), (0, 2, 0.0)])
+def test_bgemm_epilogues(gpu, act, gact, p):
+    C, M, N, K = 3, 150, 70, 45
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(C, M, K, generator=g)
+    W = torch.randn(C, N, K, generator=g)
+    bias = torch.randn(C, N, generator=g)
+    G = torch.randn(C, M, N, generator=g)
+    cg, cc = _ctl(C)
+    outs = []
+    for dev, ctl in ((DEV, cg), ("cpu", cc)):
+        Cm = torch.zeros(C, M, N, device=dev)
+        Z = torch.zeros(C, M, N, device=dev)
+        Lx.bgemm(A.to(dev), W.to(dev), Cm, bias=bias.to(dev), Z=Z, G=G.to(dev) if gact else None, act=act, gact=gact,
+                 ctl=ctl, layer=5, p=p)
+        outs.append((Cm, Z))
+    _close(outs[0][0], outs[1][0], name="C")
+    _close(outs[0][1], outs[1][1], name="Z")
+    # dropout masks identical: zeros in the same places
+    if p > 0:  # (away from relu's kink, where bf16 rounding may flip the sign)
+        z = outs[1][1]
+        sure = (torch.relu(z) if act == 1 else (torch.nn.functional.gelu(z) if act == 2 else z)).abs() > 0.5
+        assert torch.equal((outs[0][0].cpu() == 0)[sure], (outs[1][0] == 0)[sure])
+
+
+def test_bgemm_transposed_views_and_splitk(gpu):
+    C, M, N, K = 2, 2048, 96, 40
+    g = torch.Generator().manual_seed(1)
+    dY = torch.randn(C, M, N, generator=g)
+    X = torch.randn(C, M, K, generator=g)
+    ref = torch.bmm(dY.transpose(1, 2), X)
+    for splitk in (1, 6):
+        out = torch.zeros(C, N, K, device=DEV)
+        Lx.bgemm(dY.to(DEV).transpose(1, 2), X.to(DEV).transpose(1, 2), out, accum=2 if splitk > 1 else 0,
+                 splitk=splitk)
+        _close(out, ref, name=f"dW splitk={splitk}")
+    # dX = dY W with W a strided view into a flat arena
+    P = 10000
+    flat = torch.randn(C, P, generator=g)
+    W = flat[:, 100:100 + N * K].view(C, N, K)
+    out = torch.zeros(C, M, K, device=DEV)
+    Lx.bgemm(dY.to(DEV), flat.to(DEV)[:, 100:100 + N * K].view(C, N, K).transpose(1, 2), out)
+    _close(out, torch.bmm(dY, W), name="dX")
+
+
+def test_layernorm_fwd_bwd(gpu):
+    C, R = 2, 300
+    g = torch.Generator().manual_seed(2)
+    x, a, dy = (torch.randn(C, R, 64, generator=g) for _ in range(3))
+    gam, bet = 1 + 0.1 * torch.randn(C, 64, generator=g), 0.1 * torch.randn(C, 64, generator=g)
+    cg, cc = _ctl(C)
+    res = []
+    for dev, ctl in ((DEV, cg), ("cpu", cc)):
+        s = torch.zeros(C, R, 64, device=dev)
+        y = torch.zeros(C, R, 64, device=dev)
+        st = torch.zeros(C, R, 2, device=dev)
+        Lx.ln_fwd(x.to(dev), a.to(dev), s, y, st, gam.to(dev), bet.to(dev), ctl, layer_a=3, p_a=0.1, layer_o=4,
+                  p_o=0.3)
+        dx = torch.zeros(C, R, 64, device=dev)
+        da = torch.zeros(C, R, 64, device=dev)
+        dg = torch.zeros(C, 64, device=dev)
+        db = torch.zeros(C, 64, device=dev)
+        Lx.ln_bwd(dy.to(dev), s, st, gam.to(dev), dx, 0, da, dg, db, ctl, layer_a=3, p_a=0.1, layer_o=4, p_o=0.3)
+        res.append((y, dx, da, dg, db))
+    for i, n in enumerate(["y", "dx", "da", "dgamma", "dbeta"]):
+        _close(res[0][i], res[1][i], rel=1e-4, name=n)
+
+
+def test_gru_pool_conv_ops(gpu):
+    C, B = 2, 33
+    g = torch.Generator().manual_seed(3)
+    gi, bhh = torch.randn(C, B, 96, generator=g), torch.randn(C, 96, generator=g)
+    dh = torch.randn(C, B, 64, generator=g)
+    res = []
+    for dev in (DEV, "cpu"):
+        h = torch.zeros(C, B, 64, device=dev)
+        Lx.gru_fwd(gi.to(dev), bhh.to(dev), h, 32)
+        dgi = torch.zeros(C, B, 96, device=dev)
+        dbi, dbh = torch.zeros(C, 96, device=dev), torch.zeros(C, 96, device=dev)
+        Lx.gru_bwd(dh.to(dev), 32, gi.to(dev), bhh.to(dev), dgi, dbi, dbh)
+        res.append((h, dgi, dbi, dbh))
+    for i in range(4):
+        _close(res[0][i], res[1][i], rel=1e-4, name=f"gru{i}")
+    # conv patches + pooling with dropout
+    L, Cin = 7, 32
+    x = torch.relu(torch.randn(C, B * L, Cin, generator=g))
+    dcols = torch.randn(C, B * L, 3 * Cin, generator=g)
+    h3 = torch.relu(torch.randn(C, B * L, 128, generator=g))
+    dout = torch.randn(C, B, 1024, generator=g)
+    cg, cc = _ctl(C)
+    res = []
+    for dev, ctl in ((DEV, cg), ("cpu", cc)):
+        cols = torch.zeros(C, B * L, 3 * Cin, device=dev)
+        Lx.im2col3(x.to(dev), B, L, cols)
+        dx = torch.zeros(C, B * L, Cin, device=dev)
+        Lx.col2im3(dcols.to(dev), B, L, Cin, x.to(dev), dx)
+        cat = torch.zeros(C, B, 1024, device=dev)
+        Lx.pool4_fwd(h3.to(dev), B, L, cat, 512, ctl, layer=1, p=0.3)
+        dh3 = torch.zeros(C, B * L, 128, device=dev)
+        Lx.pool4_bwd(dout.to(dev), 512, h3.to(dev), B, L, dh3, ctl, layer=1, p=0.3)
+        res.append((cols, dx, cat, dh3))
+    for i, n in enumerate(["im2col", "col2im", "pool", "pool_bwd"]):
+        _close(res[0][i], res[1][i], rel=1e-5, name=n)
+
+
+@pytest.mark.parametrize("L,p", [(50, 0.0), (561, 0.1)])
+def test_flash_attention_fwd_bwd(gpu, L, p):
+    C, B = 2, 2
+    g = torch.Generator().manual_seed(4)
+    qkv = torch.randn(C, B * L, 192, generator=g)
+    dout = torch.randn(C, B * L, 64, generator=g)
+    cg, cc = _ctl(C)
+    Lp = Lx.attn_lp(L)
+    res = []
+    for dev, ctl in ((DEV, cg), ("cpu", cc)):
+        o = torch.zeros(C, B * L, 64, device=dev)
+        lse = torch.zeros(C * B * 4, Lp, device=dev)
+        Lx.attn_fwd(qkv.to(dev), o, lse, B, L, ctl, layer=2, p=p)
+        dq = torch.zeros(C, B * L, 192, device=dev)
+        Lx.attn_bwd(qkv.to(dev), o, lse, dout.to(dev), dq, B, L, ctl, layer=2, p=p)
+        res.append((o, lse[:, :L], dq))
+    for i, n in enumerate(["O", "lse", "dqkv"]):
+        _close(res[0][i], res[1][i], rel=3e-2, name=n)
+
+
+def _params(name, C):
+    lay = ParamLayout.for_model(name)
+    base = lay.flatten(build_model(name, seed=0).state_dict())
+    out = base[None].repeat(C, 1)
+    out[1:] += 0.01 * torch.randn(C - 1, lay.P, generator=torch.Generator().manual_seed(9))
+    return out
+
+
+@pytest.mark.parametrize("name,B,n", [("CNNModel", 64, 300), ("RNNModel", 64, 300), ("TransformerClassifier", 4, 24)])
+def test_program_sgd_step_matches_composite(gpu, name, B, n):
+    """One graph-free SGD step with dropout ON: native gradients vs the composite's (same masks)."""
+    C = 2
+    ds = synthetic_har(n) if name == "TransformerClassifier" else synthetic_icu(n)
+    order = torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(c))[:B] for c in range(C)])
+    plan = Plan(order[:, None, :].to(torch.int32), torch.tensor([B] * C, dtype=torch.int32), 1)
+    params = _params(name, C)
+    res = []
+    for dev in (DEV, "cpu"):
+        p = params.clone().to(dev)
+        ok, losses = ProgramRunner(make_program(name, C, B, dev), use_graph=False).train(
+            DeviceTable(ds, dev), p, Plan(plan.order.to(dev), plan.nd, 1), lr=0.0, seeds=[3, 4], sgd_lr=1.0)
+        assert ok.all()
+        res.append(((params - p.cpu()), losses))
+    _close(res[0][0], res[1][0], rel=3e-2, name=f"{name} grads")
+    assert torch.allclose(res[0][1], res[1][1], rtol=1e-2)
+
+
+@pytest.mark.parametrize("name,B,n,E", [("CNNModel", 128, 1000, 2), ("RNNModel", 128, 1000, 2),
+                                        ("TransformerClassifier", 16, 80, 1)])
+def test_program_graph_adam_training(gpu, name, B, n, E):
+    """Multi-step Adam through the captured HIP graph tracks the composite run (losses per epoch)."""
+    C = 3
+    ds = synthetic_har(n) if name == "TransformerClassifier" else synthetic_icu(n)
+    nd = [n // 2, n // 2 - 17, n // 3 + 1]
+    order = torch.stack([torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(10 * c + e))[:max(nd)]
+                                      for e in range(E)]) for c in range(C)]).to(torch.int32)
+    params = _params(name, C)
+    res = []
+    for dev in (DEV, "cpu"):
+        p = params.clone().to(dev)
+        ok, losses = ProgramRunner(make_program(name, C, B, dev)).train(
+            DeviceTable(ds, dev), p, Plan(order.to(dev), torch.tensor(nd, dtype=torch.int32), E), lr=1e-3,
+            seeds=[5, 6, 7])
+        assert ok.all()
+        res.append((p.cpu(), losses))
+    assert torch.allclose(res[0][1], res[1][1], rtol=2e-2, atol=2e-3), (res[0][1], res[1][1])
+    assert (res[0][0] - res[1][0]).abs().max() < 0.05

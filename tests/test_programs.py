@@ -1,0 +1,118 @@
+"""Layer programs (CNN / RNN / HAR classifier) on CPU: the composite ops against the reference
+``nn.Module`` math — eval forward, and the hand-written backward against autograd (one SGD step with
+dropout off), plus the Adam / size-1-skip / NaN semantics of the step runner."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from attackfl_amd.data import DeviceTable, synthetic_har, synthetic_icu
+from attackfl_amd.fl.programs import ProgramRunner, make_program, step_tables
+from attackfl_amd.fl.trainers import Plan, bce_loss
+from attackfl_amd.models import ParamLayout, build_model
+
+ICU_MODELS = ["CNNModel", "RNNModel"]
+
+
+def _params(name, C, seed=0):
+    lay = ParamLayout.for_model(name)
+    base = lay.flatten(build_model(name, seed=seed).state_dict())
+    g = torch.Generator().manual_seed(seed + 1)
+    out = base[None].repeat(C, 1)
+    out[1:] += 0.01 * torch.randn(C - 1, lay.P, generator=g)
+    return out, lay
+
+
+def _module(name, flat, lay):
+    m = build_model(name, seed=0)
+    m.load_state_dict(lay.unflatten(flat))
+    return m.eval()
+
+
+def _table(name, n):
+    return DeviceTable(synthetic_har(n) if name == "TransformerClassifier" else synthetic_icu(n), "cpu")
+
+
+@pytest.mark.parametrize("name", ICU_MODELS + ["TransformerClassifier"])
+def test_eval_forward_matches_module(name):
+    C = 2
+    params, lay = _params(name, C)
+    n = 5 if name == "TransformerClassifier" else 37
+    tab = _table(name, n)
+    prog = make_program(name, C, 16 if name != "TransformerClassifier" else 3, "cpu", train=False)
+    data = tab.x if name == "TransformerClassifier" else tab.rows
+    out = ProgramRunner(prog).predict(params, data)
+    for c in range(C):
+        m = _module(name, params[c], lay)
+        with torch.no_grad():
+            if name == "TransformerClassifier":
+                ref = m(tab.x[:, None, :])
+            else:
+                ref = m(tab.rows[:, :7], tab.rows[:, 7:23])[:, 0]
+        assert torch.allclose(out[c], ref, atol=2e-5, rtol=1e-4), (name, c, (out[c] - ref).abs().max())
+
+
+def _ref_grads(name, flat, lay, tab, idx):
+    m = _module(name, flat, lay)  # eval mode: dropout off, same as the program's dropout=False
+    for p_ in m.parameters():
+        p_.grad = None
+    if name == "TransformerClassifier":
+        x, y = tab.har_batch(idx)
+        loss = F.cross_entropy(m(x), y)
+    else:
+        v, l, y = tab.icu_batch(idx)
+        loss = bce_loss(m(v, l), y[:, None])
+    loss.backward()
+    g = torch.zeros(lay.P)
+    named = dict(m.named_parameters())
+    for s in lay.slots:
+        if s.name in named and named[s.name].grad is not None:
+            g[s.offset:s.offset + s.numel] = named[s.name].grad.reshape(-1)
+    return g, float(loss)
+
+
+@pytest.mark.parametrize("name", ICU_MODELS + ["TransformerClassifier"])
+def test_backward_matches_autograd(name):
+    C = 2
+    B = 3 if name == "TransformerClassifier" else 24
+    params, lay = _params(name, C)
+    tab = _table(name, 40)
+    g = torch.Generator().manual_seed(3)
+    order = torch.stack([torch.randperm(40, generator=g)[:B] for _ in range(C)])[:, None, :].to(torch.int32)
+    plan = Plan(order, torch.tensor([B] * C, dtype=torch.int32), 1)
+    prog = make_program(name, C, B, "cpu", train=True, dropout=False)
+    before = params.clone()
+    sgd = 1e-3
+    ok, losses = ProgramRunner(prog).train(tab, params, plan, lr=0.0, seeds=[11, 12], sgd_lr=sgd)
+    assert ok.all()
+    for c in range(C):
+        ref, ref_loss = _ref_grads(name, before[c], lay, tab, order[c, 0].long())
+        got = (before[c] - params[c]) / sgd
+        assert abs(float(losses[c, 0]) - ref_loss) < 1e-5
+        tol = 2e-3 * float(ref.abs().max()) + 1e-6
+        assert (got - ref).abs().max() < tol, (name, c, float((got - ref).abs().max()), tol)
+
+
+def test_step_tables_skip_and_padding():
+    order = torch.arange(2 * 1 * 9, dtype=torch.int32).reshape(2, 1, 9)
+    idx, bsz, ep, nb, S = step_tables(order, [9, 5], 1, 4, "cpu")
+    assert S == 3 and nb.tolist() == [3, 2]
+    assert bsz[:, 0].tolist() == [4, 4, 1] and bsz[:, 1].tolist() == [4, 1, 0]   # size-1 batch -> skipped
+    assert idx[2, 0, 0] == 8 and (idx[2, 0, 1:] == -1).all()
+
+
+def test_adam_dropout_training_runs_and_nan_fails():
+    name = "CNNModel"
+    C, B = 2, 16
+    params, lay = _params(name, C)
+    tab = _table(name, 64)
+    g = torch.Generator().manual_seed(5)
+    order = torch.stack([torch.stack([torch.randperm(64, generator=g)[:33] for _ in range(2)]) for _ in range(C)])
+    plan = Plan(order.to(torch.int32), torch.tensor([33, 33], dtype=torch.int32), 2)
+    params[1, 5] = float("nan")
+    before = params.clone()
+    ok, losses = ProgramRunner(make_program(name, C, B, "cpu")).train(tab, params, plan, lr=1e-3, seeds=[1, 2])
+    assert ok.tolist() == [True, False]
+    assert torch.isfinite(losses[0]).all() and (losses[0] > 0).all()
+    assert not torch.equal(params[0], before[0])
+    # the failed client stops before its first update
+    assert torch.equal(torch.nan_to_num(params[1]), torch.nan_to_num(before[1]))
