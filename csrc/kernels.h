@@ -88,6 +88,7 @@ struct AflGemm {
   int splitk;
   float alpha;
   AflDrop drop;
+  int avec, bvec;  // set by the launcher: operand rows 16-B aligned and k-contiguous
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
 int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s);

@@ -1,7 +1,7 @@
 // Flash attention for the HAR TransformerClassifier encoder (reference src/Model.py:435-458:
 // nn.TransformerEncoderLayer(d_model 64, nhead 4) -> SDPA with head_dim 16, L = 561, attention
 // dropout 0.1 in training).  The math path of the reference materialises [B*4, 561, 561] fp32
-// probabilities (~645 MB per layer at B=128); here one 256-thread workgroup owns one
+// probabilities (~645 MB per layer at B=128); here one 12-wave workgroup owns one
 // (client, sample, head) and streams the whole sequence through LDS, never writing P.
 //
 // Layouts: qkv [C][B*L][192] fp32 (q | k | v, head h at columns 16h..16h+15 of each), O [C][B*L][64],
@@ -13,14 +13,18 @@
 //   (xor 16, xor 32); the dropped probabilities already sit in the B-operand layout of
 //   O^T[d][q] += V^T[d][key] . P^T[key][q] (v_mfma_f32_16x16x32_bf16, key order permuted to match),
 //   and the running O^T of a query lives in the same lane as its softmax statistics (no shuffles).
-// Backward (per wave: 16 keys, loop over 32-query tiles; FA2 recurrence with Delta = rowsum(dO o O)):
-//   S, dP in [q][key] orientation (K, V fragments pinned in registers), dV += Pd^T dO and
-//   dK += dS^T Q as 16x16x32 MFMAs straight from registers, dQ += dS K through a per-wave LDS
-//   transpose of dS and LDS float atomics (summed over the 4 key-owning waves).
+// Backward (FA2 recurrence with Delta = rowsum(dO o O)), two owner-computes kernels, no atomics:
+//   k_attn_bwd_kv  each wave owns 16 keys and sweeps the queries: S, dP in [q][key] orientation (K, V
+//                  fragments pinned in registers), dV += Pd^T dO and dK += dS^T Q as 16x16x32 MFMAs
+//                  straight from registers; 12 waves share one ~80 KB LDS image (2 workgroups per CU).
+//   k_attn_bwd_dq  each wave owns 16 queries and sweeps the keys (recomputing S, dP): dQ stays in
+//                  registers.  (An LDS-atomic dQ reduction inside the kv kernel measured 5x slower:
+//                  3.7 ms vs 0.75 ms for the kv sweep alone at C=8, B=64.)
 // Dropout: keep-mask = afl_keep(step key, layer, (b*H + h)*L + q, key) regenerated in backward.
 #include "common.h"
 #include "kernels.h"
 
+#define LDS_AS __attribute__((address_space(3)))
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef short s8v __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
@@ -42,6 +46,23 @@ __device__ __forceinline__ f4v mfma32(s8v a, s8v b, f4v c) {
                                                  0);
 }
 __device__ __forceinline__ s4v ld4(const unsigned short* p) { return *(const s4v*)p; }
+// [rows][16] bf16 images read as 4-column groups by 16 consecutive rows: rows with bit 3 set swap
+// their column halves, so rows r and r+8 land on different banks (ds_read_b64: (a/4) mod 64)
+__device__ __forceinline__ int swz(int r, int d) { return r * DH + (d ^ (((r >> 3) & 1) << 3)); }
+
+// Dropout multipliers of the 8 keys a lane holds for one query row: keys kb0..kb0+3 and kb1..kb1+3
+// (kb even).  Adjacent keys share one hash (afl_keep's column pairs): 4 hashes per 8 elements.
+__device__ __forceinline__ void keep8(uint32_t key, uint32_t layer, uint32_t row, int kb0, int kb1, uint32_t thr,
+                                      float ik, float (&mk)[8]) {
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const uint32_t hsh = afl_hash4(key, layer, row, (uint32_t)(((hf ? kb1 : kb0) >> 1) + pr));
+      mk[4 * hf + 2 * pr] = (hsh & 0xFFFFu) >= thr ? ik : 0.f;
+      mk[4 * hf + 2 * pr + 1] = (hsh >> 16) >= thr ? ik : 0.f;
+    }
+}
 __device__ __forceinline__ s8v cat8(s4v a, s4v b) {
   s8v r;
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
@@ -56,7 +77,10 @@ __device__ __forceinline__ s8v pack8(const float* v) {
 }
 
 // ============================================================================ forward
-__global__ void __launch_bounds__(256) k_attn_fwd(AflAttn a) {
+constexpr int FW_WAVES = 12, FW_NT = 64 * FW_WAVES;
+
+template <bool DROP>
+__global__ void __launch_bounds__(FW_NT) k_attn_fwd(AflAttn a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = a.Lp, LDV = Lp + 8;
   unsigned short* Kl = (unsigned short*)smem;  // [Lp][16]
@@ -64,18 +88,17 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AflAttn a) {
   const int bh = blockIdx.x, h = bh % H, b = (bh / H) % a.B, c = bh / (H * a.B);
   const long rowbase = ((long)c * a.B + b) * a.L;
   const float* src = a.qkv + rowbase * QKV;
-  for (int t = threadIdx.x; t < Lp * DH; t += 256) {
+  for (int t = threadIdx.x; t < Lp * DH; t += FW_NT) {
     const int key = t >> 4, d = t & 15;
     const bool ok = key < a.L;
-    Kl[t] = bf(ok ? src[(long)key * QKV + DM + h * DH + d] : 0.f);
+    Kl[swz(key, d)] = bf(ok ? src[(long)key * QKV + DM + h * DH + d] : 0.f);
     Vt[d * LDV + key] = bf(ok ? src[(long)key * QKV + 2 * DM + h * DH + d] : 0.f);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const bool dr = a.drop.thr16 != 0;
-  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+  const uint32_t key = DROP ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
   const uint32_t drow0 = (uint32_t)((b * H + h) * a.L);
-  for (int q0 = wave * 16; q0 < Lp; q0 += 64) {
+  for (int q0 = wave * 16; q0 < Lp; q0 += 16 * FW_WAVES) {
     const int q = q0 + li;
     s4v qf;
 #pragma unroll
@@ -83,8 +106,8 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AflAttn a) {
     float m = -INFINITY, l = 0.f;
     f4v o = f4v{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < Lp; kt += 32) {
-      f4v s0 = mfma16(ld4(Kl + (kt + li) * DH + 4 * g), qf, f4v{0.f, 0.f, 0.f, 0.f});
-      f4v s1 = mfma16(ld4(Kl + (kt + 16 + li) * DH + 4 * g), qf, f4v{0.f, 0.f, 0.f, 0.f});
+      f4v s0 = mfma16(ld4(Kl + swz(kt + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
+      f4v s1 = mfma16(ld4(Kl + swz(kt + 16 + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
       float s[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -98,13 +121,13 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AflAttn a) {
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float alpha = __expf(m - mn);
-      float ps = 0.f, pd[8];
+      float ps = 0.f, pd[8], mk[8];
+      if (DROP) keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float p = __expf(s[j] - mn);
         ps += p;
-        const int kk = kt + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
-        pd[j] = dr ? p * (afl_keep(key, a.drop.layer, drow0 + q, kk, a.drop.thr16) ? a.drop.inv_keep : 0.f) : p;
+        pd[j] = DROP ? p * mk[j] : p;
       }
       ps += __shfl_xor(ps, 16, 64);
       ps += __shfl_xor(ps, 32, 64);
@@ -125,34 +148,35 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AflAttn a) {
 }
 
 // ============================================================================ backward
-__global__ void __launch_bounds__(256) k_attn_bwd(AflAttn a) {
+// ---- dK / dV: each wave owns 16 keys and sweeps every query ----
+constexpr int BW_WAVES = 12, BW_NT = 64 * BW_WAVES;  // 12 waves share one ~80 KB LDS image (2 WGs per CU)
+
+template <bool DROP>
+__global__ void __launch_bounds__(BW_NT) k_attn_bwd_kv(AflAttn a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = a.Lp, LDT = Lp + 8;
-  unsigned short* Ql = (unsigned short*)smem;  // [Lp][16]
-  unsigned short* Dl = Ql + Lp * DH;           // dO [Lp][16]
+  unsigned short* Ql = (unsigned short*)smem;  // [Lp][16] (swizzled)
+  unsigned short* Dl = Ql + Lp * DH;           // dO [Lp][16] (swizzled)
   unsigned short* Qt = Dl + Lp * DH;           // [16][LDT]
   unsigned short* Dt = Qt + DH * LDT;          // dO^T [16][LDT]
   float* LSE = (float*)(Dt + DH * LDT);        // [Lp]
-  float* DEL = LSE + Lp;                       // [Lp]
-  float* DQ = DEL + Lp;                        // [Lp][16] fp32 accumulators
-  unsigned short* SS = (unsigned short*)(DQ + Lp * DH);  // per wave dS [32][16]
+  float* DEL = LSE + Lp;                       // [Lp] Delta_q = dO_q . O_q
   const int bh = blockIdx.x, h = bh % H, b = (bh / H) % a.B, c = bh / (H * a.B);
   const long rowbase = ((long)c * a.B + b) * a.L;
   const float* src = a.qkv + rowbase * QKV;
   const float* dO = a.dout + rowbase * DM;
   const float* Oo = a.o + rowbase * DM;
-  for (int t = threadIdx.x; t < Lp * DH; t += 256) {
+  for (int t = threadIdx.x; t < Lp * DH; t += BW_NT) {
     const int q = t >> 4, d = t & 15;
     const bool ok = q < a.L;
     const unsigned short qv = bf(ok ? src[(long)q * QKV + h * DH + d] : 0.f);
     const unsigned short dv = bf(ok ? dO[(long)q * DM + h * DH + d] : 0.f);
-    Ql[t] = qv;
-    Dl[t] = dv;
+    Ql[swz(q, d)] = qv;
+    Dl[swz(q, d)] = dv;
     Qt[d * LDT + q] = qv;
     Dt[d * LDT + q] = dv;
-    DQ[t] = 0.f;
   }
-  for (int q = threadIdx.x; q < Lp; q += 256) {
+  for (int q = threadIdx.x; q < Lp; q += BW_NT) {
     float dl = 0.f;
     if (q < a.L) {
 #pragma unroll
@@ -163,20 +187,16 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AflAttn a) {
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  unsigned short* ss = SS + wave * 32 * DH;
-  const bool dr = a.drop.thr16 != 0;
-  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+  const uint32_t key = DROP ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
   const uint32_t drow0 = (uint32_t)((b * H + h) * a.L);
-  for (int k0 = wave * 16; k0 < Lp; k0 += 64) {
+  for (int k0 = wave * 16; k0 < Lp; k0 += 16 * BW_WAVES) {
     const int kk = k0 + li;  // this lane's key (column of S)
     const bool kok = kk < a.L;
-    s4v kf, vf, kq;  // K[k][d], V[k][d] (B operands); K[k0+4g+j][li] (B operand of dQ)
+    s4v kf, vf;  // K[k][d], V[k][d] (B operands)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       kf[j] = (short)bf(kok ? src[(long)kk * QKV + DM + h * DH + 4 * g + j] : 0.f);
       vf[j] = (short)bf(kok ? src[(long)kk * QKV + 2 * DM + h * DH + 4 * g + j] : 0.f);
-      const int kr = k0 + 4 * g + j;
-      kq[j] = (short)bf(kr < a.L ? src[(long)kr * QKV + DM + h * DH + li] : 0.f);
     }
     f4v dk = f4v{0.f, 0.f, 0.f, 0.f}, dv = f4v{0.f, 0.f, 0.f, 0.f};
     for (int q0 = 0; q0 < Lp; q0 += 32) {
@@ -184,15 +204,18 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AflAttn a) {
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
         const int qb = q0 + 16 * qs;
-        const f4v s = mfma16(ld4(Ql + (qb + li) * DH + 4 * g), kf, f4v{0.f, 0.f, 0.f, 0.f});
-        const f4v dp = mfma16(ld4(Dl + (qb + li) * DH + 4 * g), vf, f4v{0.f, 0.f, 0.f, 0.f});
+        const f4v s = mfma16(ld4(Ql + swz(qb + li, 4 * g)), kf, f4v{0.f, 0.f, 0.f, 0.f});
+        const f4v dp = mfma16(ld4(Dl + swz(qb + li, 4 * g)), vf, f4v{0.f, 0.f, 0.f, 0.f});
+        const f4v l4 = *(const f4v*)(LSE + qb + 4 * g);
+        const f4v d4 = *(const f4v*)(DEL + qb + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int q = qb + 4 * g + e;
-          const float p = kok ? __expf(s[e] * a.scale - LSE[q]) : 0.f;
-          const float mk = dr ? (afl_keep(key, a.drop.layer, drow0 + q, kk, a.drop.thr16) ? a.drop.inv_keep : 0.f) : 1.f;
+          const float pe = __expf(s[e] * a.scale - l4[e]);
+          const float p = kok ? pe : 0.f;
+          float mk = 1.f;
+          if (DROP) mk = afl_keep(key, a.drop.layer, drow0 + qb + 4 * g + e, kk, a.drop.thr16) ? a.drop.inv_keep : 0.f;
           pdv[4 * qs + e] = p * mk;
-          dsv[4 * qs + e] = p * (dp[e] * mk - DEL[q]);
+          dsv[4 * qs + e] = p * (dp[e] * mk - d4[e]);
         }
       }
       // dV[k][d] += sum_q Pd[q][k] dO[q][d];  dK[k][d] += sum_q dS[q][k] Q[q][d]  (query order permuted)
@@ -200,18 +223,6 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AflAttn a) {
       const s8v qtf = cat8(ld4(Qt + li * LDT + q0 + 4 * g), ld4(Qt + li * LDT + q0 + 16 + 4 * g));
       dv = mfma32(pack8(pdv), dof, dv);
       dk = mfma32(pack8(dsv), qtf, dk);
-      // dQ[q][d] += sum_k dS[q][k] K[k][d]: transpose dS through this wave's LDS scratch
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss[(16 * (j >> 2) + 4 * g + (j & 3)) * DH + li] = bf(dsv[j]);
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes visible to itself
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        const f4v dq = mfma16(ld4(ss + (16 * qs + li) * DH + 4 * g), kq, f4v{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(DQ + (q0 + 16 * qs + 4 * g + e) * DH + li, dq[e] * a.scale);
-      }
-      __builtin_amdgcn_wave_barrier();
     }
     // lane holds dK/dV[k0 + 4g + e][li]
 #pragma unroll
@@ -224,10 +235,78 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AflAttn a) {
       }
     }
   }
+}
+
+// ---- dQ: each wave owns 16 queries and sweeps every key (recomputes S and dP; no atomics) ----
+//   S^T[key][q] = K.Q^T and dP^T[key][q] = V.dO^T (16x16x16, A from the [key][16] images), so the
+//   lane holds 8 keys of ONE query — exactly the B-operand layout of dQ^T[d][q] += K^T[d][key] dS^T
+//   (16x16x32, A from the transposed K image): dQ accumulates in registers.
+constexpr int DQ_WAVES = 12, DQ_NT = 64 * DQ_WAVES;
+
+template <bool DROP>
+__global__ void __launch_bounds__(DQ_NT) k_attn_bwd_dq(AflAttn a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Lp = a.Lp, LDT = Lp + 8;
+  unsigned short* Kl = (unsigned short*)smem;  // [Lp][16] (swizzled)
+  unsigned short* Vl = Kl + Lp * DH;           // [Lp][16] (swizzled)
+  unsigned short* Kt = Vl + Lp * DH;           // [16][LDT]
+  const int bh = blockIdx.x, h = bh % H, b = (bh / H) % a.B, c = bh / (H * a.B);
+  const long rowbase = ((long)c * a.B + b) * a.L;
+  const float* src = a.qkv + rowbase * QKV;
+  const float* dO = a.dout + rowbase * DM;
+  const float* Oo = a.o + rowbase * DM;
+  for (int t = threadIdx.x; t < Lp * DH; t += DQ_NT) {
+    const int k = t >> 4, d = t & 15;
+    const bool ok = k < a.L;
+    const unsigned short kv = bf(ok ? src[(long)k * QKV + DM + h * DH + d] : 0.f);
+    Kl[swz(k, d)] = kv;
+    Vl[swz(k, d)] = bf(ok ? src[(long)k * QKV + 2 * DM + h * DH + d] : 0.f);
+    Kt[d * LDT + k] = kv;
+  }
   __syncthreads();
-  for (int t = threadIdx.x; t < a.L * DH; t += 256) {
-    const int q = t >> 4, d = t & 15;
-    a.dqkv[(rowbase + q) * QKV + h * DH + d] = DQ[t];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const uint32_t key = DROP ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+  const uint32_t drow0 = (uint32_t)((b * H + h) * a.L);
+  for (int q0 = wave * 16; q0 < Lp; q0 += 16 * DQ_WAVES) {
+    const int q = q0 + li;
+    const bool qok = q < a.L;
+    s4v qf, df;
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float dov = qok ? dO[(long)q * DM + h * DH + 4 * g + j] : 0.f;
+      qf[j] = (short)bf(qok ? src[(long)q * QKV + h * DH + 4 * g + j] : 0.f);
+      df[j] = (short)bf(dov);
+      dl += dov * (qok ? Oo[(long)q * DM + h * DH + 4 * g + j] : 0.f);
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);  // Delta_q = dO_q . O_q (fp32)
+    const float lse = a.lse[(long)bh * Lp + q];
+    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < Lp; kt += 32) {
+      const f4v s0 = mfma16(ld4(Kl + swz(kt + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
+      const f4v s1 = mfma16(ld4(Kl + swz(kt + 16 + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
+      const f4v p0 = mfma16(ld4(Vl + swz(kt + li, 4 * g)), df, f4v{0.f, 0.f, 0.f, 0.f});
+      const f4v p1 = mfma16(ld4(Vl + swz(kt + 16 + li, 4 * g)), df, f4v{0.f, 0.f, 0.f, 0.f});
+      float ds[8], mk[8];
+      if (DROP) keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = kt + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
+        const float sv = j < 4 ? s0[j] : s1[j - 4];
+        const float dp = j < 4 ? p0[j] : p1[j - 4];
+        const float pe = __expf(sv * a.scale - lse);
+        const float p = kk < a.L ? pe : 0.f;
+        ds[j] = p * (dp * (DROP ? mk[j] : 1.f) - dl);
+      }
+      const s8v kfr = cat8(ld4(Kt + li * LDT + kt + 4 * g), ld4(Kt + li * LDT + kt + 16 + 4 * g));
+      acc = mfma32(kfr, pack8(ds), acc);
+    }
+    if (qok) {
+      float* dst = a.dqkv + (rowbase + q) * QKV + h * DH + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e] = acc[e] * a.scale;
+    }
   }
 }
 
@@ -240,27 +319,38 @@ int afl_attn_lp(int L) { return attn_lp(L); }
 int afl_attn_fwd(const AflAttn& a, hipStream_t s) {
   if (a.Lp != attn_lp(a.L) || a.Lp > 1024) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)a.Lp * DH * 2 + (size_t)DH * (a.Lp + 8) * 2;
-  hipLaunchKernelGGL(k_attn_fwd, dim3(a.C * a.B * H), dim3(256), lds, s, a);
+  if (a.drop.thr16)
+    hipLaunchKernelGGL(k_attn_fwd<true>, dim3(a.C * a.B * H), dim3(FW_NT), lds, s, a);
+  else
+    hipLaunchKernelGGL(k_attn_fwd<false>, dim3(a.C * a.B * H), dim3(FW_NT), lds, s, a);
   return (int)hipGetLastError();
 }
 
-static size_t bwd_lds(int Lp) {
-  return (size_t)Lp * DH * 2 * 2 + (size_t)DH * (Lp + 8) * 2 * 2 + (size_t)Lp * 4 * 2 + (size_t)Lp * DH * 4 +
-         4 * 32 * DH * 2;
-}
+static size_t kv_lds(int Lp) { return (size_t)Lp * DH * 2 * 2 + (size_t)DH * (Lp + 8) * 2 * 2 + (size_t)Lp * 4 * 2; }
+static size_t dq_lds(int Lp) { return (size_t)Lp * DH * 2 * 2 + (size_t)DH * (Lp + 8) * 2; }
 
 int afl_attn_bwd(const AflAttn& a, hipStream_t s) {
-  if (a.Lp != attn_lp(a.L) || a.Lp > 640) return (int)hipErrorInvalidValue;
-  const size_t lds = bwd_lds(a.Lp);
-  // raise the dynamic-LDS cap once, to the largest size this kernel can ask for (the first call
-  // happens eagerly, before any graph capture, so the capture never sees this API)
+  if (a.Lp != attn_lp(a.L) || a.Lp > 1024) return (int)hipErrorInvalidValue;
+  // raise the dynamic-LDS cap once (the first call happens eagerly, before any graph capture)
   static int cap = 0;
-  if (lds > 64 * 1024 && cap == 0) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_attn_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)bwd_lds(640));
-    if (e != hipSuccess) return (int)e;
+  if (cap == 0) {
+    for (const void* f : {(const void*)k_attn_bwd_kv<true>, (const void*)k_attn_bwd_kv<false>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(1024));
+      if (e != hipSuccess) return (int)e;
+    }
+    for (const void* f : {(const void*)k_attn_bwd_dq<true>, (const void*)k_attn_bwd_dq<false>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(1024));
+      if (e != hipSuccess) return (int)e;
+    }
     cap = 1;
   }
-  hipLaunchKernelGGL(k_attn_bwd, dim3(a.C * a.B * H), dim3(256), lds, s, a);
+  const dim3 grid(a.C * a.B * H);
+  if (a.drop.thr16) {
+    hipLaunchKernelGGL(k_attn_bwd_kv<true>, grid, dim3(BW_NT), kv_lds(a.Lp), s, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<true>, grid, dim3(DQ_NT), dq_lds(a.Lp), s, a);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_kv<false>, grid, dim3(BW_NT), kv_lds(a.Lp), s, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<false>, grid, dim3(DQ_NT), dq_lds(a.Lp), s, a);
+  }
   return (int)hipGetLastError();
 }

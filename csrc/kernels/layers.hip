@@ -62,11 +62,20 @@ constexpr int GT = 64, GK = 32, GLD = 40;  // output tile, k step, LDS row strid
 // consecutive k per thread, m-contiguous ones (transposed views) read consecutive m across lanes.
 template <bool KC>
 __device__ __forceinline__ void stage_load(const float* __restrict__ X, long sr, long sk, int rows, int r0, int k0,
-                                           int ke, int tid, float (&v)[8]) {
+                                           int ke, int tid, bool vec, float (&v)[8]) {
   const int r = KC ? r0 + (tid >> 2) : r0 + (tid & 63);
   const int k = KC ? k0 + (tid & 3) * 8 : k0 + (tid >> 6) * 8;
   const bool rok = r < rows;
   const float* p = X + (long)r * sr;
+  if (KC && vec && rok && k + 8 <= ke) {  // 16-B aligned rows: two dwordx4 loads
+    const f4v x0 = *(const f4v*)(p + k), x1 = *(const f4v*)(p + k + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = x0[j];
+      v[4 + j] = x1[j];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (rok && k + j < ke) ? p[(long)(k + j) * sk] : 0.f;
 }
@@ -106,15 +115,15 @@ __global__ void __launch_bounds__(256) k_bgemm(AflGemm g) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   float ra[8], rb[8];
-  stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, kb, ke, tid, ra);
-  stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, kb, ke, tid, rb);
+  stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, kb, ke, tid, g.avec, ra);
+  stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, kb, ke, tid, g.bvec, rb);
   for (int k0 = kb; k0 < ke; k0 += GK) {
     stage_store<AK>(As, tid, ra);
     stage_store<BK>(Bs, tid, rb);
     __syncthreads();
     if (k0 + GK < ke) {  // next tile's global loads overlap this tile's MFMAs
-      stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, k0 + GK, ke, tid, ra);
-      stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, k0 + GK, ke, tid, rb);
+      stage_load<AK>(A, g.sAm, g.sAk, g.M, m0, k0 + GK, ke, tid, g.avec, ra);
+      stage_load<BK>(B, g.sBn, g.sBk, g.N, n0, k0 + GK, ke, tid, g.bvec, rb);
     }
     const s8v a0 = frag(As, wm, lane), a1 = frag(As, wm + 16, lane);
     const s8v b0 = frag(Bs, wn, lane), b1 = frag(Bs, wn + 16, lane);
@@ -682,15 +691,18 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (g.splitk > 1 && g.accum != 2) return (int)hipErrorInvalidValue;
   const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
   dim3 grid(tiles, max(1, g.splitk), g.nC);
+  AflGemm gg = g;  // 16-B aligned k-contiguous rows take the vector-load path
+  gg.avec = g.sAk == 1 && g.sAm % 4 == 0 && g.sAc % 4 == 0 && ((uintptr_t)g.A & 15) == 0;
+  gg.bvec = g.sBk == 1 && g.sBn % 4 == 0 && g.sBc % 4 == 0 && ((uintptr_t)g.B & 15) == 0;
   const bool ak = g.sAk == 1, bk = g.sBk == 1;
   if (ak && bk)
-    hipLaunchKernelGGL((k_bgemm<true, true>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((k_bgemm<true, true>), grid, dim3(256), 0, s, gg);
   else if (ak)
-    hipLaunchKernelGGL((k_bgemm<true, false>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((k_bgemm<true, false>), grid, dim3(256), 0, s, gg);
   else if (bk)
-    hipLaunchKernelGGL((k_bgemm<false, true>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((k_bgemm<false, true>), grid, dim3(256), 0, s, gg);
   else
-    hipLaunchKernelGGL((k_bgemm<false, false>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((k_bgemm<false, false>), grid, dim3(256), 0, s, gg);
   return launched();
 }
 
