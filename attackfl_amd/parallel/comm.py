@@ -74,7 +74,7 @@ class TorchComm(Comm):
         self.pg = pg
         self._staging = self.backend == "gloo" and self.device.type == "cuda"
         self._ipc = None
-        if one_shot and self.backend == "nccl" and self.world > 1:
+        if one_shot and self.device.type == "cuda" and self.world > 1:
             from .ipc import IpcAllGather
 
             try:

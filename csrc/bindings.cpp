@@ -6,6 +6,7 @@
 #include "kernels.h"
 
 void afl_register_layers(pybind11::module& m);  // layers_bind.cpp
+void afl_register_ipc(pybind11::module& m);     // comm/ipc.cpp
 
 namespace {
 
@@ -305,4 +306,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);
   afl_register_layers(m);
+  afl_register_ipc(m);
 }

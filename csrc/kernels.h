@@ -160,3 +160,14 @@ struct AflAttn {
 int afl_attn_lp(int L);
 int afl_attn_fwd(const AflAttn& a, hipStream_t s);
 int afl_attn_bwd(const AflAttn& a, hipStream_t s);
+
+// comm.hip — one-shot intra-node all-gather over IPC-mapped peer buffers (xGMI)
+#define AFL_IPC_MAX_PEERS 16
+struct AflIpcPeers {
+  float* base[AFL_IPC_MAX_PEERS];  // every rank's receive buffer (own rank = local pointer)
+  int world;
+};
+long afl_ipc_buffer_bytes(int world, long cap);
+int afl_ipc_alloc(int world, long cap, float** base);
+int afl_ipc_all_gather(const float* src, long n, const AflIpcPeers& peers, int rank, long cap, uint32_t epoch,
+                       int* status, long max_polls, hipStream_t s);
