@@ -47,6 +47,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef GAS float gf;
 typedef GAS unsigned short gu16;
 typedef GAS int gi32;
+typedef GAS uint32_t gu32;
+typedef GAS unsigned long long gu64;
 
 namespace {
 
@@ -110,7 +112,10 @@ constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8;
 constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
-constexpr long WS_FLOATS = W_DX3V + BM * 64;
+// branch-parallel mode hand-off slots (labs workgroup <-> vitals+head workgroup of one client)
+constexpr long W_XF = W_DX3V + BM * 64;  // labs branch output, bf16 [128][64]
+constexpr long W_XB = W_XF + BM * 32;    // d(labs branch output), fp32 [128][64]
+constexpr long WS_FLOATS = W_XB + BM * 64;
 
 struct AdamK {
   float lr_bc1, rsqrt_bc2;
@@ -455,6 +460,46 @@ __device__ __forceinline__ void store16bf(unsigned short* p, const float (&x)[16
   *(LDS_AS s8v*)(p + 8) = pack8bf(x + 8);
 }
 
+// ---- cross-workgroup hand-off (branch-parallel mode; cdna_hip_programming.md Guideline 16, R1) ----
+// payload: 8-byte write-through (sc1) agent-scope stores; every storing wave drains (vmcnt 0), then a
+// workgroup barrier, then ONE lane stores the flag.  Consumer: ONE wave polls the flag relaxed
+// (bounded spin), ONE agent acquire, vmcnt(0), workgroup barrier, then plain loads.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_wt(gu64* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt(gu64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xwg_publish(const Ctx& c, gu32* flag, uint32_t value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (c.tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr long XWG_MAX_SPINS = 1L << 22;  // ~seconds: a missing partner becomes an error, not a hang
+// returns the flag value once (value >> shift) >= want, or 0xFFFFFFFF on timeout (also raises *tmo)
+__device__ __forceinline__ uint32_t xwg_wait(const Ctx& c, gu32* flag, uint32_t want, int shift, gu32* tmo,
+                                             uint32_t* bcast) {
+  if (c.wave == 0) {
+    uint32_t v = 0;
+    for (long spins = 0;; ++spins) {
+      v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v >> shift) >= want) break;
+      if (spins > XWG_MAX_SPINS) {
+        v = 0xFFFFFFFFu;
+        if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (c.lane == 0) *bcast = v;
+  }
+  __syncthreads();
+  return *bcast;
+}
+
 // write the bf16 copies of one matrix from the master params
 __device__ void init_copies(const Ctx& c, MatW mw) {
   for (int e = c.tid; e < mw.n_real * mw.k_real; e += NT) {
@@ -527,7 +572,8 @@ __device__ __forceinline__ void put_x(const Ctx& c, const St& s) {
 }
 
 // ============================================================== branch forward
-template <int BR>
+// XCH: publish the branch output to the hand-off slot W_XF (write-through stores) instead of LDS CAT
+template <int BR, bool XCH = false>
 __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);
@@ -655,15 +701,26 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     rs[2] = rstd;
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = x[j] * g3[j] + b3[j];
-    store16bf(CAT + r * LD128 + BR * 64 + c0, x);
+    if (XCH) {
+      gu64* d = (gu64*)((gu16*)c.wsf(W_XF) + ro);
+      const s8v lo = pack8bf(x), hi = pack8bf(x + 8);
+      const auto l2 = __builtin_bit_cast(u64x2, lo), h2 = __builtin_bit_cast(u64x2, hi);
+      st_wt(d + 0, l2[0]);
+      st_wt(d + 1, l2[1]);
+      st_wt(d + 2, h2[0]);
+      st_wt(d + 3, h2[1]);
+    } else {
+      store16bf(CAT + r * LD128 + BR * 64 + c0, x);
+    }
   }
   BAR();
   STAMP(5);
 }
 
 // ============================================================== branch backward
-// on entry: dx3 of this branch in ACC (BR == 1) or in the DX3V workspace (BR == 0)
-template <int BR>
+// on entry: dx3 of this branch in ACC (DY == 0), the DX3V workspace (DY == 1) or the hand-off slot W_XB
+// (DY == 2, branch-parallel mode, after the acquire)
+template <int BR, int DY>
 __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);  // also DF0
@@ -687,11 +744,19 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     load16(gm2, c.P + B::o.ln2_w + c0);
     const gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
     const float rstd2 = rs[1], rstd3 = rs[2];
-    if (BR == 1) {
+    if (DY == 0) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
-    } else {
+    } else if (DY == 1) {
       load16(dy, c.wsf(W_DX3V) + ro);
+    } else {  // hand-off slot written by the other workgroup: write-through granules, sc1 loads
+      gu64* src = (gu64*)(c.wsf(W_XB) + ro);
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        const unsigned long long v = ld_wt(src + j / 2);
+        dy[j] = __uint_as_float((uint32_t)v);
+        dy[j + 1] = __uint_as_float((uint32_t)(v >> 32));
+      }
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh3[j];
@@ -859,6 +924,15 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
 
 }  // namespace
 
+template <int BR>
+__device__ void init_copies_branch(const Ctx& c) {
+  init_copies(c, BrC<BR>::dense);
+  init_copies(c, BrC<BR>::vproj);
+  init_copies(c, BrC<BR>::oproj);
+  init_copies(c, BrC<BR>::ff0);
+  init_copies(c, BrC<BR>::ff3);
+}
+
 __device__ void init_copies_all(const Ctx& c) {
   init_copies(c, BrC<0>::dense);
   init_copies(c, BrC<0>::vproj);
@@ -874,9 +948,14 @@ __device__ void init_copies_all(const Ctx& c) {
   init_copies(c, MFC2);
 }
 
-__global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int cid = blockIdx.x;
+// ROLE -1: the whole model in one workgroup per client.  Branch-parallel mode (two workgroups per
+// client, co-resident): ROLE 0 = vitals branch + head, ROLE 1 = labs branch.  Per step the labs
+// workgroup hands its branch output to ROLE 0 (flag 0) and gets d(output) back (flag 1, which also
+// carries the NaN abort); ROLE 0 publishes that gradient BEFORE its dWf1 update and its own branch
+// backward, so the two branch backwards overlap.
+template <int ROLE>
+__device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, unsigned char* smem) {
+  constexpr bool DO0 = ROLE != 1, DO1 = ROLE != 0, HEAD = ROLE != 1;
   Ctx c;
   c.smem = smem;
   c.P = (gf*)(a.params + (long)cid * NPARAM);
@@ -895,15 +974,31 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
   if (stamps && blockIdx.x == 0 && threadIdx.x == 0) t_prev = __builtin_amdgcn_s_memrealtime();
 
   // ---- init: zero Adam moments, bf16 weight copies (padding zeroed first), LDS ----
-  for (int i = tid; i < NPARAM; i += NT) {
-    c.M[i] = 0.f;
-    c.V[i] = 0.f;
+  {  // parameter / copy ranges owned by this workgroup
+    const int p_lo = DO0 ? 0 : OV.size, p_hi = HEAD ? NPARAM : FC1_W;
+    const int b_lo = DO0 ? 0 : BRW_SIZE, b_hi = HEAD ? BF_TOTAL : 2 * BRW_SIZE;
+    for (int i = p_lo + tid; i < p_hi; i += NT) {
+      if (ROLE == 0 && i >= OV.size && i < FC1_W) continue;  // labs params belong to ROLE 1
+      c.M[i] = 0.f;
+      c.V[i] = 0.f;
+    }
+    for (int i = b_lo + tid; i < b_hi; i += NT) {
+      if (ROLE == 0 && i >= BRW_SIZE && i < 2 * BRW_SIZE) continue;
+      c.BF[i] = 0;
+    }
   }
-  for (int i = tid; i < BF_TOTAL; i += NT) c.BF[i] = 0;
   for (int i = tid; i < S_TOTAL / 4; i += NT) ((float*)smem)[i] = 0.f;
   __syncthreads();
-  init_copies_all(c);
+  if (DO0) init_copies_branch<0>(c);
+  if (DO1) init_copies_branch<1>(c);
+  if (HEAD) {
+    init_copies(c, MFC1);
+    init_copies(c, MFC2);
+  }
   __syncthreads();
+  gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * 4 : nullptr);  // [0] fwd hand-off, [1] bwd, [2] timeout
+  uint32_t* bcast = (uint32_t*)(smem + S_RED) + 12;
+  bool timed_out = false;
 
   const int nd = a.nd[cid];
   const int BS = a.batch;
@@ -945,15 +1040,49 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = q * 8 + j;
-          s.xin[0][j] = (s.valid && col < D_V) ? row[col] : 0.f;
-          s.xin[1][j] = (s.valid && col < D_L) ? row[D_V + col] : 0.f;
+          s.xin[0][j] = (DO0 && s.valid && col < D_V) ? row[col] : 0.f;
+          s.xin[1][j] = (DO1 && s.valid && col < D_L) ? row[D_V + col] : 0.f;
         }
-        if (q == 0) LAB[r] = s.valid ? row[ROW - 1] : 0.f;
+        if (HEAD && q == 0) LAB[r] = s.valid ? row[ROW - 1] : 0.f;
       }
       const AdamK K = s.K;
 
-      fwd_branch<0>(c, s, stamps, t_prev);
-      fwd_branch<1>(c, s, stamps, t_prev);
+      if (DO0) fwd_branch<0>(c, s, stamps, t_prev);
+      if (ROLE == -1) fwd_branch<1>(c, s, stamps, t_prev);
+      if (ROLE == 1) {
+        fwd_branch<1, true>(c, s, stamps, t_prev);
+        xwg_publish(c, xflag, (uint32_t)step);
+        const uint32_t v = xwg_wait(c, xflag + 1, (uint32_t)step, 1, xflag + 2, bcast);
+        if (v == 0xFFFFFFFFu) {
+          timed_out = true;
+          failed = true;
+          break;
+        }
+        if (v & 1u) {  // the head saw a NaN loss: the client's round fails
+          failed = true;
+          break;
+        }
+        bwd_branch<1, 2>(c, s, stamps, t_prev);
+        c.full_sync();
+        continue;
+      }
+      if (ROLE == 0) {  // labs branch output -> CAT[:, 64:128]
+        const uint32_t v = xwg_wait(c, xflag, (uint32_t)step, 0, xflag + 2, bcast);
+        if (v == 0xFFFFFFFFu) {
+          timed_out = true;
+          failed = true;
+          break;
+        }
+        gu64* src = (gu64*)((gu16*)c.wsf(W_XF) + opaque(r * 64 + c0));
+        u64x2 lo, hi;
+        lo[0] = ld_wt(src + 0);
+        lo[1] = ld_wt(src + 1);
+        hi[0] = ld_wt(src + 2);
+        hi[1] = ld_wt(src + 3);
+        *(LDS_AS s8v*)(CAT + r * LD128 + 64 + c0) = __builtin_bit_cast(s8v, lo);
+        *(LDS_AS s8v*)(CAT + r * LD128 + 64 + c0 + 8) = __builtin_bit_cast(s8v, hi);
+        BAR();
+      }
       // =============================== head forward + loss ===============================
       WFr<64, 128> wf1;
       wload(wf1, c.BF + WFF1, c.lane);
@@ -1029,7 +1158,10 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
         if (loss != loss) failed = true;  // uniform across the workgroup
         else epoch_loss += loss;
       }
-      if (failed) break;
+      if (failed) {
+        if (ROLE == 0) xwg_publish(c, xflag + 1, ((uint32_t)step << 1) | 1u);  // release the labs workgroup
+        break;
+      }
       // =============================== head backward ===============================
       {
         float sm = 0.f;
@@ -1069,20 +1201,45 @@ __global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
       BAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1b);  // dcat[:, 64:128] (kept in ACC for the labs branch)
       BAR();
+      if (ROLE == 0) {  // hand d(labs output) to the labs workgroup before the head's dWf1 update
+        gu64* d = (gu64*)(c.wsf(W_XB) + opaque(r * 64 + c0));
+#pragma unroll
+        for (int j = 0; j < 16; j += 2)
+          st_wt(d + j / 2, ((unsigned long long)__float_as_uint(ACC[r * LDACC + c0 + j + 1]) << 32) |
+                               __float_as_uint(ACC[r * LDACC + c0 + j]));
+        xwg_publish(c, xflag + 1, (uint32_t)step << 1);
+      }
       gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, MFC1, K);  // dWf1 = dy1^T cat
       BAR();
       STAMP(9);
-      bwd_branch<1>(c, s, stamps, t_prev);
-      bwd_branch<0>(c, s, stamps, t_prev);
+      if (ROLE == -1) bwd_branch<1, 0>(c, s, stamps, t_prev);
+      bwd_branch<0, 1>(c, s, stamps, t_prev);
       // publish this step's Adam writes (bf16 weight copies, params) to every wave of the workgroup
       c.full_sync();
       r = c.r;
       q = c.q;
       c0 = q * 16;
     }
-    if (tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
+    if (HEAD && tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
   }
-  if (tid == 0) a.ok[cid] = failed ? 0 : 1;
+  if (HEAD && tid == 0) {
+    const bool tmo = timed_out || (xflag && __hip_atomic_load(xflag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    a.ok[cid] = tmo ? -1 : (failed ? 0 : 1);
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_tf_train(AflTfTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  train_body<-1>(a, blockIdx.x, smem);
+}
+
+// branch-parallel: workgroups 2c (vitals + head) and 2c+1 (labs) of client c
+__global__ void __launch_bounds__(NT) k_tf_train_bp(AflTfTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (blockIdx.x & 1)
+    train_body<1>(a, blockIdx.x >> 1, smem);
+  else
+    train_body<0>(a, blockIdx.x >> 1, smem);
 }
 
 // ================================================================================================
@@ -1240,9 +1397,20 @@ int afl_tf_param_count() { return NPARAM; }
 
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
   if (a->batch > BM || a->batch < 1) return -1;
-  if (hipFuncSetAttribute((const void*)k_tf_train, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess)
-    return -2;
-  hipLaunchKernelGGL(k_tf_train, dim3(a->C), dim3(NT), S_TOTAL, s, *a);
+  const void* fn = a->sync ? (const void*)k_tf_train_bp : (const void*)k_tf_train;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess) return -2;
+  if (a->sync) {
+    // the two workgroups of a client spin on each other: every workgroup must be resident at once
+    // (one 158 KB-LDS workgroup per CU); the caller zeroes the sync words before every launch
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -3;
+    if (2 * a->C > cus) return -4;
+    hipLaunchKernelGGL(k_tf_train_bp, dim3(2 * a->C), dim3(NT), S_TOTAL, s, *a);
+  } else {
+    hipLaunchKernelGGL(k_tf_train, dim3(a->C), dim3(NT), S_TOTAL, s, *a);
+  }
   return 0;
 }
 

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--clients", type=int, default=1)
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--opt-mode", type=int, default=0, help="1 = SGD test mode (no Adam moments)")
+    ap.add_argument("--split", type=int, default=-1, help="1 = branch-parallel launch, 0 = one workgroup, -1 = auto")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ds = synthetic_icu(60000, seed=3)
@@ -39,18 +40,20 @@ def main():
                           for i in range(args.clients)]).to(dev)
     plan = make_plan(rows.shape[0], [args.rows] * args.clients, args.epochs, torch.Generator().manual_seed(0), "cpu")
     order = plan.order.to(dev)
-    T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)))
+    split = None if args.split < 0 else bool(args.split)
+    T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
+                    split=split)
     torch.cuda.synchronize()
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
-                    opt_mode=args.opt_mode, stamps=stamps)
+                    opt_mode=args.opt_mode, stamps=stamps, split=split)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     steps = args.epochs * ((args.rows + 127) // 128)
     st = stamps.cpu().tolist()
     tot = sum(st)
-    out = {"opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
+    out = {"split": args.split, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
            "us_per_step_stamped": tot * 0.01 / steps, "phases_us_per_step": {}}
     for i, v in enumerate(st):
         if v:
