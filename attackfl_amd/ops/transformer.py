@@ -20,29 +20,31 @@ M32 = 0xFFFFFFFF
 
 
 # ------------------------------------------------------------------------------- device entry points
-def _split_ok(C: int, dev) -> bool:
-    """Branch-parallel launch needs both workgroups of every client resident (one per CU)."""
-    return 2 * C <= torch.cuda.get_device_properties(dev).multi_processor_count
+def auto_split(C: int, dev) -> int:
+    """Workgroups per client for the fused trainer: 3 (head | vitals | labs) when every workgroup of
+    every client fits on the device at once (one per CU), else 2, else 1."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return 3 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                   lr: float, seeds: Sequence[int], opt_mode: int = 0, stamps: torch.Tensor = None,
-                  split: bool = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                  split: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Train all clients in place. Returns (ok [C] int32 on host, losses [C, E] fp32 on host).
 
-    ``split``: branch-parallel launch (vitals branch + head and labs branch of a client on two
-    workgroups that hand activations/gradients to each other every step); default: whenever all
-    2*C workgroups fit on the device at once.
+    ``split``: workgroups per client — 1 (whole model in one workgroup), 2 (vitals branch + head |
+    labs branch) or 3 (head | vitals | labs); the workgroups of a client hand activations and
+    gradients to each other every step.  Default: ``auto_split``.
     ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
     workgroup 0, summed over all steps (diagnostics)."""
     dev = params.device
     C = params.shape[0]
     if split is None:
-        split = C > 0 and _split_ok(C, dev)
+        split = auto_split(C, dev) if C > 0 else 1
     nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
     seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
     ok, losses = native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
-                                   int(batch), float(lr), int(opt_mode), stamps, bool(split))
+                                   int(batch), float(lr), int(opt_mode), stamps, int(split))
     ok = ok.cpu()
     if bool((ok < 0).any()):
         raise RuntimeError("fused trainer: a cross-workgroup hand-off timed out (workgroups not co-resident?)")

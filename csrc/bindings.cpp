@@ -224,7 +224,7 @@ void hyper_adam_outer(torch::Tensor W, torch::Tensor b, torch::Tensor m, torch::
 
 std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
-                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, bool split) {
+                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
   check_dev(params, "params", torch::kFloat32);
   check_dev(rows, "rows", torch::kFloat32);
   check_dev(order, "order", torch::kInt32);
@@ -263,13 +263,14 @@ std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, to
     a.stamps = (uint64_t*)stamps->data_ptr<int64_t>();
   }
   a.sync = nullptr;
+  a.split = (int)std::max<int64_t>(1, split);
   torch::Tensor sync;
-  if (split) {  // branch-parallel launch: zeroed hand-off words, fresh every call
+  if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
     sync = torch::zeros({(long)C * 4}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
   const int rc = afl_tf_train(&a, cur());
-  TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs 2 workgroups per client resident at once (2*C <= CUs)");
+  TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
   TORCH_CHECK(rc == 0, "tf_train launch failed (", rc, ")");
   AFL_CHECK_LAUNCH();
   return {ok, losses};
@@ -309,7 +310,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hyper_adam_outer", &hyper_adam_outer);
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
-        py::arg("stamps") = py::none(), py::arg("split") = false);
+        py::arg("stamps") = py::none(), py::arg("split") = 1);
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);

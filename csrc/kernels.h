@@ -50,7 +50,8 @@ struct AflTfTrainArgs {
   float lr;
   int opt_mode;  // 0 = Adam (reference), 1 = SGD (test hook: exposes raw gradients)
   uint64_t* stamps;  // optional per-phase timers (AFL_TF_STAMPS builds), may be null
-  uint32_t* sync;    // [C][4] zeroed words: non-null = branch-parallel launch (2 workgroups per client)
+  uint32_t* sync;    // [C][4] zeroed hand-off words (branch-parallel launches)
+  int split;         // workgroups per client: 1, 2 (vitals+head | labs), 3 (head | vitals | labs)
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);

@@ -113,9 +113,12 @@ constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
 // branch-parallel mode hand-off slots (labs workgroup <-> vitals+head workgroup of one client)
-constexpr long W_XF = W_DX3V + BM * 64;  // labs branch output, bf16 [128][64]
-constexpr long W_XB = W_XF + BM * 32;    // d(labs branch output), fp32 [128][64]
-constexpr long WS_FLOATS = W_XB + BM * 64;
+constexpr long W_XF = W_DX3V + BM * 64;  // branch outputs, bf16 [2][128][64] (vitals, labs)
+constexpr long W_XB = W_XF + 2 * BM * 32;  // d(branch outputs), fp32 [2][128][64]
+constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
+// hand-off words per client: [0] vitals output ready, [1] labs output ready, [2] d(outputs) ready
+// (value step << 1 | NaN abort), [3] timeout
+constexpr int XF_VIT = 0, XF_LAB = 1, XF_BWD = 2, XF_TMO = 3;
 
 struct AdamK {
   float lr_bc1, rsqrt_bc2;
@@ -477,14 +480,16 @@ __device__ __forceinline__ void xwg_publish(const Ctx& c, gu32* flag, uint32_t v
   if (c.tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 constexpr long XWG_MAX_SPINS = 1L << 22;  // ~seconds: a missing partner becomes an error, not a hang
-// returns the flag value once (value >> shift) >= want, or 0xFFFFFFFF on timeout (also raises *tmo)
-__device__ __forceinline__ uint32_t xwg_wait(const Ctx& c, gu32* flag, uint32_t want, int shift, gu32* tmo,
-                                             uint32_t* bcast) {
+// waits until (flag_a >> shift) >= want and (flag_b >> shift) >= want (pass the same word twice for
+// one); returns flag_a's value, or 0xFFFFFFFF on timeout (also raises *tmo)
+__device__ __forceinline__ uint32_t xwg_wait(const Ctx& c, gu32* flag_a, gu32* flag_b, uint32_t want, int shift,
+                                             gu32* tmo, uint32_t* bcast) {
   if (c.wave == 0) {
     uint32_t v = 0;
     for (long spins = 0;; ++spins) {
-      v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((v >> shift) >= want) break;
+      v = __hip_atomic_load(flag_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t w = flag_b == flag_a ? v : __hip_atomic_load(flag_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v >> shift) >= want && (w >> shift) >= want) break;
       if (spins > XWG_MAX_SPINS) {
         v = 0xFFFFFFFFu;
         if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -542,11 +547,23 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-// per-phase wall-clock stamps (s_memrealtime, 100 MHz) of workgroup 0, accumulated over all steps;
-// only when the caller passes a stamps buffer (diagnostics; one uniform branch per phase otherwise)
+// ACC row r, columns c0..c0+15 (fp32) -> hand-off slot (write-through 8-byte granules)
+__device__ __forceinline__ void put_grad(const Ctx& c, long slot, int r, int c0) {
+  gu64* d = (gu64*)(c.wsf(slot) + opaque(r * 64 + c0));
+  const float* acc = c.acc() + r * LDACC + c0;
+#pragma unroll
+  for (int j = 0; j < 16; j += 2)
+    st_wt(d + j / 2, ((unsigned long long)__float_as_uint(acc[j + 1]) << 32) | __float_as_uint(acc[j]));
+}
+
+
+// per-phase wall-clock stamps (s_memrealtime, 100 MHz) of ONE workgroup (index in stamps[63]),
+// accumulated over all steps; only when the caller passes a stamps buffer (diagnostics; one uniform
+// branch per phase otherwise)
+#define stamp_block ((unsigned)stamps[63])
 #define STAMP(id)                                                                   \
   do {                                                                              \
-    if (stamps && blockIdx.x == 0 && threadIdx.x == 0) {                           \
+    if (stamps && blockIdx.x == stamp_block && threadIdx.x == 0) {                 \
       uint64_t now_ = __builtin_amdgcn_s_memrealtime();                            \
       stamps[id] += now_ - t_prev;                                                  \
       t_prev = now_;                                                                \
@@ -702,7 +719,7 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = x[j] * g3[j] + b3[j];
     if (XCH) {
-      gu64* d = (gu64*)((gu16*)c.wsf(W_XF) + ro);
+      gu64* d = (gu64*)((gu16*)c.wsf(W_XF + BR * BM * 32) + ro);
       const s8v lo = pack8bf(x), hi = pack8bf(x + 8);
       const auto l2 = __builtin_bit_cast(u64x2, lo), h2 = __builtin_bit_cast(u64x2, hi);
       st_wt(d + 0, l2[0]);
@@ -750,7 +767,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     } else if (DY == 1) {
       load16(dy, c.wsf(W_DX3V) + ro);
     } else {  // hand-off slot written by the other workgroup: write-through granules, sc1 loads
-      gu64* src = (gu64*)(c.wsf(W_XB) + ro);
+      gu64* src = (gu64*)(c.wsf(W_XB + BR * BM * 64) + ro);
 #pragma unroll
       for (int j = 0; j < 16; j += 2) {
         const unsigned long long v = ld_wt(src + j / 2);
@@ -948,14 +965,19 @@ __device__ void init_copies_all(const Ctx& c) {
   init_copies(c, MFC2);
 }
 
-// ROLE -1: the whole model in one workgroup per client.  Branch-parallel mode (two workgroups per
-// client, co-resident): ROLE 0 = vitals branch + head, ROLE 1 = labs branch.  Per step the labs
-// workgroup hands its branch output to ROLE 0 (flag 0) and gets d(output) back (flag 1, which also
-// carries the NaN abort); ROLE 0 publishes that gradient BEFORE its dWf1 update and its own branch
-// backward, so the two branch backwards overlap.
+// ROLE -1: the whole model in one workgroup per client.  Branch-parallel modes (co-resident
+// workgroups per client exchanging activations / gradients every step through hand-off slots):
+//   2 workgroups: ROLE 0 = vitals branch + head, ROLE 1 = labs branch;
+//   3 workgroups: ROLE 2 = vitals branch, ROLE 1 = labs branch, ROLE 3 = head.
+// A branch-only workgroup publishes its output (flag XF_VIT / XF_LAB) and waits for d(output)
+// (flag XF_BWD, which also carries the NaN abort); the head publishes both gradients BEFORE its
+// own dWf1 update (and, in the 2-workgroup mode, before the vitals backward) so they overlap.
 template <int ROLE>
 __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, unsigned char* smem) {
-  constexpr bool DO0 = ROLE != 1, DO1 = ROLE != 0, HEAD = ROLE != 1;
+  constexpr bool DO0 = ROLE == -1 || ROLE == 0 || ROLE == 2;
+  constexpr bool DO1 = ROLE == -1 || ROLE == 1;
+  constexpr bool HEAD = ROLE == -1 || ROLE == 0 || ROLE == 3;
+  constexpr int BONLY = ROLE == 1 ? 1 : (ROLE == 2 ? 0 : -1);  // branch of a branch-only workgroup
   Ctx c;
   c.smem = smem;
   c.P = (gf*)(a.params + (long)cid * NPARAM);
@@ -971,20 +993,21 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
   const int tid = c.tid;
   uint64_t* stamps = a.stamps;
   uint64_t t_prev = 0;
-  if (stamps && blockIdx.x == 0 && threadIdx.x == 0) t_prev = __builtin_amdgcn_s_memrealtime();
+  if (stamps && blockIdx.x == stamp_block && threadIdx.x == 0) t_prev = __builtin_amdgcn_s_memrealtime();
 
   // ---- init: zero Adam moments, bf16 weight copies (padding zeroed first), LDS ----
-  {  // parameter / copy ranges owned by this workgroup
-    const int p_lo = DO0 ? 0 : OV.size, p_hi = HEAD ? NPARAM : FC1_W;
-    const int b_lo = DO0 ? 0 : BRW_SIZE, b_hi = HEAD ? BF_TOTAL : 2 * BRW_SIZE;
-    for (int i = p_lo + tid; i < p_hi; i += NT) {
-      if (ROLE == 0 && i >= OV.size && i < FC1_W) continue;  // labs params belong to ROLE 1
-      c.M[i] = 0.f;
-      c.V[i] = 0.f;
-    }
-    for (int i = b_lo + tid; i < b_hi; i += NT) {
-      if (ROLE == 0 && i >= BRW_SIZE && i < 2 * BRW_SIZE) continue;
-      c.BF[i] = 0;
+  {  // parameter / copy ranges owned by this workgroup: vitals, labs, head
+    const int pr[4] = {0, OV.size, FC1_W, NPARAM};
+    const int br[4] = {0, BRW_SIZE, 2 * BRW_SIZE, BF_TOTAL};
+    const bool own[3] = {DO0, DO1, HEAD};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (!own[k]) continue;
+      for (int i = pr[k] + tid; i < pr[k + 1]; i += NT) {
+        c.M[i] = 0.f;
+        c.V[i] = 0.f;
+      }
+      for (int i = br[k] + tid; i < br[k + 1]; i += NT) c.BF[i] = 0;
     }
   }
   for (int i = tid; i < S_TOTAL / 4; i += NT) ((float*)smem)[i] = 0.f;
@@ -996,7 +1019,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
     init_copies(c, MFC2);
   }
   __syncthreads();
-  gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * 4 : nullptr);  // [0] fwd hand-off, [1] bwd, [2] timeout
+  gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * 4 : nullptr);  // XF_* words
   uint32_t* bcast = (uint32_t*)(smem + S_RED) + 12;
   bool timed_out = false;
 
@@ -1047,12 +1070,12 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       }
       const AdamK K = s.K;
 
-      if (DO0) fwd_branch<0>(c, s, stamps, t_prev);
+      if (ROLE == -1 || ROLE == 0) fwd_branch<0>(c, s, stamps, t_prev);
       if (ROLE == -1) fwd_branch<1>(c, s, stamps, t_prev);
-      if (ROLE == 1) {
-        fwd_branch<1, true>(c, s, stamps, t_prev);
-        xwg_publish(c, xflag, (uint32_t)step);
-        const uint32_t v = xwg_wait(c, xflag + 1, (uint32_t)step, 1, xflag + 2, bcast);
+      if (BONLY >= 0) {  // branch-only workgroup: forward, hand-off, wait, backward
+        fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev);
+        xwg_publish(c, xflag + (BONLY == 1 ? XF_LAB : XF_VIT), (uint32_t)step);
+        const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
           failed = true;
@@ -1062,25 +1085,30 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
           failed = true;
           break;
         }
-        bwd_branch<1, 2>(c, s, stamps, t_prev);
+        STAMP(21);
+        bwd_branch<BONLY < 0 ? 0 : BONLY, 2>(c, s, stamps, t_prev);
         c.full_sync();
         continue;
       }
-      if (ROLE == 0) {  // labs branch output -> CAT[:, 64:128]
-        const uint32_t v = xwg_wait(c, xflag, (uint32_t)step, 0, xflag + 2, bcast);
+      if (ROLE == 0 || ROLE == 3) {  // branch outputs from the other workgroup(s) -> CAT
+        const uint32_t v = xwg_wait(c, xflag + (ROLE == 3 ? XF_VIT : XF_LAB), xflag + XF_LAB, (uint32_t)step, 0,
+                                    xflag + XF_TMO, bcast);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
           failed = true;
           break;
         }
-        gu64* src = (gu64*)((gu16*)c.wsf(W_XF) + opaque(r * 64 + c0));
-        u64x2 lo, hi;
-        lo[0] = ld_wt(src + 0);
-        lo[1] = ld_wt(src + 1);
-        hi[0] = ld_wt(src + 2);
-        hi[1] = ld_wt(src + 3);
-        *(LDS_AS s8v*)(CAT + r * LD128 + 64 + c0) = __builtin_bit_cast(s8v, lo);
-        *(LDS_AS s8v*)(CAT + r * LD128 + 64 + c0 + 8) = __builtin_bit_cast(s8v, hi);
+#pragma unroll
+        for (int br = ROLE == 3 ? 0 : 1; br < 2; ++br) {
+          gu64* src = (gu64*)((gu16*)c.wsf(W_XF + br * BM * 32) + opaque(r * 64 + c0));
+          u64x2 lo, hi;
+          lo[0] = ld_wt(src + 0);
+          lo[1] = ld_wt(src + 1);
+          hi[0] = ld_wt(src + 2);
+          hi[1] = ld_wt(src + 3);
+          *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0) = __builtin_bit_cast(s8v, lo);
+          *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0 + 8) = __builtin_bit_cast(s8v, hi);
+        }
         BAR();
       }
       // =============================== head forward + loss ===============================
@@ -1159,7 +1187,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         else epoch_loss += loss;
       }
       if (failed) {
-        if (ROLE == 0) xwg_publish(c, xflag + 1, ((uint32_t)step << 1) | 1u);  // release the labs workgroup
+        if (ROLE == 0 || ROLE == 3) xwg_publish(c, xflag + XF_BWD, ((uint32_t)step << 1) | 1u);  // release them
         break;
       }
       // =============================== head backward ===============================
@@ -1186,13 +1214,17 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         colsum16(c, 2, d);
       }
       BAR();
-      gemm_pf<64, 64>(c, TB, LD64, wtf1a);                 // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
-      gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
-      if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
+      gemm_pf<64, 64>(c, TB, LD64, wtf1a);  // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
+      if (ROLE == -1) {                     // one workgroup: dWf2 overlaps the dcat GEMMs
+        gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
+        if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
+      }
       WFr<64, 64> wtf1b;
       wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
       BAR();
-      {
+      if (ROLE == 3) {  // vitals gradient -> its hand-off slot
+        put_grad(c, W_XB, r, c0);
+      } else {
         float t[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) t[j] = ACC[r * LDACC + c0 + j];
@@ -1201,19 +1233,17 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       BAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1b);  // dcat[:, 64:128] (kept in ACC for the labs branch)
       BAR();
-      if (ROLE == 0) {  // hand d(labs output) to the labs workgroup before the head's dWf1 update
-        gu64* d = (gu64*)(c.wsf(W_XB) + opaque(r * 64 + c0));
-#pragma unroll
-        for (int j = 0; j < 16; j += 2)
-          st_wt(d + j / 2, ((unsigned long long)__float_as_uint(ACC[r * LDACC + c0 + j + 1]) << 32) |
-                               __float_as_uint(ACC[r * LDACC + c0 + j]));
-        xwg_publish(c, xflag + 1, (uint32_t)step << 1);
+      if (ROLE == 0 || ROLE == 3) {  // hand the gradients over first: the head's own updates overlap
+        put_grad(c, W_XB + BM * 64, r, c0);
+        xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);
+        gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
+        if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       }
       gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, MFC1, K);  // dWf1 = dy1^T cat
       BAR();
       STAMP(9);
       if (ROLE == -1) bwd_branch<1, 0>(c, s, stamps, t_prev);
-      bwd_branch<0, 1>(c, s, stamps, t_prev);
+      if (ROLE == -1 || ROLE == 0) bwd_branch<0, 1>(c, s, stamps, t_prev);
       // publish this step's Adam writes (bf16 weight copies, params) to every wave of the workgroup
       c.full_sync();
       r = c.r;
@@ -1223,7 +1253,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
     if (HEAD && tid == 0) a.losses[(long)cid * a.E + e] = epoch_loss / (float)max(nb_total, 1);
   }
   if (HEAD && tid == 0) {
-    const bool tmo = timed_out || (xflag && __hip_atomic_load(xflag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const bool tmo =
+        timed_out || (xflag && __hip_atomic_load(xflag + XF_TMO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     a.ok[cid] = tmo ? -1 : (failed ? 0 : 1);
   }
 }
@@ -1240,6 +1271,18 @@ __global__ void __launch_bounds__(NT) k_tf_train_bp(AflTfTrainArgs a) {
     train_body<1>(a, blockIdx.x >> 1, smem);
   else
     train_body<0>(a, blockIdx.x >> 1, smem);
+}
+
+// branch-parallel, 3 workgroups per client: 3c (head), 3c+1 (vitals), 3c+2 (labs)
+__global__ void __launch_bounds__(NT) k_tf_train_bp3(AflTfTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int role = blockIdx.x % 3, cid = blockIdx.x / 3;
+  if (role == 0)
+    train_body<3>(a, cid, smem);
+  else if (role == 1)
+    train_body<2>(a, cid, smem);
+  else
+    train_body<1>(a, cid, smem);
 }
 
 // ================================================================================================
@@ -1397,17 +1440,22 @@ int afl_tf_param_count() { return NPARAM; }
 
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
   if (a->batch > BM || a->batch < 1) return -1;
-  const void* fn = a->sync ? (const void*)k_tf_train_bp : (const void*)k_tf_train;
+  const int wgs = a->sync ? a->split : 1;  // workgroups per client
+  if (wgs < 1 || wgs > 3) return -1;
+  const void* fn = wgs == 3 ? (const void*)k_tf_train_bp3 : (wgs == 2 ? (const void*)k_tf_train_bp : (const void*)k_tf_train);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess) return -2;
-  if (a->sync) {
-    // the two workgroups of a client spin on each other: every workgroup must be resident at once
+  if (wgs > 1) {
+    // the workgroups of a client spin on each other: every workgroup must be resident at once
     // (one 158 KB-LDS workgroup per CU); the caller zeroes the sync words before every launch
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return -3;
-    if (2 * a->C > cus) return -4;
-    hipLaunchKernelGGL(k_tf_train_bp, dim3(2 * a->C), dim3(NT), S_TOTAL, s, *a);
+    if (wgs * a->C > cus) return -4;
+    if (wgs == 3)
+      hipLaunchKernelGGL(k_tf_train_bp3, dim3(3 * a->C), dim3(NT), S_TOTAL, s, *a);
+    else
+      hipLaunchKernelGGL(k_tf_train_bp, dim3(2 * a->C), dim3(NT), S_TOTAL, s, *a);
   } else {
     hipLaunchKernelGGL(k_tf_train, dim3(a->C), dim3(NT), S_TOTAL, s, *a);
   }

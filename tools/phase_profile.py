@@ -21,7 +21,8 @@ from attackfl_amd.ops import transformer as T
 NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G4 ffn0+E4", 4: "F:G5 ffn3+E5 LN2/3",
          5: "F:branch tail", 6: "H:fc1+E6", 7: "H:fc2+E7 loss", 8: "H:bwd fc2 dX+E8", 9: "H:dcat+dWf2+dWf1",
          10: "B:E10 LN bwd", 11: "B:A10+G11", 12: "B:E11", 13: "B:G12+dW2", 14: "B:E12 LN1 bwd", 15: "B:G13+dW1",
-         16: "B:E13", 17: "B:G13b+E13b", 18: "B:G14+dWo", 19: "B:E14+dWv+z0", 20: "B:E15+dWd"}
+         16: "B:E13", 17: "B:G13b+E13b", 18: "B:G14+dWo", 19: "B:E14+dWv+z0", 20: "B:E15+dWd",
+         21: "X:publish+wait d(out)"}
 
 
 def main():
@@ -30,7 +31,8 @@ def main():
     ap.add_argument("--clients", type=int, default=1)
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--opt-mode", type=int, default=0, help="1 = SGD test mode (no Adam moments)")
-    ap.add_argument("--split", type=int, default=-1, help="1 = branch-parallel launch, 0 = one workgroup, -1 = auto")
+    ap.add_argument("--split", type=int, default=0, help="workgroups per client (1, 2, 3); 0 = auto")
+    ap.add_argument("--block", type=int, default=0, help="workgroup whose phases are stamped")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ds = synthetic_icu(60000, seed=3)
@@ -40,20 +42,21 @@ def main():
                           for i in range(args.clients)]).to(dev)
     plan = make_plan(rows.shape[0], [args.rows] * args.clients, args.epochs, torch.Generator().manual_seed(0), "cpu")
     order = plan.order.to(dev)
-    split = None if args.split < 0 else bool(args.split)
+    split = None if args.split <= 0 else args.split
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
                     split=split)
     torch.cuda.synchronize()
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
+    stamps[63] = args.block
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
                     opt_mode=args.opt_mode, stamps=stamps, split=split)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     steps = args.epochs * ((args.rows + 127) // 128)
-    st = stamps.cpu().tolist()
+    st = stamps.cpu().tolist()[:63]
     tot = sum(st)
-    out = {"split": args.split, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
+    out = {"split": args.split, "block": args.block, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
            "us_per_step_stamped": tot * 0.01 / steps, "phases_us_per_step": {}}
     for i, v in enumerate(st):
         if v:
