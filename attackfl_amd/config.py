@@ -10,6 +10,8 @@ Extensions (all optional, defaults keep reference behaviour):
   backend: auto | nccl | gloo | loopback
   clients-per-rank: int (packed launcher; 0 = clients / world)
   one-shot-allgather: bool  (IPC xGMI all-gather for small updates on a single node)
+  fedavg-allreduce: auto | true | false  (fedavg without attackers/detection: one all_reduce of
+                            [sum s_i w_i | sum s_i] instead of the update all-gather; auto = world > 1)
   timeout-s: collective timeout (failure detection)
   attackers: {client_index: {mode, round, args}}  (launcher-side attack assignment)
 ``data:``
@@ -23,6 +25,12 @@ Extensions (all optional, defaults keep reference behaviour):
   metrics: path of the JSONL metrics file ('' disables)
   checkpoint-dir: where ``*.pth`` files go (reference: CWD)
   compat-hyper-resume: bool         (True = reproduce reference A-5: a loaded hyper checkpoint is discarded)
+  compat-fltrust: bool              (True = reproduce reference A-10: FLTrust subtracts the global model twice)
+  max-retries: int                  (consecutive failed rounds before the run aborts)
+  trace: bool                       (roctx ranges around every round phase; also ATTACKFL_TRACE=1)
+  fault-inject: [{client, round}]   (NaN-poison a client's model before that training round)
+  save-state: bool                  (write {model}.state.pt + {model}.clients.r{rank}.pt every round)
+  resume: bool                      (continue from those files: counters, RNGs, optimizer moments)
 """
 from __future__ import annotations
 
@@ -63,11 +71,12 @@ REFERENCE_DEFAULTS: Dict[str, Any] = {
 
 EXTENSION_DEFAULTS: Dict[str, Any] = {
     "comm": {"backend": "auto", "address": "", "port": 29517, "clients-per-rank": 0, "one-shot-allgather": False,
-             "timeout-s": 600, "attackers": {}},
+             "fedavg-allreduce": "auto", "timeout-s": 600, "attackers": {}},
     "data": {"synthetic": "auto", "train-size": 60000, "test-size": 10000, "seed": 1234,
              "har-train-size": 2048, "har-test-size": 512, "root": "."},
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
-               "compat-hyper-resume": False},
+               "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
+               "fault-inject": [], "save-state": False, "resume": False},
 }
 
 

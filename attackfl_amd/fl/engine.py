@@ -36,6 +36,7 @@ from ..detect import HyperDetector
 from ..eval import Validation
 from ..models import ParamLayout, build_model
 from ..parallel.comm import Comm, LoopbackComm
+from ..utils import trace
 from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
 from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
@@ -145,6 +146,20 @@ class FLEngine:
         self.round_no = 1
         self.rounds_left = cfg.num_round
         self.history: List[dict] = []
+        if cfg.engine.get("trace", False):
+            trace.enable(True)
+        # fault injection: [{client: i, round: r}] -> client i's model is NaN-poisoned before
+        # its local training of training-round r, which fails that client and retries the FL round
+        self.faults = {(int(f["client"]), int(f["round"])) for f in (cfg.engine.get("fault-inject") or [])}
+        self._phase_t: Dict[str, float] = {}
+        # FedAvg fast path: with no attacker and no detection, the server needs only
+        # sum_i s_i w_i and sum_i s_i -> ONE all_reduce of [P + 3] instead of the [N, P] all-gather
+        fa = str(cfg.comm.get("fedavg-allreduce", "auto")).lower()
+        eligible = (self.mode == "fedavg" and all(ci.attack is None for ci in self.table)
+                    and not cfg.hyper_detection.get("enable", False))
+        self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1))
+        if cfg.engine.get("resume", False):
+            self.load_state()
         self.logger.log_info("### Application start ###\n")
 
     # ------------------------------------------------------------------------------------------
@@ -192,6 +207,64 @@ class FLEngine:
             torch.save(self.hyper.hnet.state_dict(), self._pth(True))
         elif self.global_params is not None:
             torch.save(self.layout.unflatten(self.global_params.detach().cpu()), self._pth(False))
+
+    # ---- resumable run state (new: the reference persists only the model) ----
+    def _state_paths(self):
+        base = os.path.join(self.ckpt_dir, self.model_name)
+        return base + ".state.pt", f"{base}.clients.r{self.rank}.pt"
+
+    def save_state(self) -> None:
+        """Replicated server state (leader) + this rank's client state, loadable with
+        ``torch.load(weights_only=True)``: round counters, RNG states, hypernetwork Adam moments,
+        the genuine pool attackers sample from, and every local client's model and RNG."""
+        os.makedirs(self.ckpt_dir, exist_ok=True)
+        srv_path, cli_path = self._state_paths()
+        if self.leader:
+            v, st, gauss = self.server_rng.getstate()
+            srv = {"round_no": self.round_no, "rounds_left": self.rounds_left, "rng_version": v,
+                   "rng_state": list(st), "rng_gauss": gauss, "selected": list(self.selected),
+                   "global": self.global_params.detach().cpu() if self.global_params is not None else None,
+                   "genuine_pool": self.genuine_pool.detach().cpu() if self.genuine_pool is not None else None}
+            if self.hyper is not None:
+                srv.update(hyper_arena=self.hyper.hnet.arena.detach().cpu(), hyper_m=self.hyper.m.cpu(),
+                           hyper_v=self.hyper.v.cpu(), hyper_step=self.hyper.step)
+            torch.save(srv, srv_path + ".tmp")
+            os.replace(srv_path + ".tmp", srv_path)
+        cli = {"params": self.local_params.detach().cpu(), "index": [lc.info.index for lc in self.local],
+               "training_round": [lc.training_round for lc in self.local],
+               "rng": [[lc.rng.getstate()[0], list(lc.rng.getstate()[1]), lc.rng.getstate()[2]] for lc in self.local]}
+        torch.save(cli, cli_path + ".tmp")
+        os.replace(cli_path + ".tmp", cli_path)
+
+    def load_state(self) -> bool:
+        srv_path, cli_path = self._state_paths()
+        if not os.path.exists(srv_path):
+            return False
+        srv = torch.load(srv_path, weights_only=True, map_location="cpu")
+        self.round_no = int(srv["round_no"])
+        self.rounds_left = int(srv["rounds_left"])
+        self.server_rng.setstate((srv["rng_version"], tuple(srv["rng_state"]), srv["rng_gauss"]))
+        if srv.get("selected"):
+            self.selected = list(srv["selected"])
+            self._selection_done = True
+        if srv.get("global") is not None:
+            self.global_params = srv["global"].to(self.device)
+        if srv.get("genuine_pool") is not None:
+            self.genuine_pool = srv["genuine_pool"].to(self.device)
+        if self.hyper is not None and "hyper_m" in srv:
+            with torch.no_grad():
+                self.hyper.hnet.arena.copy_(srv["hyper_arena"])
+            self.hyper.m.copy_(srv["hyper_m"])
+            self.hyper.v.copy_(srv["hyper_v"])
+            self.hyper.step = int(srv["hyper_step"])
+        if os.path.exists(cli_path):
+            cli = torch.load(cli_path, weights_only=True, map_location="cpu")
+            self.local_params.copy_(cli["params"].to(self.device))
+            for lc, tr, rs in zip(self.local, cli["training_round"], cli["rng"]):
+                lc.training_round = int(tr)
+                lc.rng.setstate((rs[0], tuple(rs[1]), rs[2]))
+        print_with_color(f"Resumed run state from {srv_path} at round {self.round_no}", "yellow")
+        return True
 
     # ------------------------------------------------------------------------------------------
     # START
@@ -244,6 +317,10 @@ class FLEngine:
             p = self._start_params(i)
             if p is not None:
                 self.local_params[j].copy_(p)
+            if (i, lc.training_round) in self.faults:
+                self.local_params[j, 0] = float("nan")
+                print_with_color(f"[fault-inject] client {i} poisoned with NaN (training round {lc.training_round})",
+                                 "red")
             g = genuine.get(i)
             if lc.info.attack is not None and g is not None and g.shape[0] > 0:
                 lc.genuine = g
@@ -352,10 +429,14 @@ class FLEngine:
         if self.verbose:
             print_with_color(f"Start training round {self.round_no}", "yellow")
         self._attack_info = None
-        genuine = self._genuine_for_attackers()
-        block = self._local_work(genuine)
-        self._sync()
+        with trace.range("fl/local"):
+            genuine = self._genuine_for_attackers()
+            block = self._local_work(genuine)
+            self._sync()
         t1 = time.perf_counter()
+        if self.fast_fedavg:
+            return self._finish_fedavg_allreduce(block, t0, t1)
+        trace.push("fl/gather")
         allb = self.comm.all_gather_rows(block)                        # [world*slots, P+META]
         rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
         idx = torch.tensor(rows, device=allb.device, dtype=torch.long)
@@ -363,6 +444,7 @@ class FLEngine:
         U = sel[:, :self.P].contiguous()
         meta = sel[:, self.P:].float().cpu()
         self._sync()
+        trace.pop()
         t2 = time.perf_counter()
         results = meta[:, 1] > 0.5
         sizes = meta[:, 2].clone()
@@ -373,11 +455,13 @@ class FLEngine:
         if not round_ok:
             stored = int(torch.nonzero(~results)[0, 0])
         snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) else None
-        info = self._aggregate(U, sizes, attackers, round_ok)
+        with trace.range("fl/aggregate"):
+            info = self._aggregate(U, sizes, attackers, round_ok)
+            self._sync()
         if info.get("agg_failed"):
             round_ok = False
-        self._sync()
         t3 = time.perf_counter()
+        trace.push("fl/validate")
 
         # ---- leader: detection + validation; control broadcast ----
         removed: List[int] = []
@@ -403,6 +487,7 @@ class FLEngine:
         if self.world > 1:
             self.comm.broadcast_(ctrl, src=0)
         ctrl = ctrl.cpu()
+        trace.pop()
         round_ok = bool(ctrl[0] > 0.5)
         removed = [int(ctrl[2 + k]) for k in range(int(ctrl[1]))]
         if removed:
@@ -418,8 +503,13 @@ class FLEngine:
         self.genuine_pool = U[keep].clone() if keep else None
 
         if round_ok:
-            self.save_checkpoint()
-            self.rounds_left -= 1
+            with trace.range("fl/checkpoint"):
+                self.save_checkpoint()
+                self.rounds_left -= 1
+                if self.cfg.engine.get("save-state", False):
+                    self.round_no += 1
+                    self.save_state()
+                    self.round_no -= 1
         elif self.verbose:
             print_with_color("Training failed!", "yellow")
         rec = {"round": self.round_no, "ok": round_ok, "metric": metric, "t_local": t1 - t0, "t_gather": t2 - t1,
@@ -428,6 +518,53 @@ class FLEngine:
         if self._attack_info:
             rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
         rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list))})
+        self.metrics.write(rec)
+        self.history.append(rec)
+        if round_ok:
+            self.round_no += 1
+        return rec
+
+    def _finish_fedavg_allreduce(self, block: torch.Tensor, t0: float, t1: float) -> dict:
+        """FedAvg round over one all_reduce: [sum s_i w_i | sum s_i | #failed | #reported] (fp64)."""
+        P = self.P
+        present = block[:, P] > 0.5
+        size = torch.where(present, block[:, P + 2], torch.zeros_like(block[:, P + 2])).double()
+        red = torch.zeros(P + 3, dtype=torch.float64, device=block.device)
+        red[:P] = (size[:, None] * block[:, :P].double()).sum(0)
+        red[P] = size.sum()
+        red[P + 1] = (present & (block[:, P + 1] < 0.5)).double().sum()
+        red[P + 2] = present.double().sum()
+        with trace.range("fl/allreduce"):
+            if self.world > 1:
+                self.comm.all_reduce_(red)
+            self._sync()
+        t2 = time.perf_counter()
+        round_ok = int(red[P + 1].item()) == 0 and int(red[P + 2].item()) == len(self.selected)
+        if round_ok:
+            self.global_params = (red[:P] / red[P]).to(torch.float32)
+        t3 = time.perf_counter()
+        metric = float("nan")
+        with trace.range("fl/validate"):
+            if self.leader and self.validation is not None and round_ok:
+                round_ok, metric = self.validation.test(self.global_params)
+            ctrl = torch.tensor([1.0 if round_ok else 0.0], dtype=torch.float64, device=self.device)
+            if self.world > 1:
+                self.comm.broadcast_(ctrl, src=0)
+            round_ok = bool(ctrl.item() > 0.5)
+        t4 = time.perf_counter()
+        if round_ok:
+            with trace.range("fl/checkpoint"):
+                self.save_checkpoint()
+                self.rounds_left -= 1
+                if self.cfg.engine.get("save-state", False):
+                    self.round_no += 1
+                    self.save_state()
+                    self.round_no -= 1
+        elif self.verbose:
+            print_with_color("Training failed!", "yellow")
+        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, "t_local": t1 - t0, "t_gather": t2 - t1,
+               "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
+               "n_selected": len(self.selected), "removed": [], "path": "fedavg-allreduce"}
         self.metrics.write(rec)
         self.history.append(rec)
         if round_ok:

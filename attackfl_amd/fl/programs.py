@@ -16,6 +16,7 @@ Model math mirrors ``src/Model.py:27-88`` (CNN), ``91-163`` (RNN), ``418-458`` (
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Sequence, Tuple
 
 import torch
@@ -380,7 +381,8 @@ class ProgramRunner:
 
     def __init__(self, prog: _Program, use_graph: bool = True):
         self.prog = prog
-        self.use_graph = use_graph and prog.device.type == "cuda"
+        # AFL_SYNC_CHECK=1 (synchronise + check after every native launch) cannot run inside a capture
+        self.use_graph = use_graph and prog.device.type == "cuda" and os.environ.get("AFL_SYNC_CHECK") != "1"
 
     def train(self, table, params: torch.Tensor, plan, lr: float, seeds: Sequence[int], sgd_lr: float = 0.0,
               max_steps: int = None) -> Tuple[torch.Tensor, torch.Tensor]:

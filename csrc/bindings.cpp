@@ -13,10 +13,23 @@ namespace {
 hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 
 // surface launch-configuration errors at the call that caused them
+// AFL_SYNC_CHECK=1: synchronise after every launch so an asynchronous fault is reported at the op
+// that caused it (debug mode; the GPU counterpart of HIP_LAUNCH_BLOCKING for this extension)
+bool sync_check() {
+  static const bool on = [] {
+    const char* e = getenv("AFL_SYNC_CHECK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 #define AFL_CHECK_LAUNCH()                                                              \
   do {                                                                                 \
     hipError_t e_ = hipGetLastError();                                                 \
     TORCH_CHECK(e_ == hipSuccess, "HIP launch failed: ", hipGetErrorString(e_));       \
+    if (sync_check()) {                                                                \
+      e_ = hipDeviceSynchronize();                                                     \
+      TORCH_CHECK(e_ == hipSuccess, "HIP kernel failed: ", hipGetErrorString(e_));     \
+    }                                                                                  \
   } while (0)
 
 void check_dev(const torch::Tensor& t, const char* name, c10::ScalarType dt) {

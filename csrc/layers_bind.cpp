@@ -16,6 +16,14 @@ hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 
 void ok(int e, const char* what) {
   TORCH_CHECK(e == 0, what, " launch failed: ", hipGetErrorString((hipError_t)e));
+  static const bool sync = [] {  // AFL_SYNC_CHECK=1: report asynchronous faults at the faulting op
+    const char* v = getenv("AFL_SYNC_CHECK");
+    return v && v[0] == '1';
+  }();
+  if (sync) {
+    const hipError_t s = hipDeviceSynchronize();
+    TORCH_CHECK(s == hipSuccess, what, " kernel failed: ", hipGetErrorString(s));
+  }
 }
 
 void dev(const torch::Tensor& t, const char* n, c10::ScalarType dt = torch::kFloat32) {

@@ -178,3 +178,65 @@ def test_classic_server_and_clients(tmp_path):
                 p.kill()
     assert os.path.exists(os.path.join(tmp_path, "TransformerModel.pth"))
     assert open(os.path.join(tmp_path, "app.log")).read().count("ROC_AUC") == 2
+
+
+def test_fault_injection_retries_round(tmp_path):
+    # (at training round 1 there is no global model yet, so a poisoned client would keep its NaN model
+    # and fail every retry — the reference's persistent-client semantics; inject from round 2 on)
+    d = _cfg(tmp_path, server__num_round=3)
+    d["engine"]["fault-inject"] = [{"client": 2, "round": 2}]
+    eng = FLEngine(from_dict(d), device="cpu", verbose=False)
+    hist = eng.run()
+    assert [r["ok"] for r in hist] == [True, False, True, True]   # round 2 retried once
+    assert hist[1]["round"] == hist[2]["round"] == 2
+
+
+@pytest.mark.parametrize("mode", ["fedavg", "hyper"])
+def test_save_state_resume_is_exact(tmp_path, mode):
+    """4 rounds in one run == 2 rounds, then a fresh engine resuming from the state files for 2 more."""
+    full = tmp_path / "full"
+    d = _cfg(full, server__num_round=4, server__mode=mode)
+    eng = FLEngine(from_dict(d), device="cpu", verbose=False)
+    eng.run()
+    name = "TransformerModel_hyper_4.pth" if mode == "hyper" else "TransformerModel.pth"
+    ref = torch.load(os.path.join(full, name), weights_only=True)
+
+    part = tmp_path / "part"
+    d = _cfg(part, server__num_round=4, server__mode=mode)
+    d["engine"]["save-state"] = True
+    eng = FLEngine(from_dict(d), device="cpu", verbose=False)
+    eng.run(max_rounds=2)
+    d2 = _cfg(part, server__num_round=4, server__mode=mode)
+    d2["engine"].update({"save-state": True, "resume": True})
+    eng2 = FLEngine(from_dict(d2), device="cpu", verbose=False)
+    assert eng2.round_no == 3 and eng2.rounds_left == 2
+    hist = eng2.run()
+    assert [r["round"] for r in hist] == [3, 4]
+    got = torch.load(os.path.join(part, name), weights_only=True)
+    for k in ref:
+        assert torch.allclose(ref[k], got[k], atol=1e-6), k
+
+
+def test_fedavg_allreduce_world2_matches_single_process(tmp_path):
+    """fedavg without attackers: the packed world-2 run takes the all_reduce fast path."""
+    d = _cfg(tmp_path, server__num_round=2)
+    d["comm"] = {"backend": "gloo"}
+    d["engine"]["checkpoint-dir"] = str(tmp_path / "mp")
+    d["engine"]["metrics"] = str(tmp_path / "mp" / "m.jsonl")
+    d["log_path"] = str(tmp_path / "mp")
+    cfg_path = _write_cfg(tmp_path, d)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "launch.py"), "--config", cfg_path,
+           "--device", "cpu"]
+    r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"path": "fedavg-allreduce"' in open(tmp_path / "mp" / "m.jsonl").read()
+    mp = torch.load(os.path.join(tmp_path, "mp", "TransformerModel.pth"), weights_only=True)
+    d1 = dict(d)
+    d1["engine"] = dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "sp"), "metrics": ""})
+    d1["log_path"] = str(tmp_path / "sp")
+    eng = FLEngine(from_dict(d1), device="cpu", verbose=False)
+    eng.run()
+    sp = torch.load(os.path.join(tmp_path, "sp", "TransformerModel.pth"), weights_only=True)
+    for k in sp:
+        assert torch.allclose(sp[k], mp[k], atol=1e-4), k
