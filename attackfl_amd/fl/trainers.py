@@ -56,12 +56,14 @@ def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, dev
         raise ValueError(f"num_data {maxnd} exceeds the train set size {n_train}")
     if isinstance(generator, (list, tuple)):
         gdev = torch.device(device)
-        keys, ek = [], []
-        for s in generator:
+        keys = []
+        ek = torch.full((C, epochs, maxnd), 2.0, device=gdev)
+        for c, s in enumerate(generator):
             g = torch.Generator(device=gdev).manual_seed(int(s) & 0x7FFFFFFFFFFFFFFF)
             keys.append(torch.rand(n_train, generator=g, device=gdev))
-            ek.append(torch.rand(epochs, maxnd, generator=g, device=gdev))
-        keys, ek = torch.stack(keys), torch.stack(ek)
+            # exactly nd_c draws per epoch: the plan must not depend on the other clients this rank hosts
+            ek[c, :, :num_data[c]] = torch.rand(epochs, num_data[c], generator=g, device=gdev)
+        keys = torch.stack(keys)
     else:
         gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
         keys = torch.rand(C, n_train, generator=generator, device=gdev)

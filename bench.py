@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_ROUNDS_PER_S = 0.18  # measured proxy of the reference, whole node, 8 clients
+# BASELINE.md proxy rows for the other model families (same workload, 8 clients); HAR: none measured
+MODEL_BASELINES = {"TransformerModel": BASELINE_ROUNDS_PER_S, "CNNModel": 0.075, "RNNModel": 0.15}
 
 
 def main() -> int:
@@ -38,6 +40,8 @@ def main() -> int:
     ap.add_argument("--model", default="TransformerModel")
     ap.add_argument("--mode", default="fedavg")
     ap.add_argument("--trainer", default="auto")
+    ap.add_argument("--attackers", default="", help="idx:mode:round[:arg...] comma-separated (launch.py syntax)")
+    ap.add_argument("--data-name", default="ICU")
     ap.add_argument("--profile-rounds", action="store_true", help="print per-phase timings to stderr")
     args = ap.parse_args()
 
@@ -48,6 +52,7 @@ def main() -> int:
     from attackfl_amd.fl.engine import FLEngine, build_client_table
     from attackfl_amd.parallel.comm import LoopbackComm, TorchComm, init_distributed
     from attackfl_amd.utils.log import set_quiet
+    from launch import parse_attackers
 
     set_quiet(True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -65,14 +70,16 @@ def main() -> int:
     tmp = tempfile.mkdtemp(prefix=f"attackfl_bench_r{rank}_")
     cfg = from_dict({
         "server": {"num-round": args.warmup + args.steps + 1, "clients": args.clients, "mode": args.mode,
-                   "model": args.model, "data-name": "ICU", "validation": True,
-                   "data-distribution": {"num-data-range": [12000, 15000]}},
+                   "model": args.model, "data-name": args.data_name, "validation": True,
+                   "data-distribution": {"num-data-range": [12000, 15000] if args.data_name == "ICU" else [1000, 1500]}},
         "learning": {"epoch": 5, "batch-size": 128, "learning-rate": 0.004},
-        "data": {"synthetic": True, "train-size": 60000, "test-size": 10000},
+        "data": {"synthetic": True, "train-size": 60000, "test-size": 10000, "har-train-size": 7352,
+                 "har-test-size": 2947},
         "engine": {"trainer": args.trainer, "checkpoint-dir": tmp, "seed": 1},
         "log_path": tmp,
     })
-    table = build_client_table(cfg, comm.world)
+    attackers = parse_attackers(args.attackers) if args.attackers else None
+    table = build_client_table(cfg, comm.world, attackers)
     eng = FLEngine(cfg, comm=comm, table=table, device=device, verbose=False)
     eng.client_selection()
 
@@ -102,8 +109,9 @@ def main() -> int:
     value = args.steps / elapsed
     if rank == 0:
         aucs = [r["metric"] for r in recs if r["metric"] == r["metric"]]
+        base = MODEL_BASELINES.get(args.model) if (args.data_name == "ICU" and args.clients == 8) else None
         out = {
-            "metric": "FL rounds/sec (whole node) + test-acc, TransformerModel/ICU, 8 clients",
+            "metric": f"FL rounds/sec (whole node) + test-acc, {args.model}/{args.data_name}, {args.clients} clients",
             "value": round(value, 4),
             "unit": "rounds/s",
             "n_gpus": comm.world,
@@ -112,14 +120,16 @@ def main() -> int:
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / BASELINE_ROUNDS_PER_S, 2),
+            "vs_baseline": round(value / base, 2) if base else None,
             "dtype": "bf16",
-            "data": "synthetic ICU-shaped rows (planted signal), random-init weights",
+            "data": ("synthetic ICU-shaped rows (planted signal)" if args.data_name == "ICU" else
+                     "synthetic HAR-shaped sequences (L=561, 6 classes)") + ", random-init weights",
             "config": {"model": args.model, "global_batch": 128 * args.clients, "seq_len": 1,
                        "parallelism": f"fl{args.clients}-clients-over-{comm.world}-ranks",
                        "clients": args.clients, "local_epochs": 5, "rows_per_client": "12000-15000",
-                       "mode": args.mode, "trainer": eng.trainer.kind if eng.trainer else None},
-            "test_roc_auc": round(aucs[-1], 4) if aucs else None,
+                       "mode": args.mode, "trainer": eng.trainer.kind if eng.trainer else None,
+                       "attackers": args.attackers or None},
+            ("test_roc_auc" if args.data_name == "ICU" else "test_accuracy"): round(aucs[-1], 4) if aucs else None,
             "rounds_ok": sum(1 for r in recs if r["ok"]),
         }
         print(json.dumps(out), flush=True)

@@ -46,7 +46,11 @@ def main(argv=None) -> int:
     cfg = load_config(args.config, over)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        backend, device = init_distributed(cfg.comm.get("backend", "auto"), int(cfg.comm.get("timeout-s", 600)))
+        dev_index = None
+        if args.device and args.device.startswith("cuda"):  # e.g. several gloo ranks sharing one GPU
+            dev_index = int(args.device.split(":")[1]) if ":" in args.device else None
+        backend, device = init_distributed(cfg.comm.get("backend", "auto"), int(cfg.comm.get("timeout-s", 600)),
+                                           device_index=dev_index)
         comm = TorchComm(device, backend, one_shot=bool(cfg.comm.get("one-shot-allgather", False)))
     else:
         device = torch.device(args.device) if args.device else (torch.device("cuda", 0) if torch.cuda.is_available()

@@ -240,3 +240,13 @@ def test_fedavg_allreduce_world2_matches_single_process(tmp_path):
     sp = torch.load(os.path.join(tmp_path, "sp", "TransformerModel.pth"), weights_only=True)
     for k in sp:
         assert torch.allclose(sp[k], mp[k], atol=1e-4), k
+
+
+def test_plan_is_placement_independent():
+    """A client's batches depend only on its own seed and size, not on the clients it is packed with."""
+    from attackfl_amd.fl.trainers import make_plan
+    a = make_plan(1000, [300, 120], 2, [11, 12], "cpu")
+    b = make_plan(1000, [120], 2, [12], "cpu")
+    c = make_plan(1000, [300, 500, 120], 2, [11, 99, 12], "cpu")
+    assert torch.equal(a.client(1), b.client(0)) and torch.equal(a.client(1), c.client(2))
+    assert torch.equal(a.client(0), c.client(0))
