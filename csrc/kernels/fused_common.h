@@ -1,0 +1,464 @@
+// Building blocks shared by the fused whole-step trainers (transformer.hip, rnn.hip): 512-thread
+// workgroups of 8 waves x 16 rows, activations in LDS as bf16, GEMMs on v_mfma_f32_16x16x32_bf16,
+// Adam fused into the dW epilogue, DPP / permlane row and column reductions, register LayerNorm,
+// and the write-through cross-workgroup hand-off (cdna_hip_programming.md Guideline 16, R1).
+// Everything that depends on a kernel's LDS map is templated on its context type CtxT<Layout>.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+// Global-memory pointers carry address_space(1) explicitly: they pass through opaque asm at every phase
+// barrier, and a generic pointer would demote every access to FLAT (which waits on vmcnt AND lgkmcnt).
+#define GAS __attribute__((address_space(1)))
+typedef GAS float gf;
+typedef GAS unsigned short gu16;
+typedef GAS int gi32;
+typedef GAS uint32_t gu32;
+typedef GAS unsigned long long gu64;
+
+
+constexpr int NT = 512;  // threads per fused-trainer workgroup
+constexpr int BM = 128;  // max rows per batch
+
+namespace fk {
+
+// bf16 round-to-nearest-even (hardware v_cvt_pk_bf16_f32, NaN preserving)
+typedef float tf_f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 tf_b2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((tf_f2v){lo, hi}, tf_b2v));
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+struct AdamK {
+  float lr_bc1, rsqrt_bc2;
+  float sgd_lr;  // > 0: test mode, plain SGD p -= sgd_lr * g (exposes raw gradients to the tests)
+};
+constexpr float B1 = 0.9f, B2 = 0.999f, EPS = 1e-8f;
+
+// Adam update given already-loaded state; returns the new parameter
+__device__ __forceinline__ float adam_upd(float p, float& m, float& v, float g, AdamK k) {
+  if (k.sgd_lr > 0.f) return p - k.sgd_lr * g;
+  m = m + (1.f - B1) * (g - m);
+  v = B2 * v + (1.f - B2) * g * g;
+  return p - k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_sqrtf(v) * k.rsqrt_bc2 + EPS);
+}
+__device__ __forceinline__ float adam(gf* __restrict__ p, gf* __restrict__ m, gf* __restrict__ v, int idx, float g,
+                                      AdamK k) {
+  float pp = p[idx], mm = m[idx], vv = v[idx];
+  pp = adam_upd(pp, mm, vv, g, k);
+  p[idx] = pp;
+  if (k.sgd_lr <= 0.f) {
+    m[idx] = mm;
+    v[idx] = vv;
+  }
+  return pp;
+}
+
+// Per-workgroup context of a fused trainer.  L supplies the LDS map: S_ACC / LDACC (fp32 GEMM output
+// tile [128][LDACC]) and S_CS (column-sum partials [slots][8 waves][64]).
+template <class L>
+struct CtxT {
+  static constexpr int LDACC = L::LDACC;
+  unsigned char* smem;
+  gf* P;     // master params of this client
+  gf* M;
+  gf* V;
+  gu16* BF;  // bf16 weight copies
+  gf* ws;
+  int tid, lane, wave;
+  int r, q;  // row-per-4-lanes layout: row, quarter
+
+  // Phase barrier: LDS-only (global loads stay in flight, global stores are not drained), then make
+  // every base value opaque so the compiler recomputes addresses per phase instead of keeping hundreds
+  // of CSE'd pointers live across the whole step (which spills to scratch).
+  __device__ __forceinline__ void bar() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
+    asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
+  }
+  // Full barrier (drains global stores: publishes Adam's writes to every wave)
+  __device__ __forceinline__ void full_sync() {
+    __syncthreads();
+    asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
+    asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
+  }
+
+  __device__ float* acc() const { return (float*)(smem + L::S_ACC); }
+  __device__ unsigned short* u16(int off) const { return (unsigned short*)(smem + off); }
+  __device__ float* cs(int v) const { return (float*)(smem + L::S_CS) + v * 8 * 64; }
+  __device__ gf* wsf(long off) const { return ws + off; }
+};
+
+// ---------------------------------------------------------------- fragments
+__device__ __forceinline__ s8v lds_row_frag(const unsigned short* base, int ld, int r0, int k0, int lane) {
+  const unsigned short* p = base + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4);
+  return *(const LDS_AS s8v*)p;
+}
+// A[m][k] = S[k][m] (S row-major [k rows][m cols]); two transposed 4x16 reads per 16-lane group
+__device__ __forceinline__ s8v lds_col_frag(const unsigned short* S, int ld, int k0, int m0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const unsigned short* a1 = S + (k0 + 8 * g + q) * ld + m0 + 4 * p;
+  const unsigned short* a2 = a1 + 4 * ld;
+  s4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a1);
+  s4v r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a2);
+  s8v r;
+  r[0] = r1[0]; r[1] = r1[1]; r[2] = r1[2]; r[3] = r1[3];
+  r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
+  return r;
+}
+__device__ __forceinline__ s8v glb_frag(const gu16* W, int ldk, int n0, int k0, int lane) {
+  return *(const GAS s8v*)(W + (n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+}
+__device__ __forceinline__ f4v mfma(s8v a, s8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+// ACC[128][N] = A[128][K] (LDS bf16, ld lda) x W^T, W = global bf16 [N][K] row-major (eval path)
+template <int N, int K, class CT>
+__device__ __forceinline__ void gemm_xw(const CT& c, const unsigned short* A, int lda, const gu16* W) {
+  constexpr int NTL = N / 16;
+  f4v acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int r0 = 16 * c.wave;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    s8v a = lds_row_frag(A, lda, r0, k0, c.lane);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, glb_frag(W, K, 16 * t, k0, c.lane), acc[t]);
+  }
+  float* out = c.acc();
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * CT::LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
+}
+
+// ---- weight fragments prefetched into registers a phase ahead of their GEMM ----
+template <int N, int K>
+struct WFr {
+  s8v f[N / 16][K / 32];
+};
+template <int N, int K>
+__device__ __forceinline__ void wload(WFr<N, K>& w, const gu16* W, int lane) {
+#pragma unroll
+  for (int t = 0; t < N / 16; ++t)
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) w.f[t][kk] = glb_frag(W, K, 16 * t, 32 * kk, lane);
+}
+template <int N, int K, class CT>
+__device__ __forceinline__ void gemm_pf(const CT& c, const unsigned short* A, int lda, const WFr<N, K>& w) {
+  constexpr int NTL = N / 16;
+  f4v acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int r0 = 16 * c.wave;
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk) {
+    s8v a = lds_row_frag(A, lda, r0, 32 * kk, c.lane);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = mfma(a, w.f[t][kk], acc[t]);
+  }
+  float* out = c.acc();
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(r0 + 4 * (c.lane >> 4) + i) * CT::LDACC + 16 * t + (c.lane & 15)] = acc[t][i];
+}
+
+template <class CT>
+__device__ __forceinline__ float cs_total(const CT& c, int v, int col);
+
+// Matrix weight descriptor for the dW+Adam epilogue
+struct MatW {
+  int off;        // param offset of W[n][k]
+  int n_real, k_real;
+  int wf, wf_ld;  // bf16 WF [n][k] copy (ushort offset in BF region, row stride)
+  int wt, wt_ld;  // bf16 WT [k][n] copy (-1 = none)
+};
+
+// dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows, then Adam on the real entries.  The Adam state
+// (p, m, v) of each lane's 4 accumulator elements is loaded before the MFMAs so the global latency
+// overlaps the tile's transposed LDS reads and matrix work.
+template <int MT, int NTL, class CT>
+__device__ __forceinline__ void gemm_dw_adam(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
+                                             int ldx, MatW mw, AdamK k) {
+  for (int t = c.wave; t < MT * NTL; t += 8) {
+    const int mt = t / NTL, nt = t % NTL;
+    const int kk = 16 * nt + (c.lane & 15);
+    float pp[4], mm[4], vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 16 * mt + 4 * (c.lane >> 4) + i;
+      const bool ok = n < mw.n_real && kk < mw.k_real;
+      const int idx = ok ? mw.off + n * mw.k_real + kk : mw.off;
+      pp[i] = c.P[idx];
+      mm[i] = c.M[idx];
+      vv[i] = c.V[idx];
+    }
+    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b0 = 0; b0 < BM; b0 += 32)
+      acc = mfma(lds_col_frag(DY, ldy, b0, 16 * mt, c.lane), lds_col_frag(X, ldx, b0, 16 * nt, c.lane), acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 16 * mt + 4 * (c.lane >> 4) + i;
+      if (n < mw.n_real && kk < mw.k_real) {
+        const int idx = mw.off + n * mw.k_real + kk;
+        const float pn = adam_upd(pp[i], mm[i], vv[i], acc[i], k);
+        c.P[idx] = pn;
+        if (k.sgd_lr <= 0.f) {
+          c.M[idx] = mm[i];
+          c.V[idx] = vv[i];
+        }
+        const unsigned short h = f2bf(pn);
+        c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+        if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
+      }
+    }
+  }
+}
+
+// Adam on up to 512 small-vector elements (biases, LayerNorm affine) in parallel: thread tid handles
+// element tid of the concatenation of the listed vectors; gradient = column sum CS[v] over 8 waves.
+struct VecG {
+  int off, n, csv;  // param offset, length, column-sum slot (-1: value supplied in `g0`)
+};
+template <int NV, class CT>
+__device__ __forceinline__ void adam_vecs(const CT& c, const VecG (&vs)[NV], AdamK k, float g0 = 0.f) {
+  int e = c.tid;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (e >= 0 && e < vs[i].n) {
+      const float g = vs[i].csv >= 0 ? cs_total(c, vs[i].csv, e) : g0;
+      adam(c.P, c.M, c.V, vs[i].off + e, g, k);
+    }
+    e -= vs[i].n;
+  }
+}
+
+// ---- cross-lane reductions without LDS ----
+// Element layout: lane l of wave w owns row r = 16w + (l & 15) and quarter q = l >> 4 of that row.
+// A column sum over the wave's 16 rows is a reduction over 16 consecutive lanes: 4 DPP adds
+// (quad_perm xor1, xor2, row_half_mirror, row_mirror).  A row sum over the 4 quarters pairs lanes
+// l, l^16, l^32: gfx950 v_permlane16_swap / v_permlane32_swap.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float a) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum16lanes(float a) {
+  a += dpp<0xB1>(a);   // quad_perm [1,0,3,2]
+  a += dpp<0x4E>(a);   // quad_perm [2,3,0,1]
+  a += dpp<0x141>(a);  // row_half_mirror
+  a += dpp<0x140>(a);  // row_mirror
+  return a;
+}
+__device__ __forceinline__ float xor16(float a) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]) - a;  // = a[l ^ 16]
+}
+__device__ __forceinline__ float xor32(float a) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]) - a;  // = a[l ^ 32]
+}
+
+// level-major over W independent values: the DPP read-after-VALU-write hazard is covered by the other
+// values' instructions instead of s_nop padding
+template <int W>
+__device__ __forceinline__ void sum16lanes_multi(float (&s)[W]) {
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0xB1>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x4E>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x141>(s[j]);
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] += dpp<0x140>(s[j]);
+}
+
+// column partial sums of 16 values per lane (64-wide rows): CS[v][wave][q*16 + j]
+template <class CT>
+__device__ __forceinline__ void colsum16(const CT& c, int v, const float (&x)[16]) {
+  float s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = x[j];
+  sum16lanes_multi(s);
+  if ((c.lane & 15) == 0) {
+    float* d = c.cs(v) + c.wave * 64 + (c.lane >> 4) * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = s[j];
+  }
+}
+template <int W, class CT>
+__device__ __forceinline__ void colsumW(const CT& c, int v, const float (&x)[W], int colbase) {
+  float s[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] = x[j];
+  sum16lanes_multi(s);
+  if ((c.lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) c.cs(v)[c.wave * 64 + colbase + j] = s[j];
+  }
+}
+template <class CT>
+__device__ __forceinline__ float cs_total(const CT& c, int v, int col) {
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) s += c.cs(v)[w * 64 + col];
+  return s;
+}
+
+// row-wise sum over the 4 lanes (quarters) of a row: lanes l, l^16, l^32, l^48
+__device__ __forceinline__ float rsum4(float a) {
+  a += xor16(a);
+  a += xor32(a);
+  return a;
+}
+
+// LayerNorm forward on 16 values/lane (64-wide row): returns xhat in place, rstd
+__device__ __forceinline__ float ln_fwd(float (&x)[16]) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += x[j];
+  const float mean = rsum4(s) * (1.f / 64.f);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    x[j] -= mean;
+    ss += x[j] * x[j];
+  }
+  const float var = rsum4(ss) * (1.f / 64.f);
+  const float rstd = __builtin_amdgcn_rsqf(var + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] *= rstd;
+  return rstd;
+}
+// LayerNorm backward: dy -> dx given xhat, rstd, gamma (per column, 16 values of this lane)
+__device__ __forceinline__ void ln_bwd(float (&dx)[16], const float (&dy)[16], const float (&xh)[16], float rstd,
+                                       const float (&gamma)[16]) {
+  float a = 0.f, b = 0.f, g[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    g[j] = dy[j] * gamma[j];
+    a += g[j];
+    b += g[j] * xh[j];
+  }
+  a = rsum4(a) * (1.f / 64.f);
+  b = rsum4(b) * (1.f / 64.f);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dx[j] = rstd * (g[j] - a - xh[j] * b);
+}
+
+__device__ __forceinline__ void load16(float (&x)[16], const gf* p) {
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) {
+    f4v v = *(const GAS f4v*)(p + j);
+    x[j] = v[0]; x[j + 1] = v[1]; x[j + 2] = v[2]; x[j + 3] = v[3];
+  }
+}
+__device__ __forceinline__ void load8(float (&x)[8], const gf* p) {
+  f4v a = *(const GAS f4v*)p, b = *(const GAS f4v*)(p + 4);
+  x[0] = a[0]; x[1] = a[1]; x[2] = a[2]; x[3] = a[3];
+  x[4] = b[0]; x[5] = b[1]; x[6] = b[2]; x[7] = b[3];
+}
+__device__ __forceinline__ void store16(gf* p, const float (&x)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) *(GAS f4v*)(p + j) = f4v{x[j], x[j + 1], x[j + 2], x[j + 3]};
+}
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s8v pack8bf(const float* x) {
+  u4v u;
+  u[0] = pack_bf2(x[0], x[1]);
+  u[1] = pack_bf2(x[2], x[3]);
+  u[2] = pack_bf2(x[4], x[5]);
+  u[3] = pack_bf2(x[6], x[7]);
+  return __builtin_bit_cast(s8v, u);
+}
+__device__ __forceinline__ void store16bf(unsigned short* p, const float (&x)[16]) {
+  *(LDS_AS s8v*)p = pack8bf(x);
+  *(LDS_AS s8v*)(p + 8) = pack8bf(x + 8);
+}
+
+// ---- cross-workgroup hand-off (branch-parallel mode; cdna_hip_programming.md Guideline 16, R1) ----
+// payload: 8-byte write-through (sc1) agent-scope stores; every storing wave drains (vmcnt 0), then a
+// workgroup barrier, then ONE lane stores the flag.  Consumer: ONE wave polls the flag relaxed
+// (bounded spin), ONE agent acquire, vmcnt(0), workgroup barrier, then plain loads.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_wt(gu64* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt(gu64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class CT>
+__device__ __forceinline__ void xwg_publish(const CT& c, gu32* flag, uint32_t value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (c.tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr long XWG_MAX_SPINS = 1L << 22;  // ~seconds: a missing partner becomes an error, not a hang
+// waits until (flag_a >> shift) >= want and (flag_b >> shift) >= want (pass the same word twice for
+// one); returns flag_a's value, or 0xFFFFFFFF on timeout (also raises *tmo)
+template <class CT>
+__device__ __forceinline__ uint32_t xwg_wait(const CT& c, gu32* flag_a, gu32* flag_b, uint32_t want, int shift,
+                                             gu32* tmo, uint32_t* bcast) {
+  if (c.wave == 0) {
+    uint32_t v = 0;
+    for (long spins = 0;; ++spins) {
+      v = __hip_atomic_load(flag_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t w = flag_b == flag_a ? v : __hip_atomic_load(flag_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v >> shift) >= want && (w >> shift) >= want) break;
+      if (spins > XWG_MAX_SPINS) {
+        v = 0xFFFFFFFFu;
+        if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (c.lane == 0) *bcast = v;
+  }
+  __syncthreads();
+  return *bcast;
+}
+
+// write the bf16 copies of one matrix from the master params
+template <class CT>
+__device__ void init_copies(const CT& c, MatW mw) {
+  for (int e = c.tid; e < mw.n_real * mw.k_real; e += NT) {
+    const int n = e / mw.k_real, kk = e % mw.k_real;
+    unsigned short h = f2bf(c.P[mw.off + e]);
+    c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+    if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
+  }
+}
+
+
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// ACC row r, columns c0..c0+15 (fp32) -> hand-off slot (write-through 8-byte granules)
+template <class CT>
+__device__ __forceinline__ void put_grad(const CT& c, long slot, int r, int c0) {
+  gu64* d = (gu64*)(c.wsf(slot) + opaque(r * 64 + c0));
+  const float* acc = c.acc() + r * CT::LDACC + c0;
+#pragma unroll
+  for (int j = 0; j < 16; j += 2)
+    st_wt(d + j / 2, ((unsigned long long)__float_as_uint(acc[j + 1]) << 32) | __float_as_uint(acc[j]));
+}
+
+
+
+}  // namespace fk

@@ -85,15 +85,6 @@ __device__ __forceinline__ float gelu_grad(float x) {
 }
 __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
-// bf16 round-to-nearest-even (hardware v_cvt_pk_bf16_f32, NaN preserving)
-typedef float tf_f2v __attribute__((ext_vector_type(2)));
-typedef __bf16 tf_b2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned short f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
-__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((tf_f2v){lo, hi}, tf_b2v));
-}
-__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
-
 // dropout keep-test from a stateless hash of (step key, layer, row, column pair): one 32-bit hash
 // gives the 16-bit uniforms of two adjacent columns (keep iff u16 >= p * 65536)
 __device__ __forceinline__ uint32_t hash3(uint32_t key, uint32_t layer, uint32_t r, uint32_t c) {
