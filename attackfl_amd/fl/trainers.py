@@ -156,27 +156,41 @@ class EagerTrainer:
 
 
 class FusedTrainer:
-    """All local clients' local training in one persistent HIP kernel (TransformerModel/ICU)."""
+    """All local clients' local rounds in one persistent HIP launch: TransformerModel/ICU
+    (``ops/transformer.py``) and RNNModel/ICU (``ops/rnn.py``, falls back to the graph trainer when
+    its 3 workgroups per client do not all fit on the device)."""
 
     kind = "fused"
+    MODELS = ("TransformerModel", "RNNModel")
 
     def __init__(self, model_name: str, data_name: str, table: DeviceTable, device, verbose: bool = False):
-        if model_name != "TransformerModel" or data_name != "ICU":
-            raise ValueError("fused trainer supports TransformerModel/ICU")
+        if model_name not in self.MODELS or data_name != "ICU":
+            raise ValueError("fused trainer supports TransformerModel/ICU and RNNModel/ICU")
         if torch.device(device).type != "cuda":
             raise ValueError("fused trainer needs a GPU")
+        from ..ops import rnn as R
         from ..ops import transformer as T
 
-        self.T = T
+        self.model_name = model_name
+        self.T, self.R = T, R
         self.table = table
         self.device = torch.device(device)
         self.layout = ParamLayout.for_model(model_name)
         self.verbose = verbose
+        self._fallback = None
 
     def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
               ) -> Tuple[List[bool], torch.Tensor]:
-        ok, losses = self.T.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
-                                          seeds)
+        if self.model_name == "RNNModel":
+            if not self.R.fits(params.shape[0], self.device):
+                if self._fallback is None:
+                    self._fallback = GraphTrainer(self.model_name, "ICU", self.table, self.device, self.verbose)
+                return self._fallback.train(params, plan, lr, batch, seeds)
+            ok, losses = self.R.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
+                                              seeds)
+        else:
+            ok, losses = self.T.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
+                                              seeds)
         return [bool(x) for x in ok.tolist()], losses
 
 
@@ -219,7 +233,7 @@ def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable,
     if kind == "auto":
         if dev.type != "cuda":
             kind = "eager"
-        elif model_name == "TransformerModel" and data_name == "ICU":
+        elif model_name in FusedTrainer.MODELS and data_name == "ICU":
             kind = "fused"
         elif model_name in PROGRAMS:
             kind = "graph"

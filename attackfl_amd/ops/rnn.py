@@ -1,0 +1,39 @@
+"""Fused RNNModel/ICU local training (``csrc/kernels/rnn.hip``): one launch trains all of a rank's
+clients for all their local epochs, three co-resident workgroups per client (head | vitals | labs).
+
+Dropout masks follow the layer-program convention (``fl/programs.py``), so the composite
+``RNNProgram`` on CPU is the exact-semantics oracle of this kernel (tests/test_gpu_rnn.py).
+"""
+from __future__ import annotations
+
+from typing import Sequence, Tuple
+
+import torch
+
+from . import native
+from .masks import M32
+
+NPARAM = 97665
+
+
+def fits(C: int, dev) -> bool:
+    """All 3*C workgroups must be resident at once (one per CU)."""
+    return 3 * C <= torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def _seeds(seeds, dev) -> torch.Tensor:
+    s = torch.tensor([int(x) & M32 for x in seeds], dtype=torch.int64)
+    return torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32).to(dev)
+
+
+def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
+                  lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Train ``params [C, 97665]`` in place.  Returns (ok [C] int32, losses [C, E]) on the host."""
+    dev = params.device
+    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
+    ok, losses = native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, _seeds(seeds, dev),
+                                    int(epochs), int(batch), float(lr), int(opt_mode))
+    ok = ok.cpu()
+    if bool((ok < 0).any()):
+        raise RuntimeError("fused RNN trainer: a cross-workgroup hand-off timed out (workgroups not co-resident?)")
+    return ok, losses.cpu()

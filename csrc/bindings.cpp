@@ -235,20 +235,23 @@ void hyper_adam_outer(torch::Tensor W, torch::Tensor b, torch::Tensor m, torch::
   AFL_CHECK_LAUNCH();
 }
 
-std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
-                                    torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
-                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
+// Fused whole-round trainers: kind 0 = TransformerModel (split 1 / 2 / 3 workgroups per client),
+// kind 1 = RNNModel (always 3 workgroups per client).
+std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Tensor rows, torch::Tensor order,
+                                       torch::Tensor nd, torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
+                                       int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
   check_dev(params, "params", torch::kFloat32);
   check_dev(rows, "rows", torch::kFloat32);
   check_dev(order, "order", torch::kInt32);
   check_dev(nd, "nd", torch::kInt32);
   check_dev(seeds, "seeds", torch::kInt32);
-  TORCH_CHECK(params.dim() == 2 && params.size(1) == afl_tf_param_count(), "params must be [C, 47693]");
+  const long P = kind == 0 ? afl_tf_param_count() : afl_rnn_param_count();
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == P, "params must be [C, ", P, "]");
   TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 24, "rows must be [N, 24]");
   const int C = params.size(0);
   TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
   TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
-  const long stride = ((afl_tf_ws_floats() + 63) / 64) * 64;
+  const long stride = (((kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats()) + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());
   auto ok = torch::zeros({C}, order.options());
   auto losses = torch::zeros({C, epochs}, params.options());
@@ -271,22 +274,33 @@ std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, to
   a.opt_mode = (int)opt_mode;
   a.stamps = nullptr;
   if (stamps.has_value() && stamps->defined()) {
-    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == torch::kInt64 && stamps->numel() >= 32,
-                "stamps must be a device int64 tensor with >= 32 entries");
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == torch::kInt64 && stamps->numel() >= 64,
+                "stamps must be a device int64 tensor with >= 64 entries");
     a.stamps = (uint64_t*)stamps->data_ptr<int64_t>();
   }
   a.sync = nullptr;
-  a.split = (int)std::max<int64_t>(1, split);
+  a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);
   torch::Tensor sync;
   if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
     sync = torch::zeros({(long)C * 4}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
-  const int rc = afl_tf_train(&a, cur());
+  const int rc = kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
   TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
-  TORCH_CHECK(rc == 0, "tf_train launch failed (", rc, ")");
+  TORCH_CHECK(rc == 0, "fused trainer launch failed (", rc, ")");
   AFL_CHECK_LAUNCH();
   return {ok, losses};
+}
+
+std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
+                                    torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
+                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
+  return fused_train(0, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split);
+}
+
+std::vector<torch::Tensor> rnn_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
+                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr, int64_t opt_mode) {
+  return fused_train(1, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, c10::nullopt, 3);
 }
 
 torch::Tensor tf_eval(torch::Tensor params, torch::Tensor rows) {
@@ -324,6 +338,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
         py::arg("stamps") = py::none(), py::arg("split") = 1);
+  m.def("rnn_train", &rnn_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
+        py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0);
+  m.def("rnn_param_count", &afl_rnn_param_count);
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);

@@ -56,6 +56,10 @@ struct AflTfTrainArgs {
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);
 long afl_tf_ws_floats();
+// rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
+int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);
+long afl_rnn_ws_floats();
+int afl_rnn_param_count();
 int afl_tf_bf_ushorts();
 int afl_tf_param_count();
 

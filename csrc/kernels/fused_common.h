@@ -232,6 +232,7 @@ __device__ __forceinline__ void gemm_dw_adam(const CT& c, const unsigned short* 
 // element tid of the concatenation of the listed vectors; gradient = column sum CS[v] over 8 waves.
 struct VecG {
   int off, n, csv;  // param offset, length, column-sum slot (-1: value supplied in `g0`)
+  int cbase = 0;    // first column of the slot holding element 0
 };
 template <int NV, class CT>
 __device__ __forceinline__ void adam_vecs(const CT& c, const VecG (&vs)[NV], AdamK k, float g0 = 0.f) {
@@ -239,7 +240,7 @@ __device__ __forceinline__ void adam_vecs(const CT& c, const VecG (&vs)[NV], Ada
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     if (e >= 0 && e < vs[i].n) {
-      const float g = vs[i].csv >= 0 ? cs_total(c, vs[i].csv, e) : g0;
+      const float g = vs[i].csv >= 0 ? cs_total(c, vs[i].csv, vs[i].cbase + e) : g0;
       adam(c.P, c.M, c.V, vs[i].off + e, g, k);
     }
     e -= vs[i].n;

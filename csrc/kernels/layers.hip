@@ -41,7 +41,7 @@ __device__ __forceinline__ float gelu_d(float x) {
   return cdf + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
 __device__ __forceinline__ float act_f(float v, int act) {
-  return act == 1 ? fmaxf(v, 0.f) : (act == 2 ? gelu_f(v) : v);
+  return act == 1 ? (v < 0.f ? 0.f : v) : (act == 2 ? gelu_f(v) : v);  // relu keeps NaN, like torch
 }
 __device__ __forceinline__ float act_d(float g, int gact) {
   return gact == 1 ? (g > 0.f ? 1.f : 0.f) : (gact == 2 ? gelu_d(g) : 1.f);

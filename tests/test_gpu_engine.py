@@ -28,7 +28,7 @@ def _run(tmp_path, model, data, mode, clients=4, rounds=2):
     return hist, kind
 
 
-@pytest.mark.parametrize("model,data,kind", [("CNNModel", "ICU", "graph"), ("RNNModel", "ICU", "graph"),
+@pytest.mark.parametrize("model,data,kind", [("CNNModel", "ICU", "graph"), ("RNNModel", "ICU", "fused"),
                                              ("TransformerModel", "ICU", "fused"),
                                              ("TransformerClassifier", "HAR", "graph")])
 @pytest.mark.parametrize("mode", ["fedavg", "hyper"])

@@ -1,0 +1,77 @@
+"""Fused RNNModel trainer (csrc/kernels/rnn.hip) against the composite RNNProgram on CPU, which uses the
+same dropout-mask convention: raw SGD gradients with dropout on, multi-step Adam trajectories, the
+partial / size-1 batches and the NaN abort."""
+import pytest
+import torch
+
+from attackfl_amd.data import DeviceTable, synthetic_icu
+from attackfl_amd.fl.programs import ProgramRunner, make_program
+from attackfl_amd.fl.trainers import Plan, make_plan
+from attackfl_amd.models import ParamLayout, build_model
+from attackfl_amd.ops import rnn as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(C, nd, E=1, seed=0):
+    ds = synthetic_icu(3000, seed=3)
+    lay = ParamLayout.for_model("RNNModel")
+    params = torch.stack([lay.flatten(build_model("RNNModel", seed=seed + i).state_dict()) for i in range(C)])
+    plan = make_plan(len(ds), nd, E, [101 + i for i in range(C)], "cpu")
+    return ds, params, plan
+
+
+def _composite(ds, params, plan, lr, seeds, sgd=0.0):
+    p = params.clone()
+    prog = make_program("RNNModel", p.shape[0], 128, "cpu")
+    ok, losses = ProgramRunner(prog).train(DeviceTable(ds, "cpu"), p, plan, lr=lr, seeds=seeds, sgd_lr=sgd)
+    return p, ok, losses
+
+
+def test_sgd_gradients_match_program(gpu):
+    """Raw SGD updates (dropout on): the fused kernel equals the GPU layer program (same bf16 operand
+    rounding) to < 2 % per tensor, and both stay within the bf16 band of the fp32 composite."""
+    ds, params, plan = _setup(2, [128, 100])
+    ref, ok_r, _ = _composite(ds, params, plan, 0.0, [5, 6], sgd=1.0)
+    dev = params.clone().to(gpu)
+    ok, _ = R.train_clients(dev, DeviceTable(ds, gpu).rows, plan.order.to(gpu), plan.nd, 1, 128, 1.0, [5, 6],
+                            opt_mode=1)
+    gp = params.clone().to(gpu)
+    ProgramRunner(make_program("RNNModel", 2, 128, gpu), use_graph=False).train(
+        DeviceTable(ds, gpu), gp, Plan(plan.order.to(gpu), plan.nd, 1), lr=0.0, seeds=[5, 6], sgd_lr=1.0)
+    assert ok.tolist() == [1, 1] and ok_r.all()
+    g_ref, g_dev, g_gp = params - ref, params - dev.cpu(), params - gp.cpu()
+    bad = []
+    for s in ParamLayout.for_model("RNNModel").slots:
+        a = g_dev[:, s.offset:s.offset + s.numel]
+        b = g_ref[:, s.offset:s.offset + s.numel]
+        c = g_gp[:, s.offset:s.offset + s.numel]
+        if b.abs().max().item() == 0.0:  # W_hh: exactly zero gradient (h0 = 0)
+            if a.abs().max().item() != 0.0:
+                bad.append((s.name, "nonzero"))
+            continue
+        vs_graph = float((a - c).norm() / c.norm())
+        vs_fp32 = float((a - b).norm() / b.norm())
+        if vs_graph > 0.02 or vs_fp32 > 0.12:
+            bad.append((s.name, round(vs_graph, 4), round(vs_fp32, 4)))
+    assert not bad, bad
+
+
+def test_adam_epochs_track_program(gpu):
+    ds, params, plan = _setup(3, [700, 513, 300], E=2, seed=4)
+    ref, ok_r, loss_r = _composite(ds, params, plan, 0.004, [7, 8, 9])
+    dev = params.clone().to(gpu)
+    ok, loss = R.train_clients(dev, DeviceTable(ds, gpu).rows, plan.order.to(gpu), plan.nd, 2, 128, 0.004, [7, 8, 9])
+    assert ok.tolist() == [1, 1, 1] and ok_r.all()
+    moved = (ref - params).abs().mean().item()
+    assert (dev.cpu() - ref).abs().mean().item() < 0.1 * moved
+    assert torch.allclose(loss.double(), loss_r, rtol=0.03, atol=0.01), (loss, loss_r)
+
+
+def test_nan_client_fails_others_train(gpu):
+    ds, params, plan = _setup(2, [300, 300])
+    params[1, 11] = float("nan")
+    dev = params.clone().to(gpu)
+    ok, _ = R.train_clients(dev, DeviceTable(ds, gpu).rows, plan.order.to(gpu), plan.nd, 1, 128, 0.004, [1, 2])
+    assert ok.tolist() == [1, 0]
+    assert torch.isfinite(dev[0]).all() and not torch.equal(dev[0].cpu(), params[0])
