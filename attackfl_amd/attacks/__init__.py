@@ -87,10 +87,8 @@ class DistanceEngine:
         out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
         if self.vec_slots:
             out += ops.segment_l2_sum(diffs, self.vec_slots)
-        for s in self.mat_slots:
-            r = s.shape[0]
-            mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], r, -1)
-            out += ops.batched_spectral_norm(mats).double()
+        if self.mat_slots:
+            out += ops.spectral_norm_sum(diffs, self.mat_slots)
         return out
 
     def to_rows(self, x: torch.Tensor, G: torch.Tensor) -> torch.Tensor:
@@ -144,9 +142,7 @@ class _CandidateDistances:
                 cand = self.mean - gamma * self.dev
                 diffs = cand[None, :] - self.G[1:]
                 dm = torch.zeros(K, dtype=torch.float64, device=self.G.device)
-                for s in self.engine.mat_slots:
-                    mats = diffs[:, s.offset:s.offset + s.numel].reshape(K - 1, s.shape[0], -1)
-                    dm[1:] += ops.batched_spectral_norm(mats).double()
+                dm[1:] = ops.spectral_norm_sum(diffs, self.engine.mat_slots)
                 d = d + dm
         d = d.clone()
         d[0] = 0.0  # A-7: row 0 *is* the candidate

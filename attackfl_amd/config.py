@@ -24,6 +24,7 @@ Extensions (all optional, defaults keep reference behaviour):
   seed: int                         (torch / client RNG seed; the reference seeds only ``random``)
   metrics: path of the JSONL metrics file ('' disables)
   checkpoint-dir: where ``*.pth`` files go (reference: CWD)
+  async-checkpoint: bool            (default True: the leader writes ``*.pth`` from a background thread)
   compat-hyper-resume: bool         (True = reproduce reference A-5: a loaded hyper checkpoint is discarded)
   compat-fltrust: bool              (True = reproduce reference A-10: FLTrust subtracts the global model twice)
   max-retries: int                  (consecutive failed rounds before the run aborts)
@@ -75,7 +76,7 @@ EXTENSION_DEFAULTS: Dict[str, Any] = {
     "data": {"synthetic": "auto", "train-size": 60000, "test-size": 10000, "seed": 1234,
              "har-train-size": 2048, "har-test-size": 512, "root": "."},
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
-               "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
+               "async-checkpoint": True, "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
                "fault-inject": [], "save-state": False, "resume": False},
 }
 

@@ -37,6 +37,7 @@ from ..eval import Validation
 from ..models import ParamLayout, build_model
 from ..parallel.comm import Comm, LoopbackComm
 from ..utils import trace
+from ..utils.ckpt import CheckpointWriter
 from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
 from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
@@ -95,6 +96,8 @@ class FLEngine:
         self.data_name = cfg.data_name
         self.seed = int(cfg.engine.get("seed", 0))
         self.ckpt_dir = cfg.engine.get("checkpoint-dir", ".")
+        self.ckpt_writer = CheckpointWriter(bool(cfg.engine.get("async-checkpoint", True)))
+        self._saved_params: Optional[torch.Tensor] = None
         self.max_retries = int(cfg.engine.get("max-retries", 50))
         self.layout = ParamLayout.for_model(self.model_name)
         self.P = self.layout.P
@@ -200,13 +203,22 @@ class FLEngine:
             self.fltrust_model = self.layout.flatten(m.state_dict(), device=self.device)
 
     def save_checkpoint(self):
+        """Reference ``server.py:551-553`` (same files and keys).  Every rank remembers the saved
+        global model (what ``{model}.pth`` now holds) so ``load: True`` rounds need no file read;
+        the leader writes the file in the background (``utils/ckpt.py``)."""
+        if self.mode != "hyper" and self.global_params is not None:
+            self._saved_params = self.global_params.detach().clone()
         if not self.leader:
             return
         os.makedirs(self.ckpt_dir, exist_ok=True)
         if self.mode == "hyper":
-            torch.save(self.hyper.hnet.state_dict(), self._pth(True))
+            hnet = self.hyper.hnet
+            self.ckpt_writer.submit("hyper", hnet.arena, lambda a: hnet.state_dict_of(a, clone=False),
+                                    self._pth(True))
         elif self.global_params is not None:
-            torch.save(self.layout.unflatten(self.global_params.detach().cpu()), self._pth(False))
+            layout = self.layout
+            self.ckpt_writer.submit("global", self.global_params, lambda f: layout.unflatten(f, clone=False),
+                                    self._pth(False))
 
     # ---- resumable run state (new: the reference persists only the model, SURVEY §5.4) ----
     def _state_paths(self):
@@ -278,6 +290,9 @@ class FLEngine:
         if self.mode == "hyper":
             return self.hyper.generate(i)
         if self.cfg.load_parameters:
+            if self._saved_params is not None:  # == the file this run last wrote
+                return self._saved_params
+            self.ckpt_writer.flush()
             p = self._pth(False)
             if os.path.exists(p):
                 return self.layout.flatten(torch.load(p, weights_only=True, map_location="cpu"), device=self.device)
@@ -590,9 +605,11 @@ class FLEngine:
                 break
         if self.verbose and self.rounds_left <= 0:
             print_with_color("Training finished, stopping clients.", "green")
+        self.ckpt_writer.flush()
         return self.history
 
     def close(self):
+        self.ckpt_writer.close()
         self.metrics.close()
         if hasattr(self.logger, "close"):
             self.logger.close()

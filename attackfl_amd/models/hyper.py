@@ -167,16 +167,27 @@ class PackedHyperNet:
         self.load_state_dict(hnet.state_dict(), strict=False)
 
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        return self.state_dict_of(self.arena.detach().cpu())
+
+    def state_dict_of(self, arena: torch.Tensor, clone: bool = True) -> "OrderedDict[str, torch.Tensor]":
+        """Reference ``HyperNetwork`` state_dict built from a host copy of the arena (views when
+        ``clone`` is False: the caller owns ``arena`` until the dict is consumed)."""
+        def v(name):
+            off, shp = self.slots[name]
+            n = 1
+            for x in shp:
+                n *= x
+            t = arena[off:off + n].view(shp)
+            return t.clone() if clone else t
+
         sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
-        for k, v in self.target_sd.items():
-            sd[f"target_model.{k}"] = v.clone()
-        sd["embeddings.weight"] = self.emb.detach().cpu().clone()
+        for k, t in self.target_sd.items():
+            sd[f"target_model.{k}"] = t.clone()
+        sd["embeddings.weight"] = v("emb")
         for i in range(self.n_hidden + 1):
-            Wm, bm = self.mlp(i)
-            sd[f"mlp.{2 * i}.weight"] = Wm.detach().cpu().clone()
-            sd[f"mlp.{2 * i}.bias"] = bm.detach().cpu().clone()
-        W = self.W.detach().cpu()
-        b = self.b.detach().cpu()
+            sd[f"mlp.{2 * i}.weight"] = v(f"mlp{i}.W")
+            sd[f"mlp.{2 * i}.bias"] = v(f"mlp{i}.b")
+        W, b = v("W"), v("b")
         off = 0
         for k, n in zip(self.keys, self.numels):
             safe = k.replace(".", "__")

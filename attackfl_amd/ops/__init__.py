@@ -119,6 +119,51 @@ def batched_spectral_norm(mats: torch.Tensor) -> torch.Tensor:
     return composite.batched_spectral_norm(mats)
 
 
+_SPEC_CACHE = {}
+
+
+def _spectral_table(slots, device):
+    """(tab [S', 4] int32 for slots with min(r, c) <= 128, max n, scratch floats per row, big slots)."""
+    key = (tuple((s.offset, s.numel, s.shape[0]) for s in slots), str(device))
+    if key not in _SPEC_CACHE:
+        rows, big, scr, max_n = [], [], 0, 0
+        for s in slots:
+            r = int(s.shape[0])
+            c = s.numel // r
+            n = min(r, c)
+            if n > 128:
+                big.append(s)
+                continue
+            n8 = (n + 7) & ~7
+            rows.append((s.offset, r, c, scr))
+            scr += n8 * n8
+            max_n = max(max_n, n)
+        tab = torch.tensor(rows, dtype=torch.int32).reshape(-1, 4).to(device)
+        _SPEC_CACHE[key] = (tab, max_n, scr, big)
+    return _SPEC_CACHE[key]
+
+
+def spectral_norm_sum(diffs: torch.Tensor, slots) -> torch.Tensor:
+    """sum over matrix slots of ||diffs[m, slot]||_2 (slot viewed as [shape[0], -1]) -> [M] fp64.
+
+    Device: every (row, slot) pair in one ragged launch (reference src/Utils.py:47 per-tensor norm)."""
+    if _dev(diffs):
+        diffs = diffs.contiguous()
+        tab, max_n, scr, big = _spectral_table(slots, diffs.device)
+        out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
+        if tab.shape[0]:
+            out += native().spectral_norm_slots(diffs, tab, max_n, scr).sum(dim=1)
+        for s in big:
+            mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], s.shape[0], -1)
+            out += native().spectral_norm(mats.contiguous())
+        return out
+    out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
+    for s in slots:
+        mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], s.shape[0], -1)
+        out += composite.batched_spectral_norm(mats)
+    return out
+
+
 def attack_coeffs(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tensor):
     if _dev(G):
         A, B, C = attack_coeffs_segments(G, mean, dev, [_WholeSlot(G.shape[1])])

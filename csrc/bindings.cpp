@@ -118,6 +118,22 @@ torch::Tensor spectral_norm(torch::Tensor X) {
   return out;
 }
 
+// D [M, P] fp32, tab [S, 4] int32 (off, r, c, scratch off; min(r, c) <= 128), scr = scratch per row -> [M, S] fp64
+torch::Tensor spectral_norm_slots(torch::Tensor D, torch::Tensor tab, int64_t max_n, int64_t scr) {
+  check_dev(D, "D", torch::kFloat32);
+  check_dev(tab, "tab", torch::kInt32);
+  TORCH_CHECK(D.dim() == 2 && tab.dim() == 2 && tab.size(1) == 4, "spectral_norm_slots: bad shapes");
+  const int M = D.size(0), S = tab.size(0);
+  auto out = torch::empty({M, S}, D.options().dtype(torch::kFloat64));
+  if (M == 0 || S == 0) return out;
+  auto scratch = torch::empty({(long)M * scr}, D.options());
+  TORCH_CHECK(afl_spectral_slots(D.data_ptr<float>(), M, D.size(1), tab.data_ptr<int>(), S, (int)max_n,
+                                 scratch.data_ptr<float>(), scr, out.data_ptr<double>(), cur()) == 0,
+              "spectral_norm_slots launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 torch::Tensor weighted_rows(torch::Tensor U, torch::Tensor w) {
   check_dev(U, "U", torch::kFloat32);
   check_dev(w, "w", torch::kFloat64);
@@ -326,6 +342,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_sqsum", &segment_sqsum);
   m.def("attack_coeffs", &attack_coeffs);
   m.def("spectral_norm", &spectral_norm);
+  m.def("spectral_norm_slots", &spectral_norm_slots);
   m.def("weighted_rows", &weighted_rows);
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);

@@ -31,6 +31,8 @@ void afl_hyper_adam(float* W, float* bvec, float* m, float* v, const float* delt
 // linalg.hip
 int afl_spectral_scratch(int r, int c);
 int afl_spectral(const float* X, int B, int r, int c, float* G0, double* out, hipStream_t s);
+int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int max_n, float* G0, long scr,
+                       double* out, hipStream_t st);
 
 // metrics.hip
 void afl_roc_auc_sorted(const float* s, const float* y, int n, double* out, hipStream_t st);

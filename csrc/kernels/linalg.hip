@@ -13,11 +13,10 @@
 constexpr int SN_NMAX = 128;
 constexpr int SN_SQUARINGS = 12;
 
-__global__ void __launch_bounds__(256) k_spectral(const float* __restrict__ X, int r, int c, float* __restrict__ G0,
-                                                  double* __restrict__ out) {
+// sigma_max of the r x c matrix x (row stride c) -> *out; g0 = n8*n8 floats of global scratch
+__device__ __forceinline__ void spectral_one(const float* __restrict__ x, int r, int c, float* __restrict__ g0,
+                                             double* __restrict__ out) {
   extern __shared__ float lds[];
-  const int b = blockIdx.x;
-  const float* x = X + (long)b * r * c;
   const bool rows = r <= c;  // Gram over the smaller side
   const int n = rows ? r : c;
   const int k = rows ? c : r;
@@ -25,7 +24,6 @@ __global__ void __launch_bounds__(256) k_spectral(const float* __restrict__ X, i
   const int ld = n8 + 4;  // padded row stride
   float* A = lds;
   float* B = lds + n8 * ld;
-  float* g0 = G0 + (long)b * n8 * n8;
   __shared__ float red[4];
   __shared__ int sidx;
   const int tid = threadIdx.x;
@@ -151,8 +149,39 @@ __global__ void __launch_bounds__(256) k_spectral(const float* __restrict__ X, i
     double nn = dred[0][0] + dred[0][1] + dred[0][2] + dred[0][3];
     double dd = dred[1][0] + dred[1][1] + dred[1][2] + dred[1][3];
     double lam = dd > 0 ? nn / dd : 0.0;
-    out[b] = lam > 0 ? sqrt(lam) : 0.0;
+    *out = lam > 0 ? sqrt(lam) : 0.0;
   }
+}
+
+__global__ void __launch_bounds__(256) k_spectral(const float* __restrict__ X, int r, int c, float* __restrict__ G0,
+                                                  double* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int n = r <= c ? r : c;
+  const int n8 = (n + 7) & ~7;
+  spectral_one(X + (long)b * r * c, r, c, G0 + (long)b * n8 * n8, out + b);
+}
+
+// Ragged batch: every (row m, slot s) pair of D [M, P] in ONE launch, slot s = the r x c matrix at
+// column offset tab[s].off of row m (all slots of a model at once instead of one launch per shape).
+// tab[s] = {off, r, c, scratch offset}; scratch row stride = scr; out [M, S].
+__global__ void __launch_bounds__(256) k_spectral_slots(const float* __restrict__ D, long P, const int4* __restrict__ tab,
+                                                        int S, float* __restrict__ G0, long scr, double* __restrict__ out) {
+  const int s = blockIdx.x, m = blockIdx.y;
+  const int4 t = tab[s];
+  spectral_one(D + (long)m * P + t.x, t.y, t.z, G0 + (long)m * scr + t.w, out + (long)m * S + s);
+}
+
+int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int max_n, float* G0, long scr,
+                       double* out, hipStream_t st) {
+  if (max_n > SN_NMAX) return -1;
+  int n8 = (max_n + 7) & ~7;
+  size_t lds = (size_t)2 * n8 * (n8 + 4) * sizeof(float);
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute((const void*)k_spectral_slots, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -2;
+  hipLaunchKernelGGL(k_spectral_slots, dim3(S, M), dim3(256), lds, st, D, P, (const int4*)tab, S, G0, scr, out);
+  return 0;
 }
 
 int afl_spectral_scratch(int r, int c) {

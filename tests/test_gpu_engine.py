@@ -40,3 +40,31 @@ def test_engine_rounds_native(gpu, tmp_path, model, data, kind, mode):
     assert sum(r["ok"] for r in hist) == 2
     assert all(0.0 <= r["metric"] <= 1.0 for r in hist)
     assert os.path.exists(os.path.join(tmp_path, "app.log"))
+
+
+def test_async_checkpoint_files(gpu, tmp_path):
+    """Background-written checkpoints hold the final global / hypernetwork (reference file names)."""
+    import torch
+
+    from attackfl_amd.utils.ckpt import CheckpointWriter
+
+    w = CheckpointWriter()
+    src = torch.arange(1 << 20, dtype=torch.float32, device="cuda")
+    w.submit("x", src, lambda t: {"t": t.clone()}, str(tmp_path / "x.pth"))
+    src.zero_()  # ordered after the copy on the stream: the file keeps the old values
+    w.close()
+    got = torch.load(tmp_path / "x.pth", weights_only=True)["t"]
+    assert torch.equal(got, torch.arange(1 << 20, dtype=torch.float32))
+
+    d = {"server": {"num-round": 2, "clients": 3, "mode": "hyper", "model": "RNNModel", "data-name": "ICU",
+                    "data-distribution": {"num-data-range": [200, 300]}},
+         "learning": {"epoch": 1, "batch-size": 128},
+         "data": {"synthetic": True, "train-size": 2000, "test-size": 500},
+         "engine": {"checkpoint-dir": str(tmp_path)}, "log_path": str(tmp_path)}
+    eng = FLEngine(from_dict(d), device="cuda", verbose=False)
+    eng.run()
+    sd_live = eng.hyper.hnet.state_dict()
+    eng.close()
+    sd = torch.load(tmp_path / "RNNModel_hyper_3.pth", weights_only=True)
+    assert list(sd.keys()) == list(sd_live.keys())
+    assert all(torch.equal(sd[k], sd_live[k]) for k in sd)

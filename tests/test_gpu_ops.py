@@ -73,6 +73,27 @@ def test_spectral_norm(gpu, shape):
     assert torch.allclose(got, ref, rtol=2e-5), (got, ref)
 
 
+@pytest.mark.parametrize("model", ["RNNModel", "CNNModel", "TransformerModel", "big"])
+def test_spectral_norm_slots(gpu, model):
+    """One ragged launch over every matrix slot of a model == per-slot fp64 SVD norms."""
+    from attackfl_amd.attacks import DistanceEngine
+    from attackfl_amd.models import TensorSlot
+
+    if model == "big":  # a slot past the Gram kernel's 128 limit goes to the library, mixed with small ones
+        layout = ParamLayout([TensorSlot("a", (200, 150), 0, 30000), TensorSlot("b", (7,), 30000, 7),
+                              TensorSlot("c", (96, 7), 30007, 672)])
+    else:
+        layout = ParamLayout.for_model(model)
+    eng = DistanceEngine(layout, "spectral")
+    g = torch.Generator().manual_seed(3)
+    D = torch.randn(6, layout.P, generator=g) * 0.05
+    got = ops.spectral_norm_sum(D.to(gpu), eng.mat_slots).cpu()
+    ref = sum(C.batched_spectral_norm(D[:, s.offset:s.offset + s.numel].reshape(6, s.shape[0], -1))
+              for s in eng.mat_slots)
+    assert torch.allclose(got, ref, rtol=2e-5), (got, ref)
+    assert torch.allclose(ops.spectral_norm_sum(D, eng.mat_slots), ref, rtol=1e-12)
+
+
 def test_spectral_degenerate(gpu):
     X = torch.zeros(3, 16, 16)
     X[0] = torch.eye(16) * 2.0          # repeated top singular value
