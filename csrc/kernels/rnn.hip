@@ -115,12 +115,9 @@ __device__ __forceinline__ void st8(gf* p, const float* x) {
 
 // branch output y (16 values: columns q*8..+7 and 32+q*8..+7 of row r) -> hand-off slot (bf16)
 __device__ __forceinline__ void put_out(const Ctx& c, long slot, int r, int q, const float* y) {
-  gu64* d = (gu64*)((gu16*)c.wsf(slot) + opaque(r * 64 + q * 8));
-  const u64x2 a = __builtin_bit_cast(u64x2, pack8bf(y)), b = __builtin_bit_cast(u64x2, pack8bf(y + 8));
-  st_wt(d + 0, a[0]);
-  st_wt(d + 1, a[1]);
-  st_wt(d + 8, b[0]);  // +32 columns = 64 bytes = 8 granules
-  st_wt(d + 9, b[1]);
+  const int bo = (int)slot * 4 + opaque(r * 64 + q * 8) * 2;
+  st_wt16(c, bo, __builtin_bit_cast(u32x4, pack8bf(y)));
+  st_wt16(c, bo + 64, __builtin_bit_cast(u32x4, pack8bf(y + 8)));  // +32 columns = 64 bytes
 }
 
 // ============================================================================ branch workgroup
@@ -268,15 +265,21 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
       // ---------------- backward ----------------
       float dh[16];
       {  // d(branch output) -> dropout' -> LayerNorm backward; colsums gamma (v0), beta (v1)
-        gu64* src = (gu64*)(c.wsf(W_XB + BR * BM * 64) + opaque(r * 64 + q * 8));
+        const long so = W_XB + BR * BM * 64 + opaque(r * 64 + q * 8);
         float dy[16], xh[16], gm[16];
+        {  // columns q*8..+7 and 32+q*8..+7
+          u32x4 v[4];
+          v[0] = ld_wt16(c, (int)so * 4);
+          v[1] = ld_wt16(c, (int)so * 4 + 16);
+          v[2] = ld_wt16(c, (int)(so + 32) * 4);
+          v[3] = ld_wt16(c, (int)(so + 32) * 4 + 16);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const unsigned long long lo = ld_wt(src + k), hi = ld_wt(src + 16 + k);  // +32 columns = 16 granules
-          dy[2 * k] = __uint_as_float((uint32_t)lo);
-          dy[2 * k + 1] = __uint_as_float((uint32_t)(lo >> 32));
-          dy[8 + 2 * k] = __uint_as_float((uint32_t)hi);
-          dy[8 + 2 * k + 1] = __uint_as_float((uint32_t)(hi >> 32));
+          for (int k = 0; k < 4; ++k) {
+            dy[4 * k] = __uint_as_float(v[k].x);
+            dy[4 * k + 1] = __uint_as_float(v[k].y);
+            dy[4 * k + 2] = __uint_as_float(v[k].z);
+            dy[4 * k + 3] = __uint_as_float(v[k].w);
+          }
         }
         const gf* xs = sav + SAV_XH + opaque(r) * 64 + q * 8;
         load8(*(float(*)[8])xh, xs);
@@ -453,12 +456,8 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       }
 #pragma unroll
       for (int br = 0; br < 2; ++br) {  // branch outputs -> CAT (this lane: 16 columns of its row)
-        gu64* src = (gu64*)((gu16*)c.wsf(W_XF + br * BM * 32) + opaque(r * 64 + q * 16));
-        u64x2 lo, hi;
-        lo[0] = ld_wt(src + 0);
-        lo[1] = ld_wt(src + 1);
-        hi[0] = ld_wt(src + 2);
-        hi[1] = ld_wt(src + 3);
+        const int bo = (int)(W_XF + br * BM * 32) * 4 + opaque(r * 64 + q * 16) * 2;
+        const u32x4 lo = ld_wt16(c, bo), hi = ld_wt16(c, bo + 16);
         *(LDS_AS s8v*)(CAT + r * LDC + br * 64 + q * 16) = __builtin_bit_cast(s8v, lo);
         *(LDS_AS s8v*)(CAT + r * LDC + br * 64 + q * 16 + 8) = __builtin_bit_cast(s8v, hi);
       }

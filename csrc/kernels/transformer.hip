@@ -300,13 +300,9 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = x[j] * g3[j] + b3[j];
     if (XCH) {
-      gu64* d = (gu64*)((gu16*)c.wsf(W_XF + BR * BM * 32) + ro);
-      const s8v lo = pack8bf(x), hi = pack8bf(x + 8);
-      const auto l2 = __builtin_bit_cast(u64x2, lo), h2 = __builtin_bit_cast(u64x2, hi);
-      st_wt(d + 0, l2[0]);
-      st_wt(d + 1, l2[1]);
-      st_wt(d + 2, h2[0]);
-      st_wt(d + 3, h2[1]);
+      const int bo = (int)(W_XF + BR * BM * 32) * 4 + ro * 2;
+      st_wt16(c, bo, __builtin_bit_cast(u32x4, pack8bf(x)));
+      st_wt16(c, bo + 16, __builtin_bit_cast(u32x4, pack8bf(x + 8)));
     } else {
       store16bf(CAT + r * LD128 + BR * 64 + c0, x);
     }
@@ -348,13 +344,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     } else if (DY == 1) {
       load16(dy, c.wsf(W_DX3V) + ro);
     } else {  // hand-off slot written by the other workgroup: write-through granules, sc1 loads
-      gu64* src = (gu64*)(c.wsf(W_XB + BR * BM * 64) + ro);
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) {
-        const unsigned long long v = ld_wt(src + j / 2);
-        dy[j] = __uint_as_float((uint32_t)v);
-        dy[j + 1] = __uint_as_float((uint32_t)(v >> 32));
-      }
+      ld_wt_f16(c, W_XB + BR * BM * 64 + ro, dy);
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh3[j];
@@ -681,12 +671,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         }
 #pragma unroll
         for (int br = ROLE == 3 ? 0 : 1; br < 2; ++br) {
-          gu64* src = (gu64*)((gu16*)c.wsf(W_XF + br * BM * 32) + opaque(r * 64 + c0));
-          u64x2 lo, hi;
-          lo[0] = ld_wt(src + 0);
-          lo[1] = ld_wt(src + 1);
-          hi[0] = ld_wt(src + 2);
-          hi[1] = ld_wt(src + 3);
+          const int bo = (int)(W_XF + br * BM * 32) * 4 + opaque(r * 64 + c0) * 2;
+          const u32x4 lo = ld_wt16(c, bo), hi = ld_wt16(c, bo + 16);
           *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0) = __builtin_bit_cast(s8v, lo);
           *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0 + 8) = __builtin_bit_cast(s8v, hi);
         }
