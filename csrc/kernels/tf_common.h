@@ -99,6 +99,20 @@ __device__ __forceinline__ uint32_t hash3(uint32_t key, uint32_t layer, uint32_t
 __device__ __forceinline__ bool keep(uint32_t key, uint32_t layer, uint32_t r, uint32_t c, uint32_t thr16) {
   return ((hash3(key, layer, r, c >> 1) >> ((c & 1u) << 4)) & 0xFFFFu) >= thr16;
 }
+// keep() for columns c0 .. c0+N-1 (c0 even) as a bit mask (bit j = column c0 + j): computed once in the
+// forward and reused by the backward instead of re-hashing
+template <int N>
+__device__ __forceinline__ uint32_t keep_bits(uint32_t key, uint32_t layer, uint32_t r, uint32_t c0, uint32_t thr16) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < N; j += 2) {
+    const uint32_t h = hash3(key, layer, r, (c0 + j) >> 1);
+    m |= ((h & 0xFFFFu) >= thr16 ? 1u : 0u) << j;
+    m |= ((h >> 16) >= thr16 ? 1u : 0u) << (j + 1);
+  }
+  return m;
+}
+__device__ __forceinline__ bool bit(uint32_t m, int j) { return (m >> j) & 1u; }
 
 constexpr uint32_t THR_P01 = 6554u;    // round(0.1 * 2^16)
 constexpr uint32_t THR_P03 = 19661u;   // round(0.3 * 2^16)

@@ -82,7 +82,7 @@ constexpr int WFF1 = 2 * BRW_SIZE, WTF1 = WFF1 + 64 * 128, WFF2 = WTF1 + 128 * 6
 constexpr int BF_TOTAL = WTF2 + 64 * 32;  // ushorts
 // saved activations (float offsets); every entry is written and re-read by the same lane
 constexpr long W_ACT = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
-struct BrS { long H0B, XH1, XH2, XH3, RS, F0; };
+struct BrS { long H0B, XH1, XH2, XH3, RS, F0, MK; };
 __host__ __device__ constexpr BrS brs(long base) {
   BrS s{};
   long p = base;
@@ -92,9 +92,10 @@ __host__ __device__ constexpr BrS brs(long base) {
   s.XH3 = p; p += BM * 64;
   s.RS = p; p += BM * 4 * 4;     // per lane: rstd1, rstd2, rstd3, pad
   s.F0 = p; p += BM * 8;
+  s.MK = p; p += BM * 16;        // per lane: dropout keep masks D1, DF, D2 (u32 bits), pad
   return s;
 }
-constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8;
+constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8 + BM * 16;
 constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
@@ -235,10 +236,12 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   float x1[16];  // x1 stays in registers until the second residual (E5)
   {
     const int ro = opaque(r * 64 + c0);
+    const uint32_t m1 = keep_bits<16>(s.key, 8 * BR + L_D1, r, c0, THR_P01);
+    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 0] = m1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const float o = ACC[r * LDACC + c0 + j] + bias[j];
-      x1[j] = h[j] + (keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? o * INV_K01 : 0.f);
+      x1[j] = h[j] + (bit(m1, j) ? o * INV_K01 : 0.f);
     }
     const float rstd = ln_fwd(x1);
     store16(c.wsf(B::s.XH1) + ro, x1);
@@ -257,6 +260,8 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   STAMP(3);
   {  // E4: f0 -> f2
     s8v v;
+    const uint32_t mf = q * 8 < FF ? keep_bits<8>(s.key, 8 * BR + L_DF, r, q * 8, THR_P01) : 0u;
+    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 1] = mf;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = q * 8 + j;
@@ -264,7 +269,7 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
       if (col < FF) {
         const float f0 = ACC[r * LDACC + col] + fb[j & 7];
         c.wsf(B::s.F0)[opaque(r * 8) + col] = f0;
-        f2 = keep(s.key, 8 * BR + L_DF, r, col, THR_P01) ? gelu(f0) * INV_K01 : 0.f;
+        f2 = bit(mf, j) ? gelu(f0) * INV_K01 : 0.f;
       }
       v[j] = (short)f2bf(f2);
     }
@@ -283,10 +288,12 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   {  // E5: r2 = x1 + drop(f3); LN2; LN3 -> CAT
     const int ro = opaque(r * 64 + c0);
     float x[16];
+    const uint32_t m2 = keep_bits<16>(s.key, 8 * BR + L_D2, r, c0, THR_P01);
+    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2] = m2;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const float f3 = ACC[r * LDACC + c0 + j] + bias[j];
-      x[j] = x1[j] + (keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? f3 * INV_K01 : 0.f);
+      x[j] = x1[j] + (bit(m2, j) ? f3 * INV_K01 : 0.f);
     }
     float rstd = ln_fwd(x);
     store16(c.wsf(B::s.XH2) + ro, x);
@@ -338,6 +345,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     load16(gm2, c.P + B::o.ln2_w + c0);
     const gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
     const float rstd2 = rs[1], rstd3 = rs[2];
+    const uint32_t m2 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2];
     if (DY == 0) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
@@ -357,12 +365,13 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     colsum16(c, 3, dx);
     ln_bwd(dr2, dx, xh2, rstd2, gm2);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D2, r, c0 + j, THR_P01) ? dr2[j] * INV_K01 : 0.f;
+    for (int j = 0; j < 16; ++j) t[j] = bit(m2, j) ? dr2[j] * INV_K01 : 0.f;
     store16bf(TA + r * LD64 + c0, t);
     colsum16(c, 4, t);
   }
   float f0v[8];
   load8(f0v, c.wsf(B::s.F0) + opaque(r * 8));
+  const uint32_t mf = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 1];
   BAR();
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2)
@@ -385,7 +394,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
       float d0 = 0.f, f2 = 0.f;
       if (col < FF) {
         const float f0 = f0v[j];
-        const bool kp = keep(s.key, 8 * BR + L_DF, r, col, THR_P01);
+        const bool kp = bit(mf, j);
         d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
         f2 = kp ? gelu(f0) * INV_K01 : 0.f;
       }
@@ -405,6 +414,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     load16(bt1, c.P + B::o.ln1_b + c0);
   }
   const float rstd1 = c.wsf(B::s.RS)[opaque(r * 16 + q * 4)];
+  const uint32_t m1 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 0];
   BAR();
   STAMP(12);
   gemm_pf<64, 32>(c, XIN, LD32, wt1);                    // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
@@ -425,7 +435,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     colsum16(c, 1, dx);
     ln_bwd(dh0, dx, xh1, rstd1, gm1);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = keep(s.key, 8 * BR + L_D1, r, c0 + j, THR_P01) ? dh0[j] * INV_K01 : 0.f;
+    for (int j = 0; j < 16; ++j) t[j] = bit(m1, j) ? dh0[j] * INV_K01 : 0.f;
     store16bf(TB + r * LD64 + c0, t);
     colsum16(c, 2, t);
 #pragma unroll
@@ -689,12 +699,14 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       BAR();
       STAMP(6);
       float y1[16];  // kept in registers until E8
+      uint32_t mh;   // its dropout mask bits
       {              // E6: y1 -> d1 = drop0.3(gelu(y1))
         float x[16];
+        mh = keep_bits<16>(s.key, L_HEAD, r, c0, THR_P03);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           y1[j] = ACC[r * LDACC + c0 + j] + bias[j];
-          x[j] = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? gelu(y1[j]) * INV_K03 : 0.f;
+          x[j] = bit(mh, j) ? gelu(y1[j]) * INV_K03 : 0.f;
         }
         store16bf(TA + r * LD64 + c0, x);
       }
@@ -774,7 +786,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         float d[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float g = keep(s.key, L_HEAD, r, c0 + j, THR_P03) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
+          const float g = bit(mh, j) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
           d[j] = g * gelu_grad(y1[j]);
         }
         store16bf(TB + r * LD64 + c0, d);
