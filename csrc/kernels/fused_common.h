@@ -437,28 +437,6 @@ template <class CT>
 __device__ __forceinline__ u32x4 ld_wt16(const CT& c, int byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(c.wrs(), byte_off, 0, 16);
 }
-// 16 fp32 <-> 4 x 16-B write-through granules at float offset `off` of the workspace
-template <class CT>
-__device__ __forceinline__ void st_wt_f16(const CT& c, long off, const float* x) {
-#pragma unroll
-  for (int j = 0; j < 16; j += 4)
-    st_wt16(c, (int)(off + j) * 4, u32x4{__float_as_uint(x[j]), __float_as_uint(x[j + 1]), __float_as_uint(x[j + 2]),
-                                         __float_as_uint(x[j + 3])});
-}
-template <class CT>
-__device__ __forceinline__ void ld_wt_f16(const CT& c, long off, float* x) {
-  u32x4 v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = ld_wt16(c, (int)(off + 4 * j) * 4);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    x[4 * j] = __uint_as_float(v[j].x);
-    x[4 * j + 1] = __uint_as_float(v[j].y);
-    x[4 * j + 2] = __uint_as_float(v[j].z);
-    x[4 * j + 3] = __uint_as_float(v[j].w);
-  }
-}
-
 template <class CT>
 __device__ __forceinline__ void xwg_publish(const CT& c, gu32* flag, uint32_t value) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -512,14 +490,26 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-// ACC row r, columns c0..c0+15 (fp32) -> hand-off slot (write-through 16-byte stores)
+// ACC row r, columns c0..c0+15 -> hand-off slot as bf16 (row stride 64; two write-through 16-byte
+// stores).  The gradient crosses in bf16, the precision its consumer's GEMM operands have anyway:
+// half the bytes on the step's critical hand-off.
 template <class CT>
 __device__ __forceinline__ void put_grad(const CT& c, long slot, int r, int c0) {
   const float* acc = c.acc() + r * CT::LDACC + c0;
   float x[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] = acc[j];
-  st_wt_f16(c, slot + opaque(r * 64 + c0), x);
+  const int bo = (int)slot * 4 + opaque(r * 64 + c0) * 2;
+  st_wt16(c, bo, __builtin_bit_cast(u32x4, pack8bf(x)));
+  st_wt16(c, bo + 16, __builtin_bit_cast(u32x4, pack8bf(x + 8)));
+}
+// 8 bf16 packed in a 16-byte granule -> fp32
+__device__ __forceinline__ void unpack8bf(u32x4 v, float* x) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[2 * k] = __uint_as_float(v[k] << 16);
+    x[2 * k + 1] = __uint_as_float(v[k] & 0xFFFF0000u);
+  }
 }
 
 

@@ -72,7 +72,7 @@ constexpr long W_BF = ((2L * NPARAM + 63) / 64) * 64;
 constexpr long W_SAV = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
 constexpr long SAV_RZN = 0, SAV_XH = 6L * BM * G3, SAV_RS = SAV_XH + BM * 64, SAV_BR = SAV_RS + BM;
 constexpr long W_XF = W_SAV + 2 * SAV_BR;      // branch outputs bf16 [2][128][64]
-constexpr long W_XB = W_XF + 2 * BM * 32;      // d(branch outputs) fp32 [2][128][64]
+constexpr long W_XB = W_XF + 2 * BM * 32;      // d(branch outputs) bf16 [128][64] in fp32-sized slots [2][128][64]
 constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
 constexpr int XF_VIT = 0, XF_LAB = 1, XF_BWD = 2, XF_TMO = 3;
 
@@ -265,22 +265,10 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
       // ---------------- backward ----------------
       float dh[16];
       {  // d(branch output) -> dropout' -> LayerNorm backward; colsums gamma (v0), beta (v1)
-        const long so = W_XB + BR * BM * 64 + opaque(r * 64 + q * 8);
+        const int bo = (int)(W_XB + BR * BM * 64) * 4 + opaque(r * 64 + q * 8) * 2;  // bf16 [128][64] (put_grad)
         float dy[16], xh[16], gm[16];
-        {  // columns q*8..+7 and 32+q*8..+7
-          u32x4 v[4];
-          v[0] = ld_wt16(c, (int)so * 4);
-          v[1] = ld_wt16(c, (int)so * 4 + 16);
-          v[2] = ld_wt16(c, (int)(so + 32) * 4);
-          v[3] = ld_wt16(c, (int)(so + 32) * 4 + 16);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            dy[4 * k] = __uint_as_float(v[k].x);
-            dy[4 * k + 1] = __uint_as_float(v[k].y);
-            dy[4 * k + 2] = __uint_as_float(v[k].z);
-            dy[4 * k + 3] = __uint_as_float(v[k].w);
-          }
-        }
+        unpack8bf(ld_wt16(c, bo), dy);            // columns q*8 .. +7
+        unpack8bf(ld_wt16(c, bo + 64), dy + 8);   // columns 32 + q*8 .. +7
         const gf* xs = sav + SAV_XH + opaque(r) * 64 + q * 8;
         load8(*(float(*)[8])xh, xs);
         load8(*(float(*)[8])(xh + 8), xs + HU);

@@ -101,7 +101,7 @@ constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
 // branch-parallel mode hand-off slots (labs workgroup <-> vitals+head workgroup of one client)
 constexpr long W_XF = W_DX3V + BM * 64;  // branch outputs, bf16 [2][128][64] (vitals, labs)
-constexpr long W_XB = W_XF + 2 * BM * 32;  // d(branch outputs), fp32 [2][128][64]
+constexpr long W_XB = W_XF + 2 * BM * 32;  // d(branch outputs), bf16 [128][64] in fp32-sized slots [2][128][64]
 constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
 // hand-off words per client: [0] vitals output ready, [1] labs output ready, [2] d(outputs) ready
 // (value step << 1 | NaN abort), [3] timeout
@@ -352,7 +352,13 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     } else if (DY == 1) {
       load16(dy, c.wsf(W_DX3V) + ro);
     } else {  // hand-off slot written by the other workgroup: write-through granules, sc1 loads
-      ld_wt_f16(c, W_XB + BR * BM * 64 + ro, dy);
+      const int bo = (int)(W_XB + BR * BM * 64) * 4 + ro * 2;  // bf16 [128][64] (put_grad)
+      unpack8bf(ld_wt16(c, bo), dy);
+      unpack8bf(ld_wt16(c, bo + 16), dy + 8);
+    }
+    if (DY != 2) {  // same values as the bf16 hand-off of the branch-parallel launches
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dy[j] = bf2f(f2bf(dy[j]));
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh3[j];

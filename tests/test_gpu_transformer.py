@@ -93,8 +93,9 @@ def test_size_one_batch_skipped(gpu):
 
 
 def test_branch_parallel_matches_single_workgroup(gpu):  # noqa: D401
-    """The two-workgroup launch runs the same arithmetic as the one-workgroup launch (hand-offs move
-    exact fp32 / bf16 values; only the compiler's FMA contraction may differ per instantiation), so
+    """The two- and three-workgroup launches run the same arithmetic as the one-workgroup launch
+    (hand-offs move exact bf16 values, and the one-workgroup launch rounds the branch gradient to bf16
+    too; only the compiler's FMA contraction may differ per instantiation), so
     raw SGD updates agree to float rounding and Adam runs agree closely, including the partial and
     the skipped size-1 batch."""
     nd = [700, 513, 300]
