@@ -68,10 +68,11 @@ def main() -> int:
         comm = LoopbackComm(device)
     rank = comm.rank
     tmp = tempfile.mkdtemp(prefix=f"attackfl_bench_r{rank}_")
+    rows = [12000, 15000] if args.data_name == "ICU" else [1000, 1500]  # HAR: 7352-row train set
     cfg = from_dict({
         "server": {"num-round": args.warmup + args.steps + 1, "clients": args.clients, "mode": args.mode,
                    "model": args.model, "data-name": args.data_name, "validation": True,
-                   "data-distribution": {"num-data-range": [12000, 15000] if args.data_name == "ICU" else [1000, 1500]}},
+                   "data-distribution": {"num-data-range": rows}},
         "learning": {"epoch": 5, "batch-size": 128, "learning-rate": 0.004},
         "data": {"synthetic": True, "train-size": 60000, "test-size": 10000, "har-train-size": 7352,
                  "har-test-size": 2947},
@@ -124,9 +125,10 @@ def main() -> int:
             "dtype": "bf16",
             "data": ("synthetic ICU-shaped rows (planted signal)" if args.data_name == "ICU" else
                      "synthetic HAR-shaped sequences (L=561, 6 classes)") + ", random-init weights",
-            "config": {"model": args.model, "global_batch": 128 * args.clients, "seq_len": 1,
+            "config": {"model": args.model, "global_batch": 128 * args.clients,
+                       "seq_len": 1 if args.data_name == "ICU" else 561,
                        "parallelism": f"fl{args.clients}-clients-over-{comm.world}-ranks",
-                       "clients": args.clients, "local_epochs": 5, "rows_per_client": "12000-15000",
+                       "clients": args.clients, "local_epochs": 5, "rows_per_client": f"{rows[0]}-{rows[1]}",
                        "mode": args.mode, "trainer": eng.trainer.kind if eng.trainer else None,
                        "attackers": args.attackers or None},
             ("test_roc_auc" if args.data_name == "ICU" else "test_accuracy"): round(aucs[-1], 4) if aucs else None,
