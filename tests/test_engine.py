@@ -126,7 +126,8 @@ def _env():
     return env
 
 
-def test_packed_gloo_world2_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_packed_gloo_matches_single_process(tmp_path, world):
     d = _cfg(tmp_path, server__num_round=2)
     d["comm"] = {"backend": "gloo", "attackers": {3: {"mode": "LIE", "round": 1, "args": [0.5]}}}
     d["server"]["genuine-rate"] = 1.0  # K = 3 genuine models (K = 1 would make LIE's unbiased std NaN)
@@ -134,8 +135,8 @@ def test_packed_gloo_world2_matches_single_process(tmp_path):
     d["log_path"] = str(tmp_path / "mp")
     cfg_path = _write_cfg(tmp_path, d)
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "launch.py"), "--config", cfg_path,
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "launch.py"), "--config", cfg_path,
            "--device", "cpu"]
     r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
