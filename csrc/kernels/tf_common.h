@@ -83,6 +83,12 @@ __device__ __forceinline__ float gelu_grad(float x) {
   const GeluPair g = gelu_parts(x);
   return fmaf(x, g.pdf, g.cdf);
 }
+// GELU and its derivative from one erf/exp evaluation (the forward keeps gelu' for the backward)
+__device__ __forceinline__ float gelu_and_grad(float x, float& gp) {
+  const GeluPair g = gelu_parts(x);
+  gp = fmaf(x, g.pdf, g.cdf);
+  return x * g.cdf;
+}
 __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // dropout keep-test from a stateless hash of (step key, layer, row, column pair): one 32-bit hash

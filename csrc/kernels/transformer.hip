@@ -82,7 +82,7 @@ constexpr int WFF1 = 2 * BRW_SIZE, WTF1 = WFF1 + 64 * 128, WFF2 = WTF1 + 128 * 6
 constexpr int BF_TOTAL = WTF2 + 64 * 32;  // ushorts
 // saved activations (float offsets); every entry is written and re-read by the same lane
 constexpr long W_ACT = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
-struct BrS { long H0B, XH1, XH2, XH3, RS, F0, MK; };
+struct BrS { long H0B, XH1, XH2, XH3, RS, F0, MK, GPD, F2S; };
 __host__ __device__ constexpr BrS brs(long base) {
   BrS s{};
   long p = base;
@@ -93,9 +93,11 @@ __host__ __device__ constexpr BrS brs(long base) {
   s.RS = p; p += BM * 4 * 4;     // per lane: rstd1, rstd2, rstd3, pad
   s.F0 = p; p += BM * 8;
   s.MK = p; p += BM * 16;        // per lane: dropout keep masks D1, DF, D2 (u32 bits), pad
+  s.GPD = p; p += BM * 64;       // gelu'(z0) of the dense layer
+  s.F2S = p; p += BM * 8;        // f2 = drop(gelu(f0)) (F0 holds drop'(.) * gelu'(f0))
   return s;
 }
-constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8 + BM * 16;
+constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8 + BM * 16 + BM * 64 + BM * 8;
 constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
@@ -196,9 +198,11 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   STAMP(0);
   float h[16];  // h0 stays in registers until the residual (E3)
   {
+    float gp[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) h[j] = gelu(ACC[r * LDACC + c0 + j] + bias[j]);
+    for (int j = 0; j < 16; ++j) h[j] = gelu_and_grad(ACC[r * LDACC + c0 + j] + bias[j], gp[j]);
     store16bf(TA + r * LD64 + c0, h);
+    store16(c.wsf(B::s.GPD) + opaque(r * 64 + c0), gp);
     gu16* hb = (gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
     s8v a, b;
 #pragma unroll
@@ -261,15 +265,17 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   {  // E4: f0 -> f2
     s8v v;
     const uint32_t mf = q * 8 < FF ? keep_bits<8>(s.key, 8 * BR + L_DF, r, q * 8, THR_P01) : 0u;
-    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 1] = mf;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = q * 8 + j;
       float f2 = 0.f;
       if (col < FF) {
-        const float f0 = ACC[r * LDACC + col] + fb[j & 7];
-        c.wsf(B::s.F0)[opaque(r * 8) + col] = f0;
-        f2 = bit(mf, j) ? gelu(f0) * INV_K01 : 0.f;
+        float gp;
+        const float g = gelu_and_grad(ACC[r * LDACC + col] + fb[j & 7], gp);
+        const bool kp = bit(mf, j);
+        f2 = kp ? g * INV_K01 : 0.f;
+        c.wsf(B::s.F0)[opaque(r * 8) + col] = kp ? gp * INV_K01 : 0.f;
+        c.wsf(B::s.F2S)[opaque(r * 8) + col] = f2;
       }
       v[j] = (short)f2bf(f2);
     }
@@ -375,9 +381,9 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     store16bf(TA + r * LD64 + c0, t);
     colsum16(c, 4, t);
   }
-  float f0v[8];
-  load8(f0v, c.wsf(B::s.F0) + opaque(r * 8));
-  const uint32_t mf = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 1];
+  float gk[8], f2s[8];  // drop'(.) * gelu'(f0) and f2 of the forward
+  load8(gk, c.wsf(B::s.F0) + opaque(r * 8));
+  load8(f2s, c.wsf(B::s.F2S) + opaque(r * 8));
   BAR();
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2)
@@ -391,7 +397,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   wload(wt1, c.BF + B::w.WT1, c.lane);
   BAR();
   STAMP(11);
-  {  // E11: df0 (-> DF0 = XIN region), recompute f2 (-> F2); colsum b1 (v5)
+  {  // E11: df0 (-> DF0 = XIN region), f2 (-> F2); colsum b1 (v5)
     s8v vd, vf;
     float db[8];
 #pragma unroll
@@ -399,10 +405,8 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
       const int col = q * 8 + j;
       float d0 = 0.f, f2 = 0.f;
       if (col < FF) {
-        const float f0 = f0v[j];
-        const bool kp = bit(mf, j);
-        d0 = kp ? ACC[r * LDACC + col] * INV_K01 * gelu_grad(f0) : 0.f;
-        f2 = kp ? gelu(f0) * INV_K01 : 0.f;
+        d0 = ACC[r * LDACC + col] * gk[j];
+        f2 = f2s[j];
       }
       db[j] = d0;
       vd[j] = (short)f2bf(d0);
@@ -496,26 +500,23 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   gemm_pf<64, 64>(c, TC, LD64, wtv);                       // dh0 part = dv . Wv
   gemm_dw_adam<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K);  // dWo = do^T a
   if (c.tid < 64) adam(c.P, c.M, c.V, B::o.inproj_b + 128 + c.tid, cs_total(c, 3, c.tid), K);
-  WFr<64, 32> wd;
-  wload(wd, c.BF + B::w.WFd, c.lane);
-  float bd[16];
-  load16(bd, c.P + B::o.dense_b + c0);
+  float gpd[16];  // gelu'(z0) of the forward
+  load16(gpd, c.wsf(B::s.GPD) + opaque(r * 64 + c0));
   BAR();
   STAMP(18);
-  {  // E14: dh0 += ACC ; x for the z0 recompute
+  {  // E14: dh0 += ACC ; x for dWd
 #pragma unroll
     for (int j = 0; j < 16; ++j) dh0[j] += ACC[r * LDACC + c0 + j];
     put_x<BR>(c, s);
   }
   BAR();
   gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K);  // dWv = dv^T h0
-  gemm_pf<64, 32>(c, XIN, LD32, wd);                       // z0 recompute
   BAR();
   STAMP(19);
   {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
     float d[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) d[j] = dh0[j] * gelu_grad(ACC[r * LDACC + c0 + j] + bd[j]);
+    for (int j = 0; j < 16; ++j) d[j] = dh0[j] * gpd[j];
     store16bf(TB + r * LD64 + c0, d);
     colsum16(c, 4, d);
   }
@@ -704,15 +705,16 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       wload(wf2, c.BF + WFF2, c.lane);
       BAR();
       STAMP(6);
-      float y1[16];  // kept in registers until E8
-      uint32_t mh;   // its dropout mask bits
-      {              // E6: y1 -> d1 = drop0.3(gelu(y1))
+      float gk1[16];  // drop'(.) * gelu'(y1), kept in registers until E8
+      {               // E6: y1 -> d1 = drop0.3(gelu(y1))
         float x[16];
-        mh = keep_bits<16>(s.key, L_HEAD, r, c0, THR_P03);
+        const uint32_t mh = keep_bits<16>(s.key, L_HEAD, r, c0, THR_P03);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          y1[j] = ACC[r * LDACC + c0 + j] + bias[j];
-          x[j] = bit(mh, j) ? gelu(y1[j]) * INV_K03 : 0.f;
+          float gp;
+          const float g = gelu_and_grad(ACC[r * LDACC + c0 + j] + bias[j], gp);
+          x[j] = bit(mh, j) ? g * INV_K03 : 0.f;
+          gk1[j] = bit(mh, j) ? gp * INV_K03 : 0.f;
         }
         store16bf(TA + r * LD64 + c0, x);
       }
@@ -727,12 +729,11 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       BAR();
       STAMP(7);
       {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
-        float y2[8], g2[8], dot = 0.f;
+        float gp2[8], g2[8], dot = 0.f;
         const int cc = q * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          y2[j] = ACC[r * LDACC + cc + j] + b2v[j];
-          g2[j] = gelu(y2[j]);
+          g2[j] = gelu_and_grad(ACC[r * LDACC + cc + j] + b2v[j], gp2[j]);
           dot += g2[j] * wov[j];
         }
         const float y3 = rsum4(dot) + bout;
@@ -752,7 +753,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           gw[j] = dy3 * g2[j];
-          dy2[j] = dy3 * wov[j] * gelu_grad(y2[j]);
+          dy2[j] = dy3 * wov[j] * gp2[j];
         }
         s8v v;
 #pragma unroll
@@ -791,10 +792,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
         float d[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float g = bit(mh, j) ? ACC[r * LDACC + c0 + j] * INV_K03 : 0.f;
-          d[j] = g * gelu_grad(y1[j]);
-        }
+        for (int j = 0; j < 16; ++j) d[j] = ACC[r * LDACC + c0 + j] * gk1[j];
         store16bf(TB + r * LD64 + c0, d);
         colsum16(c, 2, d);
       }
