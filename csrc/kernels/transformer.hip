@@ -82,7 +82,7 @@ constexpr int WFF1 = 2 * BRW_SIZE, WTF1 = WFF1 + 64 * 128, WFF2 = WTF1 + 128 * 6
 constexpr int BF_TOTAL = WTF2 + 64 * 32;  // ushorts
 // saved activations (float offsets); every entry is written and re-read by the same lane
 constexpr long W_ACT = ((W_BF + BF_TOTAL / 2 + 63) / 64) * 64;
-struct BrS { long H0B, XH1, XH2, XH3, RS, F0, MK, GPD, F2S; };
+struct BrS { long H0B, XH1, XH2, XH3, RS, F0, MK, GPD, F2S, AB; };
 __host__ __device__ constexpr BrS brs(long base) {
   BrS s{};
   long p = base;
@@ -95,9 +95,10 @@ __host__ __device__ constexpr BrS brs(long base) {
   s.MK = p; p += BM * 16;        // per lane: dropout keep masks D1, DF, D2 (u32 bits), pad
   s.GPD = p; p += BM * 64;       // gelu'(z0) of the dense layer
   s.F2S = p; p += BM * 8;        // f2 = drop(gelu(f0)) (F0 holds drop'(.) * gelu'(f0))
+  s.AB = p; p += BM * 64 / 2;    // bf16 a = head_dropout(v), the X operand of dWo
   return s;
 }
-constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8 + BM * 16 + BM * 64 + BM * 8;
+constexpr long BRS_SIZE = BM * 32 + 3L * BM * 64 + BM * 16 + BM * 8 + BM * 16 + BM * 64 + BM * 8 + BM * 32;
 constexpr BrS SV = brs(W_ACT);
 constexpr BrS SL = brs(W_ACT + BRS_SIZE);
 constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
@@ -220,12 +221,15 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   wload(wo, c.BF + B::w.WFo, c.lane);
   BAR();
   STAMP(1);
-  {  // E2: a = head_dropout(v)
+  {  // E2: a = head_dropout(v) (-> TB, and kept in the workspace for dWo)
     float x[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bias[j]) * m;
     store16bf(TB + r * LD64 + c0, x);
+    gu16* ab = (gu16*)c.wsf(B::s.AB) + opaque(r * 64 + c0);
+    *(GAS s8v*)ab = pack8bf(x);
+    *(GAS s8v*)(ab + 8) = pack8bf(x + 8);
   }
   load16(bias, c.P + B::o.out_b + c0);
   float g1[16], b1[16];
@@ -452,11 +456,14 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     for (int j = 0; j < 16; ++j) t[j] = xh1[j] * gm1[j] + bt1[j];
     store16bf(TC + r * LD64 + c0, t);
   }
-  s8v h0a, h0b;
+  s8v h0a, h0b, aa, ab;
   {
     const gu16* hb = (const gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
     h0a = *(const GAS s8v*)hb;
     h0b = *(const GAS s8v*)(hb + 8);
+    const gu16* abp = (const gu16*)c.wsf(B::s.AB) + opaque(r * 64 + c0);
+    aa = *(const GAS s8v*)abp;
+    ab = *(const GAS s8v*)(abp + 8);
   }
   BAR();
   STAMP(14);
@@ -466,13 +473,11 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     const VecG vs[3] = {{B::o.ln1_w, 64, 0}, {B::o.ln1_b, 64, 1}, {B::o.out_b, 64, 2}};
     adam_vecs(c, vs, K);
   }
-  WFr<64, 64> wfv;
-  wload(wfv, c.BF + B::w.WFv, c.lane);
-  float bv[16];
-  load16(bv, c.P + B::o.inproj_b + 128 + c0);
+  WFr<64, 64> wtv;
+  wload(wtv, c.BF + B::w.WTv, c.lane);
   BAR();
   STAMP(15);
-  {  // E13: dv (-> TC) ; h0 (-> TA) ; colsum bv (v3)
+  {  // E13: dv (-> TC) ; h0 (-> TA) ; a (-> TD) ; colsum bv (v3)
     float d[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
@@ -481,21 +486,11 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     colsum16(c, 3, d);
     *(LDS_AS s8v*)(TA + r * LD64 + c0) = h0a;
     *(LDS_AS s8v*)(TA + r * LD64 + c0 + 8) = h0b;
+    *(LDS_AS s8v*)(TD + r * LD64 + c0) = aa;
+    *(LDS_AS s8v*)(TD + r * LD64 + c0 + 8) = ab;
   }
   BAR();
   STAMP(16);
-  gemm_pf<64, 64>(c, TA, LD64, wfv);  // v recompute (before Wv's Adam)
-  WFr<64, 64> wtv;
-  wload(wtv, c.BF + B::w.WTv, c.lane);
-  BAR();
-  {  // E13b: a = head_dropout(v) -> TD
-    float x[16];
-    const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bv[j]) * m;
-    store16bf(TD + r * LD64 + c0, x);
-  }
-  BAR();
   STAMP(17);
   gemm_pf<64, 64>(c, TC, LD64, wtv);                       // dh0 part = dv . Wv
   gemm_dw_adam<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K);  // dWo = do^T a

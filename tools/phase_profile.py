@@ -21,7 +21,7 @@ from attackfl_amd.ops import transformer as T
 NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G4 ffn0+E4", 4: "F:G5 ffn3+E5 LN2/3",
          5: "F:branch tail", 6: "H:fc1+E6", 7: "H:fc2+E7 loss", 8: "H:bwd fc2 dX+E8", 9: "H:dcat+dWf2+dWf1",
          10: "B:E10 LN bwd", 11: "B:A10+G11", 12: "B:E11", 13: "B:G12+dW2", 14: "B:E12 LN1 bwd", 15: "B:G13+dW1",
-         16: "B:E13", 17: "B:G13b+E13b", 18: "B:G14+dWo", 19: "B:E14+dWv", 20: "B:E15+dWd",
+         16: "B:E13", 17: "B:(none)", 18: "B:G14+dWo", 19: "B:E14+dWv", 20: "B:E15+dWd",
          21: "X:publish+wait d(out)"}
 
 
