@@ -174,9 +174,12 @@ __device__ __forceinline__ void put_x(const Ctx& c, const St& s) {
 }
 
 // ============================================================== branch forward
-// XCH: publish the branch output to the hand-off slot W_XF (write-through stores) instead of LDS CAT
+// XCH: publish the branch output to the hand-off slot W_XF (write-through stores) instead of LDS CAT,
+// then raise *pub = pub_val; the backward's saved activations of the last phase are stored only after
+// the flag, so the publish drain (vmcnt 0) waits for the 16 KB payload, not for them too
 template <int BR, bool XCH = false>
-__device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
+__device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, gu32* pub = nullptr,
+                                           uint32_t pub_val = 0) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);
   unsigned short* TA = c.u16(S_TA);
@@ -297,32 +300,33 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   STAMP(4);
   {  // E5: r2 = x1 + drop(f3); LN2; LN3 -> CAT
     const int ro = opaque(r * 64 + c0);
-    float x[16];
+    float x[16], xh2[16], xh3[16];
     const uint32_t m2 = keep_bits<16>(s.key, 8 * BR + L_D2, r, c0, THR_P01);
-    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2] = m2;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const float f3 = ACC[r * LDACC + c0 + j] + bias[j];
-      x[j] = x1[j] + (bit(m2, j) ? f3 * INV_K01 : 0.f);
+      xh2[j] = x1[j] + (bit(m2, j) ? f3 * INV_K01 : 0.f);
     }
-    float rstd = ln_fwd(x);
-    store16(c.wsf(B::s.XH2) + ro, x);
-    gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
-    rs[1] = rstd;
+    const float rstd2 = ln_fwd(xh2);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = x[j] * g2[j] + bb2[j];
-    rstd = ln_fwd(x);
-    store16(c.wsf(B::s.XH3) + ro, x);
-    rs[2] = rstd;
+    for (int j = 0; j < 16; ++j) xh3[j] = xh2[j] * g2[j] + bb2[j];
+    const float rstd3 = ln_fwd(xh3);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = x[j] * g3[j] + b3[j];
+    for (int j = 0; j < 16; ++j) x[j] = xh3[j] * g3[j] + b3[j];
     if (XCH) {
       const int bo = (int)(W_XF + BR * BM * 32) * 4 + ro * 2;
       st_wt16(c, bo, __builtin_bit_cast(u32x4, pack8bf(x)));
       st_wt16(c, bo + 16, __builtin_bit_cast(u32x4, pack8bf(x + 8)));
+      xwg_publish(c, pub, pub_val);
     } else {
       store16bf(CAT + r * LD128 + BR * 64 + c0, x);
     }
+    ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2] = m2;
+    store16(c.wsf(B::s.XH2) + ro, xh2);
+    store16(c.wsf(B::s.XH3) + ro, xh3);
+    gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
+    rs[1] = rstd2;
+    rs[2] = rstd3;
   }
   BAR();
   STAMP(5);
@@ -656,8 +660,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (ROLE == -1 || ROLE == 0) fwd_branch<0>(c, s, stamps, t_prev);
       if (ROLE == -1) fwd_branch<1>(c, s, stamps, t_prev);
       if (BONLY >= 0) {  // branch-only workgroup: forward, hand-off, wait, backward
-        fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev);
-        xwg_publish(c, xflag + (BONLY == 1 ? XF_LAB : XF_VIT), (uint32_t)step);
+        fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev, xflag + (BONLY == 1 ? XF_LAB : XF_VIT),
+                                                 (uint32_t)step);
         const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
