@@ -94,6 +94,14 @@ struct CtxT {
     lane &= 63;
     wave &= 7;
   }
+  // Wave-local phase boundary: no s_barrier.  Valid where every LDS byte the next phase reads was
+  // written by the SAME wave (row-per-wave layout: a wave's GEMM rows, elementwise rows and A-operand
+  // rows coincide; a wave's LDS operations execute in order).  Keeps the opaque-address trick of bar().
+  __device__ __forceinline__ void soft() {
+    asm volatile("" : "+s"(P), "+s"(M), "+s"(V), "+s"(BF), "+s"(ws));
+    asm volatile("" : "+v"(r), "+v"(q), "+v"(lane), "+v"(wave));
+    bound();
+  }
   // Full barrier (drains global stores: publishes Adam's writes to every wave)
   __device__ __forceinline__ void full_sync() {
     __syncthreads();

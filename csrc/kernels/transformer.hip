@@ -162,6 +162,14 @@ struct St {
     q = c.q;           \
     c0 = q * 16;       \
   } while (0)
+// wave-local boundary (Ctx::soft): the next phase reads only LDS rows this wave wrote
+#define WBAR()         \
+  do {                 \
+    c.soft();          \
+    r = c.r;           \
+    q = c.q;           \
+    c0 = q * 16;       \
+  } while (0)
 
 // inputs of one branch -> XIN (bf16, K padded to 32)
 template <int BR>
@@ -192,13 +200,13 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   WFr<64, 32> wd;
   wload(wd, c.BF + B::w.WFd, c.lane);
   put_x<BR>(c, s);
-  BAR();
+  WBAR();
   gemm_pf<64, 32>(c, XIN, LD32, wd);
   WFr<64, 64> wv;
   wload(wv, c.BF + B::w.WFv, c.lane);
   float bias[16];
   load16(bias, c.P + B::o.dense_b + c0);
-  BAR();
+  WBAR();
   STAMP(0);
   float h[16];  // h0 stays in registers until the residual (E3)
   {
@@ -218,11 +226,11 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     *(GAS s8v*)(hb + 8) = b;
   }
   load16(bias, c.P + B::o.inproj_b + 128 + c0);
-  BAR();
+  WBAR();
   gemm_pf<64, 64>(c, TA, LD64, wv);
   WFr<64, 64> wo;
   wload(wo, c.BF + B::w.WFo, c.lane);
-  BAR();
+  WBAR();
   STAMP(1);
   {  // E2: a = head_dropout(v) (-> TB, and kept in the workspace for dWo)
     float x[16];
@@ -238,11 +246,11 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   float g1[16], b1[16];
   load16(g1, c.P + B::o.ln1_w + c0);
   load16(b1, c.P + B::o.ln1_b + c0);
-  BAR();
+  WBAR();
   gemm_pf<64, 64>(c, TB, LD64, wo);
   WFr<16, 64> w1;
   wload(w1, c.BF + B::w.WF1, c.lane);
-  BAR();
+  WBAR();
   STAMP(2);
   float x1[16];  // x1 stays in registers until the second residual (E5)
   {
@@ -263,11 +271,11 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   }
   float fb[8];
   load8(fb, c.P + B::o.ff0_b);  // 6 used (+2 beyond: next tensor, ignored)
-  BAR();
+  WBAR();
   gemm_pf<16, 64>(c, TC, LD64, w1);
   WFr<64, 32> w2;
   wload(w2, c.BF + B::w.WF2, c.lane);
-  BAR();
+  WBAR();
   STAMP(3);
   {  // E4: f0 -> f2
     s8v v;
@@ -294,9 +302,9 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   load16(bb2, c.P + B::o.ln2_b + c0);
   load16(g3, c.P + B::o.bn_w + c0);
   load16(b3, c.P + B::o.bn_b + c0);
-  BAR();
+  WBAR();
   gemm_pf<64, 32>(c, F2, LD32, w2);
-  BAR();
+  WBAR();
   STAMP(4);
   {  // E5: r2 = x1 + drop(f3); LN2; LN3 -> CAT
     const int ro = opaque(r * 64 + c0);
@@ -692,7 +700,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
           *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0) = __builtin_bit_cast(s8v, lo);
           *(LDS_AS s8v*)(CAT + r * LD128 + br * 64 + c0 + 8) = __builtin_bit_cast(s8v, hi);
         }
-        BAR();
+        WBAR();
       }
       // =============================== head forward + loss ===============================
       WFr<64, 128> wf1;
@@ -702,7 +710,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       gemm_pf<64, 128>(c, CAT, LD128, wf1);
       WFr<32, 64> wf2;
       wload(wf2, c.BF + WFF2, c.lane);
-      BAR();
+      WBAR();
       STAMP(6);
       float gk1[16];  // drop'(.) * gelu'(y1), kept in registers until E8
       {               // E6: y1 -> d1 = drop0.3(gelu(y1))
@@ -721,11 +729,11 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       load8(b2v, c.P + FC2_B + q * 8);
       load8(wov, c.P + OUT_W + q * 8);
       const float bout = c.P[OUT_B];
-      BAR();
+      WBAR();
       gemm_pf<32, 64>(c, TA, LD64, wf2);
       WFr<64, 32> wtf2;
       wload(wtf2, c.BF + WTF2, c.lane);
-      BAR();
+      WBAR();
       STAMP(7);
       {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
         float gp2[8], g2[8], dot = 0.f;
@@ -786,7 +794,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
       WFr<64, 64> wtf1a;
       wload(wtf1a, c.BF + WTF1, c.lane);
-      BAR();
+      WBAR();
       STAMP(8);
       {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
         float d[16];
@@ -795,7 +803,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         store16bf(TB + r * LD64 + c0, d);
         colsum16(c, 2, d);
       }
-      BAR();
+      WBAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1a);  // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
       if (ROLE == -1) {                     // one workgroup: dWf2 overlaps the dcat GEMMs
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
@@ -803,7 +811,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       }
       WFr<64, 64> wtf1b;
       wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
-      BAR();
+      WBAR();
       if (ROLE == 3) {  // vitals gradient -> its hand-off slot
         put_grad(c, W_XB, r, c0);
       } else {
@@ -812,9 +820,9 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         for (int j = 0; j < 16; ++j) t[j] = ACC[r * LDACC + c0 + j];
         store16(c.wsf(W_DX3V) + opaque(r * 64 + c0), t);
       }
-      BAR();
+      WBAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1b);  // dcat[:, 64:128] (kept in ACC for the labs branch)
-      BAR();
+      if (ROLE == -1) BAR(); else WBAR();  // ROLE -1: dWf1 below reads every wave's TB rows
       if (ROLE == 0 || ROLE == 3) {  // hand the gradients over first: the head's own updates overlap
         put_grad(c, W_XB + BM * 64, r, c0);
         xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);
