@@ -411,7 +411,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   gemm_pf<16, 64>(c, TA, LD64, wt2);
   WFr<64, 32> wt1;
   wload(wt1, c.BF + B::w.WT1, c.lane);
-  BAR();
+  WBAR();
   STAMP(11);
   {  // E11: df0 (-> DF0 = XIN region), f2 (-> F2); colsum b1 (v5)
     s8v vd, vf;
@@ -448,7 +448,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   if (c.tid < FF) adam(c.P, c.M, c.V, B::o.ff0_b + c.tid, cs_total(c, 5, c.tid), K);
   WFr<64, 64> wto;
   wload(wto, c.BF + B::w.WTo, c.lane);
-  BAR();
+  WBAR();
   STAMP(13);
   float dh0[16];  // residual gradient into h0, kept in registers until E15
   {  // E12: dx1 += dr2 ; LN1 bwd ; do ; x1 recompute ; colsums g1 (v0), be1 (v1), bo (v2)
@@ -509,14 +509,14 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   if (c.tid < 64) adam(c.P, c.M, c.V, B::o.inproj_b + 128 + c.tid, cs_total(c, 3, c.tid), K);
   float gpd[16];  // gelu'(z0) of the forward
   load16(gpd, c.wsf(B::s.GPD) + opaque(r * 64 + c0));
-  BAR();
+  WBAR();
   STAMP(18);
   {  // E14: dh0 += ACC ; x for dWd
 #pragma unroll
     for (int j = 0; j < 16; ++j) dh0[j] += ACC[r * LDACC + c0 + j];
     put_x<BR>(c, s);
   }
-  BAR();
+  WBAR();
   gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K);  // dWv = dv^T h0
   BAR();
   STAMP(19);
