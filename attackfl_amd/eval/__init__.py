@@ -38,15 +38,15 @@ class Validation:
         ds = dataset if dataset is not None else resolve_dataset(data_name, "test", data_cfg, verbose=verbose)
         self.table = DeviceTable(ds, self.device)
         self.last_metric: float = float("nan")
-        self._runner = None
+        self._runners = {}
 
-    def _program_runner(self):
-        if self._runner is None:
+    def _program_runner(self, C: int = 1):
+        if C not in self._runners:
             from ..fl.programs import ProgramRunner, make_program
 
-            self._runner = ProgramRunner(make_program(self.model_name, 1, PROGRAM_EVAL_BATCH[self.model_name],
-                                                      self.device, train=False))
-        return self._runner
+            self._runners[C] = ProgramRunner(make_program(self.model_name, C, PROGRAM_EVAL_BATCH[self.model_name],
+                                                          self.device, train=False))
+        return self._runners[C]
 
     # -- forward over the whole test set ------------------------------------------------------
     @torch.no_grad()
@@ -102,6 +102,12 @@ class Validation:
     def test_hyper(self, hnet, num_client: int) -> Tuple[bool, float]:
         if self.data_name != "ICU":
             raise ValueError(f"Not found test function for data name {self.data_name}")
+        if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and num_client > 0:
+            # every client's generated model through ONE client-batched eval program
+            flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32).contiguous()
+            data = self.table.rows
+            out = self._program_runner(num_client).predict(flats, data).reshape(-1)
+            return self._finish_icu(out, self._labels().repeat(num_client))
         outs, labs = [], []
         for i in range(num_client):
             flat = hnet.generate(i)

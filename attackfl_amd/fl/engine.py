@@ -17,6 +17,8 @@ traffic per round is the update all-gather plus a few-byte control broadcast.
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 import random
 import time
@@ -319,55 +321,100 @@ class FLEngine:
     # ------------------------------------------------------------------------------------------
     # LOCAL
     # ------------------------------------------------------------------------------------------
+    def _side_stream(self):
+        if self.device.type != "cuda":
+            return None
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def _local_work(self, genuine: Dict[int, Optional[torch.Tensor]]) -> torch.Tensor:
         cfg = self.cfg
         block = torch.zeros(self.slots, self.P + META, dtype=torch.float32, device=self.device)
+        meta = torch.zeros(self.slots, META, dtype=torch.float32)  # host-built, one copy
         lo, hi = cfg.data_range
         train_rows, train_nd, train_seeds = [], [], []
+        attack_jobs = []
+        started, faults = [], []
         for j, lc in enumerate(self.local):
             i = lc.info.index
             if i not in self.selected:
                 continue
             lc.training_round += 1
-            p = self._start_params(i)
-            if p is not None:
-                self.local_params[j].copy_(p)
+            started.append((j, i))
             if (i, lc.training_round) in self.faults:
-                self.local_params[j, 0] = float("nan")
+                faults.append(j)
                 print_with_color(f"[fault-inject] client {i} poisoned with NaN (training round {lc.training_round})",
                                  "red")
             g = genuine.get(i)
             if lc.info.attack is not None and g is not None and g.shape[0] > 0:
                 lc.genuine = g
             num_data = lc.rng.randrange(lo, hi + 1)
-            block[j, self.P + 0] = 1.0
-            block[j, self.P + 2] = float(num_data)
-            block[j, self.P + 3] = 1.0 if lc.info.attack is not None else 0.0
+            meta[j, 0] = 1.0
+            meta[j, 2] = float(num_data)
+            meta[j, 3] = 1.0 if lc.info.attack is not None else 0.0
             atk = lc.info.attack
             if atk is not None and lc.training_round >= atk.round and lc.genuine is not None and lc.genuine.shape[0] > 0:
-                gen = torch.Generator(device=self.device if self.device.type == "cuda" else "cpu")
-                gen.manual_seed(lc.seed * 1009 + lc.training_round)
-                res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist, gen)
-                if res.ok and res.params is not None:
-                    block[j, :self.P] = res.params
-                    block[j, self.P + 1] = 1.0
-                self._attack_info = res.info
-                if self.verbose:
-                    print_with_color(f"[===] Client {i} attacks with {atk.mode} {res.info}", "red")
+                attack_jobs.append((j, i, lc, atk))
             else:
                 train_rows.append(j)
                 train_nd.append(num_data)
                 train_seeds.append(lc.seed * 7 + lc.training_round)
+        # START parameters of every started client (one batched generate / broadcast copy)
+        if started:
+            js = [j for j, _ in started]
+            if self.mode == "hyper":
+                start = self.hyper.hnet.generate_many([i for _, i in started])
+            else:
+                p = self._start_params(started[0][1])
+                start = None if p is None else p[None, :].expand(len(js), -1)
+            if start is not None:
+                self.local_params.index_copy_(0, torch.tensor(js, device=self.device), start.contiguous())
+        for j in faults:
+            self.local_params[j, 0] = float("nan")
+        block[:, self.P:] = meta.to(self.device, non_blocking=False)
+        tp0 = time.perf_counter()
+        pending = None
+        ready = None
+        if attack_jobs and self.device.type == "cuda":
+            # the attackers' inputs are ready now; the side stream must not also wait for the training launch
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.device))
         if train_rows:
             sel = torch.tensor(train_rows, device=self.device)
             params = self.local_params.index_select(0, sel).contiguous()
             plan = make_plan(self.train_table.n, train_nd, cfg.epoch, [sd * 1000003 + 17 for sd in train_seeds],
                              self.device)
-            oks, losses = self.trainer.train(params, plan, cfg.lr, cfg.batch_size, train_seeds)
+            pending = self.trainer.launch(params, plan, cfg.lr, cfg.batch_size, train_seeds)
+        tp1 = time.perf_counter()
+        if attack_jobs:
+            # the attackers do not train: their math runs on a side stream while the genuine clients'
+            # training launch occupies its own CUs (the reference runs every client concurrently too)
+            side = self._side_stream()
+            if side is not None:
+                side.wait_event(ready)
+            with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                for j, i, lc, atk in attack_jobs:
+                    gen = torch.Generator(device=self.device if self.device.type == "cuda" else "cpu")
+                    gen.manual_seed(lc.seed * 1009 + lc.training_round)
+                    res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist, gen)
+                    if res.ok and res.params is not None:
+                        block[j, :self.P] = res.params
+                        block[j, self.P + 1] = 1.0
+                    self._attack_info = res.info
+                    if self.verbose:
+                        print_with_color(f"[===] Client {i} attacks with {atk.mode} {res.info}", "red")
+            if side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(side)
+        tp2 = time.perf_counter()
+        if pending is not None:
+            oks, losses = pending.result()
             self.local_params.index_copy_(0, sel, params)
             block[sel, :self.P] = params
             block[sel, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=self.device)
             self._last_losses = losses
+        tp3 = time.perf_counter()
+        self._lw_times = {"t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tp1, "t_lw_wait": tp3 - tp2}
         return block
 
     # ------------------------------------------------------------------------------------------
@@ -527,7 +574,8 @@ class FLEngine:
                     self.round_no -= 1
         elif self.verbose:
             print_with_color("Training failed!", "yellow")
-        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, "t_local": t1 - t0, "t_gather": t2 - t1,
+        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, **getattr(self, "_lw_times", {}),
+               "t_local": t1 - t0, "t_gather": t2 - t1,
                "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
                "n_selected": len(self.selected), "removed": removed}
         if self._attack_info:
@@ -577,7 +625,8 @@ class FLEngine:
                     self.round_no -= 1
         elif self.verbose:
             print_with_color("Training failed!", "yellow")
-        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, "t_local": t1 - t0, "t_gather": t2 - t1,
+        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, **getattr(self, "_lw_times", {}),
+               "t_local": t1 - t0, "t_gather": t2 - t1,
                "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
                "n_selected": len(self.selected), "removed": [], "path": "fedavg-allreduce"}
         self.metrics.write(rec)

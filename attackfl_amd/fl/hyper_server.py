@@ -83,8 +83,48 @@ class HyperServer:
                 gslot("emb")[i].copy_(da)
         return g
 
-    def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor]) -> None:
+    def layout_vec(self):
+        """Arena offsets for the native kernels: [emb, w_0, b_0, ..., L, E, H, n_nodes, offW, offB, P]."""
         h = self.hnet
+        L = h.n_hidden + 1
+        lay = [h.slots["emb"][0]]
+        for li in range(L):
+            lay += [h.slots[f"mlp{li}.W"][0], h.slots[f"mlp{li}.b"][0]]
+        lay += [L, h.E, h.H, h.n_nodes, h.slots["W"][0], h.slots["b"][0], h.P]
+        return [int(x) for x in lay]
+
+    def _native_ok(self) -> bool:
+        h = self.hnet
+        if not (self.device.type == "cuda" and h.H % 4 == 0 and h.slots["W"][0] % 4 == 0 and h.H <= 127
+                and h.E <= 128 and h.n_hidden + 1 <= 8):
+            return False
+        return h.slots["W"][0] - h.slots["mlp0.W"][0] <= ops.native().hyper_small_capacity()
+
+    def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor]) -> None:
+        """One round of the sequential server update over ``selected`` (client order kept).
+
+        On GPU the whole round is enqueued by ``ops.hyper_server_update`` (three launches per client,
+        no host synchronisation); on CPU the composite path below is the oracle."""
+        h = self.hnet
+        selected = list(selected)
+        if not selected:
+            return
+        if self._native_ok():
+            rows = [updates[i] for i in selected]
+            # the engine hands rows of one gathered matrix; stack only when they are not already views of it
+            base = rows[0]._base if rows[0]._base is not None else None
+            if base is not None and base.dim() == 2 and all(r._base is base for r in rows) and base.is_contiguous():
+                U = base
+                urows = [(r.storage_offset() - base.storage_offset()) // base.shape[1] for r in rows]
+            else:
+                U = torch.stack([r.contiguous() for r in rows])
+                urows = list(range(len(rows)))
+            info = ops.hyper_server_update(h.arena, self.m, self.v, U, urows, selected, self.layout_vec(), self.step,
+                                           self.lr, self.clip)
+            self.step += len(selected)
+            last = info[-1].double().cpu()  # the round's only host sync
+            self.last_info = {"grad_norm": float(last[0]), "clip_scale": float(last[1])}
+            return
         for i in selected:
             emb, feat, acts = h.features(i)
             delta, dfeat = ops.hyper_delta_vjp(h.W, h.b, feat, updates[i])   # δ = W f + b - u ; Wᵀδ

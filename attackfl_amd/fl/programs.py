@@ -383,10 +383,12 @@ class ProgramRunner:
         self.prog = prog
         # AFL_SYNC_CHECK=1 (synchronise + check after every native launch) cannot run inside a capture
         self.use_graph = use_graph and prog.device.type == "cuda" and os.environ.get("AFL_SYNC_CHECK") != "1"
+        self._live = None
 
     def train(self, table, params: torch.Tensor, plan, lr: float, seeds: Sequence[int], sgd_lr: float = 0.0,
-              max_steps: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Train ``params [C, P]`` in place.  Returns (ok [C] bool, losses [C, E])."""
+              max_steps: int = None, sync: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Train ``params [C, P]`` in place.  Returns (ok [C] bool, losses [C, E]) on the host, or with
+        ``sync=False`` the device (failed-count [C] int32, losses [C, E]) without synchronising."""
         pg = self.prog
         dev = pg.device
         C, P = params.shape
@@ -416,7 +418,7 @@ class ProgramRunner:
             Lx.step_end(ctl, tcount, bsz, failed)
 
         if S == 0:
-            return torch.ones(C, dtype=torch.bool), losses.double().cpu()
+            return (torch.ones(C, dtype=torch.bool), losses.double().cpu()) if sync else (failed, losses)
         step()  # eager first step: allocates every buffer and sets kernel attributes before capture
         if S > 1:
             if self.use_graph:
@@ -426,9 +428,12 @@ class ProgramRunner:
                 # capture recorded without executing; the counter still points at step 1
                 for _ in range(S - 1):
                     g.replay()
+                self._live = (g, grads, m, v, tcount)  # replays may still be running when sync=False
             else:
                 for _ in range(S - 1):
                     step()
+        if not sync:
+            return failed, losses
         return (failed == 0).cpu(), losses.double().cpu()
 
     @torch.no_grad()

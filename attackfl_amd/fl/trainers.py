@@ -41,6 +41,108 @@ class Plan:
         return self.order[c, :, : int(self.nd[c])]
 
 
+class Pending:
+    """A launched local-training job: ``result()`` synchronises and returns (ok per client, losses [C, E]).
+
+    Trainers whose work is enqueued asynchronously (fused, graph) return before the GPU finishes, so the
+    engine can run the attackers' math on a side stream while the genuine clients train."""
+
+    def __init__(self, finish):
+        self._finish = finish
+        self._res = None
+
+    def result(self) -> Tuple[List[bool], torch.Tensor]:
+        if self._res is None:
+            self._res = self._finish()
+            self._finish = None
+        return self._res
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x: torch.Tensor, c: int) -> torch.Tensor:
+    """(x * c) mod 2^32 for int64 tensors holding uint32 values (no int64 overflow)."""
+    return (x * (c & 0xFFFF) + (((x * (c >> 16)) & 0xFFFF) << 16)) & _M32
+
+
+def _mix_t(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = _mul32(x, 0x85EBCA6B)
+    x = x ^ (x >> 13)
+    x = _mul32(x, 0xC2B2AE35)
+    return x ^ (x >> 16)
+
+
+def _mix_i(x: int) -> int:
+    x &= _M32
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & _M32
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & _M32
+    return x ^ (x >> 16)
+
+
+def _half_bits(n: int) -> int:
+    k = 2
+    while (1 << k) < n:
+        k += 2
+    return k // 2
+
+
+def _perm_t(x: torch.Tensor, n: int, k0: int, k1: int) -> torch.Tensor:
+    """Keyed 6-round Feistel permutation of [0, n) with cycle walking (mirror of plan.hip:pl_perm)."""
+    half = _half_bits(n)
+    mask = (1 << half) - 1
+
+    def feistel(v):
+        L, R = v >> half, v & mask
+        for r in range(6):
+            F = _mix_t(R ^ k0 ^ ((k1 + 0x9E3779B9 * (r + 1)) & _M32)) & mask
+            L, R = R, L ^ F
+        return (L << half) | R
+
+    x = feistel(x)
+    while True:
+        bad = x >= n
+        if not bool(bad.any()):
+            return x
+        x = torch.where(bad, feistel(x), x)
+
+
+def _plan_keys(seed: int, e: int):
+    lo, hi = seed & _M32, (seed >> 32) & _M32
+    ks0, ks1 = _mix_i(lo ^ 0x5BD1E995), _mix_i(hi ^ 0x27D4EB2F)
+    ke0 = _mix_i(ks0 ^ ((0x165667B1 * (e + 1)) & _M32))
+    ke1 = _mix_i((ks1 + 0xD3A2646C * (e + 1)) & _M32)
+    return ks0, ks1, ke0, ke1
+
+
+def _feistel_plan(n_train: int, num_data: List[int], epochs: int, seeds: List[int], device) -> Plan:
+    """Per-client subset + per-epoch shuffle from keyed Feistel permutations (``csrc/kernels/plan.hip``):
+    one launch on GPU, a bit-identical vectorised mirror on CPU.  A client's plan depends only on its
+    seed and num_data (placement-independent)."""
+    dev = torch.device(device)
+    C = len(num_data)
+    maxnd = max(num_data)
+    seeds = [s & 0xFFFFFFFFFFFFFFFF for s in seeds]
+    nd = torch.tensor(num_data, dtype=torch.int32)
+    if dev.type == "cuda":
+        from .. import ops
+
+        st = torch.tensor([s - (1 << 64) if s >= (1 << 63) else s for s in seeds], dtype=torch.int64)
+        order = ops.native().make_plan(st.to(dev), nd.to(dev), int(n_train), int(epochs), int(maxnd))
+        return Plan(order, nd, epochs)
+    order = torch.zeros(C, epochs, maxnd, dtype=torch.int64)
+    for c in range(C):
+        n = num_data[c]
+        i = torch.arange(n, dtype=torch.int64)
+        for e in range(epochs):
+            ks0, ks1, ke0, ke1 = _plan_keys(seeds[c], e)
+            order[c, e, :n] = _perm_t(_perm_t(i, n, ke0, ke1), n_train, ks0, ks1)
+    return Plan(order.to(torch.int32).to(dev), nd, epochs)
+
+
 def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, device) -> Plan:
     """Random subset (without replacement) per client + a fresh permutation per epoch.
 
@@ -55,19 +157,10 @@ def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, dev
     if maxnd > n_train:
         raise ValueError(f"num_data {maxnd} exceeds the train set size {n_train}")
     if isinstance(generator, (list, tuple)):
-        gdev = torch.device(device)
-        keys = []
-        ek = torch.full((C, epochs, maxnd), 2.0, device=gdev)
-        for c, s in enumerate(generator):
-            g = torch.Generator(device=gdev).manual_seed(int(s) & 0x7FFFFFFFFFFFFFFF)
-            keys.append(torch.rand(n_train, generator=g, device=gdev))
-            # exactly nd_c draws per epoch: the plan must not depend on the other clients this rank hosts
-            ek[c, :, :num_data[c]] = torch.rand(epochs, num_data[c], generator=g, device=gdev)
-        keys = torch.stack(keys)
-    else:
-        gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
-        keys = torch.rand(C, n_train, generator=generator, device=gdev)
-        ek = None
+        return _feistel_plan(n_train, list(num_data), epochs, [int(s) for s in generator], device)
+    gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
+    keys = torch.rand(C, n_train, generator=generator, device=gdev)
+    ek = None
     subset = torch.argsort(keys, dim=1)[:, :maxnd]                              # [C, maxnd]
     if ek is None:
         ek = torch.rand(C, epochs, maxnd, generator=generator, device=gdev)
@@ -123,6 +216,10 @@ class EagerTrainer:
                 params[c].copy_(self.layout.flatten(self.model.state_dict(), device=params.device))
             oks.append(ok)
         return oks, losses
+
+    def launch(self, params, plan, lr, batch, seeds) -> Pending:
+        res = self.train(params, plan, lr, batch, seeds)
+        return Pending(lambda: res)
 
     def _train_one(self, order: torch.Tensor, lr: float, batch: int, loss_out: torch.Tensor) -> bool:
         model = self.model
@@ -181,17 +278,27 @@ class FusedTrainer:
 
     def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
               ) -> Tuple[List[bool], torch.Tensor]:
+        return self.launch(params, plan, lr, batch, seeds).result()
+
+    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]) -> Pending:
         if self.model_name == "RNNModel":
             if not self.R.fits(params.shape[0], self.device):
                 if self._fallback is None:
                     self._fallback = GraphTrainer(self.model_name, "ICU", self.table, self.device, self.verbose)
-                return self._fallback.train(params, plan, lr, batch, seeds)
-            ok, losses = self.R.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
-                                              seeds)
+                return self._fallback.launch(params, plan, lr, batch, seeds)
+            ok, losses = self.R.train_clients_async(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch,
+                                                    lr, seeds)
+            what = "fused RNN trainer"
         else:
-            ok, losses = self.T.train_clients(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch, lr,
-                                              seeds)
-        return [bool(x) for x in ok.tolist()], losses
+            ok, losses = self.T.train_clients_async(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch,
+                                                    lr, seeds)
+            what = "fused trainer"
+
+        def fin():
+            okh, lh = self.T.finish(ok, losses, what)
+            return [bool(x) for x in okh.tolist()], lh
+
+        return Pending(fin)
 
 
 class GraphTrainer:
@@ -214,16 +321,24 @@ class GraphTrainer:
 
     def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
               ) -> Tuple[List[bool], torch.Tensor]:
+        return self.launch(params, plan, lr, batch, seeds).result()
+
+    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]) -> Pending:
         C = params.shape[0]
         if self._runner is None or self._runner.prog.C != C or self._runner.prog.B != batch:
             self._runner = self.programs.ProgramRunner(
                 self.programs.make_program(self.model_name, C, batch, self.device, train=True))
-        ok, losses = self._runner.train(self.table, params, plan, lr, seeds)
-        if self.verbose:
-            for c in range(C):
-                for e in range(plan.epochs):
-                    print_with_color(f"Loss {float(losses[c, e]):.6f} ", "yellow")
-        return [bool(x) for x in ok.tolist()], losses
+        ok, losses = self._runner.train(self.table, params, plan, lr, seeds, sync=False)
+
+        def fin():
+            okh, lh = (ok == 0).cpu(), losses.double().cpu()
+            if self.verbose:
+                for c in range(C):
+                    for e in range(plan.epochs):
+                        print_with_color(f"Loss {float(lh[c, e]):.6f} ", "yellow")
+            return [bool(x) for x in okh.tolist()], lh
+
+        return Pending(fin)
 
 
 def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable, device, verbose=False):

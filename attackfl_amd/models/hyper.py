@@ -231,6 +231,11 @@ class PackedHyperNet:
             acts.append(h)
         return self.emb[idx], h, acts
 
+    def generate_many(self, idxs) -> torch.Tensor:
+        """Flat target weights [n, P] of several clients (one GEMM over the packed heads)."""
+        feats = torch.stack([self.features(int(i))[1] for i in idxs])
+        return torch.addmm(self.b[None, :], feats, self.W.t())
+
     def generate(self, idx: int) -> torch.Tensor:
         """Flat target weights [P] for client ``idx`` (one GEMV over the packed heads)."""
         _, feat, _ = self.features(idx)

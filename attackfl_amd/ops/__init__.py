@@ -266,6 +266,18 @@ def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale:
     composite.hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step, lr, scale)
 
 
+def hyper_server_update(arena, m, v, U, urows, clients, layout, step0: int, lr: float, clip: float,
+                        beta1=0.9, beta2=0.999, eps=1e-8) -> torch.Tensor:
+    """Sequential pFedHN server update of a whole round on the device (no host sync); info [n, 2]."""
+    return native().hyper_server_update(arena, m, v, U.contiguous(), [int(r) for r in urows],
+                                        [int(c) for c in clients], [int(x) for x in layout], int(step0), float(lr),
+                                        float(clip), float(beta1), float(beta2), float(eps))
+
+
+def hyper_features(arena, clients, layout) -> torch.Tensor:
+    return native().hyper_features(arena, [int(c) for c in clients], [int(x) for x in layout])
+
+
 def hyper_generate(W: torch.Tensor, b: torch.Tensor, feat: torch.Tensor) -> torch.Tensor:
     if _dev(W):
         return native().hyper_generate(W, b, feat.contiguous())

@@ -26,14 +26,19 @@ def _seeds(seeds, dev) -> torch.Tensor:
     return torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32).to(dev)
 
 
+def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
+                        lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Enqueue the launch; returns DEVICE (ok [C] int32, losses [C, E]) without synchronising."""
+    dev = params.device
+    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
+    return native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, _seeds(seeds, dev),
+                              int(epochs), int(batch), float(lr), int(opt_mode))
+
+
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                   lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """Train ``params [C, 97665]`` in place.  Returns (ok [C] int32, losses [C, E]) on the host."""
-    dev = params.device
-    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
-    ok, losses = native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, _seeds(seeds, dev),
-                                    int(epochs), int(batch), float(lr), int(opt_mode))
-    ok = ok.cpu()
-    if bool((ok < 0).any()):
-        raise RuntimeError("fused RNN trainer: a cross-workgroup hand-off timed out (workgroups not co-resident?)")
-    return ok, losses.cpu()
+    from .transformer import finish
+
+    return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode),
+                  what="fused RNN trainer")

@@ -27,6 +27,30 @@ def auto_split(C: int, dev) -> int:
     return 3 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
+def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
+                        lr: float, seeds: Sequence[int], opt_mode: int = 0, stamps: torch.Tensor = None,
+                        split: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Enqueue the training launch on the current stream and return (ok [C] int32, losses [C, E]) as
+    DEVICE tensors without synchronising (see ``finish``); arguments as ``train_clients``."""
+    dev = params.device
+    C = params.shape[0]
+    if split is None:
+        split = auto_split(C, dev) if C > 0 else 1
+    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
+    seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
+    return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
+                             int(batch), float(lr), int(opt_mode), stamps, int(split))
+
+
+def finish(ok: torch.Tensor, losses: torch.Tensor, what: str = "fused trainer") -> Tuple[torch.Tensor, torch.Tensor]:
+    """Synchronise on a launch from ``train_clients_async`` -> host (ok, losses); a negative ok means a
+    cross-workgroup hand-off timed out."""
+    ok = ok.cpu()
+    if bool((ok < 0).any()):
+        raise RuntimeError(f"{what}: a cross-workgroup hand-off timed out (workgroups not co-resident?)")
+    return ok, losses.cpu()
+
+
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                   lr: float, seeds: Sequence[int], opt_mode: int = 0, stamps: torch.Tensor = None,
                   split: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -37,18 +61,7 @@ def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor,
     gradients to each other every step.  Default: ``auto_split``.
     ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
     workgroup 0, summed over all steps (diagnostics)."""
-    dev = params.device
-    C = params.shape[0]
-    if split is None:
-        split = auto_split(C, dev) if C > 0 else 1
-    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
-    seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
-    ok, losses = native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
-                                   int(batch), float(lr), int(opt_mode), stamps, int(split))
-    ok = ok.cpu()
-    if bool((ok < 0).any()):
-        raise RuntimeError("fused trainer: a cross-workgroup hand-off timed out (workgroups not co-resident?)")
-    return ok, losses.cpu()
+    return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, stamps, split))
 
 
 def eval_forward(params: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:

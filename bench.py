@@ -105,8 +105,9 @@ def main() -> int:
         elapsed = float(t.item())
     if args.profile_rounds and rank == 0:
         for r in recs:
-            print(json.dumps({k: r[k] for k in ("round", "ok", "t_local", "t_gather", "t_aggregate", "t_validate",
-                                                "t_round", "metric")}), file=sys.stderr)
+            print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_local",
+                                                "t_gather", "t_aggregate", "t_validate", "t_round", "metric")
+                              if k in r}), file=sys.stderr)
     value = args.steps / elapsed
     if rank == 0:
         aucs = [r["metric"] for r in recs if r["metric"] == r["metric"]]

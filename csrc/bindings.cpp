@@ -251,6 +251,90 @@ void hyper_adam_outer(torch::Tensor W, torch::Tensor b, torch::Tensor m, torch::
   AFL_CHECK_LAUNCH();
 }
 
+// layout = [emb, w_0, b_0, ..., w_{L-1}, b_{L-1}, L, E, H, n_nodes, offW, offB, P] (arena float offsets)
+HySmallDesc hy_desc(const std::vector<int64_t>& lay, long& offW, long& offB, long& P) {
+  HySmallDesc d{};
+  TORCH_CHECK(lay.size() >= 8, "hyper layout too short");
+  const int L = (int)lay[lay.size() - 7];
+  TORCH_CHECK(L >= 1 && L <= 8 && (long)lay.size() == 1 + 2 * L + 7, "hyper layout: bad layer count");
+  d.emb = lay[0];
+  for (int l = 0; l < L; ++l) {
+    d.w[l] = lay[1 + 2 * l];
+    d.b[l] = lay[2 + 2 * l];
+  }
+  const size_t t = 1 + 2 * L;
+  d.L = L;
+  d.E = (int)lay[t + 1];
+  d.H = (int)lay[t + 2];
+  d.n_nodes = (int)lay[t + 3];
+  offW = lay[t + 4];
+  offB = lay[t + 5];
+  P = lay[t + 6];
+  TORCH_CHECK(d.E >= 1 && d.E <= 128 && d.H >= 1 && d.H <= 127, "hyper: embedding size must be <= 128, hidden <= 127");
+  TORCH_CHECK(offW - d.w[0] <= afl_hyper_small_capacity(), "hyper: MLP too large for the small-net kernel");
+  return d;
+}
+
+// Whole sequential hypernetwork server update of one round (every selected client in order), enqueued
+// without a host synchronisation.  Returns info [n, 2] = (grad norm, clip scale) per client (device).
+torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::Tensor v, torch::Tensor U,
+                                  std::vector<int64_t> urows, std::vector<int64_t> clients, std::vector<int64_t> lay,
+                                  int64_t step0, double lr, double clip, double b1, double b2, double eps) {
+  for (auto* t : {&arena, &m, &v, &U}) check_dev(*t, "hyper tensor", torch::kFloat32);
+  long offW, offB, P;
+  HySmallDesc d = hy_desc(lay, offW, offB, P);
+  const int n = (int)clients.size();
+  TORCH_CHECK(n >= 1 && (int)urows.size() == n, "hyper: clients / rows mismatch");
+  TORCH_CHECK(arena.numel() == offB + P && m.numel() == arena.numel() && v.numel() == arena.numel(), "hyper: arena");
+  TORCH_CHECK(U.dim() == 2 && U.size(1) == P, "hyper: updates must be [rows, P]");
+  TORCH_CHECK(d.H % 4 == 0 && offW % 4 == 0, "hyper: head block must be float4-aligned");
+  for (int k = 0; k < n; ++k) {
+    TORCH_CHECK(urows[k] >= 0 && urows[k] < U.size(0), "hyper: update row out of range");
+    TORCH_CHECK(clients[k] >= 0 && clients[k] < d.n_nodes, "hyper: client index out of range");
+  }
+  std::vector<int> cl(clients.begin(), clients.end());
+  std::vector<long> ur(urows.begin(), urows.end());
+  auto opt = arena.options();
+  auto delta = torch::empty({P}, opt);
+  auto partial = torch::empty({(long)afl_hyper_nblocks(P) * (d.H + 1)}, opt);
+  auto feat = torch::empty({2 * 128}, opt);
+  auto info = torch::empty({n, 2}, opt);
+  afl_hyper_server_update(arena.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), U.data_ptr<float>(),
+                          ur.data(), cl.data(), n, d, offW, offB, P, (int)step0, (float)lr, (float)clip, (float)b1,
+                          (float)b2, (float)eps, delta.data_ptr<float>(), partial.data_ptr<float>(),
+                          feat.data_ptr<float>(), info.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return info;
+}
+
+// hypernetwork features (embedding -> MLP output) of several clients -> [n, H]
+torch::Tensor hyper_features(torch::Tensor arena, std::vector<int64_t> clients, std::vector<int64_t> lay) {
+  check_dev(arena, "arena", torch::kFloat32);
+  long offW, offB, P;
+  HySmallDesc d = hy_desc(lay, offW, offB, P);
+  const int n = (int)clients.size();
+  for (int k = 0; k < n; ++k) TORCH_CHECK(clients[k] >= 0 && clients[k] < d.n_nodes, "hyper: client out of range");
+  std::vector<int> cl(clients.begin(), clients.end());
+  auto out = torch::empty({n, d.H}, arena.options());
+  if (n) afl_hyper_features(arena.data_ptr<float>(), d, offW, cl.data(), n, out.data_ptr<float>(), cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+// [C, E, maxnd] int32 visit plan from per-client 64-bit seeds (plan.hip); padding is 0
+torch::Tensor make_plan(torch::Tensor seeds, torch::Tensor nd, int64_t n_train, int64_t epochs, int64_t maxnd) {
+  check_dev(seeds, "seeds", torch::kInt64);
+  check_dev(nd, "nd", torch::kInt32);
+  const int C = seeds.numel();
+  TORCH_CHECK(nd.numel() == C, "make_plan: seeds / nd size mismatch");
+  TORCH_CHECK(n_train >= 1 && n_train < (1L << 30) && maxnd >= 0 && maxnd <= n_train, "make_plan: bad sizes");
+  auto order = torch::empty({C, epochs, maxnd}, nd.options());
+  afl_make_plan((const uint64_t*)seeds.data_ptr<int64_t>(), nd.data_ptr<int>(), C, (int)n_train, (int)epochs,
+                (int)maxnd, order.data_ptr<int>(), cur());
+  AFL_CHECK_LAUNCH();
+  return order;
+}
+
 // Fused whole-round trainers: kind 0 = TransformerModel (split 1 / 2 / 3 workgroups per client),
 // kind 1 = RNNModel (always 3 workgroups per client).
 std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Tensor rows, torch::Tensor order,
@@ -352,6 +436,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hyper_delta_vjp", &hyper_delta_vjp);
   m.def("hyper_generate", &hyper_generate);
   m.def("hyper_adam_outer", &hyper_adam_outer);
+  m.def("hyper_server_update", &hyper_server_update);
+  m.def("make_plan", &make_plan);
+  m.def("hyper_features", &hyper_features);
+  m.def("hyper_small_capacity", &afl_hyper_small_capacity);
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
         py::arg("stamps") = py::none(), py::arg("split") = 1);

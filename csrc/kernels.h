@@ -27,6 +27,24 @@ void afl_hyper_rows(const float* W, const float* b, const float* f, const float*
                     float* partial, float* dfeat, hipStream_t s);
 void afl_hyper_adam(float* W, float* bvec, float* m, float* v, const float* delta, const float* f, long P, int H,
                     int step, float lr, float b1, float b2, float eps, float gs, hipStream_t s);
+// arena offsets (floats) of the hypernet embedding + MLP (L layers, E -> H -> ... -> H)
+struct HySmallDesc {
+  long emb;
+  long w[8];
+  long b[8];
+  int L, E, H, n_nodes;
+};
+void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
+                             int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
+                             float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
+                             float* info, hipStream_t s);
+void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const int* clients, int n, float* out,
+                        hipStream_t s);
+long afl_hyper_small_capacity();  // max floats of embedding-MLP parameters the small-net kernel stages in LDS
+
+// plan.hip
+void afl_make_plan(const uint64_t* seeds, const int* nd, int C, int n_train, int E, int maxnd, int* order,
+                   hipStream_t s);
 
 // linalg.hip
 int afl_spectral_scratch(int r, int c);

@@ -14,11 +14,14 @@ constexpr int HR_HMAX = 128;  // max hidden size supported
 
 __global__ void __launch_bounds__(256) k_hyper_rows(const float* __restrict__ W, const float* __restrict__ b,
                                                     const float* __restrict__ f, const float* __restrict__ u, long P,
-                                                    int H, float* __restrict__ out, float* __restrict__ partial) {
+                                                    int H, float* __restrict__ out, float* __restrict__ partial,
+                                                    int pstride) {
   __shared__ float tile[HR_ROWS * HR_HMAX];
   __shared__ float fs[HR_HMAX];
   __shared__ float ds[HR_ROWS];
+  __shared__ float sq[4];
   const int tid = threadIdx.x;
+  float dsq = 0.f;  // sum of delta^2 over this thread's rows (pstride == H + 1)
   if (tid < H) fs[tid] = f[tid];
   float acc = 0.f;  // dfeat[tid] partial (tid < H)
   const long ntiles = (P + HR_ROWS - 1) / HR_ROWS;
@@ -41,13 +44,20 @@ __global__ void __launch_bounds__(256) k_hyper_rows(const float* __restrict__ W,
       if (u) val -= u[r0 + r];
       out[r0 + r] = val;
       ds[r] = val;
+      dsq += val * val;
     }
     __syncthreads();
     if (u && tid < H) {
       for (int rr = 0; rr < nr; ++rr) acc += tile[rr * H + tid] * ds[rr];
     }
   }
-  if (u && tid < H) partial[(long)blockIdx.x * H + tid] = acc;
+  if (u && tid < H) partial[(long)blockIdx.x * pstride + tid] = acc;
+  if (u && pstride > H) {
+    for (int o = 32; o > 0; o >>= 1) dsq += __shfl_xor(dsq, o, 64);
+    if ((tid & 63) == 0) sq[tid >> 6] = dsq;
+    __syncthreads();
+    if (tid == 0) partial[(long)blockIdx.x * pstride + H] = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+  }
 }
 
 __global__ void k_hyper_reduce(const float* __restrict__ partial, int nb, int H, float* __restrict__ dfeat) {
@@ -58,12 +68,12 @@ __global__ void k_hyper_reduce(const float* __restrict__ partial, int nb, int H,
   dfeat[h] = (float)a;
 }
 
-int afl_hyper_nblocks(long P) { return (int)min(1024L, (P + HR_ROWS - 1) / HR_ROWS); }
+int afl_hyper_nblocks(long P) { return (int)min(256L, (P + HR_ROWS - 1) / HR_ROWS); }
 
 void afl_hyper_rows(const float* W, const float* b, const float* f, const float* u, long P, int H, float* out,
                     float* partial, float* dfeat, hipStream_t s) {
   int nb = afl_hyper_nblocks(P);
-  hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, b, f, u, P, H, out, partial);
+  hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, b, f, u, P, H, out, partial, H);
   if (u) hipLaunchKernelGGL(k_hyper_reduce, dim3(1), dim3(128), 0, s, partial, nb, H, dfeat);
 }
 
@@ -103,3 +113,278 @@ void afl_hyper_adam(float* W, float* bvec, float* m, float* v, const float* delt
   hipLaunchKernelGGL(k_hyper_adam, dim3(nb), dim3(256), 0, s, W, bvec, m, v, delta, f, P, H, (float)(lr / bc1),
                      (float)(1.0 / sqrt(bc2)), b1, b2, eps, gs);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Sync-free sequential server update: per selected client c_k, three launches and no host round trip
+//   rows   : delta = W f + b - u,  partial W^T delta and |delta|^2 per block        (streams W once)
+//   small  : one workgroup: reduce partials, recompute the MLP activations of c_k, back-propagate
+//            into the embedding + MLP, global grad norm (head part in closed form:
+//            |delta (x) f|^2 = |delta|^2 |f|^2), clip coefficient -> device scalar, Adam on the
+//            embedding+MLP region, then the features f of c_{k+1} with the updated MLP
+//   head   : Adam on W, b with grad = scale * delta (x) f computed on the fly (float4 streams)
+// ------------------------------------------------------------------------------------------------
+constexpr int HS_HMAX = 128;
+constexpr int HS_LMAX = 8;
+constexpr int HS_NT = 1024;          // threads of the small-net workgroup (16 waves)
+constexpr int HS_SMEM = 28 * 1024;   // floats of MLP parameters staged in LDS (112 KB)
+
+// relu that keeps NaN like torch.relu
+__device__ __forceinline__ float hs_relu(float z) { return z < 0.f ? 0.f : z; }
+
+// sum over the 8 lanes of an aligned lane group (all inside one wave)
+__device__ __forceinline__ float hs_sum8(float x) {
+  x += __shfl_xor(x, 1, 64);
+  x += __shfl_xor(x, 2, 64);
+  x += __shfl_xor(x, 4, 64);
+  return x;
+}
+
+__device__ __forceinline__ float hs_wave_sum(float x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// MLP forward of client c from the LDS copy (sm = parameters from d.w[0] on) -> acts[0..L]
+// 8 lanes per output neuron.
+__device__ void hs_forward(const float* __restrict__ A, const float* sm, const HySmallDesc& d, int c,
+                           float (*acts)[HS_HMAX]) {
+  const int tid = threadIdx.x;
+  if (tid < d.E) acts[0][tid] = A[d.emb + (long)c * d.E + tid];
+  __syncthreads();
+  const long base = d.w[0];
+  const int o = tid >> 3, sub = tid & 7;
+  int din = d.E;
+  for (int l = 0; l < d.L; ++l) {
+    float acc = 0.f;
+    if (o < d.H) {
+      const float* w = sm + (d.w[l] - base) + (long)o * din;
+      for (int k = sub; k < din; k += 8) acc = fmaf(w[k], acts[l][k], acc);
+    }
+    acc = hs_sum8(acc);
+    if (o < d.H && sub == 0) {
+      const float z = acc + sm[d.b[l] - base + o];
+      acts[l + 1][o] = (l < d.L - 1) ? hs_relu(z) : z;
+    }
+    __syncthreads();
+    din = d.H;
+  }
+}
+
+// Adam on one element (gradient already scaled)
+__device__ __forceinline__ float hs_adam(float p, float g, float& mm, float& vv, float lr_bc1, float rsqrt_bc2,
+                                         float b1, float b2, float eps) {
+  mm = mm + (1.f - b1) * (g - mm);
+  vv = b2 * vv + (1.f - b2) * g * g;
+  return p - lr_bc1 * mm / (sqrtf(vv) * rsqrt_bc2 + eps);
+}
+
+__global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, float* __restrict__ m,
+                                                       float* __restrict__ v, const float* __restrict__ partial,
+                                                       int nb, int ci, int cj, float* __restrict__ feat_j,
+                                                       float* __restrict__ info, HySmallDesc d, long nmlp,
+                                                       float clip, float lr_bc1, float rsqrt_bc2, float b1, float b2,
+                                                       float eps) {
+  __shared__ float sm[HS_SMEM];
+  __shared__ float acts[HS_LMAX + 1][HS_HMAX];
+  __shared__ float dz[HS_LMAX][HS_HMAX];  // dL/d(output of layer l)
+  __shared__ float gemb[HS_HMAX];
+  __shared__ float red[HS_NT / 64][4];
+  __shared__ float sc;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int H = d.H, L = d.L, E = d.E;
+  const long base = d.w[0];
+  // stage the MLP parameters (contiguous [w_0 .. b_{L-1}]) in LDS, float4 when aligned
+  if ((base & 3) == 0 && (nmlp & 3) == 0) {
+    const float4* src = reinterpret_cast<const float4*>(A + base);
+    float4* dst = reinterpret_cast<float4*>(sm);
+    for (long e = tid; e < nmlp / 4; e += HS_NT) dst[e] = src[e];
+  } else {
+    for (long e = tid; e < nmlp; e += HS_NT) sm[e] = A[base + e];
+  }
+  if (ci >= 0) {
+    const int P1 = H + 1;
+    // reduce the rows kernel's per-block partials: 8 lanes per column (W^T delta [H] and |delta|^2)
+    {
+      const int c = tid >> 3, sub = tid & 7;
+      float s = 0.f;
+      if (c <= H)
+        for (int bb = sub; bb < nb; bb += 8) s += partial[(long)bb * P1 + c];
+      s = hs_sum8(s);
+      if (c <= H && sub == 0) {
+        if (c < H) dz[L - 1][c] = s;
+        else sc = s;  // |delta|^2 (sc is rewritten with the clip scale below)
+      }
+    }
+    hs_forward(A, sm, d, ci, acts);  // its barriers publish sm, dz[L-1] and sc
+    const float dd = sc;
+    for (int l = L - 1; l >= 0; --l) {
+      const int din = l == 0 ? E : H;
+      const int k = tid >> 3, sub = tid & 7;
+      float da = 0.f;
+      if (k < din) {
+        const float* w = sm + (d.w[l] - base) + k;
+        for (int o = sub; o < H; o += 8) da = fmaf(w[(long)o * din], dz[l][o], da);
+      }
+      da = hs_sum8(da);
+      if (k < din && sub == 0) {
+        if (l > 0) dz[l - 1][k] = acts[l][k] > 0.f ? da : 0.f;
+        else gemb[k] = da;
+      }
+      __syncthreads();
+    }
+    // squared norms (wave 0): sum_l |dz_l|^2 (|a_l|^2 + 1) + |gemb|^2 ; |f|^2
+    if (wv == 0) {
+      float small = 0.f;
+      for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? E : H;
+        float dzs = 0.f, as = 0.f;
+        for (int k = lane; k < H; k += 64) dzs += dz[l][k] * dz[l][k];
+        for (int k = lane; k < din; k += 64) as += acts[l][k] * acts[l][k];
+        small += hs_wave_sum(dzs) * (hs_wave_sum(as) + 1.f);
+      }
+      float ff = 0.f, ge = 0.f;
+      for (int k = lane; k < H; k += 64) ff += acts[L][k] * acts[L][k];
+      for (int k = lane; k < E; k += 64) ge += gemb[k] * gemb[k];
+      ff = hs_wave_sum(ff);
+      ge = hs_wave_sum(ge);
+      if (lane == 0) {
+        const float total = sqrtf(dd * ff + dd + small + ge);
+        float scale = 1.f;
+        if (clip > 0.f) {
+          const float coef = clip / (total + 1e-6f);
+          if (coef < 1.f) scale = coef;
+        }
+        red[0][0] = scale;
+        info[0] = total;
+        info[1] = scale;
+      }
+    }
+    __syncthreads();
+    const float gs = red[0][0];
+    // Adam over the embedding table (zero-gradient rows still move: torch's dense Embedding grad)
+    const long nemb = (long)d.n_nodes * E;
+    for (long e = tid; e < nemb; e += HS_NT) {
+      const int row = (int)(e / E), col = (int)(e - (long)row * E);
+      float mm = m[d.emb + e], vv = v[d.emb + e];
+      const float p = hs_adam(A[d.emb + e], row == ci ? gs * gemb[col] : 0.f, mm, vv, lr_bc1, rsqrt_bc2, b1, b2, eps);
+      m[d.emb + e] = mm;
+      v[d.emb + e] = vv;
+      A[d.emb + e] = p;
+    }
+    // Adam over the MLP (params from LDS, moments streamed; the LDS copy is updated for the next forward)
+    for (int l = 0; l < L; ++l) {
+      const int din = l == 0 ? E : H;
+      const long ow = d.w[l] - base, ob = d.b[l] - base;
+      const long nw = (long)H * din;
+#pragma unroll 4
+      for (long e = tid; e < nw; e += HS_NT) {
+        const int o = (int)(e / din), k = (int)(e - (long)o * din);
+        const long ge = d.w[l] + e;
+        float mm = m[ge], vv = v[ge];
+        const float p = hs_adam(sm[ow + e], gs * dz[l][o] * acts[l][k], mm, vv, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        m[ge] = mm;
+        v[ge] = vv;
+        A[ge] = p;
+        sm[ow + e] = p;
+      }
+      for (int o = tid; o < H; o += HS_NT) {
+        const long ge = d.b[l] + o;
+        float mm = m[ge], vv = v[ge];
+        const float p = hs_adam(sm[ob + o], gs * dz[l][o], mm, vv, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        m[ge] = mm;
+        v[ge] = vv;
+        A[ge] = p;
+        sm[ob + o] = p;
+      }
+    }
+    __syncthreads();  // updated embedding (global, this workgroup's writes) and LDS MLP visible
+  }
+  if (cj >= 0) {
+    hs_forward(A, sm, d, cj, acts);
+    if (tid < H) feat_j[tid] = acts[L][tid];
+  }
+}
+
+// head Adam with grad = (*gsp) * delta (x) f ; float4 over W (H % 4 == 0, 16-B aligned), scalar over b
+__global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, float* __restrict__ bvec,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      const float* __restrict__ delta, const float* __restrict__ f,
+                                                      long P, int H, float lr_bc1, float rsqrt_bc2, float b1,
+                                                      float b2, float eps, const float* __restrict__ gsp) {
+  __shared__ float fs[HS_HMAX];
+  if (threadIdx.x < H) fs[threadIdx.x] = f[threadIdx.x];
+  __syncthreads();
+  const float gs = *gsp;
+  const long nW4 = P * H / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float4* W4 = reinterpret_cast<float4*>(W);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nW4; i += stride) {
+    const long e = 4 * i;
+    const long r = e / H;
+    const int h = (int)(e - r * H);
+    const float dr = gs * delta[r];
+    float4 p = W4[i], mm = m4[i], vv = v4[i];
+    float* pp = &p.x;
+    float* mp = &mm.x;
+    float* vp = &vv.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float g = dr * fs[h + q];
+      mp[q] = mp[q] + (1.f - b1) * (g - mp[q]);
+      vp[q] = b2 * vp[q] + (1.f - b2) * g * g;
+      pp[q] -= lr_bc1 * mp[q] / (sqrtf(vp[q]) * rsqrt_bc2 + eps);
+    }
+    W4[i] = p;
+    m4[i] = mm;
+    v4[i] = vv;
+  }
+  const long nW = P * H;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < P; r += stride) {
+    const float g = gs * delta[r];
+    const long e = nW + r;
+    const float mi = m[e] + (1.f - b1) * (g - m[e]);
+    const float vi = b2 * v[e] + (1.f - b2) * g * g;
+    m[e] = mi;
+    v[e] = vi;
+    bvec[r] -= lr_bc1 * mi / (sqrtf(vi) * rsqrt_bc2 + eps);
+  }
+}
+
+void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
+                             int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
+                             float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
+                             float* info, hipStream_t s) {
+  const int H = d.H;
+  const int nb = afl_hyper_nblocks(P);
+  float* W = A + offW;
+  float* bv = A + offB;
+  const long nmlp = offW - d.w[0];
+  hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, -1, clients[0], feat, info, d,
+                     nmlp, clip, 0.f, 0.f, b1, b2, eps);
+  const long nW4 = P * H / 4;
+  const int nba = (int)min(4096L, (nW4 + 255) / 256);
+  for (int k = 0; k < n; ++k) {
+    const int step = step0 + k + 1;
+    const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+    const float lr_bc1 = (float)(lr / bc1), rbc2 = (float)(1.0 / sqrt(bc2));
+    float* fk = feat + (k & 1) * HS_HMAX;
+    float* fn = feat + ((k + 1) & 1) * HS_HMAX;
+    hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta, partial,
+                       H + 1);
+    hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
+                       k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps);
+    hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, delta, fk, P, H,
+                       lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1);
+  }
+}
+
+void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const int* clients, int n, float* out,
+                        hipStream_t s) {
+  for (int k = 0; k < n; ++k)
+    hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, const_cast<float*>(A), nullptr, nullptr, nullptr, 0,
+                       -1, clients[k], out + (long)k * d.H, nullptr, d, offW - d.w[0], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
+}
+
+long afl_hyper_small_capacity() { return HS_SMEM; }

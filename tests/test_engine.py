@@ -251,3 +251,16 @@ def test_plan_is_placement_independent():
     c = make_plan(1000, [300, 500, 120], 2, [11, 99, 12], "cpu")
     assert torch.equal(a.client(1), b.client(0)) and torch.equal(a.client(1), c.client(2))
     assert torch.equal(a.client(0), c.client(0))
+
+
+def test_plan_subset_and_epoch_permutations():
+    """Each client visits nd distinct rows; every epoch is a permutation of the same subset."""
+    from attackfl_amd.fl.trainers import make_plan
+    nd = [700, 333, 1000]
+    p = make_plan(1000, nd, 3, [5, 6, 7], "cpu")
+    for c, n in enumerate(nd):
+        sub = p.order[c, 0, :n]
+        assert len(set(sub.tolist())) == n and int(sub.min()) >= 0 and int(sub.max()) < 1000
+        for e in range(1, 3):
+            ep = p.order[c, e, :n]
+            assert torch.equal(ep.sort().values, sub.sort().values) and not torch.equal(ep, sub)

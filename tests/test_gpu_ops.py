@@ -146,3 +146,48 @@ def test_stoch_quant(gpu):
     assert torch.allclose(smin.cpu(), U.min(1).values) and torch.allclose(smax.cpu(), U.max(1).values)
     probs = (U - U.min(1, keepdim=True).values) / (U.max(1, keepdim=True).values - U.min(1, keepdim=True).values + 1e-6)
     assert abs(sigma.cpu().mean().item() - probs.mean().item()) < 5e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,clip", [("TransformerModel", 1e9), ("RNNModel", 0.05)])
+def test_hyper_server_update_matches_composite(gpu, model, clip):
+    """Sync-free native round update (rows / small-net / head-Adam kernels) vs the CPU composite path."""
+    from attackfl_amd.fl.hyper_server import HyperServer
+    from attackfl_amd.models import build_model
+
+    sd = build_model(model, seed=0).state_dict()
+    n = 5
+    cpu = HyperServer(sd, n, 0.01, clip, "cpu", seed=3)
+    dev = HyperServer(sd, n, 0.01, clip, gpu, seed=3)
+    assert dev._native_ok()
+    g = torch.Generator().manual_seed(1)
+    for rnd in range(2):
+        sel = [3, 0, 4, 1] if rnd == 0 else [2, 1]
+        # |delta| >= 0.05 everywhere: Adam's first steps are sign-like, so a cancellation-sized delta would
+        # amplify fp32 summation-order differences into O(lr) parameter differences
+        r = torch.randn(len(sel), cpu.hnet.P, generator=g)
+        U = torch.stack([cpu.generate(i) for i in sel]) - 0.1 * torch.sign(r) * (0.5 + r.abs())
+        cpu.train(sel, {i: U[k] for k, i in enumerate(sel)})
+        Ud = U.to(gpu)
+        dev.train(sel, {i: Ud[k] for k, i in enumerate(sel)})
+        assert dev.step == cpu.step
+        assert abs(dev.last_info["grad_norm"] - cpu.last_info["grad_norm"]) <= 1e-3 * cpu.last_info["grad_norm"]
+        assert abs(dev.last_info["clip_scale"] - cpu.last_info["clip_scale"]) <= 1e-3 * cpu.last_info["clip_scale"]
+    a, b = dev.hnet.arena.cpu(), cpu.hnet.arena
+    # fp32 reduction order differs (per-block partials); Adam amplifies it where clipped grads approach eps
+    assert torch.allclose(a, b, rtol=1e-4, atol=2e-4), float((a - b).abs().max())
+    feats = ops.hyper_features(dev.hnet.arena, [0, 2, 4], dev.layout_vec()).cpu()
+    cpu.hnet.arena.copy_(a)  # same parameters on both sides
+    ref = torch.stack([cpu.hnet.features(i)[1] for i in (0, 2, 4)])
+    assert torch.allclose(feats, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_make_plan_native_matches_cpu_mirror(gpu):
+    from attackfl_amd.fl.trainers import make_plan
+    nd, seeds = [15000, 12001, 2, 13999], [17, 2 ** 40 + 3, 99, 2 ** 63 + 5]
+    a = make_plan(60000, nd, 5, seeds, gpu)
+    b = make_plan(60000, nd, 5, seeds, "cpu")
+    assert a.order.is_cuda
+    for c, n in enumerate(nd):
+        assert torch.equal(a.order[c, :, :n].cpu(), b.order[c, :, :n])
