@@ -33,6 +33,7 @@ class _Program:
 
     model_name = ""
     loss = "bce"
+    fused_loss = False  # True: backward_loss() computes the loss itself (the runner skips its loss kernel)
 
     def __init__(self, C: int, B: int, device, train: bool = True, dropout: bool = True):
         self.layout = ParamLayout.for_model(self.model_name)
@@ -130,60 +131,74 @@ class _ICUProgram(_Program):
 
 
 class CNNProgram(_ICUProgram):
-    """CNNModel: Conv1d towers as im2col + MFMA GEMM (bias+ReLU epilogue), pool+dropout, MLP head."""
+    """CNNModel: both Conv1d towers (conv1..3 + ReLU + pool + dropout) in one fused launch each way
+    (``Lx.cnn_towers_fwd/bwd``, ``csrc/kernels/cnn.hip``), every conv weight gradient in one more
+    (``Lx.conv_dw``), MLP head as MFMA GEMMs with fused epilogues."""
 
     model_name = "CNNModel"
     CH = (1, 32, 64, 128)
 
-    def _tower(self, br, L, params, ctl, bi):
+    def wimg(self):
+        if self.device.type != "cuda":
+            return None
+        if "wimg" not in self._bufs:
+            self._bufs["wimg"] = Lx.cnn_wimg_buffer(self.C, self.device)
+        return self._bufs["wimg"]
+
+    def towers(self, params):
         C, B = self.C, self.B
-        x = self.buf("xv" if br == "vitals" else "xl", C, B, L).view(C, B * L, 1)
-        for i in (1, 2, 3):
-            cin, cout = self.CH[i - 1], self.CH[i]
-            cols = self.buf(f"{br}_cols{i}", C, B * L, 3 * cin)
-            h = self.buf(f"{br}_h{i}", C, B * L, cout)
-            Lx.im2col3(x, B, L, cols)
-            Lx.bgemm(cols, self.w(params, f"{br}_conv{i}.weight"), h, bias=self.w(params, f"{br}_conv{i}.bias"),
-                     act=ACT_RELU)
-            x = h
-        Lx.pool4_fwd(x, B, L, self.buf("cat", C, B, 1024), 512 * bi, ctl, layer=bi, p=self.p(0.3))
+        out = []
+        for bi, (br, L) in enumerate((("vitals", VIT), ("labs", LAB))):
+            h = [self.buf(f"{br}_h{i}", C, B * L, self.CH[i]) for i in (1, 2, 3)]
+            dh = [self.buf(f"{br}_dh{i}", C, B * L, self.CH[i]) for i in (1, 2, 3)] if self.train else h
+            out.append(Lx.CnnTower(self.buf("xv" if bi == 0 else "xl", C, B, L),
+                                   self.w(params, f"{br}_conv1.weight"), self.w(params, f"{br}_conv1.bias"),
+                                   self.w(params, f"{br}_conv2.weight"), self.w(params, f"{br}_conv2.bias"),
+                                   self.w(params, f"{br}_conv3.weight"), self.w(params, f"{br}_conv3.bias"),
+                                   h[0], h[1], h[2], dh[0], dh[1], dh[2], L, 512 * bi, bi))
+        return out
+
+    fused_loss = True
 
     def forward(self, params, ctl):
+        """Training: towers + the fc1 pre-activation (split-K; the head kernel inside ``backward_loss`` adds
+        the bias and the ReLU); eval: the full forward -> z."""
         C, B = self.C, self.B
-        self._tower("vitals", VIT, params, ctl, 0)
-        self._tower("labs", LAB, params, ctl, 1)
+        cat = self.buf("cat", C, B, 1024)
+        head = [self.w(params, "fc2.weight"), self.w(params, "fc3.weight")] if self.train else []
+        Lx.cnn_towers_fwd(self.towers(params), B, cat, ctl, self.p(0.3), self.wimg(), head)
+        if self.train:
+            z1 = self.buf("z1", C, B, 128)
+            z1.zero_()
+            Lx.bgemm(cat, self.w(params, "fc1.weight"), z1, accum=2 if cat.is_cuda else 0,
+                     splitk=8 if cat.is_cuda else 1)
+            return None
         f1, f2, f3 = self.buf("f1", C, B, 128), self.buf("f2", C, B, 64), self.buf("f3", C, B, 32)
         z = self.buf("z", C, B, 1)
-        self.linear(self.buf("cat", C, B, 1024), params, "fc1.weight", "fc1.bias", f1, act=ACT_RELU)
+        self.linear(cat, params, "fc1.weight", "fc1.bias", f1, act=ACT_RELU)
         self.linear(f1, params, "fc2.weight", "fc2.bias", f2, act=ACT_RELU)
         self.linear(f2, params, "fc3.weight", "fc3.bias", f3, act=ACT_RELU)
         self.linear(f3, params, "output.weight", "output.bias", z)
         return z
 
-    def backward(self, params, grads, ctl):
+    def backward_loss(self, params, grads, ctl, loss_ctx):
         C, B = self.C, self.B
-        f1, f2, f3 = self.buf("f1", C, B, 128), self.buf("f2", C, B, 64), self.buf("f3", C, B, 32)
-        dz = self.buf("dz", C, B, 1)
-        d3, d2, d1 = self.buf("d3", C, B, 32), self.buf("d2", C, B, 64), self.buf("d1", C, B, 128)
-        dcat = self.buf("dcat", C, B, 1024)
-        self.linear_bwd(dz, f3, params, grads, "output.weight", "output.bias", d3, G=f3, gact=ACT_RELU)
-        self.linear_bwd(d3, f2, params, grads, "fc3.weight", "fc3.bias", d2, G=f2, gact=ACT_RELU)
-        self.linear_bwd(d2, f1, params, grads, "fc2.weight", "fc2.bias", d1, G=f1, gact=ACT_RELU)
-        self.linear_bwd(d1, self.buf("cat", C, B, 1024), params, grads, "fc1.weight", "fc1.bias", dcat)
-        for bi, (br, L) in enumerate((("vitals", VIT), ("labs", LAB))):
-            dh = self.buf(f"{br}_dh3", C, B * L, 128)
-            Lx.pool4_bwd(dcat, 512 * bi, self.buf(f"{br}_h3", C, B * L, 128), B, L, dh, ctl, layer=bi, p=self.p(0.3))
-            for i in (3, 2, 1):
-                cin = self.CH[i - 1]
-                cols = self.buf(f"{br}_cols{i}", C, B * L, 3 * cin)
-                self.dw(dh, cols, self.w(grads, f"{br}_conv{i}.weight"))
-                Lx.colsum(dh, self.w(grads, f"{br}_conv{i}.bias"))
-                if i > 1:
-                    dcols = self.buf(f"{br}_dcols{i}", C, B * L, 3 * cin)
-                    Lx.bgemm(dh, self.w(params, f"{br}_conv{i}.weight").transpose(1, 2), dcols)
-                    dprev = self.buf(f"{br}_dh{i - 1}", C, B * L, cin)
-                    Lx.col2im3(dcols, B, L, cin, self.buf(f"{br}_h{i - 1}", C, B * L, cin), dprev)
-                    dh = dprev
+        bsz, ep, nb, failed, losses = loss_ctx
+        d1, cat, dcat = self.buf("d1", C, B, 128), self.buf("cat", C, B, 1024), self.buf("dcat", C, B, 1024)
+        names = ("fc2.weight", "fc2.bias", "fc3.weight", "fc3.bias", "output.weight", "output.bias")
+        Lx.cnn_head(self.buf("z1", C, B, 128), self.labels(), [self.w(params, n) for n in names + ("fc1.bias",)],
+                    [self.w(grads, n) for n in names] + [self.w(grads, "fc1.bias")], d1, bsz, ep, nb, ctl, failed,
+                    losses, wimg=self.wimg())
+        self.dw(d1, cat, self.w(grads, "fc1.weight"))
+        Lx.bgemm(d1, self.w(params, "fc1.weight").transpose(1, 2), dcat)
+        tw = self.towers(params)
+        Lx.cnn_towers_bwd(tw, B, dcat, ctl, self.p(0.3), self.wimg())
+        jobs = []
+        for t, br in zip(tw, ("vitals", "labs")):
+            hp = (t.x, t.h1, t.h2)
+            for i, (dh, h) in enumerate(zip((t.dh1, t.dh2, t.dh3), hp), start=1):
+                jobs.append((dh, h, self.w(grads, f"{br}_conv{i}.weight"), self.w(grads, f"{br}_conv{i}.bias"), t.L))
+        Lx.conv_dw(jobs, B)
 
 
 class RNNProgram(_ICUProgram):
@@ -407,6 +422,12 @@ class ProgramRunner:
         def step():
             pg.inputs(table, idx, ctl)
             out = pg.forward(params, ctl)
+            if pg.fused_loss:
+                grads.zero_()
+                pg.backward_loss(params, grads, ctl, (bsz, ep, nb, failed, losses))
+                Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr)
+                Lx.step_end(ctl, tcount, bsz, failed)
+                return
             dz = pg.buf("dz", *out.shape)
             if pg.loss == "bce":
                 Lx.bce(out, pg.labels(), bsz, ep, nb, ctl, failed, losses, dz)

@@ -170,6 +170,129 @@ def col2im3(dcols, B: int, L: int, Cin: int, relu_src, dx) -> None:
     dx.copy_(g.reshape(dx.shape))
 
 
+# --------------------------------------------------------------------- fused CNNModel towers
+@dataclass
+class CnnTower:
+    """One Conv1d tower of CNNModel (vitals or labs) and its step buffers.
+
+    ``x [C, B, L]`` input; weights as arena views ``W1 [C,32,3] b1 [C,32] W2 [C,64,96] b2 W3 [C,128,192] b3``;
+    saved activations ``h1..h3 [C, B*L, 32|64|128]`` and their gradients ``dh1..dh3``; the tower's pooled
+    output fills concat columns ``[col0, col0 + 512)`` with dropout site ``layer``."""
+
+    x: torch.Tensor
+    W1: torch.Tensor
+    b1: torch.Tensor
+    W2: torch.Tensor
+    b2: torch.Tensor
+    W3: torch.Tensor
+    b3: torch.Tensor
+    h1: torch.Tensor
+    h2: torch.Tensor
+    h3: torch.Tensor
+    dh1: torch.Tensor
+    dh2: torch.Tensor
+    dh3: torch.Tensor
+    L: int
+    col0: int
+    layer: int
+
+    def tensors(self):
+        return [self.x, self.W1, self.b1, self.W2, self.b2, self.W3, self.b3, self.h1, self.h2, self.h3, self.dh1,
+                self.dh2, self.dh3]
+
+    def meta(self):
+        return [self.L, self.col0, self.layer]
+
+
+def cnn_wimg_buffer(C: int, device) -> torch.Tensor:
+    """Scratch for the towers' per-step bf16 weight images (built by the forward, read by the backward)."""
+    return torch.zeros(int(_native().cnn_wimg_size(C)), dtype=torch.int16, device=device)
+
+
+def cnn_towers_fwd(towers, B: int, cat, ctl: Optional[StepCtl] = None, p: float = 0.0, wimg=None,
+                   head=()) -> None:
+    """conv1..conv3 (+bias, ReLU) -> AdaptiveAvgPool1d(4) -> dropout into ``cat`` for both towers
+    (on device: ``cnn.hip:k_cnn_wimg`` + ``k_cnn_fwd``; ``wimg`` from ``cnn_wimg_buffer``; ``head`` =
+    optional ``[fc2.weight, fc3.weight]`` views whose bf16 images ``cnn_head`` then reads)."""
+    if _nat(cat):
+        s, sc = _dargs(ctl, p)
+        _native().cnn_towers_fwd(towers[0].tensors(), towers[1].tensors(), towers[0].meta(), towers[1].meta(), B,
+                                 cat, s, sc, p, wimg, list(head))
+        return
+    for tw in towers:
+        C = tw.x.shape[0]
+        h = tw.x.reshape(C, B * tw.L, 1)
+        for W, b, out in ((tw.W1, tw.b1, tw.h1), (tw.W2, tw.b2, tw.h2), (tw.W3, tw.b3, tw.h3)):
+            v = torch.bmm(_im2col(h, B, tw.L), W.reshape(C, W.shape[1], -1).transpose(1, 2)) + b[:, None, :]
+            out.copy_(F.relu(v).reshape(out.shape))
+            h = out.reshape(C, B * tw.L, -1)
+        pool4_fwd(h, B, tw.L, cat, tw.col0, ctl, tw.layer, p)
+
+
+def cnn_towers_bwd(towers, B: int, dcat, ctl: Optional[StepCtl] = None, p: float = 0.0, wimg=None) -> None:
+    """pool'/dropout'/ReLU' -> dh3; dh2 = col2im(dh3 . W3) * relu'(h2); dh1 = col2im(dh2 . W2) * relu'(h1)
+    (device: reads the weight images the same step's ``cnn_towers_fwd`` built in ``wimg``)."""
+    if _nat(dcat):
+        s, sc = _dargs(ctl, p)
+        _native().cnn_towers_bwd(towers[0].tensors(), towers[1].tensors(), towers[0].meta(), towers[1].meta(), B,
+                                 dcat, s, sc, p, wimg)
+        return
+    for tw in towers:
+        C, L = tw.x.shape[0], tw.L
+        h3 = tw.h3.reshape(C, B * L, 128)
+        pool4_bwd(dcat, tw.col0, h3, B, L, tw.dh3.reshape(C, B * L, 128), ctl, tw.layer, p)
+        for W, hprev, dcur, dprev, cin in ((tw.W3, tw.h2, tw.dh3, tw.dh2, 64), (tw.W2, tw.h1, tw.dh2, tw.dh1, 32)):
+            dcols = torch.bmm(dcur.reshape(C, B * L, -1), W.reshape(C, W.shape[1], -1))
+            col2im3(dcols, B, L, cin, hprev.reshape(C, B * L, cin), dprev.reshape(C, B * L, cin))
+
+
+def conv_dw(jobs, B: int, splitk: int = 4) -> None:
+    """Conv weight / bias gradients of several (dh, h_prev, gW, gb, L) jobs, ACCUMULATED into gW / gb
+    (the step's zeroed gradient arena): ``gW += dh^T . im2col(h_prev)``, ``gb += colsum(dh)``."""
+    if _nat(jobs[0][0]):
+        _native().conv_dw([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs], [j[3] for j in jobs],
+                          [int(j[4]) for j in jobs], int(B), int(splitk))
+        return
+    for dh, hp, gW, gb, L in jobs:
+        C, Cout, K = gW.shape
+        cols = _im2col(hp.reshape(C, B * L, K // 3), B, L)
+        d = dh.reshape(C, B * L, Cout)
+        gW.add_(torch.bmm(d.transpose(1, 2), cols))
+        gb.add_(d.sum(dim=1))
+
+
+def cnn_head(z1, y, w, g, d1, bsz, epoch, nb, ctl: StepCtl, failed, losses, z=None, wimg=None) -> None:
+    """CNNModel head in one launch per step: ``f1 = ReLU(z1 + b1)`` from the fc1 pre-activation, ``fc2 ->
+    ReLU -> fc3 -> ReLU -> output``, the sigmoid-BCE of ``bce`` (same masking / NaN abort / epoch losses),
+    and the backward: gradients of fc2 / fc3 / output and the fc1 bias (``g = [gW2, gb2, gW3, gb3, gWo,
+    gbo, gb1]``, stored) and ``d1`` = d(fc1 pre-activation).  ``w = [W2, b2, W3, b3, Wo, bo, b1]``; on
+    device the fc2 / fc3 weights come from the bf16 images the towers' forward built in ``wimg``."""
+    W2, b2, W3, b3, Wo, bo, b1 = w
+    if _nat(z1):
+        _native().cnn_head(z1, y, list(w), list(g), d1, z, bsz, epoch, nb, ctl.stepctl, failed, losses, wimg)
+        return
+    f1 = F.relu(z1 + b1[:, None, :])
+    f2 = F.relu(torch.bmm(f1, W2.transpose(1, 2)) + b2[:, None, :])
+    f3 = F.relu(torch.bmm(f2, W3.transpose(1, 2)) + b3[:, None, :])
+    zz = torch.bmm(f3, Wo.reshape(Wo.shape[0], 1, 32).transpose(1, 2)) + bo.reshape(-1, 1, 1)
+    if z is not None:
+        z.copy_(zz.reshape(z.shape))
+    dz = torch.zeros_like(zz)
+    bce(zz, y, bsz, epoch, nb, ctl, failed, losses, dz)
+    gW2, gb2, gW3, gb3, gWo, gbo, gb1 = g
+    gWo.copy_(torch.bmm(dz.transpose(1, 2), f3).reshape(gWo.shape))
+    gbo.copy_(dz.sum(dim=1).reshape(gbo.shape))
+    d3 = torch.bmm(dz, Wo.reshape(Wo.shape[0], 1, 32)) * (f3 > 0).float()
+    gW3.copy_(torch.bmm(d3.transpose(1, 2), f2))
+    gb3.copy_(d3.sum(dim=1))
+    d2 = torch.bmm(d3, W3) * (f2 > 0).float()
+    gW2.copy_(torch.bmm(d2.transpose(1, 2), f1))
+    gb2.copy_(d2.sum(dim=1))
+    dd1 = torch.bmm(d2, W2) * (f1 > 0).float()
+    gb1.copy_(dd1.sum(dim=1))
+    d1.copy_(dd1.reshape(d1.shape))
+
+
 # --------------------------------------------------------------------- AdaptiveAvgPool1d(4)
 def _pool4(h, B, L):
     C, _, Ch = h.shape

@@ -117,6 +117,61 @@ struct AflGemm {
   int avec, bvec;  // set by the launcher: operand rows 16-B aligned and k-contiguous
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
+
+// cnn.hip: fused CNNModel towers (conv1-3 + pool + dropout) forward / backward, conv weight grads
+struct AflCnnBranch {
+  const float* x;                    // input [C][B*L] (one channel); client stride sXc
+  long sXc;
+  const float *W1, *b1, *W2, *b2, *W3, *b3;  // client-0 parameter views (client c at + c * sWc)
+  float *h1, *h2, *h3;               // saved activations [C][B*L][32 | 64 | 128] (dense)
+  float *dh1, *dh2, *dh3;            // backward outputs, same layout
+  int L, R, ntiles, col0;            // R samples per workgroup tile (R * L <= 64)
+  uint32_t layer;                    // dropout site id of the tower's concat slice
+};
+struct AflCnnTowers {
+  AflCnnBranch br[2];
+  long sWc;
+  float* cat;                        // [C][B][1024] concat (forward output)
+  const float* dcat;                 // its gradient (backward input), same strides
+  long sCatc, sCatr;
+  int C, B;
+  AflDrop drop;                      // seeds / step / p (layer per branch)
+  unsigned short* wimg;              // bf16 weight images (afl_cnn_wimg_ushorts(C)), built by the forward
+  const float *W2h, *W3h;            // optional head fc2 / fc3 weights (client-0 views): images for k_cnn_head
+};
+long afl_cnn_wimg_ushorts(int C);
+int afl_cnn_towers_fwd(const AflCnnTowers& a, hipStream_t s);
+int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s);
+struct AflConvDwJob {
+  const float* dh;   // [C][B*L][Cout] dense
+  const float* hp;   // [C][B*L][Cin] dense (conv input)
+  float* gW;         // client-0 grad view [Cout][3*Cin] (client c at + c * sGc)
+  float* gb;         // client-0 bias grad [Cout]
+  int Cin, Cout, L, tile_base;
+};
+struct AflConvDw {
+  AflConvDwJob job[6];
+  int njobs, total_tiles, splitk, C, B;
+  long sGc;
+};
+int afl_conv_dw(const AflConvDw& a, hipStream_t s);
+struct AflCnnHead {
+  const float* f1;                   // [C][B][128] fc1 PRE-activation (bias + ReLU applied here; B <= 128)
+  const float* b1;                   // fc1 bias (client-0 view)
+  const unsigned short* wimg;        // head weight images of client 0 (built by the towers' forward)
+  const float* y;                    // [C][B] labels
+  const float *W2, *b2, *W3, *b3, *Wo, *bo;  // client-0 parameter views (+ c * sWc)
+  long sWc;
+  float *gW2, *gb2, *gW3, *gb3, *gWo, *gbo, *gb1;  // client-0 gradient views (+ c * sGc)
+  long sGc;
+  float* d1;                         // [C][B][128] d(fc1 pre-activation)
+  float* z;                          // optional [C][B] logits
+  const int *bsz, *epoch, *nb, *stepctl;
+  int* failed;
+  float* losses;
+  int S, E, C, B;
+};
+int afl_cnn_head(const AflCnnHead& h, hipStream_t s);
 int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s);
 int afl_gather_icu(const float* rows, const int* idx, const int* stepctl, int C, int B, int mask, float* vit,
                    float* lab, float* y, hipStream_t s);

@@ -1,0 +1,754 @@
+// CNNModel towers as three fused client-batched kernels (reference src/Model.py:27-88:
+// Conv1d(1->32->64->128, k3, p1) + ReLU per tower, AdaptiveAvgPool1d(4), Dropout(0.3)).
+// They replace the per-layer im2col / GEMM / col2im / pool / colsum launch chain of the CNN step
+// program (attackfl_amd/fl/programs.py) — the step was launch-bound at ~60 tiny launches.
+//
+//   k_cnn_fwd  one workgroup = one (client, tower, tile of R samples, <= 64 positions): conv1 on
+//              VALU, conv2 / conv3 as MFMA GEMMs over an im2col image built in LDS (bf16 operands,
+//              fp32 accumulate), bias + ReLU epilogues, AdaptiveAvgPool1d(4) + hash dropout straight
+//              into the [B, 1024] concat.  Saves h1 / h2 / h3 (channels-last fp32) for the backward.
+//   k_cnn_bwd  same tiling: pool' + dropout' + ReLU' -> dh3; dcols2 = dh3 . W3 (MFMA), col2im + ReLU'
+//              -> dh2; dcols1 = dh2 . W2, col2im + ReLU' -> dh1.  Writes dh1..dh3.
+//   k_conv_dw  every conv weight/bias gradient of both towers in one launch: dW = dh^T . im2col(h_prev)
+//              over the B*L positions (im2col gathered while staging; split-K, atomic accumulation
+//              into the zeroed per-step gradient arena), bias = column sums of dh.
+// Dropout mask sites match k_pool4_fwd/bwd: (layer, sample b, concat column col0 + ch*4 + p).
+#include "common.h"
+#include "kernels.h"
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ unsigned short bfu(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ f4v mfma32(s8v a, s8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0,
+                                                 0);
+}
+// A / B fragment of v_mfma_f32_16x16x32_bf16 from a [rows][ld] bf16 LDS image: row r0 + (lane & 15),
+// k = k0 + 8 * (lane >> 4) .. +7
+__device__ __forceinline__ s8v frag(const unsigned short* S, int ld, int r0, int k0, int lane) {
+  return *(const s8v*)(S + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));
+}
+__device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }  // keeps NaN like torch
+__device__ __forceinline__ int bin_lo(int p, int L) { return (p * L) / 4; }
+__device__ __forceinline__ int bin_hi(int p, int L) { return ((p + 1) * L + 3) / 4; }
+
+constexpr int NT = 512;  // 8 waves
+constexpr int MT = 64;   // positions per tile
+
+// bf16 weight images per (client, tower), rebuilt once per step by k_cnn_wimg: the tower kernels read
+// MFMA B fragments straight from them (16-B global loads, L2 resident) instead of staging fp32 weights
+constexpr int WI_W2 = 0;                  // [64][96]   (n = out, k = ci*3+j)   forward conv2
+constexpr int WI_W3 = WI_W2 + 64 * 96;    // [128][192] forward conv3
+constexpr int WI_W2T = WI_W3 + 128 * 192; // [96][64]   (n = ci*3+j, k = out)  backward dcols1
+constexpr int WI_W3T = WI_W2T + 96 * 64;  // [192][128] backward dcols2
+constexpr int WI_SIZE = WI_W3T + 192 * 128;  // ushorts per (client, tower)
+// head images follow the towers' images of every client: [C][64 * 128 + 32 * 64] (fc2 | fc3 weights)
+constexpr int WI_HEAD = 64 * 128 + 32 * 64;
+
+__global__ void __launch_bounds__(256) k_cnn_wimg(AflCnnTowers a) {
+  const AflCnnBranch& br = a.br[blockIdx.y];
+  const int c = blockIdx.z;
+  const long wo = (long)c * a.sWc;
+  if (a.W2h && blockIdx.y == 0) {  // head fc2 / fc3 weights (row-major bf16)
+    unsigned short* hi = a.wimg + (long)a.C * 2 * WI_SIZE + (long)c * WI_HEAD;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < WI_HEAD; e += gridDim.x * 256)
+      hi[e] = bfu(e < 64 * 128 ? a.W2h[wo + e] : a.W3h[wo + e - 64 * 128]);
+  }
+  unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < 64 * 96 + 128 * 192; e += gridDim.x * 256) {
+    if (e < 64 * 96) {
+      const float v = br.W2[wo + e];
+      const int o = e / 96, k = e - o * 96;
+      img[WI_W2 + e] = bfu(v);
+      img[WI_W2T + k * 64 + o] = bfu(v);
+    } else {
+      const int f = e - 64 * 96;
+      const float v = br.W3[wo + f];
+      const int o = f / 192, k = f - o * 192;
+      img[WI_W3 + f] = bfu(v);
+      img[WI_W3T + k * 128 + o] = bfu(v);
+    }
+  }
+}
+
+__device__ __forceinline__ s8v gfrag(const unsigned short* __restrict__ W, int ldk, int n0, int k0, int lane) {
+  return *(const s8v*)(W + (n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+}
+
+// ------------------------------------------------------------------------------------------ forward
+// LDS map (bytes): A3 and h2f are dead once conv3's MFMAs are done, h3f reuses them
+constexpr int F_LD3 = 200, F_LD2 = 104, F_LH1 = 36, F_LH2 = 68, F_LH3 = 132;
+constexpr int F_A3 = 0;                               // [64][200] bf16   25600
+constexpr int F_H2 = F_A3 + MT * F_LD3 * 2;           // [64][68] f32     17408
+constexpr int F_H3 = 0;                               // [64][132] f32    33792 (after conv3)
+constexpr int F_H1 = F_H2 + MT * F_LH2 * 4;           // [64][36] f32     9216
+constexpr int F_A2 = F_H1 + MT * F_LH1 * 4;           // [64][104] bf16   13312
+constexpr int F_X = F_A2 + MT * F_LD2 * 2;
+constexpr int F_TOTAL = F_X + (MT + 8) * 4;
+static_assert(F_H3 + MT * F_LH3 * 4 <= F_H1, "h3 alias");
+static_assert(F_TOTAL <= 80 * 1024, "cnn fwd LDS: two workgroups per CU");
+
+template <int L>
+__device__ void cnn_fwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsigned char* smem) {
+  const int tile = blockIdx.x, c = blockIdx.z;
+  const int b0 = tile * br.R, nb = min(br.R, a.B - b0), M = nb * L;
+  const long row0 = (long)b0 * L, cb = (long)c * a.B * L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned short* A3 = (unsigned short*)(smem + F_A3);
+  float* h2f = (float*)(smem + F_H2);
+  float* h3f = (float*)(smem + F_H3);
+  float* h1f = (float*)(smem + F_H1);
+  unsigned short* A2 = (unsigned short*)(smem + F_A2);
+  float* xs = (float*)(smem + F_X);
+  const long wo = (long)c * a.sWc;
+  const unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
+  if (tid < MT) xs[tid] = tid < M ? br.x[(long)c * br.sXc + row0 + tid] : 0.f;
+  __syncthreads();
+  // conv1 (1 -> 32) on VALU
+  {
+    const float* W1 = br.W1 + wo;
+    const int o = tid & 31;
+    const float w0 = W1[o * 3], w1 = W1[o * 3 + 1], w2 = W1[o * 3 + 2], bo = br.b1[wo + o];
+    for (int m = tid >> 5; m < MT; m += NT / 32) {
+      const int l = m % L;
+      float v = 0.f;
+      if (m < M) {
+        float s = bo + w1 * xs[m];
+        if (l > 0) s += w0 * xs[m - 1];
+        if (l < L - 1) s += w2 * xs[m + 1];
+        v = relu(s);
+        br.h1[(cb + row0 + m) * 32 + o] = v;
+      }
+      h1f[m * F_LH1 + o] = v;
+    }
+  }
+  __syncthreads();
+  // im2col(h1): A2[m][ci*3 + j] = h1[m + j - 1][ci] within the sample; one (m, ci) per thread step
+  for (int e = tid; e < MT * 32; e += NT) {
+    const int m = e >> 5, ci = e & 31, l = m % L;
+    const bool ok = m < M;
+    const float c0 = ok && l > 0 ? h1f[(m - 1) * F_LH1 + ci] : 0.f;
+    const float c1 = ok ? h1f[m * F_LH1 + ci] : 0.f;
+    const float c2 = ok && l < L - 1 ? h1f[(m + 1) * F_LH1 + ci] : 0.f;
+    unsigned short* d = A2 + m * F_LD2 + ci * 3;
+    d[0] = bfu(c0);
+    d[1] = bfu(c1);
+    d[2] = bfu(c2);
+  }
+  __syncthreads();
+  // conv2: [64 x 96] . W2^T -> [64 x 64]; wave -> m-tile (wave & 3), n-tiles 2*(wave >> 2) + {0,1}
+  {
+    const int mt = (wave & 3) * 16;
+    f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k0 = 0; k0 < 96; k0 += 32) {
+      const s8v af = frag(A2, F_LD2, mt, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = mfma32(af, gfrag(img + WI_W2, 96, ((wave >> 2) * 2 + j) * 16, k0, lane), acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = ((wave >> 2) * 2 + j) * 16 + (lane & 15);
+      const float bn = br.b2[wo + n];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = mt + 4 * (lane >> 4) + e;
+        const float v = m < M ? relu(acc[j][e] + bn) : 0.f;
+        h2f[m * F_LH2 + n] = v;
+        if (m < M) br.h2[(cb + row0 + m) * 64 + n] = v;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < MT * 64; e += NT) {
+    const int m = e >> 6, ci = e & 63, l = m % L;
+    const bool ok = m < M;
+    const float c0 = ok && l > 0 ? h2f[(m - 1) * F_LH2 + ci] : 0.f;
+    const float c1 = ok ? h2f[m * F_LH2 + ci] : 0.f;
+    const float c2 = ok && l < L - 1 ? h2f[(m + 1) * F_LH2 + ci] : 0.f;
+    unsigned short* d = A3 + m * F_LD3 + ci * 3;
+    d[0] = bfu(c0);
+    d[1] = bfu(c1);
+    d[2] = bfu(c2);
+  }
+  __syncthreads();
+  // conv3: [64 x 192] . W3^T -> [64 x 128]; wave -> m-tile (wave & 3), n-tiles 4*(wave >> 2) + 0..3
+  {
+    const int mt = (wave & 3) * 16;
+    f4v acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 192; k0 += 32) {
+      const s8v af = frag(A3, F_LD3, mt, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = mfma32(af, gfrag(img + WI_W3, 192, ((wave >> 2) * 4 + j) * 16, k0, lane), acc[j]);
+    }
+    __syncthreads();  // h3f overwrites A3 / h2f
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = ((wave >> 2) * 4 + j) * 16 + (lane & 15);
+      const float bn = br.b3[wo + n];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = mt + 4 * (lane >> 4) + e;
+        const float v = m < M ? relu(acc[j][e] + bn) : 0.f;
+        h3f[m * F_LH3 + n] = v;
+        if (m < M) br.h3[(cb + row0 + m) * 128 + n] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // AdaptiveAvgPool1d(4) + dropout -> concat columns col0 + ch*4 + p
+  const bool dr = a.drop.thr16 != 0;
+  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+  for (int e = tid; e < nb * 512; e += NT) {
+    const int r = e >> 9, ch = (e >> 2) & 127, p = e & 3;
+    const int lo = bin_lo(p, L), hi = bin_hi(p, L);
+    float sum = 0.f;
+    for (int l = lo; l < hi; ++l) sum += h3f[(r * L + l) * F_LH3 + ch];
+    sum /= (float)(hi - lo);
+    const int col = br.col0 + ch * 4 + p;
+    if (dr) sum *= afl_keep(key, br.layer, (uint32_t)(b0 + r), (uint32_t)col, a.drop.thr16) ? a.drop.inv_keep : 0.f;
+    a.cat[(long)c * a.sCatc + (long)(b0 + r) * a.sCatr + col] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_cnn_fwd(AflCnnTowers a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const AflCnnBranch& br = a.br[blockIdx.y];
+  if ((int)blockIdx.x >= br.ntiles) return;
+  if (br.L == 16)
+    cnn_fwd_tile<16>(a, br, smem);
+  else
+    cnn_fwd_tile<7>(a, br, smem);
+}
+
+// ------------------------------------------------------------------------------------------ backward
+constexpr int B_LD3 = 136, B_LC2 = 196, B_LD2 = 72, B_LC1 = 100;
+constexpr int B_DH3 = 0;                              // [64][136] bf16   17408
+constexpr int B_DC2 = B_DH3 + MT * B_LD3 * 2;         // [64][196] f32    50176
+constexpr int B_DH2 = B_DC2 + MT * B_LC2 * 4;         // [64][72] bf16    9216
+constexpr int B_DC1 = B_DC2;                          // [64][100] f32 (after dc2 is consumed)
+constexpr int B_TOTAL = B_DH2 + MT * B_LD2 * 2;       // 76800
+static_assert(B_TOTAL <= 80 * 1024, "cnn bwd LDS: two workgroups per CU");
+
+template <int L>
+__device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsigned char* smem) {
+  const int tile = blockIdx.x, c = blockIdx.z;
+  const int b0 = tile * br.R, nb = min(br.R, a.B - b0), M = nb * L;
+  const long row0 = (long)b0 * L, cbase = (long)c * a.B * L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned short* dh3b = (unsigned short*)(smem + B_DH3);
+  float* dc2 = (float*)(smem + B_DC2);
+  unsigned short* dh2b = (unsigned short*)(smem + B_DH2);
+  float* dc1 = (float*)(smem + B_DC1);
+  const unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
+  // dh3 = relu'(h3) * pool'(dropout'(dcat))
+  const bool dr = a.drop.thr16 != 0;
+  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+  for (int e = tid; e < MT * 128; e += NT) {
+    const int m = e >> 7, ch = e & 127;
+    float sum = 0.f;
+    if (m < M) {
+      const int r = m / L, l = m - r * L, b = b0 + r;
+      const float* dcr = a.dcat + (long)c * a.sCatc + (long)b * a.sCatr;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int lo = bin_lo(p, L), hi = bin_hi(p, L);
+        if (l >= lo && l < hi) {
+          const int col = br.col0 + ch * 4 + p;
+          float g = dcr[col] / (float)(hi - lo);
+          if (dr) g *= afl_keep(key, br.layer, (uint32_t)b, (uint32_t)col, a.drop.thr16) ? a.drop.inv_keep : 0.f;
+          sum += g;
+        }
+      }
+      if (!(br.h3[(cbase + row0 + m) * 128 + ch] > 0.f)) sum = 0.f;
+      br.dh3[(cbase + row0 + m) * 128 + ch] = sum;
+    }
+    dh3b[m * B_LD3 + ch] = bfu(sum);
+  }
+  __syncthreads();
+  // dcols2 = dh3 . W3 : [64 x 128] . (W3^T image [192 x 128])^T -> [64 x 192]; 48 tiles, 6 per wave
+  {
+    const int mt = (wave & 3) * 16, nb0 = (wave >> 2) * 6;
+    f4v acc[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 128; k0 += 32) {
+      const s8v af = frag(dh3b, B_LD3, mt, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[j] = mfma32(af, gfrag(img + WI_W3T, 128, (nb0 + j) * 16, k0, lane), acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dc2[(mt + 4 * (lane >> 4) + e) * B_LC2 + (nb0 + j) * 16 + (lane & 15)] = acc[j][e];
+  }
+  __syncthreads();
+  // col2im + relu'(h2) -> dh2
+  for (int e = tid; e < MT * 64; e += NT) {
+    const int m = e >> 6, ci = e & 63;
+    float sum = 0.f;
+    if (m < M) {
+      const int l = m % L;
+      if (l < L - 1) sum += dc2[(m + 1) * B_LC2 + ci * 3 + 0];  // output l+1, tap 0 reads input l
+      sum += dc2[m * B_LC2 + ci * 3 + 1];
+      if (l > 0) sum += dc2[(m - 1) * B_LC2 + ci * 3 + 2];
+      if (!(br.h2[(cbase + row0 + m) * 64 + ci] > 0.f)) sum = 0.f;
+      br.dh2[(cbase + row0 + m) * 64 + ci] = sum;
+    }
+    dh2b[m * B_LD2 + ci] = bfu(sum);
+  }
+  __syncthreads();
+  // dcols1 = dh2 . W2 : [64 x 64] . (W2^T image [96 x 64])^T -> [64 x 96]; 24 tiles, 3 per wave
+  {
+    const int mt = (wave & 3) * 16, nb0 = (wave >> 2) * 3;
+    f4v acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 64; k0 += 32) {
+      const s8v af = frag(dh2b, B_LD2, mt, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma32(af, gfrag(img + WI_W2T, 64, (nb0 + j) * 16, k0, lane), acc[j]);
+    }
+    __syncthreads();  // dc1 overwrites dc2 (read by other waves' col2im above: already fenced) — keep order
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dc1[(mt + 4 * (lane >> 4) + e) * B_LC1 + (nb0 + j) * 16 + (lane & 15)] = acc[j][e];
+  }
+  __syncthreads();
+  for (int e = tid; e < MT * 32; e += NT) {
+    const int m = e >> 5, ci = e & 31;
+    if (m >= M) continue;
+    const int l = m % L;
+    float sum = dc1[m * B_LC1 + ci * 3 + 1];
+    if (l < L - 1) sum += dc1[(m + 1) * B_LC1 + ci * 3 + 0];
+    if (l > 0) sum += dc1[(m - 1) * B_LC1 + ci * 3 + 2];
+    if (!(br.h1[(cbase + row0 + m) * 32 + ci] > 0.f)) sum = 0.f;
+    br.dh1[(cbase + row0 + m) * 32 + ci] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_cnn_bwd(AflCnnTowers a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const AflCnnBranch& br = a.br[blockIdx.y];
+  if ((int)blockIdx.x >= br.ntiles) return;
+  if (br.L == 16)
+    cnn_bwd_tile<16>(a, br, smem);
+  else
+    cnn_bwd_tile<7>(a, br, smem);
+}
+
+// ------------------------------------------------------------------------------------------ weight grads
+constexpr int DW_T = 64, DW_K = 32, DW_LD = 40;
+
+template <int L>
+__device__ void conv_dw_tile(const AflConvDw& a, const AflConvDwJob& J, int t, unsigned short* As, unsigned short* Bs,
+                             float (*bred)[DW_T]) {
+  const int K = 3 * J.Cin;
+  const int tk = (K + DW_T - 1) / DW_T;
+  const int o0 = (t / tk) * DW_T, k0t = (t % tk) * DW_T;
+  const int c = blockIdx.z;
+  const int BL = a.B * L;
+  const int chunk = ((BL + a.splitk - 1) / a.splitk + DW_K - 1) / DW_K * DW_K;
+  const int mb = blockIdx.y * chunk, me = min(BL, mb + chunk);
+  if (mb >= me) return;
+  const float* dh = J.dh + (long)c * BL * J.Cout;
+  const float* hp = J.hp + (long)c * BL * J.Cin;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int so = tid & 63, sm0 = (tid >> 6) * 8;  // staging: row (o or kk) and 8 consecutive positions
+  const bool bias = k0t == 0 && J.gb != nullptr;
+  const int kk = k0t + so, ci = kk / 3, jj = kk - ci * 3;
+  const bool ook = o0 + so < J.Cout, kok = kk < K;
+  float bsum = 0.f;
+  f4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  // software pipeline: the next k-step's global loads are in flight during this step's MFMAs
+  float va[8], vb[8];
+  auto load = [&](int m0) {
+    int l = (m0 + sm0) % L;  // position within the sample, advanced incrementally
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + sm0 + i;
+      const bool mok = m < me;
+      va[i] = (mok && ook) ? dh[(long)m * J.Cout + o0 + so] : 0.f;
+      const int lj = l + jj - 1;
+      vb[i] = (mok && kok && lj >= 0 && lj < L) ? hp[(long)(m + jj - 1) * J.Cin + ci] : 0.f;
+      l = (l == L - 1) ? 0 : l + 1;
+    }
+  };
+  load(mb);
+  for (int m0 = mb; m0 < me; m0 += DW_K) {
+    s8v pa, pb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pa[i] = (short)bfu(va[i]);
+      pb[i] = (short)bfu(vb[i]);
+      bsum += va[i];
+    }
+    __syncthreads();
+    *(s8v*)(As + so * DW_LD + sm0) = pa;
+    *(s8v*)(Bs + so * DW_LD + sm0) = pb;
+    __syncthreads();
+    if (m0 + DW_K < me) load(m0 + DW_K);
+    const s8v a0 = frag(As, DW_LD, wm, 0, lane), a1 = frag(As, DW_LD, wm + 16, 0, lane);
+    const s8v b0 = frag(Bs, DW_LD, wn, 0, lane), b1 = frag(Bs, DW_LD, wn + 16, 0, lane);
+    acc[0][0] = mfma32(a0, b0, acc[0][0]);
+    acc[0][1] = mfma32(a0, b1, acc[0][1]);
+    acc[1][0] = mfma32(a1, b0, acc[1][0]);
+    acc[1][1] = mfma32(a1, b1, acc[1][1]);
+  }
+  float* gW = J.gW + (long)c * a.sGc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o0 + wm + 16 * i + 4 * (lane >> 4) + e;
+        const int k = k0t + wn + 16 * j + (lane & 15);
+        if (o < J.Cout && k < K) atomicAdd(gW + (long)o * K + k, acc[i][j][e]);
+      }
+  if (bias) {
+    bred[tid >> 6][so] = bsum;
+    __syncthreads();
+    if (tid < DW_T && o0 + tid < J.Cout)
+      atomicAdd(J.gb + (long)c * a.sGc + o0 + tid, (bred[0][tid] + bred[1][tid]) + (bred[2][tid] + bred[3][tid]));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_conv_dw(AflConvDw a) {
+  __shared__ __attribute__((aligned(16))) unsigned short As[DW_T * DW_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[DW_T * DW_LD];
+  __shared__ float bred[4][DW_T];
+  int jb = 0;
+  while (jb + 1 < a.njobs && (int)blockIdx.x >= a.job[jb + 1].tile_base) ++jb;
+  const AflConvDwJob& J = a.job[jb];
+  const int t = blockIdx.x - J.tile_base;
+  if (J.L == 16)
+    conv_dw_tile<16>(a, J, t, As, Bs, bred);
+  else if (J.L == 7)
+    conv_dw_tile<7>(a, J, t, As, Bs, bred);
+}
+
+// ------------------------------------------------------------------------------------------ MLP head
+// One workgroup per client: fc2 -> ReLU -> fc3 -> ReLU -> output -> sigmoid-BCE (mean over the step's
+// rows, NaN abort, per-epoch loss) -> every head gradient (fc2 / fc3 / output weights and biases, fc1
+// bias) -> d(fc1 pre-activation) for the fc1 input-gradient / weight-gradient GEMMs.
+// Weight gradients dW = dY^T X read both operands transposed from the [b][feature] LDS images with
+// ds_read_b64_tr_b16; input gradients dY . W read W^T the same way.
+#define LDS_AS __attribute__((address_space(3)))
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s8v col_frag(const unsigned short* S, int ld, int k0, int m0, int lane) {
+  // A[m][k] = S[k][m] (S row-major [k rows][m cols]); two transposed 4x16 reads per 16-lane group
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const unsigned short* a1 = S + (k0 + 8 * g + q) * ld + m0 + 4 * p;
+  const unsigned short* a2 = a1 + 4 * ld;
+  const s4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a1);
+  const s4v r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a2);
+  s8v r;
+  r[0] = r1[0]; r[1] = r1[1]; r[2] = r1[2]; r[3] = r1[3];
+  r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
+  return r;
+}
+
+constexpr int H_L1 = 136, H_L2 = 72, H_L3 = 40, H_F3 = 33;
+constexpr int H_F1S = 0;                          // f1   [128][136] bf16
+constexpr int H_W2S = H_F1S + 128 * H_L1 * 2;     // W2   [64][136] bf16
+constexpr int H_F2S = H_W2S + 64 * H_L1 * 2;      // f2   [128][72] bf16
+constexpr int H_W3S = H_F2S + 128 * H_L2 * 2;     // W3   [32][72] bf16
+constexpr int H_F3F = H_W3S + 32 * H_L2 * 2;      // f3   [128][33] f32
+constexpr int H_D3S = H_F3F + 128 * H_F3 * 4;     // d3   [128][40] bf16
+constexpr int H_D2S = H_D3S + 128 * H_L3 * 2;     // d2   [128][72] bf16
+constexpr int H_DZ = H_D2S + 128 * H_L2 * 2;      // dz   [128] f32
+constexpr int H_GB = H_DZ + 128 * 4;              // gb2 [64] | gb1 [128] f32
+constexpr int H_RED = H_GB + 192 * 4;             // [8] f32
+constexpr int H_TOTAL = H_RED + 8 * 4;
+static_assert(H_TOTAL <= 160 * 1024, "cnn head LDS");
+
+__device__ __forceinline__ float wsum(float x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+constexpr int HNT = 512;  // 8 waves
+
+__global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned short* f1s = (unsigned short*)(smem + H_F1S);
+  unsigned short* W2s = (unsigned short*)(smem + H_W2S);
+  unsigned short* f2s = (unsigned short*)(smem + H_F2S);
+  unsigned short* W3s = (unsigned short*)(smem + H_W3S);
+  float* f3f = (float*)(smem + H_F3F);
+  unsigned short* d3s = (unsigned short*)(smem + H_D3S);
+  unsigned short* d2s = (unsigned short*)(smem + H_D2S);
+  float* dz = (float*)(smem + H_DZ);
+  float* gb2 = (float*)(smem + H_GB);
+  float* gb1 = gb2 + 64;
+  float* red = (float*)(smem + H_RED);
+  const int c = blockIdx.x, B = h.B;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long wo = (long)c * h.sWc, go = (long)c * h.sGc;
+  // f1 = relu(z1 + b1) from the split-K fc1 pre-activation (16-B loads)
+  const float* z1 = h.f1 + (long)c * B * 128;
+  for (int e = tid; e < 128 * 32; e += HNT) {
+    const int b = e >> 5, i = 4 * (e & 31);
+    f4v v = f4v{0.f, 0.f, 0.f, 0.f};
+    if (b < B) v = *(const f4v*)(z1 + (long)b * 128 + i);
+    unsigned short* d = f1s + b * H_L1 + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = bfu(b < B ? relu(v[q] + h.b1[wo + i + q]) : 0.f);
+  }
+  // fc2 / fc3 weight images (bf16, 16-B loads)
+  {
+    const unsigned short* img = h.wimg + (long)c * WI_HEAD;
+    for (int e = tid; e < 64 * 16; e += HNT) {
+      const int r = e >> 4, k = 8 * (e & 15);
+      *(s8v*)(W2s + r * H_L1 + k) = *(const s8v*)(img + r * 128 + k);
+    }
+    for (int e = tid; e < 32 * 8; e += HNT) {
+      const int r = e >> 3, k = 8 * (e & 7);
+      *(s8v*)(W3s + r * H_L2 + k) = *(const s8v*)(img + 64 * 128 + r * 64 + k);
+    }
+  }
+  for (int e = tid; e < 192; e += HNT) gb2[e] = 0.f;
+  __syncthreads();
+  // fc2: [128 x 128] . W2^T -> [128 x 64]; wave -> m-tile w, n-tiles 0..3
+  {
+    const int m0 = wave * 16;
+    f4v acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 128; k0 += 32) {
+      const s8v af = frag(f1s, H_L1, m0, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = mfma32(af, frag(W2s, H_L1, 16 * j, k0, lane), acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = 16 * j + (lane & 15);
+      const float bn = h.b2[wo + n];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) f2s[(m0 + 4 * (lane >> 4) + e) * H_L2 + n] = bfu(relu(acc[j][e] + bn));
+    }
+  }
+  __syncthreads();
+  // fc3: [128 x 64] . W3^T -> [128 x 32]; wave -> m-tile w, n-tiles 0, 1
+  {
+    const int m0 = wave * 16;
+    f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k0 = 0; k0 < 64; k0 += 32) {
+      const s8v af = frag(f2s, H_L2, m0, k0, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = mfma32(af, frag(W3s, H_L2, 16 * j, k0, lane), acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * j + (lane & 15);
+      const float bn = h.b3[wo + n];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) f3f[(m0 + 4 * (lane >> 4) + e) * H_F3 + n] = relu(acc[j][e] + bn);
+    }
+  }
+  __syncthreads();
+  // output logit + sigmoid-BCE (same arithmetic as k_bce)
+  const int s = h.stepctl ? *h.stepctl : 0;
+  const int bs = s < h.S ? h.bsz[(long)s * h.C + c] : 0;
+  const bool act = bs >= 2 && h.failed[c] == 0;
+  float zb = 0.f, lb = 0.f;
+  if (tid < 128) {
+    float acc = h.bo[wo];
+    for (int j = 0; j < 32; ++j) acc += f3f[tid * H_F3 + j] * h.Wo[wo + j];
+    zb = acc;
+    if (h.z && tid < B) h.z[(long)c * B + tid] = zb;
+    if (act && tid < bs) {
+      const float p = 1.f / (1.f + expf(-zb));
+      const float t = h.y[(long)c * B + tid];
+      lb = -(t * fmaxf(logf(p), -100.f) + (1.f - t) * fmaxf(log1pf(-p), -100.f));
+      if (p != p) lb = p;
+    }
+  }
+  lb = wsum(lb);
+  if (lane == 0) red[wave] = lb;
+  __syncthreads();
+  const float loss = ((red[0] + red[1]) + (red[2] + red[3])) / (float)max(bs, 1);
+  const bool nan = act && (loss != loss);
+  if (tid < 128) {
+    float g = 0.f;
+    if (act && !nan && tid < bs) {
+      const float p = 1.f / (1.f + expf(-zb));
+      const float w = p * (1.f - p);
+      g = (p - h.y[(long)c * B + tid]) / fmaxf(w, 1e-12f) * w / (float)bs;
+    }
+    dz[tid] = g;
+  }
+  if (tid == 0 && act) {
+    if (nan)
+      h.failed[c] = 1;
+    else
+      h.losses[(long)c * h.E + h.epoch[(long)s * h.C + c]] += loss / (float)h.nb[c];
+  }
+  __syncthreads();
+  // d3 = dz wo^T * relu'(f3); output-layer and fc3-bias gradients
+  for (int e = tid; e < 128 * 32; e += HNT) {
+    const int b = e >> 5, j = e & 31;
+    d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * h.Wo[wo + j] : 0.f);
+  }
+  if (tid < 32) {
+    float a = 0.f, w = 0.f;
+    for (int b = 0; b < 128; ++b) {
+      a += f3f[b * H_F3 + tid] > 0.f ? dz[b] : 0.f;
+      w += dz[b] * f3f[b * H_F3 + tid];
+    }
+    h.gb3[go + tid] = a * h.Wo[wo + tid];
+    h.gWo[go + tid] = w;
+  } else if (tid == 64) {
+    float a = 0.f;
+    for (int b = 0; b < 128; ++b) a += dz[b];
+    h.gbo[go] = a;
+  }
+  __syncthreads();
+  // dW3 [32 x 64] = d3^T f2 ; wave -> o-tile (w >> 2), i-tile (w & 3)
+  {
+    const int o0 = (wave >> 2) * 16, i0 = (wave & 3) * 16;
+    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 128; k0 += 32) acc = mfma32(col_frag(d3s, H_L3, k0, o0, lane), col_frag(f2s, H_L2, k0, i0, lane), acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) h.gW3[go + (long)(o0 + 4 * (lane >> 4) + e) * 64 + i0 + (lane & 15)] = acc[e];
+  }
+  // d2 = d3 . W3 * relu'(f2) -> [128 x 64]; wave -> m-tile w; column sums -> gb2
+  {
+    const int m0 = wave * 16;
+    const s8v af = frag(d3s, H_L3, m0, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f4v acc = mfma32(af, col_frag(W3s, H_L2, 0, 16 * j, lane), f4v{0.f, 0.f, 0.f, 0.f});
+      const int n = 16 * j + (lane & 15);
+      float cs = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 4 * (lane >> 4) + e;
+        const unsigned short fb = f2s[m * H_L2 + n];
+        const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;  // relu'(f2): bf16 > 0
+        d2s[m * H_L2 + n] = bfu(v);
+        cs += v;
+      }
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (lane < 16) atomicAdd(gb2 + n, cs);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) h.gb2[go + tid] = gb2[tid];
+  // dW2 [64 x 128] = d2^T f1 ; wave -> o-tile (w >> 1), i-tiles 4 (w & 1) + 0..3
+  {
+    const int o0 = (wave >> 1) * 16, ib = (wave & 1) * 4;
+    f4v acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 128; k0 += 32) {
+      const s8v af = col_frag(d2s, H_L2, k0, o0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = mfma32(af, col_frag(f1s, H_L1, k0, 16 * (ib + j), lane), acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        h.gW2[go + (long)(o0 + 4 * (lane >> 4) + e) * 128 + 16 * (ib + j) + (lane & 15)] = acc[j][e];
+  }
+  // d1 = d2 . W2 * relu'(f1) -> [128 x 128] (global, rows < B); wave -> m-tile w; column sums -> gb1
+  float* d1 = h.d1 + (long)c * B * 128;
+  {
+    const int m0 = wave * 16;
+    const s8v a0 = frag(d2s, H_L2, m0, 0, lane), a1 = frag(d2s, H_L2, m0, 32, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f4v acc = mfma32(a0, col_frag(W2s, H_L1, 0, 16 * j, lane), f4v{0.f, 0.f, 0.f, 0.f});
+      acc = mfma32(a1, col_frag(W2s, H_L1, 32, 16 * j, lane), acc);
+      const int n = 16 * j + (lane & 15);
+      float cs = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 4 * (lane >> 4) + e;
+        const unsigned short fb = f1s[m * H_L1 + n];
+        const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
+        if (m < B) d1[(long)m * 128 + n] = v;
+        cs += v;
+      }
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (lane < 16) atomicAdd(gb1 + n, cs);
+    }
+  }
+  __syncthreads();
+  if (tid < 128) h.gb1[go + tid] = gb1[tid];
+}
+
+}  // namespace
+
+int afl_cnn_towers_fwd(const AflCnnTowers& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cnn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             F_TOTAL);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int nt = max(a.br[0].ntiles, a.br[1].ntiles);
+  hipLaunchKernelGGL(k_cnn_wimg, dim3(8, 2, a.C), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_cnn_fwd, dim3(nt, 2, a.C), dim3(NT), F_TOTAL, s, a);
+  return (int)hipGetLastError();
+}
+
+long afl_cnn_wimg_ushorts(int C) { return (long)C * (2 * WI_SIZE + WI_HEAD); }
+
+int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cnn_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             B_TOTAL);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int nt = max(a.br[0].ntiles, a.br[1].ntiles);
+  hipLaunchKernelGGL(k_cnn_bwd, dim3(nt, 2, a.C), dim3(NT), B_TOTAL, s, a);
+  return (int)hipGetLastError();
+}
+
+int afl_conv_dw(const AflConvDw& a, hipStream_t s) {
+  if (a.njobs <= 0) return 0;
+  hipLaunchKernelGGL(k_conv_dw, dim3(a.total_tiles, a.splitk, a.C), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int afl_cnn_head(const AflCnnHead& h, hipStream_t s) {
+  if (h.B > 128 || h.B < 1) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cnn_head, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             H_TOTAL);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_cnn_head, dim3(h.C), dim3(HNT), H_TOTAL, s, h);
+  return (int)hipGetLastError();
+}

@@ -194,6 +194,221 @@ void pool4_bwd(torch::Tensor dout, int64_t col0, torch::Tensor h, int64_t B, int
      "pool4_bwd");
 }
 
+// ---- fused CNNModel towers (cnn.hip) ----
+// t = [x, W1, b1, W2, b2, W3, b3, h1, h2, h3, dh1, dh2, dh3]; meta = [L, col0, layer]
+AflCnnBranch cnn_branch(const std::vector<torch::Tensor>& t, const std::vector<int64_t>& meta, int64_t B,
+                        long& sWc, bool bwd) {
+  TORCH_CHECK(t.size() == 13 && meta.size() == 3, "cnn tower: 13 tensors and [L, col0, layer] expected");
+  AflCnnBranch br{};
+  const int L = (int)meta[0];
+  TORCH_CHECK(L >= 2 && L <= 64, "cnn tower: 2 <= L <= 64");
+  const auto& x = t[0];
+  dev(x, "x");
+  const long C = x.size(0);
+  TORCH_CHECK(x.dim() == 3 && x.size(1) == B && x.size(2) == L && x.stride(2) == 1 && x.stride(1) == L,
+              "cnn tower: x must be [C, B, L] with contiguous samples");
+  br.x = x.data_ptr<float>();
+  br.sXc = x.stride(0);
+  const int shp[6][2] = {{32, 3}, {32, 1}, {64, 96}, {64, 1}, {128, 192}, {128, 1}};
+  const float* wp[6];
+  for (int i = 0; i < 6; ++i) {
+    const auto& w = t[1 + i];
+    dev(w, "cnn weight");
+    TORCH_CHECK(w.size(0) == C && w.stride(-1) == 1, "cnn weight: [C, ...] with contiguous rows");
+    TORCH_CHECK(w.numel() == C * shp[i][0] * shp[i][1], "cnn weight: unexpected size");
+    if (w.dim() == 3) TORCH_CHECK(w.stride(1) == w.size(2), "cnn weight rows must be dense");
+    if (i == 0) sWc = C > 1 ? w.stride(0) : 0;
+    TORCH_CHECK(C == 1 || w.stride(0) == sWc, "cnn weights must share the client stride (views of one arena)");
+    wp[i] = w.data_ptr<float>();
+  }
+  br.W1 = wp[0]; br.b1 = wp[1]; br.W2 = wp[2]; br.b2 = wp[3]; br.W3 = wp[4]; br.b3 = wp[5];
+  const int chs[3] = {32, 64, 128};
+  float* hp[3];
+  float* dp[3];
+  for (int i = 0; i < 3; ++i) {
+    dense(t[7 + i], "h");
+    TORCH_CHECK(t[7 + i].numel() == C * B * L * chs[i], "cnn tower: h buffer size");
+    hp[i] = t[7 + i].data_ptr<float>();
+    dp[i] = nullptr;
+    if (bwd) {
+      dense(t[10 + i], "dh");
+      TORCH_CHECK(t[10 + i].numel() == C * B * L * chs[i], "cnn tower: dh buffer size");
+      dp[i] = t[10 + i].data_ptr<float>();
+    }
+  }
+  br.h1 = hp[0]; br.h2 = hp[1]; br.h3 = hp[2];
+  br.dh1 = dp[0]; br.dh2 = dp[1]; br.dh3 = dp[2];
+  br.L = L;
+  br.R = 64 / L;
+  br.ntiles = (int)((B + br.R - 1) / br.R);
+  br.col0 = (int)meta[1];
+  br.layer = (uint32_t)meta[2];
+  TORCH_CHECK(br.col0 >= 0 && br.col0 + 512 <= 1024, "cnn tower: concat slice out of range");
+  return br;
+}
+
+AflCnnTowers cnn_towers(const std::vector<torch::Tensor>& t0, const std::vector<torch::Tensor>& t1,
+                        const std::vector<int64_t>& m0, const std::vector<int64_t>& m1, int64_t B, torch::Tensor cat,
+                        const c10::optional<torch::Tensor>& seeds, const c10::optional<torch::Tensor>& stepctl,
+                        double p, bool bwd, torch::Tensor wimg) {
+  AflCnnTowers a{};
+  long s0 = 0, s1 = 0;
+  a.br[0] = cnn_branch(t0, m0, B, s0, bwd);
+  a.br[1] = cnn_branch(t1, m1, B, s1, bwd);
+  TORCH_CHECK(s0 == s1, "both towers' weights must be views of one arena");
+  a.sWc = s0;
+  view3(cat, "cat");
+  TORCH_CHECK(cat.size(1) == B && cat.size(2) == 1024 && cat.stride(2) == 1, "cat must be [C, B, 1024]");
+  a.C = (int)t0[0].size(0);
+  TORCH_CHECK(cat.size(0) == a.C && t1[0].size(0) == a.C, "client count mismatch");
+  a.B = (int)B;
+  a.cat = cat.data_ptr<float>();
+  a.dcat = a.cat;
+  a.sCatc = cat.stride(0);
+  a.sCatr = cat.stride(1);
+  a.drop = make_drop(seeds, stepctl, 0, p);
+  dense(wimg, "wimg", torch::kInt16);
+  TORCH_CHECK(wimg.numel() >= afl_cnn_wimg_ushorts(a.C), "cnn towers: weight-image buffer too small");
+  a.wimg = (unsigned short*)wimg.data_ptr<int16_t>();
+  return a;
+}
+
+void cnn_towers_fwd(std::vector<torch::Tensor> t0, std::vector<torch::Tensor> t1, std::vector<int64_t> m0,
+                    std::vector<int64_t> m1, int64_t B, torch::Tensor cat, c10::optional<torch::Tensor> seeds,
+                    c10::optional<torch::Tensor> stepctl, double p, torch::Tensor wimg, std::vector<torch::Tensor> head) {
+  AflCnnTowers a = cnn_towers(t0, t1, m0, m1, B, cat, seeds, stepctl, p, false, wimg);
+  a.W2h = a.W3h = nullptr;
+  if (!head.empty()) {  // fc2 / fc3 weight views: their bf16 images feed k_cnn_head
+    TORCH_CHECK(head.size() == 2, "cnn towers: head = [fc2.weight, fc3.weight]");
+    const long hn[2] = {64 * 128, 32 * 64};
+    for (int i = 0; i < 2; ++i) {
+      dev(head[i], "head weight");
+      TORCH_CHECK(head[i].dim() == 3 && head[i].size(0) == a.C && head[i].numel() == a.C * hn[i] &&
+                      head[i].stride(2) == 1 && head[i].stride(1) == head[i].size(2) &&
+                      (a.C == 1 || head[i].stride(0) == a.sWc),
+                  "cnn towers: head weights must be [C, out, in] views of the same arena");
+    }
+    a.W2h = head[0].data_ptr<float>();
+    a.W3h = head[1].data_ptr<float>();
+  }
+  ok(afl_cnn_towers_fwd(a, cur()), "cnn_towers_fwd");
+}
+
+void cnn_towers_bwd(std::vector<torch::Tensor> t0, std::vector<torch::Tensor> t1, std::vector<int64_t> m0,
+                    std::vector<int64_t> m1, int64_t B, torch::Tensor dcat, c10::optional<torch::Tensor> seeds,
+                    c10::optional<torch::Tensor> stepctl, double p, torch::Tensor wimg) {
+  const AflCnnTowers a = cnn_towers(t0, t1, m0, m1, B, dcat, seeds, stepctl, p, true, wimg);
+  ok(afl_cnn_towers_bwd(a, cur()), "cnn_towers_bwd");
+}
+
+// conv weight/bias grads: job k = (dh [C, B*L, Cout], hp [C, B*L, Cin], gW [C, Cout, 3*Cin] view, gb [C, Cout] view)
+void conv_dw(std::vector<torch::Tensor> dh, std::vector<torch::Tensor> hp, std::vector<torch::Tensor> gW,
+             std::vector<torch::Tensor> gb, std::vector<int64_t> L, int64_t B, int64_t splitk) {
+  const size_t n = dh.size();
+  TORCH_CHECK(n >= 1 && n <= 6 && hp.size() == n && gW.size() == n && gb.size() == n && L.size() == n,
+              "conv_dw: 1..6 jobs");
+  AflConvDw a{};
+  a.njobs = (int)n;
+  a.B = (int)B;
+  a.splitk = (int)std::max<int64_t>(1, splitk);
+  a.C = (int)dh[0].size(0);
+  int tiles = 0;
+  for (size_t k = 0; k < n; ++k) {
+    dense(dh[k], "dh");
+    dense(hp[k], "hp");
+    view3(gW[k], "gW");
+    dev(gb[k], "gb");
+    const int Cout = (int)gW[k].size(1), K = (int)gW[k].size(2);
+    TORCH_CHECK(K % 3 == 0, "conv_dw: gW must be [C, Cout, 3*Cin]");
+    const int Cin = K / 3;
+    TORCH_CHECK(gW[k].stride(2) == 1 && gW[k].stride(1) == K, "conv_dw: gW rows dense");
+    TORCH_CHECK(dh[k].numel() == (long)a.C * B * L[k] * Cout && hp[k].numel() == (long)a.C * B * L[k] * Cin,
+                "conv_dw: activation sizes");
+    TORCH_CHECK(gb[k].size(0) == a.C && gb[k].size(-1) == Cout && gb[k].stride(-1) == 1, "conv_dw: gb [C, Cout]");
+    if (k == 0) a.sGc = a.C > 1 ? gW[k].stride(0) : 0;
+    TORCH_CHECK(a.C == 1 || (gW[k].stride(0) == a.sGc && gb[k].stride(0) == a.sGc),
+                "conv_dw: grads must be views of one arena");
+    AflConvDwJob& j = a.job[k];
+    j.dh = dh[k].data_ptr<float>();
+    j.hp = hp[k].data_ptr<float>();
+    j.gW = gW[k].data_ptr<float>();
+    j.gb = gb[k].data_ptr<float>();
+    j.Cin = Cin;
+    j.Cout = Cout;
+    j.L = (int)L[k];
+    j.tile_base = tiles;
+    tiles += ((Cout + 63) / 64) * ((K + 63) / 64);
+  }
+  a.total_tiles = tiles;
+  ok(afl_conv_dw(a, cur()), "conv_dw");
+}
+
+// CNNModel MLP head fc2 -> fc3 -> output + BCE + backward (cnn.hip:k_cnn_head)
+// w = [W2, b2, W3, b3, Wo, bo] parameter views, g = [gW2, gb2, gW3, gb3, gWo, gbo, gb1] gradient views
+void cnn_head(torch::Tensor f1, torch::Tensor y, std::vector<torch::Tensor> w, std::vector<torch::Tensor> g,
+              torch::Tensor d1, c10::optional<torch::Tensor> z, torch::Tensor bsz, torch::Tensor epoch, torch::Tensor nb,
+              torch::Tensor stepctl, torch::Tensor failed, torch::Tensor losses, torch::Tensor wimg) {
+  dense(f1, "f1");
+  dense(y, "y");
+  dense(d1, "d1");
+  TORCH_CHECK(w.size() == 7 && g.size() == 7, "cnn_head: 7 parameters and 7 gradients");
+  const int C = f1.size(0), B = f1.size(1);
+  TORCH_CHECK(f1.dim() == 3 && f1.size(2) == 128 && B <= 128, "cnn_head: f1 must be [C, B<=128, 128]");
+  TORCH_CHECK(y.numel() == (long)C * B && d1.numel() == (long)C * B * 128, "cnn_head: y / d1 sizes");
+  const long wn[7] = {64 * 128, 64, 32 * 64, 32, 32, 1, 128};
+  const long gn[7] = {64 * 128, 64, 32 * 64, 32, 32, 1, 128};
+  AflCnnHead h{};
+  const float* wp[7];
+  float* gp[7];
+  for (int i = 0; i < 7; ++i) {
+    dev(w[i], "head weight");
+    TORCH_CHECK(w[i].size(0) == C && w[i].numel() == C * wn[i] && w[i].stride(-1) == 1, "cnn_head: weight view");
+    if (i == 0) h.sWc = C > 1 ? w[i].stride(0) : 0;
+    TORCH_CHECK(C == 1 || w[i].stride(0) == h.sWc, "cnn_head: weights must be views of one arena");
+    wp[i] = w[i].data_ptr<float>();
+  }
+  for (int i = 0; i < 7; ++i) {
+    dev(g[i], "head grad");
+    TORCH_CHECK(g[i].size(0) == C && g[i].numel() == C * gn[i] && g[i].stride(-1) == 1, "cnn_head: grad view");
+    if (i == 0) h.sGc = C > 1 ? g[i].stride(0) : 0;
+    TORCH_CHECK(C == 1 || g[i].stride(0) == h.sGc, "cnn_head: grads must be views of one arena");
+    gp[i] = g[i].data_ptr<float>();
+  }
+  for (int i : {0, 2}) TORCH_CHECK(w[i].dim() == 3 && w[i].stride(1) == w[i].size(2), "cnn_head: dense weight rows");
+  h.f1 = f1.data_ptr<float>();
+  h.y = y.data_ptr<float>();
+  h.W2 = wp[0]; h.b2 = wp[1]; h.W3 = wp[2]; h.b3 = wp[3]; h.Wo = wp[4]; h.bo = wp[5]; h.b1 = wp[6];
+  dense(wimg, "wimg", torch::kInt16);
+  TORCH_CHECK(wimg.numel() >= afl_cnn_wimg_ushorts(C), "cnn_head: weight-image buffer too small");
+  h.wimg = (const unsigned short*)wimg.data_ptr<int16_t>() + (afl_cnn_wimg_ushorts(C) - (long)C * (64 * 128 + 32 * 64));
+  h.gW2 = gp[0]; h.gb2 = gp[1]; h.gW3 = gp[2]; h.gb3 = gp[3]; h.gWo = gp[4]; h.gbo = gp[5]; h.gb1 = gp[6];
+  h.d1 = d1.data_ptr<float>();
+  h.z = nullptr;
+  if (z.has_value() && z->defined()) {
+    dense(*z, "z");
+    TORCH_CHECK(z->numel() == (long)C * B, "cnn_head: z size");
+    h.z = z->data_ptr<float>();
+  }
+  dense(bsz, "bsz", torch::kInt32);
+  dense(epoch, "epoch", torch::kInt32);
+  dense(nb, "nb", torch::kInt32);
+  dense(stepctl, "stepctl", torch::kInt32);
+  dense(failed, "failed", torch::kInt32);
+  dense(losses, "losses");
+  TORCH_CHECK(bsz.dim() == 2 && bsz.size(1) == C, "cnn_head: bsz [S, C]");
+  h.bsz = bsz.data_ptr<int>();
+  h.epoch = epoch.data_ptr<int>();
+  h.nb = nb.data_ptr<int>();
+  h.stepctl = stepctl.data_ptr<int>();
+  h.failed = failed.data_ptr<int>();
+  h.losses = losses.data_ptr<float>();
+  h.S = bsz.size(0);
+  h.E = losses.size(1);
+  h.C = C;
+  h.B = B;
+  ok(afl_cnn_head(h, cur()), "cnn_head");
+}
+
 void ln_fwd(torch::Tensor x, c10::optional<torch::Tensor> a, c10::optional<torch::Tensor> s, torch::Tensor y,
             torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, c10::optional<torch::Tensor> seeds,
             c10::optional<torch::Tensor> stepctl, int64_t layer_a, double p_a, int64_t layer_o, double p_o) {
@@ -419,6 +634,11 @@ void afl_register_layers(pybind11::module& m) {
   m.def("im2col3", &im2col3);
   m.def("col2im3", &col2im3);
   m.def("pool4_fwd", &pool4_fwd);
+  m.def("cnn_towers_fwd", &cnn_towers_fwd);
+  m.def("cnn_towers_bwd", &cnn_towers_bwd);
+  m.def("conv_dw", &conv_dw);
+  m.def("cnn_head", &cnn_head);
+  m.def("cnn_wimg_size", &afl_cnn_wimg_ushorts);
   m.def("pool4_bwd", &pool4_bwd);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

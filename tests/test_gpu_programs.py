@@ -197,3 +197,51 @@ def test_program_graph_adam_training(gpu, name, B, n, E):
         res.append((p.cpu(), losses))
     assert torch.allclose(res[0][1], res[1][1], rtol=2e-2, atol=2e-3), (res[0][1], res[1][1])
     assert (res[0][0] - res[1][0]).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("B,p", [(128, 0.3), (37, 0.0)])
+def test_cnn_tower_kernels_match_composite(gpu, B, p):
+    """Fused CNN tower fwd / bwd and the one-launch conv weight gradients vs the fp32 composites.
+    Each stage runs on the SAME inputs on both sides (the device's activations are copied to the CPU
+    buffers first), so bf16 rounding cannot flip a ReLU mask between the two."""
+    C = 3
+    lay = ParamLayout.for_model("CNNModel")
+    g = torch.Generator().manual_seed(4)
+    params = torch.stack([lay.flatten(build_model("CNNModel", seed=s).state_dict()) for s in range(C)])
+    x = {"vitals": torch.randn(C, B, 7, generator=g), "labs": torch.randn(C, B, 16, generator=g)}
+    dcat = torch.randn(C, B, 1024, generator=g) * 0.1
+    st = {}
+    for dev in (DEV, "cpu"):
+        prog = make_program("CNNModel", C, B, dev, train=True)
+        P = params.to(dev).contiguous()
+        prog.buf("xv", C, B, 7).copy_(x["vitals"])
+        prog.buf("xl", C, B, 16).copy_(x["labs"])
+        st[dev] = (prog, P, torch.zeros_like(P), Lx.StepCtl.create([7 + 3 * c for c in range(C)], dev))
+    tw = {d: st[d][0].towers(st[d][1]) for d in st}
+    cat = {d: st[d][0].buf("cat", C, B, 1024) for d in st}
+    for d in st:
+        Lx.cnn_towers_fwd(tw[d], B, cat[d], st[d][3], p, st[d][0].wimg())
+    _close(cat[DEV], cat["cpu"], rel=3e-2, name="cat")
+    for tg, tc in zip(tw[DEV], tw["cpu"]):
+        for k in ("h1", "h2", "h3"):
+            _close(getattr(tg, k), getattr(tc, k), rel=3e-2, name=k)
+            getattr(tc, k).copy_(getattr(tg, k).cpu())
+    for d in st:
+        Lx.cnn_towers_bwd(tw[d], B, dcat.to(d), st[d][3], p, st[d][0].wimg())
+    for tg, tc in zip(tw[DEV], tw["cpu"]):
+        for k in ("dh3", "dh2", "dh1"):
+            _close(getattr(tg, k), getattr(tc, k), rel=3e-2, name=k)
+            getattr(tc, k).copy_(getattr(tg, k).cpu())
+    for d in st:
+        prog, _, grads, _ = st[d]
+        jobs = []
+        for t, br in zip(tw[d], ("vitals", "labs")):
+            for i, (dh, h) in enumerate(zip((t.dh1, t.dh2, t.dh3), (t.x, t.h1, t.h2)), start=1):
+                jobs.append((dh, h, prog.w(grads, f"{br}_conv{i}.weight"), prog.w(grads, f"{br}_conv{i}.bias"), t.L))
+        Lx.conv_dw(jobs, B)
+    prog = st["cpu"][0]
+    for br in ("vitals", "labs"):
+        for i in (1, 2, 3):
+            for kind in ("weight", "bias"):
+                name = f"{br}_conv{i}.{kind}"
+                _close(prog.w(st[DEV][2], name), prog.w(st["cpu"][2], name), rel=2e-2, name=name)
