@@ -784,13 +784,15 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         break;
       }
       // =============================== head backward ===============================
-      {
+      // Adam of the output weights / fc2 bias (colsum slots 0, 1 and DY3) runs after the gradient
+      // hand-off: nothing on the way to d(cat) reads them
+      auto head_vec_adam = [&]() {
         float sm = 0.f;
         if (tid == 64)
           for (int i = 0; i < BM; ++i) sm += DY3[i];
         const VecG vs[3] = {{OUT_W, 32, 0}, {FC2_B, 32, 1}, {OUT_B, 1, -1}};
         adam_vecs(c, vs, K, sm);
-      }
+      };
       gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
       WFr<64, 64> wtf1a;
       wload(wtf1a, c.BF + WTF1, c.lane);
@@ -806,6 +808,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       WBAR();
       gemm_pf<64, 64>(c, TB, LD64, wtf1a);  // dcat[:, 0:64] = dy1 . Wf1[:, 0:64]
       if (ROLE == -1) {                     // one workgroup: dWf2 overlaps the dcat GEMMs
+        head_vec_adam();
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
         if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       }
@@ -826,6 +829,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (ROLE == 0 || ROLE == 3) {  // hand the gradients over first: the head's own updates overlap
         put_grad(c, W_XB + BM * 64, r, c0);
         xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);
+        head_vec_adam();
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
         if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       }
