@@ -59,7 +59,10 @@ def main() -> int:
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     if world > 1:
-        backend, device = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+        # AFL_BENCH_BACKEND / AFL_BENCH_DEVICE: test hooks (e.g. two gloo ranks sharing one GPU)
+        backend = os.environ.get("AFL_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        dev_idx = os.environ.get("AFL_BENCH_DEVICE")
+        backend, device = init_distributed(backend, device_index=int(dev_idx) if dev_idx is not None else None)
         comm = TorchComm(device)
     else:
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")

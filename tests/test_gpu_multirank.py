@@ -52,3 +52,21 @@ def test_two_ranks_match_single_process(gpu, tmp_path, attackers):
     sp = torch.load(tmp_path / "sp" / "TransformerModel.pth", weights_only=True)
     for k in sp:
         assert torch.allclose(sp[k].cpu(), mp[k].cpu(), atol=1e-5), k
+
+
+@pytest.mark.parametrize("extra", [[], ["--attackers", "3:Min-Max:2"]])
+def test_bench_two_ranks(gpu, tmp_path, extra):
+    """bench.py's multi-rank path (the driver's scaling run) end to end: two gloo ranks sharing the GPU."""
+    import json
+
+    env = dict(os.environ, PYTHONPATH=ROOT, AFL_BENCH_BACKEND="gloo", AFL_BENCH_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1"] + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rounds_ok"] == 2 and out["value"] > 0
+    assert out["config"]["parallelism"] == "fl8-clients-over-2-ranks"
