@@ -76,28 +76,107 @@ __device__ __forceinline__ s8v pack8(const float* v) {
   return r;
 }
 
+// Loads of the staging helpers: quad (row = t >> 2, dims 4 (t & 3) .. +3) of two [rows][stride] sources
+template <int NT, int NI>
+__device__ __forceinline__ void load_quads(const float* __restrict__ s1, long st1, int off1, const float* __restrict__ s2,
+                                           long st2, int off2, int nrows, int nvalid, f4v (&v1)[NI], f4v (&v2)[NI]) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int t = threadIdx.x + i * NT, row = t >> 2, qd = t & 3;
+    const bool ok = row < nvalid && t < nrows * 4;
+    v1[i] = ok ? *(const f4v*)(s1 + (long)row * st1 + off1 + 4 * qd) : f4v{0.f, 0.f, 0.f, 0.f};
+    v2[i] = ok ? *(const f4v*)(s2 + (long)row * st2 + off2 + 4 * qd) : f4v{0.f, 0.f, 0.f, 0.f};
+  }
+}
+__device__ __forceinline__ void put_quad(unsigned short* X, unsigned short* XT, int ldt, int row, int qd, f4v v) {
+  s4v a;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = (short)bf(v[j]);
+  if (X) *(s4v*)(X + swz(row, 4 * qd)) = a;
+  if (XT) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) XT[(4 * qd + j) * ldt + row] = (unsigned short)a[j];
+  }
+}
+constexpr int STAGE_MAXR = 1024 + 64;
+
+// Stage rows [0, nrows) of two 16-wide head slices of a [rows][stride] fp32 matrix into LDS as bf16:
+// X1 row-major swizzled ([row][16], swz) and X2 either row-major swizzled or transposed ([16][ldt]).
+// Every thread issues ALL its 16-B global loads before the first LDS store (the naive per-element
+// loop waited out one HBM latency per element: it dominated the kernels).
+template <int NT, bool X2T>
+__device__ __forceinline__ void stage2(const float* __restrict__ src, long stride, int off1, int off2, int nrows,
+                                       int nvalid, unsigned short* X1, unsigned short* X2, int ldt) {
+  constexpr int MAXR = 1024 + 64;
+  constexpr int NI = (MAXR * 4 + NT - 1) / NT;
+  f4v v1[NI], v2[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int t = threadIdx.x + i * NT, row = t >> 2, qd = t & 3;
+    const bool ok = row < nvalid && t < nrows * 4;
+    v1[i] = ok ? *(const f4v*)(src + (long)row * stride + off1 + 4 * qd) : f4v{0.f, 0.f, 0.f, 0.f};
+    v2[i] = ok ? *(const f4v*)(src + (long)row * stride + off2 + 4 * qd) : f4v{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int t = threadIdx.x + i * NT, row = t >> 2, qd = t & 3;
+    if (t < nrows * 4) {
+      s4v a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = (short)bf(v1[i][j]);
+      *(s4v*)(X1 + swz(row, 4 * qd)) = a;
+      if (X2T) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) X2[(4 * qd + j) * ldt + row] = bf(v2[i][j]);
+      } else {
+        s4v b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = (short)bf(v2[i][j]);
+        *(s4v*)(X2 + swz(row, 4 * qd)) = b;
+      }
+    }
+  }
+}
+
 // ============================================================================ forward
 constexpr int FW_WAVES = 12, FW_NT = 64 * FW_WAVES;
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 
+// cross-lane max / sum over lanes l, l^16, l^32 with the gfx950 permlane swaps (no LDS round trip).
+// permlane{16,32}_swap(a, a) returns {own value, partner value} in some order, so max / sum of the
+// pair is exact.
+__device__ __forceinline__ float max_x16_x32(float a) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  a = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+__device__ __forceinline__ float sum_x16_x32(float a) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  a = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 64 keys per step: four 16-key S^T subtiles (lane: keys kt + 16 t + 4 g + e of query li), one
+// max / sum reduction and one rescale per 64 keys, two O^T MFMAs (32 keys each).  Scores are kept in
+// the log2 domain (scale * log2 e folded in) so every exponential is one v_exp_f32.
 template <bool DROP>
 __global__ void __launch_bounds__(FW_NT) k_attn_fwd(AflAttn a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int Lp = a.Lp, LDV = Lp + 8;
-  unsigned short* Kl = (unsigned short*)smem;  // [Lp][16]
-  unsigned short* Vt = Kl + Lp * DH;           // [16][LDV]
+  const int Lp = a.Lp, LDV = Lp + 8 + 32;  // +32: the last 64-key step may read one zero 32-key half
+  unsigned short* Kl = (unsigned short*)smem;  // [Lp + 32][16]
+  unsigned short* Vt = Kl + (Lp + 32) * DH;    // [16][LDV]
   const int bh = blockIdx.x, h = bh % H, b = (bh / H) % a.B, c = bh / (H * a.B);
   const long rowbase = ((long)c * a.B + b) * a.L;
   const float* src = a.qkv + rowbase * QKV;
-  for (int t = threadIdx.x; t < Lp * DH; t += FW_NT) {
-    const int key = t >> 4, d = t & 15;
-    const bool ok = key < a.L;
-    Kl[swz(key, d)] = bf(ok ? src[(long)key * QKV + DM + h * DH + d] : 0.f);
-    Vt[d * LDV + key] = bf(ok ? src[(long)key * QKV + 2 * DM + h * DH + d] : 0.f);
-  }
+  stage2<FW_NT, true>(src, QKV, DM + h * DH, 2 * DM + h * DH, Lp + 32, a.L, Kl, Vt, LDV);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const uint32_t key = DROP ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
   const uint32_t drow0 = (uint32_t)((b * H + h) * a.L);
+  const float sc2 = a.scale * LOG2E;
   for (int q0 = wave * 16; q0 < Lp; q0 += 16 * FW_WAVES) {
     const int q = q0 + li;
     s4v qf;
@@ -105,37 +184,40 @@ __global__ void __launch_bounds__(FW_NT) k_attn_fwd(AflAttn a) {
     for (int j = 0; j < 4; ++j) qf[j] = (short)bf(q < a.L ? src[(long)q * QKV + h * DH + 4 * g + j] : 0.f);
     float m = -INFINITY, l = 0.f;
     f4v o = f4v{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < Lp; kt += 32) {
-      f4v s0 = mfma16(ld4(Kl + swz(kt + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
-      f4v s1 = mfma16(ld4(Kl + swz(kt + 16 + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
-      float s[8];
+    for (int kt = 0; kt < Lp; kt += 64) {
+      float s[16];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[e] = (kt + 4 * g + e < a.L) ? s0[e] * a.scale : -INFINITY;
-        s[4 + e] = (kt + 16 + 4 * g + e < a.L) ? s1[e] * a.scale : -INFINITY;
+      for (int t = 0; t < 4; ++t) {
+        const f4v st = mfma16(ld4(Kl + swz(kt + 16 * t + li, 4 * g)), qf, f4v{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[4 * t + e] = (kt + 16 * t + 4 * g + e < a.L) ? st[e] * sc2 : -INFINITY;
       }
       float mx = s[0];
 #pragma unroll
-      for (int j = 1; j < 8; ++j) mx = fmaxf(mx, s[j]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = __expf(m - mn);
-      float ps = 0.f, pd[8], mk[8];
-      if (DROP) keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk);
+      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
+      const float mn = fmaxf(m, max_x16_x32(mx));
+      const float alpha = ex2(m - mn);
+      float ps = 0.f, pd[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = __expf(s[j] - mn);
-        ps += p;
-        pd[j] = DROP ? p * mk[j] : p;
+      for (int j = 0; j < 16; ++j) {
+        pd[j] = ex2(s[j] - mn);
+        ps += pd[j];
       }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l = l * alpha + ps;
+      if (DROP) {
+        float mk[16];
+        keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, *(float(*)[8])mk);
+        keep8(key, a.drop.layer, drow0 + q, kt + 32 + 4 * g, kt + 48 + 4 * g, a.drop.thr16, a.drop.inv_keep,
+              *(float(*)[8])(mk + 8));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pd[j] *= mk[j];
+      }
+      l = l * alpha + sum_x16_x32(ps);
       m = mn;
       o *= alpha;
-      const s8v vf = cat8(ld4(Vt + li * LDV + kt + 4 * g), ld4(Vt + li * LDV + kt + 16 + 4 * g));
-      o = mfma32(vf, pack8(pd), o);
+      const s8v v0 = cat8(ld4(Vt + li * LDV + kt + 4 * g), ld4(Vt + li * LDV + kt + 16 + 4 * g));
+      const s8v v1 = cat8(ld4(Vt + li * LDV + kt + 32 + 4 * g), ld4(Vt + li * LDV + kt + 48 + 4 * g));
+      o = mfma32(v0, pack8(pd), o);
+      o = mfma32(v1, pack8(pd + 8), o);
     }
     if (q < a.L) {
       const float inv = 1.f / l;
@@ -143,7 +225,7 @@ __global__ void __launch_bounds__(FW_NT) k_attn_fwd(AflAttn a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) dst[e] = o[e] * inv;
     }
-    if (g == 0) a.lse[(long)bh * Lp + q] = q < a.L ? m + __logf(l) : INFINITY;
+    if (g == 0) a.lse[(long)bh * Lp + q] = q < a.L ? (m + __log2f(l)) * LN2 : INFINITY;
   }
 }
 
@@ -166,24 +248,33 @@ __global__ void __launch_bounds__(BW_NT) k_attn_bwd_kv(AflAttn a) {
   const float* src = a.qkv + rowbase * QKV;
   const float* dO = a.dout + rowbase * DM;
   const float* Oo = a.o + rowbase * DM;
-  for (int t = threadIdx.x; t < Lp * DH; t += BW_NT) {
-    const int q = t >> 4, d = t & 15;
-    const bool ok = q < a.L;
-    const unsigned short qv = bf(ok ? src[(long)q * QKV + h * DH + d] : 0.f);
-    const unsigned short dv = bf(ok ? dO[(long)q * DM + h * DH + d] : 0.f);
-    Ql[swz(q, d)] = qv;
-    Dl[swz(q, d)] = dv;
-    Qt[d * LDT + q] = qv;
-    Dt[d * LDT + q] = dv;
-  }
-  for (int q = threadIdx.x; q < Lp; q += BW_NT) {
-    float dl = 0.f;
-    if (q < a.L) {
+  {  // Q, dO -> row-major + transposed images; Delta_q = dO_q . O_q; lse
+    constexpr int NI = (STAGE_MAXR * 4 + BW_NT - 1) / BW_NT;
+    f4v vq[NI], vd[NI];
+    load_quads<BW_NT, NI>(src, QKV, h * DH, dO, DM, h * DH, Lp, a.L, vq, vd);
+    float dl[NI];
 #pragma unroll
-      for (int d = 0; d < DH; ++d) dl += dO[(long)q * DM + h * DH + d] * Oo[(long)q * DM + h * DH + d];
+    for (int i = 0; i < NI; ++i) {
+      const int t = threadIdx.x + i * BW_NT, row = t >> 2, qd = t & 3;
+      f4v vo = f4v{0.f, 0.f, 0.f, 0.f};
+      if (row < a.L && t < Lp * 4) vo = *(const f4v*)(Oo + (long)row * DM + h * DH + 4 * qd);
+      dl[i] = vd[i][0] * vo[0] + vd[i][1] * vo[1] + vd[i][2] * vo[2] + vd[i][3] * vo[3];
     }
-    DEL[q] = dl;
-    LSE[q] = a.lse[(long)bh * Lp + q];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int t = threadIdx.x + i * BW_NT, row = t >> 2, qd = t & 3;
+      float d = dl[i];
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      if (t < Lp * 4) {
+        put_quad(Ql, Qt, LDT, row, qd, vq[i]);
+        put_quad(Dl, Dt, LDT, row, qd, vd[i]);
+        if (qd == 0) {
+          DEL[row] = d;
+          LSE[row] = a.lse[(long)bh * Lp + row];
+        }
+      }
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
@@ -255,13 +346,18 @@ __global__ void __launch_bounds__(DQ_NT) k_attn_bwd_dq(AflAttn a) {
   const float* src = a.qkv + rowbase * QKV;
   const float* dO = a.dout + rowbase * DM;
   const float* Oo = a.o + rowbase * DM;
-  for (int t = threadIdx.x; t < Lp * DH; t += DQ_NT) {
-    const int k = t >> 4, d = t & 15;
-    const bool ok = k < a.L;
-    const unsigned short kv = bf(ok ? src[(long)k * QKV + DM + h * DH + d] : 0.f);
-    Kl[swz(k, d)] = kv;
-    Vl[swz(k, d)] = bf(ok ? src[(long)k * QKV + 2 * DM + h * DH + d] : 0.f);
-    Kt[d * LDT + k] = kv;
+  {
+    constexpr int NI = (STAGE_MAXR * 4 + DQ_NT - 1) / DQ_NT;
+    f4v vk[NI], vv[NI];
+    load_quads<DQ_NT, NI>(src, QKV, DM + h * DH, src, QKV, 2 * DM + h * DH, Lp, a.L, vk, vv);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int t = threadIdx.x + i * DQ_NT, row = t >> 2, qd = t & 3;
+      if (t < Lp * 4) {
+        put_quad(Kl, Kt, LDT, row, qd, vk[i]);
+        put_quad(Vl, nullptr, 0, row, qd, vv[i]);
+      }
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
@@ -318,7 +414,7 @@ int afl_attn_lp(int L) { return attn_lp(L); }
 
 int afl_attn_fwd(const AflAttn& a, hipStream_t s) {
   if (a.Lp != attn_lp(a.L) || a.Lp > 1024) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)a.Lp * DH * 2 + (size_t)DH * (a.Lp + 8) * 2;
+  const size_t lds = (size_t)(a.Lp + 32) * DH * 2 + (size_t)DH * (a.Lp + 8 + 32) * 2;
   if (a.drop.thr16)
     hipLaunchKernelGGL(k_attn_fwd<true>, dim3(a.C * a.B * H), dim3(FW_NT), lds, s, a);
   else
