@@ -168,9 +168,8 @@ class CNNProgram(_ICUProgram):
         head = [self.w(params, "fc2.weight"), self.w(params, "fc3.weight")] if self.train else []
         Lx.cnn_towers_fwd(self.towers(params), B, cat, ctl, self.p(0.3), self.wimg(), head)
         if self.train:
-            z1 = self.buf("z1", C, B, 128)
-            z1.zero_()
-            Lx.bgemm(cat, self.w(params, "fc1.weight"), z1, accum=2 if cat.is_cuda else 0,
+            # device: split-K accumulation into z1, which the head kernel zeroes after reading it
+            Lx.bgemm(cat, self.w(params, "fc1.weight"), self.buf("z1", C, B, 128), accum=2 if cat.is_cuda else 0,
                      splitk=8 if cat.is_cuda else 1)
             return None
         f1, f2, f3 = self.buf("f1", C, B, 128), self.buf("f2", C, B, 64), self.buf("f3", C, B, 32)
@@ -419,13 +418,16 @@ class ProgramRunner:
         losses = torch.zeros(C, plan.epochs, device=dev)
         skip = pg.skip_range()
 
+        on_dev = params.is_cuda
+
         def step():
             pg.inputs(table, idx, ctl)
             out = pg.forward(params, ctl)
             if pg.fused_loss:
-                grads.zero_()
+                if not on_dev:
+                    grads.zero_()
                 pg.backward_loss(params, grads, ctl, (bsz, ep, nb, failed, losses))
-                Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr)
+                Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr, zero_grads=on_dev)
                 Lx.step_end(ctl, tcount, bsz, failed)
                 return
             dz = pg.buf("dz", *out.shape)
@@ -433,9 +435,10 @@ class ProgramRunner:
                 Lx.bce(out, pg.labels(), bsz, ep, nb, ctl, failed, losses, dz)
             else:
                 Lx.ce(out, pg.labels(), bsz, ep, nb, ctl, failed, losses, dz)
-            grads.zero_()
+            if not on_dev:  # on the device Adam zeroes each gradient entry it consumes
+                grads.zero_()
             pg.backward(params, grads, ctl)
-            Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr)
+            Lx.adam_clients(params, grads, m, v, tcount, bsz, ctl, failed, lr, skip, sgd_lr, zero_grads=on_dev)
             Lx.step_end(ctl, tcount, bsz, failed)
 
         if S == 0:

@@ -262,7 +262,8 @@ def conv_dw(jobs, B: int, splitk: int = 4) -> None:
 
 
 def cnn_head(z1, y, w, g, d1, bsz, epoch, nb, ctl: StepCtl, failed, losses, z=None, wimg=None) -> None:
-    """CNNModel head in one launch per step: ``f1 = ReLU(z1 + b1)`` from the fc1 pre-activation, ``fc2 ->
+    """CNNModel head in one launch per step: ``f1 = ReLU(z1 + b1)`` from the fc1 pre-activation (the
+    device kernel zeroes ``z1`` after reading it: the next split-K fc1 accumulates into it), ``fc2 ->
     ReLU -> fc3 -> ReLU -> output``, the sigmoid-BCE of ``bce`` (same masking / NaN abort / epoch losses),
     and the backward: gradients of fc2 / fc3 / output and the fc1 bias (``g = [gW2, gb2, gW3, gb3, gWo,
     gbo, gb1]``, stored) and ``d1`` = d(fc1 pre-activation).  ``w = [W2, b2, W3, b3, Wo, bo, b1]``; on
@@ -474,12 +475,15 @@ def ce(logits, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
 
 
 # ---------------------------------------------------------------------------------- optimizer
-def adam_clients(p, g, m, v, tcount, bsz, ctl: StepCtl, failed, lr: float, skip=(0, 0), sgd_lr: float = 0.0) -> None:
+def adam_clients(p, g, m, v, tcount, bsz, ctl: StepCtl, failed, lr: float, skip=(0, 0), sgd_lr: float = 0.0,
+                 zero_grads: bool = False) -> None:
     """``torch.optim.Adam(lr)`` step (β 0.9/0.999, eps 1e-8) of every client active this step;
-    ``skip`` = [lo, hi) of non-trainable entries (buffers); ``sgd_lr > 0`` = plain SGD (test hook)."""
+    ``skip`` = [lo, hi) of non-trainable entries (buffers); ``sgd_lr > 0`` = plain SGD (test hook);
+    ``zero_grads``: zero each consumed gradient entry (the next step then needs no zero-fill launch;
+    inactive clients' entries are left alone — they never step again)."""
     if _nat(p):
         _native().adam_clients(p, g, m, v, tcount, bsz, ctl.stepctl, failed, float(lr), int(skip[0]), int(skip[1]),
-                               float(sgd_lr))
+                               float(sgd_lr), int(zero_grads))
         return
     s = ctl.step()
     keep = torch.ones(p.shape[1], dtype=torch.bool)

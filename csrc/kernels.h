@@ -156,7 +156,7 @@ struct AflConvDw {
 };
 int afl_conv_dw(const AflConvDw& a, hipStream_t s);
 struct AflCnnHead {
-  const float* f1;                   // [C][B][128] fc1 PRE-activation (bias + ReLU applied here; B <= 128)
+  float* f1;                         // [C][B][128] fc1 PRE-activation (bias + ReLU applied here, then zeroed)
   const float* b1;                   // fc1 bias (client-0 view)
   const unsigned short* wimg;        // head weight images of client 0 (built by the towers' forward)
   const float* y;                    // [C][B] labels
@@ -216,9 +216,9 @@ int afl_bce(const float* z, const float* y, const int* bsz, const int* epoch, co
             int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s);
 int afl_ce(const float* logits, const long* y, int K, const int* bsz, const int* epoch, const int* nb,
            const int* stepctl, int C, int B, int S, int* failed, float* losses, int E, float* dz, hipStream_t s);
-int afl_adam_clients(float* p, const float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
-                     const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi,
-                     float sgd_lr, hipStream_t s);
+int afl_adam_clients(float* p, float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
+                     const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi, float sgd_lr,
+                     int zero_g, hipStream_t s);
 int afl_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, int C, int S, hipStream_t s);
 int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off,
                     int pe_off, float* h, hipStream_t s);

@@ -503,12 +503,16 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
   const int c = blockIdx.x, B = h.B;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long wo = (long)c * h.sWc, go = (long)c * h.sGc;
-  // f1 = relu(z1 + b1) from the split-K fc1 pre-activation (16-B loads)
-  const float* z1 = h.f1 + (long)c * B * 128;
+  // f1 = relu(z1 + b1) from the split-K fc1 pre-activation (16-B loads); z1 is zeroed behind the read
+  // so the next step's split-K accumulates into zeros without a fill launch
+  float* z1 = h.f1 + (long)c * B * 128;
   for (int e = tid; e < 128 * 32; e += HNT) {
     const int b = e >> 5, i = 4 * (e & 31);
     f4v v = f4v{0.f, 0.f, 0.f, 0.f};
-    if (b < B) v = *(const f4v*)(z1 + (long)b * 128 + i);
+    if (b < B) {
+      v = *(const f4v*)(z1 + (long)b * 128 + i);
+      *(f4v*)(z1 + (long)b * 128 + i) = f4v{0.f, 0.f, 0.f, 0.f};
+    }
     unsigned short* d = f1s + b * H_L1 + i;
 #pragma unroll
     for (int q = 0; q < 4; ++q) d[q] = bfu(b < B ? relu(v[q] + h.b1[wo + i + q]) : 0.f);

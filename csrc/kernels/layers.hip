@@ -572,11 +572,11 @@ __global__ void __launch_bounds__(256) k_ce(const float* __restrict__ logits, co
 }
 
 // ============================================================================ optimizer
-__global__ void __launch_bounds__(256) k_adam_clients(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) k_adam_clients(float* __restrict__ p, float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v, long P,
                                                       const int* tcount, const int* bsz, const int* stepctl, int C,
                                                       int S, const int* failed, float lr, long skip_lo, long skip_hi,
-                                                      float sgd_lr) {
+                                                      float sgd_lr, int zero_g) {
   const int c = blockIdx.y;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   int bs;
@@ -584,6 +584,7 @@ __global__ void __launch_bounds__(256) k_adam_clients(float* __restrict__ p, con
   if (i >= skip_lo && i < skip_hi) return;  // buffers (e.g. the positional-encoding table)
   const long k = (long)c * P + i;
   const float gi = g[k];
+  if (zero_g) g[k] = 0.f;  // the next step accumulates into a zeroed arena without a fill launch
   if (sgd_lr > 0.f) {
     p[k] -= sgd_lr * gi;
     return;
@@ -786,11 +787,11 @@ int afl_ce(const float* logits, const long* y, int K, const int* bsz, const int*
   return launched();
 }
 
-int afl_adam_clients(float* p, const float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
+int afl_adam_clients(float* p, float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
                      const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi, float sgd_lr,
-                     hipStream_t s) {
+                     int zero_g, hipStream_t s) {
   hipLaunchKernelGGL(k_adam_clients, dim3(nb256(P), C), dim3(256), 0, s, p, g, m, v, P, tcount, bsz, stepctl, C, S,
-                     failed, lr, skip_lo, skip_hi, sgd_lr);
+                     failed, lr, skip_lo, skip_hi, sgd_lr, zero_g);
   return launched();
 }
 

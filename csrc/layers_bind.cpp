@@ -375,7 +375,7 @@ void cnn_head(torch::Tensor f1, torch::Tensor y, std::vector<torch::Tensor> w, s
     gp[i] = g[i].data_ptr<float>();
   }
   for (int i : {0, 2}) TORCH_CHECK(w[i].dim() == 3 && w[i].stride(1) == w[i].size(2), "cnn_head: dense weight rows");
-  h.f1 = f1.data_ptr<float>();
+  h.f1 = f1.data_ptr<float>();  // read, then zeroed by the kernel
   h.y = y.data_ptr<float>();
   h.W2 = wp[0]; h.b2 = wp[1]; h.W3 = wp[2]; h.b3 = wp[3]; h.Wo = wp[4]; h.bo = wp[5]; h.b1 = wp[6];
   dense(wimg, "wimg", torch::kInt16);
@@ -528,7 +528,7 @@ void ce(torch::Tensor logits, torch::Tensor y, torch::Tensor bsz, torch::Tensor 
 
 void adam_clients(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor tcount,
                   torch::Tensor bsz, torch::Tensor stepctl, torch::Tensor failed, double lr, int64_t skip_lo,
-                  int64_t skip_hi, double sgd_lr) {
+                  int64_t skip_hi, double sgd_lr, int64_t zero_grads) {
   dense(p, "p");
   dense(g, "g");
   dense(m, "m");
@@ -538,7 +538,7 @@ void adam_clients(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tens
   const int C = p.size(0), S = bsz.size(0);
   ok(afl_adam_clients(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.size(1), C,
                       tcount.data_ptr<int>(), bsz.data_ptr<int>(), stepctl.data_ptr<int>(), S,
-                      failed.data_ptr<int>(), (float)lr, skip_lo, skip_hi, (float)sgd_lr, cur()),
+                      failed.data_ptr<int>(), (float)lr, skip_lo, skip_hi, (float)sgd_lr, (int)zero_grads, cur()),
      "adam_clients");
 }
 
