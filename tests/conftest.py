@@ -8,6 +8,12 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("ATTACKFL_QUIET", "1")
 
+if os.environ.get("PYTEST_XDIST_WORKER"):  # pytest -n: split the cores instead of oversubscribing them
+    import torch
+
+    _n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1"))
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, _n)))
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built native extension")
