@@ -504,13 +504,6 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
         xwg_publish(c, xflag + XF_BWD, ((uint32_t)step << 1) | 1u);  // release the branch workgroups
         break;
       }
-      {
-        float sm = 0.f;
-        if (tid == 32)
-          for (int i = 0; i < BM; ++i) sm += DY3[i];
-        const VecG vs[3] = {{OUT_W, 16, 0}, {FC2_B, 16, 1}, {OUT_B, 1, -1}};
-        adam_vecs(c, vs, K, sm);
-      }
       gemm_pf<32, 32>(c, T2D, LDX, wt2);  // d(fc1 out) = d(fc2 out) . W2
       WFr<64, 32> wa, wb;
       wload(wa, c.BF + WT1, c.lane);
@@ -527,6 +520,13 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       gemm_pf<64, 32>(c, T1D, LDX, wb);  // d(labs output)
       put_grad(c, W_XB + BM * 64, r, q * 16);
       xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);  // (also the barrier before the dW GEMMs)
+      {  // output-layer / fc2-bias Adam (colsum slots 0, 1, DY3): off the way to the branch gradients
+        float sm = 0.f;
+        if (tid == 32)
+          for (int i = 0; i < BM; ++i) sm += DY3[i];
+        const VecG vs[3] = {{OUT_W, 16, 0}, {FC2_B, 16, 1}, {OUT_B, 1, -1}};
+        adam_vecs(c, vs, K, sm);
+      }
       gemm_dw_adam<1, 2>(c, T2D, LDX, T1, LDX, MFC2, K);    // dW2 = d2^T f1
       if (tid < 32) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       gemm_dw_adam<2, 8>(c, T1D, LDX, CAT, LDC, MFC1, K);   // dW1 = d1^T cat
