@@ -108,6 +108,10 @@ class Validation:
             data = self.table.rows
             out = self._program_runner(num_client).predict(flats, data).reshape(-1)
             return self._finish_icu(out, self._labels().repeat(num_client))
+        if self.device.type == "cuda" and num_client > 0:
+            flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32)  # one GEMM
+            out = torch.cat([self._outputs(flats[i]).reshape(-1) for i in range(num_client)])
+            return self._finish_icu(out, self._labels().repeat(num_client))
         outs, labs = [], []
         for i in range(num_client):
             flat = hnet.generate(i)

@@ -231,10 +231,19 @@ class PackedHyperNet:
             acts.append(h)
         return self.emb[idx], h, acts
 
+    def features_many(self, idxs) -> torch.Tensor:
+        """MLP features [n, H] of several clients, batched through every layer."""
+        h = self.emb[torch.as_tensor(list(idxs), dtype=torch.long, device=self.emb.device)]
+        for i in range(self.n_hidden + 1):
+            Wm, bm = self.mlp(i)
+            h = torch.addmm(bm[None, :], h, Wm.t())
+            if i < self.n_hidden:
+                h = torch.relu(h)
+        return h
+
     def generate_many(self, idxs) -> torch.Tensor:
         """Flat target weights [n, P] of several clients (one GEMM over the packed heads)."""
-        feats = torch.stack([self.features(int(i))[1] for i in idxs])
-        return torch.addmm(self.b[None, :], feats, self.W.t())
+        return torch.addmm(self.b[None, :], self.features_many(idxs), self.W.t())
 
     def generate(self, idx: int) -> torch.Tensor:
         """Flat target weights [P] for client ``idx`` (one GEMV over the packed heads)."""
