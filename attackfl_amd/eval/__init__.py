@@ -20,7 +20,7 @@ from ..models import ParamLayout, build_model
 from ..utils.log import print_with_color
 
 EVAL_CHUNK = 65536
-PROGRAM_EVAL_BATCH = {"CNNModel": 4096, "RNNModel": 8192, "TransformerClassifier": 256}
+PROGRAM_EVAL_BATCH = {"CNNModel": 4096, "RNNModel": 16384, "TransformerClassifier": 256}
 
 
 class Validation:
