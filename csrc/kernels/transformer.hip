@@ -341,10 +341,38 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
 }
 
 // ============================================================== branch backward
+// Everything the first backward phase reads that does NOT depend on d(output): this lane's saved
+// forward values, the LayerNorm affines, the W2 fragments.  A branch-only workgroup issues these loads
+// BEFORE it waits for the head's gradient hand-off, so their latency overlaps the wait.
+struct BwdPre {
+  float xh3[16], xh2[16], gm3[16], gm2[16];
+  float rstd2, rstd3;
+  uint32_t m2;
+  float gk[8], f2s[8];  // drop'(.) * gelu'(f0) and f2 of the forward
+  WFr<16, 64> wt2;
+};
+template <int BR>
+__device__ __forceinline__ void bwd_prefetch(const Ctx& c, BwdPre& p) {
+  using B = BrC<BR>;
+  const int r = c.r, q = c.q, c0 = q * 16;
+  const int ro = opaque(r * 64 + c0);
+  wload(p.wt2, c.BF + B::w.WT2, c.lane);
+  load16(p.xh3, c.wsf(B::s.XH3) + ro);
+  load16(p.xh2, c.wsf(B::s.XH2) + ro);
+  load16(p.gm3, c.P + B::o.bn_w + c0);
+  load16(p.gm2, c.P + B::o.ln2_w + c0);
+  const gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
+  p.rstd2 = rs[1];
+  p.rstd3 = rs[2];
+  p.m2 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2];
+  load8(p.gk, c.wsf(B::s.F0) + opaque(r * 8));
+  load8(p.f2s, c.wsf(B::s.F2S) + opaque(r * 8));
+}
+
 // on entry: dx3 of this branch in ACC (DY == 0), the DX3V workspace (DY == 1) or the hand-off slot W_XB
-// (DY == 2, branch-parallel mode, after the acquire)
+// (DY == 2, branch-parallel mode, after the acquire); p from bwd_prefetch<BR>
 template <int BR, int DY>
-__device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev) {
+__device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, const BwdPre& p) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);  // also DF0
   unsigned short* TA = c.u16(S_TA);
@@ -356,18 +384,16 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   int r = c.r, q = c.q, c0 = q * 16;
   const AdamK K = s.K;
   float dr2[16];  // residual gradient into x1, kept in registers until E12
-  WFr<16, 64> wt2;
-  wload(wt2, c.BF + B::w.WT2, c.lane);
+  const WFr<16, 64>& wt2 = p.wt2;
   {  // E10: LN3 bwd, LN2 bwd, df3 ; colsums g3 (v0), b3 (v1), g2 (v2), be2 (v3), b2 (v4)
     const int ro = opaque(r * 64 + c0);
-    float dy[16], xh3[16], xh2[16], gm3[16], gm2[16], dx[16], t[16];
-    load16(xh3, c.wsf(B::s.XH3) + ro);
-    load16(xh2, c.wsf(B::s.XH2) + ro);
-    load16(gm3, c.P + B::o.bn_w + c0);
-    load16(gm2, c.P + B::o.ln2_w + c0);
-    const gf* rs = c.wsf(B::s.RS) + opaque(r * 16 + q * 4);
-    const float rstd2 = rs[1], rstd3 = rs[2];
-    const uint32_t m2 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 2];
+    float dy[16], dx[16], t[16];
+    const float(&xh3)[16] = p.xh3;
+    const float(&xh2)[16] = p.xh2;
+    const float(&gm3)[16] = p.gm3;
+    const float(&gm2)[16] = p.gm2;
+    const float rstd2 = p.rstd2, rstd3 = p.rstd3;
+    const uint32_t m2 = p.m2;
     if (DY == 0) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) dy[j] = ACC[r * LDACC + c0 + j];
@@ -397,9 +423,8 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     store16bf(TA + r * LD64 + c0, t);
     colsum16(c, 4, t);
   }
-  float gk[8], f2s[8];  // drop'(.) * gelu'(f0) and f2 of the forward
-  load8(gk, c.wsf(B::s.F0) + opaque(r * 8));
-  load8(f2s, c.wsf(B::s.F2S) + opaque(r * 8));
+  const float(&gk)[8] = p.gk;  // drop'(.) * gelu'(f0) and f2 of the forward
+  const float(&f2s)[8] = p.f2s;
   BAR();
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2)
@@ -670,6 +695,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (BONLY >= 0) {  // branch-only workgroup: forward, hand-off, wait, backward
         fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev, xflag + (BONLY == 1 ? XF_LAB : XF_VIT),
                                                  (uint32_t)step);
+        BwdPre pre;  // issued before the wait: the loads complete while the head works
+        bwd_prefetch<BONLY < 0 ? 0 : BONLY>(c, pre);
         const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
@@ -681,10 +708,16 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
           break;
         }
         STAMP(21);
-        bwd_branch<BONLY < 0 ? 0 : BONLY, 2>(c, s, stamps, t_prev);
+        bwd_branch<BONLY < 0 ? 0 : BONLY, 2>(c, s, stamps, t_prev, pre);
         c.full_sync();
         continue;
       }
+      // fc1 weight fragments and bias are issued BEFORE the wait for the branch outputs: their global
+      // latency overlaps the wait instead of sitting on the critical path after it
+      WFr<64, 128> wf1;
+      wload(wf1, c.BF + WFF1, c.lane);
+      float bias[16];
+      load16(bias, c.P + FC1_B + q * 16);
       if (ROLE == 0 || ROLE == 3) {  // branch outputs from the other workgroup(s) -> CAT
         const uint32_t v = xwg_wait(c, xflag + (ROLE == 3 ? XF_VIT : XF_LAB), xflag + XF_LAB, (uint32_t)step, 0,
                                     xflag + XF_TMO, bcast);
@@ -703,10 +736,6 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         WBAR();
       }
       // =============================== head forward + loss ===============================
-      WFr<64, 128> wf1;
-      wload(wf1, c.BF + WFF1, c.lane);
-      float bias[16];
-      load16(bias, c.P + FC1_B + q * 16);
       gemm_pf<64, 128>(c, CAT, LD128, wf1);
       WFr<32, 64> wf2;
       wload(wf2, c.BF + WFF2, c.lane);
@@ -836,8 +865,16 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       gemm_dw_adam<4, 8>(c, TB, LD64, CAT, LD128, MFC1, K);  // dWf1 = dy1^T cat
       BAR();
       STAMP(9);
-      if (ROLE == -1) bwd_branch<1, 0>(c, s, stamps, t_prev);
-      if (ROLE == -1 || ROLE == 0) bwd_branch<0, 1>(c, s, stamps, t_prev);
+      if (ROLE == -1) {
+        BwdPre pre;
+        bwd_prefetch<1>(c, pre);
+        bwd_branch<1, 0>(c, s, stamps, t_prev, pre);
+      }
+      if (ROLE == -1 || ROLE == 0) {
+        BwdPre pre;
+        bwd_prefetch<0>(c, pre);
+        bwd_branch<0, 1>(c, s, stamps, t_prev, pre);
+      }
       // publish this step's Adam writes (bf16 weight copies, params) to every wave of the workgroup
       c.full_sync();
       r = c.r;
