@@ -661,6 +661,9 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
   St s;
   s.rows = (const gf*)a.rows;
   int r = c.r, q = c.q, c0 = q * 16;
+  bool have_next = false;  // inputs of the next step prefetched (branch-only workgroups)
+  int ridx_next = 0;
+  float xin_next[2][8];
 
   for (int e = 0; e < a.E && !failed; ++e) {
     const gi32* ord = (const gi32*)(a.order + ((long)cid * a.E + e) * a.maxnd);
@@ -677,8 +680,17 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       r = c.r;
       q = c.q;
       s.valid = r < Bn;
-      s.ridx = s.valid ? ord[b0 + r] : 0;
-      {  // both branches' input columns and the label, loaded once per step
+      if (have_next) {  // a branch-only workgroup loaded this step's inputs while it waited for the head
+        s.ridx = ridx_next;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s.xin[0][j] = xin_next[0][j];
+          s.xin[1][j] = xin_next[1][j];
+        }
+        have_next = false;
+      } else {
+        s.ridx = s.valid ? ord[b0 + r] : 0;
+        // both branches' input columns and the label, loaded once per step
         const gf* row = s.rows + (long)s.ridx * ROW;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -697,6 +709,35 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
                                                  (uint32_t)step);
         BwdPre pre;  // issued before the wait: the loads complete while the head works
         bwd_prefetch<BONLY < 0 ? 0 : BONLY>(c, pre);
+        {  // the NEXT step's input rows too (two dependent loads: row index, then the row)
+          int en = e, bn = b0 + BS;
+          for (;;) {  // same walk as the loops: next batch, skipping size-1 batches
+            if (bn >= nd) {
+              ++en;
+              bn = 0;
+              if (en >= a.E) break;
+              continue;
+            }
+            if (min(BS, nd - bn) == 1) {
+              bn += BS;
+              continue;
+            }
+            break;
+          }
+          if (en < a.E) {
+            const gi32* ordn = (const gi32*)(a.order + ((long)cid * a.E + en) * a.maxnd);
+            const bool vn = r < min(BS, nd - bn);
+            ridx_next = vn ? ordn[bn + r] : 0;
+            const gf* row = s.rows + (long)ridx_next * ROW;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int col = q * 8 + j;
+              xin_next[0][j] = (DO0 && vn && col < D_V) ? row[col] : 0.f;
+              xin_next[1][j] = (DO1 && vn && col < D_L) ? row[D_V + col] : 0.f;
+            }
+            have_next = true;
+          }
+        }
         const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
