@@ -168,6 +168,8 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
   int step = 0;
   bool failed = false;
   int r = c.r, q = c.q;
+  bool have_next = false;  // next step's inputs prefetched during the wait for the head
+  float x_next[8];
 
   for (int e = 0; e < a.E && !failed; ++e) {
     const gi32* ord = (const gi32*)(a.order + ((long)cid * a.E + e) * a.maxnd);
@@ -182,14 +184,20 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
       r = c.r;
       q = c.q;
       {  // masked inputs (RNNModel maps -2.0 to 0) -> XIN (bf16, K padded to 32)
-        const bool valid = r < Bn;
-        const gf* row = rows + (long)(valid ? ord[b0 + r] : 0) * ROWW + (BR == 0 ? 0 : DV);
         float x[8];
+        if (have_next) {  // loaded while this workgroup waited for the head's previous hand-off
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = q * 8 + j;
-          float v = (valid && col < B::din) ? row[col] : 0.f;
-          x[j] = v == -2.0f ? 0.f : v;
+          for (int j = 0; j < 8; ++j) x[j] = x_next[j];
+          have_next = false;
+        } else {
+          const bool valid = r < Bn;
+          const gf* row = rows + (long)(valid ? ord[b0 + r] : 0) * ROWW + (BR == 0 ? 0 : DV);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            float v = (valid && col < B::din) ? row[col] : 0.f;
+            x[j] = v == -2.0f ? 0.f : v;
+          }
         }
         store8bf(XIN + r * LDX + q * 8, x);
       }
@@ -237,26 +245,57 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           }
         }
       }
-      {  // LayerNorm(64) + dropout 0.3 -> hand-off slot; save xhat, rstd
-        float g[16], bt[16];
-        load8(*(float(*)[8])g, c.P + B::ln_w + q * 8);
-        load8(*(float(*)[8])(g + 8), c.P + B::ln_w + HU + q * 8);
+      // LayerNorm(64) + dropout 0.3 -> hand-off slot.  xhat, gamma, rstd and the dropout bits stay in
+      // registers for the backward (nothing to reload or re-hash after the wait for the head)
+      float lxh[16], lgm[16], lrstd;
+      uint32_t lkeep = 0;
+      {
+        float bt[16];
+        load8(*(float(*)[8])lgm, c.P + B::ln_w + q * 8);
+        load8(*(float(*)[8])(lgm + 8), c.P + B::ln_w + HU + q * 8);
         load8(*(float(*)[8])bt, c.P + B::ln_b + q * 8);
         load8(*(float(*)[8])(bt + 8), c.P + B::ln_b + HU + q * 8);
-        const float rstd = ln_fwd(h3);  // h3 -> xhat
-        gf* xs = (gf*)sav + SAV_XH + opaque(r) * 64 + q * 8;
-        st8(xs, h3);
-        st8(xs + HU, h3 + 8);
-        if (q == 0) ((gf*)sav)[SAV_RS + r] = rstd;
+        lrstd = ln_fwd(h3);  // h3 -> xhat
         float y[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int col = (i < 8 ? 0 : HU) + q * 8 + (i & 7);
-          y[i] = (h3[i] * g[i] + bt[i]) * (afl_keep(key, BR, r, col, THR_P03) ? INV_K03 : 0.f);
+          const bool kp = afl_keep(key, BR, r, col, THR_P03);
+          lkeep |= (kp ? 1u : 0u) << i;
+          lxh[i] = h3[i];
+          y[i] = (h3[i] * lgm[i] + bt[i]) * (kp ? INV_K03 : 0.f);
         }
         put_out(c, W_XF + BR * BM * 32, r, q, y);
       }
       xwg_publish(c, xflag + (BR == 0 ? XF_VIT : XF_LAB), (uint32_t)step);
+      {  // the NEXT step's input row (two dependent loads) while the head works
+        int en = e, bn = b0 + BS;
+        for (;;) {  // same walk as the loops: next batch, skipping size-1 batches
+          if (bn >= nd) {
+            ++en;
+            bn = 0;
+            if (en >= a.E) break;
+            continue;
+          }
+          if (min(BS, nd - bn) == 1) {
+            bn += BS;
+            continue;
+          }
+          break;
+        }
+        if (en < a.E) {
+          const gi32* ordn = (const gi32*)(a.order + ((long)cid * a.E + en) * a.maxnd);
+          const bool vn = r < min(BS, nd - bn);
+          const gf* row = rows + (long)(vn ? ordn[bn + r] : 0) * ROWW + (BR == 0 ? 0 : DV);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = q * 8 + j;
+            const float v = (vn && col < B::din) ? row[col] : 0.f;
+            x_next[j] = v == -2.0f ? 0.f : v;
+          }
+          have_next = true;
+        }
+      }
       const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
       if (v == 0xFFFFFFFFu || (v & 1u)) {  // timeout, or the head saw a NaN loss
         failed = true;
@@ -266,20 +305,16 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
       float dh[16];
       {  // d(branch output) -> dropout' -> LayerNorm backward; colsums gamma (v0), beta (v1)
         const int bo = (int)(W_XB + BR * BM * 64) * 4 + opaque(r * 64 + q * 8) * 2;  // bf16 [128][64] (put_grad)
-        float dy[16], xh[16], gm[16];
+        float dy[16];
         unpack8bf(ld_wt16(c, bo), dy);            // columns q*8 .. +7
         unpack8bf(ld_wt16(c, bo + 64), dy + 8);   // columns 32 + q*8 .. +7
-        const gf* xs = sav + SAV_XH + opaque(r) * 64 + q * 8;
-        load8(*(float(*)[8])xh, xs);
-        load8(*(float(*)[8])(xh + 8), xs + HU);
-        load8(*(float(*)[8])gm, c.P + B::ln_w + q * 8);
-        load8(*(float(*)[8])(gm + 8), c.P + B::ln_w + HU + q * 8);
-        const float rstd = sav[SAV_RS + r];
+        const float(&xh)[16] = lxh;
+        const float(&gm)[16] = lgm;
+        const float rstd = lrstd;
         float t[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int col = (i < 8 ? 0 : HU) + q * 8 + (i & 7);
-          dy[i] *= afl_keep(key, BR, r, col, THR_P03) ? INV_K03 : 0.f;
+          dy[i] *= (lkeep >> i) & 1u ? INV_K03 : 0.f;
           t[i] = dy[i] * xh[i];
         }
         colsumW<8>(c, 0, *(const float(*)[8])t, q * 8);
