@@ -170,6 +170,14 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
   int r = c.r, q = c.q;
   bool have_next = false;  // next step's inputs prefetched during the wait for the head
   float x_next[8];
+  float grr[8], gzz[8], gnn[8], gbhn[8];  // saved r, z, n gates + b_hn of the next gate backward
+  auto gate_prefetch = [&](int l, int d) {
+    const gf* sv = sav + SAV_RZN + ((long)((l - 1) * 2 + d) * BM + opaque(c.r)) * G3 + c.q * 8;
+    load8(grr, sv);
+    load8(gzz, sv + HU);
+    load8(gnn, sv + 2 * HU);
+    load8(gbhn, c.P + B::bhh(l, d) + 2 * HU + c.q * 8);
+  };
 
   for (int e = 0; e < a.E && !failed; ++e) {
     const gi32* ord = (const gi32*)(a.order + ((long)cid * a.E + e) * a.maxnd);
@@ -296,6 +304,7 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           have_next = true;
         }
       }
+      gate_prefetch(3, 0);  // the first gate backward's saved gates / bias, also before the wait
       const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
       if (v == 0xFFFFFFFFu || (v & 1u)) {  // timeout, or the head saw a NaN loss
         failed = true;
@@ -337,12 +346,20 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           {  // gate backward for direction d: dgi (-> DGI), bias-gradient colsums v2 (r | z), v3 (n | n*r)
-            const gf* sv = sav + SAV_RZN + ((long)((l - 1) * 2 + d) * BM + opaque(r)) * G3 + q * 8;
+            // this (layer, direction)'s saved gates were loaded one iteration ahead (the first before
+            // the wait for the head); issue the next one's loads now, behind this iteration's GEMMs
             float rr[8], zz[8], nn[8], bhn[8], dr[8], dz[8], dn[8], dnr[8];
-            load8(rr, sv);
-            load8(zz, sv + HU);
-            load8(nn, sv + 2 * HU);
-            load8(bhn, c.P + B::bhh(l, d) + 2 * HU + q * 8);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              rr[i] = grr[i];
+              zz[i] = gzz[i];
+              nn[i] = gnn[i];
+              bhn[i] = gbhn[i];
+            }
+            {
+              const int nl = d == 0 ? l : l - 1, ndr = d == 0 ? 1 : 0;
+              if (nl >= 1) gate_prefetch(nl, ndr);
+            }
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const float g = dh[d * 8 + i];
