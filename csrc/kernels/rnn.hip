@@ -345,6 +345,8 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         for (int i = 0; i < 16; ++i) dsum[i] = 0.f;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
+          WFr<64, 96> wdx;  // W_ih^T fragments of the dX GEMM below: issued before the gate math
+          if (l > 1) wload(wdx, c.BF + bf_wt(BR, l, d), c.lane);
           {  // gate backward for direction d: dgi (-> DGI), bias-gradient colsums v2 (r | z), v3 (n | n*r)
             // this (layer, direction)'s saved gates were loaded one iteration ahead (the first before
             // the wait for the head); issue the next one's loads now, behind this iteration's GEMMs
@@ -383,9 +385,7 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           r = c.r;
           q = c.q;
           if (l > 1) {  // d(layer input) += dgi . W_ih (transposed copy, before this matrix's Adam)
-            WFr<64, 96> w;
-            wload(w, c.BF + bf_wt(BR, l, d), c.lane);
-            gemm_pf<64, 96>(c, DGI, LDD, w);
+            gemm_pf<64, 96>(c, DGI, LDD, wdx);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               dsum[i] += ACC[r * LDACC_R + q * 8 + i];
