@@ -70,12 +70,13 @@ struct AflTfTrainArgs {
   float lr;
   int opt_mode;  // 0 = Adam (reference), 1 = SGD (test hook: exposes raw gradients)
   uint64_t* stamps;  // optional per-phase timers (AFL_TF_STAMPS builds), may be null
-  uint32_t* sync;    // [C][4] zeroed hand-off words (branch-parallel launches)
+  uint32_t* sync;    // zeroed hand-off words (branch-parallel launches): [C][AFL_TF_SYNC_WORDS] / RNN [C][4]
   int split;         // workgroups per client: 1, 2 (vitals+head | labs), 3 (head | vitals | labs)
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);
 long afl_tf_ws_floats();
+constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lines) + timeout word
 // rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
 int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);
 long afl_rnn_ws_floats();

@@ -353,6 +353,7 @@ __device__ __forceinline__ void colsumW(const CT& c, int v, const float (&x)[W],
 }
 template <class CT>
 __device__ __forceinline__ float cs_total(const CT& c, int v, int col) {
+  asm volatile("" : "+v"(col));  // recompute the 8 addresses here: hoisted out of the step loop they spill
   float s = 0.f;
 #pragma unroll
   for (int w = 0; w < 8; ++w) s += c.cs(v)[w * 64 + col];
@@ -479,6 +480,40 @@ __device__ __forceinline__ uint32_t xwg_wait(const CT& c, gu32* flag_a, gu32* fl
   }
   __syncthreads();
   return *bcast;
+}
+
+// Per-WAVE hand-off (row-per-wave layout: wave w produces and consumes rows 16w..16w+15 on both sides).
+// The same R1 protocol with the wave as the storing unit: the wave's own sc1 payload stores, its own
+// vmcnt(0) drain, then its lane 0 stores the wave's flag; the consumer wave polls its flag (all lanes one
+// address: one request) and only then issues its sc1 payload loads.  No workgroup barrier on either
+// side: a wave hands its rows over when IT is done instead of when the slowest wave is, and the consumer
+// wave starts when ITS rows have landed.  Flags sit on 128-byte lines of their own.
+template <class CT>
+__device__ __forceinline__ void wave_publish(const CT& c, gu32* flag, uint32_t value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (c.lane == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// waits until (flag_a >> shift) >= want and (flag_b >> shift) >= want; returns flag_a's value
+// (wave-uniform), or 0xFFFFFFFF on timeout (also raises *tmo)
+template <class CT>
+__device__ __forceinline__ uint32_t wave_wait(const CT& c, gu32* flag_a, gu32* flag_b, uint32_t want, int shift,
+                                              gu32* tmo) {
+  uint32_t v = 0;
+  for (long spins = 0;; ++spins) {
+    v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t w = flag_b == flag_a
+                           ? v
+                           : __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if ((v >> shift) >= want && (w >> shift) >= want) break;
+    if (spins > XWG_MAX_SPINS) {
+      v = 0xFFFFFFFFu;
+      if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+  return v;
 }
 
 // write the bf16 copies of one matrix from the master params

@@ -106,9 +106,11 @@ constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
 constexpr long W_XF = W_DX3V + BM * 64;  // branch outputs, bf16 [2][128][64] (vitals, labs)
 constexpr long W_XB = W_XF + 2 * BM * 32;  // d(branch outputs), bf16 [128][64] in fp32-sized slots [2][128][64]
 constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
-// hand-off words per client: [0] vitals output ready, [1] labs output ready, [2] d(outputs) ready
-// (value step << 1 | NaN abort), [3] timeout
-constexpr int XF_VIT = 0, XF_LAB = 1, XF_BWD = 2, XF_TMO = 3;
+// per-wave hand-off flags of one client (wave_publish / wave_wait), each on a 128-byte line:
+// group XF_VIT / XF_LAB: the branch output rows of wave w are ready (value = step); XF_BVIT / XF_BLAB:
+// d(branch output) rows of wave w are ready (value = step << 1 | NaN abort); word XF_TMO: timeout
+constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
+__device__ __forceinline__ gu32* xf(gu32* xflag, int group, int wave) { return xflag + (group * 8 + wave) * 32; }
 
 struct TfLayout {
   static constexpr int S_ACC = ::S_ACC, LDACC = ::LDACC, S_CS = ::S_CS;
@@ -183,10 +185,11 @@ __device__ __forceinline__ void put_x(const Ctx& c, const St& s) {
 
 // ============================================================== branch forward
 // XCH: publish the branch output to the hand-off slot W_XF (write-through stores) instead of LDS CAT,
-// then raise *pub = pub_val; the backward's saved activations of the last phase are stored only after
-// the flag, so the publish drain (vmcnt 0) waits for the 16 KB payload, not for them too
+// each wave its own rows with its own flag xf(xflag, BR, wave) = pub_val; the backward's saved
+// activations of the last phase are stored only after the flag, so the publish drain (vmcnt 0) waits
+// for the payload, not for them too
 template <int BR, bool XCH = false>
-__device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, gu32* pub = nullptr,
+__device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, gu32* xflag = nullptr,
                                            uint32_t pub_val = 0) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);
@@ -325,7 +328,7 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
       const int bo = (int)(W_XF + BR * BM * 32) * 4 + ro * 2;
       st_wt16(c, bo, __builtin_bit_cast(u32x4, pack8bf(x)));
       st_wt16(c, bo + 16, __builtin_bit_cast(u32x4, pack8bf(x + 8)));
-      xwg_publish(c, pub, pub_val);
+      wave_publish(c, xf(xflag, BR, c.wave), pub_val);
     } else {
       store16bf(CAT + r * LD128 + BR * 64 + c0, x);
     }
@@ -639,8 +642,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
     init_copies(c, MFC2);
   }
   __syncthreads();
-  gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * 4 : nullptr);  // XF_* words
-  uint32_t* bcast = (uint32_t*)(smem + S_RED) + 12;
+  gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * AFL_TF_SYNC_WORDS : nullptr);  // XF_* words
   bool timed_out = false;
 
   const int nd = a.nd[cid];
@@ -705,8 +707,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (ROLE == -1 || ROLE == 0) fwd_branch<0>(c, s, stamps, t_prev);
       if (ROLE == -1) fwd_branch<1>(c, s, stamps, t_prev);
       if (BONLY >= 0) {  // branch-only workgroup: forward, hand-off, wait, backward
-        fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev, xflag + (BONLY == 1 ? XF_LAB : XF_VIT),
-                                                 (uint32_t)step);
+        fwd_branch<BONLY < 0 ? 0 : BONLY, true>(c, s, stamps, t_prev, xflag, (uint32_t)step);
         BwdPre pre;  // issued before the wait: the loads complete while the head works
         bwd_prefetch<BONLY < 0 ? 0 : BONLY>(c, pre);
         {  // the NEXT step's input rows too (two dependent loads: row index, then the row)
@@ -738,7 +739,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
             have_next = true;
           }
         }
-        const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
+        gu32* fb = xf(xflag, BONLY == 1 ? XF_BLAB : XF_BVIT, c.wave);  // this wave's rows of d(output)
+        const uint32_t v = wave_wait(c, fb, fb, (uint32_t)step, 1, xflag + XF_TMO);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
           failed = true;
@@ -760,8 +762,9 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       float bias[16];
       load16(bias, c.P + FC1_B + q * 16);
       if (ROLE == 0 || ROLE == 3) {  // branch outputs from the other workgroup(s) -> CAT
-        const uint32_t v = xwg_wait(c, xflag + (ROLE == 3 ? XF_VIT : XF_LAB), xflag + XF_LAB, (uint32_t)step, 0,
-                                    xflag + XF_TMO, bcast);
+        // this wave's CAT rows: its own flags, no workgroup barrier
+        const uint32_t v = wave_wait(c, xf(xflag, ROLE == 3 ? XF_VIT : XF_LAB, c.wave), xf(xflag, XF_LAB, c.wave),
+                                     (uint32_t)step, 0, xflag + XF_TMO);
         if (v == 0xFFFFFFFFu) {
           timed_out = true;
           failed = true;
@@ -850,7 +853,10 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         else epoch_loss += loss;
       }
       if (failed) {
-        if (ROLE == 0 || ROLE == 3) xwg_publish(c, xflag + XF_BWD, ((uint32_t)step << 1) | 1u);  // release them
+        if (ROLE == 0 || ROLE == 3) {  // release them (every wave its rows' flags)
+          if (ROLE == 3) wave_publish(c, xf(xflag, XF_BVIT, c.wave), ((uint32_t)step << 1) | 1u);
+          wave_publish(c, xf(xflag, XF_BLAB, c.wave), ((uint32_t)step << 1) | 1u);
+        }
         break;
       }
       // =============================== head backward ===============================
@@ -885,8 +891,9 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       WFr<64, 64> wtf1b;
       wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
       WBAR();
-      if (ROLE == 3) {  // vitals gradient -> its hand-off slot
+      if (ROLE == 3) {  // vitals gradient -> its hand-off slot, released row-wave by row-wave
         put_grad(c, W_XB, r, c0);
+        wave_publish(c, xf(xflag, XF_BVIT, c.wave), (uint32_t)step << 1);
       } else {
         float t[16];
 #pragma unroll
@@ -898,7 +905,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (ROLE == -1) BAR(); else WBAR();  // ROLE -1: dWf1 below reads every wave's TB rows
       if (ROLE == 0 || ROLE == 3) {  // hand the gradients over first: the head's own updates overlap
         put_grad(c, W_XB + BM * 64, r, c0);
-        xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);
+        wave_publish(c, xf(xflag, XF_BLAB, c.wave), (uint32_t)step << 1);
+        BAR();  // the updates below read every wave's E8 column sums and TB rows
         head_vec_adam();
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
         if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
