@@ -382,7 +382,7 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);
   torch::Tensor sync;
   if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
-    sync = torch::zeros({(long)C * (kind == 0 ? AFL_TF_SYNC_WORDS : 4)}, order.options());
+    sync = torch::zeros({(long)C * AFL_TF_SYNC_WORDS}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
   const int rc = kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());

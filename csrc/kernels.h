@@ -70,7 +70,7 @@ struct AflTfTrainArgs {
   float lr;
   int opt_mode;  // 0 = Adam (reference), 1 = SGD (test hook: exposes raw gradients)
   uint64_t* stamps;  // optional per-phase timers (AFL_TF_STAMPS builds), may be null
-  uint32_t* sync;    // zeroed hand-off words (branch-parallel launches): [C][AFL_TF_SYNC_WORDS] / RNN [C][4]
+  uint32_t* sync;    // zeroed hand-off words (branch-parallel launches): [C][AFL_TF_SYNC_WORDS]
   int split;         // workgroups per client: 1, 2 (vitals+head | labs), 3 (head | vitals | labs)
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);

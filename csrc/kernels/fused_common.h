@@ -432,9 +432,9 @@ __device__ __forceinline__ void store16bf(unsigned short* p, const float (&x)[16
 }
 
 // ---- cross-workgroup hand-off (branch-parallel mode; cdna_hip_programming.md Guideline 16, R1) ----
-// payload: 16-byte write-through (sc1) stores; every storing wave drains (vmcnt 0), then a workgroup
-// barrier, then ONE lane stores the flag.  Consumer: ONE wave polls the flag relaxed (bounded spin),
-// workgroup barrier, then sc1 loads of the payload (never plain loads: there is no acquire).
+// payload: 16-byte write-through (sc1) stores; the storing wave drains (vmcnt 0), then ONE lane stores
+// the flag.  Consumer: the wave polls the flag relaxed (bounded spin), then sc1 loads of the payload
+// (never plain loads: there is no acquire).
 // 16-byte write-through store / sc1 load at a BYTE offset from the workspace base (buffer_*_dwordx4
 // sc1; a 16-B sc1 store costs what a plain one does, 8-B ones 2.7x per byte: MI355X_MICROARCH price list)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -446,42 +446,7 @@ template <class CT>
 __device__ __forceinline__ u32x4 ld_wt16(const CT& c, int byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(c.wrs(), byte_off, 0, 16);
 }
-template <class CT>
-__device__ __forceinline__ void xwg_publish(const CT& c, gu32* flag, uint32_t value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (c.tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 constexpr long XWG_MAX_SPINS = 1L << 22;  // ~seconds: a missing partner becomes an error, not a hang
-// waits until (flag_a >> shift) >= want and (flag_b >> shift) >= want (pass the same word twice for
-// one); returns flag_a's value, or 0xFFFFFFFF on timeout (also raises *tmo)
-template <class CT>
-__device__ __forceinline__ uint32_t xwg_wait(const CT& c, gu32* flag_a, gu32* flag_b, uint32_t want, int shift,
-                                             gu32* tmo, uint32_t* bcast) {
-  if (c.wave == 0) {
-    uint32_t v = 0;
-    for (long spins = 0;; ++spins) {
-      v = __hip_atomic_load(flag_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t w = flag_b == flag_a ? v : __hip_atomic_load(flag_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((v >> shift) >= want && (w >> shift) >= want) break;
-      if (spins > XWG_MAX_SPINS) {
-        v = 0xFFFFFFFFu;
-        if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    // No agent acquire (buffer_inv sc1, ~1.5 us): every handed-off byte is stored sc1 and drained by its
-    // storing wave before the flag (xwg_publish), and EVERY load of it is a buffer_load sc1 to registers
-    // (ld_wt16), so no stale L1 line can be read (Guideline 16, sc1-load form; MI355X_MICROARCH Valid
-    // forms, table row 1).  The wavefront fence only keeps the compiler from hoisting loads above the poll.
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (c.lane == 0) *bcast = v;
-  }
-  __syncthreads();
-  return *bcast;
-}
-
 // Per-WAVE hand-off (row-per-wave layout: wave w produces and consumes rows 16w..16w+15 on both sides).
 // The same R1 protocol with the wave as the storing unit: the wave's own sc1 payload stores, its own
 // vmcnt(0) drain, then its lane 0 stores the wave's flag; the consumer wave polls its flag (all lanes one
@@ -493,6 +458,11 @@ __device__ __forceinline__ void wave_publish(const CT& c, gu32* flag, uint32_t v
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (c.lane == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Per-wave hand-off flags of one client ([AFL_TF_SYNC_WORDS] zeroed words), each on a 128-byte line:
+// group XF_VIT / XF_LAB: the branch output rows of wave w are ready (value = step); XF_BVIT / XF_BLAB:
+// d(branch output) rows of wave w are ready (value = step << 1 | NaN abort); word XF_TMO: timeout
+constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
+__device__ __forceinline__ gu32* xf(gu32* xflag, int group, int wave) { return xflag + (group * 8 + wave) * 32; }
 // waits until (flag_a >> shift) >= want and (flag_b >> shift) >= want; returns flag_a's value
 // (wave-uniform), or 0xFFFFFFFF on timeout (also raises *tmo)
 template <class CT>

@@ -74,7 +74,6 @@ constexpr long SAV_RZN = 0, SAV_XH = 6L * BM * G3, SAV_RS = SAV_XH + BM * 64, SA
 constexpr long W_XF = W_SAV + 2 * SAV_BR;      // branch outputs bf16 [2][128][64]
 constexpr long W_XB = W_XF + 2 * BM * 32;      // d(branch outputs) bf16 [128][64] in fp32-sized slots [2][128][64]
 constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
-constexpr int XF_VIT = 0, XF_LAB = 1, XF_BWD = 2, XF_TMO = 3;
 
 // ------------------------------------------------------------------------ LDS map (bytes)
 constexpr int LDACC_R = 100, LDX = 40, LDH = 72, LDD = 104, LDC = 136;
@@ -153,8 +152,7 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
                           G3});
   __syncthreads();
 
-  gu32* xflag = (gu32*)(a.sync + (long)cid * 4);
-  uint32_t* bcast = (uint32_t*)(smem + S_RED) + 12;
+  gu32* xflag = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);  // per-wave XF_* flags (fused_common.h)
   unsigned short* XIN = c.u16(S_XIN);
   unsigned short* DGI = c.u16(S_DGI);
   float* ACC = c.acc();
@@ -275,7 +273,7 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         }
         put_out(c, W_XF + BR * BM * 32, r, q, y);
       }
-      xwg_publish(c, xflag + (BR == 0 ? XF_VIT : XF_LAB), (uint32_t)step);
+      wave_publish(c, xf(xflag, BR == 0 ? XF_VIT : XF_LAB, c.wave), (uint32_t)step);  // this wave's rows
       {  // the NEXT step's input row (two dependent loads) while the head works
         int en = e, bn = b0 + BS;
         for (;;) {  // same walk as the loops: next batch, skipping size-1 batches
@@ -305,7 +303,8 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         }
       }
       gate_prefetch(3, 0);  // the first gate backward's saved gates / bias, also before the wait
-      const uint32_t v = xwg_wait(c, xflag + XF_BWD, xflag + XF_BWD, (uint32_t)step, 1, xflag + XF_TMO, bcast);
+      gu32* fb = xf(xflag, BR == 0 ? XF_BVIT : XF_BLAB, c.wave);  // this wave's rows of d(output)
+      const uint32_t v = wave_wait(c, fb, fb, (uint32_t)step, 1, xflag + XF_TMO);
       if (v == 0xFFFFFFFFu || (v & 1u)) {  // timeout, or the head saw a NaN loss
         failed = true;
         break;
@@ -445,8 +444,7 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
   init_copies(c, MFC2);
   __syncthreads();
 
-  gu32* xflag = (gu32*)(a.sync + (long)cid * 4);
-  uint32_t* bcast = (uint32_t*)(smem + S_RED) + 12;
+  gu32* xflag = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);  // per-wave XF_* flags (fused_common.h)
   unsigned short* CAT = c.u16(S_CAT);
   unsigned short* T1 = c.u16(S_T1);
   unsigned short* T1D = c.u16(S_T1D);
@@ -489,7 +487,9 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
         wo[i] = c.P[OUT_W + q * 4 + i];
       }
       const float bo = c.P[OUT_B];
-      const uint32_t v = xwg_wait(c, xflag + XF_VIT, xflag + XF_LAB, (uint32_t)step, 0, xflag + XF_TMO, bcast);
+      // this wave's CAT rows: its own flags, no workgroup barrier
+      const uint32_t v = wave_wait(c, xf(xflag, XF_VIT, c.wave), xf(xflag, XF_LAB, c.wave), (uint32_t)step, 0,
+                                   xflag + XF_TMO);
       if (v == 0xFFFFFFFFu) {
         timed_out = failed = true;
         break;
@@ -553,7 +553,8 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
         else epoch_loss += loss;
       }
       if (failed) {
-        xwg_publish(c, xflag + XF_BWD, ((uint32_t)step << 1) | 1u);  // release the branch workgroups
+        wave_publish(c, xf(xflag, XF_BVIT, c.wave), ((uint32_t)step << 1) | 1u);  // release the branch workgroups
+        wave_publish(c, xf(xflag, XF_BLAB, c.wave), ((uint32_t)step << 1) | 1u);
         break;
       }
       gemm_pf<32, 32>(c, T2D, LDX, wt2);  // d(fc1 out) = d(fc2 out) . W2
@@ -569,9 +570,13 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       }
       gemm_pf<64, 32>(c, T1D, LDX, wa);  // d(vitals output) = d1 . W1[:, 0:64]
       put_grad(c, W_XB, r, q * 16);
+      wave_publish(c, xf(xflag, XF_BVIT, c.wave), (uint32_t)step << 1);
       gemm_pf<64, 32>(c, T1D, LDX, wb);  // d(labs output)
       put_grad(c, W_XB + BM * 64, r, q * 16);
-      xwg_publish(c, xflag + XF_BWD, (uint32_t)step << 1);  // (also the barrier before the dW GEMMs)
+      wave_publish(c, xf(xflag, XF_BLAB, c.wave), (uint32_t)step << 1);
+      c.bar();  // the updates below read every wave's rows and column sums
+      r = c.r;
+      q = c.q;
       {  // output-layer / fc2-bias Adam (colsum slots 0, 1, DY3): off the way to the branch gradients
         float sm = 0.f;
         if (tid == 32)

@@ -106,11 +106,6 @@ constexpr long W_DX3V = W_ACT + 2 * BRS_SIZE;
 constexpr long W_XF = W_DX3V + BM * 64;  // branch outputs, bf16 [2][128][64] (vitals, labs)
 constexpr long W_XB = W_XF + 2 * BM * 32;  // d(branch outputs), bf16 [128][64] in fp32-sized slots [2][128][64]
 constexpr long WS_FLOATS = W_XB + 2 * BM * 64;
-// per-wave hand-off flags of one client (wave_publish / wave_wait), each on a 128-byte line:
-// group XF_VIT / XF_LAB: the branch output rows of wave w are ready (value = step); XF_BVIT / XF_BLAB:
-// d(branch output) rows of wave w are ready (value = step << 1 | NaN abort); word XF_TMO: timeout
-constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
-__device__ __forceinline__ gu32* xf(gu32* xflag, int group, int wave) { return xflag + (group * 8 + wave) * 32; }
 
 struct TfLayout {
   static constexpr int S_ACC = ::S_ACC, LDACC = ::LDACC, S_CS = ::S_CS;
