@@ -13,6 +13,7 @@ typedef short s8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define LDS_AS __attribute__((address_space(3)))
 // Global-memory pointers carry address_space(1) explicitly: they pass through opaque asm at every phase
 // barrier, and a generic pointer would demote every access to FLAT (which waits on vmcnt AND lgkmcnt).
@@ -211,62 +212,141 @@ struct MatW {
 // dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows, then Adam on the real entries.  The Adam state
 // (p, m, v) of each lane's 4 accumulator elements is loaded before the MFMAs so the global latency
 // overlaps the tile's transposed LDS reads and matrix work.
+// gfx9 counts loads and stores in ONE vmcnt queue, in issue order: a load issued behind a burst of
+// Adam stores waits for their acknowledgements before its data can be used.  So every update below is
+// split into a load part (issue it BEFORE the stores of earlier updates) and an apply part.
+template <int MT, int NTL>
+struct DwS {  // Adam state of this wave's dW tiles (tile t = wave + 8j)
+  static constexpr int T = (MT * NTL + 7) / 8;
+  float p[T][4], m[T][4], v[T][4];
+};
 template <int MT, int NTL, class CT>
-__device__ __forceinline__ void gemm_dw_adam(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
-                                             int ldx, MatW mw, AdamK k) {
-  for (int t = c.wave; t < MT * NTL; t += 8) {
+__device__ __forceinline__ void dw_ld(const CT& c, MatW mw, DwS<MT, NTL>& s) {
+#pragma unroll
+  for (int j = 0; j < DwS<MT, NTL>::T; ++j) {
+    const int t = c.wave + 8 * j;
+    if (t >= MT * NTL) break;
     const int mt = t / NTL, nt = t % NTL;
     const int kk = 16 * nt + (c.lane & 15);
-    float pp[4], mm[4], vv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = 16 * mt + 4 * (c.lane >> 4) + i;
       const bool ok = n < mw.n_real && kk < mw.k_real;
       const int idx = ok ? mw.off + n * mw.k_real + kk : mw.off;
-      pp[i] = c.P[idx];
-      mm[i] = c.M[idx];
-      vv[i] = c.V[idx];
-    }
-    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int b0 = 0; b0 < BM; b0 += 32)
-      acc = mfma(lds_col_frag(DY, ldy, b0, 16 * mt, c.lane), lds_col_frag(X, ldx, b0, 16 * nt, c.lane), acc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = 16 * mt + 4 * (c.lane >> 4) + i;
-      if (n < mw.n_real && kk < mw.k_real) {
-        const int idx = mw.off + n * mw.k_real + kk;
-        const float pn = adam_upd(pp[i], mm[i], vv[i], acc[i], k);
-        c.P[idx] = pn;
-        if (k.sgd_lr <= 0.f) {
-          c.M[idx] = mm[i];
-          c.V[idx] = vv[i];
-        }
-        const unsigned short h = f2bf(pn);
-        c.BF[mw.wf + n * mw.wf_ld + kk] = h;
-        if (mw.wt >= 0) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
-      }
+      s.p[j][i] = c.P[idx];
+      s.m[j][i] = c.M[idx];
+      s.v[j][i] = c.V[idx];
     }
   }
+}
+// dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows (all tiles' MFMAs first), then Adam on the real entries
+template <int MT, int NTL, class CT>
+__device__ __forceinline__ void dw_apply(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
+                                         int ldx, MatW mw, AdamK k, DwS<MT, NTL>& s) {
+  constexpr int T = DwS<MT, NTL>::T;
+  f4v acc[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int t = c.wave + 8 * j;
+    acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    if (t >= MT * NTL) break;
+    const int mt = t / NTL, nt = t % NTL;
+#pragma unroll
+    for (int b0 = 0; b0 < BM; b0 += 32)
+      acc[j] = mfma(lds_col_frag(DY, ldy, b0, 16 * mt, c.lane), lds_col_frag(X, ldx, b0, 16 * nt, c.lane), acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int t = c.wave + 8 * j;
+    if (t >= MT * NTL) break;
+    const int mt = t / NTL, nt = t % NTL;
+    const int kk = 16 * nt + (c.lane & 15);
+    // the lane's 4 rows n0..n0+3 are 4 CONSECUTIVE elements of the transposed copy's row kk: one 8-byte
+    // store instead of four scattered 2-byte ones (all-or-none real when n_real % 4 == 0)
+    const int n0 = 16 * mt + 4 * (c.lane >> 4);
+    const bool vec_t = mw.wt >= 0 && ((mw.n_real | mw.wt | mw.wt_ld) & 3) == 0;
+    unsigned short hv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + i;
+      hv[i] = 0;
+      if (n < mw.n_real && kk < mw.k_real) {
+        const int idx = mw.off + n * mw.k_real + kk;
+        const float pn = adam_upd(s.p[j][i], s.m[j][i], s.v[j][i], acc[j][i], k);
+        c.P[idx] = pn;
+        if (k.sgd_lr <= 0.f) {
+          c.M[idx] = s.m[j][i];
+          c.V[idx] = s.v[j][i];
+        }
+        const unsigned short h = f2bf(pn);
+        hv[i] = h;
+        c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+        if (mw.wt >= 0 && !vec_t) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
+      }
+    }
+    if (vec_t && n0 < mw.n_real && kk < mw.k_real)
+      *(GAS u32x2*)(c.BF + mw.wt + kk * mw.wt_ld + n0) =
+          u32x2{(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+  }
+}
+template <int MT, int NTL, class CT>
+__device__ __forceinline__ void gemm_dw_adam(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
+                                             int ldx, MatW mw, AdamK k) {
+  DwS<MT, NTL> s;
+  dw_ld<MT, NTL>(c, mw, s);
+  dw_apply<MT, NTL>(c, DY, ldy, X, ldx, mw, k, s);
 }
 
 // Adam on up to 512 small-vector elements (biases, LayerNorm affine) in parallel: thread tid handles
 // element tid of the concatenation of the listed vectors; gradient = column sum CS[v] over 8 waves.
+// one parameter's Adam state, loaded ahead of the stores of earlier updates (see dw_ld)
+struct AdamS {
+  float p, m, v;
+};
+template <class CT>
+__device__ __forceinline__ AdamS adam_ld(const CT& c, int idx) {
+  return AdamS{c.P[idx], c.M[idx], c.V[idx]};
+}
+template <class CT>
+__device__ __forceinline__ void adam_st(const CT& c, int idx, AdamS s, float g, AdamK k) {
+  const float pn = adam_upd(s.p, s.m, s.v, g, k);
+  c.P[idx] = pn;
+  if (k.sgd_lr <= 0.f) {
+    c.M[idx] = s.m;
+    c.V[idx] = s.v;
+  }
+}
 struct VecG {
   int off, n, csv;  // param offset, length, column-sum slot (-1: value supplied in `g0`)
   int cbase = 0;    // first column of the slot holding element 0
 };
+// Adam on vectors whose gradients are column sums: each thread owns at most one element of the list
 template <int NV, class CT>
-__device__ __forceinline__ void adam_vecs(const CT& c, const VecG (&vs)[NV], AdamK k, float g0 = 0.f) {
+__device__ __forceinline__ AdamS adam_vecs_ld(const CT& c, const VecG (&vs)[NV]) {
+  AdamS s{0.f, 0.f, 0.f};
+  int e = c.tid;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (e >= 0 && e < vs[i].n) s = adam_ld(c, vs[i].off + e);
+    e -= vs[i].n;
+  }
+  return s;
+}
+template <int NV, class CT>
+__device__ __forceinline__ void adam_vecs_st(const CT& c, const VecG (&vs)[NV], AdamS s, AdamK k, float g0 = 0.f) {
   int e = c.tid;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     if (e >= 0 && e < vs[i].n) {
       const float g = vs[i].csv >= 0 ? cs_total(c, vs[i].csv, vs[i].cbase + e) : g0;
-      adam(c.P, c.M, c.V, vs[i].off + e, g, k);
+      adam_st(c, vs[i].off + e, s, g, k);
     }
     e -= vs[i].n;
   }
+}
+template <int NV, class CT>
+__device__ __forceinline__ void adam_vecs(const CT& c, const VecG (&vs)[NV], AdamK k, float g0 = 0.f) {
+  adam_vecs_st(c, vs, adam_vecs_ld(c, vs), k, g0);
 }
 
 // ---- cross-lane reductions without LDS ----

@@ -425,15 +425,24 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   const float(&f2s)[8] = p.f2s;
   BAR();
   STAMP(10);
-  // A10 + G11 (df2 = df3 . W2)
-  {
-    const VecG vs[5] = {{B::o.bn_w, 64, 0}, {B::o.bn_b, 64, 1}, {B::o.ln2_w, 64, 2}, {B::o.ln2_b, 64, 3},
-                        {B::o.ff3_b, 64, 4}};
-    adam_vecs(c, vs, K);
-  }
-  gemm_pf<16, 64>(c, TA, LD64, wt2);
+  // A10 + G11 (df2 = df3 . W2).  Every phase below issues its global loads (Adam state, the next
+  // GEMM's weights, saved activations) BEFORE its Adam stores: they share one vmcnt queue (dw_ld)
+  const VecG v10[5] = {{B::o.bn_w, 64, 0}, {B::o.bn_b, 64, 1}, {B::o.ln2_w, 64, 2}, {B::o.ln2_b, 64, 3},
+                       {B::o.ff3_b, 64, 4}};
+  const AdamS s10 = adam_vecs_ld(c, v10);
   WFr<64, 32> wt1;
   wload(wt1, c.BF + B::w.WT1, c.lane);
+  float xh1[16], gm1[16], bt1[16];  // for E12
+  {
+    const int ro = opaque(r * 64 + c0);
+    load16(xh1, c.wsf(B::s.XH1) + ro);
+    load16(gm1, c.P + B::o.ln1_w + c0);
+    load16(bt1, c.P + B::o.ln1_b + c0);
+  }
+  const float rstd1 = c.wsf(B::s.RS)[opaque(r * 16 + q * 4)];
+  const uint32_t m1 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 0];
+  gemm_pf<16, 64>(c, TA, LD64, wt2);
+  adam_vecs_st(c, v10, s10, K);
   WBAR();
   STAMP(11);
   {  // E11: df0 (-> DF0 = XIN region), f2 (-> F2); colsum b1 (v5)
@@ -455,22 +464,26 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = vf;
     colsumW<8>(c, 5, db, q * 8);
   }
-  float xh1[16], gm1[16], bt1[16];
-  {
-    const int ro = opaque(r * 64 + c0);
-    load16(xh1, c.wsf(B::s.XH1) + ro);
-    load16(gm1, c.P + B::o.ln1_w + c0);
-    load16(bt1, c.P + B::o.ln1_b + c0);
-  }
-  const float rstd1 = c.wsf(B::s.RS)[opaque(r * 16 + q * 4)];
-  const uint32_t m1 = ((const gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 0];
   BAR();
   STAMP(12);
-  gemm_pf<64, 32>(c, XIN, LD32, wt1);                    // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
-  gemm_dw_adam<4, 1>(c, TA, LD64, F2, LD32, B::ff3, K);  // dW2 = df3^T f2
-  if (c.tid < FF) adam(c.P, c.M, c.V, B::o.ff0_b + c.tid, cs_total(c, 5, c.tid), K);
+  DwS<4, 1> s2;
+  dw_ld<4, 1>(c, B::ff3, s2);
+  AdamS sb1{};
+  if (c.tid < FF) sb1 = adam_ld(c, B::o.ff0_b + c.tid);
   WFr<64, 64> wto;
   wload(wto, c.BF + B::w.WTo, c.lane);
+  s8v h0a, h0b, aa, ab;  // for E13
+  {
+    const gu16* hb = (const gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
+    h0a = *(const GAS s8v*)hb;
+    h0b = *(const GAS s8v*)(hb + 8);
+    const gu16* abp = (const gu16*)c.wsf(B::s.AB) + opaque(r * 64 + c0);
+    aa = *(const GAS s8v*)abp;
+    ab = *(const GAS s8v*)(abp + 8);
+  }
+  gemm_pf<64, 32>(c, XIN, LD32, wt1);                 // dx1 = df0 . W1 (reads WT1 copy: before W1's Adam)
+  dw_apply<4, 1>(c, TA, LD64, F2, LD32, B::ff3, K, s2);  // dW2 = df3^T f2
+  if (c.tid < FF) adam_st(c, B::o.ff0_b + c.tid, sb1, cs_total(c, 5, c.tid), K);
   WBAR();
   STAMP(13);
   float dh0[16];  // residual gradient into h0, kept in registers until E15
@@ -491,25 +504,17 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     for (int j = 0; j < 16; ++j) t[j] = xh1[j] * gm1[j] + bt1[j];
     store16bf(TC + r * LD64 + c0, t);
   }
-  s8v h0a, h0b, aa, ab;
-  {
-    const gu16* hb = (const gu16*)c.wsf(B::s.H0B) + opaque(r * 64 + c0);
-    h0a = *(const GAS s8v*)hb;
-    h0b = *(const GAS s8v*)(hb + 8);
-    const gu16* abp = (const gu16*)c.wsf(B::s.AB) + opaque(r * 64 + c0);
-    aa = *(const GAS s8v*)abp;
-    ab = *(const GAS s8v*)(abp + 8);
-  }
   BAR();
   STAMP(14);
-  gemm_pf<64, 64>(c, TB, LD64, wto);                      // da = do . Wo
-  gemm_dw_adam<1, 4>(c, XIN, LD32, TC, LD64, B::ff0, K);  // dW1 = df0^T x1
-  {
-    const VecG vs[3] = {{B::o.ln1_w, 64, 0}, {B::o.ln1_b, 64, 1}, {B::o.out_b, 64, 2}};
-    adam_vecs(c, vs, K);
-  }
+  DwS<1, 4> s1;
+  dw_ld<1, 4>(c, B::ff0, s1);
+  const VecG v14[3] = {{B::o.ln1_w, 64, 0}, {B::o.ln1_b, 64, 1}, {B::o.out_b, 64, 2}};
+  const AdamS s14 = adam_vecs_ld(c, v14);
   WFr<64, 64> wtv;
   wload(wtv, c.BF + B::w.WTv, c.lane);
+  gemm_pf<64, 64>(c, TB, LD64, wto);                      // da = do . Wo
+  dw_apply<1, 4>(c, XIN, LD32, TC, LD64, B::ff0, K, s1);  // dW1 = df0^T x1
+  adam_vecs_st(c, v14, s14, K);
   BAR();
   STAMP(15);
   {  // E13: dv (-> TC) ; h0 (-> TA) ; a (-> TD) ; colsum bv (v3)
@@ -527,11 +532,17 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   BAR();
   STAMP(16);
   STAMP(17);
-  gemm_pf<64, 64>(c, TC, LD64, wtv);                       // dh0 part = dv . Wv
-  gemm_dw_adam<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K);  // dWo = do^T a
-  if (c.tid < 64) adam(c.P, c.M, c.V, B::o.inproj_b + 128 + c.tid, cs_total(c, 3, c.tid), K);
+  DwS<4, 4> so;
+  dw_ld<4, 4>(c, B::oproj, so);
+  AdamS sbv{};
+  if (c.tid < 64) sbv = adam_ld(c, B::o.inproj_b + 128 + c.tid);
   float gpd[16];  // gelu'(z0) of the forward
   load16(gpd, c.wsf(B::s.GPD) + opaque(r * 64 + c0));
+  DwS<4, 4> sv;  // for dWv below
+  dw_ld<4, 4>(c, B::vproj, sv);
+  gemm_pf<64, 64>(c, TC, LD64, wtv);                          // dh0 part = dv . Wv
+  dw_apply<4, 4>(c, TB, LD64, TD, LD64, B::oproj, K, so);  // dWo = do^T a
+  if (c.tid < 64) adam_st(c, B::o.inproj_b + 128 + c.tid, sbv, cs_total(c, 3, c.tid), K);
   WBAR();
   STAMP(18);
   {  // E14: dh0 += ACC ; x for dWd
@@ -540,7 +551,11 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     put_x<BR>(c, s);
   }
   WBAR();
-  gemm_dw_adam<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K);  // dWv = dv^T h0
+  DwS<4, 1> sd;  // for dWd below
+  dw_ld<4, 1>(c, B::dense, sd);
+  AdamS sbd{};
+  if (c.tid < 64) sbd = adam_ld(c, B::o.dense_b + c.tid);
+  dw_apply<4, 4>(c, TC, LD64, TA, LD64, B::vproj, K, sv);  // dWv = dv^T h0
   BAR();
   STAMP(19);
   {  // E15: dz0 = dh0 * gelu'(z0) ; colsum bd (v4)
@@ -551,8 +566,8 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     colsum16(c, 4, d);
   }
   BAR();
-  gemm_dw_adam<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K);  // dWd = dz0^T x
-  if (c.tid < 64) adam(c.P, c.M, c.V, B::o.dense_b + c.tid, cs_total(c, 4, c.tid), K);
+  dw_apply<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K, sd);  // dWd = dz0^T x
+  if (c.tid < 64) adam_st(c, B::o.dense_b + c.tid, sbd, cs_total(c, 4, c.tid), K);
   BAR();
   STAMP(20);
 }
@@ -587,9 +602,10 @@ __device__ void init_copies_all(const Ctx& c) {
 // workgroups per client exchanging activations / gradients every step through hand-off slots):
 //   2 workgroups: ROLE 0 = vitals branch + head, ROLE 1 = labs branch;
 //   3 workgroups: ROLE 2 = vitals branch, ROLE 1 = labs branch, ROLE 3 = head.
-// A branch-only workgroup publishes its output (flag XF_VIT / XF_LAB) and waits for d(output)
-// (flag XF_BWD, which also carries the NaN abort); the head publishes both gradients BEFORE its
-// own dWf1 update (and, in the 2-workgroup mode, before the vitals backward) so they overlap.
+// Every wave of a branch-only workgroup publishes its output rows (flags XF_VIT / XF_LAB, one per
+// wave) and waits for its rows of d(output) (XF_BVIT / XF_BLAB, which also carry the NaN abort); the
+// head publishes the gradients BEFORE its own dWf1 update (and, in the 2-workgroup mode, before the
+// vitals backward) so they overlap.
 template <int ROLE>
 __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, unsigned char* smem) {
   constexpr bool DO0 = ROLE == -1 || ROLE == 0 || ROLE == 2;
