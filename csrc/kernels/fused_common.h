@@ -215,15 +215,18 @@ struct MatW {
 // gfx9 counts loads and stores in ONE vmcnt queue, in issue order: a load issued behind a burst of
 // Adam stores waits for their acknowledgements before its data can be used.  So every update below is
 // split into a load part (issue it BEFORE the stores of earlier updates) and an apply part.
-template <int MT, int NTL>
-struct DwS {  // Adam state of this wave's dW tiles (tile t = wave + 8j)
-  static constexpr int T = (MT * NTL + 7) / 8;
-  float p[T][4], m[T][4], v[T][4];
+template <int TS>
+struct DwSt {  // Adam state of up to TS of this wave's dW tiles (tile t = wave + 8j)
+  float p[TS][4], m[TS][4], v[TS][4];
 };
-template <int MT, int NTL, class CT>
-__device__ __forceinline__ void dw_ld(const CT& c, MatW mw, DwS<MT, NTL>& s) {
+template <int MT, int NTL>
+using DwS = DwSt<(MT * NTL + 7) / 8>;
+template <int MT, int NTL, int TS, class CT>
+__device__ __forceinline__ void dw_ld(const CT& c, MatW mw, DwSt<TS>& s) {
+  constexpr int T = (MT * NTL + 7) / 8;
+  static_assert(TS >= T, "state too small");
 #pragma unroll
-  for (int j = 0; j < DwS<MT, NTL>::T; ++j) {
+  for (int j = 0; j < T; ++j) {
     const int t = c.wave + 8 * j;
     if (t >= MT * NTL) break;
     const int mt = t / NTL, nt = t % NTL;
@@ -240,10 +243,11 @@ __device__ __forceinline__ void dw_ld(const CT& c, MatW mw, DwS<MT, NTL>& s) {
   }
 }
 // dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows (all tiles' MFMAs first), then Adam on the real entries
-template <int MT, int NTL, class CT>
+template <int MT, int NTL, int TS, class CT>
 __device__ __forceinline__ void dw_apply(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
-                                         int ldx, MatW mw, AdamK k, DwS<MT, NTL>& s) {
-  constexpr int T = DwS<MT, NTL>::T;
+                                         int ldx, MatW mw, AdamK k, DwSt<TS>& s) {
+  constexpr int T = (MT * NTL + 7) / 8;
+  static_assert(TS >= T, "state too small");
   f4v acc[T];
 #pragma unroll
   for (int j = 0; j < T; ++j) {
