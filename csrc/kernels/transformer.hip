@@ -195,15 +195,22 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   unsigned short* F2 = c.u16(S_F2);
   float* ACC = c.acc();
   int r = c.r, q = c.q, c0 = q * 16;
+  // Parameter loads of each elementwise phase are issued BEFORE the workspace stores of the phases in
+  // front of it (loads and stores share one vmcnt queue, so a load behind stores waits for their acks)
   WFr<64, 32> wd;
   wload(wd, c.BF + B::w.WFd, c.lane);
+  float bias[16], bias_v[16];
+  load16(bias, c.P + B::o.dense_b + c0);
+  load16(bias_v, c.P + B::o.inproj_b + 128 + c0);
   put_x<BR>(c, s);
   WBAR();
   gemm_pf<64, 32>(c, XIN, LD32, wd);
   WFr<64, 64> wv;
   wload(wv, c.BF + B::w.WFv, c.lane);
-  float bias[16];
-  load16(bias, c.P + B::o.dense_b + c0);
+  float bias_o[16], g1[16], b1[16];
+  load16(bias_o, c.P + B::o.out_b + c0);
+  load16(g1, c.P + B::o.ln1_w + c0);
+  load16(b1, c.P + B::o.ln1_b + c0);
   WBAR();
   STAMP(0);
   float h[16];  // h0 stays in registers until the residual (E3)
@@ -223,7 +230,6 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     *(GAS s8v*)hb = a;
     *(GAS s8v*)(hb + 8) = b;
   }
-  load16(bias, c.P + B::o.inproj_b + 128 + c0);
   WBAR();
   gemm_pf<64, 64>(c, TA, LD64, wv);
   WFr<64, 64> wo;
@@ -234,16 +240,14 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     float x[16];
     const float m = keep(s.key, 8 * BR + L_ATT, r, q, THR_P01) ? INV_K01 : 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bias[j]) * m;
+    for (int j = 0; j < 16; ++j) x[j] = (ACC[r * LDACC + c0 + j] + bias_v[j]) * m;
     store16bf(TB + r * LD64 + c0, x);
     gu16* ab = (gu16*)c.wsf(B::s.AB) + opaque(r * 64 + c0);
     *(GAS s8v*)ab = pack8bf(x);
     *(GAS s8v*)(ab + 8) = pack8bf(x + 8);
   }
-  load16(bias, c.P + B::o.out_b + c0);
-  float g1[16], b1[16];
-  load16(g1, c.P + B::o.ln1_w + c0);
-  load16(b1, c.P + B::o.ln1_b + c0);
+  float fb[8];
+  load8(fb, c.P + B::o.ff0_b);  // 6 used (+2 beyond: next tensor, ignored)
   WBAR();
   gemm_pf<64, 64>(c, TB, LD64, wo);
   WFr<16, 64> w1;
@@ -257,7 +261,7 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     ((gu32*)c.wsf(B::s.MK))[opaque(r * 16 + q * 4) + 0] = m1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float o = ACC[r * LDACC + c0 + j] + bias[j];
+      const float o = ACC[r * LDACC + c0 + j] + bias_o[j];
       x1[j] = h[j] + (bit(m1, j) ? o * INV_K01 : 0.f);
     }
     const float rstd = ln_fwd(x1);
@@ -267,39 +271,47 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     for (int j = 0; j < 16; ++j) x1[j] = x1[j] * g1[j] + b1[j];
     store16bf(TC + r * LD64 + c0, x1);
   }
-  float fb[8];
-  load8(fb, c.P + B::o.ff0_b);  // 6 used (+2 beyond: next tensor, ignored)
   WBAR();
   gemm_pf<16, 64>(c, TC, LD64, w1);
   WFr<64, 32> w2;
   wload(w2, c.BF + B::w.WF2, c.lane);
   WBAR();
   STAMP(3);
-  {  // E4: f0 -> f2
-    s8v v;
-    const uint32_t mf = q * 8 < FF ? keep_bits<8>(s.key, 8 * BR + L_DF, r, q * 8, THR_P01) : 0u;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = q * 8 + j;
-      float f2 = 0.f;
-      if (col < FF) {
-        float gp;
-        const float g = gelu_and_grad(ACC[r * LDACC + col] + fb[j & 7], gp);
-        const bool kp = bit(mf, j);
-        f2 = kp ? g * INV_K01 : 0.f;
-        c.wsf(B::s.F0)[opaque(r * 8) + col] = kp ? gp * INV_K01 : 0.f;
-        c.wsf(B::s.F2S)[opaque(r * 8) + col] = f2;
-      }
-      v[j] = (short)f2bf(f2);
-    }
-    *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
-  }
   float g2[16], bb2[16], g3[16], b3[16];
   load16(bias, c.P + B::o.ff3_b + c0);
   load16(g2, c.P + B::o.ln2_w + c0);
   load16(bb2, c.P + B::o.ln2_b + c0);
   load16(g3, c.P + B::o.bn_w + c0);
   load16(b3, c.P + B::o.bn_b + c0);
+  {  // E4: f0 -> f2 (the FF <= 8 real columns live in quarter 0)
+    static_assert(FF <= 8, "E4 keeps the ffn width in one quarter");
+    s8v v;
+    const uint32_t mf = q == 0 ? keep_bits<8>(s.key, 8 * BR + L_DF, r, 0, THR_P01) : 0u;
+    float f0s[8], f2s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f2 = 0.f, f0 = 0.f;
+      if (q == 0 && j < FF) {
+        float gp;
+        const float g = gelu_and_grad(ACC[r * LDACC + j] + fb[j], gp);
+        const bool kp = bit(mf, j);
+        f2 = kp ? g * INV_K01 : 0.f;
+        f0 = kp ? gp * INV_K01 : 0.f;
+      }
+      f0s[j] = f0;
+      f2s[j] = f2;
+      v[j] = (short)f2bf(f2);
+    }
+    if (q == 0) {  // [128][8] rows, two 16-byte stores each (not FF scalar ones: fewer ops for the drain)
+      gf* f0p = c.wsf(B::s.F0) + opaque(r * 8);
+      gf* f2p = c.wsf(B::s.F2S) + opaque(r * 8);
+      *(GAS f4v*)f0p = f4v{f0s[0], f0s[1], f0s[2], f0s[3]};
+      *(GAS f4v*)(f0p + 4) = f4v{f0s[4], f0s[5], f0s[6], f0s[7]};
+      *(GAS f4v*)f2p = f4v{f2s[0], f2s[1], f2s[2], f2s[3]};
+      *(GAS f4v*)(f2p + 4) = f4v{f2s[4], f2s[5], f2s[6], f2s[7]};
+    }
+    *(LDS_AS s8v*)(F2 + r * LD32 + q * 8) = v;
+  }
   WBAR();
   gemm_pf<64, 32>(c, F2, LD32, w2);
   WBAR();
