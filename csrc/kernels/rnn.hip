@@ -208,7 +208,12 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         store8bf(XIN + r * LDX + q * 8, x);
       }
       // ---------------- forward: 3 bidirectional GRU layers (row-local per wave) ----------------
+      // The saved gates of each (layer, direction) are stored only after the NEXT one's weight and
+      // bias loads are issued: loads and stores share one vmcnt queue, so loads behind the stores would
+      // wait for their acknowledgements
       float h3[16];
+      float sr[8], sz[8], sn[8];
+      gf* ssv = nullptr;
 #pragma unroll
       for (int l = 1; l <= 3; ++l) {
         const unsigned short* IN = l == 1 ? XIN : c.u16(l == 2 ? S_H1 : S_H2);
@@ -224,10 +229,20 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           if (l == 1) {
             WFr<96, 32> w;
             wload(w, c.BF + bf_wf(BR, l, d), c.lane);
+            if (ssv) {
+              st8(ssv, sr);
+              st8(ssv + HU, sz);
+              st8(ssv + 2 * HU, sn);
+            }
             gemm_pf<96, 32>(c, IN, LDX, w);
           } else {
             WFr<96, 64> w;
             wload(w, c.BF + bf_wf(BR, l, d), c.lane);
+            if (ssv) {
+              st8(ssv, sr);
+              st8(ssv + HU, sz);
+              st8(ssv + 2 * HU, sn);
+            }
             gemm_pf<96, 64>(c, IN, LDH, w);
           }
           float rr[8], zz[8], nn[8], h[8];
@@ -239,10 +254,13 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
             nn[i] = tanhf(ACC[r * LDACC_R + 2 * HU + j] + bi[2][i] + rr[i] * bh[2][i]);
             h[i] = (1.f - zz[i]) * nn[i];
           }
-          gf* sv = (gf*)sav + SAV_RZN + ((long)((l - 1) * 2 + d) * BM + opaque(r)) * G3 + q * 8;
-          st8(sv, rr);
-          st8(sv + HU, zz);
-          st8(sv + 2 * HU, nn);
+          ssv = (gf*)sav + SAV_RZN + ((long)((l - 1) * 2 + d) * BM + opaque(r)) * G3 + q * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            sr[i] = rr[i];
+            sz[i] = zz[i];
+            sn[i] = nn[i];
+          }
           if (l < 3) {  // layer 1/2 outputs stay in LDS: next layer's input and its dW operand
             store8bf(HOUT + r * LDH + d * HU + q * 8, h);
           } else {
@@ -261,6 +279,9 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         load8(*(float(*)[8])(lgm + 8), c.P + B::ln_w + HU + q * 8);
         load8(*(float(*)[8])bt, c.P + B::ln_b + q * 8);
         load8(*(float(*)[8])(bt + 8), c.P + B::ln_b + HU + q * 8);
+        st8(ssv, sr);  // the last (layer, direction)'s saved gates
+        st8(ssv + HU, sz);
+        st8(ssv + 2 * HU, sn);
         lrstd = ln_fwd(h3);  // h3 -> xhat
         float y[16];
 #pragma unroll
