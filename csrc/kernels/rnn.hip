@@ -357,6 +357,8 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         const VecG vs[2] = {{B::ln_w, 64, 0}, {B::ln_b, 64, 1}};
         adam_vecs(c, vs, K);
       }
+      WFr<64, 96> wdx;  // W_ih^T fragments of the dX GEMMs: the first one here, each next one right after
+      wload(wdx, c.BF + bf_wt(BR, 3, 0), c.lane);  // the previous dX GEMM (before that matrix's Adam stores)
 #pragma unroll
       for (int l = 3; l >= 1; --l) {
         const unsigned short* IN = l == 1 ? XIN : c.u16(l == 2 ? S_H1 : S_H2);
@@ -365,8 +367,6 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         for (int i = 0; i < 16; ++i) dsum[i] = 0.f;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          WFr<64, 96> wdx;  // W_ih^T fragments of the dX GEMM below: issued before the gate math
-          if (l > 1) wload(wdx, c.BF + bf_wt(BR, l, d), c.lane);
           {  // gate backward for direction d: dgi (-> DGI), bias-gradient colsums v2 (r | z), v3 (n | n*r)
             // this (layer, direction)'s saved gates were loaded one iteration ahead (the first before
             // the wait for the head); issue the next one's loads now, behind this iteration's GEMMs
@@ -406,6 +406,10 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           q = c.q;
           if (l > 1) {  // d(layer input) += dgi . W_ih (transposed copy, before this matrix's Adam)
             gemm_pf<64, 96>(c, DGI, LDD, wdx);
+            {
+              const int nl = d == 0 ? l : l - 1, ndr = d == 0 ? 1 : 0;
+              if (nl > 1) wload(wdx, c.BF + bf_wt(BR, nl, ndr), c.lane);
+            }
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               dsum[i] += ACC[r * LDACC_R + q * 8 + i];
@@ -418,15 +422,14 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
           // dW_ih = dgi^T x (Adam fused), then the two bias vectors
           const MatW mw{B::wih(l, d), G3, B::kin(l), bf_wf(BR, l, d), l == 1 ? 32 : 64, l == 1 ? -1 : bf_wt(BR, l, d),
                         G3};
+          const VecG vs[4] = {{B::bih(l, d), 64, 2}, {B::bih(l, d) + 64, 32, 3}, {B::bhh(l, d), 64, 2},
+                              {B::bhh(l, d) + 64, 32, 3, 32}};
+          const AdamS sb = adam_vecs_ld(c, vs);  // the biases' state before the matrix's stores
           if (l == 1)
             gemm_dw_adam<6, 2>(c, DGI, LDD, IN, LDX, mw, K);
           else
             gemm_dw_adam<6, 4>(c, DGI, LDD, IN, LDH, mw, K);
-          {
-            const VecG vs[4] = {{B::bih(l, d), 64, 2}, {B::bih(l, d) + 64, 32, 3}, {B::bhh(l, d), 64, 2},
-                                {B::bhh(l, d) + 64, 32, 3, 32}};
-            adam_vecs(c, vs, K);
-          }
+          adam_vecs_st(c, vs, sb, K);
           c.bar();
           r = c.r;
           q = c.q;
