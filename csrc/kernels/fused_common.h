@@ -243,9 +243,11 @@ __device__ __forceinline__ void dw_ld(const CT& c, MatW mw, DwSt<TS>& s) {
   }
 }
 // dW[n][k] = sum_b DY[b][n] X[b][k] over 128 rows (all tiles' MFMAs first), then Adam on the real entries
+// img (optional): an LDS copy [n][img_ld] of the bf16 weight that also receives the updated values
 template <int MT, int NTL, int TS, class CT>
 __device__ __forceinline__ void dw_apply(const CT& c, const unsigned short* DY, int ldy, const unsigned short* X,
-                                         int ldx, MatW mw, AdamK k, DwSt<TS>& s) {
+                                         int ldx, MatW mw, AdamK k, DwSt<TS>& s, unsigned short* img = nullptr,
+                                         int img_ld = 0) {
   constexpr int T = (MT * NTL + 7) / 8;
   static_assert(TS >= T, "state too small");
   f4v acc[T];
@@ -285,6 +287,7 @@ __device__ __forceinline__ void dw_apply(const CT& c, const unsigned short* DY, 
         const unsigned short h = f2bf(pn);
         hv[i] = h;
         c.BF[mw.wf + n * mw.wf_ld + kk] = h;
+        if (img) img[n * img_ld + kk] = h;
         if (mw.wt >= 0 && !vec_t) c.BF[mw.wt + kk * mw.wt_ld + n] = h;
       }
     }

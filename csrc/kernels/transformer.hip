@@ -55,6 +55,12 @@ constexpr int S_DY3 = S_LAB + BM * 4;             // 158208
 constexpr int S_RED = S_DY3 + BM * 4;             // 158720
 constexpr int S_TOTAL = S_RED + 16 * 4;           // 158784
 static_assert(S_TOTAL <= 160 * 1024, "LDS budget");
+// Branch-only workgroups: bf16 image [64][LDW] of the dense weight inside the CAT region (past TD,
+// which those workgroups never use as CAT).  The dWd Adam epilogue writes the updated weights here, so
+// the next step's first GEMM reads them from LDS instead of waiting for the stores and a global reload.
+constexpr int LDW = 40;
+constexpr int S_WDI = S_CAT + BM * LD64 * 2;      // 118784
+static_assert(S_WDI + 64 * LDW * 2 <= S_F2, "dense image fits behind TD");
 
 // ---- workspace layout (float units) ----
 constexpr long W_M = 0, W_V = NPARAM;
@@ -198,7 +204,12 @@ __device__ __forceinline__ void fwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   // Parameter loads of each elementwise phase are issued BEFORE the workspace stores of the phases in
   // front of it (loads and stores share one vmcnt queue, so a load behind stores waits for their acks)
   WFr<64, 32> wd;
-  wload(wd, c.BF + B::w.WFd, c.lane);
+  if (XCH) {  // branch-only workgroup: the LDS image the last dWd epilogue wrote
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wd.f[t][0] = lds_row_frag(c.u16(S_WDI), LDW, 16 * t, 0, c.lane);
+  } else {
+    wload(wd, c.BF + B::w.WFd, c.lane);
+  }
   float bias[16], bias_v[16];
   load16(bias, c.P + B::o.dense_b + c0);
   load16(bias_v, c.P + B::o.inproj_b + 128 + c0);
@@ -578,7 +589,8 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
     colsum16(c, 4, d);
   }
   BAR();
-  dw_apply<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K, sd);  // dWd = dz0^T x
+  // dWd = dz0^T x (branch-only workgroups also refresh the LDS image the next forward reads)
+  dw_apply<4, 1>(c, TB, LD64, XIN, LD32, B::dense, K, sd, DY == 2 ? c.u16(S_WDI) : nullptr, LDW);
   if (c.tid < 64) adam_st(c, B::o.dense_b + c.tid, sbd, cs_total(c, 4, c.tid), K);
   BAR();
   STAMP(20);
@@ -665,6 +677,11 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
     init_copies(c, MFC2);
   }
   __syncthreads();
+  if (BONLY >= 0) {  // the dense weight's LDS image (see S_WDI), from the bf16 copy just written
+    constexpr int WFD = BrC<BONLY < 0 ? 0 : BONLY>::w.WFd;
+    for (int i = tid; i < 64 * 32; i += NT) c.u16(S_WDI)[(i >> 5) * LDW + (i & 31)] = c.BF[WFD + i];
+    __syncthreads();
+  }
   gu32* xflag = (gu32*)(a.sync ? a.sync + (long)cid * AFL_TF_SYNC_WORDS : nullptr);  // XF_* words
   bool timed_out = false;
 
