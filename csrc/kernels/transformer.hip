@@ -371,6 +371,7 @@ struct BwdPre {
   uint32_t m2;
   float gk[8], f2s[8];  // drop'(.) * gelu'(f0) and f2 of the forward
   WFr<16, 64> wt2;
+  bool abort = false;  // DY == 2: this wave's d(output) flag carried the head's NaN abort
 };
 template <int BR>
 __device__ __forceinline__ void bwd_prefetch(const Ctx& c, BwdPre& p) {
@@ -392,8 +393,11 @@ __device__ __forceinline__ void bwd_prefetch(const Ctx& c, BwdPre& p) {
 
 // on entry: dx3 of this branch in ACC (DY == 0), the DX3V workspace (DY == 1) or the hand-off slot W_XB
 // (DY == 2, branch-parallel mode, after the acquire); p from bwd_prefetch<BR>
+// Returns true when the step is aborted (DY == 2: some wave's hand-off flag carried the head's NaN
+// abort -- the head raises it per wave, from that wave's rows; the OR is taken at the first barrier,
+// before anything is written outside LDS, so an aborted client keeps its pre-step parameters).
 template <int BR, int DY>
-__device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, const BwdPre& p) {
+__device__ __forceinline__ bool bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint64_t& t_prev, const BwdPre& p) {
   using B = BrC<BR>;
   unsigned short* XIN = c.u16(S_XIN);  // also DF0
   unsigned short* TA = c.u16(S_TA);
@@ -446,7 +450,15 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   }
   const float(&gk)[8] = p.gk;  // drop'(.) * gelu'(f0) and f2 of the forward
   const float(&f2s)[8] = p.f2s;
+  uint32_t* abort_w = (uint32_t*)(c.smem + S_RED) + 8;  // one word per wave (RED is head-only)
+  if (DY == 2 && c.lane == 0) abort_w[c.wave] = p.abort ? 1u : 0u;
   BAR();
+  if (DY == 2) {
+    uint32_t any = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) any |= abort_w[w];
+    if (any) return true;
+  }
   STAMP(10);
   // A10 + G11 (df2 = df3 . W2).  Every phase below issues its global loads (Adam state, the next
   // GEMM's weights, saved activations) BEFORE its Adam stores: they share one vmcnt queue (dw_ld)
@@ -594,6 +606,7 @@ __device__ __forceinline__ void bwd_branch(Ctx& c, St& s, uint64_t* stamps, uint
   if (c.tid < 64) adam_st(c, B::o.dense_b + c.tid, sbd, cs_total(c, 4, c.tid), K);
   BAR();
   STAMP(20);
+  return false;
 }
 
 }  // namespace
@@ -786,12 +799,12 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
           failed = true;
           break;
         }
-        if (v & 1u) {  // the head saw a NaN loss: the client's round fails
+        pre.abort = (v & 1u) != 0;  // the head saw a NaN in this wave's rows
+        STAMP(21);
+        if (bwd_branch<BONLY < 0 ? 0 : BONLY, 2>(c, s, stamps, t_prev, pre)) {  // the client's round fails
           failed = true;
           break;
         }
-        STAMP(21);
-        bwd_branch<BONLY < 0 ? 0 : BONLY, 2>(c, s, stamps, t_prev, pre);
         c.full_sync();
         continue;
       }
@@ -848,6 +861,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       wload(wtf2, c.BF + WTF2, c.lane);
       WBAR();
       STAMP(7);
+      uint32_t wave_nan = 0;  // this wave's rows produced a NaN loss term
       {  // E7: y2, g2, y3, sigmoid, BCE, dy3, dy2 ; colsums dWout (v0), dbf2 (v1)
         float gp2[8], g2[8], dot = 0.f;
         const int cc = q * 8;
@@ -883,14 +897,21 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         colsumW<8>(c, 1, dy2, cc);
         float lsum = wave_sum(q == 0 ? lrow : 0.f);
         if (c.lane == 0) RED[c.wave] = lsum;
+        wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
       }
-      BAR();
-      {
+      // The 3-workgroup head takes the loss (and the NaN decision) only after the gradient hand-off:
+      // every wave goes on with its own rows, flags its rows' NaN in its hand-off word, and the
+      // branches OR those before they write anything (bwd_branch).  loss is NaN <=> some row's is.
+      auto take_loss = [&]() {
         float tot = 0.f;
         for (int w = 0; w < 8; ++w) tot += RED[w];
         const float loss = tot / (float)Bn;
         if (loss != loss) failed = true;  // uniform across the workgroup
         else epoch_loss += loss;
+      };
+      if (ROLE != 3) {
+        BAR();
+        take_loss();
       }
       if (failed) {
         if (ROLE == 0 || ROLE == 3) {  // release them (every wave its rows' flags)
@@ -933,7 +954,7 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       WBAR();
       if (ROLE == 3) {  // vitals gradient -> its hand-off slot, released row-wave by row-wave
         put_grad(c, W_XB, r, c0);
-        wave_publish(c, xf(xflag, XF_BVIT, c.wave), (uint32_t)step << 1);
+        wave_publish(c, xf(xflag, XF_BVIT, c.wave), ((uint32_t)step << 1) | wave_nan);
       } else {
         float t[16];
 #pragma unroll
@@ -945,8 +966,12 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       if (ROLE == -1) BAR(); else WBAR();  // ROLE -1: dWf1 below reads every wave's TB rows
       if (ROLE == 0 || ROLE == 3) {  // hand the gradients over first: the head's own updates overlap
         put_grad(c, W_XB + BM * 64, r, c0);
-        wave_publish(c, xf(xflag, XF_BLAB, c.wave), (uint32_t)step << 1);
+        wave_publish(c, xf(xflag, XF_BLAB, c.wave), ((uint32_t)step << 1) | (ROLE == 3 ? wave_nan : 0u));
         BAR();  // the updates below read every wave's E8 column sums and TB rows
+        if (ROLE == 3) {
+          take_loss();
+          if (failed) break;  // before any of the head's own updates
+        }
         head_vec_adam();
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
         if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
