@@ -326,10 +326,13 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
       gate_prefetch(3, 0);  // the first gate backward's saved gates / bias, also before the wait
       gu32* fb = xf(xflag, BR == 0 ? XF_BVIT : XF_BLAB, c.wave);  // this wave's rows of d(output)
       const uint32_t v = wave_wait(c, fb, fb, (uint32_t)step, 1, xflag + XF_TMO);
-      if (v == 0xFFFFFFFFu || (v & 1u)) {  // timeout, or the head saw a NaN loss
+      if (v == 0xFFFFFFFFu) {  // timeout
         failed = true;
         break;
       }
+      // the head flags a NaN loss term per wave of rows; the OR is taken at the first barrier below,
+      // before anything leaves LDS, so an aborted client keeps its pre-step parameters
+      const uint32_t my_abort = v & 1u;
       // ---------------- backward ----------------
       float dh[16];
       {  // d(branch output) -> dropout' -> LayerNorm backward; colsums gamma (v0), beta (v1)
@@ -352,7 +355,18 @@ __device__ __forceinline__ void branch_body(const AflTfTrainArgs& a, int cid, un
         colsumW<8>(c, 1, *(const float(*)[8])(dy + 8), HU + q * 8);
         ln_bwd(dh, dy, xh, rstd, gm);
       }
+      uint32_t* abort_w = (uint32_t*)(smem + S_RED) + 8;  // one word per wave (RED is head-only)
+      if (c.lane == 0) abort_w[c.wave] = my_abort;
       __syncthreads();
+      {
+        uint32_t any = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) any |= abort_w[w];
+        if (any) {  // the client's round fails
+          failed = true;
+          break;
+        }
+      }
       {
         const VecG vs[2] = {{B::ln_w, 64, 0}, {B::ln_b, 64, 1}};
         adam_vecs(c, vs, K);
@@ -535,6 +549,7 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       gemm_pf<16, 32>(c, T1, LDX, w2);  // fc2
       WFr<32, 32> wt2;
       wload(wt2, c.BF + WT2, c.lane);
+      uint32_t wave_nan = 0;  // this wave's rows produced a NaN loss term
       {  // fc2 relu, output, sigmoid + BCE, d(out), d(fc2) ; colsums dW_out (v0), db2 (v1)
         float f2[4], dot = 0.f;
 #pragma unroll
@@ -567,20 +582,11 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
         colsumW<4>(c, 1, *(const float(*)[4])d2, q * 4);
         const float lsum = wave_sum(q == 0 ? lrow : 0.f);
         if (c.lane == 0) RED[c.wave] = lsum;
+        wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
       }
-      __syncthreads();
-      {
-        float tot = 0.f;
-        for (int w = 0; w < 8; ++w) tot += RED[w];
-        const float loss = tot / (float)Bn;
-        if (loss != loss) failed = true;
-        else epoch_loss += loss;
-      }
-      if (failed) {
-        wave_publish(c, xf(xflag, XF_BVIT, c.wave), ((uint32_t)step << 1) | 1u);  // release the branch workgroups
-        wave_publish(c, xf(xflag, XF_BLAB, c.wave), ((uint32_t)step << 1) | 1u);
-        break;
-      }
+      // The loss (and the NaN decision) is taken only after the gradient hand-off: every wave goes on
+      // with its own rows and flags its rows' NaN in its hand-off words; the branches OR those before
+      // they write anything.  loss is NaN <=> some row's term is.
       gemm_pf<32, 32>(c, T2D, LDX, wt2);  // d(fc1 out) = d(fc2 out) . W2
       WFr<64, 32> wa, wb;
       wload(wa, c.BF + WT1, c.lane);
@@ -594,13 +600,21 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       }
       gemm_pf<64, 32>(c, T1D, LDX, wa);  // d(vitals output) = d1 . W1[:, 0:64]
       put_grad(c, W_XB, r, q * 16);
-      wave_publish(c, xf(xflag, XF_BVIT, c.wave), (uint32_t)step << 1);
+      wave_publish(c, xf(xflag, XF_BVIT, c.wave), ((uint32_t)step << 1) | wave_nan);
       gemm_pf<64, 32>(c, T1D, LDX, wb);  // d(labs output)
       put_grad(c, W_XB + BM * 64, r, q * 16);
-      wave_publish(c, xf(xflag, XF_BLAB, c.wave), (uint32_t)step << 1);
+      wave_publish(c, xf(xflag, XF_BLAB, c.wave), ((uint32_t)step << 1) | wave_nan);
       c.bar();  // the updates below read every wave's rows and column sums
       r = c.r;
       q = c.q;
+      {
+        float tot = 0.f;
+        for (int w = 0; w < 8; ++w) tot += RED[w];
+        const float loss = tot / (float)Bn;
+        if (loss != loss) failed = true;  // uniform: before any of the head's own updates
+        else epoch_loss += loss;
+      }
+      if (failed) break;
       {  // output-layer / fc2-bias Adam (colsum slots 0, 1, DY3): off the way to the branch gradients
         float sm = 0.f;
         if (tid == 32)
