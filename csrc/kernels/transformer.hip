@@ -812,6 +812,10 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       // latency overlaps the wait instead of sitting on the critical path after it
       WFr<64, 128> wf1;
       wload(wf1, c.BF + WFF1, c.lane);
+      WFr<32, 64> wf2;  // and the next two GEMMs' (small) fragments; the two dcat halves' are issued as
+      wload(wf2, c.BF + WFF2, c.lane);  // soon as fc1 / fc2 free their registers, so no load of them
+      WFr<64, 32> wtf2;                 // sits behind the gradient hand-off's drain
+      wload(wtf2, c.BF + WTF2, c.lane);
       float bias[16];
       load16(bias, c.P + FC1_B + q * 16);
       if (ROLE == 0 || ROLE == 3) {  // branch outputs from the other workgroup(s) -> CAT
@@ -834,8 +838,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       }
       // =============================== head forward + loss ===============================
       gemm_pf<64, 128>(c, CAT, LD128, wf1);
-      WFr<32, 64> wf2;
-      wload(wf2, c.BF + WFF2, c.lane);
+      WFr<64, 64> wtf1a;
+      wload(wtf1a, c.BF + WTF1, c.lane);
       WBAR();
       STAMP(6);
       float gk1[16];  // drop'(.) * gelu'(y1), kept in registers until E8
@@ -857,8 +861,8 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
       const float bout = c.P[OUT_B];
       WBAR();
       gemm_pf<32, 64>(c, TA, LD64, wf2);
-      WFr<64, 32> wtf2;
-      wload(wtf2, c.BF + WTF2, c.lane);
+      WFr<64, 64> wtf1b;
+      wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
       WBAR();
       STAMP(7);
       uint32_t wave_nan = 0;  // this wave's rows produced a NaN loss term
@@ -931,8 +935,6 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         adam_vecs(c, vs, K, sm);
       };
       gemm_pf<64, 32>(c, F2, LD32, wtf2);  // dd1 = dy2 . Wf2
-      WFr<64, 64> wtf1a;
-      wload(wtf1a, c.BF + WTF1, c.lane);
       WBAR();
       STAMP(8);
       {  // E8: dy1 = drop'(dd1) * gelu'(y1) ; colsum dbf1 (v2)
@@ -949,8 +951,6 @@ __device__ __forceinline__ void train_body(const AflTfTrainArgs& a, int cid, uns
         gemm_dw_adam<2, 4>(c, F2, LD32, TA, LD64, MFC2, K);  // dWf2 = dy2^T d1
         if (tid < 64) adam(c.P, c.M, c.V, FC1_B + tid, cs_total(c, 2, tid), K);
       }
-      WFr<64, 64> wtf1b;
-      wload(wtf1b, c.BF + WTF1 + 64 * 64, c.lane);
       WBAR();
       if (ROLE == 3) {  // vitals gradient -> its hand-off slot, released row-wave by row-wave
         put_grad(c, W_XB, r, c0);
