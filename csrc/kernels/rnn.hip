@@ -517,6 +517,15 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       // weights and biases for the whole head forward, issued before the wait
       WFr<32, 128> w1;
       wload(w1, c.BF + WF1, c.lane);
+      // every other GEMM's fragments of this step too (small): none is then loaded behind the
+      // gradient hand-off's drain or on the way to it
+      WFr<16, 32> w2;
+      wload(w2, c.BF + WF2, c.lane);
+      WFr<32, 32> wt2;
+      wload(wt2, c.BF + WT2, c.lane);
+      WFr<64, 32> wa, wb;
+      wload(wa, c.BF + WT1, c.lane);
+      wload(wb, c.BF + WT1 + 64 * 32, c.lane);
       float b1[8], b2[4], wo[4];
       load8(b1, c.P + FC1_B + q * 8);
 #pragma unroll
@@ -540,15 +549,11 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
         *(LDS_AS s8v*)(CAT + r * LDC + br * 64 + q * 16 + 8) = __builtin_bit_cast(s8v, hi);
       }
       gemm_pf<32, 128>(c, CAT, LDC, w1);  // fc1 (row-local)
-      WFr<16, 32> w2;
-      wload(w2, c.BF + WF2, c.lane);
       float f1[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) f1[i] = relu_nan(ACC[r * LDACC_R + q * 8 + i] + b1[i]);
       store8bf(T1 + r * LDX + q * 8, f1);
       gemm_pf<16, 32>(c, T1, LDX, w2);  // fc2
-      WFr<32, 32> wt2;
-      wload(wt2, c.BF + WT2, c.lane);
       uint32_t wave_nan = 0;  // this wave's rows produced a NaN loss term
       {  // fc2 relu, output, sigmoid + BCE, d(out), d(fc2) ; colsums dW_out (v0), db2 (v1)
         float f2[4], dot = 0.f;
@@ -588,9 +593,6 @@ __device__ __forceinline__ void head_body(const AflTfTrainArgs& a, int cid, unsi
       // with its own rows and flags its rows' NaN in its hand-off words; the branches OR those before
       // they write anything.  loss is NaN <=> some row's term is.
       gemm_pf<32, 32>(c, T2D, LDX, wt2);  // d(fc1 out) = d(fc2 out) . W2
-      WFr<64, 32> wa, wb;
-      wload(wa, c.BF + WT1, c.lane);
-      wload(wb, c.BF + WT1 + 64 * 32, c.lane);
       {
         float d1[8];
 #pragma unroll
