@@ -7,7 +7,8 @@
 // Both are 6-round balanced Feistel networks on the smallest even bit-width domain covering n, with
 // cycle walking back into [0, n) (a bijection of [0, 2^k) restricted to [0, n) by walking the cycle).
 // No sort, no host work: one launch builds the whole [C, E, maxnd] plan.  The integer math is
-// mirrored bit-for-bit by attackfl_amd/fl/trainers.py:_feistel_plan_cpu.
+// mirrored bit-for-bit by attackfl_amd/fl/trainers.py:_feistel_plan (CPU branch); the helpers are
+// __host__ __device__ so csrc/host/host_check.hip can run them under ASan/UBSan on the CPU.
 #include "common.h"
 #include "kernels.h"
 
@@ -22,7 +23,7 @@ __host__ __device__ __forceinline__ uint32_t pl_mix(uint32_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint32_t pl_feistel(uint32_t x, int half, uint32_t mask, uint32_t k0, uint32_t k1) {
+__host__ __device__ __forceinline__ uint32_t pl_feistel(uint32_t x, int half, uint32_t mask, uint32_t k0, uint32_t k1) {
   uint32_t L = x >> half, R = x & mask;
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
@@ -34,7 +35,7 @@ __device__ __forceinline__ uint32_t pl_feistel(uint32_t x, int half, uint32_t ma
   return (L << half) | R;
 }
 
-__device__ __forceinline__ uint32_t pl_perm(uint32_t x, uint32_t n, int half, uint32_t k0, uint32_t k1) {
+__host__ __device__ __forceinline__ uint32_t pl_perm(uint32_t x, uint32_t n, int half, uint32_t k0, uint32_t k1) {
   const uint32_t mask = (1u << half) - 1u;
   do {
     x = pl_feistel(x, half, mask, k0, k1);
@@ -48,6 +49,20 @@ __host__ __device__ __forceinline__ int pl_half_bits(uint32_t n) {
   return k / 2;
 }
 
+// subset keys (s0, s1) of a client seed and shuffle keys (e0, e1) of its epoch e
+struct PlanKeys {
+  uint32_t s0, s1, e0, e1;
+};
+__host__ __device__ __forceinline__ PlanKeys pl_keys(uint64_t s, int e) {
+  const uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
+  PlanKeys k;
+  k.s0 = pl_mix(lo ^ 0x5BD1E995u);
+  k.s1 = pl_mix(hi ^ 0x27D4EB2Fu);
+  k.e0 = pl_mix(k.s0 ^ (0x165667B1u * (uint32_t)(e + 1)));
+  k.e1 = pl_mix(k.s1 + 0xD3A2646Cu * (uint32_t)(e + 1));
+  return k;
+}
+
 __global__ void __launch_bounds__(256) k_make_plan(const uint64_t* __restrict__ seeds, const int* __restrict__ nd,
                                                    int n_train, int E, int maxnd, int* __restrict__ order) {
   const int c = blockIdx.z, e = blockIdx.y;
@@ -59,12 +74,9 @@ __global__ void __launch_bounds__(256) k_make_plan(const uint64_t* __restrict__ 
     out[i] = 0;  // padding (never visited): a valid row index
     return;
   }
-  const uint64_t s = seeds[c];
-  const uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
-  const uint32_t ks0 = pl_mix(lo ^ 0x5BD1E995u), ks1 = pl_mix(hi ^ 0x27D4EB2Fu);
-  const uint32_t ke0 = pl_mix(ks0 ^ (0x165667B1u * (uint32_t)(e + 1))), ke1 = pl_mix(ks1 + 0xD3A2646Cu * (uint32_t)(e + 1));
-  const uint32_t j = pl_perm((uint32_t)i, (uint32_t)n, pl_half_bits((uint32_t)n), ke0, ke1);
-  out[i] = (int)pl_perm(j, (uint32_t)n_train, pl_half_bits((uint32_t)n_train), ks0, ks1);
+  const PlanKeys k = pl_keys(seeds[c], e);
+  const uint32_t j = pl_perm((uint32_t)i, (uint32_t)n, pl_half_bits((uint32_t)n), k.e0, k.e1);
+  out[i] = (int)pl_perm(j, (uint32_t)n_train, pl_half_bits((uint32_t)n_train), k.s0, k.s1);
 }
 
 }  // namespace
