@@ -9,6 +9,9 @@
 * ``synthetic_icu`` / ``synthetic_har`` — deterministic synthetic data with a planted signal
   (the reference's pickles are not shipped: ``.MISSING_LARGE_BLOBS``), including ``-2.0``
   missing-value markers that ``RNNModel`` masks.
+* ``ImageData`` / ``load_cifar10_bin`` / ``synthetic_cifar10`` — the reference's CIFAR10 test path
+  (``src/Validation.py:38-44``: ``ToTensor`` + ``Normalize(0.5, 0.5)``) read from the raw-byte
+  ``cifar-10-batches-bin`` layout (no pickles, no download), or synthetic images of that shape.
 * ``DeviceTable`` — the whole train set resident on device as one ``[N, 24]`` fp32 row table
   (vitals | labs | label), from which fused trainers gather batches by index.
 """
@@ -151,6 +154,49 @@ def synthetic_har(n: int, seed: int = 1234, split_seed: int = 0, length: int = 5
     return HARData(x, y)
 
 
+class ImageData(Dataset):
+    """``x [N, 3, 32, 32]`` fp32 (already normalised to [-1, 1]), ``y [N]`` int64 class labels."""
+
+    def __init__(self, x, y):
+        self.x = torch.as_tensor(x, dtype=torch.float32)
+        self.y = torch.as_tensor(y, dtype=torch.long)
+
+    def __len__(self):
+        return self.x.shape[0]
+
+    def __getitem__(self, i):
+        return self.x[i], self.y[i]
+
+
+CIFAR_FILES = {"train": [f"data_batch_{i}.bin" for i in range(1, 6)], "test": ["test_batch.bin"]}
+
+
+def load_cifar10_bin(root: str, split: str = "test") -> ImageData:
+    """CIFAR-10 binary batches: records of 1 label byte + 3072 pixel bytes (R, G, B planes, 32x32).
+
+    Pixels map through ``ToTensor`` (/255) then ``Normalize((0.5,)*3, (0.5,)*3)`` exactly like the
+    reference's ``transform_test`` (``src/Validation.py:39-42``).
+    """
+    recs = []
+    for name in CIFAR_FILES[split]:
+        raw = np.fromfile(os.path.join(root, name), dtype=np.uint8)
+        if raw.size % 3073:
+            raise ValueError(f"{name}: size {raw.size} is not a multiple of the 3073-byte CIFAR record")
+        recs.append(raw.reshape(-1, 3073))
+    r = np.concatenate(recs, 0)
+    x = (r[:, 1:].reshape(-1, 3, 32, 32).astype(np.float32) / 255.0 - 0.5) / 0.5
+    return ImageData(x, r[:, 0].astype(np.int64))
+
+
+def synthetic_cifar10(n: int, seed: int = 1234, split_seed: int = 0, classes: int = 10) -> ImageData:
+    rs = np.random.RandomState(seed)
+    protos = rs.uniform(-1, 1, (classes, 3, 32, 32)).astype(np.float32)
+    rs2 = np.random.RandomState(seed * 31 + split_seed + 11)
+    y = rs2.randint(0, classes, n)
+    x = np.clip(protos[y] * 0.6 + rs2.normal(0, 0.4, (n, 3, 32, 32)).astype(np.float32), -1, 1)
+    return ImageData(x, y)
+
+
 # ----------------------------------------------------------------------------------------------
 # dataset resolution (reference file locations, or synthetic)
 # ----------------------------------------------------------------------------------------------
@@ -177,6 +223,14 @@ def resolve_dataset(data_name: str, split: str, data_cfg: Optional[dict] = None,
                 return load_pickled_dataset(p)
         if mode in ("false", "0", "no"):
             raise FileNotFoundError(f"no {data_name}/{split} pickle under {root} and data.synthetic is false")
+    if data_name == "CIFAR10" and mode in ("auto", "false", "0", "no"):
+        d = os.path.join(root, "data", "cifar-10-batches-bin")
+        if all(os.path.exists(os.path.join(d, f)) for f in CIFAR_FILES[split]):
+            if verbose:
+                print_with_color(f"Loading CIFAR10/{split} from {d}", "green")
+            return load_cifar10_bin(d, split)
+        if mode in ("false", "0", "no"):
+            raise FileNotFoundError(f"no CIFAR10 binary batches under {d} and data.synthetic is false")
     seed = int(cfg.get("seed", 1234))
     split_seed = 0 if split == "train" else 1
     if data_name == "ICU":
@@ -185,6 +239,9 @@ def resolve_dataset(data_name: str, split: str, data_cfg: Optional[dict] = None,
     if data_name == "HAR":
         n = int(cfg.get("har-train-size" if split == "train" else "har-test-size", 2048 if split == "train" else 512))
         return synthetic_har(n, seed=seed, split_seed=split_seed)
+    if data_name == "CIFAR10":
+        n = int(cfg.get("cifar-train-size" if split == "train" else "cifar-test-size", 2048 if split == "train" else 512))
+        return synthetic_cifar10(n, seed=seed, split_seed=split_seed)
     raise ValueError(f"Data name '{data_name}' is not valid.")
 
 
@@ -205,6 +262,11 @@ class DeviceTable:
             self.x = ds.x.reshape(len(ds), -1).contiguous().to(self.device)
             self.y = ds.y.to(self.device)
             self.n = self.x.shape[0]
+        elif isinstance(ds, ImageData):
+            self.kind = "IMAGE"
+            self.x = ds.x.contiguous().to(self.device)
+            self.y = ds.y.to(self.device)
+            self.n = self.x.shape[0]
         elif isinstance(ds, TensorDataset):
             self.kind = "HAR"
             x, y = ds.tensors[0], ds.tensors[1]
@@ -217,6 +279,9 @@ class DeviceTable:
     def icu_batch(self, idx: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         r = self.rows.index_select(0, idx)
         return r[:, :VITALS_DIM], r[:, VITALS_DIM:VITALS_DIM + LABS_DIM], r[:, -1]
+
+    def image_batch(self, idx: torch.Tensor):
+        return self.x.index_select(0, idx), self.y.index_select(0, idx)
 
     def har_batch(self, idx: torch.Tensor):
         return self.x.index_select(0, idx)[:, None, :], self.y.index_select(0, idx)

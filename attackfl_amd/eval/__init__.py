@@ -1,7 +1,10 @@
 """Server-side validation (reference ``src/Validation.py:19-214``).
 
 ICU: ROC-AUC over the whole test set (``ROC_AUC: x.xxxx`` in ``app.log``); NaN outputs fail the
-round.  HAR: accuracy.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
+round.  HAR: accuracy.  CIFAR10 (``test_image`` / ``test_hyper_image``, ``src/Validation.py:69-90,
+147-175``): summed NLL of the model's log-probabilities over the test set divided by its length, and
+``100 * correct / len`` accuracy; a NaN or ``|loss| > 1e6`` fails the round.  The hyper variant
+pools every client's loss and hits but still divides by ONE test-set length, like the reference.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
 model before one ROC-AUC, like ``test_hyper_icu``.  The test set stays resident on the device
 and is evaluated in one pass (eval mode is batch-size independent).  On GPU every model runs a
 native forward: TransformerModel the fused HIP eval kernel, CNNModel / RNNModel /
@@ -33,8 +36,6 @@ class Validation:
         self.verbose = verbose
         self.model = build_model(model_name, seed=0).to(self.device).eval()
         self.layout = ParamLayout.from_state_dict(self.model.state_dict())
-        if data_name == "CIFAR10":
-            raise ValueError("CIFAR10 validation needs torchvision downloads, which this framework does not do")
         ds = dataset if dataset is not None else resolve_dataset(data_name, "test", data_cfg, verbose=verbose)
         self.table = DeviceTable(ds, self.device)
         self.last_metric: float = float("nan")
@@ -62,9 +63,13 @@ class Validation:
         sd = self.layout.unflatten(flat, clone=False)
         self.model.load_state_dict(sd, strict=True)
         outs = []
-        for a in range(0, self.table.n, EVAL_CHUNK):
-            idx = torch.arange(a, min(a + EVAL_CHUNK, self.table.n), device=self.device)
-            if self.data_name == "ICU":
+        chunk = EVAL_CHUNK if self.data_name != "CIFAR10" else 1024
+        for a in range(0, self.table.n, chunk):
+            idx = torch.arange(a, min(a + chunk, self.table.n), device=self.device)
+            if self.data_name == "CIFAR10":
+                x, _ = self.table.image_batch(idx)
+                outs.append(self.model(x))
+            elif self.data_name == "ICU":
                 v, l, _ = self.table.icu_batch(idx)
                 outs.append(self.model(v, l).reshape(-1))
             else:
@@ -87,7 +92,28 @@ class Validation:
         self.last_metric = auc
         return True, auc
 
+    def _finish_image(self, loss_sum: float, correct: int) -> Tuple[bool, float]:
+        n = self.table.n
+        loss = loss_sum / n
+        acc = 100.0 * correct / n
+        msg = f"Test set: Average loss: {loss:.4f}, Accuracy: {correct}/{n} ({acc:.2f}%)\n"
+        if self.verbose:
+            print(msg)
+        self.logger.log_info(msg)
+        self.last_metric = acc
+        if math.isnan(loss) or abs(loss) > 10e5:
+            return False, acc
+        return True, acc
+
+    def _image_stats(self, flat: torch.Tensor) -> Tuple[float, int]:
+        out = self._outputs(flat)
+        y = self._labels()
+        loss = float(torch.nn.functional.nll_loss(out.float(), y, reduction="sum"))
+        return loss, int((out.argmax(dim=1) == y).sum())
+
     def test(self, flat: torch.Tensor) -> Tuple[bool, float]:
+        if self.data_name == "CIFAR10":
+            return self._finish_image(*self._image_stats(flat))
         out = self._outputs(flat)
         if self.data_name == "ICU":
             return self._finish_icu(out, self._labels())
@@ -100,6 +126,12 @@ class Validation:
         return True, acc
 
     def test_hyper(self, hnet, num_client: int) -> Tuple[bool, float]:
+        if self.data_name == "CIFAR10":
+            loss, correct = 0.0, 0
+            for i in range(num_client):
+                l, c = self._image_stats(hnet.generate(i))
+                loss, correct = loss + l, correct + c
+            return self._finish_image(loss, correct)
         if self.data_name != "ICU":
             raise ValueError(f"Not found test function for data name {self.data_name}")
         if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and num_client > 0:
