@@ -221,7 +221,7 @@ def resolve_dataset(data_name: str, split: str, data_cfg: Optional[dict] = None,
                 if verbose:
                     print_with_color(f"Loading {data_name}/{split} from {p}", "green")
                 return load_pickled_dataset(p)
-        if mode in ("false", "0", "no"):
+        if mode in ("false", "0", "no") and (data_name, split) in REF_PATHS:
             raise FileNotFoundError(f"no {data_name}/{split} pickle under {root} and data.synthetic is false")
     if data_name == "CIFAR10" and mode in ("auto", "false", "0", "no"):
         d = os.path.join(root, "data", "cifar-10-batches-bin")

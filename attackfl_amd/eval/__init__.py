@@ -6,9 +6,10 @@ round.  HAR: accuracy.  CIFAR10 (``test_image`` / ``test_hyper_image``, ``src/Va
 ``100 * correct / len`` accuracy; a NaN or ``|loss| > 1e6`` fails the round.  The hyper variant
 pools every client's loss and hits but still divides by ONE test-set length, like the reference.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
 model before one ROC-AUC, like ``test_hyper_icu``.  The test set stays resident on the device
-and is evaluated in one pass (eval mode is batch-size independent).  On GPU every model runs a
-native forward: TransformerModel the fused HIP eval kernel, CNNModel / RNNModel /
-TransformerClassifier their layer program (``fl/programs.py``) in eval mode.
+and is evaluated in one pass (eval mode is batch-size independent).  On GPU every ICU / HAR model
+runs a native forward: TransformerModel the fused HIP eval kernel, CNNModel / RNNModel /
+TransformerClassifier their layer program (``fl/programs.py``) in eval mode.  CIFAR10 images (the
+reference ships no image model) go through the eager PyTorch module on either device.
 """
 from __future__ import annotations
 
@@ -57,7 +58,8 @@ class Validation:
             from ..ops.transformer import eval_forward
 
             return eval_forward(flat, self.table.rows)
-        if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH:
+        if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and self.data_name != "CIFAR10":
+            # the layer programs take ICU rows / HAR sequences; images go through the eager model below
             data = self.table.rows if self.data_name == "ICU" else self.table.x
             return self._program_runner().predict(flat[None], data)[0]
         sd = self.layout.unflatten(flat, clone=False)

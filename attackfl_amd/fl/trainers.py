@@ -225,7 +225,14 @@ class EagerTrainer:
         model = self.model
         model.train()
         opt = torch.optim.Adam(model.parameters(), lr=lr)
-        crit = bce_loss if self.data_name == "ICU" else torch.nn.CrossEntropyLoss()
+        if self.data_name == "ICU":
+            crit = bce_loss
+        elif self.table.kind == "IMAGE":
+            # the reference has no image trainer; its image validation scores log-probabilities with
+            # nll_loss (src/Validation.py:80-82), so image models are trained on the same objective
+            crit = torch.nn.NLLLoss()
+        else:
+            crit = torch.nn.CrossEntropyLoss()
         nd = order.shape[1]
         nbatches = max(1, (nd + batch - 1) // batch)
         for e in range(order.shape[0]):
@@ -237,6 +244,9 @@ class EagerTrainer:
                     v, l, y = self.table.icu_batch(idx)
                     out = model(v, l)
                     loss = crit(out, y[:, None])
+                elif self.table.kind == "IMAGE":
+                    x, y = self.table.image_batch(idx)
+                    loss = crit(model(x), y)
                 else:
                     x, y = self.table.har_batch(idx)
                     loss = crit(model(x), y)
@@ -311,6 +321,8 @@ class GraphTrainer:
 
         if model_name not in programs.PROGRAMS:
             raise ValueError(f"graph trainer supports {sorted(programs.PROGRAMS)}")
+        if table.kind == "IMAGE":
+            raise ValueError("graph trainer programs take ICU rows / HAR sequences; train image models eagerly")
         self.programs = programs
         self.model_name = model_name
         self.table = table
@@ -350,7 +362,7 @@ def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable,
             kind = "eager"
         elif model_name in FusedTrainer.MODELS and data_name == "ICU":
             kind = "fused"
-        elif model_name in PROGRAMS:
+        elif model_name in PROGRAMS and data_name != "CIFAR10":
             kind = "graph"
         else:
             kind = "eager"

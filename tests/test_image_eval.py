@@ -56,6 +56,16 @@ def test_cifar_bin_loader_matches_totensor_normalize(tmp_path):
     rec.tofile(d / "test_batch.bin")
     ds2 = resolve_dataset("CIFAR10", "test", {"root": str(tmp_path)}, verbose=False)
     torch.testing.assert_close(ds2.x, want)
+    # data.synthetic false forces the real records (no pickle path exists for CIFAR10)
+    ds3 = resolve_dataset("CIFAR10", "test", {"root": str(tmp_path), "synthetic": False}, verbose=False)
+    torch.testing.assert_close(ds3.x, want)
+
+
+def test_cifar_synthetic_false_without_records_raises(tmp_path):
+    import pytest
+
+    with pytest.raises(FileNotFoundError, match="CIFAR10 binary batches"):
+        resolve_dataset("CIFAR10", "test", {"root": str(tmp_path), "synthetic": False}, verbose=False)
 
 
 def test_image_validation_and_hyper_pooling(monkeypatch):
@@ -93,3 +103,24 @@ def test_image_validation_fails_on_nan(monkeypatch):
     flat[:] = float("nan")
     ok, _ = val.test(flat)
     assert not ok
+
+
+def test_image_eager_training_steps(monkeypatch):
+    """CIFAR10 is validation-only in the reference; the eager trainer still takes image batches (NLL on
+    the model's log-probabilities) instead of failing inside the forward."""
+    from attackfl_amd.fl.trainers import EagerTrainer, make_plan, make_trainer
+
+    monkeypatch.setitem(models.MODEL_REGISTRY, "TinyImageNet", TinyImageNet)
+    ds = synthetic_cifar10(64, seed=4)
+    table = DeviceTable(ds, "cpu")
+    tr = make_trainer("auto", "TinyImageNet", "CIFAR10", table, "cpu")
+    assert isinstance(tr, EagerTrainer)
+    net = TinyImageNet()
+    params = tr.layout.flatten(net.state_dict())[None].clone()
+    p0 = params.clone()
+    plan = make_plan(64, [48], 2, torch.Generator().manual_seed(0), "cpu")
+    oks, losses = tr.train(params, plan, 0.01, 16, [7])
+    assert oks == [True] and torch.isfinite(losses).all()
+    assert not torch.equal(params, p0)
+    # the first epoch's mean loss is the NLL objective (epoch 2 starts from the trained weights)
+    assert float(losses[0, 1]) < float(losses[0, 0]) + 1.0
