@@ -73,10 +73,13 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     host_flags = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM",
                            "-I" + py_inc, "-I" + os.path.join(ROCM, "include")] + ["-I" + p for p in inc] + ["-x", "c++"]
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    # per-file device flags: tf2.hip keeps its optimizer state in AGPRs, so its MFMAs must accumulate
+    # in VGPRs (otherwise their accumulators compete with that state for the AGPR half of the budget)
+    extra = {"tf2.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
     hosts = sorted(glob.glob(os.path.join(ROOT, "csrc", "*.cpp")) + glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_compile, s, dev_flags, verbose) for s in kernels]
+        futs = [ex.submit(_compile, s, dev_flags + extra.get(os.path.basename(s), []), verbose) for s in kernels]
         futs += [ex.submit(_compile, s, host_flags, verbose) for s in hosts]
         objs = [f.result() for f in futs]
     cmd = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [

@@ -21,10 +21,12 @@ M32 = 0xFFFFFFFF
 
 # ------------------------------------------------------------------------------- device entry points
 def auto_split(C: int, dev) -> int:
-    """Workgroups per client for the fused trainer: 3 (head | vitals | labs) when every workgroup of
-    every client fits on the device at once (one per CU), else 2, else 1."""
+    """Trainer variant for C clients: 4 = the on-chip trainer (``tf2.hip``: head | vitals | labs
+    workgroups with weights, optimizer state and activations held in registers / LDS) when every
+    workgroup of every client fits on the device at once (one per CU); else the global-workspace
+    kernels of ``transformer.hip`` with 2 or 1 workgroups per client."""
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    return 3 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
+    return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
 def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
@@ -58,7 +60,8 @@ def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor,
 
     ``split``: workgroups per client — 1 (whole model in one workgroup), 2 (vitals branch + head |
     labs branch) or 3 (head | vitals | labs); the workgroups of a client hand activations and
-    gradients to each other every step.  Default: ``auto_split``.
+    gradients to each other every step.  4 = the on-chip trainer (``tf2.hip``, 3 workgroups per client,
+    nothing of the model in global memory during the round).  Default: ``auto_split``.
     ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
     workgroup 0, summed over all steps (diagnostics)."""
     return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, stamps, split))

@@ -351,7 +351,9 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   const int C = params.size(0);
   TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
   TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
-  const long stride = (((kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats()) + 63) / 64) * 64;
+  // split 4 = the on-chip TransformerModel trainer (tf2.hip: 3 workgroups per client, state in registers)
+  const bool tf2 = kind == 0 && split == 4;
+  const long stride = (((tf2 ? afl_tf2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats()) + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());
   auto ok = torch::zeros({C}, order.options());
   auto losses = torch::zeros({C, epochs}, params.options());
@@ -385,7 +387,7 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
     sync = torch::zeros({(long)C * AFL_TF_SYNC_WORDS}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
-  const int rc = kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
+  const int rc = tf2 ? afl_tf2_train(&a, cur()) : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
   TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
   TORCH_CHECK(rc == 0, "fused trainer launch failed (", rc, ")");
   AFL_CHECK_LAUNCH();

@@ -77,6 +77,10 @@ int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);
 long afl_tf_ws_floats();
 constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lines) + timeout word
+// tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations
+// in registers / LDS; 3 workgroups per client, sync words required)
+int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);
+long afl_tf2_ws_floats();
 // rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
 int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);
 long afl_rnn_ws_floats();

@@ -1,0 +1,1365 @@
+// Fused TransformerModel/ICU local training, on-chip edition (reference training loop client.py:75-111,
+// model src/Model.py:166-246).  ONE persistent launch trains every client of a rank for all its local
+// epochs; each client runs on three co-resident 512-thread workgroups (head | vitals branch | labs
+// branch) that hand activations and gradients to each other once per direction per step.
+//
+// What differs from transformer.hip: after the prologue NOTHING of a client's model lives in global
+// memory.  Per workgroup:
+//   * fp32 master weights and both Adam moments stay in REGISTERS for the whole round: every lane owns
+//     the elements of the weight-gradient tiles it computes (4 per 16x16 tile, <= 6 tiles per lane) and
+//     one or two bias / LayerNorm entries; the optimizer never touches memory;
+//   * bf16 weight images (the MFMA operands) and an fp32 copy of the bias / LayerNorm vectors live in
+//     LDS; Adam rewrites them in place;
+//   * activations chain in registers: every GEMM is computed transposed, Y^T = W . X^T, so the
+//     16x16x32 MFMA leaves lane (b, g) of wave w holding features 16t + 4g + i of batch row 16w + b
+//     ("T layout") — exactly the B operand of the next GEMM once the weight image's K axis is stored in
+//     the matching permuted order (pcol below).  The forward and the d(input) backward of a wave never
+//     leave its registers and need no barrier; LayerNorm row sums are in-lane + two permlane swaps;
+//   * the activations the weight gradients need (X and dY of every dW = dY^T X) are written to
+//     XOR-swizzled LDS tiles as they are produced and read back with ds_read_b64_tr_b16 in ONE dW phase
+//     per step (the only two workgroup barriers of a step bracket it);
+//   * the only global traffic in the step loop is the next batch's input rows (prefetched during the
+//     hand-off wait) and the hand-offs themselves: 16-byte write-through (sc1) payload stores, a per-wave
+//     flag, sc1 loads on the other side (cdna_hip_programming.md Guideline 16 R1).
+// Numerics are those of transformer.hip: bf16 MFMA operands with fp32 accumulation, fp32 elementwise
+// math, exact-erf GELU, hash dropout masks (tf_common.h), torch.optim.Adam with a fresh state per round.
+#include "common.h"
+#include "kernels.h"
+#include "tf_common.h"
+#include "fused_common.h"
+
+using namespace tf;
+
+namespace t2 {
+
+using fk::AdamK;
+using fk::u32x4;
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+typedef unsigned char uchar;
+
+constexpr int NTH = 512;
+
+// ----------------------------------------------------------------------------------- LDS maps (bytes)
+// weight images: bf16 [rows][ld] with the K axis permuted (pcol); ld padded by 8 elements
+constexpr int LD32 = 40 * 2, LD64 = 72 * 2, LD128 = 136 * 2;  // row strides in bytes
+// branch workgroup
+constexpr int B_IMG_D = 0;                         // [64][32]  dense (K = din padded to 32)
+constexpr int B_IMG_V = B_IMG_D + 64 * LD32;       // [64][64]  in_proj rows 128..191 (v)
+constexpr int B_IMG_O = B_IMG_V + 64 * LD64;       // [64][64]  out_proj
+constexpr int B_IMG_F1 = B_IMG_O + 64 * LD64;      // [16][64]  ffn.0 (6 real rows)
+constexpr int B_IMG_F2 = B_IMG_F1 + 16 * LD64;     // [64][32]  ffn.3 (6 real columns)
+constexpr int B_H0 = B_IMG_F2 + 64 * LD32;         // tile64: h0 = gelu(dense)          (X of dWv)
+constexpr int B_A = B_H0 + 16384;                  // tile64: a = att_dropout(v)         (X of dWo)
+constexpr int B_X1N = B_A + 16384;                 // tile64: LN1 output                 (X of dWf1)
+constexpr int B_DF3 = B_X1N + 16384;               // tile64: d(ffn.3 out)               (dY of dWf2)
+constexpr int B_DO = B_DF3 + 16384;                // tile64: d(out_proj out)            (dY of dWo)
+constexpr int B_DV = B_DO + 16384;                 // tile64: d(v)                       (dY of dWv)
+constexpr int B_DZ0 = B_DV + 16384;                // tile64: d(dense pre-activation)    (dY of dWd)
+constexpr int B_XIN = B_DZ0 + 16384;               // tile16: branch input               (X of dWd)
+constexpr int B_F2 = B_XIN + 4096;                 // tile16: drop(gelu(ffn.0 out))      (X of dWf2)
+constexpr int B_DF0 = B_F2 + 4096;                 // tile16: d(ffn.0 pre-activation)    (dY of dWf1)
+constexpr int B_NVEC = 648;                        // 10 x 64 vectors + ffn.0 bias (8 slots, 6 real)
+constexpr int B_VEC = B_DF0 + 4096;                // fp32 [648] bias / LayerNorm parameters
+constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [648] their gradients (column sums)
+constexpr int B_MISC = B_CS + B_NVEC * 4;          // u32 [8] per-wave abort words
+constexpr int B_TOTAL = B_MISC + 64;
+// vector segments (x64 floats) of VEC / CS
+enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3 };
+constexpr int VS_F1B = 640;  // ffn.0 bias (6 real)
+
+// head workgroup
+constexpr int H_IMG_W1 = 0;                        // [64][128] fc1
+constexpr int H_IMG_W2 = H_IMG_W1 + 64 * LD128;    // [32][64]  fc2
+constexpr int H_CAT = H_IMG_W2 + 32 * LD64;        // tile128: cat(vitals, labs)     (X of dWf1)
+constexpr int H_A1 = H_CAT + 32768;                // tile64:  drop(gelu(fc1))       (X of dWf2)
+constexpr int H_DZ1 = H_A1 + 16384;                // tile64:  d(fc1 pre-activation) (dY of dWf1)
+constexpr int H_DZ2 = H_DZ1 + 16384;               // tile32:  d(fc2 pre-activation) (dY of dWf2)
+constexpr int H_NVEC = 132;                        // fc1.b 64 | fc2.b 32 | output.w 32 | output.b 1
+constexpr int H_VEC = H_DZ2 + 8192;
+constexpr int H_CS = H_VEC + H_NVEC * 4;
+constexpr int H_LOSS = H_CS + H_NVEC * 4;          // fp32 [8] per-wave loss partials
+constexpr int H_TOTAL = H_LOSS + 64;
+enum { HV_B1 = 0, HV_B2 = 64, HV_WO = 96, HV_BO = 128 };
+
+constexpr int SMEM = B_TOTAL > H_TOTAL ? B_TOTAL : H_TOTAL;
+static_assert(SMEM <= 160 * 1024, "LDS budget");
+
+// ------------------------------------------------------------------- per-client workspace (bytes)
+// hand-off payloads: [branch][wave][lane] x 32 bytes (16 bf16 in T layout)
+constexpr long WS_XF = 0;              // branch outputs -> head
+constexpr long WS_XB = WS_XF + 32768;  // d(branch outputs) -> branches
+constexpr long WS_BYTES = WS_XB + 32768;
+
+// ------------------------------------------------------------------------------ small helpers
+// every LDS access goes through an address_space(3) pointer (a generic one would become FLAT, which
+// counts in vmcnt too and breaks the hand-off's counted waits)
+__device__ __forceinline__ LDS_AS float* ldsf(uchar* base, int byte_off) { return (LDS_AS float*)(base + byte_off); }
+__device__ __forceinline__ LDS_AS uint32_t* ldsu(uchar* base, int byte_off) {
+  return (LDS_AS uint32_t*)(base + byte_off);
+}
+__device__ __forceinline__ uint32_t pk2(float a, float b) { return fk::pack_bf2(a, b); }
+__device__ __forceinline__ s8v pk8(float a0, float a1, float a2, float a3, float b0, float b1, float b2, float b3) {
+  u32x4 u{pk2(a0, a1), pk2(a2, a3), pk2(b0, b1), pk2(b2, b3)};
+  return __builtin_bit_cast(s8v, u);
+}
+// B fragment of k-step s from a T-layout register row (tiles 2s and 2s+1)
+__device__ __forceinline__ s8v bfrag(const float* v, int s) {
+  const float* a = v + 8 * s;
+  return pk8(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
+}
+__device__ __forceinline__ s8v bfrag_lo(const float* v) {  // K = 16 padded to 32: second half zero
+  return pk8(v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ f4v mma(s8v a, s8v b, f4v c) { return fk::mfma(a, b, c); }
+constexpr f4v Z4 = {0.f, 0.f, 0.f, 0.f};
+
+// permuted K position of weight column k: the 8 values lane group g of k-step s multiplies are
+// columns {32s + 4g + i, 32s + 16 + 4g + i} (tiles 2s, 2s+1 of the T layout) -> stored contiguously
+__host__ __device__ constexpr int pcol(int k) {
+  return 32 * (k >> 5) + 8 * ((k >> 2) & 3) + 4 * ((k >> 4) & 1) + (k & 3);
+}
+
+// forward A fragment: W rows 16T + (lane & 15), permuted K chunk of k-step s (one ds_read_b128)
+__device__ __forceinline__ s8v wfrag(const uchar* img, int ld, int T, int s, int lane) {
+  return *(const LDS_AS s8v*)(img + (16 * T + (lane & 15)) * ld + (32 * s + 8 * (lane >> 4)) * 2);
+}
+__device__ __forceinline__ s4v tr16(const uchar* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)p);
+}
+__device__ __forceinline__ s8v cat44(s4v a, s4v b) {
+  s8v r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+// backward A fragment (d input = dY . W, computed as W^T . dY^T): lane (m, g) needs W[n][16T + m] for
+// n = 32s + 16h + 4g + j (h = 0, 1; j = 0..3) -> two transposed reads of the same image.  Rows at or
+// past `nrows` read as zero (hi == false drops the second half: images with <= 16 rows).
+template <bool HI>
+__device__ __forceinline__ s8v wtfrag(const uchar* img, int ld, int T, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = 32 * (T >> 1) + 8 * p + 4 * (T & 1);
+  const uchar* a = img + (32 * s + 4 * g + q) * ld + col * 2;
+  s4v lo = tr16(a);
+  s4v hi = {0, 0, 0, 0};
+  if (HI) hi = tr16(a + 16 * ld);
+  return cat44(lo, hi);
+}
+
+// XOR-swizzled activation tiles [128 rows][W bf16] (8-byte chunks); chosen so the T-layout row stores
+// (16 rows x one chunk per instruction) and the dW transposed reads (rows 8g+q, 8g+q+4, chunks 4T+p)
+// are conflict-free
+__device__ __forceinline__ int sw64(int r) {
+  return (r & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3);
+}
+__device__ __forceinline__ int t64(int r, int c8) { return r * 128 + ((c8 ^ sw64(r)) << 3); }
+__device__ __forceinline__ int sw128(int r) {
+  return ((((r & 3) | (((r >> 3) & 1) << 2))) << 2) | ((r >> 2) & 1) | (((r >> 3) & 1) << 1);
+}
+__device__ __forceinline__ int t128(int r, int c8) { return r * 256 + ((c8 ^ sw128(r)) << 3); }
+__device__ __forceinline__ int t32(int r, int c8) { return r * 64 + ((c8 ^ ((r >> 1) & 7)) << 3); }
+__device__ __forceinline__ int t16(int r, int c8) {
+  const int pr = r ^ (((r >> 3) & 1) << 2);
+  return pr * 32 + ((c8 ^ ((pr >> 2) & 3)) << 3);
+}
+enum { TK16 = 0, TK32, TK64, TK128 };
+template <int K>
+__device__ __forceinline__ int toff(int r, int c8) {
+  if constexpr (K == TK16) return t16(r, c8);
+  else if constexpr (K == TK32) return t32(r, c8);
+  else if constexpr (K == TK64) return t64(r, c8);
+  else return t128(r, c8);
+}
+// 4 consecutive features (one 8-byte chunk) of a row
+template <int K>
+__device__ __forceinline__ void st4(uchar* tile, int r, int c8, const float* x) {
+  *(LDS_AS u32x2v*)(tile + toff<K>(r, c8)) = u32x2v{pk2(x[0], x[1]), pk2(x[2], x[3])};
+}
+// dW operand fragment: lane (i, g) gets tile[r0 + 8g + j][16T + i], j = 0..7 (two transposed reads)
+template <int K>
+__device__ __forceinline__ s8v tfrag(const uchar* tile, int r0, int T, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = r0 + 8 * g + q;
+  return cat44(tr16(tile + toff<K>(row, 4 * T + p)), tr16(tile + toff<K>(row + 4, 4 * T + p)));
+}
+
+// 16 fp32 of a T-layout row from an fp32 LDS vector (features 16t + 4g + i)
+__device__ __forceinline__ void vec16(float (&x)[16], const uchar* vec, int g) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f4v v = *(const LDS_AS f4v*)(vec + (16 * t + 4 * g) * 4);
+    x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
+  }
+}
+__device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  // 32-wide: tiles 0, 1
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const f4v v = *(const LDS_AS f4v*)(vec + (16 * t + 4 * g) * 4);
+    x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
+  }
+}
+
+// column sums over the wave's 16 rows of W values per lane (DPP reduce-scatter, fused_common.h), added
+// into the fp32 LDS gradient vector: value j of lane group g is feature feat(g, j)
+__device__ __forceinline__ void lds_add(uchar* p, float v) {
+  __hip_atomic_fetch_add((LDS_AS float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int W>
+__device__ __forceinline__ int rs_slot(float (&s)[W], int i) {
+  int j = 0;
+  fk::rs_level<W, 0>(s, i, j);
+  fk::rs_level<W / 2, 1>(s, i, j);
+  if constexpr (W >= 8) fk::rs_level<W / 4, 2>(s, i, j);
+  if constexpr (W >= 16) fk::rs_level<W / 8, 3>(s, i, j);
+  if constexpr (W == 4) s[0] += fk::dpp_pair<1>(s[0]);
+  if constexpr (W <= 8) s[0] += fk::dpp_pair<3>(s[0]);
+  return j;
+}
+// 16 values (64 features, T layout) -> cs[feature]
+__device__ __forceinline__ void colsum64(uchar* cs, const float (&x)[16], int lane) {
+  float s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = x[j];
+  const int j = rs_slot<16>(s, lane & 15);
+  lds_add(cs + (16 * (j >> 2) + 4 * (lane >> 4) + (j & 3)) * 4, s[0]);
+}
+// 8 values (32 features: tiles 0, 1)
+__device__ __forceinline__ void colsum32(uchar* cs, const float (&x)[8], int lane) {
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = x[j];
+  const int i = lane & 15;
+  const int j = rs_slot<8>(s, i);
+  if ((i & 8) == 0) lds_add(cs + (16 * (j >> 2) + 4 * (lane >> 4) + (j & 3)) * 4, s[0]);
+}
+// 4 values (16 features: tile 0), only features < nreal
+__device__ __forceinline__ void colsum16(uchar* cs, const float (&x)[4], int lane, int nreal) {
+  float s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s[j] = x[j];
+  const int i = lane & 15;
+  const int j = rs_slot<4>(s, i);
+  const int f = 4 * (lane >> 4) + j;
+  if ((i & 10) == 0 && f < nreal) lds_add(cs + f * 4, s[0]);
+}
+
+// dropout keep bits of features 16t + 4g + i (bit 4t + i), hash pairs as tf::keep
+__device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, int g, uint32_t thr) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t x = hash3(key, layer, (uint32_t)r, (uint32_t)(8 * t + 2 * g + h));
+      m |= ((x & 0xFFFFu) >= thr ? 1u : 0u) << (4 * t + 2 * h);
+      m |= ((x >> 16) >= thr ? 1u : 0u) << (4 * t + 2 * h + 1);
+    }
+  }
+  return m;
+}
+__device__ __forceinline__ bool bit(uint32_t m, int j) { return (m >> j) & 1u; }
+
+// ------------------------------------------------------------------------------- Adam in registers
+struct TS {  // one 16x16 weight-gradient tile's 4 elements of this lane
+  float p[4], m[4], v[4];
+};
+struct VS {
+  float p, m, v;
+};
+// The optimizer state lives in ACCUMULATION registers (AGPRs): every access goes through
+// v_accvgpr_read / v_accvgpr_write, so the register allocator gives these values the AGPR class and
+// the forward / backward working set keeps the architectural VGPRs (the two files share one 256-entry
+// budget per lane at two waves per SIMD; without this the allocator spills the state to scratch).
+__device__ __forceinline__ float ar(float a) {
+  float r;
+  asm("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(a));
+  return r;
+}
+__device__ __forceinline__ float aw(float v) {
+  float r;
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ float adam1(float& pa, float& ma, float& va, float g, const AdamK& k) {
+  float p = ar(pa);
+  if (k.sgd_lr > 0.f) {
+    p -= k.sgd_lr * g;
+  } else {
+    float m = ar(ma), v = ar(va);
+    m = m + (1.f - fk::B1) * (g - m);
+    v = fk::B2 * v + (1.f - fk::B2) * g * g;
+    p -= k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_sqrtf(v) * k.rsqrt_bc2 + fk::EPS);
+    ma = aw(m);
+    va = aw(v);
+  }
+  pa = aw(p);
+  return p;
+}
+// weight matrix W[n][k] (row-major in the flat params at `off`, n_real x k_real) and its LDS image
+struct Mat {
+  int off, n_real, k_real, img, ld;
+};
+// element (n, k) of this lane in tile (T = k tile, T' = n tile): n = 16T' + (lane & 15), k = 16T + 4g + i
+__device__ __forceinline__ void tile_load(TS& s, const Mat& M, int T, int Tn, int lane, const float* P, uchar* smem) {
+  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
+  float h[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = n < M.n_real && k0 + i < M.k_real;
+    h[i] = ok ? P[M.off + n * M.k_real + k0 + i] : 0.f;
+    s.p[i] = aw(h[i]);
+    s.m[i] = aw(0.f);
+    s.v[i] = aw(0.f);
+  }
+  if (n < 16 * ((M.n_real + 15) / 16))
+    *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
+}
+__device__ __forceinline__ void tile_store(const TS& s, const Mat& M, int T, int Tn, int lane, float* P) {
+  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (n < M.n_real && k0 + i < M.k_real) P[M.off + n * M.k_real + k0 + i] = ar(s.p[i]);
+}
+// Adam on the tile's real elements with gradient acc (= dW^T tile), new bf16 values -> image
+__device__ __forceinline__ void tile_adam(TS& s, const Mat& M, int T, int Tn, int lane, f4v acc, const AdamK& K,
+                                          uchar* smem) {
+  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
+  float h[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = n < M.n_real && k0 + i < M.k_real;
+    h[i] = ok ? adam1(s.p[i], s.m[i], s.v[i], acc[i], K) : 0.f;
+  }
+  if (n < 16 * ((M.n_real + 15) / 16))
+    *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
+}
+
+// -------------------------------------------------------------------------- cross-workgroup hand-off
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t rs, int off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1: write-through
+}
+__device__ __forceinline__ u32x4 ld_wt(__amdgpu_buffer_rsrc_t rs, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+}
+__device__ __forceinline__ void publish(gu32* flag, uint32_t value, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// waits until (*fa >> shift) >= want and (*fb >> shift) >= want; returns *fa, or 0xFFFFFFFF on timeout
+__device__ __forceinline__ uint32_t await(gu32* fa, gu32* fb, uint32_t want, int shift, gu32* tmo, int lane) {
+  uint32_t v = 0;
+  for (long spins = 0;; ++spins) {
+    v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(fa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t w =
+        fb == fa ? v : __builtin_amdgcn_readfirstlane(__hip_atomic_load(fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if ((v >> shift) >= want && (w >> shift) >= want) break;
+    if (spins > fk::XWG_MAX_SPINS) {
+      v = 0xFFFFFFFFu;
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // payload loads stay below the poll
+  return v;
+}
+constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
+__device__ __forceinline__ gu32* xf(gu32* base, int group, int wave) { return base + (group * 8 + wave) * 32; }
+
+__device__ __forceinline__ void unpack16(const u32x4 (&u)[2], float (&x)[16]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[8 * h + 2 * k] = __uint_as_float(u[h][k] << 16);
+      x[8 * h + 2 * k + 1] = __uint_as_float(u[h][k] & 0xFFFF0000u);
+    }
+}
+__device__ __forceinline__ void pack16(const float (&x)[16], u32x4 (&u)[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[h][k] = pk2(x[8 * h + 2 * k], x[8 * h + 2 * k + 1]);
+}
+
+// Phase entry: make the lane / wave indices opaque so every LDS address of the phase is recomputed
+// inside it.  Otherwise the compiler hoists the hundreds of per-lane swizzled addresses of the step out
+// of the loop and keeps them live across all phases (spilling the optimizer state to scratch).
+__device__ __forceinline__ void opq(int& lane, int& wave) {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" : "+v"(lane));
+  asm volatile("" : "+s"(wave));
+  lane &= 63;
+  wave &= 7;
+}
+// sub-phase boundary inside a phase: the scheduler may not move instructions across it (keeps the next
+// sub-phase's LDS loads from being hoisted into this one, which raises register pressure)
+__device__ __forceinline__ void sb() { __builtin_amdgcn_sched_barrier(0); }
+
+// barrier over LDS only (global loads stay in flight, stores are not drained)
+__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// --------------------------------------------------------------------------- batch walk (shared plan)
+struct Walk {
+  int e, b0;  // current epoch, batch start
+};
+// next non-skipped batch at or after (e, b0) (size-1 batches are skipped, client.py:86-87); false = done
+__device__ __forceinline__ bool walk_valid(Walk& w, int nd, int BS, int E) {
+  for (;;) {
+    if (w.b0 >= nd) {
+      ++w.e;
+      w.b0 = 0;
+      if (w.e >= E) return false;
+      continue;
+    }
+    if (min(BS, nd - w.b0) == 1) {
+      w.b0 += BS;
+      continue;
+    }
+    return true;
+  }
+}
+
+// =============================================================================== branch workgroup
+template <int BR>
+struct BrK {
+  static constexpr BrOff o = BR == 0 ? OV : OL;
+  static constexpr int din = BR == 0 ? D_V : D_L;
+  static constexpr int xoff = BR == 0 ? 0 : D_V;
+  static constexpr Mat MD{o.dense_w, 64, din, B_IMG_D, LD32};
+  static constexpr Mat MV{o.inproj_w + 128 * 64, 64, 64, B_IMG_V, LD64};
+  static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LD64};
+  static constexpr Mat MF1{o.ff0_w, FF, 64, B_IMG_F1, LD64};
+  static constexpr Mat MF2{o.ff3_w, 64, FF, B_IMG_F2, LD32};
+  // VEC segment -> flat parameter offset
+  static __device__ __forceinline__ int vec_param(int e) {
+    if (e >= VS_F1B) return e - VS_F1B < FF ? o.ff0_b + (e - VS_F1B) : -1;
+    const int s = e >> 6, i = e & 63;  // (a runtime-indexed array would live in scratch)
+    const int b = s == 0 ? o.dense_b : s == 1 ? o.inproj_b + 128 : s == 2 ? o.out_b : s == 3 ? o.ln1_w
+                : s == 4 ? o.ln1_b : s == 5 ? o.ff3_b : s == 6 ? o.ln2_w : s == 7 ? o.ln2_b : s == 8 ? o.bn_w : o.bn_b;
+    return b + i;
+  }
+};
+
+// values the backward needs from the forward, kept in registers (T layout).  The normalised LayerNorm
+// outputs and gelu' are kept as bf16 pairs (the precision the backward's GEMM operands have anyway):
+// fp32 copies of all four would not fit beside the optimizer state in the 256-register budget.
+struct Saved {
+  uint32_t xh1[8], xh2[8], gp[8];
+  float rstd1, rstd2;
+  uint32_t m1, m2, matt;
+  float gk[4];  // drop'(.) * gelu'(ffn.0 out) of features 4g + i
+};
+__device__ __forceinline__ void save16(uint32_t (&d)[8], const float (&x)[16]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = pk2(x[2 * k], x[2 * k + 1]);
+}
+__device__ __forceinline__ void load16(float (&x)[16], const uint32_t (&d)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    x[2 * k] = __uint_as_float(d[k] << 16);
+    x[2 * k + 1] = __uint_as_float(d[k] & 0xFFFF0000u);
+  }
+}
+
+// Optimizer state of one branch lane (AGPR-resident, see ar/aw):
+//  * blk: its 4 tiles of a 2x2 block of the 64x64 v (waves 0-3) or out_proj (waves 4-7) weight gradient;
+//  * cmp: up to NCMP "compact" entries: the bias / LayerNorm vectors (VEC index e < 648), then the real
+//    elements of the dense, ffn.0 and ffn.3 weights (padding-free: their gradient tiles are mostly padding,
+//    so they are staged through LDS and owned element-wise instead of tile-wise).  Entry e belongs to thread
+//    e % 512, slot e / 512.
+struct BrState {
+  TS blk[4];
+  VS cmp[5];
+};
+constexpr int NCMP = 5;
+template <int BR>
+struct Cmp {
+  static constexpr int din = BR == 0 ? D_V : D_L;
+  static constexpr int E_D = B_NVEC;             // dense weight [64][din]
+  static constexpr int E_F1 = E_D + 64 * din;    // ffn.0 weight [6][64]
+  static constexpr int E_F2 = E_F1 + FF * 64;    // ffn.3 weight [64][6]
+  static constexpr int N = E_F2 + 64 * FF;
+  static_assert(N <= NCMP * NTH, "compact entries");
+};
+// compact weight-gradient staging (fp32 [N - 648]) in the XIN / F2 / DF0 tiles, dead by then
+constexpr int B_GS = B_XIN;
+static_assert(B_GS + (Cmp<1>::N - B_NVEC) * 4 <= B_VEC, "compact gradient staging fits");
+
+template <int BR>
+__device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], uint32_t key, Saved& sv,
+                                           u32x4 (&outp)[2], int lane, int wave) {
+  using B = BrK<BR>;
+  opq(lane, wave);
+  const int g = lane >> 4, r = 16 * wave + (lane & 15);
+  const uchar* vec = smem + B_VEC;
+  st4<TK16>(smem + B_XIN, r, g, xin);
+  // ---- dense (K = din <= 16 padded to 32) + GELU
+  float h0[16];
+  sb();
+  {
+    const s8v bx = bfrag_lo(xin);
+    f4v acc[4];
+#pragma unroll
+    for (int T = 0; T < 4; ++T) acc[T] = mma(wfrag(smem + B_IMG_D, LD32, T, 0, lane), bx, Z4);
+    float bd[16], gp[16];
+    vec16(bd, vec + VS_DB * 256, g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h0[4 * t + i] = gelu_and_grad(acc[t][i] + bd[4 * t + i], gp[4 * t + i]);
+    save16(sv.gp, gp);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_H0, r, 4 * t + g, h0 + 4 * t);
+  }
+  // ---- v projection, attention dropout per (row, head); at L = 1 softmax == 1, so attn = drop(v)
+  float a[16];
+  sb();
+  {
+    const s8v b0 = bfrag(h0, 0), b1 = bfrag(h0, 1);
+    f4v acc[4];
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 0, lane), b0, Z4);
+      acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 1, lane), b1, acc[T]);
+    }
+    const uint32_t ha = hash3(key, 8 * BR + L_ATT, r, 0), hb = hash3(key, 8 * BR + L_ATT, r, 1);
+    sv.matt = ((ha & 0xFFFFu) >= THR_P01 ? 1u : 0u) | ((ha >> 16) >= THR_P01 ? 2u : 0u) |
+              ((hb & 0xFFFFu) >= THR_P01 ? 4u : 0u) | ((hb >> 16) >= THR_P01 ? 8u : 0u);
+    float bv[16];
+    vec16(bv, vec + VS_VB * 256, g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float m = bit(sv.matt, t) ? INV_K01 : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[4 * t + i] = (acc[t][i] + bv[4 * t + i]) * m;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_A, r, 4 * t + g, a + 4 * t);
+  }
+  // ---- out projection, dropout, residual, LayerNorm 1
+  float x1n[16];
+  sb();
+  {
+    const s8v b0 = bfrag(a, 0), b1 = bfrag(a, 1);
+    f4v acc[4];
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
+      acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 1, lane), b1, acc[T]);
+    }
+    sv.m1 = mask16(key, 8 * BR + L_D1, r, g, THR_P01);
+    float bo[16];
+    vec16(bo, vec + VS_OB * 256, g);
+    float x1[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = 4 * t + i;
+        x1[j] = h0[j] + (bit(sv.m1, j) ? (acc[t][i] + bo[j]) * INV_K01 : 0.f);
+      }
+    sv.rstd1 = fk::ln_fwd(x1);
+    save16(sv.xh1, x1);
+    float gm[16], bt[16];
+    vec16(gm, vec + VS_G1 * 256, g);
+    vec16(bt, vec + VS_B1 * 256, g);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x1n[j] = x1[j] * gm[j] + bt[j];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_X1N, r, 4 * t + g, x1n + 4 * t);
+  }
+  // ---- ffn.0 (64 -> 6, one output tile) + GELU + dropout
+  float f2v[4];
+  sb();
+  {
+    f4v acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 0, lane), bfrag(x1n, 0), Z4);
+    acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 1, lane), bfrag(x1n, 1), acc);
+    uint32_t hd[2] = {0u, 0u};
+    if (g < 2) {
+      hd[0] = hash3(key, 8 * BR + L_DF, r, 2 * g);
+      hd[1] = hash3(key, 8 * BR + L_DF, r, 2 * g + 1);
+    }
+    const f4v bf = g < 2 ? *(const LDS_AS f4v*)(vec + (VS_F1B + 4 * g) * 4) : Z4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = 4 * g + i;
+      float gp;
+      const float gl = gelu_and_grad(acc[i] + bf[i], gp);
+      const uint32_t u = (hd[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu;
+      const bool kp = f < FF && u >= THR_P01;
+      f2v[i] = kp ? gl * INV_K01 : 0.f;
+      sv.gk[i] = kp ? gp * INV_K01 : 0.f;
+    }
+    st4<TK16>(smem + B_F2, r, g, f2v);
+  }
+  // ---- ffn.3 (6 -> 64, K padded to 32), dropout, residual, LayerNorm 2, LayerNorm 3 (x_bn)
+  sb();
+  {
+    const s8v bf = bfrag_lo(f2v);
+    f4v acc[4];
+#pragma unroll
+    for (int T = 0; T < 4; ++T) acc[T] = mma(wfrag(smem + B_IMG_F2, LD32, T, 0, lane), bf, Z4);
+    sv.m2 = mask16(key, 8 * BR + L_D2, r, g, THR_P01);
+    float b3[16];
+    vec16(b3, vec + VS_F2B * 256, g);
+    float x2[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = 4 * t + i;
+        x2[j] = x1n[j] + (bit(sv.m2, j) ? (acc[t][i] + b3[j]) * INV_K01 : 0.f);
+      }
+    sv.rstd2 = fk::ln_fwd(x2);
+    save16(sv.xh2, x2);
+    float gm[16], bt[16];
+    vec16(gm, vec + VS_G2 * 256, g);
+    vec16(bt, vec + VS_B2 * 256, g);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x2[j] = x2[j] * gm[j] + bt[j];
+    fk::ln_fwd(x2);
+    vec16(gm, vec + VS_G3 * 256, g);
+    vec16(bt, vec + VS_B3 * 256, g);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x2[j] = x2[j] * gm[j] + bt[j];
+    pack16(x2, outp);
+  }
+}
+
+// d(branch output) -> every activation gradient of the branch (wave-local), the dY tiles of the dW
+// GEMMs and the column sums of the vector gradients
+template <int BR>
+__device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16], const Saved& sv, int lane,
+                                            int wave) {
+  opq(lane, wave);
+  const int g = lane >> 4, r = 16 * wave + (lane & 15);
+  const uchar* vec = smem + B_VEC;
+  uchar* cs = smem + B_CS;
+  float dr2[16];
+  sb();
+  {  // LayerNorm 3 and 2 backward (xh3 = LN(xh2 * gamma2 + beta2) recomputed: fewer saved registers)
+    float gm[16], t[16], dx[16], xh[16], bt[16];
+    load16(xh, sv.xh2);
+    vec16(gm, vec + VS_G2 * 256, g);
+    vec16(bt, vec + VS_B2 * 256, g);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xh[j] = xh[j] * gm[j] + bt[j];
+    const float rstd3 = fk::ln_fwd(xh);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
+    colsum64(cs + VS_G3 * 256, t, lane);
+    colsum64(cs + VS_B3 * 256, dout, lane);
+    vec16(gm, vec + VS_G3 * 256, g);
+    fk::ln_bwd(dx, dout, xh, rstd3, gm);
+    load16(xh, sv.xh2);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    colsum64(cs + VS_G2 * 256, t, lane);
+    colsum64(cs + VS_B2 * 256, dx, lane);
+    vec16(gm, vec + VS_G2 * 256, g);
+    fk::ln_bwd(dr2, dx, xh, sv.rstd2, gm);
+  }
+  float df0[4];
+  sb();
+  {  // d(ffn.3 out) -> ffn.3 backward (d f2) -> d(ffn.0 pre-activation)
+    float d3[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d3[j] = bit(sv.m2, j) ? dr2[j] * INV_K01 : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DF3, r, 4 * t + g, d3 + 4 * t);
+    f4v acc = mma(wtfrag<true>(smem + B_IMG_F2, LD32, 0, 0, lane), bfrag(d3, 0), Z4);
+    acc = mma(wtfrag<true>(smem + B_IMG_F2, LD32, 0, 1, lane), bfrag(d3, 1), acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) df0[i] = acc[i] * sv.gk[i];
+    st4<TK16>(smem + B_DF0, r, g, df0);
+  }
+  float dr1[16];
+  sb();
+  {  // ffn.0 backward (d x1n) + residual, LayerNorm 1 backward
+    const s8v bd = bfrag_lo(df0);
+    float dx[16];
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      const f4v acc = mma(wtfrag<false>(smem + B_IMG_F1, LD64, T, 0, lane), bd, Z4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dx[4 * T + i] = acc[i] + dr2[4 * T + i];
+    }
+    float t[16], gm[16], xh[16];
+    load16(xh, sv.xh1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
+    colsum64(cs + VS_G1 * 256, t, lane);
+    colsum64(cs + VS_B1 * 256, dx, lane);
+    vec16(gm, vec + VS_G1 * 256, g);
+    fk::ln_bwd(dr1, dx, xh, sv.rstd1, gm);
+  }
+  float dv[16];
+  sb();
+  {  // out_proj backward: d a = d o . Wo ; d v = attention-dropout'(d a)
+    float dO[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dO[j] = bit(sv.m1, j) ? dr1[j] * INV_K01 : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DO, r, 4 * t + g, dO + 4 * t);
+    const s8v b0 = bfrag(dO, 0), b1 = bfrag(dO, 1);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      f4v acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
+      acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 1, lane), b1, acc);
+      const float m = bit(sv.matt, T) ? INV_K01 : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dv[4 * T + i] = acc[i] * m;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DV, r, 4 * t + g, dv + 4 * t);
+  }
+  sb();
+  {  // v backward: d h0 = d r1 + d v . Wv ; d z0 = d h0 * gelu'(z0)
+    const s8v b0 = bfrag(dv, 0), b1 = bfrag(dv, 1);
+    float dz[16], gp[16];
+    load16(gp, sv.gp);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      f4v acc = mma(wtfrag<true>(smem + B_IMG_V, LD64, T, 0, lane), b0, Z4);
+      acc = mma(wtfrag<true>(smem + B_IMG_V, LD64, T, 1, lane), b1, acc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dz[4 * T + i] = (acc[i] + dr1[4 * T + i]) * gp[4 * T + i];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DZ0, r, 4 * t + g, dz + 4 * t);
+  }
+}
+
+// bias gradient = column sums of a dY tile: the dW GEMM with an all-ones X fragment (every row of the
+// 16x16 result equals the sums of the 16 columns of dY tile Tn)
+__device__ __forceinline__ s8v ones8() {
+  const short o = (short)0x3F80;  // bf16 1.0
+  return s8v{o, o, o, o, o, o, o, o};
+}
+
+// compact entry e of branch BR: flat parameter index (or -1), where the new value goes
+template <int BR>
+__device__ __forceinline__ int cmp_param(int e) {
+  using C = Cmp<BR>;
+  using B = BrK<BR>;
+  if (e < B_NVEC) return B::vec_param(e);
+  if (e < C::E_F1) return B::o.dense_w + (e - C::E_D);
+  if (e < C::E_F2) return B::o.ff0_w + (e - C::E_F1);
+  if (e < C::N) return B::o.ff3_w + (e - C::E_F2);
+  return -1;
+}
+// bf16 image byte offset of compact weight entry e (>= 648)
+template <int BR>
+__device__ __forceinline__ int cmp_img(int e) {
+  using C = Cmp<BR>;
+  if (e < C::E_F1) {
+    const int i = e - C::E_D, n = i / C::din, k = i % C::din;
+    return B_IMG_D + n * LD32 + pcol(k) * 2;
+  }
+  if (e < C::E_F2) {
+    const int i = e - C::E_F1, n = i >> 6, k = i & 63;
+    return B_IMG_F1 + n * LD64 + pcol(k) * 2;
+  }
+  const int i = e - C::E_F2, n = i / FF, k = i % FF;
+  return B_IMG_F2 + n * LD32 + pcol(k) * 2;
+}
+
+// Weight gradients + Adam for one step (after the barrier that ends the backward).  Three parts:
+//  U1  small weight-gradient tiles (dense: waves 0-3, ffn.3: waves 4-7, ffn.0: every wave one k tile of
+//      the 4) in registers; barrier (their X operands XIN / F2 die, their space stages the gradients);
+//  U2  small-tile gradients -> compact staging; the 2x2 v / out_proj block of the wave -> Adam -> image;
+//      bias sums of the dY tiles -> CS; barrier;
+//  U3  every thread: Adam on its compact entries -> VEC / images.  Gradient vector CS reset.
+template <int BR>
+__device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid) {
+  using B = BrK<BR>;
+  opq(lane, wave);
+  asm volatile("" : "+v"(tid));
+  using C = Cmp<BR>;
+  const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
+  const bool lo = wave < 4;
+  // ---- U1
+  f4v as = Z4, af1 = Z4;
+  {
+    // waves 0-3: dense tile (k 0..15, n tile w4): X = xin, dY = dz0 ; waves 4-7: ffn.3 tile: X = f2, dY = d f3
+    const uchar* X = smem + (lo ? B_XIN : B_F2);
+    const uchar* DY = smem + (lo ? B_DZ0 : B_DF3);
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      as = mma(tfrag<TK16>(X, 32 * s, 0, lane), tfrag<TK64>(DY, 32 * s, w4, lane), as);
+      // ffn.0: waves w and w + 4 split the 128 rows of k tile w4 (rows 64 (w >> 2) .. + 63)
+      if (s < 2) {
+        const int r0 = 64 * (wave >> 2) + 32 * s;
+        af1 = mma(tfrag<TK64>(smem + B_X1N, r0, w4, lane), tfrag<TK16>(smem + B_DF0, r0, 0, lane), af1);
+      }
+    }
+  }
+  lds_bar();
+  // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
+  {
+    LDS_AS float* gs = ldsf(smem, B_GS);
+    const int n = 16 * w4 + i16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 4 * g + i;
+      if (lo) {
+        if (k < C::din) gs[C::E_D - B_NVEC + n * C::din + k] = as[i];
+      } else {
+        if (k < FF) gs[C::E_F2 - B_NVEC + n * FF + k] = as[i];
+      }
+    }
+    // ffn.0 partial sums of the two row halves: wave w4 writes, wave w4 + 4 adds after the next barrier
+  }
+  {  // 2x2 block of v (waves 0-3: X = h0, dY = dv) or out_proj (waves 4-7: X = a, dY = do), bias sums
+    const uchar* X = smem + (lo ? B_H0 : B_A);
+    const uchar* DY = smem + (lo ? B_DV : B_DO);
+    const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+    f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
+    f4v bs[2] = {Z4, Z4};
+    const bool do_bias = (w4 & 1) == 0;  // one of the two waves that read dY tiles Tb, Tb + 1
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      const s8v x0 = tfrag<TK64>(X, 32 * s, Ta, lane), x1 = tfrag<TK64>(X, 32 * s, Ta + 1, lane);
+      const s8v y0 = tfrag<TK64>(DY, 32 * s, Tb, lane), y1 = tfrag<TK64>(DY, 32 * s, Tb + 1, lane);
+      acc[0][0] = mma(x0, y0, acc[0][0]);
+      acc[0][1] = mma(x0, y1, acc[0][1]);
+      acc[1][0] = mma(x1, y0, acc[1][0]);
+      acc[1][1] = mma(x1, y1, acc[1][1]);
+      if (do_bias) {
+        bs[0] = mma(ones8(), y0, bs[0]);
+        bs[1] = mma(ones8(), y1, bs[1]);
+      }
+    }
+    const Mat M = lo ? B::MV : B::MO;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) tile_adam(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
+    if (do_bias && g == 0) {
+      LDS_AS float* cs = ldsf(smem, B_CS) + (lo ? VS_VB : VS_OB) * 64;
+      cs[16 * Tb + i16] = bs[0][0];
+      cs[16 * (Tb + 1) + i16] = bs[1][0];
+    }
+  }
+  {  // dense / ffn.3 bias sums (dY tile w4 of dz0 / d f3), ffn.0 bias (d f0, 6 columns)
+    f4v bs = Z4, b1 = Z4;
+    const uchar* DY = smem + (lo ? B_DZ0 : B_DF3);
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      bs = mma(ones8(), tfrag<TK64>(DY, 32 * s, w4, lane), bs);
+      if (wave == 0) b1 = mma(ones8(), tfrag<TK16>(smem + B_DF0, 32 * s, 0, lane), b1);
+    }
+    if (g == 0) {
+      ldsf(smem, B_CS)[(lo ? VS_DB : VS_F2B) * 64 + 16 * w4 + i16] = bs[0];
+      if (wave == 0 && i16 < FF) ldsf(smem, B_CS)[VS_F1B + i16] = b1[0];
+    }
+  }
+  if (wave >= 4) {  // ffn.0 (k tile w4, n 0..5): first row half
+    LDS_AS float* gs = ldsf(smem, B_GS);
+    if (i16 < FF)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
+  }
+  lds_bar();
+  if (wave < 4) {  // ffn.0: second row half added
+    LDS_AS float* gs = ldsf(smem, B_GS);
+    if (i16 < FF)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] += af1[i];
+  }
+  lds_bar();
+  // ---- U3: compact entries
+#pragma unroll
+  for (int h = 0; h < NCMP; ++h) {
+    const int e = tid + NTH * h;
+    if (e < C::N) {
+      const int pi = cmp_param<BR>(e);
+      if (e < B_NVEC) {
+        LDS_AS float* cs = ldsf(smem, B_CS) + e;
+        const float gsum = *cs;
+        *cs = 0.f;
+        if (pi >= 0) ldsf(smem, B_VEC)[e] = adam1(st.cmp[h].p, st.cmp[h].m, st.cmp[h].v, gsum, K);
+      } else {
+        const float gr = ldsf(smem, B_GS)[e - B_NVEC];
+        const float pn = adam1(st.cmp[h].p, st.cmp[h].m, st.cmp[h].v, gr, K);
+        *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(pn);
+      }
+    }
+  }
+}
+
+template <int BR>
+__device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P, int lane, int wave, int tid) {
+  using B = BrK<BR>;
+  using C = Cmp<BR>;
+  const int w4 = wave & 3;
+  const Mat M = wave < 4 ? B::MV : B::MO;
+  const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) tile_load(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, P, smem);
+#pragma unroll
+  for (int h = 0; h < NCMP; ++h) {
+    const int e = tid + NTH * h;
+    float p0 = 0.f;
+    if (e < C::N) {
+      const int pi = cmp_param<BR>(e);
+      p0 = pi >= 0 ? P[pi] : 0.f;
+      if (e < B_NVEC) {
+        ldsf(smem, B_VEC)[e] = p0;
+        ldsf(smem, B_CS)[e] = 0.f;
+      } else {
+        *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(p0);
+      }
+    }
+    st.cmp[h] = VS{aw(p0), aw(0.f), aw(0.f)};
+  }
+}
+
+template <int BR>
+__device__ __forceinline__ void br_fini(const BrState& st, float* P, int lane, int wave, int tid) {
+  using B = BrK<BR>;
+  using C = Cmp<BR>;
+  const int w4 = wave & 3;
+  const Mat M = wave < 4 ? B::MV : B::MO;
+  const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) tile_store(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, P);
+#pragma unroll
+  for (int h = 0; h < NCMP; ++h) {
+    const int e = tid + NTH * h;
+    if (e < C::N) {
+      const int pi = cmp_param<BR>(e);
+      if (pi >= 0) P[pi] = ar(st.cmp[h].p);
+    }
+  }
+}
+
+// this lane's 4 input features (4g + i) of row r of the batch starting at b0 of epoch e
+template <int BR>
+__device__ __forceinline__ void load_x(float (&x)[4], const AflTfTrainArgs& a, int cid, const Walk& w, int r, int g) {
+  const int Bn = min(a.batch, a.nd[cid] - w.b0);
+  const gi32* ord = (const gi32*)(a.order + ((long)cid * a.E + w.e) * a.maxnd);
+  const bool valid = r < Bn;
+  const int ridx = valid ? ord[w.b0 + r] : 0;
+  const gf* row = (const gf*)a.rows + (long)ridx * ROW + BrK<BR>::xoff;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * g + i;
+    x[i] = (valid && c < BrK<BR>::din) ? row[c] : 0.f;
+  }
+}
+
+template <int BR>
+__device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  float* P = a.params + (long)cid * NPARAM;
+  uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
+  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
+  __syncthreads();
+  BrState st;
+  br_init<BR>(smem, st, P, lane, wave, tid);
+  __syncthreads();
+
+  const int nd = a.nd[cid], BS = a.batch, E = a.E;
+  const uint32_t seed = a.seeds[cid];
+  LDS_AS uint32_t* abort_w = ldsu(smem, B_MISC);
+  double b1t = 1.0, b2t = 1.0;
+  int step = 0;
+  bool failed = false;
+  Walk w{0, 0};
+  float xin[4];
+  bool more = walk_valid(w, nd, BS, E);
+  if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+  while (more) {
+    ++step;
+    b1t *= (double)fk::B1;
+    b2t *= (double)fk::B2;
+    const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+    const uint32_t key = afl_hash32(seed, (uint32_t)step);
+    Saved sv;
+    u32x4 outp[2];
+    asm volatile(";MARK fwd");
+#ifndef TF2_NO_FWD
+    br_forward<BR>(smem, xin, key, sv, outp, lane, wave);
+#else
+    sv = Saved{}; outp[0] = u32x4{0,0,0,0}; outp[1] = outp[0];
+#endif
+    asm volatile(";MARK fwd_end");
+    {  // publish this wave's output rows
+      const int off = (int)WS_XF + BR * 16384 + (wave * 64 + lane) * 32;
+      st_wt(rs, off, outp[0]);
+      st_wt(rs, off + 16, outp[1]);
+      publish(xf(sync, BR == 0 ? XF_VIT : XF_LAB, wave), (uint32_t)step, lane);
+    }
+    w.b0 += BS;  // prefetch the next batch's inputs while the head works
+    more = walk_valid(w, nd, BS, E);
+    if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+    gu32* fb = xf(sync, BR == 0 ? XF_BVIT : XF_BLAB, wave);
+    const uint32_t fv = await(fb, fb, (uint32_t)step, 1, sync + XF_TMO, lane);
+    if (fv == 0xFFFFFFFFu) {
+      failed = true;
+      break;
+    }
+    float dout[16];
+    {
+      const int off = (int)WS_XB + BR * 16384 + (wave * 64 + lane) * 32;
+      u32x4 u[2] = {ld_wt(rs, off), ld_wt(rs, off + 16)};
+      unpack16(u, dout);
+    }
+    if (lane == 0) abort_w[wave] = fv & 1u;
+#ifndef TF2_NO_BWD
+    asm volatile(";MARK bwd");
+    br_backward<BR>(smem, dout, sv, lane, wave);
+    asm volatile(";MARK bwd_end");
+#else
+    for (int j = 0; j < 16; ++j) asm volatile("" :: "v"(dout[j]));
+#endif
+    lds_bar();
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) any |= abort_w[i];
+    if (any) {  // the head saw a NaN loss: the client's round fails, this step's update is not applied
+      failed = true;
+      break;
+    }
+#ifndef TF2_NO_UPD
+    asm volatile(";MARK upd");
+    br_update<BR>(smem, st, K, lane, wave, tid);
+    asm volatile(";MARK upd_end");
+#endif
+    lds_bar();
+  }
+  (void)failed;
+  br_fini<BR>(st, P, lane, wave, tid);
+}
+
+// ================================================================================= head workgroup
+constexpr Mat HW1{FC1_W, 64, 128, H_IMG_W1, LD128};
+constexpr Mat HW2{FC2_W, 32, 64, H_IMG_W2, LD64};
+__device__ __forceinline__ int hvec_param(int e) {
+  return e < 64 ? FC1_B + e : e < 96 ? FC2_B + (e - 64) : e < 128 ? OUT_W + (e - 96) : e == 128 ? OUT_B : -1;
+}
+struct HdState {
+  TS blk[4];  // fc1: k tiles 2(w&3)+{0,1} x n tiles 2(w>>2)+{0,1}
+  TS t2;      // fc2: k tile w&3, n tile w>>2
+  VS vec;
+};
+
+__device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  const int r = 16 * wave + (lane & 15);
+  float* P = a.params + (long)cid * NPARAM;
+  uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
+  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
+  __syncthreads();
+  HdState st;
+  {
+    const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) tile_load(st.blk[2 * x + y], HW1, Ta + x, Tb + y, lane, P, smem);
+    tile_load(st.t2, HW2, wave & 3, wave >> 2, lane, P, smem);
+    float p0 = 0.f;
+    if (tid < H_NVEC) {
+      const int pi = hvec_param(tid);
+      p0 = pi >= 0 ? P[pi] : 0.f;
+      ldsf(smem, H_VEC)[tid] = p0;
+      ldsf(smem, H_CS)[tid] = 0.f;
+    }
+    st.vec = VS{aw(p0), aw(0.f), aw(0.f)};
+  }
+  __syncthreads();
+
+  const int nd = a.nd[cid], BS = a.batch, E = a.E;
+  const int nb_total = (nd + BS - 1) / BS;
+  const uint32_t seed = a.seeds[cid];
+  const uchar* vec = smem + H_VEC;
+  uchar* cs = smem + H_CS;
+  LDS_AS float* lossw = ldsf(smem, H_LOSS);
+  double b1t = 1.0, b2t = 1.0;
+  int step = 0;
+  bool failed = false, timed_out = false;
+  float epoch_loss = 0.f;
+  Walk w{0, 0};
+  int cur_e = 0;
+  bool more = walk_valid(w, nd, BS, E);
+  float lab = 0.f;
+  auto load_lab = [&](const Walk& ww) {
+    const int Bn = min(BS, nd - ww.b0);
+    const gi32* ord = (const gi32*)(a.order + ((long)cid * E + ww.e) * a.maxnd);
+    lab = r < Bn ? ((const gf*)a.rows)[(long)ord[ww.b0 + r] * ROW + ROW - 1] : 0.f;
+  };
+  if (more) load_lab(w);
+  while (more) {
+    // epoch boundaries crossed since the previous step (skipped batches included) close epoch losses
+    while (cur_e < w.e) {
+      if (tid == 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
+      epoch_loss = 0.f;
+      ++cur_e;
+    }
+    ++step;
+    b1t *= (double)fk::B1;
+    b2t *= (double)fk::B2;
+    const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+    const uint32_t key = afl_hash32(seed, (uint32_t)step);
+    const int Bn = min(BS, nd - w.b0);
+    const bool valid = r < Bn;
+    // ---- branch outputs of this wave's rows
+    const uint32_t fv = await(xf(sync, XF_VIT, wave), xf(sync, XF_LAB, wave), (uint32_t)step, 0, sync + XF_TMO, lane);
+    if (fv == 0xFFFFFFFFu) {
+      timed_out = failed = true;
+      break;
+    }
+    u32x4 cv[4];
+    {
+      const int off = (int)WS_XF + (wave * 64 + lane) * 32;
+      cv[0] = ld_wt(rs, off);
+      cv[1] = ld_wt(rs, off + 16);
+      cv[2] = ld_wt(rs, off + 16384);
+      cv[3] = ld_wt(rs, off + 16384 + 16);
+    }
+    // cat -> LDS (X of dWf1): tile t of the 8 = half (t & 1) of cv[t >> 1]
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const u32x4 u = cv[t >> 1];
+      const u32x2v v = (t & 1) ? u32x2v{u[2], u[3]} : u32x2v{u[0], u[1]};
+      *(LDS_AS u32x2v*)(smem + H_CAT + t128(r, 4 * t + g)) = v;
+    }
+    // ---- fc1 + GELU + dropout(0.3)
+    float a1[16], gk1[16];
+    {
+      f4v acc[4];
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        acc[T] = Z4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
+      }
+      const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
+      float b1[16];
+      vec16(b1, vec + HV_B1 * 4, g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 4 * t + i;
+          float gp;
+          const float gl = gelu_and_grad(acc[t][i] + b1[j], gp);
+          a1[j] = bit(mh, j) ? gl * INV_K03 : 0.f;
+          gk1[j] = bit(mh, j) ? gp * INV_K03 : 0.f;
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, r, 4 * t + g, a1 + 4 * t);
+    }
+    // ---- fc2 + GELU, output layer, sigmoid, BCE (log clamped at -100)
+    float dz2[8];
+    float lrow = 0.f, dy3 = 0.f;
+    {
+      const s8v b0 = bfrag(a1, 0), b1 = bfrag(a1, 1);
+      f4v acc[2];
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 0, lane), b0, Z4);
+        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 1, lane), b1, acc[T]);
+      }
+      float b2[8], wo[8], g2[8], gp2[8];
+      vec8(b2, vec + HV_B2 * 4, g);
+      vec8(wo, vec + HV_WO * 4, g);
+      float dot = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 4 * t + i;
+          g2[j] = gelu_and_grad(acc[t][i] + b2[j], gp2[j]);
+          dot += g2[j] * wo[j];
+        }
+      const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
+      const float p = sigmoidf_(y3);
+      if (valid) {
+        // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
+        const float lg = logf(p), lg1 = log1pf(-p);
+        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
+        lrow = -(lab * lp + (1.f - lab) * l1p);
+        const float pq = p * (1.f - p);
+        dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
+      }
+      float gw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dz2[j] = dy3 * wo[j] * gp2[j];
+        gw[j] = dy3 * g2[j];
+      }
+      colsum32(cs + HV_B2 * 4, dz2, lane);
+      colsum32(cs + HV_WO * 4, gw, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, r, 4 * t + g, dz2 + 4 * t);
+    }
+    // per-wave loss partial and d output.bias (each row counted once: lane group 0)
+    float lsum = wave_sum(g == 0 ? lrow : 0.f);
+    const float dbo = wave_sum(g == 0 ? dy3 : 0.f);
+    if (lane == 0) {
+      lossw[wave] = lsum;
+      lds_add(cs + HV_BO * 4, dbo);
+    }
+    const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
+    // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
+    float dz1[16];
+    {
+      const s8v bz = bfrag(dz2, 0);
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        const f4v acc = mma(wtfrag<true>(smem + H_IMG_W2, LD64, T, 0, lane), bz, Z4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
+      }
+      colsum64(cs + HV_B1 * 4, dz1, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, r, 4 * t + g, dz1 + 4 * t);
+    }
+    // ---- d cat = dz1 . W1, each half straight to its branch
+    {
+      const s8v b0 = bfrag(dz1, 0), b1 = bfrag(dz1, 1);
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float d[16];
+#pragma unroll
+        for (int Tl = 0; Tl < 4; ++Tl) {
+          const int T = 4 * hb + Tl;
+          f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 0, lane), b0, Z4);
+          acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 1, lane), b1, acc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) d[4 * Tl + i] = acc[i];
+        }
+        u32x4 u[2];
+        pack16(d, u);
+        const int off = (int)WS_XB + hb * 16384 + (wave * 64 + lane) * 32;
+        st_wt(rs, off, u[0]);
+        st_wt(rs, off + 16, u[1]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both payloads written through, then both flags
+      if (lane == 0) {
+        const uint32_t fl = ((uint32_t)step << 1) | wave_nan;
+        __hip_atomic_store(xf(sync, XF_BVIT, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(xf(sync, XF_BLAB, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // the next step's labels (after the hand-off stores: their drain above must not wait for these)
+    Walk wn = w;
+    wn.b0 += BS;
+    more = walk_valid(wn, nd, BS, E);
+    lds_bar();
+    {
+      float tot = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) tot += lossw[i];
+      const float loss = tot / (float)Bn;
+      if (loss != loss) {  // uniform across the workgroup; the branches see the per-wave NaN flags
+        failed = true;
+        break;
+      }
+      epoch_loss += loss;
+    }
+    if (more) load_lab(wn);
+    w = wn;
+    // ---- weight gradients + Adam
+    {
+      const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
+      f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
+      f4v a2 = Z4;
+      const int T2 = wave & 3, Tn2 = wave >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const s8v x0 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta, lane), x1 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta + 1, lane);
+        const s8v y0 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb, lane), y1 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb + 1, lane);
+        acc[0][0] = mma(x0, y0, acc[0][0]);
+        acc[0][1] = mma(x0, y1, acc[0][1]);
+        acc[1][0] = mma(x1, y0, acc[1][0]);
+        acc[1][1] = mma(x1, y1, acc[1][1]);
+        a2 = mma(tfrag<TK64>(smem + H_A1, 32 * s, T2, lane), tfrag<TK32>(smem + H_DZ2, 32 * s, Tn2, lane), a2);
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) tile_adam(st.blk[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
+      tile_adam(st.t2, HW2, T2, Tn2, lane, a2, K, smem);
+      if (tid < H_NVEC) {
+        LDS_AS float* c = ldsf(smem, H_CS) + tid;
+        const float gsum = *c;
+        *c = 0.f;
+        if (hvec_param(tid) >= 0) ldsf(smem, H_VEC)[tid] = adam1(st.vec.p, st.vec.m, st.vec.v, gsum, K);
+      }
+    }
+    lds_bar();
+  }
+  if (!failed) {
+    while (cur_e < E) {  // the last epoch (and trailing epochs that had no step)
+      if (tid == 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
+      epoch_loss = 0.f;
+      ++cur_e;
+    }
+  }
+  // parameters back (a failed client keeps its pre-step values: the failing step applied no update)
+  {
+    const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) tile_store(st.blk[2 * x + y], HW1, Ta + x, Tb + y, lane, P);
+    tile_store(st.t2, HW2, wave & 3, wave >> 2, lane, P);
+    if (tid < H_NVEC && hvec_param(tid) >= 0) P[hvec_param(tid)] = ar(st.vec.p);
+  }
+  if (tid == 0) {
+    const bool tmo = timed_out || __hip_atomic_load(sync + XF_TMO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.ok[cid] = tmo ? -1 : (failed ? 0 : 1);
+  }
+}
+
+}  // namespace t2
+
+// 3 workgroups per client: 3c (head), 3c + 1 (vitals branch), 3c + 2 (labs branch)
+__global__ void __launch_bounds__(t2::NTH) k_tf2_train(AflTfTrainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int role = blockIdx.x % 3, cid = blockIdx.x / 3;
+#if defined(TF2_ROLE)
+  if (TF2_ROLE == 0) t2::head_main(a, cid, smem);
+  else if (TF2_ROLE == 1) t2::branch_main<0>(a, cid, smem);
+  else t2::branch_main<1>(a, cid, smem);
+  (void)role;
+#else
+  if (role == 0)
+    t2::head_main(a, cid, smem);
+  else if (role == 1)
+    t2::branch_main<0>(a, cid, smem);
+  else
+    t2::branch_main<1>(a, cid, smem);
+#endif
+}
+
+long afl_tf2_ws_floats() { return t2::WS_BYTES / 4; }
+
+int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
+  if (a->batch > 128 || a->batch < 2 || !a->sync) return -1;
+  if (hipFuncSetAttribute((const void*)k_tf2_train, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess)
+    return -2;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -3;
+  if (3 * a->C > cus) return -4;  // the workgroups of a client spin on each other: all must be resident
+  hipLaunchKernelGGL(k_tf2_train, dim3(3 * a->C), dim3(t2::NTH), t2::SMEM, s, *a);
+  return 0;
+}
