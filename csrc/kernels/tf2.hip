@@ -61,7 +61,17 @@ constexpr int B_DF0 = B_F2 + 4096;                 // tile16: d(ffn.0 pre-activa
 constexpr int B_NVEC = 648;                        // 10 x 64 vectors + ffn.0 bias (8 slots, 6 real)
 constexpr int B_VEC = B_DF0 + 4096;                // fp32 [648] bias / LayerNorm parameters
 constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [648] their gradients (column sums)
-constexpr int B_MISC = B_CS + B_NVEC * 4;          // u32 [8] per-wave abort words
+// The LayerNorm gradient column sums (6 x 64, produced wave-locally during the backward) are summed over
+// the 8 waves with fp64 LDS atomics into DBL, which ALIASES CS (+ 480 bytes): the remaining CS entries are
+// written only after the backward, and the fp64 sums are moved to their CS slots at the start of the
+// update.  fp64 makes the 8-way sum independent of the order the waves arrive in (exact whenever the
+// partials span < 2^26; otherwise a double rounding below fp32 resolution), so a client's trajectory is
+// bit-reproducible whatever launch or rank trains it (fp32 LDS atomics were not: ~1e-4 drift per round).
+constexpr int B_NLN = 6 * 64;
+constexpr int B_DBL = B_CS;                        // fp64 [384]: G1 B1 G2 B2 G3 B3
+constexpr int B_DBL_BYTES = B_NLN * 8;
+static_assert(B_DBL_BYTES >= B_NVEC * 4, "DBL covers CS");
+constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words
 constexpr int B_TOTAL = B_MISC + 64;
 // vector segments (x64 floats) of VEC / CS
 enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3 };
@@ -76,8 +86,8 @@ constexpr int H_DZ1 = H_A1 + 16384;                // tile64:  d(fc1 pre-activat
 constexpr int H_DZ2 = H_DZ1 + 16384;               // tile32:  d(fc2 pre-activation) (dY of dWf2)
 constexpr int H_NVEC = 132;                        // fc1.b 64 | fc2.b 32 | output.w 32 | output.b 1
 constexpr int H_VEC = H_DZ2 + 8192;
-constexpr int H_CS = H_VEC + H_NVEC * 4;
-constexpr int H_LOSS = H_CS + H_NVEC * 4;          // fp32 [8] per-wave loss partials
+constexpr int H_PART = H_VEC + H_NVEC * 4;         // fp32 [8 waves][132] per-wave column sums (their gradients)
+constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss partials
 constexpr int H_TOTAL = H_LOSS + 64;
 enum { HV_B1 = 0, HV_B2 = 64, HV_WO = 96, HV_BO = 128 };
 
@@ -199,10 +209,11 @@ __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  
   }
 }
 
-// column sums over the wave's 16 rows of W values per lane (DPP reduce-scatter, fused_common.h), added
-// into the fp32 LDS gradient vector: value j of lane group g is feature feat(g, j)
-__device__ __forceinline__ void lds_add(uchar* p, float v) {
-  __hip_atomic_fetch_add((LDS_AS float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+// column sums over the wave's 16 rows of W values per lane (DPP reduce-scatter, fused_common.h): each
+// lane ends with the sum of one feature; the caller sends it to a per-wave slot (head) or an fp64 LDS
+// accumulator (branches)
+__device__ __forceinline__ void lds_addd(uchar* base, int idx, float v) {
+  __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 template <int W>
 __device__ __forceinline__ int rs_slot(float (&s)[W], int i) {
@@ -215,33 +226,34 @@ __device__ __forceinline__ int rs_slot(float (&s)[W], int i) {
   if constexpr (W <= 8) s[0] += fk::dpp_pair<3>(s[0]);
   return j;
 }
-// 16 values (64 features, T layout) -> cs[feature]
-__device__ __forceinline__ void colsum64(uchar* cs, const float (&x)[16], int lane) {
+// 16 values (64 features, T layout) -> (feature of this lane, its column sum)
+__device__ __forceinline__ int colsum64(const float (&x)[16], int lane, float& sum) {
   float s[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) s[j] = x[j];
   const int j = rs_slot<16>(s, lane & 15);
-  lds_add(cs + (16 * (j >> 2) + 4 * (lane >> 4) + (j & 3)) * 4, s[0]);
+  sum = s[0];
+  return 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
 }
-// 8 values (32 features: tiles 0, 1)
-__device__ __forceinline__ void colsum32(uchar* cs, const float (&x)[8], int lane) {
+// 8 values (32 features: tiles 0, 1); only lanes with (lane & 8) == 0 hold a sum (returns -1 otherwise)
+__device__ __forceinline__ int colsum32(const float (&x)[8], int lane, float& sum) {
   float s[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = x[j];
   const int i = lane & 15;
   const int j = rs_slot<8>(s, i);
-  if ((i & 8) == 0) lds_add(cs + (16 * (j >> 2) + 4 * (lane >> 4) + (j & 3)) * 4, s[0]);
+  sum = s[0];
+  return (i & 8) == 0 ? 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3) : -1;
 }
-// 4 values (16 features: tile 0), only features < nreal
-__device__ __forceinline__ void colsum16(uchar* cs, const float (&x)[4], int lane, int nreal) {
-  float s[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s[j] = x[j];
-  const int i = lane & 15;
-  const int j = rs_slot<4>(s, i);
-  const int f = 4 * (lane >> 4) + j;
-  if ((i & 10) == 0 && f < nreal) lds_add(cs + f * 4, s[0]);
+// branch LayerNorm column sums -> fp64 accumulator k of DBL (order G1 B1 G2 B2 G3 B3)
+__device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
+  float s;
+  const int f = colsum64(x, lane, s);
+  lds_addd(smem + B_DBL, 64 * k + f, s);
 }
+__host__ __device__ constexpr int ln_seg(int k) { return k < 2 ? VS_G1 + k : VS_G2 + (k - 2); }
+static_assert(ln_seg(0) == VS_G1 && ln_seg(1) == VS_B1 && ln_seg(2) == VS_G2 && ln_seg(3) == VS_B2 &&
+              ln_seg(4) == VS_G3 && ln_seg(5) == VS_B3, "DBL order");
 
 // dropout keep bits of features 16t + 4g + i (bit 4t + i), hash pairs as tf::keep
 __device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, int g, uint32_t thr) {
@@ -638,7 +650,6 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
   const uchar* vec = smem + B_VEC;
-  uchar* cs = smem + B_CS;
   float dr2[16];
   sb();
   {  // LayerNorm 3 and 2 backward (xh3 = LN(xh2 * gamma2 + beta2) recomputed: fewer saved registers)
@@ -651,15 +662,15 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     const float rstd3 = fk::ln_fwd(xh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
-    colsum64(cs + VS_G3 * 256, t, lane);
-    colsum64(cs + VS_B3 * 256, dout, lane);
+    ln_colsum(smem, 4, t, lane);
+    ln_colsum(smem, 5, dout, lane);
     vec16(gm, vec + VS_G3 * 256, g);
     fk::ln_bwd(dx, dout, xh, rstd3, gm);
     load16(xh, sv.xh2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    colsum64(cs + VS_G2 * 256, t, lane);
-    colsum64(cs + VS_B2 * 256, dx, lane);
+    ln_colsum(smem, 2, t, lane);
+    ln_colsum(smem, 3, dx, lane);
     vec16(gm, vec + VS_G2 * 256, g);
     fk::ln_bwd(dr2, dx, xh, sv.rstd2, gm);
   }
@@ -692,8 +703,8 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     load16(xh, sv.xh1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    colsum64(cs + VS_G1 * 256, t, lane);
-    colsum64(cs + VS_B1 * 256, dx, lane);
+    ln_colsum(smem, 0, t, lane);
+    ln_colsum(smem, 1, dx, lane);
     vec16(gm, vec + VS_G1 * 256, g);
     fk::ln_bwd(dr1, dx, xh, sv.rstd1, gm);
   }
@@ -798,7 +809,10 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
       }
     }
   }
+  // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
+  const float lnsum = tid < B_NLN ? (float)((LDS_AS double*)(smem + B_DBL))[tid] : 0.f;
   lds_bar();
+  if (tid < B_NLN) ldsf(smem, B_CS)[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
   // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
   {
     LDS_AS float* gs = ldsf(smem, B_GS);
@@ -872,7 +886,8 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
       for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] += af1[i];
   }
   lds_bar();
-  // ---- U3: compact entries
+  // ---- U3: compact entries (CS is zeroed as it is consumed; the DBL bytes past CS here)
+  if (tid < (B_DBL_BYTES - B_NVEC * 4) / 4) ldsf(smem, B_CS)[B_NVEC + tid] = 0.f;
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
@@ -1077,7 +1092,6 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
       const int pi = hvec_param(tid);
       p0 = pi >= 0 ? P[pi] : 0.f;
       ldsf(smem, H_VEC)[tid] = p0;
-      ldsf(smem, H_CS)[tid] = 0.f;
     }
     st.vec = VS{aw(p0), aw(0.f), aw(0.f)};
   }
@@ -1087,7 +1101,7 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
   const int nb_total = (nd + BS - 1) / BS;
   const uint32_t seed = a.seeds[cid];
   const uchar* vec = smem + H_VEC;
-  uchar* cs = smem + H_CS;
+  LDS_AS float* part = ldsf(smem, H_PART) + wave * H_NVEC;  // this wave's column sums
   LDS_AS float* lossw = ldsf(smem, H_LOSS);
   double b1t = 1.0, b2t = 1.0;
   int step = 0;
@@ -1204,8 +1218,12 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
         dz2[j] = dy3 * wo[j] * gp2[j];
         gw[j] = dy3 * g2[j];
       }
-      colsum32(cs + HV_B2 * 4, dz2, lane);
-      colsum32(cs + HV_WO * 4, gw, lane);
+      float sb2, swo;
+      const int f2 = colsum32(dz2, lane, sb2), fo = colsum32(gw, lane, swo);
+      if (f2 >= 0) {
+        part[HV_B2 + f2] = sb2;
+        part[HV_WO + fo] = swo;
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, r, 4 * t + g, dz2 + 4 * t);
     }
@@ -1214,7 +1232,7 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
     const float dbo = wave_sum(g == 0 ? dy3 : 0.f);
     if (lane == 0) {
       lossw[wave] = lsum;
-      lds_add(cs + HV_BO * 4, dbo);
+      part[HV_BO] = dbo;
     }
     const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
     // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
@@ -1227,7 +1245,9 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
 #pragma unroll
         for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
       }
-      colsum64(cs + HV_B1 * 4, dz1, lane);
+      float sb1;
+      const int f1 = colsum64(dz1, lane, sb1);
+      part[HV_B1 + f1] = sb1;
 #pragma unroll
       for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, r, 4 * t + g, dz1 + 4 * t);
     }
@@ -1298,9 +1318,11 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
         for (int y = 0; y < 2; ++y) tile_adam(st.blk[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
       tile_adam(st.t2, HW2, T2, Tn2, lane, a2, K, smem);
       if (tid < H_NVEC) {
-        LDS_AS float* c = ldsf(smem, H_CS) + tid;
-        const float gsum = *c;
-        *c = 0.f;
+        // the 8 waves' partial sums in a fixed order: bit-reproducible whatever order the waves ran in
+        const LDS_AS float* c = ldsf(smem, H_PART) + tid;
+        float gsum = c[0];
+#pragma unroll
+        for (int w8 = 1; w8 < 8; ++w8) gsum += c[w8 * H_NVEC];
         if (hvec_param(tid) >= 0) ldsf(smem, H_VEC)[tid] = adam1(st.vec.p, st.vec.m, st.vec.v, gsum, K);
       }
     }

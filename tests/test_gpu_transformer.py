@@ -33,7 +33,7 @@ def test_eval_forward_matches_reference(gpu):
     assert (mod - ref).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("split", [1, 2, 3])
+@pytest.mark.parametrize("split", [1, 2, 3, 4])
 @pytest.mark.parametrize("batch", [128, 100])
 def test_sgd_step_gradients_match(gpu, batch, split):
     """One SGD step (opt_mode 1) exposes the raw gradients: compare p1 - p0 with the oracle."""
@@ -72,7 +72,7 @@ def test_adam_epoch_tracks_reference(gpu):
     assert torch.allclose(loss, loss_r, rtol=0.05, atol=0.02), (loss, loss_r)
 
 
-@pytest.mark.parametrize("split", [1, 2, 3])
+@pytest.mark.parametrize("split", [1, 2, 3, 4])
 def test_nan_params_fail_client(gpu, split):
     rows, params, plan = _setup(2, [300, 300])
     params[1, 5] = float("nan")
@@ -116,3 +116,29 @@ def test_branch_parallel_matches_single_workgroup(gpu):  # noqa: D401
                 moved = (outs[0][0] - params).abs().max().item()
                 assert d < 0.1 * moved, (d, moved)
             assert torch.allclose(outs[0][1], o[1], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("split", [3, 4])
+def test_training_is_bit_reproducible(gpu, split):
+    """A client's result may not depend on the launch that trains it: the multi-rank engine trains
+    clients 0-1 on rank 0 and 2-3 on rank 1 and must equal the single-process run of all four (the
+    on-chip trainer once summed LayerNorm gradients with fp32 LDS atomics in wave-arrival order)."""
+    nd = [700, 650, 900, 801]
+    ds = synthetic_icu(5000, seed=3)
+    rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1).to(gpu)
+    lay = ParamLayout.for_model("TransformerModel")
+    params = torch.stack([lay.flatten(build_model("TransformerModel", seed=i).state_dict()) for i in range(4)]).to(gpu)
+    plan = make_plan(rows.shape[0], nd, 2, torch.Generator().manual_seed(7), gpu)
+    seeds = [101, 102, 103, 104]
+    full = []
+    for _ in range(2):
+        p = params.clone()
+        ok, _ = T.train_clients(p, rows, plan.order, plan.nd, 2, 128, 0.004, seeds, split=split)
+        assert ok.tolist() == [1, 1, 1, 1]
+        full.append(p)
+    assert torch.equal(full[0], full[1])
+    for lo in (0, 2):
+        p = params[lo:lo + 2].clone()
+        T.train_clients(p, rows, plan.order[lo:lo + 2].contiguous(), plan.nd[lo:lo + 2], 2, 128, 0.004,
+                        seeds[lo:lo + 2], split=split)
+        assert torch.equal(p, full[0][lo:lo + 2])
