@@ -80,6 +80,7 @@ constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lin
 // tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations
 // in registers / LDS; 3 workgroups per client, sync words required)
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);
+int afl_tf2_train_stamped(const AflTfTrainArgs* a, hipStream_t s);  // tf2_stamps.hip: per-phase timers
 long afl_tf2_ws_floats();
 // rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
 int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);

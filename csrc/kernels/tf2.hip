@@ -32,7 +32,6 @@ using namespace tf;
 
 namespace t2 {
 
-using fk::AdamK;
 using fk::u32x4;
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 typedef unsigned char uchar;
@@ -91,14 +90,26 @@ constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss par
 constexpr int H_TOTAL = H_LOSS + 64;
 enum { HV_B1 = 0, HV_B2 = 64, HV_WO = 96, HV_BO = 128 };
 
-constexpr int SMEM = B_TOTAL > H_TOTAL ? B_TOTAL : H_TOTAL;
+constexpr int SMEM_CORE = B_TOTAL > H_TOTAL ? B_TOTAL : H_TOTAL;
+#ifdef TF2_STAMPS
+constexpr int ST_OFF = SMEM_CORE, ST_N = 16;       // u64 [16] per-phase timers of the stamped workgroup
+constexpr int SMEM = ST_OFF + ST_N * 8;
+#else
+constexpr int SMEM = SMEM_CORE;
+#endif
 static_assert(SMEM <= 160 * 1024, "LDS budget");
 
 // ------------------------------------------------------------------- per-client workspace (bytes)
 // hand-off payloads: [branch][wave][lane] x 32 bytes (16 bf16 in T layout)
 constexpr long WS_XF = 0;              // branch outputs -> head
 constexpr long WS_XB = WS_XF + 32768;  // d(branch outputs) -> branches
-constexpr long WS_BYTES = WS_XB + 32768;
+// Adam moments of the register-resident weights: per-workgroup slab [slot][thread] of float4 (MOM_SLOTS
+// slots: m and v of the 4 block tiles, then the remaining moments), loaded in one batch of sc1 loads
+// ahead of each update phase and stored back after it (see "Adam" below)
+constexpr int MOM_SLOTS = 11;
+constexpr long WS_MOM = WS_XB + 32768;
+constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
+constexpr long WS_BYTES = WS_MOM + 3 * MOM_WG_BYTES;
 
 // ------------------------------------------------------------------------------ small helpers
 // every LDS access goes through an address_space(3) pointer (a generic one would become FLAT, which
@@ -271,17 +282,56 @@ __device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, 
 }
 __device__ __forceinline__ bool bit(uint32_t m, int j) { return (m >> j) & 1u; }
 
-// ------------------------------------------------------------------------------- Adam in registers
+// ------------------------------------------------------------------------ per-phase timers (diagnostics)
+// Built only into the TF2_STAMPS instantiation (tf2_stamps.hip): s_memrealtime (100 MHz) deltas of
+// wave 0 of ONE workgroup (index in stamps[63]), summed over all steps in LDS, written out at the end.
+// The production kernel gets the empty Stamp below (no code, no registers).
+#ifdef TF2_STAMPS
+// (the previous time stamp lives in LDS slot ST_N - 1 too: a register copy raised the kernel's register
+// pressure enough to change its spills, i.e. the timings being measured)
+struct Stamp {
+  bool on = false;
+  uchar* smem = nullptr;
+  __device__ __forceinline__ void operator()(int id, int tid) {
+    if (!on) return;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      LDS_AS uint64_t* t = (LDS_AS uint64_t*)(smem + ST_OFF);
+      t[id] += now - t[ST_N - 1];
+      t[ST_N - 1] = now;
+    }
+  }
+};
+#else
+struct Stamp {
+  __device__ __forceinline__ void operator()(int, int) {}
+};
+#endif
+
+// ------------------------------------------------------------------------------------------- Adam
+// fp32 master weights live in ACCUMULATION registers (AGPRs) for the whole round: every access goes
+// through v_accvgpr_read / v_accvgpr_write, so the register allocator gives them the AGPR class and the
+// forward / backward working set keeps the architectural VGPRs (the two files share one 256-entry budget
+// per lane at two waves per SIMD).  Their Adam moments m, v do NOT fit beside them: with p, m and v all in
+// AGPRs the allocator spilled ~50 dwords of state to scratch, reloaded one dependent load at a time (~8 us
+// of a 29 us step).  The moments therefore live in the workspace slab (WS_MOM) and every update phase
+// issues all of its moment loads as one batch before the work that precedes the Adam arithmetic.
 struct TS {  // one 16x16 weight-gradient tile's 4 elements of this lane
-  float p[4], m[4], v[4];
+  float p[4];
 };
 struct VS {
-  float p, m, v;
+  float p;
 };
-// The optimizer state lives in ACCUMULATION registers (AGPRs): every access goes through
-// v_accvgpr_read / v_accvgpr_write, so the register allocator gives these values the AGPR class and
-// the forward / backward working set keeps the architectural VGPRs (the two files share one 256-entry
-// budget per lane at two waves per SIMD; without this the allocator spills the state to scratch).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+}
+// moment slot s of this thread (sc1 loads: L2-served, never a stale L1 line of the previous step)
+__device__ __forceinline__ f4v mom_ld(__amdgpu_buffer_rsrc_t rs, int s, int tid) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (s * NTH + tid) * 16, 0, 16));
+}
+__device__ __forceinline__ void mom_st(__amdgpu_buffer_rsrc_t rs, int s, int tid, f4v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (s * NTH + tid) * 16, 0, 0);
+}
 __device__ __forceinline__ float ar(float a) {
   float r;
   asm("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(a));
@@ -292,18 +342,24 @@ __device__ __forceinline__ float aw(float v) {
   asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
   return r;
 }
-__device__ __forceinline__ float adam1(float& pa, float& ma, float& va, float g, const AdamK& k) {
+// Step constants.  Adam (torch.optim.Adam defaults): keep = 1, c1 = 1 - beta1, lr_bc1 = lr / (1 - beta1^t),
+// rsqrt_bc2 = 1 / sqrt(1 - beta2^t), eps = 1e-8.  SGD test mode (raw gradients for the tests): keep = 0,
+// c1 = 1, lr_bc1 = lr, rsqrt_bc2 = 0, eps = 1, so the same branch-free formula gives m = g, p -= lr g.
+struct AdamK {
+  float lr_bc1, rsqrt_bc2, keep, c1, eps;
+};
+__device__ __forceinline__ AdamK adam_k(float lr, int opt_mode, double b1t, double b2t) {
+  if (opt_mode == 1) return AdamK{lr, 0.f, 0.f, 1.f, 1.f};
+  return AdamK{(float)((double)lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), 1.f, 1.f - fk::B1, fk::EPS};
+}
+// one Adam step of an AGPR-resident weight with its moments m, v (VGPRs, updated in place); v_sqrt_f32
+// (1 ulp) instead of the correctly rounded sqrt expansion: 4x fewer instructions on the update's chain
+__device__ __forceinline__ float adam1(float& pa, float& m, float& v, float g, const AdamK& k) {
   float p = ar(pa);
-  if (k.sgd_lr > 0.f) {
-    p -= k.sgd_lr * g;
-  } else {
-    float m = ar(ma), v = ar(va);
-    m = m + (1.f - fk::B1) * (g - m);
-    v = fk::B2 * v + (1.f - fk::B2) * g * g;
-    p -= k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_sqrtf(v) * k.rsqrt_bc2 + fk::EPS);
-    ma = aw(m);
-    va = aw(v);
-  }
+  const float mk = m * k.keep;
+  m = mk + k.c1 * (g - mk);
+  v = fk::B2 * v + (1.f - fk::B2) * g * g;
+  p -= k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) * k.rsqrt_bc2 + k.eps);
   pa = aw(p);
   return p;
 }
@@ -320,8 +376,6 @@ __device__ __forceinline__ void tile_load(TS& s, const Mat& M, int T, int Tn, in
     const bool ok = n < M.n_real && k0 + i < M.k_real;
     h[i] = ok ? P[M.off + n * M.k_real + k0 + i] : 0.f;
     s.p[i] = aw(h[i]);
-    s.m[i] = aw(0.f);
-    s.v[i] = aw(0.f);
   }
   if (n < 16 * ((M.n_real + 15) / 16))
     *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
@@ -332,24 +386,24 @@ __device__ __forceinline__ void tile_store(const TS& s, const Mat& M, int T, int
   for (int i = 0; i < 4; ++i)
     if (n < M.n_real && k0 + i < M.k_real) P[M.off + n * M.k_real + k0 + i] = ar(s.p[i]);
 }
-// Adam on the tile's real elements with gradient acc (= dW^T tile), new bf16 values -> image
-__device__ __forceinline__ void tile_adam(TS& s, const Mat& M, int T, int Tn, int lane, f4v acc, const AdamK& K,
-                                          uchar* smem) {
+// Adam on the tile's real elements with gradient acc (= dW^T tile) and moments m, v, new bf16 values -> image
+__device__ __forceinline__ void tile_adam(TS& s, f4v& m, f4v& v, const Mat& M, int T, int Tn, int lane, f4v acc,
+                                          const AdamK& K, uchar* smem) {
   const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
   float h[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const bool ok = n < M.n_real && k0 + i < M.k_real;
-    h[i] = ok ? adam1(s.p[i], s.m[i], s.v[i], acc[i], K) : 0.f;
+    float mi = m[i], vi = v[i];
+    h[i] = ok ? adam1(s.p[i], mi, vi, acc[i], K) : 0.f;
+    m[i] = mi;
+    v[i] = vi;
   }
   if (n < 16 * ((M.n_real + 15) / 16))
     *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
 }
 
 // -------------------------------------------------------------------------- cross-workgroup hand-off
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-}
 __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t rs, int off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1: write-through
 }
@@ -446,6 +500,11 @@ struct BrK {
   static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LD64};
   static constexpr Mat MF1{o.ff0_w, FF, 64, B_IMG_F1, LD64};
   static constexpr Mat MF2{o.ff3_w, 64, FF, B_IMG_F2, LD32};
+  // the v (lo) or out_proj block matrix, built from constants (a `lo ? MV : MO` lvalue select would
+  // odr-use the static members and load them from memory, defeating the constant folding of n_real / k_real)
+  static __device__ __forceinline__ Mat vo(bool lo) {
+    return Mat{lo ? MV.off : MO.off, 64, 64, lo ? B_IMG_V : B_IMG_O, LD64};
+  }
   // VEC segment -> flat parameter offset
   static __device__ __forceinline__ int vec_param(int e) {
     if (e >= VS_F1B) return e - VS_F1B < FF ? o.ff0_b + (e - VS_F1B) : -1;
@@ -785,8 +844,11 @@ __device__ __forceinline__ int cmp_img(int e) {
 //  U2  small-tile gradients -> compact staging; the 2x2 v / out_proj block of the wave -> Adam -> image;
 //      bias sums of the dY tiles -> CS; barrier;
 //  U3  every thread: Adam on its compact entries -> VEC / images.  Gradient vector CS reset.
+// Moments (WS_MOM slab `rm`): the block tiles' are loaded at the start of U1 (used in U2), the compact
+// entries' at the start of U2 (used in U3); each set is stored back right after its Adam step.
 template <int BR>
-__device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid) {
+__device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid,
+                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp) {
   using B = BrK<BR>;
   opq(lane, wave);
   asm volatile("" : "+v"(tid));
@@ -794,6 +856,12 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
   const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
   const bool lo = wave < 4;
   // ---- U1
+  f4v bm[4], bv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bm[k] = mom_ld(rm, k, tid);
+    bv[k] = mom_ld(rm, 4 + k, tid);
+  }
   f4v as = Z4, af1 = Z4;
   {
     // waves 0-3: dense tile (k 0..15, n tile w4): X = xin, dY = dz0 ; waves 4-7: ffn.3 tile: X = f2, dY = d f3
@@ -812,7 +880,9 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
   // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
   const float lnsum = tid < B_NLN ? (float)((LDS_AS double*)(smem + B_DBL))[tid] : 0.f;
   lds_bar();
+  stp(5, tid);
   if (tid < B_NLN) ldsf(smem, B_CS)[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
+  const f4v cm = mom_ld(rm, 8, tid), cv = mom_ld(rm, 9, tid), cmv = mom_ld(rm, 10, tid);
   // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
   {
     LDS_AS float* gs = ldsf(smem, B_GS);
@@ -848,11 +918,17 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
         bs[1] = mma(ones8(), y1, bs[1]);
       }
     }
-    const Mat M = lo ? B::MV : B::MO;
+    const Mat M = B::vo(lo);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) tile_adam(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
+      for (int b = 0; b < 2; ++b)
+        tile_adam(st.blk[2 * a + b], bm[2 * a + b], bv[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mom_st(rm, k, tid, bm[k]);
+      mom_st(rm, 4 + k, tid, bv[k]);
+    }
     if (do_bias && g == 0) {
       LDS_AS float* cs = ldsf(smem, B_CS) + (lo ? VS_VB : VS_OB) * 64;
       cs[16 * Tb + i16] = bs[0][0];
@@ -886,8 +962,10 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
       for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] += af1[i];
   }
   lds_bar();
+  stp(6, tid);
   // ---- U3: compact entries (CS is zeroed as it is consumed; the DBL bytes past CS here)
   if (tid < (B_DBL_BYTES - B_NVEC * 4) / 4) ldsf(smem, B_CS)[B_NVEC + tid] = 0.f;
+  float mm[NCMP] = {cm[0], cm[1], cm[2], cm[3], cmv[0]}, vv[NCMP] = {cv[0], cv[1], cv[2], cv[3], cmv[1]};
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
@@ -897,14 +975,23 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
         LDS_AS float* cs = ldsf(smem, B_CS) + e;
         const float gsum = *cs;
         *cs = 0.f;
-        if (pi >= 0) ldsf(smem, B_VEC)[e] = adam1(st.cmp[h].p, st.cmp[h].m, st.cmp[h].v, gsum, K);
+        if (pi >= 0) ldsf(smem, B_VEC)[e] = adam1(st.cmp[h].p, mm[h], vv[h], gsum, K);
       } else {
         const float gr = ldsf(smem, B_GS)[e - B_NVEC];
-        const float pn = adam1(st.cmp[h].p, st.cmp[h].m, st.cmp[h].v, gr, K);
+        const float pn = adam1(st.cmp[h].p, mm[h], vv[h], gr, K);
         *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(pn);
       }
     }
   }
+  mom_st(rm, 8, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
+  mom_st(rm, 9, tid, f4v{vv[0], vv[1], vv[2], vv[3]});
+  mom_st(rm, 10, tid, f4v{mm[4], vv[4], 0.f, 0.f});
+}
+
+// fresh Adam state (torch.optim.Adam is re-created every round, client.py:78): zero moment slab
+__device__ __forceinline__ void mom_zero(__amdgpu_buffer_rsrc_t rm, int tid) {
+#pragma unroll
+  for (int k = 0; k < MOM_SLOTS; ++k) mom_st(rm, k, tid, Z4);
 }
 
 template <int BR>
@@ -912,7 +999,7 @@ __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P
   using B = BrK<BR>;
   using C = Cmp<BR>;
   const int w4 = wave & 3;
-  const Mat M = wave < 4 ? B::MV : B::MO;
+  const Mat M = B::vo(wave < 4);
   const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -932,7 +1019,7 @@ __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P
         *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(p0);
       }
     }
-    st.cmp[h] = VS{aw(p0), aw(0.f), aw(0.f)};
+    st.cmp[h] = VS{aw(p0)};
   }
 }
 
@@ -941,7 +1028,7 @@ __device__ __forceinline__ void br_fini(const BrState& st, float* P, int lane, i
   using B = BrK<BR>;
   using C = Cmp<BR>;
   const int w4 = wave & 3;
-  const Mat M = wave < 4 ? B::MV : B::MO;
+  const Mat M = B::vo(wave < 4);
   const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -972,8 +1059,24 @@ __device__ __forceinline__ void load_x(float (&x)[4], const AflTfTrainArgs& a, i
   }
 }
 
+__device__ __forceinline__ void stamp_init(Stamp& stp, const AflTfTrainArgs& a, uchar* smem) {
+#ifdef TF2_STAMPS
+  stp.on = a.stamps && (long)blockIdx.x == (long)a.stamps[63];
+  stp.smem = smem;
+  if (threadIdx.x == 0) *(LDS_AS uint64_t*)(smem + ST_OFF + 8 * (ST_N - 1)) = __builtin_amdgcn_s_memrealtime();
+#endif
+  (void)stp; (void)a; (void)smem;
+}
+__device__ __forceinline__ void stamp_fini(Stamp& stp, const AflTfTrainArgs& a, uchar* smem, int tid) {
+#ifdef TF2_STAMPS
+  if (stp.on && tid == 0)
+    for (int i = 0; i < ST_N - 1; ++i) a.stamps[i] = *(LDS_AS uint64_t*)(smem + ST_OFF + 8 * i);
+#endif
+  (void)stp; (void)a; (void)smem; (void)tid;
+}
+
 template <int BR>
-__device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
+__device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
@@ -982,8 +1085,12 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   BrState st;
+  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM + (BR + 1) * MOM_WG_BYTES);  // this workgroup's moments
+  mom_zero(rm, tid);
   br_init<BR>(smem, st, P, lane, wave, tid);
   __syncthreads();
+  Stamp stp;
+  stamp_init(stp, a, smem);
 
   const int nd = a.nd[cid], BS = a.batch, E = a.E;
   const uint32_t seed = a.seeds[cid];
@@ -999,7 +1106,7 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
     ++step;
     b1t *= (double)fk::B1;
     b2t *= (double)fk::B2;
-    const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+    const AdamK K = adam_k(a.lr, a.opt_mode, b1t, b2t);
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     Saved sv;
     u32x4 outp[2];
@@ -1010,6 +1117,7 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
     sv = Saved{}; outp[0] = u32x4{0,0,0,0}; outp[1] = outp[0];
 #endif
     asm volatile(";MARK fwd_end");
+    stp(0, tid);
     {  // publish this wave's output rows
       const int off = (int)WS_XF + BR * 16384 + (wave * 64 + lane) * 32;
       st_wt(rs, off, outp[0]);
@@ -1019,8 +1127,10 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+    stp(1, tid);
     gu32* fb = xf(sync, BR == 0 ? XF_BVIT : XF_BLAB, wave);
     const uint32_t fv = await(fb, fb, (uint32_t)step, 1, sync + XF_TMO, lane);
+    stp(2, tid);
     if (fv == 0xFFFFFFFFu) {
       failed = true;
       break;
@@ -1036,6 +1146,7 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
     asm volatile(";MARK bwd");
     br_backward<BR>(smem, dout, sv, lane, wave);
     asm volatile(";MARK bwd_end");
+    stp(3, tid);
 #else
     for (int j = 0; j < 16; ++j) asm volatile("" :: "v"(dout[j]));
 #endif
@@ -1047,14 +1158,18 @@ __device__ __noinline__ void branch_main(const AflTfTrainArgs& a, int cid, uchar
       failed = true;
       break;
     }
+    stp(4, tid);
 #ifndef TF2_NO_UPD
     asm volatile(";MARK upd");
-    br_update<BR>(smem, st, K, lane, wave, tid);
+    br_update<BR>(smem, st, K, lane, wave, tid, rm, stp);
     asm volatile(";MARK upd_end");
 #endif
+    stp(7, tid);
     lds_bar();
+    stp(8, tid);
   }
   (void)failed;
+  stamp_fini(stp, a, smem, tid);
   br_fini<BR>(st, P, lane, wave, tid);
 }
 
@@ -1070,7 +1185,7 @@ struct HdState {
   VS vec;
 };
 
-__device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
+__device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
   const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
@@ -1080,6 +1195,9 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   HdState st;
+  Stamp stp;
+  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM);  // this workgroup's Adam moments
+  mom_zero(rm, tid);
   {
     const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
 #pragma unroll
@@ -1093,9 +1211,10 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
       p0 = pi >= 0 ? P[pi] : 0.f;
       ldsf(smem, H_VEC)[tid] = p0;
     }
-    st.vec = VS{aw(p0), aw(0.f), aw(0.f)};
+    st.vec = VS{aw(p0)};
   }
   __syncthreads();
+  stamp_init(stp, a, smem);
 
   const int nd = a.nd[cid], BS = a.batch, E = a.E;
   const int nb_total = (nd + BS - 1) / BS;
@@ -1127,7 +1246,7 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
     ++step;
     b1t *= (double)fk::B1;
     b2t *= (double)fk::B2;
-    const AdamK K{(float)((double)a.lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), a.opt_mode == 1 ? a.lr : 0.f};
+    const AdamK K = adam_k(a.lr, a.opt_mode, b1t, b2t);
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
@@ -1137,6 +1256,7 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
       timed_out = failed = true;
       break;
     }
+    stp(10, tid);
     u32x4 cv[4];
     {
       const int off = (int)WS_XF + (wave * 64 + lane) * 32;
@@ -1278,6 +1398,17 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
         __hip_atomic_store(xf(sync, XF_BLAB, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    stp(11, tid);
+    // Adam moments of this step's update (after the hand-off drain, before the loss barrier)
+    f4v hm[6], hv[6];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hm[k] = mom_ld(rm, k, tid);
+      hv[k] = mom_ld(rm, 4 + k, tid);
+    }
+    hm[4] = mom_ld(rm, 8, tid);
+    hv[4] = mom_ld(rm, 9, tid);
+    hm[5] = mom_ld(rm, 10, tid);
     // the next step's labels (after the hand-off stores: their drain above must not wait for these)
     Walk wn = w;
     wn.b0 += BS;
@@ -1296,6 +1427,7 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
     }
     if (more) load_lab(wn);
     w = wn;
+    stp(12, tid);
     // ---- weight gradients + Adam
     {
       const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
@@ -1315,19 +1447,34 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
 #pragma unroll
       for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) tile_adam(st.blk[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
-      tile_adam(st.t2, HW2, T2, Tn2, lane, a2, K, smem);
+        for (int y = 0; y < 2; ++y)
+          tile_adam(st.blk[2 * x + y], hm[2 * x + y], hv[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
+      tile_adam(st.t2, hm[4], hv[4], HW2, T2, Tn2, lane, a2, K, smem);
       if (tid < H_NVEC) {
         // the 8 waves' partial sums in a fixed order: bit-reproducible whatever order the waves ran in
         const LDS_AS float* c = ldsf(smem, H_PART) + tid;
         float gsum = c[0];
 #pragma unroll
         for (int w8 = 1; w8 < 8; ++w8) gsum += c[w8 * H_NVEC];
-        if (hvec_param(tid) >= 0) ldsf(smem, H_VEC)[tid] = adam1(st.vec.p, st.vec.m, st.vec.v, gsum, K);
+        float vm = hm[5][0], vvv = hm[5][1];
+        if (hvec_param(tid) >= 0) ldsf(smem, H_VEC)[tid] = adam1(st.vec.p, vm, vvv, gsum, K);
+        hm[5][0] = vm;
+        hm[5][1] = vvv;
       }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mom_st(rm, k, tid, hm[k]);
+        mom_st(rm, 4 + k, tid, hv[k]);
+      }
+      mom_st(rm, 8, tid, hm[4]);
+      mom_st(rm, 9, tid, hv[4]);
+      mom_st(rm, 10, tid, hm[5]);
     }
+    stp(13, tid);
     lds_bar();
+    stp(14, tid);
   }
+  stamp_fini(stp, a, smem, tid);
   if (!failed) {
     while (cur_e < E) {  // the last epoch (and trailing epochs that had no step)
       if (tid == 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
@@ -1353,8 +1500,13 @@ __device__ __noinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* 
 
 }  // namespace t2
 
+#ifdef TF2_STAMPS
+#define K_TF2 k_tf2_train_stamped
+#else
+#define K_TF2 k_tf2_train
+#endif
 // 3 workgroups per client: 3c (head), 3c + 1 (vitals branch), 3c + 2 (labs branch)
-__global__ void __launch_bounds__(t2::NTH) k_tf2_train(AflTfTrainArgs a) {
+__global__ void __launch_bounds__(t2::NTH) K_TF2(AflTfTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int role = blockIdx.x % 3, cid = blockIdx.x / 3;
 #if defined(TF2_ROLE)
@@ -1372,16 +1524,21 @@ __global__ void __launch_bounds__(t2::NTH) k_tf2_train(AflTfTrainArgs a) {
 #endif
 }
 
+#ifdef TF2_STAMPS
+int afl_tf2_train_stamped(const AflTfTrainArgs* a, hipStream_t s) {
+#else
 long afl_tf2_ws_floats() { return t2::WS_BYTES / 4; }
 
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
+  if (a->stamps) return afl_tf2_train_stamped(a, s);
+#endif
   if (a->batch > 128 || a->batch < 2 || !a->sync) return -1;
-  if (hipFuncSetAttribute((const void*)k_tf2_train, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess)
+  if (hipFuncSetAttribute((const void*)K_TF2, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess)
     return -2;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -3;
   if (3 * a->C > cus) return -4;  // the workgroups of a client spin on each other: all must be resident
-  hipLaunchKernelGGL(k_tf2_train, dim3(3 * a->C), dim3(t2::NTH), t2::SMEM, s, *a);
+  hipLaunchKernelGGL(K_TF2, dim3(3 * a->C), dim3(t2::NTH), t2::SMEM, s, *a);
   return 0;
 }

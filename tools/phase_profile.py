@@ -23,6 +23,11 @@ NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G
          10: "B:E10 LN bwd", 11: "B:A10+G11", 12: "B:E11", 13: "B:G12+dW2", 14: "B:E12 LN1 bwd", 15: "B:G13+dW1",
          16: "B:E13", 17: "B:(none)", 18: "B:G14+dWo", 19: "B:E14+dWv", 20: "B:E15+dWd",
          21: "X:publish+wait d(out)"}
+# on-chip trainer (split 4, tf2.hip): branch workgroups (blocks 3c+1, 3c+2) and the head (3c)
+NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:backward", 4: "B:barrier+abort",
+          5: "B:U1 small dW (+bar)", 6: "B:U2 v/o dW+Adam, biases (+2 bars)", 7: "B:U3 compact Adam",
+          8: "B:end barrier", 10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss",
+          13: "H:dW+Adam", 14: "H:end barrier"}
 
 
 def main():
@@ -32,8 +37,9 @@ def main():
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--opt-mode", type=int, default=0, help="1 = SGD test mode (no Adam moments)")
     ap.add_argument("--split", type=int, default=0, help="workgroups per client (1, 2, 3); 0 = auto")
-    ap.add_argument("--block", type=int, default=0, help="workgroup whose phases are stamped")
+    ap.add_argument("--block", type=int, default=0, help="workgroup whose phases are stamped (-1: 0, 1, 2 in turn)")
     args = ap.parse_args()
+    blocks = [0, 1, 2] if args.block < 0 else [args.block]
     dev = torch.device("cuda", 0)
     ds = synthetic_icu(60000, seed=3)
     rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1).to(dev)
@@ -46,8 +52,15 @@ def main():
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
                     split=split)
     torch.cuda.synchronize()
+    used = split or T.auto_split(args.clients, dev)
+    for b in blocks:
+        run(args, dev, rows, order, plan, params, split, used, b)
+
+
+def run(args, dev, rows, order, plan, params, split, used, block):
+    names = NAMES4 if used == 4 else NAMES
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
-    stamps[63] = args.block
+    stamps[63] = block
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
                     opt_mode=args.opt_mode, stamps=stamps, split=split)
@@ -56,11 +69,11 @@ def main():
     steps = args.epochs * ((args.rows + 127) // 128)
     st = stamps.cpu().tolist()[:63]
     tot = sum(st)
-    out = {"split": args.split, "block": args.block, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
+    out = {"split": used, "block": block, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
            "us_per_step_stamped": tot * 0.01 / steps, "phases_us_per_step": {}}
     for i, v in enumerate(st):
         if v:
-            out["phases_us_per_step"][f"{i:02d} {NAMES.get(i, '?')}"] = round(v * 0.01 / steps, 3)
+            out["phases_us_per_step"][f"{i:02d} {names.get(i, '?')}"] = round(v * 0.01 / steps, 3)
     print(json.dumps(out, indent=1))
 
 
