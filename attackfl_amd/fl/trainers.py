@@ -36,6 +36,7 @@ class Plan:
     order: torch.Tensor
     nd: torch.Tensor
     epochs: int
+    nd_dev: Optional[torch.Tensor] = None  # nd on the order's device, when the plan was built there
 
     def client(self, c: int) -> torch.Tensor:
         return self.order[c, :, : int(self.nd[c])]
@@ -47,9 +48,14 @@ class Pending:
     Trainers whose work is enqueued asynchronously (fused, graph) return before the GPU finishes, so the
     engine can run the attackers' math on a side stream while the genuine clients train."""
 
-    def __init__(self, finish):
+    def __init__(self, finish, ok_dev: Optional[torch.Tensor] = None):
         self._finish = finish
         self._res = None
+        self._ok_dev = ok_dev
+
+    def ok_device(self) -> Optional[torch.Tensor]:
+        """Per-client success on the device (> 0 = ok) without a host round trip, when the trainer has it."""
+        return self._ok_dev
 
     def result(self) -> Tuple[List[bool], torch.Tensor]:
         if self._res is None:
@@ -118,10 +124,11 @@ def _plan_keys(seed: int, e: int):
     return ks0, ks1, ke0, ke1
 
 
-def _feistel_plan(n_train: int, num_data: List[int], epochs: int, seeds: List[int], device) -> Plan:
+def _feistel_plan(n_train: int, num_data: List[int], epochs: int, seeds: List[int], device, staged=None) -> Plan:
     """Per-client subset + per-epoch shuffle from keyed Feistel permutations (``csrc/kernels/plan.hip``):
     one launch on GPU, a bit-identical vectorised mirror on CPU.  A client's plan depends only on its
-    seed and num_data (placement-independent)."""
+    seed and num_data (placement-independent).  ``staged``: (seeds int64, num_data int32) already on the
+    device (the engine uploads them with the rest of the round's metadata)."""
     dev = torch.device(device)
     C = len(num_data)
     maxnd = max(num_data)
@@ -130,9 +137,13 @@ def _feistel_plan(n_train: int, num_data: List[int], epochs: int, seeds: List[in
     if dev.type == "cuda":
         from .. import ops
 
-        st = torch.tensor([s - (1 << 64) if s >= (1 << 63) else s for s in seeds], dtype=torch.int64)
-        order = ops.native().make_plan(st.to(dev), nd.to(dev), int(n_train), int(epochs), int(maxnd))
-        return Plan(order, nd, epochs)
+        if staged is not None:
+            st_d, nd_d = staged
+        else:
+            st_d = torch.tensor([s - (1 << 64) if s >= (1 << 63) else s for s in seeds], dtype=torch.int64).to(dev)
+            nd_d = nd.to(dev)
+        order = ops.native().make_plan(st_d, nd_d, int(n_train), int(epochs), int(maxnd))
+        return Plan(order, nd, epochs, nd_d)
     order = torch.zeros(C, epochs, maxnd, dtype=torch.int64)
     for c in range(C):
         n = num_data[c]
@@ -143,7 +154,7 @@ def _feistel_plan(n_train: int, num_data: List[int], epochs: int, seeds: List[in
     return Plan(order.to(torch.int32).to(dev), nd, epochs)
 
 
-def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, device) -> Plan:
+def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, device, staged=None) -> Plan:
     """Random subset (without replacement) per client + a fresh permutation per epoch.
 
     ``generator`` is one ``torch.Generator`` shared by all rows, or a list of per-client integer seeds
@@ -157,7 +168,7 @@ def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, dev
     if maxnd > n_train:
         raise ValueError(f"num_data {maxnd} exceeds the train set size {n_train}")
     if isinstance(generator, (list, tuple)):
-        return _feistel_plan(n_train, list(num_data), epochs, [int(s) for s in generator], device)
+        return _feistel_plan(n_train, list(num_data), epochs, [int(s) for s in generator], device, staged)
     gdev = generator.device if hasattr(generator, "device") else torch.device("cpu")
     keys = torch.rand(C, n_train, generator=generator, device=gdev)
     ek = None
@@ -217,7 +228,7 @@ class EagerTrainer:
             oks.append(ok)
         return oks, losses
 
-    def launch(self, params, plan, lr, batch, seeds) -> Pending:
+    def launch(self, params, plan, lr, batch, seeds, seeds_dev=None) -> Pending:
         res = self.train(params, plan, lr, batch, seeds)
         return Pending(lambda: res)
 
@@ -262,6 +273,10 @@ class EagerTrainer:
         return True
 
 
+def _nd(plan: Plan):
+    return plan.nd_dev if plan.nd_dev is not None else plan.nd
+
+
 class FusedTrainer:
     """All local clients' local rounds in one persistent HIP launch: TransformerModel/ICU
     (``ops/transformer.py``) and RNNModel/ICU (``ops/rnn.py``, falls back to the graph trainer when
@@ -290,25 +305,31 @@ class FusedTrainer:
               ) -> Tuple[List[bool], torch.Tensor]:
         return self.launch(params, plan, lr, batch, seeds).result()
 
-    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]) -> Pending:
+    def device_seed(self, s: int) -> int:
+        """The kernel's int32 form of client seed ``s`` (the engine stages these on the device)."""
+        return (self.R if self.model_name == "RNNModel" else self.T).device_seed(s)
+
+    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int],
+               seeds_dev: Optional[torch.Tensor] = None) -> Pending:
+        """``seeds_dev``: the same seeds already on the device in ``device_seed`` form (optional)."""
         if self.model_name == "RNNModel":
             if not self.R.fits(params.shape[0], self.device):
                 if self._fallback is None:
                     self._fallback = GraphTrainer(self.model_name, "ICU", self.table, self.device, self.verbose)
                 return self._fallback.launch(params, plan, lr, batch, seeds)
-            ok, losses = self.R.train_clients_async(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch,
-                                                    lr, seeds)
+            ok, losses = self.R.train_clients_async(params, self.table.rows, plan.order, _nd(plan), plan.epochs, batch,
+                                                    lr, seeds if seeds_dev is None else seeds_dev)
             what = "fused RNN trainer"
         else:
-            ok, losses = self.T.train_clients_async(params, self.table.rows, plan.order, plan.nd, plan.epochs, batch,
-                                                    lr, seeds)
+            ok, losses = self.T.train_clients_async(params, self.table.rows, plan.order, _nd(plan), plan.epochs, batch,
+                                                    lr, seeds if seeds_dev is None else seeds_dev)
             what = "fused trainer"
 
         def fin():
             okh, lh = self.T.finish(ok, losses, what)
             return [bool(x) for x in okh.tolist()], lh
 
-        return Pending(fin)
+        return Pending(fin, ok)
 
 
 class GraphTrainer:
@@ -335,7 +356,8 @@ class GraphTrainer:
               ) -> Tuple[List[bool], torch.Tensor]:
         return self.launch(params, plan, lr, batch, seeds).result()
 
-    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]) -> Pending:
+    def launch(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int],
+               seeds_dev=None) -> Pending:
         C = params.shape[0]
         if self._runner is None or self._runner.prog.C != C or self._runner.prog.B != batch:
             self._runner = self.programs.ProgramRunner(
@@ -350,7 +372,7 @@ class GraphTrainer:
                         print_with_color(f"Loss {float(lh[c, e]):.6f} ", "yellow")
             return [bool(x) for x in okh.tolist()], lh
 
-        return Pending(fin)
+        return Pending(fin, (ok == 0).to(torch.int32))
 
 
 def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable, device, verbose=False):

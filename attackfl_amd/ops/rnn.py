@@ -26,12 +26,30 @@ def _seeds(seeds, dev) -> torch.Tensor:
     return torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32).to(dev)
 
 
+def device_seed(s: int) -> int:
+    """The int32 the kernel receives for client seed ``s`` (low 32 bits, two's complement)."""
+    s = int(s) & M32
+    return s - 2 ** 32 if s >= 2 ** 31 else s
+
+
+def _on(t, dev) -> bool:
+    return torch.is_tensor(t) and t.device == dev and t.dtype == torch.int32
+
+
+def _dev_i32(nd, dev) -> torch.Tensor:
+    """``nd`` as a device int32 tensor (passed through when the engine already staged it there)."""
+    if _on(nd, dev):
+        return nd
+    return torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
+
+
 def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                         lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """Enqueue the launch; returns DEVICE (ok [C] int32, losses [C, E]) without synchronising."""
     dev = params.device
-    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
-    return native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, _seeds(seeds, dev),
+    nd_t = _dev_i32(nd, dev)
+    seeds_t = seeds if _on(seeds, dev) else _seeds(seeds, dev)
+    return native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t,
                               int(epochs), int(batch), float(lr), int(opt_mode))
 
 

@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from . import native
+from .rnn import _dev_i32, _on
 
 NPARAM = 47693
 M32 = 0xFFFFFFFF
@@ -29,6 +30,12 @@ def auto_split(C: int, dev) -> int:
     return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
+def device_seed(s: int) -> int:
+    """The int32 the kernel receives for client seed ``s`` (a device int32 tensor of these values may be
+    passed as ``seeds`` directly)."""
+    return int(s) & 0x7FFFFFFF
+
+
 def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                         lr: float, seeds: Sequence[int], opt_mode: int = 0, stamps: torch.Tensor = None,
                         split: int = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -38,8 +45,8 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     C = params.shape[0]
     if split is None:
         split = auto_split(C, dev) if C > 0 else 1
-    nd_t = torch.as_tensor(list(nd) if not torch.is_tensor(nd) else nd.tolist(), dtype=torch.int32, device=dev)
-    seeds_t = torch.tensor([int(s) & 0x7FFFFFFF for s in seeds], dtype=torch.int32, device=dev)
+    nd_t = _dev_i32(nd, dev)
+    seeds_t = seeds if _on(seeds, dev) else torch.tensor([device_seed(s) for s in seeds], dtype=torch.int32, device=dev)
     return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
                              int(batch), float(lr), int(opt_mode), stamps, int(split))
 

@@ -108,7 +108,7 @@ def main() -> int:
         elapsed = float(t.item())
     if args.profile_rounds and rank == 0:
         for r in recs:
-            print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_local",
+            print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_prep", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_lw_post", "t_local",
                                                 "t_gather", "t_aggregate", "t_validate", "t_round", "metric")
                               if k in r}), file=sys.stderr)
     value = args.steps / elapsed
