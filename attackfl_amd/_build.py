@@ -13,6 +13,7 @@ import concurrent.futures as cf
 import glob
 import hashlib
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -38,7 +39,14 @@ def _torch_paths():
 def _hash(path: str, flags) -> str:
     h = hashlib.sha1()
     with open(path, "rb") as fh:
-        h.update(fh.read())
+        src = fh.read()
+    h.update(src)
+    # sources included by path (e.g. tf2_stamps.hip includes tf2.hip) participate too
+    for inc in re.findall(rb'#include\s+"([^"]+\.(?:hip|cpp|inc))"', src):
+        p = os.path.join(os.path.dirname(path), inc.decode())
+        if os.path.exists(p):
+            with open(p, "rb") as fh:
+                h.update(fh.read())
     # headers under csrc/ participate in every hash (cheap, conservative)
     for hdr in sorted(glob.glob(os.path.join(ROOT, "csrc", "**", "*.h"), recursive=True)):
         with open(hdr, "rb") as fh:

@@ -47,8 +47,28 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
         split = auto_split(C, dev) if C > 0 else 1
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else torch.tensor([device_seed(s) for s in seeds], dtype=torch.int32, device=dev)
+    kt = None
+    if split == 4:
+        kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
-                             int(batch), float(lr), int(opt_mode), stamps, int(split))
+                             int(batch), float(lr), int(opt_mode), stamps, int(split), kt)
+
+
+_KT_CACHE: Dict[tuple, torch.Tensor] = {}
+
+
+def adam_step_table(lr: float, steps: int, dev) -> torch.Tensor:
+    """[n >= steps, 2] fp32 device table of torch.optim.Adam's per-step scalars, computed in double like
+    torch does on the host: (lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)) for t = 1..n.  Cached per (lr,
+    device) and grown in powers of two, so a round never uploads it again."""
+    key = (lr, str(dev))
+    t = _KT_CACHE.get(key)
+    if t is None or t.shape[0] < steps:
+        n = 1 << max(10, (max(steps, 1) - 1).bit_length())
+        tt = np.arange(1, n + 1, dtype=np.float64)
+        tab = np.stack([lr / (1.0 - 0.9 ** tt), 1.0 / np.sqrt(1.0 - 0.999 ** tt)], axis=1).astype(np.float32)
+        t = _KT_CACHE[key] = torch.from_numpy(tab).to(dev)
+    return t
 
 
 def finish(ok: torch.Tensor, losses: torch.Tensor, what: str = "fused trainer") -> Tuple[torch.Tensor, torch.Tensor]:

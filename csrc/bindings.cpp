@@ -339,7 +339,8 @@ torch::Tensor make_plan(torch::Tensor seeds, torch::Tensor nd, int64_t n_train, 
 // kind 1 = RNNModel (always 3 workgroups per client).
 std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Tensor rows, torch::Tensor order,
                                        torch::Tensor nd, torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
-                                       int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
+                                       int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split,
+                                       c10::optional<torch::Tensor> kt = c10::nullopt) {
   check_dev(params, "params", torch::kFloat32);
   check_dev(rows, "rows", torch::kFloat32);
   check_dev(order, "order", torch::kInt32);
@@ -381,6 +382,14 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
     a.stamps = (uint64_t*)stamps->data_ptr<int64_t>();
   }
   a.sync = nullptr;
+  a.kt = nullptr;
+  a.kt_n = 0;
+  if (kt.has_value() && kt->defined()) {
+    check_dev(*kt, "kt", torch::kFloat32);
+    TORCH_CHECK(kt->dim() == 2 && kt->size(1) == 2, "kt must be [steps, 2]");
+    a.kt = kt->data_ptr<float>();
+    a.kt_n = (int)kt->size(0);
+  }
   a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);
   torch::Tensor sync;
   if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
@@ -389,6 +398,7 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   }
   const int rc = tf2 ? afl_tf2_train(&a, cur()) : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
   TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
+  TORCH_CHECK(rc != -5, "on-chip trainer: Adam step table (kt) missing or shorter than the round");
   TORCH_CHECK(rc == 0, "fused trainer launch failed (", rc, ")");
   AFL_CHECK_LAUNCH();
   return {ok, losses};
@@ -396,8 +406,9 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
 
 std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr,
-                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split) {
-  return fused_train(0, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split);
+                                    int64_t opt_mode, c10::optional<torch::Tensor> stamps, int64_t split,
+                                    c10::optional<torch::Tensor> kt) {
+  return fused_train(0, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split, kt);
 }
 
 std::vector<torch::Tensor> rnn_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
@@ -444,7 +455,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hyper_small_capacity", &afl_hyper_small_capacity);
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
-        py::arg("stamps") = py::none(), py::arg("split") = 1);
+        py::arg("stamps") = py::none(), py::arg("split") = 1, py::arg("kt") = py::none());
   m.def("rnn_train", &rnn_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0);
   m.def("rnn_param_count", &afl_rnn_param_count);

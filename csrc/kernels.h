@@ -72,6 +72,9 @@ struct AflTfTrainArgs {
   uint64_t* stamps;  // optional per-phase timers (AFL_TF_STAMPS builds), may be null
   uint32_t* sync;    // zeroed hand-off words (branch-parallel launches): [C][AFL_TF_SYNC_WORDS]
   int split;         // workgroups per client: 1, 2 (vitals+head | labs), 3 (head | vitals | labs)
+  // tf2 only: per-step Adam constants [kt_n][2] = (lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)), t = 1..kt_n
+  const float* kt;
+  int kt_n;
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);

@@ -348,9 +348,12 @@ __device__ __forceinline__ float aw(float v) {
 struct AdamK {
   float lr_bc1, rsqrt_bc2, keep, c1, eps;
 };
-__device__ __forceinline__ AdamK adam_k(float lr, int opt_mode, double b1t, double b2t) {
-  if (opt_mode == 1) return AdamK{lr, 0.f, 0.f, 1.f, 1.f};
-  return AdamK{(float)((double)lr / (1.0 - b1t)), (float)(1.0 / sqrt(1.0 - b2t)), 1.f, 1.f - fk::B1, fk::EPS};
+// lr_bc1 / rsqrt_bc2 of step t come from the host-computed table a.kt (torch computes them in double on
+// the host as well); a scalar load per step instead of double-precision division / sqrt on every wave
+__device__ __forceinline__ AdamK adam_k(const AflTfTrainArgs& a, int step) {
+  if (a.opt_mode == 1) return AdamK{a.lr, 0.f, 0.f, 1.f, 1.f};
+  const float* k = a.kt + 2 * (step - 1);
+  return AdamK{k[0], k[1], 1.f, 1.f - fk::B1, fk::EPS};
 }
 // one Adam step of an AGPR-resident weight with its moments m, v (VGPRs, updated in place); v_sqrt_f32
 // (1 ulp) instead of the correctly rounded sqrt expansion: 4x fewer instructions on the update's chain
@@ -1095,7 +1098,6 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   const int nd = a.nd[cid], BS = a.batch, E = a.E;
   const uint32_t seed = a.seeds[cid];
   LDS_AS uint32_t* abort_w = ldsu(smem, B_MISC);
-  double b1t = 1.0, b2t = 1.0;
   int step = 0;
   bool failed = false;
   Walk w{0, 0};
@@ -1104,9 +1106,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
   while (more) {
     ++step;
-    b1t *= (double)fk::B1;
-    b2t *= (double)fk::B2;
-    const AdamK K = adam_k(a.lr, a.opt_mode, b1t, b2t);
+    const AdamK K = adam_k(a, step);
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     Saved sv;
     u32x4 outp[2];
@@ -1222,7 +1222,6 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   const uchar* vec = smem + H_VEC;
   LDS_AS float* part = ldsf(smem, H_PART) + wave * H_NVEC;  // this wave's column sums
   LDS_AS float* lossw = ldsf(smem, H_LOSS);
-  double b1t = 1.0, b2t = 1.0;
   int step = 0;
   bool failed = false, timed_out = false;
   float epoch_loss = 0.f;
@@ -1244,9 +1243,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       ++cur_e;
     }
     ++step;
-    b1t *= (double)fk::B1;
-    b2t *= (double)fk::B2;
-    const AdamK K = adam_k(a.lr, a.opt_mode, b1t, b2t);
+    const AdamK K = adam_k(a, step);
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
@@ -1533,6 +1530,7 @@ int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
   if (a->stamps) return afl_tf2_train_stamped(a, s);
 #endif
   if (a->batch > 128 || a->batch < 2 || !a->sync) return -1;
+  if (!a->kt || a->kt_n < a->E * ((a->maxnd + a->batch - 1) / a->batch)) return -5;  // step table too short
   if (hipFuncSetAttribute((const void*)K_TF2, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess)
     return -2;
   int dev = 0, cus = 0;
