@@ -563,8 +563,34 @@ struct Cmp {
 constexpr int B_GS = B_XIN;
 static_assert(B_GS + (Cmp<1>::N - B_NVEC) * 4 <= B_VEC, "compact gradient staging fits");
 
+// Every dropout keep-bit of a branch wave's forward for one step, packed into two words:
+//   mk0 = m1 (out_proj dropout, 16 bits) | m2 (ffn.3 dropout) << 16;
+//   mk1 = matt (attention dropout per head, 4 bits) | kf (ffn.0 dropout of features 4g + i) << 4.
+// The branch computes the NEXT step's masks while it waits for the head (the wave is idle there) and
+// parks them in two AGPRs, so the ~20 hashes per lane leave the forward's critical path.
 template <int BR>
-__device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], uint32_t key, Saved& sv,
+__device__ __forceinline__ void br_masks(uint32_t key, int r, int g, uint32_t& mk0, uint32_t& mk1) {
+  const uint32_t ha = hash3(key, 8 * BR + L_ATT, r, 0), hb = hash3(key, 8 * BR + L_ATT, r, 1);
+  const uint32_t matt = ((ha & 0xFFFFu) >= THR_P01 ? 1u : 0u) | ((ha >> 16) >= THR_P01 ? 2u : 0u) |
+                        ((hb & 0xFFFFu) >= THR_P01 ? 4u : 0u) | ((hb >> 16) >= THR_P01 ? 8u : 0u);
+  const uint32_t m1 = mask16(key, 8 * BR + L_D1, r, g, THR_P01), m2 = mask16(key, 8 * BR + L_D2, r, g, THR_P01);
+  uint32_t kf = 0u;
+  if (g < 2) {
+    const uint32_t hd[2] = {hash3(key, 8 * BR + L_DF, r, 2 * g), hash3(key, 8 * BR + L_DF, r, 2 * g + 1)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = (hd[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu;
+      kf |= (4 * g + i < FF && u >= THR_P01 ? 1u : 0u) << i;
+    }
+  }
+  mk0 = m1 | (m2 << 16);
+  mk1 = matt | (kf << 4);
+}
+__device__ __forceinline__ uint32_t aru(float a) { return __float_as_uint(ar(a)); }
+__device__ __forceinline__ float awu(uint32_t v) { return aw(__uint_as_float(v)); }
+
+template <int BR>
+__device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], uint32_t mk0, uint32_t mk1, Saved& sv,
                                            u32x4 (&outp)[2], int lane, int wave) {
   using B = BrK<BR>;
   opq(lane, wave);
@@ -600,9 +626,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
       acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 0, lane), b0, Z4);
       acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 1, lane), b1, acc[T]);
     }
-    const uint32_t ha = hash3(key, 8 * BR + L_ATT, r, 0), hb = hash3(key, 8 * BR + L_ATT, r, 1);
-    sv.matt = ((ha & 0xFFFFu) >= THR_P01 ? 1u : 0u) | ((ha >> 16) >= THR_P01 ? 2u : 0u) |
-              ((hb & 0xFFFFu) >= THR_P01 ? 4u : 0u) | ((hb >> 16) >= THR_P01 ? 8u : 0u);
+    sv.matt = mk1 & 0xFu;
     float bv[16];
     vec16(bv, vec + VS_VB * 256, g);
 #pragma unroll
@@ -625,7 +649,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
       acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
       acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 1, lane), b1, acc[T]);
     }
-    sv.m1 = mask16(key, 8 * BR + L_D1, r, g, THR_P01);
+    sv.m1 = mk0 & 0xFFFFu;
     float bo[16];
     vec16(bo, vec + VS_OB * 256, g);
     float x1[16];
@@ -652,19 +676,12 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   {
     f4v acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 0, lane), bfrag(x1n, 0), Z4);
     acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 1, lane), bfrag(x1n, 1), acc);
-    uint32_t hd[2] = {0u, 0u};
-    if (g < 2) {
-      hd[0] = hash3(key, 8 * BR + L_DF, r, 2 * g);
-      hd[1] = hash3(key, 8 * BR + L_DF, r, 2 * g + 1);
-    }
     const f4v bf = g < 2 ? *(const LDS_AS f4v*)(vec + (VS_F1B + 4 * g) * 4) : Z4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = 4 * g + i;
       float gp;
       const float gl = gelu_and_grad(acc[i] + bf[i], gp);
-      const uint32_t u = (hd[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu;
-      const bool kp = f < FF && u >= THR_P01;
+      const bool kp = (mk1 >> (4 + i)) & 1u;
       f2v[i] = kp ? gl * INV_K01 : 0.f;
       sv.gk[i] = kp ? gp * INV_K01 : 0.f;
     }
@@ -677,7 +694,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     f4v acc[4];
 #pragma unroll
     for (int T = 0; T < 4; ++T) acc[T] = mma(wfrag(smem + B_IMG_F2, LD32, T, 0, lane), bf, Z4);
-    sv.m2 = mask16(key, 8 * BR + L_D2, r, g, THR_P01);
+    sv.m2 = mk0 >> 16;
     float b3[16];
     vec16(b3, vec + VS_F2B * 256, g);
     float x2[16];
@@ -1104,15 +1121,21 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   float xin[4];
   bool more = walk_valid(w, nd, BS, E);
   if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+  float mka0, mka1;  // the next forward's dropout masks (br_masks), parked in AGPRs
+  {
+    uint32_t m0, m1;
+    br_masks<BR>(afl_hash32(seed, 1u), 16 * wave + (lane & 15), g, m0, m1);
+    mka0 = awu(m0);
+    mka1 = awu(m1);
+  }
   while (more) {
     ++step;
     const AdamK K = adam_k(a, step);
-    const uint32_t key = afl_hash32(seed, (uint32_t)step);
     Saved sv;
     u32x4 outp[2];
     asm volatile(";MARK fwd");
 #ifndef TF2_NO_FWD
-    br_forward<BR>(smem, xin, key, sv, outp, lane, wave);
+    br_forward<BR>(smem, xin, aru(mka0), aru(mka1), sv, outp, lane, wave);
 #else
     sv = Saved{}; outp[0] = u32x4{0,0,0,0}; outp[1] = outp[0];
 #endif
@@ -1127,6 +1150,12 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+    {  // the next step's dropout masks, while the head works (this wave would only spin)
+      uint32_t m0, m1;
+      br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), 16 * wave + (lane & 15), g, m0, m1);
+      mka0 = awu(m0);
+      mka1 = awu(m1);
+    }
     stp(1, tid);
     gu32* fb = xf(sync, BR == 0 ? XF_BVIT : XF_BLAB, wave);
     const uint32_t fv = await(fb, fb, (uint32_t)step, 1, sync + XF_TMO, lane);
@@ -1247,6 +1276,9 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
+    // fc1 dropout mask before the wait (the wave would only spin there)
+    const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
+    sb();
     // ---- branch outputs of this wave's rows
     const uint32_t fv = await(xf(sync, XF_VIT, wave), xf(sync, XF_LAB, wave), (uint32_t)step, 0, sync + XF_TMO, lane);
     if (fv == 0xFFFFFFFFu) {
@@ -1280,7 +1312,6 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         for (int s = 0; s < 4; ++s)
           acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
       }
-      const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
       float b1[16];
       vec16(b1, vec + HV_B1 * 4, g);
 #pragma unroll
