@@ -83,11 +83,11 @@ class Validation:
         return self.table.rows[:, -1] if self.data_name == "ICU" else self.table.y
 
     def _finish_icu(self, outputs: torch.Tensor, labels: torch.Tensor) -> Tuple[bool, float]:
-        if bool(torch.isnan(outputs).any()):
+        auc, has_nan = ops.roc_auc_checked(outputs, labels)
+        if has_nan:
             print_with_color("NaN detected in output, training false", "yellow")
             self.last_metric = float("nan")
             return False, float("nan")
-        auc = ops.roc_auc(outputs, labels)
         if self.verbose:
             print(f"ROC_AUC: {auc:.4f}")
         self.logger.log_info(f"ROC_AUC: {auc:.4f}")
@@ -144,7 +144,10 @@ class Validation:
             return self._finish_icu(out, self._labels().repeat(num_client))
         if self.device.type == "cuda" and num_client > 0:
             flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32)  # one GEMM
-            out = torch.cat([self._outputs(flats[i]).reshape(-1) for i in range(num_client)])
+            if self.model_name == "TransformerModel":
+                out = ops.native().tf_eval_many(flats.contiguous(), self.table.rows).reshape(-1)
+            else:
+                out = torch.cat([self._outputs(flats[i]).reshape(-1) for i in range(num_client)])
             return self._finish_icu(out, self._labels().repeat(num_client))
         outs, labs = [], []
         for i in range(num_client):

@@ -243,6 +243,16 @@ def roc_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
     return composite.roc_auc(scores, labels)
 
 
+def roc_auc_checked(scores: torch.Tensor, labels: torch.Tensor):
+    """(ROC-AUC, any NaN score) with ONE host synchronisation on the device path."""
+    if _dev(scores):
+        r = native().roc_auc_dev(scores.reshape(-1).float().contiguous(), labels.reshape(-1).float().contiguous())
+        auc, nan = r.cpu().tolist()
+        return auc, nan > 0.5
+    nan = bool(torch.isnan(scores).any())
+    return (float("nan") if nan else composite.roc_auc(scores, labels)), nan
+
+
 def adam_step_scaled(p, g, m, v, step: int, lr: float, scale: float, beta1=0.9, beta2=0.999, eps=1e-8) -> None:
     if _dev(p):
         native().adam_flat(p, g, m, v, int(step), float(lr), float(beta1), float(beta2), float(eps), float(scale))

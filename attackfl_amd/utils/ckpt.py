@@ -2,20 +2,22 @@
 
 The reference saves the model synchronously at the end of every successful round
 (``server.py:551-553`` ``torch.save(...)``).  Serialising a hypernetwork of tens of MB costs tens of
-milliseconds of CPU per round, which at GPU round rates is a large share of the round.  Here the leader
-copies the tensors device→pinned host on the current stream (an async DMA, ordered after the kernels
-that produced them), and one background thread waits for the copy and writes the file atomically
-(``.tmp`` + ``os.replace``), so a reader never sees a half-written checkpoint.
+milliseconds of CPU per round, which at GPU round rates is longer than a round.  Here the leader copies
+the tensors device -> pinned host on the current stream (an async DMA, ordered after the kernels that
+produced them), and one background thread waits for the copy and writes the file atomically (``.tmp`` +
+``os.replace``), so a reader never sees a half-written checkpoint.
 
-One write is in flight at a time: ``submit`` first waits for the previous write (its pinned buffer is
-reused), ``flush`` waits for the last one (called before the file is read and at shutdown).
+Latest-wins coalescing: two pinned staging slots per key; a ``submit`` that arrives while a write is in
+flight replaces any write that has not started yet (only the newest state matters), so a round never
+waits for the disk.  The file therefore always holds a complete checkpoint of a finished round, at most
+one write behind while rounds outpace the disk, and ``flush`` (called before the file is read and at
+shutdown) writes the newest one.
 """
 from __future__ import annotations
 
 import os
 import threading
-from concurrent.futures import Future, ThreadPoolExecutor
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 
@@ -23,49 +25,87 @@ import torch
 class CheckpointWriter:
     def __init__(self, asynchronous: bool = True):
         self.asynchronous = asynchronous
-        self._pool: Optional[ThreadPoolExecutor] = None
-        self._pending: Optional[Future] = None
-        self._bufs: Dict[str, torch.Tensor] = {}
-        self._lock = threading.Lock()
+        self._bufs: Dict[Tuple[str, int], torch.Tensor] = {}
+        self._cv = threading.Condition()
+        self._pending = None          # (key, slot, build, path, event) not yet started
+        self._writing: Optional[Tuple[str, int]] = None
+        self._err: Optional[BaseException] = None
+        self._thread: Optional[threading.Thread] = None
+        self._stop = False
+        self.dropped = 0               # superseded writes (diagnostics)
 
-    def _host(self, key: str, src: torch.Tensor) -> torch.Tensor:
+    def _host(self, key: str, slot: int, src: torch.Tensor) -> torch.Tensor:
         """Pinned host staging buffer for ``src`` (reused across rounds)."""
-        buf = self._bufs.get(key)
+        buf = self._bufs.get((key, slot))
         if buf is None or buf.shape != src.shape or buf.dtype != src.dtype:
             buf = torch.empty(src.shape, dtype=src.dtype, pin_memory=src.is_cuda)
-            self._bufs[key] = buf
+            self._bufs[(key, slot)] = buf
         return buf
 
     def submit(self, key: str, src: torch.Tensor, build: Callable[[torch.Tensor], object], path: str) -> None:
         """Save ``build(host copy of src)`` to ``path``.  ``src`` may be overwritten right after return."""
-        self.flush()
         src = src.detach()
         if not src.is_cuda or not self.asynchronous:
+            self.flush()
             _atomic_save(build(src.cpu() if src.is_cuda else src.clone()), path)
             return
-        host = self._host(key, src)
+        with self._cv:
+            self._raise()
+            if self._pending is not None:      # superseded before it started
+                self._pending = None
+                self.dropped += 1
+            slot = 1 if self._writing == (key, 0) else 0
+        host = self._host(key, slot, src)
         host.copy_(src, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        if self._pool is None:
-            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="afl-ckpt")
+        with self._cv:
+            self._pending = (key, slot, build, path, ev)
+            if self._thread is None:
+                self._thread = threading.Thread(target=self._run, name="afl-ckpt", daemon=True)
+                self._thread.start()
+            self._cv.notify_all()
 
-        def job():
-            ev.synchronize()
-            _atomic_save(build(host), path)
+    def _run(self) -> None:
+        while True:
+            with self._cv:
+                while self._pending is None and not self._stop:
+                    self._cv.wait()
+                if self._pending is None:
+                    return
+                key, slot, build, path, ev = self._pending
+                self._pending = None
+                self._writing = (key, slot)
+            try:
+                ev.synchronize()
+                _atomic_save(build(self._bufs[(key, slot)]), path)
+            except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+                with self._cv:
+                    self._err = e
+            with self._cv:
+                self._writing = None
+                self._cv.notify_all()
 
-        self._pending = self._pool.submit(job)
+    def _raise(self) -> None:
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e
 
     def flush(self) -> None:
-        p, self._pending = self._pending, None
-        if p is not None:
-            p.result()  # re-raises a write error in the caller
+        """Wait until the newest submitted checkpoint is on disk (re-raises a write error)."""
+        with self._cv:
+            while self._pending is not None or self._writing is not None:
+                self._cv.wait()
+            self._raise()
 
     def close(self) -> None:
         self.flush()
-        if self._pool is not None:
-            self._pool.shutdown(wait=True)
-            self._pool = None
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
 
 
 def _atomic_save(obj, path: str) -> None:

@@ -197,18 +197,21 @@ void adam_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
   AFL_CHECK_LAUNCH();
 }
 
-double roc_auc(torch::Tensor scores, torch::Tensor labels) {
+// [auc, any NaN score] (device doubles; one host read serves the NaN test and the metric)
+torch::Tensor roc_auc_dev(torch::Tensor scores, torch::Tensor labels) {
   check_dev(scores, "scores", torch::kFloat32);
   check_dev(labels, "labels", torch::kFloat32);
   const int n = scores.numel();
   auto sorted = scores.sort(/*stable=*/true, /*dim=*/0, /*descending=*/true);
   auto s = std::get<0>(sorted).contiguous();
   auto y = labels.index_select(0, std::get<1>(sorted)).contiguous();
-  auto out = torch::empty({1}, scores.options().dtype(torch::kFloat64));
+  auto out = torch::empty({2}, scores.options().dtype(torch::kFloat64));
   afl_roc_auc_sorted(s.data_ptr<float>(), y.data_ptr<float>(), n, out.data_ptr<double>(), cur());
   AFL_CHECK_LAUNCH();
-  return out.item<double>();
+  return out;
 }
+
+double roc_auc(torch::Tensor scores, torch::Tensor labels) { return roc_auc_dev(scores, labels)[0].item<double>(); }
 
 std::vector<torch::Tensor> hyper_delta_vjp(torch::Tensor W, torch::Tensor b, torch::Tensor f, torch::Tensor u) {
   check_dev(W, "W", torch::kFloat32);
@@ -416,6 +419,26 @@ std::vector<torch::Tensor> rnn_train(torch::Tensor params, torch::Tensor rows, t
   return fused_train(1, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, c10::nullopt, 3);
 }
 
+// eval forward of C TransformerModels (params [C, P]) over the same rows -> [C, n]; one call, 3 launches per
+// model from C++ (the hyper validation scores every client's generated model)
+torch::Tensor tf_eval_many(torch::Tensor params, torch::Tensor rows) {
+  check_dev(params, "params", torch::kFloat32);
+  check_dev(rows, "rows", torch::kFloat32);
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == afl_tf_param_count(), "params must be [C, 47693]");
+  const int C = params.size(0), n = rows.size(0);
+  auto out = torch::empty({C, n}, rows.options());
+  const long bfw = (afl_tf_bf_ushorts() + 1) / 2;
+  auto bf = torch::empty({(long)C * bfw}, params.options());
+  if (n == 0) return out;
+  for (int c = 0; c < C; ++c) {
+    TORCH_CHECK(afl_tf_eval_bf(params.data_ptr<float>() + (long)c * params.size(1),
+                               (unsigned short*)(bf.data_ptr<float>() + (long)c * bfw), rows.data_ptr<float>(), n,
+                               out.data_ptr<float>() + (long)c * n, cur()) == 0, "tf_eval launch failed");
+  }
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 torch::Tensor tf_eval(torch::Tensor params, torch::Tensor rows) {
   check_dev(params, "params", torch::kFloat32);
   check_dev(rows, "rows", torch::kFloat32);
@@ -446,6 +469,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stoch_quant", &stoch_quant);
   m.def("adam_flat", &adam_flat);
   m.def("roc_auc", &roc_auc);
+  m.def("roc_auc_dev", &roc_auc_dev);
+  m.def("tf_eval_many", &tf_eval_many);
   m.def("hyper_delta_vjp", &hyper_delta_vjp);
   m.def("hyper_generate", &hyper_generate);
   m.def("hyper_adam_outer", &hyper_adam_outer);

@@ -31,7 +31,10 @@ __global__ void __launch_bounds__(AUC_T) k_roc_auc(const float* __restrict__ s, 
   __shared__ int wsum[16], wmax[16];
   __shared__ int tp_l[AUC_T];
   __shared__ double dred[16];
+  __shared__ int any_nan;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) any_nan = 0;
+  bool nan_seen = false;  // out[1]: any NaN score (the validation's round-failure test), same pass
   int carry_tp = 0;           // positives before this chunk
   int carry_end = -1;         // global index of the last tie-group end before this chunk
   int carry_end_tp = 0;       // tp at that end
@@ -40,6 +43,7 @@ __global__ void __launch_bounds__(AUC_T) k_roc_auc(const float* __restrict__ s, 
     const int i = base + tid;
     const bool valid = i < n;
     const float si = valid ? s[i] : 0.f;
+    nan_seen |= si != si;
     const int yi = valid ? (y[i] > 0.5f ? 1 : 0) : 0;
     const bool end = valid && (i == n - 1 || s[i + 1] != si);
     // inclusive scan of y
@@ -92,12 +96,14 @@ __global__ void __launch_bounds__(AUC_T) k_roc_auc(const float* __restrict__ s, 
   }
   area = wave_sum(area);
   if (lane == 0) dred[w] = area;
+  if (__any(nan_seen) && lane == 0) any_nan = 1;
   __syncthreads();
   if (tid == 0) {
     double a = 0.0;
     for (int k = 0; k < 16; ++k) a += dred[k];
     double P = (double)carry_tp, N = (double)n - P;
     out[0] = (P > 0 && N > 0) ? a * 0.5 / (P * N) : __longlong_as_double(0x7ff8000000000000ll);
+    out[1] = any_nan ? 1.0 : 0.0;
   }
 }
 

@@ -68,3 +68,20 @@ def test_async_checkpoint_files(gpu, tmp_path):
     sd = torch.load(tmp_path / "RNNModel_hyper_3.pth", weights_only=True)
     assert list(sd.keys()) == list(sd_live.keys())
     assert all(torch.equal(sd[k], sd_live[k]) for k in sd)
+
+
+def test_checkpoint_latest_wins(gpu, tmp_path):
+    """Submits that outpace the disk coalesce; the file ends with the newest checkpoint, complete."""
+    import torch
+
+    from attackfl_amd.utils.ckpt import CheckpointWriter
+
+    w = CheckpointWriter()
+    src = torch.empty(1 << 22, dtype=torch.float32, device="cuda")
+    for v in range(6):
+        src.fill_(float(v))
+        w.submit("x", src, lambda t: {"t": t.clone()}, str(tmp_path / "x.pth"))
+    w.flush()
+    got = torch.load(tmp_path / "x.pth", weights_only=True)["t"]
+    assert bool((got == 5.0).all())
+    w.close()
