@@ -610,7 +610,14 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) h0[4 * t + i] = gelu_and_grad(acc[t][i] + bd[4 * t + i], gp[4 * t + i]);
+      for (int i = 0; i < 4; i += 2) {
+        gf2v g2;
+        const gf2v y = gelu2(gf2v{acc[t][i] + bd[4 * t + i], acc[t][i + 1] + bd[4 * t + i + 1]}, g2);
+        h0[4 * t + i] = y[0];
+        h0[4 * t + i + 1] = y[1];
+        gp[4 * t + i] = g2[0];
+        gp[4 * t + i + 1] = g2[1];
+      }
     save16(sv.gp, gp);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_H0, r, 4 * t + g, h0 + 4 * t);
@@ -1317,12 +1324,15 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; i += 2) {
           const int j = 4 * t + i;
-          float gp;
-          const float gl = gelu_and_grad(acc[t][i] + b1[j], gp);
-          a1[j] = bit(mh, j) ? gl * INV_K03 : 0.f;
-          gk1[j] = bit(mh, j) ? gp * INV_K03 : 0.f;
+          gf2v gp;
+          const gf2v gl = gelu2(gf2v{acc[t][i] + b1[j], acc[t][i + 1] + b1[j + 1]}, gp);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            a1[j + h] = bit(mh, j + h) ? gl[h] * INV_K03 : 0.f;
+            gk1[j + h] = bit(mh, j + h) ? gp[h] * INV_K03 : 0.f;
+          }
         }
 #pragma unroll
       for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, r, 4 * t + g, a1 + 4 * t);
@@ -1345,10 +1355,16 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; i += 2) {
           const int j = 4 * t + i;
-          g2[j] = gelu_and_grad(acc[t][i] + b2[j], gp2[j]);
+          gf2v gp;
+          const gf2v gl = gelu2(gf2v{acc[t][i] + b2[j], acc[t][i + 1] + b2[j + 1]}, gp);
+          g2[j] = gl[0];
+          g2[j + 1] = gl[1];
+          gp2[j] = gp[0];
+          gp2[j + 1] = gp[1];
           dot += g2[j] * wo[j];
+          dot += g2[j + 1] * wo[j + 1];
         }
       const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
       const float p = sigmoidf_(y3);

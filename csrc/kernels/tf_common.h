@@ -49,34 +49,48 @@ constexpr int NPARAM = OUT_B + 1;
 static_assert(NPARAM == 47693, "TransformerModel parameter count");
 
 // ---------------------------------------------------------------------------------------------
-// math helpers (fp32, branch-free).  GELU is the exact-erf form of F.gelu; erf comes from the
-// Chebyshev erfc fit of Numerical Recipes (|relative error| < 1.2e-7), whose exp(-x^2/2) is shared
-// with the Gaussian pdf of the GELU derivative.  LN eps 1e-5, biased variance.
+// math helpers (fp32, branch-free).  GELU is the exact-erf form of F.gelu; erfc comes from Abramowitz &
+// Stegun 7.1.26 (|error of erf| <= 1.5e-7: a 5-term polynomial in t = 1/(1 + p z) times exp(-z^2)), whose
+// exp(-x^2/2) is shared with the Gaussian pdf of the GELU derivative — one rcp and one exp per value.
+// LN eps 1e-5, biased variance.
 // ---------------------------------------------------------------------------------------------
 struct GeluPair {
   float cdf;  // Phi(x) = 0.5 (1 + erf(x / sqrt 2))
   float pdf;  // phi(x) = exp(-x^2 / 2) / sqrt(2 pi)
 };
+constexpr float AS_P = 0.3275911f, AS_A1 = 0.254829592f, AS_A2 = -0.284496736f, AS_A3 = 1.421413741f,
+                AS_A4 = -1.453152027f, AS_A5 = 1.061405429f, NLOG2E = -1.4426950408889634f;
 __device__ __forceinline__ GeluPair gelu_parts(float x) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(1.f + 0.5f * z);
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float e = __expf(-z * z);                 // exp(-x^2/2)
-  const float erfc_z = t * e * __expf(p);         // erfc(|x|/sqrt2)
-  const float half_erfc = 0.5f * erfc_z;
+  const float t = __builtin_amdgcn_rcpf(fmaf(AS_P, z, 1.f));
+  float p = fmaf(AS_A5, t, AS_A4);
+  p = fmaf(p, t, AS_A3);
+  p = fmaf(p, t, AS_A2);
+  p = fmaf(p, t, AS_A1);
+  const float e = __builtin_amdgcn_exp2f(z * z * NLOG2E);  // exp(-x^2/2)
+  const float half_erfc = 0.5f * (p * t) * e;            // erfc(|x|/sqrt2) / 2
   GeluPair g;
   g.cdf = x >= 0.f ? 1.f - half_erfc : half_erfc;
   g.pdf = 0.39894228040143268f * e;
   return g;
+}
+// two values at once in packed FP32 (v_pk_fma / v_pk_mul: two lanes' worth of math per instruction);
+// same formula as gelu_parts.  Returns gelu(x), sets gp = gelu'(x).
+typedef float gf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gf2v gelu2(gf2v x, gf2v& gp) {
+  const gf2v z = gf2v{fabsf(x[0]), fabsf(x[1])} * 0.70710678118654752f;
+  const gf2v u = z * AS_P + 1.f;
+  const gf2v t = {__builtin_amdgcn_rcpf(u[0]), __builtin_amdgcn_rcpf(u[1])};
+  gf2v p = t * AS_A5 + AS_A4;
+  p = p * t + AS_A3;
+  p = p * t + AS_A2;
+  p = p * t + AS_A1;
+  const gf2v q = z * z * NLOG2E;
+  const gf2v e = {__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};
+  const gf2v h = (p * t) * (e * 0.5f);
+  const gf2v cdf = {x[0] >= 0.f ? 1.f - h[0] : h[0], x[1] >= 0.f ? 1.f - h[1] : h[1]};
+  gp = x * (e * 0.39894228040143268f) + cdf;
+  return x * cdf;
 }
 __device__ __forceinline__ float gelu(float x) { return x * gelu_parts(x).cdf; }
 __device__ __forceinline__ float gelu_grad(float x) {
