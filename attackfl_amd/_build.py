@@ -84,6 +84,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     # per-file device flags: tf2.hip keeps its optimizer state in AGPRs, so its MFMAs must accumulate
     # in VGPRs (otherwise their accumulators compete with that state for the AGPR half of the budget)
     extra = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("tf2.hip", "tf2_stamps.hip")}
+    if os.environ.get("AFL_TF2_ABL"):  # diagnostic ablation build of the timed kernel (tools/phase_profile.py)
+        extra["tf2_stamps.hip"] = extra["tf2_stamps.hip"] + ["-DTF2_ABL=" + str(int(os.environ["AFL_TF2_ABL"]))]
     hosts = sorted(glob.glob(os.path.join(ROOT, "csrc", "*.cpp")) + glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -348,6 +348,15 @@ __device__ __forceinline__ float aw(float v) {
 struct AdamK {
   float lr_bc1, rsqrt_bc2, keep, c1, eps;
 };
+// Ablation switches of the diagnostic build (compile-time TF2_ABL bits, set through the AFL_TF2_ABL
+// environment variable when building tf2_stamps.hip): skip one piece of work per step to price it
+// (numerics are wrong then; timing only).  Always false in the production kernel.
+enum { ABL_U3 = 1, ABL_UADAM = 2, ABL_UDW = 4, ABL_COLSUM = 8, ABL_HEADUPD = 16, ABL_U1 = 32 };
+#if defined(TF2_STAMPS) && defined(TF2_ABL)
+#define ABL(K, b) ((TF2_ABL & (b)) != 0)
+#else
+#define ABL(K, b) false
+#endif
 // lr_bc1 / rsqrt_bc2 of step t come from the host-computed table a.kt (torch computes them in double on
 // the host as well); a scalar load per step instead of double-precision division / sqrt on every wave
 __device__ __forceinline__ AdamK adam_k(const AflTfTrainArgs& a, int step) {
@@ -548,6 +557,7 @@ __device__ __forceinline__ void load16(float (&x)[16], const uint32_t (&d)[8]) {
 struct BrState {
   TS blk[4];
   VS cmp[5];
+  float dst[5];  // AGPR: where compact entry h's new value goes (cmp_dst), fixed for the round
 };
 constexpr int NCMP = 5;
 template <int BR>
@@ -731,7 +741,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 // d(branch output) -> every activation gradient of the branch (wave-local), the dY tiles of the dW
 // GEMMs and the column sums of the vector gradients
 template <int BR>
-__device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16], const Saved& sv, int lane,
+__device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16], const Saved& sv, const AdamK& K, int lane,
                                             int wave) {
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
@@ -748,15 +758,15 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     const float rstd3 = fk::ln_fwd(xh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
-    ln_colsum(smem, 4, t, lane);
-    ln_colsum(smem, 5, dout, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 4, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 5, dout, lane);
     vec16(gm, vec + VS_G3 * 256, g);
     fk::ln_bwd(dx, dout, xh, rstd3, gm);
     load16(xh, sv.xh2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    ln_colsum(smem, 2, t, lane);
-    ln_colsum(smem, 3, dx, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 2, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 3, dx, lane);
     vec16(gm, vec + VS_G2 * 256, g);
     fk::ln_bwd(dr2, dx, xh, sv.rstd2, gm);
   }
@@ -789,8 +799,8 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     load16(xh, sv.xh1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    ln_colsum(smem, 0, t, lane);
-    ln_colsum(smem, 1, dx, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 0, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 1, dx, lane);
     vec16(gm, vec + VS_G1 * 256, g);
     fk::ln_bwd(dr1, dx, xh, sv.rstd1, gm);
   }
@@ -844,25 +854,44 @@ __device__ __forceinline__ int cmp_param(int e) {
   using C = Cmp<BR>;
   using B = BrK<BR>;
   if (e < B_NVEC) return B::vec_param(e);
-  if (e < C::E_F1) return B::o.dense_w + (e - C::E_D);
+  if (e < C::E_F1) {  // dense [64][din]: entries k-major (i = 64 k + n), so no division by din
+    const int i = e - C::E_D;
+    return B::o.dense_w + (i & 63) * C::din + (i >> 6);
+  }
   if (e < C::E_F2) return B::o.ff0_w + (e - C::E_F1);
-  if (e < C::N) return B::o.ff3_w + (e - C::E_F2);
+  if (e < C::N) {  // ffn.3 [64][6]: k-major too
+    const int i = e - C::E_F2;
+    return B::o.ff3_w + (i & 63) * FF + (i >> 6);
+  }
   return -1;
+}
+// store descriptor of compact entry e for U3: bit 31 set = fp32 store at VEC (bias / LayerNorm entries),
+// clear = bf16 store into a weight image; padding entries and entries past the end point at this lane's
+// dummy word (DF0 tile) instead
+template <int BR>
+__device__ __forceinline__ int cmp_img(int e);
+template <int BR>
+__device__ __forceinline__ uint32_t cmp_dst(int e, int lane) {
+  using C = Cmp<BR>;
+  const uint32_t dmy = B_DF0 + 768 + 4 * lane;
+  if (e >= C::N) return dmy;
+  if (e < B_NVEC) return cmp_param<BR>(e) >= 0 ? (0x80000000u | (uint32_t)(B_VEC + 4 * e)) : (0x80000000u | dmy);
+  return (uint32_t)cmp_img<BR>(e);
 }
 // bf16 image byte offset of compact weight entry e (>= 648)
 template <int BR>
 __device__ __forceinline__ int cmp_img(int e) {
   using C = Cmp<BR>;
   if (e < C::E_F1) {
-    const int i = e - C::E_D, n = i / C::din, k = i % C::din;
-    return B_IMG_D + n * LD32 + pcol(k) * 2;
+    const int i = e - C::E_D;
+    return B_IMG_D + (i & 63) * LD32 + pcol(i >> 6) * 2;
   }
   if (e < C::E_F2) {
     const int i = e - C::E_F1, n = i >> 6, k = i & 63;
     return B_IMG_F1 + n * LD64 + pcol(k) * 2;
   }
-  const int i = e - C::E_F2, n = i / FF, k = i % FF;
-  return B_IMG_F2 + n * LD32 + pcol(k) * 2;
+  const int i = e - C::E_F2;
+  return B_IMG_F2 + (i & 63) * LD32 + pcol(i >> 6) * 2;
 }
 
 // Weight gradients + Adam for one step (after the barrier that ends the backward).  Three parts:
@@ -895,7 +924,7 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     const uchar* X = smem + (lo ? B_XIN : B_F2);
     const uchar* DY = smem + (lo ? B_DZ0 : B_DF3);
 #pragma unroll 1
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
       as = mma(tfrag<TK16>(X, 32 * s, 0, lane), tfrag<TK64>(DY, 32 * s, w4, lane), as);
       // ffn.0: waves w and w + 4 split the 128 rows of k tile w4 (rows 64 (w >> 2) .. + 63)
       if (s < 2) {
@@ -918,9 +947,9 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     for (int i = 0; i < 4; ++i) {
       const int k = 4 * g + i;
       if (lo) {
-        if (k < C::din) gs[C::E_D - B_NVEC + n * C::din + k] = as[i];
+        if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as[i];
       } else {
-        if (k < FF) gs[C::E_F2 - B_NVEC + n * FF + k] = as[i];
+        if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = as[i];
       }
     }
     // ffn.0 partial sums of the two row halves: wave w4 writes, wave w4 + 4 adds after the next barrier
@@ -933,7 +962,7 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     f4v bs[2] = {Z4, Z4};
     const bool do_bias = (w4 & 1) == 0;  // one of the two waves that read dY tiles Tb, Tb + 1
 #pragma unroll 1
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < (ABL(K, ABL_UDW) ? 0 : 4); ++s) {
       const s8v x0 = tfrag<TK64>(X, 32 * s, Ta, lane), x1 = tfrag<TK64>(X, 32 * s, Ta + 1, lane);
       const s8v y0 = tfrag<TK64>(DY, 32 * s, Tb, lane), y1 = tfrag<TK64>(DY, 32 * s, Tb + 1, lane);
       acc[0][0] = mma(x0, y0, acc[0][0]);
@@ -950,7 +979,8 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        tile_adam(st.blk[2 * a + b], bm[2 * a + b], bv[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
+        if (!ABL(K, ABL_UADAM))
+          tile_adam(st.blk[2 * a + b], bm[2 * a + b], bv[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       mom_st(rm, k, tid, bm[k]);
@@ -990,24 +1020,27 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
   }
   lds_bar();
   stp(6, tid);
-  // ---- U3: compact entries (CS is zeroed as it is consumed; the DBL bytes past CS here)
+  // ---- U3: compact entries, branch-free: every entry reads its gradient (CS or GS), runs Adam and
+  // makes three stores whose addresses come from its precomputed descriptor (cmp_dst): the real ones
+  // land in VEC / CS (fp32) or a weight image (bf16), the others in per-lane dummy words of the DF0 tile
+  // (dead until the next backward).  Entries past the end or padding compute on garbage that only
+  // reaches the dummies.  (The divergent if / else version was ~1,200 instructions, 1.4 us per step.)
   if (tid < (B_DBL_BYTES - B_NVEC * 4) / 4) ldsf(smem, B_CS)[B_NVEC + tid] = 0.f;
   float mm[NCMP] = {cm[0], cm[1], cm[2], cm[3], cmv[0]}, vv[NCMP] = {cv[0], cv[1], cv[2], cv[3], cmv[1]};
+  if (!ABL(K, ABL_U3)) {
+    const int dmy = B_DF0 + 4 * (tid & 63);
 #pragma unroll
-  for (int h = 0; h < NCMP; ++h) {
-    const int e = tid + NTH * h;
-    if (e < C::N) {
-      const int pi = cmp_param<BR>(e);
-      if (e < B_NVEC) {
-        LDS_AS float* cs = ldsf(smem, B_CS) + e;
-        const float gsum = *cs;
-        *cs = 0.f;
-        if (pi >= 0) ldsf(smem, B_VEC)[e] = adam1(st.cmp[h].p, mm[h], vv[h], gsum, K);
-      } else {
-        const float gr = ldsf(smem, B_GS)[e - B_NVEC];
-        const float pn = adam1(st.cmp[h].p, mm[h], vv[h], gr, K);
-        *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(pn);
-      }
+    for (int h = 0; h < NCMP; ++h) {
+      const int e = tid + NTH * h;
+      const uint32_t d = aru(st.dst[h]);
+      const bool vec = e < B_NVEC;  // gradient in CS (bias / LayerNorm sums) or GS (staged small dW)
+      const float gr = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
+      const float pn = adam1(st.cmp[h].p, mm[h], vv[h], gr, K);
+      const bool f32 = d >> 31;
+      const int off = (int)(d & 0x7FFFFFFFu);
+      *(LDS_AS float*)(smem + (vec ? B_CS + 4 * e : dmy)) = 0.f;
+      *(LDS_AS float*)(smem + (f32 ? off : dmy + 256)) = pn;
+      *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn);
     }
   }
   mom_st(rm, 8, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
@@ -1047,6 +1080,7 @@ __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P
       }
     }
     st.cmp[h] = VS{aw(p0)};
+    st.dst[h] = awu(cmp_dst<BR>(e, lane));
   }
 }
 
@@ -1180,7 +1214,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     if (lane == 0) abort_w[wave] = fv & 1u;
 #ifndef TF2_NO_BWD
     asm volatile(";MARK bwd");
-    br_backward<BR>(smem, dout, sv, lane, wave);
+    br_backward<BR>(smem, dout, sv, K, lane, wave);
     asm volatile(";MARK bwd_end");
     stp(3, tid);
 #else
@@ -1492,8 +1526,9 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
-          tile_adam(st.blk[2 * x + y], hm[2 * x + y], hv[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
-      tile_adam(st.t2, hm[4], hv[4], HW2, T2, Tn2, lane, a2, K, smem);
+          if (!ABL(K, ABL_HEADUPD))
+            tile_adam(st.blk[2 * x + y], hm[2 * x + y], hv[2 * x + y], HW1, Ta + x, Tb + y, lane, acc[x][y], K, smem);
+      if (!ABL(K, ABL_HEADUPD)) tile_adam(st.t2, hm[4], hv[4], HW2, T2, Tn2, lane, a2, K, smem);
       if (tid < H_NVEC) {
         // the 8 waves' partial sums in a fixed order: bit-reproducible whatever order the waves ran in
         const LDS_AS float* c = ldsf(smem, H_PART) + tid;
