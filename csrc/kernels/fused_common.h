@@ -447,11 +447,14 @@ __device__ __forceinline__ float cs_total(const CT& c, int v, int col) {
   return s;
 }
 
-// row-wise sum over the 4 lanes (quarters) of a row: lanes l, l^16, l^32, l^48
+// row-wise sum over the 4 lanes (quarters) of a row: lanes l, l^16, l^32, l^48.  permlane16_swap(a, a)
+// leaves this lane's and its l^16 partner's value in the two outputs (in either order), so their sum
+// is the pair sum exactly; the same with permlane32_swap for l^32.
 __device__ __forceinline__ float rsum4(float a) {
-  a += xor16(a);
-  a += xor32(a);
-  return a;
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  a = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
 // LayerNorm forward on 16 values/lane (64-wide row): returns xhat in place, rstd

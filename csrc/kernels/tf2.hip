@@ -226,13 +226,34 @@ __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  
 __device__ __forceinline__ void lds_addd(uchar* base, int idx, float v) {
   __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// partner lane's value (bound_ctrl: 0 for a missing source, which none of these patterns has) in the
+// form the backend's DPP combine folds into the consuming add
+template <int BIT>
+__device__ __forceinline__ float dppz(float a) {
+  constexpr int C = BIT == 2 ? 0x141 : BIT == 0 ? 0xB1 : BIT == 1 ? 0x4E : 0x128;
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), C, 0xF, 0xF, true));
+}
+// one reduce-scatter level (fused_common.h rs_level, select-light form): both halves are summed with
+// the partner's copy (the DPP move folds into the add) and ONE select keeps this lane's half
+template <int N, int L>
+__device__ __forceinline__ void rs_level2(float* v, int i, int& j) {
+  constexpr int BIT = L == 0 ? 2 : L == 1 ? 0 : L == 2 ? 1 : 3;
+  constexpr int H = N / 2;
+  const bool b = (i >> BIT) & 1;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float lo = v[k] + dppz<BIT>(v[k]), hi = v[k + H] + dppz<BIT>(v[k + H]);
+    v[k] = b ? hi : lo;
+  }
+  j += b ? H : 0;
+}
 template <int W>
 __device__ __forceinline__ int rs_slot(float (&s)[W], int i) {
   int j = 0;
-  fk::rs_level<W, 0>(s, i, j);
-  fk::rs_level<W / 2, 1>(s, i, j);
-  if constexpr (W >= 8) fk::rs_level<W / 4, 2>(s, i, j);
-  if constexpr (W >= 16) fk::rs_level<W / 8, 3>(s, i, j);
+  rs_level2<W, 0>(s, i, j);
+  rs_level2<W / 2, 1>(s, i, j);
+  if constexpr (W >= 8) rs_level2<W / 4, 2>(s, i, j);
+  if constexpr (W >= 16) rs_level2<W / 8, 3>(s, i, j);
   if constexpr (W == 4) s[0] += fk::dpp_pair<1>(s[0]);
   if constexpr (W <= 8) s[0] += fk::dpp_pair<3>(s[0]);
   return j;
@@ -281,6 +302,52 @@ __device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, 
   return m;
 }
 __device__ __forceinline__ bool bit(uint32_t m, int j) { return (m >> j) & 1u; }
+
+// ------------------------------------------------------------------------ packed-FP32 row math
+// The branch workgroups are VALU-issue-bound, so the LayerNorm / affine math runs two features per
+// instruction (v_pk_add / v_pk_mul / v_pk_fma on float2 pairs of the 16 values a lane holds).
+__device__ __forceinline__ gf2v ld2(const float (&x)[16], int j) { return gf2v{x[2 * j], x[2 * j + 1]}; }
+__device__ __forceinline__ void st2(float (&x)[16], int j, gf2v v) {
+  x[2 * j] = v[0];
+  x[2 * j + 1] = v[1];
+}
+// LayerNorm forward (biased variance, eps 1e-5) of a 64-wide row held as 16 values x 4 lanes: x -> xhat
+__device__ __forceinline__ float ln_fwd2(float (&x)[16]) {
+  gf2v s = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += ld2(x, j);
+  const float mean = fk::rsum4(s[0] + s[1]) * (1.f / 64.f);
+  gf2v ss = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const gf2v d = ld2(x, j) - mean;
+    st2(x, j, d);
+    ss += d * d;
+  }
+  const float rstd = __builtin_amdgcn_rsqf(fk::rsum4(ss[0] + ss[1]) * (1.f / 64.f) + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st2(x, j, ld2(x, j) * rstd);
+  return rstd;
+}
+// LayerNorm backward: dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma
+__device__ __forceinline__ void ln_bwd2(float (&dx)[16], const float (&dy)[16], const float (&xh)[16], float rstd,
+                                        const float (&gamma)[16]) {
+  gf2v a = {0.f, 0.f}, b = {0.f, 0.f}, g[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    g[j] = ld2(dy, j) * ld2(gamma, j);
+    a += g[j];
+    b += g[j] * ld2(xh, j);
+  }
+  const float am = fk::rsum4(a[0] + a[1]) * (1.f / 64.f), bm = fk::rsum4(b[0] + b[1]) * (1.f / 64.f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st2(dx, j, (g[j] - am - ld2(xh, j) * bm) * rstd);
+}
+// y = x * gamma + beta
+__device__ __forceinline__ void affine2(float (&y)[16], const float (&x)[16], const float (&gm)[16], const float (&bt)[16]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st2(y, j, ld2(x, j) * ld2(gm, j) + ld2(bt, j));
+}
 
 // ------------------------------------------------------------------------ per-phase timers (diagnostics)
 // Built only into the TF2_STAMPS instantiation (tf2_stamps.hip): s_memrealtime (100 MHz) deltas of
@@ -677,13 +744,12 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
         const int j = 4 * t + i;
         x1[j] = h0[j] + (bit(sv.m1, j) ? (acc[t][i] + bo[j]) * INV_K01 : 0.f);
       }
-    sv.rstd1 = fk::ln_fwd(x1);
+    sv.rstd1 = ln_fwd2(x1);
     save16(sv.xh1, x1);
     float gm[16], bt[16];
     vec16(gm, vec + VS_G1 * 256, g);
     vec16(bt, vec + VS_B1 * 256, g);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x1n[j] = x1[j] * gm[j] + bt[j];
+    affine2(x1n, x1, gm, bt);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_X1N, r, 4 * t + g, x1n + 4 * t);
   }
@@ -722,18 +788,16 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
         const int j = 4 * t + i;
         x2[j] = x1n[j] + (bit(sv.m2, j) ? (acc[t][i] + b3[j]) * INV_K01 : 0.f);
       }
-    sv.rstd2 = fk::ln_fwd(x2);
+    sv.rstd2 = ln_fwd2(x2);
     save16(sv.xh2, x2);
     float gm[16], bt[16];
     vec16(gm, vec + VS_G2 * 256, g);
     vec16(bt, vec + VS_B2 * 256, g);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x2[j] = x2[j] * gm[j] + bt[j];
-    fk::ln_fwd(x2);
+    affine2(x2, x2, gm, bt);
+    ln_fwd2(x2);
     vec16(gm, vec + VS_G3 * 256, g);
     vec16(bt, vec + VS_B3 * 256, g);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x2[j] = x2[j] * gm[j] + bt[j];
+    affine2(x2, x2, gm, bt);
     pack16(x2, outp);
   }
 }
@@ -753,22 +817,21 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     load16(xh, sv.xh2);
     vec16(gm, vec + VS_G2 * 256, g);
     vec16(bt, vec + VS_B2 * 256, g);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) xh[j] = xh[j] * gm[j] + bt[j];
-    const float rstd3 = fk::ln_fwd(xh);
+    affine2(xh, xh, gm, bt);
+    const float rstd3 = ln_fwd2(xh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 4, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 5, dout, lane);
     vec16(gm, vec + VS_G3 * 256, g);
-    fk::ln_bwd(dx, dout, xh, rstd3, gm);
+    ln_bwd2(dx, dout, xh, rstd3, gm);
     load16(xh, sv.xh2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 2, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 3, dx, lane);
     vec16(gm, vec + VS_G2 * 256, g);
-    fk::ln_bwd(dr2, dx, xh, sv.rstd2, gm);
+    ln_bwd2(dr2, dx, xh, sv.rstd2, gm);
   }
   float df0[4];
   sb();
@@ -802,7 +865,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 0, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 1, dx, lane);
     vec16(gm, vec + VS_G1 * 256, g);
-    fk::ln_bwd(dr1, dx, xh, sv.rstd1, gm);
+    ln_bwd2(dr1, dx, xh, sv.rstd1, gm);
   }
   float dv[16];
   sb();
@@ -1335,13 +1398,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       cv[2] = ld_wt(rs, off + 16384);
       cv[3] = ld_wt(rs, off + 16384 + 16);
     }
-    // cat -> LDS (X of dWf1): tile t of the 8 = half (t & 1) of cv[t >> 1]
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const u32x4 u = cv[t >> 1];
-      const u32x2v v = (t & 1) ? u32x2v{u[2], u[3]} : u32x2v{u[0], u[1]};
-      *(LDS_AS u32x2v*)(smem + H_CAT + t128(r, 4 * t + g)) = v;
-    }
+    // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
+    // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
     // ---- fc1 + GELU + dropout(0.3)
     float a1[16], gk1[16];
     {
@@ -1368,11 +1426,9 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
             gk1[j + h] = bit(mh, j + h) ? gp[h] * INV_K03 : 0.f;
           }
         }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, r, 4 * t + g, a1 + 4 * t);
     }
     // ---- fc2 + GELU, output layer, sigmoid, BCE (log clamped at -100)
-    float dz2[8];
+    float dz2[8], gw[8];
     float lrow = 0.f, dy3 = 0.f;
     {
       const s8v b0 = bfrag(a1, 0), b1 = bfrag(a1, 1);
@@ -1410,28 +1466,15 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         const float pq = p * (1.f - p);
         dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
       }
-      float gw[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         dz2[j] = dy3 * wo[j] * gp2[j];
         gw[j] = dy3 * g2[j];
       }
-      float sb2, swo;
-      const int f2 = colsum32(dz2, lane, sb2), fo = colsum32(gw, lane, swo);
-      if (f2 >= 0) {
-        part[HV_B2 + f2] = sb2;
-        part[HV_WO + fo] = swo;
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, r, 4 * t + g, dz2 + 4 * t);
     }
-    // per-wave loss partial and d output.bias (each row counted once: lane group 0)
+    // per-wave loss partial (each row counted once: lane group 0); its NaN test rides on the hand-off flag
     float lsum = wave_sum(g == 0 ? lrow : 0.f);
-    const float dbo = wave_sum(g == 0 ? dy3 : 0.f);
-    if (lane == 0) {
-      lossw[wave] = lsum;
-      part[HV_BO] = dbo;
-    }
+    if (lane == 0) lossw[wave] = lsum;
     const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
     // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
     float dz1[16];
@@ -1443,11 +1486,6 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 #pragma unroll
         for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
       }
-      float sb1;
-      const int f1 = colsum64(dz1, lane, sb1);
-      part[HV_B1 + f1] = sb1;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, r, 4 * t + g, dz1 + 4 * t);
     }
     // ---- d cat = dz1 . W1, each half straight to its branch
     {
@@ -1475,6 +1513,32 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         __hip_atomic_store(xf(sync, XF_BVIT, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(xf(sync, XF_BLAB, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    }
+    // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)
+    {
+      sb();
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {  // cat: tile t of the 8 = half (t & 1) of cv[t >> 1]
+        const u32x4 u = cv[t >> 1];
+        const u32x2v v = (t & 1) ? u32x2v{u[2], u[3]} : u32x2v{u[0], u[1]};
+        *(LDS_AS u32x2v*)(smem + H_CAT + t128(r, 4 * t + g)) = v;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, r, 4 * t + g, a1 + 4 * t);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, r, 4 * t + g, dz2 + 4 * t);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, r, 4 * t + g, dz1 + 4 * t);
+      float sb2, swo, sb1;
+      const int f2 = colsum32(dz2, lane, sb2), fo = colsum32(gw, lane, swo);
+      if (f2 >= 0) {
+        part[HV_B2 + f2] = sb2;
+        part[HV_WO + fo] = swo;
+      }
+      const int f1 = colsum64(dz1, lane, sb1);
+      part[HV_B1 + f1] = sb1;
+      const float dbo = wave_sum(g == 0 ? dy3 : 0.f);  // d output.bias
+      if (lane == 0) part[HV_BO] = dbo;
     }
     stp(11, tid);
     // Adam moments of this step's update (after the hand-off drain, before the loss barrier)
