@@ -81,11 +81,13 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     host_flags = common + ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM",
                            "-I" + py_inc, "-I" + os.path.join(ROCM, "include")] + ["-I" + p for p in inc] + ["-x", "c++"]
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
-    # per-file device flags: tf2.hip keeps its optimizer state in AGPRs, so its MFMAs must accumulate
+    # per-file device flags: the on-chip trainers (tf2 / rnn2) keep their optimizer state in AGPRs, so its MFMAs must accumulate
     # in VGPRs (otherwise their accumulators compete with that state for the AGPR half of the budget)
-    extra = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("tf2.hip", "tf2_stamps.hip")}
+    extra = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("tf2.hip", "tf2_stamps.hip", "rnn2.hip", "rnn2_stamps.hip")}
     if os.environ.get("AFL_TF2_ABL"):  # diagnostic ablation build of the timed kernel (tools/phase_profile.py)
         extra["tf2_stamps.hip"] = extra["tf2_stamps.hip"] + ["-DTF2_ABL=" + str(int(os.environ["AFL_TF2_ABL"]))]
+    if os.environ.get("AFL_RNN2_DEBUG"):  # diagnostic printf build of the on-chip RNN trainer
+        extra["rnn2.hip"] = extra["rnn2.hip"] + ["-DRNN2_" + os.environ["AFL_RNN2_DEBUG"]]
     hosts = sorted(glob.glob(os.path.join(ROOT, "csrc", "*.cpp")) + glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

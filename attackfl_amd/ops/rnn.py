@@ -1,5 +1,6 @@
-"""Fused RNNModel/ICU local training (``csrc/kernels/rnn.hip``): one launch trains all of a rank's
-clients for all their local epochs, three co-resident workgroups per client (head | vitals | labs).
+"""Fused RNNModel/ICU local training (``csrc/kernels/rnn2.hip``, on-chip; ``rnn.hip`` as split 3): one
+launch trains all of a rank's clients for all their local epochs, three co-resident workgroups per client
+(head | vitals | labs).
 
 Dropout masks follow the layer-program convention (``fl/programs.py``), so the composite
 ``RNNProgram`` on CPU is the exact-semantics oracle of this kernel (tests/test_gpu_rnn.py).
@@ -44,19 +45,30 @@ def _dev_i32(nd, dev) -> torch.Tensor:
 
 
 def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
-                        lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Enqueue the launch; returns DEVICE (ok [C] int32, losses [C, E]) without synchronising."""
+                        lr: float, seeds: Sequence[int], opt_mode: int = 0, split: int = 4,
+                        stamps: torch.Tensor = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Enqueue the launch; returns DEVICE (ok [C] int32, losses [C, E]) without synchronising.
+
+    ``split`` 4 = the on-chip trainer (``rnn2.hip``: weights, optimizer state and activations in registers /
+    LDS for the whole round), 3 = the global-workspace kernel (``rnn.hip``).  ``stamps``: device int64 [64]
+    per-phase timers of workgroup ``stamps[63]`` (split 4 only; tools/phase_profile.py)."""
+    from .transformer import adam_step_table
+
     dev = params.device
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else _seeds(seeds, dev)
+    kt = None
+    if split == 4:
+        kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     return native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t,
-                              int(epochs), int(batch), float(lr), int(opt_mode))
+                              int(epochs), int(batch), float(lr), int(opt_mode), int(split), kt, stamps)
 
 
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
-                  lr: float, seeds: Sequence[int], opt_mode: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+                  lr: float, seeds: Sequence[int], opt_mode: int = 0, split: int = 4,
+                  stamps: torch.Tensor = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Train ``params [C, 97665]`` in place.  Returns (ok [C] int32, losses [C, E]) on the host."""
     from .transformer import finish
 
-    return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode),
+    return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, split, stamps),
                   what="fused RNN trainer")

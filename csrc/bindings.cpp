@@ -355,9 +355,10 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   const int C = params.size(0);
   TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
   TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
-  // split 4 = the on-chip TransformerModel trainer (tf2.hip: 3 workgroups per client, state in registers)
-  const bool tf2 = kind == 0 && split == 4;
-  const long stride = (((tf2 ? afl_tf2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats()) + 63) / 64) * 64;
+  // split 4 = the on-chip trainers (tf2.hip / rnn2.hip: 3 workgroups per client, state in registers / LDS)
+  const bool tf2 = kind == 0 && split == 4, rnn2 = kind == 1 && split == 4;
+  const long wsf = tf2 ? afl_tf2_ws_floats() : rnn2 ? afl_rnn2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats();
+  const long stride = ((wsf + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());
   auto ok = torch::zeros({C}, order.options());
   auto losses = torch::zeros({C, epochs}, params.options());
@@ -393,13 +394,14 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
     a.kt = kt->data_ptr<float>();
     a.kt_n = (int)kt->size(0);
   }
-  a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);
+  a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);  // (rnn2 / tf2: 3 workgroups per client)
   torch::Tensor sync;
   if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
     sync = torch::zeros({(long)C * AFL_TF_SYNC_WORDS}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
-  const int rc = tf2 ? afl_tf2_train(&a, cur()) : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
+  const int rc = tf2 ? afl_tf2_train(&a, cur()) : rnn2 ? afl_rnn2_train(&a, cur())
+                 : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
   TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
   TORCH_CHECK(rc != -5, "on-chip trainer: Adam step table (kt) missing or shorter than the round");
   TORCH_CHECK(rc == 0, "fused trainer launch failed (", rc, ")");
@@ -414,9 +416,11 @@ std::vector<torch::Tensor> tf_train(torch::Tensor params, torch::Tensor rows, to
   return fused_train(0, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split, kt);
 }
 
+// split 3 = rnn.hip (global-workspace kernel), 4 = rnn2.hip (on-chip; needs the Adam step table kt)
 std::vector<torch::Tensor> rnn_train(torch::Tensor params, torch::Tensor rows, torch::Tensor order, torch::Tensor nd,
-                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr, int64_t opt_mode) {
-  return fused_train(1, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, c10::nullopt, 3);
+                                     torch::Tensor seeds, int64_t epochs, int64_t batch, double lr, int64_t opt_mode,
+                                     int64_t split, c10::optional<torch::Tensor> kt, c10::optional<torch::Tensor> stamps) {
+  return fused_train(1, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split, kt);
 }
 
 // eval forward of C TransformerModels (params [C, P]) over the same rows -> [C, n]; one call, 3 launches per
@@ -482,7 +486,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
         py::arg("stamps") = py::none(), py::arg("split") = 1, py::arg("kt") = py::none());
   m.def("rnn_train", &rnn_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
-        py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0);
+        py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
+        py::arg("split") = 3, py::arg("kt") = py::none(), py::arg("stamps") = py::none());
   m.def("rnn_param_count", &afl_rnn_param_count);
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);

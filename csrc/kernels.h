@@ -88,6 +88,10 @@ long afl_tf2_ws_floats();
 // rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
 int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);
 long afl_rnn_ws_floats();
+// rnn2.hip (RNNModel on-chip trainer: 3 workgroups per client, model state on chip, Adam step table kt)
+int afl_rnn2_train(const AflTfTrainArgs* a, hipStream_t s);
+int afl_rnn2_train_stamped(const AflTfTrainArgs* a, hipStream_t s);
+long afl_rnn2_ws_floats();
 int afl_rnn_param_count();
 int afl_tf_bf_ushorts();
 int afl_tf_param_count();

@@ -27,20 +27,17 @@
 #include "kernels.h"
 #include "tf_common.h"
 #include "fused_common.h"
+#include "onchip.h"
 
 using namespace tf;
 
 namespace t2 {
 
-using fk::u32x4;
-typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-typedef unsigned char uchar;
+using namespace oc;
 
-constexpr int NTH = 512;
+
 
 // ----------------------------------------------------------------------------------- LDS maps (bytes)
-// weight images: bf16 [rows][ld] with the K axis permuted (pcol); ld padded by 8 elements
-constexpr int LD32 = 40 * 2, LD64 = 72 * 2, LD128 = 136 * 2;  // row strides in bytes
 // branch workgroup
 constexpr int B_IMG_D = 0;                         // [64][32]  dense (K = din padded to 32)
 constexpr int B_IMG_V = B_IMG_D + 64 * LD32;       // [64][64]  in_proj rows 128..191 (v)
@@ -111,172 +108,6 @@ constexpr long WS_MOM = WS_XB + 32768;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
 constexpr long WS_BYTES = WS_MOM + 3 * MOM_WG_BYTES;
 
-// ------------------------------------------------------------------------------ small helpers
-// every LDS access goes through an address_space(3) pointer (a generic one would become FLAT, which
-// counts in vmcnt too and breaks the hand-off's counted waits)
-__device__ __forceinline__ LDS_AS float* ldsf(uchar* base, int byte_off) { return (LDS_AS float*)(base + byte_off); }
-__device__ __forceinline__ LDS_AS uint32_t* ldsu(uchar* base, int byte_off) {
-  return (LDS_AS uint32_t*)(base + byte_off);
-}
-__device__ __forceinline__ uint32_t pk2(float a, float b) { return fk::pack_bf2(a, b); }
-__device__ __forceinline__ s8v pk8(float a0, float a1, float a2, float a3, float b0, float b1, float b2, float b3) {
-  u32x4 u{pk2(a0, a1), pk2(a2, a3), pk2(b0, b1), pk2(b2, b3)};
-  return __builtin_bit_cast(s8v, u);
-}
-// B fragment of k-step s from a T-layout register row (tiles 2s and 2s+1)
-__device__ __forceinline__ s8v bfrag(const float* v, int s) {
-  const float* a = v + 8 * s;
-  return pk8(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
-}
-__device__ __forceinline__ s8v bfrag_lo(const float* v) {  // K = 16 padded to 32: second half zero
-  return pk8(v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f);
-}
-__device__ __forceinline__ f4v mma(s8v a, s8v b, f4v c) { return fk::mfma(a, b, c); }
-constexpr f4v Z4 = {0.f, 0.f, 0.f, 0.f};
-
-// permuted K position of weight column k: the 8 values lane group g of k-step s multiplies are
-// columns {32s + 4g + i, 32s + 16 + 4g + i} (tiles 2s, 2s+1 of the T layout) -> stored contiguously
-__host__ __device__ constexpr int pcol(int k) {
-  return 32 * (k >> 5) + 8 * ((k >> 2) & 3) + 4 * ((k >> 4) & 1) + (k & 3);
-}
-
-// forward A fragment: W rows 16T + (lane & 15), permuted K chunk of k-step s (one ds_read_b128)
-__device__ __forceinline__ s8v wfrag(const uchar* img, int ld, int T, int s, int lane) {
-  return *(const LDS_AS s8v*)(img + (16 * T + (lane & 15)) * ld + (32 * s + 8 * (lane >> 4)) * 2);
-}
-__device__ __forceinline__ s4v tr16(const uchar* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)p);
-}
-__device__ __forceinline__ s8v cat44(s4v a, s4v b) {
-  s8v r;
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-  return r;
-}
-// backward A fragment (d input = dY . W, computed as W^T . dY^T): lane (m, g) needs W[n][16T + m] for
-// n = 32s + 16h + 4g + j (h = 0, 1; j = 0..3) -> two transposed reads of the same image.  Rows at or
-// past `nrows` read as zero (hi == false drops the second half: images with <= 16 rows).
-template <bool HI>
-__device__ __forceinline__ s8v wtfrag(const uchar* img, int ld, int T, int s, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int col = 32 * (T >> 1) + 8 * p + 4 * (T & 1);
-  const uchar* a = img + (32 * s + 4 * g + q) * ld + col * 2;
-  s4v lo = tr16(a);
-  s4v hi = {0, 0, 0, 0};
-  if (HI) hi = tr16(a + 16 * ld);
-  return cat44(lo, hi);
-}
-
-// XOR-swizzled activation tiles [128 rows][W bf16] (8-byte chunks); chosen so the T-layout row stores
-// (16 rows x one chunk per instruction) and the dW transposed reads (rows 8g+q, 8g+q+4, chunks 4T+p)
-// are conflict-free
-__device__ __forceinline__ int sw64(int r) {
-  return (r & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3);
-}
-__device__ __forceinline__ int t64(int r, int c8) { return r * 128 + ((c8 ^ sw64(r)) << 3); }
-__device__ __forceinline__ int sw128(int r) {
-  return ((((r & 3) | (((r >> 3) & 1) << 2))) << 2) | ((r >> 2) & 1) | (((r >> 3) & 1) << 1);
-}
-__device__ __forceinline__ int t128(int r, int c8) { return r * 256 + ((c8 ^ sw128(r)) << 3); }
-__device__ __forceinline__ int t32(int r, int c8) { return r * 64 + ((c8 ^ ((r >> 1) & 7)) << 3); }
-__device__ __forceinline__ int t16(int r, int c8) {
-  const int pr = r ^ (((r >> 3) & 1) << 2);
-  return pr * 32 + ((c8 ^ ((pr >> 2) & 3)) << 3);
-}
-enum { TK16 = 0, TK32, TK64, TK128 };
-template <int K>
-__device__ __forceinline__ int toff(int r, int c8) {
-  if constexpr (K == TK16) return t16(r, c8);
-  else if constexpr (K == TK32) return t32(r, c8);
-  else if constexpr (K == TK64) return t64(r, c8);
-  else return t128(r, c8);
-}
-// 4 consecutive features (one 8-byte chunk) of a row
-template <int K>
-__device__ __forceinline__ void st4(uchar* tile, int r, int c8, const float* x) {
-  *(LDS_AS u32x2v*)(tile + toff<K>(r, c8)) = u32x2v{pk2(x[0], x[1]), pk2(x[2], x[3])};
-}
-// dW operand fragment: lane (i, g) gets tile[r0 + 8g + j][16T + i], j = 0..7 (two transposed reads)
-template <int K>
-__device__ __forceinline__ s8v tfrag(const uchar* tile, int r0, int T, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int row = r0 + 8 * g + q;
-  return cat44(tr16(tile + toff<K>(row, 4 * T + p)), tr16(tile + toff<K>(row + 4, 4 * T + p)));
-}
-
-// 16 fp32 of a T-layout row from an fp32 LDS vector (features 16t + 4g + i)
-__device__ __forceinline__ void vec16(float (&x)[16], const uchar* vec, int g) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const f4v v = *(const LDS_AS f4v*)(vec + (16 * t + 4 * g) * 4);
-    x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
-  }
-}
-__device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  // 32-wide: tiles 0, 1
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const f4v v = *(const LDS_AS f4v*)(vec + (16 * t + 4 * g) * 4);
-    x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
-  }
-}
-
-// column sums over the wave's 16 rows of W values per lane (DPP reduce-scatter, fused_common.h): each
-// lane ends with the sum of one feature; the caller sends it to a per-wave slot (head) or an fp64 LDS
-// accumulator (branches)
-__device__ __forceinline__ void lds_addd(uchar* base, int idx, float v) {
-  __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// partner lane's value (bound_ctrl: 0 for a missing source, which none of these patterns has) in the
-// form the backend's DPP combine folds into the consuming add
-template <int BIT>
-__device__ __forceinline__ float dppz(float a) {
-  constexpr int C = BIT == 2 ? 0x141 : BIT == 0 ? 0xB1 : BIT == 1 ? 0x4E : 0x128;
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), C, 0xF, 0xF, true));
-}
-// one reduce-scatter level (fused_common.h rs_level, select-light form): both halves are summed with
-// the partner's copy (the DPP move folds into the add) and ONE select keeps this lane's half
-template <int N, int L>
-__device__ __forceinline__ void rs_level2(float* v, int i, int& j) {
-  constexpr int BIT = L == 0 ? 2 : L == 1 ? 0 : L == 2 ? 1 : 3;
-  constexpr int H = N / 2;
-  const bool b = (i >> BIT) & 1;
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    const float lo = v[k] + dppz<BIT>(v[k]), hi = v[k + H] + dppz<BIT>(v[k + H]);
-    v[k] = b ? hi : lo;
-  }
-  j += b ? H : 0;
-}
-template <int W>
-__device__ __forceinline__ int rs_slot(float (&s)[W], int i) {
-  int j = 0;
-  rs_level2<W, 0>(s, i, j);
-  rs_level2<W / 2, 1>(s, i, j);
-  if constexpr (W >= 8) rs_level2<W / 4, 2>(s, i, j);
-  if constexpr (W >= 16) rs_level2<W / 8, 3>(s, i, j);
-  if constexpr (W == 4) s[0] += fk::dpp_pair<1>(s[0]);
-  if constexpr (W <= 8) s[0] += fk::dpp_pair<3>(s[0]);
-  return j;
-}
-// 16 values (64 features, T layout) -> (feature of this lane, its column sum)
-__device__ __forceinline__ int colsum64(const float (&x)[16], int lane, float& sum) {
-  float s[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) s[j] = x[j];
-  const int j = rs_slot<16>(s, lane & 15);
-  sum = s[0];
-  return 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
-}
-// 8 values (32 features: tiles 0, 1); only lanes with (lane & 8) == 0 hold a sum (returns -1 otherwise)
-__device__ __forceinline__ int colsum32(const float (&x)[8], int lane, float& sum) {
-  float s[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = x[j];
-  const int i = lane & 15;
-  const int j = rs_slot<8>(s, i);
-  sum = s[0];
-  return (i & 8) == 0 ? 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3) : -1;
-}
 // branch LayerNorm column sums -> fp64 accumulator k of DBL (order G1 B1 G2 B2 G3 B3)
 __device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
   float s;
@@ -301,53 +132,7 @@ __device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, 
   }
   return m;
 }
-__device__ __forceinline__ bool bit(uint32_t m, int j) { return (m >> j) & 1u; }
 
-// ------------------------------------------------------------------------ packed-FP32 row math
-// The branch workgroups are VALU-issue-bound, so the LayerNorm / affine math runs two features per
-// instruction (v_pk_add / v_pk_mul / v_pk_fma on float2 pairs of the 16 values a lane holds).
-__device__ __forceinline__ gf2v ld2(const float (&x)[16], int j) { return gf2v{x[2 * j], x[2 * j + 1]}; }
-__device__ __forceinline__ void st2(float (&x)[16], int j, gf2v v) {
-  x[2 * j] = v[0];
-  x[2 * j + 1] = v[1];
-}
-// LayerNorm forward (biased variance, eps 1e-5) of a 64-wide row held as 16 values x 4 lanes: x -> xhat
-__device__ __forceinline__ float ln_fwd2(float (&x)[16]) {
-  gf2v s = {0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s += ld2(x, j);
-  const float mean = fk::rsum4(s[0] + s[1]) * (1.f / 64.f);
-  gf2v ss = {0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const gf2v d = ld2(x, j) - mean;
-    st2(x, j, d);
-    ss += d * d;
-  }
-  const float rstd = __builtin_amdgcn_rsqf(fk::rsum4(ss[0] + ss[1]) * (1.f / 64.f) + 1e-5f);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) st2(x, j, ld2(x, j) * rstd);
-  return rstd;
-}
-// LayerNorm backward: dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma
-__device__ __forceinline__ void ln_bwd2(float (&dx)[16], const float (&dy)[16], const float (&xh)[16], float rstd,
-                                        const float (&gamma)[16]) {
-  gf2v a = {0.f, 0.f}, b = {0.f, 0.f}, g[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    g[j] = ld2(dy, j) * ld2(gamma, j);
-    a += g[j];
-    b += g[j] * ld2(xh, j);
-  }
-  const float am = fk::rsum4(a[0] + a[1]) * (1.f / 64.f), bm = fk::rsum4(b[0] + b[1]) * (1.f / 64.f);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) st2(dx, j, (g[j] - am - ld2(xh, j) * bm) * rstd);
-}
-// y = x * gamma + beta
-__device__ __forceinline__ void affine2(float (&y)[16], const float (&x)[16], const float (&gm)[16], const float (&bt)[16]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) st2(y, j, ld2(x, j) * ld2(gm, j) + ld2(bt, j));
-}
 
 // ------------------------------------------------------------------------ per-phase timers (diagnostics)
 // Built only into the TF2_STAMPS instantiation (tf2_stamps.hip): s_memrealtime (100 MHz) deltas of
@@ -375,46 +160,6 @@ struct Stamp {
 };
 #endif
 
-// ------------------------------------------------------------------------------------------- Adam
-// fp32 master weights live in ACCUMULATION registers (AGPRs) for the whole round: every access goes
-// through v_accvgpr_read / v_accvgpr_write, so the register allocator gives them the AGPR class and the
-// forward / backward working set keeps the architectural VGPRs (the two files share one 256-entry budget
-// per lane at two waves per SIMD).  Their Adam moments m, v do NOT fit beside them: with p, m and v all in
-// AGPRs the allocator spilled ~50 dwords of state to scratch, reloaded one dependent load at a time (~8 us
-// of a 29 us step).  The moments therefore live in the workspace slab (WS_MOM) and every update phase
-// issues all of its moment loads as one batch before the work that precedes the Adam arithmetic.
-struct TS {  // one 16x16 weight-gradient tile's 4 elements of this lane
-  float p[4];
-};
-struct VS {
-  float p;
-};
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-}
-// moment slot s of this thread (sc1 loads: L2-served, never a stale L1 line of the previous step)
-__device__ __forceinline__ f4v mom_ld(__amdgpu_buffer_rsrc_t rs, int s, int tid) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (s * NTH + tid) * 16, 0, 16));
-}
-__device__ __forceinline__ void mom_st(__amdgpu_buffer_rsrc_t rs, int s, int tid, f4v v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (s * NTH + tid) * 16, 0, 0);
-}
-__device__ __forceinline__ float ar(float a) {
-  float r;
-  asm("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(a));
-  return r;
-}
-__device__ __forceinline__ float aw(float v) {
-  float r;
-  asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
-  return r;
-}
-// Step constants.  Adam (torch.optim.Adam defaults): keep = 1, c1 = 1 - beta1, lr_bc1 = lr / (1 - beta1^t),
-// rsqrt_bc2 = 1 / sqrt(1 - beta2^t), eps = 1e-8.  SGD test mode (raw gradients for the tests): keep = 0,
-// c1 = 1, lr_bc1 = lr, rsqrt_bc2 = 0, eps = 1, so the same branch-free formula gives m = g, p -= lr g.
-struct AdamK {
-  float lr_bc1, rsqrt_bc2, keep, c1, eps;
-};
 // Ablation switches of the diagnostic build (compile-time TF2_ABL bits, set through the AFL_TF2_ABL
 // environment variable when building tf2_stamps.hip): skip one piece of work per step to price it
 // (numerics are wrong then; timing only).  Always false in the production kernel.
@@ -424,149 +169,8 @@ enum { ABL_U3 = 1, ABL_UADAM = 2, ABL_UDW = 4, ABL_COLSUM = 8, ABL_HEADUPD = 16,
 #else
 #define ABL(K, b) false
 #endif
-// lr_bc1 / rsqrt_bc2 of step t come from the host-computed table a.kt (torch computes them in double on
-// the host as well); a scalar load per step instead of double-precision division / sqrt on every wave
-__device__ __forceinline__ AdamK adam_k(const AflTfTrainArgs& a, int step) {
-  if (a.opt_mode == 1) return AdamK{a.lr, 0.f, 0.f, 1.f, 1.f};
-  const float* k = a.kt + 2 * (step - 1);
-  return AdamK{k[0], k[1], 1.f, 1.f - fk::B1, fk::EPS};
-}
-// one Adam step of an AGPR-resident weight with its moments m, v (VGPRs, updated in place); v_sqrt_f32
-// (1 ulp) instead of the correctly rounded sqrt expansion: 4x fewer instructions on the update's chain
-__device__ __forceinline__ float adam1(float& pa, float& m, float& v, float g, const AdamK& k) {
-  float p = ar(pa);
-  const float mk = m * k.keep;
-  m = mk + k.c1 * (g - mk);
-  v = fk::B2 * v + (1.f - fk::B2) * g * g;
-  p -= k.lr_bc1 * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) * k.rsqrt_bc2 + k.eps);
-  pa = aw(p);
-  return p;
-}
-// weight matrix W[n][k] (row-major in the flat params at `off`, n_real x k_real) and its LDS image
-struct Mat {
-  int off, n_real, k_real, img, ld;
-};
-// element (n, k) of this lane in tile (T = k tile, T' = n tile): n = 16T' + (lane & 15), k = 16T + 4g + i
-__device__ __forceinline__ void tile_load(TS& s, const Mat& M, int T, int Tn, int lane, const float* P, uchar* smem) {
-  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
-  float h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool ok = n < M.n_real && k0 + i < M.k_real;
-    h[i] = ok ? P[M.off + n * M.k_real + k0 + i] : 0.f;
-    s.p[i] = aw(h[i]);
-  }
-  if (n < 16 * ((M.n_real + 15) / 16))
-    *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
-}
-__device__ __forceinline__ void tile_store(const TS& s, const Mat& M, int T, int Tn, int lane, float* P) {
-  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (n < M.n_real && k0 + i < M.k_real) P[M.off + n * M.k_real + k0 + i] = ar(s.p[i]);
-}
-// Adam on the tile's real elements with gradient acc (= dW^T tile) and moments m, v, new bf16 values -> image
-__device__ __forceinline__ void tile_adam(TS& s, f4v& m, f4v& v, const Mat& M, int T, int Tn, int lane, f4v acc,
-                                          const AdamK& K, uchar* smem) {
-  const int n = 16 * Tn + (lane & 15), k0 = 16 * T + 4 * (lane >> 4);
-  float h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool ok = n < M.n_real && k0 + i < M.k_real;
-    float mi = m[i], vi = v[i];
-    h[i] = ok ? adam1(s.p[i], mi, vi, acc[i], K) : 0.f;
-    m[i] = mi;
-    v[i] = vi;
-  }
-  if (n < 16 * ((M.n_real + 15) / 16))
-    *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
-}
 
-// -------------------------------------------------------------------------- cross-workgroup hand-off
-__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t rs, int off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1: write-through
-}
-__device__ __forceinline__ u32x4 ld_wt(__amdgpu_buffer_rsrc_t rs, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
-}
-__device__ __forceinline__ void publish(gu32* flag, uint32_t value, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// waits until (*fa >> shift) >= want and (*fb >> shift) >= want; returns *fa, or 0xFFFFFFFF on timeout
-__device__ __forceinline__ uint32_t await(gu32* fa, gu32* fb, uint32_t want, int shift, gu32* tmo, int lane) {
-  uint32_t v = 0;
-  for (long spins = 0;; ++spins) {
-    v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(fa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const uint32_t w =
-        fb == fa ? v : __builtin_amdgcn_readfirstlane(__hip_atomic_load(fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if ((v >> shift) >= want && (w >> shift) >= want) break;
-    if (spins > fk::XWG_MAX_SPINS) {
-      v = 0xFFFFFFFFu;
-      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // payload loads stay below the poll
-  return v;
-}
-constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
-__device__ __forceinline__ gu32* xf(gu32* base, int group, int wave) { return base + (group * 8 + wave) * 32; }
 
-__device__ __forceinline__ void unpack16(const u32x4 (&u)[2], float (&x)[16]) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x[8 * h + 2 * k] = __uint_as_float(u[h][k] << 16);
-      x[8 * h + 2 * k + 1] = __uint_as_float(u[h][k] & 0xFFFF0000u);
-    }
-}
-__device__ __forceinline__ void pack16(const float (&x)[16], u32x4 (&u)[2]) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) u[h][k] = pk2(x[8 * h + 2 * k], x[8 * h + 2 * k + 1]);
-}
-
-// Phase entry: make the lane / wave indices opaque so every LDS address of the phase is recomputed
-// inside it.  Otherwise the compiler hoists the hundreds of per-lane swizzled addresses of the step out
-// of the loop and keeps them live across all phases (spilling the optimizer state to scratch).
-__device__ __forceinline__ void opq(int& lane, int& wave) {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("" : "+v"(lane));
-  asm volatile("" : "+s"(wave));
-  lane &= 63;
-  wave &= 7;
-}
-// sub-phase boundary inside a phase: the scheduler may not move instructions across it (keeps the next
-// sub-phase's LDS loads from being hoisted into this one, which raises register pressure)
-__device__ __forceinline__ void sb() { __builtin_amdgcn_sched_barrier(0); }
-
-// barrier over LDS only (global loads stay in flight, stores are not drained)
-__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// --------------------------------------------------------------------------- batch walk (shared plan)
-struct Walk {
-  int e, b0;  // current epoch, batch start
-};
-// next non-skipped batch at or after (e, b0) (size-1 batches are skipped, client.py:86-87); false = done
-__device__ __forceinline__ bool walk_valid(Walk& w, int nd, int BS, int E) {
-  for (;;) {
-    if (w.b0 >= nd) {
-      ++w.e;
-      w.b0 = 0;
-      if (w.e >= E) return false;
-      continue;
-    }
-    if (min(BS, nd - w.b0) == 1) {
-      w.b0 += BS;
-      continue;
-    }
-    return true;
-  }
-}
 
 // =============================================================================== branch workgroup
 template <int BR>
@@ -663,8 +267,6 @@ __device__ __forceinline__ void br_masks(uint32_t key, int r, int g, uint32_t& m
   mk0 = m1 | (m2 << 16);
   mk1 = matt | (kf << 4);
 }
-__device__ __forceinline__ uint32_t aru(float a) { return __float_as_uint(ar(a)); }
-__device__ __forceinline__ float awu(uint32_t v) { return aw(__uint_as_float(v)); }
 
 template <int BR>
 __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], uint32_t mk0, uint32_t mk1, Saved& sv,
@@ -904,12 +506,6 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   }
 }
 
-// bias gradient = column sums of a dY tile: the dW GEMM with an all-ones X fragment (every row of the
-// 16x16 result equals the sums of the 16 columns of dY tile Tn)
-__device__ __forceinline__ s8v ones8() {
-  const short o = (short)0x3F80;  // bf16 1.0
-  return s8v{o, o, o, o, o, o, o, o};
-}
 
 // compact entry e of branch BR: flat parameter index (or -1), where the new value goes
 template <int BR>
