@@ -86,6 +86,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     extra = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("tf2.hip", "tf2_stamps.hip", "rnn2.hip", "rnn2_stamps.hip")}
     if os.environ.get("AFL_TF2_ABL"):  # diagnostic ablation build of the timed kernel (tools/phase_profile.py)
         extra["tf2_stamps.hip"] = extra["tf2_stamps.hip"] + ["-DTF2_ABL=" + str(int(os.environ["AFL_TF2_ABL"]))]
+    if os.environ.get("AFL_RNN2_ABL"):  # diagnostic ablation build of the stamped RNN trainer
+        extra["rnn2_stamps.hip"] = extra["rnn2_stamps.hip"] + ["-DRNN2_ABL=" + str(int(os.environ["AFL_RNN2_ABL"]))]
     if os.environ.get("AFL_RNN2_DEBUG"):  # diagnostic printf build of the on-chip RNN trainer
         extra["rnn2.hip"] = extra["rnn2.hip"] + ["-DRNN2_" + os.environ["AFL_RNN2_DEBUG"]]
     hosts = sorted(glob.glob(os.path.join(ROOT, "csrc", "*.cpp")) + glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))

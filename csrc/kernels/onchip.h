@@ -273,8 +273,10 @@ __device__ __forceinline__ void mom_st(__amdgpu_buffer_rsrc_t rs, int s, int tid
 }
 // same slab addressing with the (wave-uniform) slot part in the scalar offset: one per-lane address for
 // every slot instead of one per slot (the compiler hoists those out of the step loop and keeps them live)
+// (plain loads: the slab is private to the workgroup, written and read back on the same CU and XCD, so the
+// L1 / L2 copies are the workgroup's own writes — sc1 would send every load past the L2)
 __device__ __forceinline__ f4v slot_ld(__amdgpu_buffer_rsrc_t rs, int s, int tid16) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, tid16, s * NTH * 16, 16));
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, tid16, s * NTH * 16, 0));
 }
 __device__ __forceinline__ void slot_st(__amdgpu_buffer_rsrc_t rs, int s, int tid16, f4v v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, tid16, s * NTH * 16, 0);

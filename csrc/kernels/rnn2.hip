@@ -139,6 +139,15 @@ __device__ __forceinline__ void stamp_fini(Stamp& stp, const AflTfTrainArgs& a, 
   (void)stp; (void)a; (void)smem; (void)tid;
 }
 
+// Ablation switches of the diagnostic build (compile-time RNN2_ABL bits in the stamped build only, set through
+// AFL_RNN2_ABL): skip one piece of work per step to price it (numerics are wrong then; timing only).
+enum { ABL_TADAM = 1, ABL_BIAS = 2, ABL_MOM = 4, ABL_DWMMA = 8 };
+#if defined(RNN2_STAMPS) && defined(RNN2_ABL)
+#define ABL(b) ((RNN2_ABL & (b)) != 0)
+#else
+#define ABL(b) false
+#endif
+
 // ------------------------------------------------------------------------------ gate math
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pkh(float a, float b) {
@@ -149,17 +158,22 @@ __device__ __forceinline__ void unpkh(uint32_t u, float& a, float& b) {
   a = (float)h[0];
   b = (float)h[1];
 }
-__device__ __forceinline__ float sigm(float x) {  // exp2 -> inf / 0 gives exactly 0 / 1; NaN propagates
-  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-LOG2E * x));
-}
-// one GRU unit at h0 = 0: returns h, saves the backward factors (A, Bz) and (Cr, r) as fp16 pairs
-__device__ __forceinline__ float gru_unit(float ar, float az, float an, float bhn, uint32_t& s0, uint32_t& s1) {
-  const float r = sigm(ar), z = sigm(az);
-  const float e = __builtin_amdgcn_exp2f((2.f * LOG2E) * fmaf(r, bhn, an));
-  const float n = fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);  // tanh
-  const float omz = 1.f - z;
-  s0 = pkh(omz * fmaf(-n, n, 1.f), n * z * omz);
-  s1 = pkh(fmaf(-r, r, r), r);
+// two GRU units at h0 = 0 in packed FP32 (the branch is VALU-issue-bound; transcendentals stay scalar):
+// returns h, saves each unit's backward factors (A, Bz) and (Cr, r) as fp16 pairs.  exp2 -> inf / 0 gives
+// exactly 0 / 1 in the sigmoids and +-1 in tanh; NaN propagates.
+__device__ __forceinline__ of2v exp2v(of2v x) { return of2v{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])}; }
+__device__ __forceinline__ of2v rcpv(of2v x) { return of2v{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
+__device__ __forceinline__ of2v gru_unit2(of2v ar, of2v az, of2v an, of2v bhn, uint32_t (&s0)[2], uint32_t (&s1)[2]) {
+  const of2v r = rcpv(1.f + exp2v(ar * -LOG2E)), z = rcpv(1.f + exp2v(az * -LOG2E));
+  const of2v e = exp2v((r * bhn + an) * (2.f * LOG2E));
+  const of2v n = rcpv(1.f + e) * -2.f + 1.f;  // tanh
+  const of2v omz = 1.f - z;
+  const of2v A = omz * (n * -n + 1.f), Bz = n * z * omz, Cr = r * -r + r;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    s0[k] = pkh(A[k], Bz[k]);
+    s1[k] = pkh(Cr[k], r[k]);
+  }
   return omz * n;
 }
 
@@ -260,10 +274,20 @@ __device__ __forceinline__ void gru_fwd(uchar* smem, const s8v* bx, float (&h)[1
                 bin = *(const LDS_AS f4v*)(vb + 256 + o), bhr = *(const LDS_AS f4v*)(vb + 384 + o),
                 bhz = *(const LDS_AS f4v*)(vb + 512 + o), bhn = *(const LDS_AS f4v*)(vb + 640 + o);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; i += 2) {
         const int f = 4 * (2 * d + t) + i;
-        h[f] = gru_unit(acc[t][i] + (bir[i] + bhr[i]), acc[2 + t][i] + (biz[i] + bhz[i]), acc[4 + t][i] + bin[i], bhn[i],
-                        sv[2 * f], sv[2 * f + 1]);
+        const of2v br = of2v{bir[i], bir[i + 1]} + of2v{bhr[i], bhr[i + 1]};
+        const of2v bz = of2v{biz[i], biz[i + 1]} + of2v{bhz[i], bhz[i + 1]};
+        uint32_t s0[2], s1[2];
+        const of2v hv = gru_unit2(of2v{acc[t][i], acc[t][i + 1]} + br, of2v{acc[2 + t][i], acc[2 + t][i + 1]} + bz,
+                                  of2v{acc[4 + t][i], acc[4 + t][i + 1]} + of2v{bin[i], bin[i + 1]},
+                                  of2v{bhn[i], bhn[i + 1]}, s0, s1);
+        h[f] = hv[0];
+        h[f + 1] = hv[1];
+        sv[2 * f] = s0[0];
+        sv[2 * f + 1] = s1[0];
+        sv[2 * f + 2] = s0[1];
+        sv[2 * f + 3] = s1[1];
       }
     }
   }
@@ -283,7 +307,7 @@ __device__ __forceinline__ void sav_ld(__amdgpu_buffer_rsrc_t rsv, int L, int ti
   asm volatile("" : "+v"(tid));
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rsv, 16 * tid, ((L - 1) * 8 + k) * NTH * 16, 16);
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rsv, 16 * tid, ((L - 1) * 8 + k) * NTH * 16, 0);
     sv[4 * k] = u[0];
     sv[4 * k + 1] = u[1];
     sv[4 * k + 2] = u[2];
@@ -411,20 +435,23 @@ __device__ __forceinline__ void bias_cs(uchar* smem, int L, int Tn, int i16, flo
 // dW of layer L (3 or 2) = dG^T X with Adam on this wave's 6 tiles (k tiles Ta + a, n tiles Tn0 + b), one n
 // tile at a time so only two accumulators and one tile pair's moments are live; the moments (moment slab
 // slots mb .. mb + 11) are loaded at the phase start, behind the first n tile's MFMAs.  Then the bias sums.
+// this wave's tile moments of layer L (slab slots mb .. mb + 11), issued ahead of the barrier before its dW phase
+__device__ __forceinline__ void tile_mom_ld(__amdgpu_buffer_rsrc_t rm, int mb, int tid, f4v (&m)[6], f4v (&v)[6]) {
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    m[k] = ABL(ABL_MOM) ? Z4 : slot_ld(rm, mb + k, 16 * tid);
+    v[k] = ABL(ABL_MOM) ? Z4 : slot_ld(rm, mb + 6 + k, 16 * tid);
+  }
+}
 template <int L>
-__device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], __amdgpu_buffer_rsrc_t rm, int mb,
-                                         const AdamK& K, int lane, int wave, int tid) {
+__device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], f4v (&m)[6], f4v (&v)[6],
+                                         __amdgpu_buffer_rsrc_t rm, int mb, const AdamK& K, int lane, int wave, int tid) {
   opq(lane, wave);
   asm volatile("" : "+v"(tid));
   const int i16 = lane & 15, g = lane >> 4;
   const uchar* X = smem + (L == 3 ? B_X3 : B_X2);
   const int Ta = 2 * (wave & 1), Tn0 = 3 * (wave >> 1), d = wave >> 2;
-  f4v m[6], v[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    m[k] = slot_ld(rm, mb + k, 16 * tid);
-    v[k] = slot_ld(rm, mb + 6 + k, 16 * tid);
-  }
   const Mat M = R.mat(L, d);
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
@@ -432,20 +459,24 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
     const uchar* DY = smem + B_DG + (Tn >> 2) * 16384;
     f4v acc0 = Z4, acc1 = Z4;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < (ABL(ABL_DWMMA) ? 0 : 4); ++s) {
       const s8v y = tfrag<TK64>(DY, 32 * s, Tn & 3, lane);
       acc0 = mma(tfrag<TK64>(X, 32 * s, Ta, lane), y, acc0);
       acc1 = mma(tfrag<TK64>(X, 32 * s, Ta + 1, lane), y, acc1);
     }
-    tile_adam(wt[b], m[b], v[b], M, Ta, Tn - 6 * d, lane, acc0, K, smem);
-    tile_adam(wt[3 + b], m[3 + b], v[3 + b], M, Ta + 1, Tn - 6 * d, lane, acc1, K, smem);
-    slot_st(rm, mb + b, 16 * tid, m[b]);
-    slot_st(rm, mb + 6 + b, 16 * tid, v[b]);
-    slot_st(rm, mb + 3 + b, 16 * tid, m[3 + b]);
-    slot_st(rm, mb + 9 + b, 16 * tid, v[3 + b]);
+    if (!ABL(ABL_TADAM)) {
+      tile_adam(wt[b], m[b], v[b], M, Ta, Tn - 6 * d, lane, acc0, K, smem);
+      tile_adam(wt[3 + b], m[3 + b], v[3 + b], M, Ta + 1, Tn - 6 * d, lane, acc1, K, smem);
+    }
+    if (!ABL(ABL_MOM)) {
+      slot_st(rm, mb + b, 16 * tid, m[b]);
+      slot_st(rm, mb + 6 + b, 16 * tid, v[b]);
+      slot_st(rm, mb + 3 + b, 16 * tid, m[3 + b]);
+      slot_st(rm, mb + 9 + b, 16 * tid, v[3 + b]);
+    }
     sb();
   }
-  if ((wave & 1) == 0) {  // one of the two waves that read dG tiles Tn0 .. Tn0 + 2: their column sums
+  if ((wave & 1) == 0 && !ABL(ABL_BIAS)) {  // one of the two waves that read dG tiles Tn0 .. Tn0 + 2: their column sums
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
       const int Tn = Tn0 + b;
@@ -498,12 +529,16 @@ __device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wa
 
 // compact entries, branch-free (tf2.hip U3): gradient from CS or GS, Adam, fp32 -> VEC or bf16 -> layer-1 image;
 // the store descriptors are recomputed here (cheaper than keeping NC of them live through the step)
+__device__ __forceinline__ void compact_mom_ld(__amdgpu_buffer_rsrc_t rm, int tid, f4v (&c)[6]) {
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int k = 0; k < 6; ++k) c[k] = slot_ld(rm, 24 + k, 16 * tid);
+}
 __device__ __forceinline__ void compact_update(uchar* smem, const RB& R, BrState& st, __amdgpu_buffer_rsrc_t rm,
-                                               const AdamK& K, int lane, int tid) {
+                                               const f4v (&c)[6], const AdamK& K, int lane, int tid) {
   asm volatile("" : "+v"(tid));
   lane = tid & 63;
-  const f4v cm0 = slot_ld(rm, 24, 16 * tid), cm1 = slot_ld(rm, 25, 16 * tid), cm2 = slot_ld(rm, 26, 16 * tid);
-  const f4v cv0 = slot_ld(rm, 27, 16 * tid), cv1 = slot_ld(rm, 28, 16 * tid), cv2 = slot_ld(rm, 29, 16 * tid);
+  const f4v cm0 = c[0], cm1 = c[1], cm2 = c[2], cv0 = c[3], cv1 = c[4], cv2 = c[5];
   float mmc[12] = {cm0[0], cm0[1], cm0[2], cm0[3], cm1[0], cm1[1], cm1[2], cm1[3], cm2[0], cm2[1], cm2[2], cm2[3]};
   float vvc[12] = {cv0[0], cv0[1], cv0[2], cv0[3], cv1[0], cv1[1], cv1[2], cv1[3], cv2[0], cv2[1], cv2[2], cv2[3]};
   const int dmy = B_DG + 256 + 4 * lane;
@@ -647,6 +682,8 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     asm volatile(";MARK bwd3");
     layer_bwd<3>(smem, dh, sv.f3, dx, lane, wave);
     stp(3, tid);
+    f4v mm[6], vv[6];
+    tile_mom_ld(rm, 0, tid, mm, vv);
     lds_bar();  // A3: every row's dG3 in LDS, every wave past its use of the W3 image
     {
       uint32_t any = 0;
@@ -656,7 +693,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     }
     stp(4, tid);
     asm volatile(";MARK dw3");
-    layer_dw<3>(smem, R, st.w3, rm, 0, K, lane, wave, tid);
+    layer_dw<3>(smem, R, st.w3, mm, vv, rm, 0, K, lane, wave, tid);
     uint32_t sl[32];
     sav_ld(rsv, 2, tid, sl);
     lds_bar();  // B3: dG tile free
@@ -664,10 +701,11 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     asm volatile(";MARK bwd2");
     layer_bwd<2>(smem, dx, sl, dh, lane, wave);
     sav_ld(rsv, 1, tid, sl);
+    tile_mom_ld(rm, 12, tid, mm, vv);
     lds_bar();  // A2
     stp(6, tid);
     asm volatile(";MARK dw2");
-    layer_dw<2>(smem, R, st.w2, rm, 12, K, lane, wave, tid);
+    layer_dw<2>(smem, R, st.w2, mm, vv, rm, 12, K, lane, wave, tid);
     lds_bar();  // B2: dG tile and the h1 tile free
     stp(7, tid);
     asm volatile(";MARK bwd1");
@@ -686,10 +724,12 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     stp(8, tid);
     asm volatile(";MARK dw1");
     layer1_dw(smem, R.din, lane, wave, tid);
+    f4v cmom[6];
+    compact_mom_ld(rm, tid, cmom);
     lds_bar();  // C: every gradient of the compact entries in CS / GS
     stp(9, tid);
     asm volatile(";MARK u3");
-    compact_update(smem, R, st, rm, K, lane, tid);
+    compact_update(smem, R, st, rm, cmom, K, lane, tid);
     stp(10, tid);
     lds_bar();
     stp(11, tid);

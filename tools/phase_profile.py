@@ -1,4 +1,5 @@
-"""Per-phase wall-clock breakdown of the fused TransformerModel training kernel (workgroup 0).
+"""Per-phase wall-clock breakdown of the fused training kernels (TransformerModel: tf2 / transformer.hip,
+RNNModel: rnn2.hip with --model RNNModel), one stamped workgroup.
 
 Runs one client's local round (default 13500 rows, 5 epochs) with the stamps buffer enabled and prints
 microseconds per phase per step.  Usage: python tools/phase_profile.py [--rows N] [--clients C]
@@ -16,6 +17,7 @@ import torch
 from attackfl_amd.data import synthetic_icu
 from attackfl_amd.fl.trainers import make_plan
 from attackfl_amd.models import ParamLayout, build_model
+from attackfl_amd.ops import rnn as R
 from attackfl_amd.ops import transformer as T
 
 NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G4 ffn0+E4", 4: "F:G5 ffn3+E5 LN2/3",
@@ -30,6 +32,15 @@ NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:bac
           13: "H:dW+Adam", 14: "H:end barrier"}
 
 
+# on-chip RNN trainer (rnn2.hip): branch workgroups and the head
+NAMES_RNN_B = {0: "B:forward (3 GRU layers + LN)", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:LN bwd + layer-3 bwd",
+               4: "B:barrier A3 + abort", 5: "B:dW3+Adam (+bar B3)", 6: "B:layer-2 bwd (+bar A2)",
+               7: "B:dW2+Adam (+bar B2)", 8: "B:layer-1 gate bwd (+bar A1)", 9: "B:dW1 staging (+bar C)",
+               10: "B:compact Adam", 11: "B:end barrier"}
+NAMES_RNN_H = {0: "H:wait branches", 1: "H:fwd+loss+bwd+publish", 2: "H:tiles+bar+loss", 3: "H:dW+Adam",
+               4: "H:end barrier"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=13500)
@@ -38,7 +49,10 @@ def main():
     ap.add_argument("--opt-mode", type=int, default=0, help="1 = SGD test mode (no Adam moments)")
     ap.add_argument("--split", type=int, default=0, help="workgroups per client (1, 2, 3); 0 = auto")
     ap.add_argument("--block", type=int, default=0, help="workgroup whose phases are stamped (-1: 0, 1, 2 in turn)")
+    ap.add_argument("--model", default="TransformerModel")
     args = ap.parse_args()
+    if args.model == "RNNModel":
+        return main_rnn(args)
     blocks = [0, 1, 2] if args.block < 0 else [args.block]
     dev = torch.device("cuda", 0)
     ds = synthetic_icu(60000, seed=3)
@@ -75,6 +89,37 @@ def run(args, dev, rows, order, plan, params, split, used, block):
         if v:
             out["phases_us_per_step"][f"{i:02d} {names.get(i, '?')}"] = round(v * 0.01 / steps, 3)
     print(json.dumps(out, indent=1))
+
+
+def main_rnn(args):
+    blocks = [0, 1, 2] if args.block < 0 else [args.block]
+    dev = torch.device("cuda", 0)
+    ds = synthetic_icu(60000, seed=3)
+    rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1).to(dev)
+    lay = ParamLayout.for_model("RNNModel")
+    params = torch.stack([lay.flatten(build_model("RNNModel", seed=i).state_dict())
+                          for i in range(args.clients)]).to(dev)
+    plan = make_plan(rows.shape[0], [args.rows] * args.clients, args.epochs, torch.Generator().manual_seed(0), "cpu")
+    order = plan.order.to(dev)
+    seeds = list(range(args.clients))
+    R.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, seeds)
+    torch.cuda.synchronize()
+    steps = args.epochs * ((args.rows + 127) // 128)
+    for b in blocks:
+        stamps = torch.zeros(64, dtype=torch.int64, device=dev)
+        stamps[63] = b
+        t0 = time.perf_counter()
+        R.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, seeds, opt_mode=args.opt_mode,
+                        stamps=stamps)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        names = NAMES_RNN_H if b % 3 == 0 else NAMES_RNN_B
+        st = stamps.cpu().tolist()[:63]
+        out = {"model": "RNNModel", "block": b, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps,
+               "us_per_step_wall": wall * 1e6 / steps, "us_per_step_stamped": sum(st) * 0.01 / steps,
+               "phases_us_per_step": {f"{i:02d} {names.get(i, '?')}": round(v * 0.01 / steps, 3)
+                                      for i, v in enumerate(st) if v}}
+        print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
