@@ -58,6 +58,10 @@ class Validation:
             from ..ops.transformer import eval_forward
 
             return eval_forward(flat, self.table.rows)
+        if self.data_name == "ICU" and self.model_name == "RNNModel" and self.device.type == "cuda":
+            from ..ops.rnn import eval_many
+
+            return eval_many(flat[None], self.table.rows)[0]
         if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and self.data_name != "CIFAR10":
             # the layer programs take ICU rows / HAR sequences; images go through the eager model below
             data = self.table.rows if self.data_name == "ICU" else self.table.x
@@ -136,6 +140,13 @@ class Validation:
             return self._finish_image(loss, correct)
         if self.data_name != "ICU":
             raise ValueError(f"Not found test function for data name {self.data_name}")
+        if self.device.type == "cuda" and self.model_name == "RNNModel" and num_client > 0:
+            # every client's generated model in ONE fused launch (rnn2.hip k_rnn2_eval)
+            from ..ops.rnn import eval_many
+
+            flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32).contiguous()
+            out = eval_many(flats, self.table.rows).reshape(-1)
+            return self._finish_icu(out, self._labels().repeat(num_client))
         if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and num_client > 0:
             # every client's generated model through ONE client-batched eval program
             flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32).contiguous()

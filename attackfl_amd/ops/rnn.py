@@ -72,3 +72,10 @@ def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor,
 
     return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, split, stamps),
                   what="fused RNN trainer")
+
+
+def eval_many(params: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """Sigmoid outputs of C RNNModels (``params [C, 97665]``, eval mode) over ``rows [n, 24]`` -> ``[C, n]``:
+    one launch (``rnn2.hip`` ``k_rnn2_eval``)."""
+    p = params if params.dim() == 2 else params[None]
+    return native().rnn_eval_many(p.contiguous(), rows.contiguous())

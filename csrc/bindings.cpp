@@ -423,6 +423,20 @@ std::vector<torch::Tensor> rnn_train(torch::Tensor params, torch::Tensor rows, t
   return fused_train(1, params, rows, order, nd, seeds, epochs, batch, lr, opt_mode, stamps, split, kt);
 }
 
+// eval forward of C RNNModels (params [C, P]) over the same rows -> [C, n]: ONE launch (rnn2.hip)
+torch::Tensor rnn_eval_many(torch::Tensor params, torch::Tensor rows) {
+  check_dev(params, "params", torch::kFloat32);
+  check_dev(rows, "rows", torch::kFloat32);
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == afl_rnn_param_count(), "params must be [C, 97665]");
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) == 24, "rows must be [N, 24]");
+  const int C = params.size(0), n = rows.size(0);
+  auto out = torch::empty({C, n}, rows.options());
+  TORCH_CHECK(afl_rnn2_eval(params.data_ptr<float>(), params.stride(0), C, rows.data_ptr<float>(), n,
+                            out.data_ptr<float>(), cur()) == 0, "rnn_eval launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 // eval forward of C TransformerModels (params [C, P]) over the same rows -> [C, n]; one call, 3 launches per
 // model from C++ (the hyper validation scores every client's generated model)
 torch::Tensor tf_eval_many(torch::Tensor params, torch::Tensor rows) {
@@ -489,6 +503,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,
         py::arg("split") = 3, py::arg("kt") = py::none(), py::arg("stamps") = py::none());
   m.def("rnn_param_count", &afl_rnn_param_count);
+  m.def("rnn_eval_many", &rnn_eval_many, py::arg("params"), py::arg("rows"));
   m.def("tf_eval", &tf_eval);
   m.def("tf_param_count", &afl_tf_param_count);
   m.def("tf_ws_floats", &afl_tf_ws_floats);

@@ -92,6 +92,7 @@ long afl_rnn_ws_floats();
 int afl_rnn2_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_rnn2_train_stamped(const AflTfTrainArgs* a, hipStream_t s);
 long afl_rnn2_ws_floats();
+int afl_rnn2_eval(const float* params, long pstride, int C, const float* rows, int n, float* out, hipStream_t s);
 int afl_rnn_param_count();
 int afl_tf_bf_ushorts();
 int afl_tf_param_count();

@@ -243,16 +243,19 @@ __device__ __forceinline__ uint32_t out_mask(uint32_t key, uint32_t layer, int r
 }
 
 // layer-1 A fragment (K = din <= 16, unpermuted): W[16T + (lane & 15)][4g .. 4g + 3], upper half zero
-__device__ __forceinline__ s8v w1frag(const uchar* smem, int T, int lane) {
-  const s4v lo = *(const LDS_AS s4v*)(smem + B_W1 + (16 * T + (lane & 15)) * LDW1 + 8 * (lane >> 4));
+__device__ __forceinline__ s8v w1frag(const uchar* imgs, int T, int lane) {
+  const s4v lo = *(const LDS_AS s4v*)(imgs + B_W1 + (16 * T + (lane & 15)) * LDW1 + 8 * (lane >> 4));
   return cat44(lo, s4v{0, 0, 0, 0});
 }
 
-// one bidirectional GRU layer of this wave's rows: x (B fragments) -> h (T layout), saved factors
+// one bidirectional GRU layer of this wave's rows: x (B fragments) -> h (T layout), saved factors.
+// imgs: the branch's three weight images (W1 at +B_W1, W2 at +B_W2, W3 at +B_W3); vec: its fp32 VEC block.
+// (The forward-only eval kernel passes a scratch sv; the factor math is then dead code.)
 template <int L>
-__device__ __forceinline__ void gru_fwd(uchar* smem, const s8v* bx, float (&h)[16], uint32_t (&sv)[32], int lane) {
+__device__ __forceinline__ void gru_fwd(const uchar* imgs, const uchar* vec, const s8v* bx, float (&h)[16],
+                                        uint32_t (&sv)[32], int lane) {
   const int g = lane >> 4;
-  const uchar* img = smem + (L == 2 ? B_W2 : B_W3);
+  const uchar* img = imgs + (L == 2 ? B_W2 : B_W3);
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     f4v acc[6];
@@ -260,13 +263,13 @@ __device__ __forceinline__ void gru_fwd(uchar* smem, const s8v* bx, float (&h)[1
     for (int k = 0; k < 6; ++k) {
       const int T = 6 * d + k;
       if constexpr (L == 1) {
-        acc[k] = mma(w1frag(smem, T, lane), bx[0], Z4);
+        acc[k] = mma(w1frag(imgs, T, lane), bx[0], Z4);
       } else {
         acc[k] = mma(wfrag(img, LD64, T, 0, lane), bx[0], Z4);
         acc[k] = mma(wfrag(img, LD64, T, 1, lane), bx[1], acc[k]);
       }
     }
-    const uchar* vb = smem + B_VEC + 4 * v0(L, d);
+    const uchar* vb = vec + 4 * v0(L, d);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int o = 4 * (16 * t + 4 * g);
@@ -323,7 +326,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   {
     const s8v bx[1] = {bfrag_lo(xin)};
     uint32_t s1[32];
-    gru_fwd<1>(smem, bx, h1, s1, lane);
+    gru_fwd<1>(smem, smem + B_VEC, bx, h1, s1, lane);
     sav_st(rsv, 1, tid, s1);
   }
 #pragma unroll
@@ -332,7 +335,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   {
     const s8v bx[2] = {bfrag(h1, 0), bfrag(h1, 1)};
     uint32_t s2[32];
-    gru_fwd<2>(smem, bx, h2, s2, lane);
+    gru_fwd<2>(smem, smem + B_VEC, bx, h2, s2, lane);
     sav_st(rsv, 2, tid, s2);
   }
 #pragma unroll
@@ -340,7 +343,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   sb();
   {
     const s8v bx[2] = {bfrag(h2, 0), bfrag(h2, 1)};
-    gru_fwd<3>(smem, bx, h3, sv.f3, lane);
+    gru_fwd<3>(smem, smem + B_VEC, bx, h3, sv.f3, lane);
   }
   sb();
   // LayerNorm(64) + dropout 0.3
@@ -1055,6 +1058,114 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   }
 }
 
+
+#ifndef RNN2_STAMPS
+// ============================================================================ forward-only evaluation
+// C models over the same rows in ONE launch (validation: every client's generated model in hyper mode).
+// Block (row tile of 128, model c): the fp32 parameters are converted once into the same bf16 images /
+// fp32 vectors the trainer uses (both branches + head resident: 146 KB of LDS), then each wave runs its 16
+// rows through both branches (GRU layers in the T layout, LayerNorm; eval mode: no dropout) and the head.
+constexpr int E_BR = B_W3 + 192 * LD64;          // one branch's images
+constexpr int E_VEC = 2 * E_BR;                  // fp32 [2][1280]
+constexpr int E_HW1 = E_VEC + 2 * B_NVEC * 4;    // fc1 image [32][LD128]
+constexpr int E_HW2 = E_HW1 + 32 * LD128;        // fc2 image [16][LD32]
+constexpr int E_HV = E_HW2 + 16 * LD32;          // fp32 [68] fc1.b | fc2.b | output.w | output.b
+constexpr int E_SMEM = E_HV + H_NVEC * 4;
+static_assert(E_SMEM <= 160 * 1024, "eval LDS budget");
+
+__device__ __forceinline__ void st_bf(uchar* smem, int off, float v) { *(LDS_AS unsigned short*)(smem + off) = fk::f2bf(v); }
+
+__global__ void __launch_bounds__(NTH) k_rnn2_eval(const float* __restrict__ params, long pstride,
+                                                  const float* __restrict__ rows, int n, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const float* P = params + (long)c * pstride;
+#pragma unroll 1
+  for (int br = 0; br < 2; ++br) {
+    const RB R(br);
+    uchar* imgs = smem + br * E_BR;
+    for (int i = tid; i < 192 * 24; i += NTH) {  // layer 1, K = din (zero to the 24-element row stride)
+      const int nn = i / 24, k = i - 24 * nn;
+      st_bf(imgs, B_W1 + nn * LDW1 + 2 * k, k < R.din ? P[R.wih(1, nn / 96) + (nn % 96) * R.din + k] : 0.f);
+    }
+#pragma unroll 1
+    for (int l = 2; l <= 3; ++l)
+      for (int i = tid; i < 192 * 64; i += NTH) {
+        const int nn = i >> 6, k = i & 63;
+        st_bf(imgs, (l == 2 ? B_W2 : B_W3) + nn * LD64 + pcol(k) * 2, P[R.wih(l, nn / 96) + (nn % 96) * 64 + k]);
+      }
+    for (int e = tid; e < B_NVEC; e += NTH) ldsf(smem, E_VEC + br * B_NVEC * 4)[e] = P[R.cmp_param(e)];
+  }
+  for (int i = tid; i < 32 * 128; i += NTH) st_bf(smem, E_HW1 + (i >> 7) * LD128 + pcol(i & 127) * 2, P[FC1_W + i]);
+  for (int i = tid; i < 16 * 32; i += NTH) st_bf(smem, E_HW2 + (i >> 5) * LD32 + pcol(i & 31) * 2, P[FC2_W + i]);
+  if (tid < H_NVEC) ldsf(smem, E_HV)[tid] = tid < HV_N ? P[hvec_param(tid)] : 0.f;
+  __syncthreads();
+
+  const int r = blockIdx.x * 128 + 16 * wave + (lane & 15);
+  const bool valid = r < n;
+  float y[2][16];
+#pragma unroll 1
+  for (int br = 0; br < 2; ++br) {
+    const RB R(br);
+    const uchar* imgs = smem + br * E_BR;
+    const uchar* vec = smem + E_VEC + br * B_NVEC * 4;
+    float xin[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = 4 * g + i;
+      const float v = (valid && col < R.din) ? rows[(long)r * ROWW + R.xoff + col] : 0.f;
+      xin[i] = v == -2.0f ? 0.f : v;
+    }
+    float h1[16], h2[16], h3[16];
+    uint32_t scratch[32];
+    {
+      const s8v bx[1] = {bfrag_lo(xin)};
+      gru_fwd<1>(imgs, vec, bx, h1, scratch, lane);
+    }
+    {
+      const s8v bx[2] = {bfrag(h1, 0), bfrag(h1, 1)};
+      gru_fwd<2>(imgs, vec, bx, h2, scratch, lane);
+    }
+    {
+      const s8v bx[2] = {bfrag(h2, 0), bfrag(h2, 1)};
+      gru_fwd<3>(imgs, vec, bx, h3, scratch, lane);
+    }
+    ln_fwd2(h3);
+    float gm[16], bt[16];
+    vec16(gm, vec + 4 * VL_LNW, g);
+    vec16(bt, vec + 4 * VL_LNB, g);
+    affine2(h3, h3, gm, bt);
+    if (br == 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) y[0][j] = h3[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) y[1][j] = h3[j];
+    }
+  }
+  // head: fc1 (K = 128: vitals tiles 0-3, labs tiles 4-7) + ReLU, fc2 + ReLU, output, sigmoid
+  f4v acc[2] = {Z4, Z4};
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[T] = mma(wfrag(smem + E_HW1, LD128, T, s, lane), bfrag(y[s >> 1], s & 1), acc[T]);
+  float a1[8], b1[8];
+  vec8(b1, smem + E_HV + HV_B1 * 4, g);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a1[4 * t + i] = relu_nan(acc[t][i] + b1[4 * t + i]);
+  const f4v a2 = mma(wfrag(smem + E_HW2, LD32, 0, 0, lane), bfrag(a1, 0), Z4);
+  const f4v b2 = *(const LDS_AS f4v*)(smem + E_HV + (HV_B2 + 4 * g) * 4), wo = *(const LDS_AS f4v*)(smem + E_HV + (HV_WO + 4 * g) * 4);
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dot += relu_nan(a2[i] + b2[i]) * wo[i];
+  const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(smem + E_HV + HV_BO * 4);
+  const float p = __builtin_amdgcn_rcpf(1.f + __expf(-y3));
+  if (valid && g == 0) out[(long)c * n + r] = p;
+}
+#endif
 }  // namespace r2
 
 #ifdef RNN2_STAMPS
@@ -1100,3 +1211,16 @@ int afl_rnn2_train(const AflTfTrainArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(K_RNN2, dim3(3 * a->C), dim3(oc::NTH), r2::SMEM, s, *a);
   return 0;
 }
+
+#ifndef RNN2_STAMPS
+// eval: out [C][n] = sigmoid outputs of C RNNModels (params [C][pstride]) over rows [n][24]
+int afl_rnn2_eval(const float* params, long pstride, int C, const float* rows, int n, float* out, hipStream_t s) {
+  if (C <= 0 || n <= 0) return 0;
+  if (hipFuncSetAttribute((const void*)r2::k_rnn2_eval, hipFuncAttributeMaxDynamicSharedMemorySize, r2::E_SMEM) !=
+      hipSuccess)
+    return -2;
+  hipLaunchKernelGGL(r2::k_rnn2_eval, dim3((n + 127) / 128, C), dim3(oc::NTH), r2::E_SMEM, s, params, pstride, rows, n,
+                     out);
+  return 0;
+}
+#endif

@@ -119,3 +119,21 @@ def test_batch_sizes_and_tiny_clients(gpu):
         assert ok.tolist() == [1, 1, 1] and ok_r.all()
         moved = (ref - params).abs().mean().item()
         assert (dev.cpu() - ref).abs().mean().item() < 0.1 * moved, batch
+
+
+def test_eval_many_matches_eager_model(gpu):
+    """Fused forward-only eval of C models (k_rnn2_eval) against torch's fp32 RNNModel in eval mode (bf16
+    MFMA operands: outputs within 2e-2, mean error far below)."""
+    ds = synthetic_icu(1000, seed=5)
+    n = 333  # not a multiple of the 128-row tile
+    lay = ParamLayout.for_model("RNNModel")
+    models = [build_model("RNNModel", seed=20 + i).eval() for i in range(3)]
+    params = torch.stack([lay.flatten(m.state_dict()) for m in models]).to(gpu)
+    rows = torch.cat([ds.vitals[:n], ds.labs[:n], ds.labels[:n, None]], 1)
+    rows[::7, 2] = -2.0  # masked values
+    out = R.eval_many(params, rows.to(gpu)).cpu()
+    with torch.no_grad():
+        ref = torch.stack([m(rows[:, :7], rows[:, 7:23]).reshape(-1) for m in models])
+    assert out.shape == (3, n)
+    err = (out - ref).abs()
+    assert err.max().item() < 2e-2 and err.mean().item() < 3e-3, (err.max().item(), err.mean().item())
