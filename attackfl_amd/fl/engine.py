@@ -511,6 +511,7 @@ class FLEngine:
         mode = self.mode
         if mode == "hyper":
             ups = {i: U[k] for k, i in enumerate(self.selected)}
+            self.ckpt_writer.fence()  # the previous round's checkpoint copy of the arena, updated in place below
             self.hyper.train(self.selected, ups)
             info.update(self.hyper.last_info)
             return info

@@ -7,6 +7,10 @@ the tensors device -> pinned host on the current stream (an async DMA, ordered a
 produced them), and one background thread waits for the copy and writes the file atomically (``.tmp`` +
 ``os.replace``), so a reader never sees a half-written checkpoint.
 
+The device -> host copy runs on a side stream (``fence`` makes the compute stream wait for it before a
+submitted tensor is overwritten in place): on the compute stream the copy of a hypernetwork arena (tens of
+MB, a blit kernel) sat in front of the next round's training launch.
+
 Latest-wins coalescing: two pinned staging slots per key; a ``submit`` that arrives while a write is in
 flight replaces any write that has not started yet (only the newest state matters), so a round never
 waits for the disk.  The file therefore always holds a complete checkpoint of a finished round, at most
@@ -33,6 +37,8 @@ class CheckpointWriter:
         self._thread: Optional[threading.Thread] = None
         self._stop = False
         self.dropped = 0               # superseded writes (diagnostics)
+        self._stream = None            # side stream of the device -> host copies
+        self._copied = None            # event: the last copy has read its source
 
     def _host(self, key: str, slot: int, src: torch.Tensor) -> torch.Tensor:
         """Pinned host staging buffer for ``src`` (reused across rounds)."""
@@ -56,15 +62,27 @@ class CheckpointWriter:
                 self.dropped += 1
             slot = 1 if self._writing == (key, 0) else 0
         host = self._host(key, slot, src)
-        host.copy_(src, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=src.device)
+        self._stream.wait_stream(torch.cuda.current_stream(src.device))  # src as produced so far
+        with torch.cuda.stream(self._stream):
+            host.copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        src.record_stream(self._stream)  # the allocator keeps src's memory until the copy has run
+        self._copied = ev
         with self._cv:
             self._pending = (key, slot, build, path, ev)
             if self._thread is None:
                 self._thread = threading.Thread(target=self._run, name="afl-ckpt", daemon=True)
                 self._thread.start()
             self._cv.notify_all()
+
+    def fence(self) -> None:
+        """Make the current stream wait (on the device, no host sync) until the last submitted copy has
+        read its source: call before overwriting a submitted tensor in place."""
+        if self._copied is not None:
+            torch.cuda.current_stream().wait_event(self._copied)
 
     def _run(self) -> None:
         while True:
