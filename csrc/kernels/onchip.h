@@ -361,6 +361,70 @@ __device__ __forceinline__ void tile_adam(TS& s, f4v& m, f4v& v, const Mat& M, i
   if (n < 16 * ((M.n_real + 15) / 16))
     *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(h[0], h[1]), pk2(h[2], h[3])};
 }
+// Adam on a PAIR of tiles in explicit stages (all weights read, packed m / v updates, all square roots, all
+// reciprocals, all weights written): eight independent element chains in flight, so the transcendental
+// latencies overlap (element by element the sqrt -> rcp -> fma chain serialised).  Tiles whose elements are
+// all real (n_real / k_real multiples of 16 covering them): no per-element masks.
+__device__ __forceinline__ void tile_adam_pair(TS& s0, TS& s1, f4v& m0, f4v& v0, f4v& m1, f4v& v1, const Mat& M, int T0,
+                                               int T1, int Tn, int lane, f4v g0, f4v g1, const AdamK& K,
+                                               uchar* smem) {
+  float p[8], mm[8], vv[8], g[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = ar(s0.p[i]);
+    p[4 + i] = ar(s1.p[i]);
+    mm[i] = m0[i]; mm[4 + i] = m1[i];
+    vv[i] = v0[i]; vv[4 + i] = v1[i];
+    g[i] = g0[i]; g[4 + i] = g1[i];
+  }
+  float den[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float mk = mm[i] * K.keep;
+    mm[i] = mk + K.c1 * (g[i] - mk);
+    vv[i] = fk::B2 * vv[i] + (1.f - fk::B2) * g[i] * g[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) den[i] = __builtin_amdgcn_sqrtf(vv[i]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) den[i] = __builtin_amdgcn_rcpf(den[i] * K.rsqrt_bc2 + K.eps);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p[i] -= K.lr_bc1 * mm[i] * den[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s0.p[i] = aw(p[i]);
+    s1.p[i] = aw(p[4 + i]);
+    m0[i] = mm[i]; m1[i] = mm[4 + i];
+    v0[i] = vv[i]; v1[i] = vv[4 + i];
+  }
+  const int n = 16 * Tn + (lane & 15), g4 = 4 * (lane >> 4);
+  *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(16 * T0 + g4) * 2) = u32x2v{pk2(p[0], p[1]), pk2(p[2], p[3])};
+  *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(16 * T1 + g4) * 2) = u32x2v{pk2(p[4], p[5]), pk2(p[6], p[7])};
+}
+
+// Adam on N independent entries in the same stages as tile_adam_pair (AGPR weights pa[], moments in place,
+// gradients g[]); returns the new weights in pn[]
+template <int N>
+__device__ __forceinline__ void adam_staged(VS (&pa)[N], float (&m)[N], float (&v)[N], const float (&g)[N],
+                                            float (&pn)[N], const AdamK& K) {
+  float den[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    pn[i] = ar(pa[i].p);
+    const float mk = m[i] * K.keep;
+    m[i] = mk + K.c1 * (g[i] - mk);
+    v[i] = fk::B2 * v[i] + (1.f - fk::B2) * g[i] * g[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_sqrtf(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_rcpf(den[i] * K.rsqrt_bc2 + K.eps);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    pn[i] -= K.lr_bc1 * m[i] * den[i];
+    pa[i].p = aw(pn[i]);
+  }
+}
 
 // -------------------------------------------------------------------------- cross-workgroup hand-off
 __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t rs, int off, u32x4 v) {

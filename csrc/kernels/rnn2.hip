@@ -467,10 +467,9 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
       acc0 = mma(tfrag<TK64>(X, 32 * s, Ta, lane), y, acc0);
       acc1 = mma(tfrag<TK64>(X, 32 * s, Ta + 1, lane), y, acc1);
     }
-    if (!ABL(ABL_TADAM)) {
-      tile_adam(wt[b], m[b], v[b], M, Ta, Tn - 6 * d, lane, acc0, K, smem);
-      tile_adam(wt[3 + b], m[3 + b], v[3 + b], M, Ta + 1, Tn - 6 * d, lane, acc1, K, smem);
-    }
+    if (!ABL(ABL_TADAM))  // (the 96 x 64 direction blocks are tile-exact: no element masks)
+      tile_adam_pair(wt[b], wt[3 + b], m[b], v[b], m[3 + b], v[3 + b], M, Ta, Ta + 1, Tn - 6 * d, lane, acc0, acc1, K,
+                     smem);
     if (!ABL(ABL_MOM)) {
       slot_st(rm, mb + b, 16 * tid, m[b]);
       slot_st(rm, mb + 6 + b, 16 * tid, v[b]);
@@ -545,17 +544,25 @@ __device__ __forceinline__ void compact_update(uchar* smem, const RB& R, BrState
   float mmc[12] = {cm0[0], cm0[1], cm0[2], cm0[3], cm1[0], cm1[1], cm1[2], cm1[3], cm2[0], cm2[1], cm2[2], cm2[3]};
   float vvc[12] = {cv0[0], cv0[1], cv0[2], cv0[3], cv1[0], cv1[1], cv1[2], cv1[3], cv2[0], cv2[1], cv2[2], cv2[3]};
   const int dmy = B_DG + 256 + 4 * lane;
+  float gr[NC], mh[NC], vh[NC], pn[NC];
 #pragma unroll
   for (int h = 0; h < NC; ++h) {
     const int e = tid + NTH * h;
-    const uint32_t dd = R.cmp_dst(e, lane);
     const bool vec = e < B_NVEC;
-    const float gr = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
-    const float pn = adam1(st.cmp[h].p, mmc[h], vvc[h], gr, K);
+    gr[h] = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
+    mh[h] = mmc[h];
+    vh[h] = vvc[h];
+  }
+  adam_staged<NC>(st.cmp, mh, vh, gr, pn, K);
+#pragma unroll
+  for (int h = 0; h < NC; ++h) {
+    const uint32_t dd = R.cmp_dst(tid + NTH * h, lane);
     const bool f32 = dd >> 31;
     const int off = (int)(dd & 0x7FFFFFFFu);
-    *(LDS_AS float*)(smem + (f32 ? off : dmy)) = pn;
-    *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 256 : off)) = fk::f2bf(pn);
+    *(LDS_AS float*)(smem + (f32 ? off : dmy)) = pn[h];
+    *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 256 : off)) = fk::f2bf(pn[h]);
+    mmc[h] = mh[h];
+    vvc[h] = vh[h];
   }
   slot_st(rm, 24, 16 * tid, f4v{mmc[0], mmc[1], mmc[2], mmc[3]});
   slot_st(rm, 25, 16 * tid, f4v{mmc[4], mmc[5], mmc[6], mmc[7]});

@@ -635,11 +635,10 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     }
     const Mat M = B::vo(lo);
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        if (!ABL(K, ABL_UADAM))
-          tile_adam(st.blk[2 * a + b], bm[2 * a + b], bv[2 * a + b], M, Ta + a, Tb + b, lane, acc[a][b], K, smem);
+    for (int b = 0; b < 2; ++b)  // the two k tiles of n tile Tb + b in one staged pass (64 x 64: tile-exact)
+      if (!ABL(K, ABL_UADAM))
+        tile_adam_pair(st.blk[b], st.blk[2 + b], bm[b], bv[b], bm[2 + b], bv[2 + b], M, Ta, Ta + 1, Tb + b, lane,
+                       acc[0][b], acc[1][b], K, smem);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       mom_st(rm, k, tid, bm[k]);
@@ -688,18 +687,24 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
   float mm[NCMP] = {cm[0], cm[1], cm[2], cm[3], cmv[0]}, vv[NCMP] = {cv[0], cv[1], cv[2], cv[3], cmv[1]};
   if (!ABL(K, ABL_U3)) {
     const int dmy = B_DF0 + 4 * (tid & 63);
+    float gr[NCMP], pn[NCMP];
+#pragma unroll
+    for (int h = 0; h < NCMP; ++h) {
+      const int e = tid + NTH * h;
+      const bool vec = e < B_NVEC;  // gradient in CS (bias / LayerNorm sums) or GS (staged small dW)
+      gr[h] = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
+    }
+    adam_staged<NCMP>(st.cmp, mm, vv, gr, pn, K);
 #pragma unroll
     for (int h = 0; h < NCMP; ++h) {
       const int e = tid + NTH * h;
       const uint32_t d = aru(st.dst[h]);
-      const bool vec = e < B_NVEC;  // gradient in CS (bias / LayerNorm sums) or GS (staged small dW)
-      const float gr = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
-      const float pn = adam1(st.cmp[h].p, mm[h], vv[h], gr, K);
+      const bool vec = e < B_NVEC;
       const bool f32 = d >> 31;
       const int off = (int)(d & 0x7FFFFFFFu);
       *(LDS_AS float*)(smem + (vec ? B_CS + 4 * e : dmy)) = 0.f;
-      *(LDS_AS float*)(smem + (f32 ? off : dmy + 256)) = pn;
-      *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn);
+      *(LDS_AS float*)(smem + (f32 ? off : dmy + 256)) = pn[h];
+      *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn[h]);
     }
   }
   mom_st(rm, 8, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
