@@ -456,17 +456,33 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
   const uchar* X = smem + (L == 3 ? B_X3 : B_X2);
   const int Ta = 2 * (wave & 1), Tn0 = 3 * (wave >> 1), d = wave >> 2;
   const Mat M = R.mat(L, d);
+  // bias sums of the three dG tiles this wave pair reads, MFMAs against an all-ones operand fused into the dW
+  // loop (the dG fragment is already in registers): the even wave takes n tiles 0, 1, the odd wave tile 2
+  const bool odd = (wave & 1) != 0;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     const int Tn = Tn0 + b;
     const uchar* DY = smem + B_DG + (Tn >> 2) * 16384;
-    f4v acc0 = Z4, acc1 = Z4;
+    const bool bias = !ABL(ABL_BIAS) && (b == 2 ? odd : !odd);
+    f4v acc0 = Z4, acc1 = Z4, bs = Z4;
+    // fragments of k-step s + 1 issued before the MFMAs of k-step s (double-buffered)
+    s8v y[2], x0[2], x1[2];
+    y[0] = tfrag<TK64>(DY, 0, Tn & 3, lane);
+    x0[0] = tfrag<TK64>(X, 0, Ta, lane);
+    x1[0] = tfrag<TK64>(X, 0, Ta + 1, lane);
 #pragma unroll
     for (int s = 0; s < (ABL(ABL_DWMMA) ? 0 : 4); ++s) {
-      const s8v y = tfrag<TK64>(DY, 32 * s, Tn & 3, lane);
-      acc0 = mma(tfrag<TK64>(X, 32 * s, Ta, lane), y, acc0);
-      acc1 = mma(tfrag<TK64>(X, 32 * s, Ta + 1, lane), y, acc1);
+      const int c = s & 1, n = c ^ 1;
+      if (s < 3) {
+        y[n] = tfrag<TK64>(DY, 32 * (s + 1), Tn & 3, lane);
+        x0[n] = tfrag<TK64>(X, 32 * (s + 1), Ta, lane);
+        x1[n] = tfrag<TK64>(X, 32 * (s + 1), Ta + 1, lane);
+      }
+      acc0 = mma(x0[c], y[c], acc0);
+      acc1 = mma(x1[c], y[c], acc1);
+      if (bias) bs = mma(ones8(), y[c], bs);
     }
+    if (bias && g == 0) bias_cs(smem, L, Tn, i16, bs[0]);
     if (!ABL(ABL_TADAM))  // (the 96 x 64 direction blocks are tile-exact: no element masks)
       tile_adam_pair(wt[b], wt[3 + b], m[b], v[b], m[3 + b], v[3 + b], M, Ta, Ta + 1, Tn - 6 * d, lane, acc0, acc1, K,
                      smem);
@@ -477,16 +493,6 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
       slot_st(rm, mb + 9 + b, 16 * tid, v[3 + b]);
     }
     sb();
-  }
-  if ((wave & 1) == 0 && !ABL(ABL_BIAS)) {  // one of the two waves that read dG tiles Tn0 .. Tn0 + 2: their column sums
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const int Tn = Tn0 + b;
-      f4v bs = Z4;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) bs = mma(ones8(), tfrag<TK64>(smem + B_DG + (Tn >> 2) * 16384, 32 * s, Tn & 3, lane), bs);
-      if (g == 0) bias_cs(smem, L, Tn, i16, bs[0]);
-    }
   }
 }
 
