@@ -85,3 +85,22 @@ def test_checkpoint_latest_wins(gpu, tmp_path):
     got = torch.load(tmp_path / "x.pth", weights_only=True)["t"]
     assert bool((got == 5.0).all())
     w.close()
+
+
+def test_checkpoint_copy_fenced_against_in_place_update(gpu, tmp_path):
+    """The device -> host copy runs on a side stream: after ``fence()`` an in-place update on the compute
+    stream (the hypernetwork arena's next Adam step) cannot leak into the checkpoint being written."""
+    import torch
+
+    from attackfl_amd.utils.ckpt import CheckpointWriter
+
+    w = CheckpointWriter()
+    src = torch.full((1 << 24,), 1.0, dtype=torch.float32, device="cuda")  # 64 MB: a copy of ~1 ms
+    w.submit("y", src, lambda t: {"t": t.clone()}, str(tmp_path / "y.pth"))
+    w.fence()
+    src.fill_(2.0)
+    w.flush()
+    got = torch.load(tmp_path / "y.pth", weights_only=True)["t"]
+    assert bool((got == 1.0).all())
+    assert bool((src == 2.0).all())
+    w.close()
