@@ -142,6 +142,8 @@ class FLEngine:
         self.seed = int(cfg.engine.get("seed", 0))
         self.ckpt_dir = cfg.engine.get("checkpoint-dir", ".")
         self.ckpt_writer = CheckpointWriter(bool(cfg.engine.get("async-checkpoint", True)))
+        # synchronise after the aggregate so t_aggregate / t_validate are device times (diagnostics only)
+        self.phase_sync = bool(cfg.engine.get("phase-sync", False))
         self._saved_params: Optional[torch.Tensor] = None
         self.max_retries = int(cfg.engine.get("max-retries", 50))
         self.layout = ParamLayout.for_model(self.model_name)
@@ -258,8 +260,9 @@ class FLEngine:
         os.makedirs(self.ckpt_dir, exist_ok=True)
         if self.mode == "hyper":
             hnet = self.hyper.hnet
+            # deferred: the arena's copy is issued after the next training launch (utils/ckpt.py)
             self.ckpt_writer.submit("hyper", hnet.arena, lambda a: hnet.state_dict_of(a, clone=False),
-                                    self._pth(True))
+                                    self._pth(True), defer=True)
         elif self.global_params is not None:
             layout = self.layout
             self.ckpt_writer.submit("global", self.global_params, lambda f: layout.unflatten(f, clone=False),
@@ -309,8 +312,7 @@ class FLEngine:
         if srv.get("genuine_pool") is not None:
             self.genuine_pool = srv["genuine_pool"].to(self.device)
         if self.hyper is not None and "hyper_m" in srv:
-            with torch.no_grad():
-                self.hyper.hnet.arena.copy_(srv["hyper_arena"])
+            self.hyper.load_arena(srv["hyper_arena"])
             self.hyper.m.copy_(srv["hyper_m"])
             self.hyper.v.copy_(srv["hyper_v"])
             self.hyper.step = int(srv["hyper_step"])
@@ -431,7 +433,7 @@ class FLEngine:
         # START parameters of every started client (one batched generate / broadcast copy)
         if started:
             if self.mode == "hyper":
-                start = self.hyper.hnet.generate_many([i for _, i in started])
+                start = self.hyper.generate_many([i for _, i in started])
             else:
                 p = self._start_params(started[0][1])
                 start = None if p is None else p[None, :].expand(len(js), -1)
@@ -458,6 +460,7 @@ class FLEngine:
                              staged=(pseed_d, nd_d) if dev.type == "cuda" else None)
             pending = self.trainer.launch(params, plan, cfg.lr, cfg.batch_size, train_seeds,
                                           seeds_dev=tseed_d if self._dev_seed is not _no_dev_seed else None)
+        self.ckpt_writer.kick()  # last round's deferred checkpoint copy overlaps this round's training
         tp1 = time.perf_counter()
         if attack_jobs:
             # the attackers do not train: their math runs on a side stream while the genuine clients'
@@ -513,7 +516,7 @@ class FLEngine:
             ups = {i: U[k] for k, i in enumerate(self.selected)}
             self.ckpt_writer.fence()  # the previous round's checkpoint copy of the arena, updated in place below
             self.hyper.train(self.selected, ups)
-            info.update(self.hyper.last_info)
+            info["_lazy"] = lambda: self.hyper.last_info  # read after validation: no sync between them
             return info
         if mode == "FLTrust":
             self.global_params = self._fltrust(U)
@@ -604,7 +607,8 @@ class FLEngine:
         snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) else None
         with trace.range("fl/aggregate"):
             info = self._aggregate(U, sizes, attackers, round_ok)
-            self._sync()
+            if self.phase_sync:  # per-phase timings only; otherwise validation queues behind it
+                self._sync()
         if info.get("agg_failed"):
             round_ok = False
         t3 = time.perf_counter()
@@ -619,21 +623,22 @@ class FLEngine:
                 removed = self.detector.step(self.round_no, self.selected, embs)
             if self.validation is not None and round_ok:
                 if self.mode == "hyper":
-                    round_ok, metric = self.validation.test_hyper(self.hyper.hnet, len(self.selected))
+                    round_ok, metric = self.validation.test_hyper(self.hyper, len(self.selected))
                 else:
                     if self.global_params is None:
                         round_ok = False
                     else:
                         round_ok, metric = self.validation.test(self.global_params)
-        ctrl = torch.full((2 + self.n_clients,), -1.0, dtype=torch.float64, device=self.device)
+        ctrl = torch.full((2 + self.n_clients,), -1.0, dtype=torch.float64)
         if self.leader:
             ctrl[0] = 1.0 if round_ok else 0.0
             ctrl[1] = float(len(removed))
             for k, r in enumerate(removed):
                 ctrl[2 + k] = float(r)
-        if self.world > 1:
+        if self.world > 1:  # one host -> device -> all ranks -> host trip; a single rank keeps it on the host
+            ctrl = ctrl.to(self.device)
             self.comm.broadcast_(ctrl, src=0)
-        ctrl = ctrl.cpu()
+            ctrl = ctrl.cpu()
         trace.pop()
         round_ok = bool(ctrl[0] > 0.5)
         removed = [int(ctrl[2 + k]) for k in range(int(ctrl[1]))]
@@ -665,6 +670,9 @@ class FLEngine:
                "n_selected": len(self.selected), "removed": removed}
         if self._attack_info:
             rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
+        lazy = info.pop("_lazy", None)
+        if lazy is not None:
+            info.update(lazy())
         rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list))})
         self.metrics.write(rec)
         self.history.append(rec)

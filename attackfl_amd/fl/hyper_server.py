@@ -41,11 +41,40 @@ class HyperServer:
         self.step = 0
         off_W, _ = self.hnet.slots["W"]
         self.n_small = off_W                      # emb + MLP region [0, off_W)
-        self.last_info: Dict[str, float] = {}
+        self._last_info: Dict[str, float] = {}
+        self._info_dev = None                     # device [2] (grad norm, clip scale) of the last update
+        self._gen_cache = None                    # (client tuple, [n, P]) generated from the current arena
+
+    @property
+    def last_info(self) -> Dict[str, float]:
+        """Grad norm / clip scale of the last client update; read lazily, so the device path enqueues a
+        whole round's update without a host synchronisation (the engine reads it after validation)."""
+        if self._info_dev is not None:
+            last = self._info_dev.double().cpu()
+            self._info_dev = None
+            self._last_info = {"grad_norm": float(last[0]), "clip_scale": float(last[1])}
+        return self._last_info
 
     # ------------------------------------------------------------------------------------------
     def generate(self, i: int) -> torch.Tensor:
         return self.hnet.generate(i)
+
+    def generate_many(self, idxs) -> torch.Tensor:
+        """``hnet.generate_many`` memoised until the arena next changes (``train`` / ``restore`` /
+        ``load_arena``): a round's validation and the next round's START generate the same clients'
+        models from the same hypernetwork state.  The result is shared: callers must not modify it."""
+        key = tuple(int(i) for i in idxs)
+        c = self._gen_cache
+        if c is not None and c[0] == key:
+            return c[1]
+        out = self.hnet.generate_many(key)
+        self._gen_cache = (key, out)
+        return out
+
+    def load_arena(self, arena: torch.Tensor) -> None:
+        with torch.no_grad():
+            self.hnet.arena.copy_(arena)
+        self._gen_cache = None
 
     def embedding(self, i: int) -> torch.Tensor:
         return self.hnet.emb[i].detach().clone()
@@ -55,6 +84,7 @@ class HyperServer:
 
     def restore(self, snap: torch.Tensor) -> None:
         self.hnet.arena.copy_(snap)
+        self._gen_cache = None
 
     # ------------------------------------------------------------------------------------------
     def _mlp_backward(self, i: int, acts, dfeat: torch.Tensor) -> torch.Tensor:
@@ -104,11 +134,12 @@ class HyperServer:
         """One round of the sequential server update over ``selected`` (client order kept).
 
         On GPU the whole round is enqueued by ``ops.hyper_server_update`` (three launches per client,
-        no host synchronisation); on CPU the composite path below is the oracle."""
+        no host synchronisation, ``last_info`` read lazily); on CPU the composite path below is the oracle."""
         h = self.hnet
         selected = list(selected)
         if not selected:
             return
+        self._gen_cache = None
         if self._native_ok():
             rows = [updates[i] for i in selected]
             # the engine hands rows of one gathered matrix; stack only when they are not already views of it
@@ -122,8 +153,7 @@ class HyperServer:
             info = ops.hyper_server_update(h.arena, self.m, self.v, U, urows, selected, self.layout_vec(), self.step,
                                            self.lr, self.clip)
             self.step += len(selected)
-            last = info[-1].double().cpu()  # the round's only host sync
-            self.last_info = {"grad_norm": float(last[0]), "clip_scale": float(last[1])}
+            self._info_dev = info[-1]  # no host sync here (see last_info)
             return
         for i in selected:
             emb, feat, acts = h.features(i)
@@ -143,4 +173,5 @@ class HyperServer:
             ops.adam_step_scaled(h.arena[small], g_small, self.m[small], self.v[small], self.step, self.lr, scale)
             offW, _ = h.slots["W"]
             ops.hyper_adam_outer(h.W, h.b, self.m[offW:], self.v[offW:], delta, feat, self.step, self.lr, scale)
-            self.last_info = {"grad_norm": total, "clip_scale": scale}
+            self._info_dev = None
+            self._last_info = {"grad_norm": total, "clip_scale": scale}

@@ -11,6 +11,13 @@ The device -> host copy runs on a side stream (``fence`` makes the compute strea
 submitted tensor is overwritten in place): on the compute stream the copy of a hypernetwork arena (tens of
 MB, a blit kernel) sat in front of the next round's training launch.
 
+Deferred copies (``submit(..., defer=True)`` + ``kick``): the copy is a blit kernel that holds CUs for
+the ~0.35 ms of a 20 MB arena; issued at the end of a round it delayed the next round's small preparation
+kernels by as much.  A deferred submit only records an event on the compute stream (the state to save);
+``kick`` — called by the engine right after the next training launch, whose few workgroups leave the
+chip idle — issues the side-stream copy ordered after that event.  ``fence`` / ``flush`` / ``close``
+kick first, so a deferred copy can never miss its source.
+
 Latest-wins coalescing: two pinned staging slots per key; a ``submit`` that arrives while a write is in
 flight replaces any write that has not started yet (only the newest state matters), so a round never
 waits for the disk.  The file therefore always holds a complete checkpoint of a finished round, at most
@@ -39,6 +46,7 @@ class CheckpointWriter:
         self.dropped = 0               # superseded writes (diagnostics)
         self._stream = None            # side stream of the device -> host copies
         self._copied = None            # event: the last copy has read its source
+        self._deferred = None          # (key, src, build, path, event on the compute stream) not copied yet
 
     def _host(self, key: str, slot: int, src: torch.Tensor) -> torch.Tensor:
         """Pinned host staging buffer for ``src`` (reused across rounds)."""
@@ -48,13 +56,32 @@ class CheckpointWriter:
             self._bufs[(key, slot)] = buf
         return buf
 
-    def submit(self, key: str, src: torch.Tensor, build: Callable[[torch.Tensor], object], path: str) -> None:
-        """Save ``build(host copy of src)`` to ``path``.  ``src`` may be overwritten right after return."""
+    def submit(self, key: str, src: torch.Tensor, build: Callable[[torch.Tensor], object], path: str,
+               defer: bool = False) -> None:
+        """Save ``build(host copy of src)`` to ``path``.  ``src`` may be overwritten right after return
+        (with ``defer``: only after ``fence`` or ``kick``; the copy is taken of the state as of this call)."""
         src = src.detach()
         if not src.is_cuda or not self.asynchronous:
             self.flush()
             _atomic_save(build(src.cpu() if src.is_cuda else src.clone()), path)
             return
+        if defer:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(src.device))
+            if self._deferred is not None:
+                self.dropped += 1              # superseded before its copy was issued
+            self._deferred = (key, src, build, path, ev)
+            return
+        self._deferred = None
+        self._copy(key, src, build, path, None)
+
+    def kick(self) -> None:
+        """Issue the deferred copy, if any (side stream, ordered after the state it saves)."""
+        d, self._deferred = self._deferred, None
+        if d is not None:
+            self._copy(*d)
+
+    def _copy(self, key, src, build, path, after: Optional[torch.cuda.Event]) -> None:
         with self._cv:
             self._raise()
             if self._pending is not None:      # superseded before it started
@@ -64,7 +91,10 @@ class CheckpointWriter:
         host = self._host(key, slot, src)
         if self._stream is None:
             self._stream = torch.cuda.Stream(device=src.device)
-        self._stream.wait_stream(torch.cuda.current_stream(src.device))  # src as produced so far
+        if after is not None:
+            self._stream.wait_event(after)                                  # src as of the deferred submit
+        else:
+            self._stream.wait_stream(torch.cuda.current_stream(src.device))  # src as produced so far
         with torch.cuda.stream(self._stream):
             host.copy_(src, non_blocking=True)
             ev = torch.cuda.Event()
@@ -81,6 +111,7 @@ class CheckpointWriter:
     def fence(self) -> None:
         """Make the current stream wait (on the device, no host sync) until the last submitted copy has
         read its source: call before overwriting a submitted tensor in place."""
+        self.kick()
         if self._copied is not None:
             torch.cuda.current_stream().wait_event(self._copied)
 
@@ -111,6 +142,7 @@ class CheckpointWriter:
 
     def flush(self) -> None:
         """Wait until the newest submitted checkpoint is on disk (re-raises a write error)."""
+        self.kick()
         with self._cv:
             while self._pending is not None or self._writing is not None:
                 self._cv.wait()

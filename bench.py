@@ -93,6 +93,7 @@ def main() -> int:
         if comm.world > 1:
             comm.barrier()
 
+    eng.phase_sync = bool(args.profile_rounds)
     for _ in range(args.warmup):
         eng.run_round()
     sync()

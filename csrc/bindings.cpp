@@ -201,12 +201,13 @@ void adam_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
 torch::Tensor roc_auc_dev(torch::Tensor scores, torch::Tensor labels) {
   check_dev(scores, "scores", torch::kFloat32);
   check_dev(labels, "labels", torch::kFloat32);
+  TORCH_CHECK(labels.numel() == scores.numel(), "roc_auc: scores / labels size mismatch");
   const int n = scores.numel();
-  auto sorted = scores.sort(/*stable=*/true, /*dim=*/0, /*descending=*/true);
-  auto s = std::get<0>(sorted).contiguous();
-  auto y = labels.index_select(0, std::get<1>(sorted)).contiguous();
+  auto sorted = std::get<0>(scores.sort(/*stable=*/false, /*dim=*/0, /*descending=*/false)).contiguous();
+  auto acc = torch::empty({3}, scores.options().dtype(torch::kInt64));
   auto out = torch::empty({2}, scores.options().dtype(torch::kFloat64));
-  afl_roc_auc_sorted(s.data_ptr<float>(), y.data_ptr<float>(), n, out.data_ptr<double>(), cur());
+  afl_roc_auc(sorted.data_ptr<float>(), scores.data_ptr<float>(), labels.data_ptr<float>(), n,
+              (unsigned long long*)acc.data_ptr<int64_t>(), out.data_ptr<double>(), cur());
   AFL_CHECK_LAUNCH();
   return out;
 }
@@ -445,14 +446,12 @@ torch::Tensor tf_eval_many(torch::Tensor params, torch::Tensor rows) {
   TORCH_CHECK(params.dim() == 2 && params.size(1) == afl_tf_param_count(), "params must be [C, 47693]");
   const int C = params.size(0), n = rows.size(0);
   auto out = torch::empty({C, n}, rows.options());
-  const long bfw = (afl_tf_bf_ushorts() + 1) / 2;
-  auto bf = torch::empty({(long)C * bfw}, params.options());
-  if (n == 0) return out;
-  for (int c = 0; c < C; ++c) {
-    TORCH_CHECK(afl_tf_eval_bf(params.data_ptr<float>() + (long)c * params.size(1),
-                               (unsigned short*)(bf.data_ptr<float>() + (long)c * bfw), rows.data_ptr<float>(), n,
-                               out.data_ptr<float>() + (long)c * n, cur()) == 0, "tf_eval launch failed");
-  }
+  const long bfs = ((long)afl_tf_bf_ushorts() + 63) / 64 * 64;  // per-model bf16 copies, 128-B aligned
+  auto bf = torch::empty({(long)C * bfs / 2}, params.options());
+  if (n == 0 || C == 0) return out;
+  TORCH_CHECK(afl_tf_eval_many(params.data_ptr<float>(), params.stride(0), (unsigned short*)bf.data_ptr<float>(), bfs,
+                               C, rows.data_ptr<float>(), n, out.data_ptr<float>(), cur()) == 0,
+              "tf_eval launch failed");
   AFL_CHECK_LAUNCH();
   return out;
 }

@@ -53,7 +53,8 @@ int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int
                        double* out, hipStream_t st);
 
 // metrics.hip
-void afl_roc_auc_sorted(const float* s, const float* y, int n, double* out, hipStream_t st);
+void afl_roc_auc(const float* sorted, const float* s, const float* y, int n, unsigned long long* acc, double* out,
+                 hipStream_t st);
 
 // transformer.hip (TransformerModel / ICU fused training + eval)
 struct AflTfTrainArgs {
@@ -78,6 +79,9 @@ struct AflTfTrainArgs {
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);
+// C models (params + c * pstride) over the same rows in one launch pair; bf = C * bfstride ushorts of scratch
+int afl_tf_eval_many(const float* params, long pstride, unsigned short* bf, long bfstride, int C, const float* rows,
+                     int n, float* out, hipStream_t s);
 long afl_tf_ws_floats();
 constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lines) + timeout word
 // tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations

@@ -60,6 +60,85 @@ __global__ void __launch_bounds__(256) k_hyper_rows(const float* __restrict__ W,
   }
 }
 
+// float4 variant (H % 4 == 0, H <= 128, 16-B aligned W): no LDS staging.  A half-wave owns one row at a
+// time (lane j holds columns 4j..4j+3 and the matching f in registers), dots reduce inside the half,
+// each lane accumulates its 4 columns of W^T delta in registers; 4 rows per half in flight.
+constexpr int HR4_NT = 512;
+constexpr int HR4_U = 4;
+__global__ void __launch_bounds__(HR4_NT) k_hyper_rows4(const float* __restrict__ W, const float* __restrict__ b,
+                                                        const float* __restrict__ f, const float* __restrict__ u,
+                                                        long P, int H, float* __restrict__ out,
+                                                        float* __restrict__ partial, int pstride) {
+  __shared__ float red[HR4_NT / 64][HR_HMAX];
+  __shared__ float sq[HR4_NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, half = lane >> 5, H4 = H >> 2;
+  const bool act = j < H4;
+  const float4 fv = act ? reinterpret_cast<const float4*>(f)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* W4 = reinterpret_cast<const float4*>(W);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dsq = 0.f;
+  const long nslots = 2L * gridDim.x * (HR4_NT / 64);  // row slots per sweep
+  const long slot = 2L * ((long)blockIdx.x * (HR4_NT / 64) + wv) + half;
+  for (long r0 = slot; r0 < P; r0 += HR4_U * nslots) {
+    float4 w[HR4_U];
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {
+      const long r = r0 + q * nslots;
+      w[q] = (act && r < P) ? W4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {
+      const long r = r0 + q * nslots;
+      float d = w[q].x * fv.x + w[q].y * fv.y + w[q].z * fv.z + w[q].w * fv.w;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (r < P) {
+        float val = d + b[r];
+        if (u) val -= u[r];
+        if (j == 0) {
+          out[r] = val;
+          dsq += val * val;
+        }
+        acc.x += w[q].x * val;
+        acc.y += w[q].y * val;
+        acc.z += w[q].z * val;
+        acc.w += w[q].w * val;
+      }
+    }
+  }
+  if (!u) return;
+  acc.x += __shfl_xor(acc.x, 32, 64);
+  acc.y += __shfl_xor(acc.y, 32, 64);
+  acc.z += __shfl_xor(acc.z, 32, 64);
+  acc.w += __shfl_xor(acc.w, 32, 64);
+  if (half == 0 && act) {
+    red[wv][4 * j] = acc.x;
+    red[wv][4 * j + 1] = acc.y;
+    red[wv][4 * j + 2] = acc.z;
+    red[wv][4 * j + 3] = acc.w;
+  }
+  dsq = wave_sum(dsq);
+  if (lane == 0) sq[wv] = dsq;
+  __syncthreads();
+  if (tid < H) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < HR4_NT / 64; ++k) a += red[k][tid];
+    partial[(long)blockIdx.x * pstride + tid] = a;
+  }
+  if (pstride > H && tid == 0) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < HR4_NT / 64; ++k) a += sq[k];
+    partial[(long)blockIdx.x * pstride + H] = a;
+  }
+}
+
+__device__ __host__ inline bool hyper_rows4_ok(const float* W, const float* f, int H) {
+  return (H & 3) == 0 && H <= HR_HMAX && (((uintptr_t)W | (uintptr_t)f) & 15) == 0;
+}
+
 __global__ void k_hyper_reduce(const float* __restrict__ partial, int nb, int H, float* __restrict__ dfeat) {
   int h = threadIdx.x;
   if (h >= H) return;
@@ -73,7 +152,10 @@ int afl_hyper_nblocks(long P) { return (int)min(256L, (P + HR_ROWS - 1) / HR_ROW
 void afl_hyper_rows(const float* W, const float* b, const float* f, const float* u, long P, int H, float* out,
                     float* partial, float* dfeat, hipStream_t s) {
   int nb = afl_hyper_nblocks(P);
-  hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, b, f, u, P, H, out, partial, H);
+  if (hyper_rows4_ok(W, f, H))
+    hipLaunchKernelGGL(k_hyper_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, b, f, u, P, H, out, partial, H);
+  else
+    hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, b, f, u, P, H, out, partial, H);
   if (u) hipLaunchKernelGGL(k_hyper_reduce, dim3(1), dim3(128), 0, s, partial, nb, H, dfeat);
 }
 
@@ -184,7 +266,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
                                                        float* __restrict__ info, HySmallDesc d, long nmlp,
                                                        float clip, float lr_bc1, float rsqrt_bc2, float b1, float b2,
                                                        float eps) {
-  __shared__ float sm[HS_SMEM];
+  __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];
   __shared__ float acts[HS_LMAX + 1][HS_HMAX];
   __shared__ float dz[HS_LMAX][HS_HMAX];  // dL/d(output of layer l)
   __shared__ float gemb[HS_HMAX];
@@ -197,7 +279,16 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
   if ((base & 3) == 0 && (nmlp & 3) == 0) {
     const float4* src = reinterpret_cast<const float4*>(A + base);
     float4* dst = reinterpret_cast<float4*>(sm);
-    for (long e = tid; e < nmlp / 4; e += HS_NT) dst[e] = src[e];
+    const long n4 = nmlp / 4;
+    for (long e0 = tid; e0 < n4; e0 += 8 * HS_NT) {  // 8 loads in flight per thread
+      float4 t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (e0 + q * HS_NT < n4) t[q] = src[e0 + q * HS_NT];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (e0 + q * HS_NT < n4) dst[e0 + q * HS_NT] = t[q];
+    }
   } else {
     for (long e = tid; e < nmlp; e += HS_NT) sm[e] = A[base + e];
   }
@@ -208,6 +299,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
       const int c = tid >> 3, sub = tid & 7;
       float s = 0.f;
       if (c <= H)
+#pragma unroll 8
         for (int bb = sub; bb < nb; bb += 8) s += partial[(long)bb * P1 + c];
       s = hs_sum8(s);
       if (c <= H && sub == 0) {
@@ -276,6 +368,38 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
       const int din = l == 0 ? E : H;
       const long ow = d.w[l] - base, ob = d.b[l] - base;
       const long nw = (long)H * din;
+      if (((d.w[l] | nw | din | ow) & 3) == 0) {  // float4 moments / params, 4 chunks in flight per thread
+        const long n4 = nw / 4;
+        float4* m4 = reinterpret_cast<float4*>(m + d.w[l]);
+        float4* v4 = reinterpret_cast<float4*>(v + d.w[l]);
+        float4* A4 = reinterpret_cast<float4*>(A + d.w[l]);
+        float4* s4 = reinterpret_cast<float4*>(sm + ow);
+        for (long e0 = tid; e0 < n4; e0 += 4 * HS_NT) {
+          float4 mm[4], vv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (e0 + q * HS_NT < n4) {
+              mm[q] = m4[e0 + q * HS_NT];
+              vv[q] = v4[e0 + q * HS_NT];
+            }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const long e4 = e0 + q * HS_NT;
+            if (e4 >= n4) continue;
+            const int o = (int)(4 * e4 / din), k = (int)(4 * e4 - (long)o * din);
+            const float go = gs * dz[l][o];
+            float4 p = s4[e4];
+            p.x = hs_adam(p.x, go * acts[l][k], mm[q].x, vv[q].x, lr_bc1, rsqrt_bc2, b1, b2, eps);
+            p.y = hs_adam(p.y, go * acts[l][k + 1], mm[q].y, vv[q].y, lr_bc1, rsqrt_bc2, b1, b2, eps);
+            p.z = hs_adam(p.z, go * acts[l][k + 2], mm[q].z, vv[q].z, lr_bc1, rsqrt_bc2, b1, b2, eps);
+            p.w = hs_adam(p.w, go * acts[l][k + 3], mm[q].w, vv[q].w, lr_bc1, rsqrt_bc2, b1, b2, eps);
+            m4[e4] = mm[q];
+            v4[e4] = vv[q];
+            A4[e4] = p;
+            s4[e4] = p;
+          }
+        }
+      } else {
 #pragma unroll 4
       for (long e = tid; e < nw; e += HS_NT) {
         const int o = (int)(e / din), k = (int)(e - (long)o * din);
@@ -286,6 +410,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
         v[ge] = vv;
         A[ge] = p;
         sm[ow + e] = p;
+      }
       }
       for (int o = tid; o < H; o += HS_NT) {
         const long ge = d.b[l] + o;
@@ -371,8 +496,12 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
     const float lr_bc1 = (float)(lr / bc1), rbc2 = (float)(1.0 / sqrt(bc2));
     float* fk = feat + (k & 1) * HS_HMAX;
     float* fn = feat + ((k + 1) & 1) * HS_HMAX;
-    hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta, partial,
-                       H + 1);
+    if (hyper_rows4_ok(W, fk, H))
+      hipLaunchKernelGGL(k_hyper_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta,
+                         partial, H + 1);
+    else
+      hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta, partial,
+                         H + 1);
     hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
                        k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps);
     hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, delta, fk, P, H,

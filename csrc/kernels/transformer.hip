@@ -1113,9 +1113,14 @@ __device__ __forceinline__ void eval_branch(const Ctx& c, const gu16* BF, const 
 }
 }  // namespace
 
-__global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ Pg, const unsigned short* __restrict__ BFg,
+// blockIdx.y = model: params Pg + y * pstride, bf16 copies BFg + y * bfstride, scores out + y * n
+__global__ void __launch_bounds__(NT) k_tf_eval(const float* __restrict__ Pg, long pstride,
+                                                const unsigned short* __restrict__ BFg, long bfstride,
                                                 const float* __restrict__ rows, int n, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Pg += blockIdx.y * pstride;
+  BFg += blockIdx.y * bfstride;
+  out += (long)blockIdx.y * n;
   Ctx c;
   c.smem = smem;
   c.tid = threadIdx.x;
@@ -1164,7 +1169,10 @@ __device__ __forceinline__ void put_copy(const float* P, unsigned short* BF, Mat
     if (mw.wt >= 0) BF[mw.wt + kk * mw.wt_ld + nn] = h;
   }
 }
-__global__ void k_tf_copies(const float* __restrict__ P, unsigned short* __restrict__ BF) {
+__global__ void k_tf_copies(const float* __restrict__ P, long pstride, unsigned short* __restrict__ BF,
+                            long bfstride) {
+  P += blockIdx.y * pstride;
+  BF += blockIdx.y * bfstride;
   put_copy(P, BF, BrC<0>::dense);
   put_copy(P, BF, BrC<0>::vproj);
   put_copy(P, BF, BrC<0>::oproj);
@@ -1207,11 +1215,19 @@ int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s) {
   return 0;
 }
 
-int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s) {
-  hipMemsetAsync(bf, 0, (size_t)BF_TOTAL * 2, s);
-  hipLaunchKernelGGL(k_tf_copies, dim3(32), dim3(256), 0, s, params, bf);
+int afl_tf_eval_many(const float* params, long pstride, unsigned short* bf, long bfstride, int C, const float* rows,
+                     int n, float* out, hipStream_t s) {
+  if (C <= 0 || n <= 0) return 0;
+  if (bfstride < BF_TOTAL) return -1;
+  hipMemsetAsync(bf, 0, (size_t)bfstride * C * 2, s);
+  hipLaunchKernelGGL(k_tf_copies, dim3(32, C), dim3(256), 0, s, params, pstride, bf, bfstride);
   if (hipFuncSetAttribute((const void*)k_tf_eval, hipFuncAttributeMaxDynamicSharedMemorySize, S_TOTAL) != hipSuccess)
     return -2;
-  hipLaunchKernelGGL(k_tf_eval, dim3((n + BM - 1) / BM), dim3(NT), S_TOTAL, s, params, bf, rows, n, out);
+  hipLaunchKernelGGL(k_tf_eval, dim3((n + BM - 1) / BM, C), dim3(NT), S_TOTAL, s, params, pstride,
+                     (const unsigned short*)bf, bfstride, rows, n, out);
   return 0;
+}
+
+int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s) {
+  return afl_tf_eval_many(params, 0, bf, BF_TOTAL, 1, rows, n, out, s);
 }

@@ -114,6 +114,16 @@ def test_roc_auc(gpu):
         assert abs(a - roc_auc_score(y.numpy(), s.numpy())) < 1e-9
 
 
+def test_roc_auc_nan_flag_and_degenerate(gpu):
+    s = torch.tensor([0.3, float("nan"), 0.9, 0.1])
+    y = torch.tensor([0.0, 1.0, 1.0, 0.0])
+    assert ops.roc_auc_checked(s.to(gpu), y.to(gpu))[1] is True
+    auc, nan = ops.roc_auc_checked(torch.tensor([0.2, 0.2, 0.7]).to(gpu), torch.tensor([1.0, 0.0, 1.0]).to(gpu))
+    assert not nan and abs(auc - 0.75) < 1e-12
+    import math
+    assert math.isnan(ops.roc_auc(torch.rand(50).to(gpu), torch.ones(50).to(gpu)))  # one class only
+
+
 def test_adam_flat(gpu):
     g = torch.Generator().manual_seed(0)
     p, gr = torch.randn(1000, generator=g), torch.randn(1000, generator=g)

@@ -20,6 +20,17 @@ def _setup(C, nd, seed=0):
     return rows, params, plan
 
 
+def test_eval_many_matches_single_model_eval(gpu):
+    """Batched eval (grid.y = model, the hyper validation path) vs one launch per model: bit-identical."""
+    from attackfl_amd.ops import native
+    rows, params, _ = _setup(3, [10])
+    pd, rd = params.to(gpu).contiguous(), rows[:1500].to(gpu).contiguous()
+    many = native().tf_eval_many(pd, rd)
+    assert many.shape == (3, 1500)
+    for k in range(3):
+        assert torch.equal(many[k], T.eval_forward(pd[k], rd))
+
+
 def test_eval_forward_matches_reference(gpu):
     rows, params, _ = _setup(1, [10])
     out = T.eval_forward(params[0].to(gpu), rows.to(gpu)).cpu()

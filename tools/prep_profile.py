@@ -37,6 +37,7 @@ def main():
     pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(60)
     print(s.getvalue())
     eng.close()
 
