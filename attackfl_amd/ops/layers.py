@@ -79,14 +79,16 @@ def _rc(M, N):
 
 # ------------------------------------------------------------------------------------------ GEMM
 def bgemm(A, B, C, bias=None, Z=None, G=None, act=0, gact=0, accum=0, splitk=1, alpha=1.0,
-          ctl: Optional[StepCtl] = None, layer: int = 0, p: float = 0.0) -> None:
+          ctl: Optional[StepCtl] = None, layer: int = 0, p: float = 0.0, generic: bool = False) -> None:
     """``C (op)= epi(alpha * A @ B^T)``; A [C,M,K], B [C,N,K], C [C,M,N].
 
     Epilogue order: +bias -> (Z := pre-activation) -> act -> dropout(layer, m, n) -> *act'(G).
-    accum: 0 store, 1 add, 2 atomic add (required when splitk > 1)."""
+    accum: 0 store, 1 add, 2 atomic add (required when splitk > 1).  On the device, K <= 256 / N <= 256
+    shapes with aligned row-major operands take the tall-skinny kernel (k_tsgemm); ``generic`` forces the
+    64x64-tile kernel (k_bgemm) — the tests compare the two."""
     if _nat(A):
         s, sc = _dargs(ctl, p)
-        _native().bgemm(A, B, C, bias, Z, G, act, gact, accum, splitk, alpha, s, sc, layer, p)
+        _native().bgemm(A, B, C, bias, Z, G, act, gact, accum, splitk, alpha, s, sc, layer, p, int(generic))
         return
     v = alpha * torch.bmm(A, B.transpose(1, 2))
     if bias is not None:

@@ -133,6 +133,7 @@ struct AflGemm {
   float alpha;
   AflDrop drop;
   int avec, bvec;  // set by the launcher: operand rows 16-B aligned and k-contiguous
+  int no_ts;       // 1: never take the tall-skinny path (tests compare the two kernels)
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
 

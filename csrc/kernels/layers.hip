@@ -684,12 +684,171 @@ __global__ void k_mean_rows_bwd(const float* __restrict__ dout, long n, int L, f
 inline int launched() { return (int)hipGetLastError(); }
 inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
 
+
+// ============================================================================ tall-skinny GEMM
+// C[c][m][n] (op)= epi(alpha * A[c][m][:K] . B[c][n][:K]) for K = 32 KT <= 256, N = 16 NT <= 256 and any M
+// (the HAR layers: 72k rows per client, d_model 64, FFN 256).  k_bgemm re-stages B per 64x64 tile and
+// writes the output as 4-byte column strips; here
+//   * the whole B operand (<= 32 KB bf16) is staged ONCE per workgroup, rows padded to K+8 (conflict-free
+//     16-B fragment reads);
+//   * each wave streams 16-row tiles of A from global memory straight into MFMA fragments (two dwordx4
+//     per lane per 32-k step: no LDS, no barriers); for K = 64 (PF) it issues the NEXT tile's loads before
+//     this tile's MFMAs, for larger K the registers are worth more as occupancy (measured, tools/gemm_bench.py);
+//   * the fragment reads of B stay inside the tile loop (hoisted they cost 2x the VGPRs and half the
+//     occupancy: 0.25 -> 0.16 ms for the HAR qkv projection when they were moved back);
+//   * it computes D^T = B . A^T, so each lane ends up holding 4 consecutive n of one row m: bias, G and the
+//     output move as float4, the dropout hash pairs (afl_keep) are shared by adjacent n.
+// Persistent: a client's workgroups stride over its row tiles (grid = (blocks per client, C)).
+constexpr int TS_NTH = 256;
+constexpr int TS_WAVES = TS_NTH / 64;
+
+template <int NT, int KT, bool PF>
+__global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
+  constexpr int N = 16 * NT, K = 32 * KT, LDB = K + 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned short Bs[];  // [N][LDB] bf16, then bias [N] fp32
+  float* bias_s = reinterpret_cast<float*>(Bs + N * LDB);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = blockIdx.y;
+  if (tid < N) bias_s[tid] = g.bias ? g.bias[(long)c * g.sbc + tid] : 0.f;
+  {
+    const float* B = g.B + (long)c * g.sBc;
+    if (g.sBk == 1) {
+      for (int e = tid; e < N * K; e += TS_NTH) {
+        const int n = e / K, k = e - n * K;
+        Bs[n * LDB + k] = (unsigned short)(pk_bf2(B[(long)n * g.sBn + k], 0.f) & 0xFFFFu);
+      }
+    } else {  // transposed view (dY.W): n is the contiguous index
+      for (int e = tid; e < N * K; e += TS_NTH) {
+        const int k = e / N, n = e - k * N;
+        Bs[n * LDB + k] = (unsigned short)(pk_bf2(B[(long)n * g.sBn + (long)k * g.sBk], 0.f) & 0xFFFFu);
+      }
+    }
+  }
+  __syncthreads();
+  const float* A = g.A + (long)c * g.sAc;
+  float* Cc = g.Cm + (long)c * g.sCc;
+  const int M = g.M, ntile = (M + 15) / 16, j = lane & 15, q = lane >> 4;
+  const int wstride = gridDim.x * TS_WAVES;
+  const bool dr = g.drop.thr16 != 0;
+  const uint32_t key = dr ? drop_key(g.drop, c) : 0u;
+  f4v xa[KT][2], xn[KT][2];
+  auto load = [&](int t, f4v (&x)[KT][2]) {
+    const int m = 16 * t + j;
+    const bool ok = m < M;
+    const float* p = A + (long)(ok ? m : 0) * g.sAm + 8 * q;
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      x[kk][0] = ok ? *(const f4v*)(p + 32 * kk) : f4v{0.f, 0.f, 0.f, 0.f};
+      x[kk][1] = ok ? *(const f4v*)(p + 32 * kk + 4) : f4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int t = blockIdx.x * TS_WAVES + wave;
+  if (PF && t < ntile) load(t, xa);
+  for (; t < ntile; t += wstride) {
+    if (PF) {
+      if (t + wstride < ntile) load(t + wstride, xn);  // next tile's A in flight during this tile's work
+    } else {
+      load(t, xa);
+    }
+    s8v bx[KT];
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      u4v w;
+      w[0] = pk_bf2(xa[kk][0][0], xa[kk][0][1]);
+      w[1] = pk_bf2(xa[kk][0][2], xa[kk][0][3]);
+      w[2] = pk_bf2(xa[kk][1][0], xa[kk][1][1]);
+      w[3] = pk_bf2(xa[kk][1][2], xa[kk][1][3]);
+      bx[kk] = __builtin_bit_cast(s8v, w);
+    }
+    f4v acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f4v{0.f, 0.f, 0.f, 0.f};
+    int boff = (16 * 0 + j) * LDB + 8 * q;
+    asm volatile("" : "+v"(boff));  // keep the fragment reads in the loop (hoisted, they cost occupancy)
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const s8v wf = *(const s8v*)(Bs + boff + 16 * nt * LDB + 32 * kk);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, wf),
+                                                          __builtin_bit_cast(bf8v, bx[kk]), acc[nt], 0, 0, 0);
+      }
+    // lane holds C[m][16 nt + 4 q + e], e = 0..3
+    const int m = 16 * t + j;
+    if (m < M) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n0 = 16 * nt + 4 * q;
+        f4v v = acc[nt] * g.alpha;
+        if (g.bias) v += *(const f4v*)(bias_s + n0);
+        const long off = (long)m * g.sCm + n0;
+        if (g.Z) *(f4v*)(g.Z + (long)c * g.sCc + off) = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = act_f(v[e], g.act);
+          if (dr) x *= drop_scale(g.drop, key, m, n0 + e);
+          v[e] = x;
+        }
+        if (g.G) {
+          const f4v gv = *(const f4v*)(g.G + (long)c * g.sGc + (long)m * g.sGm + n0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= act_d(gv[e], g.gact);
+        }
+        if (g.accum == 1) v += *(const f4v*)(Cc + off);
+        *(f4v*)(Cc + off) = v;
+      }
+    }
+    if (PF) {
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        xa[kk][0] = xn[kk][0];
+        xa[kk][1] = xn[kk][1];
+      }
+    }
+  }
+}
+
+__host__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// shapes with a k_tsgemm instantiation; anything else (or misaligned / strided operands) takes k_bgemm
+int tsgemm_try(const AflGemm& g, hipStream_t s) {
+  if (g.accum == 2 || g.splitk > 1 || g.sAk != 1 || g.sCn != 1) return -1;
+  if (!al16(g.A) || (g.sAm & 3) || (g.sAc & 3) || !al16(g.Cm) || (g.sCm & 3) || (g.sCc & 3)) return -1;
+  if (g.Z && !al16(g.Z)) return -1;
+  if (g.G && (g.sGn != 1 || !al16(g.G) || (g.sGm & 3) || (g.sGc & 3))) return -1;
+  const void* fn = nullptr;
+  const int key = g.N * 1024 + g.K;
+#define TS_CASE(N_, K_)                                         \
+  case N_ * 1024 + K_:                                          \
+    fn = (const void*)k_tsgemm<N_ / 16, K_ / 32, (K_ <= 64)>;  \
+    break;
+  switch (key) {
+    TS_CASE(64, 64)
+    TS_CASE(128, 64)
+    TS_CASE(192, 64)
+    TS_CASE(256, 64)
+    TS_CASE(64, 128)
+    TS_CASE(64, 192)
+    TS_CASE(64, 256)
+    default:
+      return -1;
+  }
+#undef TS_CASE
+  const int ntile = (g.M + 15) / 16;
+  const int per_client = max(1, min((ntile + TS_WAVES - 1) / TS_WAVES, (4 * 256 + g.nC - 1) / g.nC));
+  const size_t lds = (size_t)g.N * (g.K + 8) * 2 + (size_t)g.N * 4;
+  AflGemm gg = g;
+  void* args[] = {&gg};
+  return (int)hipLaunchKernel(fn, dim3(per_client, g.nC), dim3(TS_NTH), args, lds, s);
+}
+
 }  // namespace
 
 // ============================================================================ host launchers
 int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
   if (g.splitk > 1 && g.accum != 2) return (int)hipErrorInvalidValue;
+  if (!g.no_ts && tsgemm_try(g, s) == 0) return launched();
   const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
   dim3 grid(tiles, max(1, g.splitk), g.nC);
   AflGemm gg = g;  // 16-B aligned k-contiguous rows take the vector-load path

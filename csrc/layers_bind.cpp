@@ -63,7 +63,7 @@ AflDrop make_drop(const c10::optional<torch::Tensor>& seeds, const c10::optional
 void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<torch::Tensor> bias,
            c10::optional<torch::Tensor> Z, c10::optional<torch::Tensor> G, int64_t act, int64_t gact, int64_t accum,
            int64_t splitk, double alpha, c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl,
-           int64_t layer, double p) {
+           int64_t layer, double p, int64_t generic) {
   view3(A, "A");
   view3(B, "B");
   view3(Cm, "C");
@@ -99,6 +99,7 @@ void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<tor
   g.act = act; g.gact = gact; g.accum = accum; g.splitk = std::max<int64_t>(1, splitk);
   g.alpha = (float)alpha;
   g.drop = make_drop(seeds, stepctl, layer, p);
+  g.no_ts = generic ? 1 : 0;
   ok(afl_bgemm(g, cur()), "bgemm");
 }
 
@@ -627,7 +628,7 @@ void afl_register_layers(pybind11::module& m) {
   m.def("bgemm", &bgemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias") = none, py::arg("Z") = none,
         py::arg("G") = none, py::arg("act") = 0, py::arg("gact") = 0, py::arg("accum") = 0, py::arg("splitk") = 1,
         py::arg("alpha") = 1.0, py::arg("seeds") = none, py::arg("stepctl") = none, py::arg("layer") = 0,
-        py::arg("p") = 0.0);
+        py::arg("p") = 0.0, py::arg("generic") = 0);
   m.def("colsum", &colsum);
   m.def("gather_icu", &gather_icu);
   m.def("gather_har", &gather_har);

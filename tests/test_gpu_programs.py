@@ -71,6 +71,35 @@ def test_bgemm_transposed_views_and_splitk(gpu):
     _close(out, torch.bmm(dY, W), name="dX")
 
 
+@pytest.mark.parametrize("N,K,trans", [(192, 64, False), (64, 64, False), (256, 64, False), (64, 256, False),
+                                       (256, 64, True), (64, 192, True), (128, 64, False)])
+def test_tall_skinny_gemm_matches_generic_and_composite(gpu, N, K, trans):
+    """k_tsgemm (B staged once per workgroup, A streamed into fragments, float4 epilogue) vs k_bgemm and the
+    fp32 composite, every epilogue on: bias, Z, relu, dropout, act'(G), accumulate; M not a multiple of 16."""
+    C, M = 3, 1000 + 7
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(C, M, K, generator=g)
+    flat = torch.randn(C, N * K + 64, generator=g) * 0.2
+    W = flat[:, 16:16 + N * K].view(C, K, N).transpose(1, 2) if trans else flat[:, 16:16 + N * K].view(C, N, K)
+    bias, G = torch.randn(C, N, generator=g), torch.randn(C, M, N, generator=g)
+    C0 = torch.randn(C, M, N, generator=g)
+    cg, cc = _ctl(C)
+    outs = []
+    for dev, ctl, generic in ((DEV, cg, False), (DEV, cg, True), ("cpu", cc, False)):
+        Wd = (flat.to(dev)[:, 16:16 + N * K].view(C, K, N).transpose(1, 2) if trans
+              else flat.to(dev)[:, 16:16 + N * K].view(C, N, K))
+        Cm, Z = C0.clone().to(dev), torch.zeros(C, M, N, device=dev)
+        Lx.bgemm(A.to(dev), Wd, Cm, bias=bias.to(dev), Z=Z, G=G.to(dev), act=1, gact=1, accum=1, ctl=ctl, layer=4,
+                 p=0.1, generic=generic)
+        outs.append((Cm, Z))
+    for k, name in ((0, "tsgemm"), (1, "bgemm")):
+        _close(outs[k][0], outs[2][0], name=name + " C")
+        _close(outs[k][1], outs[2][1], name=name + " Z")
+    # the two device kernels share operand rounding (bf16) and accumulate in fp32: near-identical
+    assert (outs[0][1] - outs[1][1]).abs().max().item() < 1e-3 * (outs[1][1].abs().max().item() + 1)
+    del W
+
+
 def test_layernorm_fwd_bwd(gpu):
     C, R = 2, 300
     g = torch.Generator().manual_seed(2)
