@@ -203,9 +203,15 @@ torch::Tensor roc_auc_dev(torch::Tensor scores, torch::Tensor labels) {
   check_dev(labels, "labels", torch::kFloat32);
   TORCH_CHECK(labels.numel() == scores.numel(), "roc_auc: scores / labels size mismatch");
   const int n = scores.numel();
-  auto sorted = std::get<0>(scores.sort(/*stable=*/false, /*dim=*/0, /*descending=*/false)).contiguous();
   auto acc = torch::empty({3}, scores.options().dtype(torch::kInt64));
   auto out = torch::empty({2}, scores.options().dtype(torch::kFloat64));
+  if (n <= afl_roc_auc_pairs_max()) {  // direct pair counts, no sort
+    afl_roc_auc_pairs(scores.data_ptr<float>(), labels.data_ptr<float>(), n,
+                      (unsigned long long*)acc.data_ptr<int64_t>(), out.data_ptr<double>(), cur());
+    AFL_CHECK_LAUNCH();
+    return out;
+  }
+  auto sorted = std::get<0>(scores.sort(/*stable=*/false, /*dim=*/0, /*descending=*/false)).contiguous();
   afl_roc_auc(sorted.data_ptr<float>(), scores.data_ptr<float>(), labels.data_ptr<float>(), n,
               (unsigned long long*)acc.data_ptr<int64_t>(), out.data_ptr<double>(), cur());
   AFL_CHECK_LAUNCH();

@@ -53,6 +53,8 @@ int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int
                        double* out, hipStream_t st);
 
 // metrics.hip
+int afl_roc_auc_pairs_max();
+void afl_roc_auc_pairs(const float* s, const float* y, int n, unsigned long long* acc, double* out, hipStream_t st);
 void afl_roc_auc(const float* sorted, const float* s, const float* y, int n, unsigned long long* acc, double* out,
                  hipStream_t st);
 

@@ -69,6 +69,74 @@ __global__ void k_auc_final(const unsigned long long* __restrict__ acc, int n, d
   out[1] = acc[2] ? 1.0 : 0.0;
 }
 
+// Small n (the validation set of one model, ~10k rows): count the (positive, negative) pairs directly,
+// 2 * #(s_neg < s_pos) + #(s_neg == s_pos) = 2 U, no sort (the sort's ~10 rocprim launches cost more than
+// the n^2 / 2 compares).  Grid (i blocks, j chunks); negatives' scores staged in LDS, positives staged as
+// NaN (compares false).
+constexpr int AUC_PJ = 1024;  // j chunk per workgroup
+__global__ void __launch_bounds__(AUC_T) k_auc_pairs(const float* __restrict__ s, const float* __restrict__ y, int n,
+                                                     unsigned long long* __restrict__ acc) {
+  __shared__ float sj[AUC_PJ];
+  __shared__ unsigned long long red[3][AUC_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = blockIdx.y * AUC_PJ, jn = min(AUC_PJ, n - j0);
+  for (int e = tid; e < jn; e += AUC_T) {
+    const float v = s[j0 + e];
+    sj[e] = y[j0 + e] > 0.5f ? __builtin_nanf("") : v;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * AUC_T + tid;
+  unsigned long long t = 0, p = 0, nn = 0;
+  if (i < n) {
+    const float v = s[i];
+    const bool pos = y[i] > 0.5f;
+    if (blockIdx.y == 0) {
+      p = pos ? 1 : 0;
+      nn = v != v ? 1 : 0;
+    }
+    if (pos && v == v) {
+      unsigned lt = 0, eq = 0;
+#pragma unroll 8
+      for (int e = 0; e < jn; ++e) {
+        const float u = sj[e];
+        lt += u < v ? 1u : 0u;
+        eq += u == v ? 1u : 0u;
+      }
+      t = 2ull * lt + eq;
+    }
+  }
+  t = wave_sum(t);
+  p = wave_sum(p);
+  nn = wave_sum(nn);
+  if (lane == 0) {
+    red[0][w] = t;
+    red[1][w] = p;
+    red[2][w] = nn;
+  }
+  __syncthreads();
+  if (tid < 3) {
+    unsigned long long a = 0;
+    for (int k = 0; k < AUC_T / 64; ++k) a += red[tid][k];
+    if (a) atomicAdd(acc + tid, a);
+  }
+}
+
+__global__ void k_auc_final_pairs(const unsigned long long* __restrict__ acc, int n, double* __restrict__ out) {
+  const double P = (double)acc[1], N = (double)n - P;
+  out[0] = (P > 0 && N > 0) ? (double)acc[0] / (2.0 * P * N) : __longlong_as_double(0x7ff8000000000000ll);
+  out[1] = acc[2] ? 1.0 : 0.0;
+}
+
+int afl_roc_auc_pairs_max() { return 32768; }
+
+void afl_roc_auc_pairs(const float* s, const float* y, int n, unsigned long long* acc, double* out, hipStream_t st) {
+  hipMemsetAsync(acc, 0, 3 * sizeof(unsigned long long), st);
+  if (n > 0)
+    hipLaunchKernelGGL(k_auc_pairs, dim3((n + AUC_T - 1) / AUC_T, (n + AUC_PJ - 1) / AUC_PJ), dim3(AUC_T), 0, st, s, y,
+                       n, acc);
+  hipLaunchKernelGGL(k_auc_final_pairs, dim3(1), dim3(1), 0, st, acc, n, out);
+}
+
 void afl_roc_auc(const float* sorted, const float* s, const float* y, int n, unsigned long long* acc, double* out,
                  hipStream_t st) {
   hipMemsetAsync(acc, 0, 3 * sizeof(unsigned long long), st);

@@ -106,7 +106,7 @@ def test_roc_auc(gpu):
     from sklearn.metrics import roc_auc_score
 
     g = torch.Generator().manual_seed(0)
-    for n in (10, 1000, 5000, 80000):
+    for n in (10, 1000, 5000, 32768, 32769, 80000):  # <= 32768: pair counts, above: rank sums after a sort
         y = (torch.rand(n, generator=g) < 0.3).float()
         s = torch.rand(n, generator=g) + y * 0.3
         s = (s * 50).round() / 50  # many ties
