@@ -100,6 +100,36 @@ def test_tall_skinny_gemm_matches_generic_and_composite(gpu, N, K, trans):
     del W
 
 
+@pytest.mark.parametrize("P,skip", [(1024, (5, 518)), (1003, (0, 0)), (1024, (0, 0))])
+@pytest.mark.parametrize("sgd", [0.0, 0.05])
+def test_adam_clients_vector_and_scalar_paths(gpu, P, skip, sgd):
+    """k_adam_clients: float4 path (P % 4 == 0, a skip range straddling float4 groups) and scalar path vs
+    the composite, 3 steps, one inactive client, gradients zeroed on the device as they are consumed."""
+    C = 3
+    g = torch.Generator().manual_seed(4)
+    p0, grads = torch.randn(C, P, generator=g), [torch.randn(C, P, generator=g) for _ in range(3)]
+    bsz = torch.tensor([[8, 8, 1]] * 3, dtype=torch.int32)  # client 2: batch of 1 -> inactive
+    res = []
+    for dev in (DEV, "cpu"):
+        ctl = Lx.StepCtl.create([1, 2, 3], dev)
+        p, m, v = p0.clone().to(dev), torch.zeros(C, P, device=dev), torch.zeros(C, P, device=dev)
+        tcount = torch.zeros(C, dtype=torch.int32, device=dev)
+        failed = torch.zeros(C, dtype=torch.int32, device=dev)
+        gr = torch.zeros(C, P, device=dev)
+        for s in range(3):
+            if dev == "cpu":
+                gr.copy_(grads[s])
+            else:
+                gr += grads[s].to(dev)  # zeroed by the previous step's Adam (inactive client accumulates)
+            Lx.adam_clients(p, gr, m, v, tcount, bsz.to(dev), ctl, failed, 1e-2, skip, sgd, zero_grads=dev != "cpu")
+            Lx.step_end(ctl, tcount, bsz.to(dev), failed)
+        res.append(p.cpu())
+    assert torch.allclose(res[0][:2], res[1][:2], rtol=1e-5, atol=1e-6)
+    assert torch.equal(res[0][2], p0[2])  # inactive client untouched
+    if skip[1] > skip[0]:
+        assert torch.equal(res[0][:, skip[0]:skip[1]], p0[:, skip[0]:skip[1]])
+
+
 def test_layernorm_fwd_bwd(gpu):
     C, R = 2, 300
     g = torch.Generator().manual_seed(2)
