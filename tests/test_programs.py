@@ -100,6 +100,37 @@ def test_step_tables_skip_and_padding():
     assert idx[2, 0, 0] == 8 and (idx[2, 0, 1:] == -1).all()
 
 
+def _step_tables_loop(order, nd, epochs, B):
+    """The per-batch loop form of step_tables (the oracle of the vectorised one)."""
+    C = order.shape[0]
+    nbat = [max(1, -(-int(n) // B)) for n in nd]
+    S = max([epochs * n for n in nbat] + [0])
+    idx = torch.full((S, C, B), -1, dtype=torch.int32)
+    bsz = torch.zeros(S, C, dtype=torch.int32)
+    ep = torch.zeros(S, C, dtype=torch.int32)
+    for c in range(C):
+        s = 0
+        for e in range(epochs):
+            for j in range(nbat[c]):
+                a, b = j * B, min(int(nd[c]), (j + 1) * B)
+                idx[s, c, :b - a] = order[c, e, a:b]
+                bsz[s, c] = b - a
+                ep[s, c] = e
+                s += 1
+    return idx, bsz, ep, S
+
+
+@pytest.mark.parametrize("nd,epochs,B", [([33, 17, 1, 128], 3, 16), ([129, 128, 2], 2, 128), ([5], 1, 8), ([0, 7], 2, 4)])
+def test_step_tables_match_loop_form(nd, epochs, B):
+    g = torch.Generator().manual_seed(9)
+    maxnd = max(max(nd), 1)
+    order = torch.stack([torch.stack([torch.randperm(300, generator=g)[:maxnd] for _ in range(epochs)])
+                         for _ in nd]).to(torch.int32)
+    idx, bsz, ep, nb, S = step_tables(order, nd, epochs, B, "cpu")
+    ri, rb, re, rS = _step_tables_loop(order, nd, epochs, B)
+    assert S == rS and torch.equal(idx, ri) and torch.equal(bsz, rb) and torch.equal(ep, re)
+
+
 def test_adam_dropout_training_runs_and_nan_fails():
     name = "CNNModel"
     C, B = 2, 16
