@@ -718,7 +718,7 @@ int afl_cnn_towers_fwd(const AflCnnTowers& a, hipStream_t s) {
     attr = true;
   }
   const int nt = max(a.br[0].ntiles, a.br[1].ntiles);
-  hipLaunchKernelGGL(k_cnn_wimg, dim3(8, 2, a.C), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_cnn_wimg, dim3(32, 2, a.C), dim3(256), 0, s, a);  // 8 -> 32: latency-bound scattered stores
   hipLaunchKernelGGL(k_cnn_fwd, dim3(nt, 2, a.C), dim3(NT), F_TOTAL, s, a);
   return (int)hipGetLastError();
 }

@@ -572,82 +572,79 @@ __global__ void __launch_bounds__(256) k_ce(const float* __restrict__ logits, co
 }
 
 // ============================================================================ optimizer
-// VEC: 4 consecutive entries per thread (P % 4 == 0: every client row 16-B aligned), float4 streams; the
-// per-element arithmetic is unchanged (same bits as the scalar form), the bias corrections are computed
-// once per thread instead of once per element.
-template <bool VEC>
+// One client row per grid.y.  Each thread owns 4 consecutive entries starting at a 16-B aligned address of
+// the row (the row start c*P need not be aligned: thread 0 also takes the unaligned head, the last
+// thread the tail), so the row streams as float4 whatever P is.  The per-element arithmetic is the
+// scalar form's (same bits); the bias corrections are computed once per thread.
+__device__ __forceinline__ void adam1(float& pi, float& mi, float& vi, float gi, float a, float sb) {
+  const float mn = mi + 0.1f * (gi - mi);
+  const float vn = 0.999f * vi + 0.001f * gi * gi;
+  mi = mn;
+  vi = vn;
+  pi -= a * mn / (sqrtf(vn) / sb + 1e-8f);
+}
 __global__ void __launch_bounds__(256) k_adam_clients(float* __restrict__ p, float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v, long P,
                                                       const int* tcount, const int* bsz, const int* stepctl, int C,
                                                       int S, const int* failed, float lr, long skip_lo, long skip_hi,
                                                       float sgd_lr, int zero_g) {
-  constexpr int W = VEC ? 4 : 1;
   const int c = blockIdx.y;
-  const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * W;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long row = (long)c * P;
+  const long head = (4 - (row & 3)) & 3;  // entries before the first 16-B aligned one (arena base aligned)
+  const long i0 = head + 4 * t;            // this thread's aligned group
   int bs;
-  if (i0 >= P || !step_active(bsz, stepctl, C, S, failed, c, &bs)) return;
-  if (i0 >= skip_lo && i0 + W <= skip_hi) return;  // buffers (e.g. the positional-encoding table)
-  const long k0 = (long)c * P + i0;
-  float gi[W], mi[W], vi[W], pi[W];
-  if constexpr (VEC) {
-    const f4v g4 = *(const f4v*)(g + k0), m4 = *(const f4v*)(m + k0), v4 = *(const f4v*)(v + k0),
-              p4 = *(const f4v*)(p + k0);
+  if ((t > 0 && i0 >= P) || !step_active(bsz, stepctl, C, S, failed, c, &bs)) return;
+  float a = 0.f, sb = 1.f;
+  if (sgd_lr <= 0.f) {
+    const float tt = (float)(tcount[c] + 1);
+    const float bc1 = 1.f - powf(0.9f, tt), bc2 = 1.f - powf(0.999f, tt);
+    a = lr / bc1;
+    sb = sqrtf(bc2);
+  }
+  auto one = [&](long i) {  // scalar entry i of the row
+    if (i >= skip_lo && i < skip_hi) return;  // buffers (e.g. the positional-encoding table)
+    const long k = row + i;
+    const float gi = g[k];
+    if (zero_g) g[k] = 0.f;  // the next step accumulates into a zeroed arena without a fill launch
+    if (sgd_lr > 0.f) {
+      p[k] -= sgd_lr * gi;
+      return;
+    }
+    float pi = p[k], mi = m[k], vi = v[k];
+    adam1(pi, mi, vi, gi, a, sb);
+    m[k] = mi;
+    v[k] = vi;
+    p[k] = pi;
+  };
+  if (t == 0)
+    for (long i = 0; i < head && i < P; ++i) one(i);
+  if (i0 + 4 > P) {  // tail
+    for (long i = i0; i < P; ++i) one(i);
+    return;
+  }
+  if (i0 + 4 <= skip_lo || i0 >= skip_hi) {
+    const long k = row + i0;
+    f4v g4 = *(const f4v*)(g + k), p4 = *(const f4v*)(p + k);
+    if (zero_g) *(f4v*)(g + k) = f4v{0.f, 0.f, 0.f, 0.f};
+    if (sgd_lr > 0.f) {
+      *(f4v*)(p + k) = p4 - sgd_lr * g4;
+      return;
+    }
+    f4v m4 = *(const f4v*)(m + k), v4 = *(const f4v*)(v + k);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      gi[e] = g4[e];
-      mi[e] = m4[e];
-      vi[e] = v4[e];
-      pi[e] = p4[e];
+      float pe = p4[e], me = m4[e], ve = v4[e];
+      adam1(pe, me, ve, g4[e], a, sb);
+      p4[e] = pe;
+      m4[e] = me;
+      v4[e] = ve;
     }
+    *(f4v*)(m + k) = m4;
+    *(f4v*)(v + k) = v4;
+    *(f4v*)(p + k) = p4;
   } else {
-    gi[0] = g[k0];
-    mi[0] = m[k0];
-    vi[0] = v[k0];
-    pi[0] = p[k0];
-  }
-  bool upd[W];
-#pragma unroll
-  for (int e = 0; e < W; ++e) upd[e] = !(i0 + e >= skip_lo && i0 + e < skip_hi);
-  if (zero_g) {  // the next step accumulates into a zeroed arena without a fill launch
-    if constexpr (VEC) {
-      f4v z;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) z[e] = upd[e] ? 0.f : gi[e];
-      *(f4v*)(g + k0) = z;
-    } else {
-      g[k0] = 0.f;
-    }
-  }
-  if (sgd_lr > 0.f) {
-#pragma unroll
-    for (int e = 0; e < W; ++e)
-      if (upd[e]) pi[e] -= sgd_lr * gi[e];
-  } else {
-    const float t = (float)(tcount[c] + 1);
-    const float bc1 = 1.f - powf(0.9f, t), bc2 = 1.f - powf(0.999f, t);
-    const float a = lr / bc1, sb = sqrtf(bc2);
-#pragma unroll
-    for (int e = 0; e < W; ++e) {
-      if (!upd[e]) continue;
-      const float mn = mi[e] + 0.1f * (gi[e] - mi[e]);
-      const float vn = 0.999f * vi[e] + 0.001f * gi[e] * gi[e];
-      mi[e] = mn;
-      vi[e] = vn;
-      pi[e] -= a * mn / (sqrtf(vn) / sb + 1e-8f);
-    }
-  }
-  if constexpr (VEC) {
-    if (sgd_lr <= 0.f) {
-      *(f4v*)(m + k0) = f4v{mi[0], mi[1], mi[2], mi[3]};
-      *(f4v*)(v + k0) = f4v{vi[0], vi[1], vi[2], vi[3]};
-    }
-    *(f4v*)(p + k0) = f4v{pi[0], pi[1], pi[2], pi[3]};
-  } else {
-    if (sgd_lr <= 0.f) {
-      m[k0] = mi[0];
-      v[k0] = vi[0];
-    }
-    p[k0] = pi[0];
+    for (long i = i0; i < i0 + 4; ++i) one(i);
   }
 }
 
@@ -1002,13 +999,9 @@ int afl_ce(const float* logits, const long* y, int K, const int* bsz, const int*
 int afl_adam_clients(float* p, float* g, float* m, float* v, long P, int C, const int* tcount, const int* bsz,
                      const int* stepctl, int S, const int* failed, float lr, long skip_lo, long skip_hi, float sgd_lr,
                      int zero_g, hipStream_t s) {
-  const bool vec = (P & 3) == 0 && (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
-  if (vec)
-    hipLaunchKernelGGL(k_adam_clients<true>, dim3(nb256((P + 3) / 4), C), dim3(256), 0, s, p, g, m, v, P, tcount, bsz,
-                       stepctl, C, S, failed, lr, skip_lo, skip_hi, sgd_lr, zero_g);
-  else
-    hipLaunchKernelGGL(k_adam_clients<false>, dim3(nb256(P), C), dim3(256), 0, s, p, g, m, v, P, tcount, bsz, stepctl,
-                       C, S, failed, lr, skip_lo, skip_hi, sgd_lr, zero_g);
+  if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_adam_clients, dim3(nb256(P / 4 + 1), C), dim3(256), 0, s, p, g, m, v, P, tcount, bsz, stepctl, C,
+                     S, failed, lr, skip_lo, skip_hi, sgd_lr, zero_g);
   return launched();
 }
 
