@@ -419,6 +419,7 @@ class FLEngine:
                 train_rows.append(j)
                 train_nd.append(num_data)
                 train_seeds.append(lc.seed * 7 + lc.training_round)
+        tq1 = time.perf_counter()
         # every per-round host value the device needs goes up in ONE asynchronous copy (a pageable
         # torch.tensor(..., device=) per item was a blocking copy each: ~1.5 ms of host time per round)
         js = [j for j, _ in started]
@@ -430,6 +431,7 @@ class FLEngine:
             np.asarray(train_nd, np.int32),
             np.asarray([self._dev_seed(s) for s in train_seeds], np.int32)])
         n_local = len(self.local)
+        tq2 = time.perf_counter()
         # START parameters of every started client (one batched generate / broadcast copy)
         if started:
             if self.mode == "hyper":
@@ -500,7 +502,8 @@ class FLEngine:
             self._last_losses = losses
         else:
             tp3 = time.perf_counter()
-        self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tp1,
+        self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_prep_host": tq1 - tq, "t_lw_prep_upload": tq2 - tq1,
+                          "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tp1,
                           "t_lw_wait": tp3 - tp2, "t_lw_post": time.perf_counter() - tp3}
         return block
 
@@ -695,7 +698,8 @@ class FLEngine:
                 self.comm.all_reduce_(red)
             self._sync()
         t2 = time.perf_counter()
-        round_ok = int(red[P + 1].item()) == 0 and int(red[P + 2].item()) == len(self.selected)
+        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters
+        round_ok = int(fl[0]) == 0 and int(fl[1]) == len(self.selected)
         if round_ok:
             self.global_params = (red[:P] / red[P]).to(torch.float32)
         t3 = time.perf_counter()
@@ -703,10 +707,10 @@ class FLEngine:
         with trace.range("fl/validate"):
             if self.leader and self.validation is not None and round_ok:
                 round_ok, metric = self.validation.test(self.global_params)
-            ctrl = torch.tensor([1.0 if round_ok else 0.0], dtype=torch.float64, device=self.device)
-            if self.world > 1:
+            if self.world > 1:  # a single rank keeps the decision on the host
+                ctrl = torch.tensor([1.0 if round_ok else 0.0], dtype=torch.float64, device=self.device)
                 self.comm.broadcast_(ctrl, src=0)
-            round_ok = bool(ctrl.item() > 0.5)
+                round_ok = bool(ctrl.item() > 0.5)
         t4 = time.perf_counter()
         if round_ok:
             with trace.range("fl/checkpoint"):
@@ -718,9 +722,10 @@ class FLEngine:
                     self.round_no -= 1
         elif self.verbose:
             print_with_color("Training failed!", "yellow")
+        t5 = time.perf_counter()
         rec = {"round": self.round_no, "ok": round_ok, "metric": metric, **getattr(self, "_lw_times", {}),
                "t_local": t1 - t0, "t_gather": t2 - t1,
-               "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
+               "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_checkpoint": t5 - t4, "t_round": t5 - t0,
                "n_selected": len(self.selected), "removed": [], "path": "fedavg-allreduce"}
         self.metrics.write(rec)
         self.history.append(rec)

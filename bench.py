@@ -109,8 +109,8 @@ def main() -> int:
         elapsed = float(t.item())
     if args.profile_rounds and rank == 0:
         for r in recs:
-            print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_prep", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_lw_post", "t_local",
-                                                "t_gather", "t_aggregate", "t_validate", "t_round", "metric")
+            print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_prep", "t_lw_prep_host", "t_lw_prep_upload", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_lw_post", "t_local",
+                                                "t_gather", "t_aggregate", "t_validate", "t_checkpoint", "t_round", "metric")
                               if k in r}), file=sys.stderr)
     value = args.steps / elapsed
     if rank == 0:
