@@ -83,10 +83,11 @@ class _Program:
         """Weight/bias grads of ``Y = X W^T + b`` and (optionally) ``dX = dY W`` with a fused
         dropout'/act' epilogue for the layer that produced X."""
         self.dw(dY, X, self.w(grads, wname))
-        Lx.colsum(dY, self.w(grads, bname))
-        if dX is not None:
+        if dX is not None:  # the bias gradient rides on the dX GEMM's pass over dY
             Lx.bgemm(dY, self.w(params, wname).transpose(1, 2), dX, G=G, gact=gact, accum=accum, ctl=ctl, layer=layer,
-                     p=self.p(p))
+                     p=self.p(p), asum=self.w(grads, bname))
+        else:
+            Lx.colsum(dY, self.w(grads, bname))
 
     # -- interface -----------------------------------------------------------------------------
     def inputs(self, table, idx, ctl):  # pragma: no cover - abstract

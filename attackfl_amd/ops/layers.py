@@ -79,17 +79,21 @@ def _rc(M, N):
 
 # ------------------------------------------------------------------------------------------ GEMM
 def bgemm(A, B, C, bias=None, Z=None, G=None, act=0, gact=0, accum=0, splitk=1, alpha=1.0,
-          ctl: Optional[StepCtl] = None, layer: int = 0, p: float = 0.0, generic: bool = False) -> None:
+          ctl: Optional[StepCtl] = None, layer: int = 0, p: float = 0.0, generic: bool = False, asum=None) -> None:
     """``C (op)= epi(alpha * A @ B^T)``; A [C,M,K], B [C,N,K], C [C,M,N].
 
     Epilogue order: +bias -> (Z := pre-activation) -> act -> dropout(layer, m, n) -> *act'(G).
     accum: 0 store, 1 add, 2 atomic add (required when splitk > 1).  On the device, K <= 256 / N <= 256
     shapes with aligned row-major operands take the tall-skinny kernel (k_tsgemm); ``generic`` forces the
-    64x64-tile kernel (k_bgemm) — the tests compare the two."""
+    64x64-tile kernel (k_bgemm) — the tests compare the two.  ``asum [C, K]`` (optional) accumulates the
+    column sums of A — for ``dX = dY W`` that is the bias gradient, taken from the A rows the GEMM streams
+    anyway (fused in k_tsgemm, a separate column-sum pass otherwise)."""
     if _nat(A):
         s, sc = _dargs(ctl, p)
-        _native().bgemm(A, B, C, bias, Z, G, act, gact, accum, splitk, alpha, s, sc, layer, p, int(generic))
+        _native().bgemm(A, B, C, bias, Z, G, act, gact, accum, splitk, alpha, s, sc, layer, p, int(generic), asum)
         return
+    if asum is not None:
+        asum.add_(A.sum(dim=1))
     v = alpha * torch.bmm(A, B.transpose(1, 2))
     if bias is not None:
         v = v + bias[:, None, :]

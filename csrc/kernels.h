@@ -136,6 +136,8 @@ struct AflGemm {
   AflDrop drop;
   int avec, bvec;  // set by the launcher: operand rows 16-B aligned and k-contiguous
   int no_ts;       // 1: never take the tall-skinny path (tests compare the two kernels)
+  float* asum;     // optional: asum[c * sasc + k] += sum_m A[c][m][k] (the bias gradient of a dX = dY.W GEMM)
+  long sasc;
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
 

@@ -752,7 +752,7 @@ inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
 constexpr int TS_NTH = 256;
 constexpr int TS_WAVES = TS_NTH / 64;
 
-template <int NT, int KT, bool PF>
+template <int NT, int KT, bool PF, bool CS>
 __global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
   constexpr int N = 16 * NT, K = 32 * KT, LDB = K + 8;
   extern __shared__ __attribute__((aligned(16))) unsigned short Bs[];  // [N][LDB] bf16, then bias [N] fp32
@@ -792,6 +792,9 @@ __global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
       x[kk][1] = ok ? *(const f4v*)(p + 32 * kk + 4) : f4v{0.f, 0.f, 0.f, 0.f};
     }
   };
+  f4v cs[CS ? KT : 1][2];  // CS: this lane's running column sums of A (rows j of its tiles, k = 32 kk + 8 q ..)
+#pragma unroll
+  for (int kk = 0; kk < (CS ? KT : 1); ++kk) cs[kk][0] = cs[kk][1] = f4v{0.f, 0.f, 0.f, 0.f};
   int t = blockIdx.x * TS_WAVES + wave;
   if (PF && t < ntile) load(t, xa);
   for (; t < ntile; t += wstride) {
@@ -799,6 +802,13 @@ __global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
       if (t + wstride < ntile) load(t + wstride, xn);  // next tile's A in flight during this tile's work
     } else {
       load(t, xa);
+    }
+    if constexpr (CS) {  // rows past M were loaded as zeros
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        cs[kk][0] += xa[kk][0];
+        cs[kk][1] += xa[kk][1];
+      }
     }
     s8v bx[KT];
 #pragma unroll
@@ -856,6 +866,40 @@ __global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
       }
     }
   }
+  if constexpr (CS) {
+    // reduce over the 16 lanes of a q group, then over the waves (LDS, reusing the B image), one atomic
+    // per column and workgroup
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = cs[kk][h][e];
+          x += __shfl_xor(x, 1, 64);
+          x += __shfl_xor(x, 2, 64);
+          x += __shfl_xor(x, 4, 64);
+          x += __shfl_xor(x, 8, 64);
+          cs[kk][h][e] = x;
+        }
+    __syncthreads();  // every wave is done reading the B image
+    float* red = reinterpret_cast<float*>(Bs);  // [TS_WAVES][K]
+    if (j == 0) {
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[wave * K + 32 * kk + 8 * q + 4 * h + e] = cs[kk][h][e];
+    }
+    __syncthreads();
+    if (tid < K) {
+      float x = 0.f;
+#pragma unroll
+      for (int w = 0; w < TS_WAVES; ++w) x += red[w * K + tid];
+      atomicAdd(g.asum + (long)c * g.sasc + tid, x);
+    }
+  }
 }
 
 __host__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -870,7 +914,8 @@ int tsgemm_try(const AflGemm& g, hipStream_t s) {
   const int key = g.N * 1024 + g.K;
 #define TS_CASE(N_, K_)                                         \
   case N_ * 1024 + K_:                                          \
-    fn = (const void*)k_tsgemm<N_ / 16, K_ / 32, (K_ <= 64)>;  \
+    fn = g.asum ? (const void*)k_tsgemm<N_ / 16, K_ / 32, (K_ <= 64), true>      \
+                : (const void*)k_tsgemm<N_ / 16, K_ / 32, (K_ <= 64), false>;    \
     break;
   switch (key) {
     TS_CASE(64, 64)
@@ -899,6 +944,11 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
   if (g.splitk > 1 && g.accum != 2) return (int)hipErrorInvalidValue;
   if (!g.no_ts && tsgemm_try(g, s) == 0) return launched();
+  if (g.asum) {  // the 64x64-tile kernel re-reads A per column tile: column sums as a separate pass
+    if (g.sAk != 1) return (int)hipErrorInvalidValue;
+    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s);
+    if (e) return e;
+  }
   const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
   dim3 grid(tiles, max(1, g.splitk), g.nC);
   AflGemm gg = g;  // 16-B aligned k-contiguous rows take the vector-load path

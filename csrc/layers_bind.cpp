@@ -63,7 +63,7 @@ AflDrop make_drop(const c10::optional<torch::Tensor>& seeds, const c10::optional
 void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<torch::Tensor> bias,
            c10::optional<torch::Tensor> Z, c10::optional<torch::Tensor> G, int64_t act, int64_t gact, int64_t accum,
            int64_t splitk, double alpha, c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl,
-           int64_t layer, double p, int64_t generic) {
+           int64_t layer, double p, int64_t generic, c10::optional<torch::Tensor> asum) {
   view3(A, "A");
   view3(B, "B");
   view3(Cm, "C");
@@ -100,6 +100,14 @@ void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<tor
   g.alpha = (float)alpha;
   g.drop = make_drop(seeds, stepctl, layer, p);
   g.no_ts = generic ? 1 : 0;
+  if (asum.has_value() && asum->defined()) {
+    dev(*asum, "asum");
+    TORCH_CHECK(asum->dim() == 2 && asum->size(0) == nC && asum->size(1) == K && asum->stride(1) == 1,
+                "asum must be a [C, K] view with unit column stride");
+    TORCH_CHECK(A.stride(2) == 1, "asum needs k-contiguous A rows");
+    g.asum = asum->data_ptr<float>();
+    g.sasc = asum->stride(0);
+  }
   ok(afl_bgemm(g, cur()), "bgemm");
 }
 
@@ -628,7 +636,7 @@ void afl_register_layers(pybind11::module& m) {
   m.def("bgemm", &bgemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias") = none, py::arg("Z") = none,
         py::arg("G") = none, py::arg("act") = 0, py::arg("gact") = 0, py::arg("accum") = 0, py::arg("splitk") = 1,
         py::arg("alpha") = 1.0, py::arg("seeds") = none, py::arg("stepctl") = none, py::arg("layer") = 0,
-        py::arg("p") = 0.0, py::arg("generic") = 0);
+        py::arg("p") = 0.0, py::arg("generic") = 0, py::arg("asum") = none);
   m.def("colsum", &colsum);
   m.def("gather_icu", &gather_icu);
   m.def("gather_har", &gather_har);

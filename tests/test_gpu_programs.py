@@ -89,12 +89,14 @@ def test_tall_skinny_gemm_matches_generic_and_composite(gpu, N, K, trans):
         Wd = (flat.to(dev)[:, 16:16 + N * K].view(C, K, N).transpose(1, 2) if trans
               else flat.to(dev)[:, 16:16 + N * K].view(C, N, K))
         Cm, Z = C0.clone().to(dev), torch.zeros(C, M, N, device=dev)
+        asum = torch.ones(C, K, device=dev)  # accumulates: starts at 1
         Lx.bgemm(A.to(dev), Wd, Cm, bias=bias.to(dev), Z=Z, G=G.to(dev), act=1, gact=1, accum=1, ctl=ctl, layer=4,
-                 p=0.1, generic=generic)
-        outs.append((Cm, Z))
+                 p=0.1, generic=generic, asum=asum)
+        outs.append((Cm, Z, asum))
     for k, name in ((0, "tsgemm"), (1, "bgemm")):
         _close(outs[k][0], outs[2][0], name=name + " C")
         _close(outs[k][1], outs[2][1], name=name + " Z")
+        assert torch.allclose(outs[k][2].cpu(), 1 + A.sum(dim=1), rtol=1e-5, atol=1e-3), name + " column sums"
     # the two device kernels share operand rounding (bf16) and accumulate in fp32: near-identical
     assert (outs[0][1] - outs[1][1]).abs().max().item() < 1e-3 * (outs[1][1].abs().max().item() + 1)
     del W
