@@ -104,3 +104,37 @@ def test_checkpoint_copy_fenced_against_in_place_update(gpu, tmp_path):
     assert bool((got == 1.0).all())
     assert bool((src == 2.0).all())
     w.close()
+
+
+def test_deferred_checkpoint_copies_the_submitted_state(gpu, tmp_path):
+    """``submit(defer=True)`` records the state and issues the copy at ``kick`` (after the next training
+    launch in the engine): work enqueued between submit and kick that does not touch the source must not
+    delay or change it; ``fence`` kicks a pending copy before an in-place update; a newer deferred submit
+    supersedes an older one that was never copied."""
+    import torch
+
+    from attackfl_amd.utils.ckpt import CheckpointWriter
+
+    w = CheckpointWriter()
+    src = torch.full((1 << 22,), 1.0, dtype=torch.float32, device="cuda")
+    path = str(tmp_path / "d.pth")
+    w.submit("d", src, lambda t: {"t": t.clone()}, path, defer=True)
+    other = torch.zeros_like(src)
+    other.add_(3.0)            # unrelated work queued before the copy is issued
+    w.kick()
+    w.fence()
+    src.fill_(2.0)             # the next in-place update, after the fence
+    w.flush()
+    assert bool((torch.load(path, weights_only=True)["t"] == 1.0).all())
+    # superseded deferred submits: only the newest state is written; fence() issues it first
+    src.fill_(4.0)
+    w.submit("d", src, lambda t: {"t": t.clone()}, path, defer=True)
+    dropped = w.dropped
+    src2 = torch.full_like(src, 5.0)
+    w.submit("d", src2, lambda t: {"t": t.clone()}, path, defer=True)
+    assert w.dropped == dropped + 1
+    w.fence()
+    src2.fill_(6.0)
+    w.flush()
+    assert bool((torch.load(path, weights_only=True)["t"] == 5.0).all())
+    w.close()
