@@ -49,13 +49,17 @@ META = 4  # valid, result, size, is_attacker
 
 class Staging:
     """Per-round host metadata -> device in ONE copy: the arrays are packed (8-byte aligned) into a
-    reused pinned buffer, copied with one non-blocking H2D copy, and returned as typed device views.
-    On a CPU device the arrays are simply wrapped."""
+    reused pinned buffer, copied with one non-blocking H2D copy into a reused device buffer, and returned
+    as typed device views — built once per layout (the same shapes every round), because the ~18 tensor
+    view ops per round cost more host time than the copy.  The copy is stream-ordered after the previous
+    round's kernels that read the old views.  On a CPU device the arrays are simply wrapped."""
 
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
         self.host: Optional[torch.Tensor] = None
+        self.dev: Optional[torch.Tensor] = None
         self.done: Optional[torch.cuda.Event] = None
+        self._views: Dict[tuple, List[torch.Tensor]] = {}
 
     def upload(self, arrays: Sequence[np.ndarray]) -> List[torch.Tensor]:
         if self.device.type != "cuda":
@@ -67,19 +71,25 @@ class Staging:
         n = max(n, 8)
         if self.host is None or self.host.numel() < n:
             self.host = torch.empty(max(n, 4096), dtype=torch.uint8, pin_memory=True)
+            self.dev = torch.empty(self.host.numel(), dtype=torch.uint8, device=self.device)
+            self._views.clear()
         elif self.done is not None:
             self.done.synchronize()  # the previous round's copy has long finished; never overwrite in flight
         hb = self.host.numpy()
         for a, o in zip(arrays, offs):
             hb[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-        dev = self.host[:n].to(self.device, non_blocking=True)
+        self.dev[:n].copy_(self.host[:n], non_blocking=True)
         if self.done is None:
             self.done = torch.cuda.Event()
         self.done.record(torch.cuda.current_stream(self.device))
-        out = []
-        for a, o in zip(arrays, offs):
-            t = dev[o:o + a.nbytes].view(_TORCH_DT[a.dtype.str[1:]])
-            out.append(t.reshape(a.shape))
+        key = tuple((a.shape, a.dtype.str) for a in arrays)
+        out = self._views.get(key)
+        if out is None:
+            out = []
+            for a, o in zip(arrays, offs):
+                t = self.dev[o:o + a.nbytes].view(_TORCH_DT[a.dtype.str[1:]])
+                out.append(t.reshape(a.shape))
+            self._views[key] = out
         return out
 
 

@@ -17,6 +17,7 @@ planted signal, weights are random-init (no datasets or checkpoints are download
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -96,6 +97,7 @@ def main() -> int:
     eng.phase_sync = bool(args.profile_rounds)
     for _ in range(args.warmup):
         eng.run_round()
+    gc.freeze()  # as server.py / launch.py: the long-lived objects leave the collector's full scans
     sync()
     t0 = time.perf_counter()
     recs = []

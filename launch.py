@@ -11,6 +11,7 @@ logs to ``app.log`` and writes the ``.pth`` checkpoints.  Attackers come from ``
 from __future__ import annotations
 
 import argparse
+import gc
 import os
 import sys
 
@@ -59,6 +60,7 @@ def main(argv=None) -> int:
     attackers = parse_attackers(args.attackers) if args.attackers else None
     table = build_client_table(cfg, comm.world, attackers, int(cfg.comm.get("clients-per-rank", 0)))
     eng = FLEngine(cfg, comm=comm, table=table, device=device)
+    gc.freeze()  # engine, models and tables -> permanent generation: no ms-long full GC scans mid-round
     eng.run()
     eng.close()
     comm.close()

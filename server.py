@@ -13,6 +13,7 @@ broker; updates move with ``torch.distributed`` (gloo by default for multi-proce
 from __future__ import annotations
 
 import argparse
+import gc
 import os
 import sys
 
@@ -44,6 +45,7 @@ def main(argv=None) -> int:
     init_group(store, 0, world, backend, int(cfg.comm.get("timeout-s", 600)), device.index)
     comm = TorchComm(device, backend)
     eng = FLEngine(cfg, comm=comm, table=table_from_json(table), device=device, leader=True)
+    gc.freeze()  # engine, models and tables -> permanent generation: no ms-long full GC scans mid-round
     eng.run()
     eng.close()
     torch.distributed.destroy_process_group()
