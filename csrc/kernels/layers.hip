@@ -299,6 +299,28 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// V4: every row pointer 16-B aligned (checked by the launcher) -> dwordx4 loads / stores per lane
+template <bool V>
+__device__ __forceinline__ void ld4f(const float* p, float (&v)[4]) {
+  if constexpr (V) {
+    const f4v t = *(const f4v*)p;
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = p[j];
+  }
+}
+template <bool V>
+__device__ __forceinline__ void st4f(float* p, const float (&v)[4]) {
+  if constexpr (V) {
+    *(f4v*)p = f4v{v[0], v[1], v[2], v[3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = v[j];
+  }
+}
+
+template <bool V4>
 __global__ void __launch_bounds__(256) k_ln_fwd(AflLn l) {
   const int c = blockIdx.y;
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -307,23 +329,17 @@ __global__ void __launch_bounds__(256) k_ln_fwd(AflLn l) {
   const uint32_t ka = l.da.thr16 ? drop_key(l.da, c) : 0u;
   const uint32_t ko = l.dout.thr16 ? drop_key(l.dout, c) : 0u;
   float s[4];
-  const float* xp = l.x + (long)c * l.sXc + (long)row * l.sXr + c0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s[j] = xp[j];
+  ld4f<V4>(l.x + (long)c * l.sXc + (long)row * l.sXr + c0, s);
   if (l.a) {
-    const float* ap = l.a + (long)c * l.sAc + (long)row * l.sAr + c0;
+    float a[4];
+    ld4f<V4>(l.a + (long)c * l.sAc + (long)row * l.sAr + c0, a);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float a = ap[j];
-      if (l.da.thr16) a *= drop_scale(l.da, ka, row, c0 + j);
-      s[j] += a;
+      if (l.da.thr16) a[j] *= drop_scale(l.da, ka, row, c0 + j);
+      s[j] += a[j];
     }
   }
-  if (l.s) {
-    float* sp = l.s + ((long)c * l.rows + row) * 64 + c0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) sp[j] = s[j];
-  }
+  if (l.s) st4f<V4>(l.s + ((long)c * l.rows + row) * 64 + c0, s);
   const float mean = sum16(s[0] + s[1] + s[2] + s[3]) * (1.f / 64.f);
   float q = 0.f;
 #pragma unroll
@@ -331,13 +347,13 @@ __global__ void __launch_bounds__(256) k_ln_fwd(AflLn l) {
   const float rstd = rsqrtf(sum16(q) * (1.f / 64.f) + 1e-5f);
   const float* gm = l.gamma + (long)c * l.sPc;
   const float* bt = l.beta + (long)c * l.sPc;
-  float* yp = l.y + (long)c * l.sYc + (long)row * l.sYr + c0;
+  float y[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float y = (s[j] - mean) * rstd * gm[c0 + j] + bt[c0 + j];
-    if (l.dout.thr16) y *= drop_scale(l.dout, ko, row, c0 + j);
-    yp[j] = y;
+    y[j] = (s[j] - mean) * rstd * gm[c0 + j] + bt[c0 + j];
+    if (l.dout.thr16) y[j] *= drop_scale(l.dout, ko, row, c0 + j);
   }
+  st4f<V4>(l.y + (long)c * l.sYc + (long)row * l.sYr + c0, y);
   if ((threadIdx.x & 15) == 0) {
     float* st = l.stats + ((long)c * l.rows + row) * 2;
     st[0] = mean;
@@ -347,6 +363,7 @@ __global__ void __launch_bounds__(256) k_ln_fwd(AflLn l) {
 
 constexpr int LNB_ROWS = 256;  // rows per backward block (dgamma/dbeta partials -> 128 atomics)
 
+template <bool V4>
 __global__ void __launch_bounds__(256) k_ln_bwd(AflLnB l) {
   __shared__ float red[16][129];
   const int c = blockIdx.y, li = threadIdx.x & 15, rg = threadIdx.x >> 4;
@@ -361,14 +378,13 @@ __global__ void __launch_bounds__(256) k_ln_bwd(AflLnB l) {
   for (int row = rbeg + rg; row < min(l.rows, rbeg + LNB_ROWS); row += 16) {
     const float* st = l.stats + ((long)c * l.rows + row) * 2;
     const float mean = st[0], rstd = st[1];
-    const float* dyp = l.dy + (long)c * l.sDc + (long)row * l.sDr + c0;
-    const float* sp = l.s + (long)c * l.sSc + (long)row * l.sSr + c0;
-    float g[4], xh[4], a1 = 0.f, a2 = 0.f;
+    float g[4], xh[4], sv[4], a1 = 0.f, a2 = 0.f;
+    ld4f<V4>(l.dy + (long)c * l.sDc + (long)row * l.sDr + c0, g);
+    ld4f<V4>(l.s + (long)c * l.sSc + (long)row * l.sSr + c0, sv);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      g[j] = dyp[j];
       if (l.dout.thr16) g[j] *= drop_scale(l.dout, ko, row, c0 + j);
-      xh[j] = (sp[j] - mean) * rstd;
+      xh[j] = (sv[j] - mean) * rstd;
       dg[j] += g[j] * xh[j];
       db[j] += g[j];
       const float dxh = g[j] * gam[j];
@@ -378,16 +394,21 @@ __global__ void __launch_bounds__(256) k_ln_bwd(AflLnB l) {
     a1 = sum16(a1) * (1.f / 64.f);
     a2 = sum16(a2) * (1.f / 64.f);
     float* dxp = l.dx + (long)c * l.sXc + (long)row * l.sXr + c0;
-    float* dap = l.da ? l.da + (long)c * l.sAc + (long)row * l.sAr + c0 : nullptr;
+    float dx[4], dxo[4];
+    if (l.dx_accum) ld4f<V4>(dxp, dxo);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float dx = rstd * (g[j] * gam[j] - a1 - xh[j] * a2);
-      if (l.dx_accum)
-        dxp[j] += dx;
-      else
-        dxp[j] = dx;
-      if (dap) dap[j] = l.da_drop.thr16 ? dx * drop_scale(l.da_drop, ka, row, c0 + j) : dx;
+    for (int j = 0; j < 4; ++j) dx[j] = rstd * (g[j] * gam[j] - a1 - xh[j] * a2);
+    if (l.da) {
+      float da[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) da[j] = l.da_drop.thr16 ? dx[j] * drop_scale(l.da_drop, ka, row, c0 + j) : dx[j];
+      st4f<V4>(l.da + (long)c * l.sAc + (long)row * l.sAr + c0, da);
     }
+    if (l.dx_accum) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dx[j] += dxo[j];
+    }
+    st4f<V4>(dxp, dx);
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1011,13 +1032,24 @@ int afl_pool4_bwd(const float* dout, long sOc, long sOr, int col0, const float* 
   return launched();
 }
 
+inline bool rows16(const void* p, long sc, long sr) { return (((uintptr_t)p & 15) | (sc & 3) | (sr & 3)) == 0; }
 int afl_ln_fwd(const AflLn& l, hipStream_t s) {
-  hipLaunchKernelGGL(k_ln_fwd, dim3((l.rows + 15) / 16, l.nC), dim3(256), 0, s, l);
+  const bool v4 = rows16(l.x, l.sXc, l.sXr) && (!l.a || rows16(l.a, l.sAc, l.sAr)) && (!l.s || rows16(l.s, 0, 0)) &&
+                  rows16(l.y, l.sYc, l.sYr);
+  if (v4)
+    hipLaunchKernelGGL(k_ln_fwd<true>, dim3((l.rows + 15) / 16, l.nC), dim3(256), 0, s, l);
+  else
+    hipLaunchKernelGGL(k_ln_fwd<false>, dim3((l.rows + 15) / 16, l.nC), dim3(256), 0, s, l);
   return launched();
 }
 
 int afl_ln_bwd(const AflLnB& l, hipStream_t s) {
-  hipLaunchKernelGGL(k_ln_bwd, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
+  const bool v4 = rows16(l.dy, l.sDc, l.sDr) && rows16(l.s, l.sSc, l.sSr) && rows16(l.dx, l.sXc, l.sXr) &&
+                  (!l.da || rows16(l.da, l.sAc, l.sAr));
+  if (v4)
+    hipLaunchKernelGGL(k_ln_bwd<true>, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
+  else
+    hipLaunchKernelGGL(k_ln_bwd<false>, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
   return launched();
 }
 
