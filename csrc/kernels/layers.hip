@@ -681,54 +681,71 @@ __global__ void k_step_end(int* stepctl, int* tcount, const int* bsz, const int*
 
 // ============================================================================ HAR stem and pooling
 // h[c][b*L+l][o] = conv_b[o] + sum_j conv_w[o][j] x[c][b][l+j-1] + pe[l][o]   (src/Model.py:431-452)
-__global__ void k_conv_pe_fwd(const float* __restrict__ x, int C, int B, int L, const float* __restrict__ params,
-                              long P, int w_off, int b_off, int pe_off, float* __restrict__ h) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)C * B * L * 64) return;
-  const int o = (int)(t & 63);
-  const long row = t >> 6;
-  const int l = (int)(row % L), b = (int)((row / L) % B), c = (int)(row / ((long)L * B));
+// One thread per (row, 4 channels): 32-bit row / position arithmetic (the per-element 64-bit divisions
+// of the first version dominated), float4 stores of h / loads of dh.
+__global__ void __launch_bounds__(256) k_conv_pe_fwd(const float* __restrict__ x, int C, int B, int L,
+                                                     const float* __restrict__ params, long P, int w_off, int b_off,
+                                                     int pe_off, float* __restrict__ h) {
+  const int c = blockIdx.y;
+  const int nrows = B * L;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int row = t >> 4, o0 = (t & 15) * 4;
+  if (row >= nrows) return;
+  const int l = row % L;
   const float* pp = params + (long)c * P;
-  const float* xr = x + ((long)c * B + b) * L;
-  float s = pp[b_off + o] + pp[pe_off + l * 64 + o];
+  const float* xr = x + (long)c * nrows + (row - l);
+  const float xm = l >= 1 ? xr[l - 1] : 0.f, x0 = xr[l], xp = l + 1 < L ? xr[l + 1] : 0.f;
+  f4v v;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int li = l + j - 1;
-    if (li >= 0 && li < L) s += pp[w_off + o * 3 + j] * xr[li];
+  for (int e = 0; e < 4; ++e) {
+    const int o = o0 + e;
+    const float* w = pp + w_off + o * 3;
+    float s = pp[b_off + o] + pp[pe_off + l * 64 + o];
+    if (l >= 1) s += w[0] * xm;
+    s += w[1] * x0;
+    if (l + 1 < L) s += w[2] * xp;
+    v[e] = s;
   }
-  h[t] = s;
+  *(f4v*)(h + ((long)c * nrows + row) * 64 + o0) = v;
 }
 
+// conv weight / bias gradients: 16 row groups x 16 lanes of 4 channels per workgroup, 1024 rows per workgroup
 __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x, const float* __restrict__ dh,
                                                      int C, int B, int L, float* __restrict__ grads, long P,
                                                      int w_off, int b_off) {
-  __shared__ float red[4][64][4];
-  const int c = blockIdx.y, o = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const long nrows = (long)B * L, r0 = (long)blockIdx.x * 1024;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
-  for (long row = r0 + rg; row < min(nrows, r0 + 1024); row += 4) {
-    const int l = (int)(row % L);
-    const float* xr = x + (long)c * nrows + (row - l);
-    const float d = dh[((long)c * nrows + row) * 64 + o];
-    ab += d;
-    if (l >= 1) a0 += d * xr[l - 1];
-    a1 += d * xr[l];
-    if (l + 1 < L) a2 += d * xr[l + 1];
-  }
-  red[rg][o][0] = a0;
-  red[rg][o][1] = a1;
-  red[rg][o][2] = a2;
-  red[rg][o][3] = ab;
-  __syncthreads();
-  if (rg == 0) {
-    float s[4];
+  __shared__ float red[16][64][4];
+  const int c = blockIdx.y, o0 = (threadIdx.x & 15) * 4, rg = threadIdx.x >> 4;
+  const int nrows = B * L, r0 = blockIdx.x * 1024;
+  float a[4][4] = {};  // [channel][tap 0..2, bias]
+  int row = r0 + rg, l = row % L;
+  const float* xc = x + (long)c * nrows;
+  const float* dc = dh + (long)c * nrows * 64 + o0;
+  for (; row < min(nrows, r0 + 1024); row += 16) {
+    const float* xr = xc + (row - l);
+    const float xm = l >= 1 ? xr[l - 1] : 0.f, x0 = xr[l], xp = l + 1 < L ? xr[l + 1] : 0.f;
+    const f4v d = *(const f4v*)(dc + (long)row * 64);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = red[0][o][q] + red[1][o][q] + red[2][o][q] + red[3][o][q];
+    for (int e = 0; e < 4; ++e) {
+      a[e][0] += d[e] * xm;
+      a[e][1] += d[e] * x0;
+      a[e][2] += d[e] * xp;
+      a[e][3] += d[e];
+    }
+    l += 16;
+    while (l >= L) l -= L;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[rg][o0 + e][q] = a[e][q];
+  __syncthreads();
+  {
+    const int o = threadIdx.x >> 2, q = threadIdx.x & 3;  // 64 channels x 4 sums
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += red[r][o][q];
     float* gp = grads + (long)c * P;
-    atomicAdd(gp + w_off + o * 3 + 0, s[0]);
-    atomicAdd(gp + w_off + o * 3 + 1, s[1]);
-    atomicAdd(gp + w_off + o * 3 + 2, s[2]);
-    atomicAdd(gp + b_off + o, s[3]);
+    atomicAdd(gp + (q < 3 ? w_off + o * 3 + q : b_off + o), s);
   }
 }
 
@@ -1095,13 +1112,15 @@ int afl_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, i
 
 int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,
                     float* h, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv_pe_fwd, dim3(nb256((long)C * B * L * 64)), dim3(256), 0, s, x, C, B, L, params, P, w_off,
+  if (((uintptr_t)h & 15) != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_conv_pe_fwd, dim3(nb256((long)B * L * 16), C), dim3(256), 0, s, x, C, B, L, params, P, w_off,
                      b_off, pe_off, h);
   return launched();
 }
 
 int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float* grads, long P, int w_off, int b_off,
                     hipStream_t s) {
+  if (((uintptr_t)dh & 15) != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_conv_pe_bwd, dim3((unsigned)(((long)B * L + 1023) / 1024), C), dim3(256), 0, s, x, dh, C, B, L,
                      grads, P, w_off, b_off);
   return launched();
