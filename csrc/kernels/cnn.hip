@@ -237,6 +237,7 @@ constexpr int B_DH2 = B_DC2 + MT * B_LC2 * 4;         // [64][72] bf16    9216
 constexpr int B_DC1 = B_DC2;                          // [64][100] f32 (after dc2 is consumed)
 constexpr int B_TOTAL = B_DH2 + MT * B_LD2 * 2;       // 76800
 static_assert(B_TOTAL <= 80 * 1024, "cnn bwd LDS: two workgroups per CU");
+static_assert(MT * 64 % NT == 0 && MT * 64 / NT <= 32 && MT * 32 % NT == 0, "relu' mask bits per thread");
 
 template <int L>
 __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsigned char* smem) {
@@ -249,6 +250,26 @@ __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
   unsigned short* dh2b = (unsigned short*)(smem + B_DH2);
   float* dc1 = (float*)(smem + B_DC1);
   const unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
+  // relu' masks of h2 / h1 for the two col2im phases, loaded now: their global-load latency then hides behind
+  // the dh3 and dcols2 phases instead of following a barrier (bit i: element e = tid + i * NT of that phase)
+  uint32_t m2 = 0, m1 = 0;
+  {
+    float h2v[MT * 64 / NT], h1v[MT * 32 / NT];
+#pragma unroll
+    for (int i = 0; i < MT * 64 / NT; ++i) {
+      const int e = tid + i * NT, m = e >> 6, ci = e & 63;
+      h2v[i] = m < M ? br.h2[(cbase + row0 + m) * 64 + ci] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < MT * 32 / NT; ++i) {
+      const int e = tid + i * NT, m = e >> 5, ci = e & 31;
+      h1v[i] = m < M ? br.h1[(cbase + row0 + m) * 32 + ci] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < MT * 64 / NT; ++i) m2 |= (h2v[i] > 0.f ? 1u : 0u) << i;
+#pragma unroll
+    for (int i = 0; i < MT * 32 / NT; ++i) m1 |= (h1v[i] > 0.f ? 1u : 0u) << i;
+  }
   // dh3 = relu'(h3) * pool'(dropout'(dcat))
   const bool dr = a.drop.thr16 != 0;
   const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
@@ -293,15 +314,16 @@ __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
   }
   __syncthreads();
   // col2im + relu'(h2) -> dh2
-  for (int e = tid; e < MT * 64; e += NT) {
-    const int m = e >> 6, ci = e & 63;
+#pragma unroll
+  for (int i = 0; i < MT * 64 / NT; ++i) {
+    const int e = tid + i * NT, m = e >> 6, ci = e & 63;
     float sum = 0.f;
     if (m < M) {
       const int l = m % L;
       if (l < L - 1) sum += dc2[(m + 1) * B_LC2 + ci * 3 + 0];  // output l+1, tap 0 reads input l
       sum += dc2[m * B_LC2 + ci * 3 + 1];
       if (l > 0) sum += dc2[(m - 1) * B_LC2 + ci * 3 + 2];
-      if (!(br.h2[(cbase + row0 + m) * 64 + ci] > 0.f)) sum = 0.f;
+      if (!((m2 >> i) & 1u)) sum = 0.f;
       br.dh2[(cbase + row0 + m) * 64 + ci] = sum;
     }
     dh2b[m * B_LD2 + ci] = bfu(sum);
@@ -326,14 +348,15 @@ __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
       for (int e = 0; e < 4; ++e) dc1[(mt + 4 * (lane >> 4) + e) * B_LC1 + (nb0 + j) * 16 + (lane & 15)] = acc[j][e];
   }
   __syncthreads();
-  for (int e = tid; e < MT * 32; e += NT) {
-    const int m = e >> 5, ci = e & 31;
+#pragma unroll
+  for (int i = 0; i < MT * 32 / NT; ++i) {
+    const int e = tid + i * NT, m = e >> 5, ci = e & 31;
     if (m >= M) continue;
     const int l = m % L;
     float sum = dc1[m * B_LC1 + ci * 3 + 1];
     if (l < L - 1) sum += dc1[(m + 1) * B_LC1 + ci * 3 + 0];
     if (l > 0) sum += dc1[(m - 1) * B_LC1 + ci * 3 + 2];
-    if (!(br.h1[(cbase + row0 + m) * 32 + ci] > 0.f)) sum = 0.f;
+    if (!((m1 >> i) & 1u)) sum = 0.f;
     br.dh1[(cbase + row0 + m) * 32 + ci] = sum;
   }
 }
