@@ -749,24 +749,31 @@ __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x
   }
 }
 
+// mean over L of h [C*B][L][64]: one workgroup per (client, sample), 16 row groups x 16 lanes of float4
 __global__ void __launch_bounds__(256) k_mean_rows_fwd(const float* __restrict__ h, int L, float* __restrict__ out) {
-  __shared__ float red[4][64];
+  __shared__ f4v red[16][16];
   const long cb = blockIdx.x;  // c * B + b
-  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const float* src = h + cb * L * 64 + o;
-  float s = 0.f;
-  for (int l = rg; l < L; l += 4) s += src[(long)l * 64];
-  red[rg][o] = s;
+  const int q = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const float* src = h + cb * L * 64 + 4 * q;
+  f4v s = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int l = rg; l < L; l += 16) s += *(const f4v*)(src + (long)l * 64);
+  red[rg][q] = s;
   __syncthreads();
-  if (rg == 0) out[cb * 64 + o] = (red[0][o] + red[1][o] + red[2][o] + red[3][o]) / (float)L;
+  if (rg == 0) {
+    f4v t = red[0][q];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) t += red[r][q];
+    *(f4v*)(out + cb * 64 + 4 * q) = t / (float)L;
+  }
 }
 
-__global__ void k_mean_rows_bwd(const float* __restrict__ dout, long n, int L, float* __restrict__ dh) {
+// dh[c, b, l, :] = dout[c, b, :] / L (float4 per thread)
+__global__ void k_mean_rows_bwd(const float* __restrict__ dout, long n4, int L, float* __restrict__ dh) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int o = (int)(t & 63);
-  const long cb = (t >> 6) / L;
-  dh[t] = dout[cb * 64 + o] / (float)L;
+  if (t >= n4) return;
+  const int q = (int)(t & 15);
+  const long cb = (t >> 4) / L;
+  *(f4v*)(dh + 4 * t) = *(const f4v*)(dout + cb * 64 + 4 * q) / (float)L;
 }
 
 inline int launched() { return (int)hipGetLastError(); }
@@ -1127,12 +1134,14 @@ int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float*
 }
 
 int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s) {
+  if ((((uintptr_t)h | (uintptr_t)out) & 15) != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_mean_rows_fwd, dim3(C * B), dim3(256), 0, s, h, L, out);
   return launched();
 }
 
 int afl_mean_rows_bwd(const float* dout, int C, int B, int L, float* dh, hipStream_t s) {
-  const long n = (long)C * B * L * 64;
-  hipLaunchKernelGGL(k_mean_rows_bwd, dim3(nb256(n)), dim3(256), 0, s, dout, n, L, dh);
+  if ((((uintptr_t)dout | (uintptr_t)dh) & 15) != 0) return (int)hipErrorInvalidValue;
+  const long n4 = (long)C * B * L * 16;
+  hipLaunchKernelGGL(k_mean_rows_bwd, dim3(nb256(n4)), dim3(256), 0, s, dout, n4, L, dh);
   return launched();
 }
