@@ -264,3 +264,25 @@ def test_plan_subset_and_epoch_permutations():
         for e in range(1, 3):
             ep = p.order[c, e, :n]
             assert torch.equal(ep.sort().values, sub.sort().values) and not torch.equal(ep, sub)
+
+
+def test_hyper_generate_cache_invalidated_by_every_arena_change():
+    """HyperServer.generate_many is memoised per hypernetwork state: train / restore / load_arena drop it."""
+    import torch
+
+    from attackfl_amd.fl.hyper_server import HyperServer
+    from attackfl_amd.models import build_model
+
+    sd = build_model("TransformerModel", seed=0).state_dict()
+    hs = HyperServer(sd, 3, 0.01, 1e9, "cpu", seed=1)
+    a = hs.generate_many([0, 2])
+    assert hs.generate_many([0, 2]) is a                       # same clients, same state: cached
+    assert hs.generate_many([2, 0]) is not a                   # other order: recomputed
+    snap = hs.snapshot()
+    hs.train([0], {0: a[0] + 0.1})
+    b = hs.generate_many([0, 2])
+    assert not torch.equal(a, b)                               # trained: new state
+    hs.restore(snap)
+    assert torch.equal(hs.generate_many([0, 2]), a)            # restored: recomputed from the old state
+    hs.load_arena(snap + 0.0)
+    assert hs.generate_many([0, 2]) is not a

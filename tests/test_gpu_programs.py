@@ -132,10 +132,11 @@ def test_adam_clients_vector_and_scalar_paths(gpu, P, skip, sgd):
         assert torch.equal(res[0][:, skip[0]:skip[1]], p0[:, skip[0]:skip[1]])
 
 
-def test_layernorm_fwd_bwd(gpu):
+@pytest.mark.parametrize("stride", [64, 67])  # 67: rows not 16-B aligned -> the scalar-access kernel path
+def test_layernorm_fwd_bwd(gpu, stride):
     C, R = 2, 300
     g = torch.Generator().manual_seed(2)
-    x, a, dy = (torch.randn(C, R, 64, generator=g) for _ in range(3))
+    x, a, dy = (torch.randn(C, R, stride, generator=g)[:, :, :64] for _ in range(3))
     gam, bet = 1 + 0.1 * torch.randn(C, 64, generator=g), 0.1 * torch.randn(C, 64, generator=g)
     cg, cc = _ctl(C)
     res = []
