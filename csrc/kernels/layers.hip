@@ -988,6 +988,15 @@ int tsgemm_try(const AflGemm& g, hipStream_t s) {
 int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
   if (g.splitk > 1 && g.accum != 2) return (int)hipErrorInvalidValue;
+  if (!g.no_ts && g.asum && g.N >= 256 && g.sAk == 1) {
+    // N = 256: the fused column sums' 16 extra VGPRs drop k_tsgemm<16, 2> to one wave per SIMD
+    // (HAR FFN-down dX 0.41 -> 0.64 ms); a separate column-sum pass (~0.09 ms) is cheaper there
+    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s);
+    if (e) return e;
+    AflGemm g2 = g;
+    g2.asum = nullptr;
+    return afl_bgemm(g2, s);
+  }
   if (!g.no_ts && tsgemm_try(g, s) == 0) return launched();
   if (g.asum) {  // the 64x64-tile kernel re-reads A per column tile: column sums as a separate pass
     if (g.sAk != 1) return (int)hipErrorInvalidValue;
