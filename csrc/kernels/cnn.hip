@@ -106,24 +106,42 @@ __device__ void cnn_fwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
   float* xs = (float*)(smem + F_X);
   const long wo = (long)c * a.sWc;
   const unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
-  if (tid < MT) xs[tid] = tid < M ? br.x[(long)c * br.sXc + row0 + tid] : 0.f;
+  // Global loads up front, back to back (the tile's x, conv1 weights, every bias, conv2's B fragments):
+  // the tile then waits for one round trip instead of one per dependent load.  conv3's fragments are
+  // issued right after conv2's MFMAs and arrive behind its epilogue and the second im2col.
+  const float xv = br.x[(long)c * br.sXc + row0 + min(tid & (MT - 1), M - 1)];
+  const int o1 = tid & 31;
+  const float w10 = br.W1[wo + o1 * 3], w11 = br.W1[wo + o1 * 3 + 1], w12 = br.W1[wo + o1 * 3 + 2],
+              b1o = br.b1[wo + o1];
+  // conv2 tiling: wave -> m-tile (wave & 3), n-tiles 2 * (wave >> 2) + {0, 1};
+  // conv3 tiling: wave -> m-tiles 2 * (wave & 1) + {0, 1}, n-tiles 2 * (wave >> 1) + {0, 1}
+  const int mt2 = (wave & 3) * 16, nt2 = (wave >> 2) * 32, mt3 = (wave & 1) * 32, nt3 = (wave >> 1) * 32;
+  s8v w2f[3][2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2f[k][j] = gfrag(img + WI_W2, 96, nt2 + j * 16, k * 32, lane);
+  float b2v[2], b3v[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    b2v[j] = br.b2[wo + nt2 + j * 16 + (lane & 15)];
+    b3v[j] = br.b3[wo + nt3 + j * 16 + (lane & 15)];
+  }
+  if (tid < MT) xs[tid] = tid < M ? xv : 0.f;
   __syncthreads();
   // conv1 (1 -> 32) on VALU
   {
-    const float* W1 = br.W1 + wo;
-    const int o = tid & 31;
-    const float w0 = W1[o * 3], w1 = W1[o * 3 + 1], w2 = W1[o * 3 + 2], bo = br.b1[wo + o];
     for (int m = tid >> 5; m < MT; m += NT / 32) {
       const int l = m % L;
       float v = 0.f;
       if (m < M) {
-        float s = bo + w1 * xs[m];
-        if (l > 0) s += w0 * xs[m - 1];
-        if (l < L - 1) s += w2 * xs[m + 1];
+        float s = b1o + w11 * xs[m];
+        if (l > 0) s += w10 * xs[m - 1];
+        if (l < L - 1) s += w12 * xs[m + 1];
         v = relu(s);
-        br.h1[(cb + row0 + m) * 32 + o] = v;
+        br.h1[(cb + row0 + m) * 32 + o1] = v;
       }
-      h1f[m * F_LH1 + o] = v;
+      h1f[m * F_LH1 + o1] = v;
     }
   }
   __syncthreads();
@@ -140,24 +158,27 @@ __device__ void cnn_fwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
     d[2] = bfu(c2);
   }
   __syncthreads();
-  // conv2: [64 x 96] . W2^T -> [64 x 64]; wave -> m-tile (wave & 3), n-tiles 2*(wave >> 2) + {0,1}
+  // conv2: [64 x 96] . W2^T -> [64 x 64]
+  s8v w3f[6][2];
   {
-    const int mt = (wave & 3) * 16;
     f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int k0 = 0; k0 < 96; k0 += 32) {
-      const s8v af = frag(A2, F_LD2, mt, k0, lane);
+    for (int k = 0; k < 3; ++k) {
+      const s8v af = frag(A2, F_LD2, mt2, k * 32, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = mfma32(af, gfrag(img + WI_W2, 96, ((wave >> 2) * 2 + j) * 16, k0, lane), acc[j]);
+      for (int j = 0; j < 2; ++j) acc[j] = mfma32(af, w2f[k][j], acc[j]);
     }
 #pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w3f[k][j] = gfrag(img + WI_W3, 192, nt3 + j * 16, k * 32, lane);
+#pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = ((wave >> 2) * 2 + j) * 16 + (lane & 15);
-      const float bn = br.b2[wo + n];
+      const int n = nt2 + j * 16 + (lane & 15);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = mt + 4 * (lane >> 4) + e;
-        const float v = m < M ? relu(acc[j][e] + bn) : 0.f;
+        const int m = mt2 + 4 * (lane >> 4) + e;
+        const float v = m < M ? relu(acc[j][e] + b2v[j]) : 0.f;
         h2f[m * F_LH2 + n] = v;
         if (m < M) br.h2[(cb + row0 + m) * 64 + n] = v;
       }
@@ -176,32 +197,36 @@ __device__ void cnn_fwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
     d[2] = bfu(c2);
   }
   __syncthreads();
-  // conv3: [64 x 192] . W3^T -> [64 x 128]; wave -> m-tile (wave & 3), n-tiles 4*(wave >> 2) + 0..3
+  // conv3: [64 x 192] . W3^T -> [64 x 128], 2 x 2 tiles per wave
   {
-    const int mt = (wave & 3) * 16;
-    f4v acc[4];
+    f4v acc[2][2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int k0 = 0; k0 < 192; k0 += 32) {
-      const s8v af = frag(A3, F_LD3, mt, k0, lane);
+      for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = mfma32(af, gfrag(img + WI_W3, 192, ((wave >> 2) * 4 + j) * 16, k0, lane), acc[j]);
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s8v af = frag(A3, F_LD3, mt3 + i * 16, k * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af, w3f[k][j], acc[i][j]);
+      }
     }
     __syncthreads();  // h3f overwrites A3 / h2f
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = ((wave >> 2) * 4 + j) * 16 + (lane & 15);
-      const float bn = br.b3[wo + n];
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = mt + 4 * (lane >> 4) + e;
-        const float v = m < M ? relu(acc[j][e] + bn) : 0.f;
-        h3f[m * F_LH3 + n] = v;
-        if (m < M) br.h3[(cb + row0 + m) * 128 + n] = v;
+      for (int j = 0; j < 2; ++j) {
+        const int n = nt3 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = mt3 + i * 16 + 4 * (lane >> 4) + e;
+          const float v = m < M ? relu(acc[i][j][e] + b3v[j]) : 0.f;
+          h3f[m * F_LH3 + n] = v;
+          if (m < M) br.h3[(cb + row0 + m) * 128 + n] = v;
+        }
       }
-    }
   }
   __syncthreads();
   // AdaptiveAvgPool1d(4) + dropout -> concat columns col0 + ch*4 + p
@@ -247,70 +272,123 @@ __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned short* dh3b = (unsigned short*)(smem + B_DH3);
   float* dc2 = (float*)(smem + B_DC2);
+  float* gs = (float*)(smem + B_DC2);  // [R][512] pooled-gradient slice, dead before dcols2 lands there
   unsigned short* dh2b = (unsigned short*)(smem + B_DH2);
   float* dc1 = (float*)(smem + B_DC1);
   const unsigned short* img = a.wimg + ((long)c * 2 + blockIdx.y) * WI_SIZE;
-  // relu' masks of h2 / h1 for the two col2im phases, loaded now: their global-load latency then hides behind
-  // the dh3 and dcols2 phases instead of following a barrier (bit i: element e = tid + i * NT of that phase)
+  // Every global load the tile needs before its first GEMM is issued up front, back to back and without
+  // branches (row indices clamped into the tile, the values of rows >= M are never used): the tile's
+  // dcat slice, h3 for relu' and the dcols2 B fragments.  One round trip
+  // instead of a serialized load -> wait -> store chain per element.
+  constexpr int RMAX = MT / L;
+  constexpr int NG = (RMAX * 128 + NT - 1) / NT;  // float4s of the dcat slice per thread
+  f4v gv[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int q = tid + i * NT, r = min(q >> 7, nb - 1);
+    gv[i] = *(const f4v*)(a.dcat + (long)c * a.sCatc + (long)(b0 + r) * a.sCatr + br.col0 + (q & 127) * 4);
+  }
+  f4v h3v[MT * 32 / NT];  // element group q = tid + i * NT: row q >> 5, channels 4 * (q & 31) .. +3
+#pragma unroll
+  for (int i = 0; i < MT * 32 / NT; ++i) {
+    const int q = tid + i * NT, m = min(q >> 5, M - 1);
+    h3v[i] = *(const f4v*)(br.h3 + (cbase + row0 + m) * 128 + (q & 31) * 4);
+  }
+  // dcols2 tiling: wave -> m-tiles 2 * (wave & 1) + {0, 1}, n-tiles 3 * (wave >> 1) + {0, 1, 2}
+  const int mt2 = (wave & 1) * 32, nt2 = (wave >> 1) * 48;
+  s8v w3f[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w3f[k][j] = gfrag(img + WI_W3T, 128, nt2 + j * 16, k * 32, lane);
+  // pooled gradient slice: gs[r][ch * 4 + p] = dropout'(dcat[b0 + r][col0 + ch * 4 + p]) / |bin p|
+  const bool dr = a.drop.thr16 != 0;
+  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int q = tid + i * NT, r = q >> 7;
+    if (r >= nb) continue;
+    f4v g = gv[i];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      g[p] *= 1.f / (float)(bin_hi(p, L) - bin_lo(p, L));
+      if (dr)
+        g[p] *= afl_keep(key, br.layer, (uint32_t)(b0 + r), (uint32_t)(br.col0 + (q & 127) * 4 + p), a.drop.thr16)
+                    ? a.drop.inv_keep
+                    : 0.f;
+    }
+    *(f4v*)(gs + r * 512 + (q & 127) * 4) = g;
+  }
+  __syncthreads();
+  // dh3 = relu'(h3) * pool'(dropout'(dcat)), four channels per thread step (float4 rows)
+#pragma unroll
+  for (int i = 0; i < MT * 32 / NT; ++i) {
+    const int q = tid + i * NT, m = q >> 5, ch = (q & 31) * 4;
+    f4v s = f4v{0.f, 0.f, 0.f, 0.f};
+    if (m < M) {
+      const int r = m / L, l = m - r * L;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f4v gp = *(const f4v*)(gs + r * 512 + (ch + k) * 4);  // the channel's 4 bins
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          if (l >= bin_lo(p, L) && l < bin_hi(p, L)) s[k] += gp[p];
+        if (!(h3v[i][k] > 0.f)) s[k] = 0.f;
+      }
+      *(f4v*)(br.dh3 + (cbase + row0 + m) * 128 + ch) = s;
+    }
+    typedef unsigned short u4v __attribute__((ext_vector_type(4)));
+    *(u4v*)(dh3b + m * B_LD3 + ch) = u4v{bfu(s[0]), bfu(s[1]), bfu(s[2]), bfu(s[3])};
+  }
+  // relu' masks of h2 / h1 for the two col2im phases, in flight during dcols2 (bit i: element e = tid + i * NT of that phase)
   uint32_t m2 = 0, m1 = 0;
   {
     float h2v[MT * 64 / NT], h1v[MT * 32 / NT];
 #pragma unroll
     for (int i = 0; i < MT * 64 / NT; ++i) {
-      const int e = tid + i * NT, m = e >> 6, ci = e & 63;
-      h2v[i] = m < M ? br.h2[(cbase + row0 + m) * 64 + ci] : 0.f;
+      const int e = tid + i * NT, m = min(e >> 6, M - 1), ci = e & 63;
+      h2v[i] = br.h2[(cbase + row0 + m) * 64 + ci];
     }
 #pragma unroll
     for (int i = 0; i < MT * 32 / NT; ++i) {
-      const int e = tid + i * NT, m = e >> 5, ci = e & 31;
-      h1v[i] = m < M ? br.h1[(cbase + row0 + m) * 32 + ci] : 0.f;
+      const int e = tid + i * NT, m = min(e >> 5, M - 1), ci = e & 31;
+      h1v[i] = br.h1[(cbase + row0 + m) * 32 + ci];
     }
 #pragma unroll
     for (int i = 0; i < MT * 64 / NT; ++i) m2 |= (h2v[i] > 0.f ? 1u : 0u) << i;
 #pragma unroll
     for (int i = 0; i < MT * 32 / NT; ++i) m1 |= (h1v[i] > 0.f ? 1u : 0u) << i;
   }
-  // dh3 = relu'(h3) * pool'(dropout'(dcat))
-  const bool dr = a.drop.thr16 != 0;
-  const uint32_t key = dr ? afl_hash32(a.drop.seeds[c], (uint32_t)(a.drop.stepctl ? *a.drop.stepctl : 0)) : 0u;
-  for (int e = tid; e < MT * 128; e += NT) {
-    const int m = e >> 7, ch = e & 127;
-    float sum = 0.f;
-    if (m < M) {
-      const int r = m / L, l = m - r * L, b = b0 + r;
-      const float* dcr = a.dcat + (long)c * a.sCatc + (long)b * a.sCatr;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int lo = bin_lo(p, L), hi = bin_hi(p, L);
-        if (l >= lo && l < hi) {
-          const int col = br.col0 + ch * 4 + p;
-          float g = dcr[col] / (float)(hi - lo);
-          if (dr) g *= afl_keep(key, br.layer, (uint32_t)b, (uint32_t)col, a.drop.thr16) ? a.drop.inv_keep : 0.f;
-          sum += g;
-        }
-      }
-      if (!(br.h3[(cbase + row0 + m) * 128 + ch] > 0.f)) sum = 0.f;
-      br.dh3[(cbase + row0 + m) * 128 + ch] = sum;
-    }
-    dh3b[m * B_LD3 + ch] = bfu(sum);
-  }
   __syncthreads();
-  // dcols2 = dh3 . W3 : [64 x 128] . (W3^T image [192 x 128])^T -> [64 x 192]; 48 tiles, 6 per wave
+  // dcols2 = dh3 . W3 : [64 x 128] . (W3^T image [192 x 128])^T -> [64 x 192]; 48 tiles, 2 x 3 per wave
+  s8v w2f[2][3];
   {
-    const int mt = (wave & 3) * 16, nb0 = (wave >> 2) * 6;
-    f4v acc[6];
+    f4v acc[2][3];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int k0 = 0; k0 < 128; k0 += 32) {
-      const s8v af = frag(dh3b, B_LD3, mt, k0, lane);
+      for (int j = 0; j < 3; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 6; ++j) acc[j] = mfma32(af, gfrag(img + WI_W3T, 128, (nb0 + j) * 16, k0, lane), acc[j]);
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s8v af = frag(dh3b, B_LD3, mt2 + i * 16, k * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma32(af, w3f[k][j], acc[i][j]);
+      }
     }
+    // dcols1's B fragments, in flight during this epilogue and the col2im phase
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
+    for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dc2[(mt + 4 * (lane >> 4) + e) * B_LC2 + (nb0 + j) * 16 + (lane & 15)] = acc[j][e];
+      for (int j = 0; j < 3; ++j) w2f[k][j] = gfrag(img + WI_W2T, 64, ((wave >> 2) * 3 + j) * 16, k * 32, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          dc2[(mt2 + i * 16 + 4 * (lane >> 4) + e) * B_LC2 + nt2 + j * 16 + (lane & 15)] = acc[i][j][e];
   }
   __syncthreads();
   // col2im + relu'(h2) -> dh2
@@ -336,10 +414,10 @@ __device__ void cnn_bwd_tile(const AflCnnTowers& a, const AflCnnBranch& br, unsi
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k0 = 0; k0 < 64; k0 += 32) {
-      const s8v af = frag(dh2b, B_LD2, mt, k0, lane);
+    for (int k = 0; k < 2; ++k) {
+      const s8v af = frag(dh2b, B_LD2, mt, k * 32, lane);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) acc[j] = mfma32(af, gfrag(img + WI_W2T, 64, (nb0 + j) * 16, k0, lane), acc[j]);
+      for (int j = 0; j < 3; ++j) acc[j] = mfma32(af, w2f[k][j], acc[j]);
     }
     __syncthreads();  // dc1 overwrites dc2 (read by other waves' col2im above: already fenced) — keep order
 #pragma unroll
@@ -399,40 +477,51 @@ __device__ void conv_dw_tile(const AflConvDw& a, const AflConvDwJob& J, int t, u
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  // software pipeline: the next k-step's global loads are in flight during this step's MFMAs
-  float va[8], vb[8];
-  auto load = [&](int m0) {
+  // software pipeline: three k-steps' global loads in flight (register ring), LDS double-buffered so a
+  // k-step needs one barrier; a k-step then costs its LDS + MFMA latency instead of a memory round trip
+  float va[3][8], vb[3][8];
+  auto load = [&](float* pa_, float* pb_, int m0) {
     int l = (m0 + sm0) % L;  // position within the sample, advanced incrementally
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + sm0 + i;
       const bool mok = m < me;
-      va[i] = (mok && ook) ? dh[(long)m * J.Cout + o0 + so] : 0.f;
+      pa_[i] = (mok && ook) ? dh[(long)m * J.Cout + o0 + so] : 0.f;
       const int lj = l + jj - 1;
-      vb[i] = (mok && kok && lj >= 0 && lj < L) ? hp[(long)(m + jj - 1) * J.Cin + ci] : 0.f;
+      pb_[i] = (mok && kok && lj >= 0 && lj < L) ? hp[(long)(m + jj - 1) * J.Cin + ci] : 0.f;
       l = (l == L - 1) ? 0 : l + 1;
     }
   };
-  load(mb);
-  for (int m0 = mb; m0 < me; m0 += DW_K) {
-    s8v pa, pb;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      pa[i] = (short)bfu(va[i]);
-      pb[i] = (short)bfu(vb[i]);
-      bsum += va[i];
+  for (int r = 0; r < 3; ++r)
+    if (mb + r * DW_K < me) load(va[r], vb[r], mb + r * DW_K);
+  int buf = 0;
+  for (int m0 = mb; m0 < me; m0 += 3 * DW_K) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ms = m0 + r * DW_K;
+      if (ms >= me) break;  // uniform over the workgroup
+      s8v pa, pb;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        pa[i] = (short)bfu(va[r][i]);
+        pb[i] = (short)bfu(vb[r][i]);
+        bsum += va[r][i];
+      }
+      if (ms + 3 * DW_K < me) load(va[r], vb[r], ms + 3 * DW_K);
+      unsigned short* Ab = As + buf * (DW_T * DW_LD);
+      unsigned short* Bb = Bs + buf * (DW_T * DW_LD);
+      *(s8v*)(Ab + so * DW_LD + sm0) = pa;
+      *(s8v*)(Bb + so * DW_LD + sm0) = pb;
+      __syncthreads();  // also orders this buffer's reuse two k-steps later behind every wave's reads
+      const s8v a0 = frag(Ab, DW_LD, wm, 0, lane), a1 = frag(Ab, DW_LD, wm + 16, 0, lane);
+      const s8v b0 = frag(Bb, DW_LD, wn, 0, lane), b1 = frag(Bb, DW_LD, wn + 16, 0, lane);
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+      buf ^= 1;
     }
-    __syncthreads();
-    *(s8v*)(As + so * DW_LD + sm0) = pa;
-    *(s8v*)(Bs + so * DW_LD + sm0) = pb;
-    __syncthreads();
-    if (m0 + DW_K < me) load(m0 + DW_K);
-    const s8v a0 = frag(As, DW_LD, wm, 0, lane), a1 = frag(As, DW_LD, wm + 16, 0, lane);
-    const s8v b0 = frag(Bs, DW_LD, wn, 0, lane), b1 = frag(Bs, DW_LD, wn + 16, 0, lane);
-    acc[0][0] = mfma32(a0, b0, acc[0][0]);
-    acc[0][1] = mfma32(a0, b1, acc[0][1]);
-    acc[1][0] = mfma32(a1, b0, acc[1][0]);
-    acc[1][1] = mfma32(a1, b1, acc[1][1]);
   }
   float* gW = J.gW + (long)c * a.sGc;
 #pragma unroll
@@ -454,8 +543,8 @@ __device__ void conv_dw_tile(const AflConvDw& a, const AflConvDwJob& J, int t, u
 }
 
 __global__ void __launch_bounds__(256) k_conv_dw(AflConvDw a) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[DW_T * DW_LD];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[DW_T * DW_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short As[2 * DW_T * DW_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2 * DW_T * DW_LD];
   __shared__ float bred[4][DW_T];
   int jb = 0;
   while (jb + 1 < a.njobs && (int)blockIdx.x >= a.job[jb + 1].tile_base) ++jb;
@@ -756,6 +845,11 @@ int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
+  // float4 rows of dcat / h3 / dh3 (the kernel's staging loads and dh3 stores)
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(a.dcat) || a.sCatc % 4 || a.sCatr % 4) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < 2; ++i)
+    if (!al(a.br[i].h3) || !al(a.br[i].dh3) || a.br[i].col0 % 4) return (int)hipErrorInvalidValue;
   const int nt = max(a.br[0].ntiles, a.br[1].ntiles);
   hipLaunchKernelGGL(k_cnn_bwd, dim3(nt, 2, a.C), dim3(NT), B_TOTAL, s, a);
   return (int)hipGetLastError();

@@ -210,7 +210,7 @@ AflCnnBranch cnn_branch(const std::vector<torch::Tensor>& t, const std::vector<i
   TORCH_CHECK(t.size() == 13 && meta.size() == 3, "cnn tower: 13 tensors and [L, col0, layer] expected");
   AflCnnBranch br{};
   const int L = (int)meta[0];
-  TORCH_CHECK(L >= 2 && L <= 64, "cnn tower: 2 <= L <= 64");
+  TORCH_CHECK(L == 7 || L == 16, "cnn tower: the fused tower kernels are built for L = 7 (vitals) and 16 (labs)");
   const auto& x = t[0];
   dev(x, "x");
   const long C = x.size(0);
