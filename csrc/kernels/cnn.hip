@@ -589,7 +589,9 @@ constexpr int H_D2S = H_D3S + 128 * H_L3 * 2;     // d2   [128][72] bf16
 constexpr int H_DZ = H_D2S + 128 * H_L2 * 2;      // dz   [128] f32
 constexpr int H_GB = H_DZ + 128 * 4;              // gb2 [64] | gb1 [128] f32
 constexpr int H_RED = H_GB + 192 * 4;             // [8] f32
-constexpr int H_TOTAL = H_RED + 8 * 4;
+constexpr int H_WO = H_RED + 8 * 4;               // output-layer weights [32] f32
+constexpr int H_RED3 = H_WO + 32 * 4;             // gb3 | gWo | gbo partial sums [72] f32
+constexpr int H_TOTAL = H_RED3 + 72 * 4;
 static_assert(H_TOTAL <= 160 * 1024, "cnn head LDS");
 
 __device__ __forceinline__ float wsum(float x) {
@@ -612,36 +614,62 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
   float* gb2 = (float*)(smem + H_GB);
   float* gb1 = gb2 + 64;
   float* red = (float*)(smem + H_RED);
+  float* wos = (float*)(smem + H_WO);
+  float* red3 = (float*)(smem + H_RED3);
   const int c = blockIdx.x, B = h.B;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long wo = (long)c * h.sWc, go = (long)c * h.sGc;
-  // f1 = relu(z1 + b1) from the split-K fc1 pre-activation (16-B loads); z1 is zeroed behind the read
-  // so the next step's split-K accumulates into zeros without a fill launch
+  // Every global operand of the kernel is loaded up front, back to back: the z1 rows, b1, the fc2 / fc3
+  // weight images, the biases, the output layer and the step's batch metadata / labels.  The chain
+  // then waits for one round trip (the fc1 pre-activation rows) instead of one per dependent load.
   float* z1 = h.f1 + (long)c * B * 128;
-  for (int e = tid; e < 128 * 32; e += HNT) {
-    const int b = e >> 5, i = 4 * (e & 31);
-    f4v v = f4v{0.f, 0.f, 0.f, 0.f};
-    if (b < B) {
-      v = *(const f4v*)(z1 + (long)b * 128 + i);
-      *(f4v*)(z1 + (long)b * 128 + i) = f4v{0.f, 0.f, 0.f, 0.f};
-    }
-    unsigned short* d = f1s + b * H_L1 + i;
+  const int i1 = 4 * (tid & 31);  // this thread's f1 columns (e & 31 is constant over its elements)
+  f4v zv[128 * 32 / HNT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = bfu(b < B ? relu(v[q] + h.b1[wo + i + q]) : 0.f);
+  for (int q = 0; q < 128 * 32 / HNT; ++q) {
+    const int b = (tid + q * HNT) >> 5;
+    zv[q] = *(const f4v*)(z1 + (long)min(b, B - 1) * 128 + i1);
   }
-  // fc2 / fc3 weight images (bf16, 16-B loads)
-  {
-    const unsigned short* img = h.wimg + (long)c * WI_HEAD;
-    for (int e = tid; e < 64 * 16; e += HNT) {
-      const int r = e >> 4, k = 8 * (e & 15);
-      *(s8v*)(W2s + r * H_L1 + k) = *(const s8v*)(img + r * 128 + k);
-    }
-    for (int e = tid; e < 32 * 8; e += HNT) {
-      const int r = e >> 3, k = 8 * (e & 7);
-      *(s8v*)(W3s + r * H_L2 + k) = *(const s8v*)(img + 64 * 128 + r * 64 + k);
-    }
+  const float b1v[4] = {h.b1[wo + i1], h.b1[wo + i1 + 1], h.b1[wo + i1 + 2], h.b1[wo + i1 + 3]};
+  const unsigned short* himg = h.wimg + (long)c * WI_HEAD;
+  s8v w2v[2], w3v;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + q * HNT;
+    w2v[q] = *(const s8v*)(himg + (e >> 4) * 128 + 8 * (e & 15));
   }
-  for (int e = tid; e < 192; e += HNT) gb2[e] = 0.f;
+  w3v = *(const s8v*)(himg + 64 * 128 + (min(tid, 255) >> 3) * 64 + 8 * (tid & 7));
+  float b2v[4], b3v[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b2v[j] = h.b2[wo + 16 * j + (lane & 15)];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b3v[j] = h.b3[wo + 16 * j + (lane & 15)];
+  const float wov = h.Wo[wo + (tid & 31)], bov = h.bo[wo];
+  const int s = h.stepctl ? *h.stepctl : 0;
+  const int bs = s < h.S ? h.bsz[(long)s * h.C + c] : 0;
+  const bool act = bs >= 2 && h.failed[c] == 0;
+  const int ep = s < h.S ? h.epoch[(long)s * h.C + c] : 0, nbc = h.nb[c];
+  const float yv = h.y[(long)c * B + min(tid & 127, B - 1)];
+  // f1 = relu(z1 + b1) from the split-K fc1 pre-activation; z1 is zeroed behind the read so the next
+  // step's split-K accumulates into zeros without a fill launch
+#pragma unroll
+  for (int q = 0; q < 128 * 32 / HNT; ++q) {
+    const int b = (tid + q * HNT) >> 5;
+    if (b < B) *(f4v*)(z1 + (long)b * 128 + i1) = f4v{0.f, 0.f, 0.f, 0.f};
+    unsigned short* d = f1s + b * H_L1 + i1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = bfu(b < B ? relu(zv[q][k] + b1v[k]) : 0.f);
+  }
+  // fc2 / fc3 weight images into LDS; the output layer's weights beside them
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + q * HNT;
+    *(s8v*)(W2s + (e >> 4) * H_L1 + 8 * (e & 15)) = w2v[q];
+  }
+  if (tid < 256) *(s8v*)(W3s + (tid >> 3) * H_L2 + 8 * (tid & 7)) = w3v;
+  if (tid < 32) wos[tid] = wov;
+  if (tid < 192) gb2[tid] = 0.f;
+  if (tid < 72) red3[tid] = 0.f;
   __syncthreads();
   // fc2: [128 x 128] . W2^T -> [128 x 64]; wave -> m-tile w, n-tiles 0..3
   {
@@ -658,9 +686,8 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = 16 * j + (lane & 15);
-      const float bn = h.b2[wo + n];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) f2s[(m0 + 4 * (lane >> 4) + e) * H_L2 + n] = bfu(relu(acc[j][e] + bn));
+      for (int e = 0; e < 4; ++e) f2s[(m0 + 4 * (lane >> 4) + e) * H_L2 + n] = bfu(relu(acc[j][e] + b2v[j]));
     }
   }
   __syncthreads();
@@ -677,25 +704,21 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = 16 * j + (lane & 15);
-      const float bn = h.b3[wo + n];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) f3f[(m0 + 4 * (lane >> 4) + e) * H_F3 + n] = relu(acc[j][e] + bn);
+      for (int e = 0; e < 4; ++e) f3f[(m0 + 4 * (lane >> 4) + e) * H_F3 + n] = relu(acc[j][e] + b3v[j]);
     }
   }
   __syncthreads();
   // output logit + sigmoid-BCE (same arithmetic as k_bce)
-  const int s = h.stepctl ? *h.stepctl : 0;
-  const int bs = s < h.S ? h.bsz[(long)s * h.C + c] : 0;
-  const bool act = bs >= 2 && h.failed[c] == 0;
   float zb = 0.f, lb = 0.f;
   if (tid < 128) {
-    float acc = h.bo[wo];
-    for (int j = 0; j < 32; ++j) acc += f3f[tid * H_F3 + j] * h.Wo[wo + j];
+    float acc = bov;
+    for (int j = 0; j < 32; ++j) acc += f3f[tid * H_F3 + j] * wos[j];
     zb = acc;
     if (h.z && tid < B) h.z[(long)c * B + tid] = zb;
     if (act && tid < bs) {
       const float p = 1.f / (1.f + expf(-zb));
-      const float t = h.y[(long)c * B + tid];
+      const float t = yv;
       lb = -(t * fmaxf(logf(p), -100.f) + (1.f - t) * fmaxf(log1pf(-p), -100.f));
       if (p != p) lb = p;
     }
@@ -710,7 +733,7 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
     if (act && !nan && tid < bs) {
       const float p = 1.f / (1.f + expf(-zb));
       const float w = p * (1.f - p);
-      g = (p - h.y[(long)c * B + tid]) / fmaxf(w, 1e-12f) * w / (float)bs;
+      g = (p - yv) / fmaxf(w, 1e-12f) * w / (float)bs;
     }
     dz[tid] = g;
   }
@@ -718,28 +741,42 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
     if (nan)
       h.failed[c] = 1;
     else
-      h.losses[(long)c * h.E + h.epoch[(long)s * h.C + c]] += loss / (float)h.nb[c];
+      h.losses[(long)c * h.E + ep] += loss / (float)nbc;
   }
   __syncthreads();
   // d3 = dz wo^T * relu'(f3); output-layer and fc3-bias gradients
   for (int e = tid; e < 128 * 32; e += HNT) {
     const int b = e >> 5, j = e & 31;
-    d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * h.Wo[wo + j] : 0.f);
+    d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * wos[j] : 0.f);
   }
-  if (tid < 32) {
-    float a = 0.f, w = 0.f;
-    for (int b = 0; b < 128; ++b) {
-      a += f3f[b * H_F3 + tid] > 0.f ? dz[b] : 0.f;
-      w += dz[b] * f3f[b * H_F3 + tid];
+  // output-layer / fc3-bias gradients over the 128 rows: thread (j = tid & 31, rows 8 * (tid >> 5) ..)
+  // partials, the row groups folded by one lane swap and LDS atomics (red3 zeroed before the loss barrier)
+  {
+    const int j = tid & 31, r0 = 8 * (tid >> 5);
+    float a = 0.f, w = 0.f, z = 0.f;
+#pragma unroll
+    for (int b = r0; b < r0 + 8; ++b) {
+      const float f = f3f[b * H_F3 + j], d = dz[b];
+      a += f > 0.f ? d : 0.f;
+      w += d * f;
+      z += d;
     }
-    h.gb3[go + tid] = a * h.Wo[wo + tid];
-    h.gWo[go + tid] = w;
-  } else if (tid == 64) {
-    float a = 0.f;
-    for (int b = 0; b < 128; ++b) a += dz[b];
-    h.gbo[go] = a;
+    a += __shfl_xor(a, 32, 64);
+    w += __shfl_xor(w, 32, 64);
+    z += __shfl_xor(z, 32, 64);
+    if (lane < 32) {
+      atomicAdd(red3 + j, a);
+      atomicAdd(red3 + 32 + j, w);
+      if (j == 0) atomicAdd(red3 + 64, z);
+    }
   }
   __syncthreads();
+  if (tid < 32) {
+    h.gb3[go + tid] = red3[tid] * wos[tid];
+    h.gWo[go + tid] = red3[32 + tid];
+  } else if (tid == 64) {
+    h.gbo[go] = red3[64];
+  }
   // dW3 [32 x 64] = d3^T f2 ; wave -> o-tile (w >> 2), i-tile (w & 3)
   {
     const int o0 = (wave >> 2) * 16, i0 = (wave & 3) * 16;
