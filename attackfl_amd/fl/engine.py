@@ -275,8 +275,12 @@ class FLEngine:
                                     self._pth(True), defer=True)
         elif self.global_params is not None:
             layout = self.layout
+            # deferred too: an immediate copy let the writer thread's torch.save (GIL-bound, ~0.5 ms) run
+            # in the gap between two rounds' training launches and stall the next round's preparation;
+            # kicked after the next launch it runs while the GPU trains.  global_params is replaced, never
+            # updated in place, so the submitted tensor stays valid until the copy.
             self.ckpt_writer.submit("global", self.global_params, lambda f: layout.unflatten(f, clone=False),
-                                    self._pth(False))
+                                    self._pth(False), defer=True)
 
     # ---- resumable run state (new: the reference persists only the model) ----
     def _state_paths(self):
