@@ -218,6 +218,20 @@ class FLEngine:
         eligible = (self.mode == "fedavg" and all(ci.attack is None for ci in self.table)
                     and not cfg.hyper_detection.get("enable", False))
         self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1))
+        # speculative next-round launch (run_round): single rank, replicated-state modes whose retry of a
+        # failed round relaunches exactly the same client work (no attackers / detection / hypernetwork,
+        # START from the in-memory global model), no exact resume sidecars
+        self._spec = None
+        self._val_stream = None
+        self._sel_cache = None
+        self._meta_host = None
+        self._has_attackers = any(ci.attack is not None for ci in self.table)
+        self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
+                             and self.world == 1 and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
+                             and all(ci.attack is None for ci in self.table)
+                             and not cfg.hyper_detection.get("enable", False) and not cfg.load_parameters
+                             and not cfg.engine.get("save-state", False) and not self.phase_sync
+                             and self.trainer is not None)
         if cfg.engine.get("resume", False):
             self.load_state()
         self.logger.log_info("### Application start ###\n")
@@ -400,6 +414,10 @@ class FLEngine:
         return self._side
 
     def _local_work(self, genuine: Dict[int, Optional[torch.Tensor]]) -> torch.Tensor:
+        return self._finish_local(self._launch_local(genuine))
+
+    def _launch_local(self, genuine: Dict[int, Optional[torch.Tensor]]) -> dict:
+        """Prepare this rank's clients for the round and enqueue the genuine clients' training (async)."""
         tq = time.perf_counter()
         cfg = self.cfg
         dev = self.device
@@ -478,6 +496,18 @@ class FLEngine:
                                           seeds_dev=tseed_d if self._dev_seed is not _no_dev_seed else None)
         self.ckpt_writer.kick()  # last round's deferred checkpoint copy overlaps this round's training
         tp1 = time.perf_counter()
+        return {"block": block, "attack_jobs": attack_jobs, "ready": ready, "pending": pending, "params": params
+                if train_rows else None, "in_place": in_place, "rows_d": rows_d, "n_local": n_local,
+                "meta": meta, "train_rows": train_rows, "t": (tq, tq1, tq2, tp0, tp1)}
+
+    def _finish_local(self, st: dict) -> torch.Tensor:
+        """Attackers' math (side stream), then wait for the training launch and fill the update block."""
+        block, attack_jobs, ready, pending = st["block"], st["attack_jobs"], st["ready"], st["pending"]
+        params, in_place, rows_d, n_local = st["params"], st["in_place"], st["rows_d"], st["n_local"]
+        tq, tq1, tq2, tp0, tp1 = st["t"]
+        dev = self.device
+        hm = st["meta"]  # host mirror of the block's meta columns (ok filled in below): no device read needed
+        tw = time.perf_counter()  # a speculative launch (run_round) may have been enqueued long before
         if attack_jobs:
             # the attackers do not train: their math runs on a side stream while the genuine clients'
             # training launch occupies its own CUs (the reference runs every client concurrently too)
@@ -492,6 +522,7 @@ class FLEngine:
                     if res.ok and res.params is not None:
                         block[j, :self.P] = res.params
                         block[j, self.P + 1] = 1.0
+                        hm[j, 1] = 1.0
                     self._attack_info = res.info
                     if self.verbose:
                         print_with_color(f"[===] Client {i} attacks with {atk.mode} {res.info}", "red")
@@ -501,6 +532,8 @@ class FLEngine:
         if pending is not None:
             oks, losses = pending.result()
             tp3 = time.perf_counter()
+            for j, o in zip(st["train_rows"], oks):
+                hm[j, 1] = 1.0 if o else 0.0
             if in_place:
                 block[:n_local, :self.P] = self.local_params[:n_local]
                 okv = block[:n_local, self.P + 1]
@@ -517,8 +550,9 @@ class FLEngine:
         else:
             tp3 = time.perf_counter()
         self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_prep_host": tq1 - tq, "t_lw_prep_upload": tq2 - tq1,
-                          "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tp1,
+                          "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tw,
                           "t_lw_wait": tp3 - tp2, "t_lw_post": time.perf_counter() - tp3}
+        self._meta_host = hm
         return block
 
     # ------------------------------------------------------------------------------------------
@@ -597,20 +631,30 @@ class FLEngine:
             print_with_color(f"Start training round {self.round_no}", "yellow")
         self._attack_info = None
         with trace.range("fl/local"):
-            genuine = self._genuine_for_attackers()
-            block = self._local_work(genuine)
-            self._sync()
+            st, self._spec = self._spec, None
+            if st is None:
+                st = self._launch_local(self._genuine_for_attackers())
+            block = self._finish_local(st)
+            if self.world > 1 or self.phase_sync or self.fast_fedavg:
+                self._sync()
         t1 = time.perf_counter()
         if self.fast_fedavg:
             return self._finish_fedavg_allreduce(block, t0, t1)
         trace.push("fl/gather")
         allb = self.comm.all_gather_rows(block)                        # [world*slots, P+META]
-        rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
-        idx = torch.tensor(rows, device=allb.device, dtype=torch.long)
+        key = tuple(self.selected)
+        if self._sel_cache is None or self._sel_cache[0] != key:
+            rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
+            self._sel_cache = (key, rows, torch.tensor(rows, device=allb.device, dtype=torch.long))
+        _, rows, idx = self._sel_cache
         sel = allb.index_select(0, idx)
         U = sel[:, :self.P].contiguous()
-        meta = sel[:, self.P:].float().cpu()
-        self._sync()
+        if self.world == 1:  # every row is local: the host already knows the meta columns
+            meta = torch.from_numpy(self._meta_host[rows])
+        else:
+            meta = sel[:, self.P:].float().cpu()
+        if self.world > 1 or self.phase_sync:
+            self._sync()
         trace.pop()
         t2 = time.perf_counter()
         results = meta[:, 1] > 0.5
@@ -629,6 +673,26 @@ class FLEngine:
         if info.get("agg_failed"):
             round_ok = False
         t3 = time.perf_counter()
+        # Speculative next launch: the next round's local training is enqueued right behind the
+        # aggregate, BEFORE this round's validation / checkpoint, which then run on a side stream next to it
+        # (the trainer occupies a few CUs).  Valid whatever validation decides: a failed round is retried
+        # from the same global model with the same client counters, i.e. exactly this launch.
+        vstream = None
+        if self._speculative and round_ok and self.rounds_left > 1:
+            agg_done = torch.cuda.Event()
+            agg_done.record(torch.cuda.current_stream(self.device))
+            self._spec = self._launch_local(self._genuine_for_attackers())
+            if self._val_stream is None:
+                self._val_stream = torch.cuda.Stream(device=self.device)
+            vstream = self._val_stream
+            vstream.wait_event(agg_done)
+        with (torch.cuda.stream(vstream) if vstream is not None else contextlib.nullcontext()):
+            rec = self._finish_round(U, attackers, stored, snapshot, info, round_ok, t0, t1, t2, t3)
+        if vstream is not None:
+            self.ckpt_writer.kick()  # the next launch is already in: copy + write while it trains
+        return rec
+
+    def _finish_round(self, U, attackers, stored, snapshot, info, round_ok, t0, t1, t2, t3) -> dict:
         trace.push("fl/validate")
 
         # ---- leader: detection + validation; control broadcast ----
@@ -669,7 +733,10 @@ class FLEngine:
 
         # ---- genuine pool for the next START (non-attacker rows stored this round) ----
         keep = [k for k in range(stored) if not bool(attackers[k])]
-        self.genuine_pool = U[keep].clone() if keep else None
+        if self._has_attackers:  # only attackers ever read the pool
+            if torch.cuda.is_available() and U.is_cuda:
+                U.record_stream(torch.cuda.current_stream(U.device))  # read here, maybe on the validation stream
+            self.genuine_pool = U[keep].clone() if keep else None
 
         if round_ok:
             with trace.range("fl/checkpoint"):
@@ -770,6 +837,9 @@ class FLEngine:
         return self.history
 
     def close(self):
+        if self._spec is not None:  # a speculative launch nobody consumed (run ended by max_rounds)
+            st, self._spec = self._spec, None
+            self._finish_local(st)
         self.ckpt_writer.close()
         self.metrics.close()
         if hasattr(self.logger, "close"):
