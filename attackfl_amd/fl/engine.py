@@ -219,8 +219,8 @@ class FLEngine:
                     and not cfg.hyper_detection.get("enable", False))
         self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1))
         # speculative next-round launch (run_round): single rank, replicated-state modes whose retry of a
-        # failed round relaunches exactly the same client work (no attackers / detection / hypernetwork,
-        # START from the in-memory global model), no exact resume sidecars
+        # failed round relaunches exactly the same client work (no detection / hypernetwork, START from the
+        # in-memory global model; attackers draw from the pool set before the launch), no resume sidecars
         self._spec = None
         self._val_stream = None
         self._sel_cache = None
@@ -228,7 +228,6 @@ class FLEngine:
         self._has_attackers = any(ci.attack is not None for ci in self.table)
         self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
                              and self.world == 1 and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
-                             and all(ci.attack is None for ci in self.table)
                              and not cfg.hyper_detection.get("enable", False) and not cfg.load_parameters
                              and not cfg.engine.get("save-state", False) and not self.phase_sync
                              and self.trainer is not None)
@@ -677,6 +676,10 @@ class FLEngine:
         # aggregate, BEFORE this round's validation / checkpoint, which then run on a side stream next to it
         # (the trainer occupies a few CUs).  Valid whatever validation decides: a failed round is retried
         # from the same global model with the same client counters, i.e. exactly this launch.
+        # ---- genuine pool for the next START (non-attacker rows stored this round; only attackers read it) ----
+        if self._has_attackers:
+            keep = [k for k in range(stored) if not bool(attackers[k])]
+            self.genuine_pool = U[keep].clone() if keep else None
         vstream = None
         if self._speculative and round_ok and self.rounds_left > 1:
             agg_done = torch.cuda.Event()
@@ -731,12 +734,6 @@ class FLEngine:
             self.hyper.restore(snapshot)
         t4 = time.perf_counter()
 
-        # ---- genuine pool for the next START (non-attacker rows stored this round) ----
-        keep = [k for k in range(stored) if not bool(attackers[k])]
-        if self._has_attackers:  # only attackers ever read the pool
-            if torch.cuda.is_available() and U.is_cuda:
-                U.record_stream(torch.cuda.current_stream(U.device))  # read here, maybe on the validation stream
-            self.genuine_pool = U[keep].clone() if keep else None
 
         if round_ok:
             with trace.range("fl/checkpoint"):
