@@ -225,6 +225,7 @@ class FLEngine:
         self._val_stream = None
         self._sel_cache = None
         self._meta_host = None
+        self._plain_rows = False
         self._has_attackers = any(ci.attack is not None for ci in self.table)
         self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
                              and self.world == 1 and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
@@ -528,23 +529,31 @@ class FLEngine:
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
         tp2 = time.perf_counter()
+        # single rank, every local client trained in place, no attacker rows: the round reads the update
+        # matrix straight from local_params and the meta columns from the host mirror (run_round)
+        self._plain_rows = (pending is not None and in_place and not attack_jobs and self.world == 1
+                            and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
+                            and self._local_rows() == list(range(n_local)))
         if pending is not None:
             oks, losses = pending.result()
             tp3 = time.perf_counter()
             for j, o in zip(st["train_rows"], oks):
                 hm[j, 1] = 1.0 if o else 0.0
-            if in_place:
+            if self._plain_rows:
+                pass
+            elif in_place:
                 block[:n_local, :self.P] = self.local_params[:n_local]
                 okv = block[:n_local, self.P + 1]
             else:
                 self.local_params.index_copy_(0, rows_d, params)
                 block[rows_d, :self.P] = params
                 okv = None
-            ok_dev = pending.ok_device()
-            if ok_dev is not None and okv is not None:
-                okv.copy_(ok_dev > 0)
-            else:
-                block[rows_d, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=dev)
+            if not self._plain_rows:
+                ok_dev = pending.ok_device()
+                if ok_dev is not None and okv is not None:
+                    okv.copy_(ok_dev > 0)
+                else:
+                    block[rows_d, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=dev)
             self._last_losses = losses
         else:
             tp3 = time.perf_counter()
@@ -553,6 +562,15 @@ class FLEngine:
                           "t_lw_wait": tp3 - tp2, "t_lw_post": time.perf_counter() - tp3}
         self._meta_host = hm
         return block
+
+    def _local_rows(self) -> List[int]:
+        """Block rows of the selected clients (cached per selection)."""
+        key = tuple(self.selected)
+        if self._sel_cache is None or self._sel_cache[0] != key:
+            rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
+            idx = torch.tensor(rows, device=self.device, dtype=torch.long)
+            self._sel_cache = (key, rows, idx)
+        return self._sel_cache[1]
 
     # ------------------------------------------------------------------------------------------
     # SERVER
@@ -577,7 +595,10 @@ class FLEngine:
         if not res.ok:
             info["agg_failed"] = True
         elif res.params is not None:
-            self.global_params = res.params.to(torch.float32)
+            g = res.params.to(torch.float32)
+            if g.untyped_storage().data_ptr() == U.untyped_storage().data_ptr():
+                g = g.clone()  # a selected row (e.g. Krum) of U, which may be the live client models
+            self.global_params = g
         return info
 
     def _fltrust(self, U: torch.Tensor) -> torch.Tensor:
@@ -641,16 +662,17 @@ class FLEngine:
             return self._finish_fedavg_allreduce(block, t0, t1)
         trace.push("fl/gather")
         allb = self.comm.all_gather_rows(block)                        # [world*slots, P+META]
-        key = tuple(self.selected)
-        if self._sel_cache is None or self._sel_cache[0] != key:
-            rows = [self.table[i].owner * self.slots + self._slot_of(i) for i in self.selected]
-            self._sel_cache = (key, rows, torch.tensor(rows, device=allb.device, dtype=torch.long))
-        _, rows, idx = self._sel_cache
-        sel = allb.index_select(0, idx)
-        U = sel[:, :self.P].contiguous()
+        rows = self._local_rows()
+        idx = self._sel_cache[2]
         if self.world == 1:  # every row is local: the host already knows the meta columns
             meta = torch.from_numpy(self._meta_host[rows])
+            if self._plain_rows:
+                U = self.local_params[:len(rows)]  # the trained models ARE the update rows: no block copies
+            else:
+                U = allb.index_select(0, idx)[:, :self.P].contiguous()
         else:
+            sel = allb.index_select(0, idx)
+            U = sel[:, :self.P].contiguous()
             meta = sel[:, self.P:].float().cpu()
         if self.world > 1 or self.phase_sync:
             self._sync()

@@ -187,10 +187,12 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers):
     if model == "TransformerModel":  # the on-chip trainer is bit-reproducible
         assert h0 == h1
         assert torch.equal(p0, p1)
-    else:  # the CNN step's split-K GEMMs accumulate with atomics: run-to-run noise even between two serial
-        # runs (ROC-AUC ~0.51 after round 1 of this tiny setup moves by up to ~0.01 with it)
-        assert [ok for ok, _ in h1] == [ok for ok, _ in h0]
+    else:  # the CNN step's split-K GEMMs accumulate with atomics: two SERIAL runs already differ, so the
+        # speculative run must stay within that run-to-run noise (a race would be far outside it)
+        h2, p2 = run(False, "serial2")
+        assert [ok for ok, _ in h1] == [ok for ok, _ in h0] == [ok for ok, _ in h2]
+        noise = (p0 - p2).abs().mean().item()
+        assert (p0 - p1).abs().mean().item() <= 3 * noise + 1e-4, ((p0 - p1).abs().mean(), noise)
+        mnoise = max(abs(a - b) for (_, a), (_, b) in zip(h0, h2) if a is not None)
         for (_, a), (_, b) in zip(h0, h1):
-            assert (a is None) == (b is None) and (a is None or abs(a - b) < 2e-2), (h0, h1)
-        d = (p0 - p1).abs()  # Adam amplifies the noise on parameters with tiny second moments
-        assert d.mean() < 1e-3 and d.max() < 0.1, (d.mean(), d.max())
+            assert (a is None) == (b is None) and (a is None or abs(a - b) <= 3 * mnoise + 1e-3), (h0, h1, h2)
