@@ -655,7 +655,7 @@ class FLEngine:
             if st is None:
                 st = self._launch_local(self._genuine_for_attackers())
             block = self._finish_local(st)
-            if self.world > 1 or self.phase_sync or self.fast_fedavg:
+            if self.world > 1 or self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
                 self._sync()
         t1 = time.perf_counter()
         if self.fast_fedavg:
@@ -796,9 +796,10 @@ class FLEngine:
         with trace.range("fl/allreduce"):
             if self.world > 1:
                 self.comm.all_reduce_(red)
-            self._sync()
+            if self.phase_sync:
+                self._sync()
         t2 = time.perf_counter()
-        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters
+        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters (waits for the reduce)
         round_ok = int(fl[0]) == 0 and int(fl[1]) == len(self.selected)
         if round_ok:
             self.global_params = (red[:P] / red[P]).to(torch.float32)
