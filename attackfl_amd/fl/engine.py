@@ -219,16 +219,17 @@ class FLEngine:
                     and not cfg.hyper_detection.get("enable", False))
         self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1))
         # speculative next-round launch (run_round): single rank, replicated-state modes whose retry of a
-        # failed round relaunches exactly the same client work (no detection / hypernetwork, START from the
-        # in-memory global model; attackers draw from the pool set before the launch), no resume sidecars
+        # failed round relaunches exactly the same client work (no detection, START from the in-memory
+        # global model / hypernetwork; attackers draw from the pool set before the launch), no resume sidecars
         self._spec = None
         self._val_stream = None
+        self._start_ready = None
         self._sel_cache = None
         self._meta_host = None
         self._plain_rows = False
         self._has_attackers = any(ci.attack is not None for ci in self.table)
         self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
-                             and self.world == 1 and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
+                             and self.world == 1 and not self.fast_fedavg and self.mode != "FLTrust"
                              and not cfg.hyper_detection.get("enable", False) and not cfg.load_parameters
                              and not cfg.engine.get("save-state", False) and not self.phase_sync
                              and self.trainer is not None)
@@ -476,6 +477,11 @@ class FLEngine:
                     self.local_params[:len(js)].copy_(start)
                 else:
                     self.local_params.index_copy_(0, js_d, start.contiguous())
+        if self._speculative and dev.type == "cuda":
+            # START is generated (hyper: the memoised generate_many validation reuses): a speculative
+            # round's validation stream waits for this point, not for the training launched below
+            self._start_ready = torch.cuda.Event()
+            self._start_ready.record(torch.cuda.current_stream(dev))
         for j in faults:
             self.local_params[j, 0] = float("nan")
         block[:, self.P:] = meta_d
@@ -711,6 +717,7 @@ class FLEngine:
                 self._val_stream = torch.cuda.Stream(device=self.device)
             vstream = self._val_stream
             vstream.wait_event(agg_done)
+            vstream.wait_event(self._start_ready)
         with (torch.cuda.stream(vstream) if vstream is not None else contextlib.nullcontext()):
             rec = self._finish_round(U, attackers, stored, snapshot, info, round_ok, t0, t1, t2, t3)
         if vstream is not None:

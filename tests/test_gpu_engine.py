@@ -141,9 +141,11 @@ def test_deferred_checkpoint_copies_the_submitted_state(gpu, tmp_path):
     w.close()
 
 
-@pytest.mark.parametrize("model,attackers", [("TransformerModel", False), ("TransformerModel", True),
-                                             ("CNNModel", False)])
-def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers):
+@pytest.mark.parametrize("model,attackers,mode", [("TransformerModel", False, "fedavg"),
+                                                  ("TransformerModel", True, "fedavg"),
+                                                  ("TransformerModel", True, "hyper"), ("RNNModel", True, "hyper"),
+                                                  ("CNNModel", False, "fedavg")])
+def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode):
     """The next round's training enqueued before this round's validation (engine.speculative) gives the
     same rounds bit for bit as the serial schedule — including a round whose validation fails (the retry
     consumes the speculative launch) and one whose training fails (no speculation after it)."""
@@ -151,7 +153,7 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers):
 
     def run(spec, sub):
         d = {
-            "server": {"num-round": 4, "clients": 3, "mode": "fedavg", "model": model, "data-name": "ICU",
+            "server": {"num-round": 4, "clients": 3, "mode": mode, "model": model, "data-name": "ICU",
                        "data-distribution": {"num-data-range": [300, 500]}},
             "learning": {"epoch": 2, "batch-size": 128},
             "data": {"synthetic": True, "train-size": 4000, "test-size": 1000},
@@ -162,20 +164,22 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers):
         if attackers:  # client 2 runs Min-Max from its 2nd training round (pool drawn before the launch)
             d["server"]["random-seed"] = 11
         cfg = from_dict(d)
-        table = build_client_table(cfg, 1, parse_attackers("2:Min-Max:2") if attackers else None)
+        atk = "2:Min-Max:2" if mode == "fedavg" else "2:Opt-Fang:2"
+        table = build_client_table(cfg, 1, parse_attackers(atk) if attackers else None)
         eng = FLEngine(cfg, device="cuda", table=table, verbose=False)
         assert eng._speculative == spec
         calls = {"n": 0}
-        test = eng.validation.test
+        name = "test" if mode == "fedavg" else "test_hyper"
+        test = getattr(eng.validation, name)
 
-        def flaky(flat):  # the second validation fails once: that round is retried
+        def flaky(*a):  # the second validation fails once: that round is retried
             calls["n"] += 1
-            ok, m = test(flat)
+            ok, m = test(*a)
             return (False, m) if calls["n"] == 2 else (ok, m)
 
-        eng.validation.test = flaky
+        setattr(eng.validation, name, flaky)
         hist = eng.run()
-        out = eng.global_params.detach().cpu().clone()
+        out = (eng.global_params if mode == "fedavg" else eng.hyper.hnet.arena).detach().cpu().clone()
         eng.close()
         return [(r["ok"], None if r["metric"] != r["metric"] else r["metric"]) for r in hist], out
 
@@ -184,7 +188,7 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers):
     if not attackers:
         assert [ok for ok, _ in h0] == [True, False, True, False, True, True]
     assert sum(ok for ok, _ in h0) == 4
-    if model == "TransformerModel":  # the on-chip trainer is bit-reproducible
+    if model != "CNNModel":  # the on-chip trainers and the hyper server kernels are bit-reproducible
         assert h0 == h1
         assert torch.equal(p0, p1)
     else:  # the CNN step's split-K GEMMs accumulate with atomics: two SERIAL runs already differ, so the
