@@ -30,6 +30,8 @@ Extensions (all optional, defaults keep reference behaviour):
   max-retries: int                  (consecutive failed rounds before the run aborts)
   trace: bool                       (roctx ranges around every round phase; also ATTACKFL_TRACE=1)
   phase-sync: bool                  (synchronise after the aggregate so per-phase times are device times)
+  speculative: bool                 (default True: on one GPU rank, enqueue the next round's training
+                                    before this round's validation / checkpoint, which overlap it)
   fault-inject: [{client, round}]   (NaN-poison a client's model before that training round)
   save-state: bool                  (write {model}.state.pt + {model}.clients.r{rank}.pt every round)
   resume: bool                      (continue from those files: counters, RNGs, optimizer moments)
@@ -78,7 +80,8 @@ EXTENSION_DEFAULTS: Dict[str, Any] = {
              "har-train-size": 2048, "har-test-size": 512, "root": "."},
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
                "async-checkpoint": True, "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
-               "phase-sync": False, "fault-inject": [], "save-state": False, "resume": False},
+               "phase-sync": False, "fault-inject": [], "save-state": False, "resume": False,
+               "speculative": True},
 }
 
 
