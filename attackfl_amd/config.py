@@ -9,9 +9,12 @@ Extensions (all optional, defaults keep reference behaviour):
 ``comm:``
   backend: auto | nccl | gloo | loopback
   clients-per-rank: int (packed launcher; 0 = clients / world)
-  one-shot-allgather: bool  (IPC xGMI all-gather for small updates on a single node)
+  one-shot-allgather: auto | true | false  (IPC xGMI all-gather of the update blocks on one node:
+                            stream-ordered, no host staging; auto = on for GPU ranks of one host, verified
+                            collectively at setup with a fallback to the process group's all-gather)
   fedavg-allreduce: auto | true | false  (fedavg without attackers/detection: one all_reduce of
-                            [sum s_i w_i | sum s_i] instead of the update all-gather; auto = world > 1)
+                            [sum s_i w_i | sum s_i] instead of the update all-gather; auto = world > 1
+                            without the IPC path)
   timeout-s: collective timeout (failure detection)
   attackers: {client_index: {mode, round, args}}  (launcher-side attack assignment)
 ``data:``
@@ -30,8 +33,12 @@ Extensions (all optional, defaults keep reference behaviour):
   max-retries: int                  (consecutive failed rounds before the run aborts)
   trace: bool                       (roctx ranges around every round phase; also ATTACKFL_TRACE=1)
   phase-sync: bool                  (synchronise after the aggregate so per-phase times are device times)
-  speculative: bool                 (default True: on one GPU rank, enqueue the next round's training
+  speculative: bool                 (default True: on GPU ranks, enqueue the next round's training
                                     before this round's validation / checkpoint, which overlap it)
+  compat-har-train: bool            (True = reference train_HAR semantics: no size-1 batch skip, no NaN
+                                    abort, client.py:114-131)
+  compat-fedavg-alias: bool         (True = reproduce reference A-13: FedAvg writes the aggregate into the
+                                    first client's stored update, which attackers may receive as "genuine")
   fault-inject: [{client, round}]   (NaN-poison a client's model before that training round)
   save-state: bool                  (write {model}.state.pt + {model}.clients.r{rank}.pt every round)
   resume: bool                      (continue from those files: counters, RNGs, optimizer moments)
@@ -74,14 +81,14 @@ REFERENCE_DEFAULTS: Dict[str, Any] = {
 }
 
 EXTENSION_DEFAULTS: Dict[str, Any] = {
-    "comm": {"backend": "auto", "address": "", "port": 29517, "clients-per-rank": 0, "one-shot-allgather": False,
+    "comm": {"backend": "auto", "address": "", "port": 29517, "clients-per-rank": 0, "one-shot-allgather": "auto",
              "fedavg-allreduce": "auto", "timeout-s": 600, "attackers": {}},
     "data": {"synthetic": "auto", "train-size": 60000, "test-size": 10000, "seed": 1234,
              "har-train-size": 2048, "har-test-size": 512, "root": "."},
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
                "async-checkpoint": True, "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
                "phase-sync": False, "fault-inject": [], "save-state": False, "resume": False,
-               "speculative": True},
+               "speculative": True, "compat-har-train": False, "compat-fedavg-alias": False},
 }
 
 

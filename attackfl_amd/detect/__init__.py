@@ -22,7 +22,11 @@ HISTORY_LEN = 5
 START_ROUND = 18
 
 
-def cosine_anomaly(previous: np.ndarray, current: np.ndarray) -> bool:
+def _quiet(*_a, **_k):
+    return None
+
+
+def cosine_anomaly(previous: np.ndarray, current: np.ndarray, log=print_with_color) -> bool:
     hist = np.asarray(previous, dtype=np.float64)
     if hist.size == 0:
         return False
@@ -35,12 +39,12 @@ def cosine_anomaly(previous: np.ndarray, current: np.ndarray) -> bool:
     sigma = max(float(np.std(hist_cs)), 1e-6)
     flag = cs < mu - 2 * sigma
     if flag:
-        print_with_color("Anomalies detection !!!", "yellow")
+        log("Anomalies detection !!!", "yellow")
     return bool(flag)
 
 
 def dbscan_outliers(before: Sequence[np.ndarray], after: Sequence[np.ndarray], selected: Sequence[int],
-                    n_components: int = 3, eps: float = 0.008, min_samples: int = 3) -> List[int]:
+                    n_components: int = 3, eps: float = 0.008, min_samples: int = 3, log=print_with_color) -> List[int]:
     from sklearn.cluster import DBSCAN
     from sklearn.decomposition import PCA
 
@@ -51,18 +55,19 @@ def dbscan_outliers(before: Sequence[np.ndarray], after: Sequence[np.ndarray], s
     proj = PCA(n_components=k).fit_transform(delta)
     labels = DBSCAN(eps=eps, min_samples=min_samples).fit(proj).labels_
     out = [selected[i] for i in np.where(labels == -1)[0]]
-    print_with_color(f"DBSCAN outliers: {out}", "yellow")
+    log(f"DBSCAN outliers: {out}", "yellow")
     return out
 
 
 class HyperDetector:
     def __init__(self, n_clients: int, n_components: int = 3, eps: float = 0.007, min_samples: int = 3,
-                 save_path: str = "all_embeddings.npy"):
+                 save_path: str = "all_embeddings.npy", verbose: bool = True):
         self.hist: List[deque] = [deque(maxlen=HISTORY_LEN) for _ in range(n_clients)]
         self.n_components = n_components
         self.eps = eps
         self.min_samples = min_samples
         self.save_path = save_path
+        self.log = print_with_color if verbose else _quiet
 
     def step(self, round_no: int, selected: Sequence[int], embeddings: Dict[int, np.ndarray]) -> List[int]:
         """Feed this round's embeddings ([1, E] each); return the clients to remove."""
@@ -70,7 +75,7 @@ class HyperDetector:
         for i in selected:
             cur = np.asarray(embeddings[i], dtype=np.float32).reshape(1, -1)
             prev = np.vstack(self.hist[i]) if self.hist[i] else np.empty((0, cur.shape[1]))
-            if round_no >= START_ROUND and cosine_anomaly(prev, cur):
+            if round_no >= START_ROUND and cosine_anomaly(prev, cur, self.log):
                 flagged.append(i)
             self.hist[i].append(cur)
         if self.save_path:
@@ -81,5 +86,5 @@ class HyperDetector:
         if round_no < START_ROUND:
             return []
         outs = dbscan_outliers([h[-2] for h in self.hist], [h[-1] for h in self.hist], list(selected),
-                               self.n_components, self.eps, self.min_samples)
+                               self.n_components, self.eps, self.min_samples, self.log)
         return sorted(set(flagged) & set(outs))

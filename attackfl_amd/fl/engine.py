@@ -7,13 +7,16 @@ every rank runs:
 
   START  (replicated decisions: per-client parameters, attackers' genuine-model sample)
   LOCAL  (this rank's clients: fused training kernel for all genuine clients at once, attacks)
-  GATHER (one all-gather of fixed-layout ``[slots, P+4]`` blocks  == the UPDATE messages)
+  GATHER (one all-gather of fixed-layout ``[slots, W]`` blocks  == the UPDATE messages)
   SERVER (replicated aggregation/defense/hypernetwork update — deterministic kernels)
-  LEADER (validation, hyper-detection decision, checkpoint, app.log) -> control broadcast
+  CHECK  (replicated validation and hyper-detection decision; the leader logs and checkpoints)
   NEXT   (retry the same round on failure, exactly like the reference's ``round`` counter)
 
-Server state is replicated on every rank instead of living in one process, so the only
-traffic per round is the update all-gather plus a few-byte control broadcast.
+Server state is replicated on every rank instead of living in one process, and every decision that
+ends a round (validation, detection) is computed by deterministic kernels on identical inputs on
+every rank, so the only traffic per round is the update all-gather (or, for plain FedAvg over
+RCCL, one all-reduce): no control broadcast, and the next round's training can be enqueued before
+this round's validation at any world size (speculative launch, ``run_round``).
 """
 from __future__ import annotations
 
@@ -44,7 +47,7 @@ from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
 from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
 
-META = 4  # valid, result, size, is_attacker
+META = 4  # valid, result, size, is_attacker; then the client's per-epoch losses (E columns)
 
 
 class Staging:
@@ -158,6 +161,9 @@ class FLEngine:
         self.max_retries = int(cfg.engine.get("max-retries", 50))
         self.layout = ParamLayout.for_model(self.model_name)
         self.P = self.layout.P
+        self.E = cfg.epoch
+        # update block row: [P update | META | E epoch losses], padded to 16 bytes (aligned IPC pushes)
+        self.W = (self.P + META + self.E + 3) // 4 * 4
         self.dist = DistanceEngine(self.layout, cfg.engine.get("distance", "spectral"))
 
         # ---- logging (leader only, like the reference's single server process) ----
@@ -180,8 +186,10 @@ class FLEngine:
             self.train_table = DeviceTable(ds, self.device)
         self.trainer = make_trainer(cfg.engine.get("trainer", "auto"), self.model_name, self.data_name,
                                     self.train_table, self.device) if self.train_table is not None else None
+        # validation runs on EVERY rank: its kernels are deterministic and the global model is bit-identical
+        # on all ranks, so each rank reaches the leader's decision without a control broadcast
         self.validation = None
-        if cfg.validation and self.leader:
+        if cfg.validation:
             self.validation = Validation(self.model_name, self.data_name, self.logger, self.device, cfg.data,
                                          dataset=test_dataset, verbose=self.verbose)
         self.slots = max(sum(1 for ci in self.table if ci.owner == r) for r in range(self.world))
@@ -214,22 +222,27 @@ class FLEngine:
         self._phase_t: Dict[str, float] = {}
         # FedAvg fast path: with no attacker and no detection, the server needs only
         # sum_i s_i w_i and sum_i s_i -> ONE all_reduce of [P + 3] instead of the [N, P] all-gather
+        # auto = world > 1 without the IPC one-shot gather (which moves whole blocks in one stream-ordered hop
+        # and keeps FedAvg on the same deterministic kernel as a single rank)
         fa = str(cfg.comm.get("fedavg-allreduce", "auto")).lower()
         eligible = (self.mode == "fedavg" and all(ci.attack is None for ci in self.table)
                     and not cfg.hyper_detection.get("enable", False))
-        self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1))
-        # speculative next-round launch (run_round): single rank, replicated-state modes whose retry of a
-        # failed round relaunches exactly the same client work (no detection, START from the in-memory
-        # global model / hypernetwork; attackers draw from the pool set before the launch), no resume sidecars
+        self.fast_fedavg = eligible and (fa == "true" or (fa == "auto" and self.world > 1
+                                                          and not getattr(self.comm, "one_shot", False)))
+        # speculative next-round launch (run_round): replicated-state modes whose retry of a failed round
+        # relaunches exactly the same client work (no detection, START from the in-memory global model /
+        # hypernetwork; attackers draw from the pool set before the launch), no resume sidecars.  Any world
+        # size: validation is replicated, so no rank waits for another's decision before the next launch.
         self._spec = None
         self._val_stream = None
         self._start_ready = None
         self._sel_cache = None
         self._meta_host = None
         self._plain_rows = False
+        self._pending = None
         self._has_attackers = any(ci.attack is not None for ci in self.table)
         self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
-                             and self.world == 1 and not self.fast_fedavg and self.mode != "FLTrust"
+                             and self.mode != "FLTrust"
                              and not cfg.hyper_detection.get("enable", False) and not cfg.load_parameters
                              and not cfg.engine.get("save-state", False) and not self.phase_sync
                              and self.trainer is not None)
@@ -266,10 +279,13 @@ class FLEngine:
                     self.hyper.hnet.load_state_dict(hyper_ckpt)
                     print_with_color(f"Load state dict from hyper model: {self._pth(True)}", "yellow")
             hd = cfg.hyper_detection
-            if hd.get("enable", False) and self.leader:
+            if hd.get("enable", False):
+                # replicated like validation (the embeddings are bit-identical on every rank; PCA / DBSCAN are
+                # deterministic host code); only the leader writes all_embeddings.npy and prints
                 self.detector = HyperDetector(cfg.clients, int(hd.get("n_components", 3)), float(hd.get("eps", 0.007)),
                                               int(hd.get("min_samples", 3)),
-                                              save_path=os.path.join(self.ckpt_dir, "all_embeddings.npy"))
+                                              save_path=os.path.join(self.ckpt_dir, "all_embeddings.npy")
+                                              if self.leader else "", verbose=self.leader)
         if self.mode == "FLTrust":
             m = build_model(self.model_name, seed=self.seed + 77)
             self.fltrust_model = self.layout.flatten(m.state_dict(), device=self.device)
@@ -286,8 +302,10 @@ class FLEngine:
         if self.mode == "hyper":
             hnet = self.hyper.hnet
             # deferred: the arena's copy is issued after the next training launch (utils/ckpt.py)
+            if getattr(self, "_hyper_tail", None) is None:
+                self._hyper_tail = hnet.target_tail()
             self.ckpt_writer.submit("hyper", hnet.arena, lambda a: hnet.state_dict_of(a, clone=False),
-                                    self._pth(True), defer=True)
+                                    self._pth(True), defer=True, tail=self._hyper_tail)
         elif self.global_params is not None:
             layout = self.layout
             # deferred too: an immediate copy let the writer thread's torch.save (GIL-bound, ~0.5 ms) run
@@ -422,8 +440,8 @@ class FLEngine:
         tq = time.perf_counter()
         cfg = self.cfg
         dev = self.device
-        block = torch.zeros(self.slots, self.P + META, dtype=torch.float32, device=dev)
-        meta = np.zeros((self.slots, META), dtype=np.float32)  # host-built, uploaded once
+        block = torch.zeros(self.slots, self.W, dtype=torch.float32, device=dev)
+        meta = np.zeros((self.slots, META + self.E), dtype=np.float32)  # host-built, uploaded once (+ losses)
         lo, hi = cfg.data_range
         train_rows, train_nd, train_seeds = [], [], []
         attack_jobs = []
@@ -458,7 +476,7 @@ class FLEngine:
         js = [j for j, _ in started]
         plan_seeds = [sd * 1000003 + 17 for sd in train_seeds]
         meta_d, js_d, rows_d, pseed_d, nd_d, tseed_d = self._staging.upload([
-            meta, np.asarray(js, np.int64), np.asarray(train_rows, np.int64),
+            meta[:, :META], np.asarray(js, np.int64), np.asarray(train_rows, np.int64),
             np.asarray([(s & 0xFFFFFFFFFFFFFFFF) - (1 << 64) if (s & 0xFFFFFFFFFFFFFFFF) >= (1 << 63)
                         else (s & 0xFFFFFFFFFFFFFFFF) for s in plan_seeds], np.int64),
             np.asarray(train_nd, np.int32),
@@ -484,7 +502,7 @@ class FLEngine:
             self._start_ready.record(torch.cuda.current_stream(dev))
         for j in faults:
             self.local_params[j, 0] = float("nan")
-        block[:, self.P:] = meta_d
+        block[:, self.P:self.P + META] = meta_d
         tp0 = time.perf_counter()
         pending = None
         ready = None
@@ -540,27 +558,36 @@ class FLEngine:
         self._plain_rows = (pending is not None and in_place and not attack_jobs and self.world == 1
                             and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
                             and self._local_rows() == list(range(n_local)))
+        self._pending = pending
+        P, E = self.P, self.E
         if pending is not None:
-            oks, losses = pending.result()
+            ok_dev, loss_dev = pending.ok_device(), pending.losses_device()
+            # world > 1: the ok flags and losses travel in the block and the host learns every rank's meta from
+            # ONE read after the gather, so it does not wait for its own training here (one host round trip less)
+            host_wait = self.world == 1 or ok_dev is None or loss_dev is None
+            if host_wait:
+                oks, losses = pending.result()
+                for k, (j, o) in enumerate(zip(st["train_rows"], oks)):
+                    hm[j, 1] = 1.0 if o else 0.0
+                    hm[j, META:META + E] = np.asarray(losses[k], dtype=np.float32)[:E]
             tp3 = time.perf_counter()
-            for j, o in zip(st["train_rows"], oks):
-                hm[j, 1] = 1.0 if o else 0.0
             if self._plain_rows:
                 pass
             elif in_place:
-                block[:n_local, :self.P] = self.local_params[:n_local]
-                okv = block[:n_local, self.P + 1]
+                block[:n_local, :P] = self.local_params[:n_local]
+                if ok_dev is not None:
+                    block[:n_local, P + 1] = (ok_dev > 0).float()
+                else:
+                    block[:n_local, P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=dev)
+                block[:n_local, P + META:P + META + E] = (loss_dev if loss_dev is not None
+                                                         else losses.to(dev)).float()
             else:
                 self.local_params.index_copy_(0, rows_d, params)
-                block[rows_d, :self.P] = params
-                okv = None
-            if not self._plain_rows:
-                ok_dev = pending.ok_device()
-                if ok_dev is not None and okv is not None:
-                    okv.copy_(ok_dev > 0)
-                else:
-                    block[rows_d, self.P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=dev)
-            self._last_losses = losses
+                block[rows_d, :P] = params
+                okc = (ok_dev > 0).float() if ok_dev is not None else torch.tensor(
+                    [1.0 if o else 0.0 for o in oks], device=dev)
+                block[rows_d, P + 1] = okc
+                block[rows_d, P + META:P + META + E] = (loss_dev if loss_dev is not None else losses.to(dev)).float()
         else:
             tp3 = time.perf_counter()
         self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_prep_host": tq1 - tq, "t_lw_prep_upload": tq2 - tq1,
@@ -607,23 +634,37 @@ class FLEngine:
             self.global_params = g
         return info
 
+    def _fltrust_setup(self):
+        """Root set (first 200 test rows, ``server.py:290-293``), its device table and the server model's
+        trainer: built once and reused every round."""
+        if getattr(self, "_fl_root", None) is None:
+            from ..data import ICUData
+
+            root = resolve_dataset(self.data_name, "test", self.cfg.data, verbose=False)
+            if isinstance(root, ICUData):
+                root = ICUData(vitals=root.vitals[:200], labs=root.labs[:200], labels=root.labels[:200])
+            table = DeviceTable(root, self.device)
+            trainer = make_trainer(self.cfg.engine.get("trainer", "auto"), self.model_name, self.data_name, table,
+                                   self.device)
+            nd = min(200, table.n)
+            # DataLoader(batch_size=100, shuffle=False): the same in-order visit every epoch
+            order = torch.arange(nd, dtype=torch.int32, device=self.device)[None, None, :].expand(
+                1, self.cfg.epoch, nd).contiguous()
+            plan = Plan(order, torch.tensor([nd], dtype=torch.int32), self.cfg.epoch,
+                        nd_dev=torch.tensor([nd], dtype=torch.int32, device=self.device))
+            self._fl_root = (table, trainer, plan)
+        return self._fl_root
+
     def _fltrust(self, U: torch.Tensor) -> torch.Tensor:
-        """FLTrust with a server model trained on the first 200 test rows (``server.py:682-743``)."""
+        """FLTrust with a server model trained on the first 200 test rows (``server.py:682-743``).
+        Everything stays on the device: the server model's training is enqueued (its result is ignored,
+        like the reference's ``train_on_device`` return value), and the trust scores, norms and the
+        trust-weighted sum are device tensors; ``trust`` reaches the JSONL lazily after validation."""
         compat = bool(self.cfg.engine.get("compat-fltrust", False))
         g0 = self.global_params if self.global_params is not None else self.fltrust_model.clone()
-        root = resolve_dataset(self.data_name, "test", self.cfg.data, verbose=False)
-        from ..data import ICUData
-
-        if isinstance(root, ICUData):
-            root = ICUData(vitals=root.vitals[:200], labs=root.labs[:200], labels=root.labels[:200])
-        table = DeviceTable(root, self.device)
-        trainer = make_trainer(self.cfg.engine.get("trainer", "auto"), self.model_name, self.data_name, table,
-                               self.device)
+        _, trainer, plan = self._fltrust_setup()
         params = g0.clone()[None]
-        nd = min(200, table.n)
-        order = torch.arange(nd, dtype=torch.int32, device=self.device)[None, None, :].expand(1, self.cfg.epoch, nd)
-        plan = Plan(order.contiguous(), torch.tensor([nd], dtype=torch.int32), self.cfg.epoch)
-        trainer.train(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
+        trainer.launch(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
         server_new = params[0]
         g0_delta = server_new - g0
         if compat and self.global_params is None:
@@ -631,15 +672,15 @@ class FLEngine:
         deltas = U - g0[None, :]
         if compat:
             deltas = deltas - g0[None, :]   # A-10: the stored delta is reduced by g_0 a second time
-        norm_g0 = float(torch.linalg.vector_norm(g0_delta.double()))
-        norms = ops.row_norms(deltas).cpu()
-        cos = ops.cosine_to(deltas, g0_delta, eps=1e-8).cpu()
+        norm_g0 = torch.linalg.vector_norm(g0_delta.double())
+        norms = ops.row_norms(deltas).double()
+        cos = ops.cosine_to(deltas, g0_delta, eps=1e-8).double()
         trust = torch.clamp(cos, min=0.0)
         scale = (norm_g0 / (norms + 1e-6)) * trust
-        w = scale / (float(trust.sum()) + 1e-6)
-        agg = ops.weighted_rows(deltas, w.double())
-        self.fltrust_model = server_new.clone()
-        self._trust = trust.tolist()
+        w = scale / (trust.sum() + 1e-6)
+        agg = ops.weighted_rows(deltas, w)
+        self.fltrust_model = server_new
+        self._trust = trust
         return g0 + agg
 
     # ------------------------------------------------------------------------------------------
@@ -649,67 +690,84 @@ class FLEngine:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
-    def run_round(self) -> dict:
+    def run_round(self, last: bool = False) -> dict:
+        """One FL round.  ``last``: the caller will not run another round, so no speculative launch."""
         if not self._selection_done:
             self.client_selection()
         t0 = time.perf_counter()
         if self.verbose:
             print_with_color(f"Start training round {self.round_no}", "yellow")
         self._attack_info = None
+        self._trust = None
         with trace.range("fl/local"):
             st, self._spec = self._spec, None
             if st is None:
                 st = self._launch_local(self._genuine_for_attackers())
             block = self._finish_local(st)
-            if self.world > 1 or self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
+            if self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
                 self._sync()
         t1 = time.perf_counter()
-        if self.fast_fedavg:
-            return self._finish_fedavg_allreduce(block, t0, t1)
-        trace.push("fl/gather")
-        allb = self.comm.all_gather_rows(block)                        # [world*slots, P+META]
-        rows = self._local_rows()
-        idx = self._sel_cache[2]
-        if self.world == 1:  # every row is local: the host already knows the meta columns
-            meta = torch.from_numpy(self._meta_host[rows])
-            if self._plain_rows:
-                U = self.local_params[:len(rows)]  # the trained models ARE the update rows: no block copies
-            else:
-                U = allb.index_select(0, idx)[:, :self.P].contiguous()
-        else:
-            sel = allb.index_select(0, idx)
-            U = sel[:, :self.P].contiguous()
-            meta = sel[:, self.P:].float().cpu()
-        if self.world > 1 or self.phase_sync:
-            self._sync()
-        trace.pop()
-        t2 = time.perf_counter()
-        results = meta[:, 1] > 0.5
-        sizes = meta[:, 2].clone()
-        attackers = meta[:, 3] > 0.5
-        round_ok = bool(results.all())
-        # stored updates (arrival in client order; the reference stops storing after a failure)
+        P = self.P
+        snapshot = None
+        attackers = None
         stored = len(self.selected)
-        if not round_ok:
-            stored = int(torch.nonzero(~results)[0, 0])
-        snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) else None
-        with trace.range("fl/aggregate"):
-            info = self._aggregate(U, sizes, attackers, round_ok)
-            if self.phase_sync:  # per-phase timings only; otherwise validation queues behind it
+        if self.fast_fedavg:
+            U = None
+            round_ok, meta = self._fedavg_allreduce(block)
+            info = {"path": "fedavg-allreduce"}
+            t2 = t3 = time.perf_counter()
+        else:
+            trace.push("fl/gather")
+            allb = self.comm.all_gather_rows(block)                        # [world*slots, W]
+            rows = self._local_rows()
+            idx = self._sel_cache[2]
+            if self.world == 1:  # every row is local: the host already knows the meta columns
+                meta = torch.from_numpy(self._meta_host[rows])
+                if self._plain_rows:
+                    U = self.local_params[:len(rows)]  # the trained models ARE the update rows: no block copies
+                else:
+                    U = allb.index_select(0, idx)[:, :P].contiguous()
+            else:
+                sel = allb.index_select(0, idx)
+                U = sel[:, :P].contiguous()
+                # the round's ONE host read: every client's [valid, result, size, attacker | losses] (it also
+                # waits for the gather, i.e. for the slowest rank's clients)
+                meta = sel[:, P:P + META + self.E].double().cpu()
+                self.comm.check()
+                if self._pending is not None:
+                    self._pending.result()  # the training has finished by now: surfaces hand-off timeouts
+            if self.phase_sync:
                 self._sync()
-        if info.get("agg_failed"):
-            round_ok = False
-        t3 = time.perf_counter()
-        # Speculative next launch: the next round's local training is enqueued right behind the
-        # aggregate, BEFORE this round's validation / checkpoint, which then run on a side stream next to it
-        # (the trainer occupies a few CUs).  Valid whatever validation decides: a failed round is retried
-        # from the same global model with the same client counters, i.e. exactly this launch.
+            trace.pop()
+            t2 = time.perf_counter()
+            results = meta[:, 1] > 0.5
+            sizes = meta[:, 2].clone()
+            attackers = meta[:, 3] > 0.5
+            round_ok = bool(results.all())
+            # stored updates (arrival in client order; the reference stops storing after a failure)
+            if not round_ok:
+                stored = int(torch.nonzero(~results)[0, 0])
+            snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) \
+                else None
+            with trace.range("fl/aggregate"):
+                info = self._aggregate(U, sizes, attackers, round_ok)
+                if self.phase_sync:  # per-phase timings only; otherwise validation queues behind it
+                    self._sync()
+            if info.get("agg_failed"):
+                round_ok = False
+            t3 = time.perf_counter()
+        self._round_meta = meta
         # ---- genuine pool for the next START (non-attacker rows stored this round; only attackers read it) ----
-        if self._has_attackers:
+        if self._has_attackers and attackers is not None:
             keep = [k for k in range(stored) if not bool(attackers[k])]
             self.genuine_pool = U[keep].clone() if keep else None
+        # Speculative next launch: the next round's local training is enqueued right behind the aggregate,
+        # BEFORE this round's validation / checkpoint, which then run on a side stream next to it (the
+        # trainer occupies a few CUs).  Valid whatever validation decides: a failed round is retried from the
+        # same global model with the same client counters, i.e. exactly this launch.  Every rank decides
+        # the same (replicated validation), so the ranks' launches and gathers stay in lockstep.
         vstream = None
-        if self._speculative and round_ok and self.rounds_left > 1:
+        if self._speculative and round_ok and self.rounds_left > 1 and not last:
             agg_done = torch.cuda.Event()
             agg_done.record(torch.cuda.current_stream(self.device))
             self._spec = self._launch_local(self._genuine_for_attackers())
@@ -719,106 +777,44 @@ class FLEngine:
             vstream.wait_event(agg_done)
             vstream.wait_event(self._start_ready)
         with (torch.cuda.stream(vstream) if vstream is not None else contextlib.nullcontext()):
-            rec = self._finish_round(U, attackers, stored, snapshot, info, round_ok, t0, t1, t2, t3)
+            rec = self._finish_round(snapshot, info, round_ok, t0, t1, t2, t3)
         if vstream is not None:
             self.ckpt_writer.kick()  # the next launch is already in: copy + write while it trains
         return rec
 
-    def _finish_round(self, U, attackers, stored, snapshot, info, round_ok, t0, t1, t2, t3) -> dict:
-        trace.push("fl/validate")
+    def _client_losses(self) -> Optional[List[Optional[List[float]]]]:
+        """Per-epoch training loss of every selected client (None for attackers and failed clients), from
+        the round's meta rows (host mirror on one rank, the gathered block's loss columns otherwise)."""
+        meta = getattr(self, "_round_meta", None)
+        if meta is None or meta.shape[1] < META + self.E:
+            return None
+        return [None if (meta[r, 3] > 0.5 or meta[r, 1] < 0.5)
+                else [round(float(x), 6) for x in meta[r, META:META + self.E]] for r in range(len(self.selected))]
 
-        # ---- leader: detection + validation; control broadcast ----
+    def _finish_round(self, snapshot, info, round_ok, t0, t1, t2, t3) -> dict:
+        trace.push("fl/validate")
+        # ---- replicated detection + validation: every rank computes the same decision ----
         removed: List[int] = []
         metric = float("nan")
-        if self.leader:
-            if self.detector is not None:
-                embs = {i: self.hyper.embedding(i).cpu().numpy()[None, :] for i in self.selected}
-                removed = self.detector.step(self.round_no, self.selected, embs)
-            if self.validation is not None and round_ok:
-                if self.mode == "hyper":
-                    round_ok, metric = self.validation.test_hyper(self.hyper, len(self.selected))
+        if self.detector is not None:
+            embs = {i: self.hyper.embedding(i).cpu().numpy()[None, :] for i in self.selected}
+            removed = self.detector.step(self.round_no, self.selected, embs)
+        if self.validation is not None and round_ok:
+            if self.mode == "hyper":
+                round_ok, metric = self.validation.test_hyper(self.hyper, len(self.selected))
+            else:
+                if self.global_params is None:
+                    round_ok = False
                 else:
-                    if self.global_params is None:
-                        round_ok = False
-                    else:
-                        round_ok, metric = self.validation.test(self.global_params)
-        ctrl = torch.full((2 + self.n_clients,), -1.0, dtype=torch.float64)
-        if self.leader:
-            ctrl[0] = 1.0 if round_ok else 0.0
-            ctrl[1] = float(len(removed))
-            for k, r in enumerate(removed):
-                ctrl[2 + k] = float(r)
-        if self.world > 1:  # one host -> device -> all ranks -> host trip; a single rank keeps it on the host
-            ctrl = ctrl.to(self.device)
-            self.comm.broadcast_(ctrl, src=0)
-            ctrl = ctrl.cpu()
+                    round_ok, metric = self.validation.test(self.global_params)
         trace.pop()
-        round_ok = bool(ctrl[0] > 0.5)
-        removed = [int(ctrl[2 + k]) for k in range(int(ctrl[1]))]
         if removed:
             for r in removed:
-                print_with_color(f"Removing anomaly {r}, rolling back", "yellow")
+                if self.verbose:
+                    print_with_color(f"Removing anomaly {r}, rolling back", "yellow")
                 if r in self.selected:
                     self.selected.remove(r)
             self.hyper.restore(snapshot)
-        t4 = time.perf_counter()
-
-
-        if round_ok:
-            with trace.range("fl/checkpoint"):
-                self.save_checkpoint()
-                self.rounds_left -= 1
-                if self.cfg.engine.get("save-state", False):
-                    self.round_no += 1
-                    self.save_state()
-                    self.round_no -= 1
-        elif self.verbose:
-            print_with_color("Training failed!", "yellow")
-        rec = {"round": self.round_no, "ok": round_ok, "metric": metric, **getattr(self, "_lw_times", {}),
-               "t_local": t1 - t0, "t_gather": t2 - t1,
-               "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_round": time.perf_counter() - t0,
-               "n_selected": len(self.selected), "removed": removed}
-        if self._attack_info:
-            rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
-        lazy = info.pop("_lazy", None)
-        if lazy is not None:
-            info.update(lazy())
-        rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list))})
-        self.metrics.write(rec)
-        self.history.append(rec)
-        if round_ok:
-            self.round_no += 1
-        return rec
-
-    def _finish_fedavg_allreduce(self, block: torch.Tensor, t0: float, t1: float) -> dict:
-        """FedAvg round over one all_reduce: [sum s_i w_i | sum s_i | #failed | #reported] (fp64)."""
-        P = self.P
-        present = block[:, P] > 0.5
-        size = torch.where(present, block[:, P + 2], torch.zeros_like(block[:, P + 2])).double()
-        red = torch.zeros(P + 3, dtype=torch.float64, device=block.device)
-        red[:P] = (size[:, None] * block[:, :P].double()).sum(0)
-        red[P] = size.sum()
-        red[P + 1] = (present & (block[:, P + 1] < 0.5)).double().sum()
-        red[P + 2] = present.double().sum()
-        with trace.range("fl/allreduce"):
-            if self.world > 1:
-                self.comm.all_reduce_(red)
-            if self.phase_sync:
-                self._sync()
-        t2 = time.perf_counter()
-        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters (waits for the reduce)
-        round_ok = int(fl[0]) == 0 and int(fl[1]) == len(self.selected)
-        if round_ok:
-            self.global_params = (red[:P] / red[P]).to(torch.float32)
-        t3 = time.perf_counter()
-        metric = float("nan")
-        with trace.range("fl/validate"):
-            if self.leader and self.validation is not None and round_ok:
-                round_ok, metric = self.validation.test(self.global_params)
-            if self.world > 1:  # a single rank keeps the decision on the host
-                ctrl = torch.tensor([1.0 if round_ok else 0.0], dtype=torch.float64, device=self.device)
-                self.comm.broadcast_(ctrl, src=0)
-                round_ok = bool(ctrl.item() > 0.5)
         t4 = time.perf_counter()
         if round_ok:
             with trace.range("fl/checkpoint"):
@@ -834,12 +830,63 @@ class FLEngine:
         rec = {"round": self.round_no, "ok": round_ok, "metric": metric, **getattr(self, "_lw_times", {}),
                "t_local": t1 - t0, "t_gather": t2 - t1,
                "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_checkpoint": t5 - t4, "t_round": t5 - t0,
-               "n_selected": len(self.selected), "removed": [], "path": "fedavg-allreduce"}
+               "n_selected": len(self.selected), "removed": removed}
+        if self._attack_info:
+            rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
+        lazy = info.pop("_lazy", None)
+        if lazy is not None:
+            info.update(lazy())
+        if self._trust is not None:
+            info["trust"] = [round(float(x), 6) for x in self._trust.tolist()]
+        rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list, str))})
+        losses = self._client_losses()
+        if losses is not None:
+            rec["client_loss"] = losses
+            if self.verbose:
+                self._print_losses(losses)
         self.metrics.write(rec)
         self.history.append(rec)
         if round_ok:
             self.round_no += 1
         return rec
+
+    def _print_losses(self, losses) -> None:
+        """Reference client prints (``client.py:109`` ICU: ``Loss {mean}`` per epoch; ``client.py:130`` HAR:
+        ``Epoch {e}, Loss: {sum:.4f}``), one block per client, from the server's view of the round."""
+        for i, ls in zip(self.selected, losses):
+            if ls is None:
+                continue
+            if self.data_name == "HAR":
+                nb = max(1, -(-int(self._round_meta[self.selected.index(i), 2]) // self.cfg.batch_size))
+                for e, l in enumerate(ls):
+                    print(f"[client {i}] Epoch {e + 1}, Loss: {l * nb:.4f}")
+            else:
+                for l in ls:
+                    print_with_color(f"[client {i}] Loss {l} ", "yellow")
+
+    def _fedavg_allreduce(self, block: torch.Tensor):
+        """FedAvg over one all_reduce: [sum s_i w_i | sum s_i | #failed | #reported] (fp64).  Returns
+        (round ok, host meta of this rank's rows); sets ``global_params`` on success."""
+        P = self.P
+        present = block[:, P] > 0.5
+        size = torch.where(present, block[:, P + 2], torch.zeros_like(block[:, P + 2])).double()
+        red = torch.zeros(P + 3, dtype=torch.float64, device=block.device)
+        red[:P] = (size[:, None] * block[:, :P].double()).sum(0)
+        red[P] = size.sum()
+        red[P + 1] = (present & (block[:, P + 1] < 0.5)).double().sum()
+        red[P + 2] = present.double().sum()
+        with trace.range("fl/allreduce"):
+            if self.world > 1:
+                self.comm.all_reduce_(red)
+            if self.phase_sync:
+                self._sync()
+        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters (waits for the reduce)
+        round_ok = int(fl[0]) == 0 and int(fl[1]) == len(self.selected)
+        if round_ok:
+            self.global_params = (red[:P] / red[P]).to(torch.float32)
+        # per-client meta (losses for the JSONL): only a single rank knows every row without another read
+        meta = torch.from_numpy(self._meta_host[self._local_rows()]) if self.world == 1 else None
+        return round_ok, meta
 
     def _slot_of(self, i: int) -> int:
         owner = self.table[i].owner
@@ -851,7 +898,8 @@ class FLEngine:
         fails = 0
         done = 0
         while self.rounds_left > 0:
-            rec = self.run_round()
+            # the caller's last round launches nothing speculatively (no un-aggregated extra training)
+            rec = self.run_round(last=max_rounds is not None and done + 1 >= max_rounds)
             done += 1
             fails = 0 if rec["ok"] else fails + 1
             if self.max_retries and fails > self.max_retries:
@@ -864,9 +912,14 @@ class FLEngine:
         return self.history
 
     def close(self):
-        if self._spec is not None:  # a speculative launch nobody consumed (run ended by max_rounds)
+        if self._spec is not None:
+            # a speculative launch nobody consumed (bench.py drives run_round itself): wait for the GPU work,
+            # skip the block / meta bookkeeping.  Client state (local_params, training_round, client RNGs) is
+            # then one round ahead of history / round_no.
             st, self._spec = self._spec, None
-            self._finish_local(st)
+            if st["pending"] is not None:
+                st["pending"].result()
+            self._sync()
         self.ckpt_writer.close()
         self.metrics.close()
         if hasattr(self.logger, "close"):

@@ -48,14 +48,19 @@ class Pending:
     Trainers whose work is enqueued asynchronously (fused, graph) return before the GPU finishes, so the
     engine can run the attackers' math on a side stream while the genuine clients train."""
 
-    def __init__(self, finish, ok_dev: Optional[torch.Tensor] = None):
+    def __init__(self, finish, ok_dev: Optional[torch.Tensor] = None, losses_dev: Optional[torch.Tensor] = None):
         self._finish = finish
         self._res = None
         self._ok_dev = ok_dev
+        self._losses_dev = losses_dev
 
     def ok_device(self) -> Optional[torch.Tensor]:
         """Per-client success on the device (> 0 = ok) without a host round trip, when the trainer has it."""
         return self._ok_dev
+
+    def losses_device(self) -> Optional[torch.Tensor]:
+        """Per-client per-epoch mean losses ``[C, E]`` on the device, when the trainer has them."""
+        return self._losses_dev
 
     def result(self) -> Tuple[List[bool], torch.Tensor]:
         if self._res is None:
@@ -329,7 +334,7 @@ class FusedTrainer:
             okh, lh = self.T.finish(ok, losses, what)
             return [bool(x) for x in okh.tolist()], lh
 
-        return Pending(fin, ok)
+        return Pending(fin, ok, losses)
 
 
 class GraphTrainer:
@@ -372,7 +377,7 @@ class GraphTrainer:
                         print_with_color(f"Loss {float(lh[c, e]):.6f} ", "yellow")
             return [bool(x) for x in okh.tolist()], lh
 
-        return Pending(fin, (ok == 0).to(torch.int32))
+        return Pending(fin, (ok == 0).to(torch.int32), losses)
 
 
 def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable, device, verbose=False):

@@ -169,9 +169,15 @@ class PackedHyperNet:
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         return self.state_dict_of(self.arena.detach().cpu())
 
+    def target_tail(self) -> torch.Tensor:
+        """The (constant) target model flattened in state_dict order: appended behind a host copy of the arena
+        it lets ``state_dict_of`` return views of ONE storage (the checkpoint writer's zip-template path)."""
+        return torch.cat([t.reshape(-1) for t in self.target_sd.values()])
+
     def state_dict_of(self, arena: torch.Tensor, clone: bool = True) -> "OrderedDict[str, torch.Tensor]":
         """Reference ``HyperNetwork`` state_dict built from a host copy of the arena (views when
-        ``clone`` is False: the caller owns ``arena`` until the dict is consumed)."""
+        ``clone`` is False: the caller owns ``arena`` until the dict is consumed).  If ``arena`` also holds
+        ``target_tail()`` behind the arena, the ``target_model.*`` entries are views of it too."""
         def v(name):
             off, shp = self.slots[name]
             n = 1
@@ -180,9 +186,15 @@ class PackedHyperNet:
             t = arena[off:off + n].view(shp)
             return t.clone() if clone else t
 
+        with_tail = not clone and arena.numel() == self.numel + self.P
         sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        toff = self.numel
         for k, t in self.target_sd.items():
-            sd[f"target_model.{k}"] = t.clone()
+            if with_tail:
+                sd[f"target_model.{k}"] = arena[toff:toff + t.numel()].view(t.shape)
+                toff += t.numel()
+            else:
+                sd[f"target_model.{k}"] = t.clone()
         sd["embeddings.weight"] = v("emb")
         for i in range(self.n_hidden + 1):
             sd[f"mlp.{2 * i}.weight"] = v(f"mlp{i}.W")
@@ -191,8 +203,8 @@ class PackedHyperNet:
         off = 0
         for k, n in zip(self.keys, self.numels):
             safe = k.replace(".", "__")
-            sd[f"hyper_layers.{safe}.weight"] = W[off:off + n].clone()
-            sd[f"hyper_layers.{safe}.bias"] = b[off:off + n].clone()
+            sd[f"hyper_layers.{safe}.weight"] = W[off:off + n]
+            sd[f"hyper_layers.{safe}.bias"] = b[off:off + n]
             off += n
         return sd
 

@@ -40,6 +40,11 @@ class Comm:
     def barrier(self) -> None:
         pass
 
+    def check(self) -> None:
+        """Raise if an asynchronous exchange the host has synchronised past failed (IPC deadline)."""
+
+    one_shot = False
+
     def broadcast_object(self, obj, src: int = 0):
         return obj
 
@@ -62,9 +67,14 @@ class LoopbackComm(Comm):
 
 
 class TorchComm(Comm):
-    """``torch.distributed`` process-group transport."""
+    """``torch.distributed`` process-group transport.
 
-    def __init__(self, device, backend: Optional[str] = None, pg=None, one_shot: bool = False):
+    ``one_shot``: True / False / "auto".  With the IPC path the update all-gather is the one-shot
+    kernel (stream-ordered, no host staging even on a gloo group whose ranks share a GPU); "auto"
+    enables it for device tensors with world > 1 (setup verifies it collectively and falls back to
+    the process group's all-gather on every rank if any rank cannot use it)."""
+
+    def __init__(self, device, backend: Optional[str] = None, pg=None, one_shot=False, ipc_timeout_s: float = 60.0):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.device = torch.device(device)
@@ -74,26 +84,38 @@ class TorchComm(Comm):
         self.pg = pg
         self._staging = self.backend == "gloo" and self.device.type == "cuda"
         self._ipc = None
-        if one_shot and self.device.type == "cuda" and self.world > 1:
+        if str(one_shot).lower() in ("true", "auto", "1") and self.device.type == "cuda" and self.world > 1:
             from .ipc import IpcAllGather
 
-            try:
-                self._ipc = IpcAllGather(self.device, self.rank, self.world, pg)
-            except Exception as e:  # pragma: no cover - needs GPUs
-                from ..utils.log import print_with_color
+            self._ipc = IpcAllGather(self.device, self.rank, self.world, pg, timeout_s=ipc_timeout_s)
 
-                print_with_color(f"[comm] one-shot IPC all-gather unavailable ({e}); using RCCL", "yellow")
-                self._ipc = None
+    @property
+    def one_shot(self) -> bool:
+        """True while the IPC one-shot all-gather is (or may still become) the gather path."""
+        return self._ipc is not None
 
     def _to_comm(self, t: torch.Tensor) -> torch.Tensor:
         return t.cpu() if self._staging else t
 
+    def check(self) -> None:
+        """Raise if an IPC gather the host has synchronised past timed out (a peer is dead or hung)."""
+        if self._ipc is not None:
+            self._ipc.check()
+
     def all_gather_rows(self, local: torch.Tensor) -> torch.Tensor:
         local = local.contiguous()
         if self._ipc is not None and local.is_cuda:
-            out = self._ipc.all_gather(local)
-            if out is not None:
-                return out
+            from .ipc import IpcUnavailable
+
+            try:
+                return self._ipc.all_gather(local)
+            except IpcUnavailable as e:  # collective decision: every rank falls back together
+                from ..utils.log import print_with_color
+
+                if self.rank == 0:
+                    print_with_color(f"[comm] one-shot IPC all-gather unavailable ({e}); using {self.backend}",
+                                     "yellow")
+                self._ipc = None
         src = self._to_comm(local)
         out = torch.empty((self.world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
         if hasattr(dist, "all_gather_into_tensor") and self.backend == "nccl":

@@ -2,14 +2,21 @@
 ``csrc/kernels/comm.hip``).
 
 RCCL's all-gather walks a ring: world-1 dependent hops, each paying link latency, which dominates
-for the FL round's small blocks (one ``[slots, P+4]`` fp32 block per rank: ~190 KB for
+for the FL round's small blocks (one ``[slots, W]`` fp32 block per rank: ~190 KB for
 TransformerModel).  Here every rank maps every peer's receive buffer once (IPC handles exchanged
 through the process group) and writes its block into all of them at once over the point-to-point
-xGMI links, then raises an epoch flag per peer.  Opt-in via ``comm.one-shot-allgather``; RCCL
-stays the default path and the fallback (any setup error disables IPC with a warning).
+xGMI links, then raises an epoch flag per peer.  The whole exchange is stream-ordered (two launches,
+no host synchronisation) and returns a view of the receive buffer; ranks may also share one GPU
+(several processes per device), which RCCL does not allow.
+
+Setup is collective and verified: after mapping, every rank gathers a known pattern with a short
+deadline, checks every row, and the ranks agree (MIN all-reduce) whether the path works — any
+failure on any rank (no IPC support, another host, a peer that cannot map, corrupted data) makes
+every rank fall back to the process group's own all-gather together.
 """
 from __future__ import annotations
 
+import socket
 from typing import Optional
 
 import torch
@@ -18,37 +25,98 @@ import torch.distributed as dist
 from ..ops import native
 
 
+class IpcUnavailable(RuntimeError):
+    pass
+
+
 class IpcAllGather:
-    def __init__(self, device, rank: int, world: int, pg=None, cap: int = 0, max_polls: int = 20_000_000):
+    def __init__(self, device, rank: int, world: int, pg=None, timeout_s: float = 60.0):
         self.device = torch.device(device)
         self.rank, self.world, self.pg = rank, world, pg
-        self.max_polls = int(max_polls)
+        self.timeout_s = float(timeout_s)
         self._ctx = None
-        if cap:
-            self._setup(cap)
+        self._n = 0
 
-    def _setup(self, cap: int) -> None:
-        """Collective: every rank allocates ``cap`` floats per slot and maps all peers' buffers."""
+    def _agree(self, ok: bool) -> bool:
+        """Collective AND over the process group (gloo: host tensor, nccl: device tensor)."""
+        on_dev = dist.get_backend(self.pg) == "nccl"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
+        return bool(int(t.item()) == 1)
+
+    def setup(self, n: int) -> None:
+        """Collective: allocate ``n`` floats per sender slot, map every peer, verify.  Raises
+        ``IpcUnavailable`` on every rank if any rank fails."""
+        self.close()
+        ctx, handle, err = None, b"", ""
+        try:
+            with torch.cuda.device(self.device):
+                ctx = native().IpcContext(self.rank, self.world, int(n))
+                handle = ctx.handle()
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = f"alloc/export: {e}"
+        info = [None] * self.world
+        dist.all_gather_object(info, (socket.gethostname(), handle), group=self.pg)
+        if not err and len({h for h, _ in info}) != 1:
+            err = "ranks span several hosts"
+        if not err and any(len(hd) == 0 for _, hd in info):
+            err = "a peer could not export its buffer"
+        if not err:
+            try:
+                with torch.cuda.device(self.device):
+                    ctx.open([hd for _, hd in info])
+            except Exception as e:  # noqa: BLE001
+                err = f"open: {e}"
+        if not err:
+            # self-test with the real block size (both parities), short deadline
+            try:
+                with torch.cuda.device(self.device):
+                    for ep in range(2):
+                        src = torch.arange(n, device=self.device, dtype=torch.float32) + (1000.0 * self.rank + ep)
+                        out = ctx.all_gather(src, 5.0)
+                        torch.cuda.synchronize(self.device)
+                        if ctx.status() != 0:
+                            err = f"self-test: no signal from ranks (mask {ctx.status():#x})"
+                            break
+                        exp = (torch.arange(n, device=self.device, dtype=torch.float32)[None, :]
+                               + 1000.0 * torch.arange(self.world, device=self.device, dtype=torch.float32)[:, None]
+                               + ep)
+                        if not torch.equal(out, exp):
+                            err = "self-test: gathered data differ"
+                            break
+            except Exception as e:  # noqa: BLE001
+                err = f"self-test: {e}"
+        if not self._agree(not err):
+            if ctx is not None:
+                ctx.close()
+            raise IpcUnavailable(err or "a peer failed the IPC setup")
+        self._ctx, self._n = ctx, int(n)
+
+    def all_gather(self, local: torch.Tensor) -> torch.Tensor:
+        """``[rows, cols]`` block per rank -> ``[world * rows, cols]`` (rank-major), enqueued on the current
+        stream.  The result is a view of the receive buffer: consume it on this stream before the call
+        after next (which reuses its parity)."""
+        flat = local.reshape(-1)
+        if flat.dtype != torch.float32 or not flat.is_contiguous():
+            flat = flat.float().contiguous()
+        n = flat.numel()
+        if self._ctx is None or n != self._n:
+            self.setup(n)
+        out = self._ctx.all_gather(flat, self.timeout_s)           # [world, n], row stride = capacity
+        if out.is_contiguous():
+            return out.view((self.world * local.shape[0],) + tuple(local.shape[1:]))
+        return out.contiguous().view((self.world * local.shape[0],) + tuple(local.shape[1:]))
+
+    def check(self) -> None:
+        """Raise if a wait the host has synchronised past missed its deadline."""
         if self._ctx is not None:
-            self._ctx.close()
-        with torch.cuda.device(self.device):
-            ctx = native().IpcContext(self.rank, self.world, int(cap))
-            handles = [None] * self.world
-            dist.all_gather_object(handles, ctx.handle(), group=self.pg)
-            ctx.open(handles)
-        self._ctx = ctx
-
-    def all_gather(self, local: torch.Tensor) -> Optional[torch.Tensor]:
-        """``[rows, ...]`` block per rank -> ``[world * rows, ...]`` (rank-major), or None if the
-        block does not fit the mapped buffers (caller falls back to RCCL)."""
-        n = local.numel()
-        if self._ctx is None or n > self._ctx.capacity():
-            self._setup(n)
-        flat = local.reshape(-1).float().contiguous()
-        out = self._ctx.all_gather(flat, self.max_polls)
-        return out.view((self.world * local.shape[0],) + tuple(local.shape[1:])).to(local.dtype)
+            st = self._ctx.status()
+            if st:
+                raise RuntimeError(f"IPC all-gather: no signal within {self.timeout_s:.0f} s from ranks "
+                                   f"{[r for r in range(self.world) if st >> r & 1]} (peer dead or hung)")
 
     def close(self) -> None:
         if self._ctx is not None:
             self._ctx.close()
             self._ctx = None
+            self._n = 0

@@ -34,10 +34,38 @@ def _host_port(cfg: Config) -> Tuple[str, int]:
     return str(host), int(cfg.comm.get("port", 29517))
 
 
-def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0):
-    """Server side: open the store, wait for ``clients`` registrations, publish the client table.
+def device_descriptor(device) -> Dict:
+    """Where this process computes: host + physical GPU identity (UUID when the runtime reports one), so the
+    server can tell whether every rank owns its own GPU (RCCL) or some share one (gloo + IPC)."""
+    import socket
 
-    Returns (store, world_size, table_json)."""
+    import torch
+
+    d = {"host": socket.gethostname(), "type": getattr(device, "type", "cpu"), "gpu": None}
+    if d["type"] == "cuda" and torch.cuda.is_available():
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(idx)
+        d["gpu"] = str(getattr(props, "uuid", "") or "") or f"{getattr(props, 'pci_bus_id', '')}:{idx}"
+    return d
+
+
+def choose_backend(descs: List[Dict]) -> Tuple[str, bool]:
+    """(process-group backend, one-shot IPC) for the classic launch: RCCL when every process owns a distinct
+    GPU; gloo when some share one (RCCL refuses duplicate GPUs) or any is on the CPU.  The IPC all-gather is
+    enabled when all GPU processes run on one host (it verifies itself and falls back collectively)."""
+    if any(d.get("type") != "cuda" for d in descs):
+        return "gloo", False
+    one_host = len({d.get("host") for d in descs}) == 1
+    gpus = [(d.get("host"), d.get("gpu")) for d in descs]
+    return ("nccl" if len(set(gpus)) == len(gpus) else "gloo"), one_host
+
+
+def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0, device=None):
+    """Server side: open the store, wait for ``clients`` registrations, publish the client table and the
+    transport choice (``comm.backend: auto``).
+
+    Returns (store, world_size, table_json); the chosen (backend, one_shot) is in ``store`` under
+    ``attackfl/transport`` (``read_transport``)."""
     host, port = _host_port(cfg)
     n = cfg.clients
     store = dist.TCPStore(host, port, world_size=None, is_master=True, wait_for_workers=False,
@@ -50,16 +78,26 @@ def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0):
             raise TimeoutError("clients did not register in time")
         time.sleep(0.05)
     table = []
+    descs = [device_descriptor(device) if device is not None else {"type": "cpu", "host": "", "gpu": None}]
     for r in range(1, n + 1):
         d = json.loads(store.get(PREFIX + f"client/{r}").decode())
         table.append({"index": r - 1, "uuid": d["uuid"], "owner": r, "attack": d.get("attack")})
-        print_with_color(f"[<<<] Received message from client: {d}", "blue")
+        descs.append(d.get("device") or {"type": "cpu"})
+        print_with_color(f"[<<<] Received message from client: "
+                         f"{ {k: v for k, v in d.items() if k != 'device'} }", "blue")
+    backend, one_shot = choose_backend(descs)
+    store.set(PREFIX + "transport", json.dumps({"backend": backend, "one_shot": one_shot}))
     store.set(PREFIX + "table", json.dumps(table))
     print_with_color("All clients are connected. Sending notifications.", "green")
     return store, n + 1, table
 
 
-def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float = 3600.0):
+def read_transport(store) -> Tuple[str, bool]:
+    t = json.loads(store.get(PREFIX + "transport").decode())
+    return str(t["backend"]), bool(t["one_shot"])
+
+
+def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float = 3600.0, device=None):
     """Client side: claim a rank, publish the descriptor, wait for the table.
 
     Returns (store, rank, world_size, table_json)."""
@@ -71,7 +109,8 @@ def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float 
     if rank > n:
         raise RuntimeError(f"server expects {n} clients; this would be client #{rank}")
     desc = {"uuid": str(uuid.uuid4()), "message": "Hello from Client!",
-            "attack": None if attack is None else {"mode": attack.mode, "round": attack.round, "args": attack.args}}
+            "attack": None if attack is None else {"mode": attack.mode, "round": attack.round, "args": attack.args},
+            "device": device_descriptor(device) if device is not None else {"type": "cpu"}}
     store.set(PREFIX + f"client/{rank}", json.dumps(desc))
     print_with_color(f"[>>>] Client {desc['uuid']} registered as rank {rank}", "red")
     store.wait([PREFIX + "table"])

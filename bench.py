@@ -60,11 +60,16 @@ def main() -> int:
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     if world > 1:
-        # AFL_BENCH_BACKEND / AFL_BENCH_DEVICE: test hooks (e.g. two gloo ranks sharing one GPU)
-        backend = os.environ.get("AFL_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        # one process per GPU over RCCL; the update exchange is the one-shot IPC all-gather over xGMI (verified
+        # collectively at the first round, RCCL otherwise).  Test hooks: AFL_BENCH_DEVICE=i puts every rank on
+        # GPU i (several ranks sharing one GPU: gloo group, IPC data path), AFL_BENCH_BACKEND forces the group
+        # backend, AFL_BENCH_ONE_SHOT=false forces the process-group collectives.
         dev_idx = os.environ.get("AFL_BENCH_DEVICE")
-        backend, device = init_distributed(backend, device_index=int(dev_idx) if dev_idx is not None else None)
-        comm = TorchComm(device)
+        shared = dev_idx is not None
+        backend = os.environ.get("AFL_BENCH_BACKEND") or (
+            "nccl" if torch.cuda.is_available() and not shared else "gloo")
+        backend, device = init_distributed(backend, device_index=int(dev_idx) if shared else None)
+        comm = TorchComm(device, backend, one_shot=os.environ.get("AFL_BENCH_ONE_SHOT", "auto"))
     else:
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if device.type == "cuda":
@@ -80,7 +85,8 @@ def main() -> int:
         "learning": {"epoch": 5, "batch-size": 128, "learning-rate": 0.004},
         "data": {"synthetic": True, "train-size": 60000, "test-size": 10000, "har-train-size": 7352,
                  "har-test-size": 2947},
-        "engine": {"trainer": args.trainer, "checkpoint-dir": tmp, "seed": 1},
+        "engine": {"trainer": args.trainer, "checkpoint-dir": tmp, "seed": 1,
+                   "phase-sync": bool(args.profile_rounds)},
         "log_path": tmp,
     })
     attackers = parse_attackers(args.attackers) if args.attackers else None
@@ -94,17 +100,21 @@ def main() -> int:
         if comm.world > 1:
             comm.barrier()
 
-    eng.phase_sync = bool(args.profile_rounds)
     for _ in range(args.warmup):
         eng.run_round()
     gc.freeze()  # as server.py / launch.py: the long-lived objects leave the collector's full scans
     sync()
     t0 = time.perf_counter()
     recs = []
+    w0 = eng.ckpt_writer.written
     for _ in range(args.steps):
         recs.append(eng.run_round())
+    eng.ckpt_writer.flush()  # every timed round's .pth is on disk before the clock stops
     sync()
     elapsed = time.perf_counter() - t0
+    ckpt = {"ckpt_written": eng.ckpt_writer.written - w0, "ckpt_dropped": eng.ckpt_writer.dropped,
+            "ckpt_stalls": eng.ckpt_writer.stalls, "ckpt_template_writes": eng.ckpt_writer.template_writes,
+            "t_checkpoint_ms": round(1e3 * sum(r.get("t_checkpoint", 0.0) for r in recs) / max(1, len(recs)), 3)}
     if comm.world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -140,6 +150,11 @@ def main() -> int:
                        "attackers": args.attackers or None},
             ("test_roc_auc" if args.data_name == "ICU" else "test_accuracy"): round(aucs[-1], 4) if aucs else None,
             "rounds_ok": sum(1 for r in recs if r["ok"]),
+            "comm": ("loopback" if comm.world == 1 else
+                     ("ipc-one-shot" if getattr(comm, "one_shot", False) else comm.backend)
+                     + ("+allreduce" if eng.fast_fedavg else "")),
+            "speculative": eng._speculative,
+            **ckpt,
         }
         print(json.dumps(out), flush=True)
     eng.close()

@@ -50,6 +50,11 @@ def parse_args(argv=None):
     return args
 
 
+def _one_shot(cfg, auto_choice: bool):
+    v = str(cfg.comm.get("one-shot-allgather", "auto")).lower()
+    return auto_choice if v == "auto" else v in ("true", "1")
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     print(f"Attack: {args.attack}, Mode: {args.attack_mode}")
@@ -59,19 +64,18 @@ def main(argv=None) -> int:
     from attackfl_amd.config import AttackSpec, load_config
     from attackfl_amd.fl.engine import FLEngine
     from attackfl_amd.parallel.comm import TorchComm
-    from attackfl_amd.parallel.launcher import init_group, join_rendezvous, table_from_json
+    from attackfl_amd.parallel.launcher import init_group, join_rendezvous, read_transport, table_from_json
 
     cfg = load_config(args.config)
     device = torch.device(args.device) if args.device else (torch.device("cuda", 0) if torch.cuda.is_available()
                                                             else torch.device("cpu"))
     print(f"Using device: {device}")
     attack = AttackSpec(args.attack_mode, args.attack_round, args.attack_args or []) if args.attack else None
-    backend = cfg.comm.get("backend", "auto")
-    if backend == "auto":
-        backend = "gloo"
-    store, rank, world, table = join_rendezvous(cfg, attack)
+    store, rank, world, table = join_rendezvous(cfg, attack, device=device)
+    backend, one_shot = read_transport(store)
+    backend = backend if cfg.comm.get("backend", "auto") == "auto" else cfg.comm["backend"]
     init_group(store, rank, world, backend, int(cfg.comm.get("timeout-s", 600)), device.index)
-    comm = TorchComm(device, backend)
+    comm = TorchComm(device, backend, one_shot=_one_shot(cfg, one_shot))
     eng = FLEngine(cfg, comm=comm, table=table_from_json(table), device=device, leader=False, verbose=False)
     eng.run()
     eng.close()

@@ -1,6 +1,12 @@
 // Host side of the one-shot IPC all-gather (kernels in csrc/kernels/comm.hip): allocation, handle
-// export/import, epoch bookkeeping, copy-out into a torch tensor, timeout reporting.
-// Exposed to Python as attackfl_amd._C.IpcContext (wrapped by attackfl_amd/parallel/ipc.py).
+// export/import, epoch bookkeeping, timeout reporting.  Exposed to Python as attackfl_amd._C.IpcContext
+// (wrapped by attackfl_amd/parallel/ipc.py).
+//
+// all_gather() only enqueues (push + signal/wait on the current stream) and returns a VIEW of this
+// epoch's receive region: no host synchronisation and no copy-out.  The view stays valid until the
+// call after next reuses its parity; the caller consumes it on the same stream before then.  A
+// deadline miss inside the wait kernel shows up in status() (pinned host word) once the stream has
+// passed the wait.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -21,14 +27,16 @@ hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 
 class IpcContext {
  public:
-  IpcContext(int rank, int world, int64_t cap) : rank_(rank), world_(world), cap_(cap) {
+  IpcContext(int rank, int world, int64_t cap) : rank_(rank), world_(world), cap_((cap + 3) / 4 * 4) {
     TORCH_CHECK(world >= 1 && world <= AFL_IPC_MAX_PEERS, "IPC all-gather supports 1..16 ranks");
     TORCH_CHECK(rank >= 0 && rank < world, "bad rank");
+    TORCH_CHECK(cap >= 1, "bad capacity");
+    IPC_OK(hipGetDevice(&device_));
     float* base = nullptr;
-    IPC_OK((hipError_t)afl_ipc_alloc(world, cap, &base));
+    IPC_OK((hipError_t)afl_ipc_alloc(world, cap_, &base));
     local_ = base;
-    IPC_OK(hipMalloc((void**)&status_, sizeof(int)));
-    IPC_OK(hipMemset(status_, 0, sizeof(int)));
+    IPC_OK(hipHostMalloc((void**)&status_, sizeof(int), hipHostMallocCoherent | hipHostMallocMapped));
+    *status_ = 0;
     for (int i = 0; i < AFL_IPC_MAX_PEERS; ++i) peers_.base[i] = nullptr;
     peers_.world = world;
     peers_.base[rank] = local_;
@@ -37,6 +45,7 @@ class IpcContext {
 
   // 64-byte IPC handle of the local receive buffer
   py::bytes handle() const {
+    TORCH_CHECK(local_ != nullptr, "IPC context closed");
     hipIpcMemHandle_t h;
     IPC_OK(hipIpcGetMemHandle(&h, local_));
     return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
@@ -57,42 +66,42 @@ class IpcContext {
     ready_ = true;
   }
 
-  // out[r * n : (r+1) * n] = rank r's `src` (n floats); blocks the host until done, raises on timeout
-  torch::Tensor all_gather(torch::Tensor src, int64_t max_polls) {
+  // enqueue: rank r's `src` (n floats) -> row r of the returned [world, n] view (row stride = capacity)
+  torch::Tensor all_gather(torch::Tensor src, double timeout_s) {
     TORCH_CHECK(ready_, "IPC context not opened");
     TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kFloat32, "src: fp32 device");
+    TORCH_CHECK(src.get_device() == device_, "src is on another device than the IPC buffers");
     const long n = src.numel();
     TORCH_CHECK(n <= cap_, "block larger than the IPC buffer");
     ++epoch_;
-    hipStream_t s = cur();
-    IPC_OK((hipError_t)afl_ipc_all_gather(src.data_ptr<float>(), n, peers_, rank_, cap_, epoch_, status_, max_polls,
-                                          s));
-    auto out = torch::empty({(long)world_ * n}, src.options());
-    const float* region = local_ + (long)(epoch_ & 1u) * world_ * cap_;
-    IPC_OK(hipMemcpy2DAsync(out.data_ptr<float>(), n * sizeof(float), region, cap_ * sizeof(float),
-                            n * sizeof(float), world_, hipMemcpyDeviceToDevice, s));
-    int st = 0;
-    IPC_OK(hipMemcpyAsync(&st, status_, sizeof(int), hipMemcpyDeviceToHost, s));
-    IPC_OK(hipStreamSynchronize(s));
-    TORCH_CHECK(st == 0, "IPC all-gather timed out waiting for a peer (epoch ", epoch_, ")");
-    return out;
+    const uint64_t ticks = (uint64_t)(timeout_s > 0 ? timeout_s * 1e8 : 6e9);  // s_memrealtime: 100 MHz
+    IPC_OK((hipError_t)afl_ipc_all_gather(src.data_ptr<float>(), n, peers_, rank_, cap_, epoch_, status_, ticks,
+                                          cur()));
+    float* region = local_ + (long)(epoch_ & 1u) * world_ * cap_;
+    return torch::from_blob(region, {(long)world_, n}, {cap_, 1L},
+                            torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device_));
   }
+
+  // bitmask of senders some wait timed out on (valid for every gather the host has synchronised past)
+  int status() const { return status_ ? __atomic_load_n(status_, __ATOMIC_ACQUIRE) : 0; }
 
   void close() {
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     opened_.clear();
     if (local_) (void)hipFree(local_);
-    if (status_) (void)hipFree(status_);
+    if (status_) (void)hipHostFree(status_);
     local_ = nullptr;
     status_ = nullptr;
     ready_ = false;
   }
 
   int64_t capacity() const { return cap_; }
+  int64_t epoch() const { return epoch_; }
 
  private:
   int rank_, world_;
   long cap_;
+  int device_ = 0;
   float* local_ = nullptr;
   int* status_ = nullptr;
   uint32_t epoch_ = 0;
@@ -109,7 +118,9 @@ void afl_register_ipc(pybind11::module& m) {
       .def(py::init<int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("cap"))
       .def("handle", &IpcContext::handle)
       .def("open", &IpcContext::open)
-      .def("all_gather", &IpcContext::all_gather, py::arg("src"), py::arg("max_polls") = 20000000)
+      .def("all_gather", &IpcContext::all_gather, py::arg("src"), py::arg("timeout_s") = 60.0)
+      .def("status", &IpcContext::status)
       .def("close", &IpcContext::close)
-      .def("capacity", &IpcContext::capacity);
+      .def("capacity", &IpcContext::capacity)
+      .def("epoch", &IpcContext::epoch);
 }

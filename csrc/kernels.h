@@ -267,11 +267,21 @@ int afl_attn_bwd(const AflAttn& a, hipStream_t s);
 
 // comm.hip — one-shot intra-node all-gather over IPC-mapped peer buffers (xGMI)
 #define AFL_IPC_MAX_PEERS 16
+#define AFL_IPC_FLAG_STRIDE 32  // uint32 per flag: one 128-byte line per (parity, sender)
 struct AflIpcPeers {
   float* base[AFL_IPC_MAX_PEERS];  // every rank's receive buffer (own rank = local pointer)
   int world;
 };
 long afl_ipc_buffer_bytes(int world, long cap);
 int afl_ipc_alloc(int world, long cap, float** base);
+// stream-ordered: push + signal/wait; on a deadline miss (s_memrealtime ticks, 100 MHz) the wait sets bit r of
+// *status (pinned host memory) for every sender r it did not hear from
 int afl_ipc_all_gather(const float* src, long n, const AflIpcPeers& peers, int rank, long cap, uint32_t epoch,
-                       int* status, long max_polls, hipStream_t s);
+                       int* status, uint64_t deadline_ticks, hipStream_t s);
+
+// crc.hip — CRC-32 (IEEE 802.3, zlib's crc32) of a device buffer: the checkpoint writer's zip records
+// x_chunk = x^(8*256) mod P, x_part / x_part_last = x^(8 * bytes of a full / the last combine part) mod P,
+// x_last = x^(8 * bytes of the last chunk) mod P (all in zlib's reflected representation)
+int afl_crc32_partials(long nbytes);
+int afl_crc32(const void* data, long nbytes, uint32_t* chunk_crcs, uint32_t* out, uint32_t x_chunk, uint32_t x_last,
+              uint32_t x_part, uint32_t x_part_last, hipStream_t s);

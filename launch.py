@@ -4,8 +4,8 @@
     python launch.py [--config config.yaml] [--attackers "3:LIE:2:0.74,5:Min-Max:2"] [--device cuda:0]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 launch.py [...]
 
-Server state (aggregator, hypernetwork, genuine pool) is replicated on every rank; rank 0 validates,
-logs to ``app.log`` and writes the ``.pth`` checkpoints.  Attackers come from ``--attackers`` or the
+Server state (aggregator, hypernetwork, genuine pool) and the validation / detection decisions are
+replicated on every rank; rank 0 logs to ``app.log`` and writes the ``.pth`` checkpoints.  Attackers come from ``--attackers`` or the
 ``comm.attackers`` config map (client index -> {mode, round, args}).
 """
 from __future__ import annotations
@@ -50,9 +50,11 @@ def main(argv=None) -> int:
         dev_index = None
         if args.device and args.device.startswith("cuda"):  # e.g. several gloo ranks sharing one GPU
             dev_index = int(args.device.split(":")[1]) if ":" in args.device else None
-        backend, device = init_distributed(cfg.comm.get("backend", "auto"), int(cfg.comm.get("timeout-s", 600)),
-                                           device_index=dev_index)
-        comm = TorchComm(device, backend, one_shot=bool(cfg.comm.get("one-shot-allgather", False)))
+        backend = cfg.comm.get("backend", "auto")
+        if backend == "auto" and dev_index is not None:
+            backend = "gloo"  # ranks pinned to one GPU share it: RCCL refuses duplicate GPUs
+        backend, device = init_distributed(backend, int(cfg.comm.get("timeout-s", 600)), device_index=dev_index)
+        comm = TorchComm(device, backend, one_shot=cfg.comm.get("one-shot-allgather", "auto"))
     else:
         device = torch.device(args.device) if args.device else (torch.device("cuda", 0) if torch.cuda.is_available()
                                                                 else torch.device("cpu"))

@@ -286,3 +286,46 @@ def test_hyper_generate_cache_invalidated_by_every_arena_change():
     assert torch.equal(hs.generate_many([0, 2]), a)            # restored: recomputed from the old state
     hs.load_arena(snap + 0.0)
     assert hs.generate_many([0, 2]) is not a
+
+
+def test_replicated_detection_and_validation_world2(tmp_path):
+    """Validation and hyper-detection are replicated on every rank (no control broadcast): a 2-rank gloo run
+    with detection active from round 18 matches the single-process run; only the leader writes the
+    embeddings file, app.log and the JSONL (with every client's per-epoch losses)."""
+    d = _cfg(tmp_path, server__mode="hyper", server__num_round=19, server__clients=4)
+    d["server"]["hyper-detection"] = {"enable": True, "cosine-search": 10, "n_components": 2, "eps": 0.5,
+                                      "min_samples": 2}
+    d["server"]["data-distribution"] = {"num-data-range": [70, 80]}
+    d["comm"] = {"backend": "gloo"}
+    d["engine"]["checkpoint-dir"] = str(tmp_path / "mp")
+    d["engine"]["metrics"] = str(tmp_path / "mp" / "m.jsonl")
+    d["log_path"] = str(tmp_path / "mp")
+    cfg_path = _write_cfg(tmp_path, d)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "launch.py"), "--config", cfg_path,
+           "--device", "cpu"]
+    r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    recs = [json.loads(l) for l in open(tmp_path / "mp" / "m.jsonl")]
+    assert sum(x["ok"] for x in recs) == 19
+    assert all(len(x["client_loss"]) == 4 and all(len(l) == 1 for l in x["client_loss"]) for x in recs)
+    assert open(tmp_path / "mp" / "app.log").read().count("ROC_AUC") == 19
+    assert os.path.exists(tmp_path / "mp" / "all_embeddings.npy")
+    mp = torch.load(os.path.join(tmp_path, "mp", "TransformerModel_hyper_4.pth"), weights_only=True)
+    d1 = dict(d)
+    d1["engine"] = dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "sp"), "metrics": ""})
+    d1["log_path"] = str(tmp_path / "sp")
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)  # as under torchrun: the same CPU GEMM reduction order over 19 rounds
+    try:
+        eng = FLEngine(from_dict(d1), device="cpu", verbose=False)
+        hist = eng.run()
+        eng.close()
+    finally:
+        torch.set_num_threads(nt)
+    assert [x["removed"] for x in hist] == [x["removed"] for x in recs]
+    sp = torch.load(os.path.join(tmp_path, "sp", "TransformerModel_hyper_4.pth"), weights_only=True)
+    for k in sp:
+        assert torch.allclose(sp[k], mp[k], atol=1e-4), (k, (sp[k] - mp[k]).abs().max())

@@ -66,13 +66,21 @@ def test_async_checkpoint_files(gpu, tmp_path):
     eng.run()
     sd_live = eng.hyper.hnet.state_dict()
     eng.close()
+    assert eng.ckpt_writer.template_writes >= 1   # the 2nd round's file went through the zip template
     sd = torch.load(tmp_path / "RNNModel_hyper_3.pth", weights_only=True)
     assert list(sd.keys()) == list(sd_live.keys())
     assert all(torch.equal(sd[k], sd_live[k]) for k in sd)
+    import zipfile
+
+    with zipfile.ZipFile(tmp_path / "RNNModel_hyper_3.pth") as z:
+        assert z.testzip() is None
 
 
-def test_checkpoint_latest_wins(gpu, tmp_path):
-    """Submits that outpace the disk coalesce; the file ends with the newest checkpoint, complete."""
+def test_checkpoint_every_submit_written_in_order(gpu, tmp_path):
+    """Submits that outpace the disk wait for a staging slot instead of being dropped: every file is written,
+    in order, through the zip template with the GPU CRC (valid zip), and the file ends with the newest state."""
+    import zipfile
+
     import torch
 
     from attackfl_amd.utils.ckpt import CheckpointWriter
@@ -81,10 +89,13 @@ def test_checkpoint_latest_wins(gpu, tmp_path):
     src = torch.empty(1 << 22, dtype=torch.float32, device="cuda")
     for v in range(6):
         src.fill_(float(v))
-        w.submit("x", src, lambda t: {"t": t.clone()}, str(tmp_path / "x.pth"))
+        w.submit("x", src, lambda t: {"t": t}, str(tmp_path / "x.pth"))
     w.flush()
     got = torch.load(tmp_path / "x.pth", weights_only=True)["t"]
     assert bool((got == 5.0).all())
+    assert w.written == 6 and w.dropped == 0 and w.template_writes == 5
+    with zipfile.ZipFile(tmp_path / "x.pth") as z:
+        assert z.testzip() is None   # the patched CRC-32 (computed on the GPU) is right
     w.close()
 
 

@@ -1,6 +1,9 @@
-"""Multi-process runs on the GPU box: two ranks sharing the GPU (gloo transport with device tensors,
-staged through the host), fused trainer + LIE attacker (all-gather path) and plain FedAvg (all-reduce
-path); the final checkpoint must equal the single-process GPU run of the same configuration."""
+"""Multi-process runs on the GPU box: several ranks sharing the one GPU (gloo process group, the one-shot
+IPC all-gather as the update path — stream-ordered, no host staging — replicated validation, speculative
+launch at world > 1).  The final checkpoint of a multi-rank run must equal the single-process run of the
+same configuration BIT FOR BIT (every kernel on the round path is deterministic and a client's trajectory
+does not depend on the rank that trains it), and ``bench.py``'s multi-rank path must report the IPC path."""
+import json
 import os
 import socket
 import subprocess
@@ -25,48 +28,73 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("attackers", [{3: {"mode": "LIE", "round": 2, "args": [0.74]}}, {}])
-def test_two_ranks_match_single_process(gpu, tmp_path, attackers):
+CASES = {
+    # fedavg + a Min-Max attacker (all-gather path, attack math on the owning rank)
+    "tf-fedavg-minmax": ("TransformerModel", "fedavg", {5: {"mode": "Min-Max", "round": 2}}),
+    # hypernetwork server + Opt-Fang on the RNN (replicated hnet update and hyper validation)
+    "rnn-hyper-optfang": ("RNNModel", "hyper", {6: {"mode": "Opt-Fang", "round": 2}}),
+    # plain fedavg (no attacker): at world > 1 with IPC it stays on the gather + FedAvg kernel path
+    "tf-fedavg": ("TransformerModel", "fedavg", {}),
+}
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_ranks_sharing_gpu_match_single_process_bitwise(gpu, tmp_path, world, case):
+    model, mode, attackers = CASES[case]
     d = {
-        "server": {"num-round": 3, "clients": 4, "mode": "fedavg", "model": "TransformerModel",
-                   "genuine-rate": 1.0, "data-distribution": {"num-data-range": [600, 900]}},
+        "server": {"num-round": 3, "clients": 8, "mode": mode, "model": model, "genuine-rate": 0.5,
+                   "data-distribution": {"num-data-range": [300, 600]}},
         "learning": {"epoch": 2, "batch-size": 128},
-        "data": {"synthetic": True, "train-size": 5000, "test-size": 1000},
-        "comm": {"backend": "gloo", "attackers": attackers},
-        "engine": {"checkpoint-dir": str(tmp_path / "mp"), "trainer": "auto"},
+        "data": {"synthetic": True, "train-size": 4000, "test-size": 1000},
+        "comm": {"attackers": attackers},
+        "engine": {"checkpoint-dir": str(tmp_path / "mp"), "trainer": "auto", "seed": 2,
+                   "metrics": str(tmp_path / "mp" / "m.jsonl")},
         "log_path": str(tmp_path / "mp"),
     }
     cfg_path = tmp_path / "config.yaml"
     cfg_path.write_text(yaml.safe_dump(d))
     env = dict(os.environ, PYTHONPATH=ROOT, ATTACKFL_QUIET="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "launch.py"), "--config", str(cfg_path),
-           "--device", "cuda:0"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    cmd = ["timeout", "-k", "10", "150", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "launch.py"), "--config", str(cfg_path), "--device", "cuda:0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    mp = torch.load(tmp_path / "mp" / "TransformerModel.pth", weights_only=True)
-    d1 = dict(d, engine=dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "sp")}), log_path=str(tmp_path / "sp"))
+    name = f"{model}_hyper_8.pth" if mode == "hyper" else f"{model}.pth"
+    mp = torch.load(tmp_path / "mp" / name, weights_only=True)
+    recs = [json.loads(l) for l in open(tmp_path / "mp" / "m.jsonl")]
+    assert sum(r["ok"] for r in recs) == 3
+    assert all(r.get("path") != "fedavg-allreduce" for r in recs)  # IPC gather path, not the all-reduce
+    # per-client epoch losses of every rank's clients reach the leader's JSONL through the gathered block
+    trained = [l for l in recs[-1]["client_loss"] if l is not None]
+    assert len(trained) == 8 - len(attackers) and all(len(l) == 2 and l[0] > 0 for l in trained)
+    d1 = dict(d, engine=dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "sp"), "metrics": ""}),
+              log_path=str(tmp_path / "sp"))
     eng = FLEngine(from_dict(d1), device="cuda", verbose=False)
     eng.run()
     eng.close()
-    sp = torch.load(tmp_path / "sp" / "TransformerModel.pth", weights_only=True)
+    sp = torch.load(tmp_path / "sp" / name, weights_only=True)
+    assert list(sp) == list(mp)
     for k in sp:
-        assert torch.allclose(sp[k].cpu(), mp[k].cpu(), atol=1e-5), k
+        assert torch.equal(sp[k].cpu(), mp[k].cpu()), k
 
 
-@pytest.mark.parametrize("extra", [[], ["--attackers", "3:Min-Max:2"]])
-def test_bench_two_ranks(gpu, tmp_path, extra):
-    """bench.py's multi-rank path (the driver's scaling run) end to end: two gloo ranks sharing the GPU."""
-    import json
-
-    env = dict(os.environ, PYTHONPATH=ROOT, AFL_BENCH_BACKEND="gloo", AFL_BENCH_DEVICE="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1"] + extra
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+@pytest.mark.parametrize("world,extra", [(2, []), (8, []), (8, ["--attackers", "3:LIE:2:0.74"]),
+                                         (8, ["--mode", "hyper", "--model", "RNNModel",
+                                              "--attackers", "6:Opt-Fang:2"])])
+def test_bench_ranks_sharing_gpu(gpu, tmp_path, world, extra):
+    """bench.py's multi-rank path (the driver's scaling run): N ranks on the one GPU over the IPC path; the
+    JSON line reports it, every timed round succeeded and every round's checkpoint landed."""
+    env = dict(os.environ, PYTHONPATH=ROOT, AFL_BENCH_DEVICE="0")
+    cmd = ["timeout", "-k", "10", "150", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "4", "--warmup", "2"] + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["rounds_ok"] == 2 and out["value"] > 0
-    assert out["config"]["parallelism"] == "fl8-clients-over-2-ranks"
+    assert out["n_gpus"] == world and out["rounds_ok"] == 4 and out["value"] > 0
+    assert out["comm"] == "ipc-one-shot" and out["speculative"] is True
+    assert out["ckpt_dropped"] == 0 and out["ckpt_written"] >= 4
+    assert out["config"]["parallelism"] == f"fl8-clients-over-{world}-ranks"

@@ -5,6 +5,7 @@ import torch
 from attackfl_amd import ops
 from attackfl_amd.ops import composite as C
 from attackfl_amd.models import ParamLayout
+from attackfl_amd.ops import native
 
 pytestmark = pytest.mark.gpu
 
@@ -201,3 +202,15 @@ def test_make_plan_native_matches_cpu_mirror(gpu):
     assert a.order.is_cuda
     for c, n in enumerate(nd):
         assert torch.equal(a.order[c, :, :n].cpu(), b.order[c, :, :n])
+
+
+@pytest.mark.parametrize("n", [1, 7, 64, 65, 1000, 4096 * 3 + 5, 4885850])
+def test_crc32_matches_zlib(gpu, n):
+    """csrc/kernels/crc.hip: zlib-compatible CRC-32 of a device buffer (checkpoint zip records), any length
+    (multiple of 4 bytes) — chunk tails, run tails and one full hypernetwork arena."""
+    import zlib
+
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, generator=g)
+    got = int(native().crc32(x.cuda()).item()) & 0xFFFFFFFF
+    assert got == zlib.crc32(x.numpy().tobytes())
