@@ -186,6 +186,8 @@ class FLEngine:
             self.train_table = DeviceTable(ds, self.device)
         self.trainer = make_trainer(cfg.engine.get("trainer", "auto"), self.model_name, self.data_name,
                                     self.train_table, self.device) if self.train_table is not None else None
+        if self.trainer is not None and hasattr(self.trainer, "compat_har"):
+            self.trainer.compat_har = bool(cfg.engine.get("compat-har-train", False))
         # validation runs on EVERY rank: its kernels are deterministic and the global model is bit-identical
         # on all ranks, so each rank reaches the leader's decision without a control broadcast
         self.validation = None
@@ -761,6 +763,11 @@ class FLEngine:
         if self._has_attackers and attackers is not None:
             keep = [k for k in range(stored) if not bool(attackers[k])]
             self.genuine_pool = U[keep].clone() if keep else None
+            if (keep and keep[0] == 0 and round_ok and self.mode == "fedavg" and self.global_params is not None
+                    and self.cfg.engine.get("compat-fedavg-alias", False)):
+                # A-13: the reference averages INTO the first stored update's dict, which is also the first
+                # genuine model in the pool (server.py:263-268,763): attackers may receive the aggregate
+                self.genuine_pool[0] = self.global_params
         # Speculative next launch: the next round's local training is enqueued right behind the aggregate,
         # BEFORE this round's validation / checkpoint, which then run on a side stream next to it (the
         # trainer occupies a few CUs).  Valid whatever validation decides: a failed round is retried from the

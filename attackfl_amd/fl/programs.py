@@ -10,7 +10,8 @@ step counter, so on a GPU the whole step is captured ONCE into a HIP graph and r
 the fp32 oracle the GPU path is tested against.
 
 Semantics mirror the reference trainers (``client.py:66-131``): fresh Adam per round, BCE (ICU) /
-cross-entropy (HAR) mean loss, size-1 batches skipped (A-21), NaN loss aborts the client's round.
+cross-entropy (HAR) mean loss, size-1 batches skipped (A-21), NaN loss aborts the client's round (for HAR
+``engine.compat-har-train`` restores the reference ``train_HAR`` loop: no skip, no abort).
 Model math mirrors ``src/Model.py:27-88`` (CNN), ``91-163`` (RNN), ``418-458`` (HAR classifier).
 """
 from __future__ import annotations
@@ -411,16 +412,18 @@ class ProgramRunner:
         self._live = None
 
     def train(self, table, params: torch.Tensor, plan, lr: float, seeds: Sequence[int], sgd_lr: float = 0.0,
-              max_steps: int = None, sync: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+              max_steps: int = None, sync: bool = True, compat_har: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
         """Train ``params [C, P]`` in place.  Returns (ok [C] bool, losses [C, E]) on the host, or with
-        ``sync=False`` the device (failed-count [C] int32, losses [C, E]) without synchronising."""
+        ``sync=False`` the device (failed-count [C] int32, losses [C, E]) without synchronising.
+        ``compat_har``: the reference ``train_HAR`` loop (``client.py:114-131``) — size-1 batches train,
+        a NaN loss does not abort the client."""
         pg = self.prog
         dev = pg.device
         C, P = params.shape
         idx, bsz, ep, nb, S = step_tables(plan.order, plan.nd, plan.epochs, pg.B, dev)
         if max_steps is not None:
             S = min(S, max_steps)
-        ctl = StepCtl.create(seeds, dev)
+        ctl = StepCtl.create(seeds, dev, min_bs=1 if compat_har else 2, nan_abort=not compat_har)
         grads = torch.zeros(C, P, device=dev)
         m = torch.zeros(C, P, device=dev)
         v = torch.zeros(C, P, device=dev)

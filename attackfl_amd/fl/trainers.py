@@ -188,11 +188,12 @@ def make_plan(n_train: int, num_data: Sequence[int], epochs: int, generator, dev
     return Plan(order.to(device=device, dtype=torch.int32).contiguous(), nd.to(torch.int32).cpu(), epochs)
 
 
-def batches(nd: int, batch: int):
-    """(start, end) of each batch of one epoch; size-1 batches are skipped (A-21)."""
+def batches(nd: int, batch: int, skip_single: bool = True):
+    """(start, end) of each batch of one epoch; size-1 batches are skipped (A-21) unless ``skip_single``
+    is False (the reference ``train_HAR`` loop)."""
     for a in range(0, nd, batch):
         b = min(nd, a + batch)
-        if b - a == 1:
+        if b - a == 1 and skip_single:
             continue
         yield a, b
 
@@ -216,6 +217,7 @@ class EagerTrainer:
         self.model = build_model(model_name, seed=0).to(self.device)
         self.layout = ParamLayout.from_state_dict(self.model.state_dict())
         self.verbose = verbose
+        self.compat_har = False  # engine.compat-har-train: reference train_HAR (no size-1 skip, no NaN abort)
 
     def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
               ) -> Tuple[List[bool], torch.Tensor]:
@@ -251,9 +253,10 @@ class EagerTrainer:
             crit = torch.nn.CrossEntropyLoss()
         nd = order.shape[1]
         nbatches = max(1, (nd + batch - 1) // batch)
+        har_compat = self.compat_har and self.data_name == "HAR"
         for e in range(order.shape[0]):
             total = torch.zeros((), dtype=torch.float64, device=self.device)
-            for a, b in batches(nd, batch):
+            for a, b in batches(nd, batch, skip_single=not har_compat):
                 idx = order[e, a:b].long()
                 opt.zero_grad()
                 if self.data_name == "ICU":
@@ -266,7 +269,7 @@ class EagerTrainer:
                 else:
                     x, y = self.table.har_batch(idx)
                     loss = crit(model(x), y)
-                if bool(torch.isnan(loss).any()):
+                if not har_compat and bool(torch.isnan(loss).any()):
                     print_with_color("NaN detected in loss, stop training", "yellow")
                     return False
                 total += loss.detach().double()
@@ -356,6 +359,7 @@ class GraphTrainer:
         self.layout = ParamLayout.for_model(model_name)
         self.verbose = verbose
         self._runner = None
+        self.compat_har = False  # engine.compat-har-train (HAR data only)
 
     def train(self, params: torch.Tensor, plan: Plan, lr: float, batch: int, seeds: Sequence[int]
               ) -> Tuple[List[bool], torch.Tensor]:
@@ -367,7 +371,8 @@ class GraphTrainer:
         if self._runner is None or self._runner.prog.C != C or self._runner.prog.B != batch:
             self._runner = self.programs.ProgramRunner(
                 self.programs.make_program(self.model_name, C, batch, self.device, train=True))
-        ok, losses = self._runner.train(self.table, params, plan, lr, seeds, sync=False)
+        ok, losses = self._runner.train(self.table, params, plan, lr, seeds, sync=False,
+                                        compat_har=self.compat_har and self.table.kind == "HAR")
 
         def fin():
             okh, lh = (ok == 0).cpu(), losses.double().cpu()

@@ -33,14 +33,25 @@ class StepCtl:
     stepctl: torch.Tensor
 
     @classmethod
-    def create(cls, seeds, device) -> "StepCtl":
+    def create(cls, seeds, device, min_bs: int = 2, nan_abort: bool = True) -> "StepCtl":
+        """``stepctl = [step, min_bs, nan_abort]``: steps with fewer than ``min_bs`` rows are skipped (ICU:
+        2, A-21) and a NaN loss aborts the client (ICU); the reference ``train_HAR`` does neither (1, False)."""
         s = torch.tensor([int(x) & masks.M32 for x in seeds], dtype=torch.int64)
         s = torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32)
-        return cls(s.to(device), torch.zeros(1, dtype=torch.int32, device=device))
+        ctl = torch.tensor([0, int(min_bs), 1 if nan_abort else 0], dtype=torch.int32)
+        return cls(s.to(device), ctl.to(device))
 
     # composite helpers
     def step(self) -> int:
         return int(self.stepctl[0])
+
+    @property
+    def min_bs(self) -> int:
+        return int(self.stepctl[1])
+
+    @property
+    def nan_abort(self) -> bool:
+        return bool(int(self.stepctl[2]))
 
     def key(self, c: int) -> int:
         return masks.step_key(int(self.seeds[c]) & masks.M32, self.step())
@@ -430,9 +441,9 @@ def gru_bwd(dh, col0: int, gi, bhh, dgi, dbih, dbhh) -> None:
 
 
 # ------------------------------------------------------------------------------------- losses
-def _active(bsz, failed, s: int, c: int):
+def _active(bsz, failed, s: int, c: int, min_bs: int = 2):
     bs = int(bsz[s, c]) if s < bsz.shape[0] else 0
-    return bs >= 2 and int(failed[c]) == 0, bs
+    return bs >= max(min_bs, 1) and int(failed[c]) == 0, bs
 
 
 def bce(z, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
@@ -445,14 +456,14 @@ def bce(z, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
     C, B = y.shape[0], y.shape[1]
     zz, yy, dd = z.reshape(C, B), y.reshape(C, B), dz.reshape(C, B)
     for c in range(C):
-        act, bs = _active(bsz, failed, s, c)
+        act, bs = _active(bsz, failed, s, c, ctl.min_bs)
         if not act:
             continue
         p = torch.sigmoid(zz[c, :bs])
         t = yy[c, :bs]
         lv = -(t * torch.clamp(torch.log(p), min=-100.0) + (1 - t) * torch.clamp(torch.log1p(-p), min=-100.0))
         loss = lv.mean()
-        if bool(torch.isnan(loss)):
+        if bool(torch.isnan(loss)) and ctl.nan_abort:
             failed[c] = 1
             continue
         losses[c, int(epoch[s, c])] += loss / int(nb[c])
@@ -468,12 +479,12 @@ def ce(logits, y, bsz, epoch, nb, ctl: StepCtl, failed, losses, dz) -> None:
     s = ctl.step()
     dz.zero_()
     for c in range(logits.shape[0]):
-        act, bs = _active(bsz, failed, s, c)
+        act, bs = _active(bsz, failed, s, c, ctl.min_bs)
         if not act:
             continue
         x = logits[c, :bs]
         loss = F.cross_entropy(x, y[c, :bs])
-        if bool(torch.isnan(loss)):
+        if bool(torch.isnan(loss)) and ctl.nan_abort:
             failed[c] = 1
             continue
         losses[c, int(epoch[s, c])] += loss / int(nb[c])
@@ -495,7 +506,7 @@ def adam_clients(p, g, m, v, tcount, bsz, ctl: StepCtl, failed, lr: float, skip=
     keep = torch.ones(p.shape[1], dtype=torch.bool)
     keep[skip[0]:skip[1]] = False
     for c in range(p.shape[0]):
-        act, _ = _active(bsz, failed, s, c)
+        act, _ = _active(bsz, failed, s, c, ctl.min_bs)
         if not act:
             continue
         gi = g[c][keep]
@@ -518,7 +529,7 @@ def step_end(ctl: StepCtl, tcount, bsz, failed) -> None:
         return
     s = ctl.step()
     for c in range(tcount.shape[0]):
-        if _active(bsz, failed, s, c)[0]:
+        if _active(bsz, failed, s, c, ctl.min_bs)[0]:
             tcount[c] += 1
     ctl.stepctl[0] += 1
 

@@ -496,14 +496,18 @@ __global__ void __launch_bounds__(256) k_gru_bwd(const float* __restrict__ dh, l
 }
 
 // ============================================================================ losses
-// Per client: rows b < bsz of the current step are real; bsz < 2 (size-1 batch skip A-21, or past
+// Per client: rows b < bsz of the current step are real; bsz < min_bs (size-1 batch skip A-21, or past
 // the client's last batch) or a previous NaN -> no loss, zero gradient, no Adam update this step.
+// stepctl = [step, min_bs, nan_abort]: min_bs 2 / nan_abort 1 are the ICU semantics (client.py:86-102);
+// the reference's train_HAR (client.py:114-131) trains size-1 batches and never aborts (1 / 0).
+__device__ __forceinline__ int step_min_bs(const int* stepctl) { return stepctl ? stepctl[1] : 2; }
+__device__ __forceinline__ bool step_nan_abort(const int* stepctl) { return stepctl ? stepctl[2] != 0 : true; }
 __device__ __forceinline__ bool step_active(const int* bsz, const int* stepctl, int C, int S, const int* failed,
                                             int c, int* bs_out) {
   const int s = cur_step(stepctl);
   const int bs = s < S ? bsz[(long)s * C + c] : 0;
   *bs_out = bs;
-  return bs >= 2 && failed[c] == 0;
+  return bs >= step_min_bs(stepctl) && bs >= 1 && failed[c] == 0;
 }
 
 __global__ void __launch_bounds__(256) k_bce(const float* __restrict__ z, const float* __restrict__ y,
@@ -527,7 +531,8 @@ __global__ void __launch_bounds__(256) k_bce(const float* __restrict__ z, const 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
   __syncthreads();
   const float loss = (red[0] + red[1] + red[2] + red[3]) / (float)max(bs, 1);
-  const bool nan = act && (loss != loss);
+  const bool abort = step_nan_abort(stepctl);
+  const bool nan = act && abort && (loss != loss);
   for (int b = threadIdx.x; b < B; b += 256) {
     float g = 0.f;
     if (act && !nan && b < bs) {
@@ -569,7 +574,8 @@ __global__ void __launch_bounds__(256) k_ce(const float* __restrict__ logits, co
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
   __syncthreads();
   const float loss = (red[0] + red[1] + red[2] + red[3]) / (float)max(bs, 1);
-  const bool nan = act && (loss != loss);
+  const bool abort = step_nan_abort(stepctl);
+  const bool nan = act && abort && (loss != loss);  // without abort a NaN loss keeps training (NaN gradient)
   for (int b = threadIdx.x; b < B; b += 256) {
     const float* x = logits + ((long)c * B + b) * K;
     float* d = dz + ((long)c * B + b) * K;
