@@ -15,11 +15,19 @@ effective attack:
 * unbiased std (``torch.std`` default); ``K <= 1`` returns the attacker's own model for the
   bisection attacks, while LIE with ``K == 1`` yields NaN exactly like the reference.
 
-The bisection itself (``_bisect``) only needs, per iteration, the K distances of one
-candidate.  In flat mode every distance is ``sqrt(A_j - 2γB_j + γ²C)`` with coefficients from
-one pass over ``[K, P]`` (``ops.attack_coeffs``, a HIP kernel on GPU), so the loop is host
-scalar math.  In spectral mode vector-shaped tensors use the same closed form per tensor and
-matrix-shaped tensors use a batched σ_max (``ops.batched_spectral_norm``).
+The bisection only needs, per iteration, the K distances of one candidate.  In flat mode every
+distance is ``sqrt(A_j - 2γB_j + γ²C)`` with coefficients from one pass over ``[K, P]``
+(``ops.attack_coeffs``, a HIP kernel on GPU).  In spectral mode vector-shaped tensors use the same
+closed form per tensor and matrix-shaped tensors use a batched σ_max (``ops.spectral_norm_sum``).
+
+**Device-resident bisection (K-G5).**  The reference loop (``src/Utils.py:118-130,152-164,190-202``)
+runs ``while |γ_succ - γ| > τ`` with the step halving every iteration; after iteration i that gap is
+exactly γ0 / 2^(i+1) whatever was accepted (an accept sets γ_succ = γ and moves γ up by step/2, a
+reject moves γ down by step/2 towards the last accepted value), so the iteration count is known up
+front (6 for γ0 = 50, τ = 1) and only the path depends on the data.  ``_bisect_device`` therefore
+unrolls the loop with γ, γ_succ and every accept decision as device scalars (``torch.where``
+updates): no host synchronisation per γ — the whole attack is enqueued on the attacker's side stream
+and its γ reaches the host only when the round's record is written.
 """
 from __future__ import annotations
 
@@ -128,7 +136,8 @@ class _CandidateDistances:
             if self.vec:
                 self.A, self.B, self.C = ops.attack_coeffs_segments(G, mean, dev, self.vec)  # [K,S],[K,S],[S]
 
-    def __call__(self, gamma: float) -> torch.Tensor:
+    def __call__(self, gamma) -> torch.Tensor:
+        """``gamma``: a float or a 0-d float64 tensor on the matrices' device."""
         K = self.G.shape[0]
         if self.engine.mode == "flat":
             q = (self.A - 2.0 * gamma * self.B + gamma * gamma * self.C).clamp_min(0.0)
@@ -149,8 +158,39 @@ class _CandidateDistances:
         return d
 
 
+def bisect_iterations(gamma: float = 50.0, tau: float = 1.0) -> int:
+    """Iterations of the reference loop: the gap |γ_succ - γ| is γ0 / 2^i after i iterations."""
+    n, gap = 0, float(gamma)
+    while abs(gap) > tau:
+        n += 1
+        gap /= 2.0
+    return n
+
+
+def _bisect_device(accept: Callable[[torch.Tensor], torch.Tensor], gamma: float, tau: float, device):
+    """The reference bisection with device-side state: ``accept(γ)`` returns a 0-d bool tensor.  Returns
+    (last tried γ, iterations, last accepted γ) with the γs as 0-d float64 tensors."""
+    g = torch.full((), float(gamma), dtype=torch.float64, device=device)
+    succ = torch.zeros((), dtype=torch.float64, device=device)
+    last = g
+    step = float(gamma)
+    n = bisect_iterations(gamma, tau)
+    for _ in range(n):
+        last = g
+        acc = accept(g)
+        succ = torch.where(acc, g, succ)
+        g = g + (acc.to(torch.float64) * step - step / 2.0)   # accept: +step/2, reject: -step/2
+        step /= 2.0
+    return last, n, succ
+
+
+def host_info(info: Dict) -> Dict:
+    """An attack's info dict with device scalars read back (call where the host synchronises anyway)."""
+    return {k: (float(v) if torch.is_tensor(v) else v) for k, v in info.items()}
+
+
 def _bisect(accept: Callable[[float], bool], gamma: float = 50.0, tau: float = 1.0) -> Tuple[float, int, float]:
-    """Reference bisection: returns (last tried γ, iterations, last accepted γ)."""
+    """Reference bisection with a host predicate: returns (last tried γ, iterations, last accepted γ)."""
     step = gamma
     gamma_succ = 0.0
     last = gamma
@@ -182,19 +222,14 @@ def _minmax_family(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine, k
     st = column_stats(G)
     dev = st.sign if kind == "fang" else st.std
     D = engine.pairwise(G)
-    if kind == "sum":
-        threshold = float((D ** 2).sum(dim=1).max().item())
-    else:
-        threshold = float(D.max().item())
+    threshold = (D ** 2).sum(dim=1).max() if kind == "sum" else D.max()   # device scalar
     cand_d = _CandidateDistances(engine, G, st.mean, dev)
 
-    def accept(g: float) -> bool:
+    def accept(g: torch.Tensor) -> torch.Tensor:
         d = cand_d(g)
-        if kind == "sum":
-            return float((d ** 2).sum().item()) < threshold
-        return float(d.max().item()) < threshold
+        return ((d ** 2).sum() < threshold) if kind == "sum" else (d.max() < threshold)
 
-    last, iters, succ = _bisect(accept, gamma, tau)
+    last, iters, succ = _bisect_device(accept, gamma, tau, G.device)
     mal = st.mean - last * dev
     return AttackResult(True, mal, {"gamma": last, "gamma_succ": succ, "iters": iters, "threshold": threshold})
 
@@ -216,19 +251,18 @@ def lie(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine = None, scali
     return AttackResult(True, ops.lie_candidate(G, float(scaling_factor)), {"z": float(scaling_factor)})
 
 
-def random_noise(own: torch.Tensor, perturbation: float, generator: Optional[torch.Generator] = None) -> AttackResult:
-    """Random: own + N(0,1)·σ (reference ``create_random_base_model``)."""
-    noise = torch.randn(own.shape, generator=generator, device=own.device, dtype=own.dtype) if generator is not None \
-        else torch.randn_like(own)
-    return AttackResult(True, own + noise * float(perturbation), {"sigma": float(perturbation)})
+def random_noise(own: torch.Tensor, perturbation: float, seed: int = 0) -> AttackResult:
+    """Random: own + N(0,1)·σ (reference ``create_random_base_model``): Philox4x32-10 normals keyed by
+    ``seed`` (``k_noise_philox`` on GPU, the bit-identical uniform mirror on CPU)."""
+    return AttackResult(True, ops.noise(own, float(perturbation), int(seed)), {"sigma": float(perturbation)})
 
 
 def run_attack(mode: str, args: Sequence[float], own: torch.Tensor, G: Optional[torch.Tensor], engine: DistanceEngine,
-               generator: Optional[torch.Generator] = None) -> AttackResult:
-    """Dispatch by the reference's ``--attack_mode`` names."""
+               seed: int = 0) -> AttackResult:
+    """Dispatch by the reference's ``--attack_mode`` names.  ``seed`` keys the Random attack's noise."""
     if mode == "Random":
         sigma = args[0] if args else 1e6
-        return random_noise(own, sigma, generator)
+        return random_noise(own, sigma, seed)
     if G is None or G.shape[0] == 0:
         raise ValueError("attack needs genuine models")
     if mode == "Min-Max":

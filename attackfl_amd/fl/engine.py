@@ -34,7 +34,7 @@ import torch
 
 from .. import ops
 from ..agg import AGGREGATORS, AggResult
-from ..attacks import DistanceEngine, run_attack
+from ..attacks import DistanceEngine, host_info, run_attack
 from ..config import AttackSpec, Config
 from ..data import DeviceTable, resolve_dataset
 from ..detect import HyperDetector
@@ -542,16 +542,15 @@ class FLEngine:
                 side.wait_event(ready)
             with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
                 for j, i, lc, atk in attack_jobs:
-                    gen = torch.Generator(device=dev if dev.type == "cuda" else "cpu")
-                    gen.manual_seed(lc.seed * 1009 + lc.training_round)
-                    res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist, gen)
+                    res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist,
+                                     seed=lc.seed * 1009 + lc.training_round)
                     if res.ok and res.params is not None:
                         block[j, :self.P] = res.params
                         block[j, self.P + 1] = 1.0
                         hm[j, 1] = 1.0
                     self._attack_info = res.info
-                    if self.verbose:
-                        print_with_color(f"[===] Client {i} attacks with {atk.mode} {res.info}", "red")
+                    if self.verbose:  # (reads the attack's device scalars back: verbose runs only)
+                        print_with_color(f"[===] Client {i} attacks with {atk.mode} {host_info(res.info)}", "red")
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
         tp2 = time.perf_counter()
@@ -839,7 +838,7 @@ class FLEngine:
                "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_checkpoint": t5 - t4, "t_round": t5 - t0,
                "n_selected": len(self.selected), "removed": removed}
         if self._attack_info:
-            rec["attack"] = {k: v for k, v in self._attack_info.items() if isinstance(v, (int, float))}
+            rec["attack"] = {k: v for k, v in host_info(self._attack_info).items() if isinstance(v, (int, float))}
         lazy = info.pop("_lazy", None)
         if lazy is not None:
             info.update(lazy())

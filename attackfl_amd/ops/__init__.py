@@ -93,16 +93,30 @@ def lie_candidate(G: torch.Tensor, z: float) -> torch.Tensor:
     return composite.lie_candidate(G, z)
 
 
+def pairwise_sqdist(G: torch.Tensor) -> torch.Tensor:
+    """[K, K] fp64 squared L2 distances between rows.  Device: the centred Gram matrix on fp64 MFMA for
+    K <= 64 (``k_gram_f64``), the fp64 difference loop beyond."""
+    if _dev(G):
+        if G.shape[0] <= 64:
+            return native().pairwise_sqdist_gram(G.contiguous())
+        return native().pairwise_sqdist(G.contiguous())
+    return composite.pairwise_l2(G) ** 2
+
+
 def pairwise_l2(G: torch.Tensor) -> torch.Tensor:
     if _dev(G):
-        return native().pairwise_sqdist(G.contiguous()).clamp_min(0.0).sqrt()
+        return pairwise_sqdist(G).clamp_min(0.0).sqrt()
     return composite.pairwise_l2(G)
 
 
-def pairwise_sqdist(G: torch.Tensor) -> torch.Tensor:
-    if _dev(G):
-        return native().pairwise_sqdist(G.contiguous())
-    return composite.pairwise_l2(G) ** 2
+def noise(own: torch.Tensor, sigma: float, seed: int) -> torch.Tensor:
+    """``own + sigma * N(0, 1)`` from Philox4x32-10 keyed by ``seed`` (Random attack); the CPU mirror draws
+    the same uniforms."""
+    if _dev(own):
+        return native().noise_philox(own.contiguous(), float(sigma),
+                                     (int(seed) & 0xFFFFFFFFFFFFFFFF) - (1 << 64) if (int(seed) & (1 << 63))
+                                     else int(seed) & 0xFFFFFFFFFFFFFFFF)
+    return composite.noise(own, sigma, seed)
 
 
 def segment_l2_sum(diffs: torch.Tensor, slots) -> torch.Tensor:

@@ -164,3 +164,47 @@ def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale:
     gW = torch.outer(delta, feat) * scale
     adam_step(W.view(-1), gW.view(-1), m_wb[:P * H], v_wb[:P * H], step, lr, beta1, beta2, eps)
     adam_step(b, delta * scale, m_wb[P * H:P * H + P], v_wb[P * H:P * H + P], step, lr, beta1, beta2, eps)
+
+
+# ---------------------------------------------------------------- Philox noise (Random attack, K-G10)
+_PHILOX_M0, _PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
+_PHILOX_W0, _PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+_M32 = 0xFFFFFFFF
+
+
+def philox4x32(counter_lo, seed: int):
+    """Philox4x32-10 of counters (lo, hi, 0, 0) for a uint64 numpy array ``counter_lo`` -> 4 uint32 arrays
+    (the exact integers ``k_noise_philox`` draws; ``agg.hip``)."""
+    import numpy as np
+
+    g = counter_lo.astype(np.uint64)
+    c0, c1 = g & np.uint64(_M32), g >> np.uint64(32)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0, k1 = seed & _M32, (seed >> 32) & _M32
+    for _ in range(10):
+        p0 = c0 * np.uint64(_PHILOX_M0)
+        p1 = c2 * np.uint64(_PHILOX_M1)
+        h0, l0 = p0 >> np.uint64(32), p0 & np.uint64(_M32)
+        h1, l1 = p1 >> np.uint64(32), p1 & np.uint64(_M32)
+        c0, c1, c2, c3 = h1 ^ c1 ^ np.uint64(k0), l1, h0 ^ c3 ^ np.uint64(k1), l0
+        k0, k1 = (k0 + _PHILOX_W0) & _M32, (k1 + _PHILOX_W1) & _M32
+    return c0, c1, c2, c3
+
+
+def philox_normal(n: int, seed: int):
+    """N(0, 1) draws of ``k_noise_philox``: Box-Muller on (x + 1) * 2^-32 uniforms in fp64 -> [n] float64."""
+    import numpy as np
+
+    groups = (n + 3) // 4
+    c0, c1, c2, c3 = philox4x32(np.arange(groups, dtype=np.uint64), seed)
+    u = [(c.astype(np.float64) + 1.0) * 2.0 ** -32 for c in (c0, c1, c2, c3)]
+    r0, r1 = np.sqrt(-2.0 * np.log(u[0])), np.sqrt(-2.0 * np.log(u[2]))
+    t0, t1 = 2.0 * np.pi * u[1], 2.0 * np.pi * u[3]
+    z = np.stack([r0 * np.cos(t0), r0 * np.sin(t0), r1 * np.cos(t1), r1 * np.sin(t1)], axis=1).reshape(-1)
+    return z[:n]
+
+
+def noise(own: torch.Tensor, sigma: float, seed: int) -> torch.Tensor:
+    z = torch.from_numpy(philox_normal(own.numel(), int(seed) & 0xFFFFFFFFFFFFFFFF)).to(torch.float32)
+    return own + float(sigma) * z.reshape(own.shape).to(own.device)

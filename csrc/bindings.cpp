@@ -66,6 +66,30 @@ torch::Tensor pairwise_sqdist(torch::Tensor G) {
   return D;
 }
 
+// pairwise squared distances through the centred Gram matrix on fp64 MFMA (K <= 64)
+torch::Tensor pairwise_sqdist_gram(torch::Tensor G) {
+  check_dev(G, "G", torch::kFloat32);
+  TORCH_CHECK(G.dim() == 2 && G.size(0) >= 1 && G.size(0) <= 64, "G must be [K <= 64, P]");
+  const int K = G.size(0);
+  const long P = G.size(1);
+  auto D = torch::zeros({K, K}, G.options().dtype(torch::kFloat64));
+  auto scratch = torch::empty({(long)afl_gram_partials(K, P)}, D.options());
+  TORCH_CHECK(afl_pair_sqdist_gram(G.data_ptr<float>(), K, P, scratch.data_ptr<double>(), D.data_ptr<double>(),
+                                   cur()) == 0, "gram launch failed");
+  AFL_CHECK_LAUNCH();
+  return D;
+}
+
+// own + sigma * N(0,1), Philox4x32-10 keyed by `seed` (Random attack)
+torch::Tensor noise_philox(torch::Tensor own, double sigma, int64_t seed) {
+  check_dev(own, "own", torch::kFloat32);
+  auto out = torch::empty_like(own);
+  if (own.numel() == 0) return out;
+  afl_noise_philox(own.data_ptr<float>(), out.data_ptr<float>(), own.numel(), (float)sigma, (uint64_t)seed, cur());
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 torch::Tensor segment_sqsum(torch::Tensor X, torch::Tensor tiles, torch::Tensor segf, int64_t S) {
   check_dev(X, "X", torch::kFloat32);
   check_dev(tiles, "tiles", torch::kInt32);
@@ -527,6 +551,8 @@ torch::Tensor crc32(torch::Tensor data) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("crc32", &crc32);
+  m.def("pairwise_sqdist_gram", &pairwise_sqdist_gram);
+  m.def("noise_philox", &noise_philox);
   m.doc() = "attackfl_amd native gfx950 kernels";
   m.def("colstats", &colstats);
   m.def("pairwise_sqdist", &pairwise_sqdist);

@@ -265,6 +265,11 @@ int afl_attn_lp(int L);
 int afl_attn_fwd(const AflAttn& a, hipStream_t s);
 int afl_attn_bwd(const AflAttn& a, hipStream_t s);
 
+// agg.hip — Gram-form pairwise distances (fp64 MFMA, rows centred on row 0; K <= 64) and Philox noise
+int afl_gram_partials(int K, long P);  // doubles of scratch afl_pair_sqdist_gram needs
+int afl_pair_sqdist_gram(const float* G, int K, long P, double* partial, double* D, hipStream_t s);
+void afl_noise_philox(const float* own, float* out, long P, float sigma, uint64_t seed, hipStream_t s);
+
 // comm.hip — one-shot intra-node all-gather over IPC-mapped peer buffers (xGMI)
 #define AFL_IPC_MAX_PEERS 16
 #define AFL_IPC_FLAG_STRIDE 32  // uint32 per flag: one 128-byte line per (parity, sender)

@@ -2,7 +2,9 @@
 //
 //   colstats        column mean / unbiased std (+ LIE candidate mean + z*std)      K-G2/K-G3
 //   weighted_rows   out = sum_i w_i U_i (fp64 weights, fp64 accumulate)            K-G1 FedAvg
-//   pair_sqdist     D2[i][j] = ||U_i - U_j||^2 (difference form, no cancellation)   K-G4b / Krum
+//   pair_sqdist     D2[i][j] = ||U_i - U_j||^2 (difference form, no cancellation)   K-G4b / Krum (K > 64)
+//   gram_f64        the same from the centred Gram matrix on fp64 MFMA               K-G4b / Krum (K <= 64)
+//   noise_philox    own + sigma * N(0,1) from Philox4x32-10 + Box-Muller             K-G10
 //   seg_reduce      per-(row, state_dict tensor) partial sums over tiles             K-G4a / K-G5
 //   coord_select    coordinate-wise lower median / trimmed mean (register sort)      K-G6
 //   row_dots        <u,u>, <u,r>, <r,r> per row                                      K-G8
@@ -104,6 +106,152 @@ void afl_pair_sqdist(const float* G, int K, long P, double* partial, double* D, 
   hipLaunchKernelGGL(k_pair_sqdist, dim3(nb), dim3(256), lds, s, G, K, P, partial);
   int M = K * (K - 1) / 2;
   if (M > 0) hipLaunchKernelGGL(k_pair_reduce, dim3(afl_cdiv(M, 256)), dim3(256), 0, s, partial, nb, K, D);
+}
+
+// ============================================================================ pairwise via Gram (MFMA)
+// D2[i][j] = ||G_i - G_j||^2 from the Gram matrix of the rows CENTRED on row 0 (X_i = G_i - G_0): the
+// difference-form correction — model updates are close to each other, so ||G_i||^2 + ||G_j||^2 - 2<G_i,G_j>
+// of the raw rows would cancel catastrophically, while the centred rows have norms of the order of the
+// distances themselves.  The products run on v_mfma_f64_16x16x4_f64 (fp32 inputs widened to fp64: exact
+// products, fp64 accumulation), so the result is as accurate as the fp64 difference loop above.
+// K <= 64 (T <= 4 row tiles of 16).  Block b covers GR_CH columns; each of its 4 waves a quarter of them,
+// 16 columns per step: lane l loads 4 consecutive columns of row (tile*16 + (l & 15)), column group l >> 4,
+// and issues 4 MFMAs per tile pair (element q of the 4 = MFMA q's k = l >> 4: the 16 columns are summed in a
+// fixed, data-independent order).  f64 C/D layout: acc[r] = C[(l >> 4) + 4r][l & 15].
+constexpr int GR_CH = 1024;
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+template <int T>
+__global__ void __launch_bounds__(256) k_gram_f64(const float* __restrict__ G, int K, long P,
+                                                  double* __restrict__ partial) {
+  constexpr int NP = T * (T + 1) / 2;
+  __shared__ double red[4][NP * 256];  // NP <= 10 tile pairs x 16 x 16
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, grp = lane >> 4;
+  d4v acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = d4v{0.0, 0.0, 0.0, 0.0};
+  const long c_begin = (long)blockIdx.x * GR_CH + wave * (GR_CH / 4);
+  for (int st = 0; st < GR_CH / 4 / 16; ++st) {
+    const long c0 = c_begin + st * 16 + grp * 4;
+    float x[T][4];
+    float ctr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ctr[q] = c0 + q < P ? G[c0 + q] : 0.f;  // row 0 = the centre
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = t * 16 + r16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        x[t][q] = (row < K && c0 + q < P) ? G[(long)row * P + c0 + q] - ctr[q] : 0.f;
+    }
+    int p = 0;
+#pragma unroll
+    for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+      for (int tj = ti; tj < T; ++tj, ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)x[ti][q], (double)x[tj][q], acc[p], 0, 0, 0);
+  }
+  // fixed-order reduction over the 4 waves
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][p * 256 + (grp + 4 * r) * 16 + r16] = acc[p][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < NP * 256; e += 256)
+    partial[(long)blockIdx.x * NP * 256 + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
+// sum the block partials in block order, then D2 = g_ii + g_jj - 2 g_ij (clamped at 0), symmetric, zero diagonal
+__global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ partial, int nb, int K, int T,
+                                                     double* __restrict__ gram, double* __restrict__ D) {
+  const int NP = T * (T + 1) / 2;
+  for (int e = threadIdx.x; e < NP * 256; e += 256) {
+    double a = 0.0;
+    for (int b = 0; b < nb; ++b) a += partial[(long)b * NP * 256 + e];
+    // tile pair index -> (ti, tj)
+    int p = e >> 8, ti = 0;
+    while (p >= T - ti) { p -= T - ti; ++ti; }
+    const int tj = ti + p;
+    const int i = ti * 16 + ((e & 255) >> 4), j = tj * 16 + (e & 15);
+    if (i < K && j < K) {
+      gram[i * K + j] = a;
+      gram[j * K + i] = a;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < K * K; e += 256) {
+    const int i = e / K, j = e % K;
+    const double d = i == j ? 0.0 : gram[i * K + i] + gram[j * K + j] - 2.0 * gram[i * K + j];
+    D[e] = d > 0.0 ? d : 0.0;
+  }
+}
+
+int afl_gram_partials(int K, long P) {
+  const int T = (K + 15) / 16;
+  return afl_cdiv(P, GR_CH) * T * (T + 1) / 2 * 256 + K * K;
+}
+
+int afl_pair_sqdist_gram(const float* G, int K, long P, double* partial, double* D, hipStream_t s) {
+  if (K < 1 || K > 64) return (int)hipErrorInvalidValue;
+  const int T = (K + 15) / 16, nb = afl_cdiv(P, GR_CH);
+  switch (T) {
+    case 1: hipLaunchKernelGGL(k_gram_f64<1>, dim3(nb), dim3(256), 0, s, G, K, P, partial); break;
+    case 2: hipLaunchKernelGGL(k_gram_f64<2>, dim3(nb), dim3(256), 0, s, G, K, P, partial); break;
+    case 3: hipLaunchKernelGGL(k_gram_f64<3>, dim3(nb), dim3(256), 0, s, G, K, P, partial); break;
+    default: hipLaunchKernelGGL(k_gram_f64<4>, dim3(nb), dim3(256), 0, s, G, K, P, partial); break;
+  }
+  double* gram = partial + (long)nb * T * (T + 1) / 2 * 256;
+  hipLaunchKernelGGL(k_gram_reduce, dim3(1), dim3(256), 0, s, partial, nb, K, T, gram, D);
+  return (int)hipGetLastError();
+}
+
+// ============================================================================ Philox noise (Random attack)
+// out = own + sigma * N(0, 1) (reference create_random_base_model, src/Utils.py:52-57).  Philox4x32-10
+// (Salmon et al., SC'11) keyed by the 64-bit seed, counter = (element group, 0, 0, 0): one call gives 4
+// uniforms for 4 consecutive elements, turned into normals by Box-Muller (2 pairs).  Stateless and
+// deterministic: the same (seed, P) always yields the same noise, on any rank.  The Python mirror
+// (ops/composite.py:philox_normal) reproduces the uniforms bit for bit.
+__device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                             uint32_t k1) {
+  const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+  const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+  const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+  c0 = n0;
+  c1 = l1;
+  c2 = n2;
+  c3 = l0;
+}
+
+__global__ void __launch_bounds__(256) k_noise_philox(const float* __restrict__ own, float* __restrict__ out, long P,
+                                                      float sigma, uint32_t k0, uint32_t k1) {
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;  // element group of 4
+  if (g * 4 >= P) return;
+  uint32_t c0 = (uint32_t)g, c1 = (uint32_t)(g >> 32), c2 = 0, c3 = 0, a = k0, b = k1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c0, c1, c2, c3, a, b);
+    a += 0x9E3779B9u;
+    b += 0xBB67AE85u;
+  }
+  // uniforms in (0, 1]: (x + 1) * 2^-32 in fp64 then Box-Muller in fp64 (no log(0); one rounding at the end)
+  const double u0 = ((double)c0 + 1.0) * 2.3283064365386963e-10, u1 = ((double)c1 + 1.0) * 2.3283064365386963e-10;
+  const double u2 = ((double)c2 + 1.0) * 2.3283064365386963e-10, u3 = ((double)c3 + 1.0) * 2.3283064365386963e-10;
+  const double r0 = sqrt(-2.0 * log(u0)), r1 = sqrt(-2.0 * log(u2));
+  const double t0 = 6.283185307179586 * u1, t1 = 6.283185307179586 * u3;
+  const double z[4] = {r0 * cos(t0), r0 * sin(t0), r1 * cos(t1), r1 * sin(t1)};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long i = g * 4 + q;
+    if (i < P) out[i] = own[i] + sigma * (float)z[q];
+  }
+}
+
+void afl_noise_philox(const float* own, float* out, long P, float sigma, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_noise_philox, dim3(afl_cdiv(afl_cdiv(P, 4), 256)), dim3(256), 0, s, own, out, P, sigma,
+                     (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
 // ============================================================================ segmented reductions

@@ -65,7 +65,7 @@ def test_bisection_attacks_match_reference(kind, fn, scale):
     own = G[0].clone()
     res = fn(G, own, DistanceEngine(lay, "spectral"))
     ref_sd, ref_gamma = ref_bisection(gen, kind)
-    assert res.info["gamma"] == pytest.approx(ref_gamma)
+    assert attacks.host_info(res.info)["gamma"] == pytest.approx(ref_gamma)
     assert torch.allclose(res.params, lay.flatten(ref_sd), atol=1e-5)
 
 
@@ -79,7 +79,7 @@ def test_bisection_flat_mode_runs_and_is_consistent():
     D = torch.cdist(G.double(), G.double())
     thr = D.max().item()
     cand = res.params.double()
-    assert res.info["threshold"] == pytest.approx(thr, rel=1e-9)
+    assert attacks.host_info(res.info)["threshold"] == pytest.approx(thr, rel=1e-9)
     assert torch.isfinite(cand).all()
 
 
@@ -89,7 +89,7 @@ def test_cnn_spectral_on_3d_does_not_crash():
     G = torch.stack([lay.flatten(g) for g in gen])
     res = attacks.min_sum(G, G[0], DistanceEngine(lay, "spectral"))
     ref_sd, ref_gamma = ref_bisection(gen, "sum")  # compute_distance matricises 3-D (documented deviation)
-    assert res.info["gamma"] == pytest.approx(ref_gamma)
+    assert attacks.host_info(res.info)["gamma"] == pytest.approx(ref_gamma)
 
 
 def test_lie_matches_reference():
@@ -120,9 +120,33 @@ def test_bisection_single_genuine_returns_own():
 
 def test_random_attack_scale():
     own = torch.zeros(100000)
-    g = torch.Generator().manual_seed(0)
-    res = run_attack("Random", [0.5], own, None, None, g)
-    assert abs(res.params.std().item() - 0.5) < 0.01
+    res = run_attack("Random", [0.5], own, None, None, seed=3)
+    assert abs(res.params.std().item() - 0.5) < 0.01 and abs(res.params.mean().item()) < 0.01
+    assert torch.equal(run_attack("Random", [0.5], own, None, None, seed=3).params, res.params)
+    assert not torch.equal(run_attack("Random", [0.5], own, None, None, seed=4).params, res.params)
+
+
+def test_philox_matches_known_answer():
+    """Philox4x32-10 known-answer vector (Random123 kat_vectors: counter 0, key 0)."""
+    import numpy as np
+
+    from attackfl_amd.ops.composite import philox4x32
+
+    c = philox4x32(np.zeros(1, dtype=np.uint64), 0)
+    assert [int(x[0]) for x in c] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+
+
+@pytest.mark.parametrize("decisions", range(64))
+def test_device_bisection_matches_host_loop(decisions):
+    """Every accept/reject path of the reference loop (γ0 50, τ 1: 6 iterations) through the unrolled
+    device form gives the same last-tried and last-accepted γ."""
+    seq = [(decisions >> i) & 1 == 1 for i in range(6)]
+    it = iter(seq)
+    last, n, succ = attacks._bisect(lambda g: next(it), 50.0, 1.0)
+    it2 = iter(seq)
+    dl, dn, ds = attacks._bisect_device(lambda g: torch.tensor(next(it2)), 50.0, 1.0, "cpu")
+    assert (float(dl), dn, float(ds)) == (last, n, succ)
+    assert attacks.bisect_iterations(50.0, 1.0) == 6
 
 
 def test_unknown_attack():

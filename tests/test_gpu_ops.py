@@ -214,3 +214,29 @@ def test_crc32_matches_zlib(gpu, n):
     x = torch.randn(n, generator=g)
     got = int(native().crc32(x.cuda()).item()) & 0xFFFFFFFF
     assert got == zlib.crc32(x.numpy().tobytes())
+
+
+@pytest.mark.parametrize("K,P", [(1, 1000), (2, 47693), (8, 47693), (8, 5), (17, 20000), (40, 3001), (64, 9000)])
+def test_pairwise_gram_mfma_matches_fp64(gpu, K, P):
+    """k_gram_f64 (centred Gram on fp64 MFMA) against the fp64 difference form; nearby rows (model updates)
+    are where the uncentred Gram form would cancel."""
+    g = torch.Generator().manual_seed(K * 1000 + P)
+    G = torch.randn(1, P, generator=g) * 3.0 + 1e-3 * torch.randn(K, P, generator=g)
+    got = native().pairwise_sqdist_gram(G.cuda()).cpu()
+    Gd = G.double()
+    ref = ((Gd[:, None, :] - Gd[None, :, :]) ** 2).sum(-1)
+    assert torch.allclose(got, ref, rtol=1e-9, atol=1e-12 * float(ref.max() + 1))
+    assert torch.equal(got, got.t()) and bool((got.diagonal() == 0).all())
+    if K <= 64 and K > 1:  # the dispatcher takes this path
+        assert torch.equal(ops.pairwise_sqdist(G.cuda()).cpu(), got)
+
+
+@pytest.mark.parametrize("P", [1, 3, 4, 1001, 203649])
+def test_philox_noise_matches_cpu_mirror(gpu, P):
+    g = torch.Generator().manual_seed(P)
+    own = torch.randn(P, generator=g)
+    for seed in (0, 12345678901234):
+        got = ops.noise(own.cuda(), 0.3, seed).cpu()
+        ref = ops.noise(own, 0.3, seed)
+        assert torch.allclose(got, ref, atol=2e-6, rtol=0)
+        assert torch.equal(ops.noise(own.cuda(), 0.3, seed).cpu(), got)   # deterministic
