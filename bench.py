@@ -32,6 +32,12 @@ BASELINE_ROUNDS_PER_S = 0.18  # measured proxy of the reference, wh
 MODEL_BASELINES = {"TransformerModel": BASELINE_ROUNDS_PER_S, "CNNModel": 0.075, "RNNModel": 0.15}
 
 
+def shared_gpu_queues(ranks_per_gpu: int) -> int:
+    """Hardware queues per process when ``ranks_per_gpu`` processes share one GPU (kept in sync with
+    ``attackfl_amd.parallel.launcher.shared_gpu_queues``; bench.py must set it before importing torch)."""
+    return 4 if ranks_per_gpu <= 2 else (2 if ranks_per_gpu <= 8 else 1)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -45,6 +51,12 @@ def main() -> int:
     ap.add_argument("--data-name", default="ICU")
     ap.add_argument("--profile-rounds", action="store_true", help="print per-phase timings to stderr")
     args = ap.parse_args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1 and os.environ.get("AFL_BENCH_DEVICE") is not None:
+        # several ranks on ONE GPU: cap each process's hardware queues so that all ranks' queues stay mapped
+        # (oversubscribed queues are time-sliced: 8 ranks x 4 queues ran at 43 rounds/s, x 2 at 89)
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)  # the runtime default is 4 (never raised here)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(cur, shared_gpu_queues(world_env)))
 
     import torch
     import torch.distributed as dist

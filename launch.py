@@ -36,6 +36,13 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default=None)
     ap.add_argument("--rounds", type=int, default=None, help="override server.num-round")
     args = ap.parse_args(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1 and args.device and args.device.startswith("cuda:"):
+        # every rank pinned to one GPU: keep all ranks' hardware queues mapped (see bench.py)
+        from bench import shared_gpu_queues
+
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)  # the runtime default is 4 (never raised here)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(cur, shared_gpu_queues(world_env)))
 
     import torch
 
