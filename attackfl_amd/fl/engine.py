@@ -244,7 +244,6 @@ class FLEngine:
         self._pending = None
         self._has_attackers = any(ci.attack is not None for ci in self.table)
         self._speculative = (bool(cfg.engine.get("speculative", True)) and self.device.type == "cuda"
-                             and self.mode != "FLTrust"
                              and not cfg.hyper_detection.get("enable", False) and not cfg.load_parameters
                              and not cfg.engine.get("save-state", False) and not self.phase_sync
                              and self.trainer is not None)

@@ -211,3 +211,54 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
         mnoise = max(abs(a - b) for (_, a), (_, b) in zip(h0, h2) if a is not None)
         for (_, a), (_, b) in zip(h0, h1):
             assert (a is None) == (b is None) and (a is None or abs(a - b) <= 3 * mnoise + 1e-3), (h0, h1, h2)
+
+
+@pytest.mark.parametrize("mode", ["trimmed_mean", "median", "krum", "shieldfl", "scionfl", "gmm", "FLTrust",
+                                  "fltracer", "byzantine"])
+@pytest.mark.parametrize("attack", ["Min-Max", "LIE"])
+def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
+    """Every robust server mode on the native path (fused TransformerModel trainer, device aggregators,
+    device validation) with one attacker of 5 from round 2 (reference server.py:286-494)."""
+    d = {
+        "server": {"num-round": 3, "clients": 5, "mode": mode, "model": "TransformerModel", "data-name": "ICU",
+                   "genuine-rate": 1.0, "data-distribution": {"num-data-range": [300, 500]}},
+        "learning": {"epoch": 2, "batch-size": 128},
+        "data": {"synthetic": True, "train-size": 4000, "test-size": 1000},
+        "engine": {"checkpoint-dir": str(tmp_path), "trainer": "auto", "metrics": str(tmp_path / "m.jsonl")},
+        "log_path": str(tmp_path),
+    }
+    cfg = from_dict(d)
+    spec = "4:Min-Max:2" if attack == "Min-Max" else "4:LIE:2:0.74"
+    eng = FLEngine(cfg, device="cuda", table=build_client_table(cfg, 1, parse_attackers(spec)), verbose=False)
+    assert eng.trainer.kind == "fused"
+    hist = eng.run()
+    eng.close()
+    assert [r["ok"] for r in hist] == [True, True, True]
+    assert all(0.0 <= r["metric"] <= 1.0 for r in hist)
+    assert "attack" in hist[1] and "attack" in hist[2]
+    if mode == "FLTrust":
+        assert len(hist[-1]["trust"]) == 5 and all(t >= 0.0 for t in hist[-1]["trust"])
+    assert os.path.exists(os.path.join(tmp_path, "TransformerModel.pth"))
+
+
+def test_hyper_detection_end_to_end(gpu, tmp_path):
+    """hyper-detection on the device path (reference server.py:496-536): 19 rounds (detection from round 18),
+    embeddings history saved, decisions made on every round."""
+    d = {
+        "server": {"num-round": 19, "clients": 4, "mode": "hyper", "model": "TransformerModel", "data-name": "ICU",
+                   "hyper-detection": {"enable": True, "cosine-search": 10, "n_components": 2, "eps": 0.5,
+                                       "min_samples": 2},
+                   "data-distribution": {"num-data-range": [200, 300]}},
+        "learning": {"epoch": 1, "batch-size": 128},
+        "data": {"synthetic": True, "train-size": 3000, "test-size": 500},
+        "engine": {"checkpoint-dir": str(tmp_path), "trainer": "auto"},
+        "log_path": str(tmp_path),
+    }
+    cfg = from_dict(d)
+    eng = FLEngine(cfg, device="cuda", table=build_client_table(cfg, 1, parse_attackers("3:Opt-Fang:2")), verbose=False)
+    assert not eng._speculative  # detection may roll the hypernetwork back: no speculative launch
+    hist = eng.run()
+    eng.close()
+    assert sum(r["ok"] for r in hist) == 19
+    assert os.path.exists(os.path.join(tmp_path, "all_embeddings.npy"))
+    assert all(isinstance(r["removed"], list) for r in hist)
