@@ -21,7 +21,7 @@ import sysconfig
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "attackfl_amd")
 BUILD = os.path.join(ROOT, "build", "obj")
-OUT = os.path.join(PKG, "_C.so")
+OUT = os.environ.get("AFL_BUILD_OUT") or os.path.join(PKG, "_C.so")  # AFL_BUILD_OUT: A/B variant builds
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 

@@ -21,8 +21,9 @@ Extensions (all optional, defaults keep reference behaviour):
   synthetic: auto | true | false   (auto = use the reference pickles when present)
   train-size / test-size / seed / har-train-size / har-test-size
 ``engine:``
-  trainer: auto | fused | graph | eager  (fused = HIP persistent TransformerModel kernel; graph =
-                                    HIP-graph-replayed layer programs for CNN/RNN/HAR models)
+  trainer: auto | fused | graph | eager | oracle  (fused = HIP persistent TransformerModel / RNNModel
+                                    kernels; graph = HIP-graph-replayed layer programs for CNN/RNN/HAR models;
+                                    oracle = CPU fp32 twin of the fused TransformerModel trainer, same masks)
   distance: spectral | flat         (attack distance; spectral = reference ``torch.linalg.norm(ord=2)``)
   seed: int                         (torch / client RNG seed; the reference seeds only ``random``)
   metrics: path of the JSONL metrics file ('' disables)

@@ -340,6 +340,35 @@ class FusedTrainer:
         return Pending(fin, ok, losses)
 
 
+class OracleTrainer:
+    """CPU twin of the fused TransformerModel trainer: ``ops.transformer.reference_train`` (fp32 autograd with
+    the kernel's own hash dropout masks and Adam step sequence), so a CPU run follows the same client
+    trajectories as the GPU run up to bf16-vs-fp32 rounding (the attack study compares the two)."""
+
+    kind = "oracle"
+
+    def __init__(self, model_name: str, data_name: str, table: DeviceTable, device, verbose: bool = False):
+        if model_name != "TransformerModel" or data_name != "ICU":
+            raise ValueError("oracle trainer: TransformerModel/ICU")
+        from ..ops import transformer as T
+
+        self.T = T
+        self.table = table
+        self.device = torch.device(device)
+        self.verbose = verbose
+
+    def train(self, params, plan, lr, batch, seeds):
+        return self.launch(params, plan, lr, batch, seeds).result()
+
+    def launch(self, params, plan, lr, batch, seeds, seeds_dev=None) -> Pending:
+        p = params.detach().cpu().contiguous()
+        ok, losses = self.T.reference_train(p, self.table.rows.cpu(), plan.order.cpu(), plan.nd, plan.epochs, batch,
+                                            lr, [int(s) for s in seeds])
+        params.copy_(p.to(params.device))
+        res = ([bool(x) for x in ok.tolist()], losses.double())
+        return Pending(lambda: res)
+
+
 class GraphTrainer:
     """All local clients batched through a layer program; one HIP-graph replay per optimizer step."""
 
@@ -400,6 +429,8 @@ def make_trainer(kind: str, model_name: str, data_name: str, table: DeviceTable,
             kind = "eager"
     if kind == "fused":
         return FusedTrainer(model_name, data_name, table, device, verbose)
+    if kind == "oracle":
+        return OracleTrainer(model_name, data_name, table, device, verbose)
     if kind == "graph":
         return GraphTrainer(model_name, data_name, table, device, verbose)
     return EagerTrainer(model_name, data_name, table, device, verbose)

@@ -22,7 +22,17 @@ def native():
     global _NATIVE
     if _NATIVE is None:
         try:
-            from .. import _C  # noqa: F401
+            variant = os.environ.get("AFL_NATIVE_SO")  # A/B builds (tools/ab_native.sh): another in-tree .so
+            if variant:
+                import importlib.machinery
+                import importlib.util
+
+                loader = importlib.machinery.ExtensionFileLoader("attackfl_amd._C", variant)
+                spec = importlib.util.spec_from_file_location("attackfl_amd._C", variant, loader=loader)
+                _C = importlib.util.module_from_spec(spec)
+                loader.exec_module(_C)
+            else:
+                from .. import _C  # noqa: F401
 
             _NATIVE = _C
         except Exception as e:  # pragma: no cover - depends on build state
