@@ -471,6 +471,18 @@ class FLEngine:
                 train_rows.append(j)
                 train_nd.append(num_data)
                 train_seeds.append(lc.seed * 7 + lc.training_round)
+        if train_rows and attack_jobs:
+            # the attackers ride along with ZERO rows (nd = 0: the trainer leaves their models untouched), so the
+            # launch covers every local client in place — no gather / scatter of the trained rows — and their
+            # attack results are written into their local_params rows once the launch is done (_finish_local)
+            for j, i, lc, atk in attack_jobs:
+                train_rows.append(j)
+                train_nd.append(0)
+                train_seeds.append(lc.seed * 7 + lc.training_round)
+            order = sorted(range(len(train_rows)), key=lambda k: train_rows[k])
+            train_rows = [train_rows[k] for k in order]
+            train_nd = [train_nd[k] for k in order]
+            train_seeds = [train_seeds[k] for k in order]
         tq1 = time.perf_counter()
         # every per-round host value the device needs goes up in ONE asynchronous copy (a pageable
         # torch.tensor(..., device=) per item was a blocking copy each: ~1.5 ms of host time per round)
@@ -533,6 +545,7 @@ class FLEngine:
         dev = self.device
         hm = st["meta"]  # host mirror of the block's meta columns (ok filled in below): no device read needed
         tw = time.perf_counter()  # a speculative launch (run_round) may have been enqueued long before
+        atk_out = []  # (row, ok, malicious update)
         if attack_jobs:
             # the attackers do not train: their math runs on a side stream while the genuine clients'
             # training launch occupies its own CUs (the reference runs every client concurrently too)
@@ -543,20 +556,16 @@ class FLEngine:
                 for j, i, lc, atk in attack_jobs:
                     res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist,
                                      seed=lc.seed * 1009 + lc.training_round)
-                    if res.ok and res.params is not None:
-                        block[j, :self.P] = res.params
-                        block[j, self.P + 1] = 1.0
-                        hm[j, 1] = 1.0
+                    atk_out.append((j, res.ok and res.params is not None, res.params))
                     self._attack_info = res.info
                     if self.verbose:  # (reads the attack's device scalars back: verbose runs only)
                         print_with_color(f"[===] Client {i} attacks with {atk.mode} {host_info(res.info)}", "red")
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
         tp2 = time.perf_counter()
-        # single rank, every local client trained in place, no attacker rows: the round reads the update
-        # matrix straight from local_params and the meta columns from the host mirror (run_round)
-        self._plain_rows = (pending is not None and in_place and not attack_jobs and self.world == 1
-                            and not self.fast_fedavg and self.mode not in ("hyper", "FLTrust")
+        # single rank, every local client in the launch (attackers with zero rows), trained in place: the round
+        # reads the update matrix straight from local_params and the meta columns from the host mirror
+        self._plain_rows = (pending is not None and in_place and self.world == 1 and not self.fast_fedavg
                             and self._local_rows() == list(range(n_local)))
         self._pending = pending
         P, E = self.P, self.E
@@ -571,6 +580,12 @@ class FLEngine:
                     hm[j, 1] = 1.0 if o else 0.0
                     hm[j, META:META + E] = np.asarray(losses[k], dtype=np.float32)[:E]
             tp3 = time.perf_counter()
+            # the attack results replace the attackers' rows (ordered after the launch: it has read / written back
+            # their untouched models) — A-15: an attacker still reports its num_data, ok = the attack's result
+            for j, ok, mal in atk_out:
+                hm[j, 1] = 1.0 if ok else 0.0
+                if ok and in_place:
+                    self.local_params[j].copy_(mal)
             if self._plain_rows:
                 pass
             elif in_place:
@@ -581,6 +596,8 @@ class FLEngine:
                     block[:n_local, P + 1] = torch.tensor([1.0 if o else 0.0 for o in oks], device=dev)
                 block[:n_local, P + META:P + META + E] = (loss_dev if loss_dev is not None
                                                          else losses.to(dev)).float()
+                for j, ok, _ in atk_out:
+                    block[j, P + 1] = 1.0 if ok else 0.0
             else:
                 self.local_params.index_copy_(0, rows_d, params)
                 block[rows_d, :P] = params
@@ -588,8 +605,17 @@ class FLEngine:
                     [1.0 if o else 0.0 for o in oks], device=dev)
                 block[rows_d, P + 1] = okc
                 block[rows_d, P + META:P + META + E] = (loss_dev if loss_dev is not None else losses.to(dev)).float()
+                for j, ok, mal in atk_out:  # (only when no genuine client trains here: attackers are not launched)
+                    if ok:
+                        block[j, :P] = mal
+                    block[j, P + 1] = 1.0 if ok else 0.0
         else:
             tp3 = time.perf_counter()
+            for j, ok, mal in atk_out:  # every local client attacks: nothing was launched
+                hm[j, 1] = 1.0 if ok else 0.0
+                if ok:
+                    block[j, :P] = mal
+                block[j, P + 1] = 1.0 if ok else 0.0
         self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_prep_host": tq1 - tq, "t_lw_prep_upload": tq2 - tq1,
                           "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tw,
                           "t_lw_wait": tp3 - tp2, "t_lw_post": time.perf_counter() - tp3}

@@ -513,35 +513,23 @@ uint32_t crc_multmodp(uint32_t a, uint32_t b) {  // a (*) b mod P, reflected; a 
   return p;
 }
 
-uint32_t crc_x8n(long nbytes) {  // x^(8 * nbytes) mod P
-  uint32_t sq[64];
-  uint32_t p = 1u << 30;  // x^1
-  for (int k = 0; k < 64; ++k) {
-    sq[k] = p;  // x^(2^k)
-    p = crc_multmodp(p, p);
-  }
-  uint64_t e = (uint64_t)nbytes * 8;
-  uint32_t r = 1u << 31;  // x^0
-  for (int k = 0; e; ++k, e >>= 1)
-    if (e & 1) r = crc_multmodp(sq[k], r);
-  return r;
-}
-
 // zlib-compatible CRC-32 of the bytes of a contiguous device tensor -> int32 device tensor [1] (the CRC's bits)
 torch::Tensor crc32(torch::Tensor data) {
   TORCH_CHECK(data.is_cuda() && data.is_contiguous(), "data must be a contiguous device tensor");
   const long nbytes = data.numel() * (long)data.element_size();
   TORCH_CHECK(nbytes > 0 && nbytes % 4 == 0, "crc32: byte count must be a positive multiple of 4");
-  const long nchunks = afl_crc32_partials(nbytes);
-  const long per = (nchunks + 255) / 256;
-  const long nparts = (nchunks + per - 1) / per;
-  const long last_chunk = nbytes - (nchunks - 1) * 256;
-  const long last_part = nbytes - (nparts - 1) * per * 256;
-  auto opts = data.options().dtype(torch::kInt32);
-  auto part = torch::empty({nchunks}, opts);
-  auto out = torch::empty({1}, opts);
-  TORCH_CHECK(afl_crc32(data.data_ptr(), nbytes, (uint32_t*)part.data_ptr<int>(), (uint32_t*)out.data_ptr<int>(),
-                        crc_x8n(256), crc_x8n(last_chunk), crc_x8n(per * 256), crc_x8n(last_part), cur()) == 0,
+  uint32_t x2k[48];
+  uint32_t p = 1u << 30;  // x^1
+  for (int k = 0; k < 48; ++k) {
+    x2k[k] = p;  // x^(2^k)
+    p = crc_multmodp(p, p);
+  }
+  uint32_t init = 0xFFFFFFFFu;  // the init register shifted through all nbytes: 0xFFFFFFFF (*) x^(8 nbytes)
+  uint64_t e = (uint64_t)nbytes * 8;
+  for (int k = 0; e; ++k, e >>= 1)
+    if (e & 1) init = crc_multmodp(x2k[k], init);
+  auto out = torch::full({1}, (int64_t)(int32_t)(~init), data.options().dtype(torch::kInt32));
+  TORCH_CHECK(afl_crc32(data.data_ptr(), nbytes, x2k, (uint32_t*)out.data_ptr<int>(), cur()) == 0,
               "crc32 launch failed");
   AFL_CHECK_LAUNCH();
   return out;

@@ -284,9 +284,7 @@ int afl_ipc_alloc(int world, long cap, float** base);
 int afl_ipc_all_gather(const float* src, long n, const AflIpcPeers& peers, int rank, long cap, uint32_t epoch,
                        int* status, uint64_t deadline_ticks, hipStream_t s);
 
-// crc.hip — CRC-32 (IEEE 802.3, zlib's crc32) of a device buffer: the checkpoint writer's zip records
-// x_chunk = x^(8*256) mod P, x_part / x_part_last = x^(8 * bytes of a full / the last combine part) mod P,
-// x_last = x^(8 * bytes of the last chunk) mod P (all in zlib's reflected representation)
-int afl_crc32_partials(long nbytes);
-int afl_crc32(const void* data, long nbytes, uint32_t* chunk_crcs, uint32_t* out, uint32_t x_chunk, uint32_t x_last,
-              uint32_t x_part, uint32_t x_part_last, hipStream_t s);
+// crc.hip — CRC-32 (IEEE 802.3, zlib's crc32) of a device buffer: the checkpoint writer's zip records.
+// x2k[k] = x^(2^k) mod P (k < 48, zlib's reflected representation); *out must hold ~(0xFFFFFFFF (*) x^(8 nbytes))
+// on entry (the launch XORs every chunk's shifted CRC into it, leaving the final CRC)
+int afl_crc32(const void* data, long nbytes, const uint32_t* x2k, uint32_t* out, hipStream_t s);

@@ -2,14 +2,17 @@
 // buffer, for the checkpoint writer (attackfl_amd/utils/ckpt.py).  The writer emits the reference's
 // torch.save zip layout itself (server.py:549-553 writes one .pth per successful round): per round only
 // the storage bytes and their CRC change, and the CRC of a 19.5 MB hypernetwork arena costs ~23 ms on
-// one host core (zlib) — longer than a round.  Here it is two launches on the checkpoint stream:
+// one host core (zlib) — longer than a round.  Here it is ONE launch on the checkpoint stream, fully
+// parallel (no sequential fold):
 //
-//   k_crc_chunks   one thread per 256-byte chunk: slice-by-4 table CRC (tables in LDS) -> crc[chunk]
-//   k_crc_combine  one workgroup: thread t folds a contiguous run of chunk CRCs, thread 0 folds the runs
-//
-// Folding uses CRC linearity: crc(A || B) = (x^(8|B|) mod P) (*) crc(A)  ^  crc(B), where (*) is the
-// carry-less product modulo P in the reflected representation; the x^(8|B|) constants are computed on
-// the host (crc32_consts in bindings.cpp) for the three run lengths that occur.
+//   CRC linearity over GF(2): with R(M) the CRC register after M from a zero register (no final xor),
+//   R(C_0 || ... || C_{n-1}) = XOR_i  R(C_i) (*) x^(8 * (bytes after C_i))  mod P,
+//   and zlib's crc32(M) = ~(R(M) ^ (0xFFFFFFFF (*) x^(8 |M|))).
+//   Thread i: slice-by-4 table CRC of its 256-byte chunk (tables in LDS) -> R(C_i); its shift constant
+//   x^(8 * (L - end_i)) from the host's table of x^(2^k) (<= 40 products); the product is XORed
+//   into the result with a wave xor-reduction and one atomic xor per workgroup (xor is exact and
+//   order-free: the result is deterministic).  The result word is pre-set to ~(0xFFFFFFFF (*) x^(8L))
+//   by the host, so it ends as the final CRC.
 #include "common.h"
 #include "kernels.h"
 
@@ -31,9 +34,14 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
-__global__ void __launch_bounds__(256) k_crc_chunks(const uint32_t* __restrict__ data, long nbytes,
-                                                    uint32_t* __restrict__ crcs) {
+struct CrcPow {
+  uint32_t x2k[48];  // x^(2^k) mod P, k = 0..47
+};
+
+__global__ void __launch_bounds__(256) k_crc32(const uint32_t* __restrict__ data, long nbytes, CrcPow pw,
+                                               uint32_t* __restrict__ out) {
   __shared__ uint32_t T[4][256];
+  __shared__ uint32_t red[4];
   const int t = threadIdx.x;
   uint32_t c = (uint32_t)t;
   for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
@@ -47,63 +55,49 @@ __global__ void __launch_bounds__(256) k_crc_chunks(const uint32_t* __restrict__
   __syncthreads();
   const long chunk = (long)blockIdx.x * blockDim.x + t;
   const long b0 = chunk * kChunk;
-  if (b0 >= nbytes) return;
-  const long len = nbytes - b0 < kChunk ? nbytes - b0 : kChunk;  // multiple of 4
-  const uint32_t* w = data + b0 / 4;
-  uint32_t crc = 0xFFFFFFFFu;
-  if (len == kChunk) {
+  uint32_t term = 0;
+  if (b0 < nbytes) {
+    const long len = nbytes - b0 < kChunk ? nbytes - b0 : kChunk;  // multiple of 4
+    const uint32_t* w = data + b0 / 4;
+    uint32_t crc = 0;  // zero register: R(C_i)
+    if (len == kChunk) {
 #pragma unroll 4
-    for (int q = 0; q < kChunk / 16; ++q) {
-      const uint4 v = ((const uint4*)w)[q];
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      for (int q = 0; q < kChunk / 16; ++q) {
+        const uint4 v = ((const uint4*)w)[q];
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        crc ^= vv[j];
+        for (int j = 0; j < 4; ++j) {
+          crc ^= vv[j];
+          crc = T[3][crc & 255] ^ T[2][(crc >> 8) & 255] ^ T[1][(crc >> 16) & 255] ^ T[0][crc >> 24];
+        }
+      }
+    } else {
+      for (long j = 0; j < len / 4; ++j) {
+        crc ^= w[j];
         crc = T[3][crc & 255] ^ T[2][(crc >> 8) & 255] ^ T[1][(crc >> 16) & 255] ^ T[0][crc >> 24];
       }
     }
-  } else {
-    for (long j = 0; j < len / 4; ++j) {
-      crc ^= w[j];
-      crc = T[3][crc & 255] ^ T[2][(crc >> 8) & 255] ^ T[1][(crc >> 16) & 255] ^ T[0][crc >> 24];
-    }
+    // shift by the bytes behind this chunk: x^(8 * after) = prod over set bits k of 8*after of x^(2^k)
+    uint64_t e = (uint64_t)(nbytes - b0 - len) * 8u;
+    term = crc;
+    for (int k = 0; e; ++k, e >>= 1)
+      if (e & 1) term = multmodp(pw.x2k[k], term);
   }
-  crcs[chunk] = ~crc;
-}
-
-__global__ void __launch_bounds__(256) k_crc_combine(const uint32_t* __restrict__ crcs, long nchunks, long per,
-                                                     uint32_t x_chunk, uint32_t x_last, uint32_t x_part,
-                                                     uint32_t x_part_last, uint32_t* __restrict__ out) {
-  __shared__ uint32_t part[256];
-  const int t = threadIdx.x;
-  const long first = (long)t * per;
-  const long nparts = (nchunks + per - 1) / per;
-  if (first < nchunks) {
-    const long end = first + per < nchunks ? first + per : nchunks;
-    uint32_t acc = crcs[first];
-    for (long j = first + 1; j < end; ++j) acc = multmodp(j == nchunks - 1 ? x_last : x_chunk, acc) ^ crcs[j];
-    part[t] = acc;
-  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) term ^= __shfl_xor(term, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = term;
   __syncthreads();
-  if (t == 0) {
-    uint32_t tot = part[0];
-    for (long p = 1; p < nparts; ++p) tot = multmodp(p == nparts - 1 ? x_part_last : x_part, tot) ^ part[p];
-    out[0] = tot;
-  }
+  if (t == 0) atomicXor(out, (red[0] ^ red[1]) ^ (red[2] ^ red[3]));
 }
 
 }  // namespace
 
-int afl_crc32_partials(long nbytes) { return (int)((nbytes + kChunk - 1) / kChunk); }
-
-int afl_crc32(const void* data, long nbytes, uint32_t* chunk_crcs, uint32_t* out, uint32_t x_chunk, uint32_t x_last,
-              uint32_t x_part, uint32_t x_part_last, hipStream_t s) {
+int afl_crc32(const void* data, long nbytes, const uint32_t* x2k, uint32_t* out, hipStream_t s) {
   if (nbytes <= 0 || (nbytes & 3) || (((uintptr_t)data) & 15)) return (int)hipErrorInvalidValue;
-  const long nchunks = afl_crc32_partials(nbytes);
-  const long per = (nchunks + 255) / 256;
-  hipLaunchKernelGGL(k_crc_chunks, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s, (const uint32_t*)data,
-                     nbytes, chunk_crcs);
-  hipLaunchKernelGGL(k_crc_combine, dim3(1), dim3(256), 0, s, chunk_crcs, nchunks, per, x_chunk, x_last, x_part,
-                     x_part_last, out);
+  const long nchunks = (nbytes + kChunk - 1) / kChunk;
+  CrcPow pw;
+  for (int k = 0; k < 48; ++k) pw.x2k[k] = x2k[k];
+  hipLaunchKernelGGL(k_crc32, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s, (const uint32_t*)data,
+                     nbytes, pw, out);
   return (int)hipGetLastError();
 }

@@ -536,20 +536,12 @@ template <class CT>
 __device__ __forceinline__ u32x4 ld_wt16(const CT& c, int byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(c.wrs(), byte_off, 0, 16);
 }
-// A partner that does not show up within XWG_DEADLINE_TICKS of s_memrealtime (100 MHz: 20 s) becomes an
-// error, never a hang.  Time-based, not a spin count: under concurrent kernels (validation, checkpoint blits
-// on other streams) a co-resident partner can be late by far more polls than on an idle chip.  The clock
-// is read once per 1024 polls, so a wait that succeeds early costs nothing extra.
-constexpr uint64_t XWG_DEADLINE_TICKS = 20ull * 100000000ull;
-__device__ __forceinline__ bool xwg_expired(long spins, uint64_t& t0) {
-  if ((spins & 1023) != 1023) return false;
-  const uint64_t now = __builtin_amdgcn_s_memrealtime();
-  if (t0 == 0) {
-    t0 = now;
-    return false;
-  }
-  return now - t0 > XWG_DEADLINE_TICKS;
-}
+// A missing partner becomes an error, not a hang: ~2^24 polls of (load latency + s_sleep 1) is tens of
+// seconds, orders of magnitude above any late co-resident dispatch (validation / checkpoint kernels on other
+// streams run for milliseconds).  A time-based deadline (s_memrealtime every 1024 polls) measured 0.6 %
+// slower on the TransformerModel headline (tools/ab_native.sh, same box, 2 x 2 runs: 94.07 vs 94.68
+// rounds/s: the extra loop code moved the hot kernel's code placement), so the wait stays a poll count.
+constexpr long XWG_MAX_SPINS = 1L << 24;
 // Per-WAVE hand-off (row-per-wave layout: wave w produces and consumes rows 16w..16w+15 on both sides).
 // The same R1 protocol with the wave as the storing unit: the wave's own sc1 payload stores, its own
 // vmcnt(0) drain, then its lane 0 stores the wave's flag; the consumer wave polls its flag (all lanes one
@@ -572,14 +564,13 @@ template <class CT>
 __device__ __forceinline__ uint32_t wave_wait(const CT& c, gu32* flag_a, gu32* flag_b, uint32_t want, int shift,
                                               gu32* tmo) {
   uint32_t v = 0;
-  uint64_t t0 = 0;
   for (long spins = 0;; ++spins) {
     v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint32_t w = flag_b == flag_a
                            ? v
                            : __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if ((v >> shift) >= want && (w >> shift) >= want) break;
-    if (xwg_expired(spins, t0)) {
+    if (spins > XWG_MAX_SPINS) {
       v = 0xFFFFFFFFu;
       if (c.lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;

@@ -441,13 +441,12 @@ __device__ __forceinline__ void publish(gu32* flag, uint32_t value, int lane) {
 // waits until (*fa >> shift) >= want and (*fb >> shift) >= want; returns *fa, or 0xFFFFFFFF on timeout
 __device__ __forceinline__ uint32_t await(gu32* fa, gu32* fb, uint32_t want, int shift, gu32* tmo, int lane) {
   uint32_t v = 0;
-  uint64_t t0 = 0;
   for (long spins = 0;; ++spins) {
     v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(fa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint32_t w =
         fb == fa ? v : __builtin_amdgcn_readfirstlane(__hip_atomic_load(fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if ((v >> shift) >= want && (w >> shift) >= want) break;
-    if (fk::xwg_expired(spins, t0)) {
+    if (spins > fk::XWG_MAX_SPINS) {
       v = 0xFFFFFFFFu;
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
