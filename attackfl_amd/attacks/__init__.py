@@ -135,6 +135,9 @@ class _CandidateDistances:
             self.vec = engine.vec_slots
             if self.vec:
                 self.A, self.B, self.C = ops.attack_coeffs_segments(G, mean, dev, self.vec)  # [K,S],[K,S],[S]
+            # device: the matrix slots' Grams of X_j = mean - G_j once; every γ is then one small launch
+            self.fam = (ops.SpectralFamily(mean[None, :] - G[1:], engine.mat_slots, dev)
+                        if engine.mat_slots and K > 1 and G.is_cuda else None)
 
     def __call__(self, gamma) -> torch.Tensor:
         """``gamma``: a float or a 0-d float64 tensor on the matrices' device."""
@@ -147,7 +150,9 @@ class _CandidateDistances:
             if self.vec:
                 q = (self.A - 2.0 * gamma * self.B + gamma * gamma * self.C[None, :]).clamp_min(0.0)
                 d = d + torch.sqrt(q).sum(dim=1)
-            if self.engine.mat_slots and K > 1:
+            if self.fam is not None:
+                d = d + torch.cat([torch.zeros(1, dtype=torch.float64, device=d.device), self.fam(gamma)])
+            elif self.engine.mat_slots and K > 1:
                 cand = self.mean - gamma * self.dev
                 diffs = cand[None, :] - self.G[1:]
                 dm = torch.zeros(K, dtype=torch.float64, device=self.G.device)

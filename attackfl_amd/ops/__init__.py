@@ -8,7 +8,7 @@ the test-suite.
 from __future__ import annotations
 
 import os
-from typing import List, Sequence, Tuple
+from typing import List, Sequence, Tuple, Optional
 
 import torch
 
@@ -167,20 +167,87 @@ def _spectral_table(slots, device):
     return _SPEC_CACHE[key]
 
 
+_GRAM_CACHE = {}
+_GRAM_NMAX = 64
+_GRAM_LDS_FLOATS = 40 * 1024  # X and D of one slot staged whole in LDS (160 KB)
+
+
+def _gram_table(slots, device):
+    """Gram-form slots (n = min(r, c) <= 64, X and D fit in LDS): (tab [S', 4] int32 {offset, r, c, arena
+    offset}, sumq, max LDS floats, the remaining slots)."""
+    key = (tuple((s.offset, s.numel, s.shape[0]) for s in slots), str(device))
+    if key not in _GRAM_CACHE:
+        rows, rest, sumq, lds = [], [], 0, 0
+        for s in slots:
+            r = int(s.shape[0])
+            c = s.numel // r
+            n, k = min(r, c), max(r, c)
+            need = 2 * n * (k + 1)
+            if n > _GRAM_NMAX or need > _GRAM_LDS_FLOATS:
+                rest.append(s)
+                continue
+            n16 = (n + 15) & ~15
+            rows.append((s.offset, r, c, sumq))
+            sumq += n16 * n16
+            lds = max(lds, need)
+        tab = torch.tensor(rows, dtype=torch.int32).reshape(-1, 4).to(device)
+        _GRAM_CACHE[key] = (tab, sumq, lds, rest)
+    return _GRAM_CACHE[key]
+
+
+class SpectralFamily:
+    """sum over matrix slots of ||X[m, slot] - γ·dev[slot]||_2 for every row m, for any γ (device).
+
+    Reference: the per-tensor ord-2 norms of src/Utils.py:47 inside the bisections of src/Utils.py:101-204.
+    The n x n Grams of X, X D^T + D X^T and D D^T are formed ONCE (``k_spec_grams``); each γ then costs one
+    small launch (``k_spec_eval``: A - γS + γ²C, squarings on fp64 MFMA, Rayleigh quotient) that reads γ from
+    device memory.  Slots outside the Gram form (n > 64) fall back to materialised rows per γ."""
+
+    def __init__(self, X: torch.Tensor, slots, dev: Optional[torch.Tensor] = None):
+        self.X = X.contiguous()
+        self.dev = dev.contiguous() if dev is not None else None
+        self.slots = slots
+        self.tab, self.sumq, lds, self.rest = _gram_table(slots, X.device)
+        self.arena = None
+        if self.tab.shape[0] and X.shape[0]:
+            self.arena = native().spec_grams(self.X, self.dev, self.tab, lds, self.sumq)
+
+    def __call__(self, gamma=None) -> torch.Tensor:
+        M = self.X.shape[0]
+        out = torch.zeros(M, dtype=torch.float64, device=self.X.device)
+        if M == 0:
+            return out
+        g = None
+        if gamma is not None and self.dev is not None:
+            g = gamma if torch.is_tensor(gamma) else torch.tensor(float(gamma), dtype=torch.float64)
+            g = g.to(device=self.X.device, dtype=torch.float64).reshape(())
+        if self.arena is not None:
+            out += native().spec_eval(self.arena, self.tab, self.sumq, M, g).sum(dim=1)
+        if self.rest:
+            rows = self.X if g is None else self.X - (g * self.dev.double()).float()[None, :]
+            out += _spectral_slots_direct(rows, self.rest)
+        return out
+
+
+def _spectral_slots_direct(diffs: torch.Tensor, slots) -> torch.Tensor:
+    diffs = diffs.contiguous()
+    tab, max_n, scr, big = _spectral_table(slots, diffs.device)
+    out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
+    if tab.shape[0]:
+        out += native().spectral_norm_slots(diffs, tab, max_n, scr).sum(dim=1)
+    for s in big:
+        mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], s.shape[0], -1)
+        out += native().spectral_norm(mats.contiguous())
+    return out
+
+
 def spectral_norm_sum(diffs: torch.Tensor, slots) -> torch.Tensor:
     """sum over matrix slots of ||diffs[m, slot]||_2 (slot viewed as [shape[0], -1]) -> [M] fp64.
 
-    Device: every (row, slot) pair in one ragged launch (reference src/Utils.py:47 per-tensor norm)."""
+    Device: the Gram form (two launches for every (row, slot) pair, reference src/Utils.py:47 per-tensor
+    norm); slots with n > 64 through the direct ragged launch."""
     if _dev(diffs):
-        diffs = diffs.contiguous()
-        tab, max_n, scr, big = _spectral_table(slots, diffs.device)
-        out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
-        if tab.shape[0]:
-            out += native().spectral_norm_slots(diffs, tab, max_n, scr).sum(dim=1)
-        for s in big:
-            mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], s.shape[0], -1)
-            out += native().spectral_norm(mats.contiguous())
-        return out
+        return SpectralFamily(diffs, slots)()
     out = torch.zeros(diffs.shape[0], dtype=torch.float64, device=diffs.device)
     for s in slots:
         mats = diffs[:, s.offset:s.offset + s.numel].reshape(diffs.shape[0], s.shape[0], -1)

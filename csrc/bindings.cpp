@@ -143,6 +143,47 @@ torch::Tensor spectral_norm(torch::Tensor X) {
 }
 
 // D [M, P] fp32, tab [S, 4] int32 (off, r, c, scratch off; min(r, c) <= 128), scr = scratch per row -> [M, S] fp64
+torch::Tensor spec_grams(torch::Tensor X, c10::optional<torch::Tensor> dev, torch::Tensor tab, int64_t max_lds_floats,
+                         int64_t sumq) {
+  check_dev(X, "X", torch::kFloat32);
+  check_dev(tab, "tab", torch::kInt32);
+  TORCH_CHECK(X.dim() == 2 && tab.dim() == 2 && tab.size(1) == 4, "spec_grams: bad shapes");
+  const int M = X.size(0), S = tab.size(0);
+  const float* dp = nullptr;
+  if (dev.has_value() && dev->defined()) {
+    check_dev(*dev, "dev", torch::kFloat32);
+    TORCH_CHECK(dev->numel() == X.size(1), "spec_grams: dev must have P entries");
+    dp = dev->data_ptr<float>();
+  }
+  auto arena = torch::empty({(2L * M + 1) * sumq}, X.options().dtype(torch::kFloat64));
+  if (M == 0 || S == 0) return arena;
+  TORCH_CHECK(afl_spec_grams(X.data_ptr<float>(), M, X.size(1), dp, tab.data_ptr<int>(), S, (int)max_lds_floats, sumq,
+                             arena.data_ptr<double>(), cur()) == 0,
+              "spec_grams launch failed");
+  AFL_CHECK_LAUNCH();
+  return arena;
+}
+
+torch::Tensor spec_eval(torch::Tensor arena, torch::Tensor tab, int64_t sumq, int64_t M, c10::optional<torch::Tensor> gamma) {
+  check_dev(arena, "arena", torch::kFloat64);
+  check_dev(tab, "tab", torch::kInt32);
+  TORCH_CHECK(arena.numel() == (2 * M + 1) * sumq, "spec_eval: arena size");
+  const int S = tab.size(0);
+  const double* gp = nullptr;
+  if (gamma.has_value() && gamma->defined()) {
+    check_dev(*gamma, "gamma", torch::kFloat64);
+    TORCH_CHECK(gamma->numel() == 1, "spec_eval: gamma must be a scalar");
+    gp = gamma->data_ptr<double>();
+  }
+  auto out = torch::empty({M, S}, arena.options());
+  if (M == 0 || S == 0) return out;
+  TORCH_CHECK(afl_spec_eval(arena.data_ptr<double>(), sumq, (int)M, gp, tab.data_ptr<int>(), S, out.data_ptr<double>(),
+                            cur()) == 0,
+              "spec_eval launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 torch::Tensor spectral_norm_slots(torch::Tensor D, torch::Tensor tab, int64_t max_n, int64_t scr) {
   check_dev(D, "D", torch::kFloat32);
   check_dev(tab, "tab", torch::kInt32);
@@ -428,7 +469,7 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);  // (rnn2 / tf2: 3 workgroups per client)
   torch::Tensor sync;
   if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
-    sync = torch::zeros({(long)C * AFL_TF_SYNC_WORDS}, order.options());
+    sync = torch::zeros({(long)C * (tf2 || rnn2 ? AFL_TF2_SYNC_WORDS : AFL_TF_SYNC_WORDS)}, order.options());
     a.sync = (uint32_t*)sync.data_ptr<int>();
   }
   const int rc = tf2 ? afl_tf2_train(&a, cur()) : rnn2 ? afl_rnn2_train(&a, cur())
@@ -548,6 +589,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attack_coeffs", &attack_coeffs);
   m.def("spectral_norm", &spectral_norm);
   m.def("spectral_norm_slots", &spectral_norm_slots);
+  m.def("spec_grams", &spec_grams);
+  m.def("spec_eval", &spec_eval);
   m.def("weighted_rows", &weighted_rows);
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);

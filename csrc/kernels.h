@@ -49,6 +49,13 @@ void afl_make_plan(const uint64_t* seeds, const int* nd, int C, int n_train, int
 // linalg.hip
 int afl_spectral_scratch(int r, int c);
 int afl_spectral(const float* X, int B, int r, int c, float* G0, double* out, hipStream_t s);
+// Gram-form spectral norms (linalg.hip): per (slot, row) fp64 Grams of X (and, with dev, X D^T + D X^T and
+// D D^T) once; then sigma_max(X_m - γ D) per slot for a device-resident γ (null: γ = 0).  tab [S] int4 =
+// {offset, r, c, arena offset}; arena = [M][2][sumq] + [sumq] doubles.
+int afl_spec_grams(const float* X, int M, long P, const float* dev, const int* tab, int S, int max_lds_floats, long sumq,
+                   double* arena, hipStream_t st);
+int afl_spec_eval(const double* arena, long sumq, int M, const double* gamma, const int* tab, int S, double* out,
+                  hipStream_t st);
 int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int max_n, float* G0, long scr,
                        double* out, hipStream_t st);
 
@@ -86,6 +93,10 @@ int afl_tf_eval_many(const float* params, long pstride, unsigned short* bf, long
                      int n, float* out, hipStream_t s);
 long afl_tf_ws_floats();
 constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lines) + timeout word
+// on-chip trainers (tf2 / rnn2): the flag words, then the granule hand-off slots (onchip.h gr_put / gr_get):
+// 2 directions x 2 branches x 8 waves x 4 KB of {value, tag} granules, zeroed with the flags every call
+constexpr int AFL_GR_WORDS = 2 * 2 * 8 * 1024;
+constexpr int AFL_TF2_SYNC_WORDS = AFL_TF_SYNC_WORDS + AFL_GR_WORDS;
 // tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations
 // in registers / LDS; 3 workgroups per client, sync words required)
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);

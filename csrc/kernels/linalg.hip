@@ -202,3 +202,215 @@ int afl_spectral(const float* X, int B, int r, int c, float* G0, double* out, hi
   hipLaunchKernelGGL(k_spectral, dim3(B), dim3(256), lds, s, X, r, c, G0, out);
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Gram-form spectral norms for the bisection attacks (reference src/Utils.py:101-204: per-γ distances
+// ||c(γ) - G_j||_2 summed over the 2-D tensors, c(γ) = mean - γ·dev).  With X_j = mean - G_j the slot
+// matrix is M_j(γ) = X_j - γ D, and its Gram over the smaller side is
+//     M M^T = X X^T - γ (X D^T + D X^T) + γ² D D^T,
+// so the three n x n Grams are computed ONCE per attack (k_spec_grams, fp64 accumulation) and every γ of
+// the bisection only forms A - γS + γ²C (fp64) and runs the squarings (k_spec_eval) — no pass over the
+// [K, P] models and no materialised candidate rows per γ.  γ is read from device memory (the bisection
+// keeps it there: no host synchronisation per step).  The pairwise distances use the same two kernels
+// with D absent (γ = 0).
+// Squarings: v_mfma_f64_16x16x4f64 on the fp32 LDS image (products and sums in fp64, the image rounded
+// to fp32 between squarings like spectral_one), 12 normalised squarings, best column, Rayleigh quotient
+// against the fp64 Gram.  Slots qualify when n = min(r, c) <= 64 and X and D fit in LDS.
+constexpr int SG_NMAX = 64;
+constexpr int SG_LD = 68;  // fp32 image row stride (bank spread for the MFMA operand reads)
+typedef double sg_d4 __attribute__((ext_vector_type(4)));
+
+template <bool DEV>
+__global__ void __launch_bounds__(256) k_spec_grams(const float* __restrict__ X, long P, const float* __restrict__ dev,
+                                                    const int4* __restrict__ tab, long sumq, double* __restrict__ arena) {
+  extern __shared__ float sg_lds[];
+  const int s = blockIdx.x, m = blockIdx.y, M = gridDim.y, tid = threadIdx.x;
+  const int4 t = tab[s];
+  const int r = t.y, c = t.z;
+  const bool rows = r <= c;
+  const int n = rows ? r : c, k = rows ? c : r, n16 = (n + 15) & ~15, kp = k + 1;
+  float* xs = sg_lds;       // [n][k + 1]: xs[i * kp + u] = X(i, u) over the smaller side i
+  float* ds = xs + n * kp;  // the same for D
+  const float* x = X + (long)m * P + t.x;
+  for (int e = tid; e < r * c; e += 256) {
+    const int rr = e / c, cc = e - rr * c;
+    const int i = rows ? rr : cc, u = rows ? cc : rr;
+    xs[i * kp + u] = x[e];
+    if (DEV) ds[i * kp + u] = dev[t.x + e];
+  }
+  __syncthreads();
+  double* A = arena + (long)m * 2 * sumq + t.w;
+  double* S = A + sumq;
+  double* C = arena + (long)M * 2 * sumq + t.w;
+  const bool doC = DEV && m == 0;
+  for (int e = tid; e < n16 * n16; e += 256) {
+    const int i = e / n16, l = e - i * n16;
+    double a = 0.0, sx = 0.0, cc2 = 0.0;
+    if (i < n && l < n) {
+      const float* xi = xs + i * kp;
+      const float* xl = xs + l * kp;
+      if (DEV) {
+        const float* di = ds + i * kp;
+        const float* dl = ds + l * kp;
+        for (int u = 0; u < k; ++u) {
+          a = fma((double)xi[u], (double)xl[u], a);
+          sx = fma((double)xi[u], (double)dl[u], sx);
+          sx = fma((double)di[u], (double)xl[u], sx);
+          if (doC) cc2 = fma((double)di[u], (double)dl[u], cc2);
+        }
+      } else {
+        for (int u = 0; u < k; ++u) a = fma((double)xi[u], (double)xl[u], a);
+      }
+    }
+    A[e] = a;
+    if (DEV) {
+      S[e] = sx;
+      if (doC) C[e] = cc2;
+    }
+  }
+}
+
+__device__ __forceinline__ double sg_block_max(double v, double* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
+__global__ void __launch_bounds__(256) k_spec_eval(const double* __restrict__ arena, long sumq, const double* __restrict__ gamma,
+                                                   const int4* __restrict__ tab, int S, double* __restrict__ out) {
+  __shared__ float F[2][SG_NMAX * SG_LD];
+  __shared__ double red[4];
+  __shared__ double dred[2][4];
+  __shared__ float wb[4];
+  __shared__ int wi[4];
+  const int s = blockIdx.x, m = blockIdx.y, M = gridDim.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int4 t = tab[s];
+  const int n = t.y <= t.z ? t.y : t.z, n16 = (n + 15) & ~15, T = n16 / 16;
+  const double g = gamma ? *gamma : 0.0;
+  const double* A = arena + (long)m * 2 * sumq + t.w;
+  const double* Sg = A + sumq;
+  const double* C = arena + (long)M * 2 * sumq + t.w;
+  auto gram = [&](int e) -> double { return gamma ? (A[e] - g * Sg[e]) + (g * g) * C[e] : A[e]; };
+  // ---- 1. G(γ), normalised, as the fp32 image
+  double mx = 0.0;
+  for (int e = tid; e < n16 * n16; e += 256) mx = fmax(mx, fabs(gram(e)));
+  mx = sg_block_max(mx, red);
+  double inv = mx > 0.0 ? 1.0 / mx : 0.0;
+  for (int e = tid; e < n16 * n16; e += 256) {
+    const int i = e / n16, l = e - i * n16;
+    F[0][i * SG_LD + l] = (float)(gram(e) * inv);
+  }
+  __syncthreads();
+  // ---- 2. normalised squarings on fp64 MFMA (wave w: output tiles w, w + 4, ...; f64 C/D layout
+  //         acc[r] = C[(lane >> 4) + 4r][lane & 15], A operand [lane & 15][lane >> 4], B operand [lane >> 4][lane & 15])
+  int cur = 0;
+  for (int it = 0; it < SN_SQUARINGS; ++it) {
+    sg_d4 acc[4];
+    double lmx = 0.0;
+    const float* Fc = F[cur];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[q] = sg_d4{0.0, 0.0, 0.0, 0.0};
+      const int p = wave + 4 * q;
+      if (p < T * T) {
+        const int ti = p / T, tj = p - ti * T;
+        const float* arow = Fc + (ti * 16 + (lane & 15)) * SG_LD + (lane >> 4);
+        const float* bcol = Fc + (lane >> 4) * SG_LD + tj * 16 + (lane & 15);
+        for (int k0 = 0; k0 < n16; k0 += 4)
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)arow[k0], (double)bcol[k0 * SG_LD], acc[q], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lmx = fmax(lmx, fabs(acc[q][r]));
+      }
+    }
+    mx = sg_block_max(lmx, red);
+    inv = mx > 0.0 ? 1.0 / mx : 0.0;
+    float* Fn = F[cur ^ 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = wave + 4 * q;
+      if (p < T * T) {
+        const int ti = p / T, tj = p - ti * T;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Fn[(ti * 16 + (lane >> 4) + 4 * r) * SG_LD + tj * 16 + (lane & 15)] = (float)(acc[q][r] * inv);
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const float* Fc = F[cur];
+  // ---- 3. the column of largest norm (ties: lowest index)
+  float best = -1.f;
+  int bi = 0;
+  for (int j = tid; j < n; j += 256) {
+    float sum = 0.f;
+    for (int i = 0; i < n; ++i) sum += Fc[i * SG_LD + j] * Fc[i * SG_LD + j];
+    if (sum > best) {
+      best = sum;
+      bi = j;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    wb[wave] = best;
+    wi[wave] = bi;
+  }
+  __syncthreads();
+  int col = wi[0];
+  float bb = wb[0];
+  for (int w = 1; w < 4; ++w)
+    if (wb[w] > bb || (wb[w] == bb && wi[w] < col)) {
+      bb = wb[w];
+      col = wi[w];
+    }
+  // ---- 4. Rayleigh quotient v^T G v / v^T v against the fp64 Gram
+  double num = 0.0, den = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const double vi = Fc[i * SG_LD + col];
+    double gv = 0.0;
+    for (int l = 0; l < n; ++l) gv = fma(gram(i * n16 + l), (double)Fc[l * SG_LD + col], gv);
+    num = fma(vi, gv, num);
+    den = fma(vi, vi, den);
+  }
+  num = wave_sum(num);
+  den = wave_sum(den);
+  if (lane == 0) {
+    dred[0][wave] = num;
+    dred[1][wave] = den;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double nn = (dred[0][0] + dred[0][1]) + (dred[0][2] + dred[0][3]);
+    const double dd = (dred[1][0] + dred[1][1]) + (dred[1][2] + dred[1][3]);
+    const double lam = dd > 0.0 ? nn / dd : 0.0;
+    out[(long)m * S + s] = lam > 0.0 ? sqrt(lam) : 0.0;
+  }
+}
+
+int afl_spec_grams(const float* X, int M, long P, const float* dev, const int* tab, int S, int max_lds_floats, long sumq,
+                   double* arena, hipStream_t st) {
+  const size_t lds = (size_t)max_lds_floats * sizeof(float);
+  if (lds > 160 * 1024) return -1;
+  const void* fn = dev ? (const void*)k_spec_grams<true> : (const void*)k_spec_grams<false>;
+  if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -2;
+  if (dev)
+    hipLaunchKernelGGL(k_spec_grams<true>, dim3(S, M), dim3(256), lds, st, X, P, dev, (const int4*)tab, sumq, arena);
+  else
+    hipLaunchKernelGGL(k_spec_grams<false>, dim3(S, M), dim3(256), lds, st, X, P, dev, (const int4*)tab, sumq, arena);
+  return 0;
+}
+
+int afl_spec_eval(const double* arena, long sumq, int M, const double* gamma, const int* tab, int S, double* out,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(k_spec_eval, dim3(S, M), dim3(256), 0, st, arena, sumq, gamma, (const int4*)tab, S, out);
+  return 0;
+}

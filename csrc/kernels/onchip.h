@@ -457,6 +457,57 @@ __device__ __forceinline__ uint32_t await(gu32* fa, gu32* fb, uint32_t want, int
   return v;
 }
 constexpr int XF_VIT = 0, XF_LAB = 1, XF_BVIT = 2, XF_BLAB = 3, XF_TMO = 4 * 8 * 32;
+
+// ---- granule hand-off (cdna_hip_programming.md Guideline 16 R2: the data IS the flag) ----
+// A wave hands its 64 lanes x 8 payload words over as {value, tag} granules: 4 write-through (sc1) 16-byte
+// stores per lane, each carrying two granules (each 8-byte half lands untorn).  No drain, no flag store: the
+// producer wave moves on at once, and the consumer's ONE sc1 sweep both detects and fetches the data (the
+// flag form costs a drain on the producer plus a second dependent round trip on the consumer:
+// MI355X_MICROARCH price list, handoff-1to1 vs handoff-flag).  Tags count steps within the launch (never 0),
+// and the slots live in the per-call zeroed sync block, so a previous launch's granules never match.
+// Slot (dir, src, wave): 4 KB = [k 0..3][lane] x 16 B — one store instruction writes 1 KB contiguously.
+constexpr int GR_DIR_BYTES = 2 * 8 * 4096;
+__device__ __forceinline__ int gr_off(int dir, int src, int wave, int lane) {
+  return dir * GR_DIR_BYTES + (src * 8 + wave) * 4096 + lane * 16;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gr_rsrc(gu32* sync) { return rsrc((void*)(sync + AFL_TF_SYNC_WORDS)); }
+__device__ __forceinline__ void gr_put(__amdgpu_buffer_rsrc_t rg, int off, const u32x4 (&u)[2], uint32_t tag) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = 2 * (k & 1);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{u[k >> 1][j], tag, u[k >> 1][j + 1], tag}, rg, off + k * 1024, 0, 16);
+    store_guard();
+  }
+}
+// sweeps the S slots at off[] until every granule's (tag >> shift) == want; returns the payload in out[2S]
+// and the tag (wave-uniform), or 0xFFFFFFFF on timeout (also raises *tmo)
+template <int S>
+__device__ __forceinline__ uint32_t gr_get(__amdgpu_buffer_rsrc_t rg, const int (&off)[S], u32x4 (&out)[2 * S],
+                                           uint32_t want, int shift, gu32* tmo, int lane) {
+  for (long spins = 0;; ++spins) {
+    u32x4 v[4 * S];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 * s + k] = __builtin_amdgcn_raw_buffer_load_b128(rg, off[s] + k * 1024, 0, 16);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4 * S; ++i) ok = ok && (v[i][1] >> shift) == want && (v[i][3] >> shift) == want;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        out[2 * s] = u32x4{v[4 * s][0], v[4 * s][2], v[4 * s + 1][0], v[4 * s + 1][2]};
+        out[2 * s + 1] = u32x4{v[4 * s + 2][0], v[4 * s + 2][2], v[4 * s + 3][0], v[4 * s + 3][2]};
+      }
+      return __builtin_amdgcn_readfirstlane(v[0][1]);
+    }
+    if (spins > fk::XWG_MAX_SPINS) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0xFFFFFFFFu;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 __device__ __forceinline__ gu32* xf(gu32* base, int group, int wave) { return base + (group * 8 + wave) * 32; }
 
 __device__ __forceinline__ void unpack16(const u32x4 (&u)[2], float (&x)[16]) {

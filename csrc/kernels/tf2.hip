@@ -19,8 +19,10 @@
 //     XOR-swizzled LDS tiles as they are produced and read back with ds_read_b64_tr_b16 in ONE dW phase
 //     per step (the only two workgroup barriers of a step bracket it);
 //   * the only global traffic in the step loop is the next batch's input rows (prefetched during the
-//     hand-off wait) and the hand-offs themselves: 16-byte write-through (sc1) payload stores, a per-wave
-//     flag, sc1 loads on the other side (cdna_hip_programming.md Guideline 16 R1).
+//     hand-off wait) and the hand-offs themselves: per wave 2 KB of bf16 rows as {value, step tag}
+//     granules in 16-byte write-through (sc1) stores, swept with sc1 loads until every tag matches — the
+//     data is the flag (cdna_hip_programming.md Guideline 16 R2): no drain on the producer, one round trip
+//     on the consumer.
 // Numerics are those of transformer.hip: bf16 MFMA operands with fp32 accumulation, fp32 elementwise
 // math, exact-erf GELU, hash dropout masks (tf_common.h), torch.optim.Adam with a fresh state per round.
 #include "common.h"
@@ -97,14 +99,12 @@ constexpr int SMEM = SMEM_CORE;
 static_assert(SMEM <= 160 * 1024, "LDS budget");
 
 // ------------------------------------------------------------------- per-client workspace (bytes)
-// hand-off payloads: [branch][wave][lane] x 32 bytes (16 bf16 in T layout)
-constexpr long WS_XF = 0;              // branch outputs -> head
-constexpr long WS_XB = WS_XF + 32768;  // d(branch outputs) -> branches
+// (the hand-off payloads travel as tagged granules in the per-call zeroed sync block: onchip.h gr_put / gr_get)
 // Adam moments of the register-resident weights: per-workgroup slab [slot][thread] of float4 (MOM_SLOTS
 // slots: m and v of the 4 block tiles, then the remaining moments), loaded in one batch of sc1 loads
 // ahead of each update phase and stored back after it (see "Adam" below)
 constexpr int MOM_SLOTS = 11;
-constexpr long WS_MOM = WS_XB + 32768;
+constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
 constexpr long WS_BYTES = WS_MOM + 3 * MOM_WG_BYTES;
 
@@ -805,8 +805,8 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
-  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
+  const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // granule hand-off slots
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   BrState st;
@@ -846,12 +846,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
 #endif
     asm volatile(";MARK fwd_end");
     stp(0, tid);
-    {  // publish this wave's output rows
-      const int off = (int)WS_XF + BR * 16384 + (wave * 64 + lane) * 32;
-      st_wt(rs, off, outp[0]);
-      st_wt(rs, off + 16, outp[1]);
-      publish(xf(sync, BR == 0 ? XF_VIT : XF_LAB, wave), (uint32_t)step, lane);
-    }
+    gr_put(rg, gr_off(0, BR, wave, lane), outp, (uint32_t)step);  // this wave's output rows -> head
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
@@ -862,19 +857,16 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       mka1 = awu(m1);
     }
     stp(1, tid);
-    gu32* fb = xf(sync, BR == 0 ? XF_BVIT : XF_BLAB, wave);
-    const uint32_t fv = await(fb, fb, (uint32_t)step, 1, sync + XF_TMO, lane);
+    u32x4 du[2];
+    const int go[1] = {gr_off(1, BR, wave, lane)};
+    const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) {
       failed = true;
       break;
     }
     float dout[16];
-    {
-      const int off = (int)WS_XB + BR * 16384 + (wave * 64 + lane) * 32;
-      u32x4 u[2] = {ld_wt(rs, off), ld_wt(rs, off + 16)};
-      unpack16(u, dout);
-    }
+    unpack16(du, dout);
     if (lane == 0) abort_w[wave] = fv & 1u;
 #ifndef TF2_NO_BWD
     asm volatile(";MARK bwd");
@@ -924,8 +916,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
-  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
+  const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // granule hand-off slots
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   HdState st;
@@ -985,20 +977,14 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
     sb();
     // ---- branch outputs of this wave's rows
-    const uint32_t fv = await(xf(sync, XF_VIT, wave), xf(sync, XF_LAB, wave), (uint32_t)step, 0, sync + XF_TMO, lane);
+    u32x4 cv[4];  // vitals rows (cv[0..1]) | labs rows (cv[2..3])
+    const int go[2] = {gr_off(0, 0, wave, lane), gr_off(0, 1, wave, lane)};
+    const uint32_t fv = gr_get<2>(rg, go, cv, (uint32_t)step, 0, sync + XF_TMO, lane);
     if (fv == 0xFFFFFFFFu) {
       timed_out = failed = true;
       break;
     }
     stp(10, tid);
-    u32x4 cv[4];
-    {
-      const int off = (int)WS_XF + (wave * 64 + lane) * 32;
-      cv[0] = ld_wt(rs, off);
-      cv[1] = ld_wt(rs, off + 16);
-      cv[2] = ld_wt(rs, off + 16384);
-      cv[3] = ld_wt(rs, off + 16384 + 16);
-    }
     // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
     // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
     // ---- fc1 + GELU + dropout(0.3)
@@ -1104,15 +1090,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         }
         u32x4 u[2];
         pack16(d, u);
-        const int off = (int)WS_XB + hb * 16384 + (wave * 64 + lane) * 32;
-        st_wt(rs, off, u[0]);
-        st_wt(rs, off + 16, u[1]);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both payloads written through, then both flags
-      if (lane == 0) {
-        const uint32_t fl = ((uint32_t)step << 1) | wave_nan;
-        __hip_atomic_store(xf(sync, XF_BVIT, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(xf(sync, XF_BLAB, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gr_put(rg, gr_off(1, hb, wave, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
       }
     }
     // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)

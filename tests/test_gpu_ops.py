@@ -95,6 +95,43 @@ def test_spectral_norm_slots(gpu, model):
     assert torch.allclose(ops.spectral_norm_sum(D, eng.mat_slots), ref, rtol=1e-12)
 
 
+@pytest.mark.parametrize("model", ["RNNModel", "TransformerModel", "big"])
+def test_spectral_family_matches_materialised_rows(gpu, model):
+    """Gram form (k_spec_grams once + k_spec_eval per γ, γ read from device memory) == fp64 SVD norms of
+    the materialised rows X_m - γ·dev, for the γs a bisection visits."""
+    from attackfl_amd.attacks import DistanceEngine
+    from attackfl_amd.models import TensorSlot
+
+    if model == "big":
+        layout = ParamLayout([TensorSlot("a", (200, 150), 0, 30000), TensorSlot("b", (7,), 30000, 7),
+                              TensorSlot("c", (96, 7), 30007, 672), TensorSlot("d", (16, 3, 5), 30679, 240)])
+    else:
+        layout = ParamLayout.for_model(model)
+    slots = DistanceEngine(layout, "spectral").mat_slots
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(4, layout.P, generator=g) * 0.05
+    dev = torch.rand(layout.P, generator=g) * 0.01
+    fam = ops.SpectralFamily(X.to(gpu), slots, dev.to(gpu))
+    for gamma in (50.0, 25.0, 37.5, 0.0, -3.0):
+        got = fam(torch.tensor(gamma, dtype=torch.float64, device=gpu)).cpu()
+        rows = X - gamma * dev
+        ref = sum(C.batched_spectral_norm(rows[:, s.offset:s.offset + s.numel].reshape(4, s.shape[0], -1).double())
+                  for s in slots)
+        assert torch.allclose(got, ref, rtol=2e-5), (gamma, got, ref)
+    assert torch.allclose(fam(None).cpu(), ops.spectral_norm_sum(X.to(gpu), slots).cpu(), rtol=1e-12)
+
+
+def test_spectral_family_degenerate(gpu):
+    from attackfl_amd.models import TensorSlot
+
+    layout = ParamLayout([TensorSlot("a", (16, 16), 0, 256), TensorSlot("b", (5, 40), 256, 200)])
+    X = torch.zeros(3, layout.P)
+    X[0, :256] = (torch.eye(16) * 2.0).reshape(-1)   # repeated top singular value
+    X[2, 0] = 1e-3
+    got = ops.spectral_norm_sum(X.to(gpu), layout.slots).cpu()
+    assert torch.allclose(got, torch.tensor([2.0, 0.0, 1e-3], dtype=torch.float64), rtol=1e-5), got
+
+
 def test_spectral_degenerate(gpu):
     X = torch.zeros(3, 16, 16)
     X[0] = torch.eye(16) * 2.0          # repeated top singular value
