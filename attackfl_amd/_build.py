@@ -84,6 +84,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     # per-file device flags: the on-chip trainers (tf2 / rnn2) keep their optimizer state in AGPRs, so its MFMAs must accumulate
     # in VGPRs (otherwise their accumulators compete with that state for the AGPR half of the budget)
     extra = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form"] for f in ("tf2.hip", "tf2_stamps.hip", "rnn2.hip", "rnn2_stamps.hip")}
+    if os.environ.get("AFL_DEV_DEFINES"):  # A/B variant builds (tools/ab_native.sh): extra -D flags on every kernel
+        dev_flags = dev_flags + os.environ["AFL_DEV_DEFINES"].split()
     if os.environ.get("AFL_TF2_ABL"):  # diagnostic ablation build of the timed kernel (tools/phase_profile.py)
         extra["tf2_stamps.hip"] = extra["tf2_stamps.hip"] + ["-DTF2_ABL=" + str(int(os.environ["AFL_TF2_ABL"]))]
     if os.environ.get("AFL_RNN2_ABL"):  # diagnostic ablation build of the stamped RNN trainer

@@ -90,12 +90,11 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 static_assert(192 * 16 * 4 <= 16384, "layer-1 gradient staging fits the h2 tile");
 
 // ------------------------------------------------------------------- per-client workspace (bytes)
-constexpr long WS_XF = 0;              // branch outputs -> head: [branch][wave][lane] x 32 bytes
-constexpr long WS_XB = WS_XF + 32768;  // d(branch outputs) -> branches
+// (hand-off payloads travel as tagged granules in the per-call zeroed sync block: onchip.h gr_put / gr_get)
 // Adam moment slab per workgroup [slot][thread] of float4.  Branch: W3 tiles m 0-5 / v 6-11, W2 tiles m 12-17
 // / v 18-23, compact entries m 24-26 / v 27-29.  Head: fc1 tiles m 0-1 / v 2-3, fc2 tile m 4 / v 5, vector 6.
 constexpr int MOM_SLOTS = 30;
-constexpr long WS_MOM = WS_XB + 32768;
+constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
 // saved backward factors of layers 1 and 2 (registers hold only layer 3's): per branch [layer][slot 0-7][thread]
 // of 16 bytes, written during the forward, read back a phase ahead of each gate backward (L2-resident)
@@ -599,8 +598,8 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
-  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
+  const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // granule hand-off slots
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   BrState st;
@@ -652,12 +651,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     br_forward(smem, xin, aru(mka), sv, outp, rsv, lane, wave, tid);
     const uint32_t xpk[2] = {pk2(xin[0], xin[1]), pk2(xin[2], xin[3])};  // xin -> X1 tile after dW2
     stp(0, tid);
-    {  // publish this wave's output rows
-      const int off = (int)WS_XF + BR * 16384 + (wave * 64 + lane) * 32;
-      st_wt(rs, off, outp[0]);
-      st_wt(rs, off + 16, outp[1]);
-      publish(xf(sync, BR == 0 ? XF_VIT : XF_LAB, wave), (uint32_t)step, lane);
-    }
+    gr_put(rg, gr_off(0, BR, wave, lane), outp, (uint32_t)step);  // this wave's output rows -> head
     w.b0 += BS;  // the next batch's inputs and dropout masks while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) {
@@ -666,14 +660,13 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     }
     asm volatile(";MARK wait");
     stp(1, tid);
-    gu32* fb = xf(sync, BR == 0 ? XF_BVIT : XF_BLAB, wave);
-    const uint32_t fv = await(fb, fb, (uint32_t)step, 1, sync + XF_TMO, lane);
+    u32x4 u[2];
+    const int go[1] = {gr_off(1, BR, wave, lane)};
+    const uint32_t fv = gr_get<1>(rg, go, u, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) break;
     float dh[16];
     {  // d(branch output) -> dropout' -> LayerNorm backward; gamma / beta sums -> fp64
-      const int off = (int)WS_XB + BR * 16384 + (wave * 64 + lane) * 32;
-      u32x4 u[2] = {ld_wt(rs, off), ld_wt(rs, off + 16)};
       float dy[16], xh[16], t[16], gm[16];
       unpack16(u, dy);
 #pragma unroll
@@ -787,8 +780,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  const __amdgpu_buffer_rsrc_t rs = rsrc(ws);
-  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF_SYNC_WORDS);
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
+  const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // granule hand-off slots
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   HdState st;
@@ -840,20 +833,14 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
     sb();
-    const uint32_t fv = await(xf(sync, XF_VIT, wave), xf(sync, XF_LAB, wave), (uint32_t)step, 0, sync + XF_TMO, lane);
+    u32x4 cv[4];  // vitals rows (cv[0..1]) | labs rows (cv[2..3])
+    const int go[2] = {gr_off(0, 0, wave, lane), gr_off(0, 1, wave, lane)};
+    const uint32_t fv = gr_get<2>(rg, go, cv, (uint32_t)step, 0, sync + XF_TMO, lane);
     if (fv == 0xFFFFFFFFu) {
       timed_out = failed = true;
       break;
     }
     stp(0, tid);
-    u32x4 cv[4];
-    {
-      const int off = (int)WS_XF + (wave * 64 + lane) * 32;
-      cv[0] = ld_wt(rs, off);
-      cv[1] = ld_wt(rs, off + 16);
-      cv[2] = ld_wt(rs, off + 16384);
-      cv[3] = ld_wt(rs, off + 16384 + 16);
-    }
     // ---- fc1 + ReLU
     float z1[8], a1[8];
     {
@@ -930,15 +917,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         }
         u32x4 u[2];
         pack16(dd, u);
-        const int off = (int)WS_XB + hb * 16384 + (wave * 64 + lane) * 32;
-        st_wt(rs, off, u[0]);
-        st_wt(rs, off + 16, u[1]);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both payloads written through, then both flags
-      if (lane == 0) {
-        const uint32_t fl = ((uint32_t)step << 1) | wave_nan;
-        __hip_atomic_store(xf(sync, XF_BVIT, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(xf(sync, XF_BLAB, wave), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gr_put(rg, gr_off(1, hb, wave, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
       }
     }
     stp(1, tid);

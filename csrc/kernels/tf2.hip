@@ -136,18 +136,20 @@ __device__ __forceinline__ uint32_t mask16(uint32_t key, uint32_t layer, int r, 
 
 // ------------------------------------------------------------------------ per-phase timers (diagnostics)
 // Built only into the TF2_STAMPS instantiation (tf2_stamps.hip): s_memrealtime (100 MHz) deltas of
-// wave 0 of ONE workgroup (index in stamps[63]), summed over all steps in LDS, written out at the end.
+// lane 0 of ONE wave (stamps[62], default 0) of ONE workgroup (stamps[63]), summed over all steps in LDS,
+// written out at the end.
 // The production kernel gets the empty Stamp below (no code, no registers).
 #ifdef TF2_STAMPS
 // (the previous time stamp lives in LDS slot ST_N - 1 too: a register copy raised the kernel's register
 // pressure enough to change its spills, i.e. the timings being measured)
 struct Stamp {
   bool on = false;
+  int who = 0;  // the stamping thread: lane 0 of wave stamps[62]
   uchar* smem = nullptr;
   __device__ __forceinline__ void operator()(int id, int tid) {
     if (!on) return;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) {
+    if (tid == who) {
       LDS_AS uint64_t* t = (LDS_AS uint64_t*)(smem + ST_OFF);
       t[id] += now - t[ST_N - 1];
       t[ST_N - 1] = now;
@@ -171,6 +173,19 @@ enum { ABL_U3 = 1, ABL_UADAM = 2, ABL_UDW = 4, ABL_COLSUM = 8, ABL_HEADUPD = 16,
 #endif
 
 
+
+// Wave priorities: the two waves sharing a SIMD (w and w + 4) run the same critical chain, and the
+// arbiter favours the older one, so waves 4-7 finished the forward 1.35 us after waves 0-3 (per-wave
+// stamps) while waves 0-3 already hashed the NEXT step's dropout masks beside them.  Critical sections
+// (forward, backward, update; the head's forward / backward) run at priority 2, the work that only has
+// to be done before the next hand-off arrives (masks, prefetch, deferred head tiles) at 0.
+#ifndef TF2_NO_PRIO
+__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(2); }
+__device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
+#else
+__device__ __forceinline__ void prio_hi() {}
+__device__ __forceinline__ void prio_lo() {}
+#endif
 
 // =============================================================================== branch workgroup
 template <int BR>
@@ -554,8 +569,8 @@ __device__ __forceinline__ int cmp_img(int e) {
 }
 
 // Weight gradients + Adam for one step (after the barrier that ends the backward).  Three parts:
-//  U1  small weight-gradient tiles (dense: waves 0-3, ffn.3: waves 4-7, ffn.0: every wave one k tile of
-//      the 4) in registers; barrier (their X operands XIN / F2 die, their space stages the gradients);
+//  U1  small weight-gradient tiles (dense and ffn.0: waves 0-3, ffn.3: waves 4-7) in registers; barrier
+//      (their X operands XIN / F2 die, their space stages the gradients);
 //  U2  small-tile gradients -> compact staging; the 2x2 v / out_proj block of the wave -> Adam -> image;
 //      bias sums of the dY tiles -> CS; barrier;
 //  U3  every thread: Adam on its compact entries -> VEC / images.  Gradient vector CS reset.
@@ -585,11 +600,8 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
 #pragma unroll 1
     for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
       as = mma(tfrag<TK16>(X, 32 * s, 0, lane), tfrag<TK64>(DY, 32 * s, w4, lane), as);
-      // ffn.0: waves w and w + 4 split the 128 rows of k tile w4 (rows 64 (w >> 2) .. + 63)
-      if (s < 2) {
-        const int r0 = 64 * (wave >> 2) + 32 * s;
-        af1 = mma(tfrag<TK64>(smem + B_X1N, r0, w4, lane), tfrag<TK16>(smem + B_DF0, r0, 0, lane), af1);
-      }
+      // ffn.0 (k tile w4, all 128 rows) on waves 0-3 alone: no cross-wave partial sum, one barrier less
+      if (lo) af1 = mma(tfrag<TK64>(smem + B_X1N, 32 * s, w4, lane), tfrag<TK16>(smem + B_DF0, 32 * s, 0, lane), af1);
     }
   }
   // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
@@ -663,18 +675,11 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
       if (wave == 0 && i16 < FF) ldsf(smem, B_CS)[VS_F1B + i16] = b1[0];
     }
   }
-  if (wave >= 4) {  // ffn.0 (k tile w4, n 0..5): first row half
+  if (lo) {  // ffn.0 (k tile w4, n 0..5)
     LDS_AS float* gs = ldsf(smem, B_GS);
     if (i16 < FF)
 #pragma unroll
       for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
-  }
-  lds_bar();
-  if (wave < 4) {  // ffn.0: second row half added
-    LDS_AS float* gs = ldsf(smem, B_GS);
-    if (i16 < FF)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] += af1[i];
   }
   lds_bar();
   stp(6, tid);
@@ -787,6 +792,7 @@ __device__ __forceinline__ void load_x(float (&x)[4], const AflTfTrainArgs& a, i
 __device__ __forceinline__ void stamp_init(Stamp& stp, const AflTfTrainArgs& a, uchar* smem) {
 #ifdef TF2_STAMPS
   stp.on = a.stamps && (long)blockIdx.x == (long)a.stamps[63];
+  stp.who = a.stamps ? 64 * (int)(a.stamps[62] & 7) : 0;
   stp.smem = smem;
   if (threadIdx.x == 0) *(LDS_AS uint64_t*)(smem + ST_OFF + 8 * (ST_N - 1)) = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -838,6 +844,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     const AdamK K = adam_k(a, step);
     Saved sv;
     u32x4 outp[2];
+    prio_hi();
     asm volatile(";MARK fwd");
 #ifndef TF2_NO_FWD
     br_forward<BR>(smem, xin, aru(mka0), aru(mka1), sv, outp, lane, wave);
@@ -847,6 +854,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     asm volatile(";MARK fwd_end");
     stp(0, tid);
     gr_put(rg, gr_off(0, BR, wave, lane), outp, (uint32_t)step);  // this wave's output rows -> head
+    prio_lo();
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
@@ -860,6 +868,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     u32x4 du[2];
     const int go[1] = {gr_off(1, BR, wave, lane)};
     const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
+    prio_hi();
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) {
       failed = true;
@@ -984,6 +993,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       timed_out = failed = true;
       break;
     }
+    prio_hi();
     stp(10, tid);
     // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
     // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
@@ -1093,6 +1103,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         gr_put(rg, gr_off(1, hb, wave, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
       }
     }
+    prio_lo();
     // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)
     {
       sb();

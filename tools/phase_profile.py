@@ -27,7 +27,7 @@ NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G
          21: "X:publish+wait d(out)"}
 # on-chip trainer (split 4, tf2.hip): branch workgroups (blocks 3c+1, 3c+2) and the head (3c)
 NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:backward", 4: "B:barrier+abort",
-          5: "B:U1 small dW (+bar)", 6: "B:U2 v/o dW+Adam, biases (+2 bars)", 7: "B:U3 compact Adam",
+          5: "B:U1 small dW (+bar)", 6: "B:U2 v/o dW+Adam, biases (+bar)", 7: "B:U3 compact Adam",
           8: "B:end barrier", 10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss",
           13: "H:dW+Adam", 14: "H:end barrier"}
 
@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--split", type=int, default=0, help="workgroups per client (1, 2, 3); 0 = auto")
     ap.add_argument("--block", type=int, default=0, help="workgroup whose phases are stamped (-1: 0, 1, 2 in turn)")
     ap.add_argument("--model", default="TransformerModel")
+    ap.add_argument("--wave", type=int, default=0, help="stamping wave of the workgroup (-1: 0..7 in turn; tf2 only)")
     args = ap.parse_args()
     if args.model == "RNNModel":
         return main_rnn(args)
@@ -68,13 +69,15 @@ def main():
     torch.cuda.synchronize()
     used = split or T.auto_split(args.clients, dev)
     for b in blocks:
-        run(args, dev, rows, order, plan, params, split, used, b)
+        for wv in (range(8) if args.wave < 0 else [args.wave]):
+            run(args, dev, rows, order, plan, params, split, used, b, wv)
 
 
-def run(args, dev, rows, order, plan, params, split, used, block):
+def run(args, dev, rows, order, plan, params, split, used, block, wave=0):
     names = NAMES4 if used == 4 else NAMES
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
     stamps[63] = block
+    stamps[62] = wave
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
                     opt_mode=args.opt_mode, stamps=stamps, split=split)
@@ -83,7 +86,7 @@ def run(args, dev, rows, order, plan, params, split, used, block):
     steps = args.epochs * ((args.rows + 127) // 128)
     st = stamps.cpu().tolist()[:63]
     tot = sum(st)
-    out = {"split": used, "block": block, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
+    out = {"split": used, "block": block, "wave": wave, "opt_mode": args.opt_mode, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps, "us_per_step_wall": wall * 1e6 / steps,
            "us_per_step_stamped": tot * 0.01 / steps, "phases_us_per_step": {}}
     for i, v in enumerate(st):
         if v:
