@@ -54,45 +54,49 @@ class Staging:
     """Per-round host metadata -> device in ONE copy: the arrays are packed (8-byte aligned) into a
     reused pinned buffer, copied with one non-blocking H2D copy into a reused device buffer, and returned
     as typed device views — built once per layout (the same shapes every round), because the ~18 tensor
-    view ops per round cost more host time than the copy.  The copy is stream-ordered after the previous
-    round's kernels that read the old views.  On a CPU device the arrays are simply wrapped."""
+    view ops per round cost more host time than the copy.  Two buffers alternate, so the next round's
+    metadata can be staged (``FLEngine._prepare_local``) while kernels of the current round that read the
+    previous views are still queued; a buffer's copy is stream-ordered after the kernels of the round
+    before that read it.  On a CPU device the arrays are simply wrapped."""
+
+    SLOTS = 2
 
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
-        self.host: Optional[torch.Tensor] = None
-        self.dev: Optional[torch.Tensor] = None
-        self.done: Optional[torch.cuda.Event] = None
-        self._views: Dict[tuple, List[torch.Tensor]] = {}
+        self._slots = [{"host": None, "dev": None, "done": None, "views": {}} for _ in range(self.SLOTS)]
+        self._next = 0
 
     def upload(self, arrays: Sequence[np.ndarray]) -> List[torch.Tensor]:
         if self.device.type != "cuda":
             return [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+        sl = self._slots[self._next]
+        self._next = (self._next + 1) % self.SLOTS
         offs, n = [], 0
         for a in arrays:
             offs.append(n)
             n += (a.nbytes + 7) // 8 * 8
         n = max(n, 8)
-        if self.host is None or self.host.numel() < n:
-            self.host = torch.empty(max(n, 4096), dtype=torch.uint8, pin_memory=True)
-            self.dev = torch.empty(self.host.numel(), dtype=torch.uint8, device=self.device)
-            self._views.clear()
-        elif self.done is not None:
-            self.done.synchronize()  # the previous round's copy has long finished; never overwrite in flight
-        hb = self.host.numpy()
+        if sl["host"] is None or sl["host"].numel() < n:
+            sl["host"] = torch.empty(max(n, 4096), dtype=torch.uint8, pin_memory=True)
+            sl["dev"] = torch.empty(sl["host"].numel(), dtype=torch.uint8, device=self.device)
+            sl["views"].clear()
+        elif sl["done"] is not None:
+            sl["done"].synchronize()  # this buffer's last copy finished long ago; never overwrite one in flight
+        hb = sl["host"].numpy()
         for a, o in zip(arrays, offs):
             hb[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-        self.dev[:n].copy_(self.host[:n], non_blocking=True)
-        if self.done is None:
-            self.done = torch.cuda.Event()
-        self.done.record(torch.cuda.current_stream(self.device))
+        sl["dev"][:n].copy_(sl["host"][:n], non_blocking=True)
+        if sl["done"] is None:
+            sl["done"] = torch.cuda.Event()
+        sl["done"].record(torch.cuda.current_stream(self.device))
         key = tuple((a.shape, a.dtype.str) for a in arrays)
-        out = self._views.get(key)
+        out = sl["views"].get(key)
         if out is None:
             out = []
             for a, o in zip(arrays, offs):
-                t = self.dev[o:o + a.nbytes].view(_TORCH_DT[a.dtype.str[1:]])
+                t = sl["dev"][o:o + a.nbytes].view(_TORCH_DT[a.dtype.str[1:]])
                 out.append(t.reshape(a.shape))
-            self._views[key] = out
+            sl["views"][key] = out
         return out
 
 
@@ -236,6 +240,8 @@ class FLEngine:
         # hypernetwork; attackers draw from the pool set before the launch), no resume sidecars.  Any world
         # size: validation is replicated, so no rank waits for another's decision before the next launch.
         self._spec = None
+        self._next_prep = None  # the next launch's host half, staged while the current training runs
+        self._fedavg_w = None
         self._val_stream = None
         self._start_ready = None
         self._sel_cache = None
@@ -437,45 +443,65 @@ class FLEngine:
         return self._finish_local(self._launch_local(genuine))
 
     def _launch_local(self, genuine: Dict[int, Optional[torch.Tensor]]) -> dict:
-        """Prepare this rank's clients for the round and enqueue the genuine clients' training (async)."""
+        """Prepare this rank's clients for the round and enqueue the genuine clients' training (async).
+        Uses the preparation staged ahead by ``run_round`` when there is one."""
+        prep, self._next_prep = self._next_prep, None
+        if prep is None or prep["selected"] != tuple(self.selected):
+            prep = self._prepare_local()
+        return self._enqueue_local(prep, genuine)
+
+    def _prepare_local(self) -> dict:
+        """Host half of a launch — client counters, the data draws, fault injection, the plan — none of which
+        depends on the previous round's outcome, so ``run_round`` stages the NEXT launch's half before it
+        waits for the current training (the draws are the same whenever they happen: one per launch, in
+        launch order).  Uploads and the plan kernel are enqueued here; which clients attack is re-checked at
+        enqueue time (an attacker's first attack round waits for its genuine sample)."""
         tq = time.perf_counter()
         cfg = self.cfg
-        dev = self.device
-        block = torch.zeros(self.slots, self.W, dtype=torch.float32, device=dev)
         meta = np.zeros((self.slots, META + self.E), dtype=np.float32)  # host-built, uploaded once (+ losses)
         lo, hi = cfg.data_range
-        train_rows, train_nd, train_seeds = [], [], []
-        attack_jobs = []
-        started, faults = [], []
+        clients, faults = [], []
         for j, lc in enumerate(self.local):
             i = lc.info.index
             if i not in self.selected:
                 continue
             lc.training_round += 1
-            started.append((j, i))
             if (i, lc.training_round) in self.faults:
                 faults.append(j)
                 print_with_color(f"[fault-inject] client {i} poisoned with NaN (training round {lc.training_round})",
                                  "red")
-            g = genuine.get(i)
-            if lc.info.attack is not None and g is not None and g.shape[0] > 0:
-                lc.genuine = g
             num_data = lc.rng.randrange(lo, hi + 1)
             meta[j, 0] = 1.0
             meta[j, 2] = float(num_data)
             meta[j, 3] = 1.0 if lc.info.attack is not None else 0.0
-            atk = lc.info.attack
-            if atk is not None and lc.training_round >= atk.round and lc.genuine is not None and lc.genuine.shape[0] > 0:
-                attack_jobs.append((j, i, lc, atk))
+            clients.append((j, i, lc, num_data))
+        prep = {"tq": tq, "meta": meta, "clients": clients, "faults": faults, "selected": tuple(self.selected)}
+        self._stage(prep, self._attack_decisions(prep))
+        return prep
+
+    @staticmethod
+    def _attack_decisions(prep: dict) -> tuple:
+        return tuple(lc.info.attack is not None and lc.training_round >= lc.info.attack.round
+                     and lc.genuine is not None and lc.genuine.shape[0] > 0 for _, _, lc, _ in prep["clients"])
+
+    def _stage(self, prep: dict, decisions: tuple) -> None:
+        """Training rows / sizes / seeds for the given attack decisions, their ONE upload and the plan."""
+        cfg, dev = self.cfg, self.device
+        tq1 = time.perf_counter()
+        train_rows, train_nd, train_seeds = [], [], []
+        attack_rows = []
+        for (j, i, lc, num_data), atk in zip(prep["clients"], decisions):
+            if atk:
+                attack_rows.append((j, lc))
             else:
                 train_rows.append(j)
                 train_nd.append(num_data)
                 train_seeds.append(lc.seed * 7 + lc.training_round)
-        if train_rows and attack_jobs:
+        if train_rows and attack_rows:
             # the attackers ride along with ZERO rows (nd = 0: the trainer leaves their models untouched), so the
             # launch covers every local client in place — no gather / scatter of the trained rows — and their
             # attack results are written into their local_params rows once the launch is done (_finish_local)
-            for j, i, lc, atk in attack_jobs:
+            for j, lc in attack_rows:
                 train_rows.append(j)
                 train_nd.append(0)
                 train_seeds.append(lc.seed * 7 + lc.training_round)
@@ -483,25 +509,62 @@ class FLEngine:
             train_rows = [train_rows[k] for k in order]
             train_nd = [train_nd[k] for k in order]
             train_seeds = [train_seeds[k] for k in order]
-        tq1 = time.perf_counter()
+        # FedAvg weights of the selected rows (single rank, every row stored): staged with the rest, so the
+        # aggregate needs no host -> device copy after the training (== ops.fedavg's s / s.sum(), exact sums)
+        sel_nd = np.asarray([prep["meta"][r, 2] for r in self._local_rows()], np.float64) if self.world == 1 else None
+        fw = sel_nd / sel_nd.sum() if sel_nd is not None and sel_nd.size and sel_nd.sum() > 0 else np.zeros(1)
         # every per-round host value the device needs goes up in ONE asynchronous copy (a pageable
         # torch.tensor(..., device=) per item was a blocking copy each: ~1.5 ms of host time per round)
-        js = [j for j, _ in started]
+        js = [j for j, _, _, _ in prep["clients"]]
         plan_seeds = [sd * 1000003 + 17 for sd in train_seeds]
-        meta_d, js_d, rows_d, pseed_d, nd_d, tseed_d = self._staging.upload([
-            meta[:, :META], np.asarray(js, np.int64), np.asarray(train_rows, np.int64),
+        meta_d, js_d, rows_d, pseed_d, nd_d, tseed_d, fw_d = self._staging.upload([
+            prep["meta"][:, :META], np.asarray(js, np.int64), np.asarray(train_rows, np.int64),
             np.asarray([(s & 0xFFFFFFFFFFFFFFFF) - (1 << 64) if (s & 0xFFFFFFFFFFFFFFFF) >= (1 << 63)
                         else (s & 0xFFFFFFFFFFFFFFFF) for s in plan_seeds], np.int64),
             np.asarray(train_nd, np.int32),
-            np.asarray([self._dev_seed(s) for s in train_seeds], np.int32)])
+            np.asarray([self._dev_seed(s) for s in train_seeds], np.int32), fw])
+        tq2 = time.perf_counter()
+        plan = None
+        if train_rows:
+            plan = make_plan(self.train_table.n, train_nd, cfg.epoch, plan_seeds, dev,
+                             staged=(pseed_d, nd_d) if dev.type == "cuda" else None)
+        prep.update({"dec": decisions, "train_rows": train_rows, "train_seeds": train_seeds,
+                     "attack_rows": [j for j, _ in attack_rows], "js": js, "meta_d": meta_d, "js_d": js_d,
+                     "rows_d": rows_d, "tseed_d": tseed_d, "plan": plan,
+                     "fedavg_w": fw_d if sel_nd is not None and fw.size == len(self.selected) else None,
+                     "tq1": tq1, "tq2": tq2})
+
+    def _enqueue_local(self, prep: dict, genuine: Dict[int, Optional[torch.Tensor]]) -> dict:
+        """Device half of a launch: START parameters, the update block, the training launch."""
+        cfg = self.cfg
+        dev = self.device
+        tq = time.perf_counter()
+        for j, i, lc, _ in prep["clients"]:
+            g = genuine.get(i)
+            if lc.info.attack is not None and g is not None and g.shape[0] > 0:
+                lc.genuine = g
+        dec = self._attack_decisions(prep)
+        if dec != prep["dec"]:
+            self._stage(prep, dec)  # (an attacker's first attack round)
+        attack_jobs = [(j, i, lc, lc.info.attack) for (j, i, lc, _), a in zip(prep["clients"], dec) if a]
+        train_rows, train_seeds, js, js_d = prep["train_rows"], prep["train_seeds"], prep["js"], prep["js_d"]
+        rows_d = prep["rows_d"]
         n_local = len(self.local)
+        # the common case (every local client trains) trains local_params in place: no gather / scatter
+        in_place = train_rows == list(range(n_local))
+        # single rank, every local client in the launch (attackers with zero rows), trained in place: the round
+        # reads the update matrix straight from local_params and the meta columns from the host mirror, so
+        # no update block is built at all
+        plain = (bool(train_rows) and in_place and self.world == 1 and not self.fast_fedavg
+                 and self._local_rows() == list(range(n_local)))
+        block = None if plain else torch.zeros(self.slots, self.W, dtype=torch.float32, device=dev)
         tq2 = time.perf_counter()
         # START parameters of every started client (one batched generate / broadcast copy)
-        if started:
+        if prep["clients"]:
             if self.mode == "hyper":
-                start = self.hyper.generate_many([i for _, i in started])
+                start = self.hyper.generate_many([i for _, i, _, _ in prep["clients"]])
             else:
-                p = self._start_params(started[0][1])
+                p = self._start_params(prep["clients"][0][1])
                 start = None if p is None else p[None, :].expand(len(js), -1)
             if start is not None:
                 if js == list(range(len(js))):
@@ -513,9 +576,10 @@ class FLEngine:
             # round's validation stream waits for this point, not for the training launched below
             self._start_ready = torch.cuda.Event()
             self._start_ready.record(torch.cuda.current_stream(dev))
-        for j in faults:
+        for j in prep["faults"]:
             self.local_params[j, 0] = float("nan")
-        block[:, self.P:self.P + META] = meta_d
+        if block is not None:
+            block[:, self.P:self.P + META] = prep["meta_d"]
         tp0 = time.perf_counter()
         pending = None
         ready = None
@@ -523,19 +587,17 @@ class FLEngine:
             # the attackers' inputs are ready now; the side stream must not also wait for the training launch
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(dev))
-        # the common case (every local client trains) trains local_params in place: no gather / scatter
-        in_place = train_rows == list(range(n_local))
+        params = None
         if train_rows:
             params = self.local_params if in_place else self.local_params.index_select(0, rows_d).contiguous()
-            plan = make_plan(self.train_table.n, train_nd, cfg.epoch, plan_seeds, dev,
-                             staged=(pseed_d, nd_d) if dev.type == "cuda" else None)
-            pending = self.trainer.launch(params, plan, cfg.lr, cfg.batch_size, train_seeds,
-                                          seeds_dev=tseed_d if self._dev_seed is not _no_dev_seed else None)
+            pending = self.trainer.launch(params, prep["plan"], cfg.lr, cfg.batch_size, train_seeds,
+                                          seeds_dev=prep["tseed_d"] if self._dev_seed is not _no_dev_seed else None)
         self.ckpt_writer.kick()  # last round's deferred checkpoint copy overlaps this round's training
         tp1 = time.perf_counter()
-        return {"block": block, "attack_jobs": attack_jobs, "ready": ready, "pending": pending, "params": params
-                if train_rows else None, "in_place": in_place, "rows_d": rows_d, "n_local": n_local,
-                "meta": meta, "train_rows": train_rows, "t": (tq, tq1, tq2, tp0, tp1)}
+        return {"block": block, "attack_jobs": attack_jobs, "ready": ready, "pending": pending, "params": params,
+                "in_place": in_place, "rows_d": rows_d, "n_local": n_local, "meta": prep["meta"],
+                "train_rows": train_rows, "fedavg_w": prep["fedavg_w"], "plain": plain,
+                "t": (prep["tq"], prep["tq1"], prep["tq2"], tp0, tp1), "t_enqueue": tp0 - tq}
 
     def _finish_local(self, st: dict) -> torch.Tensor:
         """Attackers' math (side stream), then wait for the training launch and fill the update block."""
@@ -563,10 +625,7 @@ class FLEngine:
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
         tp2 = time.perf_counter()
-        # single rank, every local client in the launch (attackers with zero rows), trained in place: the round
-        # reads the update matrix straight from local_params and the meta columns from the host mirror
-        self._plain_rows = (pending is not None and in_place and self.world == 1 and not self.fast_fedavg
-                            and self._local_rows() == list(range(n_local)))
+        self._plain_rows = pending is not None and st["plain"]  # (_enqueue_local: no update block)
         self._pending = pending
         P, E = self.P, self.E
         if pending is not None:
@@ -616,8 +675,9 @@ class FLEngine:
                 if ok:
                     block[j, :P] = mal
                 block[j, P + 1] = 1.0 if ok else 0.0
-        self._lw_times = {"t_lw_prep": tp0 - tq, "t_lw_prep_host": tq1 - tq, "t_lw_prep_upload": tq2 - tq1,
-                          "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tw,
+        self._fedavg_w = st.get("fedavg_w")
+        self._lw_times = {"t_lw_prep": (tq2 - tq) + st.get("t_enqueue", 0.0), "t_lw_prep_host": tq1 - tq,
+                          "t_lw_prep_upload": tq2 - tq1, "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tw,
                           "t_lw_wait": tp3 - tp2, "t_lw_post": time.perf_counter() - tp3}
         self._meta_host = hm
         return block
@@ -647,6 +707,11 @@ class FLEngine:
             return info
         if mode == "FLTrust":
             self.global_params = self._fltrust(U)
+            return info
+        if mode == "fedavg" and self._fedavg_w is not None and U.shape[0] == self._fedavg_w.shape[0] and U.is_cuda:
+            # the weights were staged with the launch (sizes known then): no host -> device copy here
+            self.global_params = ops.weighted_rows(U, self._fedavg_w)
+            info["n"] = int(U.shape[0])
             return info
         fn = AGGREGATORS[mode]
         res: AggResult = fn(U, sizes, attackers=attackers, seed=self.seed * 13 + self.round_no)
@@ -729,6 +794,10 @@ class FLEngine:
             st, self._spec = self._spec, None
             if st is None:
                 st = self._launch_local(self._genuine_for_attackers())
+            if self._speculative and self.rounds_left > 1 and not last and self._next_prep is None:
+                # the next launch's host half (draws, uploads, plan) while this round's training runs: after
+                # it, only the aggregate, START and the launch itself separate two training kernels
+                self._next_prep = self._prepare_local()
             block = self._finish_local(st)
             if self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
                 self._sync()
@@ -744,16 +813,16 @@ class FLEngine:
             t2 = t3 = time.perf_counter()
         else:
             trace.push("fl/gather")
-            allb = self.comm.all_gather_rows(block)                        # [world*slots, W]
             rows = self._local_rows()
             idx = self._sel_cache[2]
             if self.world == 1:  # every row is local: the host already knows the meta columns
                 meta = torch.from_numpy(self._meta_host[rows])
                 if self._plain_rows:
-                    U = self.local_params[:len(rows)]  # the trained models ARE the update rows: no block copies
+                    U = self.local_params[:len(rows)]  # the trained models ARE the update rows: no block at all
                 else:
-                    U = allb.index_select(0, idx)[:, :P].contiguous()
+                    U = self.comm.all_gather_rows(block).index_select(0, idx)[:, :P].contiguous()
             else:
+                allb = self.comm.all_gather_rows(block)                    # [world*slots, W]
                 sel = allb.index_select(0, idx)
                 U = sel[:, :P].contiguous()
                 # the round's ONE host read: every client's [valid, result, size, attacker | losses] (it also
@@ -766,13 +835,14 @@ class FLEngine:
                 self._sync()
             trace.pop()
             t2 = time.perf_counter()
-            results = meta[:, 1] > 0.5
-            sizes = meta[:, 2].clone()
-            attackers = meta[:, 3] > 0.5
+            mn = meta.numpy()  # (numpy: a handful of tiny host ops, cheaper than torch CPU tensors)
+            results = mn[:, 1] > 0.5
+            sizes = torch.from_numpy(mn[:, 2].copy())
+            attackers = torch.from_numpy(mn[:, 3] > 0.5)
             round_ok = bool(results.all())
             # stored updates (arrival in client order; the reference stops storing after a failure)
             if not round_ok:
-                stored = int(torch.nonzero(~results)[0, 0])
+                stored = int(np.nonzero(~results)[0][0])
             snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) \
                 else None
             with trace.range("fl/aggregate"):

@@ -22,6 +22,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
+import time
+
 import torch
 
 from ..data import DeviceTable
@@ -333,11 +335,35 @@ class FusedTrainer:
                                                     lr, seeds if seeds_dev is None else seeds_dev)
             what = "fused trainer"
 
+        # ok + losses come back in ONE asynchronous copy into a pinned buffer, and result() waits on an event
+        # (two blocking .cpu() reads cost two host round trips between the round's training and its aggregate)
+        C, E = losses.shape
+        buf = self._pinned(C, E)
+        buf.copy_(torch.cat([ok.to(torch.float32)[:, None], losses], 1), non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(self.device))
+
         def fin():
-            okh, lh = self.T.finish(ok, losses, what)
-            return [bool(x) for x in okh.tolist()], lh
+            # poll instead of a blocking wait: the host then wakes within microseconds of the launch's end
+            # (a blocking event wait sleeps on an interrupt); sleep(0) lets the checkpoint thread run
+            while not done.query():
+                time.sleep(0)
+            okh = buf[:, 0].to(torch.int32)
+            if bool((okh < 0).any()):
+                raise RuntimeError(f"{what}: a cross-workgroup hand-off timed out (workgroups not co-resident?)")
+            return [bool(x) for x in okh.tolist()], buf[:, 1:].clone()
 
         return Pending(fin, ok, losses)
+
+    def _pinned(self, C: int, E: int) -> torch.Tensor:
+        """Pinned [C, 1 + E] result buffers, a ring of 3 (a launch's result is read before the launch after
+        next is enqueued: at most two are in flight)."""
+        ring = getattr(self, "_pin_ring", None)
+        if ring is None or ring[0][0].shape != (C, 1 + E):
+            ring = self._pin_ring = ([torch.empty(C, 1 + E, dtype=torch.float32, pin_memory=True) for _ in range(3)], [0])
+        bufs, k = ring
+        k[0] = (k[0] + 1) % len(bufs)
+        return bufs[k[0]]
 
 
 class OracleTrainer:

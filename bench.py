@@ -131,6 +131,10 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if os.environ.get("AFL_BENCH_TIMES") and rank == 0:  # per-round host timings of the timed rounds (JSONL)
+        with open(os.environ["AFL_BENCH_TIMES"], "w") as f:
+            for r in recs:
+                f.write(json.dumps({k: v for k, v in r.items() if k.startswith("t_") or k in ("round", "ok")}) + "\n")
     if args.profile_rounds and rank == 0:
         for r in recs:
             print(json.dumps({k: r[k] for k in ("round", "ok", "t_lw_prep", "t_lw_prep_host", "t_lw_prep_upload", "t_lw_launch", "t_lw_attack", "t_lw_wait", "t_lw_post", "t_local",

@@ -432,8 +432,13 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   const long wsf = tf2 ? afl_tf2_ws_floats() : rnn2 ? afl_rnn2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats();
   const long stride = ((wsf + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());
-  auto ok = torch::zeros({C}, order.options());
-  auto losses = torch::zeros({C, epochs}, params.options());
+  const int split_eff = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);  // (rnn2 / tf2: 3 workgroups per client)
+  const long sync_words = split_eff > 1 ? (long)C * (tf2 || rnn2 ? AFL_TF2_SYNC_WORDS : AFL_TF_SYNC_WORDS) : 0;
+  // ok [C] | losses [C, E] | the hand-off words (16-byte aligned): ONE zero fill per launch
+  const long head = ((long)C + (long)C * epochs + 3) / 4 * 4;
+  auto zero = torch::zeros({head + sync_words}, order.options());
+  auto ok = zero.narrow(0, 0, C);
+  auto losses = zero.narrow(0, C, (long)C * epochs).view(torch::kFloat32).view({(long)C, epochs});
   if (C == 0) return {ok, losses};
   AflTfTrainArgs a;
   a.params = params.data_ptr<float>();
@@ -466,12 +471,8 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
     a.kt = kt->data_ptr<float>();
     a.kt_n = (int)kt->size(0);
   }
-  a.split = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);  // (rnn2 / tf2: 3 workgroups per client)
-  torch::Tensor sync;
-  if (a.split > 1) {  // branch-parallel launch: zeroed hand-off words, fresh every call
-    sync = torch::zeros({(long)C * (tf2 || rnn2 ? AFL_TF2_SYNC_WORDS : AFL_TF_SYNC_WORDS)}, order.options());
-    a.sync = (uint32_t*)sync.data_ptr<int>();
-  }
+  a.split = split_eff;
+  if (a.split > 1) a.sync = (uint32_t*)zero.data_ptr<int>() + head;  // branch-parallel: zeroed hand-off words
   const int rc = tf2 ? afl_tf2_train(&a, cur()) : rnn2 ? afl_rnn2_train(&a, cur())
                  : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
   TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");

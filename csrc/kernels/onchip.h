@@ -190,6 +190,12 @@ __device__ __forceinline__ int colsum32(const float (&x)[8], int lane, float& su
 }
 
 __device__ __forceinline__ bool mbit(uint32_t m, int j) { return (m >> j) & 1u; }
+// x if bit j of m is set, else +0.0 (== bit ? x : 0.f bit for bit, NaN included): the bit becomes an
+// all-ones / zero word with ONE signed bitfield extract and masks x with one AND — two VALU instructions
+// instead of the test, compare and select
+__device__ __forceinline__ float keepf(float x, uint32_t m, int j) {
+  return __uint_as_float(__float_as_uint(x) & (uint32_t)__builtin_amdgcn_sbfe((int)m, j, 1));
+}
 
 // ------------------------------------------------------------------------ packed-FP32 row math
 // The branch workgroups are VALU-issue-bound, so the LayerNorm / affine math runs two features per

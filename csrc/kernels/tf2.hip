@@ -332,7 +332,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     vec16(bv, vec + VS_VB * 256, g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float m = bit(sv.matt, t) ? INV_K01 : 0.f;
+      const float m = keepf(INV_K01, sv.matt, t);
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[4 * t + i] = (acc[t][i] + bv[4 * t + i]) * m;
     }
@@ -359,7 +359,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int j = 4 * t + i;
-        x1[j] = h0[j] + (bit(sv.m1, j) ? (acc[t][i] + bo[j]) * INV_K01 : 0.f);
+        x1[j] = h0[j] + keepf((acc[t][i] + bo[j]) * INV_K01, sv.m1, j);
       }
     sv.rstd1 = ln_fwd2(x1);
     save16(sv.xh1, x1);
@@ -381,9 +381,8 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     for (int i = 0; i < 4; ++i) {
       float gp;
       const float gl = gelu_and_grad(acc[i] + bf[i], gp);
-      const bool kp = (mk1 >> (4 + i)) & 1u;
-      f2v[i] = kp ? gl * INV_K01 : 0.f;
-      sv.gk[i] = kp ? gp * INV_K01 : 0.f;
+      f2v[i] = keepf(gl * INV_K01, mk1, 4 + i);
+      sv.gk[i] = keepf(gp * INV_K01, mk1, 4 + i);
     }
     st4<TK16>(smem + B_F2, r, g, f2v);
   }
@@ -403,7 +402,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int j = 4 * t + i;
-        x2[j] = x1n[j] + (bit(sv.m2, j) ? (acc[t][i] + b3[j]) * INV_K01 : 0.f);
+        x2[j] = x1n[j] + keepf((acc[t][i] + b3[j]) * INV_K01, sv.m2, j);
       }
     sv.rstd2 = ln_fwd2(x2);
     save16(sv.xh2, x2);
@@ -455,7 +454,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   {  // d(ffn.3 out) -> ffn.3 backward (d f2) -> d(ffn.0 pre-activation)
     float d3[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) d3[j] = bit(sv.m2, j) ? dr2[j] * INV_K01 : 0.f;
+    for (int j = 0; j < 16; ++j) d3[j] = keepf(dr2[j] * INV_K01, sv.m2, j);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DF3, r, 4 * t + g, d3 + 4 * t);
     f4v acc = mma(wtfrag<true>(smem + B_IMG_F2, LD32, 0, 0, lane), bfrag(d3, 0), Z4);
@@ -489,7 +488,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   {  // out_proj backward: d a = d o . Wo ; d v = attention-dropout'(d a)
     float dO[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dO[j] = bit(sv.m1, j) ? dr1[j] * INV_K01 : 0.f;
+    for (int j = 0; j < 16; ++j) dO[j] = keepf(dr1[j] * INV_K01, sv.m1, j);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DO, r, 4 * t + g, dO + 4 * t);
     const s8v b0 = bfrag(dO, 0), b1 = bfrag(dO, 1);
@@ -497,7 +496,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     for (int T = 0; T < 4; ++T) {
       f4v acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
       acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 1, lane), b1, acc);
-      const float m = bit(sv.matt, T) ? INV_K01 : 0.f;
+      const float m = keepf(INV_K01, sv.matt, T);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dv[4 * T + i] = acc[i] * m;
     }
@@ -1019,8 +1018,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
           const gf2v gl = gelu2(gf2v{acc[t][i] + b1[j], acc[t][i + 1] + b1[j + 1]}, gp);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            a1[j + h] = bit(mh, j + h) ? gl[h] * INV_K03 : 0.f;
-            gk1[j + h] = bit(mh, j + h) ? gp[h] * INV_K03 : 0.f;
+            a1[j + h] = keepf(gl[h] * INV_K03, mh, j + h);
+            gk1[j + h] = keepf(gp[h] * INV_K03, mh, j + h);
           }
         }
     }
