@@ -599,13 +599,11 @@ class FLEngine:
                 "train_rows": train_rows, "fedavg_w": prep["fedavg_w"], "plain": plain,
                 "t": (prep["tq"], prep["tq1"], prep["tq2"], tp0, tp1), "t_enqueue": tp0 - tq}
 
-    def _finish_local(self, st: dict) -> torch.Tensor:
-        """Attackers' math (side stream), then wait for the training launch and fill the update block."""
-        block, attack_jobs, ready, pending = st["block"], st["attack_jobs"], st["ready"], st["pending"]
-        params, in_place, rows_d, n_local = st["params"], st["in_place"], st["rows_d"], st["n_local"]
-        tq, tq1, tq2, tp0, tp1 = st["t"]
+    def _finish_attacks(self, st: dict) -> None:
+        """Attackers' math on a side stream; their results replace their local_params rows (stream-ordered
+        after the training launch, which read / wrote back their untouched models: no host wait)."""
+        attack_jobs, ready, pending, in_place = st["attack_jobs"], st["ready"], st["pending"], st["in_place"]
         dev = self.device
-        hm = st["meta"]  # host mirror of the block's meta columns (ok filled in below): no device read needed
         tw = time.perf_counter()  # a speculative launch (run_round) may have been enqueued long before
         atk_out = []  # (row, ok, malicious update)
         if attack_jobs:
@@ -624,7 +622,23 @@ class FLEngine:
                         print_with_color(f"[===] Client {i} attacks with {atk.mode} {host_info(res.info)}", "red")
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
-        tp2 = time.perf_counter()
+        if pending is not None and in_place:
+            for j, ok, mal in atk_out:
+                if ok:
+                    self.local_params[j].copy_(mal)
+        st["atk_out"], st["tw"], st["tp2"] = atk_out, tw, time.perf_counter()
+
+    def _finish_local(self, st: dict) -> Optional[torch.Tensor]:
+        """Attackers' math (``_finish_attacks``, unless done already), then wait for the training launch and
+        fill the update block (none at world 1 with plain rows)."""
+        if "atk_out" not in st:
+            self._finish_attacks(st)
+        block, pending = st["block"], st["pending"]
+        params, in_place, rows_d, n_local = st["params"], st["in_place"], st["rows_d"], st["n_local"]
+        tq, tq1, tq2, tp0, tp1 = st["t"]
+        atk_out, tw, tp2 = st["atk_out"], st["tw"], st["tp2"]
+        dev = self.device
+        hm = st["meta"]  # host mirror of the block's meta columns (ok filled in below): no device read needed
         self._plain_rows = pending is not None and st["plain"]  # (_enqueue_local: no update block)
         self._pending = pending
         P, E = self.P, self.E
@@ -639,12 +653,9 @@ class FLEngine:
                     hm[j, 1] = 1.0 if o else 0.0
                     hm[j, META:META + E] = np.asarray(losses[k], dtype=np.float32)[:E]
             tp3 = time.perf_counter()
-            # the attack results replace the attackers' rows (ordered after the launch: it has read / written back
-            # their untouched models) — A-15: an attacker still reports its num_data, ok = the attack's result
+            # A-15: an attacker still reports its num_data, ok = the attack's result (its row: _finish_attacks)
             for j, ok, mal in atk_out:
                 hm[j, 1] = 1.0 if ok else 0.0
-                if ok and in_place:
-                    self.local_params[j].copy_(mal)
             if self._plain_rows:
                 pass
             elif in_place:
@@ -798,6 +809,7 @@ class FLEngine:
                 # the next launch's host half (draws, uploads, plan) while this round's training runs: after
                 # it, only the aggregate, START and the launch itself separate two training kernels
                 self._next_prep = self._prepare_local()
+            esl = self._early_launch(st, last)
             block = self._finish_local(st)
             if self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
                 self._sync()
@@ -806,7 +818,17 @@ class FLEngine:
         snapshot = None
         attackers = None
         stored = len(self.selected)
-        if self.fast_fedavg:
+        if esl is not None:
+            # FedAvg, one rank: the aggregate and the next launch went in before the wait (_early_launch)
+            U = None
+            meta = torch.from_numpy(self._meta_host[self._local_rows()])
+            results = meta.numpy()[:, 1] > 0.5
+            round_ok = bool(results.all())
+            info = {"n": len(self.selected), "path": "early-launch"} if round_ok else {}
+            if not round_ok:
+                self._early_launch_failed(esl, results)
+            t2 = t3 = time.perf_counter()
+        elif self.fast_fedavg:
             U = None
             round_ok, meta = self._fedavg_allreduce(block)
             info = {"path": "fedavg-allreduce"}
@@ -868,10 +890,14 @@ class FLEngine:
         # same global model with the same client counters, i.e. exactly this launch.  Every rank decides
         # the same (replicated validation), so the ranks' launches and gathers stay in lockstep.
         vstream = None
-        if self._speculative and round_ok and self.rounds_left > 1 and not last:
+        agg_done = None
+        if esl is not None and self._spec is not None:
+            agg_done = esl["agg_done"]
+        elif self._speculative and round_ok and self.rounds_left > 1 and not last:
             agg_done = torch.cuda.Event()
             agg_done.record(torch.cuda.current_stream(self.device))
             self._spec = self._launch_local(self._genuine_for_attackers())
+        if agg_done is not None:
             if self._val_stream is None:
                 self._val_stream = torch.cuda.Stream(device=self.device)
             vstream = self._val_stream
@@ -882,6 +908,57 @@ class FLEngine:
         if vstream is not None:
             self.ckpt_writer.kick()  # the next launch is already in: copy + write while it trains
         return rec
+
+    def _early_launch(self, st: dict, last: bool) -> Optional[dict]:
+        """FedAvg on one rank with plain rows: this round's aggregate and the NEXT round's launch are enqueued
+        before the host waits for this round's training, so no host work separates two training kernels.
+        The aggregate keeps the old global model on the device when a client failed (the host learns that
+        after the wait), which makes the launch exactly this round's retry (same START, the next client
+        draws); with attackers a failure discards it and restores the host state it consumed, because their
+        genuine sample then comes from the stored prefix.  Returns None where the ordinary path runs."""
+        if not (self._speculative and self.mode == "fedavg" and self.world == 1 and st.get("plain")
+                and st.get("fedavg_w") is not None and self.global_params is not None and self.rounds_left > 1
+                and not last and not self.cfg.engine.get("compat-fedavg-alias", False)):
+            return None
+        self._finish_attacks(st)
+        if not all(ok for _, ok, _ in st["atk_out"]):
+            return None
+        n = len(self.selected)
+        U = self.local_params[:n]
+        ok_all = (st["pending"].ok_device()[:n] > 0).all()
+        g_old = self.global_params
+        g = torch.where(ok_all, ops.weighted_rows(U, st["fedavg_w"]), g_old)
+        snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
+                self.server_rng.getstate(), self.genuine_pool)
+        keep = None
+        if self._has_attackers:  # the pool of a fully stored round (before the next START overwrites U)
+            keep = [k for k, i in enumerate(self.selected) if self.table[i].attack is None]
+            self.genuine_pool = U[keep].clone() if keep else None
+        self.global_params = g
+        agg_done = torch.cuda.Event()
+        agg_done.record(torch.cuda.current_stream(self.device))
+        prep = self._next_prep  # (staged ahead: the snapshot above already includes its draws)
+        self._spec = self._launch_local(self._genuine_for_attackers())
+        return {"g_old": g_old, "snap": snap, "keep": keep, "pool": self.genuine_pool, "agg_done": agg_done,
+                "prep": prep}
+
+    def _early_launch_failed(self, esl: dict, results: np.ndarray) -> None:
+        self.global_params = esl["g_old"]  # (the device selected the same values: the launch's START)
+        if esl["keep"] is None:
+            return  # no attackers: the launch in flight is this round's retry
+        # attackers sample the stored prefix's genuine rows: discard the launch, restore what it consumed
+        stored = int(np.nonzero(~results)[0][0])
+        pos = [esl["keep"].index(k) for k in range(stored) if k in esl["keep"]]
+        pool = esl["pool"][pos] if pos else None
+        states, srng, _ = esl["snap"]
+        for lc, (rs, tr, gen) in zip(self.local, states):
+            lc.rng.setstate(rs)
+            lc.training_round = tr
+            lc.genuine = gen
+        self.server_rng.setstate(srng)
+        self._spec = None
+        self._next_prep = esl["prep"]  # the launch's host half is reused as it was (same draws)
+        self.genuine_pool = pool
 
     def _client_losses(self) -> Optional[List[Optional[List[float]]]]:
         """Per-epoch training loss of every selected client (None for attackers and failed clients), from

@@ -106,11 +106,12 @@ constexpr long WS_BYTES = WS_SAV + 2 * SAV_BR_BYTES;
 #ifdef RNN2_STAMPS
 struct Stamp {
   bool on = false;
+  int who = 0;  // the stamping thread: lane 0 of wave stamps[62]
   uchar* smem = nullptr;
   __device__ __forceinline__ void operator()(int id, int tid) {
     if (!on) return;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) {
+    if (tid == who) {
       LDS_AS uint64_t* t = (LDS_AS uint64_t*)(smem + ST_OFF);
       t[id] += now - t[ST_N - 1];
       t[ST_N - 1] = now;
@@ -122,9 +123,19 @@ struct Stamp {
   __device__ __forceinline__ void operator()(int, int) {}
 };
 #endif
+// Wave priorities (as in tf2.hip): the critical chain at 2, the work that only has to finish before the next
+// hand-off arrives (prefetch, masks, the head's deferred tiles) at 0.
+#ifndef RNN2_NO_PRIO
+__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(2); }
+__device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
+#else
+__device__ __forceinline__ void prio_hi() {}
+__device__ __forceinline__ void prio_lo() {}
+#endif
 __device__ __forceinline__ void stamp_init(Stamp& stp, const AflTfTrainArgs& a, uchar* smem) {
 #ifdef RNN2_STAMPS
   stp.on = a.stamps && (long)blockIdx.x == (long)a.stamps[63];
+  stp.who = a.stamps ? 64 * (int)(a.stamps[62] & 7) : 0;
   stp.smem = smem;
   if (threadIdx.x == 0) *(LDS_AS uint64_t*)(smem + ST_OFF + 8 * (ST_N - 1)) = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -647,11 +658,13 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     const AdamK K = adam_k(a, step);
     Saved sv;
     u32x4 outp[2];
+    prio_hi();
     asm volatile(";MARK fwd");
     br_forward(smem, xin, aru(mka), sv, outp, rsv, lane, wave, tid);
     const uint32_t xpk[2] = {pk2(xin[0], xin[1]), pk2(xin[2], xin[3])};  // xin -> X1 tile after dW2
     stp(0, tid);
     gr_put(rg, gr_off(0, BR, wave, lane), outp, (uint32_t)step);  // this wave's output rows -> head
+    prio_lo();
     w.b0 += BS;  // the next batch's inputs and dropout masks while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) {
@@ -663,6 +676,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     u32x4 u[2];
     const int go[1] = {gr_off(1, BR, wave, lane)};
     const uint32_t fv = gr_get<1>(rg, go, u, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
+    prio_hi();
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) break;
     float dh[16];
@@ -840,6 +854,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       timed_out = failed = true;
       break;
     }
+    prio_hi();
     stp(0, tid);
     // ---- fc1 + ReLU
     float z1[8], a1[8];
@@ -920,6 +935,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         gr_put(rg, gr_off(1, hb, wave, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
       }
     }
+    prio_lo();
     stp(1, tid);
     // ---- deferred: dW operand tiles and column sums of this wave's rows
     {

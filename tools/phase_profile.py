@@ -108,9 +108,10 @@ def main_rnn(args):
     R.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, seeds)
     torch.cuda.synchronize()
     steps = args.epochs * ((args.rows + 127) // 128)
-    for b in blocks:
+    for b, wv in [(b, wv) for b in blocks for wv in (range(8) if args.wave < 0 else [args.wave])]:
         stamps = torch.zeros(64, dtype=torch.int64, device=dev)
         stamps[63] = b
+        stamps[62] = wv
         t0 = time.perf_counter()
         R.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, seeds, opt_mode=args.opt_mode,
                         stamps=stamps)
@@ -118,7 +119,7 @@ def main_rnn(args):
         wall = time.perf_counter() - t0
         names = NAMES_RNN_H if b % 3 == 0 else NAMES_RNN_B
         st = stamps.cpu().tolist()[:63]
-        out = {"model": "RNNModel", "block": b, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps,
+        out = {"model": "RNNModel", "block": b, "wave": wv, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps,
                "us_per_step_wall": wall * 1e6 / steps, "us_per_step_stamped": sum(st) * 0.01 / steps,
                "phases_us_per_step": {f"{i:02d} {names.get(i, '?')}": round(v * 0.01 / steps, 3)
                                       for i, v in enumerate(st) if v}}
