@@ -847,6 +847,8 @@ class FLEngine:
                 allb = self.comm.all_gather_rows(block)                    # [world*slots, W]
                 sel = allb.index_select(0, idx)
                 U = sel[:, :P].contiguous()
+                # FedAvg: the aggregate and the next launch go in on the device before the host read below
+                esl = self._early_launch(st, last, U=U, sel=sel)
                 # the round's ONE host read: every client's [valid, result, size, attacker | losses] (it also
                 # waits for the gather, i.e. for the slowest rank's clients)
                 meta = sel[:, P:P + META + self.E].double().cpu()
@@ -867,16 +869,21 @@ class FLEngine:
                 stored = int(np.nonzero(~results)[0][0])
             snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) \
                 else None
-            with trace.range("fl/aggregate"):
-                info = self._aggregate(U, sizes, attackers, round_ok)
-                if self.phase_sync:  # per-phase timings only; otherwise validation queues behind it
-                    self._sync()
+            if esl is not None:  # (several ranks: the aggregate and the next launch are in already)
+                info = {"n": len(self.selected), "path": "early-launch"} if round_ok else {}
+                if not round_ok:
+                    self._early_launch_failed(esl, results)
+            else:
+                with trace.range("fl/aggregate"):
+                    info = self._aggregate(U, sizes, attackers, round_ok)
+                    if self.phase_sync:  # per-phase timings only; otherwise validation queues behind it
+                        self._sync()
             if info.get("agg_failed"):
                 round_ok = False
             t3 = time.perf_counter()
         self._round_meta = meta
         # ---- genuine pool for the next START (non-attacker rows stored this round; only attackers read it) ----
-        if self._has_attackers and attackers is not None:
+        if self._has_attackers and attackers is not None and esl is None:
             keep = [k for k in range(stored) if not bool(attackers[k])]
             self.genuine_pool = U[keep].clone() if keep else None
             if (keep and keep[0] == 0 and round_ok and self.mode == "fedavg" and self.global_params is not None
@@ -909,25 +916,38 @@ class FLEngine:
             self.ckpt_writer.kick()  # the next launch is already in: copy + write while it trains
         return rec
 
-    def _early_launch(self, st: dict, last: bool) -> Optional[dict]:
+    def _early_ok(self, last: bool) -> bool:
+        return (self._speculative and self.mode == "fedavg" and not self.fast_fedavg
+                and self.global_params is not None and self.rounds_left > 1 and not last
+                and not self.cfg.engine.get("compat-fedavg-alias", False))
+
+    def _early_launch(self, st: dict, last: bool, U: Optional[torch.Tensor] = None,
+                      sel: Optional[torch.Tensor] = None) -> Optional[dict]:
         """FedAvg on one rank with plain rows: this round's aggregate and the NEXT round's launch are enqueued
         before the host waits for this round's training, so no host work separates two training kernels.
         The aggregate keeps the old global model on the device when a client failed (the host learns that
         after the wait), which makes the launch exactly this round's retry (same START, the next client
         draws); with attackers a failure discards it and restores the host state it consumed, because their
         genuine sample then comes from the stored prefix.  Returns None where the ordinary path runs."""
-        if not (self._speculative and self.mode == "fedavg" and self.world == 1 and st.get("plain")
-                and st.get("fedavg_w") is not None and self.global_params is not None and self.rounds_left > 1
-                and not last and not self.cfg.engine.get("compat-fedavg-alias", False)):
+        if not self._early_ok(last):
             return None
-        self._finish_attacks(st)
-        if not all(ok for _, ok, _ in st["atk_out"]):
-            return None
-        n = len(self.selected)
-        U = self.local_params[:n]
-        ok_all = (st["pending"].ok_device()[:n] > 0).all()
+        if sel is None:  # one rank, plain rows: called before _finish_local
+            if not (self.world == 1 and st.get("plain") and st.get("fedavg_w") is not None):
+                return None
+            self._finish_attacks(st)
+            if not all(ok for _, ok, _ in st["atk_out"]):
+                return None
+            n = len(self.selected)
+            U = self.local_params[:n]
+            ok_all = (st["pending"].ok_device()[:n] > 0).all()
+            w = st["fedavg_w"]
+        else:  # several ranks: called on the gathered rows (device), before the host reads their meta
+            P = self.P
+            ok_all = ((sel[:, P] > 0.5) & (sel[:, P + 1] > 0.5)).all()
+            s = sel[:, P + 2].double()
+            w = s / s.sum()
         g_old = self.global_params
-        g = torch.where(ok_all, ops.weighted_rows(U, st["fedavg_w"]), g_old)
+        g = torch.where(ok_all, ops.weighted_rows(U, w), g_old)
         snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
                 self.server_rng.getstate(), self.genuine_pool)
         keep = None
