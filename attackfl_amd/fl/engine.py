@@ -412,10 +412,25 @@ class FLEngine:
                 G = pool.shape[0]
                 k = max(int(self.cfg.genuine_rate * G), 1)
                 idx = self.server_rng.sample(range(G), k)
-                out[i] = pool[idx] if ci.owner == self.rank else None
+                out[i] = self._take_rows(pool, idx) if ci.owner == self.rank else None
             else:
                 out[i] = None
         return out
+
+    def _take_rows(self, pool: torch.Tensor, idx: List[int]) -> torch.Tensor:
+        """``pool[idx]`` with the index list on the device through a small cache: indexing a device tensor
+        with a Python list makes a pageable host -> device copy, which synchronises the stream (the host
+        would wait for the training launch already enqueued — the early launch's whole point)."""
+        if pool.device.type != "cuda":
+            return pool[idx]
+        key = tuple(idx)
+        cache = self.__dict__.setdefault("_rows_idx", {})
+        ix = cache.get(key)
+        if ix is None:
+            if len(cache) > 1024:
+                cache.clear()
+            ix = cache[key] = torch.tensor(idx, dtype=torch.long).to(pool.device)
+        return pool.index_select(0, ix)
 
     # ------------------------------------------------------------------------------------------
     # LOCAL
@@ -824,7 +839,7 @@ class FLEngine:
             meta = torch.from_numpy(self._meta_host[self._local_rows()])
             results = meta.numpy()[:, 1] > 0.5
             round_ok = bool(results.all())
-            info = {"n": len(self.selected), "path": "early-launch"} if round_ok else {}
+            info = self._early_info(round_ok)
             if not round_ok:
                 self._early_launch_failed(esl, results)
             t2 = t3 = time.perf_counter()
@@ -870,7 +885,7 @@ class FLEngine:
             snapshot = self.hyper.snapshot() if (self.mode == "hyper" and self.cfg.hyper_detection.get("enable")) \
                 else None
             if esl is not None:  # (several ranks: the aggregate and the next launch are in already)
-                info = {"n": len(self.selected), "path": "early-launch"} if round_ok else {}
+                info = self._early_info(round_ok)
                 if not round_ok:
                     self._early_launch_failed(esl, results)
             else:
@@ -917,9 +932,12 @@ class FLEngine:
         return rec
 
     def _early_ok(self, last: bool) -> bool:
-        return (self._speculative and self.mode == "fedavg" and not self.fast_fedavg
-                and self.global_params is not None and self.rounds_left > 1 and not last
-                and not self.cfg.engine.get("compat-fedavg-alias", False))
+        if self.mode == "hyper":
+            mode_ok = self.device.type == "cuda" and self.hyper._native_ok()
+        else:
+            mode_ok = (self.mode == "fedavg" and not self.fast_fedavg and self.global_params is not None
+                       and not self.cfg.engine.get("compat-fedavg-alias", False))
+        return self._speculative and mode_ok and self.rounds_left > 1 and not last
 
     def _early_launch(self, st: dict, last: bool, U: Optional[torch.Tensor] = None,
                       sel: Optional[torch.Tensor] = None) -> Optional[dict]:
@@ -946,10 +964,17 @@ class FLEngine:
             ok_all = ((sel[:, P] > 0.5) & (sel[:, P + 1] > 0.5)).all()
             s = sel[:, P + 2].double()
             w = s / s.sum()
-        g_old = self.global_params
-        g = torch.where(ok_all, ops.weighted_rows(U, w), g_old)
         snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
                 self.server_rng.getstate(), self.genuine_pool)
+        g_old, hyper_step = self.global_params, None
+        if self.mode == "hyper":  # the update runs, or leaves the hypernetwork untouched, as the device decides
+            hyper_step = self.hyper.step
+            self.ckpt_writer.fence()  # the previous round's checkpoint copy of the arena, updated in place below
+            self.hyper.train(self.selected, {i: U[k] for k, i in enumerate(self.selected)},
+                             enable=ok_all.to(torch.int32).reshape(1))
+            g = g_old
+        else:
+            g = torch.where(ok_all, ops.weighted_rows(U, w), g_old)
         keep = None
         if self._has_attackers:  # the pool of a fully stored round (before the next START overwrites U)
             keep = [k for k, i in enumerate(self.selected) if self.table[i].attack is None]
@@ -960,10 +985,20 @@ class FLEngine:
         prep = self._next_prep  # (staged ahead: the snapshot above already includes its draws)
         self._spec = self._launch_local(self._genuine_for_attackers())
         return {"g_old": g_old, "snap": snap, "keep": keep, "pool": self.genuine_pool, "agg_done": agg_done,
-                "prep": prep}
+                "prep": prep, "hyper_step": hyper_step}
+
+    def _early_info(self, round_ok: bool) -> dict:
+        if not round_ok:
+            return {}
+        if self.mode == "hyper":
+            return {"path": "early-launch", "_lazy": lambda: self.hyper.last_info}  # (as _aggregate)
+        return {"n": len(self.selected), "path": "early-launch"}
 
     def _early_launch_failed(self, esl: dict, results: np.ndarray) -> None:
         self.global_params = esl["g_old"]  # (the device selected the same values: the launch's START)
+        if esl["hyper_step"] is not None:  # the device skipped the hypernetwork update: its step count too
+            self.hyper.step = esl["hyper_step"]
+            self.hyper._info_dev = None
         if esl["keep"] is None:
             return  # no attackers: the launch in flight is this round's retry
         # attackers sample the stored prefix's genuine rows: discard the launch, restore what it consumed

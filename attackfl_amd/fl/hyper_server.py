@@ -19,7 +19,7 @@ computed locally and no scatter is needed.
 from __future__ import annotations
 
 from collections import OrderedDict
-from typing import Dict, Sequence
+from typing import Optional, Dict, Sequence
 
 import torch
 
@@ -130,11 +130,14 @@ class HyperServer:
             return False
         return h.slots["W"][0] - h.slots["mlp0.W"][0] <= ops.native().hyper_small_capacity()
 
-    def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor]) -> None:
+    def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor],
+              enable: Optional[torch.Tensor] = None) -> None:
         """One round of the sequential server update over ``selected`` (client order kept).
 
         On GPU the whole round is enqueued by ``ops.hyper_server_update`` (three launches per client,
-        no host synchronisation, ``last_info`` read lazily); on CPU the composite path below is the oracle."""
+        no host synchronisation, ``last_info`` read lazily); on CPU the composite path below is the oracle.
+        ``enable`` (GPU only): device int32 word decided on the device — 0 leaves the hypernetwork and its
+        moments untouched (the caller then rolls ``step`` back)."""
         h = self.hnet
         selected = list(selected)
         if not selected:
@@ -151,10 +154,12 @@ class HyperServer:
                 U = torch.stack([r.contiguous() for r in rows])
                 urows = list(range(len(rows)))
             info = ops.hyper_server_update(h.arena, self.m, self.v, U, urows, selected, self.layout_vec(), self.step,
-                                           self.lr, self.clip)
+                                           self.lr, self.clip, enable=enable)
             self.step += len(selected)
             self._info_dev = info[-1]  # no host sync here (see last_info)
             return
+        if enable is not None:
+            raise RuntimeError("a device-decided hypernetwork update needs the native server kernels")
         for i in selected:
             emb, feat, acts = h.features(i)
             delta, dfeat = ops.hyper_delta_vjp(h.W, h.b, feat, updates[i])   # δ = W f + b - u ; Wᵀδ

@@ -245,7 +245,16 @@ class PackedHyperNet:
 
     def features_many(self, idxs) -> torch.Tensor:
         """MLP features [n, H] of several clients, batched through every layer."""
-        h = self.emb[torch.as_tensor(list(idxs), dtype=torch.long, device=self.emb.device)]
+        key = tuple(int(i) for i in idxs)
+        cache = self.__dict__.setdefault("_idx_dev", {})
+        ix = cache.get(key)
+        if ix is None:
+            # (built once per client set: a pageable host -> device copy synchronises the stream, i.e. would
+            # make the host wait for the training launch enqueued before it)
+            if len(cache) > 256:
+                cache.clear()
+            ix = cache[key] = torch.as_tensor(list(key), dtype=torch.long, device=self.emb.device)
+        h = self.emb[ix]
         for i in range(self.n_hidden + 1):
             Wm, bm = self.mlp(i)
             h = torch.addmm(bm[None, :], h, Wm.t())

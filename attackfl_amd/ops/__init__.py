@@ -368,11 +368,12 @@ def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale:
 
 
 def hyper_server_update(arena, m, v, U, urows, clients, layout, step0: int, lr: float, clip: float,
-                        beta1=0.9, beta2=0.999, eps=1e-8) -> torch.Tensor:
-    """Sequential pFedHN server update of a whole round on the device (no host sync); info [n, 2]."""
+                        beta1=0.9, beta2=0.999, eps=1e-8, enable: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sequential pFedHN server update of a whole round on the device (no host sync); info [n, 2].
+    ``enable``: optional device int32 word; 0 leaves arena / moments untouched (decided on the device)."""
     return native().hyper_server_update(arena, m, v, U.contiguous(), [int(r) for r in urows],
                                         [int(c) for c in clients], [int(x) for x in layout], int(step0), float(lr),
-                                        float(clip), float(beta1), float(beta2), float(eps))
+                                        float(clip), float(beta1), float(beta2), float(eps), enable)
 
 
 def hyper_features(arena, clients, layout) -> torch.Tensor:

@@ -354,8 +354,15 @@ HySmallDesc hy_desc(const std::vector<int64_t>& lay, long& offW, long& offB, lon
 // without a host synchronisation.  Returns info [n, 2] = (grad norm, clip scale) per client (device).
 torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::Tensor v, torch::Tensor U,
                                   std::vector<int64_t> urows, std::vector<int64_t> clients, std::vector<int64_t> lay,
-                                  int64_t step0, double lr, double clip, double b1, double b2, double eps) {
+                                  int64_t step0, double lr, double clip, double b1, double b2, double eps,
+                                  c10::optional<torch::Tensor> enable) {
   for (auto* t : {&arena, &m, &v, &U}) check_dev(*t, "hyper tensor", torch::kFloat32);
+  const int* en = nullptr;
+  if (enable.has_value() && enable->defined()) {
+    check_dev(*enable, "enable", torch::kInt32);
+    TORCH_CHECK(enable->numel() == 1, "hyper: enable must be one int32");
+    en = enable->data_ptr<int>();
+  }
   long offW, offB, P;
   HySmallDesc d = hy_desc(lay, offW, offB, P);
   const int n = (int)clients.size();
@@ -377,7 +384,7 @@ torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::T
   afl_hyper_server_update(arena.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), U.data_ptr<float>(),
                           ur.data(), cl.data(), n, d, offW, offB, P, (int)step0, (float)lr, (float)clip, (float)b1,
                           (float)b2, (float)eps, delta.data_ptr<float>(), partial.data_ptr<float>(),
-                          feat.data_ptr<float>(), info.data_ptr<float>(), cur());
+                          feat.data_ptr<float>(), info.data_ptr<float>(), en, cur());
   AFL_CHECK_LAUNCH();
   return info;
 }

@@ -37,7 +37,7 @@ struct HySmallDesc {
 void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
                              int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
                              float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
-                             float* info, hipStream_t s);
+                             float* info, const int* enable, hipStream_t s);
 void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const int* clients, int n, float* out,
                         hipStream_t s);
 long afl_hyper_small_capacity();  // max floats of embedding-MLP parameters the small-net kernel stages in LDS

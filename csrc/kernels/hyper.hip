@@ -265,7 +265,10 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
                                                        int nb, int ci, int cj, float* __restrict__ feat_j,
                                                        float* __restrict__ info, HySmallDesc d, long nmlp,
                                                        float clip, float lr_bc1, float rsqrt_bc2, float b1, float b2,
-                                                       float eps) {
+                                                       float eps, const int* __restrict__ enable) {
+  // enable (device word, optional): 0 = the round failed, leave the hypernetwork untouched (the engine enqueues
+  // the update before it knows; FLEngine._early_launch)
+  if (enable != nullptr && *enable == 0) return;
   __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];
   __shared__ float acts[HS_LMAX + 1][HS_HMAX];
   __shared__ float dz[HS_LMAX][HS_HMAX];  // dL/d(output of layer l)
@@ -435,7 +438,9 @@ __global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, flo
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       const float* __restrict__ delta, const float* __restrict__ f,
                                                       long P, int H, float lr_bc1, float rsqrt_bc2, float b1,
-                                                      float b2, float eps, const float* __restrict__ gsp) {
+                                                      float b2, float eps, const float* __restrict__ gsp,
+                                                      const int* __restrict__ enable) {
+  if (enable != nullptr && *enable == 0) return;
   __shared__ float fs[HS_HMAX];
   if (threadIdx.x < H) fs[threadIdx.x] = f[threadIdx.x];
   __syncthreads();
@@ -480,14 +485,14 @@ __global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, flo
 void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
                              int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
                              float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
-                             float* info, hipStream_t s) {
+                             float* info, const int* enable, hipStream_t s) {
   const int H = d.H;
   const int nb = afl_hyper_nblocks(P);
   float* W = A + offW;
   float* bv = A + offB;
   const long nmlp = offW - d.w[0];
   hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, -1, clients[0], feat, info, d,
-                     nmlp, clip, 0.f, 0.f, b1, b2, eps);
+                     nmlp, clip, 0.f, 0.f, b1, b2, eps, enable);
   const long nW4 = P * H / 4;
   const int nba = (int)min(4096L, (nW4 + 255) / 256);
   for (int k = 0; k < n; ++k) {
@@ -503,9 +508,10 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
       hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta, partial,
                          H + 1);
     hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
-                       k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps);
+                       k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps,
+                       enable);
     hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, delta, fk, P, H,
-                       lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1);
+                       lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1, enable);
   }
 }
 
@@ -513,7 +519,8 @@ void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const i
                         hipStream_t s) {
   for (int k = 0; k < n; ++k)
     hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, const_cast<float*>(A), nullptr, nullptr, nullptr, 0,
-                       -1, clients[k], out + (long)k * d.H, nullptr, d, offW - d.w[0], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
+                       -1, clients[k], out + (long)k * d.H, nullptr, d, offW - d.w[0], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                       nullptr);
 }
 
 long afl_hyper_small_capacity() { return HS_SMEM; }

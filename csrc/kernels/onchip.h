@@ -477,6 +477,49 @@ __device__ __forceinline__ int gr_off(int dir, int src, int wave, int lane) {
   return dir * GR_DIR_BYTES + (src * 8 + wave) * 4096 + lane * 16;
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gr_rsrc(gu32* sync) { return rsrc((void*)(sync + AFL_TF_SYNC_WORDS)); }
+#ifdef ONCHIP_R1_HANDOFF
+// A/B variant (tools/ab_native.sh): the flag form (R1) on the same slots — 32 B of write-through payload per
+// lane at the slot's start, the storing wave drains, lane 0 stores the tag into the slot's flag line
+// (+2048); the consumer polls the flag(s), then issues its payload loads.
+__device__ __forceinline__ void gr_put(__amdgpu_buffer_rsrc_t rg, int off, const u32x4 (&u)[2], uint32_t tag) {
+  const int lane = threadIdx.x & 63, base = off - lane * 16;
+  __builtin_amdgcn_raw_buffer_store_b128(u[0], rg, base + lane * 32, 0, 16);
+  store_guard();
+  __builtin_amdgcn_raw_buffer_store_b128(u[1], rg, base + lane * 32 + 16, 0, 16);
+  store_guard();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(tag, rg, base + 2048, 0, 16);
+}
+template <int S>
+__device__ __forceinline__ uint32_t gr_get(__amdgpu_buffer_rsrc_t rg, const int (&off)[S], u32x4 (&out)[2 * S],
+                                           uint32_t want, int shift, gu32* tmo, int lane) {
+  uint32_t v = 0;
+  for (long spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t f = __builtin_amdgcn_readfirstlane(
+          __builtin_amdgcn_raw_buffer_load_b32(rg, off[s] - lane * 16 + 2048, 0, 16));
+      if (s == 0) v = f;
+      ok = ok && (f >> shift) == want;
+    }
+    if (ok) break;
+    if (spins > fk::XWG_MAX_SPINS) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0xFFFFFFFFu;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // payload loads stay below the poll
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int base = off[s] - lane * 16;
+    out[2 * s] = __builtin_amdgcn_raw_buffer_load_b128(rg, base + lane * 32, 0, 16);
+    out[2 * s + 1] = __builtin_amdgcn_raw_buffer_load_b128(rg, base + lane * 32 + 16, 0, 16);
+  }
+  return v;
+}
+#else
 __device__ __forceinline__ void gr_put(__amdgpu_buffer_rsrc_t rg, int off, const u32x4 (&u)[2], uint32_t tag) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -514,6 +557,7 @@ __device__ __forceinline__ uint32_t gr_get(__amdgpu_buffer_rsrc_t rg, const int 
     __builtin_amdgcn_s_sleep(1);
   }
 }
+#endif
 __device__ __forceinline__ gu32* xf(gu32* base, int group, int wave) { return base + (group * 8 + wave) * 32; }
 
 __device__ __forceinline__ void unpack16(const u32x4 (&u)[2], float (&x)[16]) {
