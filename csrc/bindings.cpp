@@ -377,7 +377,7 @@ torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::T
   std::vector<int> cl(clients.begin(), clients.end());
   std::vector<long> ur(urows.begin(), urows.end());
   auto opt = arena.options();
-  auto delta = torch::empty({P}, opt);
+  auto delta = torch::empty({2 * P}, opt);  // (two: the fused head Adam reads client k's, writes client k+1's)
   auto partial = torch::empty({(long)afl_hyper_nblocks(P) * (d.H + 1)}, opt);
   auto feat = torch::empty({2 * 128}, opt);
   auto info = torch::empty({n, 2}, opt);

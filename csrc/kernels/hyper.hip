@@ -433,6 +433,124 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
   }
 }
 
+// Client k's head Adam (grad = (*gsp) * delta_k (x) f_k, as k_hyper_adam_v) FUSED with client k+1's rows
+// pass (k_hyper_rows4) over the rows it has just updated: delta_n = W' f_n + b' - u_n, per-block partials of
+// W'^T delta_n and |delta_n|^2.  One sweep over the [P, H] heads per client instead of two (the heads are
+// 19.5 MB for TransformerModel; the rows pass needs the updated rows, which this thread holds in registers).
+// Same row mapping as k_hyper_rows4, same partial layout (k_hyper_small reduces it), same arithmetic as the
+// two kernels it replaces.
+__global__ void __launch_bounds__(HR4_NT) k_hyper_adam_rows4(float* __restrict__ W, float* __restrict__ b,
+                                                             float* __restrict__ m, float* __restrict__ v,
+                                                             const float* __restrict__ delta_k,
+                                                             const float* __restrict__ f_k,
+                                                             const float* __restrict__ gsp,
+                                                             const float* __restrict__ f_n,
+                                                             const float* __restrict__ u_n,
+                                                             float* __restrict__ delta_n, float* __restrict__ partial,
+                                                             long P, int H, float lr_bc1, float rsqrt_bc2, float b1,
+                                                             float b2, float eps, const int* __restrict__ enable) {
+  if (enable != nullptr && *enable == 0) return;
+  __shared__ float red[HR4_NT / 64][HR_HMAX];
+  __shared__ float sq[HR4_NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, half = lane >> 5, H4 = H >> 2;
+  const bool act = j < H4;
+  const float4 fk = act ? reinterpret_cast<const float4*>(f_k)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 fn = act ? reinterpret_cast<const float4*>(f_n)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float gs = *gsp;
+  float4* W4 = reinterpret_cast<float4*>(W);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const long nW = P * H;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dsq = 0.f;
+  const long nslots = 2L * gridDim.x * (HR4_NT / 64);
+  const long slot = 2L * ((long)blockIdx.x * (HR4_NT / 64) + wv) + half;
+  for (long r0 = slot; r0 < P; r0 += HR4_U * nslots) {
+    float4 w[HR4_U], mm[HR4_U], vv[HR4_U];
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {
+      const long r = r0 + q * nslots;
+      const bool ok = act && r < P;
+      w[q] = ok ? W4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      mm[q] = ok ? m4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      vv[q] = ok ? v4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {
+      const long r = r0 + q * nslots;
+      const bool rv = r < P;  // (no early exit: the half-wave reduction below needs every lane of the half)
+      const long rr = rv ? r : 0;
+      const float dr = gs * delta_k[rr];
+      {  // head Adam on this lane's 4 columns (k_hyper_adam_v)
+        float* pp = &w[q].x;
+        float* mp = &mm[q].x;
+        float* vp = &vv[q].x;
+        const float* fp = &fk.x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float g = dr * fp[c];
+          mp[c] = mp[c] + (1.f - b1) * (g - mp[c]);
+          vp[c] = b2 * vp[c] + (1.f - b2) * g * g;
+          pp[c] -= lr_bc1 * mp[c] / (sqrtf(vp[c]) * rsqrt_bc2 + eps);
+        }
+        if (act && rv) {
+          W4[r * H4 + j] = w[q];
+          m4[r * H4 + j] = mm[q];
+          v4[r * H4 + j] = vv[q];
+        }
+      }
+      // bias Adam (every lane of the half computes it, lane 0 stores)
+      const float bm = m[nW + rr] + (1.f - b1) * (dr - m[nW + rr]);
+      const float bv = b2 * v[nW + rr] + (1.f - b2) * dr * dr;
+      const float bn = b[rr] - lr_bc1 * bm / (sqrtf(bv) * rsqrt_bc2 + eps);
+      // client k+1's rows pass on the updated row
+      float d = w[q].x * fn.x + w[q].y * fn.y + w[q].z * fn.z + w[q].w * fn.w;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (!rv) continue;
+      float val = d + bn;
+      val -= u_n[r];
+      if (j == 0) {
+        m[nW + r] = bm;
+        v[nW + r] = bv;
+        b[r] = bn;
+        delta_n[r] = val;
+        dsq += val * val;
+      }
+      acc.x += w[q].x * val;
+      acc.y += w[q].y * val;
+      acc.z += w[q].z * val;
+      acc.w += w[q].w * val;
+    }
+  }
+  acc.x += __shfl_xor(acc.x, 32, 64);
+  acc.y += __shfl_xor(acc.y, 32, 64);
+  acc.z += __shfl_xor(acc.z, 32, 64);
+  acc.w += __shfl_xor(acc.w, 32, 64);
+  if (half == 0 && act) {
+    red[wv][4 * j] = acc.x;
+    red[wv][4 * j + 1] = acc.y;
+    red[wv][4 * j + 2] = acc.z;
+    red[wv][4 * j + 3] = acc.w;
+  }
+  dsq = wave_sum(dsq);
+  if (lane == 0) sq[wv] = dsq;
+  __syncthreads();
+  if (tid < H) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < HR4_NT / 64; ++k) a += red[k][tid];
+    partial[(long)blockIdx.x * (H + 1) + tid] = a;
+  }
+  if (tid == 0) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < HR4_NT / 64; ++k) a += sq[k];
+    partial[(long)blockIdx.x * (H + 1) + H] = a;
+  }
+}
+
 // head Adam with grad = (*gsp) * delta (x) f ; float4 over W (H % 4 == 0, 16-B aligned), scalar over b
 __global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, float* __restrict__ bvec,
                                                       float* __restrict__ m, float* __restrict__ v,
@@ -495,23 +613,39 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
                      nmlp, clip, 0.f, 0.f, b1, b2, eps, enable);
   const long nW4 = P * H / 4;
   const int nba = (int)min(4096L, (nW4 + 255) / 256);
+  // the rows pass of client k + 1 rides in client k's head Adam (k_hyper_adam_rows4) when the heads are
+  // float4-shaped; otherwise (and for the first client) it is its own launch.  delta: two [P] buffers.
+#ifndef HYPER_NO_FUSE
+  const bool fused = hyper_rows4_ok(W, feat, H) && ((uintptr_t)(m + offW) & 15) == 0 && ((uintptr_t)(v + offW) & 15) == 0;
+#else
+  const bool fused = false;  // A/B build
+#endif
   for (int k = 0; k < n; ++k) {
     const int step = step0 + k + 1;
     const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
     const float lr_bc1 = (float)(lr / bc1), rbc2 = (float)(1.0 / sqrt(bc2));
     float* fk = feat + (k & 1) * HS_HMAX;
     float* fn = feat + ((k + 1) & 1) * HS_HMAX;
-    if (hyper_rows4_ok(W, fk, H))
-      hipLaunchKernelGGL(k_hyper_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta,
-                         partial, H + 1);
-    else
-      hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, delta, partial,
-                         H + 1);
+    float* dk = delta + (k & 1) * P;
+    float* dn = delta + ((k + 1) & 1) * P;
+    if (k == 0 || !fused) {
+      if (hyper_rows4_ok(W, fk, H))
+        hipLaunchKernelGGL(k_hyper_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, fk, U + urow[k] * P, P, H, dk,
+                           partial, H + 1);
+      else
+        hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, dk, partial,
+                           H + 1);
+    }
     hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
                        k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps,
                        enable);
-    hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, delta, fk, P, H,
-                       lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1, enable);
+    if (fused && k + 1 < n)
+      hipLaunchKernelGGL(k_hyper_adam_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, m + offW, v + offW, dk, fk,
+                         info + 2 * k + 1, fn, U + urow[k + 1] * P, dn, partial, P, H, lr_bc1, rbc2, b1, b2, eps,
+                         enable);
+    else
+      hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, dk, fk, P, H,
+                         lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1, enable);
   }
 }
 
