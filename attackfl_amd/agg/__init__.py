@@ -178,6 +178,9 @@ def byzantine(U: torch.Tensor, sizes=None, threshold: float = 0.9, **_) -> AggRe
     return AggResult(mean_of(U[keep]), True, {"kept": keep})
 
 
+# Contract of every aggregator: ``U`` is READ-ONLY and may be the live client-model rows (single rank: the
+# engine hands ``local_params`` itself, FLEngine._plain_rows) — never write it in place; a returned tensor may
+# alias one of its rows (Krum), which the engine clones before the next launch overwrites the rows.
 AGGREGATORS = {
     "fedavg": fedavg,
     "trimmed_mean": trimmed_mean,
