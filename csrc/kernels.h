@@ -149,8 +149,11 @@ struct AflGemm {
   int no_ts;       // 1: never take the tall-skinny path (tests compare the two kernels)
   float* asum;     // optional: asum[c * sasc + k] += sum_m A[c][m][k] (the bias gradient of a dX = dY.W GEMM)
   long sasc;
+  float* ws;       // optional split-K workspace [splitk][C][M][N]: with it, accum 2 is DETERMINISTIC — each
+                   // split stores its partial tile, a second pass adds the splits to C in split order
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
+long afl_bgemm_ws_floats(const AflGemm& g);  // workspace the deterministic split-K path needs (0: none)
 
 // cnn.hip: fused CNNModel towers (conv1-3 + pool + dropout) forward / backward, conv weight grads
 struct AflCnnBranch {
@@ -182,11 +185,14 @@ struct AflConvDwJob {
   float* gW;         // client-0 grad view [Cout][3*Cin] (client c at + c * sGc)
   float* gb;         // client-0 bias grad [Cout]
   int Cin, Cout, L, tile_base;
+  long ws_off;       // this job's [Cout][3*Cin] + [Cout] block in a split's workspace slice
 };
 struct AflConvDw {
   AflConvDwJob job[6];
   int njobs, total_tiles, splitk, C, B;
   long sGc;
+  float* ws;         // optional [splitk][C][ws_tot] workspace: deterministic split-K (partials, ordered sum)
+  long ws_tot;
 };
 int afl_conv_dw(const AflConvDw& a, hipStream_t s);
 struct AflCnnHead {

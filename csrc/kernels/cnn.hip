@@ -465,6 +465,7 @@ __device__ void conv_dw_tile(const AflConvDw& a, const AflConvDwJob& J, int t, u
   if (mb >= me) return;
   const float* dh = J.dh + (long)c * BL * J.Cout;
   const float* hp = J.hp + (long)c * BL * J.Cin;
+  float* wsp = a.ws ? a.ws + ((long)blockIdx.y * a.C + c) * a.ws_tot + J.ws_off : nullptr;  // this split's partials
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int so = tid & 63, sm0 = (tid >> 6) * 8;  // staging: row (o or kk) and 8 consecutive positions
   const bool bias = k0t == 0 && J.gb != nullptr;
@@ -532,13 +533,42 @@ __device__ void conv_dw_tile(const AflConvDw& a, const AflConvDwJob& J, int t, u
       for (int e = 0; e < 4; ++e) {
         const int o = o0 + wm + 16 * i + 4 * (lane >> 4) + e;
         const int k = k0t + wn + 16 * j + (lane & 15);
-        if (o < J.Cout && k < K) atomicAdd(gW + (long)o * K + k, acc[i][j][e]);
+        if (o < J.Cout && k < K) {
+          if (wsp)
+            wsp[(long)o * K + k] = acc[i][j][e];
+          else
+            atomicAdd(gW + (long)o * K + k, acc[i][j][e]);
+        }
       }
   if (bias) {
     bred[tid >> 6][so] = bsum;
     __syncthreads();
-    if (tid < DW_T && o0 + tid < J.Cout)
-      atomicAdd(J.gb + (long)c * a.sGc + o0 + tid, (bred[0][tid] + bred[1][tid]) + (bred[2][tid] + bred[3][tid]));
+    if (tid < DW_T && o0 + tid < J.Cout) {
+      const float bs = (bred[0][tid] + bred[1][tid]) + (bred[2][tid] + bred[3][tid]);
+      if (wsp)
+        wsp[(long)J.Cout * K + o0 + tid] = bs;
+      else
+        atomicAdd(J.gb + (long)c * a.sGc + o0 + tid, bs);
+    }
+  }
+}
+
+// deterministic split-K: grads += the splits' partials, summed in split order (splits with an empty row
+// range wrote nothing and are skipped, exactly as in conv_dw_tile)
+__global__ void __launch_bounds__(256) k_conv_dw_sum(AflConvDw a) {
+  const AflConvDwJob& J = a.job[blockIdx.y];
+  const int c = blockIdx.z, K = 3 * J.Cin;
+  const long n = (long)J.Cout * K + J.Cout;
+  const int BL = a.B * J.L;
+  const int chunk = ((BL + a.splitk - 1) / a.splitk + DW_K - 1) / DW_K * DW_K;
+  const int ns = (BL + chunk - 1) / chunk;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < ns; ++k) s += a.ws[((long)k * a.C + c) * a.ws_tot + J.ws_off + e];
+    if (e < (long)J.Cout * K)
+      J.gW[(long)c * a.sGc + e] += s;
+    else
+      J.gb[(long)c * a.sGc + (e - (long)J.Cout * K)] += s;
   }
 }
 
@@ -591,7 +621,11 @@ constexpr int H_GB = H_DZ + 128 * 4;              // gb2 [64] | gb1 [128] f32
 constexpr int H_RED = H_GB + 192 * 4;             // [8] f32
 constexpr int H_WO = H_RED + 8 * 4;               // output-layer weights [32] f32
 constexpr int H_RED3 = H_WO + 32 * 4;             // gb3 | gWo | gbo partial sums [72] f32
-constexpr int H_TOTAL = H_RED3 + 72 * 4;
+// per-wave partial sums of the bias / output-layer gradients, added in wave order afterwards (deterministic:
+// LDS atomics from 8 waves summed in arrival order)
+constexpr int H_RED3W = H_RED3 + 72 * 4;          // [8 waves][72] f32
+constexpr int H_GBW = H_RED3W + 8 * 72 * 4;       // [8 waves][gb2 64 | gb1 128] f32
+constexpr int H_TOTAL = H_GBW + 8 * 192 * 4;
 static_assert(H_TOTAL <= 160 * 1024, "cnn head LDS");
 
 __device__ __forceinline__ float wsum(float x) {
@@ -611,11 +645,10 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
   unsigned short* d3s = (unsigned short*)(smem + H_D3S);
   unsigned short* d2s = (unsigned short*)(smem + H_D2S);
   float* dz = (float*)(smem + H_DZ);
-  float* gb2 = (float*)(smem + H_GB);
-  float* gb1 = gb2 + 64;
   float* red = (float*)(smem + H_RED);
   float* wos = (float*)(smem + H_WO);
-  float* red3 = (float*)(smem + H_RED3);
+  float* red3w = (float*)(smem + H_RED3W);
+  float* gbw = (float*)(smem + H_GBW);
   const int c = blockIdx.x, B = h.B;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long wo = (long)c * h.sWc, go = (long)c * h.sGc;
@@ -668,8 +701,6 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
   }
   if (tid < 256) *(s8v*)(W3s + (tid >> 3) * H_L2 + 8 * (tid & 7)) = w3v;
   if (tid < 32) wos[tid] = wov;
-  if (tid < 192) gb2[tid] = 0.f;
-  if (tid < 72) red3[tid] = 0.f;
   __syncthreads();
   // fc2: [128 x 128] . W2^T -> [128 x 64]; wave -> m-tile w, n-tiles 0..3
   {
@@ -750,7 +781,7 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
     d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * wos[j] : 0.f);
   }
   // output-layer / fc3-bias gradients over the 128 rows: thread (j = tid & 31, rows 8 * (tid >> 5) ..)
-  // partials, the row groups folded by one lane swap and LDS atomics (red3 zeroed before the loss barrier)
+  // partials, the row groups folded by one lane swap, one slot per wave, summed in wave order
   {
     const int j = tid & 31, r0 = 8 * (tid >> 5);
     float a = 0.f, w = 0.f, z = 0.f;
@@ -765,17 +796,25 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
     w += __shfl_xor(w, 32, 64);
     z += __shfl_xor(z, 32, 64);
     if (lane < 32) {
-      atomicAdd(red3 + j, a);
-      atomicAdd(red3 + 32 + j, w);
-      if (j == 0) atomicAdd(red3 + 64, z);
+      red3w[wave * 72 + j] = a;
+      red3w[wave * 72 + 32 + j] = w;
+      if (j == 0) red3w[wave * 72 + 64] = z;
     }
   }
   __syncthreads();
-  if (tid < 32) {
-    h.gb3[go + tid] = red3[tid] * wos[tid];
-    h.gWo[go + tid] = red3[32 + tid];
-  } else if (tid == 64) {
-    h.gbo[go] = red3[64];
+  if (tid < 32 || tid == 64) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < HNT / 64; ++w) {
+      s0 += red3w[w * 72 + tid];
+      if (tid < 32) s1 += red3w[w * 72 + 32 + tid];
+    }
+    if (tid < 32) {
+      h.gb3[go + tid] = s0 * wos[tid];
+      h.gWo[go + tid] = s1;
+    } else {
+      h.gbo[go] = s0;
+    }
   }
   // dW3 [32 x 64] = d3^T f2 ; wave -> o-tile (w >> 2), i-tile (w & 3)
   {
@@ -805,11 +844,16 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
       }
       cs += __shfl_xor(cs, 16, 64);
       cs += __shfl_xor(cs, 32, 64);
-      if (lane < 16) atomicAdd(gb2 + n, cs);
+      if (lane < 16) gbw[wave * 192 + n] = cs;
     }
   }
   __syncthreads();
-  if (tid < 64) h.gb2[go + tid] = gb2[tid];
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < HNT / 64; ++w) sb += gbw[w * 192 + tid];
+    h.gb2[go + tid] = sb;
+  }
   // dW2 [64 x 128] = d2^T f1 ; wave -> o-tile (w >> 1), i-tiles 4 (w & 1) + 0..3
   {
     const int o0 = (wave >> 1) * 16, ib = (wave & 1) * 4;
@@ -849,11 +893,16 @@ __global__ void __launch_bounds__(HNT) k_cnn_head(AflCnnHead h) {
       }
       cs += __shfl_xor(cs, 16, 64);
       cs += __shfl_xor(cs, 32, 64);
-      if (lane < 16) atomicAdd(gb1 + n, cs);
+      if (lane < 16) gbw[wave * 192 + 64 + n] = cs;
     }
   }
   __syncthreads();
-  if (tid < 128) h.gb1[go + tid] = gb1[tid];
+  if (tid < 128) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < HNT / 64; ++w) sb += gbw[w * 192 + 64 + tid];
+    h.gb1[go + tid] = sb;
+  }
 }
 
 }  // namespace
@@ -895,6 +944,12 @@ int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s) {
 int afl_conv_dw(const AflConvDw& a, hipStream_t s) {
   if (a.njobs <= 0) return 0;
   hipLaunchKernelGGL(k_conv_dw, dim3(a.total_tiles, a.splitk, a.C), dim3(256), 0, s, a);
+  if (a.ws) {
+    long mx = 0;
+    for (int k = 0; k < a.njobs; ++k) mx = std::max(mx, (long)a.job[k].Cout * 3 * a.job[k].Cin + a.job[k].Cout);
+    hipLaunchKernelGGL(k_conv_dw_sum, dim3((unsigned)std::min<long>(64, (mx + 255) / 256), a.njobs, a.C), dim3(256), 0,
+                       s, a);
+  }
   return (int)hipGetLastError();
 }
 

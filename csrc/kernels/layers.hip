@@ -161,9 +161,25 @@ __global__ void __launch_bounds__(256) k_bgemm(AflGemm g) {
           Cc[off] = v;
         else if (g.accum == 1)
           Cc[off] += v;
+        else if (g.ws)  // deterministic split-K: this split's partial, summed in split order by k_split_sum
+          g.ws[(((long)blockIdx.y * g.nC + c) * g.M + m) * g.N + n] = v;
         else
           atomicAdd(Cc + off, v);
       }
+}
+
+// C[c][m][n] += sum over the first `ns` splits of ws[split][c][m][n], in split order (deterministic)
+__global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ ws, int ns, int nC, int M, int N,
+                                                   float* __restrict__ Cm, long sCc, long sCm, long sCn) {
+  const long total = (long)nC * M * N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int n = (int)(i % N);
+    const long cm = i / N;
+    const int m = (int)(cm % M), c = (int)(cm / M);
+    float s = ws[i];
+    for (int k = 1; k < ns; ++k) s += ws[(long)k * total + i];
+    Cm[(long)c * sCc + (long)m * sCm + (long)n * sCn] += s;
+  }
 }
 
 // ============================================================================ column sums
@@ -1011,6 +1027,10 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   }
   const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
   dim3 grid(tiles, max(1, g.splitk), g.nC);
+  const bool det = g.ws != nullptr && g.accum == 2 && g.splitk > 1;
+  const int kchunk = ((g.K + g.splitk - 1) / g.splitk + GK - 1) / GK * GK;
+  const int nsplit = (g.K + kchunk - 1) / kchunk;  // splits with a non-empty k range (every one of them
+                                                   // writes its whole partial tile)
   AflGemm gg = g;  // 16-B aligned k-contiguous rows take the vector-load path
   gg.avec = g.sAk == 1 && g.sAm % 4 == 0 && g.sAc % 4 == 0 && ((uintptr_t)g.A & 15) == 0;
   gg.bvec = g.sBk == 1 && g.sBn % 4 == 0 && g.sBc % 4 == 0 && ((uintptr_t)g.B & 15) == 0;
@@ -1023,7 +1043,19 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
     hipLaunchKernelGGL((k_bgemm<false, true>), grid, dim3(256), 0, s, gg);
   else
     hipLaunchKernelGGL((k_bgemm<false, false>), grid, dim3(256), 0, s, gg);
+  if (det) {
+    const long total = (long)g.nC * g.M * g.N;
+    const int nb = (int)std::min<long>(2048, (total + 255) / 256);
+    hipLaunchKernelGGL(k_split_sum, dim3(nb), dim3(256), 0, s, (const float*)g.ws, nsplit, g.nC, g.M, g.N, g.Cm,
+                       g.sCc, g.sCm, g.sCn);
+  }
   return launched();
+}
+
+long afl_bgemm_ws_floats(const AflGemm& g) {
+  if (g.accum != 2 || g.splitk <= 1 || g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
+  const int kchunk = ((g.K + g.splitk - 1) / g.splitk + GK - 1) / GK * GK;
+  return (long)((g.K + kchunk - 1) / kchunk) * g.nC * g.M * g.N;
 }
 
 int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s) {

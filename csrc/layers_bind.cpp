@@ -108,6 +108,14 @@ void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<tor
     g.asum = asum->data_ptr<float>();
     g.sasc = asum->stride(0);
   }
+  // split-K: deterministic (ordered partial sums) — the workspace lives in the caching allocator, stream-ordered
+  // (inside a captured step it comes from the graph's private pool)
+  torch::Tensor ws;
+  const long nws = afl_bgemm_ws_floats(g);
+  if (nws > 0) {
+    ws = torch::empty({nws}, A.options());
+    g.ws = ws.data_ptr<float>();
+  }
   ok(afl_bgemm(g, cur()), "bgemm");
 }
 
@@ -346,9 +354,16 @@ void conv_dw(std::vector<torch::Tensor> dh, std::vector<torch::Tensor> hp, std::
     j.Cout = Cout;
     j.L = (int)L[k];
     j.tile_base = tiles;
+    j.ws_off = a.ws_tot;
+    a.ws_tot += (long)Cout * K + Cout;
     tiles += ((Cout + 63) / 64) * ((K + 63) / 64);
   }
   a.total_tiles = tiles;
+  torch::Tensor ws;  // split-K partials: the weight gradients come out the same whatever order the splits ran in
+  if (a.splitk > 1) {
+    ws = torch::empty({(long)a.splitk * a.C * a.ws_tot}, dh[0].options());
+    a.ws = ws.data_ptr<float>();
+  }
   ok(afl_conv_dw(a, cur()), "conv_dw");
 }
 

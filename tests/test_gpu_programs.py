@@ -308,3 +308,47 @@ def test_cnn_tower_kernels_match_composite(gpu, B, p):
             for kind in ("weight", "bias"):
                 name = f"{br}_conv{i}.{kind}"
                 _close(prog.w(st[DEV][2], name), prog.w(st["cpu"][2], name), rel=2e-2, name=name)
+
+
+def test_splitk_gemm_is_deterministic(gpu):
+    """Split-K (accum 2) stores each split's partial tile and adds the splits in split order: the same
+    bits every run, whatever order the workgroups ran in (it was an atomic accumulation)."""
+    C, M, N, K = 3, 4096, 64, 40
+    g = torch.Generator().manual_seed(2)
+    dY = torch.randn(C, M, N, generator=g).to(DEV)
+    X = torch.randn(C, M, K, generator=g).to(DEV)
+    outs = []
+    for _ in range(3):
+        out = torch.zeros(C, N, K, device=DEV)
+        Lx.bgemm(dY.transpose(1, 2), X.transpose(1, 2), out, accum=2, splitk=16)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    _close(outs[0], torch.bmm(dY.cpu().transpose(1, 2), X.cpu()), name="splitk")
+
+
+def test_cnn_training_is_bit_reproducible(gpu):
+    """CNNModel: two graph-replayed training runs from the same state give the same parameters bit for bit
+    (the split-K fc1 GEMM, the conv weight gradients and the head's bias sums reduce in a fixed order), and
+    so does client 1 trained ALONE vs beside clients 0 and 2 (placement-independent: the multi-rank claim)."""
+    name, B, n, E, C = "CNNModel", 128, 1000, 2, 3
+    ds = synthetic_icu(n)
+    nd = [n // 2, n // 2 - 17, n // 3 + 1]
+    order = torch.stack([torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(10 * c + e))[:max(nd)]
+                                      for e in range(E)]) for c in range(C)]).to(torch.int32)
+    params = _params(name, C)
+    table = DeviceTable(ds, DEV)
+    runs = []
+    for _ in range(2):
+        p = params.clone().to(DEV)
+        ok, losses = ProgramRunner(make_program(name, C, B, DEV)).train(
+            table, p, Plan(order.to(DEV), torch.tensor(nd, dtype=torch.int32), E), lr=1e-3, seeds=[5, 6, 7])
+        assert ok.all()
+        runs.append((p.cpu(), losses.cpu()))
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0] - runs[1][0]).abs().max()
+    assert torch.equal(runs[0][1], runs[1][1])
+    p1 = params[1:2].clone().to(DEV)
+    ok, losses = ProgramRunner(make_program(name, 1, B, DEV)).train(
+        table, p1, Plan(order[1:2].contiguous().to(DEV), torch.tensor(nd[1:2], dtype=torch.int32), E), lr=1e-3,
+        seeds=[6])
+    assert ok.all()
+    assert torch.equal(p1.cpu()[0], runs[0][0][1]), (p1.cpu()[0] - runs[0][0][1]).abs().max()
