@@ -68,11 +68,14 @@ class _Program:
         return v.view(flat.shape[0], s.shape[0], -1)
 
     def dw(self, dY: torch.Tensor, X: torch.Tensor, gW: torch.Tensor) -> None:
-        """``gW [C, N, K] = dY^T X`` over the rows (split-K with atomic accumulation when the tile grid
-        alone would leave the GPU idle; ``grads`` is zeroed at the start of every step)."""
+        """``gW [C, N, K] = dY^T X`` over the rows (split-K — ordered per-split partials, deterministic — when
+        the tile grid alone would leave the GPU idle; ``grads`` is zeroed at the start of every step)."""
         M, N, K = dY.shape[1], dY.shape[2], X.shape[2]
-        tiles = math.ceil(N / 64) * math.ceil(K / 64) * dY.shape[0]
-        splitk = max(1, min(M // 256, math.ceil(1024 / tiles))) if dY.is_cuda else 1
+        # per-client tile count only: the split count (and with it the deterministic split-K summation order)
+        # must not depend on how many clients share the launch — a client's gradients are then the same bits
+        # whichever rank / packing trains it (128 splits x tiles per client ~ 1024 workgroups at 8 clients)
+        tiles = math.ceil(N / 64) * math.ceil(K / 64)
+        splitk = max(1, min(M // 256, math.ceil(128 / tiles))) if dY.is_cuda else 1
         Lx.bgemm(dY.transpose(1, 2), X.transpose(1, 2), gW, accum=2 if splitk > 1 else 0, splitk=splitk)
 
     def linear(self, X, params, wname, bname, out, act=0, ctl=None, layer=0, p=0.0):

@@ -151,9 +151,12 @@ struct AflGemm {
   long sasc;
   float* ws;       // optional split-K workspace [splitk][C][M][N]: with it, accum 2 is DETERMINISTIC — each
                    // split stores its partial tile, a second pass adds the splits to C in split order
+  float* ws_sum;   // optional workspace for the asum column sums (afl_bgemm_asum_ws_floats): ordered partials
 };
 int afl_bgemm(const AflGemm& g, hipStream_t s);
 long afl_bgemm_ws_floats(const AflGemm& g);  // workspace the deterministic split-K path needs (0: none)
+long afl_bgemm_asum_ws_floats(const AflGemm& g);  // workspace of the ordered asum partials (0: none)
+long afl_colsum_ws_floats(int M, int N, int nC);
 
 // cnn.hip: fused CNNModel towers (conv1-3 + pool + dropout) forward / backward, conv weight grads
 struct AflCnnBranch {
@@ -212,7 +215,9 @@ struct AflCnnHead {
   int S, E, C, B;
 };
 int afl_cnn_head(const AflCnnHead& h, hipStream_t s);
-int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s);
+// column sums; ws (optional, afl_colsum_ws_floats): per-row-block partials added in block order (deterministic)
+int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s,
+               float* ws = nullptr);
 int afl_gather_icu(const float* rows, const int* idx, const int* stepctl, int C, int B, int mask, float* vit,
                    float* lab, float* y, hipStream_t s);
 int afl_gather_har(const float* x, const long* y, int F, const int* idx, const int* stepctl, int C, int B, float* ox,
@@ -243,11 +248,13 @@ struct AflLnB {
   const float* gamma; long sPc;
   float* dx; long sXc, sXr; int dx_accum;  // d(pre-norm sum)
   float* da; long sAc, sAr;               // optional: drop_a'(dx) for the residual branch
-  float* dgamma; float* dbeta;            // grad slots (+ sPc), atomically accumulated
+  float* dgamma; float* dbeta;            // grad slots (+ sPc), accumulated
   int rows, nC;
   AflDrop da_drop, dout;
+  float* ws;  // optional [row blocks][C][128] partials (afl_ln_bwd_ws_floats): ordered, deterministic sums
 };
 int afl_ln_bwd(const AflLnB& l, hipStream_t s);
+long afl_ln_bwd_ws_floats(int rows, int nC);
 int afl_gru_fwd(const float* gi, const float* bhh, long sPc, int C, int B, float* h, long sHc, long sHr, int col0,
                 hipStream_t s);
 int afl_gru_bwd(const float* dh, long sHc, long sHr, int col0, const float* gi, const float* bhh, long sPc, int C,
@@ -263,7 +270,8 @@ int afl_step_end(int* stepctl, int* tcount, const int* bsz, const int* failed, i
 int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off,
                     int pe_off, float* h, hipStream_t s);
 int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float* grads, long P, int w_off, int b_off,
-                    hipStream_t s);
+                    hipStream_t s, float* ws = nullptr);
+long afl_conv_pe_bwd_ws_floats(int C, int B, int L);  // [row blocks][C][256] partials
 int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s);
 int afl_mean_rows_bwd(const float* dout, int C, int B, int L, float* dh, hipStream_t s);
 

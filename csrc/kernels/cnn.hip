@@ -563,8 +563,17 @@ __global__ void __launch_bounds__(256) k_conv_dw_sum(AflConvDw a) {
   const int chunk = ((BL + a.splitk - 1) / a.splitk + DW_K - 1) / DW_K * DW_K;
   const int ns = (BL + chunk - 1) / chunk;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    // (splits added in split order; their loads issued together)
+    float v[8];
     float s = 0.f;
-    for (int k = 0; k < ns; ++k) s += a.ws[((long)k * a.C + c) * a.ws_tot + J.ws_off + e];
+    int k = 0;
+    for (; k + 8 <= ns; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = a.ws[((long)(k + u) * a.C + c) * a.ws_tot + J.ws_off + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < ns; ++k) s += a.ws[((long)k * a.C + c) * a.ws_tot + J.ws_off + e];
     if (e < (long)J.Cout * K)
       J.gW[(long)c * a.sGc + e] += s;
     else

@@ -168,6 +168,23 @@ __global__ void __launch_bounds__(256) k_bgemm(AflGemm g) {
       }
 }
 
+// sum of p[0], p[stride], ... p[(n-1) * stride] added strictly in index order (deterministic), with U loads in
+// flight per batch: a plain loop issues one load, waits for it, adds, and so on (~L2 latency per partial)
+template <int U>
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ p, long stride, int n) {
+  float s = 0.f;
+  int q = 0;
+  for (; q + U <= n; q += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p[(long)(q + u) * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
+  }
+  for (; q < n; ++q) s += p[(long)q * stride];
+  return s;
+}
+
 // C[c][m][n] += sum over the first `ns` splits of ws[split][c][m][n], in split order (deterministic)
 __global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ ws, int ns, int nC, int M, int N,
                                                    float* __restrict__ Cm, long sCc, long sCm, long sCn) {
@@ -176,15 +193,39 @@ __global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ ws,
     const int n = (int)(i % N);
     const long cm = i / N;
     const int m = (int)(cm % M), c = (int)(cm / M);
-    float s = ws[i];
-    for (int k = 1; k < ns; ++k) s += ws[(long)k * total + i];
-    Cm[(long)c * sCc + (long)m * sCm + (long)n * sCn] += s;
+    Cm[(long)c * sCc + (long)m * sCm + (long)n * sCn] += ordered_sum<16>(ws + i, total, ns);
   }
+}
+
+// dst[c * sdc + j] += sum over p < np of ws[(p * nC + c) * ld + j]  (j < n), in p order: the deterministic
+// second pass of every per-block partial sum below (block order fixed, whatever order the blocks ran in)
+// (32 outputs per block, 8 partial groups per output: group g adds partials g, g + 8, ... in order, then the
+// 8 group sums are added in group order — a fixed association, so still the same bits every run)
+__global__ void __launch_bounds__(256) k_partial_sum(const float* __restrict__ ws, int np, int nC, int n, long ld,
+                                                     float* __restrict__ dst, long sdc) {
+  __shared__ float red[8][32];
+  const long total = (long)nC * n;
+  const int e = threadIdx.x & 31, gq = threadIdx.x >> 5;
+  const long i = (long)blockIdx.x * 32 + e;
+  const int c = (int)(i / n), j = (int)(i - (long)c * n);
+  const int cnt = np > gq ? (np - gq + 7) / 8 : 0;  // partials gq, gq + 8, ...
+  red[gq][e] = i < total ? ordered_sum<8>(ws + ((long)gq * nC + c) * ld + j, 8L * nC * ld, cnt) : 0.f;
+  __syncthreads();
+  if (gq == 0 && i < total) {
+    float sum = red[0][e];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) sum += red[q][e];
+    dst[(long)c * sdc + j] += sum;
+  }
+}
+void partial_sum(const float* ws, int np, int nC, int n, long ld, float* dst, long sdc, hipStream_t s) {
+  const long total = (long)nC * n;
+  hipLaunchKernelGGL(k_partial_sum, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, ws, np, nC, n, ld, dst, sdc);
 }
 
 // ============================================================================ column sums
 __global__ void __launch_bounds__(256) k_colsum(const float* __restrict__ Y, long sYc, long sYm, int M, int N,
-                                                float* __restrict__ out, long sOc) {
+                                                float* __restrict__ out, long sOc, float* __restrict__ ws) {
   __shared__ float red[4][64];
   const int c = blockIdx.z, col = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * 256;
@@ -197,7 +238,10 @@ __global__ void __launch_bounds__(256) k_colsum(const float* __restrict__ Y, lon
   __syncthreads();
   if (rg == 0 && col < N) {
     s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(out + (long)c * sOc + col, s);
+    if (ws)
+      ws[((long)blockIdx.y * gridDim.z + c) * N + col] = s;
+    else
+      atomicAdd(out + (long)c * sOc + col, s);
   }
 }
 
@@ -436,9 +480,13 @@ __global__ void __launch_bounds__(256) k_ln_bwd(AflLnB l) {
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s += red[r][threadIdx.x];
-    float* dst = threadIdx.x < 64 ? l.dgamma + (long)c * l.sPc + threadIdx.x
-                                  : l.dbeta + (long)c * l.sPc + threadIdx.x - 64;
-    atomicAdd(dst, s);
+    if (l.ws) {
+      l.ws[((long)blockIdx.x * l.nC + c) * 128 + threadIdx.x] = s;
+    } else {
+      float* dst = threadIdx.x < 64 ? l.dgamma + (long)c * l.sPc + threadIdx.x
+                                    : l.dbeta + (long)c * l.sPc + threadIdx.x - 64;
+      atomicAdd(dst, s);
+    }
   }
 }
 
@@ -734,7 +782,7 @@ __global__ void __launch_bounds__(256) k_conv_pe_fwd(const float* __restrict__ x
 // conv weight / bias gradients: 16 row groups x 16 lanes of 4 channels per workgroup, 1024 rows per workgroup
 __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x, const float* __restrict__ dh,
                                                      int C, int B, int L, float* __restrict__ grads, long P,
-                                                     int w_off, int b_off) {
+                                                     int w_off, int b_off, float* __restrict__ ws) {
   __shared__ float red[16][64][4];
   const int c = blockIdx.y, o0 = (threadIdx.x & 15) * 4, rg = threadIdx.x >> 4;
   const int nrows = B * L, r0 = blockIdx.x * 1024;
@@ -766,8 +814,12 @@ __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s += red[r][o][q];
-    float* gp = grads + (long)c * P;
-    atomicAdd(gp + (q < 3 ? w_off + o * 3 + q : b_off + o), s);
+    if (ws) {  // [block][C][192 taps | 64 biases]
+      ws[((long)blockIdx.x * C + c) * 256 + (q < 3 ? o * 3 + q : 192 + o)] = s;
+    } else {
+      float* gp = grads + (long)c * P;
+      atomicAdd(gp + (q < 3 ? w_off + o * 3 + q : b_off + o), s);
+    }
   }
 }
 
@@ -964,12 +1016,17 @@ __global__ void __launch_bounds__(TS_NTH) k_tsgemm(AflGemm g) {
       float x = 0.f;
 #pragma unroll
       for (int w = 0; w < TS_WAVES; ++w) x += red[w * K + tid];
-      atomicAdd(g.asum + (long)c * g.sasc + tid, x);
+      if (g.ws_sum)  // ordered partials [block][C][K] (deterministic)
+        g.ws_sum[((long)blockIdx.x * g.nC + c) * K + tid] = x;
+      else
+        atomicAdd(g.asum + (long)c * g.sasc + tid, x);
     }
   }
 }
 
 __host__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+constexpr int TS_ASUM_PARTS = 128;  // blocks per client of a k_tsgemm with ordered column-sum partials
 
 // shapes with a k_tsgemm instantiation; anything else (or misaligned / strided operands) takes k_bgemm
 int tsgemm_try(const AflGemm& g, hipStream_t s) {
@@ -997,11 +1054,16 @@ int tsgemm_try(const AflGemm& g, hipStream_t s) {
   }
 #undef TS_CASE
   const int ntile = (g.M + 15) / 16;
-  const int per_client = max(1, min((ntile + TS_WAVES - 1) / TS_WAVES, (4 * 256 + g.nC - 1) / g.nC));
+  // with ordered column-sum partials the block count per client must not depend on how many clients share
+  // the launch (the partials' summation order would change with the packing)
+  const int per_client = g.asum && g.ws_sum ? max(1, min((ntile + TS_WAVES - 1) / TS_WAVES, TS_ASUM_PARTS))
+                                            : max(1, min((ntile + TS_WAVES - 1) / TS_WAVES, (4 * 256 + g.nC - 1) / g.nC));
   const size_t lds = (size_t)g.N * (g.K + 8) * 2 + (size_t)g.N * 4;
   AflGemm gg = g;
   void* args[] = {&gg};
-  return (int)hipLaunchKernel(fn, dim3(per_client, g.nC), dim3(TS_NTH), args, lds, s);
+  const int e = (int)hipLaunchKernel(fn, dim3(per_client, g.nC), dim3(TS_NTH), args, lds, s);
+  if (e == 0 && g.asum && g.ws_sum) partial_sum(g.ws_sum, per_client, g.nC, g.K, g.K, g.asum, g.sasc, s);
+  return e;
 }
 
 }  // namespace
@@ -1013,7 +1075,7 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (!g.no_ts && g.asum && g.N >= 256 && g.sAk == 1) {
     // N = 256: the fused column sums' 16 extra VGPRs drop k_tsgemm<16, 2> to one wave per SIMD
     // (HAR FFN-down dX 0.41 -> 0.64 ms); a separate column-sum pass (~0.09 ms) is cheaper there
-    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s);
+    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s, g.ws_sum);
     if (e) return e;
     AflGemm g2 = g;
     g2.asum = nullptr;
@@ -1022,7 +1084,7 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   if (!g.no_ts && tsgemm_try(g, s) == 0) return launched();
   if (g.asum) {  // the 64x64-tile kernel re-reads A per column tile: column sums as a separate pass
     if (g.sAk != 1) return (int)hipErrorInvalidValue;
-    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s);
+    const int e = afl_colsum(g.A, g.sAc, g.sAm, g.M, g.K, g.nC, g.asum, g.sasc, s, g.ws_sum);
     if (e) return e;
   }
   const int tiles = ((g.M + GT - 1) / GT) * ((g.N + GT - 1) / GT);
@@ -1052,14 +1114,24 @@ int afl_bgemm(const AflGemm& g, hipStream_t s) {
   return launched();
 }
 
+long afl_bgemm_asum_ws_floats(const AflGemm& g) {
+  if (!g.asum || g.M <= 0 || g.K <= 0 || g.nC <= 0) return 0;
+  return (long)std::max<long>((g.M + 255) / 256, TS_ASUM_PARTS) * g.nC * g.K;
+}
+
+long afl_colsum_ws_floats(int M, int N, int nC) { return (long)((M + 255) / 256) * nC * N; }
+
 long afl_bgemm_ws_floats(const AflGemm& g) {
   if (g.accum != 2 || g.splitk <= 1 || g.M <= 0 || g.N <= 0 || g.K <= 0 || g.nC <= 0) return 0;
   const int kchunk = ((g.K + g.splitk - 1) / g.splitk + GK - 1) / GK * GK;
   return (long)((g.K + kchunk - 1) / kchunk) * g.nC * g.M * g.N;
 }
 
-int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64, (M + 255) / 256, nC), dim3(256), 0, s, Y, sYc, sYm, M, N, out, sOc);
+int afl_colsum(const float* Y, long sYc, long sYm, int M, int N, int nC, float* out, long sOc, hipStream_t s,
+               float* ws) {
+  hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64, (M + 255) / 256, nC), dim3(256), 0, s, Y, sYc, sYm, M, N, out, sOc,
+                     ws);
+  if (ws) partial_sum(ws, (M + 255) / 256, nC, N, N, out, sOc, s);
   return launched();
 }
 
@@ -1117,12 +1189,19 @@ int afl_ln_fwd(const AflLn& l, hipStream_t s) {
 int afl_ln_bwd(const AflLnB& l, hipStream_t s) {
   const bool v4 = rows16(l.dy, l.sDc, l.sDr) && rows16(l.s, l.sSc, l.sSr) && rows16(l.dx, l.sXc, l.sXr) &&
                   (!l.da || rows16(l.da, l.sAc, l.sAr));
+  const int np = (l.rows + LNB_ROWS - 1) / LNB_ROWS;
   if (v4)
-    hipLaunchKernelGGL(k_ln_bwd<true>, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
+    hipLaunchKernelGGL(k_ln_bwd<true>, dim3(np, l.nC), dim3(256), 0, s, l);
   else
-    hipLaunchKernelGGL(k_ln_bwd<false>, dim3((l.rows + LNB_ROWS - 1) / LNB_ROWS, l.nC), dim3(256), 0, s, l);
+    hipLaunchKernelGGL(k_ln_bwd<false>, dim3(np, l.nC), dim3(256), 0, s, l);
+  if (l.ws) {  // gamma / beta gradients: the row blocks' partials in block order
+    partial_sum(l.ws, np, l.nC, 64, 128, l.dgamma, l.sPc, s);
+    partial_sum(l.ws + 64, np, l.nC, 64, 128, l.dbeta, l.sPc, s);
+  }
   return launched();
 }
+
+long afl_ln_bwd_ws_floats(int rows, int nC) { return (long)((rows + LNB_ROWS - 1) / LNB_ROWS) * nC * 128; }
 
 int afl_gru_fwd(const float* gi, const float* bhh, long sPc, int C, int B, float* h, long sHc, long sHr, int col0,
                 hipStream_t s) {
@@ -1173,12 +1252,18 @@ int afl_conv_pe_fwd(const float* x, int C, int B, int L, const float* params, lo
 }
 
 int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float* grads, long P, int w_off, int b_off,
-                    hipStream_t s) {
+                    hipStream_t s, float* ws) {
   if (((uintptr_t)dh & 15) != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_conv_pe_bwd, dim3((unsigned)(((long)B * L + 1023) / 1024), C), dim3(256), 0, s, x, dh, C, B, L,
-                     grads, P, w_off, b_off);
+  const int np = (int)(((long)B * L + 1023) / 1024);
+  hipLaunchKernelGGL(k_conv_pe_bwd, dim3((unsigned)np, C), dim3(256), 0, s, x, dh, C, B, L, grads, P, w_off, b_off, ws);
+  if (ws) {  // the stem's tap / bias gradients: row blocks' partials in block order
+    partial_sum(ws, np, C, 192, 256, grads + w_off, P, s);
+    partial_sum(ws + 192, np, C, 64, 256, grads + b_off, P, s);
+  }
   return launched();
 }
+
+long afl_conv_pe_bwd_ws_floats(int C, int B, int L) { return (((long)B * L + 1023) / 1024) * C * 256; }
 
 int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s) {
   if ((((uintptr_t)h | (uintptr_t)out) & 15) != 0) return (int)hipErrorInvalidValue;

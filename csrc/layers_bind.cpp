@@ -110,11 +110,16 @@ void bgemm(torch::Tensor A, torch::Tensor B, torch::Tensor Cm, c10::optional<tor
   }
   // split-K: deterministic (ordered partial sums) — the workspace lives in the caching allocator, stream-ordered
   // (inside a captured step it comes from the graph's private pool)
-  torch::Tensor ws;
+  torch::Tensor ws, ws_sum;
   const long nws = afl_bgemm_ws_floats(g);
   if (nws > 0) {
     ws = torch::empty({nws}, A.options());
     g.ws = ws.data_ptr<float>();
+  }
+  const long nsum = afl_bgemm_asum_ws_floats(g);  // the fused bias-gradient column sums: ordered partials
+  if (nsum > 0) {
+    ws_sum = torch::empty({nsum}, A.options());
+    g.ws_sum = ws_sum.data_ptr<float>();
   }
   ok(afl_bgemm(g, cur()), "bgemm");
 }
@@ -125,8 +130,9 @@ void colsum(torch::Tensor Y, torch::Tensor out) {
   TORCH_CHECK(Y.stride(2) == 1, "Y columns must be contiguous");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == Y.size(0) && out.size(1) == Y.size(2) && out.stride(1) == 1,
               "out must be a [C, N] view");
+  auto ws = torch::empty({afl_colsum_ws_floats(Y.size(1), Y.size(2), Y.size(0))}, Y.options());  // ordered partials
   ok(afl_colsum(Y.data_ptr<float>(), Y.stride(0), Y.stride(1), Y.size(1), Y.size(2), Y.size(0), out.data_ptr<float>(),
-                out.stride(0), cur()),
+                out.stride(0), cur(), ws.data_ptr<float>()),
      "colsum");
 }
 
@@ -488,6 +494,8 @@ void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor stats, torch::Tenso
   l.rows = dy.size(1); l.nC = dy.size(0);
   l.da_drop = make_drop(seeds, stepctl, layer_a, p_a);
   l.dout = make_drop(seeds, stepctl, layer_o, p_o);
+  auto ws = torch::empty({afl_ln_bwd_ws_floats(l.rows, l.nC)}, dy.options());  // gamma / beta: ordered partials
+  l.ws = ws.data_ptr<float>();
   ok(afl_ln_bwd(l, cur()), "ln_bwd");
 }
 
@@ -589,8 +597,9 @@ void conv_pe_bwd(torch::Tensor x, torch::Tensor dh, torch::Tensor grads, int64_t
   dense(dh, "dh");
   dense(grads, "grads");
   const int C = x.size(0), B = x.size(1), L = x.size(2);
+  auto ws = torch::empty({afl_conv_pe_bwd_ws_floats(C, B, L)}, x.options());  // ordered partials
   ok(afl_conv_pe_bwd(x.data_ptr<float>(), dh.data_ptr<float>(), C, B, L, grads.data_ptr<float>(), grads.size(1), w_off,
-                     b_off, cur()),
+                     b_off, cur(), ws.data_ptr<float>()),
      "conv_pe_bwd");
 }
 

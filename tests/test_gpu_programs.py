@@ -326,12 +326,15 @@ def test_splitk_gemm_is_deterministic(gpu):
     _close(outs[0], torch.bmm(dY.cpu().transpose(1, 2), X.cpu()), name="splitk")
 
 
-def test_cnn_training_is_bit_reproducible(gpu):
-    """CNNModel: two graph-replayed training runs from the same state give the same parameters bit for bit
-    (the split-K fc1 GEMM, the conv weight gradients and the head's bias sums reduce in a fixed order), and
-    so does client 1 trained ALONE vs beside clients 0 and 2 (placement-independent: the multi-rank claim)."""
-    name, B, n, E, C = "CNNModel", 128, 1000, 2, 3
-    ds = synthetic_icu(n)
+@pytest.mark.parametrize("name,B,n,E", [("CNNModel", 128, 1000, 2), ("TransformerClassifier", 16, 80, 1),
+                                        ("RNNModel", 128, 1000, 2)])
+def test_program_training_is_bit_reproducible(gpu, name, B, n, E):
+    """Two graph-replayed training runs from the same state give the same parameters bit for bit (split-K
+    GEMMs, conv / stem weight gradients, LayerNorm gamma / beta, bias column sums and the CNN head's sums all
+    reduce in a fixed order), and so does client 1 trained ALONE vs beside clients 0 and 2
+    (placement-independent: the multi-rank claim)."""
+    C = 3
+    ds = synthetic_har(n) if name == "TransformerClassifier" else synthetic_icu(n)
     nd = [n // 2, n // 2 - 17, n // 3 + 1]
     order = torch.stack([torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(10 * c + e))[:max(nd)]
                                       for e in range(E)]) for c in range(C)]).to(torch.int32)
