@@ -427,6 +427,15 @@ class ProgramRunner:
         if max_steps is not None:
             S = min(S, max_steps)
         ctl = StepCtl.create(seeds, dev, min_bs=1 if compat_har else 2, nan_abort=not compat_har)
+        out_params = params
+        if params.is_cuda and P % 16:
+            # train in a copy whose client rows start 64-byte aligned (P is odd for every model here, so every
+            # client's weight views but client 0's were 4-byte aligned only: the GEMM operand loads fell back to
+            # scalar).  The padding columns get zero gradients, so Adam leaves them at zero.
+            Pp = (P + 15) // 16 * 16
+            params = torch.zeros(C, Pp, device=dev)
+            params[:, :P].copy_(out_params)
+            P = Pp
         grads = torch.zeros(C, P, device=dev)
         m = torch.zeros(C, P, device=dev)
         v = torch.zeros(C, P, device=dev)
@@ -469,10 +478,12 @@ class ProgramRunner:
                 # capture recorded without executing; the counter still points at step 1
                 for _ in range(S - 1):
                     g.replay()
-                self._live = (g, grads, m, v, tcount)  # replays may still be running when sync=False
+                self._live = (g, grads, m, v, tcount, params)  # replays may still run when sync=False
             else:
                 for _ in range(S - 1):
                     step()
+        if params is not out_params:  # (stream-ordered behind the replays)
+            out_params.copy_(params[:, :out_params.shape[1]])
         if not sync:
             return failed, losses
         return (failed == 0).cpu(), losses.double().cpu()
