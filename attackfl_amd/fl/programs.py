@@ -368,6 +368,7 @@ class HARProgram(_Program):
 
 
 PROGRAMS = {"CNNModel": CNNProgram, "RNNModel": RNNProgram, "TransformerClassifier": HARProgram}
+CNN2_TIMEOUT = "cnn2 trainer: a cross-workgroup wait timed out (workgroups not co-resident?)"
 
 
 # ================================================================================== step tables
@@ -427,6 +428,8 @@ class ProgramRunner:
         if max_steps is not None:
             S = min(S, max_steps)
         ctl = StepCtl.create(seeds, dev, min_bs=1 if compat_har else 2, nan_abort=not compat_har)
+        if self._onchip_cnn(params, sgd_lr, max_steps):
+            return self._train_cnn2(table, params, plan, lr, ctl, (idx, bsz, ep, nb, S), sync)
         out_params = params
         if params.is_cuda and P % 16:
             # train in a copy whose client rows start 64-byte aligned (P is odd for every model here, so every
@@ -487,6 +490,49 @@ class ProgramRunner:
         if not sync:
             return failed, losses
         return (failed == 0).cpu(), losses.double().cpu()
+
+    # ---- CNNModel on-chip trainer (csrc/kernels/cnn2.hip) ------------------------------------------------
+    def _onchip_cnn(self, params: torch.Tensor, sgd_lr: float, max_steps) -> bool:
+        """One persistent launch per round instead of a graph replay per step: CNNModel on a GPU with Adam
+        (the SGD gradient hook and step caps stay on the layer program), all 25 workgroups of every client
+        co-resident (one per CU).  ``AFL_CNN2=0`` forces the layer program."""
+        pg = self.prog
+        if pg.model_name != "CNNModel" or not params.is_cuda or not pg.train or sgd_lr > 0.0 or max_steps is not None:
+            return False
+        if os.environ.get("AFL_CNN2", "1") == "0" or pg.B > 128 or params.dtype != torch.float32:
+            return False
+        from .. import ops
+
+        nat = ops.native()
+        cus = torch.cuda.get_device_properties(params.device).multi_processor_count
+        return params.shape[0] * int(nat.cnn2_wgs_per_client()) <= cus
+
+    def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync):
+        from .. import ops
+
+        nat = ops.native()
+        pg = self.prog
+        C = params.shape[0]
+        idx, bsz, ep, nb, S = tables
+        dev = params.device
+        if getattr(self, "_cnn2_ws", None) is None or self._cnn2_ws[0].numel() < C * int(nat.cnn2_ws_bytes()):
+            self._cnn2_ws = (torch.empty(C * int(nat.cnn2_ws_bytes()), dtype=torch.uint8, device=dev),
+                             torch.zeros(C * int(nat.cnn2_ctr_words()), dtype=torch.int32, device=dev))
+        ws, ctr = self._cnn2_ws
+        failed = torch.zeros(C, dtype=torch.int32, device=dev)
+        losses = torch.zeros(C, plan.epochs, device=dev)
+        if S > 0:
+            ctr.zero_()
+            offs = [s.offset for s in pg.layout.slots]
+            nat.cnn2_train(params if params.is_contiguous() else params.contiguous(), offs, table.rows, idx, bsz, ep, nb,
+                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr)
+            self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params)  # the launch may still run when sync=False
+        if not sync:
+            return failed, losses  # failed: 1 = NaN loss, 2 = a cross-workgroup wait timed out (GraphTrainer raises)
+        fh = failed.cpu()
+        if bool((fh == 2).any()):
+            raise RuntimeError(CNN2_TIMEOUT)
+        return (fh == 0), losses.double().cpu()
 
     @torch.no_grad()
     def predict(self, params: torch.Tensor, data: torch.Tensor) -> torch.Tensor:

@@ -430,7 +430,10 @@ class GraphTrainer:
                                         compat_har=self.compat_har and self.table.kind == "HAR")
 
         def fin():
-            okh, lh = (ok == 0).cpu(), losses.double().cpu()
+            fh = ok.cpu()
+            if bool((fh == 2).any()):
+                raise RuntimeError(self.programs.CNN2_TIMEOUT)
+            okh, lh = (fh == 0), losses.double().cpu()
             if self.verbose:
                 for c in range(C):
                     for e in range(plan.epochs):

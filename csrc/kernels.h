@@ -180,6 +180,32 @@ struct AflCnnTowers {
   const float *W2h, *W3h;            // optional head fc2 / fc3 weights (client-0 views): images for k_cnn_head
 };
 long afl_cnn_wimg_ushorts(int C);
+// cnn2.hip: CNNModel on-chip trainer (one launch per round; 25 workgroups per client, one per CU)
+struct AflCnn2Args {
+  float* params;         // [C][pstride] fp32 arena, trained in place
+  long pstride;
+  int off[20];           // CNNModel state_dict slot offsets (ParamLayout order)
+  const float* rows;     // ICU table [N][24]
+  const int* idx;        // [S][C][B] batch rows (-1 = padding)
+  const int* bsz;        // [S][C]
+  const int* epoch;      // [S][C]
+  const int* nb;         // [C] batches per epoch (loss divisor)
+  const uint32_t* seeds; // [C] dropout seeds (StepCtl)
+  int S, C, B, E;
+  uint32_t thr16;        // dropout threshold (0 = off), keep scale
+  float inv_keep;
+  int min_bs, nan_abort;
+  float lr;
+  int* failed;           // [C] out: 1 = NaN loss
+  float* losses;         // [C][E] accumulated epoch losses (zeroed by the caller)
+  void* ws;              // [C][ws_stride] bytes workspace (afl_cnn2_ws_bytes)
+  long ws_stride;
+  uint32_t* ctr;         // [C][afl_cnn2_ctr_words] zeroed counters
+};
+long afl_cnn2_ws_bytes();
+int afl_cnn2_ctr_words();
+int afl_cnn2_wgs_per_client();
+int afl_cnn2_train(const AflCnn2Args& a, hipStream_t s);
 int afl_cnn_towers_fwd(const AflCnnTowers& a, hipStream_t s);
 int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s);
 struct AflConvDwJob {

@@ -1,0 +1,1300 @@
+// CNNModel on-chip trainer: ONE launch trains every local client for its whole local round (all epochs,
+// forward, backward, Adam) — the CNN counterpart of tf2.hip / rnn2.hip.  Reference model: src/Model.py:27-88
+// (two Conv1d(1->32->64->128, k3, p1) + ReLU towers over vitals[7] / labs[16], AdaptiveAvgPool1d(4),
+// Dropout(0.3), fc1 1024->128 -> fc2 64 -> fc3 32 -> output 1, sigmoid-BCE); trainer semantics
+// client.py:66-112 (fresh Adam per round, size-1 batches skipped, NaN loss aborts the client).
+//
+// Replaces the per-step HIP-graph replay of ~14 launches (cnn.hip + layers.hip, ~160 us per step, a third
+// of it launch floors) with a persistent cell of 25 workgroups per client, one per CU:
+//
+//   tower workgroups (8 vitals x 16 rows, 16 labs x 8 rows): the rows of a batch, both directions.
+//     Activations live in LDS as bf16 in a "padded-row" layout — every sample's L positions framed by a
+//     zero row on each side (L + 2 = 9 / 18 rows, 144 rows per workgroup in both towers) — so a k=3 conv is
+//     three row-SHIFTED MFMA GEMMs (no im2col / col2im buffers): h_out = sum_j shift_{j-1}(h_in) . W_j^T,
+//     d_in = sum_j shift_{1-j}(d_out) . W_j, dW_j = d_out^T . shift_{j-1}(h_in).  The pad rows make the
+//     sample boundaries exact zeros.  The workgroup also computes its rows' fc1 pre-activation partial over
+//     its tower's 512 concat features (z1p) and, in backward, its rows' d(concat) = d1 . W1.
+//   the head workgroup: fc1 bias + ReLU on z1 = z1p_vitals + z1p_labs (fixed order), fc2 / fc3 / output,
+//     BCE + NaN abort + epoch loss, the whole head backward (d1), Adam of fc2 / fc3 / output / fc1-bias
+//     with p, m, v held in registers for the round.
+//   ownership (ZeRO-style, all state in registers for the round): tower workgroup i owns 1/NTW of its
+//     tower's conv parameters (output-channel blocks of 8) and a column block of fc1; it reduces the
+//     tower's per-workgroup gradient partials for its block IN WORKGROUP ORDER (deterministic: no atomics),
+//     runs Adam, and republishes the block as bf16 MFMA operand images in both orientations.
+//
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): every handed-off byte is stored
+// with 16-byte sc1 (write-through) stores and loaded with sc1 loads; each storing wave drains vmcnt, the
+// workgroup barriers, one lane adds to an agent-scope counter; the consumer polls the counter with sc1
+// loads (+ s_sleep) and barriers.  Per step: towers -> head (z1p), head -> towers (d1), tower group
+// barrier after the partials, tower group barrier after the new images.  A client's 25 workgroups are
+// blockIdx c, c + C, c + 2C, ... (one XCD at C = 8 under round-robin placement: speed only).  Every wait
+// has a wall-clock deadline (s_memrealtime): a missing partner is an error, never a hang.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+#define GAS __attribute__((address_space(1)))
+typedef GAS uint32_t gu32;
+typedef unsigned char uchar;
+
+constexpr int NTH = 512;  // 8 waves
+constexpr int NWG = 25;   // workgroups per client: 8 vitals + 16 labs towers + head
+constexpr int WG_HEAD = 24;
+constexpr long DEADLINE = 200000000L;  // s_memrealtime ticks (100 MHz): 2 s per wait
+
+__device__ __forceinline__ f4v mfma(s8v a, s8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+constexpr f4v Z4 = {0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ unsigned short bfu(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
+__device__ __forceinline__ float bff(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }  // keeps NaN like torch
+__device__ __forceinline__ int bin_lo(int p, int L) { return (p * L) / 4; }
+__device__ __forceinline__ int bin_hi(int p, int L) { return ((p + 1) * L + 3) / 4; }
+
+// ---- LDS fragments ----
+// row-major [rows][ld] bf16: MFMA operand rows r0 + (lane & 15), k = k0 + 8 (lane >> 4) .. +7
+__device__ __forceinline__ s8v rfrag(const uchar* S, int ld, int r0, int k0, int lane) {
+  return *(const LDS_AS s8v*)(S + ((r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4)) * 2);
+}
+// transposed operand from a [k rows][m cols] bf16 image (ds_read_b64_tr_b16): A[m][k] = S[k][m]
+__device__ __forceinline__ s8v cfrag(const uchar* S, int ld, int k0, int m0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const uchar* a1 = S + ((k0 + 8 * g + q) * ld + m0 + 4 * p) * 2;
+  const s4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)a1);
+  const s4v r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)(a1 + 4 * ld * 2));
+  s8v r;
+  r[0] = r1[0]; r[1] = r1[1]; r[2] = r1[2]; r[3] = r1[3];
+  r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
+  return r;
+}
+__device__ __forceinline__ LDS_AS unsigned short* lu16(uchar* S, int byte_off) {
+  return (LDS_AS unsigned short*)(S + byte_off);
+}
+__device__ __forceinline__ LDS_AS float* lf(uchar* S, int byte_off) { return (LDS_AS float*)(S + byte_off); }
+
+// ---- global hand-off memory: 16-byte sc1 (write-through) stores / sc1 loads through a buffer resource ----
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+// a 16-byte vector-memory store reads its data VGPRs after issue: a VALU write to them in the next cycle can
+// land in the stored data (onchip.h store_guard); every b128 store is followed by this pinned s_nop
+__device__ __forceinline__ void sguard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t rs, int byte_off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, byte_off, 0, 16);
+  sguard();
+}
+__device__ __forceinline__ void st16f(__amdgpu_buffer_rsrc_t rs, int byte_off, f4v v) {
+  st16(rs, byte_off, __builtin_bit_cast(u32x4, v));
+}
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16);
+}
+__device__ __forceinline__ f4v ld16f(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f4v, ld16(rs, byte_off));
+}
+__device__ __forceinline__ s8v ld16s(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(s8v, ld16(rs, byte_off));
+}
+// Phase entry: the lane / wave indices become opaque, so every per-lane address of a phase is computed inside
+// it (otherwise the compiler hoists the hundreds of swizzled LDS / image addresses of the step out of the loop
+// and keeps them live across all phases, spilling to scratch)
+#define REOPQ()                                   \
+  do {                                            \
+    __builtin_amdgcn_sched_barrier(0);            \
+    asm volatile("" : "+v"(lane));                \
+    wave = __builtin_amdgcn_readfirstlane(wave);  \
+    asm volatile("" : "+s"(wave));                \
+    lane &= 63;                                   \
+    wave &= 7;                                    \
+    tid = wave * 64 + lane;                       \
+    g = lane >> 4;                                \
+    li = lane & 15;                               \
+  } while (0)
+#define SYNC()        \
+  do {                \
+    __syncthreads();  \
+    REOPQ();          \
+  } while (0)
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---- per-client workspace (bytes from the client's base) ----
+// images: per tower [W2 3x64x32 | W3 3x128x64 | W2T 3x32x64 | W3T 3x64x128] bf16, then fc1 W1 [128][1024] and
+// W1T [1024][128] bf16
+constexpr int IM_W2 = 0, IM_W3 = 6144, IM_W2T = 30720, IM_W3T = 36864, IM_TOWER = 61440;  // ushorts
+constexpr int IM_W1 = 2 * IM_TOWER, IM_W1T = IM_W1 + 131072, IM_END = IM_W1T + 131072;
+constexpr int WS_IMG = 0;
+constexpr int WS_SMALL = WS_IMG + IM_END * 2;              // [2][320] fp32: conv1 W (96) | b1 (32) | b2 (64) | b3 (128)
+constexpr int NSMALL = 320;
+constexpr int WS_FEAT = WS_SMALL + 2 * NSMALL * 4;         // [128][1024] bf16 concat features
+constexpr int WS_Z1P = WS_FEAT + 128 * 1024 * 2;           // [2][128][128] fp32 fc1 partials per tower
+constexpr int WS_D1 = WS_Z1P + 2 * 128 * 128 * 4;          // [128][128] bf16 d(fc1 pre-activation)
+constexpr int WS_STAT = WS_D1 + 128 * 128 * 2;             // 16 B: head status of the step
+constexpr int PSZ = 24576 + 6144 + NSMALL;                 // one tower workgroup's gradient partial (floats)
+constexpr int P_W3 = 0, P_W2 = 24576, P_SM = 24576 + 6144; // [3][64][128] | [3][32][64] | smalls, (ci, o) o-contiguous
+constexpr int WS_PART = WS_STAT + 16;                      // [24][PSZ] fp32 (vitals 0..7, labs 8..23)
+constexpr int WS_MV = WS_PART + 24 * PSZ * 4;              // [25 workgroups][8 slots][512 threads] {m f4, v f4}
+constexpr int MV_WG = 8 * 512 * 32;
+constexpr long WS_BYTES = WS_MV + 25L * MV_WG;
+// counters per client: F (towers -> head), H (head -> towers), P0/P1 (partials), W0/W1 (images), TMO
+constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_N = 8;  // x 32 words (own 128-B lines)
+
+struct Ctx {
+  const AflCnn2Args* a;
+  int c, tid, lane, wave, role;
+  uchar* smem;
+  uchar* wsb;                  // client workspace base (generic pointer for the buffer resources)
+  __amdgpu_buffer_rsrc_t rw;   // client workspace
+  gu32* ctr;                   // client counters
+};
+
+__device__ __forceinline__ void arrive(const Ctx& x, int which) {
+  drain();
+  __syncthreads();
+  if (x.tid == 0) __hip_atomic_fetch_add(x.ctr + which * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// true when the counter reached `target`; false (all threads) on the deadline
+__device__ __forceinline__ bool wait_ge(const Ctx& x, int which, uint32_t target, int flag_off) {
+  LDS_AS int* fl = (LDS_AS int*)(x.smem + flag_off);
+  if (x.tid == 0) {
+    int ok = 1;
+    const long t0 = (long)__builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(x.ctr + which * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if ((long)__builtin_amdgcn_s_memrealtime() - t0 > DEADLINE) {
+        ok = 0;
+        __hip_atomic_store(x.ctr + CT_TMO * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x.a->failed[x.c] = 2;  // the host raises on 2 (a NaN loss is 1)
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    fl[0] = ok;
+  }
+  __syncthreads();
+  const int ok = fl[0];
+  __syncthreads();  // fl is rewritten by the next wait
+  return ok != 0;
+}
+
+// Adam moments of this thread's slot k (private to the thread: written and read back by it alone)
+__device__ __forceinline__ int mv_off(const Ctx& x, int k) { return WS_MV + x.role * MV_WG + (k * 512 + x.tid) * 32; }
+__device__ __forceinline__ void mv_ld(const Ctx& x, int k, f4v& m, f4v& v) {
+  m = ld16f(x.rw, mv_off(x, k));
+  v = ld16f(x.rw, mv_off(x, k) + 16);
+}
+__device__ __forceinline__ void mv_st(const Ctx& x, int k, f4v m, f4v v) {
+  st16f(x.rw, mv_off(x, k), m);
+  st16f(x.rw, mv_off(x, k) + 16, v);
+}
+
+// the reference Adam step (k_adam_clients / torch.optim.Adam defaults) with bias corrections a, sb of step t
+__device__ __forceinline__ float adam1(float p, float& m, float& v, float g, float a, float sb) {
+  m = m + 0.1f * (g - m);
+  v = 0.999f * v + 0.001f * g * g;
+  return p - a * m / (sqrtf(v) / sb + 1e-8f);
+}
+struct AdamT {
+  float a, sb;
+};
+__device__ __forceinline__ AdamT adam_t(float lr, int t) {
+  const float tt = (float)t;
+  return AdamT{lr / (1.f - powf(0.9f, tt)), sqrtf(1.f - powf(0.999f, tt))};
+}
+
+// ============================================================================================ towers
+template <int T>
+struct TW {
+  static constexpr int L = T == 0 ? 7 : 16, R = T == 0 ? 16 : 8, NTW = T == 0 ? 8 : 16, LP = L + 2;
+  static constexpr int COL0 = T == 0 ? 0 : 512, XOFF = T == 0 ? 0 : 7, NC = T == 0 ? 64 : 32, FIRST = T == 0 ? 0 : 8;
+  static constexpr int NS = T == 0 ? 3 : 2;  // owner chunk slots per thread
+  static_assert(R * LP == 144, "144 padded rows per tower workgroup");
+};
+constexpr int NR = 162;  // LDS rows: padded row q at row q + 1; rows 0 and 145..161 stay zero
+constexpr int LD1 = 40, LD2 = 72, LD3 = 136, LDF = 520, LDZ = 132, LDD = 136;
+constexpr int O_H1 = 0;
+constexpr int O_H2 = O_H1 + NR * LD1 * 2;
+constexpr int O_H3 = O_H2 + NR * LD2 * 2;   // h3, then d(h3) in place
+constexpr int O_DH2 = O_H3 + NR * LD3 * 2;
+constexpr int O_XS = O_DH2 + NR * LD2 * 2;  // fp32 x per padded row
+constexpr int O_FT = O_XS + 656;            // feat bf16 [16][520] | z1p staging f32 [16][132] ; dfeat f32 [16][516]
+constexpr int O_ZS = O_FT + 16 * LDF * 2;
+constexpr int O_D1R = O_FT + 16 * 516 * 4;  // own d1 rows bf16 [16][136]
+constexpr int O_RED = O_D1R + 16 * LDD * 2; // reductions (8 KB)
+constexpr int O_FLAG = O_RED + 8192;
+constexpr int T_LDS = O_FLAG + 16;
+static_assert(O_ZS + 16 * LDZ * 4 <= O_D1R, "z1p staging");
+// owner-phase staging (dead activation regions after the backward)
+constexpr int O_S3 = 0, O_S2 = 6144, O_D1F = 8192, O_FW = O_D1F + 128 * LDD * 2, O_SW = O_FW + 128 * 72 * 2;
+static_assert(O_SW + 128 * 72 * 2 <= O_XS, "owner staging");
+// reduction slots (floats from O_RED)
+constexpr int R_DB2 = 0, R_DB3 = 128, R_C1 = 128 + 512, R_SM = 128 + 512 + 512;  // [8][16] | [4][128] | [8][16][4] | [320]
+
+__device__ __forceinline__ bool valid_q(int q, int LP) {
+  const int l = q % LP;
+  return q < 144 && l != 0 && l != LP - 1;
+}
+
+template <int T>
+struct TowerState {
+  // owned conv chunks (4 elements each; moments in slab slots 0..NS-1) and fc1 block elements (slots 4..)
+  float p[TW<T>::NS][4];
+  float p1[TW<T>::NC / 16][4];
+};
+
+// owned chunk u -> kind (0 none, 3 W3, 2 W2, 1 small), partial float offset, param element base (+ stride)
+struct Chunk {
+  int kind, poff, j, ci, o0, s0;
+};
+template <int T>
+__device__ __forceinline__ Chunk chunk_of(int i, int cid) {
+  Chunk k{0, 0, 0, 0, 0, 0};
+  int lo;
+  if (T == 0) {
+    if (cid < 768) {
+      const int bk = 2 * i + cid / 384;
+      lo = cid % 384;
+      k.kind = 3; k.j = lo / 128; k.ci = (lo % 128) >> 1; k.o0 = 8 * bk + 4 * (lo & 1);
+    } else if (cid < 960) {
+      lo = cid - 768;
+      k.kind = 2; k.j = lo / 64; k.ci = (lo % 64) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
+    } else if (cid < 1040 && i == 0) {
+      k.kind = 1; k.s0 = 4 * (cid - 960);
+    }
+  } else {
+    if (cid < 384) {
+      lo = cid;
+      k.kind = 3; k.j = lo / 128; k.ci = (lo % 128) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
+    } else if (cid < 576 && i < 8) {
+      lo = cid - 384;
+      k.kind = 2; k.j = lo / 64; k.ci = (lo % 64) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
+    } else if (cid < 464 && i == 15) {
+      k.kind = 1; k.s0 = 4 * (cid - 384);
+    }
+  }
+  if (k.kind == 3) k.poff = P_W3 + (k.j * 64 + k.ci) * 128 + k.o0;
+  if (k.kind == 2) k.poff = P_W2 + (k.j * 32 + k.ci) * 64 + k.o0;
+  if (k.kind == 1) k.poff = P_SM + k.s0;
+  return k;
+}
+// arena index of element e of a chunk
+template <int T>
+__device__ __forceinline__ int elem_idx(const AflCnn2Args& a, const Chunk& k, int e) {
+  const int* of = a.off + 6 * T;  // conv1 w, conv1 b, conv2 w, conv2 b, conv3 w, conv3 b
+  if (k.kind == 3) return of[4] + ((k.o0 + e) * 64 + k.ci) * 3 + k.j;
+  if (k.kind == 2) return of[2] + ((k.o0 + e) * 32 + k.ci) * 3 + k.j;
+  const int s = k.s0 + e;
+  if (s < 96) return of[0] + s;
+  if (s < 128) return of[1] + s - 96;
+  if (s < 192) return of[3] + s - 128;
+  return of[5] + s - 192;
+}
+
+// publish the owned conv blocks (bf16 images in both orientations) and smalls (fp32) from the owner state
+template <int T>
+__device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerState<T>& st) {
+  using C = TW<T>;
+  uchar* S = x.smem;
+  const int tw = T * IM_TOWER;
+  // stage: S3 [blk][j][ci][8 o], S2 [j][ci][8 o]
+#pragma unroll
+  for (int u = 0; u < C::NS; ++u) {
+    const Chunk k = chunk_of<T>(i, x.tid + NTH * u);
+    if (k.kind == 3) {
+      const int blk = T == 0 ? ((k.o0 >> 3) - 2 * i) : 0;
+      *(LDS_AS uint32_t*)(S + O_S3 + ((blk * 192 + k.j * 64 + k.ci) * 8 + (k.o0 & 7)) * 2) = pk2(st.p[u][0], st.p[u][1]);
+      *(LDS_AS uint32_t*)(S + O_S3 + ((blk * 192 + k.j * 64 + k.ci) * 8 + (k.o0 & 7) + 2) * 2) = pk2(st.p[u][2], st.p[u][3]);
+    } else if (k.kind == 2) {
+      *(LDS_AS uint32_t*)(S + O_S2 + ((k.j * 32 + k.ci) * 8 + (k.o0 & 7)) * 2) = pk2(st.p[u][0], st.p[u][1]);
+      *(LDS_AS uint32_t*)(S + O_S2 + ((k.j * 32 + k.ci) * 8 + (k.o0 & 7) + 2) * 2) = pk2(st.p[u][2], st.p[u][3]);
+    } else if (k.kind == 1) {
+      st16f(x.rw, WS_SMALL + (T * NSMALL + k.s0) * 4, f4v{st.p[u][0], st.p[u][1], st.p[u][2], st.p[u][3]});
+    }
+  }
+  __syncthreads();
+  constexpr int NB3 = T == 0 ? 2 : 1;
+  const bool has2 = T == 0 || i < 8;
+  // W3T [j][ci][o]: one 16-B piece (8 o) per (blk, j, ci); W3 [j][o][ci]: 8 pieces (64 ci) per (blk, j, o)
+  for (int e = x.tid; e < NB3 * 192 * 2; e += NTH) {
+    const int blk = e / 384, r = e % 384;
+    const int b3 = T == 0 ? 2 * i + blk : i;
+    if (r < 192) {
+      const int j = r / 64, ci = r % 64;
+      const u32x4 v = *(const LDS_AS u32x4*)(S + O_S3 + (blk * 192 + j * 64 + ci) * 16);
+      st16(x.rw, WS_IMG + (tw + IM_W3T + (j * 64 + ci) * 128 + 8 * b3) * 2, v);
+    } else {
+      const int q = r - 192, j = q / 64, o = (q % 64) >> 3, cc = q & 7;  // 8 o x 8 pieces per j
+      uint32_t w[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int ci = 8 * cc + 2 * h;
+        const unsigned short lo = *lu16(S, O_S3 + ((blk * 192 + j * 64 + ci) * 8 + o) * 2);
+        const unsigned short hi = *lu16(S, O_S3 + ((blk * 192 + j * 64 + ci + 1) * 8 + o) * 2);
+        w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
+      }
+      st16(x.rw, WS_IMG + (tw + IM_W3 + (j * 128 + 8 * b3 + o) * 64 + 8 * cc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+    }
+  }
+  if (has2) {
+    const int b2 = i;
+    for (int e = x.tid; e < 96 * 2; e += NTH) {
+      if (e < 96) {
+        const int j = e / 32, ci = e % 32;
+        const u32x4 v = *(const LDS_AS u32x4*)(S + O_S2 + (j * 32 + ci) * 16);
+        st16(x.rw, WS_IMG + (tw + IM_W2T + (j * 32 + ci) * 64 + 8 * b2) * 2, v);
+      } else {
+        const int q = e - 96, j = q / 32, o = (q % 32) >> 2, cc = q & 3;  // 8 o x 4 pieces per j
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int ci = 8 * cc + 2 * h;
+          const unsigned short lo = *lu16(S, O_S2 + ((j * 32 + ci) * 8 + o) * 2);
+          const unsigned short hi = *lu16(S, O_S2 + ((j * 32 + ci + 1) * 8 + o) * 2);
+          w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
+        }
+        st16(x.rw, WS_IMG + (tw + IM_W2 + (j * 64 + 8 * b2 + o) * 32 + 8 * cc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+      }
+    }
+  }
+}
+
+// fc1 column block of this owner: [128 n][NC cols]; lane element (tile t, e) = (n = 16 w + 4 g + e, col 16 t + i)
+template <int T>
+__device__ __forceinline__ void publish_fc1(const Ctx& x, int i, const TowerState<T>& st) {
+  using C = TW<T>;
+  uchar* S = x.smem;
+  const int g = x.lane >> 4, li = x.lane & 15;
+  constexpr int NT1 = C::NC / 16, LW = C::NC + 8;
+#pragma unroll
+  for (int t = 0; t < NT1; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *lu16(S, O_SW + ((16 * x.wave + 4 * g + e) * LW + 16 * t + li) * 2) = bfu(st.p1[t][e]);
+  __syncthreads();
+  const int c0 = C::COL0 + i * C::NC;
+  constexpr int PR = C::NC / 8;  // 16-B pieces per W1 row segment
+  for (int e = x.tid; e < 128 * PR; e += NTH) {
+    const int n = e / PR, pc = e % PR;
+    const u32x4 v = *(const LDS_AS u32x4*)(S + O_SW + (n * LW + 8 * pc) * 2);
+    st16(x.rw, WS_IMG + (IM_W1 + n * 1024 + c0 + 8 * pc) * 2, v);
+  }
+  for (int e = x.tid; e < C::NC * 16; e += NTH) {  // W1T [col][n]: 16 pieces of 8 n per column
+    const int col = e >> 4, pc = e & 15;
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const unsigned short lo = *lu16(S, O_SW + ((8 * pc + 2 * h) * LW + col) * 2);
+      const unsigned short hi = *lu16(S, O_SW + ((8 * pc + 2 * h + 1) * LW + col) * 2);
+      w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
+    }
+    st16(x.rw, WS_IMG + (IM_W1T + (c0 + col) * 128 + 8 * pc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void tower(const Ctx& x, int i) {
+  using C = TW<T>;
+  const AflCnn2Args& a = *x.a;
+  uchar* S = x.smem;
+  int tid = x.tid, lane = x.lane, wave = x.wave, g = lane >> 4, li = lane & 15;
+  const int c = x.c, B = a.B;
+  const int b0 = i * C::R;
+  float* P = a.params + (long)c * a.pstride;
+  const int tw = T * IM_TOWER;
+  const int pbase = WS_PART + (C::FIRST + i) * PSZ * 4;  // this workgroup's partial (bytes)
+  TowerState<T> st;
+  // ---------------------------------------------------------------- init: zero LDS, owned state, images
+  for (int e = tid; e < T_LDS / 16; e += NTH) *(LDS_AS u32x4*)(S + 16 * e) = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int u = 0; u < C::NS; ++u) {
+    const Chunk k = chunk_of<T>(i, tid + NTH * u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      st.p[u][e] = k.kind ? P[elem_idx<T>(a, k, e)] : 0.f;
+    }
+    mv_st(x, u, Z4, Z4);
+  }
+  const int c0w = C::COL0 + i * C::NC;
+#pragma unroll
+  for (int t = 0; t < C::NC / 16; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      st.p1[t][e] = P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0w + 16 * t + li];
+    }
+#pragma unroll
+  for (int t = 0; t < C::NC / 16; ++t) mv_st(x, 4 + t, Z4, Z4);
+  __syncthreads();
+  publish_conv<T>(x, i, st);
+  __syncthreads();
+  publish_fc1<T>(x, i, st);
+  arrive(x, CT_W + T);
+  __syncthreads();
+  // re-zero the staging the publishers used (rows 0.. of H1 / H2 / H3)
+  for (int e = tid; e < O_XS / 16; e += NTH) *(LDS_AS u32x4*)(S + 16 * e) = u32x4{0u, 0u, 0u, 0u};
+
+  const int min_bs = a.min_bs;
+  int kact = 0;
+  bool alive = true;
+  for (int s = 0; s < a.S && alive; ++s) {
+    const int bs = a.bsz[(long)s * a.C + c];
+    if (bs < min_bs || bs < 1) continue;
+    if (!wait_ge(x, CT_W + T, (uint32_t)(C::NTW * (kact + 1)), O_FLAG)) break;
+    REOPQ();
+    // ------------------------------------------------------------------------------ forward
+    // step inputs: x rows (plain loads: the table is read-only), conv1 weights / biases (fp32 smalls)
+    const int* idxs = a.idx + ((long)s * a.C + c) * B;
+    float xv = 0.f;
+    int xq = -1;
+    if (tid < C::R * C::L) {
+      const int r = tid / C::L, l = tid - r * C::L;
+      const int b = b0 + r;
+      const int row = b < B ? idxs[b] : -1;
+      xv = row >= 0 ? a.rows[(long)row * 24 + C::XOFF + l] : 0.f;
+      xq = r * C::LP + 1 + l;
+    }
+    const int o1 = tid & 31;
+    float w10, w11, w12, bb1;
+    {
+      // conv1 weight row o1 (3 floats at 3 o1) and bias: dword sc1 loads through the resource
+      const int base = WS_SMALL + (T * NSMALL) * 4;
+      w10 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, base + (3 * o1) * 4, 0, 16));
+      w11 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, base + (3 * o1 + 1) * 4, 0, 16));
+      w12 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, base + (3 * o1 + 2) * 4, 0, 16));
+      bb1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, base + (96 + o1) * 4, 0, 16));
+    }
+    // conv2 / conv3 B fragments (images) and biases
+    const int nt2 = wave & 3, mp2 = wave >> 2;
+    s8v w2f[3], w3f[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w2f[j] = ld16s(x.rw, WS_IMG + (tw + IM_W2 + (j * 64 + 16 * nt2 + li) * 32 + 8 * g) * 2);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      w3f[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3 + ((k >> 1) * 128 + 16 * wave + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
+    const float b2v = __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, WS_SMALL + (T * NSMALL + 128 + 16 * nt2 + li) * 4, 0, 16));
+    const float b3v = __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, WS_SMALL + (T * NSMALL + 192 + 16 * wave + li) * 4, 0, 16));
+    // boundary rows of the activation buffers back to zero (the owner phases stage through them)
+    for (int e = tid; e < 18 * 4; e += NTH) {
+      const int rr = e % 18, buf = e / 18;
+      const int row = rr == 0 ? 0 : 144 + rr;
+      const int off = buf == 0 ? O_H1 + row * LD1 * 2 : buf == 1 ? O_H2 + row * LD2 * 2 : buf == 2 ? O_H3 + row * LD3 * 2
+                                                                                                   : O_DH2 + row * LD2 * 2;
+      const int n16 = buf == 0 ? LD1 / 8 : buf == 2 ? LD3 / 8 : LD2 / 8;
+      for (int k = 0; k < n16; ++k) *(LDS_AS u32x4*)(S + off + 16 * k) = u32x4{0u, 0u, 0u, 0u};
+    }
+    if (xq >= 0) *lf(S, O_XS + (xq + 1) * 4) = xv;
+    SYNC();
+    // conv1 (1 -> 32) on VALU -> H1 (bf16), pads exact zeros
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int q = (tid >> 5) + 16 * u;
+      float h = 0.f;
+      if (valid_q(q, C::LP)) {
+        const float xm = *lf(S, O_XS + q * 4), x0 = *lf(S, O_XS + (q + 1) * 4), xp = *lf(S, O_XS + (q + 2) * 4);
+        h = relu(bb1 + w10 * xm + w11 * x0 + w12 * xp);
+      }
+      *lu16(S, O_H1 + ((q + 1) * LD1 + o1) * 2) = bfu(h);
+    }
+    SYNC();
+    // conv2: H2[q][o] = relu(b2 + sum_j H1[q - 1 + j] . W2_j^T); wave: n-tile nt2, m-tiles mp2, mp2 + 2, ...
+    for (int mt = mp2; mt < 9; mt += 2) {
+      f4v acc = Z4;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc = mfma(rfrag(S + O_H1, LD1, 16 * mt + j, 0, lane), w2f[j], acc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 16 * mt + 4 * g + e;
+        const float v = valid_q(q, C::LP) ? relu(acc[e] + b2v) : 0.f;
+        *lu16(S, O_H2 + ((q + 1) * LD2 + 16 * nt2 + li) * 2) = bfu(v);
+      }
+    }
+    SYNC();
+    // conv3: wave = n-tile, all 9 m-tiles
+#pragma unroll
+    for (int mt = 0; mt < 9; ++mt) {
+      f4v acc = Z4;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc = mfma(rfrag(S + O_H2, LD2, 16 * mt + (k >> 1), 32 * (k & 1), lane), w3f[k], acc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 16 * mt + 4 * g + e;
+        const float v = valid_q(q, C::LP) ? relu(acc[e] + b3v) : 0.f;
+        *lu16(S, O_H3 + ((q + 1) * LD3 + 16 * wave + li) * 2) = bfu(v);
+      }
+    }
+    // fc1 B fragments (this tower's half of W1, n-tile = wave), in flight during the pooling
+    s8v wf1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wf1[k] = ld16s(x.rw, WS_IMG + (IM_W1 + (16 * wave + li) * 1024 + C::COL0 + 32 * k + 8 * g) * 2);
+    SYNC();
+    // AdaptiveAvgPool1d(4) + dropout -> feat (LDS bf16 rows 0..15, zero past R) and the global concat
+    const bool dr = a.thr16 != 0;
+    const uint32_t key = dr ? afl_hash32(a.seeds[c], (uint32_t)s) : 0u;
+    for (int e = tid; e < 16 * 64; e += NTH) {  // (row r, channel pair cp): 8 concat columns
+      const int r = e >> 6, cp = e & 63;
+      float f[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = 2 * cp + h;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          float sum = 0.f;
+          if (r < C::R) {
+            const int lo = bin_lo(p, C::L), hi = bin_hi(p, C::L);
+            for (int l = lo; l < hi; ++l) sum += bff(*lu16(S, O_H3 + ((r * C::LP + 2 + l) * LD3 + ch) * 2));
+            sum /= (float)(hi - lo);
+            const int col = C::COL0 + ch * 4 + p;
+            if (dr) sum *= afl_keep(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)col, a.thr16) ? a.inv_keep : 0.f;
+          }
+          f[4 * h + p] = sum;
+        }
+      }
+      const u32x4 pkd = u32x4{pk2(f[0], f[1]), pk2(f[2], f[3]), pk2(f[4], f[5]), pk2(f[6], f[7])};
+      *(LDS_AS u32x4*)(S + O_FT + (r * LDF + 8 * cp) * 2) = pkd;
+      if (r < C::R) st16(x.rw, WS_FEAT + ((b0 + r) * 1024 + C::COL0 + 8 * cp) * 2, pkd);
+    }
+    SYNC();
+    // fc1 partial over this tower's 512 features: z1p[rows][n], wave = n-tile
+    {
+      f4v acc = Z4;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc = mfma(rfrag(S + O_FT, LDF, 0, 32 * k, lane), wf1[k], acc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *lf(S, O_ZS + ((4 * g + e) * LDZ + 16 * wave + li) * 4) = acc[e];
+    }
+    SYNC();
+    for (int e = tid; e < C::R * 32; e += NTH) {
+      const int r = e >> 5, pc = e & 31;
+      const f4v v = *(const LDS_AS f4v*)(S + O_ZS + (r * LDZ + 4 * pc) * 4);
+      st16f(x.rw, WS_Z1P + ((T * 128 + b0 + r) * 128 + 4 * pc) * 4, v);
+    }
+    arrive(x, CT_F);
+    REOPQ();
+    // d(concat) B fragments (W1T, this tower's columns: n-tiles 4 w .. 4 w + 3) in flight during the wait
+    s8v wt1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      wt1[k] = ld16s(x.rw, WS_IMG + (IM_W1T + (C::COL0 + 16 * (4 * wave + (k >> 2)) + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
+    // ------------------------------------------------------------------------------ backward
+    if (!wait_ge(x, CT_H, (uint32_t)(kact + 1), O_FLAG)) break;
+    REOPQ();
+    {
+      const u32x4 stt = ld16(x.rw, WS_STAT);
+      if (stt[0] != 0u) {  // NaN loss: the client's round ends here without an update (the head saw it too)
+        alive = false;
+        break;
+      }
+    }
+    // own d1 rows -> LDS (rows >= R zero)
+    if (tid < 16 * 16) {
+      const int r = tid >> 4, pc = tid & 15;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (r < C::R) v = ld16(x.rw, WS_D1 + ((b0 + r) * 128 + 8 * pc) * 2);
+      *(LDS_AS u32x4*)(S + O_D1R + (r * LDD + 8 * pc) * 2) = v;
+    }
+    SYNC();
+    // dfeat = d1 . W1[:, tower cols] -> f32 [16][516]
+    {
+      f4v acc[4] = {Z4, Z4, Z4, Z4};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const s8v af = rfrag(S + O_D1R, LDD, 0, 32 * k, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = mfma(af, wt1[4 * t + k], acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *lf(S, O_FT + ((4 * g + e) * 516 + 16 * (4 * wave + t) + li) * 4) = acc[t][e];
+    }
+    // W3T fragments of d(h2), in flight behind the pooling gradient
+    const int nb2 = wave & 3, mpb = wave >> 2;
+    s8v w3t[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      w3t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3T + ((k >> 2) * 64 + 16 * nb2 + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
+    SYNC();
+    // pooled gradient: gs[r][col] = dropout'(dfeat) / |bin|, in place
+    for (int e = tid; e < C::R * 512; e += NTH) {
+      const int r = e >> 9, col = e & 511, p = col & 3;
+      LDS_AS float* d = lf(S, O_FT + (r * 516 + col) * 4);
+      float gv = *d / (float)(bin_hi(p, C::L) - bin_lo(p, C::L));
+      if (dr) gv *= afl_keep(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)(C::COL0 + col), a.thr16) ? a.inv_keep : 0.f;
+      *d = gv;
+    }
+    SYNC();
+    // dh3 = relu'(h3) * pool'(gs), in place over H3 (bf16); conv3 bias partial (fp32) per (row group, channel)
+    {
+      const int ch = tid & 127, rg = tid >> 7;
+      float bsum = 0.f;
+      for (int q = rg; q < 144; q += 4) {
+        float v = 0.f;
+        const int r = q / C::LP, l = q - r * C::LP - 1;
+        LDS_AS unsigned short* hp = lu16(S, O_H3 + ((q + 1) * LD3 + ch) * 2);
+        if (l >= 0 && l < C::L && bff(*hp) > 0.f) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            if (l >= bin_lo(p, C::L) && l < bin_hi(p, C::L)) v += *lf(S, O_FT + (r * 516 + ch * 4 + p) * 4);
+        }
+        *hp = bfu(v);
+        bsum += v;
+      }
+      *lf(S, O_RED + (R_DB3 + rg * 128 + ch) * 4) = bsum;
+    }
+    SYNC();
+    // dh2 = relu'(h2) * sum_j shift_{1-j}(dh3) . W3_j  (K = 3 x 128): wave n-tile nb2, m-tiles mpb, mpb + 2, ..
+    {
+      float cs = 0.f;
+      for (int mt = mpb; mt < 9; mt += 2) {
+        f4v acc = Z4;
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+          acc = mfma(rfrag(S + O_H3, LD3, 16 * mt + 2 - (k >> 2), 32 * (k & 3), lane), w3t[k], acc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 16 * mt + 4 * g + e;
+          const float h2 = bff(*lu16(S, O_H2 + ((q + 1) * LD2 + 16 * nb2 + li) * 2));
+          const float v = h2 > 0.f ? acc[e] : 0.f;
+          *lu16(S, O_DH2 + ((q + 1) * LD2 + 16 * nb2 + li) * 2) = bfu(v);
+          cs += v;
+        }
+      }
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (lane < 16) *lf(S, O_RED + (R_DB2 + wave * 16 + li) * 4) = cs;
+    }
+    // W2T fragments of d(h1)
+    const int nb1 = wave & 1, mpa = wave >> 1;
+    s8v w2t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      w2t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W2T + ((k >> 1) * 32 + 16 * nb1 + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
+    SYNC();
+    // dh1 = relu'(h1) * sum_j shift_{1-j}(dh2) . W2_j (K = 3 x 64), straight into the conv1 gradients
+    {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, sb = 0.f;
+      for (int mt = mpa; mt < 9; mt += 4) {
+        f4v acc = Z4;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          acc = mfma(rfrag(S + O_DH2, LD2, 16 * mt + 2 - (k >> 1), 32 * (k & 1), lane), w2t[k], acc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 16 * mt + 4 * g + e;
+          const float h1 = bff(*lu16(S, O_H1 + ((q + 1) * LD1 + 16 * nb1 + li) * 2));
+          const float d = h1 > 0.f ? acc[e] : 0.f;
+          s0 += d * *lf(S, O_XS + q * 4);
+          s1 += d * *lf(S, O_XS + (q + 1) * 4);
+          s2 += d * *lf(S, O_XS + (q + 2) * 4);
+          sb += d;
+        }
+      }
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        s0 += __shfl_xor(s0, o, 64);
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+        sb += __shfl_xor(sb, o, 64);
+      }
+      if (lane < 16)
+        *(LDS_AS f4v*)(S + O_RED + (R_C1 + (wave * 16 + li) * 4) * 4) = f4v{s0, s1, s2, sb};
+    }
+    // dW3_j = dh3^T . shift_{j-1}(h2) (K = 160 rows: 144 + zero rows), wave = o-tile; partial [j][ci][o]
+    {
+      f4v acc[12];
+#pragma unroll
+      for (int t = 0; t < 12; ++t) acc[t] = Z4;
+      for (int ks = 0; ks < 5; ++ks) {
+        const s8v af = cfrag(S + O_H3 + LD3 * 2, LD3, 32 * ks, 16 * wave, lane);
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+          const int j = t >> 2, ct = t & 3;
+          acc[t] = mfma(af, cfrag(S + O_H2 + j * LD2 * 2, LD2, 32 * ks, 16 * ct, lane), acc[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 12; ++t) {
+        const int j = t >> 2, ci = 16 * (t & 3) + li;
+        st16f(x.rw, pbase + (P_W3 + (j * 64 + ci) * 128 + 16 * wave + 4 * g) * 4, acc[t]);
+      }
+    }
+    // dW2_j = dh2^T . shift_{j-1}(h1): wave -> o-tile (w & 3), ci-tile (w >> 2)
+    {
+      const int ot = wave & 3, ct = wave >> 2;
+      f4v acc[3] = {Z4, Z4, Z4};
+      for (int ks = 0; ks < 5; ++ks) {
+        const s8v af = cfrag(S + O_DH2 + LD2 * 2, LD2, 32 * ks, 16 * ot, lane);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = mfma(af, cfrag(S + O_H1 + j * LD1 * 2, LD1, 32 * ks, 16 * ct, lane), acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        st16f(x.rw, pbase + (P_W2 + (j * 32 + 16 * ct + li) * 64 + 16 * ot + 4 * g) * 4, acc[j]);
+    }
+    SYNC();
+    // small partials: conv1 W [o][j] (96) | conv1 b (32) | conv2 b (64) | conv3 b (128), waves summed in order
+    if (tid < NSMALL) {
+      float v = 0.f;
+      if (tid < 128) {
+        const int o = tid < 96 ? tid / 3 : tid - 96, comp = tid < 96 ? tid % 3 : 3;
+        const int nt = o >> 4;
+        for (int w = nt; w < 8; w += 2) v += *lf(S, O_RED + (R_C1 + (w * 16 + (o & 15)) * 4 + comp) * 4);
+      } else if (tid < 192) {
+        const int o = tid - 128;
+        v = *lf(S, O_RED + (R_DB2 + (o >> 4) * 16 + (o & 15)) * 4) + *lf(S, O_RED + (R_DB2 + ((o >> 4) + 4) * 16 + (o & 15)) * 4);
+      } else {
+        const int o = tid - 192;
+        v = (*lf(S, O_RED + (R_DB3 + o) * 4) + *lf(S, O_RED + (R_DB3 + 128 + o) * 4)) +
+            (*lf(S, O_RED + (R_DB3 + 256 + o) * 4) + *lf(S, O_RED + (R_DB3 + 384 + o) * 4));
+      }
+      *lf(S, O_RED + (R_SM + tid) * 4) = v;
+    }
+    SYNC();
+    if (tid < NSMALL / 4) st16f(x.rw, pbase + (P_SM + 4 * tid) * 4, *(const LDS_AS f4v*)(S + O_RED + (R_SM + 4 * tid) * 4));
+    arrive(x, CT_P + T);
+    REOPQ();
+    // d1 (all rows) and this owner's feature columns, for the fc1 block gradient: loads in flight across the wait
+    u32x4 d1v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
+      d1v[u] = ld16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2);
+    }
+    constexpr int FPR = C::NC / 8;  // 16-B pieces per feature row
+    constexpr int NFU = 128 * FPR / NTH;
+    u32x4 fv[NFU];
+#pragma unroll
+    for (int u = 0; u < NFU; ++u) {
+      const int e = tid + NTH * u, r = e / FPR, pc = e % FPR;
+      fv[u] = ld16(x.rw, WS_FEAT + (r * 1024 + c0w + 8 * pc) * 2);
+    }
+    if (!wait_ge(x, CT_P + T, (uint32_t)(C::NTW * (kact + 1)), O_FLAG)) break;
+    REOPQ();
+    // ------------------------------------------------------------------ owner: conv blocks
+    const AdamT ak = adam_t(a.lr, kact + 1);
+    {
+      f4v gsum[C::NS], mm[C::NS], vv[C::NS];
+      Chunk ks[C::NS];
+#pragma unroll
+      for (int u = 0; u < C::NS; ++u) {
+        ks[u] = chunk_of<T>(i, tid + NTH * u);
+        gsum[u] = Z4;
+        mv_ld(x, u, mm[u], vv[u]);
+      }
+      // partials summed in workgroup order; loads batched 4 at a time
+#pragma unroll
+      for (int u = 0; u < C::NS; ++u) {
+        if (ks[u].kind == 0) continue;
+        for (int n0 = 0; n0 < C::NTW; n0 += 4) {
+          f4v pv[4];
+#pragma unroll
+          for (int n = 0; n < 4; ++n) pv[n] = ld16f(x.rw, WS_PART + ((C::FIRST + n0 + n) * PSZ + ks[u].poff) * 4);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) gsum[u] += pv[n];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < C::NS; ++u) {
+        if (ks[u].kind == 0) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float me = mm[u][e], ve = vv[u][e];
+          st.p[u][e] = adam1(st.p[u][e], me, ve, gsum[u][e], ak.a, ak.sb);
+          mm[u][e] = me;
+          vv[u][e] = ve;
+        }
+        mv_st(x, u, mm[u], vv[u]);
+      }
+    }
+    publish_conv<T>(x, i, st);
+    REOPQ();
+    // ------------------------------------------------------------------ owner: fc1 column block
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
+      *(LDS_AS u32x4*)(S + O_D1F + (r * LDD + 8 * pc) * 2) = d1v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NFU; ++u) {
+      const int e = tid + NTH * u, r = e / FPR, pc = e % FPR;
+      *(LDS_AS u32x4*)(S + O_FW + (r * 72 + 8 * pc) * 2) = fv[u];
+    }
+    SYNC();
+    {
+      constexpr int NT1 = C::NC / 16;
+      f4v acc[NT1], m1[NT1], v1[NT1];
+#pragma unroll
+      for (int t = 0; t < NT1; ++t) mv_ld(x, 4 + t, m1[t], v1[t]);
+#pragma unroll
+      for (int t = 0; t < NT1; ++t) acc[t] = Z4;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s8v af = cfrag(S + O_D1F, LDD, 32 * ks, 16 * wave, lane);
+#pragma unroll
+        for (int t = 0; t < NT1; ++t) acc[t] = mfma(af, cfrag(S + O_FW, 72, 32 * ks, 16 * t, lane), acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < NT1; ++t) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float me = m1[t][e], ve = v1[t][e];
+          st.p1[t][e] = adam1(st.p1[t][e], me, ve, acc[t][e], ak.a, ak.sb);
+          m1[t][e] = me;
+          v1[t][e] = ve;
+        }
+        mv_st(x, 4 + t, m1[t], v1[t]);
+      }
+    }
+    SYNC();
+    publish_fc1<T>(x, i, st);
+    arrive(x, CT_W + T);
+    ++kact;
+  }
+  // ---------------------------------------------------------------- round end: owned parameters -> arena
+#pragma unroll
+  for (int u = 0; u < C::NS; ++u) {
+    const Chunk k = chunk_of<T>(i, tid + NTH * u);
+    if (k.kind == 0) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) P[elem_idx<T>(a, k, e)] = st.p[u][e];
+  }
+#pragma unroll
+  for (int t = 0; t < C::NC / 16; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0w + 16 * t + li] = st.p1[t][e];
+}
+
+// ============================================================================================== head
+// LDS map (bytes); U = f2s | f3f | d3s, reused as the d1 staging tile once the backward is past them
+constexpr int H_L1 = 136, H_L2 = 72, H_L3 = 40, H_F3 = 33;
+constexpr int H_F1S = 0;
+constexpr int H_W2S = H_F1S + 128 * H_L1 * 2;
+constexpr int H_W3S = H_W2S + 64 * H_L1 * 2;
+constexpr int H_F2S = H_W3S + 32 * H_L2 * 2;
+constexpr int H_F3F = H_F2S + 128 * H_L2 * 2;
+constexpr int H_D3S = H_F3F + 128 * H_F3 * 4;
+constexpr int H_D1S = H_F2S;  // [128][136] bf16
+constexpr int H_D2S = H_D3S + 128 * H_L3 * 2;
+static_assert(H_D1S + 128 * H_L1 * 2 <= H_D2S, "d1 staging fits U");
+constexpr int H_DZ = H_D2S + 128 * H_L2 * 2;
+constexpr int H_RED = H_DZ + 128 * 4;
+constexpr int H_WO = H_RED + 8 * 4;
+constexpr int H_RED3W = H_WO + 32 * 4;
+constexpr int H_GBW = H_RED3W + 8 * 72 * 4;
+constexpr int H_BIAS = H_GBW + 8 * 192 * 4;  // b1 [128] | b2 [64] | b3 [32] | bo [4]
+constexpr int H_SUMS = H_BIAS + 228 * 4;      // gb2 [64] | gb3 [32] | gWo [32] | gbo [1] | gb1 [128]
+constexpr int H_FLAG = H_SUMS + 260 * 4;
+constexpr int H_LDS = H_FLAG + 16;
+constexpr int LDS_TOTAL = T_LDS > H_LDS ? T_LDS : H_LDS;
+static_assert(LDS_TOTAL <= 160 * 1024, "cnn2 LDS");
+
+__device__ __forceinline__ float wsum(float x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+__device__ __forceinline__ void head(const Ctx& x) {
+  const AflCnn2Args& a = *x.a;
+  uchar* S = x.smem;
+  int tid = x.tid, lane = x.lane, wave = x.wave, g = lane >> 4, li = lane & 15;
+  const int c = x.c, B = a.B;
+  float* P = a.params + (long)c * a.pstride;
+  const int oW2 = a.off[14], ob2 = a.off[15], oW3 = a.off[16], ob3 = a.off[17], oWo = a.off[18], obo = a.off[19],
+            ob1 = a.off[13];
+  LDS_AS unsigned short* f1s = lu16(S, H_F1S);
+  LDS_AS unsigned short* W2s = lu16(S, H_W2S);
+  LDS_AS unsigned short* W3s = lu16(S, H_W3S);
+  LDS_AS unsigned short* f2s = lu16(S, H_F2S);
+  LDS_AS float* f3f = lf(S, H_F3F);
+  LDS_AS unsigned short* d3s = lu16(S, H_D3S);
+  LDS_AS unsigned short* d2s = lu16(S, H_D2S);
+  LDS_AS unsigned short* d1s = lu16(S, H_D1S);
+  LDS_AS float* dz = lf(S, H_DZ);
+  LDS_AS float* red = lf(S, H_RED);
+  LDS_AS float* wos = lf(S, H_WO);
+  LDS_AS float* red3w = lf(S, H_RED3W);
+  LDS_AS float* gbw = lf(S, H_GBW);
+  LDS_AS float* bias = lf(S, H_BIAS);
+  LDS_AS float* sums = lf(S, H_SUMS);
+  // persistent Adam state: dW2 elements (o = 16 (w >> 1) + 4 g + e, i = 16 (4 (w & 1) + j) + li), dW3 elements
+  // (o = 16 (w >> 2) + 4 g + e, i = 16 (w & 3) + li), one vector entry per thread < 257
+  float p2[16], p3[4], pv = 0.f;  // moments in slab slots 0..3 (W2), 4 (W3), 5 (vector entry)
+  const int o2b = 16 * (wave >> 1) + 4 * g, i2b = 16 * 4 * (wave & 1) + li;
+  const int o3b = 16 * (wave >> 2) + 4 * g, i3 = 16 * (wave & 3) + li;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      p2[4 * j + e] = P[oW2 + (o2b + e) * 128 + i2b + 16 * j];
+    }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    p3[e] = P[oW3 + (o3b + e) * 64 + i3];
+  }
+  for (int k = 0; k < 6; ++k) mv_st(x, k, Z4, Z4);
+  auto vidx = [&](int t) -> int {  // arena index of vector entry t
+    return t < 64 ? ob2 + t : t < 96 ? ob3 + t - 64 : t < 128 ? oWo + t - 96 : t == 128 ? obo : ob1 + t - 129;
+  };
+  if (tid < 257) pv = P[vidx(tid)];
+  // LDS images / vectors from the state
+  auto put_state = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) W2s[(o2b + e) * H_L1 + i2b + 16 * j] = bfu(p2[4 * j + e]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) W3s[(o3b + e) * H_L2 + i3] = bfu(p3[e]);
+    if (tid < 257) {
+      if (tid < 64) bias[128 + tid] = pv;
+      else if (tid < 96) bias[192 + tid - 64] = pv;
+      else if (tid < 128) wos[tid - 96] = pv;
+      else if (tid == 128) bias[224] = pv;
+      else bias[tid - 129] = pv;
+    }
+  };
+  put_state();
+  __syncthreads();
+
+  const int min_bs = a.min_bs;
+  int kact = 0;
+  for (int s = 0; s < a.S; ++s) {
+    const int bs = a.bsz[(long)s * a.C + c];
+    if (bs < min_bs || bs < 1) continue;
+    const int ep = a.epoch[(long)s * a.C + c], nbc = a.nb[c];
+    const int* idxs = a.idx + ((long)s * a.C + c) * B;
+    const int yb = min(tid & 127, B - 1);
+    const int yrow = idxs[yb];
+    const float yv = yrow >= 0 ? a.rows[(long)yrow * 24 + 23] : 0.f;
+    if (!wait_ge(*&x, CT_F, (uint32_t)(24 * (kact + 1)), H_FLAG)) break;
+    REOPQ();
+    // z1 = z1p_vitals + z1p_labs (+ b1, ReLU) -> f1s; thread: row b = (tid + 512 q) >> 5, columns i1 .. i1 + 3
+    const int i1 = 4 * (tid & 31);
+    {
+      f4v za[8], zb[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int b = (tid + NTH * q) >> 5;
+        za[q] = ld16f(x.rw, WS_Z1P + (b * 128 + i1) * 4);
+        zb[q] = ld16f(x.rw, WS_Z1P + ((128 + b) * 128 + i1) * 4);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int b = (tid + NTH * q) >> 5;
+        LDS_AS unsigned short* d = f1s + b * H_L1 + i1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = bfu(b < B ? relu((za[q][k] + zb[q][k]) + bias[i1 + k]) : 0.f);
+      }
+    }
+    SYNC();
+    // fc2: wave -> m-tile w, n-tiles 0..3
+    {
+      const int m0 = wave * 16;
+      f4v acc[4] = {Z4, Z4, Z4, Z4};
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        const s8v af = rfrag(S + H_F1S, H_L1, m0, k0, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = mfma(af, rfrag(S + H_W2S, H_L1, 16 * j, k0, lane), acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + li;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f2s[(m0 + 4 * g + e) * H_L2 + n] = bfu(relu(acc[j][e] + bias[128 + n]));
+      }
+    }
+    SYNC();
+    // fc3
+    {
+      const int m0 = wave * 16;
+      f4v acc[2] = {Z4, Z4};
+#pragma unroll
+      for (int k0 = 0; k0 < 64; k0 += 32) {
+        const s8v af = rfrag(S + H_F2S, H_L2, m0, k0, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] = mfma(af, rfrag(S + H_W3S, H_L2, 16 * j, k0, lane), acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 16 * j + li;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f3f[(m0 + 4 * g + e) * H_F3 + n] = relu(acc[j][e] + bias[192 + n]);
+      }
+    }
+    SYNC();
+    // output logit + sigmoid-BCE (k_bce arithmetic)
+    float zb = 0.f, lb = 0.f;
+    if (tid < 128) {
+      float acc = bias[224];
+      for (int j = 0; j < 32; ++j) acc += f3f[tid * H_F3 + j] * wos[j];
+      zb = acc;
+      if (tid < bs) {
+        const float p = 1.f / (1.f + expf(-zb));
+        lb = -(yv * fmaxf(logf(p), -100.f) + (1.f - yv) * fmaxf(log1pf(-p), -100.f));
+        if (p != p) lb = p;
+      }
+    }
+    lb = wsum(lb);
+    if (lane == 0) red[wave] = lb;
+    SYNC();
+    const float loss = ((red[0] + red[1]) + (red[2] + red[3])) / (float)max(bs, 1);
+    const bool nan = a.nan_abort && (loss != loss);
+    if (nan) {  // status only: no update this step, the client's round ends (towers read the status)
+      if (tid == 0) {
+        st16(x.rw, WS_STAT, u32x4{1u, (uint32_t)s, 0u, 0u});
+        a.failed[c] = 1;
+      }
+      arrive(x, CT_H);
+      break;
+    }
+    if (tid < 128) {
+      float gz = 0.f;
+      if (tid < bs) {
+        const float p = 1.f / (1.f + expf(-zb));
+        const float w = p * (1.f - p);
+        gz = (p - yv) / fmaxf(w, 1e-12f) * w / (float)bs;
+      }
+      dz[tid] = gz;
+    }
+    if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
+    SYNC();
+    // d3 = dz wo^T * relu'(f3); output-layer / fc3-bias gradient partials per wave
+    for (int e = tid; e < 128 * 32; e += NTH) {
+      const int b = e >> 5, j = e & 31;
+      d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * wos[j] : 0.f);
+    }
+    {
+      const int j = tid & 31, r0 = 8 * (tid >> 5);
+      float sa = 0.f, sw = 0.f, sz = 0.f;
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb) {
+        const int b = r0 + bb;
+        const float f = f3f[b * H_F3 + j], d = dz[b];
+        sa += f > 0.f ? d : 0.f;
+        sw += d * f;
+        sz += d;
+      }
+      sa += __shfl_xor(sa, 32, 64);
+      sw += __shfl_xor(sw, 32, 64);
+      sz += __shfl_xor(sz, 32, 64);
+      if (lane < 32) {
+        red3w[wave * 72 + j] = sa;
+        red3w[wave * 72 + 32 + j] = sw;
+        if (j == 0) red3w[wave * 72 + 64] = sz;
+      }
+    }
+    SYNC();
+    if (tid < 32 || tid == 64) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        s0 += red3w[w * 72 + tid];
+        if (tid < 32) s1 += red3w[w * 72 + 32 + tid];
+      }
+      if (tid < 32) {
+        sums[64 + tid] = s0 * wos[tid];  // gb3
+        sums[96 + tid] = s1;             // gWo
+      } else {
+        sums[128] = s0;                  // gbo
+      }
+    }
+    // dW3 [32 x 64] = d3^T f2 (registers until the Adam step)
+    f4v g3;
+    {
+      const int o0 = (wave >> 2) * 16, ii0 = (wave & 3) * 16;
+      g3 = Z4;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32)
+        g3 = mfma(cfrag(S + H_D3S, H_L3, k0, o0, lane), cfrag(S + H_F2S, H_L2, k0, ii0, lane), g3);
+    }
+    // d2 = d3 . W3 * relu'(f2); gb2 per wave
+    {
+      const int m0 = wave * 16;
+      const s8v af = rfrag(S + H_D3S, H_L3, m0, 0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4v acc = mfma(af, cfrag(S + H_W3S, H_L2, 0, 16 * j, lane), Z4);
+        const int n = 16 * j + li;
+        float cs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + 4 * g + e;
+          const unsigned short fb = f2s[m * H_L2 + n];
+          const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
+          d2s[m * H_L2 + n] = bfu(v);
+          cs += v;
+        }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        if (lane < 16) gbw[wave * 192 + n] = cs;
+      }
+    }
+    SYNC();
+    if (tid < 64) {
+      float sb = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sb += gbw[w * 192 + tid];
+      sums[tid] = sb;  // gb2
+    }
+    // dW2 [64 x 128] = d2^T f1 (registers)
+    f4v g2[4];
+    {
+      const int o0 = (wave >> 1) * 16, ib = (wave & 1) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g2[j] = Z4;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        const s8v af = cfrag(S + H_D2S, H_L2, k0, o0, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g2[j] = mfma(af, cfrag(S + H_F1S, H_L1, k0, 16 * (ib + j), lane), g2[j]);
+      }
+    }
+    SYNC();  // U (f2s / f3f / d3s) is dead: d1 staging
+    // d1 = d2 . W2 * relu'(f1) -> bf16 staging; gb1 per wave
+    {
+      const int m0 = wave * 16;
+      const s8v a0 = rfrag(S + H_D2S, H_L2, m0, 0, lane), a1 = rfrag(S + H_D2S, H_L2, m0, 32, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f4v acc = mfma(a0, cfrag(S + H_W2S, H_L1, 0, 16 * j, lane), Z4);
+        acc = mfma(a1, cfrag(S + H_W2S, H_L1, 32, 16 * j, lane), acc);
+        const int n = 16 * j + li;
+        float cs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + 4 * g + e;
+          const unsigned short fb = f1s[m * H_L1 + n];
+          const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
+          d1s[m * H_L1 + n] = bfu(v);
+          cs += v;
+        }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        if (lane < 16) gbw[wave * 192 + 64 + n] = cs;
+      }
+    }
+    SYNC();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // publish d1 (bf16 [128][128])
+      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
+      st16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2, *(const LDS_AS u32x4*)(S + H_D1S + (r * H_L1 + 8 * pc) * 2));
+    }
+    if (tid == 0) st16(x.rw, WS_STAT, u32x4{0u, (uint32_t)s, 0u, 0u});
+    if (tid < 128) {
+      float sb = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sb += gbw[w * 192 + 64 + tid];
+      sums[129 + tid] = sb;  // gb1
+    }
+    arrive(x, CT_H);
+    REOPQ();
+    // Adam on the head parameters (off the critical path: the towers run their backward meanwhile)
+    const AdamT ak = adam_t(a.lr, kact + 1);
+    {
+      f4v hm[6], hv[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) mv_ld(x, k, hm[k], hv[k]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float me = hm[j][e], ve = hv[j][e];
+          p2[4 * j + e] = adam1(p2[4 * j + e], me, ve, g2[j][e], ak.a, ak.sb);
+          hm[j][e] = me;
+          hv[j][e] = ve;
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float me = hm[4][e], ve = hv[4][e];
+        p3[e] = adam1(p3[e], me, ve, g3[e], ak.a, ak.sb);
+        hm[4][e] = me;
+        hv[4][e] = ve;
+      }
+      if (tid < 257) {
+        // vector order of the state: b2 [64] | b3 [32] | Wo [32] | bo | b1 [128] == the sums layout
+        float me = hm[5][0], ve = hv[5][0];
+        pv = adam1(pv, me, ve, sums[tid], ak.a, ak.sb);
+        hm[5][0] = me;
+        hv[5][0] = ve;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) mv_st(x, k, hm[k], hv[k]);
+    }
+    SYNC();
+    put_state();
+    SYNC();
+    ++kact;
+  }
+  // round end: parameters -> arena
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) P[oW2 + (o2b + e) * 128 + i2b + 16 * j] = p2[4 * j + e];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) P[oW3 + (o3b + e) * 64 + i3] = p3[e];
+  if (tid < 257) P[vidx(tid)] = pv;
+}
+
+__global__ void __launch_bounds__(NTH) k_cnn2_train(AflCnn2Args a) {
+  extern __shared__ __attribute__((aligned(16))) uchar smem_raw[];
+  Ctx x;
+  x.a = &a;
+  x.c = blockIdx.x % a.C;
+  const int role = blockIdx.x / a.C;
+  x.tid = threadIdx.x;
+  x.lane = threadIdx.x & 63;
+  x.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  x.role = role;
+  x.smem = smem_raw;
+  x.wsb = (uchar*)a.ws + (long)x.c * a.ws_stride;
+  x.rw = rsrc(x.wsb);
+  x.ctr = (gu32*)(a.ctr + (long)x.c * CT_N * 32);
+#if defined(CNN2_ONLY_HEAD)
+  head(x);
+#elif defined(CNN2_ONLY_VIT)
+  tower<0>(x, role);
+#elif defined(CNN2_ONLY_LAB)
+  tower<1>(x, role - 8);
+#else
+  if (role == WG_HEAD)
+    head(x);
+  else if (role < 8)
+    tower<0>(x, role);
+  else
+    tower<1>(x, role - 8);
+#endif
+}
+
+}  // namespace
+
+long afl_cnn2_ws_bytes() { return WS_BYTES; }
+int afl_cnn2_ctr_words() { return CT_N * 32; }
+int afl_cnn2_wgs_per_client() { return NWG; }
+
+int afl_cnn2_train(const AflCnn2Args& a, hipStream_t s) {
+  if (a.B < 2 || a.B > 128 || a.C < 1 || a.ws_stride < WS_BYTES || (a.ws_stride & 15)) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)k_cnn2_train, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_cnn2_train, dim3(NWG * a.C), dim3(NTH), LDS_TOTAL, s, a);
+  return (int)hipGetLastError();
+}

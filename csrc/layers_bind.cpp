@@ -652,6 +652,62 @@ void attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, torch::Tens
   ok(afl_attn_bwd(a, cur()), "attn_bwd");
 }
 
+// CNNModel on-chip trainer (cnn2.hip): one launch trains every client of params [C, P] for the whole round
+// over the step tables of fl/programs.py:step_tables; ws / ctr from cnn2_ws_bytes / cnn2_ctr_words (ctr zeroed)
+void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor rows, torch::Tensor idx, torch::Tensor bsz,
+                torch::Tensor epoch, torch::Tensor nb, torch::Tensor seeds, double p, int64_t min_bs, bool nan_abort,
+                double lr, torch::Tensor failed, torch::Tensor losses, torch::Tensor ws, torch::Tensor ctr) {
+  dense(params, "params");
+  dense(rows, "rows");
+  dense(idx, "idx", torch::kInt32);
+  dense(bsz, "bsz", torch::kInt32);
+  dense(epoch, "epoch", torch::kInt32);
+  dense(nb, "nb", torch::kInt32);
+  dense(seeds, "seeds", torch::kInt32);
+  dense(failed, "failed", torch::kInt32);
+  dense(losses, "losses");
+  dense(ws, "ws", torch::kUInt8);
+  dense(ctr, "ctr", torch::kInt32);
+  TORCH_CHECK(offs.size() == 20, "cnn2_train: 20 CNNModel slot offsets");
+  TORCH_CHECK(params.dim() == 2 && rows.dim() == 2 && rows.size(1) == 24, "cnn2_train: params [C, P], rows [N, 24]");
+  const int C = (int)params.size(0);
+  TORCH_CHECK(idx.dim() == 3 && idx.size(1) == C && bsz.dim() == 2 && bsz.size(1) == C && epoch.sizes() == bsz.sizes(),
+              "cnn2_train: step tables [S, C, B] / [S, C]");
+  const int S = (int)idx.size(0), B = (int)idx.size(2);
+  TORCH_CHECK(bsz.size(0) == S && nb.numel() == C && seeds.numel() == C && failed.numel() == C && losses.dim() == 2 &&
+                  losses.size(0) == C, "cnn2_train: per-client sizes");
+  TORCH_CHECK(ws.numel() >= (int64_t)C * afl_cnn2_ws_bytes() && ctr.numel() >= (int64_t)C * afl_cnn2_ctr_words(),
+              "cnn2_train: workspace too small");
+  AflCnn2Args a{};
+  a.params = params.data_ptr<float>();
+  a.pstride = params.size(1);
+  for (int k = 0; k < 20; ++k) {
+    TORCH_CHECK(offs[k] >= 0 && offs[k] < a.pstride, "cnn2_train: slot offset out of range");
+    a.off[k] = (int)offs[k];
+  }
+  a.rows = rows.data_ptr<float>();
+  a.idx = idx.data_ptr<int>();
+  a.bsz = bsz.data_ptr<int>();
+  a.epoch = epoch.data_ptr<int>();
+  a.nb = nb.data_ptr<int>();
+  a.seeds = (const uint32_t*)seeds.data_ptr<int>();
+  a.S = S;
+  a.C = C;
+  a.B = B;
+  a.E = (int)losses.size(1);
+  a.thr16 = p > 0.0 ? (uint32_t)std::lround(p * 65536.0) : 0u;
+  a.inv_keep = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  a.min_bs = (int)min_bs;
+  a.nan_abort = nan_abort ? 1 : 0;
+  a.lr = (float)lr;
+  a.failed = failed.data_ptr<int>();
+  a.losses = losses.data_ptr<float>();
+  a.ws = ws.data_ptr();
+  a.ws_stride = afl_cnn2_ws_bytes();
+  a.ctr = (uint32_t*)ctr.data_ptr<int>();
+  ok(afl_cnn2_train(a, cur()), "cnn2_train");
+}
+
 }  // namespace
 
 void afl_register_layers(pybind11::module& m) {
@@ -672,6 +728,10 @@ void afl_register_layers(pybind11::module& m) {
   m.def("conv_dw", &conv_dw);
   m.def("cnn_head", &cnn_head);
   m.def("cnn_wimg_size", &afl_cnn_wimg_ushorts);
+  m.def("cnn2_train", &cnn2_train);
+  m.def("cnn2_ws_bytes", &afl_cnn2_ws_bytes);
+  m.def("cnn2_ctr_words", &afl_cnn2_ctr_words);
+  m.def("cnn2_wgs_per_client", &afl_cnn2_wgs_per_client);
   m.def("pool4_bwd", &pool4_bwd);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

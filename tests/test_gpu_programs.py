@@ -355,3 +355,30 @@ def test_program_training_is_bit_reproducible(gpu, name, B, n, E):
         seeds=[6])
     assert ok.all()
     assert torch.equal(p1.cpu()[0], runs[0][0][1]), (p1.cpu()[0] - runs[0][0][1]).abs().max()
+
+
+@pytest.mark.parametrize("C,n,E", [(3, 1000, 2), (8, 600, 1)])
+def test_cnn2_onchip_trainer_tracks_layer_program(gpu, monkeypatch, C, n, E):
+    """The CNNModel on-chip trainer (csrc/kernels/cnn2.hip: one launch per round, 25 workgroups per client)
+    follows the graph-replayed layer program (same batches, dropout masks and Adam): per-epoch losses and
+    the trained parameters agree to bf16-operand tolerance, and two launches give the same bits."""
+    ds = synthetic_icu(n)
+    nd = [max(3, n // 2 - 17 * c) for c in range(C)]
+    order = torch.stack([torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(10 * c + e))[:max(nd)]
+                                      for e in range(E)]) for c in range(C)]).to(torch.int32)
+    params = _params("CNNModel", C)
+    table = DeviceTable(ds, DEV)
+    res = {}
+    for mode in ("0", "1", "1b"):
+        monkeypatch.setenv("AFL_CNN2", mode[0])
+        p = params.clone().to(DEV)
+        runner = ProgramRunner(make_program("CNNModel", C, 128, DEV))
+        assert runner._onchip_cnn(p, 0.0, None) == (mode[0] == "1")
+        ok, losses = runner.train(table, p, Plan(order.to(DEV), torch.tensor(nd, dtype=torch.int32), E), lr=1e-3,
+                                  seeds=[5 + c for c in range(C)])
+        assert ok.all()
+        res[mode] = (p.cpu(), losses)
+    assert torch.equal(res["1"][0], res["1b"][0]) and torch.equal(res["1"][1], res["1b"][1])
+    assert torch.allclose(res["1"][1], res["0"][1], rtol=2e-2, atol=2e-3), (res["1"][1], res["0"][1])
+    assert (res["1"][0] - res["0"][0]).abs().max() < 0.05
+    assert (res["1"][0] - params).abs().max() > 1e-3  # it trained
