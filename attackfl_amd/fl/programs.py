@@ -492,6 +492,8 @@ class ProgramRunner:
         return (failed == 0).cpu(), losses.double().cpu()
 
     # ---- CNNModel on-chip trainer (csrc/kernels/cnn2.hip) ------------------------------------------------
+    cnn2_stamps = None  # optional int64 [C, 25, 64, 8] per-phase wall-clock stamps (tools/cnn2_phases.py)
+
     def _onchip_cnn(self, params: torch.Tensor, sgd_lr: float, max_steps) -> bool:
         """One persistent launch per round instead of a graph replay per step: CNNModel on a GPU with Adam
         (the SGD gradient hook and step caps stay on the layer program), all 25 workgroups of every client
@@ -525,7 +527,7 @@ class ProgramRunner:
             ctr.zero_()
             offs = [s.offset for s in pg.layout.slots]
             nat.cnn2_train(params if params.is_contiguous() else params.contiguous(), offs, table.rows, idx, bsz, ep, nb,
-                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr)
+                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr, self.cnn2_stamps)
             self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params)  # the launch may still run when sync=False
         if not sync:
             return failed, losses  # failed: 1 = NaN loss, 2 = a cross-workgroup wait timed out (GraphTrainer raises)

@@ -201,6 +201,7 @@ struct AflCnn2Args {
   void* ws;              // [C][ws_stride] bytes workspace (afl_cnn2_ws_bytes)
   long ws_stride;
   uint32_t* ctr;         // [C][afl_cnn2_ctr_words] zeroed counters
+  uint64_t* stamps;      // optional [C][25][64][16] per-phase s_memrealtime stamps (null: off)
 };
 long afl_cnn2_ws_bytes();
 int afl_cnn2_ctr_words();

@@ -47,8 +47,8 @@ typedef GAS uint32_t gu32;
 typedef unsigned char uchar;
 
 constexpr int NTH = 512;  // 8 waves
-constexpr int NWG = 25;   // workgroups per client: 8 vitals + 16 labs towers + head
-constexpr int WG_HEAD = 24;
+constexpr int NWG = 32;   // workgroups per client: 8 vitals + 16 labs towers + head + 7 fc1 owners
+constexpr int WG_HEAD = 24, WG_FC1 = 25, NFC1 = 7;
 constexpr long DEADLINE = 200000000L;  // s_memrealtime ticks (100 MHz): 2 s per wait
 
 __device__ __forceinline__ f4v mfma(s8v a, s8v b, f4v c) {
@@ -61,8 +61,9 @@ __device__ __forceinline__ uint32_t pk2(float a, float b) {
 }
 __device__ __forceinline__ float bff(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
 __device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }  // keeps NaN like torch
-__device__ __forceinline__ int bin_lo(int p, int L) { return (p * L) / 4; }
-__device__ __forceinline__ int bin_hi(int p, int L) { return ((p + 1) * L + 3) / 4; }
+__host__ __device__ constexpr int bin_lo(int p, int L) { return (p * L) / 4; }
+__host__ __device__ constexpr int bin_hi(int p, int L) { return ((p + 1) * L + 3) / 4; }
+__host__ __device__ constexpr float bin_rcp(int p, int L) { return 1.f / (float)(bin_hi(p, L) - bin_lo(p, L)); }
 
 // ---- LDS fragments ----
 // row-major [rows][ld] bf16: MFMA operand rows r0 + (lane & 15), k = k0 + 8 (lane >> 4) .. +7
@@ -138,22 +139,26 @@ __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: 
 // images: per tower [W2 3x64x32 | W3 3x128x64 | W2T 3x32x64 | W3T 3x64x128] bf16, then fc1 W1 [128][1024] and
 // W1T [1024][128] bf16
 constexpr int IM_W2 = 0, IM_W3 = 6144, IM_W2T = 30720, IM_W3T = 36864, IM_TOWER = 61440;  // ushorts
-constexpr int IM_W1 = 2 * IM_TOWER, IM_W1T = IM_W1 + 131072, IM_END = IM_W1T + 131072;
+// fc1 images are double-buffered by step parity (the fc1 owners write step k + 1's while the towers read step k's)
+constexpr int IM_W1 = 2 * IM_TOWER, IM_W1T = IM_W1 + 131072, IM_FC1PAR = 262144, IM_END = IM_W1 + 2 * IM_FC1PAR;
 constexpr int WS_IMG = 0;
 constexpr int WS_SMALL = WS_IMG + IM_END * 2;              // [2][320] fp32: conv1 W (96) | b1 (32) | b2 (64) | b3 (128)
 constexpr int NSMALL = 320;
-constexpr int WS_FEAT = WS_SMALL + 2 * NSMALL * 4;         // [128][1024] bf16 concat features
-constexpr int WS_Z1P = WS_FEAT + 128 * 1024 * 2;           // [2][128][128] fp32 fc1 partials per tower
+constexpr int WS_FEAT = WS_SMALL + 2 * NSMALL * 4;         // [2 parities][128][1024] bf16 concat features
+constexpr int FEAT_PAR = 128 * 1024 * 2;
+constexpr int WS_Z1P = WS_FEAT + 2 * FEAT_PAR;             // [2][128][128] fp32 fc1 partials per tower
 constexpr int WS_D1 = WS_Z1P + 2 * 128 * 128 * 4;          // [128][128] bf16 d(fc1 pre-activation)
 constexpr int WS_STAT = WS_D1 + 128 * 128 * 2;             // 16 B: head status of the step
 constexpr int PSZ = 24576 + 6144 + NSMALL;                 // one tower workgroup's gradient partial (floats)
-constexpr int P_W3 = 0, P_W2 = 24576, P_SM = 24576 + 6144; // [3][64][128] | [3][32][64] | smalls, (ci, o) o-contiguous
+// [3 taps][16 o-blocks][64 ci][8 o] | [3][8][32][8] | smalls: an owner's o-block is one contiguous 2 KB / 1 KB run per tap
+constexpr int P_W3 = 0, P_W2 = 24576, P_SM = 24576 + 6144;
 constexpr int WS_PART = WS_STAT + 16;                      // [24][PSZ] fp32 (vitals 0..7, labs 8..23)
 constexpr int WS_MV = WS_PART + 24 * PSZ * 4;              // [25 workgroups][8 slots][512 threads] {m f4, v f4}
-constexpr int MV_WG = 8 * 512 * 32;
-constexpr long WS_BYTES = WS_MV + 25L * MV_WG;
+constexpr int MV_WG = 16 * 512 * 32;
+constexpr long WS_BYTES = WS_MV + (long)NWG * MV_WG;
 // counters per client: F (towers -> head), H (head -> towers), P0/P1 (partials), W0/W1 (images), TMO
-constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_N = 8;  // x 32 words (own 128-B lines)
+// W1R: fc1 images of the next step published (7 arrivals per step)
+constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_W1R = 7, CT_N = 8;  // x 32 words (own 128-B lines)
 
 struct Ctx {
   const AflCnn2Args* a;
@@ -164,10 +169,44 @@ struct Ctx {
   gu32* ctr;                   // client counters
 };
 
+// optional per-phase wall-clock stamps (s_memrealtime, 10 ns) of the first 64 active steps:
+// stamps[c][role][step][16] (tools/cnn2_phases.py)
+constexpr int ST_STEPS = 64;
+__device__ __forceinline__ void stamp(const Ctx& x, int k, int slot) {
+  if (x.a->stamps != nullptr && k < ST_STEPS && x.tid == 0)
+    x.a->stamps[(((long)x.c * NWG + x.role) * ST_STEPS + k) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ void arrive(const Ctx& x, int which) {
   drain();
   __syncthreads();
   if (x.tid == 0) __hip_atomic_fetch_add(x.ctr + which * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// true when counter `which` reached `target` and counter `w2` reached `t2` (both polled in one round trip);
+// false (all threads) on the deadline
+__device__ __forceinline__ bool wait_ge2(const Ctx& x, int which, uint32_t target, int w2, uint32_t t2, int flag_off) {
+  LDS_AS int* fl = (LDS_AS int*)(x.smem + flag_off);
+  if (x.tid == 0) {
+    int ok = 1;
+    const long t0 = (long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const uint32_t v1 = __hip_atomic_load(x.ctr + which * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t v2 = __hip_atomic_load(x.ctr + w2 * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v1 >= target && v2 >= t2) break;
+      if ((long)__builtin_amdgcn_s_memrealtime() - t0 > DEADLINE) {
+        ok = 0;
+        __hip_atomic_store(x.ctr + CT_TMO * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x.a->failed[x.c] = 2;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    fl[0] = ok;
+  }
+  __syncthreads();
+  const int ok = fl[0];
+  __syncthreads();
+  return ok != 0;
 }
 // true when the counter reached `target`; false (all threads) on the deadline
 __device__ __forceinline__ bool wait_ge(const Ctx& x, int which, uint32_t target, int flag_off) {
@@ -236,14 +275,16 @@ constexpr int O_FT = O_XS + 656;            // feat bf16 [16][520] | z1p staging
 constexpr int O_ZS = O_FT + 16 * LDF * 2;
 constexpr int O_D1R = O_FT + 16 * 516 * 4;  // own d1 rows bf16 [16][136]
 constexpr int O_RED = O_D1R + 16 * LDD * 2; // reductions (8 KB)
-constexpr int O_FLAG = O_RED + 8192;
+constexpr int O_FLAG = O_RED + 9216;
 constexpr int T_LDS = O_FLAG + 16;
 static_assert(O_ZS + 16 * LDZ * 4 <= O_D1R, "z1p staging");
 // owner-phase staging (dead activation regions after the backward)
 constexpr int O_S3 = 0, O_S2 = 6144, O_D1F = 8192, O_FW = O_D1F + 128 * LDD * 2, O_SW = O_FW + 128 * 72 * 2;
 static_assert(O_SW + 128 * 72 * 2 <= O_XS, "owner staging");
 // reduction slots (floats from O_RED)
-constexpr int R_DB2 = 0, R_DB3 = 128, R_C1 = 128 + 512, R_SM = 128 + 512 + 512;  // [8][16] | [4][128] | [8][16][4] | [320]
+constexpr int R_DB2 = 0, R_DB3 = 128, R_C1 = 128 + 1024, R_SM = 128 + 1024 + 512;  // [8][16] | [8][128] | [8][16][4] | [320]
+constexpr int R_KEEP = R_SM + NSMALL;  // dropout keep bytes [16 rows][64] (one byte = 8 concat columns), as floats: 256
+static_assert((R_KEEP + 256) * 4 <= 9216, "reduction slots");
 
 __device__ __forceinline__ bool valid_q(int q, int LP) {
   const int l = q % LP;
@@ -252,9 +293,8 @@ __device__ __forceinline__ bool valid_q(int q, int LP) {
 
 template <int T>
 struct TowerState {
-  // owned conv chunks (4 elements each; moments in slab slots 0..NS-1) and fc1 block elements (slots 4..)
+  // owned conv chunks (4 elements each; moments in slab slots 0..NS-1)
   float p[TW<T>::NS][4];
-  float p1[TW<T>::NC / 16][4];
 };
 
 // owned chunk u -> kind (0 none, 3 W3, 2 W2, 1 small), partial float offset, param element base (+ stride)
@@ -287,8 +327,8 @@ __device__ __forceinline__ Chunk chunk_of(int i, int cid) {
       k.kind = 1; k.s0 = 4 * (cid - 384);
     }
   }
-  if (k.kind == 3) k.poff = P_W3 + (k.j * 64 + k.ci) * 128 + k.o0;
-  if (k.kind == 2) k.poff = P_W2 + (k.j * 32 + k.ci) * 64 + k.o0;
+  if (k.kind == 3) k.poff = P_W3 + ((k.j * 16 + (k.o0 >> 3)) * 64 + k.ci) * 8 + (k.o0 & 7);
+  if (k.kind == 2) k.poff = P_W2 + ((k.j * 8 + (k.o0 >> 3)) * 32 + k.ci) * 8 + (k.o0 & 7);
   if (k.kind == 1) k.poff = P_SM + k.s0;
   return k;
 }
@@ -373,38 +413,6 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
   }
 }
 
-// fc1 column block of this owner: [128 n][NC cols]; lane element (tile t, e) = (n = 16 w + 4 g + e, col 16 t + i)
-template <int T>
-__device__ __forceinline__ void publish_fc1(const Ctx& x, int i, const TowerState<T>& st) {
-  using C = TW<T>;
-  uchar* S = x.smem;
-  const int g = x.lane >> 4, li = x.lane & 15;
-  constexpr int NT1 = C::NC / 16, LW = C::NC + 8;
-#pragma unroll
-  for (int t = 0; t < NT1; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) *lu16(S, O_SW + ((16 * x.wave + 4 * g + e) * LW + 16 * t + li) * 2) = bfu(st.p1[t][e]);
-  __syncthreads();
-  const int c0 = C::COL0 + i * C::NC;
-  constexpr int PR = C::NC / 8;  // 16-B pieces per W1 row segment
-  for (int e = x.tid; e < 128 * PR; e += NTH) {
-    const int n = e / PR, pc = e % PR;
-    const u32x4 v = *(const LDS_AS u32x4*)(S + O_SW + (n * LW + 8 * pc) * 2);
-    st16(x.rw, WS_IMG + (IM_W1 + n * 1024 + c0 + 8 * pc) * 2, v);
-  }
-  for (int e = x.tid; e < C::NC * 16; e += NTH) {  // W1T [col][n]: 16 pieces of 8 n per column
-    const int col = e >> 4, pc = e & 15;
-    uint32_t w[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const unsigned short lo = *lu16(S, O_SW + ((8 * pc + 2 * h) * LW + col) * 2);
-      const unsigned short hi = *lu16(S, O_SW + ((8 * pc + 2 * h + 1) * LW + col) * 2);
-      w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
-    }
-    st16(x.rw, WS_IMG + (IM_W1T + (c0 + col) * 128 + 8 * pc) * 2, u32x4{w[0], w[1], w[2], w[3]});
-  }
-}
-
 template <int T>
 __device__ __forceinline__ void tower(const Ctx& x, int i) {
   using C = TW<T>;
@@ -428,42 +436,46 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     mv_st(x, u, Z4, Z4);
   }
-  const int c0w = C::COL0 + i * C::NC;
-#pragma unroll
-  for (int t = 0; t < C::NC / 16; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      st.p1[t][e] = P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0w + 16 * t + li];
-    }
-#pragma unroll
-  for (int t = 0; t < C::NC / 16; ++t) mv_st(x, 4 + t, Z4, Z4);
   __syncthreads();
   publish_conv<T>(x, i, st);
-  __syncthreads();
-  publish_fc1<T>(x, i, st);
   arrive(x, CT_W + T);
   __syncthreads();
   // re-zero the staging the publishers used (rows 0.. of H1 / H2 / H3)
   for (int e = tid; e < O_XS / 16; e += NTH) *(LDS_AS u32x4*)(S + 16 * e) = u32x4{0u, 0u, 0u, 0u};
 
   const int min_bs = a.min_bs;
+  // the next active step at or after s0 (a.S: none), and this thread's input value of a step (x rows of the
+  // read-only table: prefetched one step ahead, during the backward)
+  auto next_active = [&](int s0) -> int {
+    int s2 = s0;
+    for (; s2 < a.S; ++s2) {
+      const int b2 = a.bsz[(long)s2 * a.C + c];
+      if (b2 >= min_bs && b2 >= 1) break;
+    }
+    return s2;
+  };
+  auto load_x = [&](int s2) -> float {
+    if (s2 >= a.S || tid >= C::R * C::L) return 0.f;
+    const int r = tid / C::L, l = tid - r * C::L, b = b0 + r;
+    const int row = b < B ? a.idx[((long)s2 * a.C + c) * B + b] : -1;
+    return row >= 0 ? a.rows[(long)row * 24 + C::XOFF + l] : 0.f;
+  };
+  float xv_next = load_x(next_active(0));
   int kact = 0;
   bool alive = true;
   for (int s = 0; s < a.S && alive; ++s) {
     const int bs = a.bsz[(long)s * a.C + c];
     if (bs < min_bs || bs < 1) continue;
-    if (!wait_ge(x, CT_W + T, (uint32_t)(C::NTW * (kact + 1)), O_FLAG)) break;
+    const float xv = xv_next;
+    // this step's conv images (tower group) and fc1 images (fc1 owners: normally long done), one poll
+    if (!wait_ge2(x, CT_W + T, (uint32_t)(C::NTW * (kact + 1)), CT_W1R, (uint32_t)(NFC1 * (kact + 1)), O_FLAG)) break;
     REOPQ();
+    stamp(x, kact, 0);
     // ------------------------------------------------------------------------------ forward
-    // step inputs: x rows (plain loads: the table is read-only), conv1 weights / biases (fp32 smalls)
-    const int* idxs = a.idx + ((long)s * a.C + c) * B;
-    float xv = 0.f;
+    // step inputs: x (prefetched), conv1 weights / biases (fp32 smalls)
     int xq = -1;
     if (tid < C::R * C::L) {
       const int r = tid / C::L, l = tid - r * C::L;
-      const int b = b0 + r;
-      const int row = b < B ? idxs[b] : -1;
-      xv = row >= 0 ? a.rows[(long)row * 24 + C::XOFF + l] : 0.f;
       xq = r * C::LP + 1 + l;
     }
     const int o1 = tid & 31;
@@ -511,6 +523,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       *lu16(S, O_H1 + ((q + 1) * LD1 + o1) * 2) = bfu(h);
     }
     SYNC();
+    stamp(x, kact, 7);
     // conv2: H2[q][o] = relu(b2 + sum_j H1[q - 1 + j] . W2_j^T); wave: n-tile nt2, m-tiles mp2, mp2 + 2, ...
     for (int mt = mp2; mt < 9; mt += 2) {
       f4v acc = Z4;
@@ -537,38 +550,65 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         *lu16(S, O_H3 + ((q + 1) * LD3 + 16 * wave + li) * 2) = bfu(v);
       }
     }
-    // fc1 B fragments (this tower's half of W1, n-tile = wave), in flight during the pooling
+    // fc1 B fragments (this tower's half of W1, n-tile = wave; the owners' images of this step), in flight during
+    // the pooling
+    const int par = kact & 1;
     s8v wf1[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) wf1[k] = ld16s(x.rw, WS_IMG + (IM_W1 + (16 * wave + li) * 1024 + C::COL0 + 32 * k + 8 * g) * 2);
+    for (int k = 0; k < 16; ++k)
+      wf1[k] = ld16s(x.rw, WS_IMG + (IM_W1 + par * IM_FC1PAR + (16 * wave + li) * 1024 + C::COL0 + 32 * k + 8 * g) * 2);
     SYNC();
-    // AdaptiveAvgPool1d(4) + dropout -> feat (LDS bf16 rows 0..15, zero past R) and the global concat
+    stamp(x, kact, 8);
+    // AdaptiveAvgPool1d(4) + dropout -> feat (LDS bf16 rows 0..15, zero past R) and the global concat.  Thread:
+    // (row r, channel pair cp) = 8 concat columns 8 cp .. 8 cp + 7: the channel pair moves as one dword per
+    // position, the bins are compile-time, the 8 keep bits (4 hashes) are kept as one LDS byte for the backward
     const bool dr = a.thr16 != 0;
     const uint32_t key = dr ? afl_hash32(a.seeds[c], (uint32_t)s) : 0u;
-    for (int e = tid; e < 16 * 64; e += NTH) {  // (row r, channel pair cp): 8 concat columns
-      const int r = e >> 6, cp = e & 63;
+#pragma unroll
+    for (int it = 0; it < 16 * 64 / NTH; ++it) {
+      const int e = tid + NTH * it, r = e >> 6, cp = e & 63;
       float f[8];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ch = 2 * cp + h;
+      for (int k = 0; k < 8; ++k) f[k] = 0.f;
+      if (r < C::R) {
+        float h0[C::L], h1v[C::L];
+#pragma unroll
+        for (int l = 0; l < C::L; ++l) {
+          const uint32_t w = *(const LDS_AS uint32_t*)(S + O_H3 + ((r * C::LP + 2 + l) * LD3 + 2 * cp) * 2);
+          h0[l] = __uint_as_float(w << 16);
+          h1v[l] = __uint_as_float(w & 0xFFFF0000u);
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          float sum = 0.f;
-          if (r < C::R) {
-            const int lo = bin_lo(p, C::L), hi = bin_hi(p, C::L);
-            for (int l = lo; l < hi; ++l) sum += bff(*lu16(S, O_H3 + ((r * C::LP + 2 + l) * LD3 + ch) * 2));
-            sum /= (float)(hi - lo);
-            const int col = C::COL0 + ch * 4 + p;
-            if (dr) sum *= afl_keep(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)col, a.thr16) ? a.inv_keep : 0.f;
+          float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+          for (int l = bin_lo(p, C::L); l < bin_hi(p, C::L); ++l) {
+            s0 += h0[l];
+            s1 += h1v[l];
           }
-          f[4 * h + p] = sum;
+          f[p] = s0 * bin_rcp(p, C::L);
+          f[4 + p] = s1 * bin_rcp(p, C::L);
         }
+        uint32_t kb = 0xFFu;
+        if (dr) {
+          kb = 0u;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t hsh = afl_hash4(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)((C::COL0 + 8 * cp) / 2 + k));
+            kb |= ((hsh & 0xFFFFu) >= a.thr16 ? 1u : 0u) << (2 * k);
+            kb |= ((hsh >> 16) >= a.thr16 ? 1u : 0u) << (2 * k + 1);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] *= ((kb >> k) & 1u) ? a.inv_keep : 0.f;
+        }
+        *(LDS_AS uchar*)(S + O_RED + R_KEEP * 4 + r * 64 + cp) = (uchar)kb;
       }
       const u32x4 pkd = u32x4{pk2(f[0], f[1]), pk2(f[2], f[3]), pk2(f[4], f[5]), pk2(f[6], f[7])};
       *(LDS_AS u32x4*)(S + O_FT + (r * LDF + 8 * cp) * 2) = pkd;
-      if (r < C::R) st16(x.rw, WS_FEAT + ((b0 + r) * 1024 + C::COL0 + 8 * cp) * 2, pkd);
+      if (r < C::R) st16(x.rw, WS_FEAT + par * FEAT_PAR + ((b0 + r) * 1024 + C::COL0 + 8 * cp) * 2, pkd);
     }
     SYNC();
+    stamp(x, kact, 9);
     // fc1 partial over this tower's 512 features: z1p[rows][n], wave = n-tile
     {
       f4v acc = Z4;
@@ -585,14 +625,18 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     arrive(x, CT_F);
     REOPQ();
+    stamp(x, kact, 1);
+    xv_next = load_x(next_active(s + 1));
     // d(concat) B fragments (W1T, this tower's columns: n-tiles 4 w .. 4 w + 3) in flight during the wait
     s8v wt1[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      wt1[k] = ld16s(x.rw, WS_IMG + (IM_W1T + (C::COL0 + 16 * (4 * wave + (k >> 2)) + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
+      wt1[k] = ld16s(x.rw, WS_IMG + (IM_W1T + par * IM_FC1PAR + (C::COL0 + 16 * (4 * wave + (k >> 2)) + li) * 128 +
+                                    32 * (k & 3) + 8 * g) * 2);
     // ------------------------------------------------------------------------------ backward
     if (!wait_ge(x, CT_H, (uint32_t)(kact + 1), O_FLAG)) break;
     REOPQ();
+    stamp(x, kact, 2);
     {
       const u32x4 stt = ld16(x.rw, WS_STAT);
       if (stt[0] != 0u) {  // NaN loss: the client's round ends here without an update (the head saw it too)
@@ -629,34 +673,48 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     for (int k = 0; k < 12; ++k)
       w3t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3T + ((k >> 2) * 64 + 16 * nb2 + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
     SYNC();
-    // pooled gradient: gs[r][col] = dropout'(dfeat) / |bin|, in place
-    for (int e = tid; e < C::R * 512; e += NTH) {
-      const int r = e >> 9, col = e & 511, p = col & 3;
-      LDS_AS float* d = lf(S, O_FT + (r * 516 + col) * 4);
-      float gv = *d / (float)(bin_hi(p, C::L) - bin_lo(p, C::L));
-      if (dr) gv *= afl_keep(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)(C::COL0 + col), a.thr16) ? a.inv_keep : 0.f;
-      *d = gv;
-    }
-    SYNC();
-    // dh3 = relu'(h3) * pool'(gs), in place over H3 (bf16); conv3 bias partial (fp32) per (row group, channel)
-    {
-      const int ch = tid & 127, rg = tid >> 7;
-      float bsum = 0.f;
-      for (int q = rg; q < 144; q += 4) {
-        float v = 0.f;
-        const int r = q / C::LP, l = q - r * C::LP - 1;
-        LDS_AS unsigned short* hp = lu16(S, O_H3 + ((q + 1) * LD3 + ch) * 2);
-        if (l >= 0 && l < C::L && bff(*hp) > 0.f) {
+    stamp(x, kact, 10);
+    // dh3 = relu'(h3) * pool'(dropout'(dfeat)), in place over H3 (bf16).  Thread: (row r, channel pair cp) like the
+    // forward pooling (keep byte from the forward, compile-time bins); conv3 bias partials per (row group, channel)
+    float b0s = 0.f, b1s = 0.f;
+    const int cp = tid & 63;
 #pragma unroll
-          for (int p = 0; p < 4; ++p)
-            if (l >= bin_lo(p, C::L) && l < bin_hi(p, C::L)) v += *lf(S, O_FT + (r * 516 + ch * 4 + p) * 4);
-        }
-        *hp = bfu(v);
-        bsum += v;
+    for (int it = 0; it < C::R * 64 / NTH; ++it) {
+      const int r = (tid >> 6) + 8 * it;
+      const uint32_t kb = *(const LDS_AS uchar*)(S + O_RED + R_KEEP * 4 + r * 64 + cp);
+      const f4v d0 = *(const LDS_AS f4v*)(S + O_FT + (r * 516 + 8 * cp) * 4);
+      const f4v d1 = *(const LDS_AS f4v*)(S + O_FT + (r * 516 + 8 * cp + 4) * 4);
+      float gq[8];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        gq[p] = d0[p] * bin_rcp(p, C::L);
+        gq[4 + p] = d1[p] * bin_rcp(p, C::L);
       }
-      *lf(S, O_RED + (R_DB3 + rg * 128 + ch) * 4) = bsum;
+      if (dr) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gq[k] *= ((kb >> k) & 1u) ? a.inv_keep : 0.f;
+      }
+#pragma unroll
+      for (int l = 0; l < C::L; ++l) {
+        float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          if (l >= bin_lo(p, C::L) && l < bin_hi(p, C::L)) {
+            v0 += gq[p];
+            v1 += gq[4 + p];
+          }
+        LDS_AS uint32_t* hp = (LDS_AS uint32_t*)(S + O_H3 + ((r * C::LP + 2 + l) * LD3 + 2 * cp) * 2);
+        const uint32_t w = *hp;
+        v0 = __uint_as_float(w << 16) > 0.f ? v0 : 0.f;
+        v1 = __uint_as_float(w & 0xFFFF0000u) > 0.f ? v1 : 0.f;
+        *hp = pk2(v0, v1);
+        b0s += v0;
+        b1s += v1;
+      }
     }
+    *(LDS_AS f2v*)(S + O_RED + (R_DB3 + (tid >> 6) * 128 + 2 * cp) * 4) = f2v{b0s, b1s};
     SYNC();
+    stamp(x, kact, 11);
     // dh2 = relu'(h2) * sum_j shift_{1-j}(dh3) . W3_j  (K = 3 x 128): wave n-tile nb2, m-tiles mpb, mpb + 2, ..
     {
       float cs = 0.f;
@@ -685,6 +743,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     for (int k = 0; k < 6; ++k)
       w2t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W2T + ((k >> 1) * 32 + 16 * nb1 + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
     SYNC();
+    stamp(x, kact, 12);
     // dh1 = relu'(h1) * sum_j shift_{1-j}(dh2) . W2_j (K = 3 x 64), straight into the conv1 gradients
     {
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, sb = 0.f;
@@ -730,7 +789,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
       for (int t = 0; t < 12; ++t) {
         const int j = t >> 2, ci = 16 * (t & 3) + li;
-        st16f(x.rw, pbase + (P_W3 + (j * 64 + ci) * 128 + 16 * wave + 4 * g) * 4, acc[t]);
+        st16f(x.rw, pbase + (P_W3 + ((j * 16 + 2 * wave + (g >> 1)) * 64 + ci) * 8 + 4 * (g & 1)) * 4, acc[t]);
       }
     }
     // dW2_j = dh2^T . shift_{j-1}(h1): wave -> o-tile (w & 3), ci-tile (w >> 2)
@@ -744,9 +803,10 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        st16f(x.rw, pbase + (P_W2 + (j * 32 + 16 * ct + li) * 64 + 16 * ot + 4 * g) * 4, acc[j]);
+        st16f(x.rw, pbase + (P_W2 + ((j * 8 + 2 * ot + (g >> 1)) * 32 + 16 * ct + li) * 8 + 4 * (g & 1)) * 4, acc[j]);
     }
     SYNC();
+    stamp(x, kact, 13);
     // small partials: conv1 W [o][j] (96) | conv1 b (32) | conv2 b (64) | conv3 b (128), waves summed in order
     if (tid < NSMALL) {
       float v = 0.f;
@@ -759,8 +819,8 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         v = *lf(S, O_RED + (R_DB2 + (o >> 4) * 16 + (o & 15)) * 4) + *lf(S, O_RED + (R_DB2 + ((o >> 4) + 4) * 16 + (o & 15)) * 4);
       } else {
         const int o = tid - 192;
-        v = (*lf(S, O_RED + (R_DB3 + o) * 4) + *lf(S, O_RED + (R_DB3 + 128 + o) * 4)) +
-            (*lf(S, O_RED + (R_DB3 + 256 + o) * 4) + *lf(S, O_RED + (R_DB3 + 384 + o) * 4));
+#pragma unroll
+        for (int rg = 0; rg < 8; ++rg) v += *lf(S, O_RED + (R_DB3 + 128 * rg + o) * 4);
       }
       *lf(S, O_RED + (R_SM + tid) * 4) = v;
     }
@@ -768,23 +828,10 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     if (tid < NSMALL / 4) st16f(x.rw, pbase + (P_SM + 4 * tid) * 4, *(const LDS_AS f4v*)(S + O_RED + (R_SM + 4 * tid) * 4));
     arrive(x, CT_P + T);
     REOPQ();
-    // d1 (all rows) and this owner's feature columns, for the fc1 block gradient: loads in flight across the wait
-    u32x4 d1v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
-      d1v[u] = ld16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2);
-    }
-    constexpr int FPR = C::NC / 8;  // 16-B pieces per feature row
-    constexpr int NFU = 128 * FPR / NTH;
-    u32x4 fv[NFU];
-#pragma unroll
-    for (int u = 0; u < NFU; ++u) {
-      const int e = tid + NTH * u, r = e / FPR, pc = e % FPR;
-      fv[u] = ld16(x.rw, WS_FEAT + (r * 1024 + c0w + 8 * pc) * 2);
-    }
+    stamp(x, kact, 3);
     if (!wait_ge(x, CT_P + T, (uint32_t)(C::NTW * (kact + 1)), O_FLAG)) break;
     REOPQ();
+    stamp(x, kact, 4);
     // ------------------------------------------------------------------ owner: conv blocks
     const AdamT ak = adam_t(a.lr, kact + 1);
     {
@@ -796,18 +843,17 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         gsum[u] = Z4;
         mv_ld(x, u, mm[u], vv[u]);
       }
-      // partials summed in workgroup order; loads batched 4 at a time
+      // every partial chunk of the owned slots in flight at once (owned-less slots read chunk 0 and drop it),
+      // then summed in workgroup order
+      f4v pv[C::NS][C::NTW];
 #pragma unroll
-      for (int u = 0; u < C::NS; ++u) {
-        if (ks[u].kind == 0) continue;
-        for (int n0 = 0; n0 < C::NTW; n0 += 4) {
-          f4v pv[4];
+      for (int u = 0; u < C::NS; ++u)
 #pragma unroll
-          for (int n = 0; n < 4; ++n) pv[n] = ld16f(x.rw, WS_PART + ((C::FIRST + n0 + n) * PSZ + ks[u].poff) * 4);
+        for (int n = 0; n < C::NTW; ++n) pv[u][n] = ld16f(x.rw, WS_PART + ((C::FIRST + n) * PSZ + ks[u].poff) * 4);
 #pragma unroll
-          for (int n = 0; n < 4; ++n) gsum[u] += pv[n];
-        }
-      }
+      for (int u = 0; u < C::NS; ++u)
+#pragma unroll
+        for (int n = 0; n < C::NTW; ++n) gsum[u] += pv[u][n];
 #pragma unroll
       for (int u = 0; u < C::NS; ++u) {
         if (ks[u].kind == 0) continue;
@@ -823,46 +869,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     publish_conv<T>(x, i, st);
     REOPQ();
-    // ------------------------------------------------------------------ owner: fc1 column block
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
-      *(LDS_AS u32x4*)(S + O_D1F + (r * LDD + 8 * pc) * 2) = d1v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < NFU; ++u) {
-      const int e = tid + NTH * u, r = e / FPR, pc = e % FPR;
-      *(LDS_AS u32x4*)(S + O_FW + (r * 72 + 8 * pc) * 2) = fv[u];
-    }
-    SYNC();
-    {
-      constexpr int NT1 = C::NC / 16;
-      f4v acc[NT1], m1[NT1], v1[NT1];
-#pragma unroll
-      for (int t = 0; t < NT1; ++t) mv_ld(x, 4 + t, m1[t], v1[t]);
-#pragma unroll
-      for (int t = 0; t < NT1; ++t) acc[t] = Z4;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const s8v af = cfrag(S + O_D1F, LDD, 32 * ks, 16 * wave, lane);
-#pragma unroll
-        for (int t = 0; t < NT1; ++t) acc[t] = mfma(af, cfrag(S + O_FW, 72, 32 * ks, 16 * t, lane), acc[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < NT1; ++t) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float me = m1[t][e], ve = v1[t][e];
-          st.p1[t][e] = adam1(st.p1[t][e], me, ve, acc[t][e], ak.a, ak.sb);
-          m1[t][e] = me;
-          v1[t][e] = ve;
-        }
-        mv_st(x, 4 + t, m1[t], v1[t]);
-      }
-    }
-    SYNC();
-    publish_fc1<T>(x, i, st);
+    stamp(x, kact, 5);
     arrive(x, CT_W + T);
+    stamp(x, kact, 6);
     ++kact;
   }
   // ---------------------------------------------------------------- round end: owned parameters -> arena
@@ -873,10 +882,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) P[elem_idx<T>(a, k, e)] = st.p[u][e];
   }
-#pragma unroll
-  for (int t = 0; t < C::NC / 16; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0w + 16 * t + li] = st.p1[t][e];
 }
 
 // ============================================================================================== head
@@ -982,6 +987,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     const float yv = yrow >= 0 ? a.rows[(long)yrow * 24 + 23] : 0.f;
     if (!wait_ge(*&x, CT_F, (uint32_t)(24 * (kact + 1)), H_FLAG)) break;
     REOPQ();
+    stamp(x, kact, 0);
     // z1 = z1p_vitals + z1p_labs (+ b1, ReLU) -> f1s; thread: row b = (tid + 512 q) >> 5, columns i1 .. i1 + 3
     const int i1 = 4 * (tid & 31);
     {
@@ -1151,19 +1157,6 @@ __device__ __forceinline__ void head(const Ctx& x) {
       for (int w = 0; w < 8; ++w) sb += gbw[w * 192 + tid];
       sums[tid] = sb;  // gb2
     }
-    // dW2 [64 x 128] = d2^T f1 (registers)
-    f4v g2[4];
-    {
-      const int o0 = (wave >> 1) * 16, ib = (wave & 1) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g2[j] = Z4;
-#pragma unroll
-      for (int k0 = 0; k0 < 128; k0 += 32) {
-        const s8v af = cfrag(S + H_D2S, H_L2, k0, o0, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) g2[j] = mfma(af, cfrag(S + H_F1S, H_L1, k0, 16 * (ib + j), lane), g2[j]);
-      }
-    }
     SYNC();  // U (f2s / f3f / d3s) is dead: d1 staging
     // d1 = d2 . W2 * relu'(f1) -> bf16 staging; gb1 per wave
     {
@@ -1203,6 +1196,20 @@ __device__ __forceinline__ void head(const Ctx& x) {
     }
     arrive(x, CT_H);
     REOPQ();
+    stamp(x, kact, 1);
+    // dW2 [64 x 128] = d2^T f1 (registers; after the d1 hand-off: off the critical path)
+    f4v g2[4];
+    {
+      const int o0 = (wave >> 1) * 16, ib = (wave & 1) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g2[j] = Z4;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        const s8v af = cfrag(S + H_D2S, H_L2, k0, o0, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g2[j] = mfma(af, cfrag(S + H_F1S, H_L1, k0, 16 * (ib + j), lane), g2[j]);
+      }
+    }
     // Adam on the head parameters (off the critical path: the towers run their backward meanwhile)
     const AdamT ak = adam_t(a.lr, kact + 1);
     {
@@ -1238,6 +1245,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     SYNC();
     put_state();
     SYNC();
+    stamp(x, kact, 2);
     ++kact;
   }
   // round end: parameters -> arena
@@ -1248,6 +1256,122 @@ __device__ __forceinline__ void head(const Ctx& x) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) P[oW3 + (o3b + e) * 64 + i3] = p3[e];
   if (tid < 257) P[vidx(tid)] = pv;
+}
+
+// ============================================================================================= fc1 owners
+// Workgroup j (0..6) owns fc1 weight columns [144 j, 144 j + 16 nt) (nt = 9 column tiles, 10 for the last):
+// dW1 = d1^T . feat over the batch rows (K = 128), Adam with the weights in registers (lane element (tile t, e) =
+// (n = 16 w + 4 g + e, column 16 (9 j + t) + li)), and the block republished as bf16 W1 / W1T images of the
+// NEXT step's parity.  Runs beside the towers' backward: off the step's critical path.
+constexpr int F_LDF = 168;                          // feature block rows: up to 160 columns + 8
+constexpr int F_D1 = 0, F_FW = 128 * LDD * 2, F_SW = F_FW + 128 * F_LDF * 2, F_FLAG = F_SW + 128 * F_LDF * 2;
+static_assert(F_FLAG + 16 <= T_LDS, "fc1 owner LDS");
+
+__device__ __forceinline__ void fc1_publish(const Ctx& x, int tid, int c0, int ntl, int par, const float (&p)[10][4]) {
+  uchar* S = x.smem;
+  const int lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+    if (t < ntl)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *lu16(S, F_SW + ((16 * wave + 4 * g + e) * F_LDF + 16 * t + li) * 2) = bfu(p[t][e]);
+  __syncthreads();
+  const int ncol = 16 * ntl, pr = ncol / 8;
+  for (int e = tid; e < 128 * pr; e += NTH) {  // W1 [n][1024]: pr pieces of 8 columns per row
+    const int n = e / pr, pc = e % pr;
+    st16(x.rw, WS_IMG + (IM_W1 + par * IM_FC1PAR + n * 1024 + c0 + 8 * pc) * 2,
+         *(const LDS_AS u32x4*)(S + F_SW + (n * F_LDF + 8 * pc) * 2));
+  }
+  for (int e = tid; e < ncol * 16; e += NTH) {  // W1T [1024][n]: 16 pieces of 8 n per column
+    const int col = e >> 4, pc = e & 15;
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const unsigned short lo = *lu16(S, F_SW + ((8 * pc + 2 * h) * F_LDF + col) * 2);
+      const unsigned short hi = *lu16(S, F_SW + ((8 * pc + 2 * h + 1) * F_LDF + col) * 2);
+      w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
+    }
+    st16(x.rw, WS_IMG + (IM_W1T + par * IM_FC1PAR + (c0 + col) * 128 + 8 * pc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+  }
+}
+
+__device__ __forceinline__ void fc1_owner(const Ctx& x, int j) {
+  const AflCnn2Args& a = *x.a;
+  uchar* S = x.smem;
+  int tid = x.tid, lane = x.lane, wave = x.wave, g = lane >> 4, li = lane & 15;
+  const int c = x.c;
+  float* P = a.params + (long)c * a.pstride;
+  const int ntl = j == NFC1 - 1 ? 10 : 9, c0 = 144 * j;
+  float p[10][4];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[t][e] = t < ntl ? P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0 + 16 * t + li] : 0.f;
+    mv_st(x, t, Z4, Z4);
+  }
+  fc1_publish(x, tid, c0, ntl, 0, p);
+  arrive(x, CT_W1R);
+  const int min_bs = a.min_bs;
+  int kact = 0;
+  for (int s = 0; s < a.S; ++s) {
+    const int bs = a.bsz[(long)s * a.C + c];
+    if (bs < min_bs || bs < 1) continue;
+    const int par = kact & 1;
+    if (!wait_ge(x, CT_H, (uint32_t)(kact + 1), F_FLAG)) break;
+    REOPQ();
+    stamp(x, kact, 0);
+    if (ld16(x.rw, WS_STAT)[0] != 0u) break;  // NaN loss: the client's round ends without an update
+    // d1 (all rows) and this block's feature columns -> LDS
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
+      *(LDS_AS u32x4*)(S + F_D1 + (r * LDD + 8 * pc) * 2) = ld16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2);
+    }
+    const int pr = 2 * ntl;  // 16-B pieces per feature row
+    for (int e = tid; e < 128 * pr; e += NTH) {
+      const int r = e / pr, pc = e % pr;
+      *(LDS_AS u32x4*)(S + F_FW + (r * F_LDF + 8 * pc) * 2) =
+          ld16(x.rw, WS_FEAT + par * FEAT_PAR + (r * 1024 + c0 + 8 * pc) * 2);
+    }
+    f4v m[10], v[10];  // moments in flight during the staging barrier and the MFMAs (off the critical path)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) mv_ld(x, t, m[t], v[t]);
+    SYNC();
+    f4v acc[10];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) acc[t] = Z4;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const s8v af = cfrag(S + F_D1, LDD, 32 * ks, 16 * wave, lane);
+#pragma unroll
+      for (int t = 0; t < 10; ++t)
+        if (t < ntl) acc[t] = mfma(af, cfrag(S + F_FW, F_LDF, 32 * ks, 16 * t, lane), acc[t]);
+    }
+    const AdamT ak = adam_t(a.lr, kact + 1);
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      if (t >= ntl) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float me = m[t][e], ve = v[t][e];
+        p[t][e] = adam1(p[t][e], me, ve, acc[t][e], ak.a, ak.sb);
+        m[t][e] = me;
+        v[t][e] = ve;
+      }
+      mv_st(x, t, m[t], v[t]);
+    }
+    SYNC();
+    fc1_publish(x, tid, c0, ntl, par ^ 1, p);
+    arrive(x, CT_W1R);
+    REOPQ();
+    stamp(x, kact, 1);
+    ++kact;
+  }
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+    if (t < ntl)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) P[a.off[12] + (16 * wave + 4 * g + e) * 1024 + c0 + 16 * t + li] = p[t][e];
 }
 
 __global__ void __launch_bounds__(NTH) k_cnn2_train(AflCnn2Args a) {
@@ -1271,7 +1395,9 @@ __global__ void __launch_bounds__(NTH) k_cnn2_train(AflCnn2Args a) {
 #elif defined(CNN2_ONLY_LAB)
   tower<1>(x, role - 8);
 #else
-  if (role == WG_HEAD)
+  if (role >= WG_FC1)
+    fc1_owner(x, role - WG_FC1);
+  else if (role == WG_HEAD)
     head(x);
   else if (role < 8)
     tower<0>(x, role);

@@ -656,7 +656,8 @@ void attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, torch::Tens
 // over the step tables of fl/programs.py:step_tables; ws / ctr from cnn2_ws_bytes / cnn2_ctr_words (ctr zeroed)
 void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor rows, torch::Tensor idx, torch::Tensor bsz,
                 torch::Tensor epoch, torch::Tensor nb, torch::Tensor seeds, double p, int64_t min_bs, bool nan_abort,
-                double lr, torch::Tensor failed, torch::Tensor losses, torch::Tensor ws, torch::Tensor ctr) {
+                double lr, torch::Tensor failed, torch::Tensor losses, torch::Tensor ws, torch::Tensor ctr,
+                c10::optional<torch::Tensor> stamps) {
   dense(params, "params");
   dense(rows, "rows");
   dense(idx, "idx", torch::kInt32);
@@ -705,6 +706,11 @@ void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor r
   a.ws = ws.data_ptr();
   a.ws_stride = afl_cnn2_ws_bytes();
   a.ctr = (uint32_t*)ctr.data_ptr<int>();
+  if (stamps.has_value() && stamps->defined()) {
+    dense(*stamps, "stamps", torch::kInt64);
+    TORCH_CHECK(stamps->numel() >= (int64_t)C * afl_cnn2_wgs_per_client() * 64 * 16, "cnn2_train: stamps too small");
+    a.stamps = (uint64_t*)stamps->data_ptr<int64_t>();
+  }
   ok(afl_cnn2_train(a, cur()), "cnn2_train");
 }
 
@@ -728,7 +734,9 @@ void afl_register_layers(pybind11::module& m) {
   m.def("conv_dw", &conv_dw);
   m.def("cnn_head", &cnn_head);
   m.def("cnn_wimg_size", &afl_cnn_wimg_ushorts);
-  m.def("cnn2_train", &cnn2_train);
+  m.def("cnn2_train", &cnn2_train, py::arg("params"), py::arg("offs"), py::arg("rows"), py::arg("idx"), py::arg("bsz"),
+        py::arg("epoch"), py::arg("nb"), py::arg("seeds"), py::arg("p"), py::arg("min_bs"), py::arg("nan_abort"),
+        py::arg("lr"), py::arg("failed"), py::arg("losses"), py::arg("ws"), py::arg("ctr"), py::arg("stamps") = none);
   m.def("cnn2_ws_bytes", &afl_cnn2_ws_bytes);
   m.def("cnn2_ctr_words", &afl_cnn2_ctr_words);
   m.def("cnn2_wgs_per_client", &afl_cnn2_wgs_per_client);
