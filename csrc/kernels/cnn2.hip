@@ -41,6 +41,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef __bf16 b2v __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 #define LDS_AS __attribute__((address_space(3)))
 #define GAS __attribute__((address_space(1)))
 typedef GAS uint32_t gu32;
@@ -113,6 +114,10 @@ __device__ __forceinline__ f4v ld16f(__amdgpu_buffer_rsrc_t rs, int byte_off) {
 __device__ __forceinline__ s8v ld16s(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   return __builtin_bit_cast(s8v, ld16(rs, byte_off));
 }
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its outstanding global loads
+// (__syncthreads() drains vmcnt too, which stalled every barrier behind the operand prefetches issued before it).
+// Global data written by the workgroup is published only through arrive(), which drains explicitly.
+__device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // Phase entry: the lane / wave indices become opaque, so every per-lane address of a phase is computed inside
 // it (otherwise the compiler hoists the hundreds of swizzled LDS / image addresses of the step out of the loop
 // and keeps them live across all phases, spilling to scratch)
@@ -130,7 +135,7 @@ __device__ __forceinline__ s8v ld16s(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   } while (0)
 #define SYNC()        \
   do {                \
-    __syncthreads();  \
+    lbar();  \
     REOPQ();          \
   } while (0)
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -203,9 +208,9 @@ __device__ __forceinline__ bool wait_ge2(const Ctx& x, int which, uint32_t targe
     }
     fl[0] = ok;
   }
-  __syncthreads();
+  lbar();
   const int ok = fl[0];
-  __syncthreads();
+  lbar();
   return ok != 0;
 }
 // true when the counter reached `target`; false (all threads) on the deadline
@@ -225,9 +230,9 @@ __device__ __forceinline__ bool wait_ge(const Ctx& x, int which, uint32_t target
     }
     fl[0] = ok;
   }
-  __syncthreads();
+  lbar();
   const int ok = fl[0];
-  __syncthreads();  // fl is rewritten by the next wait
+  lbar();  // fl is rewritten by the next wait
   return ok != 0;
 }
 
@@ -366,7 +371,7 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
       st16f(x.rw, WS_SMALL + (T * NSMALL + k.s0) * 4, f4v{st.p[u][0], st.p[u][1], st.p[u][2], st.p[u][3]});
     }
   }
-  __syncthreads();
+  lbar();
   constexpr int NB3 = T == 0 ? 2 : 1;
   const bool has2 = T == 0 || i < 8;
   // W3T [j][ci][o]: one 16-B piece (8 o) per (blk, j, ci); W3 [j][o][ci]: 8 pieces (64 ci) per (blk, j, o)
@@ -436,10 +441,10 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     mv_st(x, u, Z4, Z4);
   }
-  __syncthreads();
+  lbar();
   publish_conv<T>(x, i, st);
   arrive(x, CT_W + T);
-  __syncthreads();
+  lbar();
   // re-zero the staging the publishers used (rows 0.. of H1 / H2 / H3)
   for (int e = tid; e < O_XS / 16; e += NTH) *(LDS_AS u32x4*)(S + 16 * e) = u32x4{0u, 0u, 0u, 0u};
 
@@ -496,10 +501,10 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
     for (int k = 0; k < 6; ++k)
       w3f[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3 + ((k >> 1) * 128 + 16 * wave + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
-    const float b2v = __builtin_bit_cast(
-        float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, WS_SMALL + (T * NSMALL + 128 + 16 * nt2 + li) * 4, 0, 16));
-    const float b3v = __builtin_bit_cast(
-        float, __builtin_amdgcn_raw_buffer_load_b32(x.rw, WS_SMALL + (T * NSMALL + 192 + 16 * wave + li) * 4, 0, 16));
+    // (the conv GEMMs run transposed, D[o][q] = W . H^T: a lane ends with 4 consecutive channels of one position,
+    // stored as one 8-byte LDS write; its 4 biases come as one 16-byte load)
+    const f4v b2v = ld16f(x.rw, WS_SMALL + (T * NSMALL + 128 + 16 * nt2 + 4 * g) * 4);
+    const f4v b3v = ld16f(x.rw, WS_SMALL + (T * NSMALL + 192 + 16 * wave + 4 * g) * 4);
     // boundary rows of the activation buffers back to zero (the owner phases stage through them)
     for (int e = tid; e < 18 * 4; e += NTH) {
       const int rr = e % 18, buf = e / 18;
@@ -528,13 +533,13 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     for (int mt = mp2; mt < 9; mt += 2) {
       f4v acc = Z4;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) acc = mfma(rfrag(S + O_H1, LD1, 16 * mt + j, 0, lane), w2f[j], acc);
+      for (int j = 0; j < 3; ++j) acc = mfma(w2f[j], rfrag(S + O_H1, LD1, 16 * mt + j, 0, lane), acc);
+      const int q = 16 * mt + li;
+      const bool ok = valid_q(q, C::LP);
+      float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = 16 * mt + 4 * g + e;
-        const float v = valid_q(q, C::LP) ? relu(acc[e] + b2v) : 0.f;
-        *lu16(S, O_H2 + ((q + 1) * LD2 + 16 * nt2 + li) * 2) = bfu(v);
-      }
+      for (int e = 0; e < 4; ++e) v[e] = ok ? relu(acc[e] + b2v[e]) : 0.f;
+      *(LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nt2 + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
     }
     SYNC();
     // conv3: wave = n-tile, all 9 m-tiles
@@ -542,13 +547,13 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     for (int mt = 0; mt < 9; ++mt) {
       f4v acc = Z4;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) acc = mfma(rfrag(S + O_H2, LD2, 16 * mt + (k >> 1), 32 * (k & 1), lane), w3f[k], acc);
+      for (int k = 0; k < 6; ++k) acc = mfma(w3f[k], rfrag(S + O_H2, LD2, 16 * mt + (k >> 1), 32 * (k & 1), lane), acc);
+      const int q = 16 * mt + li;
+      const bool ok = valid_q(q, C::LP);
+      float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = 16 * mt + 4 * g + e;
-        const float v = valid_q(q, C::LP) ? relu(acc[e] + b3v) : 0.f;
-        *lu16(S, O_H3 + ((q + 1) * LD3 + 16 * wave + li) * 2) = bfu(v);
-      }
+      for (int e = 0; e < 4; ++e) v[e] = ok ? relu(acc[e] + b3v[e]) : 0.f;
+      *(LDS_AS u32x2v*)(S + O_H3 + ((q + 1) * LD3 + 16 * wave + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
     }
     // fc1 B fragments (this tower's half of W1, n-tile = wave; the owners' images of this step), in flight during
     // the pooling
@@ -716,25 +721,30 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     SYNC();
     stamp(x, kact, 11);
     // dh2 = relu'(h2) * sum_j shift_{1-j}(dh3) . W3_j  (K = 3 x 128): wave n-tile nb2, m-tiles mpb, mpb + 2, ..
+    // (transposed: D[ci][q], 4 consecutive channels of one position per lane, 8-byte LDS accesses)
     {
-      float cs = 0.f;
+      f4v cs = Z4;
       for (int mt = mpb; mt < 9; mt += 2) {
         f4v acc = Z4;
 #pragma unroll
         for (int k = 0; k < 12; ++k)
-          acc = mfma(rfrag(S + O_H3, LD3, 16 * mt + 2 - (k >> 2), 32 * (k & 3), lane), w3t[k], acc);
+          acc = mfma(w3t[k], rfrag(S + O_H3, LD3, 16 * mt + 2 - (k >> 2), 32 * (k & 3), lane), acc);
+        const int q = 16 * mt + li;
+        const u32x2v hw = *(const LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2);
+        float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int q = 16 * mt + 4 * g + e;
-          const float h2 = bff(*lu16(S, O_H2 + ((q + 1) * LD2 + 16 * nb2 + li) * 2));
-          const float v = h2 > 0.f ? acc[e] : 0.f;
-          *lu16(S, O_DH2 + ((q + 1) * LD2 + 16 * nb2 + li) * 2) = bfu(v);
-          cs += v;
+          const uint32_t h = hw[e >> 1];
+          v[e] = __uint_as_float((e & 1) ? (h & 0xFFFF0000u) : (h << 16)) > 0.f ? acc[e] : 0.f;
+          cs[e] += v[e];
         }
+        *(LDS_AS u32x2v*)(S + O_DH2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
       }
-      cs += __shfl_xor(cs, 16, 64);
-      cs += __shfl_xor(cs, 32, 64);
-      if (lane < 16) *lf(S, O_RED + (R_DB2 + wave * 16 + li) * 4) = cs;
+#pragma unroll
+      for (int o = 1; o <= 8; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
+      if (li == 0) *(LDS_AS f4v*)(S + O_RED + (R_DB2 + wave * 16 + 4 * g) * 4) = cs;
     }
     // W2T fragments of d(h1)
     const int nb1 = wave & 1, mpa = wave >> 1;
@@ -746,32 +756,38 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     stamp(x, kact, 12);
     // dh1 = relu'(h1) * sum_j shift_{1-j}(dh2) . W2_j (K = 3 x 64), straight into the conv1 gradients
     {
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, sb = 0.f;
+      f4v s0 = Z4, s1 = Z4, s2 = Z4, sb = Z4;  // per channel 4 g + e of the tile
       for (int mt = mpa; mt < 9; mt += 4) {
         f4v acc = Z4;
 #pragma unroll
         for (int k = 0; k < 6; ++k)
-          acc = mfma(rfrag(S + O_DH2, LD2, 16 * mt + 2 - (k >> 1), 32 * (k & 1), lane), w2t[k], acc);
+          acc = mfma(w2t[k], rfrag(S + O_DH2, LD2, 16 * mt + 2 - (k >> 1), 32 * (k & 1), lane), acc);
+        const int q = 16 * mt + li;
+        const u32x2v hw = *(const LDS_AS u32x2v*)(S + O_H1 + ((q + 1) * LD1 + 16 * nb1 + 4 * g) * 2);
+        const float xm = *lf(S, O_XS + q * 4), x0 = *lf(S, O_XS + (q + 1) * 4), xp = *lf(S, O_XS + (q + 2) * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int q = 16 * mt + 4 * g + e;
-          const float h1 = bff(*lu16(S, O_H1 + ((q + 1) * LD1 + 16 * nb1 + li) * 2));
-          const float d = h1 > 0.f ? acc[e] : 0.f;
-          s0 += d * *lf(S, O_XS + q * 4);
-          s1 += d * *lf(S, O_XS + (q + 1) * 4);
-          s2 += d * *lf(S, O_XS + (q + 2) * 4);
-          sb += d;
+          const uint32_t h = hw[e >> 1];
+          const float d = __uint_as_float((e & 1) ? (h & 0xFFFF0000u) : (h << 16)) > 0.f ? acc[e] : 0.f;
+          s0[e] += d * xm;
+          s1[e] += d * x0;
+          s2[e] += d * xp;
+          sb[e] += d;
         }
       }
 #pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        s0 += __shfl_xor(s0, o, 64);
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
-        sb += __shfl_xor(sb, o, 64);
-      }
-      if (lane < 16)
-        *(LDS_AS f4v*)(S + O_RED + (R_C1 + (wave * 16 + li) * 4) * 4) = f4v{s0, s1, s2, sb};
+      for (int o = 1; o <= 8; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[e] += __shfl_xor(s0[e], o, 64);
+          s1[e] += __shfl_xor(s1[e], o, 64);
+          s2[e] += __shfl_xor(s2[e], o, 64);
+          sb[e] += __shfl_xor(sb[e], o, 64);
+        }
+      if (li == 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *(LDS_AS f4v*)(S + O_RED + (R_C1 + (wave * 16 + 4 * g + e) * 4) * 4) = f4v{s0[e], s1[e], s2[e], sb[e]};
     }
     // dW3_j = dh3^T . shift_{j-1}(h2) (K = 160 rows: 144 + zero rows), wave = o-tile; partial [j][ci][o]
     {
@@ -973,7 +989,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     }
   };
   put_state();
-  __syncthreads();
+  lbar();
 
   const int min_bs = a.min_bs;
   int kact = 0;
@@ -1275,7 +1291,7 @@ __device__ __forceinline__ void fc1_publish(const Ctx& x, int tid, int c0, int n
     if (t < ntl)
 #pragma unroll
       for (int e = 0; e < 4; ++e) *lu16(S, F_SW + ((16 * wave + 4 * g + e) * F_LDF + 16 * t + li) * 2) = bfu(p[t][e]);
-  __syncthreads();
+  lbar();
   const int ncol = 16 * ntl, pr = ncol / 8;
   for (int e = tid; e < 128 * pr; e += NTH) {  // W1 [n][1024]: pr pieces of 8 columns per row
     const int n = e / pr, pc = e % pr;
