@@ -291,6 +291,14 @@ constexpr int R_DB2 = 0, R_DB3 = 128, R_C1 = 128 + 1024, R_SM = 128 + 1024 + 512
 constexpr int R_KEEP = R_SM + NSMALL;  // dropout keep bytes [16 rows][64] (one byte = 8 concat columns), as floats: 256
 static_assert((R_KEEP + 256) * 4 <= 9216, "reduction slots");
 
+// relu(acc + b) on a valid row, exact 0 on a pad row: branch-free (the select form became exec-mask branches)
+__device__ __forceinline__ u32x2v relu_pack4(f4v acc, f4v b, bool ok) {
+  const uint32_t km = ok ? 0xFFFFFFFFu : 0u;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = __uint_as_float(__float_as_uint(relu(acc[e] + b[e])) & km);
+  return u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
+}
 __device__ __forceinline__ bool valid_q(int q, int LP) {
   const int l = q % LP;
   return q < 144 && l != 0 && l != LP - 1;
@@ -529,31 +537,43 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     SYNC();
     stamp(x, kact, 7);
+#ifdef CNN2_DIAG
+    drain();
+    stamp(x, kact, 15);
+#endif
     // conv2: H2[q][o] = relu(b2 + sum_j H1[q - 1 + j] . W2_j^T); wave: n-tile nt2, m-tiles mp2, mp2 + 2, ...
-    for (int mt = mp2; mt < 9; mt += 2) {
-      f4v acc = Z4;
+    // (two m-tiles per pass: independent accumulator chains interleave; a tile past 8 computes on zero rows and is
+    // not stored)
+    for (int mt0 = mp2; mt0 < 9; mt0 += 4) {
+      f4v acc[2] = {Z4, Z4};
 #pragma unroll
-      for (int j = 0; j < 3; ++j) acc = mfma(w2f[j], rfrag(S + O_H1, LD1, 16 * mt + j, 0, lane), acc);
-      const int q = 16 * mt + li;
-      const bool ok = valid_q(q, C::LP);
-      float v[4];
+      for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ok ? relu(acc[e] + b2v[e]) : 0.f;
-      *(LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nt2 + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
+        for (int t = 0; t < 2; ++t) acc[t] = mfma(w2f[j], rfrag(S + O_H1, LD1, 16 * (mt0 + 2 * t) + j, 0, lane), acc[t]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q = 16 * (mt0 + 2 * t) + li;
+        if (mt0 + 2 * t < 9)
+          *(LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nt2 + 4 * g) * 2) = relu_pack4(acc[t], b2v, valid_q(q, C::LP));
+      }
     }
     SYNC();
+    stamp(x, kact, 14);
     // conv3: wave = n-tile, all 9 m-tiles
+    // (three m-tiles per pass, interleaved accumulator chains)
 #pragma unroll
-    for (int mt = 0; mt < 9; ++mt) {
-      f4v acc = Z4;
+    for (int mt0 = 0; mt0 < 9; mt0 += 3) {
+      f4v acc[3] = {Z4, Z4, Z4};
 #pragma unroll
-      for (int k = 0; k < 6; ++k) acc = mfma(w3f[k], rfrag(S + O_H2, LD2, 16 * mt + (k >> 1), 32 * (k & 1), lane), acc);
-      const int q = 16 * mt + li;
-      const bool ok = valid_q(q, C::LP);
-      float v[4];
+      for (int k = 0; k < 6; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ok ? relu(acc[e] + b3v[e]) : 0.f;
-      *(LDS_AS u32x2v*)(S + O_H3 + ((q + 1) * LD3 + 16 * wave + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
+        for (int t = 0; t < 3; ++t)
+          acc[t] = mfma(w3f[k], rfrag(S + O_H2, LD2, 16 * (mt0 + t) + (k >> 1), 32 * (k & 1), lane), acc[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int q = 16 * (mt0 + t) + li;
+        *(LDS_AS u32x2v*)(S + O_H3 + ((q + 1) * LD3 + 16 * wave + 4 * g) * 2) = relu_pack4(acc[t], b3v, valid_q(q, C::LP));
+      }
     }
     // fc1 B fragments (this tower's half of W1, n-tile = wave; the owners' images of this step), in flight during
     // the pooling
@@ -724,21 +744,27 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     // (transposed: D[ci][q], 4 consecutive channels of one position per lane, 8-byte LDS accesses)
     {
       f4v cs = Z4;
-      for (int mt = mpb; mt < 9; mt += 2) {
-        f4v acc = Z4;
+      for (int mt0 = mpb; mt0 < 9; mt0 += 4) {
+        f4v acc[2] = {Z4, Z4};
 #pragma unroll
         for (int k = 0; k < 12; ++k)
-          acc = mfma(w3t[k], rfrag(S + O_H3, LD3, 16 * mt + 2 - (k >> 2), 32 * (k & 3), lane), acc);
-        const int q = 16 * mt + li;
-        const u32x2v hw = *(const LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2);
-        float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t h = hw[e >> 1];
-          v[e] = __uint_as_float((e & 1) ? (h & 0xFFFF0000u) : (h << 16)) > 0.f ? acc[e] : 0.f;
-          cs[e] += v[e];
+          for (int t = 0; t < 2; ++t)
+            acc[t] = mfma(w3t[k], rfrag(S + O_H3, LD3, 16 * (mt0 + 2 * t) + 2 - (k >> 2), 32 * (k & 3), lane), acc[t]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (mt0 + 2 * t >= 9) continue;
+          const int q = 16 * (mt0 + 2 * t) + li;
+          const u32x2v hw = *(const LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t h = hw[e >> 1];
+            v[e] = __uint_as_float((e & 1) ? (h & 0xFFFF0000u) : (h << 16)) > 0.f ? acc[t][e] : 0.f;
+            cs[e] += v[e];
+          }
+          *(LDS_AS u32x2v*)(S + O_DH2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
         }
-        *(LDS_AS u32x2v*)(S + O_DH2 + ((q + 1) * LD2 + 16 * nb2 + 4 * g) * 2) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
       }
 #pragma unroll
       for (int o = 1; o <= 8; o <<= 1)
@@ -757,11 +783,17 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     // dh1 = relu'(h1) * sum_j shift_{1-j}(dh2) . W2_j (K = 3 x 64), straight into the conv1 gradients
     {
       f4v s0 = Z4, s1 = Z4, s2 = Z4, sb = Z4;  // per channel 4 g + e of the tile
-      for (int mt = mpa; mt < 9; mt += 4) {
-        f4v acc = Z4;
+      f4v accs[3] = {Z4, Z4, Z4};
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-          acc = mfma(w2t[k], rfrag(S + O_DH2, LD2, 16 * mt + 2 - (k >> 1), 32 * (k & 1), lane), acc);
+      for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          accs[t] = mfma(w2t[k], rfrag(S + O_DH2, LD2, 16 * (mpa + 4 * t) + 2 - (k >> 1), 32 * (k & 1), lane), accs[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int mt = mpa + 4 * t;
+        if (mt >= 9) continue;
+        const f4v acc = accs[t];
         const int q = 16 * mt + li;
         const u32x2v hw = *(const LDS_AS u32x2v*)(S + O_H1 + ((q + 1) * LD1 + 16 * nb1 + 4 * g) * 2);
         const float xm = *lf(S, O_XS + q * 4), x0 = *lf(S, O_XS + (q + 1) * 4), xp = *lf(S, O_XS + (q + 2) * 4);
