@@ -934,7 +934,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 
 // ============================================================================================== head
 // LDS map (bytes); U = f2s | f3f | d3s, reused as the d1 staging tile once the backward is past them
-constexpr int H_L1 = 136, H_L2 = 72, H_L3 = 40, H_F3 = 33;
+constexpr int H_L1 = 136, H_L2 = 72, H_L3 = 40, H_F3 = 36;  // f3 rows 16-B aligned
 constexpr int H_F1S = 0;
 constexpr int H_W2S = H_F1S + 128 * H_L1 * 2;
 constexpr int H_W3S = H_W2S + 64 * H_L1 * 2;
@@ -1050,44 +1050,47 @@ __device__ __forceinline__ void head(const Ctx& x) {
       for (int q = 0; q < 8; ++q) {
         const int b = (tid + NTH * q) >> 5;
         LDS_AS unsigned short* d = f1s + b * H_L1 + i1;
+        float v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = bfu(b < B ? relu((za[q][k] + zb[q][k]) + bias[i1 + k]) : 0.f);
+        for (int k = 0; k < 4; ++k) v[k] = b < B ? relu((za[q][k] + zb[q][k]) + bias[i1 + k]) : 0.f;
+        *(LDS_AS u32x2v*)d = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
       }
     }
     SYNC();
-    // fc2: wave -> m-tile w, n-tiles 0..3
+    // fc2 (transposed, D[n][m] = W2 . f1^T: a lane ends with 4 consecutive features of one row -> one 8-byte
+    // store); wave -> m-tile w, n-tiles 0..3
     {
       const int m0 = wave * 16;
       f4v acc[4] = {Z4, Z4, Z4, Z4};
 #pragma unroll
       for (int k0 = 0; k0 < 128; k0 += 32) {
-        const s8v af = rfrag(S + H_F1S, H_L1, m0, k0, lane);
+        const s8v bf = rfrag(S + H_F1S, H_L1, m0, k0, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = mfma(af, rfrag(S + H_W2S, H_L1, 16 * j, k0, lane), acc[j]);
+        for (int j = 0; j < 4; ++j) acc[j] = mfma(rfrag(S + H_W2S, H_L1, 16 * j, k0, lane), bf, acc[j]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = 16 * j + li;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) f2s[(m0 + 4 * g + e) * H_L2 + n] = bfu(relu(acc[j][e] + bias[128 + n]));
+        const f4v bv = *(const LDS_AS f4v*)(bias + 128 + 16 * j + 4 * g);
+        *(LDS_AS u32x2v*)(f2s + (m0 + li) * H_L2 + 16 * j + 4 * g) =
+            u32x2v{pk2(relu(acc[j][0] + bv[0]), relu(acc[j][1] + bv[1])), pk2(relu(acc[j][2] + bv[2]), relu(acc[j][3] + bv[3]))};
       }
     }
     SYNC();
-    // fc3
+    // fc3 (transposed: one 16-byte store of 4 features per lane)
     {
       const int m0 = wave * 16;
       f4v acc[2] = {Z4, Z4};
 #pragma unroll
       for (int k0 = 0; k0 < 64; k0 += 32) {
-        const s8v af = rfrag(S + H_F2S, H_L2, m0, k0, lane);
+        const s8v bf = rfrag(S + H_F2S, H_L2, m0, k0, lane);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j] = mfma(af, rfrag(S + H_W3S, H_L2, 16 * j, k0, lane), acc[j]);
+        for (int j = 0; j < 2; ++j) acc[j] = mfma(rfrag(S + H_W3S, H_L2, 16 * j, k0, lane), bf, acc[j]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int n = 16 * j + li;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) f3f[(m0 + 4 * g + e) * H_F3 + n] = relu(acc[j][e] + bias[192 + n]);
+        const f4v bv = *(const LDS_AS f4v*)(bias + 192 + 16 * j + 4 * g);
+        *(LDS_AS f4v*)(f3f + (m0 + li) * H_F3 + 16 * j + 4 * g) =
+            f4v{relu(acc[j][0] + bv[0]), relu(acc[j][1] + bv[1]), relu(acc[j][2] + bv[2]), relu(acc[j][3] + bv[3])};
       }
     }
     SYNC();
@@ -1095,7 +1098,13 @@ __device__ __forceinline__ void head(const Ctx& x) {
     float zb = 0.f, lb = 0.f;
     if (tid < 128) {
       float acc = bias[224];
-      for (int j = 0; j < 32; ++j) acc += f3f[tid * H_F3 + j] * wos[j];
+#pragma unroll
+      for (int j = 0; j < 32; j += 4) {
+        const f4v fv = *(const LDS_AS f4v*)(f3f + tid * H_F3 + j);
+        const f4v wv = *(const LDS_AS f4v*)(wos + j);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += fv[k] * wv[k];
+      }
       zb = acc;
       if (tid < bs) {
         const float p = 1.f / (1.f + expf(-zb));
@@ -1128,9 +1137,14 @@ __device__ __forceinline__ void head(const Ctx& x) {
     if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
     SYNC();
     // d3 = dz wo^T * relu'(f3); output-layer / fc3-bias gradient partials per wave
-    for (int e = tid; e < 128 * 32; e += NTH) {
-      const int b = e >> 5, j = e & 31;
-      d3s[b * H_L3 + j] = bfu(f3f[b * H_F3 + j] > 0.f ? dz[b] * wos[j] : 0.f);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {  // (row b, 4 features) per thread step: one 16-byte read, one 8-byte store
+      const int e = tid + NTH * it, b = e >> 3, j = 4 * (e & 7);
+      const f4v fv = *(const LDS_AS f4v*)(f3f + b * H_F3 + j);
+      const f4v wv = *(const LDS_AS f4v*)(wos + j);
+      const float d = dz[b];
+      *(LDS_AS u32x2v*)(d3s + b * H_L3 + j) = u32x2v{pk2(fv[0] > 0.f ? d * wv[0] : 0.f, fv[1] > 0.f ? d * wv[1] : 0.f),
+                                                    pk2(fv[2] > 0.f ? d * wv[2] : 0.f, fv[3] > 0.f ? d * wv[3] : 0.f)};
     }
     {
       const int j = tid & 31, r0 = 8 * (tid >> 5);
