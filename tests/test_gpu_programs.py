@@ -359,7 +359,7 @@ def test_program_training_is_bit_reproducible(gpu, name, B, n, E):
 
 @pytest.mark.parametrize("C,n,E", [(3, 1000, 2), (8, 600, 1)])
 def test_cnn2_onchip_trainer_tracks_layer_program(gpu, monkeypatch, C, n, E):
-    """The CNNModel on-chip trainer (csrc/kernels/cnn2.hip: one launch per round, 25 workgroups per client)
+    """The CNNModel on-chip trainer (csrc/kernels/cnn2.hip: one launch per round, 32 workgroups per client)
     follows the graph-replayed layer program (same batches, dropout masks and Adam): per-epoch losses and
     the trained parameters agree to bf16-operand tolerance, and two launches give the same bits."""
     ds = synthetic_icu(n)
