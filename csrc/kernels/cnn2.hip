@@ -821,24 +821,34 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         for (int e = 0; e < 4; ++e)
           *(LDS_AS f4v*)(S + O_RED + (R_C1 + (wave * 16 + 4 * g + e) * 4) * 4) = f4v{s0[e], s1[e], s2[e], sb[e]};
     }
-    // dW3_j = dh3^T . shift_{j-1}(h2) (K = 160 rows: 144 + zero rows), wave = o-tile; partial [j][ci][o]
+    // dW3_j = dh3^T . shift_{j-1}(h2) (K = 160 rows: 144 + zero rows).  Wave: o-tiles 2 (w & 3) + {0, 1} x six of
+    // the twelve (tap, ci-tile) blocks (w >> 2 picks the half): per k-step 2 + 6 transposed fragment reads for 12
+    // MFMAs (was 1 + 12 with one o-tile per wave)
     {
-      f4v acc[12];
+      const int ob = 2 * (wave & 3), tb = 6 * (wave >> 2);
+      f4v acc[2][6];
 #pragma unroll
-      for (int t = 0; t < 12; ++t) acc[t] = Z4;
+      for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+        for (int t = 0; t < 6; ++t) acc[oi][t] = Z4;
       for (int ks = 0; ks < 5; ++ks) {
-        const s8v af = cfrag(S + O_H3 + LD3 * 2, LD3, 32 * ks, 16 * wave, lane);
+        const s8v a0 = cfrag(S + O_H3 + LD3 * 2, LD3, 32 * ks, 16 * ob, lane);
+        const s8v a1 = cfrag(S + O_H3 + LD3 * 2, LD3, 32 * ks, 16 * (ob + 1), lane);
 #pragma unroll
-        for (int t = 0; t < 12; ++t) {
-          const int j = t >> 2, ct = t & 3;
-          acc[t] = mfma(af, cfrag(S + O_H2 + j * LD2 * 2, LD2, 32 * ks, 16 * ct, lane), acc[t]);
+        for (int t = 0; t < 6; ++t) {
+          const int j = (tb + t) >> 2, ct = (tb + t) & 3;
+          const s8v bf = cfrag(S + O_H2 + j * LD2 * 2, LD2, 32 * ks, 16 * ct, lane);
+          acc[0][t] = mfma(a0, bf, acc[0][t]);
+          acc[1][t] = mfma(a1, bf, acc[1][t]);
         }
       }
 #pragma unroll
-      for (int t = 0; t < 12; ++t) {
-        const int j = t >> 2, ci = 16 * (t & 3) + li;
-        st16f(x.rw, pbase + (P_W3 + ((j * 16 + 2 * wave + (g >> 1)) * 64 + ci) * 8 + 4 * (g & 1)) * 4, acc[t]);
-      }
+      for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          const int j = (tb + t) >> 2, ci = 16 * ((tb + t) & 3) + li;
+          st16f(x.rw, pbase + (P_W3 + ((j * 16 + 2 * (ob + oi) + (g >> 1)) * 64 + ci) * 8 + 4 * (g & 1)) * 4, acc[oi][t]);
+        }
     }
     // dW2_j = dh2^T . shift_{j-1}(h1): wave -> o-tile (w & 3), ci-tile (w >> 2)
     {
