@@ -266,7 +266,7 @@ template <int T>
 struct TW {
   static constexpr int L = T == 0 ? 7 : 16, R = T == 0 ? 16 : 8, NTW = T == 0 ? 8 : 16, LP = L + 2;
   static constexpr int COL0 = T == 0 ? 0 : 512, XOFF = T == 0 ? 0 : 7, NC = T == 0 ? 64 : 32, FIRST = T == 0 ? 0 : 8;
-  static constexpr int NS = T == 0 ? 3 : 2;  // owner chunk slots per thread
+  static constexpr int NS = T == 0 ? 2 : 1;  // owner chunk slots per thread (970 / 485 chunks per owner)
   static_assert(R * LP == 144, "144 padded rows per tower workgroup");
 };
 constexpr int NR = 162;  // LDS rows: padded row q at row q + 1; rows 0 and 145..161 stay zero
@@ -326,18 +326,19 @@ __device__ __forceinline__ Chunk chunk_of(int i, int cid) {
     } else if (cid < 960) {
       lo = cid - 768;
       k.kind = 2; k.j = lo / 64; k.ci = (lo % 64) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
-    } else if (cid < 1040 && i == 0) {
-      k.kind = 1; k.s0 = 4 * (cid - 960);
+    } else if (cid < 970) {  // 10 of the 80 small-vector chunks per owner
+      k.kind = 1; k.s0 = 4 * (10 * i + cid - 960);
     }
   } else {
+    // labs: W3 block i, half (ci 16 (i & 1) ..) of W2 block i >> 1, 5 of the 80 small-vector chunks
     if (cid < 384) {
       lo = cid;
       k.kind = 3; k.j = lo / 128; k.ci = (lo % 128) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
-    } else if (cid < 576 && i < 8) {
+    } else if (cid < 480) {
       lo = cid - 384;
-      k.kind = 2; k.j = lo / 64; k.ci = (lo % 64) >> 1; k.o0 = 8 * i + 4 * (lo & 1);
-    } else if (cid < 464 && i == 15) {
-      k.kind = 1; k.s0 = 4 * (cid - 384);
+      k.kind = 2; k.j = lo / 32; k.ci = 16 * (i & 1) + ((lo % 32) >> 1); k.o0 = 8 * (i >> 1) + 4 * (lo & 1);
+    } else if (cid < 485) {
+      k.kind = 1; k.s0 = 4 * (5 * i + cid - 480);
     }
   }
   if (k.kind == 3) k.poff = P_W3 + ((k.j * 16 + (k.o0 >> 3)) * 64 + k.ci) * 8 + (k.o0 & 7);
@@ -381,7 +382,6 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
   }
   lbar();
   constexpr int NB3 = T == 0 ? 2 : 1;
-  const bool has2 = T == 0 || i < 8;
   // W3T [j][ci][o]: one 16-B piece (8 o) per (blk, j, ci); W3 [j][o][ci]: 8 pieces (64 ci) per (blk, j, o)
   for (int e = x.tid; e < NB3 * 192 * 2; e += NTH) {
     const int blk = e / 384, r = e % 384;
@@ -403,15 +403,17 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
       st16(x.rw, WS_IMG + (tw + IM_W3 + (j * 128 + 8 * b3 + o) * 64 + 8 * cc) * 2, u32x4{w[0], w[1], w[2], w[3]});
     }
   }
-  if (has2) {
-    const int b2 = i;
-    for (int e = x.tid; e < 96 * 2; e += NTH) {
-      if (e < 96) {
-        const int j = e / 32, ci = e % 32;
+  {
+    // W2 block b2 (8 output channels), input channels ci0 .. ci0 + nci (labs owners hold half a block)
+    const int b2 = T == 0 ? i : (i >> 1), ci0 = T == 0 ? 0 : 16 * (i & 1);
+    constexpr int nci = T == 0 ? 32 : 16, npc = nci / 8;
+    for (int e = x.tid; e < 3 * nci * 2; e += NTH) {
+      if (e < 3 * nci) {
+        const int j = e / nci, ci = ci0 + e % nci;
         const u32x4 v = *(const LDS_AS u32x4*)(S + O_S2 + (j * 32 + ci) * 16);
         st16(x.rw, WS_IMG + (tw + IM_W2T + (j * 32 + ci) * 64 + 8 * b2) * 2, v);
       } else {
-        const int q = e - 96, j = q / 32, o = (q % 32) >> 2, cc = q & 3;  // 8 o x 4 pieces per j
+        const int q = e - 3 * nci, j = q / (8 * npc), o = (q % (8 * npc)) / npc, cc = ci0 / 8 + q % npc;
         uint32_t w[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
