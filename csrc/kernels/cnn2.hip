@@ -284,6 +284,9 @@ constexpr int O_FLAG = O_RED + 9216;
 constexpr int T_LDS = O_FLAG + 16;
 static_assert(O_ZS + 16 * LDZ * 4 <= O_D1R, "z1p staging");
 // owner-phase staging (dead activation regions after the backward)
+// S3 / S2: [blk][tap][ci][8 o] (W^T pieces), S3B / S2B: [blk][tap][8 o][ci] (W pieces): both staged from registers
+constexpr int O_S3B = 8192, O_S2B = O_S3B + 6144;
+static_assert(O_S2B + 1536 <= O_XS, "owner staging");
 constexpr int O_S3 = 0, O_S2 = 6144, O_D1F = 8192, O_FW = O_D1F + 128 * LDD * 2, O_SW = O_FW + 128 * 72 * 2;
 static_assert(O_SW + 128 * 72 * 2 <= O_XS, "owner staging");
 // reduction slots (floats from O_RED)
@@ -373,9 +376,14 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
       const int blk = T == 0 ? ((k.o0 >> 3) - 2 * i) : 0;
       *(LDS_AS uint32_t*)(S + O_S3 + ((blk * 192 + k.j * 64 + k.ci) * 8 + (k.o0 & 7)) * 2) = pk2(st.p[u][0], st.p[u][1]);
       *(LDS_AS uint32_t*)(S + O_S3 + ((blk * 192 + k.j * 64 + k.ci) * 8 + (k.o0 & 7) + 2) * 2) = pk2(st.p[u][2], st.p[u][3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        *lu16(S, O_S3B + (((blk * 3 + k.j) * 8 + (k.o0 & 7) + e) * 64 + k.ci) * 2) = bfu(st.p[u][e]);
     } else if (k.kind == 2) {
       *(LDS_AS uint32_t*)(S + O_S2 + ((k.j * 32 + k.ci) * 8 + (k.o0 & 7)) * 2) = pk2(st.p[u][0], st.p[u][1]);
       *(LDS_AS uint32_t*)(S + O_S2 + ((k.j * 32 + k.ci) * 8 + (k.o0 & 7) + 2) * 2) = pk2(st.p[u][2], st.p[u][3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *lu16(S, O_S2B + ((k.j * 8 + (k.o0 & 7) + e) * 32 + k.ci) * 2) = bfu(st.p[u][e]);
     } else if (k.kind == 1) {
       st16f(x.rw, WS_SMALL + (T * NSMALL + k.s0) * 4, f4v{st.p[u][0], st.p[u][1], st.p[u][2], st.p[u][3]});
     }
@@ -392,15 +400,8 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
       st16(x.rw, WS_IMG + (tw + IM_W3T + (j * 64 + ci) * 128 + 8 * b3) * 2, v);
     } else {
       const int q = r - 192, j = q / 64, o = (q % 64) >> 3, cc = q & 7;  // 8 o x 8 pieces per j
-      uint32_t w[4];
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const int ci = 8 * cc + 2 * h;
-        const unsigned short lo = *lu16(S, O_S3 + ((blk * 192 + j * 64 + ci) * 8 + o) * 2);
-        const unsigned short hi = *lu16(S, O_S3 + ((blk * 192 + j * 64 + ci + 1) * 8 + o) * 2);
-        w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
-      }
-      st16(x.rw, WS_IMG + (tw + IM_W3 + (j * 128 + 8 * b3 + o) * 64 + 8 * cc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+      st16(x.rw, WS_IMG + (tw + IM_W3 + (j * 128 + 8 * b3 + o) * 64 + 8 * cc) * 2,
+           *(const LDS_AS u32x4*)(S + O_S3B + (((blk * 3 + j) * 8 + o) * 64 + 8 * cc) * 2));
     }
   }
   {
@@ -414,15 +415,8 @@ __device__ __forceinline__ void publish_conv(const Ctx& x, int i, const TowerSta
         st16(x.rw, WS_IMG + (tw + IM_W2T + (j * 32 + ci) * 64 + 8 * b2) * 2, v);
       } else {
         const int q = e - 3 * nci, j = q / (8 * npc), o = (q % (8 * npc)) / npc, cc = ci0 / 8 + q % npc;
-        uint32_t w[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int ci = 8 * cc + 2 * h;
-          const unsigned short lo = *lu16(S, O_S2 + ((j * 32 + ci) * 8 + o) * 2);
-          const unsigned short hi = *lu16(S, O_S2 + ((j * 32 + ci + 1) * 8 + o) * 2);
-          w[h] = (uint32_t)lo | ((uint32_t)hi << 16);
-        }
-        st16(x.rw, WS_IMG + (tw + IM_W2 + (j * 64 + 8 * b2 + o) * 32 + 8 * cc) * 2, u32x4{w[0], w[1], w[2], w[3]});
+        st16(x.rw, WS_IMG + (tw + IM_W2 + (j * 64 + 8 * b2 + o) * 32 + 8 * cc) * 2,
+             *(const LDS_AS u32x4*)(S + O_S2B + ((j * 8 + o) * 32 + 8 * cc) * 2));
       }
     }
   }
@@ -539,10 +533,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     }
     SYNC();
     stamp(x, kact, 7);
-#ifdef CNN2_DIAG
-    drain();
-    stamp(x, kact, 15);
-#endif
     // conv2: H2[q][o] = relu(b2 + sum_j H1[q - 1 + j] . W2_j^T); wave: n-tile nt2, m-tiles mp2, mp2 + 2, ...
     // (two m-tiles per pass: independent accumulator chains interleave; a tile past 8 computes on zero rows and is
     // not stored)
@@ -914,6 +904,10 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       for (int u = 0; u < C::NS; ++u)
 #pragma unroll
         for (int n = 0; n < C::NTW; ++n) gsum[u] += pv[u][n];
+#ifdef CNN2_DIAG
+      drain();
+      stamp(x, kact, 15);
+#endif
 #pragma unroll
       for (int u = 0; u < C::NS; ++u) {
         if (ks[u].kind == 0) continue;

@@ -66,10 +66,11 @@ def main():
             rows["fc1_slack"].append(float(tn[:, 8].min() - fc1[c, :, k, 1].max()))
             rows["W_barrier"].append(float(tn[:, 0].min() - t[:, 6].max()))
             rows["step"].append(float(tn[:, 0].min() - t[:, 0].min()))
-    fine = {"f.inputs+conv1": (0, 7), "f.conv2": (7, 14), "f.conv3": (14, 8), "f.conv1->operands(diag)": (7, 15), "f.pool": (8, 9), "f.fc1+publish": (9, 1),
+    fine = {"f.inputs+conv1": (0, 7), "f.conv2": (7, 14), "f.conv3": (14, 8), "o.wait+loads(diag)": (4, 15), "o.adam+publish(diag)": (15, 5), "o.arrive": (5, 6), "f.pool": (8, 9), "f.fc1+publish": (9, 1),
             "b.d1+dfeat": (2, 10), "b.dh3": (10, 11), "b.dh2": (11, 12), "b.dh1+dW": (12, 13), "b.partials": (13, 3)}
     if not bool((towers[:, :, 8:63, 15] != 0).all()):  # stamp 15 only in -DCNN2_DIAG builds
-        fine.pop("f.conv1->operands(diag)")
+        fine.pop("o.wait+loads(diag)")
+        fine.pop("o.adam+publish(diag)")
     for name, (a, b) in fine.items():
         rows[name] = [float((towers[c, :, k, b] - towers[c, :, k, a]).max()) for c in range(C) for k in range(8, 63)]
     for k, v in rows.items():
