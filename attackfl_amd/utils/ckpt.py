@@ -230,6 +230,12 @@ class CheckpointWriter:
             ev = torch.cuda.Event()
             ev.record(self._stream)
         src.record_stream(self._stream)  # the allocator keeps src's memory until the copy has run
+        if after is None:
+            # an immediate submit promises that src may be overwritten right after return: the caller's stream
+            # waits (on the device) for the copy AND the CRC pass — without it a write queued behind the submit
+            # could land between the two, and the GPU CRC then disagreed with the staged bytes (the template
+            # path was dropped for the key: tests/test_gpu_engine.py::test_checkpoint_every_submit_written_in_order)
+            torch.cuda.current_stream(src.device).wait_event(ev)
         self._copied = ev
         with self._cv:
             self._queue.append((key, slot, build, path, ev))
