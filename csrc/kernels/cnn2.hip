@@ -153,17 +153,18 @@ constexpr int WS_FEAT = WS_SMALL + 2 * NSMALL * 4;         // [2 parities][128][
 constexpr int FEAT_PAR = 128 * 1024 * 2;
 constexpr int WS_Z1P = WS_FEAT + 2 * FEAT_PAR;             // [2][128][128] fp32 fc1 partials per tower
 constexpr int WS_D1 = WS_Z1P + 2 * 128 * 128 * 4;          // [128][128] bf16 d(fc1 pre-activation)
-constexpr int WS_STAT = WS_D1 + 128 * 128 * 2;             // 16 B: head status of the step
+constexpr int WS_STAT = WS_D1 + 128 * 128 * 2;             // [8 waves] x 16 B: head status of the step
 constexpr int PSZ = 24576 + 6144 + NSMALL;                 // one tower workgroup's gradient partial (floats)
 // [3 taps][16 o-blocks][64 ci][8 o] | [3][8][32][8] | smalls: an owner's o-block is one contiguous 2 KB / 1 KB run per tap
 constexpr int P_W3 = 0, P_W2 = 24576, P_SM = 24576 + 6144;
-constexpr int WS_PART = WS_STAT + 16;                      // [24][PSZ] fp32 (vitals 0..7, labs 8..23)
+constexpr int WS_PART = WS_STAT + 128;                     // [24][PSZ] fp32 (vitals 0..7, labs 8..23)
 constexpr int WS_MV = WS_PART + 24 * PSZ * 4;              // [25 workgroups][8 slots][512 threads] {m f4, v f4}
 constexpr int MV_WG = 16 * 512 * 32;
 constexpr long WS_BYTES = WS_MV + (long)NWG * MV_WG;
 // counters per client: F (towers -> head), H (head -> towers), P0/P1 (partials), W0/W1 (images), TMO
 // W1R: fc1 images of the next step published (7 arrivals per step)
-constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_W1R = 7, CT_N = 8;  // x 32 words (own 128-B lines)
+// HW + w: head wave w published d1 rows 16 w .. 16 w + 15 (the towers of those rows wait on it alone)
+constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_W1R = 7, CT_HW = 8, CT_N = 16;  // x 32 words
 
 struct Ctx {
   const AflCnn2Args* a;
@@ -651,11 +652,12 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       wt1[k] = ld16s(x.rw, WS_IMG + (IM_W1T + par * IM_FC1PAR + (C::COL0 + 16 * (4 * wave + (k >> 2)) + li) * 128 +
                                     32 * (k & 3) + 8 * g) * 2);
     // ------------------------------------------------------------------------------ backward
-    if (!wait_ge(x, CT_H, (uint32_t)(kact + 1), O_FLAG)) break;
+    const int hw = T == 0 ? i : (i >> 1);  // the head wave that computes this workgroup's d1 rows
+    if (!wait_ge(x, CT_HW + hw, (uint32_t)(kact + 1), O_FLAG)) break;
     REOPQ();
     stamp(x, kact, 2);
     {
-      const u32x4 stt = ld16(x.rw, WS_STAT);
+      const u32x4 stt = ld16(x.rw, WS_STAT + 16 * hw);
       if (stt[0] != 0u) {  // NaN loss: the client's round ends here without an update (the head saw it too)
         alive = false;
         break;
@@ -1125,10 +1127,12 @@ __device__ __forceinline__ void head(const Ctx& x) {
     const bool nan = a.nan_abort && (loss != loss);
     if (nan) {  // status only: no update this step, the client's round ends (towers read the status)
       if (tid == 0) {
-        st16(x.rw, WS_STAT, u32x4{1u, (uint32_t)s, 0u, 0u});
+        for (int w = 0; w < 8; ++w) st16(x.rw, WS_STAT + 16 * w, u32x4{1u, (uint32_t)s, 0u, 0u});
         a.failed[c] = 1;
       }
       arrive(x, CT_H);
+      if (tid == 0)
+        for (int w = 0; w < 8; ++w) __hip_atomic_fetch_add(x.ctr + (CT_HW + w) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
     if (tid < 128) {
@@ -1249,13 +1253,17 @@ __device__ __forceinline__ void head(const Ctx& x) {
         if (lane < 16) gbw[wave * 192 + 64 + n] = cs;
       }
     }
-    SYNC();
+    // per-wave hand-off: this wave's 16 d1 rows (its own LDS writes: no barrier) + its status slot, drained, then
+    // its counter — the tower workgroups of those rows start without waiting for the other waves
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // publish d1 (bf16 [128][128])
-      const int e = tid + NTH * u, r = e >> 4, pc = e & 15;
+    for (int u = 0; u < 4; ++u) {
+      const int e = lane + 64 * u, r = 16 * wave + (e >> 4), pc = e & 15;
       st16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2, *(const LDS_AS u32x4*)(S + H_D1S + (r * H_L1 + 8 * pc) * 2));
     }
-    if (tid == 0) st16(x.rw, WS_STAT, u32x4{0u, (uint32_t)s, 0u, 0u});
+    if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
+    drain();
+    if (lane == 0) __hip_atomic_fetch_add(x.ctr + (CT_HW + wave) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SYNC();
     if (tid < 128) {
       float sb = 0.f;
 #pragma unroll
