@@ -174,24 +174,36 @@ def bisect_iterations(gamma: float = 50.0, tau: float = 1.0) -> int:
 
 def _bisect_device(accept: Callable[[torch.Tensor], torch.Tensor], gamma: float, tau: float, device):
     """The reference bisection with device-side state: ``accept(γ)`` returns a 0-d bool tensor.  Returns
-    (last tried γ, iterations, last accepted γ) with the γs as 0-d float64 tensors."""
+    (last tried γ, iterations, last accepted γ, every tried γ [n], every decision [n]) with the γs as float64
+    device tensors (the trace the reference prints as ``Gamma is {γ}``, ``src/Utils.py:119,153,191``)."""
     g = torch.full((), float(gamma), dtype=torch.float64, device=device)
     succ = torch.zeros((), dtype=torch.float64, device=device)
     last = g
     step = float(gamma)
     n = bisect_iterations(gamma, tau)
+    tried, accs = [], []
     for _ in range(n):
         last = g
         acc = accept(g)
+        tried.append(g)
+        accs.append(acc)
         succ = torch.where(acc, g, succ)
         g = g + (acc.to(torch.float64) * step - step / 2.0)   # accept: +step/2, reject: -step/2
         step /= 2.0
-    return last, n, succ
+    if n:
+        return last, n, succ, torch.stack(tried), torch.stack(accs)
+    return last, n, succ, torch.zeros(0, dtype=torch.float64), torch.zeros(0, dtype=torch.bool)
 
 
 def host_info(info: Dict) -> Dict:
-    """An attack's info dict with device scalars read back (call where the host synchronises anyway)."""
-    return {k: (float(v) if torch.is_tensor(v) else v) for k, v in info.items()}
+    """An attack's info dict with device values read back (call where the host synchronises anyway): 0-d
+    tensors become floats, vectors (the per-γ trace) lists."""
+    out = {}
+    for k, v in info.items():
+        if torch.is_tensor(v):
+            v = float(v) if v.dim() == 0 else [float(x) if v.dtype != torch.bool else bool(x) for x in v.tolist()]
+        out[k] = v
+    return out
 
 
 def _bisect(accept: Callable[[float], bool], gamma: float = 50.0, tau: float = 1.0) -> Tuple[float, int, float]:
@@ -234,9 +246,10 @@ def _minmax_family(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine, k
         d = cand_d(g)
         return ((d ** 2).sum() < threshold) if kind == "sum" else (d.max() < threshold)
 
-    last, iters, succ = _bisect_device(accept, gamma, tau, G.device)
+    last, iters, succ, tried, accs = _bisect_device(accept, gamma, tau, G.device)
     mal = st.mean - last * dev
-    return AttackResult(True, mal, {"gamma": last, "gamma_succ": succ, "iters": iters, "threshold": threshold})
+    return AttackResult(True, mal, {"gamma": last, "gamma_succ": succ, "iters": iters, "threshold": threshold,
+                                    "gammas": tried, "accepted": accs})
 
 
 def min_max(G, own, engine, **kw) -> AttackResult:

@@ -21,11 +21,11 @@ this round's validation at any world size (speculative launch, ``run_round``).
 from __future__ import annotations
 
 import contextlib
-
 import os
 import random
 import time
 import uuid
+import zlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -47,7 +47,8 @@ from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
 from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
 
-META = 4  # valid, result, size, is_attacker; then the client's per-epoch losses (E columns)
+META = 5  # valid, result, size, is_attacker, decision word; then the client's per-epoch losses (E columns)
+DECISION = 4  # column of the sender's decision word (``FLEngine._decision_word``)
 
 
 class Staging:
@@ -634,7 +635,11 @@ class FLEngine:
                     atk_out.append((j, res.ok and res.params is not None, res.params))
                     self._attack_info = res.info
                     if self.verbose:  # (reads the attack's device scalars back: verbose runs only)
-                        print_with_color(f"[===] Client {i} attacks with {atk.mode} {host_info(res.info)}", "red")
+                        hi = host_info(res.info)
+                        for g in hi.get("gammas", []):  # the reference's per-iteration print (src/Utils.py:119)
+                            print(f"Gamma is {g}")
+                        print_with_color(f"[===] Client {i} attacks with {atk.mode} "
+                                         f"{ {k: v for k, v in hi.items() if not isinstance(v, list)} }", "red")
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)
         if pending is not None and in_place:
@@ -701,6 +706,10 @@ class FLEngine:
                 if ok:
                     block[j, :P] = mal
                 block[j, P + 1] = 1.0 if ok else 0.0
+        if block is not None:
+            # every rank stamps its view of the replicated server state into its rows; the gather's reader checks
+            # that all ranks agree (_check_decisions), so a rank whose validation / detection diverged fails loudly
+            block[:, P + DECISION] = float(self._decision_word())
         self._fedavg_w = st.get("fedavg_w")
         self._lw_times = {"t_lw_prep": (tq2 - tq) + st.get("t_enqueue", 0.0), "t_lw_prep_host": tq1 - tq,
                           "t_lw_prep_upload": tq2 - tq1, "t_lw_launch": tp1 - tp0, "t_lw_attack": tp2 - tw,
@@ -781,7 +790,9 @@ class FLEngine:
         g0 = self.global_params if self.global_params is not None else self.fltrust_model.clone()
         _, trainer, plan = self._fltrust_setup()
         params = g0.clone()[None]
-        trainer.launch(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
+        # kept and read at the round's host synchronisation (_finish_round): a NaN result is ignored like the
+        # reference's train_on_device return value, a cross-workgroup timeout still raises
+        self._fl_pending = trainer.launch(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
         server_new = params[0]
         g0_delta = server_new - g0
         if compat and self.global_params is None:
@@ -862,12 +873,15 @@ class FLEngine:
                 allb = self.comm.all_gather_rows(block)                    # [world*slots, W]
                 sel = allb.index_select(0, idx)
                 U = sel[:, :P].contiguous()
-                # FedAvg: the aggregate and the next launch go in on the device before the host read below
+                # the round's ONE host read: every client's [valid, result, size, attacker, decision | losses]; it
+                # is queued BEFORE the early launch and waited for through its own event, so the host waits for
+                # the gather (the slowest rank's clients), not for the next round's training queued behind it
+                mread = self._meta_read(sel[:, P:P + META + self.E])
+                # FedAvg / hyper: the aggregate and the next launch go in on the device before the host read
                 esl = self._early_launch(st, last, U=U, sel=sel)
-                # the round's ONE host read: every client's [valid, result, size, attacker | losses] (it also
-                # waits for the gather, i.e. for the slowest rank's clients)
-                meta = sel[:, P:P + META + self.E].double().cpu()
+                meta = mread()
                 self.comm.check()
+                self._check_decisions(meta.numpy())
                 if self._pending is not None:
                     self._pending.result()  # the training has finished by now: surfaces hand-off timeouts
             if self.phase_sync:
@@ -930,6 +944,41 @@ class FLEngine:
         if vstream is not None:
             self.ckpt_writer.kick()  # the next launch is already in: copy + write while it trains
         return rec
+
+    def _meta_read(self, cols: torch.Tensor):
+        """Start the device -> host copy of the gathered meta columns; returns a callable that waits for THAT
+        copy only (an event recorded right after it) and yields the fp64 host matrix."""
+        if cols.device.type != "cuda":
+            m = cols.double().cpu()
+            return lambda: m
+        buf = getattr(self, "_meta_pinned", None)
+        if buf is None or buf.shape != cols.shape:
+            buf = self._meta_pinned = torch.empty(cols.shape, dtype=torch.float32, pin_memory=True)
+        buf.copy_(cols, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+
+        def wait():
+            ev.synchronize()
+            return buf.double()  # (a copy: the pinned buffer is reused next round)
+        return wait
+
+    def _decision_word(self) -> int:
+        """23-bit digest (exact in fp32) of the replicated server state every rank must agree on: the round
+        counters (which encode every past round_ok) and the selected set (which encodes every removal)."""
+        key = f"{self.round_no}|{self.rounds_left}|{','.join(map(str, self.selected))}".encode()
+        return zlib.crc32(key) & 0x7FFFFF
+
+    def _check_decisions(self, mn: np.ndarray) -> None:
+        """Raise if the ranks' decision words differ: a rank's validation or detection decided otherwise (e.g.
+        a mixed CPU / GPU gloo world whose kernels are not bit-identical), and continuing would desynchronise
+        the collectives or silently diverge the replicated models."""
+        valid = mn[:, 0] > 0.5
+        words = mn[valid, DECISION]
+        if words.size and not np.all(words == words[0]):
+            raise RuntimeError(f"ranks disagree on the replicated server state (round {self.round_no}): decision "
+                               f"words {sorted(set(int(w) for w in words))}; validation / detection must be "
+                               "bit-identical on every rank (do not mix devices in one world)")
 
     def _early_ok(self, last: bool) -> bool:
         if self.mode == "hyper":
@@ -1029,25 +1078,33 @@ class FLEngine:
         # ---- replicated detection + validation: every rank computes the same decision ----
         removed: List[int] = []
         metric = float("nan")
+        # the reference validates len(all_model_parameters) generated models: the clients that reported this
+        # round, counted before any removal (server.py:541)
+        n_val = len(self.selected)
         if self.detector is not None:
             embs = {i: self.hyper.embedding(i).cpu().numpy()[None, :] for i in self.selected}
             removed = self.detector.step(self.round_no, self.selected, embs)
-        if self.validation is not None and round_ok:
-            if self.mode == "hyper":
-                round_ok, metric = self.validation.test_hyper(self.hyper, len(self.selected))
-            else:
-                if self.global_params is None:
-                    round_ok = False
-                else:
-                    round_ok, metric = self.validation.test(self.global_params)
-        trace.pop()
         if removed:
+            # removal and rollback come BEFORE validation, so the logged metric and the round's success are
+            # those of the rolled-back hypernetwork (server.py:532-543)
             for r in removed:
                 if self.verbose:
                     print_with_color(f"Removing anomaly {r}, rolling back", "yellow")
                 if r in self.selected:
                     self.selected.remove(r)
             self.hyper.restore(snapshot)
+        if self.validation is not None and round_ok:
+            if self.mode == "hyper":
+                round_ok, metric = self.validation.test_hyper(self.hyper, n_val)
+            else:
+                if self.global_params is None:
+                    round_ok = False
+                else:
+                    round_ok, metric = self.validation.test(self.global_params)
+        trace.pop()
+        fl_pending, self._fl_pending = getattr(self, "_fl_pending", None), None
+        if fl_pending is not None:
+            fl_pending.result()  # (FLTrust's root training: finished by now; raises on a hand-off timeout)
         t4 = time.perf_counter()
         if round_ok:
             with trace.range("fl/checkpoint"):
@@ -1065,7 +1122,8 @@ class FLEngine:
                "t_aggregate": t3 - t2, "t_validate": t4 - t3, "t_checkpoint": t5 - t4, "t_round": t5 - t0,
                "n_selected": len(self.selected), "removed": removed}
         if self._attack_info:
-            rec["attack"] = {k: v for k, v in host_info(self._attack_info).items() if isinstance(v, (int, float))}
+            # every tried γ and its accept decision, not just the last one (the reference prints each γ)
+            rec["attack"] = {k: v for k, v in host_info(self._attack_info).items() if isinstance(v, (int, float, list))}
         lazy = info.pop("_lazy", None)
         if lazy is not None:
             info.update(lazy())
@@ -1103,17 +1161,24 @@ class FLEngine:
         P = self.P
         present = block[:, P] > 0.5
         size = torch.where(present, block[:, P + 2], torch.zeros_like(block[:, P + 2])).double()
-        red = torch.zeros(P + 3, dtype=torch.float64, device=block.device)
+        red = torch.zeros(P + 5, dtype=torch.float64, device=block.device)
         red[:P] = (size[:, None] * block[:, :P].double()).sum(0)
         red[P] = size.sum()
         red[P + 1] = (present & (block[:, P + 1] < 0.5)).double().sum()
         red[P + 2] = present.double().sum()
+        # decision words: all equal iff n * sum(w^2) == (sum w)^2 (exact in fp64 for 23-bit words)
+        word = float(self._decision_word())
+        red[P + 3] = word
+        red[P + 4] = word * word
         with trace.range("fl/allreduce"):
             if self.world > 1:
                 self.comm.all_reduce_(red)
             if self.phase_sync:
                 self._sync()
-        fl = red[P + 1:P + 3].cpu()  # one device -> host read for both counters (waits for the reduce)
+        fl = red[P + 1:P + 5].cpu()  # one device -> host read for the counters (waits for the reduce)
+        if float(fl[2]) ** 2 != self.world * float(fl[3]):
+            raise RuntimeError(f"ranks disagree on the replicated server state (round {self.round_no}); "
+                               "validation / detection must be bit-identical on every rank")
         round_ok = int(fl[0]) == 0 and int(fl[1]) == len(self.selected)
         if round_ok:
             self.global_params = (red[:P] / red[P]).to(torch.float32)

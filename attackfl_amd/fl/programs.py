@@ -501,12 +501,15 @@ class ProgramRunner:
         pg = self.prog
         if pg.model_name != "CNNModel" or not params.is_cuda or not pg.train or sgd_lr > 0.0 or max_steps is not None:
             return False
-        if os.environ.get("AFL_CNN2", "1") == "0" or pg.B > 128 or params.dtype != torch.float32:
-            return False
+        if os.environ.get("AFL_CNN2", "1") == "0" or pg.B > 128 or pg.B < 2 or params.dtype != torch.float32:
+            return False  # (the kernel needs 2 <= B <= 128: hipErrorInvalidValue otherwise)
         from .. import ops
+        from ..parallel.launcher import gpu_sharers
 
         nat = ops.native()
-        cus = torch.cuda.get_device_properties(params.device).multi_processor_count
+        # every workgroup must be resident at once; processes sharing the GPU run their own persistent launches
+        # on the same CUs, so this launch may count on only its share of them
+        cus = torch.cuda.get_device_properties(params.device).multi_processor_count // gpu_sharers()
         return params.shape[0] * int(nat.cnn2_wgs_per_client()) <= cus
 
     def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync):

@@ -18,8 +18,11 @@ NPARAM = 97665
 
 
 def fits(C: int, dev) -> bool:
-    """All 3*C workgroups must be resident at once (one per CU)."""
-    return 3 * C <= torch.cuda.get_device_properties(dev).multi_processor_count
+    """All 3*C workgroups must be resident at once (one per CU), next to the persistent launches of any other
+    process sharing the GPU (``parallel.launcher.gpu_sharers``)."""
+    from ..parallel.launcher import gpu_sharers
+
+    return 3 * C <= torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
 
 
 def _seeds(seeds, dev) -> torch.Tensor:

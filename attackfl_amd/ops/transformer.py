@@ -26,7 +26,10 @@ def auto_split(C: int, dev) -> int:
     workgroups with weights, optimizer state and activations held in registers / LDS) when every
     workgroup of every client fits on the device at once (one per CU); else the global-workspace
     kernels of ``transformer.hip`` with 2 or 1 workgroups per client."""
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    from ..parallel.launcher import gpu_sharers
+
+    # (processes sharing the GPU run their own persistent launches on the same CUs: count only this one's share)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
     return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 

@@ -49,6 +49,51 @@ def device_descriptor(device) -> Dict:
     return d
 
 
+_SHARERS: Optional[int] = None
+
+
+def set_gpu_sharers(n: int) -> None:
+    """Record how many processes of this run compute on this process's GPU (the classic launch learns it from
+    the registered device descriptors, ``serve_rendezvous``)."""
+    global _SHARERS
+    _SHARERS = max(1, int(n))
+
+
+def gpu_sharers() -> int:
+    """Processes of this run sharing this process's GPU.  Kernels that need all their workgroups co-resident
+    (the on-chip trainers spin on each other's counters) size themselves to ``CUs // gpu_sharers()``, because
+    the other processes' persistent launches occupy CUs too.  Sources, in order: ``set_gpu_sharers``,
+    ``AFL_GPU_SHARERS``, a packed launch with every rank pinned to one GPU (``AFL_BENCH_DEVICE`` or the
+    ``AFL_SHARED_GPU`` flag launch.py sets: all local ranks), otherwise local ranks per visible GPU."""
+    import os
+
+    if _SHARERS is not None:
+        return _SHARERS
+    env = os.environ.get("AFL_GPU_SHARERS")
+    if env:
+        return max(1, int(env))
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")) or 1)
+    if os.environ.get("AFL_BENCH_DEVICE") is not None or os.environ.get("AFL_SHARED_GPU") == "1":
+        return max(1, local)
+    try:
+        import torch
+
+        ndev = torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        ndev = 0
+    return max(1, -(-local // ndev)) if ndev > 0 else 1
+
+
+def max_sharers(descs: List[Dict]) -> int:
+    """Largest number of registered processes on one physical GPU (1 when none shares)."""
+    cnt: Dict[Tuple, int] = {}
+    for d in descs:
+        if d.get("type") == "cuda":
+            k = (d.get("host"), d.get("gpu"))
+            cnt[k] = cnt.get(k, 0) + 1
+    return max(cnt.values()) if cnt else 1
+
+
 def choose_backend(descs: List[Dict]) -> Tuple[str, bool]:
     """(process-group backend, one-shot IPC) for the classic launch: RCCL when every process owns a distinct
     GPU; gloo when some share one (RCCL refuses duplicate GPUs) or any is on the CPU.  The IPC all-gather is
@@ -86,7 +131,8 @@ def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0, device=None):
         print_with_color(f"[<<<] Received message from client: "
                          f"{ {k: v for k, v in d.items() if k != 'device'} }", "blue")
     backend, one_shot = choose_backend(descs)
-    store.set(PREFIX + "transport", json.dumps({"backend": backend, "one_shot": one_shot}))
+    store.set(PREFIX + "transport", json.dumps({"backend": backend, "one_shot": one_shot,
+                                                "sharers": max_sharers(descs)}))
     store.set(PREFIX + "table", json.dumps(table))
     print_with_color("All clients are connected. Sending notifications.", "green")
     return store, n + 1, table
@@ -94,6 +140,7 @@ def serve_rendezvous(cfg: Config, timeout_s: float = 3600.0, device=None):
 
 def read_transport(store) -> Tuple[str, bool]:
     t = json.loads(store.get(PREFIX + "transport").decode())
+    set_gpu_sharers(int(t.get("sharers", 1)))
     return str(t["backend"]), bool(t["one_shot"])
 
 

@@ -41,6 +41,8 @@ def main(argv=None) -> int:
         # every rank pinned to one GPU: keep all ranks' hardware queues mapped (see bench.py)
         from bench import shared_gpu_queues
 
+        os.environ["AFL_SHARED_GPU"] = "1"  # (parallel.launcher.gpu_sharers: all local ranks on one GPU)
+
         cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)  # the runtime default is 4 (never raised here)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(cur, shared_gpu_queues(world_env)))
 

@@ -65,7 +65,9 @@ def test_bisection_attacks_match_reference(kind, fn, scale):
     own = G[0].clone()
     res = fn(G, own, DistanceEngine(lay, "spectral"))
     ref_sd, ref_gamma = ref_bisection(gen, kind)
-    assert attacks.host_info(res.info)["gamma"] == pytest.approx(ref_gamma)
+    hi = attacks.host_info(res.info)
+    assert hi["gamma"] == pytest.approx(ref_gamma)
+    assert len(hi["gammas"]) == 6 and hi["gammas"][0] == 50.0 and hi["gammas"][-1] == pytest.approx(ref_gamma)
     assert torch.allclose(res.params, lay.flatten(ref_sd), atol=1e-5)
 
 
@@ -144,8 +146,16 @@ def test_device_bisection_matches_host_loop(decisions):
     it = iter(seq)
     last, n, succ = attacks._bisect(lambda g: next(it), 50.0, 1.0)
     it2 = iter(seq)
-    dl, dn, ds = attacks._bisect_device(lambda g: torch.tensor(next(it2)), 50.0, 1.0, "cpu")
+    dl, dn, ds, tried, accs = attacks._bisect_device(lambda g: torch.tensor(next(it2)), 50.0, 1.0, "cpu")
     assert (float(dl), dn, float(ds)) == (last, n, succ)
+    # the per-γ trace: the host loop's sequence of tried γs (src/Utils.py:119 prints each one)
+    host_tried, it3 = [], iter(seq)
+
+    def rec(g):
+        host_tried.append(g)
+        return next(it3)
+    attacks._bisect(rec, 50.0, 1.0)
+    assert tried.tolist() == host_tried and accs.tolist() == seq
     assert attacks.bisect_iterations(50.0, 1.0) == 6
 
 

@@ -102,6 +102,25 @@ def test_hyper_detection_runs(tmp_path):
     assert os.path.exists(os.path.join(tmp_path, "all_embeddings.npy"))
 
 
+def test_hyper_detection_rolls_back_before_validation(tmp_path):
+    """On a removal round the reference removes the flagged clients, rolls the hypernetwork back and only then
+    validates (server.py:532-543): the logged metric is test_hyper of the ROLLED-BACK hypernetwork over the
+    clients that reported (len(all_model_parameters)), and the removed client is not selected afterwards."""
+    d = _cfg(tmp_path, server__mode="hyper", server__num_round=3, server__clients=4)
+    d["server"]["hyper-detection"] = {"enable": True, "cosine-search": 10, "n_components": 2, "eps": 0.5,
+                                      "min_samples": 2}
+    eng = FLEngine(from_dict(d), device="cpu", verbose=False)
+    eng.run_round()
+    before = eng.hyper.snapshot()
+    eng.detector.step = lambda rnd, sel, embs: [3]           # force a removal this round
+    rec = eng.run_round()
+    assert rec["removed"] == [3] and eng.selected == [0, 1, 2]
+    assert torch.equal(eng.hyper.hnet.arena, before)          # rolled back
+    ok, auc = eng.validation.test_hyper(eng.hyper, 4)
+    assert rec["ok"] and ok and rec["metric"] == auc
+    eng.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
