@@ -26,7 +26,6 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..utils.log import print_with_color
 
 
 @dataclass
@@ -43,8 +42,40 @@ def fedavg(U: torch.Tensor, sizes: torch.Tensor, **_) -> AggResult:
 
 
 def mean_of(U: torch.Tensor) -> torch.Tensor:
-    w = torch.full((U.shape[0],), 1.0 / U.shape[0], dtype=torch.float64)
+    w = torch.full((U.shape[0],), 1.0 / U.shape[0], dtype=torch.float64, device=U.device)
     return ops.weighted_rows(U, w)
+
+
+def host_info(info: Dict) -> Dict:
+    """An aggregator's info with device values read back (the engine calls it where the host waits anyway,
+    after validation): bool masks become index lists, 0-d tensors numbers, vectors lists."""
+    out = {}
+    for k, v in info.items():
+        if torch.is_tensor(v):
+            v = v.cpu()
+            if v.dtype == torch.bool:
+                v = torch.nonzero(v).reshape(-1).tolist() if v.dim() else bool(v)
+            elif v.dim() == 0:
+                v = int(v) if not v.is_floating_point() else float(v)
+            else:
+                v = v.tolist()
+        out[k] = v
+    return out
+
+
+def _device_weights(sizes: torch.Tensor, device) -> torch.Tensor:
+    """Host sizes -> a device fp64 vector without a synchronising pageable copy."""
+    s = sizes.to(torch.float64)
+    if torch.device(device).type == "cuda" and s.device.type == "cpu":
+        s = s.pin_memory().to(device, non_blocking=True)
+    return s.to(device)
+
+
+def _masked_mean(U: torch.Tensor, keep: torch.Tensor, w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Weighted mean over the rows where ``keep`` (all rows when none is kept), on the device."""
+    keep = torch.where(keep.any(), keep, torch.ones_like(keep))
+    w = keep.double() if w is None else keep.double() * w
+    return ops.weighted_rows(U, w / w.sum())
 
 
 def trimmed_mean(U: torch.Tensor, sizes=None, trim_ratio: float = 0.1, **_) -> AggResult:
@@ -60,28 +91,27 @@ def median(U: torch.Tensor, sizes=None, **_) -> AggResult:
 
 
 def krum(U: torch.Tensor, sizes=None, f_rate: float = 0.0, **_) -> AggResult:
+    """Krum without a host read: fp64 Gram distances, each row's own distance pushed to +inf, a row sort,
+    the n-f-2 smallest summed and the argmin (first minimum, like ``np.argmin``) selected on the device."""
     n = U.shape[0]
     f = int(n * f_rate)
-    d2 = ops.pairwise_sqdist(U).double().cpu()
-    m = n - f - 2
-    scores = []
-    for i in range(n):
-        row = torch.cat([d2[i, :i], d2[i, i + 1:]])
-        closest = torch.sort(row).values[:max(m, 0)]
-        scores.append(float(closest.sum().item()))
-    sel = int(np.argmin(scores))
-    return AggResult(U[sel].clone(), True, {"selected": sel, "f": f, "scores": scores})
+    m = max(n - f - 2, 0)
+    d2 = ops.pairwise_sqdist(U).double()
+    d2 = d2 + torch.diag(torch.full((n,), float("inf"), dtype=torch.float64, device=d2.device))
+    scores = torch.sort(d2, dim=1).values[:, :m].sum(dim=1)
+    sel = torch.argmin(scores)
+    return AggResult(U.index_select(0, sel.reshape(1))[0], True, {"selected": sel, "f": f, "scores": scores})
 
 
 def shieldfl(U: torch.Tensor, sizes=None, **_) -> AggResult:
     norms = ops.row_norms(U).to(U.device)
     Un = U / (norms.to(U.dtype)[:, None] + 1e-8)
     ref = mean_of(Un)
-    cos = ops.cosine_to(Un, ref, eps=1e-8).float().cpu()
+    cos = ops.cosine_to(Un, ref, eps=1e-8).float()
     dev = 1.0 - cos
     w = 1.0 / (dev + 1e-6)
     w = w / w.sum()
-    return AggResult(ops.weighted_rows(U, w.double()), True, {"weights": w.tolist(), "cos": cos.tolist()})
+    return AggResult(ops.weighted_rows(U, w.double()), True, {"weights": w, "cos": cos})
 
 
 def _pca_project(U: torch.Tensor, r: int) -> np.ndarray:
@@ -128,31 +158,28 @@ def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, s
 
 
 def scionfl(U: torch.Tensor, sizes: torch.Tensor, seed: int = 0, **_) -> AggResult:
+    """All on the device: quantisation, L2-from-counts, the 3x-mean clip, the cosine-distance threshold
+    (the int(0.5 n)-th largest score) and the size-weighted FedAvg of the kept originals."""
     n = U.shape[0]
     sigma, smin, smax = ops.stochastic_quantize(U, seed)
-    smin = smin.double().cpu()
-    smax = smax.double().cpu()
-    ones = sigma.double().sum(dim=1).cpu()
+    smin = smin.double()
+    smax = smax.double()
+    ones = sigma.double().sum(dim=1)
     zeros = U.shape[1] - ones
     l2 = torch.sqrt(zeros * smin ** 2 + ones * smax ** 2)
-    l2_avg = float(l2.mean())
     MU, TOPK = 3.0, 0.5
-    for i in range(n):
-        if l2[i] > MU * l2_avg:
-            f = (MU * l2_avg) / float(l2[i])
-            smin[i] *= f
-            smax[i] *= f
-    deq = smin.to(U.device)[:, None].to(U.dtype) + sigma * (smax - smin).to(U.device)[:, None].to(U.dtype)
+    lim = MU * l2.mean()
+    fac = torch.where(l2 > lim, lim / l2, torch.ones_like(l2))
+    smin = smin * fac
+    smax = smax * fac
+    deq = smin.to(U.dtype)[:, None] + sigma * (smax - smin).to(U.dtype)[:, None]
     agg = mean_of(deq)
-    cosd = (1.0 - ops.cosine_to(deq, agg, eps=1e-8)).cpu()
-    scores = cosd.tolist()
-    thr = sorted(scores, reverse=True)[int(TOPK * n)] if n > 0 else 0.0
-    keep = [i for i, s in enumerate(scores) if s > thr]
-    if not keep:
-        print_with_color("[Warning] ScionFL kept no client (reference would crash); using all clients", "yellow")
-        keep = list(range(n))
-    kept_sizes = sizes[keep]
-    return AggResult(ops.fedavg(U[keep], kept_sizes), True, {"kept": keep, "scores": scores, "threshold": thr})
+    cosd = 1.0 - ops.cosine_to(deq, agg, eps=1e-8).double()
+    thr = torch.sort(cosd, descending=True).values[int(TOPK * n)] if n > 0 else torch.zeros((), device=U.device)
+    keep = cosd > thr
+    # (no client kept: the reference would crash; all clients are averaged instead)
+    out = _masked_mean(U, keep, _device_weights(sizes, U.device))
+    return AggResult(out, True, {"kept": keep, "scores": cosd, "threshold": thr})
 
 
 def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) -> AggResult:
@@ -170,12 +197,9 @@ def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) 
 
 
 def byzantine(U: torch.Tensor, sizes=None, threshold: float = 0.9, **_) -> AggResult:
-    cos = ops.cosine_to(U, U[0], eps=1e-8).cpu()
-    keep = [i for i in range(U.shape[0]) if float(cos[i]) >= threshold]
-    if not keep:
-        print_with_color("[Warning] No model passed the similarity threshold. Using fallback.", "yellow")
-        keep = list(range(U.shape[0]))
-    return AggResult(mean_of(U[keep]), True, {"kept": keep})
+    """Cosine >= 0.9 to model 0, mean of the kept rows (all rows when none passes), on the device."""
+    keep = ops.cosine_to(U, U[0], eps=1e-8) >= threshold
+    return AggResult(_masked_mean(U, keep), True, {"kept": keep})
 
 
 # Contract of every aggregator: ``U`` is READ-ONLY and may be the live client-model rows (single rank: the

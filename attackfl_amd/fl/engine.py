@@ -34,6 +34,7 @@ import torch
 
 from .. import ops
 from ..agg import AGGREGATORS, AggResult
+from ..agg import host_info as agg_host_info
 from ..attacks import DistanceEngine, host_info, run_attack
 from ..config import AttackSpec, Config
 from ..data import DeviceTable, resolve_dataset
@@ -1127,6 +1128,7 @@ class FLEngine:
         lazy = info.pop("_lazy", None)
         if lazy is not None:
             info.update(lazy())
+        info = agg_host_info(info)  # (device-resident aggregator outputs: read now, after validation)
         if self._trust is not None:
             info["trust"] = [round(float(x), 6) for x in self._trust.tolist()]
         rec.update({k: v for k, v in info.items() if isinstance(v, (int, float, list, str))})

@@ -201,9 +201,12 @@ def batches(nd: int, batch: int, skip_single: bool = True):
 
 
 def bce_loss(p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """``BCELoss`` (mean, log clamped at -100) without the input-range check, so a NaN output
-    reaches the NaN test (``client.py:100-102``) instead of raising inside the loss."""
-    return -(y * torch.clamp(torch.log(p), min=-100.0) + (1 - y) * torch.clamp(torch.log1p(-p), min=-100.0)).mean()
+    """``BCELoss`` (mean, log clamped at -100, torch's finite gradient at a saturated sigmoid) without the
+    input-range check, so a NaN output reaches the NaN test (``client.py:100-102``) instead of raising
+    inside the loss (``ops.composite.bce_loss``)."""
+    from ..ops.composite import bce_loss as _bce
+
+    return _bce(p, y)
 
 
 class EagerTrainer:

@@ -314,9 +314,7 @@ def stochastic_quantize(U: torch.Tensor, seed: int):
     if _dev(U):
         sigma, smin, smax = native().stoch_quant(U.contiguous(), int(seed) & 0x7FFFFFFFFFFFFFFF)
         return sigma, smin, smax
-    g = torch.Generator(device="cpu")
-    g.manual_seed(int(seed))
-    return composite.stochastic_quantize(U, g)
+    return composite.stochastic_quantize(U, int(seed) & 0x7FFFFFFFFFFFFFFF)  # (the kernel's uniforms)
 
 
 # ---------------------------------------------------------------- optimizer

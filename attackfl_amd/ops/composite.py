@@ -10,6 +10,35 @@ from typing import List, Sequence, Tuple
 import torch
 
 
+# ---------------------------------------------------------------- loss
+class _BCE(torch.autograd.Function):
+    """``nn.BCELoss`` (mean) forward AND backward, minus the [0, 1] input-range check.
+
+    Forward: ``-(y·max(log p, -100) + (1-y)·max(log1p(-p), -100))``, mean.  Backward: torch's
+    ``(p - y) / max(p (1 - p), 1e-12)`` per element over N — finite where the sigmoid saturates to exactly
+    0 or 1 in fp32.  Autograd through the clamped logs instead gives ``0 · inf = NaN`` there (the derivative
+    of the clamped branch is 0, of the log ∓inf), a NaN gradient the reference (``client.py:76`` BCELoss)
+    never produces: after an Opt-Fang round that turned a healthy reference client into a NaN-loss failure.
+    A NaN input still yields a NaN loss (the NaN abort test, ``client.py:100-102``)."""
+
+    @staticmethod
+    def forward(ctx, p, y):
+        ctx.save_for_backward(p, y)
+        lv = -(y * torch.clamp(torch.log(p), min=-100.0) + (1 - y) * torch.clamp(torch.log1p(-p), min=-100.0))
+        return lv.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        p, y = ctx.saved_tensors
+        gp = g * (p - y) / torch.clamp((1 - p) * p, min=1e-12) / p.numel()
+        return gp, None
+
+
+def bce_loss(p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Mean BCE of probabilities ``p`` against targets ``y`` with ``nn.BCELoss``'s gradient (``_BCE``)."""
+    return _BCE.apply(p, y.to(p.dtype).expand_as(p))
+
+
 # ---------------------------------------------------------------- column statistics / attacks
 def column_mean_std(G: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     mean = G.mean(dim=0)
@@ -102,13 +131,39 @@ def cosine_to(U: torch.Tensor, ref: torch.Tensor, eps: float = 1e-8) -> torch.Te
     return num / den
 
 
-def stochastic_quantize(U: torch.Tensor, generator: torch.Generator = None):
-    """ScionFL 1-bit quantisation per row: returns (sigma [N,P] {0,1}, smin [N], smax [N])."""
+def _mix64(z):
+    """``afl_mix64`` (csrc/common.h, splitmix64 finaliser) on a numpy uint64 array."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def afl_uniform(seed: int, n: int) -> torch.Tensor:
+    """The [n] fp32 uniforms ``afl_uniform(seed, 0..n-1)`` of the device kernels (bit-identical)."""
+    import numpy as np
+
+    ctr = np.arange(n, dtype=np.uint64)
+    x = _mix64(np.uint64(int(seed) & 0xFFFFFFFFFFFFFFFF) ^ _mix64(ctr)) >> np.uint64(40)
+    return torch.from_numpy((x.astype(np.float32) * np.float32(1.0 / 16777216.0)).astype(np.float32))
+
+
+def stochastic_quantize(U: torch.Tensor, seed=None):
+    """ScionFL 1-bit quantisation per row: returns (sigma [N,P] {0,1}, smin [N], smax [N]).  ``seed`` (int):
+    the device kernel's counter-based uniforms ``afl_uniform(seed, row * P + col)`` — the same bits as
+    ``k_stoch_quant``; a ``torch.Generator`` or None draws with torch instead."""
     smin = U.min(dim=1).values
     smax = U.max(dim=1).values
     probs = (U - smin[:, None]) / (smax - smin + 1e-6)[:, None]
-    u = torch.rand(U.shape, generator=generator, device=U.device, dtype=U.dtype) if generator is not None \
-        else torch.rand_like(U)
+    if isinstance(seed, int):
+        u = afl_uniform(seed, U.numel()).reshape(U.shape).to(U.device)
+    elif seed is not None:
+        u = torch.rand(U.shape, generator=seed, device=U.device, dtype=U.dtype)
+    else:
+        u = torch.rand_like(U)
     sigma = (u < probs).to(U.dtype)
     return sigma, smin, smax
 

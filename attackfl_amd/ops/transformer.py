@@ -191,7 +191,7 @@ def step_masks(seed: int, step: int, n: int) -> dict:
 def reference_train(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,
                     lr: float, seeds: Sequence[int], opt_mode: int = 0, max_steps: int = -1):
     """fp32 PyTorch oracle of ``train_clients`` (CPU).  Returns (ok [C], losses [C, E])."""
-    from .composite import adam_step
+    from .composite import adam_step, bce_loss
 
     C = params.shape[0]
     oks, losses = [], torch.zeros(C, epochs)
@@ -220,7 +220,7 @@ def reference_train(params: torch.Tensor, rows: torch.Tensor, order: torch.Tenso
                 leaf = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
                 out = reference_forward(leaf, r[:, :7], r[:, 7:23], step_masks(int(seeds[ci]) & 0x7FFFFFFF, step, Bn))
                 y = r[:, 23:24]
-                loss = -(y * torch.clamp(torch.log(out), min=-100) + (1 - y) * torch.clamp(torch.log1p(-out), min=-100)).mean()
+                loss = bce_loss(out, y)  # (nn.BCELoss forward and backward, as the kernel)
                 if torch.isnan(loss):
                     ok = False
                     break

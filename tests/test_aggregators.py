@@ -36,6 +36,7 @@ def test_krum_picks_reference_argmin():
     U = _U(7)
     U[3] += 5.0  # outlier
     res = agg.krum(U)
+    res.info = agg.host_info(res.info)
     n, f = 7, 0
     vec = U.numpy().astype(np.float64)
     scores = []
@@ -49,6 +50,7 @@ def test_krum_picks_reference_argmin():
 def test_shieldfl_weights():
     U = _U(5)
     res = agg.shieldfl(U)
+    res.info = agg.host_info(res.info)
     vecs = [u / (u.norm() + 1e-8) for u in U]
     ref = sum(vecs) / len(vecs)
     cos = torch.tensor([F.cosine_similarity(v.view(1, -1), ref.view(1, -1)).item() for v in vecs])
@@ -61,6 +63,7 @@ def test_shieldfl_weights():
 def test_scionfl_keeps_least_similar_half():
     U = _U(6)
     res = agg.scionfl(U, torch.full((6,), 100.0), seed=3)
+    res.info = agg.host_info(res.info)
     s = res.info["scores"]
     thr = sorted(s, reverse=True)[3]
     assert res.info["kept"] == [i for i, x in enumerate(s) if x > thr]
@@ -85,6 +88,7 @@ def test_byzantine_filter():
     U = _U(5)
     U[2] = -U[2]
     res = agg.byzantine(U)
+    res.info = agg.host_info(res.info)
     assert 2 not in res.info["kept"]
 
 

@@ -223,14 +223,44 @@ def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
     spec = "4:Min-Max:2" if attack == "Min-Max" else "4:LIE:2:0.74"
     eng = FLEngine(cfg, device="cuda", table=build_client_table(cfg, 1, parse_attackers(spec)), verbose=False)
     assert eng.trainer.kind == "fused"
+    # every round's device aggregate against the CPU composite of the same rule on the same gathered rows
+    seen = []
+    orig = eng._aggregate
+
+    def capture(U, sizes, attackers, round_ok):
+        rows = U.detach().cpu().clone()
+        info = orig(U, sizes, attackers, round_ok)
+        seen.append((rows, sizes.clone(), attackers.clone(), eng.global_params.detach().cpu().clone(), eng.round_no))
+        return info
+
+    eng._aggregate = capture
     hist = eng.run()
     eng.close()
     assert [r["ok"] for r in hist] == [True, True, True]
+    assert len(seen) == 3
+    if mode != "FLTrust":  # (FLTrust trains a server model: its composite would need the CPU trainer)
+        from attackfl_amd.agg import AGGREGATORS
+        for rows, sizes, att, got, rnd in seen:
+            ref = AGGREGATORS[mode](rows, sizes, attackers=att, seed=eng.seed * 13 + rnd).params
+            tol = 1e-6 if mode in ("median", "trimmed_mean", "krum") else 2e-5
+            assert (got - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (mode, rnd)
     assert all(0.0 <= r["metric"] <= 1.0 for r in hist)
     assert "attack" in hist[1] and "attack" in hist[2]
     if mode == "FLTrust":
         assert len(hist[-1]["trust"]) == 5 and all(t >= 0.0 for t in hist[-1]["trust"])
     assert os.path.exists(os.path.join(tmp_path, "TransformerModel.pth"))
+
+
+def test_stoch_quant_matches_cpu_mirror(gpu):
+    """k_stoch_quant's Bernoulli draws are the counter-based afl_uniform the CPU composite mirrors bit for bit."""
+    from attackfl_amd import ops
+    from attackfl_amd.ops import composite as C
+
+    U = torch.randn(6, 5000, generator=torch.Generator().manual_seed(0))
+    s_d, lo_d, hi_d = ops.stochastic_quantize(U.to(gpu), 1234)
+    s_c, lo_c, hi_c = C.stochastic_quantize(U, 1234)
+    assert torch.equal(lo_d.cpu(), lo_c) and torch.equal(hi_d.cpu(), hi_c)
+    assert (s_d.cpu() != s_c).sum().item() == 0
 
 
 def test_hyper_detection_end_to_end(gpu, tmp_path):

@@ -153,3 +153,25 @@ def test_training_is_bit_reproducible(gpu, split):
         T.train_clients(p, rows, plan.order[lo:lo + 2].contiguous(), plan.nd[lo:lo + 2], 2, 128, 0.004,
                         seeds[lo:lo + 2], split=split)
         assert torch.equal(p, full[0][lo:lo + 2])
+
+
+def test_saturated_sigmoid_start_matches_oracle(gpu):
+    """The post-Opt-Fang start whose fp32 outputs saturate (tests/test_loss_parity.py): the fused trainer and
+    the fp32 oracle both train it (no NaN abort) and end close — torch's BCELoss gradient on both sides."""
+    from test_loss_parity import saturated_start
+
+    ds = synthetic_icu(4000, seed=3)
+    rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1)
+    start = saturated_start()
+    plan = make_plan(rows.shape[0], [1000, 1000], 2, [5, 6], "cpu")
+    params = torch.stack([start, start])
+    ref = params.clone()
+    ok_r, loss_r = T.reference_train(ref, rows, plan.order, plan.nd, 2, 128, 0.004, [11, 12])
+    dev = params.clone().to(gpu)
+    ok, loss = T.train_clients(dev, rows.to(gpu), plan.order.to(gpu), plan.nd, 2, 128, 0.004, [11, 12])
+    assert ok.tolist() == ok_r.tolist() == [1, 1]
+    assert torch.isfinite(dev).all()
+    d = (dev.cpu() - ref).abs()
+    moved = (ref - params).abs()
+    assert d.mean().item() < 0.15 * moved.mean().item(), (d.mean(), moved.mean())
+    assert torch.allclose(loss, loss_r, rtol=0.1, atol=0.05), (loss, loss_r)

@@ -36,7 +36,8 @@ def cells(spec: str):
     return [(m, a) for m in MODES for a in ATTACKS]
 
 
-def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0) -> dict:
+def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0, genuine_rate: float = 0.5,
+             distance: str = "spectral") -> dict:
     import torch
 
     if threads:
@@ -49,11 +50,11 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0)
     tmp = tempfile.mkdtemp(prefix="afl_study_")
     d = {
         "server": {"num-round": rounds, "clients": 8, "mode": mode, "model": "TransformerModel", "data-name": "ICU",
-                   "genuine-rate": 0.5, "random-seed": 1, "data-distribution": {"num-data-range": [800, 1200]}},
+                   "genuine-rate": genuine_rate, "random-seed": 1, "data-distribution": {"num-data-range": [800, 1200]}},
         "learning": {"epoch": 2, "batch-size": 128, "learning-rate": 0.004},
         "data": {"synthetic": True, "train-size": 20000, "test-size": 3000},
         "engine": {"checkpoint-dir": tmp, "trainer": "auto" if device.startswith("cuda") else "oracle", "seed": 7,
-                   "max-retries": 5},
+                   "max-retries": 5, "distance": distance},
         "log_path": tmp,
     }
     cfg = from_dict(d)
@@ -69,15 +70,18 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0)
     eng.close()
     ok = [r for r in hist if r["ok"]]
     return {"device": "gpu" if device.startswith("cuda") else "cpu", "mode": mode, "attack": attack,
+            "genuine_rate": genuine_rate, "distance": distance,
             "attackers": len(atk), "rounds": len(ok), "failed_rounds": len(hist) - len(ok), "stalled": stalled,
             "auc": [round(r["metric"], 5) for r in ok], "final_auc": round(ok[-1]["metric"], 5) if ok else None,
             "attack_gamma": [round(r["attack"]["gamma"], 4) for r in ok if "attack" in r and "gamma" in r["attack"]],
+            # every tried γ of the last attacking round (the reference prints each, src/Utils.py:119)
+            "gammas_last": next((r["attack"]["gammas"] for r in reversed(hist) if "gammas" in r.get("attack", {})), None),
             "seconds": round(time.time() - t0, 2)}
 
 
 def _worker(args):
-    mode, attack, device, rounds, threads = args
-    return run_cell(mode, attack, device, rounds, threads)
+    mode, attack, device, rounds, threads, gr, dist = args
+    return run_cell(mode, attack, device, rounds, threads, gr, dist)
 
 
 def main() -> int:
@@ -87,6 +91,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--cells", default="", help="mode:attack,... (default: every mode x attack)")
     ap.add_argument("--jobs", type=int, default=1, help="parallel CPU processes")
+    ap.add_argument("--genuine-rate", type=float, default=0.5, help="server.genuine-rate (reference default 0.5)")
+    ap.add_argument("--distance", default="spectral", choices=["spectral", "flat"])
     args = ap.parse_args()
     todo = cells(args.cells)
     with open(args.out, "a") as fh:
@@ -95,13 +101,14 @@ def main() -> int:
 
             threads = max(1, (os.cpu_count() or 8) // args.jobs)
             with mp.get_context("spawn").Pool(args.jobs) as pool:
-                for res in pool.imap_unordered(_worker, [(m, a, args.device, args.rounds, threads) for m, a in todo]):
+                for res in pool.imap_unordered(_worker, [(m, a, args.device, args.rounds, threads, args.genuine_rate,
+                                                                   args.distance) for m, a in todo]):
                     fh.write(json.dumps(res) + "\n")
                     fh.flush()
                     print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)
         else:
             for m, a in todo:
-                res = run_cell(m, a, args.device, args.rounds)
+                res = run_cell(m, a, args.device, args.rounds, 0, args.genuine_rate, args.distance)
                 fh.write(json.dumps(res) + "\n")
                 fh.flush()
                 print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)

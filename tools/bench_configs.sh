@@ -10,6 +10,13 @@ run() {
   tail -1 /tmp/bench_cfg.log >> "$OUT"
   tail -1 /tmp/bench_cfg.log | cut -c1-160
 }
+if [ "${SET:-all}" = "robust" ] || [ "${SET:-all}" = "all" ]; then
+  # robust server modes (reference server.py:286-494, 682-743), each with one Min-Max attacker
+  for m in trimmed_mean median krum shieldfl scionfl FLTrust gmm fltracer byzantine; do
+    run --model TransformerModel --mode $m --attackers "7:Min-Max:2"
+  done
+fi
+[ "${SET:-all}" = "robust" ] && exit 0
 run --model TransformerModel
 run --model TransformerModel --attackers "7:LIE:2:0.74"
 run --model TransformerModel --attackers "7:Min-Max:2"
