@@ -195,6 +195,44 @@ def _bisect_device(accept: Callable[[torch.Tensor], torch.Tensor], gamma: float,
     return last, n, succ, torch.zeros(0, dtype=torch.float64), torch.zeros(0, dtype=torch.bool)
 
 
+def _bisect_fused(cd: "_CandidateDistances", threshold: torch.Tensor, kind: str, gamma: float, tau: float):
+    """The whole bisection as fused HIP launches (``linalg.hip`` ``bisect_decide``): ONE launch for every
+    iteration when no distance needs a spectral norm (flat mode, or vector-shaped tensors only); otherwise
+    one ``k_spec_eval<true>`` per γ whose last-arriving workgroup sums the K distances, makes the accept
+    decision and moves γ on the device.  Returns the ``_bisect_device`` tuple, or None where a distance
+    needs the generic path (matrix slots outside the Gram form, e.g. CNN fc1 / convs)."""
+    from .. import ops
+
+    n = bisect_iterations(gamma, tau)
+    if n == 0 or n > 16:
+        return None
+    K = cd.G.shape[0]
+    dev = cd.G.device
+    if cd.engine.mode == "flat":
+        vA, vB, vC = cd.A.reshape(K, 1), cd.B.reshape(K, 1), cd.C.reshape(1)
+        fam = None
+    else:
+        if cd.engine.mat_slots and (cd.fam is None or cd.fam.rest or cd.fam.arena is None):
+            return None
+        fam = cd.fam if cd.engine.mat_slots else None
+        vA, vB, vC = (cd.A, cd.B, cd.C) if cd.vec else (None, None, None)
+    vA, vB, vC = [None if t is None else t.to(torch.float64).contiguous() for t in (vA, vB, vC)]
+    st = torch.zeros(40, dtype=torch.float64, device=dev)
+    st[0] = float(gamma)
+    thr = threshold.to(device=dev, dtype=torch.float64).reshape(1)
+    k = 1 if kind == "sum" else 0
+    nat = ops.native()
+    if fam is None:
+        nat.bisect_vec(st, vA, vB, vC, thr, K, k, n, float(gamma))
+    else:
+        ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        step = float(gamma)
+        for it in range(n):
+            nat.spec_bisect(fam.arena, fam.tab, fam.sumq, K - 1, st, ctr, vA, vB, vC, thr, k, it, step)
+            step /= 2.0
+    return st[2], n, st[1], st[4:4 + n], st[20:20 + n] > 0.5
+
+
 def host_info(info: Dict) -> Dict:
     """An attack's info dict with device values read back (call where the host synchronises anyway): 0-d
     tensors become floats, vectors (the per-γ trace) lists."""
@@ -246,7 +284,8 @@ def _minmax_family(G: torch.Tensor, own: torch.Tensor, engine: DistanceEngine, k
         d = cand_d(g)
         return ((d ** 2).sum() < threshold) if kind == "sum" else (d.max() < threshold)
 
-    last, iters, succ, tried, accs = _bisect_device(accept, gamma, tau, G.device)
+    fused = _bisect_fused(cand_d, threshold, kind, gamma, tau) if G.is_cuda else None
+    last, iters, succ, tried, accs = fused if fused is not None else _bisect_device(accept, gamma, tau, G.device)
     mal = st.mean - last * dev
     return AttackResult(True, mal, {"gamma": last, "gamma_succ": succ, "iters": iters, "threshold": threshold,
                                     "gammas": tried, "accepted": accs})

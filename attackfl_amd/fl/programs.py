@@ -296,7 +296,113 @@ class HARProgram(_Program):
         s = self.slot["pe.pe"]
         return (s.offset, s.offset + s.numel)
 
+    # ---- device path: the bf16 encoder of csrc/kernels/har.hip (five launches per layer) --------------
+    def _fused(self, params) -> bool:
+        return params.is_cuda and os.environ.get("AFL_HAR_FUSED", "1") != "0"
+
+    def _lw(self, i) -> list:
+        """Flat offsets of layer i's parameters (AflHarLayerW order)."""
+        names = ["self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight",
+                 "self_attn.out_proj.bias", "norm1.weight", "norm1.bias", "linear1.weight", "linear1.bias",
+                 "linear2.weight", "linear2.bias", "norm2.weight", "norm2.bias"]
+        return [self.slot[self.lyr(i, n)].offset for n in names]
+
+    def _lp(self) -> int:
+        return (self.L + 63) // 64 * 64
+
+    def _groups(self) -> int:
+        """Workgroups per client of the backward row passes (8 clients: one per CU).  Fixed, NOT a function of
+        the client count: the weight-gradient partials are summed in workgroup order, so a client's gradients
+        are the same bits whichever clients share the launch (placement independence)."""
+        return 32
+
+    def _post_seg(self, i) -> torch.Tensor:
+        key = f"_seg_post{i}"
+        if key not in self._bufs:
+            o = self._lw(i)
+            # partial layout (har.hip G_*): Wo | W1 | W2 | bo g1 be1 b1(256) b2 g2 be2
+            segs = [(0, o[2], 4096), (4096, o[6], 16384), (20480, o[8], 16384), (36864, o[3], 64), (36928, o[4], 64),
+                    (36992, o[5], 64), (37056, o[7], 256), (37312, o[9], 64), (37376, o[10], 64), (37440, o[11], 64)]
+            self._bufs[key] = torch.tensor(segs, dtype=torch.int32, device=self.device)
+        return self._bufs[key]
+
+    def _qkv_seg(self, i) -> torch.Tensor:
+        key = f"_seg_qkv{i}"
+        if key not in self._bufs:
+            o = self._lw(i)
+            self._bufs[key] = torch.tensor([(0, o[0], 192 * 64), (192 * 64, o[1], 192)], dtype=torch.int32,
+                                           device=self.device)
+        return self._bufs[key]
+
+    def _forward_fused(self, params, ctl):
+        from .. import ops
+
+        nat = ops.native()
+        C, B, L = self.C, self.B, self.L
+        R, Lp = B * L, self._lp()
+        bf = torch.bfloat16
+        p = self.p(0.1)
+        seeds, stepctl = (ctl.seeds, ctl.stepctl) if (ctl is not None and p > 0.0) else (None, None)
+        h = self.buf("hb0", C, R, 64, dtype=bf)
+        nat.har_stem(self.buf("x", C, B, L), params, self.slot["conv.weight"].offset, self.slot["conv.bias"].offset,
+                     self.slot["pe.pe"].offset, h)
+        for i in range(self.NL):
+            w = self._lw(i)
+            qkv = self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf)  # padding rows stay zero
+            nat.har_qkv(h, params, w[0], w[1], qkv, B, L, 0.25)
+            o, lse2 = self.buf(f"ob{i}", C, R, 64, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp)
+            nat.har_attn_fwd(qkv, o, lse2, B, L, seeds, stepctl, 10 * i, p)
+            y = self.buf(f"hb{i + 1}", C, R, 64, dtype=bf)
+            nat.har_post(o, h, self.buf(f"xh1_{i}", C, R, 64, dtype=bf), self.buf(f"xh2_{i}", C, R, 64, dtype=bf),
+                         self.buf(f"rs{i}", C, R, 2), y, params, w, seeds, stepctl, 10 * i, p)
+            h = y
+        pooled, c1, logits = self.buf("pool", C, B, 64), self.buf("c1", C, B, 64), self.buf("logits", C, B, 6)
+        nat.har_pool(h, B, L, pooled)
+        self.linear(pooled, params, "classifier.0.weight", "classifier.0.bias", c1, act=ACT_RELU, ctl=ctl, layer=30,
+                    p=0.3)
+        self.linear(c1, params, "classifier.3.weight", "classifier.3.bias", logits)
+        return logits
+
+    def _backward_fused(self, params, grads, ctl):
+        from .. import ops
+
+        nat = ops.native()
+        C, B, L = self.C, self.B, self.L
+        R, Lp, G = B * L, self._lp(), self._groups()
+        bf = torch.bfloat16
+        p = self.p(0.1)
+        seeds, stepctl = (ctl.seeds, ctl.stepctl) if (ctl is not None and p > 0.0) else (None, None)
+        dlog, dc1, dpool = self.buf("dz", C, B, 6), self.buf("dc1", C, B, 64), self.buf("dpool", C, B, 64)
+        c1 = self.buf("c1", C, B, 64)
+        self.linear_bwd(dlog, c1, params, grads, "classifier.3.weight", "classifier.3.bias", dc1, G=c1,
+                        gact=ACT_RELU, ctl=ctl, layer=30, p=0.3)
+        self.linear_bwd(dc1, self.buf("pool", C, B, 64), params, grads, "classifier.0.weight", "classifier.0.bias",
+                        dpool)
+        ws_p = self.buf("ws_post", C * G * int(nat.har_post_ng))
+        ws_q = self.buf("ws_qkv", C * G * int(nat.har_qkv_ng))
+        dres, dout = self.buf("dres", C, R, 64), self.buf("doutb", C, R, 64, dtype=bf)
+        delta, dqkv = self.buf("delta", C * B * 4, Lp), self.buf("dqkvb", C * B * 4, 3, Lp, 16, dtype=bf)
+        dxs = [self.buf("dxA", C, R, 64), self.buf("dxB", C, R, 64)]
+        dy = None
+        for i in reversed(range(self.NL)):
+            w = self._lw(i)
+            nat.har_post_bwd(dy, dpool if dy is None else None, B, L, self.buf(f"ob{i}", C, R, 64, dtype=bf),
+                             self.buf(f"xh1_{i}", C, R, 64, dtype=bf), self.buf(f"xh2_{i}", C, R, 64, dtype=bf),
+                             self.buf(f"rs{i}", C, R, 2), dres, dout, delta, ws_p, params, w, seeds, stepctl, 10 * i,
+                             p, G)
+            nat.har_reduce(ws_p, G, int(nat.har_post_ng), self._post_seg(i), grads)
+            nat.har_attn_bwd(self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp),
+                             dout, delta, dqkv, B, L, seeds, stepctl, 10 * i, p)
+            dx = dxs[i % 2]
+            nat.har_qkv_bwd(dqkv, dres, self.buf(f"hb{i}", C, R, 64, dtype=bf), dx, ws_q, params, w[0], B, L, G)
+            nat.har_reduce(ws_q, G, int(nat.har_qkv_ng), self._qkv_seg(i), grads)
+            dy = dx
+        Lx.conv_pe_bwd(self.buf("x", C, B, L), dy, grads, self.slot["conv.weight"].offset,
+                       self.slot["conv.bias"].offset)
+
     def forward(self, params, ctl):
+        if self._fused(params):
+            return self._forward_fused(params, ctl)
         C, B, L = self.C, self.B, self.L
         R = B * L
         h = self.buf("h0", C, R, 64)
@@ -327,6 +433,8 @@ class HARProgram(_Program):
         return logits
 
     def backward(self, params, grads, ctl):
+        if self._fused(params):
+            return self._backward_fused(params, grads, ctl)
         C, B, L = self.C, self.B, self.L
         R = B * L
         dlog, dc1, dpool = self.buf("dz", C, B, 6), self.buf("dc1", C, B, 64), self.buf("dpool", C, B, 64)

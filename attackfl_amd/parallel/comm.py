@@ -1,9 +1,11 @@
 """Collective transport for FL rounds (replaces the reference's RabbitMQ/pika/pickle transport,
 ``server.py:102-108,187-203``, ``src/RpcClient.py:42-56,174-188``).
 
-One round moves, per rank, a fixed-layout ``[S, P+4]`` fp32 block (S client slots: flat update
-row + [valid, result, size, is_attacker]) with ONE all-gather, and one small control broadcast
-from the leader.  Backends:
+One round moves, per rank, a fixed-layout ``[S, W]`` fp32 block (S client slots: flat update row +
+[valid, result, size, is_attacker, decision word] + the epoch losses) with ONE all-gather — or, for plain
+FedAvg over the process group, ONE all-reduce.  There is no control message: every rank runs the same
+deterministic server step on the gathered rows and reaches the same decisions (the decision word checks
+that they did, ``FLEngine._check_decisions``).  Backends:
 
 * ``LoopbackComm``  — single process (world 1), zero-copy.
 * ``TorchComm``     — ``torch.distributed``: ``nccl`` (= RCCL over xGMI on MI355X) for device

@@ -16,13 +16,34 @@ every rank fall back to the process group's own all-gather together.
 """
 from __future__ import annotations
 
+import contextlib
 import socket
-from typing import Optional
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
-from ..ops import native
+from .. import ops
+
+
+def setup_verdict(local_err: str, infos: Sequence[Tuple[str, int, bytes]], rank: int,
+                  can_access=None) -> str:
+    """This rank's verdict on the IPC path from everyone's ``(host, device index, handle)`` (``""`` = usable):
+    a local failure, ranks on several hosts, a peer without an exported buffer, or a peer GPU this GPU cannot
+    map (``can_access(peer device index) -> bool``, hipDeviceCanAccessPeer; a peer on the same device needs
+    no peer access).  Pure host logic — the ranks then AND their verdicts (``IpcAllGather._agree``)."""
+    if local_err:
+        return local_err
+    if len({h for h, _, _ in infos}) != 1:
+        return "ranks span several hosts"
+    if any(len(hd) == 0 for _, _, hd in infos):
+        return "a peer could not export its buffer"
+    me = infos[rank][1]
+    if can_access is not None:
+        bad = sorted({d for r, (_, d, _) in enumerate(infos) if r != rank and d != me and not can_access(d)})
+        if bad:
+            return f"no peer access from GPU {me} to GPU(s) {bad}"
+    return ""
 
 
 class IpcUnavailable(RuntimeError):
@@ -44,33 +65,43 @@ class IpcAllGather:
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
         return bool(int(t.item()) == 1)
 
+    def _on_device(self):
+        return torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
+
+    def _can_access(self, peer: int) -> bool:
+        if self.device.type != "cuda":
+            return False
+        try:
+            return bool(torch.cuda.can_device_access_peer(self.device.index or 0, int(peer)))
+        except Exception:  # noqa: BLE001 - a device index this process cannot see
+            return False
+
     def setup(self, n: int) -> None:
         """Collective: allocate ``n`` floats per sender slot, map every peer, verify.  Raises
-        ``IpcUnavailable`` on every rank if any rank fails."""
+        ``IpcUnavailable`` on every rank if any rank fails (alloc / export, hosts, peer access, open, the
+        self-test) — the ranks AND their verdicts, so they all fall back to the process group together."""
         self.close()
         ctx, handle, err = None, b"", ""
         try:
-            with torch.cuda.device(self.device):
-                ctx = native().IpcContext(self.rank, self.world, int(n))
+            with self._on_device():
+                ctx = ops.native().IpcContext(self.rank, self.world, int(n))
                 handle = ctx.handle()
         except Exception as e:  # noqa: BLE001 - reported collectively below
             err = f"alloc/export: {e}"
         info = [None] * self.world
-        dist.all_gather_object(info, (socket.gethostname(), handle), group=self.pg)
-        if not err and len({h for h, _ in info}) != 1:
-            err = "ranks span several hosts"
-        if not err and any(len(hd) == 0 for _, hd in info):
-            err = "a peer could not export its buffer"
+        dev_index = (self.device.index or 0) if self.device.type == "cuda" else -1
+        dist.all_gather_object(info, (socket.gethostname(), dev_index, handle), group=self.pg)
+        err = setup_verdict(err, info, self.rank, self._can_access)
         if not err:
             try:
-                with torch.cuda.device(self.device):
-                    ctx.open([hd for _, hd in info])
+                with self._on_device():
+                    ctx.open([hd for _, _, hd in info])
             except Exception as e:  # noqa: BLE001
                 err = f"open: {e}"
         if not err:
             # self-test with the real block size (both parities), short deadline
             try:
-                with torch.cuda.device(self.device):
+                with self._on_device():
                     for ep in range(2):
                         src = torch.arange(n, device=self.device, dtype=torch.float32) + (1000.0 * self.rank + ep)
                         out = ctx.all_gather(src, 5.0)

@@ -7,6 +7,7 @@
 
 void afl_register_layers(pybind11::module& m);  // layers_bind.cpp
 void afl_register_ipc(pybind11::module& m);     // comm/ipc.cpp
+void afl_register_har(pybind11::module& m);     // har_bind.cpp
 
 namespace {
 
@@ -180,6 +181,62 @@ torch::Tensor spec_eval(torch::Tensor arena, torch::Tensor tab, int64_t sumq, in
   TORCH_CHECK(afl_spec_eval(arena.data_ptr<double>(), sumq, (int)M, gp, tab.data_ptr<int>(), S, out.data_ptr<double>(),
                             cur()) == 0,
               "spec_eval launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
+// fused bisection (linalg.hip): st [40] fp64, ctr [1] int32, vA/vB [K, Sv] + vC [Sv] fp64 (optional), thr [1] fp64
+static AflBisect make_bisect(torch::Tensor st, c10::optional<torch::Tensor> ctr, c10::optional<torch::Tensor> vA,
+                             c10::optional<torch::Tensor> vB, c10::optional<torch::Tensor> vC, torch::Tensor thr,
+                             int64_t K, int64_t kind) {
+  check_dev(st, "st", torch::kFloat64);
+  check_dev(thr, "thr", torch::kFloat64);
+  TORCH_CHECK(st.numel() >= 40 && thr.numel() == 1, "bisect: state [40], threshold scalar");
+  AflBisect b{};
+  b.st = st.data_ptr<double>();
+  b.thr = thr.data_ptr<double>();
+  b.K = (int)K;
+  b.kind = (int)kind;
+  if (ctr.has_value() && ctr->defined()) {
+    check_dev(*ctr, "ctr", torch::kInt32);
+    b.ctr = (unsigned*)ctr->data_ptr<int>();
+  }
+  if (vA.has_value() && vA->defined()) {
+    check_dev(*vA, "vA", torch::kFloat64);
+    check_dev(*vB, "vB", torch::kFloat64);
+    check_dev(*vC, "vC", torch::kFloat64);
+    TORCH_CHECK(vA->dim() == 2 && vA->size(0) == K && vB->sizes() == vA->sizes() && vC->numel() == vA->size(1) &&
+                    vA->is_contiguous() && vB->is_contiguous() && vC->is_contiguous(),
+                "bisect: vA/vB [K, Sv] and vC [Sv], contiguous");
+    b.vA = vA->data_ptr<double>();
+    b.vB = vB->data_ptr<double>();
+    b.vC = vC->data_ptr<double>();
+    b.Sv = (int)vA->size(1);
+  }
+  return b;
+}
+
+void bisect_vec(torch::Tensor st, torch::Tensor vA, torch::Tensor vB, torch::Tensor vC, torch::Tensor thr, int64_t K,
+                int64_t kind, int64_t n_iter, double step0) {
+  const AflBisect b = make_bisect(st, c10::nullopt, vA, vB, vC, thr, K, kind);
+  TORCH_CHECK(afl_bisect_vec(&b, (int)n_iter, step0, cur()) == 0, "bisect_vec: at most 16 iterations");
+  AFL_CHECK_LAUNCH();
+}
+
+torch::Tensor spec_bisect(torch::Tensor arena, torch::Tensor tab, int64_t sumq, int64_t M, torch::Tensor st,
+                          torch::Tensor ctr, c10::optional<torch::Tensor> vA, c10::optional<torch::Tensor> vB,
+                          c10::optional<torch::Tensor> vC, torch::Tensor thr, int64_t kind, int64_t it, double step) {
+  check_dev(arena, "arena", torch::kFloat64);
+  check_dev(tab, "tab", torch::kInt32);
+  TORCH_CHECK(arena.numel() == (2 * M + 1) * sumq, "spec_bisect: arena size");
+  TORCH_CHECK(it >= 0 && it < 16, "spec_bisect: iteration index");
+  const AflBisect b = make_bisect(st, ctr, vA, vB, vC, thr, M + 1, kind);
+  TORCH_CHECK(b.ctr != nullptr, "spec_bisect: arrival counter required");
+  const int S = tab.size(0);
+  auto out = torch::empty({M, S}, arena.options());
+  TORCH_CHECK(afl_spec_bisect(arena.data_ptr<double>(), sumq, (int)M, tab.data_ptr<int>(), S, out.data_ptr<double>(),
+                              &b, (int)it, step, cur()) == 0,
+              "spec_bisect: needs M > 0 rows and S > 0 Gram slots");
   AFL_CHECK_LAUNCH();
   return out;
 }
@@ -599,6 +656,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spectral_norm_slots", &spectral_norm_slots);
   m.def("spec_grams", &spec_grams);
   m.def("spec_eval", &spec_eval);
+  m.def("spec_bisect", &spec_bisect);
+  m.def("bisect_vec", &bisect_vec);
   m.def("weighted_rows", &weighted_rows);
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
@@ -627,4 +686,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tf_ws_floats", &afl_tf_ws_floats);
   afl_register_layers(m);
   afl_register_ipc(m);
+  afl_register_har(m);
 }

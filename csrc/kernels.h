@@ -54,6 +54,19 @@ int afl_spectral(const float* X, int B, int r, int c, float* G0, double* out, hi
 // {offset, r, c, arena offset}; arena = [M][2][sumq] + [sumq] doubles.
 int afl_spec_grams(const float* X, int M, long P, const float* dev, const int* tab, int S, int max_lds_floats, long sumq,
                    double* arena, hipStream_t st);
+// device-resident bisection state + inputs (linalg.hip bisect_decide)
+struct AflBisect {
+  double* st;            // [40] fp64 state (γ, γ_succ, last γ, tried[16], accepted[16])
+  unsigned* ctr;         // arrival counter of a k_spec_eval<true> launch (zero before the first; self-resetting)
+  const double* vA;      // [K, Sv] closed-form vector slots (A - 2γB + γ²C per slot), or null with Sv = 0
+  const double* vB;      // [K, Sv]
+  const double* vC;      // [Sv]
+  const double* thr;     // device scalar threshold
+  int Sv, K, kind;       // kind 0: max d < thr, 1: sum d² < thr
+};
+int afl_spec_bisect(const double* arena, long sumq, int M, const int* tab, int S, double* out, const AflBisect* b, int it,
+                    double step, hipStream_t st);
+int afl_bisect_vec(const AflBisect* b, int n_iter, double step0, hipStream_t st);
 int afl_spec_eval(const double* arena, long sumq, int M, const double* gamma, const int* tab, int S, double* out,
                   hipStream_t st);
 int afl_spectral_slots(const float* D, int M, long P, const int* tab, int S, int max_n, float* G0, long scr,
@@ -301,6 +314,76 @@ int afl_conv_pe_bwd(const float* x, const float* dh, int C, int B, int L, float*
 long afl_conv_pe_bwd_ws_floats(int C, int B, int L);  // [row blocks][C][256] partials
 int afl_mean_rows_fwd(const float* h, int C, int B, int L, float* out, hipStream_t s);
 int afl_mean_rows_bwd(const float* dout, int C, int B, int L, float* dh, hipStream_t s);
+
+// har.hip — HAR encoder on bf16 activations (row passes + head-major flash attention)
+struct AflHarLayerW {  // flat-parameter offsets of one encoder layer
+  int inw, inb, ow, ob, n1w, n1b, l1w, l1b, l2w, l2b, n2w, n2b;
+};
+struct AflHarQkv {
+  const unsigned short* x;  // [C][R][64] bf16 layer input
+  const float* params; long P; int w_off, b_off;
+  unsigned short* qkv;      // [C*B*4][3][Lp][16] bf16, q scaled by qscale
+  int C, B, L, Lp;
+  float qscale;
+};
+struct AflHarPost {
+  const unsigned short* o;  // [C][R][64] attention output
+  const unsigned short* x;  // [C][R][64] layer input (residual)
+  unsigned short* xh1;      // [C][R][64] saved normalised LN1 input
+  unsigned short* xh2;      // [C][R][64] saved normalised LN2 input
+  float* rs;                // [C][R][2] rstd1, rstd2
+  unsigned short* y;        // [C][R][64] layer output
+  const float* params; long P; AflHarLayerW w;
+  int C; long R;
+  AflDrop d1, df, d2;       // dropout1 (out_proj), FFN activation, dropout2 (linear2)
+};
+struct AflHarPostB {
+  const float* dy;          // [C][R][64] d(layer output) fp32 — or null with dpool set
+  const float* dpool;       // [C][B][64] d(mean over L): dy[c][b*L + l] = dpool[c][b] / L (last layer)
+  int B, L;
+  const unsigned short* o;  // attention output (bf16)
+  const unsigned short* xh1; const unsigned short* xh2; const float* rs;
+  float* dres;              // [C][R][64] d(layer input) through the residual path (fp32)
+  unsigned short* dout;     // [C][R][64] d(attention output) (bf16)
+  float* delta;             // [C*B*4][Lp] rowsum(dO o O) per head
+  int Lp;
+  float* ws;                // [C][G][AFL_HAR_POST_NG] per-workgroup gradient partials
+  const float* params; long P; AflHarLayerW w;
+  int C; long R;
+  AflDrop d1, df, d2;
+};
+struct AflHarQkvB {
+  const unsigned short* dqkv;  // [C*B*4][3][Lp][16] d(q|k|v projection outputs) (bf16)
+  const float* dres;           // [C][R][64]
+  const unsigned short* x;     // [C][R][64] layer input
+  float* dx;                   // [C][R][64] d(layer input) (fp32)
+  float* ws;                   // [C][G][AFL_HAR_QKV_NG]
+  const float* params; long P; int w_off;
+  int C, B, L, Lp;
+};
+struct AflHarAttn {
+  const unsigned short* qkv;   // [C*B*4][3][Lp][16] (q pre-scaled by 1/4)
+  unsigned short* o;           // [C][B*L][64]
+  float* lse2;                 // [C*B*4][Lp] log2-domain logsumexp of the scaled scores
+  const unsigned short* dout;  // [C][B*L][64] (bwd)
+  const float* delta;          // [C*B*4][Lp] (bwd)
+  unsigned short* dqkv;        // [C*B*4][3][Lp][16] (bwd): d(q projection) (x 1/4 folded in), dk, dv
+  int C, B, L, Lp;
+  AflDrop drop;
+};
+#define AFL_HAR_POST_NG (64 * 64 + 256 * 64 + 64 * 256 + 640)
+#define AFL_HAR_QKV_NG (192 * 64 + 192)
+int afl_har_stem(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,
+                 unsigned short* h, hipStream_t s);
+int afl_har_pool(const unsigned short* y, int C, int B, int L, float* out, hipStream_t s);
+int afl_har_qkv(const AflHarQkv& a, hipStream_t s);
+int afl_har_post(const AflHarPost& a, hipStream_t s);
+int afl_har_post_bwd(const AflHarPostB& a, int G, hipStream_t s);
+int afl_har_qkv_bwd(const AflHarQkvB& a, int G, hipStream_t s);
+int afl_har_blocks(long R);
+int afl_har_attn_fwd(const AflHarAttn& a, hipStream_t s);
+int afl_har_attn_bwd(const AflHarAttn& a, hipStream_t s);
+int afl_har_reduce(const float* ws, int C, int G, int n, const int* seg, int nseg, float* grads, long P, hipStream_t s);
 
 // attention.hip — flash attention (HAR encoder: 4 heads x 16, L <= 640)
 struct AflAttn {

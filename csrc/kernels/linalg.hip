@@ -278,8 +278,73 @@ __device__ __forceinline__ double sg_block_max(double v, double* red) {
   return fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 
+// ---- the bisection's decision, fused (K-G5; reference loop src/Utils.py:118-130, 152-164, 190-202) ----
+// Device state of one bisection (fp64): st[0] γ to try next, st[1] last accepted γ, st[2] last tried γ,
+// st[4 + i] the γ tried at iteration i, st[20 + i] 1.0 if it was accepted.  One workgroup of 256 threads
+// forms the K candidate distances at the current γ — row 0 is the candidate itself (A-7: distance 0), row j
+// the closed-form vector slots sqrt(max(A - 2γB + γ²C, 0)) summed over Sv slots, plus the Gram-form
+// spectral sums spec[(j - 1) S + s] of this launch — tests them (kind 0: max_j d_j < thr, Min-Max / Opt-Fang;
+// 1: sum_j d_j² < thr, Min-Sum; a NaN distance rejects, as the torch comparison does) and moves γ by ±step/2.
+constexpr int BS_TRIED = 4, BS_ACC = 20, BS_WORDS = 40;
+__device__ void bisect_decide(const AflBisect& b, const double* spec, int S, int it, double step) {
+  __shared__ double rs[4], rm[4];
+  __shared__ int rn[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double g = b.st[0];
+  double s2 = 0.0, mx = 0.0;
+  int nan = 0;
+  for (int j = tid; j < b.K; j += 256) {
+    double d = 0.0;
+    if (j > 0) {
+      for (int v = 0; v < b.Sv; ++v) {
+        const double q = (b.vA[(long)j * b.Sv + v] - 2.0 * g * b.vB[(long)j * b.Sv + v]) + g * g * b.vC[v];
+        d += sqrt(q > 0.0 ? q : 0.0);
+      }
+      for (int v = 0; v < S; ++v)  // (written by the other workgroups of this launch: coherent loads)
+        d += __builtin_bit_cast(double, __hip_atomic_load((const unsigned long long*)(spec + (long)(j - 1) * S + v),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    nan |= d != d;
+    s2 += d * d;
+    mx = fmax(mx, d);
+  }
+  s2 = wave_sum(s2);
+  mx = wave_max(mx);
+  nan = (int)wave_max((double)nan);
+  if (lane == 0) {
+    rs[wave] = s2;
+    rm[wave] = mx;
+    rn[wave] = nan;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double tot = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+    const double mxx = fmax(fmax(rm[0], rm[1]), fmax(rm[2], rm[3]));
+    const bool bad = (rn[0] | rn[1] | rn[2] | rn[3]) != 0;
+    const double thr = *b.thr;
+    const bool acc = !bad && (b.kind == 1 ? tot < thr : mxx < thr);
+    b.st[BS_TRIED + it] = g;
+    b.st[BS_ACC + it] = acc ? 1.0 : 0.0;
+    b.st[2] = g;
+    if (acc) b.st[1] = g;
+    b.st[0] = acc ? g + step / 2.0 : g - step / 2.0;
+  }
+  __syncthreads();
+}
+
+// every iteration in ONE launch (no spectral slots: flat distances, or vector-shaped tensors only)
+__global__ void __launch_bounds__(256) k_bisect_vec(AflBisect b, int n_iter, double step0) {
+  double step = step0;
+  for (int it = 0; it < n_iter; ++it) {
+    bisect_decide(b, nullptr, 0, it, step);
+    step *= 0.5;
+  }
+}
+
+template <bool BIS>
 __global__ void __launch_bounds__(256) k_spec_eval(const double* __restrict__ arena, long sumq, const double* __restrict__ gamma,
-                                                   const int4* __restrict__ tab, int S, double* __restrict__ out) {
+                                                   const int4* __restrict__ tab, int S, double* __restrict__ out,
+                                                   AflBisect bis, int it, double step) {
   __shared__ float F[2][SG_NMAX * SG_LD];
   __shared__ double red[4];
   __shared__ double dred[2][4];
@@ -391,7 +456,23 @@ __global__ void __launch_bounds__(256) k_spec_eval(const double* __restrict__ ar
     const double nn = (dred[0][0] + dred[0][1]) + (dred[0][2] + dred[0][3]);
     const double dd = (dred[1][0] + dred[1][1]) + (dred[1][2] + dred[1][3]);
     const double lam = dd > 0.0 ? nn / dd : 0.0;
-    out[(long)m * S + s] = lam > 0.0 ? sqrt(lam) : 0.0;
+    const double val = lam > 0.0 ? sqrt(lam) : 0.0;
+    if (!BIS) {
+      out[(long)m * S + s] = val;
+    } else {  // fan-in: publish (coherent store), count arrivals; the last workgroup decides this γ
+      __hip_atomic_store((unsigned long long*)(out + (long)m * S + s), __builtin_bit_cast(unsigned long long, val),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev = __hip_atomic_fetch_add(bis.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      wi[0] = prev == gridDim.x * gridDim.y - 1 ? 1 : 0;
+    }
+  }
+  if (BIS) {
+    __syncthreads();
+    if (wi[0]) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      bisect_decide(bis, out, S, it, step);
+      if (tid == 0) __hip_atomic_store(bis.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    }
   }
 }
 
@@ -411,6 +492,21 @@ int afl_spec_grams(const float* X, int M, long P, const float* dev, const int* t
 
 int afl_spec_eval(const double* arena, long sumq, int M, const double* gamma, const int* tab, int S, double* out,
                   hipStream_t st) {
-  hipLaunchKernelGGL(k_spec_eval, dim3(S, M), dim3(256), 0, st, arena, sumq, gamma, (const int4*)tab, S, out);
+  hipLaunchKernelGGL(k_spec_eval<false>, dim3(S, M), dim3(256), 0, st, arena, sumq, gamma, (const int4*)tab, S, out,
+                     AflBisect{}, 0, 0.0);
+  return 0;
+}
+
+int afl_spec_bisect(const double* arena, long sumq, int M, const int* tab, int S, double* out, const AflBisect* b, int it,
+                    double step, hipStream_t st) {
+  if (M <= 0 || S <= 0 || b->K != M + 1) return -1;
+  hipLaunchKernelGGL(k_spec_eval<true>, dim3(S, M), dim3(256), 0, st, arena, sumq, b->st, (const int4*)tab, S, out, *b,
+                     it, step);
+  return 0;
+}
+
+int afl_bisect_vec(const AflBisect* b, int n_iter, double step0, hipStream_t st) {
+  if (n_iter > 16) return -1;
+  hipLaunchKernelGGL(k_bisect_vec, dim3(1), dim3(256), 0, st, *b, n_iter, step0);
   return 0;
 }

@@ -1,0 +1,37 @@
+"""Fused device bisection (K-G5, linalg.hip ``bisect_decide``) vs the generic unrolled device loop and the
+CPU reference loop (src/Utils.py:101-204): same tried γ sequence, same decisions, same malicious model."""
+import pytest
+import torch
+
+from attackfl_amd import attacks
+from attackfl_amd.attacks import DistanceEngine
+from attackfl_amd.models import ParamLayout, build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _G(name, K, scale, seed):
+    torch.manual_seed(seed)
+    lay = ParamLayout.for_model(name)
+    base = lay.flatten(build_model(name, seed=seed).state_dict())
+    return lay, base[None] + scale * torch.randn(K, lay.P)
+
+
+@pytest.mark.parametrize("name", ["TransformerModel", "RNNModel"])
+@pytest.mark.parametrize("mode", ["spectral", "flat"])
+@pytest.mark.parametrize("fn", [attacks.min_max, attacks.min_sum, attacks.opt_fang])
+@pytest.mark.parametrize("scale", [0.02, 0.5])
+def test_fused_bisection_matches_generic_and_cpu(gpu, name, mode, fn, scale, monkeypatch):
+    lay, G = _G(name, 5, scale, 3)
+    eng = DistanceEngine(lay, mode)
+    cpu = attacks.host_info(fn(G, G[0], eng).info)
+    Gd = G.to(gpu)
+    fused = fn(Gd, Gd[0], eng)
+    hf = attacks.host_info(fused.info)
+    monkeypatch.setattr(attacks, "_bisect_fused", lambda *a, **k: None)  # force the generic device loop
+    gen = fn(Gd, Gd[0], eng)
+    hg = attacks.host_info(gen.info)
+    assert hf["gammas"] == hg["gammas"] == cpu["gammas"]
+    assert hf["accepted"] == hg["accepted"] == cpu["accepted"]
+    assert hf["gamma"] == cpu["gamma"] and hf["gamma_succ"] == cpu["gamma_succ"]
+    assert torch.equal(fused.params, gen.params)

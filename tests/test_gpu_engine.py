@@ -4,6 +4,7 @@ eval forward; fedavg and hyper modes."""
 import os
 
 import pytest
+import torch
 
 from attackfl_amd.config import from_dict
 from attackfl_amd.fl.engine import FLEngine, build_client_table

@@ -1,0 +1,67 @@
+"""bf16 HAR encoder kernels (csrc/kernels/har.hip) against the fp32 composites of the layer program."""
+import numpy as np
+import pytest
+import torch
+
+from attackfl_amd.ops import layers as Lx
+from attackfl_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctl(C, dev):
+    return Lx.StepCtl.create(list(range(3, 3 + C)), dev)
+
+
+def _close(a, b, rel, name):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-12
+    assert err <= rel * scale, (name, err, scale)
+
+
+def _headmajor(qkv, B, L, Lp):
+    """[C, B*L, 192] fp32 -> [C*B*4, 3, Lp, 16] bf16 (q scaled by 1/4)."""
+    C = qkv.shape[0]
+    x = qkv.reshape(C, B, L, 3, 4, 16).permute(0, 1, 4, 3, 2, 5).clone()  # [C, B, H, 3, L, 16]
+    x[:, :, :, 0] *= 0.25
+    out = torch.zeros(C, B, 4, 3, Lp, 16, dtype=torch.bfloat16, device=qkv.device)
+    out[..., :L, :] = x.to(torch.bfloat16)
+    return out.reshape(C * B * 4, 3, Lp, 16)
+
+
+@pytest.mark.parametrize("L,p", [(50, 0.0), (561, 0.1)])
+def test_har_attention_matches_composite(gpu, L, p):
+    C, B = 2, 2
+    g = torch.Generator().manual_seed(4)
+    qkv = torch.randn(C, B * L, 192, generator=g)
+    # bf16-exact inputs, so the composite sees what the kernel reads
+    qkv = qkv.to(torch.bfloat16).float()
+    dout = torch.randn(C, B * L, 64, generator=g).to(torch.bfloat16).float()
+    Lp = (L + 63) // 64 * 64
+    nat = native()
+    ctl = _ctl(C, gpu)
+    hm = _headmajor(qkv.to(gpu), B, L, Lp)
+    o = torch.zeros(C, B * L, 64, dtype=torch.bfloat16, device=gpu)
+    lse2 = torch.zeros(C * B * 4, Lp, device=gpu)
+    nat.har_attn_fwd(hm, o, lse2, B, L, ctl.seeds if p else None, ctl.stepctl if p else None, 2, p)
+    cc = _ctl(C, "cpu")
+    ref_o, ref_lse = Lx._attn_ref(qkv, B, L, cc, 2, p)
+    _close(o, ref_o, 2e-2, "O")
+    _close(lse2[:, :L] * np.log(2.0), ref_lse.reshape(-1, L), 1e-3, "lse")
+    # backward: Delta from the kernel's own (bf16) O, as the post pass computes it
+    ob = o.float()
+    delta = torch.zeros(C * B * 4, Lp, device=gpu)
+    dd = (dout.to(gpu) * ob).reshape(C, B, L, 4, 16).sum(-1).permute(0, 1, 3, 2).reshape(C * B * 4, L)
+    delta[:, :L] = dd
+    dq = torch.zeros_like(hm)
+    nat.har_attn_bwd(hm, lse2, dout.to(gpu).to(torch.bfloat16), delta, dq, B, L, ctl.seeds if p else None,
+                     ctl.stepctl if p else None, 2, p)
+    x = qkv.clone().requires_grad_(True)
+    with torch.enable_grad():
+        out, _ = Lx._attn_ref(x, B, L, cc, 2, p)
+        (gref,) = torch.autograd.grad(out, x, dout)
+    gq = gref.reshape(C, B, L, 3, 4, 16).permute(0, 1, 4, 3, 2, 5).reshape(C * B * 4, 3, L, 16)
+    got = dq[:, :, :L].float().cpu()
+    for w, n in enumerate(["dq", "dk", "dv"]):
+        _close(got[:, w], gq[:, w], 3e-2, n)

@@ -35,6 +35,9 @@ CASES = {
     "rnn-hyper-optfang": ("RNNModel", "hyper", {6: {"mode": "Opt-Fang", "round": 2}}),
     # plain fedavg (no attacker): at world > 1 with IPC it stays on the gather + FedAvg kernel path
     "tf-fedavg": ("TransformerModel", "fedavg", {}),
+    # the on-chip CNN trainer needs all 32 workgroups of a client co-resident: ranks sharing the GPU size their
+    # launches to CUs / sharers (parallel.launcher.gpu_sharers) instead of spinning on absent workgroups
+    "cnn-fedavg": ("CNNModel", "fedavg", {}),
 }
 
 

@@ -37,7 +37,7 @@ def cells(spec: str):
 
 
 def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0, genuine_rate: float = 0.5,
-             distance: str = "spectral") -> dict:
+             distance: str = "spectral", seed: int = 7) -> dict:
     import torch
 
     if threads:
@@ -50,10 +50,10 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0,
     tmp = tempfile.mkdtemp(prefix="afl_study_")
     d = {
         "server": {"num-round": rounds, "clients": 8, "mode": mode, "model": "TransformerModel", "data-name": "ICU",
-                   "genuine-rate": genuine_rate, "random-seed": 1, "data-distribution": {"num-data-range": [800, 1200]}},
+                   "genuine-rate": genuine_rate, "random-seed": seed - 6, "data-distribution": {"num-data-range": [800, 1200]}},
         "learning": {"epoch": 2, "batch-size": 128, "learning-rate": 0.004},
         "data": {"synthetic": True, "train-size": 20000, "test-size": 3000},
-        "engine": {"checkpoint-dir": tmp, "trainer": "auto" if device.startswith("cuda") else "oracle", "seed": 7,
+        "engine": {"checkpoint-dir": tmp, "trainer": "auto" if device.startswith("cuda") else "oracle", "seed": seed,
                    "max-retries": 5, "distance": distance},
         "log_path": tmp,
     }
@@ -70,7 +70,7 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0,
     eng.close()
     ok = [r for r in hist if r["ok"]]
     return {"device": "gpu" if device.startswith("cuda") else "cpu", "mode": mode, "attack": attack,
-            "genuine_rate": genuine_rate, "distance": distance,
+            "genuine_rate": genuine_rate, "distance": distance, "seed": seed,
             "attackers": len(atk), "rounds": len(ok), "failed_rounds": len(hist) - len(ok), "stalled": stalled,
             "auc": [round(r["metric"], 5) for r in ok], "final_auc": round(ok[-1]["metric"], 5) if ok else None,
             "attack_gamma": [round(r["attack"]["gamma"], 4) for r in ok if "attack" in r and "gamma" in r["attack"]],
@@ -80,8 +80,8 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0,
 
 
 def _worker(args):
-    mode, attack, device, rounds, threads, gr, dist = args
-    return run_cell(mode, attack, device, rounds, threads, gr, dist)
+    mode, attack, device, rounds, threads, gr, dist, seed = args
+    return run_cell(mode, attack, device, rounds, threads, gr, dist, seed)
 
 
 def main() -> int:
@@ -93,8 +93,10 @@ def main() -> int:
     ap.add_argument("--jobs", type=int, default=1, help="parallel CPU processes")
     ap.add_argument("--genuine-rate", type=float, default=0.5, help="server.genuine-rate (reference default 0.5)")
     ap.add_argument("--distance", default="spectral", choices=["spectral", "flat"])
+    ap.add_argument("--seeds", default="7", help="comma-separated run seeds (engine seed; server random-seed = seed - 6)")
     args = ap.parse_args()
-    todo = cells(args.cells)
+    seeds = [int(x) for x in args.seeds.split(",")]
+    todo = [(m, a, sd) for m, a in cells(args.cells) for sd in seeds]
     with open(args.out, "a") as fh:
         if args.jobs > 1 and not args.device.startswith("cuda"):
             import multiprocessing as mp
@@ -102,13 +104,13 @@ def main() -> int:
             threads = max(1, (os.cpu_count() or 8) // args.jobs)
             with mp.get_context("spawn").Pool(args.jobs) as pool:
                 for res in pool.imap_unordered(_worker, [(m, a, args.device, args.rounds, threads, args.genuine_rate,
-                                                                   args.distance) for m, a in todo]):
+                                                                   args.distance, sd) for m, a, sd in todo]):
                     fh.write(json.dumps(res) + "\n")
                     fh.flush()
                     print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)
         else:
-            for m, a in todo:
-                res = run_cell(m, a, args.device, args.rounds, 0, args.genuine_rate, args.distance)
+            for m, a, sd in todo:
+                res = run_cell(m, a, args.device, args.rounds, 0, args.genuine_rate, args.distance, sd)
                 fh.write(json.dumps(res) + "\n")
                 fh.flush()
                 print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)
