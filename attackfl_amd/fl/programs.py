@@ -300,6 +300,11 @@ class HARProgram(_Program):
     def _fused(self, params) -> bool:
         return params.is_cuda and os.environ.get("AFL_HAR_FUSED", "1") != "0"
 
+    def _scheme(self, params) -> str:
+        """Attention dropout hash of this path: the CPU composite mirrors the bf16 device kernels ("rc");
+        the device layer-library fallback (AFL_HAR_FUSED=0) has attention.hip's "pair" draws."""
+        return "pair" if params.is_cuda else "rc"
+
     def _lw(self, i) -> list:
         """Flat offsets of layer i's parameters (AflHarLayerW order)."""
         names = ["self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight",
@@ -349,7 +354,7 @@ class HARProgram(_Program):
         for i in range(self.NL):
             w = self._lw(i)
             qkv = self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf)  # padding rows stay zero
-            nat.har_qkv(h, params, w[0], w[1], qkv, B, L, 0.25)
+            nat.har_qkv(h, params, w[0], w[1], qkv, B, L, 0.25 * 1.4426950408889634)  # 1/sqrt(16) * log2(e)
             o, lse2 = self.buf(f"ob{i}", C, R, 64, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp)
             nat.har_attn_fwd(qkv, o, lse2, B, L, seeds, stepctl, 10 * i, p)
             y = self.buf(f"hb{i + 1}", C, R, 64, dtype=bf)
@@ -412,7 +417,7 @@ class HARProgram(_Program):
             qkv, o, a = self.buf(f"qkv{i}", C, R, 192), self.buf(f"o{i}", C, R, 64), self.buf(f"a{i}", C, R, 64)
             lse = self.buf(f"lse{i}", C * B * 4, Lx.attn_lp(L))
             self.linear(h, params, self.lyr(i, "self_attn.in_proj_weight"), self.lyr(i, "self_attn.in_proj_bias"), qkv)
-            Lx.attn_fwd(qkv, o, lse, B, L, ctl, layer=10 * i, p=self.p(0.1))
+            Lx.attn_fwd(qkv, o, lse, B, L, ctl, layer=10 * i, p=self.p(0.1), scheme=self._scheme(params))
             self.linear(o, params, self.lyr(i, "self_attn.out_proj.weight"), self.lyr(i, "self_attn.out_proj.bias"), a)
             s1, h1 = self.buf(f"s1_{i}", C, R, 64), self.buf(f"h1_{i}", C, R, 64)
             Lx.ln_fwd(h, a, s1, h1, self.buf(f"st1_{i}", C, R, 2), self.w(params, self.lyr(i, "norm1.weight")),
@@ -467,7 +472,8 @@ class HARProgram(_Program):
             self.linear_bwd(da, self.buf(f"o{i}", C, R, 64), params, grads, self.lyr(i, "self_attn.out_proj.weight"),
                             self.lyr(i, "self_attn.out_proj.bias"), do)
             Lx.attn_bwd(self.buf(f"qkv{i}", C, R, 192), self.buf(f"o{i}", C, R, 64),
-                        self.buf(f"lse{i}", C * B * 4, Lx.attn_lp(L)), do, dqkv, B, L, ctl, layer=10 * i, p=self.p(0.1))
+                        self.buf(f"lse{i}", C * B * 4, Lx.attn_lp(L)), do, dqkv, B, L, ctl, layer=10 * i, p=self.p(0.1),
+                        scheme=self._scheme(params))
             self.linear_bwd(dqkv, hin, params, grads, self.lyr(i, "self_attn.in_proj_weight"),
                             self.lyr(i, "self_attn.in_proj_bias"), other, accum=1)
             dh, other = other, dh
@@ -537,7 +543,9 @@ class ProgramRunner:
             S = min(S, max_steps)
         ctl = StepCtl.create(seeds, dev, min_bs=1 if compat_har else 2, nan_abort=not compat_har)
         if self._onchip_cnn(params, sgd_lr, max_steps):
-            return self._train_cnn2(table, params, plan, lr, ctl, (idx, bsz, ep, nb, S), sync)
+            # sgd_lr > 0: the gradient-test mode (one plain SGD step p -= sgd_lr g exposes the raw gradients)
+            return self._train_cnn2(table, params, plan, sgd_lr if sgd_lr > 0.0 else lr, ctl, (idx, bsz, ep, nb, S),
+                                    sync, opt_mode=1 if sgd_lr > 0.0 else 0)
         out_params = params
         if params.is_cuda and P % 16:
             # train in a copy whose client rows start 64-byte aligned (P is odd for every model here, so every
@@ -603,11 +611,11 @@ class ProgramRunner:
     cnn2_stamps = None  # optional int64 [C, 25, 64, 8] per-phase wall-clock stamps (tools/cnn2_phases.py)
 
     def _onchip_cnn(self, params: torch.Tensor, sgd_lr: float, max_steps) -> bool:
-        """One persistent launch per round instead of a graph replay per step: CNNModel on a GPU with Adam
-        (the SGD gradient hook and step caps stay on the layer program), all 25 workgroups of every client
+        """One persistent launch per round instead of a graph replay per step: CNNModel on a GPU (Adam, or the
+        raw-SGD gradient-test mode; step caps stay on the layer program), all 32 workgroups of every client
         co-resident (one per CU).  ``AFL_CNN2=0`` forces the layer program."""
         pg = self.prog
-        if pg.model_name != "CNNModel" or not params.is_cuda or not pg.train or sgd_lr > 0.0 or max_steps is not None:
+        if pg.model_name != "CNNModel" or not params.is_cuda or not pg.train or max_steps is not None:
             return False
         if os.environ.get("AFL_CNN2", "1") == "0" or pg.B > 128 or pg.B < 2 or params.dtype != torch.float32:
             return False  # (the kernel needs 2 <= B <= 128: hipErrorInvalidValue otherwise)
@@ -620,7 +628,7 @@ class ProgramRunner:
         cus = torch.cuda.get_device_properties(params.device).multi_processor_count // gpu_sharers()
         return params.shape[0] * int(nat.cnn2_wgs_per_client()) <= cus
 
-    def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync):
+    def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync, opt_mode: int = 0):
         from .. import ops
 
         nat = ops.native()
@@ -638,7 +646,8 @@ class ProgramRunner:
             ctr.zero_()
             offs = [s.offset for s in pg.layout.slots]
             nat.cnn2_train(params if params.is_contiguous() else params.contiguous(), offs, table.rows, idx, bsz, ep, nb,
-                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr, self.cnn2_stamps)
+                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr, self.cnn2_stamps,
+                           int(opt_mode))
             self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params)  # the launch may still run when sync=False
         if not sync:
             return failed, losses  # failed: 1 = NaN loss, 2 = a cross-workgroup wait timed out (GraphTrainer raises)

@@ -585,8 +585,9 @@ def attn_lp(L: int) -> int:
     return (L + 31) // 32 * 32
 
 
-def _attn_ref(qkv, B, L, ctl, layer, p):
-    """Composite SDPA (4 heads x 16, scale 1/4, dropout on the probabilities) -> (O, lse)."""
+def _attn_ref(qkv, B, L, ctl, layer, p, scheme: str = "pair"):
+    """Composite SDPA (4 heads x 16, scale 1/4, dropout on the probabilities) -> (O, lse).  ``scheme``: the
+    probability-dropout hash — "pair" (``afl_keep``, attention.hip) or "rc" (``masks.keep_rc``, har.hip)."""
     C = qkv.shape[0]
     q, k, v = qkv.reshape(C, B, L, 3, 4, 16).permute(3, 0, 1, 4, 2, 5)  # each [C, B, H, L, 16]
     s = torch.matmul(q, k.transpose(-1, -2)) * 0.25
@@ -595,18 +596,22 @@ def _attn_ref(qkv, B, L, ctl, layer, p):
     if p > 0.0:
         rows = (np.arange(B * 4)[:, None] * L + np.arange(L)[None, :]).reshape(B, 4, L, 1)
         cols = np.arange(L).reshape(1, 1, 1, L)
-        pr = pr * torch.stack([_scale(ctl, ci, layer, rows, cols, p) for ci in range(C)])
+        keepfn = masks.keep_rc if scheme == "rc" else masks.keep
+        pr = pr * torch.stack([keepfn(ctl.key(ci), layer, rows, cols, p).float() / (1.0 - p) for ci in range(C)])
     o = torch.matmul(pr, v)  # [C, B, H, L, 16]
     return o.permute(0, 1, 3, 2, 4).reshape(C, B * L, 64), lse
 
 
-def attn_fwd(qkv, o, lse, B: int, L: int, ctl=None, layer=0, p=0.0) -> None:
-    """Multi-head self-attention of ``qkv [C, B*L, 192]`` -> ``o [C, B*L, 64]``, ``lse [C*B*4, Lp]``."""
+def attn_fwd(qkv, o, lse, B: int, L: int, ctl=None, layer=0, p=0.0, scheme: str = "pair") -> None:
+    """Multi-head self-attention of ``qkv [C, B*L, 192]`` -> ``o [C, B*L, 64]``, ``lse [C*B*4, Lp]``.
+    ``scheme`` (composite only): the dropout hash of the kernel being mirrored (``_attn_ref``)."""
     if _nat(qkv):
+        if scheme != "pair" and p > 0.0:
+            raise ValueError("attention.hip draws its dropout with the 'pair' scheme")
         s, sc = _dargs(ctl, p)
         _native().attn_fwd(qkv, o, lse, B, L, s, sc, layer, p)
         return
-    out, ls = _attn_ref(qkv, B, L, ctl, layer, p)
+    out, ls = _attn_ref(qkv, B, L, ctl, layer, p, scheme)
     o.copy_(out)
     Lp = attn_lp(L)
     lv = lse.view(-1, Lp)
@@ -614,13 +619,15 @@ def attn_fwd(qkv, o, lse, B: int, L: int, ctl=None, layer=0, p=0.0) -> None:
     lv[:, :L] = ls.reshape(-1, L)
 
 
-def attn_bwd(qkv, o, lse, dout, dqkv, B: int, L: int, ctl=None, layer=0, p=0.0) -> None:
+def attn_bwd(qkv, o, lse, dout, dqkv, B: int, L: int, ctl=None, layer=0, p=0.0, scheme: str = "pair") -> None:
     if _nat(qkv):
+        if scheme != "pair" and p > 0.0:
+            raise ValueError("attention.hip draws its dropout with the 'pair' scheme")
         s, sc = _dargs(ctl, p)
         _native().attn_bwd(qkv, o, lse, dout, dqkv, B, L, s, sc, layer, p)
         return
     x = qkv.detach().clone().requires_grad_(True)
     with torch.enable_grad():
-        out, _ = _attn_ref(x, B, L, ctl, layer, p)
+        out, _ = _attn_ref(x, B, L, ctl, layer, p, scheme)
         (g,) = torch.autograd.grad(out, x, dout)
     dqkv.copy_(g)

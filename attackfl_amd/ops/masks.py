@@ -67,3 +67,39 @@ def scale_grid(seeds, step: int, layer: int, n_rows: int, n_cols: int, p: float)
     for ci, s in enumerate(seeds):
         out[ci] = keep_grid(step_key(int(s), step), layer, n_rows, n_cols, p).float() / (1.0 - p)
     return out
+
+
+def _hash4(key: int, layer: int, r, c) -> np.ndarray:
+    """``afl_hash4`` on broadcastable uint64 arrays (32-bit arithmetic) -> uint64 array of 32-bit values."""
+    m = np.uint64(M32)
+    r = np.asarray(r, dtype=np.uint64)
+    c = np.asarray(c, dtype=np.uint64)
+    x = (np.uint64(key & M32) ^ ((np.uint64(layer & M32) * np.uint64(0x9E3779B9)) & m)
+         ^ ((r * np.uint64(0x85EBCA6B)) & m) ^ ((c * np.uint64(0xC2B2AE35)) & m))
+    x &= m
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & m
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & m
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def keep_rc(key: int, layer: int, rows, cols, p: float) -> torch.Tensor:
+    """Attention-probability dropout of the bf16 HAR kernels (``har.hip`` ``attn_keep``): a strong hash per
+    ROW and one per column PAIR, combined by xor and two multiply-xorshift rounds; the 32-bit result gives the
+    16-bit uniforms of the pair's two columns.  The per-row and per-column hashes are computed once per
+    workgroup (registers / an LDS table), so a probability costs half a 2-round mix instead of half a full
+    hash4 — the attention kernels are VALU-bound and the full hash was most of their work."""
+    m = np.uint64(M32)
+    r = np.asarray(rows, dtype=np.uint64)
+    col = np.asarray(cols, dtype=np.uint64)
+    hr = _hash4(key, layer, r, M32)
+    hc = _hash4(key ^ 0xA5A5A5A5, layer, 0, col >> np.uint64(1))
+    x = (hr ^ hc) & m
+    x = (x * np.uint64(0x7FEB352D)) & m
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & m
+    x ^= x >> np.uint64(16)
+    u16 = (x >> ((col & np.uint64(1)) << np.uint64(4))) & np.uint64(0xFFFF)
+    return torch.from_numpy(np.ascontiguousarray(u16 >= np.uint64(thr16(p))))

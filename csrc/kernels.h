@@ -209,6 +209,7 @@ struct AflCnn2Args {
   float inv_keep;
   int min_bs, nan_abort;
   float lr;
+  int opt_mode;          // 0 Adam, 1 plain SGD p -= lr g (gradient tests)
   int* failed;           // [C] out: 1 = NaN loss
   float* losses;         // [C][E] accumulated epoch losses (zeroed by the caller)
   void* ws;              // [C][ws_stride] bytes workspace (afl_cnn2_ws_bytes)

@@ -248,18 +248,22 @@ __device__ __forceinline__ void mv_st(const Ctx& x, int k, f4v m, f4v v) {
   st16f(x.rw, mv_off(x, k) + 16, v);
 }
 
-// the reference Adam step (k_adam_clients / torch.optim.Adam defaults) with bias corrections a, sb of step t
-__device__ __forceinline__ float adam1(float p, float& m, float& v, float g, float a, float sb) {
-  m = m + 0.1f * (g - m);
-  v = 0.999f * v + 0.001f * g * g;
-  return p - a * m / (sqrtf(v) / sb + 1e-8f);
-}
+// the reference Adam step (k_adam_clients / torch.optim.Adam defaults) with bias corrections a, sb of step t;
+// sgd (the gradient-test mode, opt_mode 1): p - lr g, moments untouched — the step exposes the raw gradient
 struct AdamT {
   float a, sb;
+  int sgd;
 };
-__device__ __forceinline__ AdamT adam_t(float lr, int t) {
+__device__ __forceinline__ float adam1(float p, float& m, float& v, float g, const AdamT& k) {
+  if (k.sgd) return p - k.a * g;
+  m = m + 0.1f * (g - m);
+  v = 0.999f * v + 0.001f * g * g;
+  return p - k.a * m / (sqrtf(v) / k.sb + 1e-8f);
+}
+__device__ __forceinline__ AdamT adam_t(float lr, int t, int opt_mode) {
   const float tt = (float)t;
-  return AdamT{lr / (1.f - powf(0.9f, tt)), sqrtf(1.f - powf(0.999f, tt))};
+  if (opt_mode == 1) return AdamT{lr, 1.f, 1};
+  return AdamT{lr / (1.f - powf(0.9f, tt)), sqrtf(1.f - powf(0.999f, tt)), 0};
 }
 
 // ============================================================================================ towers
@@ -885,7 +889,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     REOPQ();
     stamp(x, kact, 4);
     // ------------------------------------------------------------------ owner: conv blocks
-    const AdamT ak = adam_t(a.lr, kact + 1);
+    const AdamT ak = adam_t(a.lr, kact + 1, a.opt_mode);
     {
       f4v gsum[C::NS], mm[C::NS], vv[C::NS];
       Chunk ks[C::NS];
@@ -916,7 +920,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float me = mm[u][e], ve = vv[u][e];
-          st.p[u][e] = adam1(st.p[u][e], me, ve, gsum[u][e], ak.a, ak.sb);
+          st.p[u][e] = adam1(st.p[u][e], me, ve, gsum[u][e], ak);
           mm[u][e] = me;
           vv[u][e] = ve;
         }
@@ -1287,7 +1291,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
       }
     }
     // Adam on the head parameters (off the critical path: the towers run their backward meanwhile)
-    const AdamT ak = adam_t(a.lr, kact + 1);
+    const AdamT ak = adam_t(a.lr, kact + 1, a.opt_mode);
     {
       f4v hm[6], hv[6];
 #pragma unroll
@@ -1297,21 +1301,21 @@ __device__ __forceinline__ void head(const Ctx& x) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float me = hm[j][e], ve = hv[j][e];
-          p2[4 * j + e] = adam1(p2[4 * j + e], me, ve, g2[j][e], ak.a, ak.sb);
+          p2[4 * j + e] = adam1(p2[4 * j + e], me, ve, g2[j][e], ak);
           hm[j][e] = me;
           hv[j][e] = ve;
         }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float me = hm[4][e], ve = hv[4][e];
-        p3[e] = adam1(p3[e], me, ve, g3[e], ak.a, ak.sb);
+        p3[e] = adam1(p3[e], me, ve, g3[e], ak);
         hm[4][e] = me;
         hv[4][e] = ve;
       }
       if (tid < 257) {
         // vector order of the state: b2 [64] | b3 [32] | Wo [32] | bo | b1 [128] == the sums layout
         float me = hm[5][0], ve = hv[5][0];
-        pv = adam1(pv, me, ve, sums[tid], ak.a, ak.sb);
+        pv = adam1(pv, me, ve, sums[tid], ak);
         hm[5][0] = me;
         hv[5][0] = ve;
       }
@@ -1423,14 +1427,14 @@ __device__ __forceinline__ void fc1_owner(const Ctx& x, int j) {
       for (int t = 0; t < 10; ++t)
         if (t < ntl) acc[t] = mfma(af, cfrag(S + F_FW, F_LDF, 32 * ks, 16 * t, lane), acc[t]);
     }
-    const AdamT ak = adam_t(a.lr, kact + 1);
+    const AdamT ak = adam_t(a.lr, kact + 1, a.opt_mode);
 #pragma unroll
     for (int t = 0; t < 10; ++t) {
       if (t >= ntl) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float me = m[t][e], ve = v[t][e];
-        p[t][e] = adam1(p[t][e], me, ve, acc[t][e], ak.a, ak.sb);
+        p[t][e] = adam1(p[t][e], me, ve, acc[t][e], ak);
         m[t][e] = me;
         v[t][e] = ve;
       }

@@ -5,7 +5,8 @@
 // HBM (a 574k-row step moved ~10 GB); here a layer is five launches over bf16 rows:
 //
 //   k_har_qkv      x -> q | k | v (bf16, head-major [cb*H + h][3][Lp][16]: every attention workgroup reads
-//                  one contiguous 36 KB block; q pre-scaled by 1/sqrt(16) = 0.25, exact in bf16)
+//                  one contiguous 36 KB block; q pre-scaled by log2(e) / sqrt(16), so a score is already in the
+//                  log2 domain of the softmax's v_exp_f32)
 //   k_har_attn_*   flash attention fwd / bwd on the head-major blocks (below)
 //   k_har_post     ONE row pass: out_proj + dropout + residual + LN1 -> linear1 + ReLU + dropout -> linear2
 //                  + dropout + residual + LN2; the 256-wide FFN activation never leaves registers (the
@@ -22,8 +23,10 @@
 // the B operand of the next GEMM when that weight's LDS image stores its K axis permuted (pcol).  A
 // LayerNorm row sum is an in-lane sum plus two lane swaps.  Weights are staged once per workgroup (each
 // workgroup serves one client's rows: grid = (blocks per client, clients)).
-// Dropout masks are the layer library's (afl_keep of (step key, layer id, row, column)), so the layer
-// program on CPU (ops/layers.py composites) is the oracle of these kernels.
+// Dropout masks: the row passes use the layer library's (afl_keep of (step key, layer id, row, column)); the
+// attention probabilities use a row hash x column-pair hash mix (attn_mix, masks.keep_rc) that costs a
+// fraction of a full hash per probability.  The layer program on CPU (ops/layers.py composites, attention
+// scheme "rc") is the oracle of these kernels.
 #include "common.h"
 #include "kernels.h"
 #include "onchip.h"
@@ -327,7 +330,7 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
 // Transposed operands (V^T for O += V^T P^T, K^T for dQ, Q^T / dO^T for dK / dV) come straight from these
 // row-major images through ds_read_b64_tr_b16: lane i of a 16-lane group gets column i of 4 rows whose
 // order the lanes' addresses choose — the permuted key order of the score fragments — so no transposed
-// copy is staged.  Scores stay in the log2 domain (one v_exp_f32 per probability; q carries the 1/4 scale).
+// copy is staged.  Scores stay in the log2 domain (one v_exp_f32 per probability; q carries log2(e) / 4).
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int AT_WAVES = 12, AT_NT = 64 * AT_WAVES;
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
@@ -366,17 +369,34 @@ __device__ __forceinline__ float sum_x16_x32(float a) {
   p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
-// dropout multipliers of keys kb0..kb0+3 and kb1..kb1+3 (kb even) of one probability row: 4 hashes / 8 keys
-__device__ __forceinline__ void keep8(uint32_t key, uint32_t layer, uint32_t row, int kb0, int kb1, uint32_t thr,
-                                      float ik, float* mk) {
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const uint32_t x = afl_hash4(key, layer, row, (uint32_t)(((hf ? kb1 : kb0) >> 1) + pr));
-      mk[4 * hf + 2 * pr] = (x & 0xFFFFu) >= thr ? ik : 0.f;
-      mk[4 * hf + 2 * pr + 1] = (x >> 16) >= thr ? ik : 0.f;
-    }
+// Probability dropout (masks.keep_rc): a strong hash per row (attn_hr) and per column pair (attn_hc, an LDS
+// table per workgroup) combined by xor and two multiply-xorshift rounds; 16 bits per column.  Kept
+// probabilities are NOT scaled here: 1/(1-p) is folded into O (forward), dV and dP (backward).
+__device__ __forceinline__ uint32_t attn_hr(uint32_t key, uint32_t layer, uint32_t r) {
+  return afl_hash4(key, layer, r, 0xFFFFFFFFu);
+}
+__device__ __forceinline__ uint32_t attn_hc(uint32_t key, uint32_t layer, uint32_t cp) {
+  return afl_hash4(key ^ 0xA5A5A5A5u, layer, 0u, cp);
+}
+__device__ __forceinline__ uint32_t attn_mix(uint32_t hr, uint32_t hc) {
+  uint32_t x = hr ^ hc;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep flags of keys kb .. kb+3 (kb even) of the row with hash hr: pairs kb/2, kb/2 + 1 from the LDS table
+__device__ __forceinline__ void keep4(const LDS_AS uint32_t* HC, uint32_t hr, int kb, uint32_t thr, bool* k) {
+  const u32x2v hc = *(const LDS_AS u32x2v*)(HC + (kb >> 1));
+  const uint32_t x0 = attn_mix(hr, hc[0]), x1 = attn_mix(hr, hc[1]);
+  k[0] = (x0 & 0xFFFFu) >= thr;
+  k[1] = (x0 >> 16) >= thr;
+  k[2] = (x1 & 0xFFFFu) >= thr;
+  k[3] = (x1 >> 16) >= thr;
+}
+__device__ void fill_hc(LDS_AS uint32_t* HC, int npairs, uint32_t key, uint32_t layer) {
+  for (int e = threadIdx.x; e < npairs; e += blockDim.x) HC[e] = attn_hc(key, layer, (uint32_t)e);
 }
 
 template <bool DROP>
@@ -385,18 +405,21 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
   const int Lp = a.Lp, L = a.L;
   uchar* Ki = smem;
   uchar* Vi = smem + Lp * 32;
+  LDS_AS uint32_t* HC = (LDS_AS uint32_t*)(smem + 2 * Lp * 32);
   const int cbh = blockIdx.x, h = cbh % NH, cb = cbh / NH, c = cb / a.B, b = cb - c * a.B;
   const u16* blk = a.qkv + (long)cbh * 3 * Lp * DH;
+  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
   stage16(Ki, blk + (long)Lp * DH, DH, Lp, Lp);
   stage16(Vi, blk + 2L * Lp * DH, DH, Lp, Lp);
+  if (DROP) fill_hc(HC, Lp / 2, key, a.drop.layer);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
   const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
   const long orow0 = (long)c * a.B * L + (long)b * L;
   for (int q0 = wave * 16; q0 < Lp; q0 += 16 * AT_WAVES) {
     const int q = q0 + li;
     const s4v qf = *(const s4v*)(blk + (long)q * DH + 4 * g);
+    const uint32_t hr = DROP ? attn_hr(key, a.drop.layer, drow0 + q) : 0u;
     float m = -INFINITY, l = 0.f;
     f4v o = Z4;
     for (int kt = 0; kt < Lp; kt += 64) {
@@ -405,7 +428,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
       for (int t = 0; t < 4; ++t) {
         const f4v st = mfma16(lds4(Ki, kt + 16 * t + li, g), qf, Z4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) s[4 * t + e] = st[e] * LOG2E;
+        for (int e = 0; e < 4; ++e) s[4 * t + e] = st[e];  // (q carries 1/4 * log2 e: already log2-domain)
       }
       if (kt + 64 > L) {
 #pragma unroll
@@ -424,11 +447,13 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
         ps += pd[j];
       }
       if (DROP) {
-        float mk[16];
-        keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk);
-        keep8(key, a.drop.layer, drow0 + q, kt + 32 + 4 * g, kt + 48 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk + 8);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) pd[j] *= mk[j];
+        for (int t = 0; t < 4; ++t) {
+          bool k4[4];
+          keep4(HC, hr, kt + 16 * t + 4 * g, a.drop.thr16, k4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pd[4 * t + e] = k4[e] ? pd[4 * t + e] : 0.f;
+        }
       }
       l = l * alpha + sum_x16_x32(ps);
       m = mn;
@@ -437,7 +462,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
       o = mfma32(trfrag(Vi, kt + 32 + 4 * g, kt + 48 + 4 * g, lane), pack8f(pd + 8), o);
     }
     if (q < L) {
-      const float inv = 1.f / l;
+      const float inv = (DROP ? a.drop.inv_keep : 1.f) / l;
       *(u32x2v*)(a.o + (orow0 + q) * D + h * DH + 4 * g) = u32x2v{pk2(o[0] * inv, o[1] * inv), pk2(o[2] * inv, o[3] * inv)};
     }
     if (g == 0) a.lse2[(long)cbh * Lp + q] = q < L ? m + __log2f(l) : INFINITY;
@@ -458,24 +483,28 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
   uchar* Di = smem + Lp * 32;
   LDS_AS float* LS = (LDS_AS float*)(smem + 2 * Lp * 32);
   LDS_AS float* DL = LS + Lp;
+  LDS_AS uint32_t* HR = (LDS_AS uint32_t*)(DL + Lp);  // per-query row hashes of the dropout mask
   const int cbh = blockIdx.x, h = cbh % NH, cb = cbh / NH, c = cb / a.B, b = cb - c * a.B;
   const u16* blk = a.qkv + (long)cbh * 3 * Lp * DH;
   const long orow0 = (long)c * a.B * L + (long)b * L;
+  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
+  const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
   stage16(Qi, blk, DH, Lp, Lp);
   stage16(Di, a.dout + orow0 * D + h * DH, D, Lp, L);
   for (int e = threadIdx.x; e < Lp; e += blockDim.x) {
     LS[e] = a.lse2[(long)cbh * Lp + e];
     DL[e] = e < L ? a.delta[(long)cbh * Lp + e] : 0.f;
+    if (DROP) HR[e] = attn_hr(key, a.drop.layer, drow0 + e);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15, odd = lane & 1;
-  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
-  const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
+  const float ik = DROP ? a.drop.inv_keep : 1.f;
   for (int k0 = wave * 16; k0 < Lp; k0 += 16 * AT_WAVES) {
     const int kk = k0 + li;
     const bool kok = kk < L;
     const s4v kf = *(const s4v*)(blk + (long)(Lp + kk) * DH + 4 * g);
     const s4v vf = *(const s4v*)(blk + (long)(2 * Lp + kk) * DH + 4 * g);
+    const uint32_t hc = DROP ? attn_hc(key, a.drop.layer, (uint32_t)(kk >> 1)) : 0u;
     f4v dkT = Z4, dvT = Z4;
     for (int q0 = 0; q0 < L; q0 += 32) {
       float pdv[8], dsv[8];
@@ -486,22 +515,21 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
         const f4v dp = mfma16(lds4(Di, qb + li, g), vf, Z4);
         const f4v l4 = *(const LDS_AS f4v*)(LS + qb + 4 * g);
         const f4v d4 = *(const LDS_AS f4v*)(DL + qb + 4 * g);
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (DROP) {
-          const uint32_t r0 = drow0 + qb + 4 * g + 2 * odd;
-          const uint32_t ha = afl_hash4(key, a.drop.layer, r0, (uint32_t)(kk >> 1));
-          const uint32_t hb = afl_hash4(key, a.drop.layer, r0 + 1, (uint32_t)(kk >> 1));
+        bool kp[4] = {true, true, true, true};
+        if (DROP) {  // this lane mixes two of the four rows, its pair partner the other two (DPP swap)
+          const u32x2v hr = *(const LDS_AS u32x2v*)(HR + qb + 4 * g + 2 * odd);
+          const uint32_t ha = attn_mix(hr[0], hc), hb = attn_mix(hr[1], hc);
           const uint32_t pa = swap1(ha), pb = swap1(hb);
           const uint32_t hx[4] = {odd ? pa : ha, odd ? pb : hb, odd ? ha : pa, odd ? hb : pb};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) mk[e] = ((hx[e] >> (16 * odd)) & 0xFFFFu) >= a.drop.thr16 ? a.drop.inv_keep : 0.f;
+          for (int e = 0; e < 4; ++e) kp[e] = ((hx[e] >> (16 * odd)) & 0xFFFFu) >= a.drop.thr16;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pe = __builtin_amdgcn_exp2f(fmaf(s[e], LOG2E, -l4[e]));
+          const float pe = __builtin_amdgcn_exp2f(s[e] - l4[e]);
           const float p = kok ? pe : 0.f;
-          pdv[4 * qs + e] = p * mk[e];
-          dsv[4 * qs + e] = p * (dp[e] * mk[e] - d4[e]);
+          pdv[4 * qs + e] = kp[e] ? p : 0.f;  // (x 1/(1-p) on dV at the end)
+          dsv[4 * qs + e] = p * fmaf(kp[e] ? dp[e] : 0.f, ik, -d4[e]);
         }
       }
       // dV^T[d][key] += dO^T[d][q] Pd[q][key] ; dK^T[d][key] += Q_s^T[d][q] dS[q][key] (query order permuted)
@@ -511,8 +539,9 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
     if (kok) {  // lane: d = 4g + e of key kk
       u16* dk = a.dqkv + ((long)cbh * 3 + 1) * Lp * DH + (long)kk * DH + 4 * g;
       u16* dv = a.dqkv + ((long)cbh * 3 + 2) * Lp * DH + (long)kk * DH + 4 * g;
-      *(u32x2v*)dk = u32x2v{pk2(dkT[0], dkT[1]), pk2(dkT[2], dkT[3])};
-      *(u32x2v*)dv = u32x2v{pk2(dvT[0], dvT[1]), pk2(dvT[2], dvT[3])};
+      constexpr float iq = 1.f / LOG2E;  // dK = dS^T (q / 4) and the image holds q log2(e) / 4
+      *(u32x2v*)dk = u32x2v{pk2(dkT[0] * iq, dkT[1] * iq), pk2(dkT[2] * iq, dkT[3] * iq)};
+      *(u32x2v*)dv = u32x2v{pk2(dvT[0] * ik, dvT[1] * ik), pk2(dvT[2] * ik, dvT[3] * ik)};
     }
   }
 }
@@ -524,18 +553,22 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   const int Lp = a.Lp, L = a.L;
   uchar* Ki = smem;
   uchar* Vi = smem + Lp * 32;
+  LDS_AS uint32_t* HC = (LDS_AS uint32_t*)(smem + 2 * Lp * 32);
   const int cbh = blockIdx.x, h = cbh % NH, cb = cbh / NH, c = cb / a.B, b = cb - c * a.B;
   const u16* blk = a.qkv + (long)cbh * 3 * Lp * DH;
   const long orow0 = (long)c * a.B * L + (long)b * L;
+  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
   stage16(Ki, blk + (long)Lp * DH, DH, Lp, Lp);
   stage16(Vi, blk + 2L * Lp * DH, DH, Lp, Lp);
+  if (DROP) fill_hc(HC, Lp / 2, key, a.drop.layer);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
   const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
+  const float ik = DROP ? a.drop.inv_keep : 1.f;
   for (int q0 = wave * 16; q0 < L; q0 += 16 * AT_WAVES) {
     const int q = q0 + li;
     const bool qok = q < L;
+    const uint32_t hr = DROP ? attn_hr(key, a.drop.layer, drow0 + q) : 0u;
     const s4v qf = *(const s4v*)(blk + (long)q * DH + 4 * g);
     const s4v df = qok ? *(const s4v*)(a.dout + (orow0 + q) * D + h * DH + 4 * g) : s4v{0, 0, 0, 0};
     const float ls = a.lse2[(long)cbh * Lp + q];
@@ -546,16 +579,20 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
       const f4v s1 = mfma16(lds4(Ki, kt + 16 + li, g), qf, Z4);
       const f4v p0 = mfma16(lds4(Vi, kt + li, g), df, Z4);
       const f4v p1 = mfma16(lds4(Vi, kt + 16 + li, g), df, Z4);
-      float ds[8], mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-      if (DROP) keep8(key, a.drop.layer, drow0 + q, kt + 4 * g, kt + 16 + 4 * g, a.drop.thr16, a.drop.inv_keep, mk);
+      float ds[8];
+      bool kp[8] = {true, true, true, true, true, true, true, true};
+      if (DROP) {
+        keep4(HC, hr, kt + 4 * g, a.drop.thr16, kp);
+        keep4(HC, hr, kt + 16 + 4 * g, a.drop.thr16, kp + 4);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int kk = kt + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
         const float sv = j < 4 ? s0[j] : s1[j - 4];
         const float dp = j < 4 ? p0[j] : p1[j - 4];
-        const float pe = __builtin_amdgcn_exp2f(fmaf(sv, LOG2E, -ls));
+        const float pe = __builtin_amdgcn_exp2f(sv - ls);
         const float p = kk < L ? pe : 0.f;
-        ds[j] = p * (dp * mk[j] - dl);
+        ds[j] = p * fmaf(kp[j] ? dp : 0.f, ik, -dl);
       }
       acc = mfma32(trfrag(Ki, kt + 4 * g, kt + 16 + 4 * g, lane), pack8f(ds), acc);
     }
@@ -599,7 +636,8 @@ __device__ __forceinline__ int csum_feature(int lane) {
 
 __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
-  const int c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
+            g = lane >> 4, li = lane & 15;
   const float* pp = a.params + (long)c * a.P;
   build_img<true>(smem, PB_WO, LDK64, pp + a.w.ow, 64, 64);
   build_img<true>(smem, PB_W1, LDK64, pp + a.w.l1w, 256, 64);
@@ -619,7 +657,46 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
   for (int j = 0; j < 4; ++j) aWo[j] = Z4;
   float cg2 = 0.f, cb2 = 0.f, cbf2 = 0.f, cbf[4] = {0.f, 0.f, 0.f, 0.f}, cg1 = 0.f, cb1 = 0.f, cbo = 0.f;
   const int rl = 16 * wave + li;  // this lane's row within a block
+  // this lane's row inputs of one block; the NEXT block's are loaded while the current one computes
+  struct In {
+    f4v dy[4];
+    u32x2v xh2[4], xh1[4], o[4];
+    float rs1, rs2;
+  };
+  auto load = [&](int blk, In& in) {
+    const long r = 64L * blk + rl;
+    const bool ok = blk < nblk && r < R;
+    const long row = (long)c * R + (ok ? r : 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      in.dy[t] = (ok && !a.dpool) ? *(const f4v*)(a.dy + row * 64 + 16 * t + 4 * g) : Z4;
+      in.xh2[t] = ok ? *(const u32x2v*)(a.xh2 + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
+      in.xh1[t] = ok ? *(const u32x2v*)(a.xh1 + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
+      in.o[t] = ok ? *(const u32x2v*)(a.o + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
+    }
+    in.rs1 = ok ? a.rs[row * 2] : 0.f;
+    in.rs2 = ok ? a.rs[row * 2 + 1] : 0.f;
+  };
+  auto unbf = [](float (&x)[16], const u32x2v (&u)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x[4 * t] = __uint_as_float(u[t][0] << 16);
+      x[4 * t + 1] = __uint_as_float(u[t][0] & 0xFFFF0000u);
+      x[4 * t + 2] = __uint_as_float(u[t][1] << 16);
+      x[4 * t + 3] = __uint_as_float(u[t][1] & 0xFFFF0000u);
+    }
+  };
+  In cur;
+  load(blockIdx.x, cur);
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    In nxt;
+    load(blk + gridDim.x, nxt);
+    // lane / wave made opaque per block: every LDS address is recomputed inside the iteration (hoisted out of
+    // the loop, the per-lane swizzled addresses of all phases stayed live and spilled the accumulators)
+    int ln_ = lane, wv_ = wave;
+    opq(ln_, wv_);
+    {
+    const int lane = ln_, wave = wv_, g = ln_ >> 4, li = ln_ & 15, rl = 16 * wv_ + li;
     const long r = 64L * blk + rl;
     const bool ok = r < R;
     const long row = (long)c * R + (ok ? r : 0);
@@ -634,10 +711,13 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) dy[4 * t + i] = ok ? dp[16 * t + 4 * g + i] * il : 0.f;
     } else {
-      ldt16f(dy, a.dy + row * 64, g, ok);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dy[4 * t] = cur.dy[t][0]; dy[4 * t + 1] = cur.dy[t][1]; dy[4 * t + 2] = cur.dy[t][2]; dy[4 * t + 3] = cur.dy[t][3];
+      }
     }
-    ldt16(xh2, a.xh2 + row * 64, g, ok);
-    const float rstd2 = ok ? a.rs[row * 2 + 1] : 0.f;
+    unbf(xh2, cur.xh2);
+    const float rstd2 = cur.rs2;
     {
       float t2[16];
 #pragma unroll
@@ -658,8 +738,8 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
     csum_add(cbf2, df2, lane);
     // ---- h1 and the FFN activation, recomputed; stage d f2 and f for dW2
     float xh1[16], h1[16];
-    ldt16(xh1, a.xh1 + row * 64, g, ok);
-    const float rstd1 = ok ? a.rs[row * 2] : 0.f;
+    unbf(xh1, cur.xh1);
+    const float rstd1 = cur.rs1;
     {
       float g1[16], b1[16];
       vec16(g1, vec + V_G1 * 4, g);
@@ -695,7 +775,10 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
       for (int s = 0; s < 2; ++s) {
         const s8v y = tfrag<TK64>(smem + PB_DF2, 32 * s, wave, lane);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) aW2[j] = mma(tfrag<TK64>(smem + PB_F + (j >> 2) * TILE, 32 * s, j & 3, lane), y, aW2[j]);
+        for (int j = 0; j < 16; ++j) {
+          if ((j & 3) == 0) sb();  // (bounds the operand reads in flight: all 32 hoisted would cost 128 VGPRs)
+          aW2[j] = mma(tfrag<TK64>(smem + PB_F + (j >> 2) * TILE, 32 * s, j & 3, lane), y, aW2[j]);
+        }
       }
     }
     __syncthreads();
@@ -747,6 +830,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
         for (int kt = 0; kt < 4; ++kt) x[kt] = tfrag<TK64>(smem + PB_H1, 32 * s, kt, lane);
 #pragma unroll
         for (int jn = 0; jn < 4; ++jn) {
+          sb();
           const int tn = wave + 4 * jn;
           const s8v y = tfrag<TK64>(smem + PB_F + (tn >> 2) * TILE, 32 * s, tn & 3, lane);
 #pragma unroll
@@ -772,7 +856,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
       for (int j = 0; j < 16; ++j) da[j] = kf(ds1[j], m1, j, inv1);
     }
     csum_add(cbo, da, lane);
-    ldt16(ov, a.o + row * 64, g, ok);
+    unbf(ov, cur.o);
     __syncthreads();  // (the dW1 reads of H1 / F are done: DA / O live elsewhere, but keep the phases ordered)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -806,6 +890,8 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
         for (int kt = 0; kt < 4; ++kt) aWo[kt] = mma(tfrag<TK64>(smem + PB_O, 32 * s, kt, lane), y, aWo[kt]);
       }
     }
+    }
+    cur = nxt;
   }
   // ---- this workgroup's partials: dW tiles straight from the accumulators, vector sums in wave order
   float* ws = a.ws + ((long)c * gridDim.x + blockIdx.x) * AFL_HAR_POST_NG;
@@ -858,17 +944,41 @@ __global__ void __launch_bounds__(NTR) k_har_qkv_bwd(AflHarQkvB a) {
   for (int j = 0; j < 12; ++j) aW[j] = Z4;
   float cs[3] = {0.f, 0.f, 0.f};
   const int rl = 16 * wave + li;
-  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  // this lane's inputs of one block; the NEXT block's are loaded while the current one computes (the pass is
+  // latency-bound: a block's loads, two barriers and the dW MFMAs would otherwise run back to back)
+  struct In {
+    u32x2v dq[12], x[4];
+    f4v dr[4];
+  };
+  auto load = [&](int blk, In& in) {
     const long r = 64L * blk + rl;
-    const bool ok = r < R;
+    const bool ok = blk < nblk && r < R;
     const long row = (long)c * R + (ok ? r : 0);
-    const int bb = (int)(r / a.L), ll = (int)(r - (long)bb * a.L);
-    float dq[48];
+    const int bb = ok ? (int)(r / a.L) : 0, ll = ok ? (int)(r - (long)bb * a.L) : 0;
 #pragma unroll
     for (int T = 0; T < 12; ++T) {
       const int which = T >> 2, h = T & 3;
-      const u16* src = a.dqkv + ((((long)c * a.B + (ok ? bb : 0)) * NH + h) * 3 + which) * (long)a.Lp * DH + (long)ll * DH + 4 * g;
-      const u32x2v u = ok ? *(const u32x2v*)src : u32x2v{0u, 0u};
+      const u16* src = a.dqkv + ((((long)c * a.B + bb) * NH + h) * 3 + which) * (long)a.Lp * DH + (long)ll * DH + 4 * g;
+      in.dq[T] = ok ? *(const u32x2v*)src : u32x2v{0u, 0u};
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      in.dr[t] = ok ? *(const f4v*)(a.dres + row * 64 + 16 * t + 4 * g) : Z4;
+      in.x[t] = ok ? *(const u32x2v*)(a.x + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
+    }
+  };
+  In cur;
+  load(blockIdx.x, cur);
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    In nxt;
+    load(blk + gridDim.x, nxt);
+    const long r = 64L * blk + rl;
+    const bool ok = r < R;
+    const long row = (long)c * R + (ok ? r : 0);
+    float dq[48];
+#pragma unroll
+    for (int T = 0; T < 12; ++T) {
+      const u32x2v u = cur.dq[T];
       dq[4 * T] = __uint_as_float(u[0] << 16);
       dq[4 * T + 1] = __uint_as_float(u[0] & 0xFFFF0000u);
       dq[4 * T + 2] = __uint_as_float(u[1] << 16);
@@ -883,7 +993,14 @@ __global__ void __launch_bounds__(NTR) k_har_qkv_bwd(AflHarQkvB a) {
       csum_add(cs[q], x16, lane);
     }
     float dx[16], xv[16];
-    ldt16f(dx, a.dres + row * 64, g, ok);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dx[4 * t] = cur.dr[t][0]; dx[4 * t + 1] = cur.dr[t][1]; dx[4 * t + 2] = cur.dr[t][2]; dx[4 * t + 3] = cur.dr[t][3];
+      xv[4 * t] = __uint_as_float(cur.x[t][0] << 16);
+      xv[4 * t + 1] = __uint_as_float(cur.x[t][0] & 0xFFFF0000u);
+      xv[4 * t + 2] = __uint_as_float(cur.x[t][1] << 16);
+      xv[4 * t + 3] = __uint_as_float(cur.x[t][1] & 0xFFFF0000u);
+    }
     {
       f4v acc[4] = {Z4, Z4, Z4, Z4};
 #pragma unroll
@@ -898,7 +1015,6 @@ __global__ void __launch_bounds__(NTR) k_har_qkv_bwd(AflHarQkvB a) {
         for (int i = 0; i < 4; ++i) dx[4 * T + i] += acc[T][i];
     }
     if (ok) stt16f(a.dx + row * 64, dx, g);
-    ldt16(xv, a.x + row * 64, g, ok);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + QB_X, rl, 4 * t + g, xv + 4 * t);
     __syncthreads();
@@ -916,6 +1032,7 @@ __global__ void __launch_bounds__(NTR) k_har_qkv_bwd(AflHarQkvB a) {
       }
     }
     __syncthreads();
+    cur = nxt;
   }
   float* ws = a.ws + ((long)c * gridDim.x + blockIdx.x) * AFL_HAR_QKV_NG;
 #pragma unroll
@@ -984,7 +1101,7 @@ int afl_har_qkv(const AflHarQkv& a, hipStream_t s) {
 
 int afl_har_attn_fwd(const AflHarAttn& a, hipStream_t s) {
   if (a.Lp % 64 || a.Lp < a.L || a.Lp > 1024) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)a.Lp * 32 * 2;
+  const size_t lds = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 2;  // K, V images + the column-pair hash table
   if (a.drop.thr16)
     hipLaunchKernelGGL(k_har_attn_fwd<true>, dim3(a.C * a.B * NH), dim3(AT_NT), lds, s, a);
   else
@@ -994,7 +1111,7 @@ int afl_har_attn_fwd(const AflHarAttn& a, hipStream_t s) {
 
 int afl_har_attn_bwd(const AflHarAttn& a, hipStream_t s) {
   if (a.Lp % 64 || a.Lp < a.L || a.Lp > 1024) return (int)hipErrorInvalidValue;
-  const size_t kv = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 8, dq = (size_t)a.Lp * 32 * 2;
+  const size_t kv = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 12, dq = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 2;
   const dim3 grid(a.C * a.B * NH);
   if (a.drop.thr16) {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<true>, grid, dim3(AT_NT), kv, s, a);

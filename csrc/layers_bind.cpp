@@ -657,7 +657,7 @@ void attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse, torch::Tens
 void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor rows, torch::Tensor idx, torch::Tensor bsz,
                 torch::Tensor epoch, torch::Tensor nb, torch::Tensor seeds, double p, int64_t min_bs, bool nan_abort,
                 double lr, torch::Tensor failed, torch::Tensor losses, torch::Tensor ws, torch::Tensor ctr,
-                c10::optional<torch::Tensor> stamps) {
+                c10::optional<torch::Tensor> stamps, int64_t opt_mode) {
   dense(params, "params");
   dense(rows, "rows");
   dense(idx, "idx", torch::kInt32);
@@ -701,6 +701,8 @@ void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor r
   a.min_bs = (int)min_bs;
   a.nan_abort = nan_abort ? 1 : 0;
   a.lr = (float)lr;
+  TORCH_CHECK(opt_mode == 0 || opt_mode == 1, "cnn2_train: opt_mode 0 (Adam) or 1 (SGD)");
+  a.opt_mode = (int)opt_mode;
   a.failed = failed.data_ptr<int>();
   a.losses = losses.data_ptr<float>();
   a.ws = ws.data_ptr();
@@ -736,7 +738,8 @@ void afl_register_layers(pybind11::module& m) {
   m.def("cnn_wimg_size", &afl_cnn_wimg_ushorts);
   m.def("cnn2_train", &cnn2_train, py::arg("params"), py::arg("offs"), py::arg("rows"), py::arg("idx"), py::arg("bsz"),
         py::arg("epoch"), py::arg("nb"), py::arg("seeds"), py::arg("p"), py::arg("min_bs"), py::arg("nan_abort"),
-        py::arg("lr"), py::arg("failed"), py::arg("losses"), py::arg("ws"), py::arg("ctr"), py::arg("stamps") = none);
+        py::arg("lr"), py::arg("failed"), py::arg("losses"), py::arg("ws"), py::arg("ctr"), py::arg("stamps") = none,
+        py::arg("opt_mode") = 0);
   m.def("cnn2_ws_bytes", &afl_cnn2_ws_bytes);
   m.def("cnn2_ctr_words", &afl_cnn2_ctr_words);
   m.def("cnn2_wgs_per_client", &afl_cnn2_wgs_per_client);

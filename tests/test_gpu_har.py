@@ -21,10 +21,10 @@ def _close(a, b, rel, name):
 
 
 def _headmajor(qkv, B, L, Lp):
-    """[C, B*L, 192] fp32 -> [C*B*4, 3, Lp, 16] bf16 (q scaled by 1/4)."""
+    """[C, B*L, 192] fp32 -> [C*B*4, 3, Lp, 16] bf16 (q scaled by log2(e) / 4, as the program stores it)."""
     C = qkv.shape[0]
     x = qkv.reshape(C, B, L, 3, 4, 16).permute(0, 1, 4, 3, 2, 5).clone()  # [C, B, H, 3, L, 16]
-    x[:, :, :, 0] *= 0.25
+    x[:, :, :, 0] *= 0.25 * 1.4426950408889634
     out = torch.zeros(C, B, 4, 3, Lp, 16, dtype=torch.bfloat16, device=qkv.device)
     out[..., :L, :] = x.to(torch.bfloat16)
     return out.reshape(C * B * 4, 3, Lp, 16)
@@ -42,11 +42,16 @@ def test_har_attention_matches_composite(gpu, L, p):
     nat = native()
     ctl = _ctl(C, gpu)
     hm = _headmajor(qkv.to(gpu), B, L, Lp)
+    # the composite sees the q the kernel reads (rounded after the log2(e)/4 scale)
+    qr = hm.float().cpu().reshape(C, B, 4, 3, Lp, 16)[..., :L, :][:, :, :, 0] / (0.25 * 1.4426950408889634)
+    qkv = qkv.reshape(C, B, L, 3, 4, 16).clone()
+    qkv[:, :, :, 0] = qr.permute(0, 1, 3, 2, 4)
+    qkv = qkv.reshape(C, B * L, 192)
     o = torch.zeros(C, B * L, 64, dtype=torch.bfloat16, device=gpu)
     lse2 = torch.zeros(C * B * 4, Lp, device=gpu)
     nat.har_attn_fwd(hm, o, lse2, B, L, ctl.seeds if p else None, ctl.stepctl if p else None, 2, p)
     cc = _ctl(C, "cpu")
-    ref_o, ref_lse = Lx._attn_ref(qkv, B, L, cc, 2, p)
+    ref_o, ref_lse = Lx._attn_ref(qkv, B, L, cc, 2, p, "rc")
     _close(o, ref_o, 2e-2, "O")
     _close(lse2[:, :L] * np.log(2.0), ref_lse.reshape(-1, L), 1e-3, "lse")
     # backward: Delta from the kernel's own (bf16) O, as the post pass computes it
@@ -59,7 +64,7 @@ def test_har_attention_matches_composite(gpu, L, p):
                      ctl.stepctl if p else None, 2, p)
     x = qkv.clone().requires_grad_(True)
     with torch.enable_grad():
-        out, _ = Lx._attn_ref(x, B, L, cc, 2, p)
+        out, _ = Lx._attn_ref(x, B, L, cc, 2, p, "rc")
         (gref,) = torch.autograd.grad(out, x, dout)
     gq = gref.reshape(C, B, L, 3, 4, 16).permute(0, 1, 4, 3, 2, 5).reshape(C * B * 4, 3, L, 16)
     got = dq[:, :, :L].float().cpu()

@@ -382,3 +382,36 @@ def test_cnn2_onchip_trainer_tracks_layer_program(gpu, monkeypatch, C, n, E):
     assert torch.allclose(res["1"][1], res["0"][1], rtol=2e-2, atol=2e-3), (res["1"][1], res["0"][1])
     assert (res["1"][0] - res["0"][0]).abs().max() < 0.05
     assert (res["1"][0] - params).abs().max() > 1e-3  # it trained
+
+
+@pytest.mark.parametrize("B,drop", [(128, True), (128, False), (37, True)])
+def test_cnn2_sgd_gradients_match_composite(gpu, monkeypatch, B, drop):
+    """One raw-SGD step (opt_mode 1: p -= lr g) of the on-chip CNN trainer exposes its gradients: per tensor
+    they match the fp32 composite of the same program (CPU, same batch rows and dropout masks), as the tf2 /
+    rnn2 trainers are tested (tests/test_gpu_transformer.py, test_gpu_rnn.py)."""
+    from attackfl_amd.models import ParamLayout
+
+    monkeypatch.setenv("AFL_CNN2", "1")
+    C, n = 2, 400
+    ds = synthetic_icu(n)
+    order = torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(c))[:B] for c in range(C)])
+    plan = Plan(order[:, None, :].to(torch.int32), torch.tensor([B] * C, dtype=torch.int32), 1)
+    params = _params("CNNModel", C)
+    res = []
+    for dev in (DEV, "cpu"):
+        p = params.clone().to(dev)
+        runner = ProgramRunner(make_program("CNNModel", C, B, dev, dropout=drop), use_graph=False)
+        if dev == DEV:
+            assert runner._onchip_cnn(p, 1.0, None)
+        ok, losses = runner.train(DeviceTable(ds, dev), p, Plan(plan.order.to(dev), plan.nd, 1), lr=0.0, seeds=[3, 4],
+                                  sgd_lr=1.0)
+        assert ok.all()
+        res.append(((params - p.cpu()), losses))
+    assert torch.allclose(res[0][1], res[1][1], rtol=1e-2)
+    lay = ParamLayout.for_model("CNNModel")
+    for s in lay.slots:
+        a = res[0][0][:, s.offset:s.offset + s.numel]
+        b = res[1][0][:, s.offset:s.offset + s.numel]
+        scale = b.abs().max().item() + 1e-6
+        err = (a - b).abs().max().item() / scale
+        assert err < 0.08, (s.name, err, scale)

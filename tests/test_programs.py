@@ -147,3 +147,19 @@ def test_adam_dropout_training_runs_and_nan_fails():
     assert not torch.equal(params[0], before[0])
     # the failed client stops before its first update
     assert torch.equal(torch.nan_to_num(params[1]), torch.nan_to_num(before[1]))
+
+
+def test_attention_rc_mask_statistics():
+    """The row / column-pair attention dropout hash (masks.keep_rc, har.hip attn_mix): keep rate 1 - p, no
+    row or column structure (every row's and column's keep rate near 1 - p), independent of the pair hash."""
+    import numpy as np
+
+    from attackfl_amd.ops import masks
+
+    rows, cols = np.arange(512)[:, None], np.arange(576)[None, :]
+    k = masks.keep_rc(masks.step_key(7, 3), 10, rows, cols, 0.1).numpy()
+    assert abs(k.mean() - 0.9) < 0.003
+    assert np.abs(k.mean(axis=1) - 0.9).max() < 0.06 and np.abs(k.mean(axis=0) - 0.9).max() < 0.06
+    kp = masks.keep(masks.step_key(7, 3), 10, rows, cols, 0.1).numpy()
+    agree = (k == kp).mean()
+    assert abs(agree - (0.9 * 0.9 + 0.1 * 0.1)) < 0.01  # independent draws
