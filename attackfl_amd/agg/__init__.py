@@ -182,18 +182,42 @@ def scionfl(U: torch.Tensor, sizes: torch.Tensor, seed: int = 0, **_) -> AggResu
     return AggResult(out, True, {"kept": keep, "scores": cosd, "threshold": thr})
 
 
-def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) -> AggResult:
-    from scipy.stats import median_abs_deviation
+def _median(x: torch.Tensor) -> torch.Tensor:
+    """np.median: the mean of the two middle values for an even count."""
+    s = torch.sort(x).values
+    n = s.shape[0]
+    return 0.5 * (s[(n - 1) // 2] + s[n // 2])
 
-    z = _pca_project(U, 1)[:, 0]
-    mad = median_abs_deviation(z)
-    med = np.median(z)
-    scores = np.abs(z - med) / (1.4826 * mad + 1e-6)
-    bad = set(np.where(scores > threshold)[0].tolist())
-    keep = [i for i in range(U.shape[0]) if i not in bad]
-    if not keep:
-        keep = list(range(U.shape[0]))
-    return AggResult(ops.fedavg(U[keep], sizes[keep]), True, {"anomalies": sorted(bad)})
+
+def _top_pc_scores(U: torch.Tensor, squarings: int = 12) -> torch.Tensor:
+    """First principal-component scores of the rows (sklearn ``PCA(1).fit_transform`` up to the sign) with no
+    host synchronisation: the n x n Gram of the centred rows, its leading eigenvector by repeated squaring
+    (the gap ratio raised to 2^squarings, trace-normalised every step in fp64), score = v * sqrt(lambda)."""
+    X = U.double()
+    Xc = X - X.mean(dim=0, keepdim=True)
+    G = Xc @ Xc.t()
+    M = G / G.diagonal().sum().clamp_min(1e-300)
+    for _ in range(squarings):
+        M = M @ M
+        M = M / M.diagonal().sum().clamp_min(1e-300)
+    i = torch.argmax(M.diagonal())
+    v = M.index_select(1, i.reshape(1))[:, 0]
+    v = v / torch.linalg.vector_norm(v).clamp_min(1e-300)
+    lam = (v @ G @ v).clamp_min(0.0)
+    return v * torch.sqrt(lam)
+
+
+def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) -> AggResult:
+    """FLTracer anomaly filter (reference ``fltracer_detect_anomalies``, src/Utils.py:363-369): robust z-score
+    |z - median| / (1.4826 MAD + 1e-6) of the first-PC scores, rows above ``threshold`` dropped, size-weighted
+    FedAvg of the rest (every row when all are flagged).  All on the device."""
+    z = _top_pc_scores(U)
+    med = _median(z)
+    mad = _median((z - med).abs())
+    scores = (z - med).abs() / (1.4826 * mad + 1e-6)
+    bad = scores > threshold
+    out = _masked_mean(U, ~bad, _device_weights(sizes, U.device))
+    return AggResult(out, True, {"anomalies": bad, "scores": scores})
 
 
 def byzantine(U: torch.Tensor, sizes=None, threshold: float = 0.9, **_) -> AggResult:

@@ -315,19 +315,20 @@ def random_noise(own: torch.Tensor, perturbation: float, seed: int = 0) -> Attac
 
 
 def run_attack(mode: str, args: Sequence[float], own: torch.Tensor, G: Optional[torch.Tensor], engine: DistanceEngine,
-               seed: int = 0) -> AttackResult:
-    """Dispatch by the reference's ``--attack_mode`` names.  ``seed`` keys the Random attack's noise."""
+               seed: int = 0, gamma: float = 50.0, tau: float = 1.0) -> AttackResult:
+    """Dispatch by the reference's ``--attack_mode`` names.  ``seed`` keys the Random attack's noise;
+    ``gamma`` / ``tau`` start and stop the bisection attacks (reference: fixed 50 / 1)."""
     if mode == "Random":
         sigma = args[0] if args else 1e6
         return random_noise(own, sigma, seed)
     if G is None or G.shape[0] == 0:
         raise ValueError("attack needs genuine models")
     if mode == "Min-Max":
-        return min_max(G, own, engine)
+        return min_max(G, own, engine, gamma=gamma, tau=tau)
     if mode == "Min-Sum":
-        return min_sum(G, own, engine)
+        return min_sum(G, own, engine, gamma=gamma, tau=tau)
     if mode == "Opt-Fang":
-        return opt_fang(G, own, engine)
+        return opt_fang(G, own, engine, gamma=gamma, tau=tau)
     if mode == "LIE":
         z = args[0] if args else 0.74
         if G.shape[0] == 1:

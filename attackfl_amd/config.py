@@ -105,15 +105,31 @@ def _deep_merge(base: Dict[str, Any], over: Dict[str, Any]) -> Dict[str, Any]:
 
 @dataclass
 class AttackSpec:
+    """One attacker's schedule.  ``gamma`` / ``tau`` are the Min-Max / Min-Sum / Opt-Fang bisection's start
+    value and stop gap; the reference hard-codes them to 50 and 1 (``src/Utils.py:101,134,167``), which
+    stay the defaults.  With those the tried γs are 50, 25, ..., 1.5625 and a candidate can only be
+    accepted at γ ≥ 1.5625 (profiles/attack_study/README.md shows why that rarely passes the distance check)."""
     mode: str
     round: int
     args: List[float] = field(default_factory=list)
+    gamma: float = 50.0
+    tau: float = 1.0
 
     def __post_init__(self):
         if self.mode not in ATTACK_MODES:
             raise ValueError(f"Attack mode '{self.mode}' is not valid (choose from {ATTACK_MODES}).")
         self.round = int(self.round)
         self.args = [float(a) for a in (self.args or [])]
+        self.gamma, self.tau = float(self.gamma), float(self.tau)
+        if not (self.gamma > 0 and self.tau > 0):
+            raise ValueError(f"bisection gamma / tau must be positive (got {self.gamma}, {self.tau})")
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {"mode": self.mode, "round": self.round, "args": self.args, "gamma": self.gamma, "tau": self.tau}
+
+    @classmethod
+    def from_dict(cls, v: Dict[str, Any]) -> "AttackSpec":
+        return cls(v["mode"], v.get("round", 1), v.get("args", []), v.get("gamma", 50.0), v.get("tau", 1.0))
 
 
 @dataclass
@@ -211,7 +227,7 @@ class Config:
     def attackers(self) -> Dict[int, AttackSpec]:
         out: Dict[int, AttackSpec] = {}
         for k, v in (self.raw["comm"].get("attackers") or {}).items():
-            out[int(k)] = AttackSpec(v["mode"], v.get("round", 1), v.get("args", []))
+            out[int(k)] = AttackSpec.from_dict(v)
         return out
 
     def validate(self) -> "Config":

@@ -632,7 +632,7 @@ class FLEngine:
             with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
                 for j, i, lc, atk in attack_jobs:
                     res = run_attack(atk.mode, atk.args, self.local_params[j], lc.genuine, self.dist,
-                                     seed=lc.seed * 1009 + lc.training_round)
+                                     seed=lc.seed * 1009 + lc.training_round, gamma=atk.gamma, tau=atk.tau)
                     atk_out.append((j, res.ok and res.params is not None, res.params))
                     self._attack_info = res.info
                     if self.verbose:  # (reads the attack's device scalars back: verbose runs only)

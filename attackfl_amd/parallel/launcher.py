@@ -156,7 +156,7 @@ def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float 
     if rank > n:
         raise RuntimeError(f"server expects {n} clients; this would be client #{rank}")
     desc = {"uuid": str(uuid.uuid4()), "message": "Hello from Client!",
-            "attack": None if attack is None else {"mode": attack.mode, "round": attack.round, "args": attack.args},
+            "attack": None if attack is None else attack.to_dict(),
             "device": device_descriptor(device) if device is not None else {"type": "cpu"}}
     store.set(PREFIX + f"client/{rank}", json.dumps(desc))
     print_with_color(f"[>>>] Client {desc['uuid']} registered as rank {rank}", "red")
@@ -172,7 +172,7 @@ def table_from_json(table_json: List[Dict]):
     for d in table_json:
         a = d.get("attack")
         out.append(ClientInfo(int(d["index"]), str(d["uuid"]), int(d["owner"]),
-                              AttackSpec(a["mode"], a["round"], a.get("args", [])) if a else None))
+                              AttackSpec.from_dict(a) if a else None))
     return out
 
 

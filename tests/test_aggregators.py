@@ -81,7 +81,43 @@ def test_fltracer_flags_outlier():
     U = _U(10)
     U[4] += 3.0
     res = agg.fltracer(U, torch.ones(10))
-    assert 4 in res.info["anomalies"]
+    assert 4 in agg.host_info(res.info)["anomalies"]
+
+
+def _fltracer_numpy(U, sizes, threshold=2.5):
+    """The reference pipeline on the host: PCA(1) scores via eigh, scipy MAD, np.median."""
+    import numpy as np
+    from scipy.stats import median_abs_deviation
+
+    X = U.double().numpy()
+    Xc = X - X.mean(axis=0, keepdims=True)
+    ev, V = np.linalg.eigh(Xc @ Xc.T)
+    z = V[:, -1] * np.sqrt(max(ev[-1], 0.0))
+    scores = np.abs(z - np.median(z)) / (1.4826 * median_abs_deviation(z) + 1e-6)
+    bad = scores > threshold
+    keep = [i for i in range(len(z)) if not bad[i]] or list(range(len(z)))
+    w = sizes.double().numpy()[keep]
+    return sorted(np.where(bad)[0].tolist()), (X[keep] * (w / w.sum())[:, None]).sum(axis=0), scores
+
+
+@pytest.mark.parametrize("n,seed", [(8, 0), (9, 1), (10, 2), (6, 3)])
+def test_fltracer_device_form_matches_host_pipeline(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    U = torch.randn(n, 3000, generator=g)
+    U[1] += 2.5 * torch.randn(3000, generator=g)  # one dominant direction
+    U[n - 1] *= 4.0
+    sizes = torch.randint(50, 200, (n,), generator=g).float()
+    res = agg.fltracer(U, sizes)
+    bad, ref, scores = _fltracer_numpy(U, sizes)
+    assert agg.host_info(res.info)["anomalies"] == bad
+    assert torch.allclose(res.info["scores"], torch.from_numpy(scores), rtol=1e-6, atol=1e-6)
+    assert torch.allclose(res.params.double(), torch.from_numpy(ref), rtol=1e-5, atol=1e-6)
+
+
+def test_fltracer_identical_rows_keep_everyone():
+    U = torch.ones(5, 100)
+    res = agg.fltracer(U, torch.ones(5))
+    assert agg.host_info(res.info)["anomalies"] == [] and torch.allclose(res.params, U[0])
 
 
 def test_byzantine_filter():

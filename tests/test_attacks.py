@@ -171,3 +171,33 @@ def test_compute_distance_spectral_vs_frobenius():
     d = compute_distance(a, b)
     assert d == pytest.approx(torch.linalg.matrix_norm(a["w"], 2).item() + a["b"].norm().item(), rel=1e-5)
     assert d < a["w"].norm().item()
+
+
+@pytest.mark.parametrize("kind,fn", [("max", attacks.min_max), ("sum", attacks.min_sum)])
+def test_bisection_tau_extension_matches_reference_loop(kind, fn):
+    """A smaller stop gap (AttackSpec.tau, an extension: the reference fixes τ = 1) runs the same reference
+    loop further and reaches the accept boundary γ* ≈ 1 that the reference's last γ (1.5625) never does."""
+    gen = _genuine("TransformerModel", 5, 0.1, seed=4)
+    lay = ParamLayout.from_state_dict(gen[0])
+    G = torch.stack([lay.flatten(g) for g in gen])
+    res = fn(G, G[0].clone(), DistanceEngine(lay, "spectral"), tau=0.05)
+    ref_sd, ref_gamma = ref_bisection(gen, kind, tau=0.05)
+    hi = attacks.host_info(res.info)
+    assert len(hi["gammas"]) == attacks.bisect_iterations(50.0, 0.05) == 10
+    assert hi["gamma"] == pytest.approx(ref_gamma)
+    assert 0.0 < hi["gamma_succ"] < 1.5625 and any(hi["accepted"])
+    assert torch.allclose(res.params, lay.flatten(ref_sd), atol=1e-5)
+    default = attacks.host_info(fn(G, G[0].clone(), DistanceEngine(lay, "spectral")).info)
+    assert default["gamma_succ"] == 0.0 and default["gamma"] == 1.5625  # every reference γ rejected
+
+
+def test_attack_spec_bisection_fields_round_trip():
+    from attackfl_amd.config import AttackSpec
+
+    a = AttackSpec("Min-Max", 3, [], tau=0.05)
+    assert (a.gamma, a.tau) == (50.0, 0.05)
+    b = AttackSpec.from_dict(a.to_dict())
+    assert b == a
+    assert AttackSpec.from_dict({"mode": "LIE", "args": [0.74]}).tau == 1.0  # reference default
+    with pytest.raises(ValueError):
+        AttackSpec("Min-Max", 1, [], tau=0.0)

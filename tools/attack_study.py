@@ -27,7 +27,6 @@ sys.path.insert(0, ROOT)
 
 MODES = ["fedavg", "median", "trimmed_mean", "krum", "hyper"]
 ATTACKS = {"none": None, "LIE": [0.74], "Min-Max": [], "Min-Sum": [], "Opt-Fang": [], "Random": [0.5]}
-ATTACKERS = (5, 6, 7)
 
 
 def cells(spec: str):
@@ -37,7 +36,7 @@ def cells(spec: str):
 
 
 def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0, genuine_rate: float = 0.5,
-             distance: str = "spectral", seed: int = 7) -> dict:
+             distance: str = "spectral", seed: int = 7, tau: float = 1.0, attackers: int = 3) -> dict:
     import torch
 
     if threads:
@@ -58,7 +57,8 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0,
         "log_path": tmp,
     }
     cfg = from_dict(d)
-    atk = {} if ATTACKS[attack] is None else {c: AttackSpec(attack, 2, ATTACKS[attack]) for c in ATTACKERS}
+    who = range(8 - attackers, 8)
+    atk = {} if ATTACKS[attack] is None else {c: AttackSpec(attack, 2, ATTACKS[attack], tau=tau) for c in who}
     eng = FLEngine(cfg, device=device, table=build_client_table(cfg, 1, atk), verbose=False)
     t0 = time.time()
     stalled = False
@@ -70,18 +70,20 @@ def run_cell(mode: str, attack: str, device: str, rounds: int, threads: int = 0,
     eng.close()
     ok = [r for r in hist if r["ok"]]
     return {"device": "gpu" if device.startswith("cuda") else "cpu", "mode": mode, "attack": attack,
-            "genuine_rate": genuine_rate, "distance": distance, "seed": seed,
+            "genuine_rate": genuine_rate, "distance": distance, "seed": seed, "tau": tau,
             "attackers": len(atk), "rounds": len(ok), "failed_rounds": len(hist) - len(ok), "stalled": stalled,
             "auc": [round(r["metric"], 5) for r in ok], "final_auc": round(ok[-1]["metric"], 5) if ok else None,
             "attack_gamma": [round(r["attack"]["gamma"], 4) for r in ok if "attack" in r and "gamma" in r["attack"]],
+            # last ACCEPTED γ per attacking round (0: every tried γ was rejected)
+            "gamma_succ": [round(r["attack"]["gamma_succ"], 4) for r in ok if "gamma_succ" in r.get("attack", {})],
             # every tried γ of the last attacking round (the reference prints each, src/Utils.py:119)
             "gammas_last": next((r["attack"]["gammas"] for r in reversed(hist) if "gammas" in r.get("attack", {})), None),
             "seconds": round(time.time() - t0, 2)}
 
 
 def _worker(args):
-    mode, attack, device, rounds, threads, gr, dist, seed = args
-    return run_cell(mode, attack, device, rounds, threads, gr, dist, seed)
+    mode, attack, device, rounds, threads, gr, dist, seed, tau, na = args
+    return run_cell(mode, attack, device, rounds, threads, gr, dist, seed, tau, na)
 
 
 def main() -> int:
@@ -93,6 +95,8 @@ def main() -> int:
     ap.add_argument("--jobs", type=int, default=1, help="parallel CPU processes")
     ap.add_argument("--genuine-rate", type=float, default=0.5, help="server.genuine-rate (reference default 0.5)")
     ap.add_argument("--distance", default="spectral", choices=["spectral", "flat"])
+    ap.add_argument("--tau", type=float, default=1.0, help="bisection stop gap (reference: 1.0)")
+    ap.add_argument("--attackers", type=int, default=3, help="attacking clients (the last N of 8)")
     ap.add_argument("--seeds", default="7", help="comma-separated run seeds (engine seed; server random-seed = seed - 6)")
     args = ap.parse_args()
     seeds = [int(x) for x in args.seeds.split(",")]
@@ -104,13 +108,15 @@ def main() -> int:
             threads = max(1, (os.cpu_count() or 8) // args.jobs)
             with mp.get_context("spawn").Pool(args.jobs) as pool:
                 for res in pool.imap_unordered(_worker, [(m, a, args.device, args.rounds, threads, args.genuine_rate,
-                                                                   args.distance, sd) for m, a, sd in todo]):
+                                                                   args.distance, sd, args.tau, args.attackers)
+                                                                  for m, a, sd in todo]):
                     fh.write(json.dumps(res) + "\n")
                     fh.flush()
                     print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)
         else:
             for m, a, sd in todo:
-                res = run_cell(m, a, args.device, args.rounds, 0, args.genuine_rate, args.distance, sd)
+                res = run_cell(m, a, args.device, args.rounds, 0, args.genuine_rate, args.distance, sd, args.tau,
+                               args.attackers)
                 fh.write(json.dumps(res) + "\n")
                 fh.flush()
                 print(res["mode"], res["attack"], res["final_auc"], res["seconds"], flush=True)

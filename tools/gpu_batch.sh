@@ -22,6 +22,7 @@ for s in "$@"; do
     bench) step bench 300 python bench.py --steps 20 --warmup 3 ;;
     gpu_all) step gpu_all 900 $PYT tests -m gpu ;;
     har_prof) step har_prof 320 bash tools/rocprof_har.sh ;;
+    valu) step valu_rates 90 ./tools/valu_rates.bin ;;
     study) step study_g10 600 python tools/attack_study.py --device cuda --out gpurun_out/study_gpu_r4_g10.jsonl --genuine-rate 1.0
            step study_g10f 300 python tools/attack_study.py --device cuda --out gpurun_out/study_gpu_r4_g10_flat.jsonl --genuine-rate 1.0 --distance flat
            step study_seeds 300 python tools/attack_study.py --device cuda --out gpurun_out/study_gpu_r4_seeds.jsonl --cells fedavg:Opt-Fang,trimmed_mean:Opt-Fang,trimmed_mean:Random,hyper:Opt-Fang,fedavg:Random --seeds 7,8,9,10,11 ;;
