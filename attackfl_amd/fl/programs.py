@@ -321,6 +321,13 @@ class HARProgram(_Program):
         are the same bits whichever clients share the launch (placement independence)."""
         return 32
 
+    def _mask(self, i) -> torch.Tensor:
+        """Layer i's attention-dropout keep words: written by the forward kernel, read by both backward kernels."""
+        from .. import ops
+
+        return self.buf(f"amask{i}", self.C * self.B * 4, int(ops.native().har_mask_words(self._lp())),
+                        dtype=torch.int64)
+
     def _post_seg(self, i) -> torch.Tensor:
         key = f"_seg_post{i}"
         if key not in self._bufs:
@@ -356,7 +363,7 @@ class HARProgram(_Program):
             qkv = self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf)  # padding rows stay zero
             nat.har_qkv(h, params, w[0], w[1], qkv, B, L, 0.25 * 1.4426950408889634)  # 1/sqrt(16) * log2(e)
             o, lse2 = self.buf(f"ob{i}", C, R, 64, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp)
-            nat.har_attn_fwd(qkv, o, lse2, B, L, seeds, stepctl, 10 * i, p)
+            nat.har_attn_fwd(qkv, o, lse2, B, L, seeds, stepctl, 10 * i, p, self._mask(i) if seeds is not None else None)
             y = self.buf(f"hb{i + 1}", C, R, 64, dtype=bf)
             nat.har_post(o, h, self.buf(f"xh1_{i}", C, R, 64, dtype=bf), self.buf(f"xh2_{i}", C, R, 64, dtype=bf),
                          self.buf(f"rs{i}", C, R, 2), y, params, w, seeds, stepctl, 10 * i, p)
@@ -397,7 +404,8 @@ class HARProgram(_Program):
                              p, G)
             nat.har_reduce(ws_p, G, int(nat.har_post_ng), self._post_seg(i), grads)
             nat.har_attn_bwd(self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp),
-                             dout, delta, dqkv, B, L, seeds, stepctl, 10 * i, p)
+                             dout, delta, dqkv, B, L, seeds, stepctl, 10 * i, p,
+                             self._mask(i) if seeds is not None else None)
             dx = dxs[i % 2]
             nat.har_qkv_bwd(dqkv, dres, self.buf(f"hb{i}", C, R, 64, dtype=bf), dx, ws_q, params, w[0], B, L, G)
             nat.har_reduce(ws_q, G, int(nat.har_qkv_ng), self._qkv_seg(i), grads)

@@ -129,9 +129,21 @@ AflHarAttn attn_args(torch::Tensor qkv, torch::Tensor lse2, int64_t B, int64_t L
   return a;
 }
 
+// dropout keep words (written by the forward, read by the backward): int64 [C*B*4, AFL_HAR_MASK_WORDS(Lp)]
+void attn_mask(AflHarAttn& a, const c10::optional<torch::Tensor>& mask) {
+  if (!a.drop.thr16) return;
+  TORCH_CHECK(mask.has_value() && mask->defined(), "attention dropout needs the keep-word buffer");
+  TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == torch::kInt64 && mask->is_contiguous(), "mask: int64 cuda");
+  TORCH_CHECK(mask->numel() == (int64_t)a.C * a.B * 4 * AFL_HAR_MASK_WORDS(a.Lp), "mask must be [C*B*4, ",
+              AFL_HAR_MASK_WORDS(a.Lp), "]");
+  a.mask = (unsigned long long*)mask->data_ptr<int64_t>();
+}
+
 void har_attn_fwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse2, int64_t B, int64_t L,
-                  c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+                  c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p,
+                  c10::optional<torch::Tensor> mask) {
   AflHarAttn a = attn_args(qkv, lse2, B, L, seeds, stepctl, layer, p);
+  attn_mask(a, mask);
   rows64(o, a.C, B * L, "o");
   a.o = bf(o, "o");
   ok(afl_har_attn_fwd(a, cur()), "har_attn_fwd");
@@ -139,8 +151,9 @@ void har_attn_fwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor lse2, int64_
 
 void har_attn_bwd(torch::Tensor qkv, torch::Tensor lse2, torch::Tensor dout, torch::Tensor delta, torch::Tensor dqkv,
                   int64_t B, int64_t L, c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl,
-                  int64_t layer, double p) {
+                  int64_t layer, double p, c10::optional<torch::Tensor> mask) {
   AflHarAttn a = attn_args(qkv, lse2, B, L, seeds, stepctl, layer, p);
+  attn_mask(a, mask);
   rows64(dout, a.C, B * L, "dout");
   headmajor(dqkv, a.C, B, a.Lp, "dqkv");
   TORCH_CHECK(delta.numel() == (int64_t)a.C * B * 4 * a.Lp, "delta must be [C*B*4, Lp]");
@@ -223,8 +236,12 @@ void afl_register_har(pybind11::module& m) {
   m.def("har_pool", &har_pool);
   m.def("har_qkv", &har_qkv);
   m.def("har_post", &har_post);
-  m.def("har_attn_fwd", &har_attn_fwd);
-  m.def("har_attn_bwd", &har_attn_bwd);
+  m.def("har_attn_fwd", &har_attn_fwd, py::arg("qkv"), py::arg("o"), py::arg("lse2"), py::arg("B"), py::arg("L"),
+        py::arg("seeds"), py::arg("stepctl"), py::arg("layer"), py::arg("p"), py::arg("mask") = py::none());
+  m.def("har_attn_bwd", &har_attn_bwd, py::arg("qkv"), py::arg("lse2"), py::arg("dout"), py::arg("delta"),
+        py::arg("dqkv"), py::arg("B"), py::arg("L"), py::arg("seeds"), py::arg("stepctl"), py::arg("layer"),
+        py::arg("p"), py::arg("mask") = py::none());
+  m.def("har_mask_words", [](int64_t Lp) { return (int64_t)AFL_HAR_MASK_WORDS(Lp); });
   m.def("har_post_bwd", &har_post_bwd);
   m.def("har_qkv_bwd", &har_qkv_bwd);
   m.def("har_reduce", &har_reduce);

@@ -369,9 +369,13 @@ struct AflHarAttn {
   const unsigned short* dout;  // [C][B*L][64] (bwd)
   const float* delta;          // [C*B*4][Lp] (bwd)
   unsigned short* dqkv;        // [C*B*4][3][Lp][16] (bwd): d(q projection) (x 1/4 folded in), dk, dv
+  unsigned long long* mask;    // [C*B*4][AFL_HAR_MASK_WORDS(Lp)] probability-dropout keep words: written by the
+                               // forward, read by both backward kernels (dropout only)
   int C, B, L, Lp;
   AflDrop drop;
 };
+// keep words per (client, sample, head): [query tile Lp/16][key chunk Lp/64][t 4][e 4], bit = lane of the forward
+#define AFL_HAR_MASK_WORDS(Lp) ((long)((Lp) / 16) * ((Lp) / 64) * 16)
 #define AFL_HAR_POST_NG (64 * 64 + 256 * 64 + 64 * 256 + 640)
 #define AFL_HAR_QKV_NG (192 * 64 + 192)
 int afl_har_stem(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,

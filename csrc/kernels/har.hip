@@ -27,6 +27,7 @@
 // attention probabilities use a row hash x column-pair hash mix (attn_mix, masks.keep_rc) that costs a
 // fraction of a full hash per probability.  The layer program on CPU (ops/layers.py composites, attention
 // scheme "rc") is the oracle of these kernels.
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 #include "onchip.h"
@@ -370,8 +371,9 @@ __device__ __forceinline__ float sum_x16_x32(float a) {
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
 // Probability dropout (masks.keep_rc): a strong hash per row (attn_hr) and per column pair (attn_hc, an LDS
-// table per workgroup) combined by xor and two multiply-xorshift rounds; 16 bits per column.  Kept
-// probabilities are NOT scaled here: 1/(1-p) is folded into O (forward), dV and dP (backward).
+// table per workgroup) combined by xor and two multiply-xorshift rounds; 16 bits per column.  Only the forward
+// hashes: it stores the flags as 64-bit ballot words (AflHarAttn::mask) that the backward kernels read back.
+// Kept probabilities are NOT scaled here: 1/(1-p) is folded into O (forward), dV and dP (backward).
 __device__ __forceinline__ uint32_t attn_hr(uint32_t key, uint32_t layer, uint32_t r) {
   return afl_hash4(key, layer, r, 0xFFFFFFFFu);
 }
@@ -416,13 +418,16 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
   const long orow0 = (long)c * a.B * L + (long)b * L;
+  const int nkc = Lp >> 6;
+  uint32_t* mrow = DROP ? (uint32_t*)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp)) : nullptr;
   for (int q0 = wave * 16; q0 < Lp; q0 += 16 * AT_WAVES) {
     const int q = q0 + li;
     const s4v qf = *(const s4v*)(blk + (long)q * DH + 4 * g);
     const uint32_t hr = DROP ? attn_hr(key, a.drop.layer, drow0 + q) : 0u;
     float m = -INFINITY, l = 0.f;
     f4v o = Z4;
-    for (int kt = 0; kt < Lp; kt += 64) {
+    // one 64-key chunk; only the last (partial) chunk masks keys >= L (peeled: no per-chunk compare/select)
+    auto chunk = [&](int kt, auto tail) {
       float s[16];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -430,7 +435,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[4 * t + e] = st[e];  // (q carries 1/4 * log2 e: already log2-domain)
       }
-      if (kt + 64 > L) {
+      if constexpr (decltype(tail)::value) {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
           if (kt + 16 * (j >> 2) + 4 * g + (j & 3) >= L) s[j] = -INFINITY;
@@ -447,20 +452,32 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
         ps += pd[j];
       }
       if (DROP) {
+        // keep word (t, e) = ballot of the flags of keys kt + 16t + 4g + e over the wave (bit = lane): lanes 0..31
+        // of mw collect the chunk's 16 words, stored for both backward kernels (no hashing there)
+        uint32_t mw = 0u;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           bool k4[4];
           keep4(HC, hr, kt + 16 * t + 4 * g, a.drop.thr16, k4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) pd[4 * t + e] = k4[e] ? pd[4 * t + e] : 0.f;
+          for (int e = 0; e < 4; ++e) {
+            pd[4 * t + e] = k4[e] ? pd[4 * t + e] : 0.f;
+            const uint64_t bw = __builtin_amdgcn_ballot_w64(k4[e]);
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(mw) : "s"((uint32_t)bw), "n"(2 * (4 * t + e)));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(mw) : "s"((uint32_t)(bw >> 32)), "n"(2 * (4 * t + e) + 1));
+          }
         }
+        if (lane < 32) mrow[(long)((q0 >> 4) * nkc + (kt >> 6)) * 32 + lane] = mw;
       }
       l = l * alpha + sum_x16_x32(ps);
       m = mn;
       o *= alpha;
       o = mfma32(trfrag(Vi, kt + 4 * g, kt + 16 + 4 * g, lane), pack8f(pd), o);
       o = mfma32(trfrag(Vi, kt + 32 + 4 * g, kt + 48 + 4 * g, lane), pack8f(pd + 8), o);
-    }
+    };
+    int kt = 0;
+    for (; kt + 64 <= L; kt += 64) chunk(kt, std::false_type{});
+    if (kt < L) chunk(kt, std::true_type{});
     if (q < L) {
       const float inv = (DROP ? a.drop.inv_keep : 1.f) / l;
       *(u32x2v*)(a.o + (orow0 + q) * D + h * DH + 4 * g) = u32x2v{pk2(o[0] * inv, o[1] * inv), pk2(o[2] * inv, o[3] * inv)};
@@ -470,11 +487,8 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
 }
 
 // ---- dK / dV: each wave owns 16 keys and sweeps the queries (32 per step) ----
-// A lane holds one key (lane & 15) x 4 queries; a dropout hash covers a key PAIR, so lanes 2j and 2j + 1
-// each hash two of the four rows and swap the results (DPP quad_perm [1, 0, 3, 2]): 2 hashes per 4 elements.
-__device__ __forceinline__ uint32_t swap1(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
-}
+// A lane holds one key (lane & 15) x 4 queries.  The dropout flags are the forward's keep words (no hashing
+// in either backward kernel): one dword load per lane and query tile, one bit per element.
 template <bool DROP>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
@@ -483,31 +497,43 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
   uchar* Di = smem + Lp * 32;
   LDS_AS float* LS = (LDS_AS float*)(smem + 2 * Lp * 32);
   LDS_AS float* DL = LS + Lp;
-  LDS_AS uint32_t* HR = (LDS_AS uint32_t*)(DL + Lp);  // per-query row hashes of the dropout mask
   const int cbh = blockIdx.x, h = cbh % NH, cb = cbh / NH, c = cb / a.B, b = cb - c * a.B;
   const u16* blk = a.qkv + (long)cbh * 3 * Lp * DH;
   const long orow0 = (long)c * a.B * L + (long)b * L;
-  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
-  const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
   stage16(Qi, blk, DH, Lp, Lp);
   stage16(Di, a.dout + orow0 * D + h * DH, D, Lp, L);
   for (int e = threadIdx.x; e < Lp; e += blockDim.x) {
     LS[e] = a.lse2[(long)cbh * Lp + e];
     DL[e] = e < L ? a.delta[(long)cbh * Lp + e] : 0.f;
-    if (DROP) HR[e] = attn_hr(key, a.drop.layer, drow0 + e);
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15, odd = lane & 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const float ik = DROP ? a.drop.inv_keep : 1.f;
+  const long wq = (long)(Lp >> 6) * 16;  // keep words per query tile
   for (int k0 = wave * 16; k0 < Lp; k0 += 16 * AT_WAVES) {
     const int kk = k0 + li;
-    const bool kok = kk < L;
     const s4v kf = *(const s4v*)(blk + (long)(Lp + kk) * DH + 4 * g);
     const s4v vf = *(const s4v*)(blk + (long)(2 * Lp + kk) * DH + 4 * g);
-    const uint32_t hc = DROP ? attn_hc(key, a.drop.layer, (uint32_t)(kk >> 1)) : 0u;
+    // the forward's keep word of key kk for query tile T: [T][kk >> 6][(kk >> 4) & 3][kk & 3]; the flags of
+    // queries 16T + 4g + e sit at bits 16((kk >> 2) & 3) + 4g + e: one dword per (lane, tile), bit e of a nibble
+    const int sh = 16 * ((kk >> 2) & 3) + 4 * g;
+    const uint32_t* mw = DROP ? (const uint32_t*)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp) + (kk >> 6) * 16 +
+                                                  ((kk >> 4) & 3) * 4 + (kk & 3)) + (sh >> 5)
+                              : nullptr;
     f4v dkT = Z4, dvT = Z4;
+    // keep dwords of the two query tiles of a step, loaded one step ahead
+    uint32_t wn[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (DROP) {
+      wn[0] = mw[0];
+      wn[1] = mw[wq * 2];
+    }
     for (int q0 = 0; q0 < L; q0 += 32) {
       float pdv[8], dsv[8];
+      const uint32_t wc[2] = {wn[0], wn[1]};
+      if (DROP && q0 + 32 < L) {
+        wn[0] = mw[(long)((q0 + 32) >> 4) * wq * 2];
+        wn[1] = mw[(long)((q0 + 48) >> 4) * wq * 2];
+      }
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
         const int qb = q0 + 16 * qs;
@@ -515,28 +541,22 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
         const f4v dp = mfma16(lds4(Di, qb + li, g), vf, Z4);
         const f4v l4 = *(const LDS_AS f4v*)(LS + qb + 4 * g);
         const f4v d4 = *(const LDS_AS f4v*)(DL + qb + 4 * g);
-        bool kp[4] = {true, true, true, true};
-        if (DROP) {  // this lane mixes two of the four rows, its pair partner the other two (DPP swap)
-          const u32x2v hr = *(const LDS_AS u32x2v*)(HR + qb + 4 * g + 2 * odd);
-          const uint32_t ha = attn_mix(hr[0], hc), hb = attn_mix(hr[1], hc);
-          const uint32_t pa = swap1(ha), pb = swap1(hb);
-          const uint32_t hx[4] = {odd ? pa : ha, odd ? pb : hb, odd ? ha : pa, odd ? hb : pb};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) kp[e] = ((hx[e] >> (16 * odd)) & 0xFFFFu) >= a.drop.thr16;
-        }
+        const uint32_t wd = wc[qs];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pe = __builtin_amdgcn_exp2f(s[e] - l4[e]);
-          const float p = kok ? pe : 0.f;
-          pdv[4 * qs + e] = kp[e] ? p : 0.f;  // (x 1/(1-p) on dV at the end)
-          dsv[4 * qs + e] = p * fmaf(kp[e] ? dp[e] : 0.f, ik, -d4[e]);
+          // (keys >= L need no mask: a lane's values only reach its own key's dK / dV column, never stored)
+          const float p = __builtin_amdgcn_exp2f(s[e] - l4[e]);
+          // keep flag -> all-ones / zero word (sign-extended one-bit field)
+          const uint32_t km = DROP ? (uint32_t)__builtin_amdgcn_sbfe((int)wd, (sh & 31) + e, 1) : 0xFFFFFFFFu;
+          pdv[4 * qs + e] = __uint_as_float(__float_as_uint(p) & km);  // (x 1/(1-p) on dV at the end)
+          dsv[4 * qs + e] = p * fmaf(__uint_as_float(__float_as_uint(dp[e]) & km), ik, -d4[e]);
         }
       }
       // dV^T[d][key] += dO^T[d][q] Pd[q][key] ; dK^T[d][key] += Q_s^T[d][q] dS[q][key] (query order permuted)
       dvT = mfma32(trfrag(Di, q0 + 4 * g, q0 + 16 + 4 * g, lane), pack8f(pdv), dvT);
       dkT = mfma32(trfrag(Qi, q0 + 4 * g, q0 + 16 + 4 * g, lane), pack8f(dsv), dkT);
     }
-    if (kok) {  // lane: d = 4g + e of key kk
+    if (kk < L) {  // lane: d = 4g + e of key kk
       u16* dk = a.dqkv + ((long)cbh * 3 + 1) * Lp * DH + (long)kk * DH + 4 * g;
       u16* dv = a.dqkv + ((long)cbh * 3 + 2) * Lp * DH + (long)kk * DH + 4 * g;
       constexpr float iq = 1.f / LOG2E;  // dK = dS^T (q / 4) and the image holds q log2(e) / 4
@@ -547,55 +567,70 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
 }
 
 // ---- dQ: each wave owns 16 queries and sweeps the keys (recomputing S and dP; no atomics) ----
+// x where bit `lane` of the wave-uniform 64-bit keep word m is set, else 0 (one v_cndmask on an SGPR-pair mask)
+__device__ __forceinline__ float keep_sel(uint64_t m, float x) {
+  float r;
+  asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
+  return r;
+}
 template <bool DROP>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
   const int Lp = a.Lp, L = a.L;
   uchar* Ki = smem;
   uchar* Vi = smem + Lp * 32;
-  LDS_AS uint32_t* HC = (LDS_AS uint32_t*)(smem + 2 * Lp * 32);
   const int cbh = blockIdx.x, h = cbh % NH, cb = cbh / NH, c = cb / a.B, b = cb - c * a.B;
   const u16* blk = a.qkv + (long)cbh * 3 * Lp * DH;
   const long orow0 = (long)c * a.B * L + (long)b * L;
-  const uint32_t key = DROP ? dkey(a.drop, c) : 0u;
   stage16(Ki, blk + (long)Lp * DH, DH, Lp, Lp);
   stage16(Vi, blk + 2L * Lp * DH, DH, Lp, Lp);
-  if (DROP) fill_hc(HC, Lp / 2, key, a.drop.layer);
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const uint32_t drow0 = (uint32_t)((b * NH + h) * L);
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float ik = DROP ? a.drop.inv_keep : 1.f;
+  const int nkc = Lp >> 6;
+  // (constant address space: wave-uniform addresses become scalar loads, so the words land in SGPR pairs; the
+  // words are read-only here and the dispatch's acquire fence makes the forward's stores visible to the K$)
+  typedef const __attribute__((address_space(4))) uint64_t ku64;
+  ku64* mblk = DROP ? (ku64*)(uintptr_t)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp)) : nullptr;
   for (int q0 = wave * 16; q0 < L; q0 += 16 * AT_WAVES) {
     const int q = q0 + li;
     const bool qok = q < L;
-    const uint32_t hr = DROP ? attn_hr(key, a.drop.layer, drow0 + q) : 0u;
     const s4v qf = *(const s4v*)(blk + (long)q * DH + 4 * g);
     const s4v df = qok ? *(const s4v*)(a.dout + (orow0 + q) * D + h * DH + 4 * g) : s4v{0, 0, 0, 0};
     const float ls = a.lse2[(long)cbh * Lp + q];
     const float dl = qok ? a.delta[(long)cbh * Lp + q] : 0.f;
+    // the forward's words of this query tile: element j of the 32-key step at kt is word 4((kt & 63) >> 4) + j of
+    // chunk kt >> 6, bit = lane (same lane <-> (query, key) map as the forward)
+    ku64* mt = DROP ? mblk + (long)(q0 >> 4) * nkc * 16 : nullptr;
     f4v acc = Z4;
-    for (int kt = 0; kt < L; kt += 32) {
+    auto step = [&](int kt, auto tail) {
       const f4v s0 = mfma16(lds4(Ki, kt + li, g), qf, Z4);
       const f4v s1 = mfma16(lds4(Ki, kt + 16 + li, g), qf, Z4);
       const f4v p0 = mfma16(lds4(Vi, kt + li, g), df, Z4);
       const f4v p1 = mfma16(lds4(Vi, kt + 16 + li, g), df, Z4);
-      float ds[8];
-      bool kp[8] = {true, true, true, true, true, true, true, true};
+      uint64_t mw[8];
       if (DROP) {
-        keep4(HC, hr, kt + 4 * g, a.drop.thr16, kp);
-        keep4(HC, hr, kt + 16 + 4 * g, a.drop.thr16, kp + 4);
+        ku64* w = mt + (kt >> 6) * 16 + ((kt & 63) >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mw[j] = w[j];
       }
+      float ds[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int kk = kt + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
         const float sv = j < 4 ? s0[j] : s1[j - 4];
-        const float dp = j < 4 ? p0[j] : p1[j - 4];
-        const float pe = __builtin_amdgcn_exp2f(sv - ls);
-        const float p = kk < L ? pe : 0.f;
-        ds[j] = p * fmaf(kp[j] ? dp : 0.f, ik, -dl);
+        float dp = j < 4 ? p0[j] : p1[j - 4];
+        if (DROP) dp = keep_sel(mw[j], dp);
+        float p = __builtin_amdgcn_exp2f(sv - ls);
+        if constexpr (decltype(tail)::value) p = kk < L ? p : 0.f;  // keys >= L: last step only
+        ds[j] = p * fmaf(dp, ik, -dl);
       }
       acc = mfma32(trfrag(Ki, kt + 4 * g, kt + 16 + 4 * g, lane), pack8f(ds), acc);
-    }
+    };
+    int kt = 0;
+    for (; kt + 32 <= L; kt += 32) step(kt, std::false_type{});
+    if (kt < L) step(kt, std::true_type{});
     if (qok) {  // d(q projection) = 1/4 d(q_s)
       u16* dq = a.dqkv + (long)cbh * 3 * Lp * DH + (long)q * DH + 4 * g;
       *(u32x2v*)dq = u32x2v{pk2(acc[0] * 0.25f, acc[1] * 0.25f), pk2(acc[2] * 0.25f, acc[3] * 0.25f)};
@@ -1101,6 +1136,7 @@ int afl_har_qkv(const AflHarQkv& a, hipStream_t s) {
 
 int afl_har_attn_fwd(const AflHarAttn& a, hipStream_t s) {
   if (a.Lp % 64 || a.Lp < a.L || a.Lp > 1024) return (int)hipErrorInvalidValue;
+  if (a.drop.thr16 && !a.mask) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 2;  // K, V images + the column-pair hash table
   if (a.drop.thr16)
     hipLaunchKernelGGL(k_har_attn_fwd<true>, dim3(a.C * a.B * NH), dim3(AT_NT), lds, s, a);
@@ -1111,7 +1147,8 @@ int afl_har_attn_fwd(const AflHarAttn& a, hipStream_t s) {
 
 int afl_har_attn_bwd(const AflHarAttn& a, hipStream_t s) {
   if (a.Lp % 64 || a.Lp < a.L || a.Lp > 1024) return (int)hipErrorInvalidValue;
-  const size_t kv = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 12, dq = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 2;
+  if (a.drop.thr16 && !a.mask) return (int)hipErrorInvalidValue;
+  const size_t kv = (size_t)a.Lp * 32 * 2 + (size_t)a.Lp * 8, dq = (size_t)a.Lp * 32 * 2;
   const dim3 grid(a.C * a.B * NH);
   if (a.drop.thr16) {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<true>, grid, dim3(AT_NT), kv, s, a);

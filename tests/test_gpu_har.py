@@ -49,7 +49,8 @@ def test_har_attention_matches_composite(gpu, L, p):
     qkv = qkv.reshape(C, B * L, 192)
     o = torch.zeros(C, B * L, 64, dtype=torch.bfloat16, device=gpu)
     lse2 = torch.zeros(C * B * 4, Lp, device=gpu)
-    nat.har_attn_fwd(hm, o, lse2, B, L, ctl.seeds if p else None, ctl.stepctl if p else None, 2, p)
+    mask = torch.zeros(C * B * 4, nat.har_mask_words(Lp), dtype=torch.int64, device=gpu) if p else None
+    nat.har_attn_fwd(hm, o, lse2, B, L, ctl.seeds if p else None, ctl.stepctl if p else None, 2, p, mask)
     cc = _ctl(C, "cpu")
     ref_o, ref_lse = Lx._attn_ref(qkv, B, L, cc, 2, p, "rc")
     _close(o, ref_o, 2e-2, "O")
@@ -61,7 +62,7 @@ def test_har_attention_matches_composite(gpu, L, p):
     delta[:, :L] = dd
     dq = torch.zeros_like(hm)
     nat.har_attn_bwd(hm, lse2, dout.to(gpu).to(torch.bfloat16), delta, dq, B, L, ctl.seeds if p else None,
-                     ctl.stepctl if p else None, 2, p)
+                     ctl.stepctl if p else None, 2, p, mask)
     x = qkv.clone().requires_grad_(True)
     with torch.enable_grad():
         out, _ = Lx._attn_ref(x, B, L, cc, 2, p, "rc")
@@ -70,3 +71,38 @@ def test_har_attention_matches_composite(gpu, L, p):
     got = dq[:, :, :L].float().cpu()
     for w, n in enumerate(["dq", "dk", "dv"]):
         _close(got[:, w], gq[:, w], 3e-2, n)
+
+
+def _decode_keep_words(words, L, Lp):
+    """[Lp/16, Lp/64, 4, 4] int64 ballot words of one (client, sample, head) -> bool [L, L] (query, key):
+    word (T, c, t, e) bit 16 g + i = keep(query 16 T + i, key 64 c + 16 t + 4 g + e)."""
+    w = words.reshape(Lp // 16, Lp // 64, 4, 4).numpy().view(np.uint64)
+    bits = ((w[..., None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)  # [T, c, t, e, 64]
+    bits = bits.reshape(Lp // 16, Lp // 64, 4, 4, 4, 16)  # [T, c, t, e, g, i]
+    keep = bits.transpose(0, 5, 1, 2, 4, 3).reshape(Lp, Lp)  # [(T, i), (c, t, g, e)]
+    return keep[:L, :L]
+
+
+def test_har_attention_keep_words_match_keep_rc(gpu):
+    """The forward's stored dropout flags are exactly masks.keep_rc (the draws both backward kernels use)."""
+    from attackfl_amd.ops import masks
+
+    C, B, L, p = 2, 2, 200, 0.1
+    Lp = (L + 63) // 64 * 64
+    nat = native()
+    ctl = _ctl(C, gpu)
+    qkv = torch.randn(C, B * L, 192, generator=torch.Generator().manual_seed(1))
+    hm = _headmajor(qkv.to(gpu), B, L, Lp)
+    o = torch.zeros(C, B * L, 64, dtype=torch.bfloat16, device=gpu)
+    lse2 = torch.zeros(C * B * 4, Lp, device=gpu)
+    mask = torch.zeros(C * B * 4, nat.har_mask_words(Lp), dtype=torch.int64, device=gpu)
+    nat.har_attn_fwd(hm, o, lse2, B, L, ctl.seeds, ctl.stepctl, 12, p, mask)
+    cc = _ctl(C, "cpu")
+    words = mask.cpu()
+    for cbh in (0, 5, C * B * 4 - 1):
+        c, bh = divmod(cbh, B * 4)
+        rows = (bh * L + np.arange(L))[:, None]
+        ref = masks.keep_rc(cc.key(c), 12, rows, np.arange(L)[None, :], p).numpy()
+        got = _decode_keep_words(words[cbh], L, Lp)
+        assert (got == ref).all(), (cbh, int((got != ref).sum()))
+        assert abs(got.mean() - 0.9) < 0.01
