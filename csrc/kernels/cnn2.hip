@@ -945,7 +945,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 }
 
 // ============================================================================================== head
-// LDS map (bytes); U = f2s | f3f | d3s, reused as the d1 staging tile once the backward is past them
+// LDS map (bytes)
 constexpr int H_L1 = 136, H_L2 = 72, H_L3 = 40, H_F3 = 36;  // f3 rows 16-B aligned
 constexpr int H_F1S = 0;
 constexpr int H_W2S = H_F1S + 128 * H_L1 * 2;
@@ -953,9 +953,7 @@ constexpr int H_W3S = H_W2S + 64 * H_L1 * 2;
 constexpr int H_F2S = H_W3S + 32 * H_L2 * 2;
 constexpr int H_F3F = H_F2S + 128 * H_L2 * 2;
 constexpr int H_D3S = H_F3F + 128 * H_F3 * 4;
-constexpr int H_D1S = H_F2S;  // [128][136] bf16
 constexpr int H_D2S = H_D3S + 128 * H_L3 * 2;
-static_assert(H_D1S + 128 * H_L1 * 2 <= H_D2S, "d1 staging fits U");
 constexpr int H_DZ = H_D2S + 128 * H_L2 * 2;
 constexpr int H_RED = H_DZ + 128 * 4;
 constexpr int H_WO = H_RED + 8 * 4;
@@ -988,7 +986,6 @@ __device__ __forceinline__ void head(const Ctx& x) {
   LDS_AS float* f3f = lf(S, H_F3F);
   LDS_AS unsigned short* d3s = lu16(S, H_D3S);
   LDS_AS unsigned short* d2s = lu16(S, H_D2S);
-  LDS_AS unsigned short* d1s = lu16(S, H_D1S);
   LDS_AS float* dz = lf(S, H_DZ);
   LDS_AS float* red = lf(S, H_RED);
   LDS_AS float* wos = lf(S, H_WO);
@@ -1042,37 +1039,38 @@ __device__ __forceinline__ void head(const Ctx& x) {
     if (bs < min_bs || bs < 1) continue;
     const int ep = a.epoch[(long)s * a.C + c], nbc = a.nb[c];
     const int* idxs = a.idx + ((long)s * a.C + c) * B;
-    const int yb = min(tid & 127, B - 1);
+    // Every phase up to the d1 hand-off is ROW-LOCAL: wave w owns batch rows m0 = 16 w .. m0 + 15 from the z1 sum
+    // to its d1 rows, so the critical path has ONE workgroup barrier (the batch loss, for the NaN abort); the
+    // cross-row sums (bias / output-layer gradients, dW2, dW3) run after the hand-off, under the towers' backward.
+    const int m0 = wave * 16;
+    const int yb = min(m0 + li, B - 1);
     const int yrow = idxs[yb];
     const float yv = yrow >= 0 ? a.rows[(long)yrow * 24 + 23] : 0.f;
     if (!wait_ge(*&x, CT_F, (uint32_t)(24 * (kact + 1)), H_FLAG)) break;
     REOPQ();
     stamp(x, kact, 0);
-    // z1 = z1p_vitals + z1p_labs (+ b1, ReLU) -> f1s; thread: row b = (tid + 512 q) >> 5, columns i1 .. i1 + 3
-    const int i1 = 4 * (tid & 31);
+    // z1 = z1p_vitals + z1p_labs (+ b1, ReLU) -> f1s rows of this wave; lane: row m0 + (lane >> 2), columns
+    // 16 q + 4 (lane & 3) .. +3
     {
+      const int b = m0 + (lane >> 2), i0 = 4 * (lane & 3);
       f4v za[8], zb[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int b = (tid + NTH * q) >> 5;
-        za[q] = ld16f(x.rw, WS_Z1P + (b * 128 + i1) * 4);
-        zb[q] = ld16f(x.rw, WS_Z1P + ((128 + b) * 128 + i1) * 4);
+        za[q] = ld16f(x.rw, WS_Z1P + (b * 128 + 16 * q + i0) * 4);
+        zb[q] = ld16f(x.rw, WS_Z1P + ((128 + b) * 128 + 16 * q + i0) * 4);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int b = (tid + NTH * q) >> 5;
-        LDS_AS unsigned short* d = f1s + b * H_L1 + i1;
+        const int i1 = 16 * q + i0;
+        const f4v bb = *(const LDS_AS f4v*)(bias + i1);
         float v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = b < B ? relu((za[q][k] + zb[q][k]) + bias[i1 + k]) : 0.f;
-        *(LDS_AS u32x2v*)d = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
+        for (int k = 0; k < 4; ++k) v[k] = b < B ? relu((za[q][k] + zb[q][k]) + bb[k]) : 0.f;
+        *(LDS_AS u32x2v*)(f1s + b * H_L1 + i1) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
       }
     }
-    SYNC();
-    // fc2 (transposed, D[n][m] = W2 . f1^T: a lane ends with 4 consecutive features of one row -> one 8-byte
-    // store); wave -> m-tile w, n-tiles 0..3
+    // fc2 (transposed, D[n][m] = W2 . f1^T: a lane ends with 4 consecutive features of one row)
     {
-      const int m0 = wave * 16;
       f4v acc[4] = {Z4, Z4, Z4, Z4};
 #pragma unroll
       for (int k0 = 0; k0 < 128; k0 += 32) {
@@ -1087,10 +1085,8 @@ __device__ __forceinline__ void head(const Ctx& x) {
             u32x2v{pk2(relu(acc[j][0] + bv[0]), relu(acc[j][1] + bv[1])), pk2(relu(acc[j][2] + bv[2]), relu(acc[j][3] + bv[3]))};
       }
     }
-    SYNC();
     // fc3 (transposed: one 16-byte store of 4 features per lane)
     {
-      const int m0 = wave * 16;
       f4v acc[2] = {Z4, Z4};
 #pragma unroll
       for (int k0 = 0; k0 < 64; k0 += 32) {
@@ -1105,29 +1101,84 @@ __device__ __forceinline__ void head(const Ctx& x) {
             f4v{relu(acc[j][0] + bv[0]), relu(acc[j][1] + bv[1]), relu(acc[j][2] + bv[2]), relu(acc[j][3] + bv[3])};
       }
     }
-    SYNC();
-    // output logit + sigmoid-BCE (k_bce arithmetic)
-    float zb = 0.f, lb = 0.f;
-    if (tid < 128) {
-      float acc = bias[224];
+    // output logit (lane: row m0 + li, features 8 g .. 8 g + 7, summed over the 4 lane groups) + sigmoid-BCE
+    // (k_bce arithmetic); d3 = dz wo^T * relu'(f3) for the same 8 features
+    const int row = m0 + li;
+    float gz = 0.f, lb = 0.f;
+    {
+      const f4v f0 = *(const LDS_AS f4v*)(f3f + row * H_F3 + 8 * g), f1 = *(const LDS_AS f4v*)(f3f + row * H_F3 + 8 * g + 4);
+      const f4v w0 = *(const LDS_AS f4v*)(wos + 8 * g), w1 = *(const LDS_AS f4v*)(wos + 8 * g + 4);
+      float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; j += 4) {
-        const f4v fv = *(const LDS_AS f4v*)(f3f + tid * H_F3 + j);
-        const f4v wv = *(const LDS_AS f4v*)(wos + j);
+      for (int k = 0; k < 4; ++k) acc += f0[k] * w0[k];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc += fv[k] * wv[k];
+      for (int k = 0; k < 4; ++k) acc += f1[k] * w1[k];
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      const float zl = bias[224] + acc;
+      if (row < bs) {
+        const float p = 1.f / (1.f + expf(-zl));
+        if (g == 0) {
+          lb = -(yv * fmaxf(logf(p), -100.f) + (1.f - yv) * fmaxf(log1pf(-p), -100.f));
+          if (p != p) lb = p;
+        }
+        const float w = p * (1.f - p);
+        gz = (p - yv) / fmaxf(w, 1e-12f) * w / (float)bs;
       }
-      zb = acc;
-      if (tid < bs) {
-        const float p = 1.f / (1.f + expf(-zb));
-        lb = -(yv * fmaxf(logf(p), -100.f) + (1.f - yv) * fmaxf(log1pf(-p), -100.f));
-        if (p != p) lb = p;
-      }
+      if (g == 0) dz[row] = gz;
+      const float f[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
+      const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+      uint32_t d3[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        d3[k] = pk2(f[2 * k] > 0.f ? gz * wv[2 * k] : 0.f, f[2 * k + 1] > 0.f ? gz * wv[2 * k + 1] : 0.f);
+      *(LDS_AS u32x4*)(d3s + row * H_L3 + 8 * g) = u32x4{d3[0], d3[1], d3[2], d3[3]};
     }
     lb = wsum(lb);
     if (lane == 0) red[wave] = lb;
-    SYNC();
-    const float loss = ((red[0] + red[1]) + (red[2] + red[3])) / (float)max(bs, 1);
+    // d2 = d3 . W3 * relu'(f2) (rows of this wave); gb2 partials per wave
+    {
+      const s8v af = rfrag(S + H_D3S, H_L3, m0, 0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4v acc = mfma(af, cfrag(S + H_W3S, H_L2, 0, 16 * j, lane), Z4);
+        const int n = 16 * j + li;
+        float cs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + 4 * g + e;
+          const unsigned short fb = f2s[m * H_L2 + n];
+          const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
+          d2s[m * H_L2 + n] = bfu(v);
+          cs += v;
+        }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        if (lane < 16) gbw[wave * 192 + n] = cs;
+      }
+    }
+    // d1^T = W2^T . d2^T * relu'(f1) (transposed: 4 consecutive features of one row per lane -> one 8-byte
+    // write-through store each, no LDS staging), held until the batch loss is known
+    uint32_t d1p[16];
+    {
+      const s8v b0 = rfrag(S + H_D2S, H_L2, m0, 0, lane), b1 = rfrag(S + H_D2S, H_L2, m0, 32, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f4v acc = mfma(cfrag(S + H_W2S, H_L1, 0, 16 * j, lane), b0, Z4);
+        acc = mfma(cfrag(S + H_W2S, H_L1, 32, 16 * j, lane), b1, acc);
+        const u32x2v fb = *(const LDS_AS u32x2v*)(f1s + row * H_L1 + 16 * j + 4 * g);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t h = (fb[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+          v[e] = (h != 0 && !(h & 0x8000u)) ? acc[e] : 0.f;
+        }
+        d1p[2 * j] = pk2(v[0], v[1]);
+        d1p[2 * j + 1] = pk2(v[2], v[3]);
+      }
+    }
+    SYNC();  // the only barrier before the hand-off: every wave's loss partial
+    const float loss = ((red[0] + red[1]) + (red[2] + red[3]) + ((red[4] + red[5]) + (red[6] + red[7]))) / (float)max(bs, 1);
     const bool nan = a.nan_abort && (loss != loss);
     if (nan) {  // status only: no update this step, the client's round ends (towers read the status)
       if (tid == 0) {
@@ -1139,27 +1190,43 @@ __device__ __forceinline__ void head(const Ctx& x) {
         for (int w = 0; w < 8; ++w) __hip_atomic_fetch_add(x.ctr + (CT_HW + w) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
-    if (tid < 128) {
-      float gz = 0.f;
-      if (tid < bs) {
-        const float p = 1.f / (1.f + expf(-zb));
-        const float w = p * (1.f - p);
-        gz = (p - yv) / fmaxf(w, 1e-12f) * w / (float)bs;
-      }
-      dz[tid] = gz;
-    }
     if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
-    SYNC();
-    // d3 = dz wo^T * relu'(f3); output-layer / fc3-bias gradient partials per wave
+    // per-wave hand-off: this wave's 16 d1 rows + its status slot, drained, then its counter — the tower
+    // workgroups of those rows start without waiting for the other waves
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {  // (row b, 4 features) per thread step: one 16-byte read, one 8-byte store
-      const int e = tid + NTH * it, b = e >> 3, j = 4 * (e & 7);
-      const f4v fv = *(const LDS_AS f4v*)(f3f + b * H_F3 + j);
-      const f4v wv = *(const LDS_AS f4v*)(wos + j);
-      const float d = dz[b];
-      *(LDS_AS u32x2v*)(d3s + b * H_L3 + j) = u32x2v{pk2(fv[0] > 0.f ? d * wv[0] : 0.f, fv[1] > 0.f ? d * wv[1] : 0.f),
-                                                    pk2(fv[2] > 0.f ? d * wv[2] : 0.f, fv[3] > 0.f ? d * wv[3] : 0.f)};
+    for (int j = 0; j < 8; ++j) {
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{d1p[2 * j], d1p[2 * j + 1]}, x.rw,
+                                            WS_D1 + (row * 128 + 16 * j + 4 * g) * 2, 0, 16);
+      sguard();
     }
+    if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
+    drain();
+    if (lane == 0) __hip_atomic_fetch_add(x.ctr + (CT_HW + wave) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    arrive(x, CT_H);
+    REOPQ();
+    stamp(x, kact, 1);
+    // ---- off the critical path: gb1 (d1 again in the row-major layout for its column sums), output-layer /
+    // fc3 / fc2 bias sums, dW3
+    {
+      const s8v a0 = rfrag(S + H_D2S, H_L2, m0, 0, lane), a1 = rfrag(S + H_D2S, H_L2, m0, 32, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f4v acc = mfma(a0, cfrag(S + H_W2S, H_L1, 0, 16 * j, lane), Z4);
+        acc = mfma(a1, cfrag(S + H_W2S, H_L1, 32, 16 * j, lane), acc);
+        const int n = 16 * j + li;
+        float cs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + 4 * g + e;
+          const unsigned short fb = f1s[m * H_L1 + n];
+          cs += (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
+        }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        if (lane < 16) gbw[wave * 192 + 64 + n] = cs;
+      }
+    }
+    SYNC();
     {
       const int j = tid & 31, r0 = 8 * (tid >> 5);
       float sa = 0.f, sw = 0.f, sz = 0.f;
@@ -1180,6 +1247,15 @@ __device__ __forceinline__ void head(const Ctx& x) {
         if (j == 0) red3w[wave * 72 + 64] = sz;
       }
     }
+    // dW3 [32 x 64] = d3^T f2 (registers until the Adam step)
+    f4v g3;
+    {
+      const int o0 = (wave >> 2) * 16, ii0 = (wave & 3) * 16;
+      g3 = Z4;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32)
+        g3 = mfma(cfrag(S + H_D3S, H_L3, k0, o0, lane), cfrag(S + H_F2S, H_L2, k0, ii0, lane), g3);
+    }
     SYNC();
     if (tid < 32 || tid == 64) {
       float s0 = 0.f, s1 = 0.f;
@@ -1195,88 +1271,19 @@ __device__ __forceinline__ void head(const Ctx& x) {
         sums[128] = s0;                  // gbo
       }
     }
-    // dW3 [32 x 64] = d3^T f2 (registers until the Adam step)
-    f4v g3;
-    {
-      const int o0 = (wave >> 2) * 16, ii0 = (wave & 3) * 16;
-      g3 = Z4;
-#pragma unroll
-      for (int k0 = 0; k0 < 128; k0 += 32)
-        g3 = mfma(cfrag(S + H_D3S, H_L3, k0, o0, lane), cfrag(S + H_F2S, H_L2, k0, ii0, lane), g3);
-    }
-    // d2 = d3 . W3 * relu'(f2); gb2 per wave
-    {
-      const int m0 = wave * 16;
-      const s8v af = rfrag(S + H_D3S, H_L3, m0, 0, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f4v acc = mfma(af, cfrag(S + H_W3S, H_L2, 0, 16 * j, lane), Z4);
-        const int n = 16 * j + li;
-        float cs = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + 4 * g + e;
-          const unsigned short fb = f2s[m * H_L2 + n];
-          const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
-          d2s[m * H_L2 + n] = bfu(v);
-          cs += v;
-        }
-        cs += __shfl_xor(cs, 16, 64);
-        cs += __shfl_xor(cs, 32, 64);
-        if (lane < 16) gbw[wave * 192 + n] = cs;
-      }
-    }
-    SYNC();
     if (tid < 64) {
       float sb = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) sb += gbw[w * 192 + tid];
       sums[tid] = sb;  // gb2
     }
-    SYNC();  // U (f2s / f3f / d3s) is dead: d1 staging
-    // d1 = d2 . W2 * relu'(f1) -> bf16 staging; gb1 per wave
-    {
-      const int m0 = wave * 16;
-      const s8v a0 = rfrag(S + H_D2S, H_L2, m0, 0, lane), a1 = rfrag(S + H_D2S, H_L2, m0, 32, lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f4v acc = mfma(a0, cfrag(S + H_W2S, H_L1, 0, 16 * j, lane), Z4);
-        acc = mfma(a1, cfrag(S + H_W2S, H_L1, 32, 16 * j, lane), acc);
-        const int n = 16 * j + li;
-        float cs = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + 4 * g + e;
-          const unsigned short fb = f1s[m * H_L1 + n];
-          const float v = (fb != 0 && !(fb & 0x8000)) ? acc[e] : 0.f;
-          d1s[m * H_L1 + n] = bfu(v);
-          cs += v;
-        }
-        cs += __shfl_xor(cs, 16, 64);
-        cs += __shfl_xor(cs, 32, 64);
-        if (lane < 16) gbw[wave * 192 + 64 + n] = cs;
-      }
-    }
-    // per-wave hand-off: this wave's 16 d1 rows (its own LDS writes: no barrier) + its status slot, drained, then
-    // its counter — the tower workgroups of those rows start without waiting for the other waves
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = lane + 64 * u, r = 16 * wave + (e >> 4), pc = e & 15;
-      st16(x.rw, WS_D1 + (r * 128 + 8 * pc) * 2, *(const LDS_AS u32x4*)(S + H_D1S + (r * H_L1 + 8 * pc) * 2));
-    }
-    if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
-    drain();
-    if (lane == 0) __hip_atomic_fetch_add(x.ctr + (CT_HW + wave) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    SYNC();
     if (tid < 128) {
       float sb = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) sb += gbw[w * 192 + 64 + tid];
       sums[129 + tid] = sb;  // gb1
     }
-    arrive(x, CT_H);
-    REOPQ();
-    stamp(x, kact, 1);
+    SYNC();
     // dW2 [64 x 128] = d2^T f1 (registers; after the d1 hand-off: off the critical path)
     f4v g2[4];
     {
