@@ -22,6 +22,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
+import math
+
 import numpy as np
 import torch
 
@@ -114,47 +116,190 @@ def shieldfl(U: torch.Tensor, sizes=None, **_) -> AggResult:
     return AggResult(ops.weighted_rows(U, w.double()), True, {"weights": w, "cos": cos})
 
 
-def _pca_project(U: torch.Tensor, r: int) -> np.ndarray:
+def _centred_gram(U: torch.Tensor) -> torch.Tensor:
     X = U.double()
     Xc = X - X.mean(dim=0, keepdim=True)
-    # thin SVD through the N x N Gram (N <= a few hundred): never forms a P x P matrix
-    Gm = (Xc @ Xc.t()).cpu().numpy()
-    evals, evecs = np.linalg.eigh(Gm)
-    order = np.argsort(evals)[::-1][:r]
-    evals = np.clip(evals[order], 1e-30, None)
-    # scores = Xc V = U_svd * S  ->  evecs * sqrt(evals)
-    return evecs[:, order] * np.sqrt(evals)[None, :]
+    return Xc @ Xc.t()
+
+
+def _gmm_chol(S, r):
+    Lc = np.zeros((4, 4))
+    for i in range(r):
+        for j in range(i + 1):
+            s = S[i][j]
+            for k in range(j):
+                s -= Lc[i][k] * Lc[j][k]
+            if i == j:
+                if not s > 0.0:
+                    return None
+                Lc[i][i] = math.sqrt(s)
+            else:
+                Lc[i][j] = s / Lc[j][j]
+    return Lc
+
+
+def _gmm_md2(Lc, r, x, mu):
+    y = [0.0] * r
+    s = 0.0
+    for i in range(r):
+        v = x[i] - mu[i]
+        for k in range(i):
+            v -= Lc[i][k] * y[k]
+        y[i] = v / Lc[i][i]
+        s += y[i] * y[i]
+    return s
+
+
+def gmm_filter_ref(G: np.ndarray, att: np.ndarray):
+    """Host mirror of ``agg.hip`` ``k_gmm_filter`` (same algorithm and operation order, fp64): returns
+    (keep [n] bool, threshold, kept, ok).  See the kernel for the algorithm and its reference mapping."""
+    n = G.shape[0]
+    A = [list(map(float, row)) for row in G]
+    V = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
+    for _ in range(12):
+        for p in range(n - 1):
+            for q in range(p + 1, n):
+                apq = A[p][q]
+                if abs(apq) < 1e-300:
+                    continue
+                th = (A[q][q] - A[p][p]) / (2.0 * apq)
+                t = (1.0 if th >= 0.0 else -1.0) / (abs(th) + math.sqrt(th * th + 1.0))
+                c = 1.0 / math.sqrt(t * t + 1.0)
+                sn = t * c
+                for k in range(n):
+                    akp, akq = A[k][p], A[k][q]
+                    A[k][p] = c * akp - sn * akq
+                    A[k][q] = sn * akp + c * akq
+                for k in range(n):
+                    apk, aqk = A[p][k], A[q][k]
+                    A[p][k] = c * apk - sn * aqk
+                    A[q][k] = sn * apk + c * aqk
+                for k in range(n):
+                    vkp, vkq = V[k][p], V[k][q]
+                    V[k][p] = c * vkp - sn * vkq
+                    V[k][q] = sn * vkp + c * vkq
+    order = sorted(range(n), key=lambda i: -A[i][i])  # stable: ties keep index order (as the insertion sort)
+    ev = [A[i][i] for i in order]
+    r = max(1, min(4, n // 2 - 1))
+    Z = [[V[i][order[k]] * math.sqrt(max(ev[k], 1e-30)) for k in range(r)] for i in range(n)]
+    zmax = max(1e-30, max(abs(z) for row in Z for z in row))
+    Z = [[z / zmax for z in row] for row in Z]
+    idx = [i for i in range(n) if not att[i]]
+    nb = len(idx)
+    idx += [i for i in range(n) if att[i]]
+    X = [Z[i] for i in idx]
+    m = len(X)
+    K = 2 if m >= 2 else 1
+    mu = [list(X[0]), list(X[0])]
+    resp = [[1.0, 0.0] for _ in range(m)]
+    if K == 2:
+        far, best = 0, -1.0
+        for i in range(m):
+            d = sum((X[i][k] - X[0][k]) * (X[i][k] - X[0][k]) for k in range(r))
+            if d > best:
+                best, far = d, i
+        mu[1] = list(X[far])
+        for _ in range(10):
+            s = [[0.0] * r, [0.0] * r]
+            cnt = [0.0, 0.0]
+            for i in range(m):
+                d0 = d1 = 0.0
+                for k in range(r):
+                    d0 += (X[i][k] - mu[0][k]) * (X[i][k] - mu[0][k])
+                    d1 += (X[i][k] - mu[1][k]) * (X[i][k] - mu[1][k])
+                lab = 1 if d1 < d0 else 0
+                resp[i] = [1.0 if lab == 0 else 0.0, 1.0 if lab == 1 else 0.0]
+                cnt[lab] += 1.0
+                for k in range(r):
+                    s[lab][k] += X[i][k]
+            for cc in range(2):
+                if cnt[cc] > 0.0:
+                    mu[cc] = [s[cc][k] / cnt[cc] for k in range(r)]
+    eps10, reg, LOG2PI = 10.0 * 2.220446049250313e-16, 1e-6, 1.8378770664093453
+    st = {"w": [0.0, 0.0], "Lc": [None, None], "logdet": [0.0, 0.0], "ok": True}
+
+    def mstep():
+        nks = 0.0
+        for cc in range(K):
+            nk = eps10
+            for i in range(m):
+                nk += resp[i][cc]
+            for k in range(r):
+                sm = 0.0
+                for i in range(m):
+                    sm += resp[i][cc] * X[i][k]
+                mu[cc][k] = sm / nk
+            cov = [[0.0] * 4 for _ in range(4)]
+            for a_ in range(r):
+                for b_ in range(r):
+                    sm = 0.0
+                    for i in range(m):
+                        sm += resp[i][cc] * (X[i][a_] - mu[cc][a_]) * (X[i][b_] - mu[cc][b_])
+                    cov[a_][b_] = sm / nk + (reg if a_ == b_ else 0.0)
+            st["w"][cc] = nk
+            nks += nk
+            Lc = _gmm_chol(cov, r)
+            if Lc is None:
+                st["ok"] = False
+                Lc = np.eye(4)
+            st["Lc"][cc] = Lc
+            st["logdet"][cc] = 2.0 * sum(math.log(Lc[k][k]) for k in range(r))
+        for cc in range(K):
+            st["w"][cc] /= nks
+
+    def wlogp(x, cc):
+        return math.log(st["w"][cc]) - 0.5 * (r * LOG2PI + _gmm_md2(st["Lc"][cc], r, x, mu[cc]) + st["logdet"][cc])
+
+    mstep()
+    lb = -math.inf
+    it = 0
+    while it < 100 and st["ok"]:
+        prev = lb
+        tot = 0.0
+        for i in range(m):
+            lp = [wlogp(X[i], 0), wlogp(X[i], 1) if K == 2 else -math.inf]
+            mx = max(lp)
+            lse = mx + math.log(math.exp(lp[0] - mx) + math.exp(lp[1] - mx))
+            tot += lse
+            resp[i] = [math.exp(lp[0] - lse), math.exp(lp[1] - lse) if K == 2 else 0.0]
+        mstep()
+        lb = tot / m
+        it += 1
+        if abs(lb - prev) < 1e-3:
+            break
+    mds = [math.sqrt(_gmm_md2(st["Lc"][0], r, X[i], mu[0])) for i in range(nb)]
+    if nb:
+        mb = sum(mds) / nb
+        thr = 3.0 * math.sqrt(sum((d - mb) ** 2 for d in mds) / nb)
+    else:
+        thr = math.inf
+    keep = np.zeros(n, dtype=bool)
+    for i in range(n):
+        cc = 1 if (K == 2 and wlogp(Z[i], 1) > wlogp(Z[i], 0)) else 0
+        keep[i] = st["ok"] and math.sqrt(_gmm_md2(st["Lc"][cc], r, Z[i], mu[cc])) <= thr
+    return keep, thr, int(keep.sum()), st["ok"]
 
 
 def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, seed: int = 0, **_) -> AggResult:
-    """Low-rank GMM filter (reference intent; the reference itself crashes, A-8)."""
-    from sklearn.mixture import GaussianMixture
-
+    """GMM gradient filter (reference server.py:352-370; its full-covariance fit on raw P-dim updates crashes, A-8):
+    a 2-component GMM on the updates' leading PCA scores, deterministic (agg.hip ``k_gmm_filter``, one fused
+    launch on the device; ``gmm_filter_ref`` on the host).  The mean of the kept rows; the round fails when no
+    row is kept (reference ``round_result = False``) — the only host read of the mode, one byte after the kernel."""
     n = U.shape[0]
-    att = attackers.bool().cpu().numpy() if attackers is not None else np.zeros(n, bool)
-    # subspace rank small enough that each of the 2 components has well-conditioned covariance
-    r = max(1, min(4, n // 2 - 1))
-    Z = _pca_project(U, r)
-    Z = Z / max(float(np.abs(Z).max()), 1e-30)
-    benign = Z[~att]
-    mal = Z[att]
-    allz = np.vstack([benign, mal]) if len(mal) else benign
-    ncomp = 2 if allz.shape[0] >= 2 else 1
-    g = GaussianMixture(n_components=ncomp, covariance_type="full", random_state=seed, reg_covar=1e-6).fit(allz)
-
-    def md(x, k):
-        d = x - g.means_[k]
-        return float(np.sqrt(d @ np.linalg.inv(g.covariances_[k]) @ d))
-
-    thr = 3 * np.std([md(x, 0) for x in benign]) if len(benign) else np.inf
-    keep = []
-    for i in range(n):
-        k = int(np.argmax(g.predict_proba(Z[i:i + 1])[0]))
-        if md(Z[i], k) <= thr:
-            keep.append(i)
-    if not keep:
+    att = attackers.bool() if attackers is not None else torch.zeros(n, dtype=torch.bool)
+    G = _centred_gram(U)
+    if U.is_cuda and n <= 64:
+        keep_d, inf_d = ops.native().gmm_filter(G.contiguous(), att.to(U.device, torch.uint8).contiguous())
+        keep = keep_d.bool()
+        thr = inf_d[0]
+        if not bool(inf_d[1] > 0):  # (the one synchronising read)
+            return AggResult(None, False, {"kept": keep, "threshold": thr})
+        return AggResult(_masked_mean(U, keep), True, {"kept": keep, "threshold": thr})
+    keep, thr, kept, _ = gmm_filter_ref(G.cpu().numpy(), att.cpu().numpy())
+    if not kept:
         return AggResult(None, False, {"kept": []})
-    return AggResult(mean_of(U[keep]), True, {"kept": keep, "threshold": float(thr)})
+    return AggResult(mean_of(U[torch.from_numpy(np.nonzero(keep)[0]).to(U.device)]), True,
+                     {"kept": np.nonzero(keep)[0].tolist(), "threshold": float(thr)})
 
 
 def scionfl(U: torch.Tensor, sizes: torch.Tensor, seed: int = 0, **_) -> AggResult:

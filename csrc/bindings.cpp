@@ -81,6 +81,20 @@ torch::Tensor pairwise_sqdist_gram(torch::Tensor G) {
   return D;
 }
 
+// GMM filter (agg.gmm): G = centred Gram [n, n] fp64, att [n] uint8 -> (keep [n] uint8, info [3] fp64)
+std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
+  check_dev(G, "G", torch::kFloat64);
+  check_dev(att, "att", torch::kUInt8);
+  const int64_t n = G.size(0);
+  TORCH_CHECK(G.dim() == 2 && G.size(1) == n && att.numel() == n && n >= 1 && n <= 64, "gmm_filter: G [n, n], n <= 64");
+  auto keep = torch::zeros({n}, att.options());
+  auto info = torch::zeros({3}, G.options());
+  TORCH_CHECK(afl_gmm_filter(G.data_ptr<double>(), (int)n, att.data_ptr<uint8_t>(), keep.data_ptr<uint8_t>(),
+                             info.data_ptr<double>(), cur()) == 0, "gmm_filter launch failed");
+  AFL_CHECK_LAUNCH();
+  return {keep, info};
+}
+
 // own + sigma * N(0,1), Philox4x32-10 keyed by `seed` (Random attack)
 torch::Tensor noise_philox(torch::Tensor own, double sigma, int64_t seed) {
   check_dev(own, "own", torch::kFloat32);
@@ -661,6 +675,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weighted_rows", &weighted_rows);
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
+  m.def("gmm_filter", &gmm_filter);
   m.def("stoch_quant", &stoch_quant);
   m.def("adam_flat", &adam_flat);
   m.def("roc_auc", &roc_auc);

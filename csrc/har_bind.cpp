@@ -1,3 +1,4 @@
+#include <cstdlib>
 // torch bindings of the bf16 HAR encoder kernels (kernels/har.hip).  Every op writes into caller-provided
 // tensors: bf16 activations are torch.bfloat16 tensors, gradients / statistics fp32.  The HAR layer
 // program (attackfl_amd/fl/programs.py HARProgram, device path) preallocates them once and captures the
@@ -126,6 +127,8 @@ AflHarAttn attn_args(torch::Tensor qkv, torch::Tensor lse2, int64_t B, int64_t L
   a.L = (int)L;
   a.Lp = (int)Lp;
   a.drop = drop(seeds, stepctl, layer, p);
+  const char* vl = std::getenv("AFL_HAR_DQ_VLOAD");
+  a.dbg = (vl && vl[0] == '1') ? 1 : 0;
   return a;
 }
 

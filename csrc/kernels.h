@@ -373,6 +373,7 @@ struct AflHarAttn {
                                // forward, read by both backward kernels (dropout only)
   int C, B, L, Lp;
   AflDrop drop;
+  int dbg;  // diagnostics: bit 0 = dQ reads the keep words with vector loads (AFL_HAR_DQ_VLOAD=1)
 };
 // keep words per (client, sample, head): [query tile Lp/16][key chunk Lp/64][t 4][e 4], bit = lane of the forward
 #define AFL_HAR_MASK_WORDS(Lp) ((long)((Lp) / 16) * ((Lp) / 64) * 16)
@@ -408,6 +409,8 @@ int afl_attn_bwd(const AflAttn& a, hipStream_t s);
 // agg.hip — Gram-form pairwise distances (fp64 MFMA, rows centred on row 0; K <= 64) and Philox noise
 int afl_gram_partials(int K, long P);  // doubles of scratch afl_pair_sqdist_gram needs
 int afl_pair_sqdist_gram(const float* G, int K, long P, double* partial, double* D, hipStream_t s);
+// GMM gradient filter on the centred Gram matrix (agg.hip k_gmm_filter): keep[n] (0/1), info = {threshold, kept, ok}
+int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, hipStream_t s);
 void afl_noise_philox(const float* own, float* out, long P, float sigma, uint64_t seed, hipStream_t s);
 
 // comm.hip — one-shot intra-node all-gather over IPC-mapped peer buffers (xGMI)

@@ -476,3 +476,232 @@ void afl_adam_flat(float* p, const float* g, float* m, float* v, long n, int ste
   hipLaunchKernelGGL(k_adam_flat, dim3(afl_cdiv(n, 256)), dim3(256), 0, s, p, g, m, v, n, (float)(lr / bc1),
                      (float)(1.0 / sqrt(bc2)), b1, b2, eps, gscale);
 }
+
+// ============================================================================ gmm_filter
+// GMM gradient filter (reference server.py:352-370, src/Utils.py:257-323), all decisions on the device so the
+// round needs no host round trip: input the centred Gram matrix G = Xc Xc^T [n][n] (fp64) of the client updates.
+//   1. PCA scores in r = max(1, min(4, n/2 - 1)) dims: cyclic Jacobi eigen-decomposition of G (12 sweeps),
+//      eigenvalues in descending order, Z = V_r sqrt(lambda_r), scaled by 1 / max |Z|;
+//   2. rows ordered benign then malicious (train_gmm_model's vstack), a 2-component full-covariance GMM
+//      (reg_covar 1e-6, tol 1e-3, <= 100 EM iterations, sklearn's M / E steps) initialised by a deterministic
+//      k-means (centres: row 0 and the row farthest from it, 10 Lloyd iterations) — sklearn's k-means++ init
+//      draws from an unseeded RNG in the reference, so any fixed init is one of its possible runs;
+//   3. threshold = 3 x population std of the benign rows' Mahalanobis distances to component 0; a row is kept
+//      when its distance to its most probable component is <= threshold.
+// One lane does the O(n^3 + 100 n r^2) work (n <= 64); agg.gmm_filter_ref in Python is the bit-level mirror.
+constexpr int GMM_MAXN = 64, GMM_R = 4;
+
+__device__ __host__ inline bool gmm_chol(const double (&S)[GMM_R][GMM_R], int r, double (&Lc)[GMM_R][GMM_R]) {
+  for (int i = 0; i < r; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = S[i][j];
+      for (int k = 0; k < j; ++k) s -= Lc[i][k] * Lc[j][k];
+      if (i == j) {
+        if (!(s > 0.0)) return false;
+        Lc[i][i] = sqrt(s);
+      } else {
+        Lc[i][j] = s / Lc[j][j];
+      }
+    }
+  return true;
+}
+// squared Mahalanobis distance through the Cholesky factor (forward substitution)
+__device__ __host__ inline double gmm_md2(const double (&Lc)[GMM_R][GMM_R], int r, const double* x, const double* mu) {
+  double y[GMM_R], s = 0.0;
+  for (int i = 0; i < r; ++i) {
+    double v = x[i] - mu[i];
+    for (int k = 0; k < i; ++k) v -= Lc[i][k] * y[k];
+    y[i] = v / Lc[i][i];
+    s += y[i] * y[i];
+  }
+  return s;
+}
+
+__global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G, int n, const unsigned char* __restrict__ att,
+                                                   unsigned char* __restrict__ keep, double* __restrict__ info) {
+  __shared__ double A[GMM_MAXN * GMM_MAXN], V[GMM_MAXN * GMM_MAXN], Z[GMM_MAXN * GMM_R], X[GMM_MAXN * GMM_R];
+  __shared__ double resp[GMM_MAXN * 2], ev[GMM_MAXN];
+  __shared__ int ord[GMM_MAXN], evi[GMM_MAXN];
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    A[e] = G[e];
+    V[e] = (e / n == e % n) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  // ---- 1. Jacobi eigen-decomposition (cyclic sweeps, fixed count)
+  for (int sweep = 0; sweep < 12; ++sweep)
+    for (int p = 0; p < n - 1; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
+        if (fabs(apq) < 1e-300) continue;
+        const double th = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
+        const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < n; ++k) {  // columns p, q
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = c * akp - s * akq;
+          A[k * n + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; ++k) {  // rows p, q
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = c * apk - s * aqk;
+          A[q * n + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - s * vkq;
+          V[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+  for (int i = 0; i < n; ++i) {
+    ev[i] = A[i * n + i];
+    evi[i] = i;
+  }
+  for (int i = 1; i < n; ++i) {  // stable insertion sort, descending
+    const double v = ev[i];
+    const int ix = evi[i];
+    int j = i - 1;
+    while (j >= 0 && ev[j] < v) {
+      ev[j + 1] = ev[j];
+      evi[j + 1] = evi[j];
+      --j;
+    }
+    ev[j + 1] = v;
+    evi[j + 1] = ix;
+  }
+  const int r = max(1, min(GMM_R, n / 2 - 1));
+  double zmax = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < r; ++k) {
+      const double z = V[i * n + evi[k]] * sqrt(fmax(ev[k], 1e-30));
+      Z[i * GMM_R + k] = z;
+      zmax = fmax(zmax, fabs(z));
+    }
+  zmax = fmax(zmax, 1e-30);
+  int m = 0, nb = 0;
+  for (int i = 0; i < n; ++i)
+    if (!att[i]) ord[m++] = i;
+  nb = m;
+  for (int i = 0; i < n; ++i)
+    if (att[i]) ord[m++] = i;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < r; ++k) Z[i * GMM_R + k] /= zmax;
+  for (int i = 0; i < m; ++i)
+    for (int k = 0; k < r; ++k) X[i * GMM_R + k] = Z[ord[i] * GMM_R + k];
+  const int K = m >= 2 ? 2 : 1;
+  // ---- 2a. deterministic k-means initialisation
+  double mu[2][GMM_R];
+  for (int k = 0; k < r; ++k) mu[0][k] = mu[1][k] = X[k];
+  if (K == 2) {
+    int far = 0;
+    double best = -1.0;
+    for (int i = 0; i < m; ++i) {
+      double d = 0.0;
+      for (int k = 0; k < r; ++k) d += (X[i * GMM_R + k] - X[k]) * (X[i * GMM_R + k] - X[k]);
+      if (d > best) {
+        best = d;
+        far = i;
+      }
+    }
+    for (int k = 0; k < r; ++k) mu[1][k] = X[far * GMM_R + k];
+    for (int it = 0; it < 10; ++it) {
+      double s[2][GMM_R] = {}, cnt[2] = {0.0, 0.0};
+      for (int i = 0; i < m; ++i) {
+        double d0 = 0.0, d1 = 0.0;
+        for (int k = 0; k < r; ++k) {
+          d0 += (X[i * GMM_R + k] - mu[0][k]) * (X[i * GMM_R + k] - mu[0][k]);
+          d1 += (X[i * GMM_R + k] - mu[1][k]) * (X[i * GMM_R + k] - mu[1][k]);
+        }
+        const int l = d1 < d0 ? 1 : 0;
+        resp[i * 2 + 0] = l == 0 ? 1.0 : 0.0;
+        resp[i * 2 + 1] = l == 1 ? 1.0 : 0.0;
+        cnt[l] += 1.0;
+        for (int k = 0; k < r; ++k) s[l][k] += X[i * GMM_R + k];
+      }
+      for (int c = 0; c < 2; ++c)
+        if (cnt[c] > 0.0)
+          for (int k = 0; k < r; ++k) mu[c][k] = s[c][k] / cnt[c];
+    }
+  } else {
+    for (int i = 0; i < m; ++i) {
+      resp[i * 2] = 1.0;
+      resp[i * 2 + 1] = 0.0;
+    }
+  }
+  // ---- 2b. EM (sklearn GaussianMixture, covariance_type "full")
+  const double eps10 = 10.0 * 2.220446049250313e-16, reg = 1e-6, LOG2PI = 1.8378770664093453;
+  double w[2], cov[2][GMM_R][GMM_R], Lc[2][GMM_R][GMM_R], logdet[2];
+  bool okc = true;
+  auto mstep = [&]() {
+    double nks = 0.0;
+    for (int c = 0; c < K; ++c) {
+      double nk = eps10;
+      for (int i = 0; i < m; ++i) nk += resp[i * 2 + c];
+      for (int k = 0; k < r; ++k) {
+        double s = 0.0;
+        for (int i = 0; i < m; ++i) s += resp[i * 2 + c] * X[i * GMM_R + k];
+        mu[c][k] = s / nk;
+      }
+      for (int a = 0; a < r; ++a)
+        for (int b = 0; b < r; ++b) {
+          double s = 0.0;
+          for (int i = 0; i < m; ++i)
+            s += resp[i * 2 + c] * (X[i * GMM_R + a] - mu[c][a]) * (X[i * GMM_R + b] - mu[c][b]);
+          cov[c][a][b] = s / nk + (a == b ? reg : 0.0);
+        }
+      w[c] = nk;
+      nks += nk;
+      okc = okc && gmm_chol(cov[c], r, Lc[c]);
+      double ld = 0.0;
+      for (int k = 0; k < r; ++k) ld += log(Lc[c][k][k]);
+      logdet[c] = 2.0 * ld;
+    }
+    for (int c = 0; c < K; ++c) w[c] /= nks;
+  };
+  auto wlogp = [&](const double* x, int c) {
+    return log(w[c]) - 0.5 * (r * LOG2PI + gmm_md2(Lc[c], r, x, mu[c]) + logdet[c]);
+  };
+  mstep();
+  double lb = -INFINITY;
+  for (int it = 0; it < 100 && okc; ++it) {
+    const double prev = lb;
+    double tot = 0.0;
+    for (int i = 0; i < m; ++i) {
+      double lp[2] = {wlogp(X + i * GMM_R, 0), K == 2 ? wlogp(X + i * GMM_R, 1) : -INFINITY};
+      const double mx = fmax(lp[0], lp[1]);
+      const double lse = mx + log(exp(lp[0] - mx) + exp(lp[1] - mx));
+      tot += lse;
+      resp[i * 2] = exp(lp[0] - lse);
+      resp[i * 2 + 1] = K == 2 ? exp(lp[1] - lse) : 0.0;
+    }
+    mstep();
+    lb = tot / m;
+    if (fabs(lb - prev) < 1e-3) break;
+  }
+  // ---- 3. threshold and decisions
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < nb; ++i) s1 += sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0]));
+  const double meanb = nb ? s1 / nb : 0.0;
+  for (int i = 0; i < nb; ++i) {
+    const double d = sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0])) - meanb;
+    s2 += d * d;
+  }
+  const double thr = nb ? 3.0 * sqrt(s2 / nb) : INFINITY;
+  int kept = 0;
+  for (int i = 0; i < n; ++i) {
+    const double* x = Z + i * GMM_R;
+    const int c = (K == 2 && wlogp(x, 1) > wlogp(x, 0)) ? 1 : 0;
+    const bool k = okc && sqrt(gmm_md2(Lc[c], r, x, mu[c])) <= thr;
+    keep[i] = k ? 1 : 0;
+    kept += k ? 1 : 0;
+  }
+  info[0] = thr;
+  info[1] = (double)kept;
+  info[2] = okc ? 1.0 : 0.0;
+}
+
+int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, hipStream_t s) {
+  if (n < 1 || n > GMM_MAXN) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gmm_filter, dim3(1), dim3(64), 0, s, G, n, att, keep, info);
+  return (int)hipGetLastError();
+}

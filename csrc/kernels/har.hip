@@ -573,7 +573,7 @@ __device__ __forceinline__ float keep_sel(uint64_t m, float x) {
   asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
   return r;
 }
-template <bool DROP>
+template <bool DROP, bool VL = false>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
   const int Lp = a.Lp, L = a.L;
@@ -610,10 +610,19 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
       const f4v p0 = mfma16(lds4(Vi, kt + li, g), df, Z4);
       const f4v p1 = mfma16(lds4(Vi, kt + 16 + li, g), df, Z4);
       uint64_t mw[8];
-      if (DROP) {
+      if (DROP && !VL) {
         ku64* w = mt + (kt >> 6) * 16 + ((kt & 63) >> 4) * 4;
 #pragma unroll
         for (int j = 0; j < 8; ++j) mw[j] = w[j];
+      }
+      if (DROP && VL) {  // diagnostic variant: vector loads, made uniform with readfirstlane
+        const uint32_t* w = (const uint32_t*)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp) + (long)(q0 >> 4) * nkc * 16 +
+                                              (kt >> 6) * 16 + ((kt & 63) >> 4) * 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t lo = __builtin_amdgcn_readfirstlane(w[2 * j]), hi = __builtin_amdgcn_readfirstlane(w[2 * j + 1]);
+          mw[j] = ((uint64_t)hi << 32) | lo;
+        }
       }
       float ds[8];
 #pragma unroll
@@ -1152,7 +1161,10 @@ int afl_har_attn_bwd(const AflHarAttn& a, hipStream_t s) {
   const dim3 grid(a.C * a.B * NH);
   if (a.drop.thr16) {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<true>, grid, dim3(AT_NT), kv, s, a);
-    hipLaunchKernelGGL(k_har_attn_bwd_dq<true>, grid, dim3(AT_NT), dq, s, a);
+    if (a.dbg & 1)
+      hipLaunchKernelGGL((k_har_attn_bwd_dq<true, true>), grid, dim3(AT_NT), dq, s, a);
+    else
+      hipLaunchKernelGGL((k_har_attn_bwd_dq<true, false>), grid, dim3(AT_NT), dq, s, a);
   } else {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<false>, grid, dim3(AT_NT), kv, s, a);
     hipLaunchKernelGGL(k_har_attn_bwd_dq<false>, grid, dim3(AT_NT), dq, s, a);

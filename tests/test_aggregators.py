@@ -135,3 +135,59 @@ def test_composite_roc_auc_matches_sklearn():
     y = (torch.rand(3000, generator=g) < 0.2).float()
     s = ((torch.rand(3000, generator=g) + 0.4 * y) * 20).round() / 20
     assert C.roc_auc(s, y) == pytest.approx(roc_auc_score(y.numpy(), s.numpy()), abs=1e-12)
+
+
+def _gmm_case(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    U = torch.randn(n, 3000, generator=g) * 0.1
+    U[n - 2:] += 0.4 * torch.randn(3000, generator=g)  # two displaced attackers
+    att = torch.zeros(n, dtype=torch.bool)
+    att[n - 2:] = True
+    return U, att
+
+
+@pytest.mark.parametrize("n,seed", [(8, 0), (10, 1), (12, 2)])
+def test_gmm_filter_em_matches_sklearn_from_the_same_init(n, seed):
+    """The mirror's EM (after its deterministic k-means init) equals sklearn's GaussianMixture started from the
+    same weights / means / precisions (reference train_gmm_model, src/Utils.py:257-262)."""
+    import math as m_
+    import numpy as np
+    from sklearn.mixture import GaussianMixture
+
+    U, att = _gmm_case(n, seed)
+    G = agg._centred_gram(U).numpy()
+    keep, thr, kept, ok = agg.gmm_filter_ref(G, att.numpy())
+    assert ok and 0 < kept <= n
+    # independent PCA scores (eigh) and the same k-means init
+    ev, V = np.linalg.eigh(G)
+    r = max(1, min(4, n // 2 - 1))
+    Z = V[:, ::-1][:, :r] * np.sqrt(np.maximum(ev[::-1][:r], 1e-30))
+    Z = Z / np.abs(Z).max()
+    X = np.vstack([Z[~att.numpy()], Z[att.numpy()]])
+    c0 = X[0]
+    c1 = X[np.argmax(((X - c0) ** 2).sum(1))]
+    mu = np.stack([c0, c1])
+    for _ in range(10):
+        lab = (((X - mu[1]) ** 2).sum(1) < ((X - mu[0]) ** 2).sum(1)).astype(int)
+        mu = np.stack([X[lab == k].mean(0) if (lab == k).any() else mu[k] for k in range(2)])
+    resp = np.eye(2)[lab]
+    nk = resp.sum(0) + 10 * np.finfo(float).eps
+    means = resp.T @ X / nk[:, None]
+    covs = np.stack([((resp[:, k, None] * (X - means[k])).T @ (X - means[k])) / nk[k] + 1e-6 * np.eye(r)
+                     for k in range(2)])
+    gm = GaussianMixture(2, covariance_type="full", reg_covar=1e-6, tol=1e-3, max_iter=100,
+                         weights_init=nk / nk.sum(), means_init=means,
+                         precisions_init=np.linalg.inv(covs)).fit(X)
+    md0 = [m_.sqrt((x - gm.means_[0]) @ np.linalg.inv(gm.covariances_[0]) @ (x - gm.means_[0]))
+           for x in X[:int((~att).sum())]]
+    assert thr == pytest.approx(3 * np.std(md0), rel=1e-4, abs=1e-9)
+    lab = gm.predict(Z)
+    ref_keep = np.array([m_.sqrt((z - gm.means_[k]) @ np.linalg.inv(gm.covariances_[k]) @ (z - gm.means_[k])) <= thr
+                         for z, k in zip(Z, lab)])
+    assert (keep == ref_keep).all()
+
+
+def test_gmm_round_fails_when_nothing_is_kept():
+    U = torch.full((6, 100), float("nan"))
+    res = agg.gmm(U, torch.ones(6), attackers=torch.zeros(6, dtype=torch.bool))
+    assert not res.ok and res.params is None

@@ -30,8 +30,9 @@ def _headmajor(qkv, B, L, Lp):
     return out.reshape(C * B * 4, 3, Lp, 16)
 
 
-@pytest.mark.parametrize("L,p", [(50, 0.0), (561, 0.1)])
-def test_har_attention_matches_composite(gpu, L, p):
+@pytest.mark.parametrize("L,p,vload", [(50, 0.0, "0"), (561, 0.1, "0"), (561, 0.1, "1"), (200, 0.1, "0")])
+def test_har_attention_matches_composite(gpu, L, p, vload, monkeypatch):
+    monkeypatch.setenv("AFL_HAR_DQ_VLOAD", vload)
     C, B = 2, 2
     g = torch.Generator().manual_seed(4)
     qkv = torch.randn(C, B * L, 192, generator=g)
@@ -69,8 +70,12 @@ def test_har_attention_matches_composite(gpu, L, p):
         (gref,) = torch.autograd.grad(out, x, dout)
     gq = gref.reshape(C, B, L, 3, 4, 16).permute(0, 1, 4, 3, 2, 5).reshape(C * B * 4, 3, L, 16)
     got = dq[:, :, :L].float().cpu()
+    errs = {}
     for w, n in enumerate(["dq", "dk", "dv"]):
-        _close(got[:, w], gq[:, w], 3e-2, n)
+        e = (got[:, w] - gq[:, w]).abs().max().item() / (gq[:, w].abs().max().item() + 1e-12)
+        if e > 3e-2:
+            errs[n] = round(e, 4)
+    assert not errs, errs
 
 
 def _decode_keep_words(words, L, Lp):
