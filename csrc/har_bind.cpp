@@ -127,8 +127,6 @@ AflHarAttn attn_args(torch::Tensor qkv, torch::Tensor lse2, int64_t B, int64_t L
   a.L = (int)L;
   a.Lp = (int)Lp;
   a.drop = drop(seeds, stepctl, layer, p);
-  const char* vl = std::getenv("AFL_HAR_DQ_VLOAD");
-  a.dbg = (vl && vl[0] == '1') ? 1 : 0;
   return a;
 }
 

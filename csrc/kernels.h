@@ -373,7 +373,6 @@ struct AflHarAttn {
                                // forward, read by both backward kernels (dropout only)
   int C, B, L, Lp;
   AflDrop drop;
-  int dbg;  // diagnostics: bit 0 = dQ reads the keep words with vector loads (AFL_HAR_DQ_VLOAD=1)
 };
 // keep words per (client, sample, head): [query tile Lp/16][key chunk Lp/64][t 4][e 4], bit = lane of the forward
 #define AFL_HAR_MASK_WORDS(Lp) ((long)((Lp) / 16) * ((Lp) / 64) * 16)

@@ -573,7 +573,7 @@ __device__ __forceinline__ float keep_sel(uint64_t m, float x) {
   asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
   return r;
 }
-template <bool DROP, bool VL = false>
+template <bool DROP>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
   const int Lp = a.Lp, L = a.L;
@@ -589,10 +589,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float ik = DROP ? a.drop.inv_keep : 1.f;
   const int nkc = Lp >> 6;
-  // (constant address space: wave-uniform addresses become scalar loads, so the words land in SGPR pairs; the
-  // words are read-only here and the dispatch's acquire fence makes the forward's stores visible to the K$)
-  typedef const __attribute__((address_space(4))) uint64_t ku64;
-  ku64* mblk = DROP ? (ku64*)(uintptr_t)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp)) : nullptr;
+  const uint32_t* mblk = DROP ? (const uint32_t*)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp)) : nullptr;
   for (int q0 = wave * 16; q0 < L; q0 += 16 * AT_WAVES) {
     const int q = q0 + li;
     const bool qok = q < L;
@@ -602,22 +599,18 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
     const float dl = qok ? a.delta[(long)cbh * Lp + q] : 0.f;
     // the forward's words of this query tile: element j of the 32-key step at kt is word 4((kt & 63) >> 4) + j of
     // chunk kt >> 6, bit = lane (same lane <-> (query, key) map as the forward)
-    ku64* mt = DROP ? mblk + (long)(q0 >> 4) * nkc * 16 : nullptr;
+    const uint32_t* mt = DROP ? mblk + (long)(q0 >> 4) * nkc * 32 : nullptr;
     f4v acc = Z4;
     auto step = [&](int kt, auto tail) {
       const f4v s0 = mfma16(lds4(Ki, kt + li, g), qf, Z4);
       const f4v s1 = mfma16(lds4(Ki, kt + 16 + li, g), qf, Z4);
       const f4v p0 = mfma16(lds4(Vi, kt + li, g), df, Z4);
       const f4v p1 = mfma16(lds4(Vi, kt + 16 + li, g), df, Z4);
+      // the step's 8 keep words: wave-uniform vector loads made scalar with readfirstlane (a scalar s_load of
+      // the same words read stale data from the scalar cache, which nothing invalidates between launches)
       uint64_t mw[8];
-      if (DROP && !VL) {
-        ku64* w = mt + (kt >> 6) * 16 + ((kt & 63) >> 4) * 4;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) mw[j] = w[j];
-      }
-      if (DROP && VL) {  // diagnostic variant: vector loads, made uniform with readfirstlane
-        const uint32_t* w = (const uint32_t*)(a.mask + (long)cbh * AFL_HAR_MASK_WORDS(Lp) + (long)(q0 >> 4) * nkc * 16 +
-                                              (kt >> 6) * 16 + ((kt & 63) >> 4) * 4);
+      if (DROP) {
+        const uint32_t* w = mt + (kt >> 6) * 32 + ((kt & 63) >> 4) * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t lo = __builtin_amdgcn_readfirstlane(w[2 * j]), hi = __builtin_amdgcn_readfirstlane(w[2 * j + 1]);
@@ -1161,10 +1154,7 @@ int afl_har_attn_bwd(const AflHarAttn& a, hipStream_t s) {
   const dim3 grid(a.C * a.B * NH);
   if (a.drop.thr16) {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<true>, grid, dim3(AT_NT), kv, s, a);
-    if (a.dbg & 1)
-      hipLaunchKernelGGL((k_har_attn_bwd_dq<true, true>), grid, dim3(AT_NT), dq, s, a);
-    else
-      hipLaunchKernelGGL((k_har_attn_bwd_dq<true, false>), grid, dim3(AT_NT), dq, s, a);
+    hipLaunchKernelGGL(k_har_attn_bwd_dq<true>, grid, dim3(AT_NT), dq, s, a);
   } else {
     hipLaunchKernelGGL(k_har_attn_bwd_kv<false>, grid, dim3(AT_NT), kv, s, a);
     hipLaunchKernelGGL(k_har_attn_bwd_dq<false>, grid, dim3(AT_NT), dq, s, a);

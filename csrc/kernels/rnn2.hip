@@ -1181,10 +1181,12 @@ __global__ void __launch_bounds__(NTH) k_rnn2_eval(const float* __restrict__ par
 #else
 #define K_RNN2 k_rnn2_train
 #endif
-// 3 workgroups per client: 3c (head), 3c + 1 (vitals branch), 3c + 2 (labs branch)
+// 3 workgroups per client: blocks c (head), C + c (vitals branch), 2C + c (labs branch)
 __global__ void __launch_bounds__(oc::NTH) K_RNN2(AflTfTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int role = blockIdx.x % 3, cid = blockIdx.x / 3;
+  // role-major block order: a client's workgroups are blocks cid, C + cid, 2C + cid, which the round-robin
+  // dispatch deals to ONE XCD when C is a multiple of 8 (same-L2 hand-offs; speed only, never correctness)
+  const int role = blockIdx.x / a.C, cid = blockIdx.x - role * a.C;
 #if defined(RNN2_ROLE)  // register-pressure diagnostics: one role per build
   if (RNN2_ROLE == 0) r2::head_main(a, cid, smem);
   else if (RNN2_ROLE == 1) r2::branch_main(a, cid, smem, 0);

@@ -30,9 +30,8 @@ def _headmajor(qkv, B, L, Lp):
     return out.reshape(C * B * 4, 3, Lp, 16)
 
 
-@pytest.mark.parametrize("L,p,vload", [(50, 0.0, "0"), (561, 0.1, "0"), (561, 0.1, "1"), (200, 0.1, "0")])
-def test_har_attention_matches_composite(gpu, L, p, vload, monkeypatch):
-    monkeypatch.setenv("AFL_HAR_DQ_VLOAD", vload)
+@pytest.mark.parametrize("L,p", [(50, 0.0), (561, 0.1), (200, 0.1)])
+def test_har_attention_matches_composite(gpu, L, p):
     C, B = 2, 2
     g = torch.Generator().manual_seed(4)
     qkv = torch.randn(C, B * L, 192, generator=g)

@@ -74,9 +74,9 @@ def main():
 
 
 def run(args, dev, rows, order, plan, params, split, used, block, wave=0):
-    names = NAMES4 if used == 4 else NAMES
+    names = NAMES4 if used in (4, 5) else NAMES
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
-    stamps[63] = block
+    stamps[63] = block * args.clients  # role-major block order: role r of client 0 is block r * C
     stamps[62] = wave
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
@@ -110,14 +110,14 @@ def main_rnn(args):
     steps = args.epochs * ((args.rows + 127) // 128)
     for b, wv in [(b, wv) for b in blocks for wv in (range(8) if args.wave < 0 else [args.wave])]:
         stamps = torch.zeros(64, dtype=torch.int64, device=dev)
-        stamps[63] = b
+        stamps[63] = b * args.clients  # role-major block order: role r of client 0 is block r * C
         stamps[62] = wv
         t0 = time.perf_counter()
         R.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, seeds, opt_mode=args.opt_mode,
                         stamps=stamps)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        names = NAMES_RNN_H if b % 3 == 0 else NAMES_RNN_B
+        names = NAMES_RNN_H if b == 0 else NAMES_RNN_B
         st = stamps.cpu().tolist()[:63]
         out = {"model": "RNNModel", "block": b, "wave": wv, "clients": args.clients, "wall_ms": wall * 1e3, "steps": steps,
                "us_per_step_wall": wall * 1e6 / steps, "us_per_step_stamped": sum(st) * 0.01 / steps,
