@@ -7,7 +7,6 @@ masks, Adam (or the SGD test mode) — used by the numerics tests to check the k
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -23,17 +22,14 @@ M32 = 0xFFFFFFFF
 
 # ------------------------------------------------------------------------------- device entry points
 def auto_split(C: int, dev) -> int:
-    """Trainer variant for C clients: 5 = the on-chip trainer (``tf2.hip``) with its head split over two
-    workgroups (head half 0 | vitals | labs | head half 1: the fc1 -> loss -> d(cat) chain at one wave per
-    SIMD) and 4 = the same with one head workgroup, when every workgroup of every client fits on the device at
-    once (one per CU); else the global-workspace kernels of ``transformer.hip`` with 2 or 1 workgroups per
-    client.  ``AFL_TF2_SPLIT_HEAD=0`` keeps one head workgroup."""
+    """Trainer variant for C clients: 4 = the on-chip trainer (``tf2.hip``: head | vitals | labs
+    workgroups with weights, optimizer state and activations held in registers / LDS) when every
+    workgroup of every client fits on the device at once (one per CU); else the global-workspace
+    kernels of ``transformer.hip`` with 2 or 1 workgroups per client."""
     from ..parallel.launcher import gpu_sharers
 
     # (processes sharing the GPU run their own persistent launches on the same CUs: count only this one's share)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
-    if 4 * C <= cus and os.environ.get("AFL_TF2_SPLIT_HEAD", "1") != "0":
-        return 5
     return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
@@ -55,7 +51,7 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else torch.tensor([device_seed(s) for s in seeds], dtype=torch.int32, device=dev)
     kt = None
-    if split in (4, 5):
+    if split == 4:
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
                              int(batch), float(lr), int(opt_mode), stamps, int(split), kt)

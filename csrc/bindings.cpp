@@ -505,9 +505,8 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   const int C = params.size(0);
   TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
   TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
-  // split 4 = the on-chip trainers (tf2.hip / rnn2.hip: 3 workgroups per client, state in registers / LDS);
-  // split 5 = tf2 with its head split over two workgroups (4 per client)
-  const bool tf2 = kind == 0 && (split == 4 || split == 5), rnn2 = kind == 1 && split == 4;
+  // split 4 = the on-chip trainers (tf2.hip / rnn2.hip: 3 workgroups per client, state in registers / LDS)
+  const bool tf2 = kind == 0 && split == 4, rnn2 = kind == 1 && split == 4;
   const long wsf = tf2 ? afl_tf2_ws_floats() : rnn2 ? afl_rnn2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats();
   const long stride = ((wsf + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());

@@ -106,14 +106,7 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 constexpr int MOM_SLOTS = 11;
 constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
-// slabs: 0 head (half 0), 1 vitals, 2 labs, 3 head half 1 (split head only)
-// Split-head exchange (see head_main): per half and step parity, [5 slots][512 threads] float4 of weight-gradient
-// partials (the thread's 4 fc1 tiles and its fc2 tile), then the half's 4 column-sum rows [4][132] and 4 loss partials
-constexpr long XH_TILES = 5L * NTH * 16, XH_PART = XH_TILES, XH_LOSS = XH_PART + 4 * 132 * 4;
-constexpr long XH_BYTES = (XH_LOSS + 16 + 255) / 256 * 256;
-constexpr long WS_XH = WS_MOM + 4 * MOM_WG_BYTES;
-constexpr long WS_BYTES = WS_XH + 4 * XH_BYTES;
-constexpr int XH_FLAG = 0;  // sync words: split-head half h publishes its step-s partials as flag word 32 h = s
+constexpr long WS_BYTES = WS_MOM + 3 * MOM_WG_BYTES;
 
 // branch LayerNorm column sums -> fp64 accumulator k of DBL (order G1 B1 G2 B2 G3 B3)
 __device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
@@ -926,24 +919,9 @@ struct HdState {
   VS vec;
 };
 
-// half < 0: ONE head workgroup, wave w serves batch rows 16 w .. 16 w + 15 (two waves per SIMD).
-// half 0 / 1 (split head, two head workgroups per client): waves 0-3 of half h serve rows 64 h + 16 w .. — the
-// critical fc1 -> loss -> d(cat) chain runs at one wave per SIMD, the rows of branch waves 0-3 no longer wait
-// behind those of waves 4-7 — and all 8 waves run the update: each half's weight-gradient partials (its 64
-// rows) are exchanged through the workspace (write-through stores, drain, flag word; the partner polls the flag
-// and loads), both halves sum them in the same order (half 0's + half 1's) and run the same Adam step on the
-// same replicated state, so the two copies of the head stay bit-identical without a second exchange.  The
-// exchange sits after the d(cat) hand-off: off the branches' critical path.
-template <int HALF>
 __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, uchar* smem) {
-  constexpr int half = HALF;
-  constexpr bool split = HALF >= 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
-  const bool active = !split || wave < 4;
-  const int rw = split ? 4 * half + (wave & 3) : wave;       // the row block (= branch wave) this wave serves
-  const int r = 16 * rw + (lane & 15);                        // batch row
-  const int rl = 16 * (split ? (wave & 3) : wave) + (lane & 15);  // its row in this workgroup's dW operand tiles
-  constexpr int nks = split ? 2 : 4;                          // 32-row k steps of the dW GEMMs
+  const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
   gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
@@ -952,7 +930,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   __syncthreads();
   HdState st;
   Stamp stp;
-  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM + (half == 1 ? 3 * MOM_WG_BYTES : 0));  // this WG's moments
+  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM);  // this workgroup's Adam moments
   mom_zero(rm, tid);
   {
     const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
@@ -976,7 +954,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   const int nb_total = (nd + BS - 1) / BS;
   const uint32_t seed = a.seeds[cid];
   const uchar* vec = smem + H_VEC;
-  LDS_AS float* part = ldsf(smem, H_PART) + rw * H_NVEC;  // this wave's column sums (slot = row block)
+  LDS_AS float* part = ldsf(smem, H_PART) + wave * H_NVEC;  // this wave's column sums
   LDS_AS float* lossw = ldsf(smem, H_LOSS);
   int step = 0;
   bool failed = false, timed_out = false;
@@ -994,7 +972,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   while (more) {
     // epoch boundaries crossed since the previous step (skipped batches included) close epoch losses
     while (cur_e < w.e) {
-      if (tid == 0 && half <= 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
+      if (tid == 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
       epoch_loss = 0.f;
       ++cur_e;
     }
@@ -1003,216 +981,156 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
-    if (active) {  // (split head: waves 4-7 wait for the update)
-      // fc1 dropout mask before the wait (the wave would only spin there)
-      const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
+    // fc1 dropout mask before the wait (the wave would only spin there)
+    const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
+    sb();
+    // ---- branch outputs of this wave's rows
+    u32x4 cv[4];  // vitals rows (cv[0..1]) | labs rows (cv[2..3])
+    const int go[2] = {gr_off(0, 0, wave, lane), gr_off(0, 1, wave, lane)};
+    const uint32_t fv = gr_get<2>(rg, go, cv, (uint32_t)step, 0, sync + XF_TMO, lane);
+    if (fv == 0xFFFFFFFFu) {
+      timed_out = failed = true;
+      break;
+    }
+    prio_hi();
+    stp(10, tid);
+    // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
+    // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
+    // ---- fc1 + GELU + dropout(0.3)
+    float a1[16], gk1[16];
+    {
+      f4v acc[4];
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        acc[T] = Z4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
+      }
+      float b1[16];
+      vec16(b1, vec + HV_B1 * 4, g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int j = 4 * t + i;
+          gf2v gp;
+          const gf2v gl = gelu2(gf2v{acc[t][i] + b1[j], acc[t][i + 1] + b1[j + 1]}, gp);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            a1[j + h] = keepf(gl[h] * INV_K03, mh, j + h);
+            gk1[j + h] = keepf(gp[h] * INV_K03, mh, j + h);
+          }
+        }
+    }
+    // ---- fc2 + GELU, output layer, sigmoid, BCE (log clamped at -100)
+    float dz2[8], gw[8];
+    float lrow = 0.f, dy3 = 0.f;
+    {
+      const s8v b0 = bfrag(a1, 0), b1 = bfrag(a1, 1);
+      f4v acc[2];
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 0, lane), b0, Z4);
+        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 1, lane), b1, acc[T]);
+      }
+      float b2[8], wo[8], g2[8], gp2[8];
+      vec8(b2, vec + HV_B2 * 4, g);
+      vec8(wo, vec + HV_WO * 4, g);
+      float dot = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int j = 4 * t + i;
+          gf2v gp;
+          const gf2v gl = gelu2(gf2v{acc[t][i] + b2[j], acc[t][i + 1] + b2[j + 1]}, gp);
+          g2[j] = gl[0];
+          g2[j + 1] = gl[1];
+          gp2[j] = gp[0];
+          gp2[j + 1] = gp[1];
+          dot += g2[j] * wo[j];
+          dot += g2[j + 1] * wo[j + 1];
+        }
+      const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
+      const float p = sigmoidf_(y3);
+      if (valid) {
+        // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
+        const float lg = logf(p), lg1 = log1pf(-p);
+        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
+        lrow = -(lab * lp + (1.f - lab) * l1p);
+        const float pq = p * (1.f - p);
+        dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dz2[j] = dy3 * wo[j] * gp2[j];
+        gw[j] = dy3 * g2[j];
+      }
+    }
+    // per-wave loss partial (each row counted once: lane group 0); its NaN test rides on the hand-off flag
+    float lsum = wave_sum(g == 0 ? lrow : 0.f);
+    if (lane == 0) lossw[wave] = lsum;
+    const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
+    // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
+    float dz1[16];
+    {
+      const s8v bz = bfrag(dz2, 0);
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        const f4v acc = mma(wtfrag<true>(smem + H_IMG_W2, LD64, T, 0, lane), bz, Z4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
+      }
+    }
+    // ---- d cat = dz1 . W1, each half straight to its branch
+    {
+      const s8v b0 = bfrag(dz1, 0), b1 = bfrag(dz1, 1);
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float d[16];
+#pragma unroll
+        for (int Tl = 0; Tl < 4; ++Tl) {
+          const int T = 4 * hb + Tl;
+          f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 0, lane), b0, Z4);
+          acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 1, lane), b1, acc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) d[4 * Tl + i] = acc[i];
+        }
+        u32x4 u[2];
+        pack16(d, u);
+        gr_put(rg, gr_off(1, hb, wave, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
+      }
+    }
+    prio_lo();
+    // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)
+    {
       sb();
-      // ---- branch outputs of this wave's rows
-      u32x4 cv[4];  // vitals rows (cv[0..1]) | labs rows (cv[2..3])
-      const int go[2] = {gr_off(0, 0, rw, lane), gr_off(0, 1, rw, lane)};
-      const uint32_t fv = gr_get<2>(rg, go, cv, (uint32_t)step, 0, sync + XF_TMO, lane);
-      if (fv == 0xFFFFFFFFu) {
-        timed_out = failed = true;
-        break;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {  // cat: tile t of the 8 = half (t & 1) of cv[t >> 1]
+        const u32x4 u = cv[t >> 1];
+        const u32x2v v = (t & 1) ? u32x2v{u[2], u[3]} : u32x2v{u[0], u[1]};
+        *(LDS_AS u32x2v*)(smem + H_CAT + t128(r, 4 * t + g)) = v;
       }
-      prio_hi();
-      stp(10, tid);
-      // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
-      // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
-      // ---- fc1 + GELU + dropout(0.3)
-      float a1[16], gk1[16];
-      {
-        f4v acc[4];
-  #pragma unroll
-        for (int T = 0; T < 4; ++T) {
-          acc[T] = Z4;
-  #pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
-        }
-        float b1[16];
-        vec16(b1, vec + HV_B1 * 4, g);
-  #pragma unroll
-        for (int t = 0; t < 4; ++t)
-  #pragma unroll
-          for (int i = 0; i < 4; i += 2) {
-            const int j = 4 * t + i;
-            gf2v gp;
-            const gf2v gl = gelu2(gf2v{acc[t][i] + b1[j], acc[t][i + 1] + b1[j + 1]}, gp);
-  #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              a1[j + h] = keepf(gl[h] * INV_K03, mh, j + h);
-              gk1[j + h] = keepf(gp[h] * INV_K03, mh, j + h);
-            }
-          }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, r, 4 * t + g, a1 + 4 * t);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, r, 4 * t + g, dz2 + 4 * t);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, r, 4 * t + g, dz1 + 4 * t);
+      float sb2, swo, sb1;
+      const int f2 = colsum32(dz2, lane, sb2), fo = colsum32(gw, lane, swo);
+      if (f2 >= 0) {
+        part[HV_B2 + f2] = sb2;
+        part[HV_WO + fo] = swo;
       }
-      // ---- fc2 + GELU, output layer, sigmoid, BCE (log clamped at -100)
-      float dz2[8], gw[8];
-      float lrow = 0.f, dy3 = 0.f;
-      {
-        const s8v b0 = bfrag(a1, 0), b1 = bfrag(a1, 1);
-        f4v acc[2];
-  #pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 0, lane), b0, Z4);
-          acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 1, lane), b1, acc[T]);
-        }
-        float b2[8], wo[8], g2[8], gp2[8];
-        vec8(b2, vec + HV_B2 * 4, g);
-        vec8(wo, vec + HV_WO * 4, g);
-        float dot = 0.f;
-  #pragma unroll
-        for (int t = 0; t < 2; ++t)
-  #pragma unroll
-          for (int i = 0; i < 4; i += 2) {
-            const int j = 4 * t + i;
-            gf2v gp;
-            const gf2v gl = gelu2(gf2v{acc[t][i] + b2[j], acc[t][i + 1] + b2[j + 1]}, gp);
-            g2[j] = gl[0];
-            g2[j + 1] = gl[1];
-            gp2[j] = gp[0];
-            gp2[j + 1] = gp[1];
-            dot += g2[j] * wo[j];
-            dot += g2[j + 1] * wo[j + 1];
-          }
-        const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
-        const float p = sigmoidf_(y3);
-        if (valid) {
-          // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
-          const float lg = logf(p), lg1 = log1pf(-p);
-          const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
-          lrow = -(lab * lp + (1.f - lab) * l1p);
-          const float pq = p * (1.f - p);
-          dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
-        }
-  #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          dz2[j] = dy3 * wo[j] * gp2[j];
-          gw[j] = dy3 * g2[j];
-        }
-      }
-      // per-wave loss partial (each row counted once: lane group 0); its NaN test rides on the hand-off flag
-      float lsum = wave_sum(g == 0 ? lrow : 0.f);
-      if (lane == 0) lossw[rw] = lsum;
-      const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
-      // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
-      float dz1[16];
-      {
-        const s8v bz = bfrag(dz2, 0);
-  #pragma unroll
-        for (int T = 0; T < 4; ++T) {
-          const f4v acc = mma(wtfrag<true>(smem + H_IMG_W2, LD64, T, 0, lane), bz, Z4);
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
-        }
-      }
-      // ---- d cat = dz1 . W1, each half straight to its branch
-      {
-        const s8v b0 = bfrag(dz1, 0), b1 = bfrag(dz1, 1);
-  #pragma unroll
-        for (int hb = 0; hb < 2; ++hb) {
-          float d[16];
-  #pragma unroll
-          for (int Tl = 0; Tl < 4; ++Tl) {
-            const int T = 4 * hb + Tl;
-            f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 0, lane), b0, Z4);
-            acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 1, lane), b1, acc);
-  #pragma unroll
-            for (int i = 0; i < 4; ++i) d[4 * Tl + i] = acc[i];
-          }
-          u32x4 u[2];
-          pack16(d, u);
-          gr_put(rg, gr_off(1, hb, rw, lane), u, ((uint32_t)step << 1) | wave_nan);  // NaN abort rides on the tag
-        }
-      }
-      prio_lo();
-      // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)
-      {
-        sb();
-  #pragma unroll
-        for (int t = 0; t < 8; ++t) {  // cat: tile t of the 8 = half (t & 1) of cv[t >> 1]
-          const u32x4 u = cv[t >> 1];
-          const u32x2v v = (t & 1) ? u32x2v{u[2], u[3]} : u32x2v{u[0], u[1]};
-          *(LDS_AS u32x2v*)(smem + H_CAT + t128(rl, 4 * t + g)) = v;
-        }
-  #pragma unroll
-        for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_A1, rl, 4 * t + g, a1 + 4 * t);
-  #pragma unroll
-        for (int t = 0; t < 2; ++t) st4<TK32>(smem + H_DZ2, rl, 4 * t + g, dz2 + 4 * t);
-  #pragma unroll
-        for (int t = 0; t < 4; ++t) st4<TK64>(smem + H_DZ1, rl, 4 * t + g, dz1 + 4 * t);
-        float sb2, swo, sb1;
-        const int f2 = colsum32(dz2, lane, sb2), fo = colsum32(gw, lane, swo);
-        if (f2 >= 0) {
-          part[HV_B2 + f2] = sb2;
-          part[HV_WO + fo] = swo;
-        }
-        const int f1 = colsum64(dz1, lane, sb1);
-        part[HV_B1 + f1] = sb1;
-        const float dbo = wave_sum(g == 0 ? dy3 : 0.f);  // d output.bias
-        if (lane == 0) part[HV_BO] = dbo;
-      }
+      const int f1 = colsum64(dz1, lane, sb1);
+      part[HV_B1 + f1] = sb1;
+      const float dbo = wave_sum(g == 0 ? dy3 : 0.f);  // d output.bias
+      if (lane == 0) part[HV_BO] = dbo;
     }
     stp(11, tid);
-    // the next step's labels (after the hand-off stores: their drain above must not wait for these)
-    Walk wn = w;
-    wn.b0 += BS;
-    more = walk_valid(wn, nd, BS, E);
-    lds_bar();
-    // ---- weight-gradient partials of this workgroup's rows
-    const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2), T2 = wave & 3, Tn2 = wave >> 2;
-    f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
-    f4v a2 = Z4;
-#pragma unroll
-    for (int s = 0; s < nks; ++s) {
-      const s8v x0 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta, lane), x1 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta + 1, lane);
-      const s8v y0 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb, lane), y1 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb + 1, lane);
-      acc[0][0] = mma(x0, y0, acc[0][0]);
-      acc[0][1] = mma(x0, y1, acc[0][1]);
-      acc[1][0] = mma(x1, y0, acc[1][0]);
-      acc[1][1] = mma(x1, y1, acc[1][1]);
-      a2 = mma(tfrag<TK64>(smem + H_A1, 32 * s, T2, lane), tfrag<TK32>(smem + H_DZ2, 32 * s, Tn2, lane), a2);
-    }
-    if constexpr (split) {  // ---- exchange with the other half (see head_main's comment)
-      const int par = step & 1;
-      const __amdgpu_buffer_rsrc_t xo = rsrc(ws + WS_XH + (2 * half + par) * XH_BYTES);
-      const __amdgpu_buffer_rsrc_t xi = rsrc(ws + WS_XH + (2 * (1 - half) + par) * XH_BYTES);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[k >> 1][k & 1]), xo, (k * NTH + tid) * 16, 0, 16);
-        store_guard();
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a2), xo, (4 * NTH + tid) * 16, 0, 16);
-      store_guard();
-      for (int e = tid; e < 4 * H_NVEC; e += NTH)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ldsf(smem, H_PART)[4 * half * H_NVEC + e]), xo,
-                                              (int)XH_PART + 4 * e, 0, 16);
-      if (tid < 4) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lossw[4 * half + tid]), xo, (int)XH_LOSS + 4 * tid, 0, 16);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_bar();
-      if (tid == 0) __hip_atomic_store(sync + XH_FLAG + 32 * half, (uint32_t)step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (wave == 0) {
-        gu32* pf = sync + XH_FLAG + 32 * (1 - half);
-        if (await(pf, pf, (uint32_t)step, 0, sync + XF_TMO, lane) == 0xFFFFFFFFu && lane == 0) lossw[15] = 1.f;
-      }
-      lds_bar();
-      if (lossw[15] != 0.f) {
-        timed_out = failed = true;
-        break;
-      }
-      f4v o[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) o[k] = __builtin_bit_cast(f4v, ld_wt(xi, (k * NTH + tid) * 16));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc[k >> 1][k & 1] = half == 0 ? acc[k >> 1][k & 1] + o[k] : o[k] + acc[k >> 1][k & 1];
-      a2 = half == 0 ? a2 + o[4] : o[4] + a2;
-      for (int e = tid; e < 4 * H_NVEC; e += NTH)
-        ldsf(smem, H_PART)[4 * (1 - half) * H_NVEC + e] =
-            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xi, (int)XH_PART + 4 * e, 0, 16));
-      if (tid < 4) lossw[4 * (1 - half) + tid] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xi, (int)XH_LOSS + 4 * tid, 0, 16));
-      lds_bar();
-    }
-    // Adam moments of this step's update
+    // Adam moments of this step's update (after the hand-off drain, before the loss barrier)
     f4v hm[6], hv[6];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1222,6 +1140,11 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     hm[4] = mom_ld(rm, 8, tid);
     hv[4] = mom_ld(rm, 9, tid);
     hm[5] = mom_ld(rm, 10, tid);
+    // the next step's labels (after the hand-off stores: their drain above must not wait for these)
+    Walk wn = w;
+    wn.b0 += BS;
+    more = walk_valid(wn, nd, BS, E);
+    lds_bar();
     {
       float tot = 0.f;
 #pragma unroll
@@ -1236,8 +1159,22 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     if (more) load_lab(wn);
     w = wn;
     stp(12, tid);
-    // ---- Adam (both halves of a split head: the same sums, the same state, the same result)
+    // ---- weight gradients + Adam
     {
+      const int Ta = 2 * (wave & 3), Tb = 2 * (wave >> 2);
+      f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
+      f4v a2 = Z4;
+      const int T2 = wave & 3, Tn2 = wave >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const s8v x0 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta, lane), x1 = tfrag<TK128>(smem + H_CAT, 32 * s, Ta + 1, lane);
+        const s8v y0 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb, lane), y1 = tfrag<TK64>(smem + H_DZ1, 32 * s, Tb + 1, lane);
+        acc[0][0] = mma(x0, y0, acc[0][0]);
+        acc[0][1] = mma(x0, y1, acc[0][1]);
+        acc[1][0] = mma(x1, y0, acc[1][0]);
+        acc[1][1] = mma(x1, y1, acc[1][1]);
+        a2 = mma(tfrag<TK64>(smem + H_A1, 32 * s, T2, lane), tfrag<TK32>(smem + H_DZ2, 32 * s, Tn2, lane), a2);
+      }
 #pragma unroll
       for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -1270,7 +1207,6 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     stp(14, tid);
   }
   stamp_fini(stp, a, smem, tid);
-  if constexpr (HALF == 1) return;  // (the split head's second half holds a bit-identical copy: half 0 writes back)
   if (!failed) {
     while (cur_e < E) {  // the last epoch (and trailing epochs that had no step)
       if (tid == 0) a.losses[(long)cid * E + cur_e] = epoch_loss / (float)max(nb_total, 1);
@@ -1301,25 +1237,20 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 #else
 #define K_TF2 k_tf2_train
 #endif
-// 3 workgroups per client: blocks c (head), C + c (vitals branch), 2C + c (labs branch); split 5 adds the second
-// head half at 3C + c
+// 3 workgroups per client: blocks c (head), C + c (vitals branch), 2C + c (labs branch)
 __global__ void __launch_bounds__(t2::NTH) K_TF2(AflTfTrainArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // role-major block order: a client's workgroups are blocks cid, C + cid, 2C + cid, which the round-robin
   // dispatch deals to ONE XCD when C is a multiple of 8 (same-L2 hand-offs; speed only, never correctness)
   const int role = blockIdx.x / a.C, cid = blockIdx.x - role * a.C;
 #if defined(TF2_ROLE)
-  if (TF2_ROLE == 0) t2::head_main<-1>(a, cid, smem);
+  if (TF2_ROLE == 0) t2::head_main(a, cid, smem);
   else if (TF2_ROLE == 1) t2::branch_main<0>(a, cid, smem);
   else t2::branch_main<1>(a, cid, smem);
   (void)role;
 #else
-  if (role == 0 && a.split == 5)
-    t2::head_main<0>(a, cid, smem);
-  else if (role == 0)
-    t2::head_main<-1>(a, cid, smem);
-  else if (role == 3)
-    t2::head_main<1>(a, cid, smem);
+  if (role == 0)
+    t2::head_main(a, cid, smem);
   else if (role == 1)
     t2::branch_main<0>(a, cid, smem);
   else
@@ -1342,8 +1273,7 @@ int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -3;
-  const int roles = a->split == 5 ? 4 : 3;  // split 5: two head workgroups per client (head_main)
-  if (roles * a->C > cus) return -4;  // the workgroups of a client spin on each other: all must be resident
-  hipLaunchKernelGGL(K_TF2, dim3(roles * a->C), dim3(t2::NTH), t2::SMEM, s, *a);
+  if (3 * a->C > cus) return -4;  // the workgroups of a client spin on each other: all must be resident
+  hipLaunchKernelGGL(K_TF2, dim3(3 * a->C), dim3(t2::NTH), t2::SMEM, s, *a);
   return 0;
 }

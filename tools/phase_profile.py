@@ -74,7 +74,7 @@ def main():
 
 
 def run(args, dev, rows, order, plan, params, split, used, block, wave=0):
-    names = NAMES4 if used in (4, 5) else NAMES
+    names = NAMES4 if used == 4 else NAMES
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
     stamps[63] = block * args.clients  # role-major block order: role r of client 0 is block r * C
     stamps[62] = wave
