@@ -401,6 +401,16 @@ __device__ void fill_hc(LDS_AS uint32_t* HC, int npairs, uint32_t key, uint32_t 
   for (int e = threadIdx.x; e < npairs; e += blockDim.x) HC[e] = attn_hc(key, layer, (uint32_t)e);
 }
 
+// lanes 2j / 2j + 1 of mw <- low / high half of keep word j (j = 0 .. 15), in two asm blocks of 16 writelanes
+__device__ __forceinline__ void keep_words(uint32_t& mw, const uint32_t (&bl)[16], const uint32_t (&bh)[16]) {
+  asm("s_nop 4\n\t" "v_writelane_b32 %0, %1, 0\n\t""v_writelane_b32 %0, %2, 1\n\t""v_writelane_b32 %0, %3, 2\n\t""v_writelane_b32 %0, %4, 3\n\t""v_writelane_b32 %0, %5, 4\n\t""v_writelane_b32 %0, %6, 5\n\t""v_writelane_b32 %0, %7, 6\n\t""v_writelane_b32 %0, %8, 7\n\t""v_writelane_b32 %0, %9, 8\n\t""v_writelane_b32 %0, %10, 9\n\t""v_writelane_b32 %0, %11, 10\n\t""v_writelane_b32 %0, %12, 11\n\t""v_writelane_b32 %0, %13, 12\n\t""v_writelane_b32 %0, %14, 13\n\t""v_writelane_b32 %0, %15, 14\n\t""v_writelane_b32 %0, %16, 15\n\t"
+      : "+v"(mw)
+      : "s"(bl[0]), "s"(bh[0]), "s"(bl[1]), "s"(bh[1]), "s"(bl[2]), "s"(bh[2]), "s"(bl[3]), "s"(bh[3]), "s"(bl[4]), "s"(bh[4]), "s"(bl[5]), "s"(bh[5]), "s"(bl[6]), "s"(bh[6]), "s"(bl[7]), "s"(bh[7]));
+  asm("s_nop 4\n\t" "v_writelane_b32 %0, %1, 16\n\t""v_writelane_b32 %0, %2, 17\n\t""v_writelane_b32 %0, %3, 18\n\t""v_writelane_b32 %0, %4, 19\n\t""v_writelane_b32 %0, %5, 20\n\t""v_writelane_b32 %0, %6, 21\n\t""v_writelane_b32 %0, %7, 22\n\t""v_writelane_b32 %0, %8, 23\n\t""v_writelane_b32 %0, %9, 24\n\t""v_writelane_b32 %0, %10, 25\n\t""v_writelane_b32 %0, %11, 26\n\t""v_writelane_b32 %0, %12, 27\n\t""v_writelane_b32 %0, %13, 28\n\t""v_writelane_b32 %0, %14, 29\n\t""v_writelane_b32 %0, %15, 30\n\t""v_writelane_b32 %0, %16, 31\n\t"
+      : "+v"(mw)
+      : "s"(bl[8]), "s"(bh[8]), "s"(bl[9]), "s"(bh[9]), "s"(bl[10]), "s"(bh[10]), "s"(bl[11]), "s"(bh[11]), "s"(bl[12]), "s"(bh[12]), "s"(bl[13]), "s"(bh[13]), "s"(bl[14]), "s"(bh[14]), "s"(bl[15]), "s"(bh[15]));
+}
+
 template <bool DROP>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
@@ -454,7 +464,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
       if (DROP) {
         // keep word (t, e) = ballot of the flags of keys kt + 16t + 4g + e over the wave (bit = lane): lanes 0..31
         // of mw collect the chunk's 16 words, stored for both backward kernels (no hashing there)
-        uint32_t mw = 0u;
+        uint32_t mw = 0u, bl[16], bh[16];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           bool k4[4];
@@ -463,10 +473,14 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
           for (int e = 0; e < 4; ++e) {
             pd[4 * t + e] = k4[e] ? pd[4 * t + e] : 0.f;
             const uint64_t bw = __builtin_amdgcn_ballot_w64(k4[e]);
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(mw) : "s"((uint32_t)bw), "n"(2 * (4 * t + e)));
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(mw) : "s"((uint32_t)(bw >> 32)), "n"(2 * (4 * t + e) + 1));
+            bl[4 * t + e] = (uint32_t)bw;
+            bh[4 * t + e] = (uint32_t)(bw >> 32);
           }
         }
+        // v_writelane reading an SGPR that a VALU compare has just written needs wait states the compiler does
+        // not insert inside inline asm (measured: ~5 % of the low-half flags wrong without them): every ballot is
+        // computed before the block, and the block opens with s_nop 4
+        keep_words(mw, bl, bh);
         if (lane < 32) mrow[(long)((q0 >> 4) * nkc + (kt >> 6)) * 32 + lane] = mw;
       }
       l = l * alpha + sum_x16_x32(ps);

@@ -1,6 +1,11 @@
 """Dump the HAR attention forward's keep words and the keep_rc reference for offline layout checks."""
+import os
+import sys
+
 import numpy as np
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from attackfl_amd.ops import layers as Lx
 from attackfl_amd.ops import masks, native
