@@ -117,6 +117,11 @@ def shieldfl(U: torch.Tensor, sizes=None, **_) -> AggResult:
 
 
 def _centred_gram(U: torch.Tensor) -> torch.Tensor:
+    """n x n Gram of the rows centred on their mean (fp64).  On the device: the fp64-MFMA Gram pass of
+    ``agg.hip`` (rows centred on row 0, then double-centred) instead of a generic fp64 GEMM with M = N = n and
+    K = P (~50 k), a shape the library GEMM handles poorly."""
+    if U.is_cuda and 1 <= U.shape[0] <= 64:
+        return ops.native().gram_centred(U.to(torch.float32).contiguous())[0]
     X = U.double()
     Xc = X - X.mean(dim=0, keepdim=True)
     return Xc @ Xc.t()
@@ -338,9 +343,7 @@ def _top_pc_scores(U: torch.Tensor, squarings: int = 12) -> torch.Tensor:
     """First principal-component scores of the rows (sklearn ``PCA(1).fit_transform`` up to the sign) with no
     host synchronisation: the n x n Gram of the centred rows, its leading eigenvector by repeated squaring
     (the gap ratio raised to 2^squarings, trace-normalised every step in fp64), score = v * sqrt(lambda)."""
-    X = U.double()
-    Xc = X - X.mean(dim=0, keepdim=True)
-    G = Xc @ Xc.t()
+    G = _centred_gram(U)
     M = G / G.diagonal().sum().clamp_min(1e-300)
     for _ in range(squarings):
         M = M @ M

@@ -95,6 +95,23 @@ std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
   return {keep, info};
 }
 
+// Gram matrix of the rows centred on the MEAN row (PCA of the updates: agg.fltracer / agg.gmm), through the same
+// fp64-MFMA pass (rows centred on row 0, H) followed by the double centring C = H - rowmean - colmean + mean
+std::vector<torch::Tensor> gram_centred(torch::Tensor G) {
+  check_dev(G, "G", torch::kFloat32);
+  TORCH_CHECK(G.dim() == 2 && G.size(0) >= 1 && G.size(0) <= 64, "G must be [K <= 64, P]");
+  const int K = G.size(0);
+  const long P = G.size(1);
+  auto D = torch::zeros({K, K}, G.options().dtype(torch::kFloat64));
+  auto scratch = torch::empty({(long)afl_gram_partials(K, P)}, D.options());
+  TORCH_CHECK(afl_pair_sqdist_gram(G.data_ptr<float>(), K, P, scratch.data_ptr<double>(), D.data_ptr<double>(),
+                                   cur()) == 0, "gram launch failed");
+  AFL_CHECK_LAUNCH();
+  auto H = scratch.narrow(0, scratch.numel() - (long)K * K, (long)K * K).view({K, K});
+  auto C = H - H.mean(0, true) - H.mean(1, true) + H.mean();
+  return {C, D};
+}
+
 // own + sigma * N(0,1), Philox4x32-10 keyed by `seed` (Random attack)
 torch::Tensor noise_philox(torch::Tensor own, double sigma, int64_t seed) {
   check_dev(own, "own", torch::kFloat32);
@@ -676,6 +693,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
   m.def("gmm_filter", &gmm_filter);
+  m.def("gram_centred", &gram_centred);
   m.def("stoch_quant", &stoch_quant);
   m.def("adam_flat", &adam_flat);
   m.def("roc_auc", &roc_auc);

@@ -1069,6 +1069,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
         *(LDS_AS u32x2v*)(f1s + b * H_L1 + i1) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
       }
     }
+    stamp(x, kact, 3);
     // fc2 (transposed, D[n][m] = W2 . f1^T: a lane ends with 4 consecutive features of one row)
     {
       f4v acc[4] = {Z4, Z4, Z4, Z4};
@@ -1101,6 +1102,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
             f4v{relu(acc[j][0] + bv[0]), relu(acc[j][1] + bv[1]), relu(acc[j][2] + bv[2]), relu(acc[j][3] + bv[3])};
       }
     }
+    stamp(x, kact, 4);
     // output logit (lane: row m0 + li, features 8 g .. 8 g + 7, summed over the 4 lane groups) + sigmoid-BCE
     // (k_bce arithmetic); d3 = dz wo^T * relu'(f3) for the same 8 features
     const int row = m0 + li;
@@ -1136,6 +1138,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     }
     lb = wsum(lb);
     if (lane == 0) red[wave] = lb;
+    stamp(x, kact, 5);
     // d2 = d3 . W3 * relu'(f2) (rows of this wave); gb2 partials per wave
     {
       const s8v af = rfrag(S + H_D3S, H_L3, m0, 0, lane);
@@ -1177,7 +1180,9 @@ __device__ __forceinline__ void head(const Ctx& x) {
         d1p[2 * j + 1] = pk2(v[2], v[3]);
       }
     }
+    stamp(x, kact, 6);
     SYNC();  // the only barrier before the hand-off: every wave's loss partial
+    stamp(x, kact, 7);
     const float loss = ((red[0] + red[1]) + (red[2] + red[3]) + ((red[4] + red[5]) + (red[6] + red[7]))) / (float)max(bs, 1);
     const bool nan = a.nan_abort && (loss != loss);
     if (nan) {  // status only: no update this step, the client's round ends (towers read the status)
@@ -1201,6 +1206,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     }
     if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
     drain();
+    stamp(x, kact, 8);
     if (lane == 0) __hip_atomic_fetch_add(x.ctr + (CT_HW + wave) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     arrive(x, CT_H);
     REOPQ();

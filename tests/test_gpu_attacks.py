@@ -56,3 +56,14 @@ def test_gmm_filter_kernel_matches_host_mirror(gpu, n, seed):
     assert int(info[1].item()) == kept and bool(info[2].item()) == ok
     res = agg.gmm(U.to(gpu), torch.ones(n), attackers=att)
     assert res.ok and torch.allclose(res.params.cpu(), U[torch.from_numpy(keep)].mean(0), atol=1e-6)
+
+
+def test_gram_centred_matches_fp64_reference(gpu):
+    from attackfl_amd.ops import native
+
+    g = torch.Generator().manual_seed(5)
+    U = torch.randn(9, 47693, generator=g) * 0.01 + 0.5
+    C = native().gram_centred(U.to(gpu))[0].cpu()
+    X = U.double() - U.double().mean(0, keepdim=True)
+    ref = X @ X.t()
+    assert torch.allclose(C, ref, rtol=1e-9, atol=1e-9 * ref.abs().max().item())
