@@ -164,7 +164,8 @@ constexpr long WS_BYTES = WS_MV + (long)NWG * MV_WG;
 // counters per client: F (towers -> head), H (head -> towers), P0/P1 (partials), W0/W1 (images), TMO
 // W1R: fc1 images of the next step published (7 arrivals per step)
 // HW + w: head wave w published d1 rows 16 w .. 16 w + 15 (the towers of those rows wait on it alone)
-constexpr int CT_F = 0, CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_W1R = 7, CT_HW = 8, CT_N = 16;  // x 32 words
+// FW + w: the tower workgroups of head wave w's rows (1 vitals + 2 labs) published their z1 partials
+constexpr int CT_H = 1, CT_P = 2, CT_W = 4, CT_TMO = 6, CT_W1R = 7, CT_HW = 8, CT_FW = 16, CT_N = 24;  // x 32 words
 
 struct Ctx {
   const AflCnn2Args* a;
@@ -234,6 +235,27 @@ __device__ __forceinline__ bool wait_ge(const Ctx& x, int which, uint32_t target
   lbar();
   const int ok = fl[0];
   lbar();  // fl is rewritten by the next wait
+  return ok != 0;
+}
+
+// one wave waits (lane 0 polls) until counter `which` reached `target`; false on the deadline.  The payload
+// loads that follow stay below the poll (wavefront acquire fence, as onchip.h await).
+__device__ __forceinline__ bool wait_wave(const Ctx& x, int which, uint32_t target) {
+  int ok = 1;
+  if ((threadIdx.x & 63) == 0) {
+    const long t0 = (long)__builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(x.ctr + which * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if ((long)__builtin_amdgcn_s_memrealtime() - t0 > DEADLINE) {
+        ok = 0;
+        __hip_atomic_store(x.ctr + CT_TMO * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x.a->failed[x.c] = 2;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  ok = __builtin_amdgcn_readfirstlane(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return ok != 0;
 }
 
@@ -645,7 +667,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       const f4v v = *(const LDS_AS f4v*)(S + O_ZS + (r * LDZ + 4 * pc) * 4);
       st16f(x.rw, WS_Z1P + ((T * 128 + b0 + r) * 128 + 4 * pc) * 4, v);
     }
-    arrive(x, CT_F);
+    arrive(x, CT_FW + (T == 0 ? i : (i >> 1)));  // (per head wave: it starts on its own rows' partials)
     REOPQ();
     stamp(x, kact, 1);
     xv_next = load_x(next_active(s + 1));
@@ -1046,7 +1068,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     const int yb = min(m0 + li, B - 1);
     const int yrow = idxs[yb];
     const float yv = yrow >= 0 ? a.rows[(long)yrow * 24 + 23] : 0.f;
-    if (!wait_ge(*&x, CT_F, (uint32_t)(24 * (kact + 1)), H_FLAG)) break;
+    if (!wait_wave(x, CT_FW + wave, 3u * (uint32_t)(kact + 1))) break;  // 1 vitals + 2 labs tower workgroups
     REOPQ();
     stamp(x, kact, 0);
     // z1 = z1p_vitals + z1p_labs (+ b1, ReLU) -> f1s rows of this wave; lane: row m0 + (lane >> 2), columns
@@ -1180,6 +1202,14 @@ __device__ __forceinline__ void head(const Ctx& x) {
         d1p[2 * j + 1] = pk2(v[2], v[3]);
       }
     }
+    // the d1 rows go out BEFORE the loss barrier (the write-through stores drain while the waves meet); the
+    // towers read them only after this wave's counter, i.e. after the status word says the loss was not NaN
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{d1p[2 * j], d1p[2 * j + 1]}, x.rw,
+                                            WS_D1 + (row * 128 + 16 * j + 4 * g) * 2, 0, 16);
+      sguard();
+    }
     stamp(x, kact, 6);
     SYNC();  // the only barrier before the hand-off: every wave's loss partial
     stamp(x, kact, 7);
@@ -1196,14 +1226,8 @@ __device__ __forceinline__ void head(const Ctx& x) {
       break;
     }
     if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
-    // per-wave hand-off: this wave's 16 d1 rows + its status slot, drained, then its counter — the tower
+    // per-wave hand-off: this wave's status slot, drained with its d1 rows, then its counter — the tower
     // workgroups of those rows start without waiting for the other waves
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{d1p[2 * j], d1p[2 * j + 1]}, x.rw,
-                                            WS_D1 + (row * 128 + 16 * j + 4 * g) * 2, 0, 16);
-      sguard();
-    }
     if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
     drain();
     stamp(x, kact, 8);
