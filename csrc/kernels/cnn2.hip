@@ -1056,6 +1056,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
 
   const int min_bs = a.min_bs;
   int kact = 0;
+  bool nan_seen = false;  // the last finished step's batch loss was NaN (abort at the next step's start)
   for (int s = 0; s < a.S; ++s) {
     const int bs = a.bsz[(long)s * a.C + c];
     if (bs < min_bs || bs < 1) continue;
@@ -1068,6 +1069,16 @@ __device__ __forceinline__ void head(const Ctx& x) {
     const int yb = min(m0 + li, B - 1);
     const int yrow = idxs[yb];
     const float yv = yrow >= 0 ? a.rows[(long)yrow * 24 + 23] : 0.f;
+    if (nan_seen) {  // the previous step's loss was NaN: status only, the client's round ends (towers read it)
+      if (tid == 0) {
+        for (int w = 0; w < 8; ++w) st16(x.rw, WS_STAT + 16 * w, u32x4{1u, (uint32_t)s, 0u, 0u});
+        a.failed[c] = 1;
+      }
+      arrive(x, CT_H);
+      if (tid == 0)
+        for (int w = 0; w < 8; ++w) __hip_atomic_fetch_add(x.ctr + (CT_HW + w) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     if (!wait_wave(x, CT_FW + wave, 3u * (uint32_t)(kact + 1))) break;  // 1 vitals + 2 labs tower workgroups
     REOPQ();
     stamp(x, kact, 0);
@@ -1211,23 +1222,11 @@ __device__ __forceinline__ void head(const Ctx& x) {
       sguard();
     }
     stamp(x, kact, 6);
-    SYNC();  // the only barrier before the hand-off: every wave's loss partial
-    stamp(x, kact, 7);
-    const float loss = ((red[0] + red[1]) + (red[2] + red[3]) + ((red[4] + red[5]) + (red[6] + red[7]))) / (float)max(bs, 1);
-    const bool nan = a.nan_abort && (loss != loss);
-    if (nan) {  // status only: no update this step, the client's round ends (towers read the status)
-      if (tid == 0) {
-        for (int w = 0; w < 8; ++w) st16(x.rw, WS_STAT + 16 * w, u32x4{1u, (uint32_t)s, 0u, 0u});
-        a.failed[c] = 1;
-      }
-      arrive(x, CT_H);
-      if (tid == 0)
-        for (int w = 0; w < 8; ++w) __hip_atomic_fetch_add(x.ctr + (CT_HW + w) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
-    // per-wave hand-off: this wave's status slot, drained with its d1 rows, then its counter — the tower
-    // workgroups of those rows start without waiting for the other waves
+    // per-wave hand-off with NO workgroup barrier: this wave's status slot, drained with its d1 rows, then its
+    // counter — the tower workgroups of those rows start without waiting for the other waves.  The batch loss
+    // (and its NaN test) is summed after the hand-off; a NaN step is caught at the next step's start, where
+    // the abort goes out through the same status slots (the failed client's round is discarded either way:
+    // the reference's client.py:100-102 abort, one step later on the device)
     if (lane == 0) st16(x.rw, WS_STAT + 16 * wave, u32x4{0u, (uint32_t)s, 0u, 0u});
     drain();
     stamp(x, kact, 8);
@@ -1235,6 +1234,11 @@ __device__ __forceinline__ void head(const Ctx& x) {
     arrive(x, CT_H);
     REOPQ();
     stamp(x, kact, 1);
+    {
+      const float loss = ((red[0] + red[1]) + (red[2] + red[3]) + ((red[4] + red[5]) + (red[6] + red[7]))) / (float)max(bs, 1);
+      if (a.nan_abort && loss != loss) nan_seen = true;
+      if (tid == 0) a.losses[(long)c * a.E + ep] += loss / (float)nbc;
+    }
     // ---- off the critical path: gb1 (d1 again in the row-major layout for its column sums), output-layer /
     // fc3 / fc2 bias sums, dW3
     {
@@ -1365,6 +1369,7 @@ __device__ __forceinline__ void head(const Ctx& x) {
     stamp(x, kact, 2);
     ++kact;
   }
+  if (nan_seen && tid == 0) a.failed[c] = 1;  // (a NaN loss on the round's last step)
   // round end: parameters -> arena
 #pragma unroll
   for (int j = 0; j < 4; ++j)

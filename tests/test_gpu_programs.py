@@ -419,3 +419,37 @@ def test_cnn2_sgd_gradients_match_composite(gpu, monkeypatch, B, drop):
         if vs_layer > 0.06 or vs_fp32 > 0.12:
             bad[s.name] = (round(vs_layer, 4), round(vs_fp32, 4))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("nan_at", ["first", "weights"])
+def test_cnn2_nan_loss_fails_only_that_client(gpu, monkeypatch, nan_at):
+    """A NaN batch loss aborts the client's round (reference client.py:100-102) on the on-chip CNN trainer: the
+    abort is detected after the hand-off and goes out at the next step's start (or at the round's end), the
+    other clients of the launch train normally and match their single-client runs."""
+    monkeypatch.setenv("AFL_CNN2", "1")
+    C, n, B = 3, 600, 64
+    ds = synthetic_icu(n)
+    order = torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(c))[:n] for c in range(C)])
+    plan = Plan(order[:, None, :].to(torch.int32), torch.tensor([n] * C, dtype=torch.int32), 1)
+    params = _params("CNNModel", C)
+    from attackfl_amd.models import ParamLayout
+
+    lay = ParamLayout.for_model("CNNModel")
+    s = lay.slots[[x.name for x in lay.slots].index("output.bias")]
+    params[1, s.offset] = float("nan") if nan_at == "weights" else 1e30  # client 1: NaN loss at step 1
+    if nan_at == "first":
+        s2 = lay.slots[[x.name for x in lay.slots].index("output.weight")]
+        params[1, s2.offset:s2.offset + s2.numel] = float("inf")
+    p = params.clone().to(DEV)
+    runner = ProgramRunner(make_program("CNNModel", C, B, DEV), use_graph=False)
+    assert runner._onchip_cnn(p, 0.0, None)
+    ok, losses = runner.train(DeviceTable(ds, DEV), p, Plan(plan.order.to(DEV), plan.nd, 1), lr=1e-3, seeds=[3, 4, 5])
+    ok = ok.cpu().tolist()
+    assert ok[1] == 0 and ok[0] == 1 and ok[2] == 1, ok
+    # the healthy clients are unaffected by the failing one (placement independence)
+    for c in (0, 2):
+        q = params[c:c + 1].clone().to(DEV)
+        r1 = ProgramRunner(make_program("CNNModel", 1, B, DEV), use_graph=False)
+        ok1, _ = r1.train(DeviceTable(ds, DEV), q, Plan(plan.order[c:c + 1].to(DEV), plan.nd[c:c + 1], 1), lr=1e-3,
+                          seeds=[3 + c])
+        assert bool(ok1.all()) and torch.equal(q[0], p[c])
