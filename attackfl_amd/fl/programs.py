@@ -328,6 +328,13 @@ class HARProgram(_Program):
         return self.buf(f"amask{i}", self.C * self.B * 4, int(ops.native().har_mask_words(self._lp())),
                         dtype=torch.int64)
 
+    def _kbits(self, i) -> torch.Tensor:
+        """Layer i's row-pass dropout keep bits (out_proj, FFN, linear2): written by ``har_post``, read by
+        ``har_post_bwd`` (64 B per row instead of 24 hashes per lane and row in the backward)."""
+        from .. import ops
+
+        return self.buf(f"kbits{i}", self.C, self.B * self.L, int(ops.native().har_kbits_per_row), dtype=torch.int32)
+
     def _post_seg(self, i) -> torch.Tensor:
         key = f"_seg_post{i}"
         if key not in self._bufs:
@@ -366,7 +373,8 @@ class HARProgram(_Program):
             nat.har_attn_fwd(qkv, o, lse2, B, L, seeds, stepctl, 10 * i, p, self._mask(i) if seeds is not None else None)
             y = self.buf(f"hb{i + 1}", C, R, 64, dtype=bf)
             nat.har_post(o, h, self.buf(f"xh1_{i}", C, R, 64, dtype=bf), self.buf(f"xh2_{i}", C, R, 64, dtype=bf),
-                         self.buf(f"rs{i}", C, R, 2), y, params, w, seeds, stepctl, 10 * i, p)
+                         self.buf(f"rs{i}", C, R, 2), y, params, w, seeds, stepctl, 10 * i, p,
+                         self._kbits(i) if seeds is not None else None)
             h = y
         pooled, c1, logits = self.buf("pool", C, B, 64), self.buf("c1", C, B, 64), self.buf("logits", C, B, 6)
         nat.har_pool(h, B, L, pooled)
@@ -401,7 +409,7 @@ class HARProgram(_Program):
             nat.har_post_bwd(dy, dpool if dy is None else None, B, L, self.buf(f"ob{i}", C, R, 64, dtype=bf),
                              self.buf(f"xh1_{i}", C, R, 64, dtype=bf), self.buf(f"xh2_{i}", C, R, 64, dtype=bf),
                              self.buf(f"rs{i}", C, R, 2), dres, dout, delta, ws_p, params, w, seeds, stepctl, 10 * i,
-                             p, G)
+                             p, G, self._kbits(i) if seeds is not None else None)
             nat.har_reduce(ws_p, G, int(nat.har_post_ng), self._post_seg(i), grads)
             nat.har_attn_bwd(self.buf(f"qkvb{i}", C * B * 4, 3, Lp, 16, dtype=bf), self.buf(f"lse2_{i}", C * B * 4, Lp),
                              dout, delta, dqkv, B, L, seeds, stepctl, 10 * i, p,

@@ -173,11 +173,14 @@ def main() -> int:
             **ckpt,
         }
         print(json.dumps(out), flush=True)
+        if out["rounds_ok"] < args.steps:
+            # a failed round skips its update and validation: a timing over failed rounds is not the metric
+            print(f"[bench] WARNING: only {out['rounds_ok']} of {args.steps} timed rounds succeeded", file=sys.stderr)
     eng.close()
     comm.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return 0 if (rank != 0 or any(r["ok"] for r in recs)) else 3  # no successful round: fail loudly
 
 
 if __name__ == "__main__":

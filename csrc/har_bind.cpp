@@ -90,9 +90,18 @@ void har_qkv(torch::Tensor x, torch::Tensor params, int64_t w_off, int64_t b_off
   ok(afl_har_qkv(a, cur()), "har_qkv");
 }
 
+// row-pass keep bits (written by har_post, read by har_post_bwd): int32 [C, R, AFL_HAR_KBITS_PER_ROW], dropout only
+unsigned* kbits_of(const c10::optional<torch::Tensor>& kb, int64_t C, int64_t R, bool drop) {
+  if (!drop) return nullptr;
+  TORCH_CHECK(kb.has_value() && kb->defined(), "row-pass dropout needs the keep-bit buffer");
+  TORCH_CHECK(kb->is_cuda() && kb->scalar_type() == torch::kInt32 && kb->is_contiguous(), "kbits: int32 cuda");
+  TORCH_CHECK(kb->numel() == C * R * AFL_HAR_KBITS_PER_ROW, "kbits must be [C, R, ", AFL_HAR_KBITS_PER_ROW, "]");
+  return (unsigned*)kb->data_ptr<int32_t>();
+}
+
 void har_post(torch::Tensor o, torch::Tensor x, torch::Tensor xh1, torch::Tensor xh2, torch::Tensor rs, torch::Tensor y,
               torch::Tensor params, std::vector<int64_t> w, c10::optional<torch::Tensor> seeds,
-              c10::optional<torch::Tensor> stepctl, int64_t layer, double p) {
+              c10::optional<torch::Tensor> stepctl, int64_t layer, double p, c10::optional<torch::Tensor> kbits) {
   const int64_t C = params.size(0), R = o.size(1);
   for (auto* t : {&o, &x, &xh1, &xh2, &y}) rows64(*t, C, R, "activation");
   TORCH_CHECK(rs.numel() == C * R * 2, "rs must be [C, R, 2]");
@@ -111,6 +120,7 @@ void har_post(torch::Tensor o, torch::Tensor x, torch::Tensor xh1, torch::Tensor
   a.d1 = drop(seeds, stepctl, layer + 1, p);
   a.df = drop(seeds, stepctl, layer + 2, p);
   a.d2 = drop(seeds, stepctl, layer + 3, p);
+  a.kbits = kbits_of(kbits, C, R, a.d1.thr16 || a.df.thr16 || a.d2.thr16);
   ok(afl_har_post(a, cur()), "har_post");
 }
 
@@ -168,7 +178,7 @@ void har_post_bwd(c10::optional<torch::Tensor> dy, c10::optional<torch::Tensor> 
                   torch::Tensor o, torch::Tensor xh1, torch::Tensor xh2, torch::Tensor rs, torch::Tensor dres,
                   torch::Tensor dout, torch::Tensor delta, torch::Tensor ws, torch::Tensor params, std::vector<int64_t> w,
                   c10::optional<torch::Tensor> seeds, c10::optional<torch::Tensor> stepctl, int64_t layer, double p,
-                  int64_t G) {
+                  int64_t G, c10::optional<torch::Tensor> kbits) {
   const int64_t C = params.size(0), R = B * L;
   for (auto* t : {&o, &xh1, &xh2, &dout}) rows64(*t, C, R, "activation");
   rows64(dres, C, R, "dres");
@@ -203,6 +213,7 @@ void har_post_bwd(c10::optional<torch::Tensor> dy, c10::optional<torch::Tensor> 
   a.d1 = drop(seeds, stepctl, layer + 1, p);
   a.df = drop(seeds, stepctl, layer + 2, p);
   a.d2 = drop(seeds, stepctl, layer + 3, p);
+  a.kbits = kbits_of(kbits, C, R, a.d1.thr16 || a.df.thr16 || a.d2.thr16);
   ok(afl_har_post_bwd(a, (int)G, cur()), "har_post_bwd");
 }
 
@@ -236,14 +247,20 @@ void afl_register_har(pybind11::module& m) {
   m.def("har_stem", &har_stem);
   m.def("har_pool", &har_pool);
   m.def("har_qkv", &har_qkv);
-  m.def("har_post", &har_post);
+  m.def("har_post", &har_post, py::arg("o"), py::arg("x"), py::arg("xh1"), py::arg("xh2"), py::arg("rs"), py::arg("y"),
+        py::arg("params"), py::arg("w"), py::arg("seeds"), py::arg("stepctl"), py::arg("layer"), py::arg("p"),
+        py::arg("kbits") = py::none());
+  m.attr("har_kbits_per_row") = py::int_(AFL_HAR_KBITS_PER_ROW);
   m.def("har_attn_fwd", &har_attn_fwd, py::arg("qkv"), py::arg("o"), py::arg("lse2"), py::arg("B"), py::arg("L"),
         py::arg("seeds"), py::arg("stepctl"), py::arg("layer"), py::arg("p"), py::arg("mask") = py::none());
   m.def("har_attn_bwd", &har_attn_bwd, py::arg("qkv"), py::arg("lse2"), py::arg("dout"), py::arg("delta"),
         py::arg("dqkv"), py::arg("B"), py::arg("L"), py::arg("seeds"), py::arg("stepctl"), py::arg("layer"),
         py::arg("p"), py::arg("mask") = py::none());
   m.def("har_mask_words", [](int64_t Lp) { return (int64_t)AFL_HAR_MASK_WORDS(Lp); });
-  m.def("har_post_bwd", &har_post_bwd);
+  m.def("har_post_bwd", &har_post_bwd, py::arg("dy"), py::arg("dpool"), py::arg("B"), py::arg("L"), py::arg("o"),
+        py::arg("xh1"), py::arg("xh2"), py::arg("rs"), py::arg("dres"), py::arg("dout"), py::arg("delta"), py::arg("ws"),
+        py::arg("params"), py::arg("w"), py::arg("seeds"), py::arg("stepctl"), py::arg("layer"), py::arg("p"),
+        py::arg("G"), py::arg("kbits") = py::none());
   m.def("har_qkv_bwd", &har_qkv_bwd);
   m.def("har_reduce", &har_reduce);
   m.def("har_blocks", [](int64_t R) { return afl_har_blocks(R); });

@@ -337,6 +337,8 @@ struct AflHarPost {
   const float* params; long P; AflHarLayerW w;
   int C; long R;
   AflDrop d1, df, d2;       // dropout1 (out_proj), FFN activation, dropout2 (linear2)
+  unsigned* kbits;          // [C][R][4 g][4] keep bits of the row pass (dropout only, else null): word 0 = d1 (bits
+                            // 0-15) | d2 (16-31), words 1-2 = the FFN's 64, word 3 unused; read back by the backward
 };
 struct AflHarPostB {
   const float* dy;          // [C][R][64] d(layer output) fp32 — or null with dpool set
@@ -352,6 +354,7 @@ struct AflHarPostB {
   const float* params; long P; AflHarLayerW w;
   int C; long R;
   AflDrop d1, df, d2;
+  const unsigned* kbits;    // the forward's keep bits (AflHarPost::kbits); null = no dropout
 };
 struct AflHarQkvB {
   const unsigned short* dqkv;  // [C*B*4][3][Lp][16] d(q|k|v projection outputs) (bf16)
@@ -376,6 +379,7 @@ struct AflHarAttn {
 };
 // keep words per (client, sample, head): [query tile Lp/16][key chunk Lp/64][t 4][e 4], bit = lane of the forward
 #define AFL_HAR_MASK_WORDS(Lp) ((long)((Lp) / 16) * ((Lp) / 64) * 16)
+#define AFL_HAR_KBITS_PER_ROW 16  // u32 words of AflHarPost::kbits per row
 #define AFL_HAR_POST_NG (64 * 64 + 256 * 64 + 64 * 256 + 640)
 #define AFL_HAR_QKV_NG (192 * 64 + 192)
 int afl_har_stem(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,

@@ -10,7 +10,8 @@
 //   k_har_attn_*   flash attention fwd / bwd on the head-major blocks (below)
 //   k_har_post     ONE row pass: out_proj + dropout + residual + LN1 -> linear1 + ReLU + dropout -> linear2
 //                  + dropout + residual + LN2; the 256-wide FFN activation never leaves registers (the
-//                  backward recomputes it); saves the two normalised LN inputs (bf16) and their rstd
+//                  backward recomputes it); saves the two normalised LN inputs (bf16), their rstd and the
+//                  row's dropout keep bits (16 B per lane: the backward does no hashing)
 //   k_har_post_bwd the matching backward row pass: LN2', FFN (recomputed), LN1', out_proj'; weight
 //                  gradients accumulated per workgroup in MFMA accumulators over ~35 64-row blocks (the dW
 //                  operands staged in XOR-swizzled LDS tiles, read with ds_read_b64_tr_b16), ordered
@@ -240,13 +241,13 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
     const long row = (long)c * R + (ok ? r : 0);
     // ---- a = Wo . o + bo, dropout1, residual, LayerNorm 1
     float s1[16];
+    uint32_t m1[1] = {0xFFFFFFFFu};
     {
       const u16* orow = a.o + row * 64;
       const s8v o0 = ldx8(orow, 0, g, ok), o1 = ldx8(orow, 1, g, ok);
       float xres[16], bo[16];
       ldt16(xres, a.x + row * 64, g, ok);
       vec16(bo, vec + V_BO * 4, g);
-      uint32_t m1[1] = {0xFFFFFFFFu};
       if (a.d1.thr16) keep_bits<4>(m1, k1, a.d1.layer, (uint32_t)r, g, a.d1.thr16);
       const float inv1 = a.d1.thr16 ? a.d1.inv_keep : 1.f;
 #pragma unroll
@@ -273,9 +274,9 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
     //      exactly linear2's B fragment of k-step s, consumed at once (the 256-wide activation is never
     //      materialised), then y = W2 . f + b2, dropout2, residual
     float s2[16];
+    uint32_t mf[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, m2[1] = {0xFFFFFFFFu};
     {
       const s8v b0 = bfrag(h1, 0), b1 = bfrag(h1, 1);
-      uint32_t mf[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
       if (a.df.thr16) ffn_bits(mf, kf_, a.df.layer, (uint32_t)r, g, a.df.thr16);
       const float invf = a.df.thr16 ? a.df.inv_keep : 1.f;
       f4v acc2[4] = {Z4, Z4, Z4, Z4};
@@ -302,7 +303,6 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
       sb();
       float b2[16];
       vec16(b2, vec + V_B2 * 4, g);
-      uint32_t m2[1] = {0xFFFFFFFFu};
       if (a.d2.thr16) keep_bits<4>(m2, k2, a.d2.layer, (uint32_t)r, g, a.d2.thr16);
       const float inv2 = a.d2.thr16 ? a.d2.inv_keep : 1.f;
 #pragma unroll
@@ -311,6 +311,8 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
         for (int i = 0; i < 4; ++i) s2[4 * T + i] = h1[4 * T + i] + kf(acc2[T][i] + b2[4 * T + i], m2, 4 * T + i, inv2);
     }
     const float rstd2 = ln_fwd2(s2);
+    if (ok && a.kbits)  // the keep bits for the backward (one 16-byte store per lane: no hashing there)
+      *(u32x4*)(a.kbits + (row * 4 + g) * 4) = u32x4{(m1[0] & 0xFFFFu) | (m2[0] << 16), mf[0], mf[1], 0u};
     if (ok) {
       stt16(a.xh2 + row * 64, s2, g);
       if (g == 0) a.rs[row * 2 + 1] = rstd2;
@@ -581,12 +583,11 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
 }
 
 // ---- dQ: each wave owns 16 queries and sweeps the keys (recomputing S and dP; no atomics) ----
-// x where bit `lane` of the wave-uniform 64-bit keep word m is set, else 0 (one v_cndmask on an SGPR-pair mask)
-__device__ __forceinline__ float keep_sel(uint64_t m, float x) {
-  float r;
-  asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
-  return r;
-}
+// x where bit `lane` of the wave-uniform 64-bit keep word m is set, else 0 (one v_cndmask on an SGPR-pair mask).
+// Not inline asm: the compiler's hazard recognizer does not pad an asm VALU that reads an MFMA result, and the
+// v_cndmask read the dP accumulator a few cycles after its MFMA issued (garbage, NaN dQ in whole 16-row tiles,
+// nondeterministically); inverse_ballot gives the same single instruction with the wait states inserted.
+__device__ __forceinline__ float keep_sel(uint64_t m, float x) { return __builtin_amdgcn_inverse_ballot_w64(m) ? x : 0.f; }
 template <bool DROP>
 __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
@@ -696,7 +697,6 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
   post_vectors(smem, pp, a.w);
   __syncthreads();
   const uchar* vec = smem + PB_VEC;
-  const uint32_t k1 = dkey(a.d1, c), kff = dkey(a.df, c), k2 = dkey(a.d2, c);
   const float inv1 = a.d1.thr16 ? a.d1.inv_keep : 1.f, invf = a.df.thr16 ? a.df.inv_keep : 1.f,
               inv2 = a.d2.thr16 ? a.d2.inv_keep : 1.f;
   const long R = a.R;
@@ -712,6 +712,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
   struct In {
     f4v dy[4];
     u32x2v xh2[4], xh1[4], o[4];
+    u32x4 kb;  // the forward's keep bits (all set without dropout)
     float rs1, rs2;
   };
   auto load = [&](int blk, In& in) {
@@ -725,6 +726,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
       in.xh1[t] = ok ? *(const u32x2v*)(a.xh1 + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
       in.o[t] = ok ? *(const u32x2v*)(a.o + row * 64 + 16 * t + 4 * g) : u32x2v{0u, 0u};
     }
+    in.kb = (ok && a.kbits) ? *(const u32x4*)(a.kbits + (row * 4 + g) * 4) : u32x4{~0u, ~0u, ~0u, ~0u};
     in.rs1 = ok ? a.rs[row * 2] : 0.f;
     in.rs2 = ok ? a.rs[row * 2 + 1] : 0.f;
   };
@@ -781,8 +783,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
     ln_bwd2(ds2, dy, xh2, rstd2, gm);
     float df2[16];
     {
-      uint32_t m2[1] = {0xFFFFFFFFu};
-      if (a.d2.thr16) keep_bits<4>(m2, k2, a.d2.layer, (uint32_t)r, g, a.d2.thr16);
+      const uint32_t m2[1] = {cur.kb[0] >> 16};
 #pragma unroll
       for (int j = 0; j < 16; ++j) df2[j] = kf(ds2[j], m2, j, inv2);
     }
@@ -797,8 +798,8 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
       vec16(b1, vec + V_BE1 * 4, g);
       affine2(h1, xh1, g1, b1);
     }
-    uint32_t mf[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, relu[2] = {0u, 0u};
-    if (a.df.thr16) ffn_bits(mf, kff, a.df.layer, (uint32_t)r, g, a.df.thr16);
+    const uint32_t mf[2] = {cur.kb[1], cur.kb[2]};
+    uint32_t relu[2] = {0u, 0u};
     {
       const s8v b0 = bfrag(h1, 0), b1 = bfrag(h1, 1);
 #pragma unroll
@@ -901,14 +902,14 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
     ln_bwd2(ds1, dh1, xh1, rstd1, gm);
     if (ok) stt16f(a.dres + row * 64, ds1, g);
     {
-      uint32_t m1[1] = {0xFFFFFFFFu};
-      if (a.d1.thr16) keep_bits<4>(m1, k1, a.d1.layer, (uint32_t)r, g, a.d1.thr16);
+      const uint32_t m1[1] = {cur.kb[0]};
 #pragma unroll
       for (int j = 0; j < 16; ++j) da[j] = kf(ds1[j], m1, j, inv1);
     }
     csum_add(cbo, da, lane);
     unbf(ov, cur.o);
-    __syncthreads();  // (the dW1 reads of H1 / F are done: DA / O live elsewhere, but keep the phases ordered)
+    // (no barrier: DA / O are not read before the next one, and the previous block's dWo reads of them are
+    // ordered by this block's first barrier)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       st4<TK64>(smem + PB_DA, rl, 4 * t + g, da + 4 * t);
@@ -1185,7 +1186,7 @@ int afl_har_post_bwd(const AflHarPostB& a, int G, hipStream_t s) {
       return -2;
     attr = true;
   }
-  if (G < 1) return (int)hipErrorInvalidValue;
+  if (G < 1 || ((a.d1.thr16 || a.df.thr16 || a.d2.thr16) && !a.kbits)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_har_post_bwd, dim3(G, a.C), dim3(NTR), PB_SMEM, s, a);
   return (int)hipGetLastError();
 }
@@ -1208,6 +1209,7 @@ int afl_har_post(const AflHarPost& a, hipStream_t s) {
       return -2;
     attr = true;
   }
+  if ((a.d1.thr16 || a.df.thr16 || a.d2.thr16) && !a.kbits) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_har_post, dim3(har_blocks(a.R, a.C), a.C), dim3(NTF), PF_SMEM, s, a);
   return (int)hipGetLastError();
 }

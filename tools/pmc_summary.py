@@ -19,7 +19,7 @@ def load(root):
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                k = row.get("Kernel_Name", "?")
+                k = row.get("Kernel_Name", "?").replace("(anonymous namespace)::", "")
                 tot[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 disp[k].add(row.get("Dispatch_Id", ""))
     return tot, disp
