@@ -36,14 +36,17 @@ def main():
     names = sorted((k for k in tot if not want or any(w in k for w in want)),
                    key=lambda k: -tot[k].get("SQ_WAVE_CYCLES", 0.0))
     print(f"# {a.title}\n")
-    print("| kernel | dispatches | VALU:MFMA | VALU busy | MFMA busy | wait / wave-cycles | LDS conflicts / LDS inst |")
+    print("VALU / wave-cycles = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of a wave's cycles spent issuing VALU); "
+          "MFMA busy / busy = SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES (raw counter ratio: the two count in different "
+          "units, compare it between kernels only).\n")
+    print("| kernel | dispatches | VALU:MFMA | VALU / wave-cycles | MFMA busy / busy | wait / wave-cycles | LDS conflicts / LDS inst |")
     print("|---|---|---|---|---|---|---|")
     for k in names:
         c = tot[k]
         g = lambda n: c.get(n, 0.0)
         ratio = g("SQ_INSTS_VALU") / g("SQ_INSTS_MFMA") if g("SQ_INSTS_MFMA") else float("nan")
         busy = g("SQ_BUSY_CYCLES") or float("nan")
-        vb = g("SQ_ACTIVE_INST_VALU") / busy
+        vb = g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES") if g("SQ_WAVE_CYCLES") else float("nan")
         mb = g("SQ_VALU_MFMA_BUSY_CYCLES") / busy
         wt = g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES") if g("SQ_WAVE_CYCLES") else float("nan")
         lc = g("SQ_LDS_BANK_CONFLICT") / g("SQ_INSTS_LDS") if g("SQ_INSTS_LDS") else float("nan")
