@@ -26,3 +26,15 @@ def test_checker_flags_the_pattern(tmp_path):
                    "\tglobal_store_dwordx4 v[0:1], v[4:7], off\n\ts_nop 0\n\tv_mov_b32_e32 v4, v1\n")
     hits = chk.scan(str(asm))
     assert len(hits) == 1 and "v22" in hits[0][1]
+
+
+def test_checker_flags_asm_reading_a_fresh_mfma_result(tmp_path):
+    import check_store_hazard as chk
+
+    asm = tmp_path / "k.s"
+    asm.write_text("\tv_mfma_f32_16x16x16_bf16 v[44:47], v[36:37], v[18:19], 0\n\tv_mov_b32_e32 v1, v2\n"
+                   "\t;;#ASMSTART\n\tv_cndmask_b32 v44, 0, v44, s[24:25]\n\t;;#ASMEND\n"
+                   "\tv_mfma_f32_16x16x16_bf16 v[8:11], v[36:37], v[18:19], 0\n\ts_nop 15\n\ts_nop 7\n"
+                   "\t;;#ASMSTART\n\tv_cndmask_b32 v9, 0, v8, s[24:25]\n\t;;#ASMEND\n")
+    hits = chk.scan_asm_mfma(str(asm))
+    assert len(hits) == 1 and "v44" in hits[0][0] and hits[0][2] == 1

@@ -4,6 +4,11 @@ them (observed on MI355X: rnn2.hip's moment stores picked up the next v_mov's va
 lanes; the backend inserted no wait state).  Compiles every csrc/kernels/*.hip to gfx950 assembly with the
 build's flags and lists each store whose data registers the following instruction overwrites.
 
+Second audit (round 4): an inline-asm instruction that READS the result of a recent `v_mfma`.  The compiler
+pads its own VALU reads of an MFMA result with the required wait states, but not an asm block's (har.hip's
+first dQ keep select, an asm `v_cndmask`, read the dP accumulator two instructions after its MFMA and
+returned garbage).  Flagged: an asm source VGPR that an MFMA wrote fewer than MFMA_WAIT wait states earlier.
+
     python tools/check_store_hazard.py [file.hip ...]
 """
 import glob
@@ -61,6 +66,59 @@ def scan(asm_path):
     return hits
 
 
+MFMA_WAIT = 19  # the longest MFMA result latency (32x32, 16 passes) plus margin, in wait states
+
+
+def src_regs(line):
+    """source VGPR / AGPR names of an instruction line (every operand after the destination)"""
+    m = INSN.match(line)
+    if not m:
+        return set()
+    out = set()
+    for op in (m.group(3) or "").split(",")[1:]:
+        out |= regs(op.strip().split()[0]) if op.strip() else set()
+    return out
+
+
+def scan_asm_mfma(asm_path):
+    """(asm line, mfma line, wait states) for every inline-asm read of a too-recent MFMA result"""
+    recent = []  # [(dest regs, mfma line, wait states since)]
+    hits = []
+    in_asm = False
+    for raw in open(asm_path):
+        l = raw.rstrip()
+        st = l.strip()
+        if st.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if st.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not st or st.startswith((";", ".", "//")) or st.endswith(":"):
+            if st.endswith(":"):
+                recent = []  # a label: control flow merges, stay conservative only within a block
+            continue
+        m = INSN.match(l)
+        if not m:
+            continue
+        if in_asm:
+            srcs = src_regs(l)
+            for dr, ml, w in recent:
+                if dr & srcs:
+                    hits.append((st, ml, w))
+        ws = 1
+        if m.group(1) == "s_nop":
+            try:
+                ws = int((m.group(3) or "0").split()[0], 0) + 1
+            except ValueError:
+                ws = 1
+        recent = [(dr, ml, w + ws) for dr, ml, w in recent if w + ws < MFMA_WAIT]
+        if m.group(1).startswith("v_mfma"):
+            ops = (m.group(3) or "").split(",")
+            recent.append((regs(ops[0].strip()), st, 0))
+    return hits
+
+
 def check_file(f):
     extra = ["-mllvm", "-amdgpu-mfma-vgpr-form"] if os.path.basename(f).startswith(("tf2", "rnn2")) else []
     with tempfile.TemporaryDirectory() as td:
@@ -71,7 +129,7 @@ def check_file(f):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             return None
-        return scan(out)
+        return scan(out) + [(a, f"{m}  ({w} wait states)") for a, m, w in scan_asm_mfma(out)]
 
 
 def main(files=None, jobs=8):

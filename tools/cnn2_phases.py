@@ -75,8 +75,8 @@ def main():
         rows[name] = [float((towers[c, :, k, b] - towers[c, :, k, a]).max()) for c in range(C) for k in range(8, 63)]
     # the head's own timeline (wave 0): z1 partial loads + ReLU, fc2 + fc3, output + BCE + d3, d2 + d1 (in
     # registers), the loss barrier, the d1 write-through stores + drain, the hand-off counters
-    hfine = {"h.z1": (0, 3), "h.fc2+fc3": (3, 4), "h.out+d3": (4, 5), "h.d2+d1": (5, 6), "h.loss_bar": (6, 7),
-             "h.store+drain": (7, 8), "h.arrive": (8, 1)}
+    hfine = {"h.z1": (0, 3), "h.fc2+fc3": (3, 4), "h.out+d3": (4, 5), "h.d2+d1": (5, 6),
+             "h.status+drain": (6, 8), "h.arrive": (8, 1)}  # (no loss barrier since the NaN check moved after it)
     if bool((headr[:, 8:63, 8] != 0).all()):
         for name, (a, b) in hfine.items():
             rows[name] = [float(headr[c, k, b] - headr[c, k, a]) for c in range(C) for k in range(8, 63)]
