@@ -285,3 +285,31 @@ def test_hyper_detection_end_to_end(gpu, tmp_path):
     assert sum(r["ok"] for r in hist) == 19
     assert os.path.exists(os.path.join(tmp_path, "all_embeddings.npy"))
     assert all(isinstance(r["removed"], list) for r in hist)
+
+
+def test_hyper_detection_rollback_before_validation_on_device(gpu, tmp_path):
+    """GPU twin of test_engine.py's rollback test: a forced removal rolls the hypernetwork back BEFORE
+    validation (reference server.py:532-543), so the logged metric equals test_hyper of the rolled-back arena
+    bit for bit, and the removed client is not selected afterwards."""
+    import torch
+
+    d = {
+        "server": {"num-round": 3, "clients": 4, "mode": "hyper", "model": "TransformerModel", "data-name": "ICU",
+                   "hyper-detection": {"enable": True, "cosine-search": 10, "n_components": 2, "eps": 0.5,
+                                       "min_samples": 2},
+                   "data-distribution": {"num-data-range": [200, 300]}},
+        "learning": {"epoch": 1, "batch-size": 128},
+        "data": {"synthetic": True, "train-size": 3000, "test-size": 500},
+        "engine": {"checkpoint-dir": str(tmp_path), "trainer": "auto"},
+        "log_path": str(tmp_path),
+    }
+    eng = FLEngine(from_dict(d), device="cuda", verbose=False)
+    eng.run_round()
+    before = eng.hyper.snapshot().clone()
+    eng.detector.step = lambda rnd, sel, embs: [3]  # force a removal this round
+    rec = eng.run_round()
+    assert rec["removed"] == [3] and eng.selected == [0, 1, 2]
+    assert torch.equal(eng.hyper.hnet.arena, before)
+    ok, auc = eng.validation.test_hyper(eng.hyper, 4)
+    assert rec["ok"] and ok and rec["metric"] == auc
+    eng.close()
