@@ -559,7 +559,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
       *lu16(S, O_H1 + ((q + 1) * LD1 + o1) * 2) = bfu(h);
     }
     SYNC();
+#ifndef CNN2_DIAG2
     stamp(x, kact, 7);
+#endif
     // conv2: H2[q][o] = relu(b2 + sum_j H1[q - 1 + j] . W2_j^T); wave: n-tile nt2, m-tiles mp2, mp2 + 2, ...
     // (two m-tiles per pass: independent accumulator chains interleave; a tile past 8 computes on zero rows and is
     // not stored)
@@ -841,6 +843,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         for (int e = 0; e < 4; ++e)
           *(LDS_AS f4v*)(S + O_RED + (R_C1 + (wave * 16 + 4 * g + e) * 4) * 4) = f4v{s0[e], s1[e], s2[e], sb[e]};
     }
+#ifdef CNN2_DIAG2  // sub-phases of the dh1 + dW phase (slot 15: dh1 done; slot 7: dW3 done)
+    stamp(x, kact, 15);
+#endif
     // dW3_j = dh3^T . shift_{j-1}(h2) (K = 160 rows: 144 + zero rows).  Wave: o-tiles 2 (w & 3) + {0, 1} x six of
     // the twelve (tap, ci-tile) blocks (w >> 2 picks the half): per k-step 2 + 6 transposed fragment reads for 12
     // MFMAs (was 1 + 12 with one o-tile per wave)
@@ -870,6 +875,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
           st16f(x.rw, pbase + (P_W3 + ((j * 16 + 2 * (ob + oi) + (g >> 1)) * 64 + ci) * 8 + 4 * (g & 1)) * 4, acc[oi][t]);
         }
     }
+#ifdef CNN2_DIAG2
+    stamp(x, kact, 7);
+#endif
     // dW2_j = dh2^T . shift_{j-1}(h1): wave -> o-tile (w & 3), ci-tile (w >> 2)
     {
       const int ot = wave & 3, ct = wave >> 2;

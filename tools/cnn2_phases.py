@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--rows", type=int, default=13000)
+    ap.add_argument("--diag2", action="store_true", help="a -DCNN2_DIAG2 build: split b.dh1+dW into dh1 / dW3 / dW2")
     args = ap.parse_args()
     C, dev = args.clients, "cuda"
     ds = synthetic_icu(max(20000, args.rows + 1))
@@ -68,9 +69,13 @@ def main():
             rows["step"].append(float(tn[:, 0].min() - t[:, 0].min()))
     fine = {"f.inputs+conv1": (0, 7), "f.conv2": (7, 14), "f.conv3": (14, 8), "o.wait+loads(diag)": (4, 15), "o.adam+publish(diag)": (15, 5), "o.arrive": (5, 6), "f.pool": (8, 9), "f.fc1+publish": (9, 1),
             "b.d1+dfeat": (2, 10), "b.dh3": (10, 11), "b.dh2": (11, 12), "b.dh1+dW": (12, 13), "b.partials": (13, 3)}
-    if not bool((towers[:, :, 8:63, 15] != 0).all()):  # stamp 15 only in -DCNN2_DIAG builds
+    if args.diag2 or not bool((towers[:, :, 8:63, 15] != 0).all()):  # stamp 15 only in -DCNN2_DIAG builds
         fine.pop("o.wait+loads(diag)")
         fine.pop("o.adam+publish(diag)")
+    if args.diag2:  # slot 15 = dh1 done, slot 7 = dW3 done (f.inputs+conv1 / f.conv2 are not stamped then)
+        for k in ("f.inputs+conv1", "f.conv2", "f.conv3", "o.wait+loads(diag)", "o.adam+publish(diag)"):
+            fine.pop(k, None)
+        fine.update({"b.dh1": (12, 15), "b.dW3": (15, 7), "b.dW2+sync": (7, 13)})
     for name, (a, b) in fine.items():
         rows[name] = [float((towers[c, :, k, b] - towers[c, :, k, a]).max()) for c in range(C) for k in range(8, 63)]
     # the head's own timeline (wave 0): z1 partial loads + ReLU, fc2 + fc3, output + BCE + d3, d2 + d1 (in
