@@ -578,6 +578,14 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
           *(LDS_AS u32x2v*)(S + O_H2 + ((q + 1) * LD2 + 16 * nt2 + 4 * g) * 2) = relu_pack4(acc[t], b2v, valid_q(q, C::LP));
       }
     }
+    // fc1 B fragments (this tower's half of W1, n-tile = wave; the owners' images of this step), issued before
+    // conv3: the 128 KB per workgroup take ~2.7 us to issue whatever phase they land in (every tower of every
+    // client reads its half at once), and before conv3 they overlap its MFMA / LDS work (fwd 12.2 -> 11.5 us)
+    const int par = kact & 1;
+    s8v wf1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      wf1[k] = ld16s(x.rw, WS_IMG + (IM_W1 + par * IM_FC1PAR + (16 * wave + li) * 1024 + C::COL0 + 32 * k + 8 * g) * 2);
     SYNC();
     stamp(x, kact, 14);
     // conv3: wave = n-tile, all 9 m-tiles
@@ -596,13 +604,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         *(LDS_AS u32x2v*)(S + O_H3 + ((q + 1) * LD3 + 16 * wave + 4 * g) * 2) = relu_pack4(acc[t], b3v, valid_q(q, C::LP));
       }
     }
-    // fc1 B fragments (this tower's half of W1, n-tile = wave; the owners' images of this step), in flight during
-    // the pooling
-    const int par = kact & 1;
-    s8v wf1[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      wf1[k] = ld16s(x.rw, WS_IMG + (IM_W1 + par * IM_FC1PAR + (16 * wave + li) * 1024 + C::COL0 + 32 * k + 8 * g) * 2);
     SYNC();
     stamp(x, kact, 8);
     // AdaptiveAvgPool1d(4) + dropout -> feat (LDS bf16 rows 0..15, zero past R) and the global concat.  Thread:
