@@ -189,32 +189,6 @@ __device__ __forceinline__ void arrive(const Ctx& x, int which) {
   __syncthreads();
   if (x.tid == 0) __hip_atomic_fetch_add(x.ctr + which * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// true when counter `which` reached `target` and counter `w2` reached `t2` (both polled in one round trip);
-// false (all threads) on the deadline
-__device__ __forceinline__ bool wait_ge2(const Ctx& x, int which, uint32_t target, int w2, uint32_t t2, int flag_off) {
-  LDS_AS int* fl = (LDS_AS int*)(x.smem + flag_off);
-  if (x.tid == 0) {
-    int ok = 1;
-    const long t0 = (long)__builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      const uint32_t v1 = __hip_atomic_load(x.ctr + which * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t v2 = __hip_atomic_load(x.ctr + w2 * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v1 >= target && v2 >= t2) break;
-      if ((long)__builtin_amdgcn_s_memrealtime() - t0 > DEADLINE) {
-        ok = 0;
-        __hip_atomic_store(x.ctr + CT_TMO * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        x.a->failed[x.c] = 2;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    fl[0] = ok;
-  }
-  lbar();
-  const int ok = fl[0];
-  lbar();
-  return ok != 0;
-}
 // true when the counter reached `target`; false (all threads) on the deadline
 __device__ __forceinline__ bool wait_ge(const Ctx& x, int which, uint32_t target, int flag_off) {
   LDS_AS int* fl = (LDS_AS int*)(x.smem + flag_off);
@@ -503,8 +477,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     const int bs = a.bsz[(long)s * a.C + c];
     if (bs < min_bs || bs < 1) continue;
     const float xv = xv_next;
-    // this step's conv images (tower group) and fc1 images (fc1 owners: normally long done), one poll
-    if (!wait_ge2(x, CT_W + T, (uint32_t)(C::NTW * (kact + 1)), CT_W1R, (uint32_t)(NFC1 * (kact + 1)), O_FLAG)) break;
+    // this step's conv images; the fc1 owners' images are awaited only before their first use (conv3): with the
+    // shorter tower backward the fc1 owners finish close to the step start (one poll for both: +1 us per step)
+    if (!wait_ge(x, CT_W + T, (uint32_t)(C::NTW * (kact + 1)), O_FLAG)) break;
     REOPQ();
     stamp(x, kact, 0);
     // ------------------------------------------------------------------------------ forward
@@ -582,6 +557,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     // conv3: the 128 KB per workgroup take ~2.7 us to issue whatever phase they land in (every tower of every
     // client reads its half at once), and before conv3 they overlap its MFMA / LDS work (fwd 12.2 -> 11.5 us)
     const int par = kact & 1;
+    if (!wait_ge(x, CT_W1R, (uint32_t)(NFC1 * (kact + 1)), O_FLAG)) break;
     s8v wf1[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -680,6 +656,18 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     for (int k = 0; k < 16; ++k)
       wt1[k] = ld16s(x.rw, WS_IMG + (IM_W1T + par * IM_FC1PAR + (C::COL0 + 16 * (4 * wave + (k >> 2)) + li) * 128 +
                                     32 * (k & 3) + 8 * g) * 2);
+    // the W3T / W2T fragments of the backward too, issued while the tower only waits for the head (their ~2 us
+    // of issue landed in the d1 + dfeat and dh2 phases: tower backward 15.1 -> 13.0 us)
+    const int nb2 = wave & 3, mpb = wave >> 2;
+    s8v w3t[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      w3t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3T + ((k >> 2) * 64 + 16 * nb2 + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
+    const int nb1 = wave & 1, mpa = wave >> 1;
+    s8v w2t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      w2t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W2T + ((k >> 1) * 32 + 16 * nb1 + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
     // ------------------------------------------------------------------------------ backward
     const int hw = T == 0 ? i : (i >> 1);  // the head wave that computes this workgroup's d1 rows
     if (!wait_ge(x, CT_HW + hw, (uint32_t)(kact + 1), O_FLAG)) break;
@@ -714,12 +702,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) *lf(S, O_FT + ((4 * g + e) * 516 + 16 * (4 * wave + t) + li) * 4) = acc[t][e];
     }
-    // W3T fragments of d(h2), in flight behind the pooling gradient
-    const int nb2 = wave & 3, mpb = wave >> 2;
-    s8v w3t[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k)
-      w3t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W3T + ((k >> 2) * 64 + 16 * nb2 + li) * 128 + 32 * (k & 3) + 8 * g) * 2);
     SYNC();
     stamp(x, kact, 10);
     // dh3 = relu'(h3) * pool'(dropout'(dfeat)), in place over H3 (bf16).  Thread: (row r, channel pair cp) like the
@@ -795,12 +777,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
         for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
       if (li == 0) *(LDS_AS f4v*)(S + O_RED + (R_DB2 + wave * 16 + 4 * g) * 4) = cs;
     }
-    // W2T fragments of d(h1)
-    const int nb1 = wave & 1, mpa = wave >> 1;
-    s8v w2t[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      w2t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W2T + ((k >> 1) * 32 + 16 * nb1 + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
     SYNC();
     stamp(x, kact, 12);
     // dh1 = relu'(h1) * sum_j shift_{1-j}(dh2) . W2_j (K = 3 x 64), straight into the conv1 gradients
