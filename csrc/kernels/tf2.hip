@@ -577,20 +577,14 @@ __device__ __forceinline__ int cmp_img(int e) {
 // entries' at the start of U2 (used in U3); each set is stored back right after its Adam step.
 template <int BR>
 __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid,
-                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp) {
+                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, f4v (&bm)[4], f4v (&bv)[4]) {
   using B = BrK<BR>;
   opq(lane, wave);
   asm volatile("" : "+v"(tid));
   using C = Cmp<BR>;
   const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
   const bool lo = wave < 4;
-  // ---- U1
-  f4v bm[4], bv[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    bm[k] = mom_ld(rm, k, tid);
-    bv[k] = mom_ld(rm, 4 + k, tid);
-  }
+  // ---- U1 (the block tiles' moments bm / bv were issued by the caller)
   f4v as = Z4, af1 = Z4;
   {
     // waves 0-3: dense tile (k 0..15, n tile w4): X = xin, dY = dz0 ; waves 4-7: ffn.3 tile: X = f2, dY = d f3
@@ -876,6 +870,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     float dout[16];
     unpack16(du, dout);
     if (lane == 0) abort_w[wave] = fv & 1u;
+    f4v bm[4], bv[4];  // the U1 / U2 block tiles' Adam moments (issued before the backward: measured slower)
 #ifndef TF2_NO_BWD
     asm volatile(";MARK bwd");
     br_backward<BR>(smem, dout, sv, K, lane, wave);
@@ -893,9 +888,14 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       break;
     }
     stp(4, tid);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bm[k] = mom_ld(rm, k, tid);
+      bv[k] = mom_ld(rm, 4 + k, tid);
+    }
 #ifndef TF2_NO_UPD
     asm volatile(";MARK upd");
-    br_update<BR>(smem, st, K, lane, wave, tid, rm, stp);
+    br_update<BR>(smem, st, K, lane, wave, tid, rm, stp, bm, bv);
     asm volatile(";MARK upd_end");
 #endif
     stp(7, tid);
