@@ -457,12 +457,18 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_fwd(AflHarAttn a) {
       for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
       const float mn = fmaxf(m, max_x16_x32(mx));
       const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      float ps = 0.f, pd[16];
+      // (pairs: v_pk_add_f32 for the shift and the row sum)
+      float pd[16];
+      of2v ps2 = of2v{0.f, 0.f};
+      const of2v mn2 = of2v{mn, mn};
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        pd[j] = __builtin_amdgcn_exp2f(s[j] - mn);
-        ps += pd[j];
+      for (int j = 0; j < 16; j += 2) {
+        const of2v d = of2v{s[j], s[j + 1]} - mn2;
+        pd[j] = __builtin_amdgcn_exp2f(d[0]);
+        pd[j + 1] = __builtin_amdgcn_exp2f(d[1]);
+        ps2 += of2v{pd[j], pd[j + 1]};
       }
+      const float ps = ps2[0] + ps2[1];
       if (DROP) {
         // keep word (t, e) = ballot of the flags of keys kt + 16t + 4g + e over the wave (bit = lane): lanes 0..31
         // of mw collect the chunk's 16 words, stored for both backward kernels (no hashing there)
@@ -559,13 +565,20 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_kv(AflHarAttn a) {
         const f4v d4 = *(const LDS_AS f4v*)(DL + qb + 4 * g);
         const uint32_t wd = wc[qs];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; e += 2) {
           // (keys >= L need no mask: a lane's values only reach its own key's dK / dV column, never stored)
-          const float p = __builtin_amdgcn_exp2f(s[e] - l4[e]);
+          // (pairs: v_pk_add / v_pk_fma / v_pk_mul for the shift, dP - Delta and the product)
+          const of2v sh2 = of2v{s[e], s[e + 1]} - of2v{l4[e], l4[e + 1]};
+          const of2v p = of2v{__builtin_amdgcn_exp2f(sh2[0]), __builtin_amdgcn_exp2f(sh2[1])};
           // keep flag -> all-ones / zero word (sign-extended one-bit field)
-          const uint32_t km = DROP ? (uint32_t)__builtin_amdgcn_sbfe((int)wd, (sh & 31) + e, 1) : 0xFFFFFFFFu;
-          pdv[4 * qs + e] = __uint_as_float(__float_as_uint(p) & km);  // (x 1/(1-p) on dV at the end)
-          dsv[4 * qs + e] = p * fmaf(__uint_as_float(__float_as_uint(dp[e]) & km), ik, -d4[e]);
+          const uint32_t km0 = DROP ? (uint32_t)__builtin_amdgcn_sbfe((int)wd, (sh & 31) + e, 1) : 0xFFFFFFFFu;
+          const uint32_t km1 = DROP ? (uint32_t)__builtin_amdgcn_sbfe((int)wd, (sh & 31) + e + 1, 1) : 0xFFFFFFFFu;
+          pdv[4 * qs + e] = __uint_as_float(__float_as_uint(p[0]) & km0);  // (x 1/(1-p) on dV at the end)
+          pdv[4 * qs + e + 1] = __uint_as_float(__float_as_uint(p[1]) & km1);
+          const of2v dpm = of2v{__uint_as_float(__float_as_uint(dp[e]) & km0), __uint_as_float(__float_as_uint(dp[e + 1]) & km1)};
+          const of2v ds = p * (dpm * of2v{ik, ik} - of2v{d4[e], d4[e + 1]});
+          dsv[4 * qs + e] = ds[0];
+          dsv[4 * qs + e + 1] = ds[1];
         }
       }
       // dV^T[d][key] += dO^T[d][q] Pd[q][key] ; dK^T[d][key] += Q_s^T[d][q] dS[q][key] (query order permuted)
@@ -633,15 +646,24 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
         }
       }
       float ds[8];
+      const of2v ls2 = of2v{ls, ls}, dl2 = of2v{dl, dl}, ik2 = of2v{ik, ik};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kk = kt + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
-        const float sv = j < 4 ? s0[j] : s1[j - 4];
-        float dp = j < 4 ? p0[j] : p1[j - 4];
-        if (DROP) dp = keep_sel(mw[j], dp);
-        float p = __builtin_amdgcn_exp2f(sv - ls);
-        if constexpr (decltype(tail)::value) p = kk < L ? p : 0.f;  // keys >= L: last step only
-        ds[j] = p * fmaf(dp, ik, -dl);
+      for (int j = 0; j < 8; j += 2) {  // (pairs: v_pk_add / v_pk_fma / v_pk_mul)
+        const of2v sv = j < 4 ? of2v{s0[j], s0[j + 1]} : of2v{s1[j - 4], s1[j - 3]};
+        of2v dp = j < 4 ? of2v{p0[j], p0[j + 1]} : of2v{p1[j - 4], p1[j - 3]};
+        if (DROP) dp = of2v{keep_sel(mw[j], dp[0]), keep_sel(mw[j + 1], dp[1])};
+        const of2v sh2 = sv - ls2;
+        of2v p = of2v{__builtin_amdgcn_exp2f(sh2[0]), __builtin_amdgcn_exp2f(sh2[1])};
+        if constexpr (decltype(tail)::value) {  // keys >= L: last step only
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int kk = kt + (j + h < 4 ? 4 * g + j + h : 16 + 4 * g + j + h - 4);
+            p[h] = kk < L ? p[h] : 0.f;
+          }
+        }
+        const of2v d = p * (dp * ik2 - dl2);
+        ds[j] = d[0];
+        ds[j + 1] = d[1];
       }
       acc = mfma32(trfrag(Ki, kt + 4 * g, kt + 16 + 4 * g, lane), pack8f(ds), acc);
     };
