@@ -123,31 +123,42 @@ __device__ __forceinline__ float kf(float x, const uint32_t* m, int j, float inv
 }
 
 // =================================================================================== stem
-// h0 [c][b*L + l][64] (bf16) = conv1d(x[c][b][:], k3, pad 1)[l] + bias + pe[l]
+// h0 [c][b*L + l][64] (bf16) = conv1d(x[c][b][:], k3, pad 1)[l] + bias + pe[l].  A block covers 32 rows, 8
+// threads per row with 8 channels each (one 16-byte store); the conv weights and biases are staged in LDS once per
+// block (the per-thread scattered parameter loads made this pass ~10x slower than its 73 MB of stores)
+constexpr int STEM_ROWS = 32;
 __global__ void __launch_bounds__(256) k_har_stem(const float* __restrict__ x, int B, int L, const float* __restrict__ params,
                                                   long P, int w_off, int b_off, int pe_off, u16* __restrict__ h) {
+  __shared__ float wsb[64 * 4];  // [o][w0 w1 w2 b]
   const int c = blockIdx.y;
   const long R = (long)B * L;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long row = t >> 4;
-  const int o0 = (int)(t & 15) * 4;
+  const float* pp = params + (long)c * P;
+  if (threadIdx.x < 64) {
+    const int o = threadIdx.x;
+    wsb[4 * o] = pp[w_off + 3 * o];
+    wsb[4 * o + 1] = pp[w_off + 3 * o + 1];
+    wsb[4 * o + 2] = pp[w_off + 3 * o + 2];
+    wsb[4 * o + 3] = pp[b_off + o];
+  }
+  __syncthreads();
+  const long row = (long)blockIdx.x * STEM_ROWS + (threadIdx.x >> 3);
+  const int o0 = (int)(threadIdx.x & 7) * 8;
   if (row >= R) return;
   const int l = (int)(row % L);
-  const float* pp = params + (long)c * P;
   const float* xr = x + (long)c * R + (row - l);
   const float xm = l >= 1 ? xr[l - 1] : 0.f, x0 = xr[l], xp = l + 1 < L ? xr[l + 1] : 0.f;
-  float v[4];
+  const float* pe = pp + pe_off + l * 64 + o0;
+  float v[8];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int o = o0 + e;
-    const float* w = pp + w_off + o * 3;
-    float s = pp[b_off + o] + pp[pe_off + l * 64 + o];
+  for (int e = 0; e < 8; ++e) {
+    const f4v w = *(const f4v*)(wsb + 4 * (o0 + e));
+    float s = w[3] + pe[e];  // (same operation order as the composite: bias + pe, then the taps)
     if (l >= 1) s += w[0] * xm;
     s += w[1] * x0;
     if (l + 1 < L) s += w[2] * xp;
     v[e] = s;
   }
-  *(u32x2v*)(h + ((long)c * R + row) * 64 + o0) = u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])};
+  *(u32x4*)(h + ((long)c * R + row) * 64 + o0) = u32x4{pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
 }
 
 // mean over L of the last layer's rows -> pooled [c][b][64] fp32 (fixed-order sums)
@@ -1147,9 +1158,9 @@ __global__ void __launch_bounds__(256) k_har_reduce(const float* __restrict__ ws
 // =================================================================================== launchers
 int afl_har_stem(const float* x, int C, int B, int L, const float* params, long P, int w_off, int b_off, int pe_off,
                  u16* h, hipStream_t s) {
-  const long n = (long)B * L * 16;
-  hipLaunchKernelGGL(k_har_stem, dim3((unsigned)((n + 255) / 256), C), dim3(256), 0, s, x, B, L, params, P, w_off, b_off,
-                     pe_off, h);
+  const long R = (long)B * L;
+  hipLaunchKernelGGL(k_har_stem, dim3((unsigned)((R + STEM_ROWS - 1) / STEM_ROWS), C), dim3(256), 0, s, x, B, L, params, P,
+                     w_off, b_off, pe_off, h);
   return (int)hipGetLastError();
 }
 
