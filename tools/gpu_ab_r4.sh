@@ -1,6 +1,6 @@
 #!/bin/bash
-# round-4 A/B batch: HAR attention forward / dQ workgroup size (8 / 16 waves instead of 12: 32 resident waves per CU)
+# round-4 A/B batch: CNN owner moments loaded during the partial-barrier wait (tests, phases, bench A/B)
 set -o pipefail
-for v in _C_aq8 _C_aq16; do AFL_NATIVE_SO=attackfl_amd/$v.so timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_har.py > gpurun_out/t_har_$v.log 2>&1; rc=$?; echo "$v: $(tail -1 gpurun_out/t_har_$v.log)"; [ $rc -eq 0 ] || exit $rc; done
-echo "== HAR A/B (A = 12 waves, B = 8 waves)"; timeout -k 10 600 bash tools/ab_native.sh attackfl_amd/_C_aq8.so 3 --model TransformerClassifier --data-name HAR --steps 3 --warmup 1 || exit 1
-echo "== HAR A/B (A = 12 waves, B = 16 waves)"; timeout -k 10 600 bash tools/ab_native.sh attackfl_amd/_C_aq16.so 3 --model TransformerClassifier --data-name HAR --steps 3 --warmup 1 || exit 1
+timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_programs.py -k "cnn2 or CNNModel" > gpurun_out/cnnt.log 2>&1; rc=$?; tail -1 gpurun_out/cnnt.log; [ $rc -eq 0 ] || exit $rc
+for v in _C_prev _C; do AFL_NATIVE_SO=attackfl_amd/$v.so timeout -k 10 100 python tools/cnn2_phases.py > gpurun_out/cnnph_$v.log 2>&1 || exit 1; echo "== $v"; grep -E "^step|conv_owner|P_barrier" gpurun_out/cnnph_$v.log; done
+echo "== CNN A/B (A = moments early, B = previous build)"; timeout -k 10 500 bash tools/ab_native.sh attackfl_amd/_C_prev.so 4 --model CNNModel --steps 20 --warmup 2 || exit 1
