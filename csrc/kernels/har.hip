@@ -161,24 +161,37 @@ __global__ void __launch_bounds__(256) k_har_stem(const float* __restrict__ x, i
   *(u32x4*)(h + ((long)c * R + row) * 64 + o0) = u32x4{pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
 }
 
-// mean over L of the last layer's rows -> pooled [c][b][64] fp32 (fixed-order sums)
+// mean over L of the last layer's rows -> pooled [c][b][64] fp32 (fixed-order sums): 32 row groups x 8 lanes of 8
+// channels (16-byte loads, two rows per group in flight)
 __global__ void __launch_bounds__(256) k_har_pool(const u16* __restrict__ y, int L, float* __restrict__ out) {
-  __shared__ f4v part[16][16];
-  const int cb = blockIdx.x, j4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const u16* base = y + (long)cb * L * 64 + 4 * j4;
-  f4v s = Z4;
-  for (int l = rg; l < L; l += 16) {
-    const u32x2v u = *(const u32x2v*)(base + (long)l * 64);
-    s[0] += __uint_as_float(u[0] << 16);
-    s[1] += __uint_as_float(u[0] & 0xFFFF0000u);
-    s[2] += __uint_as_float(u[1] << 16);
-    s[3] += __uint_as_float(u[1] & 0xFFFF0000u);
+  __shared__ f4v part[32][16];
+  const int cb = blockIdx.x, j8 = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const u16* base = y + (long)cb * L * 64 + 8 * j8;
+  f4v s0 = Z4, s1 = Z4;
+  auto add = [&](u32x4 u) {
+    s0[0] += __uint_as_float(u[0] << 16);
+    s0[1] += __uint_as_float(u[0] & 0xFFFF0000u);
+    s0[2] += __uint_as_float(u[1] << 16);
+    s0[3] += __uint_as_float(u[1] & 0xFFFF0000u);
+    s1[0] += __uint_as_float(u[2] << 16);
+    s1[1] += __uint_as_float(u[2] & 0xFFFF0000u);
+    s1[2] += __uint_as_float(u[3] << 16);
+    s1[3] += __uint_as_float(u[3] & 0xFFFF0000u);
+  };
+  int l = rg;
+  for (; l + 32 < L; l += 64) {
+    const u32x4 a = *(const u32x4*)(base + (long)l * 64), b = *(const u32x4*)(base + (long)(l + 32) * 64);
+    add(a);
+    add(b);
   }
-  part[rg][j4] = s;
+  if (l < L) add(*(const u32x4*)(base + (long)l * 64));
+  part[rg][2 * j8] = s0;
+  part[rg][2 * j8 + 1] = s1;
   __syncthreads();
-  if (rg == 0) {
+  if (threadIdx.x < 16) {
+    const int j4 = threadIdx.x;
     f4v t = part[0][j4];
-    for (int k = 1; k < 16; ++k) t += part[k][j4];
+    for (int k = 1; k < 32; ++k) t += part[k][j4];
     *(f4v*)(out + (long)cb * 64 + 4 * j4) = t * (1.f / (float)L);
   }
 }

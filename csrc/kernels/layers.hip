@@ -790,10 +790,19 @@ __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x
   int row = r0 + rg, l = row % L;
   const float* xc = x + (long)c * nrows;
   const float* dc = dh + (long)c * nrows * 64 + o0;
-  for (; row < min(nrows, r0 + 1024); row += 16) {
+  const int rend = min(nrows, r0 + 1024);
+  // two rows (row, row + 16) per iteration: both gradient loads in flight before either is used
+  for (; row < rend; row += 32) {
+    int l2 = l + 16;
+    while (l2 >= L) l2 -= L;
+    const bool two = row + 16 < rend;
+    const f4v d = *(const f4v*)(dc + (long)row * 64);
+    const f4v d2 = two ? *(const f4v*)(dc + (long)(row + 16) * 64) : f4v{0.f, 0.f, 0.f, 0.f};
     const float* xr = xc + (row - l);
     const float xm = l >= 1 ? xr[l - 1] : 0.f, x0 = xr[l], xp = l + 1 < L ? xr[l + 1] : 0.f;
-    const f4v d = *(const f4v*)(dc + (long)row * 64);
+    const float* xr2 = xc + (row + 16 - l2);
+    const float xm2 = two && l2 >= 1 ? xr2[l2 - 1] : 0.f, x02 = two ? xr2[l2] : 0.f,
+                xp2 = two && l2 + 1 < L ? xr2[l2 + 1] : 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       a[e][0] += d[e] * xm;
@@ -801,7 +810,16 @@ __global__ void __launch_bounds__(256) k_conv_pe_bwd(const float* __restrict__ x
       a[e][2] += d[e] * xp;
       a[e][3] += d[e];
     }
-    l += 16;
+    if (two) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e][0] += d2[e] * xm2;
+        a[e][1] += d2[e] * x02;
+        a[e][2] += d2[e] * xp2;
+        a[e][3] += d2[e];
+      }
+    }
+    l = l2 + 16;
     while (l >= L) l -= L;
   }
 #pragma unroll
