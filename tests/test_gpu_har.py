@@ -110,3 +110,50 @@ def test_har_attention_keep_words_match_keep_rc(gpu):
         got = _decode_keep_words(words[cbh], L, Lp)
         assert (got == ref).all(), (cbh, int((got != ref).sum()))
         assert abs(got.mean() - 0.9) < 0.01
+
+
+def test_har_post_keep_bits_match_afl_keep(gpu):
+    """The row pass's stored dropout flags (``AflHarPost::kbits``, read back by the post backward instead of
+    re-hashing) are exactly the layer library's ``afl_keep`` draws (``masks.keep``) of the three sites."""
+    from attackfl_amd.fl.programs import make_program
+    from attackfl_amd.models import ParamLayout, build_model
+    from attackfl_amd.ops import masks
+
+    C, B, L, p = 2, 2, 50, 0.1
+    R = B * L
+    nat = native()
+    prog = make_program("TransformerClassifier", C, B, gpu)
+    lay = ParamLayout.for_model("TransformerClassifier")
+    params = torch.stack([lay.flatten(build_model("TransformerClassifier", seed=s).state_dict()) for s in range(C)]).to(gpu)
+    g = torch.Generator().manual_seed(5)
+    bf = torch.bfloat16
+    o = torch.randn(C, R, 64, generator=g).to(gpu, bf)
+    x = torch.randn(C, R, 64, generator=g).to(gpu, bf)
+    xh1, xh2, y = (torch.zeros(C, R, 64, dtype=bf, device=gpu) for _ in range(3))
+    rs = torch.zeros(C, R, 2, device=gpu)
+    kb = torch.zeros(C, R, int(nat.har_kbits_per_row), dtype=torch.int32, device=gpu)
+    ctl = _ctl(C, gpu)
+    nat.har_post(o, x, xh1, xh2, rs, y, params, prog._lw(0), ctl.seeds, ctl.stepctl, 0, p, kb)
+    words = kb.cpu().numpy().astype(np.uint32).reshape(C, R, 4, 4)  # [c][row][g][word]
+    cc = _ctl(C, "cpu")
+    rows = np.arange(R)[:, None]
+
+    def decode(word, ntiles, t0):  # bit 4t + i <-> feature 16 (t0 + t) + 4g + i of the lane (row, g)
+        out = np.zeros((R, 16 * (t0 + ntiles)), dtype=bool)
+        for gg in range(4):
+            w = word[:, gg]
+            for t in range(ntiles):
+                for i in range(4):
+                    out[:, 16 * (t0 + t) + 4 * gg + i] = (w >> np.uint32(4 * t + i)) & np.uint32(1)
+        return out[:, 16 * t0:]
+
+    for c in range(C):
+        w = words[c]
+        d1 = decode(w[:, :, 0] & np.uint32(0xFFFF), 4, 0)
+        d2 = decode(w[:, :, 0] >> np.uint32(16), 4, 0)
+        df = np.concatenate([decode(w[:, :, 1], 8, 0), decode(w[:, :, 2], 8, 8)], axis=1)
+        key = cc.key(c)
+        for got, layer, n in ((d1, 1, 64), (df, 2, 256), (d2, 3, 64)):
+            ref = masks.keep(key, layer, rows, np.arange(n)[None, :], p).numpy()
+            assert (got == ref).all(), (c, layer, int((got != ref).sum()))
+            assert abs(got.mean() - 0.9) < 0.03
