@@ -52,9 +52,12 @@ __device__ __forceinline__ uint32_t dkey(const AflDrop& d, int c) {
 // registers) or k (natural: K fed from rows loaded straight from memory)
 template <bool PERM>
 __device__ void build_img(uchar* smem, int img, int ld, const float* __restrict__ W, int N, int K) {
-  for (int e = threadIdx.x; e < N * K; e += blockDim.x) {
-    const int n = e / K, k = e - n * K;
-    *(LDS_AS u16*)(smem + img + n * ld + (PERM ? pcol(k) : k) * 2) = fk::f2bf(W[e]);
+  // 4 consecutive k per thread, one 8-byte LDS store (pcol keeps aligned groups of 4 together)
+  const int K4 = K >> 2;
+  for (int e = threadIdx.x; e < N * K4; e += blockDim.x) {
+    const int n = e / K4, k = 4 * (e - n * K4);
+    const float* w = W + (long)n * K + k;  // (dword loads: a client's parameter row need not be 16-byte aligned)
+    *(LDS_AS u32x2v*)(smem + img + n * ld + (PERM ? pcol(k) : k) * 2) = u32x2v{pk2(w[0], w[1]), pk2(w[2], w[3])};
   }
 }
 __device__ void load_vec(uchar* smem, int off, const float* __restrict__ v, int n) {
