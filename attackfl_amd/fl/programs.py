@@ -399,7 +399,9 @@ class HARProgram(_Program):
         self.linear_bwd(dc1, self.buf("pool", C, B, 64), params, grads, "classifier.0.weight", "classifier.0.bias",
                         dpool)
         ws_p = self.buf("ws_post", C * G * int(nat.har_post_ng))
-        ws_q = self.buf("ws_qkv", C * G * int(nat.har_qkv_ng))
+        # the q|k|v backward runs two workgroups per CU (two waves per SIMD): twice the partials, same fixed order
+        GQ = int(os.environ.get("AFL_HAR_QKV_G", 2 * G))
+        ws_q = self.buf("ws_qkv", C * GQ * int(nat.har_qkv_ng))
         dres, dout = self.buf("dres", C, R, 64), self.buf("doutb", C, R, 64, dtype=bf)
         delta, dqkv = self.buf("delta", C * B * 4, Lp), self.buf("dqkvb", C * B * 4, 3, Lp, 16, dtype=bf)
         dxs = [self.buf("dxA", C, R, 64), self.buf("dxB", C, R, 64)]
@@ -415,8 +417,8 @@ class HARProgram(_Program):
                              dout, delta, dqkv, B, L, seeds, stepctl, 10 * i, p,
                              self._mask(i) if seeds is not None else None)
             dx = dxs[i % 2]
-            nat.har_qkv_bwd(dqkv, dres, self.buf(f"hb{i}", C, R, 64, dtype=bf), dx, ws_q, params, w[0], B, L, G)
-            nat.har_reduce(ws_q, G, int(nat.har_qkv_ng), self._qkv_seg(i), grads)
+            nat.har_qkv_bwd(dqkv, dres, self.buf(f"hb{i}", C, R, 64, dtype=bf), dx, ws_q, params, w[0], B, L, GQ)
+            nat.har_reduce(ws_q, GQ, int(nat.har_qkv_ng), self._qkv_seg(i), grads)
             dy = dx
         Lx.conv_pe_bwd(self.buf("x", C, B, L), dy, grads, self.slot["conv.weight"].offset,
                        self.slot["conv.bias"].offset)

@@ -1032,7 +1032,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
 constexpr int QB_W = 0, QB_DQ = 192 * LDK64, QB_X = QB_DQ + 3 * TILE, QB_RED = QB_X + TILE;
 constexpr int QB_SMEM = QB_RED + 4 * 192 * 4;
 
-__global__ void __launch_bounds__(NTR) k_har_qkv_bwd(AflHarQkvB a) {
+__global__ void __launch_bounds__(NTR) __attribute__((amdgpu_waves_per_eu(2, 2))) k_har_qkv_bwd(AflHarQkvB a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
   const int c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   const float* pp = a.params + (long)c * a.P;
