@@ -40,6 +40,7 @@ namespace {
 constexpr int D = 64, NH = 4, DH = 16, FF = 256;
 constexpr int NW = 4, NTR = 64 * NW;  // backward row passes: 4 waves (one per SIMD), 64 rows per block
 constexpr int NWF = 8, NTF = 64 * NWF;  // forward row passes: 8 waves (two per SIMD), 16 rows each
+constexpr int NWP = 16, NTP = 64 * NWP;  // post-attention forward: 16 waves (four per SIMD; LDS allows one workgroup per CU)
 constexpr int LDK64 = (64 + 8) * 2, LDK256 = (256 + 8) * 2;  // weight-image row strides (bytes)
 typedef unsigned short u16;
 typedef __attribute__((address_space(1))) const u16 gcu16;
@@ -249,7 +250,7 @@ __device__ void post_vectors(uchar* smem, const float* pp, const AflHarLayerW& w
   load_vec(smem, PF_VEC + V_BE2 * 4, pp + w.n2b, 64);
 }
 
-__global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
+__global__ void __launch_bounds__(NTP) k_har_post(AflHarPost a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
   const int c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const float* pp = a.params + (long)c * a.P;
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(NTF) k_har_post(AflHarPost a) {
   const uint32_t k1 = dkey(a.d1, c), kf_ = dkey(a.df, c), k2 = dkey(a.d2, c);
   const long R = a.R;
   const int ntiles = (int)((R + 15) / 16);
-  for (int t = blockIdx.x * NWF + wave; t < ntiles; t += gridDim.x * NWF) {
+  for (int t = blockIdx.x * NWP + wave; t < ntiles; t += gridDim.x * NWP) {
     const long r = 16L * t + (lane & 15);
     const bool ok = r < R;
     const long row = (long)c * R + (ok ? r : 0);
@@ -1259,6 +1260,6 @@ int afl_har_post(const AflHarPost& a, hipStream_t s) {
     attr = true;
   }
   if ((a.d1.thr16 || a.df.thr16 || a.d2.thr16) && !a.kbits) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_har_post, dim3(har_blocks(a.R, a.C), a.C), dim3(NTF), PF_SMEM, s, a);
+  hipLaunchKernelGGL(k_har_post, dim3(har_blocks(a.R, a.C), a.C), dim3(NTP), PF_SMEM, s, a);
   return (int)hipGetLastError();
 }
