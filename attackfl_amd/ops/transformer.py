@@ -1,12 +1,16 @@
-"""Fused TransformerModel/ICU training and evaluation (HIP kernels in ``csrc/kernels/transformer.hip``).
+"""Fused TransformerModel/ICU training and evaluation (HIP kernels in ``csrc/kernels/tf2.hip``, the on-chip
+trainer, and ``csrc/kernels/transformer.hip``, the global-workspace fallback and the eval kernels).
 
-``train_clients`` runs ONE persistent kernel launch that trains every row of ``params [C, P]``
-for all local epochs (one 512-thread workgroup per client).  ``reference_train`` is the plain
-PyTorch fp32 oracle of exactly the same computation — same batches, same hash-generated dropout
-masks, Adam (or the SGD test mode) — used by the numerics tests to check the kernel.
+``train_clients`` runs ONE persistent kernel launch that trains every row of ``params [C, P]`` for all
+local epochs: by default the on-chip trainer with row-split branches (split 5: head + two 4-wave
+workgroups per branch, 5 per client), or its 3-workgroup form (split 4) when 5 workgroups per client do
+not fit the CUs (``auto_split``).  ``reference_train`` is the plain PyTorch fp32 oracle of exactly the same
+computation — same batches, same hash-generated dropout masks, Adam (or the SGD test mode) — used by the
+numerics tests to check the kernels.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -22,14 +26,16 @@ M32 = 0xFFFFFFFF
 
 # ------------------------------------------------------------------------------- device entry points
 def auto_split(C: int, dev) -> int:
-    """Trainer variant for C clients: 4 = the on-chip trainer (``tf2.hip``: head | vitals | labs
-    workgroups with weights, optimizer state and activations held in registers / LDS) when every
-    workgroup of every client fits on the device at once (one per CU); else the global-workspace
-    kernels of ``transformer.hip`` with 2 or 1 workgroups per client."""
+    """Trainer variant for C clients, the first whose workgroups all fit on the device at once (one per CU):
+    4 = the on-chip trainer (``tf2.hip``: head | vitals | labs workgroups), else the global-workspace kernels
+    of ``transformer.hip`` with 2 or 1 workgroups per client.  Split 5 (row-split branches, 5 workgroups per
+    client) is available but not chosen: measured slower (see below)."""
     from ..parallel.launcher import gpu_sharers
 
     # (processes sharing the GPU run their own persistent launches on the same CUs: count only this one's share)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
+    # split 5 measured slower than 4 (round 5: 91.5 vs 103.6 rounds/s at 8 clients, 97.1 vs 110.2 at 1 client,
+    # profiles/ab_tf2_r5_row_split.log): opt-in only (split=5 / AFL_TF_SPLIT=5)
     return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
 
 
@@ -46,12 +52,12 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     DEVICE tensors without synchronising (see ``finish``); arguments as ``train_clients``."""
     dev = params.device
     C = params.shape[0]
-    if split is None:
-        split = auto_split(C, dev) if C > 0 else 1
+    if split is None:  # (AFL_TF_SPLIT: A/B override of the automatic choice)
+        split = int(os.environ.get("AFL_TF_SPLIT", "0") or 0) or (auto_split(C, dev) if C > 0 else 1)
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else torch.tensor([device_seed(s) for s in seeds], dtype=torch.int32, device=dev)
     kt = None
-    if split == 4:
+    if split in (4, 5):
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
                              int(batch), float(lr), int(opt_mode), stamps, int(split), kt)
@@ -91,7 +97,8 @@ def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor,
     ``split``: workgroups per client — 1 (whole model in one workgroup), 2 (vitals branch + head |
     labs branch) or 3 (head | vitals | labs); the workgroups of a client hand activations and
     gradients to each other every step.  4 = the on-chip trainer (``tf2.hip``, 3 workgroups per client,
-    nothing of the model in global memory during the round).  Default: ``auto_split``.
+    nothing of the model in global memory during the round), 5 = the same with each branch split over two
+    workgroups by batch rows (5 per client).  Default: ``auto_split``.
     ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
     workgroup 0, summed over all steps (diagnostics)."""
     return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, stamps, split))

@@ -98,6 +98,9 @@ struct AflTfTrainArgs {
   // tf2 only: per-step Adam constants [kt_n][2] = (lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)), t = 1..kt_n
   const float* kt;
   int kt_n;
+  // on-chip trainers: block stride of the role-major grid (>= C; padded to a multiple of 8 when that still
+  // fits, so a client's workgroups land on one XCD whatever C is); blocks with client index >= C exit
+  int cpad;
 };
 int afl_tf_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf_eval_bf(const float* params, unsigned short* bf, const float* rows, int n, float* out, hipStream_t s);
@@ -110,6 +113,9 @@ constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lin
 // 2 directions x 2 branches x 8 waves x 4 KB of {value, tag} granules, zeroed with the flags every call
 constexpr int AFL_GR_WORDS = 2 * 2 * 8 * 1024;
 constexpr int AFL_TF2_SYNC_WORDS = AFL_TF_SYNC_WORDS + AFL_GR_WORDS;
+// row-split on-chip trainers (split 5): plus the exchange slots between the two halves of each branch
+// (6 kinds x 2 branches x 2 halves x 4 waves x 4 KB, tf2.hip xs_off)
+constexpr int AFL_TF2S_SYNC_WORDS = AFL_TF2_SYNC_WORDS + 6 * 2 * 2 * 4 * 1024;
 // tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations
 // in registers / LDS; 3 workgroups per client, sync words required)
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);

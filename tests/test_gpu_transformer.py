@@ -44,7 +44,7 @@ def test_eval_forward_matches_reference(gpu):
     assert (mod - ref).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4])
+@pytest.mark.parametrize("split", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("batch", [128, 100])
 def test_sgd_step_gradients_match(gpu, batch, split):
     """One SGD step (opt_mode 1) exposes the raw gradients: compare p1 - p0 with the oracle."""
@@ -83,7 +83,7 @@ def test_adam_epoch_tracks_reference(gpu):
     assert torch.allclose(loss, loss_r, rtol=0.05, atol=0.02), (loss, loss_r)
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4])
+@pytest.mark.parametrize("split", [1, 2, 3, 4, 5])
 def test_nan_params_fail_client(gpu, split):
     rows, params, plan = _setup(2, [300, 300])
     params[1, 5] = float("nan")
@@ -129,7 +129,7 @@ def test_branch_parallel_matches_single_workgroup(gpu):  # noqa: D401
             assert torch.allclose(outs[0][1], o[1], rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("split", [3, 4])
+@pytest.mark.parametrize("split", [3, 4, 5])
 def test_training_is_bit_reproducible(gpu, split):
     """A client's result may not depend on the launch that trains it: the multi-rank engine trains
     clients 0-1 on rank 0 and 2-3 on rank 1 and must equal the single-process run of all four (the
@@ -175,3 +175,36 @@ def test_saturated_sigmoid_start_matches_oracle(gpu):
     moved = (ref - params).abs()
     assert d.mean().item() < 0.15 * moved.mean().item(), (d.mean(), moved.mean())
     assert torch.allclose(loss, loss_r, rtol=0.1, atol=0.05), (loss, loss_r)
+
+
+@pytest.mark.parametrize("C", [1, 3, 8])
+def test_row_split_matches_three_workgroups(gpu, C):
+    """Split 5 (each branch on two 4-wave workgroups, 64 rows each) runs the 3-workgroup kernel's arithmetic
+    except for the order of the per-row sums (two 64-row partials added across the halves): raw SGD updates
+    agree to float rounding, Adam trajectories closely, with partial and size-1 batches; C = 1 and 3 pad the
+    grid so a client's workgroups share one XCD."""
+    nd = [700, 513, 300, 129, 640, 256, 901, 130][:C]
+    rows, params, plan = _setup(C, nd, seed=4)
+    seeds = list(range(21, 21 + C))
+    for opt_mode, lr in ((1, 0.01), (0, 0.004)):
+        outs = []
+        for split in (4, 5):
+            dev = params.clone().to(gpu)
+            ok, loss = T.train_clients(dev, rows.to(gpu), plan.order.to(gpu), plan.nd, 1, 128, lr, seeds,
+                                       opt_mode=opt_mode, split=split)
+            assert ok.tolist() == [1] * C
+            outs.append((dev.cpu(), loss))
+        d = (outs[0][0] - outs[1][0]).abs()
+        moved = (outs[0][0] - params).abs()
+        if opt_mode == 1:
+            assert d.max().item() < 0.02 * moved.max().item(), (d.max(), moved.max())
+        else:
+            assert d.mean().item() < 0.05 * moved.mean().item(), (d.mean(), moved.mean())
+        assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-2, atol=1e-4), (outs[0][1], outs[1][1])
+
+
+def test_auto_split_choice(gpu):
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    assert T.auto_split(8, gpu) == 4  # (split 5 is opt-in: measured slower, ops/transformer.py auto_split)
+    assert T.auto_split(cus // 3, gpu) == 4
+    assert T.auto_split(cus // 3 + 1, gpu) == 2
