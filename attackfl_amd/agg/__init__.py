@@ -339,20 +339,18 @@ def _median(x: torch.Tensor) -> torch.Tensor:
     return 0.5 * (s[(n - 1) // 2] + s[n // 2])
 
 
-def _top_pc_scores(U: torch.Tensor, squarings: int = 12) -> torch.Tensor:
+def _top_pc_scores(U: torch.Tensor, sweeps: int = 12) -> torch.Tensor:
     """First principal-component scores of the rows (sklearn ``PCA(1).fit_transform`` up to the sign) with no
-    host synchronisation: the n x n Gram of the centred rows, its leading eigenvector by repeated squaring
-    (the gap ratio raised to 2^squarings, trace-normalised every step in fp64), score = v * sqrt(lambda)."""
+    host synchronisation: the n x n Gram of the centred rows, its leading eigenpair by a fixed-sweep Jacobi
+    eigen-decomposition on the device (``k_top_pc``, n <= 64; ``torch.linalg.eigh`` on the CPU / larger n),
+    score = v sqrt(lambda).  Exact for any spectrum gap (repeated squaring, the round-4 form, let the second
+    eigenvector leak in when the top two eigenvalues are close)."""
     G = _centred_gram(U)
-    M = G / G.diagonal().sum().clamp_min(1e-300)
-    for _ in range(squarings):
-        M = M @ M
-        M = M / M.diagonal().sum().clamp_min(1e-300)
-    i = torch.argmax(M.diagonal())
-    v = M.index_select(1, i.reshape(1))[:, 0]
-    v = v / torch.linalg.vector_norm(v).clamp_min(1e-300)
-    lam = (v @ G @ v).clamp_min(0.0)
-    return v * torch.sqrt(lam)
+    n = G.shape[0]
+    if G.is_cuda and n <= 64:
+        return ops.native().top_pc(G.contiguous(), int(sweeps))
+    ev, V = torch.linalg.eigh(G)
+    return V[:, -1] * torch.sqrt(ev[-1].clamp_min(0.0))
 
 
 def fltracer(U: torch.Tensor, sizes: torch.Tensor, threshold: float = 2.5, **_) -> AggResult:

@@ -229,7 +229,8 @@ class FLEngine:
         self.faults = {(int(f["client"]), int(f["round"])) for f in (cfg.engine.get("fault-inject") or [])}
         self._phase_t: Dict[str, float] = {}
         # FedAvg fast path: with no attacker and no detection, the server needs only
-        # sum_i s_i w_i and sum_i s_i -> ONE all_reduce of [P + 3] instead of the [N, P] all-gather
+        # sum_i s_i w_i and sum_i s_i -> ONE all_reduce of [P + 5] (+ #failed, #reported, the decision word and its
+        # square) instead of the [N, P] all-gather
         # auto = world > 1 without the IPC one-shot gather (which moves whole blocks in one stream-ordered hop
         # and keeps FedAvg on the same deterministic kernel as a single rank)
         fa = str(cfg.comm.get("fedavg-allreduce", "auto")).lower()
@@ -877,12 +878,17 @@ class FLEngine:
                 # the round's ONE host read: every client's [valid, result, size, attacker, decision | losses]; it
                 # is queued BEFORE the early launch and waited for through its own event, so the host waits for
                 # the gather (the slowest rank's clients), not for the next round's training queued behind it
-                mread = self._meta_read(sel[:, P:P + META + self.E])
+                # (+ one row per rank — its first slot — so every rank's decision word is checked, also a rank
+                # none of whose clients is selected or valid this round)
+                nsel = sel.shape[0]
+                per_rank = allb[0::block.shape[0], P:P + META + self.E] if block.shape[0] else allb[:0, P:P + META + self.E]
+                mread = self._meta_read(torch.cat([sel[:, P:P + META + self.E], per_rank], 0))
                 # FedAvg / hyper: the aggregate and the next launch go in on the device before the host read
                 esl = self._early_launch(st, last, U=U, sel=sel)
-                meta = mread()
+                mall = mread()
+                meta, rank_rows = mall[:nsel], mall[nsel:]
                 self.comm.check()
-                self._check_decisions(meta.numpy())
+                self._check_decisions(meta.numpy(), rank_rows.numpy()[:, DECISION])
                 if self._pending is not None:
                     self._pending.result()  # the training has finished by now: surfaces hand-off timeouts
             if self.phase_sync:
@@ -970,12 +976,15 @@ class FLEngine:
         key = f"{self.round_no}|{self.rounds_left}|{','.join(map(str, self.selected))}".encode()
         return zlib.crc32(key) & 0x7FFFFF
 
-    def _check_decisions(self, mn: np.ndarray) -> None:
+    def _check_decisions(self, mn: np.ndarray, rank_words: np.ndarray = None) -> None:
         """Raise if the ranks' decision words differ: a rank's validation or detection decided otherwise (e.g.
         a mixed CPU / GPU gloo world whose kernels are not bit-identical), and continuing would desynchronise
-        the collectives or silently diverge the replicated models."""
+        the collectives or silently diverge the replicated models.  ``rank_words``: one word per rank (its
+        first slot row), so a rank without a selected, valid client is checked too (as the all-reduce path)."""
         valid = mn[:, 0] > 0.5
         words = mn[valid, DECISION]
+        if rank_words is not None:
+            words = np.concatenate([words, np.asarray(rank_words, dtype=words.dtype)])
         if words.size and not np.all(words == words[0]):
             raise RuntimeError(f"ranks disagree on the replicated server state (round {self.round_no}): decision "
                                f"words {sorted(set(int(w) for w in words))}; validation / detection must be "

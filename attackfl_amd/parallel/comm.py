@@ -169,6 +169,7 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, store=None, ra
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl" and torch.cuda.is_available():
         lr = device_index if device_index is not None else int(os.environ.get("LOCAL_RANK", "0"))
+        lr %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(lr)
         device = torch.device("cuda", lr)
     elif torch.cuda.is_available() and device_index is not None:
@@ -184,4 +185,8 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, store=None, ra
         kw["device_id"] = device
     if not dist.is_initialized():
         dist.init_process_group(**kw)
+    if device.type == "cuda" and dist.get_world_size() > 1 and not os.environ.get("AFL_GPU_SHARERS"):
+        from .launcher import sync_gpu_sharers
+
+        sync_gpu_sharers(device)  # processes per physical GPU -> the on-chip trainers' CU budget
     return backend, device

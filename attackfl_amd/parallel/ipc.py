@@ -26,12 +26,15 @@ import torch.distributed as dist
 from .. import ops
 
 
-def setup_verdict(local_err: str, infos: Sequence[Tuple[str, int, bytes]], rank: int,
+def setup_verdict(local_err: str, infos: Sequence[Tuple[str, object, bytes]], rank: int,
                   can_access=None) -> str:
-    """This rank's verdict on the IPC path from everyone's ``(host, device index, handle)`` (``""`` = usable):
+    """This rank's verdict on the IPC path from everyone's ``(host, GPU identity, handle)`` (``""`` = usable):
     a local failure, ranks on several hosts, a peer without an exported buffer, or a peer GPU this GPU cannot
-    map (``can_access(peer device index) -> bool``, hipDeviceCanAccessPeer; a peer on the same device needs
-    no peer access).  Pure host logic — the ranks then AND their verdicts (``IpcAllGather._agree``)."""
+    map.  The identity is physical (``launcher.gpu_key``: the same in every process whatever its device
+    ordinals); ``can_access(peer identity)`` answers True / False (hipDeviceCanAccessPeer on this process's
+    ordinal of that GPU) or None for a GPU this process cannot see — unknown, left to the open and the
+    self-test.  A peer on the same GPU needs no peer access.  Pure host logic — the ranks then AND their
+    verdicts (``IpcAllGather._agree``)."""
     if local_err:
         return local_err
     if len({h for h, _, _ in infos}) != 1:
@@ -40,7 +43,8 @@ def setup_verdict(local_err: str, infos: Sequence[Tuple[str, int, bytes]], rank:
         return "a peer could not export its buffer"
     me = infos[rank][1]
     if can_access is not None:
-        bad = sorted({d for r, (_, d, _) in enumerate(infos) if r != rank and d != me and not can_access(d)})
+        bad = sorted({str(d) for r, (_, d, _) in enumerate(infos)
+                      if r != rank and d != me and can_access(d) is False})
         if bad:
             return f"no peer access from GPU {me} to GPU(s) {bad}"
     return ""
@@ -68,13 +72,20 @@ class IpcAllGather:
     def _on_device(self):
         return torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
 
-    def _can_access(self, peer: int) -> bool:
+    def _can_access(self, peer_key):
+        """Peer access from this GPU to the GPU with identity ``peer_key`` (``launcher.gpu_key``): True / False,
+        None when this process cannot see that GPU (visibility narrowed per rank)."""
         if self.device.type != "cuda":
             return False
+        from .launcher import local_gpu_keys
+
+        idx = local_gpu_keys().get(peer_key)
+        if idx is None:
+            return None
         try:
-            return bool(torch.cuda.can_device_access_peer(self.device.index or 0, int(peer)))
-        except Exception:  # noqa: BLE001 - a device index this process cannot see
-            return False
+            return bool(torch.cuda.can_device_access_peer(self.device.index or 0, int(idx)))
+        except Exception:  # noqa: BLE001
+            return None
 
     def setup(self, n: int) -> None:
         """Collective: allocate ``n`` floats per sender slot, map every peer, verify.  Raises
@@ -89,8 +100,10 @@ class IpcAllGather:
         except Exception as e:  # noqa: BLE001 - reported collectively below
             err = f"alloc/export: {e}"
         info = [None] * self.world
-        dev_index = (self.device.index or 0) if self.device.type == "cuda" else -1
-        dist.all_gather_object(info, (socket.gethostname(), dev_index, handle), group=self.pg)
+        from .launcher import gpu_key
+
+        me = gpu_key(self.device.index or 0) if self.device.type == "cuda" else "cpu"
+        dist.all_gather_object(info, (socket.gethostname(), me, handle), group=self.pg)
         err = setup_verdict(err, info, self.rank, self._can_access)
         if not err:
             try:

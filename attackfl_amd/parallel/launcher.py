@@ -34,9 +34,34 @@ def _host_port(cfg: Config) -> Tuple[str, int]:
     return str(host), int(cfg.comm.get("port", 29517))
 
 
+def gpu_key(index: int) -> str:
+    """Physical identity of visible GPU ``index``, the same in every process whatever its device ordinals
+    (HIP_VISIBLE_DEVICES narrowing renumbers them): the UUID, else the PCI location, else (last resort, per
+    process) the ordinal."""
+    import torch
+
+    props = torch.cuda.get_device_properties(index)
+    u = str(getattr(props, "uuid", "") or "")
+    if u.strip("0-"):
+        return "uuid:" + u
+    bus = getattr(props, "pci_bus_id", None)
+    if bus is not None:
+        return f"pci:{getattr(props, 'pci_domain_id', 0)}:{bus}:{getattr(props, 'pci_device_id', 0)}"
+    return f"ord:{index}"
+
+
+def local_gpu_keys() -> Dict[str, int]:
+    """gpu_key -> this process's ordinal, for every visible GPU."""
+    import torch
+
+    if not torch.cuda.is_available():
+        return {}
+    return {gpu_key(i): i for i in range(torch.cuda.device_count())}
+
+
 def device_descriptor(device) -> Dict:
-    """Where this process computes: host + physical GPU identity (UUID when the runtime reports one), so the
-    server can tell whether every rank owns its own GPU (RCCL) or some share one (gloo + IPC)."""
+    """Where this process computes: host + physical GPU identity (``gpu_key``), so the server can tell whether
+    every rank owns its own GPU (RCCL) or some share one (gloo + IPC)."""
     import socket
 
     import torch
@@ -44,9 +69,33 @@ def device_descriptor(device) -> Dict:
     d = {"host": socket.gethostname(), "type": getattr(device, "type", "cpu"), "gpu": None}
     if d["type"] == "cuda" and torch.cuda.is_available():
         idx = device.index if device.index is not None else torch.cuda.current_device()
-        props = torch.cuda.get_device_properties(idx)
-        d["gpu"] = str(getattr(props, "uuid", "") or "") or f"{getattr(props, 'pci_bus_id', '')}:{idx}"
+        d["gpu"] = gpu_key(idx)
     return d
+
+
+def client_device(arg: Optional[str], rank: int, ndev: int) -> str:
+    """Device of classic client ``rank`` (1..N; rank 0 is the server).  An explicit ``--device cuda:i`` / ``cpu``
+    wins; ``--device cuda`` or none puts client r on GPU ``r % ndev`` — one FL client per MI355X, the server
+    alone on GPU 0 whenever there are fewer clients than GPUs (with N = ndev clients the last one shares GPU 0
+    with the server, the only way 9 processes fit 8 GPUs).  Reference: client.py:50-61 (cuda if available)."""
+    if arg and arg != "cuda":
+        return arg
+    if ndev <= 0:
+        return arg or "cpu"
+    return f"cuda:{rank % ndev}"
+
+
+def sync_gpu_sharers(device) -> int:
+    """Collective (after ``init_process_group``): count the processes of the group on each physical GPU (by
+    ``gpu_key``, so ranks whose visibility was narrowed to 'their' GPU are told apart) and record the largest
+    count for this process's co-residency budget.  Returns it."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return gpu_sharers()
+    descs: List[Dict] = [None] * dist.get_world_size()  # type: ignore[list-item]
+    dist.all_gather_object(descs, device_descriptor(device))
+    n = max_sharers(descs)
+    set_gpu_sharers(n)
+    return n
 
 
 _SHARERS: Optional[int] = None
@@ -75,13 +124,10 @@ def gpu_sharers() -> int:
     local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")) or 1)
     if os.environ.get("AFL_BENCH_DEVICE") is not None or os.environ.get("AFL_SHARED_GPU") == "1":
         return max(1, local)
-    try:
-        import torch
-
-        ndev = torch.cuda.device_count()
-    except Exception:  # pragma: no cover
-        ndev = 0
-    return max(1, -(-local // ndev)) if ndev > 0 else 1
+    # no explicit information: assume one process per GPU.  (Guessing local ranks / visible GPUs over-counts
+    # when each rank sees only its own GPU; multi-process launches call sync_gpu_sharers, which counts the
+    # processes per physical GPU.)
+    return 1
 
 
 def max_sharers(descs: List[Dict]) -> int:
@@ -144,10 +190,12 @@ def read_transport(store) -> Tuple[str, bool]:
     return str(t["backend"]), bool(t["one_shot"])
 
 
-def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float = 3600.0, device=None):
-    """Client side: claim a rank, publish the descriptor, wait for the table.
+def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float = 3600.0, device=None,
+                    device_fn=None):
+    """Client side: claim a rank, publish the descriptor, wait for the table.  ``device_fn(rank)`` (optional)
+    picks the device once the rank is known (``client_device``); it overrides ``device``.
 
-    Returns (store, rank, world_size, table_json)."""
+    Returns (store, rank, world_size, table_json, device)."""
     host, port = _host_port(cfg)
     store = dist.TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s),
                           use_libuv=False)
@@ -155,6 +203,8 @@ def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float 
     n = int(store.get(PREFIX + "n_clients").decode())
     if rank > n:
         raise RuntimeError(f"server expects {n} clients; this would be client #{rank}")
+    if device_fn is not None:
+        device = device_fn(rank)
     desc = {"uuid": str(uuid.uuid4()), "message": "Hello from Client!",
             "attack": None if attack is None else attack.to_dict(),
             "device": device_descriptor(device) if device is not None else {"type": "cpu"}}
@@ -162,7 +212,7 @@ def join_rendezvous(cfg: Config, attack: Optional[AttackSpec], timeout_s: float 
     print_with_color(f"[>>>] Client {desc['uuid']} registered as rank {rank}", "red")
     store.wait([PREFIX + "table"])
     table = json.loads(store.get(PREFIX + "table").decode())
-    return store, rank, n + 1, table
+    return store, rank, n + 1, table, device
 
 
 def table_from_json(table_json: List[Dict]):
@@ -184,4 +234,6 @@ def init_group(store, rank: int, world: int, backend: str, timeout_s: int = 600,
     if backend == "nccl" and torch.cuda.is_available():
         torch.cuda.set_device(device_index or 0)
         kw["device_id"] = torch.device("cuda", device_index or 0)
+    elif torch.cuda.is_available() and device_index is not None:
+        torch.cuda.set_device(device_index)
     dist.init_process_group(**kw)

@@ -5,7 +5,8 @@
                       --attack_round R --attack_args F ...]
 
 Registers with the server's rendezvous, receives its client index (registration order), and runs its
-rounds inside the SPMD engine: local training through the fused HIP trainer on GPU (eager PyTorch on
+rounds inside the SPMD engine, on GPU ``rank % device_count`` unless ``--device`` names one (one FL client per
+MI355X; ``parallel.launcher.client_device``): local training through the fused HIP trainer on GPU (eager PyTorch on
 CPU) or, once ``training_round >= attack_round`` and genuine models have been received, the attack.
 Unlike the reference (``type=bool``, A-9) ``--attack False`` really disables the attack.
 """
@@ -64,14 +65,16 @@ def main(argv=None) -> int:
     from attackfl_amd.config import AttackSpec, load_config
     from attackfl_amd.fl.engine import FLEngine
     from attackfl_amd.parallel.comm import TorchComm
-    from attackfl_amd.parallel.launcher import init_group, join_rendezvous, read_transport, table_from_json
+    from attackfl_amd.parallel.launcher import (client_device, init_group, join_rendezvous, read_transport,
+                                                table_from_json)
 
     cfg = load_config(args.config)
-    device = torch.device(args.device) if args.device else (torch.device("cuda", 0) if torch.cuda.is_available()
-                                                            else torch.device("cpu"))
-    print(f"Using device: {device}")
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
     attack = AttackSpec(args.attack_mode, args.attack_round, args.attack_args or []) if args.attack else None
-    store, rank, world, table = join_rendezvous(cfg, attack, device=device)
+    # the device follows the claimed rank: client r -> cuda:{r % ndev} unless --device names one (launcher.client_device)
+    store, rank, world, table, device = join_rendezvous(
+        cfg, attack, device_fn=lambda r: torch.device(client_device(args.device, r, ndev)))
+    print(f"Using device: {device}")
     backend, one_shot = read_transport(store)
     backend = backend if cfg.comm.get("backend", "auto") == "auto" else cfg.comm["backend"]
     init_group(store, rank, world, backend, int(cfg.comm.get("timeout-s", 600)), device.index)

@@ -95,6 +95,18 @@ std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
   return {keep, info};
 }
 
+// FLTracer PCA(1) scores (agg.fltracer): G = centred Gram [n, n] fp64 -> z [n] fp64
+torch::Tensor top_pc(torch::Tensor G, int64_t sweeps) {
+  check_dev(G, "G", torch::kFloat64);
+  const int64_t n = G.size(0);
+  TORCH_CHECK(G.dim() == 2 && G.size(1) == n && n >= 1 && n <= 64, "top_pc: G [n, n], n <= 64");
+  auto z = torch::empty({n}, G.options());
+  TORCH_CHECK(afl_top_pc(G.data_ptr<double>(), (int)n, (int)sweeps, z.data_ptr<double>(), cur()) == 0,
+              "top_pc launch failed");
+  AFL_CHECK_LAUNCH();
+  return z;
+}
+
 // Gram matrix of the rows centred on the MEAN row (PCA of the updates: agg.fltracer / agg.gmm), through the same
 // fp64-MFMA pass (rows centred on row 0, H) followed by the double centring C = H - rowmean - colmean + mean
 std::vector<torch::Tensor> gram_centred(torch::Tensor G) {
@@ -696,6 +708,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
   m.def("gmm_filter", &gmm_filter);
+  m.def("top_pc", &top_pc);
   m.def("gram_centred", &gram_centred);
   m.def("stoch_quant", &stoch_quant);
   m.def("adam_flat", &adam_flat);

@@ -62,6 +62,12 @@ def main(argv=None) -> int:
         backend = cfg.comm.get("backend", "auto")
         if backend == "auto" and dev_index is not None:
             backend = "gloo"  # ranks pinned to one GPU share it: RCCL refuses duplicate GPUs
+        if backend == "auto" and torch.cuda.is_available():
+            # one rank per GPU (LOCAL_RANK % GPUs, comm.init_distributed); more local ranks than GPUs share some
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            backend = "nccl" if local <= torch.cuda.device_count() else "gloo"
+            if backend == "gloo":
+                dev_index = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
         backend, device = init_distributed(backend, int(cfg.comm.get("timeout-s", 600)), device_index=dev_index)
         comm = TorchComm(device, backend, one_shot=cfg.comm.get("one-shot-allgather", "auto"))
     else:

@@ -41,8 +41,9 @@ def main(argv=None) -> int:
     from attackfl_amd.utils.log import print_with_color
 
     cfg = load_config(args.config)
-    device = torch.device(args.device) if args.device else (torch.device("cuda", 0) if torch.cuda.is_available()
-                                                            else torch.device("cpu"))
+    # (--device cuda = cuda:0; the clients take GPUs 1, 2, ... in registration order: launcher.client_device)
+    device = (torch.device(args.device) if args.device and args.device != "cuda" else
+              torch.device("cuda", 0) if torch.cuda.is_available() else torch.device(args.device or "cpu"))
     print_with_color(f"Using device: {device}", "green")
     store, world, table = serve_rendezvous(cfg, device=device)
     backend, one_shot = read_transport(store)

@@ -114,6 +114,35 @@ def test_fltracer_device_form_matches_host_pipeline(n, seed):
     assert torch.allclose(res.params.double(), torch.from_numpy(ref), rtol=1e-5, atol=1e-6)
 
 
+def _near_degenerate(n, ratio, seed=0, P=2000):
+    """fp32 rows whose centred Gram has eigenvalues 1, ratio, 0.25, 0.09 (nearly iid updates: a flat top)."""
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randn(n, 4, generator=g, dtype=torch.float64)
+    A -= A.mean(0)  # orthogonal to the all-ones vector: centring leaves the rows' span alone
+    Q, _ = torch.linalg.qr(A)
+    B, _ = torch.linalg.qr(torch.randn(P, 4, generator=g, dtype=torch.float64))
+    s = torch.tensor([1.0, ratio ** 0.5, 0.5, 0.3], dtype=torch.float64)
+    return (Q * s) @ B.T * 10.0 + 0.25
+
+
+@pytest.mark.parametrize("ratio", [0.9, 0.999, 0.9999])
+def test_fltracer_near_degenerate_spectrum_matches_host_pipeline(ratio):
+    """ADVICE r4: PCA(1) by repeated squaring leaked the second eigenvector at (l2/l1)^4096 (66 % at 0.9999);
+    the eigen-decomposition matches numpy's eigh for any gap."""
+    U = _near_degenerate(9, ratio).float()
+    sizes = torch.ones(9)
+    res = agg.fltracer(U, sizes)
+    bad, ref, scores = _fltracer_numpy(U, sizes)
+    assert agg.host_info(res.info)["anomalies"] == bad
+    assert torch.allclose(res.info["scores"].double().cpu(), torch.from_numpy(scores), rtol=1e-6, atol=1e-6)
+    z = agg._top_pc_scores(U).double().cpu().abs()
+    X = U.double().numpy()
+    import numpy as np
+    Xc = X - X.mean(axis=0, keepdims=True)
+    ev, V = np.linalg.eigh(Xc @ Xc.T)
+    assert torch.allclose(z, torch.from_numpy(np.abs(V[:, -1]) * np.sqrt(ev[-1])), rtol=1e-6, atol=1e-8)
+
+
 def test_fltracer_identical_rows_keep_everyone():
     U = torch.ones(5, 100)
     res = agg.fltracer(U, torch.ones(5))

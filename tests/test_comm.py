@@ -20,9 +20,16 @@ def test_setup_verdict_rules():
     assert "export" in setup_verdict("", [("n0", 0, h), ("n0", 1, b"")], 0, lambda d: True)
     # no peer access from GPU 0 to GPU 2 (and 1 is fine)
     v = setup_verdict("", ok, 0, lambda d: d != 2)
-    assert "GPU(s) [2]" in v
+    assert "GPU(s) ['2']" in v
     # ranks sharing one GPU need no peer access
     assert setup_verdict("", [("n0", 0, h), ("n0", 0, h)], 1, lambda d: False) == ""
+    # physical identities: a peer GPU this process cannot see (visibility narrowed per rank) is unknown, not
+    # refused — the open and the self-test decide
+    ids = [("n0", "uuid:a", h), ("n0", "uuid:b", h), ("n0", "uuid:c", h)]
+    seen = {"uuid:a": True, "uuid:c": False}
+    assert setup_verdict("", ids, 0, lambda d: seen.get(d)) == "no peer access from GPU uuid:a to GPU(s) ['uuid:c']"
+    seen["uuid:c"] = None
+    assert setup_verdict("", ids, 0, lambda d: seen.get(d)) == ""
 
 
 class _FakeCtx:

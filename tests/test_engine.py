@@ -348,3 +348,22 @@ def test_replicated_detection_and_validation_world2(tmp_path):
     sp = torch.load(os.path.join(tmp_path, "sp", "TransformerModel_hyper_4.pth"), weights_only=True)
     for k in sp:
         assert torch.allclose(sp[k], mp[k], atol=1e-4), (k, (sp[k] - mp[k]).abs().max())
+
+
+def test_decision_check_covers_ranks_without_selected_clients():
+    """the gather path saw decision words only on selected, valid rows, so a rank with no such
+    client could diverge unchecked; its first slot row's word is now checked too."""
+    import numpy as np
+    import pytest as _pytest
+    from attackfl_amd.fl.engine import DECISION, FLEngine
+
+    stub = type("S", (), {"round_no": 3})()
+    mn = np.zeros((2, DECISION + 1))
+    mn[:, 0] = 1.0
+    mn[:, DECISION] = 77.0
+    FLEngine._check_decisions(stub, mn, np.array([77.0, 77.0]))
+    with _pytest.raises(RuntimeError, match="disagree"):
+        FLEngine._check_decisions(stub, mn, np.array([77.0, 78.0]))
+    mn[1, 0] = 0.0  # an invalid row's word is ignored, the per-rank words are not
+    mn[1, DECISION] = 5.0
+    FLEngine._check_decisions(stub, mn, np.array([77.0, 77.0]))

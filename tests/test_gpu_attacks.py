@@ -67,3 +67,25 @@ def test_gram_centred_matches_fp64_reference(gpu):
     X = U.double() - U.double().mean(0, keepdim=True)
     ref = X @ X.t()
     assert torch.allclose(C, ref, rtol=1e-9, atol=1e-9 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("n,ratio", [(9, 0.999), (9, 0.9999), (64, 0.99), (5, 0.5)])
+def test_fltracer_top_pc_kernel_matches_eigh(gpu, n, ratio):
+    """k_top_pc (Jacobi, one wave) gives numpy eigh's first principal-component scores (up to the sign), also
+    for a nearly flat spectrum top, and FLTracer's device decisions equal the host pipeline's."""
+    import numpy as np
+    from test_aggregators import _fltracer_numpy, _near_degenerate
+
+    from attackfl_amd import agg
+
+    U = _near_degenerate(n, ratio, seed=n).float()
+    z = agg._top_pc_scores(U.to(gpu)).cpu().abs()
+    X = U.double().numpy()
+    Xc = X - X.mean(axis=0, keepdims=True)
+    ev, V = np.linalg.eigh(Xc @ Xc.T)
+    assert torch.allclose(z, torch.from_numpy(np.abs(V[:, -1]) * np.sqrt(ev[-1])), rtol=1e-6, atol=1e-8)
+    sizes = torch.arange(1, n + 1).float()
+    res = agg.fltracer(U.to(gpu), sizes.to(gpu))
+    bad, ref, scores = _fltracer_numpy(U, sizes)
+    assert agg.host_info(res.info)["anomalies"] == bad
+    assert torch.allclose(res.info["scores"].double().cpu(), torch.from_numpy(scores), rtol=1e-5, atol=1e-6)
