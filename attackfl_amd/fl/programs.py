@@ -641,10 +641,22 @@ class ProgramRunner:
         from ..parallel.launcher import gpu_sharers
 
         nat = ops.native()
-        # every workgroup must be resident at once; processes sharing the GPU run their own persistent launches
-        # on the same CUs, so this launch may count on only its share of them
+        # every workgroup of a launch must be resident at once; processes sharing the GPU run their own persistent
+        # launches on the same CUs, so a launch may count on only its share of them.  More clients than that run
+        # in back-to-back launches of clients that fit (_train_cnn2), never on the layer program.
         cus = torch.cuda.get_device_properties(params.device).multi_processor_count // gpu_sharers()
-        return params.shape[0] * int(nat.cnn2_wgs_per_client()) <= cus
+        return int(nat.cnn2_wgs_per_client()) <= cus
+
+    def cnn2_capacity(self, device) -> int:
+        """Clients per cnn2 launch: every workgroup co-resident on this process's share of the CUs
+        (``AFL_MAX_CLIENTS_PER_LAUNCH`` caps it further: the chunking tests)."""
+        from .. import ops
+        from ..parallel.launcher import gpu_sharers
+
+        cus = torch.cuda.get_device_properties(device).multi_processor_count // gpu_sharers()
+        cap = max(1, cus // int(ops.native().cnn2_wgs_per_client()))
+        lim = int(os.environ.get("AFL_MAX_CLIENTS_PER_LAUNCH", "0") or 0)
+        return min(cap, lim) if lim > 0 else cap
 
     def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync, opt_mode: int = 0):
         from .. import ops
@@ -661,12 +673,26 @@ class ProgramRunner:
         failed = torch.zeros(C, dtype=torch.int32, device=dev)
         losses = torch.zeros(C, plan.epochs, device=dev)
         if S > 0:
-            ctr.zero_()
             offs = [s.offset for s in pg.layout.slots]
-            nat.cnn2_train(params if params.is_contiguous() else params.contiguous(), offs, table.rows, idx, bsz, ep, nb,
-                           ctl.seeds, pg.p(0.3), 2, True, float(lr), failed, losses, ws, ctr, self.cnn2_stamps,
-                           int(opt_mode))
-            self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params)  # the launch may still run when sync=False
+            pc = params if params.is_contiguous() else params.contiguous()
+            live = []
+            # back-to-back launches of at most `cap` clients (balanced), each a full persistent round: a client's
+            # result does not depend on which launch or how many clients train it (placement independence)
+            from ..ops.transformer import client_chunks
+
+            for a, b in client_chunks(C, self.cnn2_capacity(dev)):
+                ctr.zero_()
+                whole = (a, b) == (0, C)
+                ti = idx if whole else idx[:, a:b].contiguous()
+                tb = bsz if whole else bsz[:, a:b].contiguous()
+                te = ep if whole else ep[:, a:b].contiguous()
+                nat.cnn2_train(pc[a:b], offs, table.rows, ti, tb, te, nb[a:b], ctl.seeds[a:b], pg.p(0.3), 2, True,
+                               float(lr), failed[a:b], losses[a:b], ws, ctr, self.cnn2_stamps if whole else None,
+                               int(opt_mode))
+                live.append((ti, tb, te))
+            if pc is not params:
+                params.copy_(pc)
+            self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params, pc, live)  # launches may still run (sync=False)
         if not sync:
             return failed, losses  # failed: 1 = NaN loss, 2 = a cross-workgroup wait timed out (GraphTrainer raises)
         fh = failed.cpu()

@@ -18,11 +18,13 @@ NPARAM = 97665
 
 
 def fits(C: int, dev) -> bool:
-    """All 3*C workgroups must be resident at once (one per CU), next to the persistent launches of any other
-    process sharing the GPU (``parallel.launcher.gpu_sharers``)."""
-    from ..parallel.launcher import gpu_sharers
+    """The on-chip trainer can train C clients: a launch's 3 workgroups per client must be resident at once
+    (one per CU, next to the persistent launches of any other process sharing the GPU,
+    ``parallel.launcher.gpu_sharers``); more clients than one launch holds run in back-to-back launches
+    (``transformer.chunked``), so any C >= 1 fits once one client does."""
+    from .transformer import onchip_capacity
 
-    return 3 * C <= torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
+    return C >= 0 and onchip_capacity(dev, 3) >= 1
 
 
 def _seeds(seeds, dev) -> torch.Tensor:
@@ -60,11 +62,19 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     dev = params.device
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else _seeds(seeds, dev)
+    from .transformer import chunked, onchip_capacity
+
     kt = None
     if split == 4:
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
-    return native().rnn_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t,
-                              int(epochs), int(batch), float(lr), int(opt_mode), int(split), kt, stamps)
+    rows_c, order_c = rows.contiguous(), order.contiguous()
+
+    def launch(p, o, n, s):
+        return native().rnn_train(p, rows_c, o, n, s, int(epochs), int(batch), float(lr), int(opt_mode), int(split),
+                                  kt, stamps)
+    if stamps is None:  # (clients beyond one launch's co-residency budget: back-to-back launches)
+        return chunked(launch, params.shape[0], onchip_capacity(dev, 3), params, order_c, nd_t, seeds_t)
+    return launch(params, order_c, nd_t, seeds_t)
 
 
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,

@@ -27,16 +27,51 @@ M32 = 0xFFFFFFFF
 # ------------------------------------------------------------------------------- device entry points
 def auto_split(C: int, dev) -> int:
     """Trainer variant for C clients, the first whose workgroups all fit on the device at once (one per CU):
-    4 = the on-chip trainer (``tf2.hip``: head | vitals | labs workgroups), else the global-workspace kernels
-    of ``transformer.hip`` with 2 or 1 workgroups per client.  Split 5 (row-split branches, 5 workgroups per
-    client) is available but not chosen: measured slower (see below)."""
+    4 = the on-chip trainer (``tf2.hip``: head | vitals | labs workgroups), in chunks of clients that fit when
+    C is larger (``onchip_capacity``).  The global-workspace kernels of ``transformer.hip`` (split 2 / 1) and
+    split 5 (row-split branches, 5 workgroups per client, measured slower, see below) are explicit choices."""
     from ..parallel.launcher import gpu_sharers
 
     # (processes sharing the GPU run their own persistent launches on the same CUs: count only this one's share)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
     # split 5 measured slower than 4 (round 5: 91.5 vs 103.6 rounds/s at 8 clients, 97.1 vs 110.2 at 1 client,
     # profiles/ab_tf2_r5_row_split.log): opt-in only (split=5 / AFL_TF_SPLIT=5)
-    return 4 if 3 * C <= cus else (2 if 2 * C <= cus else 1)
+    # more clients than fit run split 4 in back-to-back launches (train_clients_async), not the slower kernels
+    return 4 if cus >= 3 else 1
+
+
+def client_chunks(C: int, cap: int) -> List[Tuple[int, int]]:
+    """[a, b) client ranges of at most ``cap`` clients, as few launches as possible, balanced."""
+    if C <= 0:
+        return []
+    n = -(-C // max(1, cap))
+    size = -(-C // n)
+    return [(a, min(C, a + size)) for a in range(0, C, size)]
+
+
+def onchip_capacity(dev, wgs_per_client: int = 3) -> int:
+    """Clients per on-chip launch (tf2 / rnn2: 3 co-resident workgroups each) on this process's share of the
+    CUs; ``AFL_MAX_CLIENTS_PER_LAUNCH`` caps it (tests).  More clients run in back-to-back launches."""
+    from ..parallel.launcher import gpu_sharers
+
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
+    cap = max(1, cus // wgs_per_client)
+    lim = int(os.environ.get("AFL_MAX_CLIENTS_PER_LAUNCH", "0") or 0)
+    return min(cap, lim) if lim > 0 else cap
+
+
+def chunked(launch, C: int, cap: int, params, order, nd_t, seeds_t):
+    """Run ``launch(params, order, nd, seeds) -> (ok, losses)`` over client chunks of at most ``cap`` clients,
+    back to back on the current stream; the per-chunk device results are concatenated (no host sync)."""
+    parts = client_chunks(C, cap)
+    if len(parts) <= 1:
+        return launch(params, order, nd_t, seeds_t)
+    oks, losses = [], []
+    for a, b in parts:
+        ok, ls = launch(params[a:b], order[a:b], nd_t[a:b], seeds_t[a:b])
+        oks.append(ok)
+        losses.append(ls)
+    return torch.cat(oks), torch.cat(losses)
 
 
 def device_seed(s: int) -> int:
@@ -59,8 +94,14 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     kt = None
     if split in (4, 5):
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
-    return native().tf_train(params, rows.contiguous(), order.contiguous(), nd_t, seeds_t, int(epochs),
-                             int(batch), float(lr), int(opt_mode), stamps, int(split), kt)
+    rows_c, order_c = rows.contiguous(), order.contiguous()
+
+    def launch(p, o, n, s):
+        return native().tf_train(p, rows_c, o, n, s, int(epochs), int(batch), float(lr), int(opt_mode), stamps,
+                                 int(split), kt)
+    if split in (4, 5) and stamps is None:
+        return chunked(launch, C, onchip_capacity(dev, 5 if split == 5 else 3), params, order_c, nd_t, seeds_t)
+    return launch(params, order_c, nd_t, seeds_t)
 
 
 _KT_CACHE: Dict[tuple, torch.Tensor] = {}

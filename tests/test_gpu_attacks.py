@@ -83,9 +83,12 @@ def test_fltracer_top_pc_kernel_matches_eigh(gpu, n, ratio):
     X = U.double().numpy()
     Xc = X - X.mean(axis=0, keepdims=True)
     ev, V = np.linalg.eigh(Xc @ Xc.T)
-    assert torch.allclose(z, torch.from_numpy(np.abs(V[:, -1]) * np.sqrt(ev[-1])), rtol=1e-6, atol=1e-8)
+    # (the device Gram's fp64 rounding differs from numpy's in the last bits; an eigenvector amplifies that by
+    # 1 / gap = 1e4 here — the repeated-squaring form it replaces was off by 2 % at 0.999 and 66 % at 0.9999)
+    tol = max(1e-5, 1e-7 / (1.0 - ratio))  # both solvers see a problem conditioned like 1 / gap
+    assert torch.allclose(z, torch.from_numpy(np.abs(V[:, -1]) * np.sqrt(ev[-1])), rtol=tol, atol=1e-7)
     sizes = torch.arange(1, n + 1).float()
     res = agg.fltracer(U.to(gpu), sizes.to(gpu))
     bad, ref, scores = _fltracer_numpy(U, sizes)
     assert agg.host_info(res.info)["anomalies"] == bad
-    assert torch.allclose(res.info["scores"].double().cpu(), torch.from_numpy(scores), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(res.info["scores"].double().cpu(), torch.from_numpy(scores), rtol=tol, atol=1e-6)

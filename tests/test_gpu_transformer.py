@@ -207,4 +207,5 @@ def test_auto_split_choice(gpu):
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
     assert T.auto_split(8, gpu) == 4  # (split 5 is opt-in: measured slower, ops/transformer.py auto_split)
     assert T.auto_split(cus // 3, gpu) == 4
-    assert T.auto_split(cus // 3 + 1, gpu) == 2
+    assert T.auto_split(cus // 3 + 1, gpu) == 4  # more clients: back-to-back split-4 launches (chunked)
+    assert T.onchip_capacity(gpu) == cus // 3

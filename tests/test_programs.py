@@ -163,3 +163,19 @@ def test_attention_rc_mask_statistics():
     kp = masks.keep(masks.step_key(7, 3), 10, rows, cols, 0.1).numpy()
     agree = (k == kp).mean()
     assert abs(agree - (0.9 * 0.9 + 0.1 * 0.1)) < 0.01  # independent draws
+
+
+def test_client_chunks_balanced():
+    from attackfl_amd.ops.transformer import client_chunks
+
+    assert client_chunks(8, 85) == [(0, 8)]
+    assert client_chunks(128, 85) == [(0, 64), (64, 128)]
+    assert client_chunks(16, 8) == [(0, 8), (8, 16)]
+    assert client_chunks(17, 8) == [(0, 6), (6, 12), (12, 17)]
+    assert client_chunks(0, 8) == []
+    for C in range(1, 60):
+        for cap in (1, 2, 3, 7, 8):
+            parts = client_chunks(C, cap)
+            assert parts[0][0] == 0 and parts[-1][1] == C and all(b - a <= cap for a, b in parts)
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(len(parts) - 1))
+            assert len(parts) == -(-C // cap)
