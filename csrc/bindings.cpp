@@ -95,6 +95,17 @@ std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
   return {keep, info};
 }
 
+// cross-wave column-sum determinism check (tests): vals [W, 64] fp32 -> [64]
+torch::Tensor fxsum_test(torch::Tensor vals, int64_t seed, int64_t mode) {
+  check_dev(vals, "vals", torch::kFloat32);
+  TORCH_CHECK(vals.dim() == 2 && vals.size(1) == 64 && vals.size(0) >= 1 && vals.size(0) <= 16, "vals [W <= 16, 64]");
+  auto out = torch::empty({64}, vals.options());
+  TORCH_CHECK(afl_fxsum_test(vals.data_ptr<float>(), (int)vals.size(0), (uint32_t)seed, (int)mode, out.data_ptr<float>(),
+                             cur()) == 0, "fxsum_test launch failed");
+  AFL_CHECK_LAUNCH();
+  return out;
+}
+
 // FLTracer PCA(1) scores (agg.fltracer): G = centred Gram [n, n] fp64 -> z [n] fp64
 torch::Tensor top_pc(torch::Tensor G, int64_t sweeps) {
   check_dev(G, "G", torch::kFloat64);
@@ -709,6 +720,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_dots", &row_dots);
   m.def("gmm_filter", &gmm_filter);
   m.def("top_pc", &top_pc);
+  m.def("fxsum_test", &fxsum_test);
   m.def("gram_centred", &gram_centred);
   m.def("stoch_quant", &stoch_quant);
   m.def("adam_flat", &adam_flat);

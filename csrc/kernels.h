@@ -121,6 +121,8 @@ constexpr int AFL_TF2S_SYNC_WORDS = AFL_TF2_SYNC_WORDS + 6 * 2 * 2 * 4 * 1024;
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);
 int afl_tf2_train_stamped(const AflTfTrainArgs* a, hipStream_t s);  // tf2_stamps.hip: per-phase timers
 long afl_tf2_ws_floats();
+// determinism check of the on-chip trainers' cross-wave column sums (tf2.hip k_fxsum_test; tests only)
+int afl_fxsum_test(const float* vals, int W, uint32_t seed, int mode, float* out, hipStream_t s);
 // rnn.hip (RNNModel / ICU fused training: 3 workgroups per client, sync words required)
 int afl_rnn_train(const AflTfTrainArgs* a, hipStream_t s);
 long afl_rnn_ws_floats();

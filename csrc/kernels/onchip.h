@@ -132,10 +132,37 @@ __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  
 }
 
 // column sums over the wave's 16 rows of W values per lane (DPP reduce-scatter, fused_common.h): each
-// lane ends with the sum of one feature; the caller sends it to a per-wave slot (head) or an fp64 LDS
-// accumulator (branches)
-__device__ __forceinline__ void lds_addd(uchar* base, int idx, float v) {
+// lane ends with the sum of one feature; the caller sends it to a per-wave slot (head) or a fixed-point LDS
+// accumulator (branches, below)
+//
+// Cross-wave accumulation that is bit-reproducible BY CONSTRUCTION: every fp32 partial becomes an int64 fixed-
+// point number (quantum 2^-40, rounded to nearest) and the waves add them with 64-bit LDS integer atomics.
+// Integer addition is exact and associative, so the sum has the same bits whatever order the waves arrive
+// in (the fp64 atomics this replaces were order-independent only while the partials' exponents spanned
+// fewer than ~29 bits).  Range: |partial| < 2^19 (8 of them cannot overflow); a NaN / inf / out-of-range
+// partial instead sets its slot group's bit in `flag` (idx >> 6), and the group decodes as NaN — the
+// non-finite result an fp32 sum would have given.  Resolution 2^-40 (~9e-13) absolute: gradient column sums
+// of this size carry ~1e-9 relative error, below fp32's.
+constexpr double FX_ONE = 1099511627776.0;  // 2^40
+__device__ __forceinline__ void lds_addq(uchar* base, int idx, float v, LDS_AS uint32_t* flag) {
+#ifdef ONCHIP_FP64_COLSUM  // A/B variant (tools/ab_native.sh): the round-4 fp64 atomics
   __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return;
+#endif
+  if (!(fabsf(v) < 524288.f)) {
+    __hip_atomic_fetch_or(flag, 1u << (idx >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  const long long q = (long long)__builtin_rint((double)v * FX_ONE);
+  __hip_atomic_fetch_add((LDS_AS long long*)base + idx, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the accumulated value of slot idx (read after the barrier that follows every add)
+__device__ __forceinline__ float lds_getq(const uchar* base, int idx, const LDS_AS uint32_t* flag) {
+#ifdef ONCHIP_FP64_COLSUM
+  return (float)((const LDS_AS double*)base)[idx];
+#endif
+  if ((*flag >> (idx >> 6)) & 1u) return __builtin_nanf("");
+  return (float)((double)((const LDS_AS long long*)base)[idx] * (1.0 / FX_ONE));
 }
 // partner lane's value (bound_ctrl: 0 for a missing source, which none of these patterns has) in the
 // form the backend's DPP combine folds into the consuming add

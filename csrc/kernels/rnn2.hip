@@ -56,11 +56,12 @@ constexpr int B_DG = B_X3 + 16384;                 // 3 x tile64: d(gate pre-act
 constexpr int B_NVEC = 1280;                       // 6 x (b_ih 96 | b_hh 96) in (layer, direction) order, LN w | b
 constexpr int B_VEC = B_DG + 3 * 16384;            // fp32 [1280] bias / LayerNorm parameters
 constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [1280] their gradients
-// fp64 column sums produced wave-locally (order-independent 8-wave sums, as tf2.hip): LN weight / bias
-// (0..127), then per layer the d(b_hn) sums of both directions (128 + 64 (l - 1) + 32 d + j)
+// int64 fixed-point column sums produced wave-locally (onchip.h lds_addq: 8-wave sums independent of the wave
+// order by construction, as tf2.hip): LN weight / bias (0..127), then per layer the d(b_hn) sums of both
+// directions (128 + 64 (l - 1) + 32 d + j)
 constexpr int B_NDBL = 128 + 3 * 64;
 constexpr int B_DBL = B_CS + B_NVEC * 4;
-constexpr int B_MISC = B_DBL + B_NDBL * 8;         // u32 [8] per-wave abort words
+constexpr int B_MISC = B_DBL + B_NDBL * 8;         // u32 [8] per-wave abort words, [8] the DBL poison flags
 constexpr int B_TOTAL = B_MISC + 64;
 constexpr int B_X1 = B_X2, B_GS = B_X3;
 enum { VL_LNW = 1152, VL_LNB = 1216 };
@@ -406,7 +407,7 @@ __device__ __forceinline__ void gate_bwd(uchar* smem, const float (&dh)[16], con
 __device__ __forceinline__ void dnr_colsum(uchar* smem, int L, const float (&dnr)[16], int lane) {
   float s;
   const int f = colsum64(dnr, lane, s);
-  lds_addd(smem + B_DBL, 128 + 64 * (L - 1) + f, s);
+  lds_addq(smem + B_DBL, 128 + 64 * (L - 1) + f, s, ldsu(smem, B_MISC) + 8);
 }
 
 // backward of layer L (3 or 2) up to its d(input): dh (in) -> dG tile, dx (out)
@@ -531,9 +532,8 @@ __device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wa
     if (g == 0) bias_cs(smem, 1, Tn, i16, bs[0]);
   }
   if (tid < B_NDBL) {
-    LDS_AS double* dbl = (LDS_AS double*)(smem + B_DBL);
-    const float s = (float)dbl[tid];
-    dbl[tid] = 0.0;
+    const float s = lds_getq(smem + B_DBL, tid, ldsu(smem, B_MISC) + 8);
+    ((LDS_AS long long*)(smem + B_DBL))[tid] = 0;
     int e;
     if (tid < 128) {
       e = VL_LNW + tid;
@@ -694,9 +694,9 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
       float s;
       int f = colsum64(t, lane, s);
-      lds_addd(smem + B_DBL, f, s);
+      lds_addq(smem + B_DBL, f, s, abort_w + 8);
       f = colsum64(dy, lane, s);
-      lds_addd(smem + B_DBL, 64 + f, s);
+      lds_addq(smem + B_DBL, 64 + f, s, abort_w + 8);
       vec16(gm, smem + B_VEC + 4 * VL_LNW, g);
       ln_bwd2(dh, dy, xh, sv.rstd, gm);
     }
@@ -751,6 +751,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     compact_mom_ld(rm, tid, cmom);
     lds_bar();  // C: every gradient of the compact entries in CS / GS
     stp(9, tid);
+    if (tid == 0) abort_w[8] = 0u;  // (the DBL poison flags: every read is behind barrier C)
     asm volatile(";MARK u3");
     compact_update(smem, R, st, rm, cmom, K, lane, tid);
     stp(10, tid);

@@ -60,16 +60,17 @@ constexpr int B_NVEC = 648;                        // 10 x 64 vectors + ffn.0 bi
 constexpr int B_VEC = B_DF0 + 4096;                // fp32 [648] bias / LayerNorm parameters
 constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [648] their gradients (column sums)
 // The LayerNorm gradient column sums (6 x 64, produced wave-locally during the backward) are summed over
-// the 8 waves with fp64 LDS atomics into DBL, which ALIASES CS (+ 480 bytes): the remaining CS entries are
-// written only after the backward, and the fp64 sums are moved to their CS slots at the start of the
-// update.  fp64 makes the 8-way sum independent of the order the waves arrive in (exact whenever the
-// partials span < 2^26; otherwise a double rounding below fp32 resolution), so a client's trajectory is
-// bit-reproducible whatever launch or rank trains it (fp32 LDS atomics were not: ~1e-4 drift per round).
+// the 8 waves as int64 fixed point with LDS integer atomics (onchip.h lds_addq) into DBL, which ALIASES CS
+// (+ 480 bytes): the remaining CS entries are written only after the backward, and the sums are moved to
+// their CS slots at the start of the update.  Integer addition makes the 8-way sum independent of the order
+// the waves arrive in by construction, so a client's trajectory is bit-reproducible whatever launch or rank
+// trains it (fp32 LDS atomics were not: ~1e-4 drift per round; fp64 ones only while the partials spanned
+// < 2^29).
 constexpr int B_NLN = 6 * 64;
-constexpr int B_DBL = B_CS;                        // fp64 [384]: G1 B1 G2 B2 G3 B3
+constexpr int B_DBL = B_CS;                        // int64 [384]: G1 B1 G2 B2 G3 B3
 constexpr int B_DBL_BYTES = B_NLN * 8;
 static_assert(B_DBL_BYTES >= B_NVEC * 4, "DBL covers CS");
-constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words
+constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words, [8] the DBL poison flags
 constexpr int B_TOTAL = B_MISC + 64;
 // vector segments (x64 floats) of VEC / CS
 enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3 };
@@ -112,7 +113,7 @@ constexpr long WS_BYTES = WS_MOM + 5 * MOM_WG_BYTES;  // head, 2 branches x (1 o
 __device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
   float s;
   const int f = colsum64(x, lane, s);
-  lds_addd(smem + B_DBL, 64 * k + f, s);
+  lds_addq(smem + B_DBL, 64 * k + f, s, ldsu(smem, B_MISC) + 8);
 }
 __host__ __device__ constexpr int ln_seg(int k) { return k < 2 ? VS_G1 + k : VS_G2 + (k - 2); }
 static_assert(ln_seg(0) == VS_G1 && ln_seg(1) == VS_B1 && ln_seg(2) == VS_G2 && ln_seg(3) == VS_B2 &&
@@ -668,9 +669,10 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     }
   }
   // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
-  const float lnsum = tid < B_NLN ? (float)((LDS_AS double*)(smem + B_DBL))[tid] : 0.f;
+  const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid, ldsu(smem, B_MISC) + 8) : 0.f;
   lds_bar();
   stp(5, tid);
+  if (tid == 0) ldsu(smem, B_MISC)[8] = 0u;  // (poison flags: every read is behind the barrier)
   if (tid < B_NLN) ldsf(smem, B_CS)[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
   const f4v cm = mom_ld(rm, 8, tid), cv = mom_ld(rm, 9, tid), cmv = mom_ld(rm, 10, tid);
   // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
@@ -1735,6 +1737,38 @@ __global__ void __launch_bounds__(t2::NTH) K_TF2S(AflTfTrainArgs a) {
       t2::branch_split<1>(a, cid, smem, h);
   }
 }
+
+#ifndef TF2_STAMPS
+// Determinism check of the cross-wave column-sum accumulator (onchip.h lds_addq), used by the tests: W waves
+// each add their 64 partials (vals [W][64]) into 64 slots after a per-wave delay drawn from `seed` (so the
+// arrival order changes from launch to launch); out [64] = the decoded sums.  mode 1: the fp64 LDS atomics the
+// trainers used before (order-dependent once the partials span more than ~2^29).
+__global__ void __launch_bounds__(1024) k_fxsum_test(const float* __restrict__ vals, int W, uint32_t seed, int mode,
+                                                   float* __restrict__ out) {
+  __shared__ long long q[64];
+  __shared__ uint32_t flag;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x < 64) q[threadIdx.x] = 0;
+  if (threadIdx.x == 0) flag = 0u;
+  __syncthreads();
+  const uint32_t spins = afl_hash32(seed, (uint32_t)w) & 1023u;
+  for (uint32_t i = 0; i < spins; ++i) __builtin_amdgcn_s_sleep(1);
+  const float v = vals[w * 64 + lane];
+  if (mode == 0)
+    oc::lds_addq((oc::uchar*)q, lane, v, (LDS_AS uint32_t*)&flag);
+  else
+    __hip_atomic_fetch_add((LDS_AS double*)q + lane, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  if (threadIdx.x < 64)
+    out[lane] = mode == 0 ? oc::lds_getq((const oc::uchar*)q, lane, (const LDS_AS uint32_t*)&flag)
+                          : (float)((LDS_AS double*)q)[lane];
+}
+int afl_fxsum_test(const float* vals, int W, uint32_t seed, int mode, float* out, hipStream_t s) {
+  if (W < 1 || W > 16) return -1;
+  hipLaunchKernelGGL(k_fxsum_test, dim3(1), dim3(64 * W), 0, s, vals, W, seed, mode, out);
+  return (int)hipGetLastError();
+}
+#endif
 
 #ifdef TF2_STAMPS
 int afl_tf2_train_stamped(const AflTfTrainArgs* a, hipStream_t s) {

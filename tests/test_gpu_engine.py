@@ -235,10 +235,35 @@ def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
         return info
 
     eng._aggregate = capture
+    fl_seen = []
+    if mode == "FLTrust":  # the rows, g_0 and the server model around every device FLTrust aggregate
+        orig_fl = eng._fltrust
+
+        def cap_fl(U):
+            g0 = (eng.global_params if eng.global_params is not None else eng.fltrust_model).detach().cpu().clone()
+            out = orig_fl(U)
+            fl_seen.append((U.detach().cpu().clone(), g0, eng.fltrust_model.detach().cpu().clone(),
+                            out.detach().cpu().clone()))
+            return out
+
+        eng._fltrust = cap_fl
     hist = eng.run()
     eng.close()
     assert [r["ok"] for r in hist] == [True, True, True]
     assert len(seen) == 3
+    if mode == "FLTrust":
+        # the trust / rescale math of server.py:714-740 in fp64 on the captured rows and server delta
+        assert len(fl_seen) == 3
+        for U, g0, server_new, out in fl_seen:
+            d = (U - g0[None, :]).double()
+            gd = (server_new - g0).double()
+            dn = d.norm(dim=1)
+            cos = (d @ gd) / torch.clamp(dn * gd.norm(), min=1e-8)
+            trust = cos.clamp_min(0.0)
+            w = (gd.norm() / (dn + 1e-6)) * trust / (trust.sum() + 1e-6)
+            ref = g0.double() + (w[:, None] * d).sum(0)
+            assert (out.double() - ref).abs().max().item() <= 2e-5 * max(1.0, ref.abs().max().item())
+            assert bool((trust > 0).any())  # (some clients trusted: the check is not vacuous)
     if mode != "FLTrust":  # (FLTrust trains a server model: its composite would need the CPU trainer)
         from attackfl_amd.agg import AGGREGATORS
         for rows, sizes, att, got, rnd in seen:

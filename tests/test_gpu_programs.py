@@ -453,3 +453,79 @@ def test_cnn2_nan_loss_fails_only_that_client(gpu, monkeypatch, nan_at):
         ok1, _ = r1.train(DeviceTable(ds, DEV), q, Plan(plan.order[c:c + 1].to(DEV), plan.nd[c:c + 1], 1), lr=1e-3,
                           seeds=[3 + c])
         assert bool(ok1.all()) and torch.equal(q[0], p[c])
+
+
+
+def _har_slot_errors(res, lay):
+    """Per ParamLayout slot: (relative norm error, max error / the slot's own max) of res[0] vs res[1]."""
+    out = {}
+    for sl in lay.slots:
+        a, b = (r[:, sl.offset:sl.offset + sl.numel] for r in res)
+        if float(b.abs().max()) == 0.0 and float(a.abs().max()) == 0.0:
+            continue  # (the positional-encoding buffer: no gradient)
+        out[sl.name] = (((a - b).norm() / (b.norm() + 1e-12)).item(),
+                        ((a - b).abs().max() / (b.abs().max() + 1e-12)).item())
+    return out
+
+
+@pytest.mark.parametrize("B,drop", [(16, True), (24, False)])
+def test_har_encoder_sgd_gradients_per_tensor(gpu, B, drop):
+    """har.hip (the bf16 TransformerClassifier encoder: stem, q|k|v, flash attention, post / FFN row passes and
+    their backward) at the reference shape L = 561, C = 2: one raw-SGD step exposes every gradient, compared
+    PER TENSOR with the fp32 composite (CPU) on the same rows and dropout masks — each slot judged against its
+    own scale, so a wrong LayerNorm / bias / conv gradient far below in_proj's magnitude cannot hide
+    (reference model src/Model.py:418-458)."""
+    C, n = 2, 4 * B
+    ds = synthetic_har(n)
+    order = torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(c))[:B] for c in range(C)])
+    plan = Plan(order[:, None, :].to(torch.int32), torch.tensor([B] * C, dtype=torch.int32), 1)
+    params = _params("TransformerClassifier", C)
+    res, losses = [], []
+    for dev in (DEV, "cpu"):
+        p = params.clone().to(dev)
+        ok, ls = ProgramRunner(make_program("TransformerClassifier", C, B, dev, dropout=drop), use_graph=False).train(
+            DeviceTable(ds, dev), p, Plan(plan.order.to(dev), plan.nd, 1), lr=0.0, seeds=[3, 4], sgd_lr=1.0)
+        assert ok.all()
+        res.append(params - p.cpu())
+        losses.append(ls.cpu())
+    assert torch.allclose(losses[0], losses[1], rtol=1e-2), (losses[0], losses[1])
+    errs = _har_slot_errors(res, ParamLayout.for_model("TransformerClassifier"))
+    print({k: (round(a, 4), round(b, 4)) for k, a in errs.items()})
+    bad = {k: v for k, v in errs.items() if v[0] > HAR_GRAD_NORM_TOL or v[1] > HAR_GRAD_MAX_TOL}
+    assert not bad, bad
+
+
+HAR_GRAD_NORM_TOL, HAR_GRAD_MAX_TOL = 0.10, 0.25
+
+
+def test_har_encoder_adam_epochs_track_composite(gpu):
+    """Three epochs of Adam (9 steps per client, dropout on) through the fused HAR path track the fp32
+    composite: per-epoch losses, and per tensor the device-vs-composite deviation stays a small fraction of
+    the distance the composite moved."""
+    C, B, E, n = 2, 16, 3, 96
+    ds = synthetic_har(n)
+    nd = [48, 41]
+    order = torch.stack([torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(10 * c + e))[:max(nd)]
+                                      for e in range(E)]) for c in range(C)]).to(torch.int32)
+    params = _params("TransformerClassifier", C)
+    res, losses = [], []
+    for dev in (DEV, "cpu"):
+        p = params.clone().to(dev)
+        ok, ls = ProgramRunner(make_program("TransformerClassifier", C, B, dev)).train(
+            DeviceTable(ds, dev), p, Plan(order.to(dev), torch.tensor(nd, dtype=torch.int32), E), lr=1e-3,
+            seeds=[5, 6])
+        assert ok.all()
+        res.append(p.cpu())
+        losses.append(ls.cpu())
+    assert torch.allclose(losses[0], losses[1], rtol=2e-2, atol=2e-3), (losses[0], losses[1])
+    lay = ParamLayout.for_model("TransformerClassifier")
+    bad = {}
+    for sl in lay.slots:
+        a, b, p0 = (t[:, sl.offset:sl.offset + sl.numel] for t in (res[0], res[1], params))
+        moved = (b - p0).norm().item()
+        if moved == 0.0:
+            continue
+        r = (a - b).norm().item() / moved
+        if r > 0.15:
+            bad[sl.name] = round(r, 4)
+    assert not bad, bad

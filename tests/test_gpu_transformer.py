@@ -209,3 +209,31 @@ def test_auto_split_choice(gpu):
     assert T.auto_split(cus // 3, gpu) == 4
     assert T.auto_split(cus // 3 + 1, gpu) == 4  # more clients: back-to-back split-4 launches (chunked)
     assert T.onchip_capacity(gpu) == cus // 3
+
+
+def test_cross_wave_column_sums_are_order_independent(gpu):
+    """The on-chip trainers' cross-wave gradient column sums (onchip.h lds_addq: int64 fixed point, LDS integer
+    atomics) give the same bits whatever order the 8 waves arrive in, with adversarial partials whose exponents
+    span more than 2^50 and cancel (the fp64 atomics they replace were order-independent only within ~2^29),
+    and equal the exactly rounded fixed-point sum."""
+    from fractions import Fraction
+
+    from attackfl_amd.ops import native
+
+    g = torch.Generator().manual_seed(0)
+    W = 8
+    mant = 1.0 + torch.rand(W, 64, generator=g)
+    expo = torch.tensor([18, -35, 18, -30, 10, -36, 17, -20], dtype=torch.float64)[:, None]
+    sign = torch.where(torch.rand(W, 64, generator=g) < 0.5, -1.0, 1.0)
+    vals = (sign * mant.double() * torch.pow(2.0, expo)).float()
+    vals[2] = -vals[0]  # exact cancellation of the two largest partials: the result lives in the low bits
+    outs = {native().fxsum_test(vals.to(gpu), seed, 0).cpu().numpy().tobytes() for seed in range(48)}
+    assert len(outs) == 1
+    got = torch.frombuffer(bytearray(outs.pop()), dtype=torch.float32)
+    q = [[round(Fraction(float(v)) * 2 ** 40) for v in vals[:, j].tolist()] for j in range(64)]
+    exp = torch.tensor([float(Fraction(sum(c), 2 ** 40)) for c in q], dtype=torch.float64).float()
+    assert torch.equal(got, exp)
+    # a non-finite partial poisons its slot group (decoded NaN, as an fp32 sum would give)
+    bad = vals.clone()
+    bad[3, 5] = float("nan")
+    assert torch.isnan(native().fxsum_test(bad.to(gpu), 1, 0).cpu()).all()
