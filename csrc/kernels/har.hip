@@ -371,7 +371,17 @@ __device__ __forceinline__ f4v mfma16(s4v a, s4v b, f4v c) { return __builtin_am
 __device__ __forceinline__ f4v mfma32(s8v a, s8v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
 }
-__device__ __forceinline__ s4v lds4(const uchar* img, int r, int p) { return *(const LDS_AS s4v*)(img + rch(r, p)); }
+// One ds_read_b64 per call: the row is made opaque so the compiler cannot pair two reads 16 rows apart into a
+// ds_read2st64_b64 / ds_read2_b64, whose banking is (a/4) mod 32 in 16-lane groups — rows r and r + 4 of this
+// layout then share banks (2-way conflicts; the round-4 PMC pass measured 3.63 conflict cycles per LDS
+// instruction in dQ, 1.97 in the forward).  As ds_read_b64 (mod 64, two 32-lane halves) the swizzle is
+// conflict-free.
+__device__ __forceinline__ s4v lds4(const uchar* img, int r, int p) {
+#ifndef HAR_LDS_PAIRED  // (A/B variant: the round-4 code the compiler paired)
+  asm volatile("" : "+v"(r));
+#endif
+  return *(const LDS_AS s4v*)(img + rch(r, p));
+}
 // transposed fragment: lane (q, p) of group g addresses row base(g) + q, chunk p -> column (lane & 15) of the 4 rows
 __device__ __forceinline__ s8v trfrag(const uchar* img, int base0, int base1, int lane) {
   const int i = lane & 15;

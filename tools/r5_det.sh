@@ -12,3 +12,5 @@ grep -E "passed|failed|Error" gpurun_out/det_tests.log | tail -5
 bash tools/ab_native.sh attackfl_amd/_C_ab.so 4 --steps 20 --warmup 3 > gpurun_out/ab_fxsum_tf.log 2>&1 || exit 1
 bash tools/ab_native.sh attackfl_amd/_C_ab.so 3 --steps 20 --warmup 3 --model RNNModel > gpurun_out/ab_fxsum_rnn.log 2>&1 || exit 1
 cat gpurun_out/ab_fxsum_tf.log gpurun_out/ab_fxsum_rnn.log
+bash tools/ab_native.sh attackfl_amd/_C_ab.so 2 --steps 3 --warmup 1 --model TransformerClassifier --data-name HAR > gpurun_out/ab_har_lds.log 2>&1 || exit 1
+cat gpurun_out/ab_har_lds.log
