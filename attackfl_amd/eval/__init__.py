@@ -7,8 +7,8 @@ round.  HAR: accuracy.  CIFAR10 (``test_image`` / ``test_hyper_image``, ``src/Va
 pools every client's loss and hits but still divides by ONE test-set length, like the reference.  ``test_hyper`` pools the outputs of every client's hypernetwork-generated
 model before one ROC-AUC, like ``test_hyper_icu``.  The test set stays resident on the device
 and is evaluated in one pass (eval mode is batch-size independent).  On GPU every ICU / HAR model
-runs a native forward: TransformerModel the fused HIP eval kernel, CNNModel / RNNModel /
-TransformerClassifier their layer program (``fl/programs.py``) in eval mode.  CIFAR10 images (the
+runs a native forward: TransformerModel / RNNModel / CNNModel their fused HIP eval kernels (C models per launch),
+TransformerClassifier its layer program (``fl/programs.py``) in eval mode.  CIFAR10 images (the
 reference ships no image model) go through the eager PyTorch module on either device.
 """
 from __future__ import annotations
@@ -25,6 +25,14 @@ from ..utils.log import print_with_color
 
 EVAL_CHUNK = 65536
 PROGRAM_EVAL_BATCH = {"CNNModel": 4096, "RNNModel": 16384, "TransformerClassifier": 256}
+
+
+def cnn_eval_many(params: torch.Tensor, rows: torch.Tensor, layout: Optional[ParamLayout] = None) -> torch.Tensor:
+    """Sigmoid outputs of C CNNModels (``params [C, P]``, eval mode) over ICU ``rows [n, 24]`` -> ``[C, n]``: one
+    launch (``cnn2.hip`` ``k_cnn2_eval``: bf16 MFMA convolutions and fc1, fp32 head)."""
+    lay = layout or ParamLayout.for_model("CNNModel")
+    p = params if params.dim() == 2 else params[None]
+    return ops.native().cnn2_eval(p.contiguous(), [s.offset for s in lay.slots], rows.contiguous())
 
 
 class Validation:
@@ -62,6 +70,8 @@ class Validation:
             from ..ops.rnn import eval_many
 
             return eval_many(flat[None], self.table.rows)[0]
+        if self.data_name == "ICU" and self.model_name == "CNNModel" and self.device.type == "cuda":
+            return cnn_eval_many(flat[None], self.table.rows, self.layout)[0]
         if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and self.data_name != "CIFAR10":
             # the layer programs take ICU rows / HAR sequences; images go through the eager model below
             data = self.table.rows if self.data_name == "ICU" else self.table.x
@@ -146,6 +156,11 @@ class Validation:
 
             flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32).contiguous()
             out = eval_many(flats, self.table.rows).reshape(-1)
+            return self._finish_icu(out, self._labels().repeat(num_client))
+        if self.device.type == "cuda" and self.model_name == "CNNModel" and num_client > 0:
+            # every client's generated model in ONE fused launch (cnn2.hip k_cnn2_eval)
+            flats = hnet.generate_many(range(num_client)).to(self.device, torch.float32).contiguous()
+            out = cnn_eval_many(flats, self.table.rows, self.layout).reshape(-1)
             return self._finish_icu(out, self._labels().repeat(num_client))
         if self.device.type == "cuda" and self.model_name in PROGRAM_EVAL_BATCH and num_client > 0:
             # every client's generated model through ONE client-batched eval program

@@ -98,7 +98,7 @@ std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
 // cross-wave column-sum determinism check (tests): vals [W, 64] fp32 -> [64]
 torch::Tensor fxsum_test(torch::Tensor vals, int64_t seed, int64_t mode) {
   check_dev(vals, "vals", torch::kFloat32);
-  TORCH_CHECK(vals.dim() == 2 && vals.size(1) == 64 && vals.size(0) >= 1 && vals.size(0) <= 16, "vals [W <= 16, 64]");
+  TORCH_CHECK(vals.dim() == 2 && vals.size(1) == 64 && vals.size(0) >= 1 && vals.size(0) <= 8, "vals [W <= 8, 64]");
   auto out = torch::empty({64}, vals.options());
   TORCH_CHECK(afl_fxsum_test(vals.data_ptr<float>(), (int)vals.size(0), (uint32_t)seed, (int)mode, out.data_ptr<float>(),
                              cur()) == 0, "fxsum_test launch failed");

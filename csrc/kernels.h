@@ -229,6 +229,8 @@ long afl_cnn2_ws_bytes();
 int afl_cnn2_ctr_words();
 int afl_cnn2_wgs_per_client();
 int afl_cnn2_train(const AflCnn2Args& a, hipStream_t s);
+int afl_cnn2_eval(const float* params, long pstride, const int* off, int C, const float* rows, int n, float* out,
+                  hipStream_t s);
 int afl_cnn_towers_fwd(const AflCnnTowers& a, hipStream_t s);
 int afl_cnn_towers_bwd(const AflCnnTowers& a, hipStream_t s);
 struct AflConvDwJob {

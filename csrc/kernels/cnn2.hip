@@ -1513,6 +1513,229 @@ __global__ void __launch_bounds__(NTH) k_cnn2_train(AflCnn2Args a) {
 #endif
 }
 
+// ============================================================================================== eval
+// Forward-only CNNModel (eval mode: dropout off) of C models over rows [n][24] in ONE launch, grid (ceil(n / 16), C):
+// the validation pass (src/Validation.py:19-68; the layer program spent ~1 ms per 4096 rows in k_cnn_fwd).  A workgroup
+// takes 16 samples through both towers with the trainer's padded-row bf16 MFMA convolutions (the vitals tower as one
+// 144-row pass, the labs tower as two 8-sample passes), fc1 on MFMA from the concat features in LDS, and the small
+// fc2 / fc3 / output head in fp32.  Weights are read straight from the fp32 arena (bf16 fragments built in registers),
+// so no image preparation launch is needed.
+constexpr int E_H1 = 0, E_H2 = E_H1 + NR * LD1 * 2, E_H3 = E_H2 + NR * LD2 * 2, E_XS = E_H3 + NR * LD3 * 2;
+constexpr int ELDF = 1032;                     // concat feature row stride (1024 + 8 bf16)
+constexpr int E_FT = E_XS + 656;               // concat features bf16 [16][ELDF]
+constexpr int E_A1 = E_FT + 16 * ELDF * 2;     // relu(fc1) fp32 [16][132]
+constexpr int E_A2 = E_A1 + 16 * 132 * 4;      // relu(fc2) fp32 [16][68]
+constexpr int E_A3 = E_A2 + 16 * 68 * 4;       // relu(fc3) fp32 [16][36]
+constexpr int E_LDS = E_A3 + 16 * 36 * 4;
+static_assert(E_LDS <= 160 * 1024 && (E_FT & 15) == 0 && (E_A1 & 15) == 0, "cnn2 eval LDS");
+
+__device__ __forceinline__ s8v bf8(f4v lo, f4v hi) {
+  return s8v{(short)bfu(lo[0]), (short)bfu(lo[1]), (short)bfu(lo[2]), (short)bfu(lo[3]),
+             (short)bfu(hi[0]), (short)bfu(hi[1]), (short)bfu(hi[2]), (short)bfu(hi[3])};
+}
+// 8 elements at stride 3 (a conv weight column over 8 input channels of one tap) -> bf16 fragment
+__device__ __forceinline__ s8v bf8s3(const float* p) {
+  s8v r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (short)bfu(p[3 * e]);
+  return r;
+}
+
+// one tower pass: samples s0 .. s0 + R - 1 (R = 16 vitals / 8 labs) -> feature rows fr0 .. fr0 + R - 1
+template <int T>
+__device__ __forceinline__ void eval_tower(const float* P, const int* of, const float* rows, int n, int s0, int fr0,
+                                           uchar* S, int tid, int lane, int wave) {
+  using C = TW<T>;
+  const int g = lane >> 4, li = lane & 15;
+  const float* cp1 = P + of[6 * T + 0];
+  // x per padded row (XS index i holds padded row i - 1; pads and samples past n are zeros)
+  for (int i = tid; i < 146; i += NTH) {
+    const int q = i - 1;
+    float v = 0.f;
+    if (q >= 0 && valid_q(q, C::LP)) {
+      const int smp = s0 + q / C::LP, l = q % C::LP - 1;
+      if (smp < n) v = rows[(long)smp * 24 + C::XOFF + l];
+    }
+    *lf(S, E_XS + i * 4) = v;
+  }
+  const int o1 = tid & 31;
+  const float w10 = cp1[3 * o1], w11 = cp1[3 * o1 + 1], w12 = cp1[3 * o1 + 2], bb1 = P[of[6 * T + 1] + o1];
+  const int nt2 = wave & 3, mp2 = wave >> 2;
+  s8v w2f[3], w3f[6];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) w2f[j] = bf8s3(P + of[6 * T + 2] + ((16 * nt2 + li) * 32 + 8 * g) * 3 + j);
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    w3f[k] = bf8s3(P + of[6 * T + 4] + ((16 * wave + li) * 64 + 32 * (k & 1) + 8 * g) * 3 + (k >> 1));
+  const f4v b2v = *(const f4v*)(P + of[6 * T + 3] + 16 * nt2 + 4 * g);
+  const f4v b3v = *(const f4v*)(P + of[6 * T + 5] + 16 * wave + 4 * g);
+  lbar();
+  // conv1 (1 -> 32) on VALU -> H1 (bf16), pads exact zeros
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int q = (tid >> 5) + 16 * u;
+    float h = 0.f;
+    if (valid_q(q, C::LP)) {
+      const float xm = *lf(S, E_XS + q * 4), x0 = *lf(S, E_XS + (q + 1) * 4), xp = *lf(S, E_XS + (q + 2) * 4);
+      h = relu(bb1 + w10 * xm + w11 * x0 + w12 * xp);
+    }
+    *lu16(S, E_H1 + ((q + 1) * LD1 + o1) * 2) = bfu(h);
+  }
+  lbar();
+  // conv2 (transposed GEMM, as the trainer): wave n-tile nt2, m-tiles mp2, mp2 + 2, ...
+  for (int mt0 = mp2; mt0 < 9; mt0 += 4) {
+    f4v acc[2] = {Z4, Z4};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = mfma(w2f[j], rfrag(S + E_H1, LD1, 16 * (mt0 + 2 * t) + j, 0, lane), acc[t]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int q = 16 * (mt0 + 2 * t) + li;
+      if (mt0 + 2 * t < 9)
+        *(LDS_AS u32x2v*)(S + E_H2 + ((q + 1) * LD2 + 16 * nt2 + 4 * g) * 2) = relu_pack4(acc[t], b2v, valid_q(q, C::LP));
+    }
+  }
+  lbar();
+  // conv3: wave = n-tile, all 9 m-tiles
+#pragma unroll
+  for (int mt0 = 0; mt0 < 9; mt0 += 3) {
+    f4v acc[3] = {Z4, Z4, Z4};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        acc[t] = mfma(w3f[k], rfrag(S + E_H2, LD2, 16 * (mt0 + t) + (k >> 1), 32 * (k & 1), lane), acc[t]);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int q = 16 * (mt0 + t) + li;
+      *(LDS_AS u32x2v*)(S + E_H3 + ((q + 1) * LD3 + 16 * wave + 4 * g) * 2) = relu_pack4(acc[t], b3v, valid_q(q, C::LP));
+    }
+  }
+  lbar();
+  // AdaptiveAvgPool1d(4) -> feature rows (concat column COL0 + 4 channel + bin)
+#pragma unroll
+  for (int it = 0; it < 16 * 64 / NTH; ++it) {
+    const int e = tid + NTH * it, r = e >> 6, cp = e & 63;
+    if (r < C::R) {
+      float h0[C::L], h1v[C::L], f[8];
+#pragma unroll
+      for (int l = 0; l < C::L; ++l) {
+        const uint32_t w = *(const LDS_AS uint32_t*)(S + E_H3 + ((r * C::LP + 2 + l) * LD3 + 2 * cp) * 2);
+        h0[l] = __uint_as_float(w << 16);
+        h1v[l] = __uint_as_float(w & 0xFFFF0000u);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int l = bin_lo(p, C::L); l < bin_hi(p, C::L); ++l) {
+          a0 += h0[l];
+          a1 += h1v[l];
+        }
+        f[p] = a0 * bin_rcp(p, C::L);
+        f[4 + p] = a1 * bin_rcp(p, C::L);
+      }
+      *(LDS_AS u32x4*)(S + E_FT + ((fr0 + r) * ELDF + C::COL0 + 8 * cp) * 2) =
+          u32x4{pk2(f[0], f[1]), pk2(f[2], f[3]), pk2(f[4], f[5]), pk2(f[6], f[7])};
+    }
+  }
+  lbar();
+}
+
+struct AflCnn2Eval {
+  const float* params;
+  long pstride;
+  int off[20];
+  const float* rows;
+  int n;
+  float* out;  // [C][n]
+};
+
+__global__ void __launch_bounds__(NTH) k_cnn2_eval(AflCnn2Eval a) {
+  extern __shared__ __attribute__((aligned(16))) uchar smem_raw[];
+  uchar* S = smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15, c = blockIdx.y, s0 = blockIdx.x * 16;
+  const float* P = a.params + (long)c * a.pstride;
+  // zero the activation buffers once: their boundary rows are never written (exact zeros for every pass)
+  for (int e = tid; e < E_XS / 16; e += NTH) *(LDS_AS u32x4*)(S + 16 * e) = u32x4{0u, 0u, 0u, 0u};
+  lbar();
+#if !defined(CNN2_EVAL_ABL) || !(CNN2_EVAL_ABL & 2)  // (timing ablation: no towers)
+  eval_tower<0>(P, a.off, a.rows, a.n, s0, 0, S, tid, lane, wave);
+  eval_tower<1>(P, a.off, a.rows, a.n, s0, 0, S, tid, lane, wave);
+  eval_tower<1>(P, a.off, a.rows, a.n, s0 + 8, 8, S, tid, lane, wave);
+#endif
+  // fc1: z1[16 samples][128] = feat . W1^T, wave = n-tile; W1 rows 16 w + li converted to bf16 in registers
+  {
+    const float* W1 = P + a.off[12] + (long)(16 * wave + li) * 1024 + 8 * g;
+    f4v acc = Z4;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s8v wf[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+#if defined(CNN2_EVAL_ABL) && (CNN2_EVAL_ABL & 1)  // (timing ablation: no W1 loads)
+        wf[k] = s8v{(short)k, 1, 2, 3, 4, 5, 6, (short)kb};
+#else
+        const f4v lo = *(const f4v*)(W1 + 32 * (8 * kb + k)), hi = *(const f4v*)(W1 + 32 * (8 * kb + k) + 4);
+        wf[k] = bf8(lo, hi);
+#endif
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = mfma(rfrag(S + E_FT, ELDF, 0, 32 * (8 * kb + k), lane), wf[k], acc);
+    }
+    const float b1 = P[a.off[13] + 16 * wave + li];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *lf(S, E_A1 + ((4 * g + e) * 132 + 16 * wave + li) * 4) = relu(acc[e] + b1);
+  }
+  lbar();
+  // fc2 (128 -> 64) + ReLU: thread (sample r, outputs o, o + 32)
+  {
+    const int r = tid >> 5, o = tid & 31;
+    const float* w0 = P + a.off[14] + o * 128;
+    const float* w1 = w0 + 32 * 128;
+    float s0v = 0.f, s1v = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 128; k += 4) {
+      const f4v x = *(const LDS_AS f4v*)(S + E_A1 + (r * 132 + k) * 4);
+      const f4v u = *(const f4v*)(w0 + k), v = *(const f4v*)(w1 + k);
+      s0v += x[0] * u[0] + x[1] * u[1] + x[2] * u[2] + x[3] * u[3];
+      s1v += x[0] * v[0] + x[1] * v[1] + x[2] * v[2] + x[3] * v[3];
+    }
+    *lf(S, E_A2 + (r * 68 + o) * 4) = relu(s0v + P[a.off[15] + o]);
+    *lf(S, E_A2 + (r * 68 + o + 32) * 4) = relu(s1v + P[a.off[15] + o + 32]);
+  }
+  lbar();
+  // fc3 (64 -> 32) + ReLU: thread (sample r, output o)
+  {
+    const int r = tid >> 5, o = tid & 31;
+    const float* w = P + a.off[16] + o * 64;
+    float sv = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 64; k += 4) {
+      const f4v x = *(const LDS_AS f4v*)(S + E_A2 + (r * 68 + k) * 4);
+      const f4v u = *(const f4v*)(w + k);
+      sv += x[0] * u[0] + x[1] * u[1] + x[2] * u[2] + x[3] * u[3];
+    }
+    *lf(S, E_A3 + (r * 36 + o) * 4) = relu(sv + P[a.off[17] + o]);
+  }
+  lbar();
+  // output (32 -> 1) + sigmoid: wave 0, lane (sample lane >> 2, quarter lane & 3)
+  if (wave == 0) {
+    const int r = lane >> 2, qt = lane & 3;
+    float sv = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sv += *lf(S, E_A3 + (r * 36 + 8 * qt + k) * 4) * P[a.off[18] + 8 * qt + k];
+    sv += __shfl_xor(sv, 1, 64);
+    sv += __shfl_xor(sv, 2, 64);
+    const float z = sv + P[a.off[19]];
+    if (qt == 0 && s0 + r < a.n) a.out[(long)c * a.n + s0 + r] = 1.f / (1.f + __expf(-z));
+  }
+  (void)g;
+  (void)li;
+}
+
 }  // namespace
 
 long afl_cnn2_ws_bytes() { return WS_BYTES; }
@@ -1529,5 +1752,26 @@ int afl_cnn2_train(const AflCnn2Args& a, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL(k_cnn2_train, dim3(NWG * a.C), dim3(NTH), LDS_TOTAL, s, a);
+  return (int)hipGetLastError();
+}
+
+// eval forward of C CNNModels (params [C][pstride], slot offsets off[20]) over rows [n][24] -> out [C][n]
+int afl_cnn2_eval(const float* params, long pstride, const int* off, int C, const float* rows, int n, float* out,
+                  hipStream_t s) {
+  if (C <= 0 || n <= 0) return 0;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cnn2_eval, hipFuncAttributeMaxDynamicSharedMemorySize, E_LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  AflCnn2Eval a{};
+  a.params = params;
+  a.pstride = pstride;
+  for (int k = 0; k < 20; ++k) a.off[k] = off[k];
+  a.rows = rows;
+  a.n = n;
+  a.out = out;
+  hipLaunchKernelGGL(k_cnn2_eval, dim3((n + 15) / 16, C), dim3(NTH), E_LDS, s, a);
   return (int)hipGetLastError();
 }

@@ -356,8 +356,9 @@ __global__ void __launch_bounds__(NTP) k_har_post(AflHarPost a) {
 // =================================================================================== attention
 // One workgroup per (client, sample, head) over the head-major block [3][Lp][16] (q | k | v).
 // K / V / Q / dO are staged as row-major [rows][16] bf16 images (32-byte rows); the 8-byte chunk p of row r
-// sits at chunk p ^ 2((r >> 3) & 1), so the 16 rows of one A-operand read (rows r0..r0+15, one chunk)
-// spread over all banks, while the transposed reads (4 consecutive rows x 4 chunks) stay contiguous.
+// sits at chunk p ^ ((r >> 2) & 3) (rch), so the 16 rows of one A-operand read (rows r0..r0+15, one chunk)
+// spread over all banks in both the single and the compiler-paired read forms, while the transposed reads
+// (4 consecutive rows x 4 chunks) only permute chunks within their rows.
 // Transposed operands (V^T for O += V^T P^T, K^T for dQ, Q^T / dO^T for dK / dV) come straight from these
 // row-major images through ds_read_b64_tr_b16: lane i of a 16-lane group gets column i of 4 rows whose
 // order the lanes' addresses choose — the permuted key order of the score fragments — so no transposed
@@ -366,22 +367,19 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr int AT_WAVES = 12, AT_NT = 64 * AT_WAVES;
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ int rch(int r, int p) { return r * 32 + ((p ^ (((r >> 3) & 1) << 1)) << 3); }
+__device__ __forceinline__ int rch(int r, int p) { return r * 32 + ((p ^ ((r >> 2) & 3)) << 3); }
 __device__ __forceinline__ f4v mfma16(s4v a, s4v b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ f4v mfma32(s8v a, s8v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
 }
-// One ds_read_b64 per call: the row is made opaque so the compiler cannot pair two reads 16 rows apart into a
-// ds_read2st64_b64 / ds_read2_b64, whose banking is (a/4) mod 32 in 16-lane groups — rows r and r + 4 of this
-// layout then share banks (2-way conflicts; the round-4 PMC pass measured 3.63 conflict cycles per LDS
-// instruction in dQ, 1.97 in the forward).  As ds_read_b64 (mod 64, two 32-lane halves) the swizzle is
-// conflict-free.
-__device__ __forceinline__ s4v lds4(const uchar* img, int r, int p) {
-#ifndef HAR_LDS_PAIRED  // (A/B variant: the round-4 code the compiler paired)
-  asm volatile("" : "+v"(r));
-#endif
-  return *(const LDS_AS s4v*)(img + rch(r, p));
-}
+// One 8-byte fragment row.  The chunk swizzle p ^ ((r >> 2) & 3) keeps every access pattern of these images
+// conflict-free: 16 consecutive rows of one chunk hit 16 distinct bank pairs mod 32 (the ds_read2st64_b64 /
+// ds_read2_b64 the compiler pairs two such reads into: 16-lane groups, (a / 4) mod 32), two chunks of them 32
+// distinct pairs mod 64 (ds_read_b64: 32-lane halves), and the transposed reads (4 rows x 4 chunks) permute the
+// chunks within a row quad.  (Round 4 swizzled by row bit 3 only: rows r and r + 4 shared banks in the paired
+// form, 3.63 / 1.97 conflict cycles per LDS instruction in dQ / the forward; forcing unpaired reads instead cost
+// an address computation per read, -5 % HAR rounds/s.)
+__device__ __forceinline__ s4v lds4(const uchar* img, int r, int p) { return *(const LDS_AS s4v*)(img + rch(r, p)); }
 // transposed fragment: lane (q, p) of group g addresses row base(g) + q, chunk p -> column (lane & 15) of the 4 rows
 __device__ __forceinline__ s8v trfrag(const uchar* img, int base0, int base1, int lane) {
   const int i = lane & 15;
@@ -395,7 +393,10 @@ __device__ void stage16(uchar* img, const u16* __restrict__ src, long stride, in
   for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
     const int r = e >> 1, hf = e & 1;
     const u32x4 v = r < nvalid ? *(const u32x4*)(src + (long)r * stride + 8 * hf) : u32x4{0u, 0u, 0u, 0u};
-    *(LDS_AS u32x4*)(img + r * 32 + (((2 * hf) ^ (((r >> 3) & 1) << 1)) << 3)) = v;
+    // chunks 2 hf, 2 hf + 1 land at (2 hf) ^ sw, (2 hf + 1) ^ sw: one 16-byte pair, halves swapped when sw is odd
+    const int sw = (r >> 2) & 3;
+    const u32x4 w = (sw & 1) ? u32x4{v[2], v[3], v[0], v[1]} : v;
+    *(LDS_AS u32x4*)(img + r * 32 + (((2 * hf) ^ (sw & 2)) << 3)) = w;
   }
 }
 __device__ __forceinline__ float max_x16_x32(float a) {

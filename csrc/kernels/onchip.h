@@ -44,6 +44,14 @@ __device__ __forceinline__ s8v bfrag_lo(const float* v) {  // K = 16 padded to 3
 }
 __device__ __forceinline__ f4v mma(s8v a, s8v b, f4v c) { return fk::mfma(a, b, c); }
 constexpr f4v Z4 = {0.f, 0.f, 0.f, 0.f};
+// K <= 16 GEMMs (a branch's dense / ffn.3 input, ffn.0's 6 outputs, layer 1 of the GRU, the RNN head's fc2
+// outputs): v_mfma_f32_16x16x16_bf16 with 4-element operands — lane group g supplies k = 4g .. 4g + 3 for both
+// operands and the D layout is that of the 16x16x32 form, so the same T-layout chain works without the zero
+// upper half (one MFMA pass less and no zero-filled operand registers)
+__device__ __forceinline__ f4v mma16(s4v a, s4v b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ s4v bfrag4(const float* v) {
+  return __builtin_bit_cast(s4v, u32x2v{pk2(v[0], v[1]), pk2(v[2], v[3])});
+}
 
 // permuted K position of weight column k: the 8 values lane group g of k-step s multiplies are
 // columns {32s + 4g + i, 32s + 16 + 4g + i} (tiles 2s, 2s+1 of the T layout) -> stored contiguously
@@ -54,6 +62,10 @@ __host__ __device__ constexpr int pcol(int k) {
 // forward A fragment: W rows 16T + (lane & 15), permuted K chunk of k-step s (one ds_read_b128)
 __device__ __forceinline__ s8v wfrag(const uchar* img, int ld, int T, int s, int lane) {
   return *(const LDS_AS s8v*)(img + (16 * T + (lane & 15)) * ld + (32 * s + 8 * (lane >> 4)) * 2);
+}
+// its K <= 16 form for mma16: the first 4 (pcol stores k = 4g .. 4g + 3 at 8g .. 8g + 3; one ds_read_b64)
+__device__ __forceinline__ s4v wfrag4(const uchar* img, int ld, int T, int lane) {
+  return *(const LDS_AS s4v*)(img + (16 * T + (lane & 15)) * ld + 16 * (lane >> 4));
 }
 __device__ __forceinline__ s4v tr16(const uchar* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4v*)p);
@@ -76,6 +88,12 @@ __device__ __forceinline__ s8v wtfrag(const uchar* img, int ld, int T, int s, in
   s4v hi = {0, 0, 0, 0};
   if (HI) hi = tr16(a + 16 * ld);
   return cat44(lo, hi);
+}
+
+// the K <= 16 form of wtfrag<false> (images with <= 16 rows: the first transposed read only) for mma16
+__device__ __forceinline__ s4v wtfrag4(const uchar* img, int ld, int T, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  return tr16(img + (4 * g + q) * ld + (32 * (T >> 1) + 8 * p + 4 * (T & 1)) * 2);
 }
 
 // XOR-swizzled activation tiles [128 rows][W bf16] (8-byte chunks); chosen so the T-layout row stores
@@ -123,6 +141,21 @@ __device__ __forceinline__ void vec16(float (&x)[16], const uchar* vec, int g) {
     x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
   }
 }
+// The fp32 vectors sit past 64 KB of LDS, beyond a ds_read's 16-bit immediate offset: addressed from the
+// vector base plus per-read constants the compiler materialises one v_add per read.  lane_vec() makes
+// (vector base + this lane's 16 g bytes) ONE opaque VGPR per phase; vec16g reads at immediate offsets from it.
+__device__ __forceinline__ const uchar* lane_vec(const uchar* vec, int g) {
+  int o = 16 * g;
+  asm volatile("" : "+v"(o));
+  return vec + o;
+}
+__device__ __forceinline__ void vec16g(float (&x)[16], const uchar* vg) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f4v v = *(const LDS_AS f4v*)(vg + 64 * t);
+    x[4 * t] = v[0]; x[4 * t + 1] = v[1]; x[4 * t + 2] = v[2]; x[4 * t + 3] = v[3];
+  }
+}
 __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  // 32-wide: tiles 0, 1
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -135,34 +168,33 @@ __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  
 // lane ends with the sum of one feature; the caller sends it to a per-wave slot (head) or a fixed-point LDS
 // accumulator (branches, below)
 //
-// Cross-wave accumulation that is bit-reproducible BY CONSTRUCTION: every fp32 partial becomes an int64 fixed-
-// point number (quantum 2^-40, rounded to nearest) and the waves add them with 64-bit LDS integer atomics.
-// Integer addition is exact and associative, so the sum has the same bits whatever order the waves arrive
-// in (the fp64 atomics this replaces were order-independent only while the partials' exponents spanned
-// fewer than ~29 bits).  Range: |partial| < 2^19 (8 of them cannot overflow); a NaN / inf / out-of-range
-// partial instead sets its slot group's bit in `flag` (idx >> 6), and the group decodes as NaN — the
-// non-finite result an fp32 sum would have given.  Resolution 2^-40 (~9e-13) absolute: gradient column sums
-// of this size carry ~1e-9 relative error, below fp32's.
-constexpr double FX_ONE = 1099511627776.0;  // 2^40
-__device__ __forceinline__ void lds_addq(uchar* base, int idx, float v, LDS_AS uint32_t* flag) {
-#ifdef ONCHIP_FP64_COLSUM  // A/B variant (tools/ab_native.sh): the round-4 fp64 atomics
+// Cross-wave accumulation that is bit-reproducible BY CONSTRUCTION: every fp32 partial is rounded to an integer
+// number of quanta (quantum 2^-34) and the waves add these integers with fp64 LDS atomics.  With |partial| < 2^16
+// an addend is an integer below 2^50 and any sum of at most 8 of them stays below 2^53, so every intermediate sum
+// is exactly representable: the fp64 additions are exact, hence associative, and the result has the same bits
+// whatever order the waves arrive in (unquantised fp64 partials were order-independent only while their exponents
+// spanned fewer than ~29 bits).  A NaN / inf / out-of-range partial enters as NaN, which any order propagates:
+// the non-finite result an fp32 sum would have given.  Resolution 2^-34 (~5.8e-11) absolute.
+// Cost: rint + scale + convert + one select in front of the same ds_add_f64, straight-line (an int64 form with
+// the conversion done in fp32 / int32 pieces lengthened each call's dependent chain by ~150 cycles: +0.4 us per
+// TransformerModel step, measured; a poison flag through a uniform-address LDS atomic became a 64-iteration
+// scalar loop).
+constexpr float FX_SCALE = 17179869184.0f;  // 2^34
+__device__ __forceinline__ void lds_addq(uchar* base, int idx, float v) {
+#ifdef ONCHIP_FP64_COLSUM  // A/B variant (tools/ab_native.sh): the round-4 unquantised fp64 atomics
   __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return;
 #endif
-  if (!(fabsf(v) < 524288.f)) {
-    __hip_atomic_fetch_or(flag, 1u << (idx >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
-  }
-  const long long q = (long long)__builtin_rint((double)v * FX_ONE);
-  __hip_atomic_fetch_add((LDS_AS long long*)base + idx, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  float x = fabsf(v) < 65536.f ? __builtin_rintf(v * FX_SCALE) : __builtin_nanf("");
+  asm volatile("" : "+v"(x));  // (select in fp32, then convert: one VGPR pair live, not a 64-bit NaN constant)
+  __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // the accumulated value of slot idx (read after the barrier that follows every add)
-__device__ __forceinline__ float lds_getq(const uchar* base, int idx, const LDS_AS uint32_t* flag) {
+__device__ __forceinline__ float lds_getq(const uchar* base, int idx) {
 #ifdef ONCHIP_FP64_COLSUM
   return (float)((const LDS_AS double*)base)[idx];
 #endif
-  if ((*flag >> (idx >> 6)) & 1u) return __builtin_nanf("");
-  return (float)((double)((const LDS_AS long long*)base)[idx] * (1.0 / FX_ONE));
+  return (float)(((const LDS_AS double*)base)[idx] * (1.0 / 17179869184.0));
 }
 // partner lane's value (bound_ctrl: 0 for a missing source, which none of these patterns has) in the
 // form the backend's DPP combine folds into the consuming add

@@ -56,12 +56,12 @@ constexpr int B_DG = B_X3 + 16384;                 // 3 x tile64: d(gate pre-act
 constexpr int B_NVEC = 1280;                       // 6 x (b_ih 96 | b_hh 96) in (layer, direction) order, LN w | b
 constexpr int B_VEC = B_DG + 3 * 16384;            // fp32 [1280] bias / LayerNorm parameters
 constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [1280] their gradients
-// int64 fixed-point column sums produced wave-locally (onchip.h lds_addq: 8-wave sums independent of the wave
-// order by construction, as tf2.hip): LN weight / bias (0..127), then per layer the d(b_hn) sums of both
-// directions (128 + 64 (l - 1) + 32 d + j)
+// column sums produced wave-locally, accumulated as integer quanta in fp64 (onchip.h lds_addq: exact, so the
+// 8-wave sums are independent of the wave order by construction, as tf2.hip): LN weight / bias (0..127), then
+// per layer the d(b_hn) sums of both directions (128 + 64 (l - 1) + 32 d + j)
 constexpr int B_NDBL = 128 + 3 * 64;
 constexpr int B_DBL = B_CS + B_NVEC * 4;
-constexpr int B_MISC = B_DBL + B_NDBL * 8;         // u32 [8] per-wave abort words, [8] the DBL poison flags
+constexpr int B_MISC = B_DBL + B_NDBL * 8;         // u32 [8] per-wave abort words (+ pad)
 constexpr int B_TOTAL = B_MISC + 64;
 constexpr int B_X1 = B_X2, B_GS = B_X3;
 enum { VL_LNW = 1152, VL_LNB = 1216 };
@@ -152,7 +152,11 @@ __device__ __forceinline__ void stamp_fini(Stamp& stp, const AflTfTrainArgs& a, 
 
 // Ablation switches of the diagnostic build (compile-time RNN2_ABL bits in the stamped build only, set through
 // AFL_RNN2_ABL): skip one piece of work per step to price it (numerics are wrong then; timing only).
-enum { ABL_TADAM = 1, ABL_BIAS = 2, ABL_MOM = 4, ABL_DWMMA = 8 };
+// ABL_HALF prices a row split of the branch (two workgroups of 64 rows, one wave per SIMD) without its exchanges:
+// waves 4-7 skip every per-row and per-tile computation (still joining every barrier and hand-off), so waves 0-3
+// run their rows' forward / backward and their dW tiles (half of the branch's, as an owned-half split would) alone
+// on the SIMDs: the step time of that build bounds the split from below.
+enum { ABL_TADAM = 1, ABL_BIAS = 2, ABL_MOM = 4, ABL_DWMMA = 8, ABL_HALF = 16 };
 #if defined(RNN2_STAMPS) && defined(RNN2_ABL)
 #define ABL(b) ((RNN2_ABL & (b)) != 0)
 #else
@@ -267,23 +271,26 @@ __device__ __forceinline__ void gru_fwd(const uchar* imgs, const uchar* vec, con
                                         uint32_t (&sv)[32], int lane) {
   const int g = lane >> 4;
   const uchar* img = imgs + (L == 2 ? B_W2 : B_W3);
+  const uchar* vgl = lane_vec(vec, g);  // (this lane's vector base: immediate offsets for every bias read)
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     f4v acc[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int T = 6 * d + k;
-      if constexpr (L == 1) {
-        acc[k] = mma(w1frag(imgs, T, lane), bx[0], Z4);
+      if constexpr (L == 1) {  // K = din <= 16: the 16x16x16 form, no zero upper halves
+        const s8v b = bx[0];
+        acc[k] = mma16(*(const LDS_AS s4v*)(imgs + B_W1 + (16 * T + (lane & 15)) * LDW1 + 8 * (lane >> 4)),
+                       s4v{b[0], b[1], b[2], b[3]}, Z4);
       } else {
         acc[k] = mma(wfrag(img, LD64, T, 0, lane), bx[0], Z4);
         acc[k] = mma(wfrag(img, LD64, T, 1, lane), bx[1], acc[k]);
       }
     }
-    const uchar* vb = vec + 4 * v0(L, d);
+    const uchar* vb = vgl + 4 * v0(L, d);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int o = 4 * (16 * t + 4 * g);
+      const int o = 4 * (16 * t);
       const f4v bir = *(const LDS_AS f4v*)(vb + o), biz = *(const LDS_AS f4v*)(vb + 128 + o),
                 bin = *(const LDS_AS f4v*)(vb + 256 + o), bhr = *(const LDS_AS f4v*)(vb + 384 + o),
                 bhz = *(const LDS_AS f4v*)(vb + 512 + o), bhn = *(const LDS_AS f4v*)(vb + 640 + o);
@@ -362,8 +369,11 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 #pragma unroll
   for (int k = 0; k < 8; ++k) sv.xh[k] = pk2(h3[2 * k], h3[2 * k + 1]);
   float gm[16], bt[16];
-  vec16(gm, smem + B_VEC + 4 * VL_LNW, g);
-  vec16(bt, smem + B_VEC + 4 * VL_LNB, g);
+  {
+    const uchar* vgl = lane_vec(smem + B_VEC, g);
+    vec16g(gm, vgl + 4 * VL_LNW);
+    vec16g(bt, vgl + 4 * VL_LNB);
+  }
   affine2(h3, h3, gm, bt);
   sv.keep = keep;
 #pragma unroll
@@ -377,10 +387,10 @@ template <int L>
 __device__ __forceinline__ void gate_bwd(uchar* smem, const float (&dh)[16], const uint32_t (&sv)[32], int d, f4v (&dg)[6],
                                          float (&dnr)[16], int lane, int r) {
   const int g = lane >> 4;
-  const uchar* vb = smem + B_VEC + 4 * v0(L, d);
+  const uchar* vb = lane_vec(smem + B_VEC, g) + 4 * v0(L, d);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const f4v bhn = *(const LDS_AS f4v*)(vb + 640 + 4 * (16 * t + 4 * g));
+    const f4v bhn = *(const LDS_AS f4v*)(vb + 640 + 4 * (16 * t));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = 4 * (2 * d + t) + i;
@@ -407,7 +417,7 @@ __device__ __forceinline__ void gate_bwd(uchar* smem, const float (&dh)[16], con
 __device__ __forceinline__ void dnr_colsum(uchar* smem, int L, const float (&dnr)[16], int lane) {
   float s;
   const int f = colsum64(dnr, lane, s);
-  lds_addq(smem + B_DBL, 128 + 64 * (L - 1) + f, s, ldsu(smem, B_MISC) + 8);
+  lds_addq(smem + B_DBL, 128 + 64 * (L - 1) + f, s);
 }
 
 // backward of layer L (3 or 2) up to its d(input): dh (in) -> dG tile, dx (out)
@@ -532,8 +542,8 @@ __device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wa
     if (g == 0) bias_cs(smem, 1, Tn, i16, bs[0]);
   }
   if (tid < B_NDBL) {
-    const float s = lds_getq(smem + B_DBL, tid, ldsu(smem, B_MISC) + 8);
-    ((LDS_AS long long*)(smem + B_DBL))[tid] = 0;
+    const float s = lds_getq(smem + B_DBL, tid);
+    ((LDS_AS double*)(smem + B_DBL))[tid] = 0.0;
     int e;
     if (tid < 128) {
       e = VL_LNW + tid;
@@ -566,6 +576,7 @@ __device__ __forceinline__ void compact_update(uchar* smem, const RB& R, BrState
     const int e = tid + NTH * h;
     const bool vec = e < B_NVEC;
     gr[h] = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
+    if (ABL(ABL_HALF) && !vec) gr[h] = 0.f;  // (ablation: waves 4-7 stage no layer-1 tiles; the rest is stale h2 data)
     mh[h] = mmc[h];
     vh[h] = vvc[h];
   }
@@ -648,6 +659,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   const uint32_t seed = a.seeds[cid];
   LDS_AS uint32_t* abort_w = ldsu(smem, B_MISC);
   int step = 0;
+  const bool half_idle = ABL(ABL_HALF) && wave >= 4;
   Walk w{0, 0};
   float xin[4];
   bool more = walk_valid(w, nd, BS, E);
@@ -660,7 +672,20 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     u32x4 outp[2];
     prio_hi();
     asm volatile(";MARK fwd");
-    br_forward(smem, xin, aru(mka), sv, outp, rsv, lane, wave, tid);
+    if (!half_idle) br_forward(smem, xin, aru(mka), sv, outp, rsv, lane, wave, tid);
+    if (half_idle) {  // (ablation build only: defined values for the skipped waves' hand-off rows, and zero X rows
+                      // for the active waves' dW tiles: the h2 tile doubles as layer-1 gradient staging)
+      outp[0] = outp[1] = u32x4{0u, 0u, 0u, 0u};
+      sv.keep = 0u;
+      const float zr[16] = {};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        st4<TK64>(smem + B_X2, r, 4 * t + g, zr + 4 * t);
+        st4<TK64>(smem + B_X3, r, 4 * t + g, zr + 4 * t);
+      }
+#pragma unroll
+      for (int T = 0; T < 12; ++T) st4<TK64>(smem + B_DG + (T >> 2) * 16384, r, 4 * (T & 3) + g, zr);
+    }
     const uint32_t xpk[2] = {pk2(xin[0], xin[1]), pk2(xin[2], xin[3])};  // xin -> X1 tile after dW2
     stp(0, tid);
     gr_put(rg, gr_off(0, BR, wave, lane), outp, (uint32_t)step);  // this wave's output rows -> head
@@ -680,7 +705,10 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) break;
     float dh[16];
-    {  // d(branch output) -> dropout' -> LayerNorm backward; gamma / beta sums -> fp64
+    if (half_idle)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dh[j] = 0.f;
+    if (!half_idle) {  // d(branch output) -> dropout' -> LayerNorm backward; gamma / beta sums -> fixed point
       float dy[16], xh[16], t[16], gm[16];
       unpack16(u, dy);
 #pragma unroll
@@ -694,16 +722,19 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
       float s;
       int f = colsum64(t, lane, s);
-      lds_addq(smem + B_DBL, f, s, abort_w + 8);
+      lds_addq(smem + B_DBL, f, s);
       f = colsum64(dy, lane, s);
-      lds_addq(smem + B_DBL, 64 + f, s, abort_w + 8);
-      vec16(gm, smem + B_VEC + 4 * VL_LNW, g);
+      lds_addq(smem + B_DBL, 64 + f, s);
+      vec16g(gm, lane_vec(smem + B_VEC, g) + 4 * VL_LNW);
       ln_bwd2(dh, dy, xh, sv.rstd, gm);
     }
     if (lane == 0) abort_w[wave] = fv & 1u;
     float dx[16];
+    if (half_idle)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dx[j] = 0.f;
     asm volatile(";MARK bwd3");
-    layer_bwd<3>(smem, dh, sv.f3, dx, lane, wave);
+    if (!half_idle) layer_bwd<3>(smem, dh, sv.f3, dx, lane, wave);
     stp(3, tid);
     f4v mm[6], vv[6];
     tile_mom_ld(rm, 0, tid, mm, vv);
@@ -716,23 +747,23 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     }
     stp(4, tid);
     asm volatile(";MARK dw3");
-    layer_dw<3>(smem, R, st.w3, mm, vv, rm, 0, K, lane, wave, tid);
+    if (!half_idle) layer_dw<3>(smem, R, st.w3, mm, vv, rm, 0, K, lane, wave, tid);
     uint32_t sl[32];
     sav_ld(rsv, 2, tid, sl);
     lds_bar();  // B3: dG tile free
     stp(5, tid);
     asm volatile(";MARK bwd2");
-    layer_bwd<2>(smem, dx, sl, dh, lane, wave);
+    if (!half_idle) layer_bwd<2>(smem, dx, sl, dh, lane, wave);
     sav_ld(rsv, 1, tid, sl);
     tile_mom_ld(rm, 12, tid, mm, vv);
     lds_bar();  // A2
     stp(6, tid);
     asm volatile(";MARK dw2");
-    layer_dw<2>(smem, R, st.w2, mm, vv, rm, 12, K, lane, wave, tid);
+    if (!half_idle) layer_dw<2>(smem, R, st.w2, mm, vv, rm, 12, K, lane, wave, tid);
     lds_bar();  // B2: dG tile and the h1 tile free
     stp(7, tid);
     asm volatile(";MARK bwd1");
-    {  // layer 1: gate backward only (no input gradient); xin -> X1 tile
+    if (!half_idle) {  // layer 1: gate backward only (no input gradient); xin -> X1 tile
       int ln = lane, wv = wave;
       opq(ln, wv);
       const int rr = 16 * wv + (ln & 15);
@@ -746,12 +777,11 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     lds_bar();  // A1
     stp(8, tid);
     asm volatile(";MARK dw1");
-    layer1_dw(smem, R.din, lane, wave, tid);
+    if (!half_idle) layer1_dw(smem, R.din, lane, wave, tid);
     f4v cmom[6];
     compact_mom_ld(rm, tid, cmom);
     lds_bar();  // C: every gradient of the compact entries in CS / GS
     stp(9, tid);
-    if (tid == 0) abort_w[8] = 0u;  // (the DBL poison flags: every read is behind barrier C)
     asm volatile(";MARK u3");
     compact_update(smem, R, st, rm, cmom, K, lane, tid);
     stp(10, tid);
@@ -911,10 +941,10 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     // ---- d a1 = dz2 . W2 -> d z1
     float dz1[8];
     {
-      const s8v bz = bfrag_lo(dz2);
+      const s4v bz = bfrag4(dz2);
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        const f4v acc = mma(wtfrag<false>(smem + H_IMG_W2, LD32, T, 0, lane), bz, Z4);
+        const f4v acc = mma16(wtfrag4(smem + H_IMG_W2, LD32, T, lane), bz, Z4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) dz1[4 * T + i] = z1[4 * T + i] > 0.f ? acc[i] : 0.f;
       }

@@ -60,17 +60,17 @@ constexpr int B_NVEC = 648;                        // 10 x 64 vectors + ffn.0 bi
 constexpr int B_VEC = B_DF0 + 4096;                // fp32 [648] bias / LayerNorm parameters
 constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [648] their gradients (column sums)
 // The LayerNorm gradient column sums (6 x 64, produced wave-locally during the backward) are summed over
-// the 8 waves as int64 fixed point with LDS integer atomics (onchip.h lds_addq) into DBL, which ALIASES CS
+// the 8 waves as integer quanta in fp64 LDS atomics (onchip.h lds_addq: exact) into DBL, which ALIASES CS
 // (+ 480 bytes): the remaining CS entries are written only after the backward, and the sums are moved to
 // their CS slots at the start of the update.  Integer addition makes the 8-way sum independent of the order
 // the waves arrive in by construction, so a client's trajectory is bit-reproducible whatever launch or rank
 // trains it (fp32 LDS atomics were not: ~1e-4 drift per round; fp64 ones only while the partials spanned
 // < 2^29).
 constexpr int B_NLN = 6 * 64;
-constexpr int B_DBL = B_CS;                        // int64 [384]: G1 B1 G2 B2 G3 B3
+constexpr int B_DBL = B_CS;                        // fp64 [384]: G1 B1 G2 B2 G3 B3
 constexpr int B_DBL_BYTES = B_NLN * 8;
 static_assert(B_DBL_BYTES >= B_NVEC * 4, "DBL covers CS");
-constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words, [8] the DBL poison flags
+constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words
 constexpr int B_TOTAL = B_MISC + 64;
 // vector segments (x64 floats) of VEC / CS
 enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3 };
@@ -113,7 +113,7 @@ constexpr long WS_BYTES = WS_MOM + 5 * MOM_WG_BYTES;  // head, 2 branches x (1 o
 __device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
   float s;
   const int f = colsum64(x, lane, s);
-  lds_addq(smem + B_DBL, 64 * k + f, s, ldsu(smem, B_MISC) + 8);
+  lds_addq(smem + B_DBL, 64 * k + f, s);
 }
 __host__ __device__ constexpr int ln_seg(int k) { return k < 2 ? VS_G1 + k : VS_G2 + (k - 2); }
 static_assert(ln_seg(0) == VS_G1 && ln_seg(1) == VS_B1 && ln_seg(2) == VS_G2 && ln_seg(3) == VS_B2 &&
@@ -358,18 +358,18 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
   const int rl = S ? 16 * (wave & 3) + (lane & 15) : r;
-  const uchar* vec = smem + M::VEC;
+  const uchar* vg = lane_vec(smem + M::VEC, g);  // (one lane base for every vector read of the phase)
   st4<TK16>(smem + M::XIN, rl, g, xin);
   // ---- dense (K = din <= 16 padded to 32) + GELU
   float h0[16];
   sb();
   {
-    const s8v bx = bfrag_lo(xin);
+    const s4v bx = bfrag4(xin);
     f4v acc[4];
 #pragma unroll
-    for (int T = 0; T < 4; ++T) acc[T] = mma(wfrag(smem + B_IMG_D, LD32, T, 0, lane), bx, Z4);
+    for (int T = 0; T < 4; ++T) acc[T] = mma16(wfrag4(smem + B_IMG_D, LD32, T, lane), bx, Z4);
     float bd[16], gp[16];
-    vec16(bd, vec + VS_DB * 256, g);
+    vec16g(bd, vg + VS_DB * 256);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -398,7 +398,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     }
     sv.matt = mk1 & 0xFu;
     float bv[16];
-    vec16(bv, vec + VS_VB * 256, g);
+    vec16g(bv, vg + VS_VB * 256);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const float m = keepf(INV_K01, sv.matt, t);
@@ -421,7 +421,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     }
     sv.m1 = mk0 & 0xFFFFu;
     float bo[16];
-    vec16(bo, vec + VS_OB * 256, g);
+    vec16g(bo, vg + VS_OB * 256);
     float x1[16];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -433,8 +433,8 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     sv.rstd1 = ln_fwd2(x1);
     save16(sv.xh1, x1);
     float gm[16], bt[16];
-    vec16(gm, vec + VS_G1 * 256, g);
-    vec16(bt, vec + VS_B1 * 256, g);
+    vec16g(gm, vg + VS_G1 * 256);
+    vec16g(bt, vg + VS_B1 * 256);
     affine2(x1n, x1, gm, bt);
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::X1N, rl, 4 * t + g, x1n + 4 * t);
@@ -445,7 +445,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   {
     f4v acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 0, lane), bfrag(x1n, 0), Z4);
     acc = mma(wfrag(smem + B_IMG_F1, LD64, 0, 1, lane), bfrag(x1n, 1), acc);
-    const f4v bf = g < 2 ? *(const LDS_AS f4v*)(vec + (VS_F1B + 4 * g) * 4) : Z4;
+    const f4v bf = g < 2 ? *(const LDS_AS f4v*)(vg + VS_F1B * 4) : Z4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float gp;
@@ -458,13 +458,13 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
   // ---- ffn.3 (6 -> 64, K padded to 32), dropout, residual, LayerNorm 2, LayerNorm 3 (x_bn)
   sb();
   {
-    const s8v bf = bfrag_lo(f2v);
+    const s4v bf = bfrag4(f2v);
     f4v acc[4];
 #pragma unroll
-    for (int T = 0; T < 4; ++T) acc[T] = mma(wfrag(smem + B_IMG_F2, LD32, T, 0, lane), bf, Z4);
+    for (int T = 0; T < 4; ++T) acc[T] = mma16(wfrag4(smem + B_IMG_F2, LD32, T, lane), bf, Z4);
     sv.m2 = mk0 >> 16;
     float b3[16];
-    vec16(b3, vec + VS_F2B * 256, g);
+    vec16g(b3, vg + VS_F2B * 256);
     float x2[16];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -476,12 +476,12 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     sv.rstd2 = ln_fwd2(x2);
     save16(sv.xh2, x2);
     float gm[16], bt[16];
-    vec16(gm, vec + VS_G2 * 256, g);
-    vec16(bt, vec + VS_B2 * 256, g);
+    vec16g(gm, vg + VS_G2 * 256);
+    vec16g(bt, vg + VS_B2 * 256);
     affine2(x2, x2, gm, bt);
     ln_fwd2(x2);
-    vec16(gm, vec + VS_G3 * 256, g);
-    vec16(bt, vec + VS_B3 * 256, g);
+    vec16g(gm, vg + VS_G3 * 256);
+    vec16g(bt, vg + VS_B3 * 256);
     affine2(x2, x2, gm, bt);
     pack16(x2, outp);
   }
@@ -496,28 +496,28 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
   const int rl = S ? 16 * (wave & 3) + (lane & 15) : r;
-  const uchar* vec = smem + M::VEC;
+  const uchar* vg = lane_vec(smem + M::VEC, g);
   float dr2[16];
   sb();
   {  // LayerNorm 3 and 2 backward (xh3 = LN(xh2 * gamma2 + beta2) recomputed: fewer saved registers)
     float gm[16], t[16], dx[16], xh[16], bt[16];
     load16(xh, sv.xh2);
-    vec16(gm, vec + VS_G2 * 256, g);
-    vec16(bt, vec + VS_B2 * 256, g);
+    vec16g(gm, vg + VS_G2 * 256);
+    vec16g(bt, vg + VS_B2 * 256);
     affine2(xh, xh, gm, bt);
     const float rstd3 = ln_fwd2(xh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 4, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 5, dout, lane);
-    vec16(gm, vec + VS_G3 * 256, g);
+    vec16g(gm, vg + VS_G3 * 256);
     ln_bwd2(dx, dout, xh, rstd3, gm);
     load16(xh, sv.xh2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 2, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 3, dx, lane);
-    vec16(gm, vec + VS_G2 * 256, g);
+    vec16g(gm, vg + VS_G2 * 256);
     ln_bwd2(dr2, dx, xh, sv.rstd2, gm);
   }
   float df0[4];
@@ -537,11 +537,11 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
   float dr1[16];
   sb();
   {  // ffn.0 backward (d x1n) + residual, LayerNorm 1 backward
-    const s8v bd = bfrag_lo(df0);
+    const s4v bd = bfrag4(df0);
     float dx[16];
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
-      const f4v acc = mma(wtfrag<false>(smem + B_IMG_F1, LD64, T, 0, lane), bd, Z4);
+      const f4v acc = mma16(wtfrag4(smem + B_IMG_F1, LD64, T, lane), bd, Z4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dx[4 * T + i] = acc[i] + dr2[4 * T + i];
     }
@@ -551,7 +551,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 0, t, lane);
     if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 1, dx, lane);
-    vec16(gm, vec + VS_G1 * 256, g);
+    vec16g(gm, vg + VS_G1 * 256);
     ln_bwd2(dr1, dx, xh, sv.rstd1, gm);
   }
   float dv[16];
@@ -669,10 +669,9 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
     }
   }
   // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
-  const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid, ldsu(smem, B_MISC) + 8) : 0.f;
+  const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
   lds_bar();
   stp(5, tid);
-  if (tid == 0) ldsu(smem, B_MISC)[8] = 0u;  // (poison flags: every read is behind the barrier)
   if (tid < B_NLN) ldsf(smem, B_CS)[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
   const f4v cm = mom_ld(rm, 8, tid), cv = mom_ld(rm, 9, tid), cmv = mom_ld(rm, 10, tid);
   // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
@@ -1741,30 +1740,28 @@ __global__ void __launch_bounds__(t2::NTH) K_TF2S(AflTfTrainArgs a) {
 #ifndef TF2_STAMPS
 // Determinism check of the cross-wave column-sum accumulator (onchip.h lds_addq), used by the tests: W waves
 // each add their 64 partials (vals [W][64]) into 64 slots after a per-wave delay drawn from `seed` (so the
-// arrival order changes from launch to launch); out [64] = the decoded sums.  mode 1: the fp64 LDS atomics the
-// trainers used before (order-dependent once the partials span more than ~2^29).
+// arrival order changes from launch to launch); out [64] = the decoded sums.  mode 1: the unquantised fp64 LDS
+// atomics the trainers used before (order-dependent once the partials span more than ~2^29).
 __global__ void __launch_bounds__(1024) k_fxsum_test(const float* __restrict__ vals, int W, uint32_t seed, int mode,
                                                    float* __restrict__ out) {
-  __shared__ long long q[64];
-  __shared__ uint32_t flag;
+  __shared__ double q[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x < 64) q[threadIdx.x] = 0;
-  if (threadIdx.x == 0) flag = 0u;
   __syncthreads();
   const uint32_t spins = afl_hash32(seed, (uint32_t)w) & 1023u;
   for (uint32_t i = 0; i < spins; ++i) __builtin_amdgcn_s_sleep(1);
   const float v = vals[w * 64 + lane];
   if (mode == 0)
-    oc::lds_addq((oc::uchar*)q, lane, v, (LDS_AS uint32_t*)&flag);
+    oc::lds_addq((oc::uchar*)q, lane, v);
   else
     __hip_atomic_fetch_add((LDS_AS double*)q + lane, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __syncthreads();
   if (threadIdx.x < 64)
-    out[lane] = mode == 0 ? oc::lds_getq((const oc::uchar*)q, lane, (const LDS_AS uint32_t*)&flag)
+    out[lane] = mode == 0 ? oc::lds_getq((const oc::uchar*)q, lane)
                           : (float)((LDS_AS double*)q)[lane];
 }
 int afl_fxsum_test(const float* vals, int W, uint32_t seed, int mode, float* out, hipStream_t s) {
-  if (W < 1 || W > 16) return -1;
+  if (W < 1 || W > 8) return -1;  // (at most 8 partials per slot: onchip.h lds_addq)
   hipLaunchKernelGGL(k_fxsum_test, dim3(1), dim3(64 * W), 0, s, vals, W, seed, mode, out);
   return (int)hipGetLastError();
 }

@@ -716,6 +716,35 @@ void cnn2_train(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor r
   ok(afl_cnn2_train(a, cur()), "cnn2_train");
 }
 
+// eval forward of C CNNModels (params [C, P], 20 slot offsets) over rows [n, 24] -> sigmoid outputs [C, n]: ONE launch
+torch::Tensor cnn2_eval(torch::Tensor params, std::vector<int64_t> offs, torch::Tensor rows) {
+  dense(params, "params");
+  dense(rows, "rows");
+  TORCH_CHECK(offs.size() == 20, "cnn2_eval: 20 CNNModel slot offsets");
+  TORCH_CHECK(params.dim() == 2 && rows.dim() == 2 && rows.size(1) == 24, "cnn2_eval: params [C, P], rows [N, 24]");
+  int off[20];
+  // every slot's extent (the kernel reads whole weight matrices from each offset)
+  static const int64_t numel[20] = {96, 32, 6144, 64, 24576, 128, 96, 32, 6144, 64, 24576, 128,
+                                    131072, 128, 8192, 64, 2048, 32, 32, 1};
+  for (int k = 0; k < 20; ++k) {
+    TORCH_CHECK(offs[k] >= 0 && offs[k] + numel[k] <= params.size(1), "cnn2_eval: slot offset out of range");
+    off[k] = (int)offs[k];
+  }
+  // the kernel reads these slots (conv biases, fc weights) as 16-byte vectors: 4-float aligned offsets, and a row
+  // stride and base that keep them aligned for every model (an odd stride such as CNNModel's 203649 is padded)
+  for (int k : {3, 5, 9, 11, 12, 14, 16}) TORCH_CHECK(off[k] % 4 == 0, "cnn2_eval: slot offset not 4-float aligned");
+  torch::Tensor p = params;
+  if (p.size(1) % 4 != 0 || (reinterpret_cast<uintptr_t>(p.data_ptr<float>()) & 15) != 0) {
+    p = torch::zeros({p.size(0), (p.size(1) + 3) / 4 * 4}, p.options());
+    p.narrow(1, 0, params.size(1)).copy_(params);
+  }
+  const int C = (int)p.size(0), n = (int)rows.size(0);
+  auto out = torch::empty({C, n}, rows.options());
+  ok(afl_cnn2_eval(p.data_ptr<float>(), p.size(1), off, C, rows.data_ptr<float>(), n, out.data_ptr<float>(), cur()),
+     "cnn2_eval");
+  return out;
+}
+
 }  // namespace
 
 void afl_register_layers(pybind11::module& m) {
@@ -740,6 +769,7 @@ void afl_register_layers(pybind11::module& m) {
         py::arg("epoch"), py::arg("nb"), py::arg("seeds"), py::arg("p"), py::arg("min_bs"), py::arg("nan_abort"),
         py::arg("lr"), py::arg("failed"), py::arg("losses"), py::arg("ws"), py::arg("ctr"), py::arg("stamps") = none,
         py::arg("opt_mode") = 0);
+  m.def("cnn2_eval", &cnn2_eval, py::arg("params"), py::arg("offs"), py::arg("rows"));
   m.def("cnn2_ws_bytes", &afl_cnn2_ws_bytes);
   m.def("cnn2_ctr_words", &afl_cnn2_ctr_words);
   m.def("cnn2_wgs_per_client", &afl_cnn2_wgs_per_client);

@@ -456,6 +456,29 @@ def test_cnn2_nan_loss_fails_only_that_client(gpu, monkeypatch, nan_at):
 
 
 
+def test_cnn2_eval_many_matches_eager_model(gpu):
+    """Fused forward-only CNN eval of C models (cnn2.hip k_cnn2_eval, the validation pass) against torch's fp32
+    CNNModel in eval mode: bf16 MFMA convolutions / fc1 -> outputs within 2e-2, mean error far below; n not a
+    multiple of the 16-sample tile; an odd arena row stride (padded by the binding)."""
+    from attackfl_amd.eval import cnn_eval_many
+
+    ds = synthetic_icu(1000, seed=5)
+    n = 333
+    lay = ParamLayout.for_model("CNNModel")
+    models = [build_model("CNNModel", seed=20 + i).eval() for i in range(3)]
+    params = torch.stack([lay.flatten(m.state_dict()) for m in models])
+    assert params.shape[1] % 4 != 0  # (203649: the padded-copy path)
+    rows = torch.cat([ds.vitals[:n], ds.labs[:n], ds.labels[:n, None]], 1)
+    out = cnn_eval_many(params.to(DEV), rows.to(DEV), lay).cpu()
+    with torch.no_grad():
+        ref = torch.stack([m(rows[:, :7], rows[:, 7:23]).reshape(-1) for m in models])
+    assert out.shape == (3, n)
+    err = (out - ref).abs()
+    assert err.max().item() < 2e-2 and err.mean().item() < 3e-3, (err.max().item(), err.mean().item())
+    # one model through Validation's path equals its row of the batched launch
+    one = cnn_eval_many(params[1].to(DEV), rows.to(DEV), lay).cpu()
+    assert torch.equal(one[0], out[1])
+
 def _har_slot_errors(res, lay):
     """Per ParamLayout slot: (relative norm error, max error / the slot's own max) of res[0] vs res[1]."""
     out = {}
@@ -490,7 +513,7 @@ def test_har_encoder_sgd_gradients_per_tensor(gpu, B, drop):
         losses.append(ls.cpu())
     assert torch.allclose(losses[0], losses[1], rtol=1e-2), (losses[0], losses[1])
     errs = _har_slot_errors(res, ParamLayout.for_model("TransformerClassifier"))
-    print({k: (round(a, 4), round(b, 4)) for k, a in errs.items()})
+    print({k: (round(a, 4), round(b, 4)) for k, (a, b) in errs.items()})
     bad = {k: v for k, v in errs.items() if v[0] > HAR_GRAD_NORM_TOL or v[1] > HAR_GRAD_MAX_TOL}
     assert not bad, bad
 
@@ -519,13 +542,24 @@ def test_har_encoder_adam_epochs_track_composite(gpu):
         losses.append(ls.cpu())
     assert torch.allclose(losses[0], losses[1], rtol=2e-2, atol=2e-3), (losses[0], losses[1])
     lay = ParamLayout.for_model("TransformerClassifier")
-    bad = {}
+    ratios = {}
     for sl in lay.slots:
         a, b, p0 = (t[:, sl.offset:sl.offset + sl.numel] for t in (res[0], res[1], params))
+        if sl.name.endswith("in_proj_bias"):
+            # the key bias adds q.b_k to every score of a query row: softmax is shift-invariant, so its gradient is
+            # exactly zero and Adam (m / sqrt(v)) turns the rounding noise of either side into full-size steps
+            keep = torch.ones(sl.numel, dtype=torch.bool)
+            keep[64:128] = False
+            a, b, p0 = a[:, keep], b[:, keep], p0[:, keep]
         moved = (b - p0).norm().item()
         if moved == 0.0:
             continue
-        r = (a - b).norm().item() / moved
-        if r > 0.15:
-            bad[sl.name] = round(r, 4)
+        ratios[sl.name] = round((a - b).norm().item() / moved, 4)
+    print(ratios)
+    # Adam's per-element normalisation amplifies bf16-operand differences where a gradient is small: a deviation
+    # of a few tenths of the distance moved is that noise; a wrong gradient moves the tensor elsewhere (ratio >= 1)
+    bad = {k: r for k, r in ratios.items() if r > HAR_ADAM_TOL}
     assert not bad, bad
+
+
+HAR_ADAM_TOL = 0.4

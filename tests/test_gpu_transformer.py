@@ -212,10 +212,10 @@ def test_auto_split_choice(gpu):
 
 
 def test_cross_wave_column_sums_are_order_independent(gpu):
-    """The on-chip trainers' cross-wave gradient column sums (onchip.h lds_addq: int64 fixed point, LDS integer
-    atomics) give the same bits whatever order the 8 waves arrive in, with adversarial partials whose exponents
-    span more than 2^50 and cancel (the fp64 atomics they replace were order-independent only within ~2^29),
-    and equal the exactly rounded fixed-point sum."""
+    """The on-chip trainers' cross-wave gradient column sums (onchip.h lds_addq: partials rounded to integer quanta
+    of 2^-34, summed exactly in fp64 LDS atomics) give the same bits whatever order the 8 waves arrive in, with
+    adversarial partials (|partial| < 2^16) whose exponents span more than 2^50 and cancel — the unquantised fp64
+    atomics they replace were order-independent only within ~2^29 — and equal the exactly rounded sum."""
     from fractions import Fraction
 
     from attackfl_amd.ops import native
@@ -223,17 +223,28 @@ def test_cross_wave_column_sums_are_order_independent(gpu):
     g = torch.Generator().manual_seed(0)
     W = 8
     mant = 1.0 + torch.rand(W, 64, generator=g)
-    expo = torch.tensor([18, -35, 18, -30, 10, -36, 17, -20], dtype=torch.float64)[:, None]
+    expo = torch.tensor([15, -35, 15, -30, 10, -36, 14, -20], dtype=torch.float64)[:, None]
     sign = torch.where(torch.rand(W, 64, generator=g) < 0.5, -1.0, 1.0)
     vals = (sign * mant.double() * torch.pow(2.0, expo)).float()
     vals[2] = -vals[0]  # exact cancellation of the two largest partials: the result lives in the low bits
     outs = {native().fxsum_test(vals.to(gpu), seed, 0).cpu().numpy().tobytes() for seed in range(48)}
     assert len(outs) == 1
     got = torch.frombuffer(bytearray(outs.pop()), dtype=torch.float32)
-    q = [[round(Fraction(float(v)) * 2 ** 40) for v in vals[:, j].tolist()] for j in range(64)]
-    exp = torch.tensor([float(Fraction(sum(c), 2 ** 40)) for c in q], dtype=torch.float64).float()
+    q = [[round(Fraction(float(v)) * 2 ** 34) for v in vals[:, j].tolist()] for j in range(64)]
+    exp = torch.tensor([float(Fraction(sum(c), 2 ** 34)) for c in q], dtype=torch.float64).float()
     assert torch.equal(got, exp)
-    # a non-finite partial poisons its slot group (decoded NaN, as an fp32 sum would give)
+    # (the round-4 unquantised fp64 atomics on the same partials, for the log: distinct results over the orders)
+    print("fp64 atomics:", len({native().fxsum_test(vals.to(gpu), seed, 1).cpu().numpy().tobytes() for seed in range(48)}),
+          "distinct results over 48 launches")
+    # a non-finite or out-of-range (|v| >= 2^16) partial poisons its slot (decoded NaN, as an fp32 sum of a
+    # non-finite partial would give); the other slots keep their exact sums
+    for badv in (float("nan"), float("inf"), -float("inf"), 70000.0):
+        bad = vals.clone()
+        bad[3, 5] = badv
+        res = native().fxsum_test(bad.to(gpu), 1, 0).cpu()
+        assert torch.isnan(res[5]) and not torch.isnan(res[torch.arange(64) != 5]).any(), badv
+        assert torch.equal(res[torch.arange(64) != 5], exp[torch.arange(64) != 5])
+    # eight poisoned partials in one slot decode as NaN
     bad = vals.clone()
-    bad[3, 5] = float("nan")
-    assert torch.isnan(native().fxsum_test(bad.to(gpu), 1, 0).cpu()).all()
+    bad[:, 7] = float("inf")
+    assert torch.isnan(native().fxsum_test(bad.to(gpu), 2, 0).cpu()[7])
