@@ -281,7 +281,7 @@ constexpr int O_FT = O_XS + 656;            // feat bf16 [16][520] | z1p staging
 constexpr int O_ZS = O_FT + 16 * LDF * 2;
 constexpr int O_D1R = O_FT + 16 * 516 * 4;  // own d1 rows bf16 [16][136]
 constexpr int O_RED = O_D1R + 16 * LDD * 2; // reductions (8 KB)
-constexpr int O_FLAG = O_RED + 9216;
+constexpr int O_FLAG = O_RED + 10240;
 constexpr int T_LDS = O_FLAG + 16;
 static_assert(O_ZS + 16 * LDZ * 4 <= O_D1R, "z1p staging");
 // owner-phase staging (dead activation regions after the backward)
@@ -292,8 +292,10 @@ constexpr int O_S3 = 0, O_S2 = 6144, O_D1F = 8192, O_FW = O_D1F + 128 * LDD * 2,
 static_assert(O_SW + 128 * 72 * 2 <= O_XS, "owner staging");
 // reduction slots (floats from O_RED)
 constexpr int R_DB2 = 0, R_DB3 = 128, R_C1 = 128 + 1024, R_SM = 128 + 1024 + 512;  // [8][16] | [8][128] | [8][16][4] | [320]
-constexpr int R_KEEP = R_SM + NSMALL;  // dropout keep bytes [16 rows][64] (one byte = 8 concat columns), as floats: 256
-static_assert((R_KEEP + 256) * 4 <= 9216, "reduction slots");
+// dropout keep bytes [2 step parities][16 rows][64] (one byte = 8 concat columns), as floats: 2 x 256.  A step's
+// bytes are hashed during the PREVIOUS step's wait for the head (idle time), not in the forward's pooling
+constexpr int R_KEEP = R_SM + NSMALL;
+static_assert((R_KEEP + 512) * 4 <= 10240, "reduction slots");
 
 // relu(acc + b) on a valid row, exact 0 on a pad row: branch-free (the select form became exec-mask branches)
 __device__ __forceinline__ u32x2v relu_pack4(f4v acc, f4v b, bool ok) {
@@ -306,6 +308,25 @@ __device__ __forceinline__ u32x2v relu_pack4(f4v acc, f4v b, bool ok) {
 __device__ __forceinline__ bool valid_q(int q, int LP) {
   const int l = q % LP;
   return q < 144 && l != 0 && l != LP - 1;
+}
+
+// dropout keep bytes of step s (all rows of this tower workgroup) -> keep buffer `buf` (bit k of byte (r, cp) keeps
+// concat column COL0 + 8 cp + k of row b0 + r: the layer-program hash convention, 16 bits per column pair)
+template <int T>
+__device__ __forceinline__ void keep_bytes(const AflCnn2Args& a, int c, int b0, int s, uchar* S, int buf, int tid) {
+  using C = TW<T>;
+  const uint32_t key = afl_hash32(a.seeds[c], (uint32_t)s);
+  for (int e = tid; e < C::R * 64; e += NTH) {
+    const int r = e >> 6, cp = e & 63;
+    uint32_t kb = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t hsh = afl_hash4(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)((C::COL0 + 8 * cp) / 2 + k));
+      kb |= ((hsh & 0xFFFFu) >= a.thr16 ? 1u : 0u) << (2 * k);
+      kb |= ((hsh >> 16) >= a.thr16 ? 1u : 0u) << (2 * k + 1);
+    }
+    *(LDS_AS uchar*)(S + O_RED + (R_KEEP + 256 * buf) * 4 + r * 64 + cp) = (uchar)kb;
+  }
 }
 
 template <int T>
@@ -470,7 +491,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     const int row = b < B ? a.idx[((long)s2 * a.C + c) * B + b] : -1;
     return row >= 0 ? a.rows[(long)row * 24 + C::XOFF + l] : 0.f;
   };
-  float xv_next = load_x(next_active(0));
+  const int s_first = next_active(0);
+  float xv_next = load_x(s_first);
+  if (a.thr16 != 0 && s_first < a.S) keep_bytes<T>(a, c, b0, s_first, S, 0, tid);  // (behind the step's first barrier)
   int kact = 0;
   bool alive = true;
   for (int s = 0; s < a.S && alive; ++s) {
@@ -586,7 +609,6 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     // (row r, channel pair cp) = 8 concat columns 8 cp .. 8 cp + 7: the channel pair moves as one dword per
     // position, the bins are compile-time, the 8 keep bits (4 hashes) are kept as one LDS byte for the backward
     const bool dr = a.thr16 != 0;
-    const uint32_t key = dr ? afl_hash32(a.seeds[c], (uint32_t)s) : 0u;
 #pragma unroll
     for (int it = 0; it < 16 * 64 / NTH; ++it) {
       const int e = tid + NTH * it, r = e >> 6, cp = e & 63;
@@ -612,19 +634,11 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
           f[p] = s0 * bin_rcp(p, C::L);
           f[4 + p] = s1 * bin_rcp(p, C::L);
         }
-        uint32_t kb = 0xFFu;
         if (dr) {
-          kb = 0u;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t hsh = afl_hash4(key, (uint32_t)T, (uint32_t)(b0 + r), (uint32_t)((C::COL0 + 8 * cp) / 2 + k));
-            kb |= ((hsh & 0xFFFFu) >= a.thr16 ? 1u : 0u) << (2 * k);
-            kb |= ((hsh >> 16) >= a.thr16 ? 1u : 0u) << (2 * k + 1);
-          }
+          const uint32_t kb = *(const LDS_AS uchar*)(S + O_RED + (R_KEEP + 256 * par) * 4 + r * 64 + cp);
 #pragma unroll
           for (int k = 0; k < 8; ++k) f[k] *= ((kb >> k) & 1u) ? a.inv_keep : 0.f;
         }
-        *(LDS_AS uchar*)(S + O_RED + R_KEEP * 4 + r * 64 + cp) = (uchar)kb;
       }
       const u32x4 pkd = u32x4{pk2(f[0], f[1]), pk2(f[2], f[3]), pk2(f[4], f[5]), pk2(f[6], f[7])};
       *(LDS_AS u32x4*)(S + O_FT + (r * LDF + 8 * cp) * 2) = pkd;
@@ -649,7 +663,8 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
     arrive(x, CT_FW + (T == 0 ? i : (i >> 1)));  // (per head wave: it starts on its own rows' partials)
     REOPQ();
     stamp(x, kact, 1);
-    xv_next = load_x(next_active(s + 1));
+    const int s_next = next_active(s + 1);
+    xv_next = load_x(s_next);
     // d(concat) B fragments (W1T, this tower's columns: n-tiles 4 w .. 4 w + 3) in flight during the wait
     s8v wt1[16];
 #pragma unroll
@@ -668,6 +683,9 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
     for (int k = 0; k < 6; ++k)
       w2t[k] = ld16s(x.rw, WS_IMG + (tw + IM_W2T + ((k >> 1) * 32 + 16 * nb1 + li) * 64 + 32 * (k & 1) + 8 * g) * 2);
+    // the next step's dropout keep bytes, hashed while the head works (the other parity's buffer; read after the
+    // barriers of the wait below and of the next step)
+    if (dr && s_next < a.S) keep_bytes<T>(a, c, b0, s_next, S, par ^ 1, tid);
     // ------------------------------------------------------------------------------ backward
     const int hw = T == 0 ? i : (i >> 1);  // the head wave that computes this workgroup's d1 rows
     if (!wait_ge(x, CT_HW + hw, (uint32_t)(kact + 1), O_FLAG)) break;
@@ -711,7 +729,7 @@ __device__ __forceinline__ void tower(const Ctx& x, int i) {
 #pragma unroll
     for (int it = 0; it < C::R * 64 / NTH; ++it) {
       const int r = (tid >> 6) + 8 * it;
-      const uint32_t kb = *(const LDS_AS uchar*)(S + O_RED + R_KEEP * 4 + r * 64 + cp);
+      const uint32_t kb = *(const LDS_AS uchar*)(S + O_RED + (R_KEEP + 256 * par) * 4 + r * 64 + cp);
       const f4v d0 = *(const LDS_AS f4v*)(S + O_FT + (r * 516 + 8 * cp) * 4);
       const f4v d1 = *(const LDS_AS f4v*)(S + O_FT + (r * 516 + 8 * cp + 4) * 4);
       float gq[8];
