@@ -678,6 +678,8 @@ __device__ __forceinline__ float awu(uint32_t v) { return aw(__uint_as_float(v))
 
 // bias gradient = column sums of a dY tile: the dW GEMM with an all-ones X fragment (every row of the
 // 16x16 result equals the sums of the 16 columns of dY tile Tn)
+// (as a plain constant the compiler hoists the quad out of a step loop as one invariant value, and under register
+// pressure spills it and reloads it before every use: a loop that uses it materialises it per phase, opaque)
 __device__ __forceinline__ s8v ones8() {
   const short o = (short)0x3F80;  // bf16 1.0
   return s8v{o, o, o, o, o, o, o, o};

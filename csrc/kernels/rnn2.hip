@@ -486,6 +486,10 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
     const uchar* DY = smem + B_DG + (Tn >> 2) * 16384;
     const bool bias = !ABL(ABL_BIAS) && (b == 2 ? odd : !odd);
     f4v acc0 = Z4, acc1 = Z4, bs = Z4;
+    // (the all-ones operand materialised here, opaque: hoisted out of the step loop it was spilled and reloaded from
+    // scratch before each of these MFMAs, 24 scratch round trips per dW phase)
+    s8v one = ones8();
+    asm volatile("" : "+v"(one));
     // fragments of k-step s + 1 issued before the MFMAs of k-step s (double-buffered)
     s8v y[2], x0[2], x1[2];
     y[0] = tfrag<TK64>(DY, 0, Tn & 3, lane);
@@ -501,7 +505,7 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
       }
       acc0 = mma(x0[c], y[c], acc0);
       acc1 = mma(x1[c], y[c], acc1);
-      if (bias) bs = mma(ones8(), y[c], bs);
+      if (bias) bs = mma(one, y[c], bs);
     }
     if (bias && g == 0) bias_cs(smem, L, Tn, i16, bs[0]);
     if (!ABL(ABL_TADAM))  // (the 96 x 64 direction blocks are tile-exact: no element masks)
