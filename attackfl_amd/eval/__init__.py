@@ -98,6 +98,9 @@ class Validation:
 
     def _finish_icu(self, outputs: torch.Tensor, labels: torch.Tensor) -> Tuple[bool, float]:
         auc, has_nan = ops.roc_auc_checked(outputs, labels)
+        return self._icu_result(auc, has_nan)
+
+    def _icu_result(self, auc: float, has_nan: bool) -> Tuple[bool, float]:
         if has_nan:
             print_with_color("NaN detected in output, training false", "yellow")
             self.last_metric = float("nan")
@@ -127,7 +130,30 @@ class Validation:
         loss = float(torch.nn.functional.nll_loss(out.float(), y, reduction="sum"))
         return loss, int((out.argmax(dim=1) == y).sum())
 
+    def prefetch(self, flat: torch.Tensor) -> bool:
+        """Enqueue the device half of ``test(flat)`` (ICU on a GPU: forward + device ROC-AUC, result copied to pinned
+        host memory) on the current stream now; a later ``test`` of the same, unmodified tensor only reads it.
+        The engine calls this ahead of a speculative launch whose trainer occupies every CU (cnn2: 32 workgroups
+        per client): a validation queued behind that launch on a side stream could not start before it ended,
+        and the host, waiting for the metric, then enqueued the round after it late (GPU idle in between)."""
+        self._pre = None
+        if not (self.device.type == "cuda" and self.data_name == "ICU"):
+            return False
+        out = self._outputs(flat)
+        r = ops.native().roc_auc_dev(out.reshape(-1).float().contiguous(), self._labels().reshape(-1).float().contiguous())
+        buf = torch.empty(r.shape, dtype=r.dtype, pin_memory=True)
+        buf.copy_(r, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pre = (flat, flat._version, buf, ev)
+        return True
+
     def test(self, flat: torch.Tensor) -> Tuple[bool, float]:
+        pre, self._pre = getattr(self, "_pre", None), None
+        if pre is not None and pre[0] is flat and pre[1] == flat._version:
+            pre[3].synchronize()
+            auc, nan = pre[2].tolist()
+            return self._icu_result(auc, nan > 0.5)
         if self.data_name == "CIFAR10":
             return self._finish_image(*self._image_stats(flat))
         out = self._outputs(flat)

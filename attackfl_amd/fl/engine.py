@@ -937,6 +937,8 @@ class FLEngine:
         if esl is not None and self._spec is not None:
             agg_done = esl["agg_done"]
         elif self._speculative and round_ok and self.rounds_left > 1 and not last:
+            if self.mode != "hyper":  # (test() falls back to the ordinary path if the model changes after this)
+                self._prefetch_validation(self.global_params)
             agg_done = torch.cuda.Event()
             agg_done.record(torch.cuda.current_stream(self.device))
             self._spec = self._launch_local(self._genuine_for_attackers())
@@ -990,6 +992,23 @@ class FLEngine:
                                f"words {sorted(set(int(w) for w in words))}; validation / detection must be "
                                "bit-identical on every rank (do not mix devices in one world)")
 
+    def _fills_gpu(self) -> bool:
+        """The training launch occupies every CU (the on-chip CNN trainer: 32 workgroups per client), so nothing
+        queued beside it on another stream starts before it ends."""
+        if self.device.type != "cuda" or getattr(self.trainer, "kind", "") != "graph" or self.model_name != "CNNModel":
+            return False
+        from .. import ops
+        from ..parallel.launcher import gpu_sharers
+
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count // gpu_sharers()
+        return len(self.local) * int(ops.native().cnn2_wgs_per_client()) >= cus
+
+    def _prefetch_validation(self, g: Optional[torch.Tensor]) -> None:
+        """Ahead of a speculative launch that fills the GPU: this round's validation forward + AUC go in FIRST
+        (stream order), so the host has its metric while the next training runs (Validation.prefetch)."""
+        if g is not None and self.validation is not None and self._fills_gpu():
+            self.validation.prefetch(g)
+
     def _early_ok(self, last: bool) -> bool:
         if self.mode == "hyper":
             mode_ok = self.device.type == "cuda" and self.hyper._native_ok()
@@ -1039,6 +1058,8 @@ class FLEngine:
             keep = [k for k, i in enumerate(self.selected) if self.table[i].attack is None]
             self.genuine_pool = U[keep].clone() if keep else None
         self.global_params = g
+        if self.mode != "hyper":
+            self._prefetch_validation(g)
         agg_done = torch.cuda.Event()
         agg_done.record(torch.cuda.current_stream(self.device))
         prep = self._next_prep  # (staged ahead: the snapshot above already includes its draws)

@@ -509,33 +509,38 @@ def step_tables(order: torch.Tensor, nd: Sequence[int], epochs: int, B: int, dev
     ``epoch [S, C]``, ``nb [C]`` (batches per epoch, the loss divisor).  Client c's s-th step is its
     s-th batch in (epoch, batch) order; steps past its last batch have ``bsz = 0``.
 
-    Built with a few gathers per client on the plan's device (a per-batch Python loop of slice copies cost
-    ~30 ms per round at 8 clients x 5 epochs x 118 batches; ``tests/test_programs.py`` pins this against
-    that loop)."""
+    Built for all clients at once with a dozen tensor ops on the plan's device (one gather into the plan):
+    on a GPU these run between two rounds' training launches, where the earlier per-client loop (~15 small
+    kernels per client) cost ~1 ms of back-to-back dispatch per round; a per-batch Python loop of slice copies
+    cost ~30 ms.  ``tests/test_programs.py`` pins this against that loop."""
     C = order.shape[0]
     nd = [int(x) for x in nd]
     nbat = [max(1, math.ceil(n / B)) for n in nd]
     S = max([epochs * n for n in nbat] + [0])
     dev = order.device
-    idx = torch.full((S, C, B), -1, dtype=torch.int32, device=dev)
-    bsz = torch.zeros(S, C, dtype=torch.int32, device=dev)
-    ep = torch.zeros(S, C, dtype=torch.int32, device=dev)
-    ar = torch.arange(B, device=dev)
-    for c in range(C):
-        n, nbc = nd[c], nbat[c]
-        steps = epochs * nbc
-        bsz[:steps, c] = (n - (torch.arange(steps, device=dev) % nbc) * B).clamp(max=B).clamp(min=0).to(torch.int32)
-        ep[:steps, c] = (torch.arange(steps, device=dev) // nbc).to(torch.int32)
-        if n == 0 or order.shape[2] == 0:
-            continue
-        st = torch.arange(steps, device=dev)
-        e, j = st // nbc, st % nbc
-        pos = j[:, None] * B + ar[None, :]                                   # [steps, B] row within the epoch
-        ok = pos < n
-        vals = order[c][e[:, None].expand(-1, B), pos.clamp(max=max(order.shape[2] - 1, 0))]
-        idx[:steps, c] = torch.where(ok, vals.to(torch.int32), torch.full_like(vals, -1, dtype=torch.int32))
     dvc = torch.device(device)
-    return (idx.to(dvc), bsz.to(dvc), ep.to(dvc), torch.tensor(nbat, dtype=torch.int32, device=dvc), S)
+    nb_t = Lx.upload(torch.tensor(nbat, dtype=torch.int32), dvc)
+    if S == 0 or C == 0:
+        return (torch.full((S, C, B), -1, dtype=torch.int32, device=dvc), torch.zeros(S, C, dtype=torch.int32, device=dvc),
+                torch.zeros(S, C, dtype=torch.int32, device=dvc), nb_t, S)
+    small = Lx.upload(torch.tensor([nbat, nd], dtype=torch.int64), dev)     # [2, C]: batches per epoch, rows
+    nbc, ndc = small[0][None, :], small[1][None, :]
+    st = torch.arange(S, device=dev)[:, None]                                 # [S, 1]
+    valid = st < nbc * epochs                                                  # [S, C]
+    e, j = st // nbc, st % nbc
+    bsz = torch.where(valid, (ndc - j * B).clamp(min=0, max=B), 0).to(torch.int32)
+    ep = torch.where(valid, e, 0).to(torch.int32)
+    maxnd = order.shape[2]
+    if maxnd == 0:
+        idx = torch.full((S, C, B), -1, dtype=torch.int32, device=dev)
+    else:
+        pos = j[:, :, None] * B + torch.arange(B, device=dev)                 # [S, C, B] row within the epoch
+        ok = (pos < ndc[:, :, None]) & valid[:, :, None]
+        cc = torch.arange(C, device=dev)[None, :, None]
+        lin = (cc * epochs + e.clamp(max=epochs - 1)[:, :, None]) * maxnd + pos.clamp(max=maxnd - 1)
+        vals = order.reshape(-1)[lin.reshape(-1)].reshape(S, C, B)
+        idx = torch.where(ok, vals.to(torch.int32), -1).to(torch.int32)
+    return (idx.to(dvc).contiguous(), bsz.to(dvc).contiguous(), ep.to(dvc).contiguous(), nb_t, S)
 
 
 class ProgramRunner:

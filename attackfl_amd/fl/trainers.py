@@ -431,12 +431,30 @@ class GraphTrainer:
                 self.programs.make_program(self.model_name, C, batch, self.device, train=True))
         ok, losses = self._runner.train(self.table, params, plan, lr, seeds, sync=False,
                                         compat_har=self.compat_har and self.table.kind == "HAR")
+        if ok.is_cuda:
+            # failed counts + losses come back in ONE asynchronous copy into a pinned buffer queued right behind
+            # this launch, and fin() waits on its event: a .cpu() read in fin() went on the stream BEHIND the
+            # speculative next launch enqueued meanwhile, so the host waited for that whole training too and
+            # enqueued the round after it late (cnn2, which fills the GPU: ~1-2 ms idle per round)
+            C, E = losses.shape
+            buf = FusedTrainer._pinned(self, C, E)
+            buf.copy_(torch.cat([ok.to(torch.float32)[:, None], losses], 1), non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.device))
+
+            def host():
+                while not done.query():
+                    time.sleep(0)
+                return buf[:, 0].to(torch.int32), buf[:, 1:].double()
+        else:
+            def host():
+                return ok.cpu(), losses.double().cpu()
 
         def fin():
-            fh = ok.cpu()
+            fh, lh = host()
             if bool((fh == 2).any()):
                 raise RuntimeError(self.programs.CNN2_TIMEOUT)
-            okh, lh = (fh == 0), losses.double().cpu()
+            okh = fh == 0
             if self.verbose:
                 for c in range(C):
                     for e in range(plan.epochs):

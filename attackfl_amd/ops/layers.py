@@ -25,6 +25,17 @@ from . import native as _native
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
 
+def upload(t: torch.Tensor, device) -> torch.Tensor:
+    """Small host tensor -> ``device`` without blocking the host behind queued GPU work: pinned staging and a
+    non-blocking copy (the caching host allocator keeps the staging block until the copy has run).  A pageable
+    ``.to(device)`` waits for the stream, which held a speculative next-round launch of the layer-program /
+    cnn2 path behind the round's running training kernel (the GPU then idled while the host enqueued it)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 @dataclass
 class StepCtl:
     """Per-client dropout seeds (int32 [C]) + the device step counter (int32 [1])."""
@@ -39,7 +50,7 @@ class StepCtl:
         s = torch.tensor([int(x) & masks.M32 for x in seeds], dtype=torch.int64)
         s = torch.where(s >= 2 ** 31, s - 2 ** 32, s).to(torch.int32)
         ctl = torch.tensor([0, int(min_bs), 1 if nan_abort else 0], dtype=torch.int32)
-        return cls(s.to(device), ctl.to(device))
+        return cls(upload(s, device), upload(ctl, device))
 
     # composite helpers
     def step(self) -> int:

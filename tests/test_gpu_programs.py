@@ -479,6 +479,32 @@ def test_cnn2_eval_many_matches_eager_model(gpu):
     one = cnn_eval_many(params[1].to(DEV), rows.to(DEV), lay).cpu()
     assert torch.equal(one[0], out[1])
 
+
+class _NullLog:
+    def log_info(self, *a, **k):
+        pass
+
+
+def test_validation_prefetch_equals_direct(gpu):
+    """Validation.prefetch (the engine queues the validation forward + AUC ahead of a speculative launch that
+    fills the GPU) gives the direct test()'s metric, and falls back to a fresh evaluation when the model tensor
+    changed in place after the prefetch."""
+    from attackfl_amd.eval import Validation
+    from attackfl_amd.data import synthetic_icu
+
+    ds = synthetic_icu(700, seed=9)
+    val = Validation("CNNModel", "ICU", _NullLog(), DEV, dataset=ds, verbose=False)
+    lay = ParamLayout.for_model("CNNModel")
+    flat = lay.flatten(build_model("CNNModel", seed=4).state_dict()).to(DEV)
+    direct = val.test(flat)
+    assert val.prefetch(flat)
+    assert val.test(flat) == direct
+    assert val.prefetch(flat)
+    flat.mul_(1.5)  # (in place: the prefetched metric is stale)
+    again = val.test(flat)
+    val2 = Validation("CNNModel", "ICU", _NullLog(), DEV, dataset=ds, verbose=False)
+    assert again == val2.test(flat)
+
 def _har_slot_errors(res, lay):
     """Per ParamLayout slot: (relative norm error, max error / the slot's own max) of res[0] vs res[1]."""
     out = {}
