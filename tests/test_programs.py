@@ -179,3 +179,24 @@ def test_client_chunks_balanced():
             assert parts[0][0] == 0 and parts[-1][1] == C and all(b - a <= cap for a, b in parts)
             assert all(parts[i][1] == parts[i + 1][0] for i in range(len(parts) - 1))
             assert len(parts) == -(-C // cap)
+
+
+def test_upload_and_prefetch_cpu_paths():
+    """ops.layers.upload is a plain copy off the GPU; Validation.prefetch is a no-op there (test() recomputes)."""
+    from attackfl_amd.eval import Validation
+    from attackfl_amd.ops.layers import upload
+
+    t = torch.arange(5, dtype=torch.int32)
+    u = upload(t, "cpu")
+    assert torch.equal(u, t)
+
+    class _Log:
+        def log_info(self, *a, **k):
+            pass
+
+    ds = synthetic_icu(300, seed=2)
+    val = Validation("CNNModel", "ICU", _Log(), "cpu", dataset=ds, verbose=False)
+    flat = ParamLayout.for_model("CNNModel").flatten(build_model("CNNModel", seed=1).state_dict())
+    assert val.prefetch(flat) is False
+    ok, auc = val.test(flat)
+    assert ok and 0.0 <= auc <= 1.0
