@@ -1535,15 +1535,15 @@ __global__ void __launch_bounds__(NTH) k_cnn2_train(AflCnn2Args a) {
 // Forward-only CNNModel (eval mode: dropout off) of C models over rows [n][24] in ONE launch, grid (ceil(n / 16), C):
 // the validation pass (src/Validation.py:19-68; the layer program spent ~1 ms per 4096 rows in k_cnn_fwd).  A workgroup
 // takes 16 samples through both towers with the trainer's padded-row bf16 MFMA convolutions (the vitals tower as one
-// 144-row pass, the labs tower as two 8-sample passes), fc1 on MFMA from the concat features in LDS, and the small
-// fc2 / fc3 / output head in fp32.  Weights are read straight from the fp32 arena (bf16 fragments built in registers),
+// 144-row pass, the labs tower as two 8-sample passes), fc1 / fc2 / fc3 on MFMA (bf16 operands, fp32 accumulation,
+// as the trainer), the output unit in fp32.  Weights are read straight from the fp32 arena (bf16 fragments built in registers),
 // so no image preparation launch is needed.
 constexpr int E_H1 = 0, E_H2 = E_H1 + NR * LD1 * 2, E_H3 = E_H2 + NR * LD2 * 2, E_XS = E_H3 + NR * LD3 * 2;
 constexpr int ELDF = 1032;                     // concat feature row stride (1024 + 8 bf16)
 constexpr int E_FT = E_XS + 656;               // concat features bf16 [16][ELDF]
-constexpr int E_A1 = E_FT + 16 * ELDF * 2;     // relu(fc1) fp32 [16][132]
-constexpr int E_A2 = E_A1 + 16 * 132 * 4;      // relu(fc2) fp32 [16][68]
-constexpr int E_A3 = E_A2 + 16 * 68 * 4;       // relu(fc3) fp32 [16][36]
+constexpr int E_A1 = E_FT + 16 * ELDF * 2;     // relu(fc1) bf16 [16][136] (fc2's MFMA operand)
+constexpr int E_A2 = E_A1 + 16 * 136 * 2;      // relu(fc2) bf16 [16][72]
+constexpr int E_A3 = E_A2 + 16 * 72 * 2;       // relu(fc3) fp32 [16][36]
 constexpr int E_LDS = E_A3 + 16 * 36 * 4;
 static_assert(E_LDS <= 160 * 1024 && (E_FT & 15) == 0 && (E_A1 & 15) == 0, "cnn2 eval LDS");
 
@@ -1705,38 +1705,31 @@ __global__ void __launch_bounds__(NTH) k_cnn2_eval(AflCnn2Eval a) {
     }
     const float b1 = P[a.off[13] + 16 * wave + li];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) *lf(S, E_A1 + ((4 * g + e) * 132 + 16 * wave + li) * 4) = relu(acc[e] + b1);
+    for (int e = 0; e < 4; ++e) *lu16(S, E_A1 + ((4 * g + e) * 136 + 16 * wave + li) * 2) = bfu(relu(acc[e] + b1));
   }
   lbar();
-  // fc2 (128 -> 64) + ReLU: thread (sample r, outputs o, o + 32)
-  {
-    const int r = tid >> 5, o = tid & 31;
-    const float* w0 = P + a.off[14] + o * 128;
-    const float* w1 = w0 + 32 * 128;
-    float s0v = 0.f, s1v = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < 128; k += 4) {
-      const f4v x = *(const LDS_AS f4v*)(S + E_A1 + (r * 132 + k) * 4);
-      const f4v u = *(const f4v*)(w0 + k), v = *(const f4v*)(w1 + k);
-      s0v += x[0] * u[0] + x[1] * u[1] + x[2] * u[2] + x[3] * u[3];
-      s1v += x[0] * v[0] + x[1] * v[1] + x[2] * v[2] + x[3] * v[3];
-    }
-    *lf(S, E_A2 + (r * 68 + o) * 4) = relu(s0v + P[a.off[15] + o]);
-    *lf(S, E_A2 + (r * 68 + o + 32) * 4) = relu(s1v + P[a.off[15] + o + 32]);
+  // fc2 (128 -> 64) + ReLU on MFMA (bf16 operands, as the trainer's head): waves 0-3, n-tile = wave
+  if (wave < 4) {
+    const float* W2 = P + a.off[14] + (16 * wave + li) * 128 + 8 * g;
+    f4v acc = Z4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      acc = mfma(rfrag(S + E_A1, 136, 0, 32 * k, lane), bf8(*(const f4v*)(W2 + 32 * k), *(const f4v*)(W2 + 32 * k + 4)), acc);
+    const float b2 = P[a.off[15] + 16 * wave + li];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *lu16(S, E_A2 + ((4 * g + e) * 72 + 16 * wave + li) * 2) = bfu(relu(acc[e] + b2));
   }
   lbar();
-  // fc3 (64 -> 32) + ReLU: thread (sample r, output o)
-  {
-    const int r = tid >> 5, o = tid & 31;
-    const float* w = P + a.off[16] + o * 64;
-    float sv = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < 64; k += 4) {
-      const f4v x = *(const LDS_AS f4v*)(S + E_A2 + (r * 68 + k) * 4);
-      const f4v u = *(const f4v*)(w + k);
-      sv += x[0] * u[0] + x[1] * u[1] + x[2] * u[2] + x[3] * u[3];
-    }
-    *lf(S, E_A3 + (r * 36 + o) * 4) = relu(sv + P[a.off[17] + o]);
+  // fc3 (64 -> 32) + ReLU on MFMA: waves 0-1
+  if (wave < 2) {
+    const float* W3 = P + a.off[16] + (16 * wave + li) * 64 + 8 * g;
+    f4v acc = Z4;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      acc = mfma(rfrag(S + E_A2, 72, 0, 32 * k, lane), bf8(*(const f4v*)(W3 + 32 * k), *(const f4v*)(W3 + 32 * k + 4)), acc);
+    const float b3 = P[a.off[17] + 16 * wave + li];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *lf(S, E_A3 + ((4 * g + e) * 36 + 16 * wave + li) * 4) = relu(acc[e] + b3);
   }
   lbar();
   // output (32 -> 1) + sigmoid: wave 0, lane (sample lane >> 2, quarter lane & 3)
