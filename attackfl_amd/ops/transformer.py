@@ -2,11 +2,12 @@
 trainer, and ``csrc/kernels/transformer.hip``, the global-workspace fallback and the eval kernels).
 
 ``train_clients`` runs ONE persistent kernel launch that trains every row of ``params [C, P]`` for all
-local epochs: by default the on-chip trainer with row-split branches (split 5: head + two 4-wave
-workgroups per branch, 5 per client), or its 3-workgroup form (split 4) when 5 workgroups per client do
-not fit the CUs (``auto_split``).  ``reference_train`` is the plain PyTorch fp32 oracle of exactly the same
-computation — same batches, same hash-generated dropout masks, Adam (or the SGD test mode) — used by the
-numerics tests to check the kernels.
+local epochs: by default the on-chip trainer (split 4: head | vitals | labs workgroups, 3 per client), in
+back-to-back launches of the clients that fit when C exceeds one launch's co-residency budget
+(``auto_split``, ``chunked``).  Split 5 (each branch over two 4-wave workgroups by rows, 5 per client) is an
+opt-in variant measured slower; splits 1 / 2 are the global-workspace kernels.  ``reference_train`` is the
+plain PyTorch fp32 oracle of exactly the same computation — same batches, same hash-generated dropout masks,
+Adam (or the SGD test mode) — used by the numerics tests to check the kernels.
 """
 from __future__ import annotations
 
