@@ -271,7 +271,11 @@ struct TW {
   static_assert(R * LP == 144, "144 padded rows per tower workgroup");
 };
 constexpr int NR = 162;  // LDS rows: padded row q at row q + 1; rows 0 and 145..161 stay zero
-constexpr int LD1 = 40, LD2 = 72, LD3 = 136, LDF = 520, LDZ = 132, LDD = 136;
+// activation row strides padded by 16 elements (32 B): the conv GEMMs' ds_read_b128 operand reads (rfrag) are then
+// conflict-free in gfx950's 4 x 16-lane banking (8 extra bytes left 2-way conflicts on every read: 4 extra cycles
+// per instruction, tools/dbg/lds_banks.py); the T-layout row stores get worse (4 -> 12 extra cycles) but are
+// rarer: CNNModel +0.7-1.0 % (profiles/ab_r5_cnn_pad.log; the head's rows padded the same way measured neutral)
+constexpr int LD1 = 48, LD2 = 80, LD3 = 144, LDF = 520, LDZ = 132, LDD = 136;
 constexpr int O_H1 = 0;
 constexpr int O_H2 = O_H1 + NR * LD1 * 2;
 constexpr int O_H3 = O_H2 + NR * LD2 * 2;   // h3, then d(h3) in place
