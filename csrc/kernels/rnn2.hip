@@ -47,10 +47,22 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ----------------------------------------------------------------------------------- LDS maps (bytes)
 // branch workgroup
 constexpr int LDW1 = 24 * 2;                       // layer-1 image row stride: K = din <= 16 (unpermuted) + pad
+#ifndef RNN2_LDW2
+#define RNN2_LDW2 (LD64 + 16)
+#endif
+#ifndef RNN2_LDW3
+#define RNN2_LDW3 (LD64 + 16)
+#endif
+// layer-2 / 3 image row strides (bytes): rows padded by 16 elements (32 B), so the gate GEMMs' fragment reads are
+// conflict-free in gfx950 banking (wfrag ds_read_b128 4 -> 0 extra cycles per instruction, wtfrag 4 -> 2;
+// tools/dbg/lds_banks.py): RNNModel +3.45 % (profiles/ab_r5_img_pad.log).  The room comes from the fp64 column-sum
+// slots moving into the layer-1 image's row padding (dbl_slot).
+constexpr int LDW2 = RNN2_LDW2, LDW3 = RNN2_LDW3;
+__host__ __device__ constexpr int ldg(int l) { return l == 2 ? LDW2 : LDW3; }
 constexpr int B_W1 = 0;                            // [192][24] layer 1 combined gate matrix
 constexpr int B_W2 = B_W1 + 192 * LDW1;            // [192][72] layer 2 (K permuted, pcol)
-constexpr int B_W3 = B_W2 + 192 * LD64;            // [192][72] layer 3
-constexpr int B_X2 = B_W3 + 192 * LD64;            // tile64: h1 (X of dW2); after dW2: tile16 xin (X of dW1)
+constexpr int B_W3 = B_W2 + 192 * LDW2;            // [192][72] layer 3
+constexpr int B_X2 = B_W3 + 192 * LDW3;            // tile64: h1 (X of dW2); after dW2: tile16 xin (X of dW1)
 constexpr int B_X3 = B_X2 + 16384;                 // tile64: h2 (X of dW3); after dW3: layer-1 gradient staging
 constexpr int B_DG = B_X3 + 16384;                 // 3 x tile64: d(gate pre-activations) [128][192] of one layer
 constexpr int B_NVEC = 1280;                       // 6 x (b_ih 96 | b_hh 96) in (layer, direction) order, LN w | b
@@ -59,11 +71,14 @@ constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [1280] their gradient
 // column sums produced wave-locally, accumulated as integer quanta in fp64 (onchip.h lds_addq: exact, so the
 // 8-wave sums are independent of the wave order by construction, as tf2.hip): LN weight / bias (0..127), then
 // per layer the d(b_hn) sums of both directions (128 + 64 (l - 1) + 32 d + j)
+// The fp64 slots live in the layer-1 image's row padding (bytes 32..47 of each 48-byte row: the forward reads
+// bytes 0..31 of a row, the compact update writes only real entries k < din <= 16), two slots per row (dbl_slot).
 constexpr int B_NDBL = 128 + 3 * 64;
-constexpr int B_DBL = B_CS + B_NVEC * 4;
-constexpr int B_MISC = B_DBL + B_NDBL * 8;         // u32 [8] per-wave abort words (+ pad)
+static_assert(B_NDBL <= 2 * 192 && LDW1 == 48, "fp64 column-sum slots fit the layer-1 image padding");
+constexpr int B_MISC = B_CS + B_NVEC * 4;          // u32 [8] per-wave abort words (+ pad)
 constexpr int B_TOTAL = B_MISC + 64;
 constexpr int B_X1 = B_X2, B_GS = B_X3;
+__device__ __forceinline__ uchar* dbl_slot(uchar* smem, int idx) { return smem + B_W1 + (idx >> 1) * LDW1 + 32 + 8 * (idx & 1); }
 enum { VL_LNW = 1152, VL_LNB = 1216 };
 
 // head workgroup
@@ -210,7 +225,7 @@ struct RB {
   __device__ __forceinline__ int ln_w() const { return base + 2 * dir_block(din) + 4 * dir_block(64); }
   // direction d's 96 x 64 block of the layer-l (2, 3) combined image
   __device__ __forceinline__ Mat mat(int l, int d) const {
-    return Mat{wih(l, d), G3, 64, (l == 2 ? B_W2 : B_W3) + 96 * d * LD64, LD64};
+    return Mat{wih(l, d), G3, 64, (l == 2 ? B_W2 : B_W3) + 96 * d * ldg(l), ldg(l)};
   }
   // compact entry -> flat parameter index
   __device__ __forceinline__ int cmp_param(int e) const {
@@ -283,8 +298,8 @@ __device__ __forceinline__ void gru_fwd(const uchar* imgs, const uchar* vec, con
         acc[k] = mma16(*(const LDS_AS s4v*)(imgs + B_W1 + (16 * T + (lane & 15)) * LDW1 + 8 * (lane >> 4)),
                        s4v{b[0], b[1], b[2], b[3]}, Z4);
       } else {
-        acc[k] = mma(wfrag(img, LD64, T, 0, lane), bx[0], Z4);
-        acc[k] = mma(wfrag(img, LD64, T, 1, lane), bx[1], acc[k]);
+        acc[k] = mma(wfrag(img, ldg(L), T, 0, lane), bx[0], Z4);
+        acc[k] = mma(wfrag(img, ldg(L), T, 1, lane), bx[1], acc[k]);
       }
     }
     const uchar* vb = vgl + 4 * v0(L, d);
@@ -417,7 +432,7 @@ __device__ __forceinline__ void gate_bwd(uchar* smem, const float (&dh)[16], con
 __device__ __forceinline__ void dnr_colsum(uchar* smem, int L, const float (&dnr)[16], int lane) {
   float s;
   const int f = colsum64(dnr, lane, s);
-  lds_addq(smem + B_DBL, 128 + 64 * (L - 1) + f, s);
+  lds_addq(dbl_slot(smem, 128 + 64 * (L - 1) + f), 0, s);
 }
 
 // backward of layer L (3 or 2) up to its d(input): dh (in) -> dG tile, dx (out)
@@ -438,7 +453,7 @@ __device__ __forceinline__ void layer_bwd(uchar* smem, const float (&dh)[16], co
       const s8v b = pk8(dg[2 * sl][0], dg[2 * sl][1], dg[2 * sl][2], dg[2 * sl][3], dg[2 * sl + 1][0], dg[2 * sl + 1][1],
                         dg[2 * sl + 1][2], dg[2 * sl + 1][3]);
 #pragma unroll
-      for (int T = 0; T < 4; ++T) acc[T] = mma(wtfrag<true>(img, LD64, T, 3 * d + sl, lane), b, acc[T]);
+      for (int T = 0; T < 4; ++T) acc[T] = mma(wtfrag<true>(img, ldg(L), T, 3 * d + sl, lane), b, acc[T]);
     }
   }
   dnr_colsum(smem, L, dnr, lane);
@@ -546,8 +561,8 @@ __device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wa
     if (g == 0) bias_cs(smem, 1, Tn, i16, bs[0]);
   }
   if (tid < B_NDBL) {
-    const float s = lds_getq(smem + B_DBL, tid);
-    ((LDS_AS double*)(smem + B_DBL))[tid] = 0.0;
+    const float s = lds_getq(dbl_slot(smem, tid), 0);
+    *(LDS_AS double*)dbl_slot(smem, tid) = 0.0;
     int e;
     if (tid < 128) {
       e = VL_LNW + tid;
@@ -726,9 +741,9 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       for (int j = 0; j < 16; ++j) t[j] = dy[j] * xh[j];
       float s;
       int f = colsum64(t, lane, s);
-      lds_addq(smem + B_DBL, f, s);
+      lds_addq(dbl_slot(smem, f), 0, s);
       f = colsum64(dy, lane, s);
-      lds_addq(smem + B_DBL, 64 + f, s);
+      lds_addq(dbl_slot(smem, 64 + f), 0, s);
       vec16g(gm, lane_vec(smem + B_VEC, g) + 4 * VL_LNW);
       ln_bwd2(dh, dy, xh, sv.rstd, gm);
     }
@@ -1108,7 +1123,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 // Block (row tile of 128, model c): the fp32 parameters are converted once into the same bf16 images /
 // fp32 vectors the trainer uses (both branches + head resident: 146 KB of LDS), then each wave runs its 16
 // rows through both branches (GRU layers in the T layout, LayerNorm; eval mode: no dropout) and the head.
-constexpr int E_BR = B_W3 + 192 * LD64;          // one branch's images
+constexpr int E_BR = B_W3 + 192 * LDW3;          // one branch's images
 constexpr int E_VEC = 2 * E_BR;                  // fp32 [2][1280]
 constexpr int E_HW1 = E_VEC + 2 * B_NVEC * 4;    // fc1 image [32][LD128]
 constexpr int E_HW2 = E_HW1 + 32 * LD128;        // fc2 image [16][LD32]
@@ -1136,7 +1151,7 @@ __global__ void __launch_bounds__(NTH) k_rnn2_eval(const float* __restrict__ par
     for (int l = 2; l <= 3; ++l)
       for (int i = tid; i < 192 * 64; i += NTH) {
         const int nn = i >> 6, k = i & 63;
-        st_bf(imgs, (l == 2 ? B_W2 : B_W3) + nn * LD64 + pcol(k) * 2, P[R.wih(l, nn / 96) + (nn % 96) * 64 + k]);
+        st_bf(imgs, (l == 2 ? B_W2 : B_W3) + nn * ldg(l) + pcol(k) * 2, P[R.wih(l, nn / 96) + (nn % 96) * 64 + k]);
       }
     for (int e = tid; e < B_NVEC; e += NTH) ldsf(smem, E_VEC + br * B_NVEC * 4)[e] = P[R.cmp_param(e)];
   }

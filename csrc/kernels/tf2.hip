@@ -41,10 +41,17 @@ using namespace oc;
 
 // ----------------------------------------------------------------------------------- LDS maps (bytes)
 // branch workgroup
+#ifndef TF2_NO_BPAD
+// dense image compact (k unpermuted: the K <= 16 MFMA reads k = 4g .. 4g + 3 at byte 8g), which pays for 32-byte
+// padding of the v / out_proj images (ds_read_b128 fragment reads conflict-free in gfx950 banking)
+constexpr int LDDN = 24 * 2, LDVO = LD64 + 16;
+#else
+constexpr int LDDN = LD32, LDVO = LD64;
+#endif
 constexpr int B_IMG_D = 0;                         // [64][32]  dense (K = din padded to 32)
-constexpr int B_IMG_V = B_IMG_D + 64 * LD32;       // [64][64]  in_proj rows 128..191 (v)
-constexpr int B_IMG_O = B_IMG_V + 64 * LD64;       // [64][64]  out_proj
-constexpr int B_IMG_F1 = B_IMG_O + 64 * LD64;      // [16][64]  ffn.0 (6 real rows)
+constexpr int B_IMG_V = B_IMG_D + 64 * LDDN;       // [64][64]  in_proj rows 128..191 (v)
+constexpr int B_IMG_O = B_IMG_V + 64 * LDVO;       // [64][64]  out_proj
+constexpr int B_IMG_F1 = B_IMG_O + 64 * LDVO;      // [16][64]  ffn.0 (6 real rows)
 constexpr int B_IMG_F2 = B_IMG_F1 + 16 * LD64;     // [64][32]  ffn.3 (6 real columns)
 constexpr int B_H0 = B_IMG_F2 + 64 * LD32;         // tile64: h0 = gelu(dense)          (X of dWv)
 constexpr int B_A = B_H0 + 16384;                  // tile64: a = att_dropout(v)         (X of dWo)
@@ -77,9 +84,19 @@ enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3
 constexpr int VS_F1B = 640;  // ffn.0 bias (6 real)
 
 // head workgroup
+#ifndef TF2_HLD1
+#define TF2_HLD1 (LD128 + 16)
+#endif
+#ifndef TF2_HLD2
+#define TF2_HLD2 (LD64 + 16)
+#endif
+// head image row strides (bytes): rows padded by 16 elements (32 B), so the fragment reads are conflict-free in
+// gfx950 banking (wfrag ds_read_b128 4 -> 0 extra cycles, wtfrag 4 / 6 -> 2; tools/dbg/lds_banks.py,
+// profiles/ab_r5_img_pad.log); the head's LDS map has the room
+constexpr int HLD1 = TF2_HLD1, HLD2 = TF2_HLD2;
 constexpr int H_IMG_W1 = 0;                        // [64][128] fc1
-constexpr int H_IMG_W2 = H_IMG_W1 + 64 * LD128;    // [32][64]  fc2
-constexpr int H_CAT = H_IMG_W2 + 32 * LD64;        // tile128: cat(vitals, labs)     (X of dWf1)
+constexpr int H_IMG_W2 = H_IMG_W1 + 64 * HLD1;     // [32][64]  fc2
+constexpr int H_CAT = H_IMG_W2 + 32 * HLD2;        // tile128: cat(vitals, labs)     (X of dWf1)
 constexpr int H_A1 = H_CAT + 32768;                // tile64:  drop(gelu(fc1))       (X of dWf2)
 constexpr int H_DZ1 = H_A1 + 16384;                // tile64:  d(fc1 pre-activation) (dY of dWf1)
 constexpr int H_DZ2 = H_DZ1 + 16384;               // tile32:  d(fc2 pre-activation) (dY of dWf2)
@@ -195,14 +212,14 @@ struct BrK {
   static constexpr int din = BR == 0 ? D_V : D_L;
   static constexpr int xoff = BR == 0 ? 0 : D_V;
   static constexpr Mat MD{o.dense_w, 64, din, B_IMG_D, LD32};
-  static constexpr Mat MV{o.inproj_w + 128 * 64, 64, 64, B_IMG_V, LD64};
-  static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LD64};
+  static constexpr Mat MV{o.inproj_w + 128 * 64, 64, 64, B_IMG_V, LDVO};
+  static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LDVO};
   static constexpr Mat MF1{o.ff0_w, FF, 64, B_IMG_F1, LD64};
   static constexpr Mat MF2{o.ff3_w, 64, FF, B_IMG_F2, LD32};
   // the v (lo) or out_proj block matrix, built from constants (a `lo ? MV : MO` lvalue select would
   // odr-use the static members and load them from memory, defeating the constant folding of n_real / k_real)
   static __device__ __forceinline__ Mat vo(bool lo) {
-    return Mat{lo ? MV.off : MO.off, 64, 64, lo ? B_IMG_V : B_IMG_O, LD64};
+    return Mat{lo ? MV.off : MO.off, 64, 64, lo ? B_IMG_V : B_IMG_O, LDVO};
   }
   // VEC segment -> flat parameter offset
   static __device__ __forceinline__ int vec_param(int e) {
@@ -367,7 +384,12 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     const s4v bx = bfrag4(xin);
     f4v acc[4];
 #pragma unroll
+#ifndef TF2_NO_BPAD
+    for (int T = 0; T < 4; ++T)
+      acc[T] = mma16(*(const LDS_AS s4v*)(smem + B_IMG_D + (16 * T + (lane & 15)) * LDDN + 8 * (lane >> 4)), bx, Z4);
+#else
     for (int T = 0; T < 4; ++T) acc[T] = mma16(wfrag4(smem + B_IMG_D, LD32, T, lane), bx, Z4);
+#endif
     float bd[16], gp[16];
     vec16g(bd, vg + VS_DB * 256);
 #pragma unroll
@@ -393,8 +415,8 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     f4v acc[4];
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
-      acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 0, lane), b0, Z4);
-      acc[T] = mma(wfrag(smem + B_IMG_V, LD64, T, 1, lane), b1, acc[T]);
+      acc[T] = mma(wfrag(smem + B_IMG_V, LDVO, T, 0, lane), b0, Z4);
+      acc[T] = mma(wfrag(smem + B_IMG_V, LDVO, T, 1, lane), b1, acc[T]);
     }
     sv.matt = mk1 & 0xFu;
     float bv[16];
@@ -416,8 +438,8 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     f4v acc[4];
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
-      acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
-      acc[T] = mma(wfrag(smem + B_IMG_O, LD64, T, 1, lane), b1, acc[T]);
+      acc[T] = mma(wfrag(smem + B_IMG_O, LDVO, T, 0, lane), b0, Z4);
+      acc[T] = mma(wfrag(smem + B_IMG_O, LDVO, T, 1, lane), b1, acc[T]);
     }
     sv.m1 = mk0 & 0xFFFFu;
     float bo[16];
@@ -565,8 +587,8 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     const s8v b0 = bfrag(dO, 0), b1 = bfrag(dO, 1);
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
-      f4v acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 0, lane), b0, Z4);
-      acc = mma(wtfrag<true>(smem + B_IMG_O, LD64, T, 1, lane), b1, acc);
+      f4v acc = mma(wtfrag<true>(smem + B_IMG_O, LDVO, T, 0, lane), b0, Z4);
+      acc = mma(wtfrag<true>(smem + B_IMG_O, LDVO, T, 1, lane), b1, acc);
       const float m = keepf(INV_K01, sv.matt, T);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dv[4 * T + i] = acc[i] * m;
@@ -581,8 +603,8 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     load16(gp, sv.gp);
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
-      f4v acc = mma(wtfrag<true>(smem + B_IMG_V, LD64, T, 0, lane), b0, Z4);
-      acc = mma(wtfrag<true>(smem + B_IMG_V, LD64, T, 1, lane), b1, acc);
+      f4v acc = mma(wtfrag<true>(smem + B_IMG_V, LDVO, T, 0, lane), b0, Z4);
+      acc = mma(wtfrag<true>(smem + B_IMG_V, LDVO, T, 1, lane), b1, acc);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dz[4 * T + i] = (acc[i] + dr1[4 * T + i]) * gp[4 * T + i];
     }
@@ -628,7 +650,11 @@ __device__ __forceinline__ int cmp_img(int e) {
   using C = Cmp<BR>;
   if (e < C::E_F1) {
     const int i = e - C::E_D;
+#ifndef TF2_NO_BPAD
+    return B_IMG_D + (i & 63) * LDDN + (i >> 6) * 2;
+#else
     return B_IMG_D + (i & 63) * LD32 + pcol(i >> 6) * 2;
+#endif
   }
   if (e < C::E_F2) {
     const int i = e - C::E_F1, n = i >> 6, k = i & 63;
@@ -1363,8 +1389,8 @@ __device__ __forceinline__ void branch_split(const AflTfTrainArgs& a, int cid, u
 }
 
 // ================================================================================= head workgroup
-constexpr Mat HW1{FC1_W, 64, 128, H_IMG_W1, LD128};
-constexpr Mat HW2{FC2_W, 32, 64, H_IMG_W2, LD64};
+constexpr Mat HW1{FC1_W, 64, 128, H_IMG_W1, HLD1};
+constexpr Mat HW2{FC2_W, 32, 64, H_IMG_W2, HLD2};
 __device__ __forceinline__ int hvec_param(int e) {
   return e < 64 ? FC1_B + e : e < 96 ? FC2_B + (e - 64) : e < 128 ? OUT_W + (e - 96) : e == 128 ? OUT_B : -1;
 }
@@ -1460,7 +1486,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         acc[T] = Z4;
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
+          acc[T] = mma(wfrag(smem + H_IMG_W1, HLD1, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
       }
       float b1[16];
       vec16(b1, vec + HV_B1 * 4, g);
@@ -1486,8 +1512,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       f4v acc[2];
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 0, lane), b0, Z4);
-        acc[T] = mma(wfrag(smem + H_IMG_W2, LD64, T, 1, lane), b1, acc[T]);
+        acc[T] = mma(wfrag(smem + H_IMG_W2, HLD2, T, 0, lane), b0, Z4);
+        acc[T] = mma(wfrag(smem + H_IMG_W2, HLD2, T, 1, lane), b1, acc[T]);
       }
       float b2[8], wo[8], g2[8], gp2[8];
       vec8(b2, vec + HV_B2 * 4, g);
@@ -1533,7 +1559,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       const s8v bz = bfrag(dz2, 0);
 #pragma unroll
       for (int T = 0; T < 4; ++T) {
-        const f4v acc = mma(wtfrag<true>(smem + H_IMG_W2, LD64, T, 0, lane), bz, Z4);
+        const f4v acc = mma(wtfrag<true>(smem + H_IMG_W2, HLD2, T, 0, lane), bz, Z4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) dz1[4 * T + i] = acc[i] * gk1[4 * T + i];
       }
@@ -1547,8 +1573,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 #pragma unroll
         for (int Tl = 0; Tl < 4; ++Tl) {
           const int T = 4 * hb + Tl;
-          f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 0, lane), b0, Z4);
-          acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, T, 1, lane), b1, acc);
+          f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, HLD1, T, 0, lane), b0, Z4);
+          acc = mma(wtfrag<true>(smem + H_IMG_W1, HLD1, T, 1, lane), b1, acc);
 #pragma unroll
           for (int i = 0; i < 4; ++i) d[4 * Tl + i] = acc[i];
         }
