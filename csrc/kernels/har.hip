@@ -41,7 +41,16 @@ constexpr int D = 64, NH = 4, DH = 16, FF = 256;
 constexpr int NW = 4, NTR = 64 * NW;  // backward row passes: 4 waves (one per SIMD), 64 rows per block
 constexpr int NWF = 8, NTF = 64 * NWF;  // forward row passes: 8 waves (two per SIMD), 16 rows each
 constexpr int NWP = 16, NTP = 64 * NWP;  // post-attention forward: 16 waves (four per SIMD; LDS allows one workgroup per CU)
-constexpr int LDK64 = (64 + 8) * 2, LDK256 = (256 + 8) * 2;  // weight-image row strides (bytes)
+#ifndef HAR_IMG_PAD
+#define HAR_IMG_PAD 8
+#endif
+// weight-image row strides (bytes).  HAR_IMG_PAD=16 (32-byte padding) makes the fragment reads conflict-free in
+// gfx950 banking (wfrag ds_read_b128: 4 -> 0 extra cycles per instruction, wtfrag tr_b16 4 / 6 -> 2;
+// tools/dbg/lds_banks.py), but measured neutral here (3.381 vs 3.380 rounds/s, profiles/ab_r5_img_pad.log): these
+// row passes are not bound by their image reads, unlike the on-chip trainers
+constexpr int LDK64 = (64 + HAR_IMG_PAD) * 2, LDK256 = (256 + HAR_IMG_PAD) * 2;
+// (the post backward's FFN-down image keeps the 8-element padding in any case: 16 more bytes per row do not fit)
+constexpr int LDK256B = (256 + 8) * 2;
 typedef unsigned short u16;
 typedef __attribute__((address_space(1))) const u16 gcu16;
 
@@ -240,14 +249,14 @@ constexpr int PF_WO = 0, PF_W1 = PF_WO + 64 * LDK64, PF_W2 = PF_W1 + 256 * LDK64
 enum { V_BO = 0, V_G1 = 64, V_BE1 = 128, V_B1 = 192, V_B2 = 448, V_G2 = 512, V_BE2 = 576, V_N = 640 };
 constexpr int PF_SMEM = PF_VEC + V_N * 4;
 
-__device__ void post_vectors(uchar* smem, const float* pp, const AflHarLayerW& w) {
-  load_vec(smem, PF_VEC + V_BO * 4, pp + w.ob, 64);
-  load_vec(smem, PF_VEC + V_G1 * 4, pp + w.n1w, 64);
-  load_vec(smem, PF_VEC + V_BE1 * 4, pp + w.n1b, 64);
-  load_vec(smem, PF_VEC + V_B1 * 4, pp + w.l1b, 256);
-  load_vec(smem, PF_VEC + V_B2 * 4, pp + w.l2b, 64);
-  load_vec(smem, PF_VEC + V_G2 * 4, pp + w.n2w, 64);
-  load_vec(smem, PF_VEC + V_BE2 * 4, pp + w.n2b, 64);
+__device__ void post_vectors(uchar* smem, int vec, const float* pp, const AflHarLayerW& w) {
+  load_vec(smem, vec + V_BO * 4, pp + w.ob, 64);
+  load_vec(smem, vec + V_G1 * 4, pp + w.n1w, 64);
+  load_vec(smem, vec + V_BE1 * 4, pp + w.n1b, 64);
+  load_vec(smem, vec + V_B1 * 4, pp + w.l1b, 256);
+  load_vec(smem, vec + V_B2 * 4, pp + w.l2b, 64);
+  load_vec(smem, vec + V_G2 * 4, pp + w.n2w, 64);
+  load_vec(smem, vec + V_BE2 * 4, pp + w.n2b, 64);
 }
 
 __global__ void __launch_bounds__(NTP) k_har_post(AflHarPost a) {
@@ -257,7 +266,7 @@ __global__ void __launch_bounds__(NTP) k_har_post(AflHarPost a) {
   build_img<false>(smem, PF_WO, LDK64, pp + a.w.ow, 64, 64);
   build_img<true>(smem, PF_W1, LDK64, pp + a.w.l1w, 256, 64);
   build_img<true>(smem, PF_W2, LDK256, pp + a.w.l2w, 64, 256);
-  post_vectors(smem, pp, a.w);
+  post_vectors(smem, PF_VEC, pp, a.w);
   __syncthreads();
   const uchar* vec = smem + PF_VEC;
   const uint32_t k1 = dkey(a.d1, c), kf_ = dkey(a.df, c), k2 = dkey(a.d2, c);
@@ -723,7 +732,7 @@ __global__ void __launch_bounds__(AT_NT) k_har_attn_bwd_dq(AflHarAttn a) {
 // workgroup serves; the vector gradients (biases, LayerNorm) are per-lane column-sum registers.
 constexpr int TILE = 64 * 128;
 // LDS map of the post backward (bytes)
-constexpr int PB_WO = 0, PB_W1 = PB_WO + 64 * LDK64, PB_W2 = PB_W1 + 256 * LDK64, PB_VEC = PB_W2 + 64 * LDK256;
+constexpr int PB_WO = 0, PB_W1 = PB_WO + 64 * LDK64, PB_W2 = PB_W1 + 256 * LDK64, PB_VEC = PB_W2 + 64 * LDK256B;
 constexpr int PB_F = PB_VEC + V_N * 4;    // 4 tiles: f (dW2 operand), then d f (dW1 operand)
 constexpr int PB_DF2 = PB_F + 4 * TILE;   // d f2
 constexpr int PB_H1 = PB_DF2 + TILE;      // h1
@@ -754,8 +763,8 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
   const float* pp = a.params + (long)c * a.P;
   build_img<true>(smem, PB_WO, LDK64, pp + a.w.ow, 64, 64);
   build_img<true>(smem, PB_W1, LDK64, pp + a.w.l1w, 256, 64);
-  build_img<true>(smem, PB_W2, LDK256, pp + a.w.l2w, 64, 256);
-  post_vectors(smem, pp, a.w);
+  build_img<true>(smem, PB_W2, LDK256B, pp + a.w.l2w, 64, 256);
+  post_vectors(smem, PB_VEC, pp, a.w);
   __syncthreads();
   const uchar* vec = smem + PB_VEC;
   const float inv1 = a.d1.thr16 ? a.d1.inv_keep : 1.f, invf = a.df.thr16 ? a.df.inv_keep : 1.f,
@@ -908,8 +917,8 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int T = 4 * q + u;
-          f4v acc = mma(wtfrag<true>(smem + PB_W2, LDK256, T, 0, lane), b0, Z4);
-          acc = mma(wtfrag<true>(smem + PB_W2, LDK256, T, 1, lane), b1, acc);
+          f4v acc = mma(wtfrag<true>(smem + PB_W2, LDK256B, T, 0, lane), b0, Z4);
+          acc = mma(wtfrag<true>(smem + PB_W2, LDK256B, T, 1, lane), b1, acc);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int j = 4 * T + i;
@@ -1043,6 +1052,7 @@ __global__ void __launch_bounds__(NTR) k_har_post_bwd(AflHarPostB a) {
 // ---- q | k | v backward: dx = d(residual) + dqkv . W_in ; d(in_proj) partials ----
 constexpr int QB_W = 0, QB_DQ = 192 * LDK64, QB_X = QB_DQ + 3 * TILE, QB_RED = QB_X + TILE;
 constexpr int QB_SMEM = QB_RED + 4 * 192 * 4;
+static_assert(QB_SMEM <= 160 * 1024 && PB_SMEM <= 160 * 1024 && PF_SMEM <= 160 * 1024, "HAR LDS budgets");
 
 __global__ void __launch_bounds__(NTR) __attribute__((amdgpu_waves_per_eu(2, 2))) k_har_qkv_bwd(AflHarQkvB a) {
   extern __shared__ __attribute__((aligned(16))) uchar smem[];
@@ -1254,6 +1264,12 @@ int afl_har_post_bwd(const AflHarPostB& a, int G, hipStream_t s) {
 
 int afl_har_qkv_bwd(const AflHarQkvB& a, int G, hipStream_t s) {
   if (G < 1 || a.Lp % 64 || a.Lp < a.L) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {  // (QB_SMEM passes 64 KB with HAR_IMG_PAD=16)
+    if (hipFuncSetAttribute((const void*)k_har_qkv_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, QB_SMEM) != hipSuccess)
+      return -2;
+    attr = true;
+  }
   hipLaunchKernelGGL(k_har_qkv_bwd, dim3(G, a.C), dim3(NTR), QB_SMEM, s, a);
   return (int)hipGetLastError();
 }
