@@ -82,9 +82,15 @@ __device__ __forceinline__ uchar* dbl_slot(uchar* smem, int idx) { return smem +
 enum { VL_LNW = 1152, VL_LNB = 1216 };
 
 // head workgroup
+#ifndef RNN2_HPAD
+#define RNN2_HPAD 0
+#endif
+// head image row strides (bytes): RNN2_HPAD=16 (32-byte padding, as tf2's head) measured neutral here (+0.07 %,
+// profiles/ab_r5_img_pad.log)
+constexpr int HLD1 = LD128 + RNN2_HPAD, HLD2 = LD32 + RNN2_HPAD;
 constexpr int H_IMG_W1 = 0;                        // [32][128] fc1
-constexpr int H_IMG_W2 = H_IMG_W1 + 32 * LD128;    // [16][32]  fc2
-constexpr int H_CAT = H_IMG_W2 + 16 * LD32;        // tile128: cat(vitals, labs)     (X of dW1)
+constexpr int H_IMG_W2 = H_IMG_W1 + 32 * HLD1;     // [16][32]  fc2
+constexpr int H_CAT = H_IMG_W2 + 16 * HLD2;        // tile128: cat(vitals, labs)     (X of dW1)
 constexpr int H_A1 = H_CAT + 32768;                // tile32:  relu(fc1)              (X of dW2)
 constexpr int H_DZ1 = H_A1 + 8192;                 // tile32:  d(fc1 pre-activation)  (dY of dW1)
 constexpr int H_DZ2 = H_DZ1 + 8192;                // tile16:  d(fc2 pre-activation)  (dY of dW2)
@@ -827,8 +833,8 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
 }
 
 // ================================================================================= head workgroup
-constexpr Mat HW1{FC1_W, 32, 128, H_IMG_W1, LD128};
-constexpr Mat HW2{FC2_W, 16, 32, H_IMG_W2, LD32};
+constexpr Mat HW1{FC1_W, 32, 128, H_IMG_W1, HLD1};
+constexpr Mat HW2{FC2_W, 16, 32, H_IMG_W2, HLD2};
 __device__ __forceinline__ int hvec_param(int e) {
   return e < 32 ? FC1_B + e : e < 48 ? FC2_B + (e - 32) : e < 64 ? OUT_W + (e - 48) : e == 64 ? OUT_B : -1;
 }
@@ -915,7 +921,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         acc[T] = Z4;
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          acc[T] = mma(wfrag(smem + H_IMG_W1, LD128, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
+          acc[T] = mma(wfrag(smem + H_IMG_W1, HLD1, T, s, lane), __builtin_bit_cast(s8v, cv[s]), acc[T]);
       }
       float b1[8];
       vec8(b1, vec + HV_B1 * 4, g);
@@ -931,7 +937,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     float dz2[4], gw[4], f2[4];
     float lrow = 0.f, dy3 = 0.f;
     {
-      const f4v acc = mma(wfrag(smem + H_IMG_W2, LD32, 0, 0, lane), bfrag(a1, 0), Z4);
+      const f4v acc = mma(wfrag(smem + H_IMG_W2, HLD2, 0, 0, lane), bfrag(a1, 0), Z4);
       const f4v b2 = *(const LDS_AS f4v*)(vec + (HV_B2 + 4 * g) * 4), wo = *(const LDS_AS f4v*)(vec + (HV_WO + 4 * g) * 4);
       float dot = 0.f;
 #pragma unroll
@@ -963,7 +969,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       const s4v bz = bfrag4(dz2);
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        const f4v acc = mma16(wtfrag4(smem + H_IMG_W2, LD32, T, lane), bz, Z4);
+        const f4v acc = mma16(wtfrag4(smem + H_IMG_W2, HLD2, T, lane), bz, Z4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) dz1[4 * T + i] = z1[4 * T + i] > 0.f ? acc[i] : 0.f;
       }
@@ -976,7 +982,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
         float dd[16];
 #pragma unroll
         for (int Tl = 0; Tl < 4; ++Tl) {
-          const f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, LD128, 4 * hb + Tl, 0, lane), b0, Z4);
+          const f4v acc = mma(wtfrag<true>(smem + H_IMG_W1, HLD1, 4 * hb + Tl, 0, lane), b0, Z4);
 #pragma unroll
           for (int i = 0; i < 4; ++i) dd[4 * Tl + i] = acc[i];
         }
