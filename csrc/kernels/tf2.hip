@@ -211,11 +211,9 @@ struct BrK {
   static constexpr BrOff o = BR == 0 ? OV : OL;
   static constexpr int din = BR == 0 ? D_V : D_L;
   static constexpr int xoff = BR == 0 ? 0 : D_V;
-  static constexpr Mat MD{o.dense_w, 64, din, B_IMG_D, LD32};
+  // (the dense, ffn.0 and ffn.3 weights are compact entries: their image positions come from cmp_img, not a Mat)
   static constexpr Mat MV{o.inproj_w + 128 * 64, 64, 64, B_IMG_V, LDVO};
   static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LDVO};
-  static constexpr Mat MF1{o.ff0_w, FF, 64, B_IMG_F1, LD64};
-  static constexpr Mat MF2{o.ff3_w, 64, FF, B_IMG_F2, LD32};
   // the v (lo) or out_proj block matrix, built from constants (a `lo ? MV : MO` lvalue select would
   // odr-use the static members and load them from memory, defeating the constant folding of n_real / k_real)
   static __device__ __forceinline__ Mat vo(bool lo) {
