@@ -508,9 +508,12 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
     const bool bias = !ABL(ABL_BIAS) && (b == 2 ? odd : !odd);
     f4v acc0 = Z4, acc1 = Z4, bs = Z4;
     // (the all-ones operand materialised here, opaque: hoisted out of the step loop it was spilled and reloaded from
-    // scratch before each of these MFMAs, 24 scratch round trips per dW phase)
-    s8v one = ones8();
-    asm volatile("" : "+v"(one));
+    // scratch before each of these MFMAs, 24 scratch round trips per dW phase.  Made opaque as a VGPR vector it was
+    // still kept in an AGPR across the step and went through scratch once per step (a 16-byte reload in front of the
+    // dW3 MFMAs); from an opaque SGPR the step loop has no scratch traffic at all)
+    uint32_t o1 = 0x3F803F80u;  // bf16 1.0 pairs
+    asm volatile("" : "+s"(o1));
+    const s8v one = __builtin_bit_cast(s8v, u32x4{o1, o1, o1, o1});
     // fragments of k-step s + 1 issued before the MFMAs of k-step s (double-buffered)
     s8v y[2], x0[2], x1[2];
     y[0] = tfrag<TK64>(DY, 0, Tn & 3, lane);
