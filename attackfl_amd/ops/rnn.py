@@ -69,12 +69,11 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     rows_c, order_c = rows.contiguous(), order.contiguous()
 
-    def launch(p, o, n, s):
+    def launch(p, o, n, s, first=True):
         return native().rnn_train(p, rows_c, o, n, s, int(epochs), int(batch), float(lr), int(opt_mode), int(split),
-                                  kt, stamps)
-    if stamps is None:  # (clients beyond one launch's co-residency budget: back-to-back launches)
-        return chunked(launch, params.shape[0], onchip_capacity(dev, 3), params, order_c, nd_t, seeds_t)
-    return launch(params, order_c, nd_t, seeds_t)
+                                  kt, stamps if first else None)
+    # (clients beyond one launch's co-residency budget: back-to-back launches; a stamped run stamps the first)
+    return chunked(launch, params.shape[0], onchip_capacity(dev, 3), params, order_c, nd_t, seeds_t)
 
 
 def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor, nd, epochs: int, batch: int,

@@ -4,8 +4,7 @@ trainer, and ``csrc/kernels/transformer.hip``, the global-workspace fallback and
 ``train_clients`` runs ONE persistent kernel launch that trains every row of ``params [C, P]`` for all
 local epochs: by default the on-chip trainer (split 4: head | vitals | labs workgroups, 3 per client), in
 back-to-back launches of the clients that fit when C exceeds one launch's co-residency budget
-(``auto_split``, ``chunked``).  Split 5 (each branch over two 4-wave workgroups by rows, 5 per client) is an
-opt-in variant measured slower; splits 1 / 2 are the global-workspace kernels.  ``reference_train`` is the
+(``auto_split``, ``chunked``); splits 1 / 2 / 3 are the global-workspace kernels (``transformer.hip``).  ``reference_train`` is the
 plain PyTorch fp32 oracle of exactly the same computation — same batches, same hash-generated dropout masks,
 Adam (or the SGD test mode) — used by the numerics tests to check the kernels.
 """
@@ -29,14 +28,14 @@ M32 = 0xFFFFFFFF
 def auto_split(C: int, dev) -> int:
     """Trainer variant for C clients, the first whose workgroups all fit on the device at once (one per CU):
     4 = the on-chip trainer (``tf2.hip``: head | vitals | labs workgroups), in chunks of clients that fit when
-    C is larger (``onchip_capacity``).  The global-workspace kernels of ``transformer.hip`` (split 2 / 1) and
-    split 5 (row-split branches, 5 workgroups per client, measured slower, see below) are explicit choices."""
+    C is larger (``onchip_capacity``).  The global-workspace kernels of ``transformer.hip`` (split 3 / 2 / 1) are
+    explicit choices (the tests' cross-checks) or the fallback below 3 CUs per process.  (A row-split variant —
+    each branch over two 4-wave workgroups, 5 per client — was built and measured slower in round 5, 91.5 vs
+    103.6 rounds/s, ``profiles/ab_tf2_r5_row_split.log``, and removed.)"""
     from ..parallel.launcher import gpu_sharers
 
     # (processes sharing the GPU run their own persistent launches on the same CUs: count only this one's share)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count // gpu_sharers()
-    # split 5 measured slower than 4 (round 5: 91.5 vs 103.6 rounds/s at 8 clients, 97.1 vs 110.2 at 1 client,
-    # profiles/ab_tf2_r5_row_split.log): opt-in only (split=5 / AFL_TF_SPLIT=5)
     # more clients than fit run split 4 in back-to-back launches (train_clients_async), not the slower kernels
     return 4 if cus >= 3 else 1
 
@@ -62,14 +61,15 @@ def onchip_capacity(dev, wgs_per_client: int = 3) -> int:
 
 
 def chunked(launch, C: int, cap: int, params, order, nd_t, seeds_t):
-    """Run ``launch(params, order, nd, seeds) -> (ok, losses)`` over client chunks of at most ``cap`` clients,
-    back to back on the current stream; the per-chunk device results are concatenated (no host sync)."""
+    """Run ``launch(params, order, nd, seeds, first) -> (ok, losses)`` over client chunks of at most ``cap``
+    clients, back to back on the current stream (``first``: the chunk that takes the diagnostic stamps, if any);
+    the per-chunk device results are concatenated (no host sync)."""
     parts = client_chunks(C, cap)
     if len(parts) <= 1:
-        return launch(params, order, nd_t, seeds_t)
+        return launch(params, order, nd_t, seeds_t, True)
     oks, losses = [], []
-    for a, b in parts:
-        ok, ls = launch(params[a:b], order[a:b], nd_t[a:b], seeds_t[a:b])
+    for i, (a, b) in enumerate(parts):
+        ok, ls = launch(params[a:b], order[a:b], nd_t[a:b], seeds_t[a:b], i == 0)
         oks.append(ok)
         losses.append(ls)
     return torch.cat(oks), torch.cat(losses)
@@ -93,15 +93,15 @@ def train_clients_async(params: torch.Tensor, rows: torch.Tensor, order: torch.T
     nd_t = _dev_i32(nd, dev)
     seeds_t = seeds if _on(seeds, dev) else torch.tensor([device_seed(s) for s in seeds], dtype=torch.int32, device=dev)
     kt = None
-    if split in (4, 5):
+    if split == 4:
         kt = adam_step_table(float(lr), int(epochs) * -(-int(order.shape[2]) // int(batch)), dev)
     rows_c, order_c = rows.contiguous(), order.contiguous()
 
-    def launch(p, o, n, s):
-        return native().tf_train(p, rows_c, o, n, s, int(epochs), int(batch), float(lr), int(opt_mode), stamps,
-                                 int(split), kt)
-    if split in (4, 5) and stamps is None:
-        return chunked(launch, C, onchip_capacity(dev, 5 if split == 5 else 3), params, order_c, nd_t, seeds_t)
+    def launch(p, o, n, s, first=True):
+        return native().tf_train(p, rows_c, o, n, s, int(epochs), int(batch), float(lr), int(opt_mode),
+                                 stamps if first else None, int(split), kt)
+    if split == 4:  # (a stamped run stamps its first chunk only)
+        return chunked(launch, C, onchip_capacity(dev, 3), params, order_c, nd_t, seeds_t)
     return launch(params, order_c, nd_t, seeds_t)
 
 
@@ -139,10 +139,9 @@ def train_clients(params: torch.Tensor, rows: torch.Tensor, order: torch.Tensor,
     ``split``: workgroups per client — 1 (whole model in one workgroup), 2 (vitals branch + head |
     labs branch) or 3 (head | vitals | labs); the workgroups of a client hand activations and
     gradients to each other every step.  4 = the on-chip trainer (``tf2.hip``, 3 workgroups per client,
-    nothing of the model in global memory during the round), 5 = the same with each branch split over two
-    workgroups by batch rows (5 per client).  Default: ``auto_split``.
-    ``stamps``: optional device int64 [>=32] buffer receiving per-phase wall time (10 ns ticks) of
-    workgroup 0, summed over all steps (diagnostics)."""
+    nothing of the model in global memory during the round).  Default: ``auto_split``.
+    ``stamps``: optional device int64 [>=64] buffer receiving per-phase wall time (10 ns ticks) of
+    workgroup ``stamps[63]`` of the first launch, summed over all steps (diagnostics)."""
     return finish(*train_clients_async(params, rows, order, nd, epochs, batch, lr, seeds, opt_mode, stamps, split))
 
 

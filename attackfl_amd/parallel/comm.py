@@ -168,8 +168,16 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, store=None, ra
     if backend == "auto":
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl" and torch.cuda.is_available():
+        ndev = max(1, torch.cuda.device_count())
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+        if device_index is None and local > ndev:
+            # RCCL needs one GPU per rank; wrapping the ordinal would put two ranks on one GPU and fail later
+            # with an obscure communicator error
+            raise RuntimeError(f"backend 'nccl' with {local} local ranks but {ndev} visible GPU(s): RCCL needs one "
+                               "GPU per rank — use comm.backend 'gloo' or 'auto' (gloo + the IPC all-gather)")
         lr = device_index if device_index is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        lr %= max(1, torch.cuda.device_count())
+        if not 0 <= lr < ndev:
+            raise RuntimeError(f"rank's GPU ordinal {lr} is out of range ({ndev} visible)")
         torch.cuda.set_device(lr)
         device = torch.device("cuda", lr)
     elif torch.cuda.is_available() and device_index is not None:

@@ -545,15 +545,14 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   const int C = params.size(0);
   TORCH_CHECK(order.dim() == 3 && order.size(0) == C && order.size(1) == epochs, "order must be [C, E, maxnd]");
   TORCH_CHECK(batch >= 2 && batch <= 128, "fused trainer supports batch sizes 2..128");
+  TORCH_CHECK(kind == 1 || (split >= 1 && split <= 4), "TransformerModel trainer split must be 1..4, got ", split);
   // split 4 = the on-chip trainers (tf2.hip / rnn2.hip: 3 workgroups per client, state in registers / LDS)
-  // split 5 = tf2.hip with row-split branches (5 workgroups per client: head + two halves per branch)
-  const bool tf2 = kind == 0 && (split == 4 || split == 5), rnn2 = kind == 1 && split == 4;
+  const bool tf2 = kind == 0 && split == 4, rnn2 = kind == 1 && split == 4;
   const long wsf = tf2 ? afl_tf2_ws_floats() : rnn2 ? afl_rnn2_ws_floats() : kind == 0 ? afl_tf_ws_floats() : afl_rnn_ws_floats();
   const long stride = ((wsf + 63) / 64) * 64;
   auto ws = torch::empty({(long)C * stride}, params.options());
   const int split_eff = kind == 1 ? 3 : (int)std::max<int64_t>(1, split);  // (rnn2 / tf2: 3 workgroups per client)
-  const long sync_words = split_eff > 1 ? (long)C * (tf2 && split == 5 ? AFL_TF2S_SYNC_WORDS
-                                                    : tf2 || rnn2 ? AFL_TF2_SYNC_WORDS : AFL_TF_SYNC_WORDS) : 0;
+  const long sync_words = split_eff > 1 ? (long)C * (tf2 || rnn2 ? AFL_TF2_SYNC_WORDS : AFL_TF_SYNC_WORDS) : 0;
   // ok [C] | losses [C, E] | the hand-off words (16-byte aligned): ONE zero fill per launch
   const long head = ((long)C + (long)C * epochs + 3) / 4 * 4;
   auto zero = torch::zeros({head + sync_words}, order.options());
@@ -596,7 +595,9 @@ std::vector<torch::Tensor> fused_train(int kind, torch::Tensor params, torch::Te
   if (a.split > 1) a.sync = (uint32_t*)zero.data_ptr<int>() + head;  // branch-parallel: zeroed hand-off words
   const int rc = tf2 ? afl_tf2_train(&a, cur()) : rnn2 ? afl_rnn2_train(&a, cur())
                  : kind == 0 ? afl_tf_train(&a, cur()) : afl_rnn_train(&a, cur());
-  TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once)");
+  TORCH_CHECK(rc != -4, "branch-parallel fused trainer needs split * C <= CUs (all workgroups resident at once): "
+              "launch at most onchip_capacity() clients at a time (ops/transformer.py chunked; AFL_MAX_CLIENTS_PER_LAUNCH "
+              "caps it)");
   TORCH_CHECK(rc != -5, "on-chip trainer: Adam step table (kt) missing or shorter than the round");
   TORCH_CHECK(rc == 0, "fused trainer launch failed (", rc, ")");
   AFL_CHECK_LAUNCH();

@@ -113,9 +113,6 @@ constexpr int AFL_TF_SYNC_WORDS = 4 * 8 * 32 + 32;  // per-wave flags (128-B lin
 // 2 directions x 2 branches x 8 waves x 4 KB of {value, tag} granules, zeroed with the flags every call
 constexpr int AFL_GR_WORDS = 2 * 2 * 8 * 1024;
 constexpr int AFL_TF2_SYNC_WORDS = AFL_TF_SYNC_WORDS + AFL_GR_WORDS;
-// row-split on-chip trainers (split 5): plus the exchange slots between the two halves of each branch
-// (6 kinds x 2 branches x 2 halves x 4 waves x 4 KB, tf2.hip xs_off)
-constexpr int AFL_TF2S_SYNC_WORDS = AFL_TF2_SYNC_WORDS + 6 * 2 * 2 * 4 * 1024;
 // tf2.hip (TransformerModel / ICU fused training, on-chip edition: weights, Adam state and activations
 // in registers / LDS; 3 workgroups per client, sync words required)
 int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s);

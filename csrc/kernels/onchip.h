@@ -173,19 +173,25 @@ __device__ __forceinline__ void vec8(float (&x)[8], const uchar* vec, int g) {  
 // an addend is an integer below 2^50 and any sum of at most 8 of them stays below 2^53, so every intermediate sum
 // is exactly representable: the fp64 additions are exact, hence associative, and the result has the same bits
 // whatever order the waves arrive in (unquantised fp64 partials were order-independent only while their exponents
-// spanned fewer than ~29 bits).  A NaN / inf / out-of-range partial enters as NaN, which any order propagates:
-// the non-finite result an fp32 sum would have given.  Resolution 2^-34 (~5.8e-11) absolute.
+// spanned fewer than ~29 bits).  A NaN / inf partial enters as NaN, which any order propagates: the non-finite
+// result an fp32 sum would have given.  A FINITE partial with |v| >= 2^16 (a diverging client) saturates to
+// +-(2^50 - 2^26) quanta (~ +-65536): the sum stays finite and order-independent, and that client keeps training
+// like the fp32 reference would (with its column sum clipped to |partial| < 2^16 per wave).  Resolution 2^-34
+// (~5.8e-11) absolute.
 // Cost: rint + scale + convert + one select in front of the same ds_add_f64, straight-line (an int64 form with
 // the conversion done in fp32 / int32 pieces lengthened each call's dependent chain by ~150 cycles: +0.4 us per
 // TransformerModel step, measured; a poison flag through a uniform-address LDS atomic became a 64-iteration
 // scalar loop).
 constexpr float FX_SCALE = 17179869184.0f;  // 2^34
+constexpr float FX_SAT = 1125899839733760.0f;  // 2^50 - 2^26: the largest fp32 below 2^50 quanta (8 of them < 2^53)
 __device__ __forceinline__ void lds_addq(uchar* base, int idx, float v) {
 #ifdef ONCHIP_FP64_COLSUM  // A/B variant (tools/ab_native.sh): the round-4 unquantised fp64 atomics
   __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return;
 #endif
-  float x = fabsf(v) < 65536.f ? __builtin_rintf(v * FX_SCALE) : __builtin_nanf("");
+  const float av = fabsf(v);
+  float x = av < 65536.f ? __builtin_rintf(v * FX_SCALE)
+          : av <= 3.402823466e38f ? __builtin_copysignf(FX_SAT, v) : __builtin_nanf("");
   asm volatile("" : "+v"(x));  // (select in fp32, then convert: one VGPR pair live, not a 64-bit NaN constant)
   __hip_atomic_fetch_add((LDS_AS double*)base + idx, (double)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }

@@ -275,70 +275,6 @@ struct Cmp {
 constexpr int B_GS = B_XIN;
 static_assert(B_GS + (Cmp<1>::N - B_NVEC) * 4 <= B_VEC, "compact gradient staging fits");
 
-// ---------------------------------------------------------------------------- row-split branches (split 5)
-// A branch runs on TWO workgroups of 4 waves, each owning 64 of the 128 batch rows (wave w of half h owns
-// rows 16 (4h + w) .. + 15: the same rows, hand-off slots and dropout masks as wave 4h + w of the 3-workgroup
-// kernel), so every SIMD runs one branch wave instead of two: the branch forward / backward are VALU-issue-
-// bound at two waves per SIMD (tf2 round-3 / round-4 stamps), one wave per SIMD halves the issue time.
-// Per step the halves exchange (granules, onchip.h; slots xs_off):
-//   FWD  after the forward:  the partner's dW operand rows of the block it owns (half 0 owns in_proj.v and
-//        needs h0 from half 1; half 1 owns out_proj and needs a from half 0);
-//   BWD  after the backward: the matching dY rows (d v to half 0, d o to half 1), the tag carrying the wave's
-//        NaN-abort bit, so both halves take the same abort decision before any update;
-//   CA/CB after U1: this half's partial sums over its 64 rows of every compact gradient (small dense / ffn
-//        weights, bias and LayerNorm vectors); both halves then add own + partner (IEEE addition commutes: the
-//        same bits on both) and run the compact Adam REPLICATED — no second hop before the next forward;
-//   IMG  after U2: the owned block's new bf16 image tiles, written into the partner's image at the step end.
-// LDS map of a half: images as above; 128-row tiles for the block operands (H0 A DO DV), 64-row tiles for the
-// half's own small-GEMM operands; the LayerNorm column sums go to per-wave slots summed in a fixed order
-// (no atomics: bit-reproducible by construction).
-constexpr int S_H0 = B_H0;
-constexpr int S_A = S_H0 + 16384;
-constexpr int S_DO = S_A + 16384;
-constexpr int S_DV = S_DO + 16384;
-constexpr int S_X1N = S_DV + 16384;                // 64-row tile64s
-constexpr int S_DF3 = S_X1N + 8192;
-constexpr int S_DZ0 = S_DF3 + 8192;
-constexpr int S_XIN = S_DZ0 + 8192;                // 64-row tile16s
-constexpr int S_F2 = S_XIN + 2048;
-constexpr int S_DF0 = S_F2 + 2048;
-constexpr int S_VEC = S_DF0 + 2048;
-constexpr int S_CS = S_VEC + B_NVEC * 4;
-constexpr int S_LNS = S_CS + B_NVEC * 4;           // fp32 [4 waves][384] LayerNorm gradient column sums
-constexpr int S_MISC = S_LNS + 4 * B_NLN * 4;      // u32 [8] abort words: own waves 0-3, partner waves 4-7
-constexpr int S_TOTAL = S_MISC + 64;
-constexpr int S_GS = S_DZ0;                        // compact weight-gradient staging (DZ0 is dead after U1)
-constexpr int SNTH = 256;
-static_assert(S_GS + (Cmp<1>::N - B_NVEC) * 4 <= S_DZ0 + 8192, "split compact staging fits");
-static_assert(S_TOTAL <= SMEM_CORE, "split LDS map");
-static_assert(S_DF0 + 768 + 256 <= S_VEC, "split dummy words inside DF0");
-// LDS offsets of the activation tiles / vectors: the 3-workgroup map or the split map
-template <bool S>
-struct TM {
-  static constexpr int H0 = S ? S_H0 : B_H0, A = S ? S_A : B_A, X1N = S ? S_X1N : B_X1N, DF3 = S ? S_DF3 : B_DF3,
-                       DO = S ? S_DO : B_DO, DV = S ? S_DV : B_DV, DZ0 = S ? S_DZ0 : B_DZ0, XIN = S ? S_XIN : B_XIN,
-                       F2 = S ? S_F2 : B_F2, DF0 = S ? S_DF0 : B_DF0, VEC = S ? S_VEC : B_VEC;
-};
-// granule exchange slot (kind, branch, sending half, sending wave): 4 KB each, after the head hand-off slots
-enum { XK_FWD = 0, XK_BWD, XK_CA, XK_CB, XK_CC, XK_IMG, XK_N };
-__device__ __forceinline__ int xs_off(int kind, int br, int h, int w, int lane) {
-  return 2 * GR_DIR_BYTES + (((kind * 2 + br) * 2 + h) * 4 + w) * 4096 + lane * 16;
-}
-static_assert(2 * GR_DIR_BYTES + XK_N * 2 * 2 * 4 * 4096 <= (AFL_TF2S_SYNC_WORDS - AFL_TF_SYNC_WORDS) * 4,
-              "split exchange slots inside the sync block");
-// LayerNorm gradient column sums k (G1 B1 G2 B2 G3 B3) of a wave's rows: fp64 accumulators (3-workgroup map)
-// or, split, this wave's own slot (summed over the 4 waves in a fixed order in U1)
-template <bool S>
-__device__ __forceinline__ void ln_cs(uchar* smem, int wave, int k, const float (&x)[16], int lane) {
-  if constexpr (S) {
-    float s;
-    const int f = colsum64(x, lane, s);
-    ldsf(smem, S_LNS)[(wave & 3) * B_NLN + 64 * k + f] = s;
-  } else {
-    ln_colsum(smem, k, x, lane);
-  }
-}
-
 // Every dropout keep-bit of a branch wave's forward for one step, packed into two words:
 //   mk0 = m1 (out_proj dropout, 16 bits) | m2 (ffn.3 dropout) << 16;
 //   mk1 = matt (attention dropout per head, 4 bits) | kf (ffn.0 dropout of features 4g + i) << 4.
@@ -363,18 +299,14 @@ __device__ __forceinline__ void br_masks(uint32_t key, int r, int g, uint32_t& m
   mk1 = matt | (kf << 4);
 }
 
-// (S: a row-split half — `wave` is then the global wave 4h + w: rows, masks and hand-off slots as in the
-// 3-workgroup kernel; the half's own small-GEMM operand tiles are indexed by the local row rl)
-template <int BR, bool S = false>
+template <int BR>
 __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], uint32_t mk0, uint32_t mk1, Saved& sv,
                                            u32x4 (&outp)[2], int lane, int wave) {
   using B = BrK<BR>;
-  using M = TM<S>;
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
-  const int rl = S ? 16 * (wave & 3) + (lane & 15) : r;
-  const uchar* vg = lane_vec(smem + M::VEC, g);  // (one lane base for every vector read of the phase)
-  st4<TK16>(smem + M::XIN, rl, g, xin);
+  const uchar* vg = lane_vec(smem + B_VEC, g);  // (one lane base for every vector read of the phase)
+  st4<TK16>(smem + B_XIN, r, g, xin);
   // ---- dense (K = din <= 16 padded to 32) + GELU
   float h0[16];
   sb();
@@ -403,7 +335,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
       }
     save16(sv.gp, gp);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::H0, r, 4 * t + g, h0 + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_H0, r, 4 * t + g, h0 + 4 * t);
   }
   // ---- v projection, attention dropout per (row, head); at L = 1 softmax == 1, so attn = drop(v)
   float a[16];
@@ -426,7 +358,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
       for (int i = 0; i < 4; ++i) a[4 * t + i] = (acc[t][i] + bv[4 * t + i]) * m;
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::A, r, 4 * t + g, a + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_A, r, 4 * t + g, a + 4 * t);
   }
   // ---- out projection, dropout, residual, LayerNorm 1
   float x1n[16];
@@ -457,7 +389,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     vec16g(bt, vg + VS_B1 * 256);
     affine2(x1n, x1, gm, bt);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::X1N, rl, 4 * t + g, x1n + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_X1N, r, 4 * t + g, x1n + 4 * t);
   }
   // ---- ffn.0 (64 -> 6, one output tile) + GELU + dropout
   float f2v[4];
@@ -473,7 +405,7 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
       f2v[i] = keepf(gl * INV_K01, mk1, 4 + i);
       sv.gk[i] = keepf(gp * INV_K01, mk1, 4 + i);
     }
-    st4<TK16>(smem + M::F2, rl, g, f2v);
+    st4<TK16>(smem + B_F2, r, g, f2v);
   }
   // ---- ffn.3 (6 -> 64, K padded to 32), dropout, residual, LayerNorm 2, LayerNorm 3 (x_bn)
   sb();
@@ -509,14 +441,12 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
 
 // d(branch output) -> every activation gradient of the branch (wave-local), the dY tiles of the dW
 // GEMMs and the column sums of the vector gradients
-template <int BR, bool S = false>
+template <int BR>
 __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16], const Saved& sv, const AdamK& K, int lane,
                                             int wave) {
-  using M = TM<S>;
   opq(lane, wave);
   const int g = lane >> 4, r = 16 * wave + (lane & 15);
-  const int rl = S ? 16 * (wave & 3) + (lane & 15) : r;
-  const uchar* vg = lane_vec(smem + M::VEC, g);
+  const uchar* vg = lane_vec(smem + B_VEC, g);
   float dr2[16];
   sb();
   {  // LayerNorm 3 and 2 backward (xh3 = LN(xh2 * gamma2 + beta2) recomputed: fewer saved registers)
@@ -528,15 +458,15 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     const float rstd3 = ln_fwd2(xh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dout[j] * xh[j];
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 4, t, lane);
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 5, dout, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 4, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 5, dout, lane);
     vec16g(gm, vg + VS_G3 * 256);
     ln_bwd2(dx, dout, xh, rstd3, gm);
     load16(xh, sv.xh2);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 2, t, lane);
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 3, dx, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 2, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 3, dx, lane);
     vec16g(gm, vg + VS_G2 * 256);
     ln_bwd2(dr2, dx, xh, sv.rstd2, gm);
   }
@@ -547,12 +477,12 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
 #pragma unroll
     for (int j = 0; j < 16; ++j) d3[j] = keepf(dr2[j] * INV_K01, sv.m2, j);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::DF3, rl, 4 * t + g, d3 + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DF3, r, 4 * t + g, d3 + 4 * t);
     f4v acc = mma(wtfrag<true>(smem + B_IMG_F2, LD32, 0, 0, lane), bfrag(d3, 0), Z4);
     acc = mma(wtfrag<true>(smem + B_IMG_F2, LD32, 0, 1, lane), bfrag(d3, 1), acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) df0[i] = acc[i] * sv.gk[i];
-    st4<TK16>(smem + M::DF0, rl, g, df0);
+    st4<TK16>(smem + B_DF0, r, g, df0);
   }
   float dr1[16];
   sb();
@@ -569,8 +499,8 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     load16(xh, sv.xh1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t[j] = dx[j] * xh[j];
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 0, t, lane);
-    if (!ABL(K, ABL_COLSUM)) ln_cs<S>(smem, wave, 1, dx, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 0, t, lane);
+    if (!ABL(K, ABL_COLSUM)) ln_colsum(smem, 1, dx, lane);
     vec16g(gm, vg + VS_G1 * 256);
     ln_bwd2(dr1, dx, xh, sv.rstd1, gm);
   }
@@ -581,7 +511,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
 #pragma unroll
     for (int j = 0; j < 16; ++j) dO[j] = keepf(dr1[j] * INV_K01, sv.m1, j);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::DO, r, 4 * t + g, dO + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DO, r, 4 * t + g, dO + 4 * t);
     const s8v b0 = bfrag(dO, 0), b1 = bfrag(dO, 1);
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
@@ -592,7 +522,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
       for (int i = 0; i < 4; ++i) dv[4 * T + i] = acc[i] * m;
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::DV, r, 4 * t + g, dv + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DV, r, 4 * t + g, dv + 4 * t);
   }
   sb();
   {  // v backward: d h0 = d r1 + d v . Wv ; d z0 = d h0 * gelu'(z0)
@@ -607,7 +537,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
       for (int i = 0; i < 4; ++i) dz[4 * T + i] = (acc[i] + dr1[4 * T + i]) * gp[4 * T + i];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) st4<TK64>(smem + M::DZ0, rl, 4 * t + g, dz + 4 * t);
+    for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DZ0, r, 4 * t + g, dz + 4 * t);
   }
 }
 
@@ -634,12 +564,12 @@ __device__ __forceinline__ int cmp_param(int e) {
 // dummy word (DF0 tile) instead
 template <int BR>
 __device__ __forceinline__ int cmp_img(int e);
-template <int BR, bool S = false>
+template <int BR>
 __device__ __forceinline__ uint32_t cmp_dst(int e, int lane) {
   using C = Cmp<BR>;
-  const uint32_t dmy = TM<S>::DF0 + 768 + 4 * lane;
+  const uint32_t dmy = B_DF0 + 768 + 4 * lane;
   if (e >= C::N) return dmy;
-  if (e < B_NVEC) return cmp_param<BR>(e) >= 0 ? (0x80000000u | (uint32_t)(TM<S>::VEC + 4 * e)) : (0x80000000u | dmy);
+  if (e < B_NVEC) return cmp_param<BR>(e) >= 0 ? (0x80000000u | (uint32_t)(B_VEC + 4 * e)) : (0x80000000u | dmy);
   return (uint32_t)cmp_img<BR>(e);
 }
 // bf16 image byte offset of compact weight entry e (>= 648)
@@ -1002,390 +932,6 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   br_fini<BR>(st, P, lane, wave, tid);
 }
 
-// ============================================================================ row-split branch half (split 5)
-// this half's rows of a 128-row activation tile as a granule payload (the 16 features of row r this lane
-// wrote, in T-layout order: chunk t = words 2t, 2t + 1) and back into another tile
-__device__ __forceinline__ void rows_get(const uchar* tile, int r, int g, u32x4 (&u)[2]) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const u32x2v v = *(const LDS_AS u32x2v*)(tile + toff<TK64>(r, 4 * t + g));
-    u[t >> 1][2 * (t & 1)] = v[0];
-    u[t >> 1][2 * (t & 1) + 1] = v[1];
-  }
-}
-__device__ __forceinline__ void rows_put(uchar* tile, int r, int g, const u32x4 (&u)[2]) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    *(LDS_AS u32x2v*)(tile + toff<TK64>(r, 4 * t + g)) = u32x2v{u[t >> 1][2 * (t & 1)], u[t >> 1][2 * (t & 1) + 1]};
-}
-// image chunk of this lane's elements of block tile (k tile T, n tile Tn) (tile_adam_pair's store address)
-__device__ __forceinline__ int blk_chunk(const Mat& M, int T, int Tn, int lane) {
-  return M.img + (16 * Tn + (lane & 15)) * M.ld + pcol(16 * T + 4 * (lane >> 4)) * 2;
-}
-// moment slab of a half, [slot][256 threads] of float4: block tiles m 0-3 / v 4-7, compact chunk c m 8 + 2c / v 9 + 2c
-constexpr int SMOM_SLOTS = 14;
-static_assert((long)SMOM_SLOTS * SNTH <= (long)MOM_SLOTS * NTH, "split moment slab fits a workgroup slab");
-__device__ __forceinline__ f4v smom_ld(__amdgpu_buffer_rsrc_t rs, int s, int tid) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (s * SNTH + tid) * 16, 0, 16));
-}
-__device__ __forceinline__ void smom_st(__amdgpu_buffer_rsrc_t rs, int s, int tid, f4v v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (s * SNTH + tid) * 16, 0, 0);
-  store_guard();
-}
-template <int BR>
-struct SpState {
-  static constexpr int NC = (Cmp<BR>::N + SNTH - 1) / SNTH;  // compact entries per thread (replicated Adam)
-  static constexpr int NS = (NC + 3) / 4;                     // their chunks of 4 (one m and one v slot each)
-  static_assert(8 + 2 * NS <= SMOM_SLOTS, "compact moment slots");
-  TS blk[4];      // the owned block's 2 x 2 tiles (in_proj.v on half 0, out_proj on half 1)
-  VS cmp[NC];     // compact entry e = tid + 256 k (every entry, on both halves)
-  float dst[NC];  // AGPR: its store descriptor (cmp_dst, split map)
-};
-
-// Phase-local lane / wave indices (onchip.h opq): each block of the step recomputes its per-lane addresses
-// from opaque copies, so the compiler cannot hoist them out of the loop and keep them live (spills).
-#define SPLIT_IDX                                                                                         \
-  int lane_o = lane, w_o = w;                                                                             \
-  opq(lane_o, w_o);                                                                                       \
-  const int lane = lane_o, w = w_o, tid = 64 * w_o + lane_o, g = lane_o >> 4;                            \
-  const int r = 16 * (4 * h + w_o) + (lane_o & 15), rp = 16 * (4 * ph + w_o) + (lane_o & 15);           \
-  (void)lane; (void)w; (void)tid; (void)g; (void)r; (void)rp
-template <int BR>
-__device__ __forceinline__ void branch_split(const AflTfTrainArgs& a, int cid, uchar* smem, int h) {
-  using B = BrK<BR>;
-  using C = Cmp<BR>;
-  using SS = SpState<BR>;
-  constexpr int NC = SS::NC, NS = SS::NS;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
-  const int gw = 4 * h + w;               // the 3-workgroup kernel's wave of these rows
-  const int r = 16 * gw + (lane & 15);
-  const int ph = 1 - h;                   // partner half
-  const int rp = 16 * (4 * ph + w) + (lane & 15);  // the partner wave's row for this lane
-  float* P = a.params + (long)cid * NPARAM;
-  uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2S_SYNC_WORDS);
-  const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // head hand-off + exchange slots
-  for (int i = tid; i < SMEM / 4; i += SNTH) ldsf(smem, 0)[i] = 0.f;
-  __syncthreads();
-  SS st;
-  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM + (1 + 2 * BR + h) * MOM_WG_BYTES);  // (head: slab 0)
-#pragma unroll
-  for (int k = 0; k < SMOM_SLOTS; ++k) smom_st(rm, k, tid, Z4);
-  const int Ta = 2 * (w & 1), Tb = 2 * (w >> 1);
-  const Mat Mo = B::vo(h == 0), Mp = B::vo(h != 0);  // owned / partner block
-  {
-#pragma unroll
-    for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) tile_load(st.blk[2 * a2 + b], Mo, Ta + a2, Tb + b, lane, P, smem);
-    for (int i = tid; i < 64 * 16; i += SNTH) {  // the partner's block: image only
-      const int n = i >> 4, k0 = 4 * (i & 15);
-      const float* src = P + Mp.off + n * 64 + k0;
-      *(LDS_AS u32x2v*)(smem + Mp.img + n * Mp.ld + pcol(k0) * 2) = u32x2v{pk2(src[0], src[1]), pk2(src[2], src[3])};
-    }
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      const int e = tid + SNTH * k;
-      float p0 = 0.f;
-      if (e < C::N) {
-        const int pi = cmp_param<BR>(e);
-        p0 = pi >= 0 ? P[pi] : 0.f;
-        if (e < B_NVEC) {
-          ldsf(smem, S_VEC)[e] = p0;
-        } else {
-          *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(p0);
-        }
-      }
-      st.cmp[k] = VS{aw(p0)};
-      st.dst[k] = awu(cmp_dst<BR, true>(e, lane));
-    }
-  }
-  __syncthreads();
-  Stamp stp;
-  stamp_init(stp, a, smem);
-
-  const int nd = a.nd[cid], BS = a.batch, E = a.E;
-  const uint32_t seed = a.seeds[cid];
-  LDS_AS uint32_t* abort_w = ldsu(smem, S_MISC);
-  const int XO = h == 0 ? S_H0 : S_A, YO = h == 0 ? S_DV : S_DO;  // the owned block's X / dY tiles
-  const int XS = h == 0 ? S_A : S_H0, YS = h == 0 ? S_DO : S_DV;  // the tiles whose rows the partner owns
-  int step = 0;
-  Walk wk{0, 0};
-  float xin[4];
-  bool more = walk_valid(wk, nd, BS, E);
-  if (more) load_x<BR>(xin, a, cid, wk, r, g);
-  float mka0, mka1;
-  {
-    uint32_t m0, m1;
-    br_masks<BR>(afl_hash32(seed, 1u), r, g, m0, m1);
-    mka0 = awu(m0);
-    mka1 = awu(m1);
-  }
-  while (more) {
-    ++step;
-    const AdamK K = adam_k(a, step);
-    Saved sv;
-    u32x4 outp[2];
-    prio_hi();
-    asm volatile(";MARK sfwd");
-    br_forward<BR, true>(smem, xin, aru(mka0), aru(mka1), sv, outp, lane, gw);
-    stp(0, tid);
-    gr_put(rg, gr_off(0, BR, gw, lane), outp, (uint32_t)step);  // this wave's output rows -> head
-    prio_lo();
-    {  // FWD: the partner block's operand rows of this wave
-      SPLIT_IDX;
-      u32x4 u[2];
-      rows_get(smem + XS, r, g, u);
-      gr_put(rg, xs_off(XK_FWD, BR, h, w, lane), u, (uint32_t)step);
-    }
-    wk.b0 += BS;  // the next batch's inputs and dropout masks while the head works
-    more = walk_valid(wk, nd, BS, E);
-    if (more) load_x<BR>(xin, a, cid, wk, r, g);
-    {
-      SPLIT_IDX;
-      uint32_t m0, m1;
-      br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), r, g, m0, m1);
-      mka0 = awu(m0);
-      mka1 = awu(m1);
-    }
-    stp(1, tid);
-    u32x4 du[2];
-    const int go[1] = {gr_off(1, BR, gw, lane)};
-    const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
-    prio_hi();
-    stp(2, tid);
-    if (fv == 0xFFFFFFFFu) break;
-    float dout[16];
-    unpack16(du, dout);
-    if (lane == 0) abort_w[w] = fv & 1u;
-    asm volatile(";MARK sbwd");
-    br_backward<BR, true>(smem, dout, sv, K, lane, gw);
-    stp(3, tid);
-    {  // BWD: the partner block's dY rows, this wave's NaN-abort bit in the tag
-      SPLIT_IDX;
-      u32x4 u[2];
-      rows_get(smem + YS, r, g, u);
-      gr_put(rg, xs_off(XK_BWD, BR, h, w, lane), u, ((uint32_t)step << 1) | (fv & 1u));
-    }
-    {  // the partner's FWD rows (sent a whole backward ago) -> the owned block's X tile
-      SPLIT_IDX;
-      u32x4 u[2];
-      const int xo[1] = {xs_off(XK_FWD, BR, ph, w, lane)};
-      if (gr_get<1>(rg, xo, u, (uint32_t)step, 0, sync + XF_TMO, lane) == 0xFFFFFFFFu) break;
-      rows_put(smem + XO, rp, g, u);
-    }
-    lds_bar();  // A: the half's tiles and LayerNorm slots complete
-    stp(4, tid);
-    asm volatile(";MARK su1");
-    // ---- U1: this half's partial sums over its 64 rows: small weight gradients (dense, ffn.3: n tile w;
-    // ffn.0: k tile w), bias sums (MFMA against ones), LayerNorm sums (the 4 waves' slots in a fixed order)
-    f4v as_d = Z4, as_f3 = Z4, af1 = Z4;
-    {
-      SPLIT_IDX;
-      int ln = lane, wv = w;
-      opq(ln, wv);
-      f4v bd = Z4, bf3 = Z4, bo = Z4, bvv = Z4, bf1 = Z4;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const s8v ydz = tfrag<TK64>(smem + S_DZ0, 32 * s, wv, ln), ydf3 = tfrag<TK64>(smem + S_DF3, 32 * s, wv, ln);
-        const s8v ydf0 = tfrag<TK16>(smem + S_DF0, 32 * s, 0, ln);
-        as_d = mma(tfrag<TK16>(smem + S_XIN, 32 * s, 0, ln), ydz, as_d);
-        as_f3 = mma(tfrag<TK16>(smem + S_F2, 32 * s, 0, ln), ydf3, as_f3);
-        af1 = mma(tfrag<TK64>(smem + S_X1N, 32 * s, wv, ln), ydf0, af1);
-        bd = mma(ones8(), ydz, bd);
-        bf3 = mma(ones8(), ydf3, bf3);
-        bo = mma(ones8(), tfrag<TK64>(smem + S_DO, 64 * h + 32 * s, wv, ln), bo);
-        bvv = mma(ones8(), tfrag<TK64>(smem + S_DV, 64 * h + 32 * s, wv, ln), bvv);
-        bf1 = mma(ones8(), ydf0, bf1);
-      }
-      LDS_AS float* cs = ldsf(smem, S_CS);
-      if ((ln >> 4) == 0) {
-        const int c = 16 * wv + (ln & 15);
-        cs[VS_DB * 64 + c] = bd[0];
-        cs[VS_F2B * 64 + c] = bf3[0];
-        cs[VS_OB * 64 + c] = bo[0];
-        cs[VS_VB * 64 + c] = bvv[0];
-        if (wv == 0 && (ln & 15) < FF) cs[VS_F1B + (ln & 15)] = bf1[0];
-      }
-      const LDS_AS float* lns = ldsf(smem, S_LNS);
-      for (int i = tid; i < B_NLN; i += SNTH)
-        cs[ln_seg(i >> 6) * 64 + (i & 63)] = ((lns[i] + lns[B_NLN + i]) + lns[2 * B_NLN + i]) + lns[3 * B_NLN + i];
-    }
-    f4v bm[4], bv[4];  // the owned block's moments (U2), in flight during the partner's BWD wait
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bm[k] = smom_ld(rm, k, tid);
-      bv[k] = smom_ld(rm, 4 + k, tid);
-    }
-    {  // the partner's BWD rows -> the owned block's dY tile; its abort bits
-      SPLIT_IDX;
-      u32x4 u[2];
-      const int yo[1] = {xs_off(XK_BWD, BR, ph, w, lane)};
-      const uint32_t pv = gr_get<1>(rg, yo, u, (uint32_t)step, 1, sync + XF_TMO, lane);
-      if (pv == 0xFFFFFFFFu) break;
-      rows_put(smem + YO, rp, g, u);
-      if (lane == 0) abort_w[4 + w] = pv & 1u;
-    }
-    {  // CA / CB: this half's small weight-gradient partials -> the partner
-      SPLIT_IDX;
-      const u32x4 pa[2] = {__builtin_bit_cast(u32x4, as_d), __builtin_bit_cast(u32x4, as_f3)};
-      gr_put(rg, xs_off(XK_CA, BR, h, w, lane), pa, (uint32_t)step);
-      const u32x4 pb[2] = {__builtin_bit_cast(u32x4, af1), u32x4{0u, 0u, 0u, 0u}};
-      gr_put(rg, xs_off(XK_CB, BR, h, w, lane), pb, (uint32_t)step);
-    }
-    lds_bar();  // B: partials in CS, both halves' block operands complete, every abort bit known
-    stp(5, tid);
-    {
-      SPLIT_IDX;
-      uint32_t any = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) any |= abort_w[i];
-      if (any) break;  // the head saw a NaN loss in some row: no update this step, on either half
-    }
-    {  // CC: this half's vector partial sums -> the partner; the small-GEMM partials park in the (dead) X1N /
-      SPLIT_IDX;
-       // DF3 tiles until the combine (registers are short across U2)
-      LDS_AS float* cs = ldsf(smem, S_CS);
-      const float c2 = tid + 2 * SNTH < B_NVEC ? cs[tid + 2 * SNTH] : 0.f;
-      const u32x4 pc[2] = {u32x4{__float_as_uint(cs[tid]), __float_as_uint(cs[tid + SNTH]), __float_as_uint(c2), 0u},
-                           u32x4{0u, 0u, 0u, 0u}};
-      gr_put(rg, xs_off(XK_CC, BR, h, w, lane), pc, (uint32_t)step);
-      LDS_AS f4v* park = (LDS_AS f4v*)(smem + S_X1N) + 3 * tid;
-      park[0] = as_d;
-      park[1] = as_f3;
-      park[2] = af1;
-    }
-    asm volatile(";MARK su2");
-    {  // ---- U2: the owned block over all 128 rows, Adam, new image tiles -> the partner (IMG)
-      SPLIT_IDX;
-      int ln = lane, wv = w;
-      opq(ln, wv);
-      f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
-#pragma unroll 1
-      for (int s = 0; s < 4; ++s) {
-        const s8v x0 = tfrag<TK64>(smem + XO, 32 * s, Ta, ln), x1 = tfrag<TK64>(smem + XO, 32 * s, Ta + 1, ln);
-        const s8v y0 = tfrag<TK64>(smem + YO, 32 * s, Tb, ln), y1 = tfrag<TK64>(smem + YO, 32 * s, Tb + 1, ln);
-        acc[0][0] = mma(x0, y0, acc[0][0]);
-        acc[0][1] = mma(x0, y1, acc[0][1]);
-        acc[1][0] = mma(x1, y0, acc[1][0]);
-        acc[1][1] = mma(x1, y1, acc[1][1]);
-      }
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        tile_adam_pair(st.blk[b], st.blk[2 + b], bm[b], bv[b], bm[2 + b], bv[2 + b], Mo, Ta, Ta + 1, Tb + b, ln, acc[0][b],
-                       acc[1][b], K, smem);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        smom_st(rm, k, tid, bm[k]);
-        smom_st(rm, 4 + k, tid, bv[k]);
-      }
-      u32x4 u[2];  // the new tiles, read back from this lane's own image stores
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const u32x2v c0 = *(const LDS_AS u32x2v*)(smem + blk_chunk(Mo, Ta, Tb + b, ln));
-        const u32x2v c1 = *(const LDS_AS u32x2v*)(smem + blk_chunk(Mo, Ta + 1, Tb + b, ln));
-        u[b] = u32x4{c0[0], c0[1], c1[0], c1[1]};
-      }
-      gr_put(rg, xs_off(XK_IMG, BR, h, w, lane), u, (uint32_t)step);
-    }
-    stp(6, tid);
-    f4v cm[NS], cv[NS];  // compact moments (U3), in flight during the partner's partials
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      cm[k] = smom_ld(rm, 8 + 2 * k, tid);
-      cv[k] = smom_ld(rm, 9 + 2 * k, tid);
-    }
-    {  // the partner's partials: own + partner (the same sum on both halves) -> GS / CS
-      SPLIT_IDX;
-      u32x4 q[6];
-      const int qo[3] = {xs_off(XK_CA, BR, ph, w, lane), xs_off(XK_CB, BR, ph, w, lane), xs_off(XK_CC, BR, ph, w, lane)};
-      if (gr_get<3>(rg, qo, q, (uint32_t)step, 0, sync + XF_TMO, lane) == 0xFFFFFFFFu) break;
-      const f4v pd = __builtin_bit_cast(f4v, q[0]), pf3 = __builtin_bit_cast(f4v, q[1]), pf1 = __builtin_bit_cast(f4v, q[2]);
-      const LDS_AS f4v* park = (const LDS_AS f4v*)(smem + S_X1N) + 3 * tid;
-      const f4v as_d = park[0], as_f3 = park[1], af1 = park[2];
-      LDS_AS float* gs = ldsf(smem, S_GS);
-      const int i16 = lane & 15, n = 16 * w + i16;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 4 * g + i;
-        if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as_d[i] + pd[i];
-        if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = as_f3[i] + pf3[i];
-        if (i16 < FF) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w + 4 * g + i] = af1[i] + pf1[i];
-      }
-      LDS_AS float* cs = ldsf(smem, S_CS);
-      cs[tid] += __uint_as_float(q[4][0]);
-      cs[tid + SNTH] += __uint_as_float(q[4][1]);
-      if (tid + 2 * SNTH < B_NVEC) cs[tid + 2 * SNTH] += __uint_as_float(q[4][2]);
-    }
-    lds_bar();  // C: full gradients of every compact entry in CS / GS
-    stp(7, tid);
-    asm volatile(";MARK su3");
-    {  // ---- U3: compact entries, replicated on both halves (branch-free, as br_update's U3), 4 at a time
-      SPLIT_IDX;
-      const int dmy = S_DF0 + 4 * lane;
-#pragma unroll
-      for (int c = 0; c < NS; ++c) {
-        constexpr int Q = 4;
-        float mm[Q], vv[Q], gr[Q], pn[Q];
-        VS pa[Q];
-#pragma unroll
-        for (int i = 0; i < Q; ++i) {
-          const int k = 4 * c + i < NC ? 4 * c + i : NC - 1;  // (a short last chunk repeats an entry on dummies)
-          const int e = tid + SNTH * (4 * c + i);
-          mm[i] = cm[c][i];
-          vv[i] = cv[c][i];
-          pa[i] = st.cmp[k];
-          gr[i] = *(const LDS_AS float*)(smem + (e < B_NVEC ? S_CS + 4 * e : S_GS + 4 * (e - B_NVEC)));
-        }
-        adam_staged<Q>(pa, mm, vv, gr, pn, K);
-#pragma unroll
-        for (int i = 0; i < Q; ++i) {
-          if (4 * c + i >= NC) continue;
-          const int k = 4 * c + i;
-          st.cmp[k] = pa[i];
-          const uint32_t d = aru(st.dst[k]);
-          const bool f32 = d >> 31;
-          const int off = (int)(d & 0x7FFFFFFFu);
-          *(LDS_AS float*)(smem + (f32 ? off : dmy + 256)) = pn[i];
-          *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn[i]);
-        }
-        smom_st(rm, 8 + 2 * c, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
-        smom_st(rm, 9 + 2 * c, tid, f4v{vv[0], vv[1], vv[2], vv[3]});
-      }
-    }
-    {  // IMG: the partner's new block tiles -> its image here (read by the next step's forward, after D)
-      SPLIT_IDX;
-      u32x4 u[2];
-      const int io[1] = {xs_off(XK_IMG, BR, ph, w, lane)};
-      if (gr_get<1>(rg, io, u, (uint32_t)step, 0, sync + XF_TMO, lane) == 0xFFFFFFFFu) break;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        *(LDS_AS u32x2v*)(smem + blk_chunk(Mp, Ta, Tb + b, lane)) = u32x2v{u[b][0], u[b][1]};
-        *(LDS_AS u32x2v*)(smem + blk_chunk(Mp, Ta + 1, Tb + b, lane)) = u32x2v{u[b][2], u[b][3]};
-      }
-    }
-    stp(8, tid);
-    lds_bar();  // D
-    stp(9, tid);
-  }
-  stamp_fini(stp, a, smem, tid);
-  // parameters back: the owned block tiles (each half), the replicated compact entries (half 0)
-#pragma unroll
-  for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) tile_store(st.blk[2 * a2 + b], Mo, Ta + a2, Tb + b, lane, P);
-  if (h == 0) {
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      const int e = tid + SNTH * k;
-      if (e < C::N) {
-        const int pi = cmp_param<BR>(e);
-        if (pi >= 0) P[pi] = ar(st.cmp[k].p);
-      }
-    }
-  }
-}
-
 // ================================================================================= head workgroup
 constexpr Mat HW1{FC1_W, 64, 128, H_IMG_W1, HLD1};
 constexpr Mat HW2{FC2_W, 32, 64, H_IMG_W2, HLD2};
@@ -1403,7 +949,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
   const int r = 16 * wave + (lane & 15);
   float* P = a.params + (long)cid * NPARAM;
   uchar* ws = (uchar*)(a.ws + (long)cid * a.ws_stride);
-  gu32* sync = (gu32*)(a.sync + (long)cid * (a.split == 5 ? AFL_TF2S_SYNC_WORDS : AFL_TF2_SYNC_WORDS));
+  gu32* sync = (gu32*)(a.sync + (long)cid * AFL_TF2_SYNC_WORDS);
   const __amdgpu_buffer_rsrc_t rg = gr_rsrc(sync);  // granule hand-off slots
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
@@ -1713,10 +1259,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
 
 #ifdef TF2_STAMPS
 #define K_TF2 k_tf2_train_stamped
-#define K_TF2S k_tf2s_train_stamped
 #else
 #define K_TF2 k_tf2_train
-#define K_TF2S k_tf2s_train
 #endif
 // 3 workgroups per client: blocks c (head), CP + c (vitals branch), 2 CP + c (labs branch).  Role-major block order
 // with a block stride CP padded to a multiple of 8 when the grid still fits: a client's workgroups are blocks
@@ -1740,25 +1284,6 @@ __global__ void __launch_bounds__(t2::NTH) K_TF2(AflTfTrainArgs a) {
   else
     t2::branch_main<1>(a, cid, smem);
 #endif
-}
-// split 5 (a separate kernel: its own register allocation): 5 workgroups per client, blocks c (head) and
-// (1 + 2 br + h) CP + c (half h of branch br), which run 4 waves (the other 4 exit at once; s_barrier waits only
-// for the waves that have not ended)
-__global__ void __launch_bounds__(t2::NTH) K_TF2S(AflTfTrainArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int cp = a.cpad > 0 ? a.cpad : a.C;
-  const int role = blockIdx.x / cp, cid = blockIdx.x - role * cp;
-  if (cid >= a.C) return;
-  if (role == 0) {
-    t2::head_main(a, cid, smem);
-  } else {
-    if (threadIdx.x >= t2::SNTH) return;
-    const int br = (role - 1) >> 1, h = (role - 1) & 1;
-    if (br == 0)
-      t2::branch_split<0>(a, cid, smem, h);
-    else
-      t2::branch_split<1>(a, cid, smem, h);
-  }
 }
 
 #ifndef TF2_STAMPS
@@ -1801,12 +1326,11 @@ int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
 #endif
   if (a->batch > 128 || a->batch < 2 || !a->sync) return -1;
   if (!a->kt || a->kt_n < a->E * ((a->maxnd + a->batch - 1) / a->batch)) return -5;  // step table too short
-  const void* kfn = a->split == 5 ? (const void*)K_TF2S : (const void*)K_TF2;
-  if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess) return -2;
+  if (hipFuncSetAttribute((const void*)K_TF2, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM) != hipSuccess) return -2;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -3;
-  const int wgs = a->split == 5 ? 5 : 3;
+  const int wgs = 3;
   if (wgs * a->C > cus) return -4;  // the workgroups of a client spin on each other: all must be resident
   AflTfTrainArgs b = *a;
   b.cpad = (a->C + 7) / 8 * 8;
@@ -1814,9 +1338,6 @@ int afl_tf2_train(const AflTfTrainArgs* a, hipStream_t s) {
   b.cpad = a->C;
 #endif
   if (wgs * b.cpad > cus) b.cpad = a->C;
-  if (a->split == 5)
-    hipLaunchKernelGGL(K_TF2S, dim3(wgs * b.cpad), dim3(t2::NTH), t2::SMEM, s, b);
-  else
-    hipLaunchKernelGGL(K_TF2, dim3(wgs * b.cpad), dim3(t2::NTH), t2::SMEM, s, b);
+  hipLaunchKernelGGL(K_TF2, dim3(wgs * b.cpad), dim3(t2::NTH), t2::SMEM, s, b);
   return 0;
 }

@@ -6,24 +6,22 @@ register, then runs the rounds: aggregation / defenses / hypernetwork training, 
 ``app.log``) and the per-round ``{model}.pth`` / ``{model}_hyper_{clients}.pth`` checkpoints.
 
 Transport: a TCPStore rendezvous at ``comm.address`` (default ``rabbit.address``) replaces the RabbitMQ
-broker.  With ``comm.backend: auto`` the server picks the process group from the registered devices: RCCL
-when every process owns its own GPU, gloo when several share one (or run on the CPU); on one host the
-update all-gather is the one-shot IPC kernel either way (``comm.one-shot-allgather: auto``).  For
-one-process-per-GPU packed runs use ``launch.py`` under torchrun.
+broker.  The registered CLIENTS form the device process group (client r = group rank r - 1), with server state
+replicated on every client rank; group rank 0 is the leader that writes ``app.log`` and the checkpoints into this
+server's ``log_path`` / checkpoint directory.  This process holds the store and the client table, echoes the
+leader's ``app.log`` to its console and exits when the run is done — it computes nothing and needs no GPU, so 8
+clients on an 8-GPU node are 8 ranks on 8 distinct GPUs.  With ``comm.backend: auto`` the clients' group is RCCL
+when every client owns its own GPU, gloo when several share one (or run on the CPU); on one host the update
+all-gather is the one-shot IPC kernel either way (``comm.one-shot-allgather: auto``).  For packed runs (several
+clients per process) use ``launch.py`` under torchrun.
 """
 from __future__ import annotations
 
 import argparse
-import gc
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-
-def _one_shot(cfg, auto_choice: bool):
-    v = str(cfg.comm.get("one-shot-allgather", "auto")).lower()
-    return auto_choice if v == "auto" else v in ("true", "1")
 
 
 def main(argv=None) -> int:
@@ -32,29 +30,20 @@ def main(argv=None) -> int:
     ap.add_argument("--config", type=str, default="config.yaml")
     args = ap.parse_args(argv)
 
-    import torch
+    import os as _os
 
     from attackfl_amd.config import load_config
-    from attackfl_amd.fl.engine import FLEngine
-    from attackfl_amd.parallel.comm import TorchComm
-    from attackfl_amd.parallel.launcher import init_group, read_transport, serve_rendezvous, table_from_json
+    from attackfl_amd.parallel.launcher import serve_rendezvous, serve_until_done
     from attackfl_amd.utils.log import print_with_color
 
     cfg = load_config(args.config)
-    # (--device cuda = cuda:0; the clients take GPUs 1, 2, ... in registration order: launcher.client_device)
-    device = (torch.device(args.device) if args.device and args.device != "cuda" else
-              torch.device("cuda", 0) if torch.cuda.is_available() else torch.device(args.device or "cpu"))
-    print_with_color(f"Using device: {device}", "green")
-    store, world, table = serve_rendezvous(cfg, device=device)
-    backend, one_shot = read_transport(store)
-    backend = backend if cfg.comm.get("backend", "auto") == "auto" else cfg.comm["backend"]
-    init_group(store, 0, world, backend, int(cfg.comm.get("timeout-s", 600)), device.index)
-    comm = TorchComm(device, backend, one_shot=_one_shot(cfg, one_shot))
-    eng = FLEngine(cfg, comm=comm, table=table_from_json(table), device=device, leader=True)
-    gc.freeze()  # engine, models and tables -> permanent generation: no ms-long full GC scans mid-round
-    eng.run()
-    eng.close()
-    torch.distributed.destroy_process_group()
+    # (--device is accepted for the reference's command line; the server computes nothing: every client rank
+    # holds the replicated server state and the leader client validates, logs and checkpoints)
+    print_with_color(f"Using device: {args.device or 'none (state replicated on the client ranks)'}", "green")
+    store, n, _table = serve_rendezvous(cfg)
+    ok = serve_until_done(store, _os.path.join(_os.path.abspath(cfg.log_path), "app.log"), n)
+    if not ok:
+        return 1
     print_with_color("Ok, ready!", "green")
     return 0
 

@@ -172,21 +172,57 @@ def test_packed_gloo_matches_single_process(tmp_path, world):
         assert torch.allclose(sp[k], mp[k], atol=1e-4), k
 
 
+def _log_lines(path):
+    """app.log messages without the timestamp (``asctime - my_logger - LEVEL - message``)."""
+    return [ln.split(" - ", 1)[1] for ln in open(path).read().splitlines() if " - " in ln]
+
+
 def test_classic_server_and_clients(tmp_path):
+    """The reference-style launch (server.py + N x client.py): the N clients are the whole device group (client r
+    = rank r - 1; on an 8-GPU node 8 clients are 8 RCCL ranks, tests/test_launcher.py), the server holds the store
+    and echoes the leader's app.log; the leader (client 1) writes app.log and the .pth into the server's log_path /
+    checkpoint directory.  The result equals the packed launch with one client per rank byte for byte: same
+    checkpoint tensors, same app.log messages."""
+    import datetime
+
+    import torch.distributed as dist
+
     d = _cfg(tmp_path, server__num_round=2, server__clients=3)
-    d["comm"] = {"backend": "gloo", "address": "127.0.0.1", "port": _free_port()}
+    port = _free_port()
+    d["comm"] = {"backend": "gloo", "address": "127.0.0.1", "port": port}
+    d["engine"]["checkpoint-dir"] = "ckpt"   # relative: resolved against the SERVER's working directory
+    d["log_path"] = "logs"
     cfg_path = _write_cfg(tmp_path, d)
     env = _env()
+    env["OMP_NUM_THREADS"] = "1"
+    srv_dir, cli_dir = tmp_path / "srv", tmp_path / "cli"
+    srv_dir.mkdir()
+    cli_dir.mkdir()
     srv = subprocess.Popen([sys.executable, os.path.join(ROOT, "server.py"), "--device", "cpu", "--config", cfg_path],
-                           env=env, cwd=str(tmp_path), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                           env=env, cwd=str(srv_dir), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     cls = []
-    for i in range(3):
-        extra = ["--attack", "True", "--attack_mode", "Random", "--attack_round", "2", "--attack_args", "0.01"] \
-            if i == 2 else []
-        cls.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "client.py"), "--device", "cpu", "--config",
-                                     cfg_path] + extra, env=env, cwd=str(tmp_path), stdout=subprocess.PIPE,
-                                    stderr=subprocess.PIPE, text=True))
     try:
+        store = None
+        for _ in range(600):
+            try:
+                store = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=5),
+                                      use_libuv=False)
+                break
+            except Exception:  # (the server is still starting)
+                import time
+                time.sleep(0.1)
+        assert store is not None
+        for i in range(3):
+            extra = ["--attack", "True", "--attack_mode", "Random", "--attack_round", "2", "--attack_args", "0.01"] \
+                if i == 2 else []
+            cls.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "client.py"), "--device", "cpu",
+                                         "--config", cfg_path] + extra, env=env, cwd=str(cli_dir),
+                                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+            # registration order = client index: start the next client once this one has registered
+            while int(store.add("attackfl/next_rank", 0)) < i + 1:
+                assert cls[-1].poll() is None, cls[-1].communicate()[1][-3000:]
+                import time
+                time.sleep(0.05)
         out, err = srv.communicate(timeout=600)
         assert srv.returncode == 0, err[-3000:]
         for c in cls:
@@ -196,8 +232,28 @@ def test_classic_server_and_clients(tmp_path):
         for p in [srv] + cls:
             if p.poll() is None:
                 p.kill()
-    assert os.path.exists(os.path.join(tmp_path, "TransformerModel.pth"))
-    assert open(os.path.join(tmp_path, "app.log")).read().count("ROC_AUC") == 2
+    log = srv_dir / "logs" / "app.log"
+    assert (srv_dir / "ckpt" / "TransformerModel.pth").exists() and log.exists()
+    assert not (cli_dir / "logs").exists() and not (cli_dir / "ckpt").exists()
+    assert open(log).read().count("ROC_AUC") == 2
+    assert "ROC_AUC" in out  # the server console echoes the leader's log
+    # the packed launch, one client per rank (same attacker), in one torchrun world of 3
+    dp = dict(d)
+    dp["comm"] = {"backend": "gloo", "attackers": {2: {"mode": "Random", "round": 2, "args": [0.01]}}}
+    dp["engine"] = dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "mp")})
+    dp["log_path"] = str(tmp_path / "mp")
+    p2 = os.path.join(tmp_path, "packed.yaml")
+    with open(p2, "w") as fh:
+        yaml.safe_dump(dp, fh)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "launch.py"),
+           "--config", p2, "--device", "cpu"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _log_lines(log) == _log_lines(tmp_path / "mp" / "app.log")
+    a = torch.load(srv_dir / "ckpt" / "TransformerModel.pth", weights_only=True)
+    b = torch.load(tmp_path / "mp" / "TransformerModel.pth", weights_only=True)
+    assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
 
 
 def test_fault_injection_retries_round(tmp_path):

@@ -101,3 +101,68 @@ def test_bench_ranks_sharing_gpu(gpu, tmp_path, world, extra):
     assert out["comm"] == "ipc-one-shot" and out["speculative"] is True
     assert out["ckpt_dropped"] == 0 and out["ckpt_written"] >= 4
     assert out["config"]["parallelism"] == f"fl8-clients-over-{world}-ranks"
+
+
+def test_classic_launch_on_the_gpu_matches_single_process_bitwise(gpu, tmp_path):
+    """The reference-style launch on the GPU box: server.py + 4 x client.py (clients 1-4 -> group ranks 0-3, all on
+    the one visible GPU: gloo group + IPC all-gather, each client's co-residency budget a quarter of the CUs); the
+    leader client writes the server's checkpoint, which equals the single-process run bit for bit."""
+    import datetime
+    import time
+
+    import torch.distributed as dist
+
+    port = _port()
+    d = {
+        "server": {"num-round": 2, "clients": 4, "mode": "fedavg", "model": "TransformerModel",
+                   "data-distribution": {"num-data-range": [300, 600]}},
+        "learning": {"epoch": 2, "batch-size": 128},
+        "data": {"synthetic": True, "train-size": 4000, "test-size": 1000},
+        "comm": {"address": "127.0.0.1", "port": port},
+        "engine": {"checkpoint-dir": "ckpt", "trainer": "auto", "seed": 3},
+        "log_path": "logs",
+    }
+    cfg_path = tmp_path / "config.yaml"
+    cfg_path.write_text(yaml.safe_dump(d))
+    env = dict(os.environ, PYTHONPATH=ROOT, ATTACKFL_QUIET="1")
+    srv = subprocess.Popen(["timeout", "-k", "10", "170", sys.executable, os.path.join(ROOT, "server.py"),
+                            "--config", str(cfg_path)], env=env, cwd=str(tmp_path), stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True)
+    cls = []
+    try:
+        store = None
+        for _ in range(300):
+            try:
+                store = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=5),
+                                      use_libuv=False)
+                break
+            except Exception:
+                time.sleep(0.2)
+        assert store is not None
+        for i in range(4):
+            cls.append(subprocess.Popen(["timeout", "-k", "10", "160", sys.executable, os.path.join(ROOT, "client.py"),
+                                         "--config", str(cfg_path)], env=env, cwd=str(tmp_path),
+                                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+            while int(store.add("attackfl/next_rank", 0)) < i + 1:  # registration order = client index
+                assert cls[-1].poll() is None, cls[-1].communicate()[1][-3000:]
+                time.sleep(0.05)
+        out, err = srv.communicate(timeout=180)
+        assert srv.returncode == 0, err[-3000:]
+        for c in cls:
+            o, e = c.communicate(timeout=60)
+            assert c.returncode == 0, e[-3000:]
+    finally:
+        for p in [srv] + cls:
+            if p.poll() is None:
+                p.kill()
+    mp = torch.load(tmp_path / "ckpt" / "TransformerModel.pth", weights_only=True)
+    assert open(tmp_path / "logs" / "app.log").read().count("ROC_AUC") == 2
+    d1 = dict(d, engine=dict(d["engine"], **{"checkpoint-dir": str(tmp_path / "sp")}), log_path=str(tmp_path / "sp"))
+    d1["comm"] = {}
+    eng = FLEngine(from_dict(d1), device="cuda", verbose=False)
+    eng.run()
+    eng.close()
+    sp = torch.load(tmp_path / "sp" / "TransformerModel.pth", weights_only=True)
+    assert list(sp) == list(mp)
+    for k in sp:
+        assert torch.equal(sp[k].cpu(), mp[k].cpu()), k

@@ -44,7 +44,7 @@ def test_eval_forward_matches_reference(gpu):
     assert (mod - ref).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("split", [1, 2, 3, 4])
 @pytest.mark.parametrize("batch", [128, 100])
 def test_sgd_step_gradients_match(gpu, batch, split):
     """One SGD step (opt_mode 1) exposes the raw gradients: compare p1 - p0 with the oracle."""
@@ -83,7 +83,7 @@ def test_adam_epoch_tracks_reference(gpu):
     assert torch.allclose(loss, loss_r, rtol=0.05, atol=0.02), (loss, loss_r)
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("split", [1, 2, 3, 4])
 def test_nan_params_fail_client(gpu, split):
     rows, params, plan = _setup(2, [300, 300])
     params[1, 5] = float("nan")
@@ -129,7 +129,7 @@ def test_branch_parallel_matches_single_workgroup(gpu):  # noqa: D401
             assert torch.allclose(outs[0][1], o[1], rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("split", [3, 4, 5])
+@pytest.mark.parametrize("split", [3, 4])
 def test_training_is_bit_reproducible(gpu, split):
     """A client's result may not depend on the launch that trains it: the multi-rank engine trains
     clients 0-1 on rank 0 and 2-3 on rank 1 and must equal the single-process run of all four (the
@@ -177,35 +177,9 @@ def test_saturated_sigmoid_start_matches_oracle(gpu):
     assert torch.allclose(loss, loss_r, rtol=0.1, atol=0.05), (loss, loss_r)
 
 
-@pytest.mark.parametrize("C", [1, 3, 8])
-def test_row_split_matches_three_workgroups(gpu, C):
-    """Split 5 (each branch on two 4-wave workgroups, 64 rows each) runs the 3-workgroup kernel's arithmetic
-    except for the order of the per-row sums (two 64-row partials added across the halves): raw SGD updates
-    agree to float rounding, Adam trajectories closely, with partial and size-1 batches; C = 1 and 3 pad the
-    grid so a client's workgroups share one XCD."""
-    nd = [700, 513, 300, 129, 640, 256, 901, 130][:C]
-    rows, params, plan = _setup(C, nd, seed=4)
-    seeds = list(range(21, 21 + C))
-    for opt_mode, lr in ((1, 0.01), (0, 0.004)):
-        outs = []
-        for split in (4, 5):
-            dev = params.clone().to(gpu)
-            ok, loss = T.train_clients(dev, rows.to(gpu), plan.order.to(gpu), plan.nd, 1, 128, lr, seeds,
-                                       opt_mode=opt_mode, split=split)
-            assert ok.tolist() == [1] * C
-            outs.append((dev.cpu(), loss))
-        d = (outs[0][0] - outs[1][0]).abs()
-        moved = (outs[0][0] - params).abs()
-        if opt_mode == 1:
-            assert d.max().item() < 0.02 * moved.max().item(), (d.max(), moved.max())
-        else:
-            assert d.mean().item() < 0.05 * moved.mean().item(), (d.mean(), moved.mean())
-        assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-2, atol=1e-4), (outs[0][1], outs[1][1])
-
-
 def test_auto_split_choice(gpu):
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
-    assert T.auto_split(8, gpu) == 4  # (split 5 is opt-in: measured slower, ops/transformer.py auto_split)
+    assert T.auto_split(8, gpu) == 4
     assert T.auto_split(cus // 3, gpu) == 4
     assert T.auto_split(cus // 3 + 1, gpu) == 4  # more clients: back-to-back split-4 launches (chunked)
     assert T.onchip_capacity(gpu) == cus // 3
@@ -236,13 +210,27 @@ def test_cross_wave_column_sums_are_order_independent(gpu):
     # (the round-4 unquantised fp64 atomics on the same partials, for the log: distinct results over the orders)
     print("fp64 atomics:", len({native().fxsum_test(vals.to(gpu), seed, 1).cpu().numpy().tobytes() for seed in range(48)}),
           "distinct results over 48 launches")
-    # a non-finite or out-of-range (|v| >= 2^16) partial poisons its slot (decoded NaN, as an fp32 sum of a
-    # non-finite partial would give); the other slots keep their exact sums
-    for badv in (float("nan"), float("inf"), -float("inf"), 70000.0):
+    # a non-finite partial poisons its slot (decoded NaN, as an fp32 sum of a non-finite partial would give); the
+    # other slots keep their exact sums
+    for badv in (float("nan"), float("inf"), -float("inf")):
         bad = vals.clone()
         bad[3, 5] = badv
         res = native().fxsum_test(bad.to(gpu), 1, 0).cpu()
         assert torch.isnan(res[5]) and not torch.isnan(res[torch.arange(64) != 5]).any(), badv
+        assert torch.equal(res[torch.arange(64) != 5], exp[torch.arange(64) != 5])
+    # a FINITE partial at or beyond 2^16 saturates to +-(2^50 - 2^26) quanta: the slot stays finite (the fp32
+    # reference keeps training such a client) and exact / order-independent; 65535.99 stays unsaturated
+    sat = 2 ** 50 - 2 ** 26
+    for badv, q_bad in ((65536.0, sat), (-70000.0, -sat), (3.0e38, sat), (65535.99, None)):
+        bad = vals.clone()
+        bad[3, 5] = badv
+        outs = {native().fxsum_test(bad.to(gpu), seed, 0).cpu().numpy().tobytes() for seed in range(8)}
+        assert len(outs) == 1, badv
+        res = torch.frombuffer(bytearray(outs.pop()), dtype=torch.float32)
+        col = [round(Fraction(float(v)) * 2 ** 34) for v in bad[:, 5].tolist()]
+        if q_bad is not None:
+            col[3] = q_bad
+        assert torch.isfinite(res[5]) and res[5].item() == float(Fraction(sum(col), 2 ** 34)), (badv, res[5])
         assert torch.equal(res[torch.arange(64) != 5], exp[torch.arange(64) != 5])
     # eight poisoned partials in one slot decode as NaN
     bad = vals.clone()

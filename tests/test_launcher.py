@@ -24,32 +24,40 @@ def test_client_device_mapping():
     # explicit devices win
     assert L.client_device("cuda:5", 1, 8) == "cuda:5"
     assert L.client_device("cpu", 3, 8) == "cpu"
-    # --device cuda / none: client r -> GPU r % ndev (server = rank 0 on GPU 0)
-    assert [L.client_device(None, r, 8) for r in range(1, 9)] == [f"cuda:{i}" for i in (1, 2, 3, 4, 5, 6, 7, 0)]
-    assert L.client_device("cuda", 3, 8) == "cuda:3"
-    # fewer GPUs than clients: round robin, some GPUs shared
-    assert [L.client_device(None, r, 2) for r in range(1, 5)] == ["cuda:1", "cuda:0", "cuda:1", "cuda:0"]
+    # --device cuda / none: client r -> GPU (r - 1) % ndev (the server takes no GPU)
+    assert [L.client_device(None, r, 8) for r in range(1, 9)] == [f"cuda:{i}" for i in range(8)]
+    assert L.client_device("cuda", 3, 8) == "cuda:2"
+    # more clients than GPUs: round robin, some GPUs shared
+    assert [L.client_device(None, r, 2) for r in range(1, 5)] == ["cuda:0", "cuda:1", "cuda:0", "cuda:1"]
     # no GPU at all
     assert L.client_device(None, 1, 0) == "cpu"
 
 
 def test_classic_backend_on_an_8_gpu_node():
-    server = "cuda:0"
-    # 7 clients + server: every process owns a GPU -> RCCL, IPC all-gather on the one host
-    devs7 = [server] + [L.client_device(None, r, 8) for r in range(1, 8)]
-    assert L.choose_backend(_descs(devs7)) == ("nccl", True)
-    assert L.max_sharers(_descs(devs7)) == 1
-    # 8 clients + server on 8 GPUs: client 8 shares GPU 0 with the server -> gloo group, IPC data path
-    devs8 = [server] + [L.client_device(None, r, 8) for r in range(1, 9)]
-    assert L.choose_backend(_descs(devs8)) == ("gloo", True)
-    assert L.max_sharers(_descs(devs8)) == 2
-    # one visible GPU (the GPU-box classic test): everyone shares it
-    devs1 = [server] + [L.client_device(None, r, 1) for r in range(1, 4)]
-    assert devs1 == ["cuda:0"] * 4
+    # the reference-style launch (server + 8 clients) on an 8-GPU node: the device group is the 8 clients
+    # alone, each on its own GPU -> RCCL, IPC all-gather on the one host, every client with the whole chip
+    devs8 = [L.client_device(None, r, 8) for r in range(1, 9)]
+    assert L.choose_backend(_descs(devs8)) == ("nccl", True)
+    assert L.max_sharers(_descs(devs8)) == 1
+    # 16 clients on 8 GPUs: two per GPU -> gloo group, IPC data path, half the CUs each
+    devs16 = [L.client_device(None, r, 8) for r in range(1, 17)]
+    assert L.choose_backend(_descs(devs16)) == ("gloo", True)
+    assert [L.sharers_of(_descs(devs16), d) for d in _descs(devs16)] == [2] * 16
+    # one visible GPU (the GPU-box classic test): every client shares it
+    devs1 = [L.client_device(None, r, 1) for r in range(1, 4)]
+    assert devs1 == ["cuda:0"] * 3
     assert L.choose_backend(_descs(devs1)) == ("gloo", True)
-    assert L.max_sharers(_descs(devs1)) == 4
+    assert L.max_sharers(_descs(devs1)) == 3
     # CPU processes: gloo, no IPC
     assert L.choose_backend(_descs(["cpu", "cpu"])) == ("gloo", False)
+
+
+def test_sharers_are_counted_per_gpu():
+    """one shared GPU must not halve the budget of clients that own theirs."""
+    devs = ["cuda:0", "cuda:0", "cuda:1", "cuda:2"]
+    d = _descs(devs)
+    assert [L.sharers_of(d, x) for x in d] == [2, 2, 1, 1]
+    assert L.sharers_of(d, {"type": "cpu"}) == 1
 
 
 def test_gpu_sharers_default_does_not_guess_from_local_world(monkeypatch):
@@ -96,6 +104,7 @@ def _run_sharers(world, same):
 
 
 def test_sync_gpu_sharers_counts_processes_per_physical_gpu():
-    # 3 ranks, all on one GPU -> 3; ranks 0, 1 on one GPU and rank 2 on its own -> 2 (the largest group)
+    # 3 ranks, all on one GPU -> 3 each; ranks 0, 1 on one GPU and rank 2 on its own -> 2, 2 and 1 (each rank's
+    # budget follows its own GPU)
     assert [(n, m) for _, n, m in _run_sharers(3, same=True)] == [(3, 3)] * 3
-    assert [(n, m) for _, n, m in _run_sharers(3, same=False)] == [(2, 2)] * 3
+    assert [(n, m) for _, n, m in _run_sharers(3, same=False)] == [(2, 2), (2, 2), (1, 1)]

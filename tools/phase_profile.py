@@ -31,13 +31,6 @@ NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:bac
           8: "B:end barrier", 10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss",
           13: "H:dW+Adam", 14: "H:end barrier"}
 
-# row-split on-chip trainer (split 5, tf2.hip branch_split): blocks 1..4 = (branch, half) (0,0) (0,1) (1,0) (1,1)
-NAMES5 = {0: "S:forward", 1: "S:publish+FWD put+prefetch", 2: "S:wait d(out)", 3: "S:backward",
-          4: "S:BWD put+FWD get+bar A", 5: "S:U1 partials+BWD get+bar B", 6: "S:CC+U2 block dW+Adam+IMG put",
-          7: "S:partner partials+bar C", 8: "S:U3 compact Adam+IMG get", 9: "S:end barrier",
-          10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss", 13: "H:dW+Adam", 14: "H:end barrier"}
-
-
 def block_stride(clients: int, wgs: int, dev) -> int:
     """tf2.hip's role-major block stride: C padded to a multiple of 8 when the padded grid still fits."""
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -68,8 +61,7 @@ def main():
     if args.model == "RNNModel":
         return main_rnn(args)
     dev = torch.device("cuda", 0)
-    used0 = args.split if args.split > 0 else T.auto_split(args.clients, dev)
-    blocks = (list(range(5)) if used0 == 5 else [0, 1, 2]) if args.block < 0 else [args.block]
+    blocks = [0, 1, 2] if args.block < 0 else [args.block]
     ds = synthetic_icu(60000, seed=3)
     rows = torch.cat([ds.vitals, ds.labs, ds.labels[:, None]], 1).to(dev)
     lay = ParamLayout.for_model("TransformerModel")
@@ -88,10 +80,10 @@ def main():
 
 
 def run(args, dev, rows, order, plan, params, split, used, block, wave=0):
-    names = NAMES4 if used == 4 else NAMES5 if used == 5 else NAMES
+    names = NAMES4 if used == 4 else NAMES
     stamps = torch.zeros(64, dtype=torch.int64, device=dev)
     # role-major block order: role r of client 0 is block r * CP (the padded stride of the on-chip trainers)
-    stamps[63] = block * (block_stride(args.clients, 5 if used == 5 else 3, dev) if used in (4, 5) else args.clients)
+    stamps[63] = block * (block_stride(args.clients, 3, dev) if used == 4 else args.clients)
     stamps[62] = wave
     t0 = time.perf_counter()
     T.train_clients(params.clone(), rows, order, plan.nd, args.epochs, 128, 0.004, list(range(args.clients)),
