@@ -504,6 +504,16 @@ CNN2_TIMEOUT = "cnn2 trainer: a cross-workgroup wait timed out (workgroups not c
 
 
 # ================================================================================== step tables
+def step_tables_native(order: torch.Tensor, nd_dev: torch.Tensor, S: int, B: int, zero_i=None, zero_f=None):
+    """``step_tables`` on the GPU in ONE launch (``plan.hip`` ``k_step_tables``), which also zero-fills the given
+    per-round int32 / fp32 tensors: (idx, bsz, ep, nb).  ``S`` = max over clients of epochs x batches."""
+    from .. import ops
+
+    zi = [zero_i] if zero_i is not None else []
+    zf = [zero_f] if zero_f is not None else []
+    return tuple(ops.native().step_tables(order.contiguous(), nd_dev, int(B), int(S), zi, zf))
+
+
 def step_tables(order: torch.Tensor, nd: Sequence[int], epochs: int, B: int, device):
     """Per-step batch tables from a ``Plan``: ``idx [S, C, B]`` (-1 = padding), ``bsz [S, C]``,
     ``epoch [S, C]``, ``nb [C]`` (batches per epoch, the loss divisor).  Client c's s-th step is its
@@ -561,14 +571,14 @@ class ProgramRunner:
         pg = self.prog
         dev = pg.device
         C, P = params.shape
-        idx, bsz, ep, nb, S = step_tables(plan.order, plan.nd, plan.epochs, pg.B, dev)
-        if max_steps is not None:
-            S = min(S, max_steps)
         ctl = StepCtl.create(seeds, dev, min_bs=1 if compat_har else 2, nan_abort=not compat_har)
         if self._onchip_cnn(params, sgd_lr, max_steps):
             # sgd_lr > 0: the gradient-test mode (one plain SGD step p -= sgd_lr g exposes the raw gradients)
-            return self._train_cnn2(table, params, plan, sgd_lr if sgd_lr > 0.0 else lr, ctl, (idx, bsz, ep, nb, S),
-                                    sync, opt_mode=1 if sgd_lr > 0.0 else 0)
+            return self._train_cnn2(table, params, plan, sgd_lr if sgd_lr > 0.0 else lr, ctl, sync,
+                                    opt_mode=1 if sgd_lr > 0.0 else 0)
+        idx, bsz, ep, nb, S = step_tables(plan.order, plan.nd, plan.epochs, pg.B, dev)
+        if max_steps is not None:
+            S = min(S, max_steps)
         out_params = params
         if params.is_cuda and P % 16:
             # train in a copy whose client rows start 64-byte aligned (P is odd for every model here, so every
@@ -663,20 +673,27 @@ class ProgramRunner:
         lim = int(os.environ.get("AFL_MAX_CLIENTS_PER_LAUNCH", "0") or 0)
         return min(cap, lim) if lim > 0 else cap
 
-    def _train_cnn2(self, table, params, plan, lr, ctl, tables, sync, opt_mode: int = 0):
+    def _train_cnn2(self, table, params, plan, lr, ctl, sync, opt_mode: int = 0):
         from .. import ops
 
         nat = ops.native()
         pg = self.prog
         C = params.shape[0]
-        idx, bsz, ep, nb, S = tables
         dev = params.device
-        if getattr(self, "_cnn2_ws", None) is None or self._cnn2_ws[0].numel() < C * int(nat.cnn2_ws_bytes()):
-            self._cnn2_ws = (torch.empty(C * int(nat.cnn2_ws_bytes()), dtype=torch.uint8, device=dev),
-                             torch.zeros(C * int(nat.cnn2_ctr_words()), dtype=torch.int32, device=dev))
-        ws, ctr = self._cnn2_ws
-        failed = torch.zeros(C, dtype=torch.int32, device=dev)
-        losses = torch.zeros(C, plan.epochs, device=dev)
+        if getattr(self, "_cnn2_ws", None) is None or self._cnn2_ws.numel() < C * int(nat.cnn2_ws_bytes()):
+            self._cnn2_ws = torch.empty(C * int(nat.cnn2_ws_bytes()), dtype=torch.uint8, device=dev)
+        ws = self._cnn2_ws
+        # the round boundary in one launch: step tables + zeroed failed flags (int32 [C] | the first chunk's cross-
+        # workgroup counters) and losses
+        ncw = C * int(nat.cnn2_ctr_words())
+        zi = torch.empty(C + ncw, dtype=torch.int32, device=dev)
+        failed = zi[:C]
+        losses = torch.empty(C, plan.epochs, device=dev)
+        nd_dev = plan.nd_dev if plan.nd_dev is not None and plan.nd_dev.device == dev else \
+            Lx.upload(torch.as_tensor(plan.nd, dtype=torch.int32), dev)
+        nbat = [max(1, math.ceil(int(n) / pg.B)) for n in plan.nd]
+        S = max([plan.epochs * n for n in nbat] + [0])
+        idx, bsz, ep, nb = step_tables_native(plan.order, nd_dev, S, pg.B, zi, losses)
         if S > 0:
             offs = [s.offset for s in pg.layout.slots]
             pc = params if params.is_contiguous() else params.contiguous()
@@ -686,18 +703,20 @@ class ProgramRunner:
             from ..ops.transformer import client_chunks
 
             for a, b in client_chunks(C, self.cnn2_capacity(dev)):
-                ctr.zero_()
+                cc = zi[C:C + (b - a) * int(nat.cnn2_ctr_words())]  # (zeroed by the step-table launch)
+                if a > 0:  # (later chunks: counters left by the previous chunk's launch)
+                    cc.zero_()
                 whole = (a, b) == (0, C)
                 ti = idx if whole else idx[:, a:b].contiguous()
                 tb = bsz if whole else bsz[:, a:b].contiguous()
                 te = ep if whole else ep[:, a:b].contiguous()
                 nat.cnn2_train(pc[a:b], offs, table.rows, ti, tb, te, nb[a:b], ctl.seeds[a:b], pg.p(0.3), 2, True,
-                               float(lr), failed[a:b], losses[a:b], ws, ctr, self.cnn2_stamps if whole else None,
+                               float(lr), failed[a:b], losses[a:b], ws, cc, self.cnn2_stamps if whole else None,
                                int(opt_mode))
                 live.append((ti, tb, te))
             if pc is not params:
                 params.copy_(pc)
-            self._live = (ws, ctr, idx, bsz, ep, nb, ctl, params, pc, live)  # launches may still run (sync=False)
+            self._live = (ws, zi, idx, bsz, ep, nb, ctl, params, pc, live)  # launches may still run (sync=False)
         if not sync:
             return failed, losses  # failed: 1 = NaN loss, 2 = a cross-workgroup wait timed out (GraphTrainer raises)
         fh = failed.cpu()

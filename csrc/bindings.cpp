@@ -514,6 +514,41 @@ torch::Tensor hyper_features(torch::Tensor arena, std::vector<int64_t> clients, 
   return out;
 }
 
+// per-step batch tables (idx [S, C, B], bsz [S, C], ep [S, C], nb [C]) from a visit plan, plus zeroed per-round
+// words: zi int32 / zf fp32 tensors (any shape, contiguous) are zero-filled by the same launch (plan.hip)
+std::vector<torch::Tensor> step_tables(torch::Tensor order, torch::Tensor nd, int64_t B, int64_t S,
+                                       std::vector<torch::Tensor> zi, std::vector<torch::Tensor> zf) {
+  check_dev(order, "order", torch::kInt32);
+  check_dev(nd, "nd", torch::kInt32);
+  TORCH_CHECK(order.dim() == 3 && nd.numel() == order.size(0), "step_tables: order [C, E, maxnd], nd [C]");
+  TORCH_CHECK(B >= 1 && S >= 0, "step_tables: bad sizes");
+  TORCH_CHECK(zi.size() <= 1 && zf.size() <= 1, "step_tables: at most one int32 and one fp32 tensor to zero");
+  const int C = order.size(0), E = order.size(1), maxnd = order.size(2);
+  auto idx = torch::empty({S, C, B}, order.options());
+  auto bsz = torch::empty({S, C}, order.options());
+  auto ep = torch::empty({S, C}, order.options());
+  auto nb = torch::empty({C}, order.options());
+  int* zip = nullptr;
+  float* zfp = nullptr;
+  long nzi = 0, nzf = 0;
+  if (!zi.empty()) {
+    check_dev(zi[0], "zi", torch::kInt32);
+    zip = zi[0].data_ptr<int>();
+    nzi = zi[0].numel();
+  }
+  if (!zf.empty()) {
+    check_dev(zf[0], "zf", torch::kFloat32);
+    zfp = zf[0].data_ptr<float>();
+    nzf = zf[0].numel();
+  }
+  TORCH_CHECK(E >= 1 || S == 0, "step_tables: no epochs");
+  afl_step_tables(order.data_ptr<int>(), nd.data_ptr<int>(), C, std::max(E, 1), std::max(maxnd, 1), (int)B, (int)S,
+                  idx.data_ptr<int>(), bsz.data_ptr<int>(), ep.data_ptr<int>(), nb.data_ptr<int>(), zip, nzi, zfp, nzf,
+                  cur());
+  AFL_CHECK_LAUNCH();
+  return {idx, bsz, ep, nb};
+}
+
 // [C, E, maxnd] int32 visit plan from per-client 64-bit seeds (plan.hip); padding is 0
 torch::Tensor make_plan(torch::Tensor seeds, torch::Tensor nd, int64_t n_train, int64_t epochs, int64_t maxnd) {
   check_dev(seeds, "seeds", torch::kInt64);
@@ -733,6 +768,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hyper_adam_outer", &hyper_adam_outer);
   m.def("hyper_server_update", &hyper_server_update);
   m.def("make_plan", &make_plan);
+  m.def("step_tables", &step_tables);
   m.def("hyper_features", &hyper_features);
   m.def("hyper_small_capacity", &afl_hyper_small_capacity);
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),

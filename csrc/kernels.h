@@ -45,6 +45,8 @@ long afl_hyper_small_capacity();  // max floats of embedding-MLP parameters the 
 // plan.hip
 void afl_make_plan(const uint64_t* seeds, const int* nd, int C, int n_train, int E, int maxnd, int* order,
                    hipStream_t s);
+void afl_step_tables(const int* order, const int* nd, int C, int E, int maxnd, int B, int S, int* idx, int* bsz,
+                     int* ep, int* nb, int* zi, long nzi, float* zf, long nzf, hipStream_t s);
 
 // linalg.hip
 int afl_spectral_scratch(int r, int c);

@@ -254,12 +254,26 @@ __device__ __forceinline__ int colsum32(const float (&x)[8], int lane, float& su
   return (i & 8) == 0 ? 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3) : -1;
 }
 
+// ln p and ln(1 - p) of a sigmoid output for the BCE loss VALUE (reported per epoch, and its NaN test rides on the
+// head's hand-off); the gradient does not use them.  v_log_f32 (log2) instead of the correctly rounded logf / log1pf
+// expansions (dozens of instructions each on the head's critical path, and a spilled constant pair): ~1e-7
+// absolute error per row; ln(1 - p) loses relative precision only where p < 2^-24, i.e. a term below 6e-8
+__device__ __forceinline__ void bce_logs(float p, float& lg, float& lg1) {
+  constexpr float LN2 = 0.69314718055994531f;
+  lg = __builtin_amdgcn_logf(p) * LN2;
+  lg1 = __builtin_amdgcn_logf(1.f - p) * LN2;
+}
+
 __device__ __forceinline__ bool mbit(uint32_t m, int j) { return (m >> j) & 1u; }
 // x if bit j of m is set, else +0.0 (== bit ? x : 0.f bit for bit, NaN included): the bit becomes an
 // all-ones / zero word with ONE signed bitfield extract and masks x with one AND — two VALU instructions
 // instead of the test, compare and select
+// (the extracted mask goes through an empty asm: otherwise the backend turns the pair back into a bit test, a
+// compare and a v_cndmask — three instructions per element, measured in the tf2 forward's assembly)
 __device__ __forceinline__ float keepf(float x, uint32_t m, int j) {
-  return __uint_as_float(__float_as_uint(x) & (uint32_t)__builtin_amdgcn_sbfe((int)m, j, 1));
+  int s = __builtin_amdgcn_sbfe((int)m, j, 1);
+  asm("" : "+v"(s));
+  return __uint_as_float(__float_as_uint(x) & (uint32_t)s);
 }
 
 // ------------------------------------------------------------------------ packed-FP32 row math
@@ -657,6 +671,27 @@ __device__ __forceinline__ void sb() { __builtin_amdgcn_sched_barrier(0); }
 
 // barrier over LDS only (global loads stay in flight, stores are not drained)
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Intra-workgroup progress counters (monotone LDS words): a wave signals once its LDS stores AND reads before the
+// signal have completed (so a waiter may overwrite what the signaller read); a waiter spins until the count
+// reaches its target, then issues its LDS accesses (ordered after the count's read).  Lets the waves that are
+// ahead start work that depends on every wave's progress without a full barrier.
+__device__ __forceinline__ void lds_signal(uchar* smem, int off, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add((LDS_AS uint32_t*)(smem + off), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (bounded like the cross-workgroup hand-offs: false after XWG_MAX_SPINS, which the caller treats as a failed client
+// — only a wave that never signals, i.e. a bug or a dead hand-off partner, gets there)
+__device__ __forceinline__ bool lds_wait(const uchar* smem, int off, uint32_t target) {
+  for (long spins = 0;; ++spins) {
+    const uint32_t v = __builtin_amdgcn_readfirstlane(*(volatile const LDS_AS uint32_t*)(smem + off));
+    if (v >= target) break;
+    if (spins > fk::XWG_MAX_SPINS) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
 
 // --------------------------------------------------------------------------- batch walk (shared plan)
 struct Walk {

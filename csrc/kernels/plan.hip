@@ -9,6 +9,7 @@
 // No sort, no host work: one launch builds the whole [C, E, maxnd] plan.  The integer math is
 // mirrored bit-for-bit by attackfl_amd/fl/trainers.py:_feistel_plan (CPU branch); the helpers are
 // __host__ __device__ so csrc/host/host_check.hip can run them under ASan/UBSan on the CPU.
+#include <algorithm>
 #include "common.h"
 #include "kernels.h"
 
@@ -79,7 +80,46 @@ __global__ void __launch_bounds__(256) k_make_plan(const uint64_t* __restrict__ 
   out[i] = (int)pl_perm(j, (uint32_t)n_train, pl_half_bits((uint32_t)n_train), k.s0, k.s1);
 }
 
+// Per-step batch tables of a round (the layer-program and cnn2 trainers' step indexing, reference client.py:75-111:
+// client c's s-th step is its s-th batch in (epoch, batch) order): idx [S, C, B] train-row index or -1,
+// bsz [S, C] rows in the batch (0 past the client's last batch), ep [S, C] its epoch, nb [C] batches per epoch
+// (the loss divisor).  The same launch zeroes the trainer's per-round words (zi [nzi] int32, zf [nzf] fp32), so
+// the round boundary between two training launches is this one kernel instead of ~40 small tensor ops.
+__global__ void __launch_bounds__(256) k_step_tables(const int* __restrict__ order, const int* __restrict__ nd, int C,
+                                                     int E, int maxnd, int B, int S, int* __restrict__ idx,
+                                                     int* __restrict__ bsz, int* __restrict__ ep, int* __restrict__ nb,
+                                                     int* __restrict__ zi, long nzi, float* __restrict__ zf, long nzf) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < (long)S * C * B) {
+    const int b = (int)(i % B);
+    const long sc = i / B;
+    const int c = (int)(sc % C), s = (int)(sc / C);
+    const int n = nd[c];
+    const int nbc = max(1, (n + B - 1) / B);
+    const bool valid = s < nbc * E;
+    const int e = s / nbc, j = s - e * nbc;
+    const int pos = j * B + b;
+    const bool ok = valid && pos < n;
+    idx[i] = ok ? order[((long)c * E + min(e, E - 1)) * maxnd + min(pos, maxnd - 1)] : -1;
+    if (b == 0) {
+      bsz[sc] = valid ? min(max(n - j * B, 0), B) : 0;
+      ep[sc] = valid ? e : 0;
+    }
+  }
+  if (i < C) nb[i] = max(1, (nd[i] + B - 1) / B);
+  if (i < nzi) zi[i] = 0;
+  if (i < nzf) zf[i] = 0.f;
+}
+
 }  // namespace
+
+void afl_step_tables(const int* order, const int* nd, int C, int E, int maxnd, int B, int S, int* idx, int* bsz,
+                     int* ep, int* nb, int* zi, long nzi, float* zf, long nzf, hipStream_t s) {
+  const long n = std::max(std::max((long)S * C * B, (long)C), std::max(nzi, nzf));
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_step_tables, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, order, nd, C, E, maxnd, B, S,
+                     idx, bsz, ep, nb, zi, nzi, zf, nzf);
+}
 
 void afl_make_plan(const uint64_t* seeds, const int* nd, int C, int n_train, int E, int maxnd, int* order,
                    hipStream_t s) {

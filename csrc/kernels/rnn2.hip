@@ -951,7 +951,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
       const float p = __builtin_amdgcn_rcpf(1.f + __expf(-y3));
       if (valid) {
-        const float lg = logf(p), lg1 = log1pf(-p);
+        float lg, lg1;
+        bce_logs(p, lg, lg1);
         const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
         lrow = -(lab * lp + (1.f - lab) * l1p);
         const float pq = p * (1.f - p);

@@ -77,7 +77,10 @@ constexpr int B_NLN = 6 * 64;
 constexpr int B_DBL = B_CS;                        // fp64 [384]: G1 B1 G2 B2 G3 B3
 constexpr int B_DBL_BYTES = B_NLN * 8;
 static_assert(B_DBL_BYTES >= B_NVEC * 4, "DBL covers CS");
-constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words
+constexpr int B_MISC = B_DBL + B_DBL_BYTES;        // u32 [8] per-wave abort words, then the progress counters
+constexpr int B_CNT_A = B_MISC + 32;               // u32: waves past their out_proj backward (DO / DV stored, Wo read)
+constexpr int B_CNT_B = B_MISC + 36;               // u32: waves past their whole backward (DZ0 stored, Wv read)
+constexpr int B_CNT_C = B_MISC + 40;               // u32: waves past their ffn backward (DF3 / DF0 stored)
 constexpr int B_TOTAL = B_MISC + 64;
 // vector segments (x64 floats) of VEC / CS
 enum { VS_DB = 0, VS_VB, VS_OB, VS_G1, VS_B1, VS_F2B, VS_G2, VS_B2, VS_G3, VS_B3 };
@@ -118,13 +121,20 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 
 // ------------------------------------------------------------------- per-client workspace (bytes)
 // (the hand-off payloads travel as tagged granules in the per-call zeroed sync block: onchip.h gr_put / gr_get)
-// Adam moments of the register-resident weights: per-workgroup slab [slot][thread] of float4 (MOM_SLOTS
-// slots: m and v of the 4 block tiles, then the remaining moments), loaded in one batch of sc1 loads
-// ahead of each update phase and stored back after it (see "Adam" below)
+// Head: Adam moments of its register-resident weights, slab [slot][thread] of float4 (MOM_SLOTS slots: m and v
+// of the 4 fc1 tiles, then the remaining moments), loaded in one batch of sc1 loads ahead of the update phase and
+// stored back after it.
+// Branch: the compact entries' moments (CMP_SLOTS slots [slot][thread]), then the v / out_proj block UNITS: unit
+// 2 w + u (u = 0 out_proj, 1 in_proj.v) is the 2 x 2 tile block (Ta, Tb) of wave w's index w4 = w & 3, stored as
+// [unit][12][lane] float4 = m of its 4 tiles, v, then the fp32 master weights p — in memory, not registers, so
+// whichever wave is free may update a block (see br_update).
 constexpr int MOM_SLOTS = 11;
 constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
-constexpr long WS_BYTES = WS_MOM + 5 * MOM_WG_BYTES;  // head, 2 branches x (1 or 2 halves)
+constexpr int CMP_SLOTS = 3;
+constexpr long BR_UNITS = (long)CMP_SLOTS * NTH * 16;
+constexpr long BR_WG_BYTES = BR_UNITS + 8L * 12 * 64 * 16;
+constexpr long WS_BYTES = WS_MOM + MOM_WG_BYTES + 2 * BR_WG_BYTES;  // head, vitals branch, labs branch
 
 // branch LayerNorm column sums -> fp64 accumulator k of DBL (order G1 B1 G2 B2 G3 B3)
 __device__ __forceinline__ void ln_colsum(uchar* smem, int k, const float (&x)[16], int lane) {
@@ -250,14 +260,13 @@ __device__ __forceinline__ void load16(float (&x)[16], const uint32_t (&d)[8]) {
   }
 }
 
-// Optimizer state of one branch lane (AGPR-resident, see ar/aw):
-//  * blk: its 4 tiles of a 2x2 block of the 64x64 v (waves 0-3) or out_proj (waves 4-7) weight gradient;
+// Optimizer state of one branch lane (AGPR-resident, see ar/aw; the v / out_proj blocks' weights and moments live
+// in the workspace units, see br_update):
 //  * cmp: up to NCMP "compact" entries: the bias / LayerNorm vectors (VEC index e < 648), then the real
 //    elements of the dense, ffn.0 and ffn.3 weights (padding-free: their gradient tiles are mostly padding,
 //    so they are staged through LDS and owned element-wise instead of tile-wise).  Entry e belongs to thread
 //    e % 512, slot e / 512.
 struct BrState {
-  TS blk[4];
   VS cmp[5];
   float dst[5];  // AGPR: where compact entry h's new value goes (cmp_dst), fixed for the round
 };
@@ -484,6 +493,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
     for (int i = 0; i < 4; ++i) df0[i] = acc[i] * sv.gk[i];
     st4<TK16>(smem + B_DF0, r, g, df0);
   }
+  lds_signal(smem, B_CNT_C, lane);  // DF3 / DF0 rows stored: the ffn weight tiles may be computed
   float dr1[16];
   sb();
   {  // ffn.0 backward (d x1n) + residual, LayerNorm 1 backward
@@ -524,6 +534,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DV, r, 4 * t + g, dv + 4 * t);
   }
+  lds_signal(smem, B_CNT_A, lane);  // DO / DV rows stored, out_proj image read: its block may be updated
   sb();
   {  // v backward: d h0 = d r1 + d v . Wv ; d z0 = d h0 * gelu'(z0)
     const s8v b0 = bfrag(dv, 0), b1 = bfrag(dv, 1);
@@ -539,6 +550,7 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
 #pragma unroll
     for (int t = 0; t < 4; ++t) st4<TK64>(smem + B_DZ0, r, 4 * t + g, dz + 4 * t);
   }
+  lds_signal(smem, B_CNT_B, lane);  // backward done: DZ0 rows stored, v image read, LayerNorm sums added
 }
 
 
@@ -592,112 +604,221 @@ __device__ __forceinline__ int cmp_img(int e) {
   return B_IMG_F2 + (i & 63) * LD32 + pcol(i >> 6) * 2;
 }
 
-// Weight gradients + Adam for one step (after the barrier that ends the backward).  Three parts:
-//  U1  small weight-gradient tiles (dense and ffn.0: waves 0-3, ffn.3: waves 4-7) in registers; barrier
-//      (their X operands XIN / F2 die, their space stages the gradients);
-//  U2  small-tile gradients -> compact staging; the 2x2 v / out_proj block of the wave -> Adam -> image;
-//      bias sums of the dY tiles -> CS; barrier;
-//  U3  every thread: Adam on its compact entries -> VEC / images.  Gradient vector CS reset.
-// Moments (WS_MOM slab `rm`): the block tiles' are loaded at the start of U1 (used in U2), the compact
-// entries' at the start of U2 (used in U3); each set is stored back right after its Adam step.
-template <int BR>
-__device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid,
-                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, f4v (&bm)[4], f4v (&bv)[4]) {
-  using B = BrK<BR>;
-  opq(lane, wave);
-  asm volatile("" : "+v"(tid));
-  using C = Cmp<BR>;
-  const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
-  const bool lo = wave < 4;
-  // ---- U1 (the block tiles' moments bm / bv were issued by the caller)
-  f4v as = Z4, af1 = Z4;
-  {
-    // waves 0-3: dense tile (k 0..15, n tile w4): X = xin, dY = dz0 ; waves 4-7: ffn.3 tile: X = f2, dY = d f3
-    const uchar* X = smem + (lo ? B_XIN : B_F2);
-    const uchar* DY = smem + (lo ? B_DZ0 : B_DF3);
-#pragma unroll 1
-    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
-      as = mma(tfrag<TK16>(X, 32 * s, 0, lane), tfrag<TK64>(DY, 32 * s, w4, lane), as);
-      // ffn.0 (k tile w4, all 128 rows) on waves 0-3 alone: no cross-wave partial sum, one barrier less
-      if (lo) af1 = mma(tfrag<TK64>(smem + B_X1N, 32 * s, w4, lane), tfrag<TK16>(smem + B_DF0, 32 * s, 0, lane), af1);
-    }
-  }
-  // LayerNorm gradient sums out of the fp64 accumulators (DBL aliases CS: written back after the barrier)
-  const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
-  lds_bar();
-  stp(5, tid);
-  if (tid < B_NLN) ldsf(smem, B_CS)[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
-  const f4v cm = mom_ld(rm, 8, tid), cv = mom_ld(rm, 9, tid), cmv = mom_ld(rm, 10, tid);
-  // ---- U2: stage the small gradients (dW^T tile element (k = 16T + 4g + i, n = 16Tn + i16))
-  {
-    LDS_AS float* gs = ldsf(smem, B_GS);
-    const int n = 16 * w4 + i16;
+// ------------------------------------------------------------------------------ branch weight update
+// Block units (workspace, see WS layout): wave index w4 = w & 3 names the 2 x 2 tile block (Ta = 2 (w4 & 1),
+// Tb = 2 (w4 >> 1)) of the 64 x 64 out_proj (u = 0) or in_proj.v (u = 1) weight gradient; lane holds 4 elements
+// per tile, tile t = 2a + b = (Ta + a, Tb + b): slots j = t (m), 4 + t (v), 8 + t (fp32 weight p).
+__device__ __forceinline__ f4v unit_ld(__amdgpu_buffer_rsrc_t rm, int ui, int j, int lane) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rm, (int)BR_UNITS + ((ui * 12 + j) * 64 + lane) * 16,
+                                                                        0, 16));
+}
+__device__ __forceinline__ void unit_st(__amdgpu_buffer_rsrc_t rm, int ui, int j, int lane, f4v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rm, (int)BR_UNITS + ((ui * 12 + j) * 64 + lane) * 16,
+                                         0, 0);
+  store_guard();
+}
+// Adam on the 16 elements of a unit (p, m, v in U, gradients acc[a][b] of tile 2a + b), in explicit stages so the
+// 16 independent sqrt -> rcp -> fma chains overlap
+__device__ __forceinline__ void unit_adam(f4v (&U)[12], const f4v (&acc)[2][2], const AdamK& K) {
+  float p[16], mm[16], vv[16], g[16], den[16];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int k = 4 * g + i;
-      if (lo) {
-        if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as[i];
-      } else {
-        if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = as[i];
-      }
+      mm[4 * t + i] = U[t][i];
+      vv[4 * t + i] = U[4 + t][i];
+      p[4 * t + i] = U[8 + t][i];
+      g[4 * t + i] = acc[t >> 1][t & 1][i];
     }
-    // ffn.0 partial sums of the two row halves: wave w4 writes, wave w4 + 4 adds after the next barrier
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float mk = mm[e] * K.keep;
+    mm[e] = mk + K.c1 * (g[e] - mk);
+    vv[e] = fk::B2 * vv[e] + (1.f - fk::B2) * g[e] * g[e];
   }
-  {  // 2x2 block of v (waves 0-3: X = h0, dY = dv) or out_proj (waves 4-7: X = a, dY = do), bias sums
-    const uchar* X = smem + (lo ? B_H0 : B_A);
-    const uchar* DY = smem + (lo ? B_DV : B_DO);
-    const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
-    f4v acc[2][2] = {{Z4, Z4}, {Z4, Z4}};
-    f4v bs[2] = {Z4, Z4};
-    const bool do_bias = (w4 & 1) == 0;  // one of the two waves that read dY tiles Tb, Tb + 1
+#pragma unroll
+  for (int e = 0; e < 16; ++e) den[e] = __builtin_amdgcn_sqrtf(vv[e]);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) den[e] = __builtin_amdgcn_rcpf(den[e] * K.rsqrt_bc2 + K.eps);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) p[e] -= K.lr_bc1 * mm[e] * den[e];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      U[t][i] = mm[4 * t + i];
+      U[4 + t][i] = vv[4 * t + i];
+      U[8 + t][i] = p[4 * t + i];
+    }
+}
+// the unit's new bf16 weights into its image (rows n = 16 (Tb + b) + i16, permuted k chunk of tile Ta + a)
+__device__ __forceinline__ void unit_img(uchar* smem, const Mat& M, int Ta, int Tb, int lane, const u32x2v (&w)[4]) {
+  const int i16 = lane & 15, g4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    *(LDS_AS u32x2v*)(smem + M.img + (16 * (Tb + (t & 1)) + i16) * M.ld + pcol(16 * (Ta + (t >> 1)) + g4) * 2) = w[t];
+}
+__device__ __forceinline__ void unit_pack(const f4v (&U)[12], u32x2v (&w)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) w[t] = u32x2v{pk2(U[8 + t][0], U[8 + t][1]), pk2(U[8 + t][2], U[8 + t][3])};
+}
+// dW^T of a unit over all 128 rows: acc[a][b] = X tile Ta + a  x  dY tile Tb + b; bias column sums of dY tiles
+// Tb, Tb + 1 (the all-ones X fragment) when `bias`
+__device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta, int Tb, int lane, bool bias,
+                                        f4v (&acc)[2][2], f4v (&bs)[2]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = Z4;
+  bs[0] = bs[1] = Z4;
+  // (the all-ones operand from an opaque SGPR, materialised here: hoisted out of the step loop it is spilled)
+  uint32_t o1 = 0x3F803F80u;
+  asm volatile("" : "+s"(o1));
+  const s8v one = __builtin_bit_cast(s8v, u32x4{o1, o1, o1, o1});
 #pragma unroll 1
-    for (int s = 0; s < (ABL(K, ABL_UDW) ? 0 : 4); ++s) {
-      const s8v x0 = tfrag<TK64>(X, 32 * s, Ta, lane), x1 = tfrag<TK64>(X, 32 * s, Ta + 1, lane);
-      const s8v y0 = tfrag<TK64>(DY, 32 * s, Tb, lane), y1 = tfrag<TK64>(DY, 32 * s, Tb + 1, lane);
-      acc[0][0] = mma(x0, y0, acc[0][0]);
-      acc[0][1] = mma(x0, y1, acc[0][1]);
-      acc[1][0] = mma(x1, y0, acc[1][0]);
-      acc[1][1] = mma(x1, y1, acc[1][1]);
-      if (do_bias) {
-        bs[0] = mma(ones8(), y0, bs[0]);
-        bs[1] = mma(ones8(), y1, bs[1]);
-      }
+  for (int s = 0; s < 4; ++s) {
+    const s8v x0 = tfrag<TK64>(X, 32 * s, Ta, lane), x1 = tfrag<TK64>(X, 32 * s, Ta + 1, lane);
+    const s8v y0 = tfrag<TK64>(DY, 32 * s, Tb, lane), y1 = tfrag<TK64>(DY, 32 * s, Tb + 1, lane);
+    acc[0][0] = mma(x0, y0, acc[0][0]);
+    acc[0][1] = mma(x0, y1, acc[0][1]);
+    acc[1][0] = mma(x1, y0, acc[1][0]);
+    acc[1][1] = mma(x1, y1, acc[1][1]);
+    if (bias) {
+      bs[0] = mma(one, y0, bs[0]);
+      bs[1] = mma(one, y1, bs[1]);
     }
-    const Mat M = B::vo(lo);
+  }
+}
+
+// Weight gradients + Adam for one step, started by each wave as soon as its own backward is done — no barrier
+// between the backward and the weight-gradient work.  The waves of a SIMD pair run the same chain and the arbiter
+// favours the older one, so waves 0-3 ("leaders") reach this point ~2.5 us before waves 4-7 ("laggards", the
+// step's critical path).  Each wave starts what its inputs allow, tracked by progress counters (every wave signals
+// them from its backward):
+//   leaders   counter C (every wave's ffn.3 / ffn.0 dY rows): the ffn.3 tile w4 and ffn.0 k tile w4 weight
+//             gradients and the ffn.3 / ffn.0 bias sums — work that used to follow the barrier, now done while
+//             the laggards are still in their backward; then counter A (every wave's out_proj dY rows, the
+//             out_proj image no longer read): their out_proj unit — dW over the 128 rows, Adam on the workspace
+//             copy (p, m, v), image, bias sums;
+//   laggards  counter B (the whole backward: dense dY rows, the v image no longer read): the dense tile w4 and
+//             its bias sums, then their in_proj.v unit.
+// The small tiles' gradients and the bias sums are held in registers until barrier 1; then the LayerNorm sums
+// (fixed-point accumulators DBL, aliasing CS), the bias sums and the small gradients (staging GS, aliasing the dead
+// XIN / F2 tiles) are stored; barrier 2; every thread runs Adam on its compact entries (U3).  The abort decision
+// (a NaN loss anywhere in the batch) is taken by every wave after counter A or B — every abort word is written
+// before its wave signals — before anything is updated.  Returns false on abort.
+// (Measured first: the leaders taking both units after counter A was 1 % slower — A is reached only ~0.2 us
+// before B, so the leaders' two units became the tail; profiles/ab_tf2_r6_update.log.)
+template <int BR>
+__device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid, int step,
+                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo) {
+  using B = BrK<BR>;
+  using C = Cmp<BR>;
+  opq(lane, wave);
+  asm volatile("" : "+v"(tid));
+  const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
+  const bool lead = wave < 4;
+  const uint32_t all = 8u * (uint32_t)step;
+  LDS_AS uint32_t* abort_w = ldsu(smem, B_MISC);
+  const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+  const bool do_bias = (w4 & 1) == 0;  // one of the two units that read dY tiles Tb, Tb + 1
+  f4v bsu[2];                          // the unit's bias sums (out_proj on leaders, v on laggards)
+  f4v as = Z4, bd = Z4;                // laggards: dense tile + bias sums
+  f4v a3 = Z4, af1 = Z4, b3 = Z4, b1 = Z4;  // leaders: ffn.3 / ffn.0 tiles + bias sums
+  const int ui = 2 * w4 + (lead ? 0 : 1);
+  f4v U[12];
 #pragma unroll
-    for (int b = 0; b < 2; ++b)  // the two k tiles of n tile Tb + b in one staged pass (64 x 64: tile-exact)
-      if (!ABL(K, ABL_UADAM))
-        tile_adam_pair(st.blk[b], st.blk[2 + b], bm[b], bv[b], bm[2 + b], bv[2 + b], M, Ta, Ta + 1, Tb + b, lane,
-                       acc[0][b], acc[1][b], K, smem);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      mom_st(rm, k, tid, bm[k]);
-      mom_st(rm, 4 + k, tid, bv[k]);
+  for (int j = 0; j < 12; ++j) U[j] = unit_ld(rm, ui, j, lane);
+  uint32_t o1 = 0x3F803F80u;  // (all-ones operand, opaque SGPR: see unit_dw)
+  asm volatile("" : "+s"(o1));
+  const s8v one = __builtin_bit_cast(s8v, u32x4{o1, o1, o1, o1});
+  if (lead) {
+    if (!lds_wait(smem, B_CNT_C, all)) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
     }
+#pragma unroll 1
+    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
+      const s8v y3 = tfrag<TK64>(smem + B_DF3, 32 * s, w4, lane), y1 = tfrag<TK16>(smem + B_DF0, 32 * s, 0, lane);
+      a3 = mma(tfrag<TK16>(smem + B_F2, 32 * s, 0, lane), y3, a3);
+      af1 = mma(tfrag<TK64>(smem + B_X1N, 32 * s, w4, lane), y1, af1);
+      b3 = mma(one, y3, b3);
+      if (wave == 0) b1 = mma(one, y1, b1);
+    }
+    if (!lds_wait(smem, B_CNT_A, all)) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  } else {
+    if (!lds_wait(smem, B_CNT_B, all)) {
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  {
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) any |= abort_w[i];
+    if (any) return false;
+  }
+  stp(4, tid);
+  if (!lead) {
+#pragma unroll 1
+    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
+      const s8v yd = tfrag<TK64>(smem + B_DZ0, 32 * s, w4, lane);
+      as = mma(tfrag<TK16>(smem + B_XIN, 32 * s, 0, lane), yd, as);
+      bd = mma(one, yd, bd);
+    }
+  }
+  {  // the unit: out_proj (leaders: X = a, dY = d o) or in_proj.v (laggards: X = h0, dY = d v)
+    f4v acc[2][2];
+    if (!ABL(K, ABL_UDW))
+      unit_dw(smem + (lead ? B_A : B_H0), smem + (lead ? B_DO : B_DV), Ta, Tb, lane, do_bias, acc, bsu);
+    if (!ABL(K, ABL_UADAM)) unit_adam(U, acc, K);
+    u32x2v w[4];
+    unit_pack(U, w);
+    unit_img(smem, B::vo(!lead), Ta, Tb, lane, w);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) unit_st(rm, ui, j, lane, U[j]);
+  }
+  if (lead && !lds_wait(smem, B_CNT_B, all)) {  // (the LayerNorm sums below are complete at B)
+    if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  // LayerNorm gradient sums out of the fp64 accumulators (complete: counter B; DBL aliases CS, written back below)
+  const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
+  const f4v cm = mom_ld(rm, 0, tid), cv = mom_ld(rm, 1, tid), cmv = mom_ld(rm, 2, tid);
+  stp(5, tid);
+  prio_hi();
+  lds_bar();
+  {
+    LDS_AS float* cs = ldsf(smem, B_CS);
+    if (tid < B_NLN) cs[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
+    LDS_AS float* gs = ldsf(smem, B_GS);  // small gradients -> compact staging (dW^T tile element (k = 16T + 4g + i,
+    const int n = 16 * w4 + i16;          // n = 16 Tn + i16))
     if (do_bias && g == 0) {
-      LDS_AS float* cs = ldsf(smem, B_CS) + (lo ? VS_VB : VS_OB) * 64;
-      cs[16 * Tb + i16] = bs[0][0];
-      cs[16 * (Tb + 1) + i16] = bs[1][0];
-    }
-  }
-  {  // dense / ffn.3 bias sums (dY tile w4 of dz0 / d f3), ffn.0 bias (d f0, 6 columns)
-    f4v bs = Z4, b1 = Z4;
-    const uchar* DY = smem + (lo ? B_DZ0 : B_DF3);
-#pragma unroll 1
-    for (int s = 0; s < 4; ++s) {
-      bs = mma(ones8(), tfrag<TK64>(DY, 32 * s, w4, lane), bs);
-      if (wave == 0) b1 = mma(ones8(), tfrag<TK16>(smem + B_DF0, 32 * s, 0, lane), b1);
-    }
-    if (g == 0) {
-      ldsf(smem, B_CS)[(lo ? VS_DB : VS_F2B) * 64 + 16 * w4 + i16] = bs[0];
-      if (wave == 0 && i16 < FF) ldsf(smem, B_CS)[VS_F1B + i16] = b1[0];
-    }
-  }
-  if (lo) {  // ffn.0 (k tile w4, n 0..5)
-    LDS_AS float* gs = ldsf(smem, B_GS);
-    if (i16 < FF)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
+      for (int b = 0; b < 2; ++b) cs[(lead ? VS_OB : VS_VB) * 64 + 16 * (Tb + b) + i16] = bsu[b][0];
+    }
+    if (lead) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * g + i;
+        if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = a3[i];
+        if (i16 < FF) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
+      }
+      if (g == 0) {
+        cs[VS_F2B * 64 + 16 * w4 + i16] = b3[0];
+        if (wave == 0 && i16 < FF) cs[VS_F1B + i16] = b1[0];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * g + i;
+        if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as[i];
+      }
+      if (g == 0) cs[VS_DB * 64 + 16 * w4 + i16] = bd[0];
+    }
   }
   lds_bar();
   stp(6, tid);
@@ -730,9 +851,10 @@ __device__ __forceinline__ void br_update(uchar* smem, BrState& st, const AdamK&
       *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn[h]);
     }
   }
-  mom_st(rm, 8, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
-  mom_st(rm, 9, tid, f4v{vv[0], vv[1], vv[2], vv[3]});
-  mom_st(rm, 10, tid, f4v{mm[4], vv[4], 0.f, 0.f});
+  mom_st(rm, 0, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
+  mom_st(rm, 1, tid, f4v{vv[0], vv[1], vv[2], vv[3]});
+  mom_st(rm, 2, tid, f4v{mm[4], vv[4], 0.f, 0.f});
+  return true;
 }
 
 // fresh Adam state (torch.optim.Adam is re-created every round, client.py:78): zero moment slab
@@ -742,16 +864,27 @@ __device__ __forceinline__ void mom_zero(__amdgpu_buffer_rsrc_t rm, int tid) {
 }
 
 template <int BR>
-__device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P, int lane, int wave, int tid) {
+__device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P, __amdgpu_buffer_rsrc_t rm, int lane,
+                                        int wave, int tid) {
   using B = BrK<BR>;
   using C = Cmp<BR>;
-  const int w4 = wave & 3;
-  const Mat M = B::vo(wave < 4);
-  const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int k = 0; k < CMP_SLOTS; ++k) mom_st(rm, k, tid, Z4);
+  {  // wave w: unit 2 (w & 3) + (w >> 2) (every unit once): p from the parameters -> workspace + bf16 image, m = v = 0
+    const int w4 = wave & 3, u = wave >> 2, Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+    const Mat M = B::vo(u == 1);
+    const int i16 = lane & 15, g4 = 4 * (lane >> 4);
 #pragma unroll
-    for (int b = 0; b < 2; ++b) tile_load(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, P, smem);
+    for (int t = 0; t < 4; ++t) {
+      const int n = 16 * (Tb + (t & 1)) + i16, k0 = 16 * (Ta + (t >> 1)) + g4;
+      const float* src = P + M.off + n * M.k_real + k0;  // (a client's parameter row is not 16-byte aligned)
+      const f4v p = {src[0], src[1], src[2], src[3]};
+      unit_st(rm, 2 * w4 + u, t, lane, Z4);
+      unit_st(rm, 2 * w4 + u, 4 + t, lane, Z4);
+      unit_st(rm, 2 * w4 + u, 8 + t, lane, p);
+      *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(p[0], p[1]), pk2(p[2], p[3])};
+    }
+  }
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
@@ -772,16 +905,25 @@ __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P
 }
 
 template <int BR>
-__device__ __forceinline__ void br_fini(const BrState& st, float* P, int lane, int wave, int tid) {
+__device__ __forceinline__ void br_fini(const BrState& st, float* P, __amdgpu_buffer_rsrc_t rm, int lane, int wave,
+                                        int tid) {
   using B = BrK<BR>;
   using C = Cmp<BR>;
-  const int w4 = wave & 3;
-  const Mat M = B::vo(wave < 4);
-  const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+  {  // the units' weights (stored by the waves that updated them: wait for every store before reading back)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int w4 = wave & 3, u = wave >> 2, Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
+    const Mat M = B::vo(u == 1);
+    const int i16 = lane & 15, g4 = 4 * (lane >> 4);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int t = 0; t < 4; ++t) {
+      const int n = 16 * (Tb + (t & 1)) + i16, k0 = 16 * (Ta + (t >> 1)) + g4;
+      const f4v p = unit_ld(rm, 2 * w4 + u, 8 + t, lane);
+      float* dst = P + M.off + n * M.k_real + k0;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) tile_store(st.blk[2 * a + b], M, Ta + a, Tb + b, lane, P);
+      for (int i = 0; i < 4; ++i) dst[i] = p[i];
+    }
+  }
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
@@ -834,9 +976,9 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
   for (int i = tid; i < SMEM / 4; i += NTH) ldsf(smem, 0)[i] = 0.f;
   __syncthreads();
   BrState st;
-  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM + (BR + 1) * MOM_WG_BYTES);  // this workgroup's moments
-  mom_zero(rm, tid);
-  br_init<BR>(smem, st, P, lane, wave, tid);
+  const __amdgpu_buffer_rsrc_t rm = rsrc(ws + WS_MOM + MOM_WG_BYTES + BR * BR_WG_BYTES);  // this workgroup's units
+  br_init<BR>(smem, st, P, rm, lane, wave, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the units' first loads come from other waves' stores)
   __syncthreads();
   Stamp stp;
   stamp_init(stp, a, smem);
@@ -888,14 +1030,16 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
     prio_hi();
     stp(2, tid);
-    if (fv == 0xFFFFFFFFu) {
+    if (fv == 0xFFFFFFFFu) {  // timed out: abort the step for every wave (they wait on this wave's progress)
+      if (lane == 0) abort_w[wave] = 1u;
+      lds_signal(smem, B_CNT_A, lane);
+      lds_signal(smem, B_CNT_B, lane);
       failed = true;
       break;
     }
     float dout[16];
     unpack16(du, dout);
     if (lane == 0) abort_w[wave] = fv & 1u;
-    f4v bm[4], bv[4];  // the U1 / U2 block tiles' Adam moments (issued before the backward: measured slower)
 #ifndef TF2_NO_BWD
     asm volatile(";MARK bwd");
     br_backward<BR>(smem, dout, sv, K, lane, wave);
@@ -903,33 +1047,25 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     stp(3, tid);
 #else
     for (int j = 0; j < 16; ++j) asm volatile("" :: "v"(dout[j]));
+    lds_signal(smem, B_CNT_A, lane);
+    lds_signal(smem, B_CNT_B, lane);
 #endif
-    lds_bar();
-    uint32_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) any |= abort_w[i];
-    if (any) {  // the head saw a NaN loss: the client's round fails, this step's update is not applied
+    asm volatile(";MARK upd");
+    // (false: the head saw a NaN loss somewhere in the batch — the client's round fails and this step's update is
+    // not applied — or a wave stopped making progress)
+    const bool upd_ok = br_update<BR>(smem, st, K, lane, wave, tid, step, rm, stp, sync + XF_TMO);
+    asm volatile(";MARK upd_end");
+    if (!upd_ok) {
       failed = true;
       break;
     }
-    stp(4, tid);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bm[k] = mom_ld(rm, k, tid);
-      bv[k] = mom_ld(rm, 4 + k, tid);
-    }
-#ifndef TF2_NO_UPD
-    asm volatile(";MARK upd");
-    br_update<BR>(smem, st, K, lane, wave, tid, rm, stp, bm, bv);
-    asm volatile(";MARK upd_end");
-#endif
     stp(7, tid);
     lds_bar();
     stp(8, tid);
   }
   (void)failed;
   stamp_fini(stp, a, smem, tid);
-  br_fini<BR>(st, P, lane, wave, tid);
+  br_fini<BR>(st, P, rm, lane, wave, tid);
 }
 
 // ================================================================================= head workgroup
@@ -1081,7 +1217,8 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       const float p = sigmoidf_(y3);
       if (valid) {
         // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
-        const float lg = logf(p), lg1 = log1pf(-p);
+        float lg, lg1;
+        bce_logs(p, lg, lg1);
         const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
         lrow = -(lab * lp + (1.f - lab) * l1p);
         const float pq = p * (1.f - p);

@@ -54,42 +54,50 @@ static_assert(NPARAM == 47693, "TransformerModel parameter count");
 // exp(-x^2/2) is shared with the Gaussian pdf of the GELU derivative — one rcp and one exp per value.
 // LN eps 1e-5, biased variance.
 // ---------------------------------------------------------------------------------------------
+// Instruction-lean form (the on-chip trainers are VALU-issue-bound and GELU is a fifth of a branch forward): the
+// 1/2 of Phi and the pdf normalisation are folded into the constants — pdf = 2^(x^2 (-log2(e) / 2) + log2(1/sqrt(2 pi)))
+// is ONE fma + exp2 of x^2, and erfc(|x|/sqrt2)/2 = t Q(t) pdf with Q = A&S's polynomial times sqrt(2 pi) / 2;
+// t = 1/(1 + (p/sqrt2)|x|) is one fma whose |x| is a source modifier.
 struct GeluPair {
   float cdf;  // Phi(x) = 0.5 (1 + erf(x / sqrt 2))
   float pdf;  // phi(x) = exp(-x^2 / 2) / sqrt(2 pi)
 };
 constexpr float AS_P = 0.3275911f, AS_A1 = 0.254829592f, AS_A2 = -0.284496736f, AS_A3 = 1.421413741f,
-                AS_A4 = -1.453152027f, AS_A5 = 1.061405429f, NLOG2E = -1.4426950408889634f;
+                AS_A4 = -1.453152027f, AS_A5 = 1.061405429f;
+constexpr float G_PZ = (float)(0.3275911 * 0.70710678118654752);         // p / sqrt 2
+constexpr float G_QK = 1.2533141373155003f;                                // sqrt(2 pi) / 2
+constexpr float G_Q1 = (float)(0.254829592 * 1.2533141373155003), G_Q2 = (float)(-0.284496736 * 1.2533141373155003),
+                G_Q3 = (float)(1.421413741 * 1.2533141373155003), G_Q4 = (float)(-1.453152027 * 1.2533141373155003),
+                G_Q5 = (float)(1.061405429 * 1.2533141373155003);
+constexpr float G_E2 = -0.72134752044448170f;    // -log2(e) / 2
+constexpr float G_EL = -1.3257480647361593f;     // log2(1 / sqrt(2 pi))
 __device__ __forceinline__ GeluPair gelu_parts(float x) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(AS_P, z, 1.f));
-  float p = fmaf(AS_A5, t, AS_A4);
-  p = fmaf(p, t, AS_A3);
-  p = fmaf(p, t, AS_A2);
-  p = fmaf(p, t, AS_A1);
-  const float e = __builtin_amdgcn_exp2f(z * z * NLOG2E);  // exp(-x^2/2)
-  const float half_erfc = 0.5f * (p * t) * e;            // erfc(|x|/sqrt2) / 2
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(x), G_PZ, 1.f));
   GeluPair g;
-  g.cdf = x >= 0.f ? 1.f - half_erfc : half_erfc;
-  g.pdf = 0.39894228040143268f * e;
+  g.pdf = __builtin_amdgcn_exp2f(fmaf(x * x, G_E2, G_EL));
+  float q = fmaf(G_Q5, t, G_Q4);
+  q = fmaf(q, t, G_Q3);
+  q = fmaf(q, t, G_Q2);
+  q = fmaf(q, t, G_Q1);
+  const float h = (q * t) * g.pdf;  // erfc(|x| / sqrt2) / 2
+  g.cdf = x >= 0.f ? 1.f - h : h;
   return g;
 }
 // two values at once in packed FP32 (v_pk_fma / v_pk_mul: two lanes' worth of math per instruction);
 // same formula as gelu_parts.  Returns gelu(x), sets gp = gelu'(x).
 typedef float gf2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ gf2v gelu2(gf2v x, gf2v& gp) {
-  const gf2v z = gf2v{fabsf(x[0]), fabsf(x[1])} * 0.70710678118654752f;
-  const gf2v u = z * AS_P + 1.f;
+  const gf2v u = {fmaf(fabsf(x[0]), G_PZ, 1.f), fmaf(fabsf(x[1]), G_PZ, 1.f)};
   const gf2v t = {__builtin_amdgcn_rcpf(u[0]), __builtin_amdgcn_rcpf(u[1])};
-  gf2v p = t * AS_A5 + AS_A4;
-  p = p * t + AS_A3;
-  p = p * t + AS_A2;
-  p = p * t + AS_A1;
-  const gf2v q = z * z * NLOG2E;
-  const gf2v e = {__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};
-  const gf2v h = (p * t) * (e * 0.5f);
+  const gf2v e2 = (x * x) * G_E2 + G_EL;
+  const gf2v pdf = {__builtin_amdgcn_exp2f(e2[0]), __builtin_amdgcn_exp2f(e2[1])};
+  gf2v q = t * G_Q5 + G_Q4;
+  q = q * t + G_Q3;
+  q = q * t + G_Q2;
+  q = q * t + G_Q1;
+  const gf2v h = (q * t) * pdf;
   const gf2v cdf = {x[0] >= 0.f ? 1.f - h[0] : h[0], x[1] >= 0.f ? 1.f - h[1] : h[1]};
-  gp = x * (e * 0.39894228040143268f) + cdf;
+  gp = x * pdf + cdf;
   return x * cdf;
 }
 __device__ __forceinline__ float gelu(float x) { return x * gelu_parts(x).cdf; }

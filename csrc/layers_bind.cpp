@@ -3,6 +3,7 @@
 // (attackfl_amd/fl/programs.py) preallocate their buffers once and capture the launch sequence in a
 // HIP graph.  Strided operands are passed as 3-D views [C][rows][cols]; their strides go to the
 // kernels unchanged (weights are views into the flat [C][P] parameter arena, transposes are free).
+#include <map>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -733,9 +734,19 @@ torch::Tensor cnn2_eval(torch::Tensor params, std::vector<int64_t> offs, torch::
   // the kernel reads these slots (conv biases, fc weights) as 16-byte vectors: 4-float aligned offsets, and a row
   // stride and base that keep them aligned for every model (an odd stride such as CNNModel's 203649 is padded)
   for (int k : {3, 5, 9, 11, 12, 14, 16}) TORCH_CHECK(off[k] % 4 == 0, "cnn2_eval: slot offset not 4-float aligned");
+  // One model with an aligned base needs no padding (the stride is never used).  Otherwise the rows are copied
+  // into a padded buffer cached per (device, stream) across calls (validation, prefetch and hyper evaluations of every
+  // client reuse it: no allocation or zero fill on the round boundary; the padding columns are never read).
   torch::Tensor p = params;
-  if (p.size(1) % 4 != 0 || (reinterpret_cast<uintptr_t>(p.data_ptr<float>()) & 15) != 0) {
-    p = torch::zeros({p.size(0), (p.size(1) + 3) / 4 * 4}, p.options());
+  const bool aligned = (reinterpret_cast<uintptr_t>(p.data_ptr<float>()) & 15) == 0;
+  if (!(aligned && (p.size(0) == 1 || p.size(1) % 4 == 0))) {
+    // keyed by stream: calls on one stream are ordered, so the buffer is free again when the next copy runs
+    static std::map<std::pair<int, hipStream_t>, torch::Tensor> cache;
+    const int64_t Pp = (p.size(1) + 3) / 4 * 4;
+    torch::Tensor& buf = cache[{(int)p.get_device(), cur()}];
+    if (!buf.defined() || buf.size(0) < p.size(0) || buf.size(1) != Pp)
+      buf = torch::empty({std::max<int64_t>(p.size(0), buf.defined() ? buf.size(0) : 0), Pp}, p.options());
+    p = buf.narrow(0, 0, params.size(0));
     p.narrow(1, 0, params.size(1)).copy_(params);
   }
   const int C = (int)p.size(0), n = (int)rows.size(0);

@@ -589,3 +589,25 @@ def test_har_encoder_adam_epochs_track_composite(gpu):
 
 
 HAR_ADAM_TOL = 0.4
+
+
+@pytest.mark.parametrize("nd,B,E", [([700, 513, 300, 129, 0, 1], 128, 3), ([5, 64, 65], 64, 2), ([0, 0], 32, 1)])
+def test_native_step_tables_match_tensor_ops(gpu, nd, B, E):
+    """plan.hip k_step_tables (the cnn2 round boundary in one launch) equals the tensor-op step tables, and zeroes
+    the per-round words it is given."""
+    import math
+
+    from attackfl_amd.fl.programs import step_tables, step_tables_native
+    from attackfl_amd.fl.trainers import make_plan
+
+    plan = make_plan(2000, [max(n, 1) for n in nd], E, torch.Generator().manual_seed(3), gpu)
+    plan = Plan(plan.order, torch.tensor(nd, dtype=torch.int32), E)
+    ref = step_tables(plan.order, plan.nd, E, B, gpu)
+    S = max([E * max(1, math.ceil(n / B)) for n in nd] + [0])
+    assert S == ref[4]
+    zi = torch.full((37,), 7, dtype=torch.int32, device=gpu)
+    zf = torch.full((5, 3), 2.5, device=gpu)
+    got = step_tables_native(plan.order, plan.nd.to(gpu), S, B, zi, zf)
+    for a, b in zip(got, ref[:4]):
+        assert torch.equal(a.cpu(), b.cpu())
+    assert int(zi.abs().sum()) == 0 and float(zf.abs().sum()) == 0.0

@@ -26,9 +26,10 @@ NAMES = {0: "F:G1 dense+E1", 1: "F:G2 vproj+E2", 2: "F:G3 oproj+E3 LN1", 3: "F:G
          16: "B:E13", 17: "B:(none)", 18: "B:G14+dWo", 19: "B:E14+dWv", 20: "B:E15+dWd",
          21: "X:publish+wait d(out)"}
 # on-chip trainer (split 4, tf2.hip): branch workgroups (blocks 3c+1, 3c+2) and the head (3c)
-NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:backward", 4: "B:barrier+abort",
-          5: "B:U1 small dW (+bar)", 6: "B:U2 v/o dW+Adam, biases (+bar)", 7: "B:U3 compact Adam",
-          8: "B:end barrier", 10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss",
+NAMES4 = {0: "B:forward", 1: "B:publish+prefetch", 2: "B:wait d(out)", 3: "B:backward",
+          4: "B:wait counter (A leaders / B laggards)+abort",
+          5: "B:leaders out_proj+v units / laggards small tiles", 6: "B:bar 1 + sums, staging + bar 2",
+          7: "B:U3 compact Adam", 8: "B:end barrier", 10: "H:wait branches", 11: "H:fwd+loss+bwd+publish", 12: "H:bar+loss",
           13: "H:dW+Adam", 14: "H:end barrier"}
 
 def block_stride(clients: int, wgs: int, dev) -> int:
