@@ -699,9 +699,9 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
 //             gradients and the ffn.3 / ffn.0 bias sums — work that used to follow the barrier, now done while
 //             the laggards are still in their backward; then counter A (every wave's out_proj dY rows, the
 //             out_proj image no longer read): their out_proj unit — dW over the 128 rows, Adam on the workspace
-//             copy (p, m, v), image, bias sums;
-//   laggards  counter B (the whole backward: dense dY rows, the v image no longer read): the dense tile w4 and
-//             its bias sums, then their in_proj.v unit.
+//             copy (p, m, v), image, bias sums; then counter B (every wave's dense dY rows): the dense tile w4
+//             and its bias sums;
+//   laggards  counter B (the whole backward: the v image no longer read): their in_proj.v unit.
 // The small tiles' gradients and the bias sums are held in registers until barrier 1; then the LayerNorm sums
 // (fixed-point accumulators DBL, aliasing CS), the bias sums and the small gradients (staging GS, aliasing the dead
 // XIN / F2 tiles) are stored; barrier 2; every thread runs Adam on its compact entries (U3).  The abort decision
@@ -711,7 +711,8 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
 // before B, so the leaders' two units became the tail; profiles/ab_tf2_r6_update.log.)
 template <int BR>
 __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid, int step,
-                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo) {
+                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo, uint32_t seed, float& mka0,
+                                          float& mka1) {
   using B = BrK<BR>;
   using C = Cmp<BR>;
   opq(lane, wave);
@@ -723,8 +724,7 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
   const int Ta = 2 * (w4 & 1), Tb = 2 * (w4 >> 1);
   const bool do_bias = (w4 & 1) == 0;  // one of the two units that read dY tiles Tb, Tb + 1
   f4v bsu[2];                          // the unit's bias sums (out_proj on leaders, v on laggards)
-  f4v as = Z4, bd = Z4;                // laggards: dense tile + bias sums
-  f4v a3 = Z4, af1 = Z4, b3 = Z4, b1 = Z4;  // leaders: ffn.3 / ffn.0 tiles + bias sums
+  f4v as = Z4, bd = Z4, a3 = Z4, af1 = Z4, b3 = Z4, b1 = Z4;  // leaders: dense / ffn.3 / ffn.0 tiles + bias sums
   const int ui = 2 * w4 + (lead ? 0 : 1);
   f4v U[12];
 #pragma unroll
@@ -733,6 +733,13 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
   asm volatile("" : "+s"(o1));
   const s8v one = __builtin_bit_cast(s8v, u32x4{o1, o1, o1, o1});
   if (lead) {
+    // the leaders' ffn tiles run below the laggards' backward on the same SIMD (priority 0: +1.9 % against 2,
+    // +1.7 % at 1; profiles/ab_tf2_r6_update.log), the out_proj unit after A at the critical priority again
+#ifndef TF2_LEAD_PRIO
+    prio_lo();
+#else  // A/B variant
+    __builtin_amdgcn_s_setprio(TF2_LEAD_PRIO);
+#endif
     if (!lds_wait(smem, B_CNT_C, all)) {
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
@@ -749,6 +756,7 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
+    prio_hi();
   } else {
     if (!lds_wait(smem, B_CNT_B, all)) {
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -762,14 +770,6 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
     if (any) return false;
   }
   stp(4, tid);
-  if (!lead) {
-#pragma unroll 1
-    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
-      const s8v yd = tfrag<TK64>(smem + B_DZ0, 32 * s, w4, lane);
-      as = mma(tfrag<TK16>(smem + B_XIN, 32 * s, 0, lane), yd, as);
-      bd = mma(one, yd, bd);
-    }
-  }
   {  // the unit: out_proj (leaders: X = a, dY = d o) or in_proj.v (laggards: X = h0, dY = d v)
     f4v acc[2][2];
     if (!ABL(K, ABL_UDW))
@@ -781,10 +781,27 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
 #pragma unroll
     for (int j = 0; j < 12; ++j) unit_st(rm, ui, j, lane, U[j]);
   }
-  if (lead && !lds_wait(smem, B_CNT_B, all)) {  // (the LayerNorm sums below are complete at B)
-    if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
+  if (lead) {
+    if (!lds_wait(smem, B_CNT_B, all)) {  // (the dense dY rows and the LayerNorm sums below are complete at B)
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+#pragma unroll 1
+    for (int s = 0; s < (ABL(K, ABL_U1) ? 0 : 4); ++s) {
+      const s8v yd = tfrag<TK64>(smem + B_DZ0, 32 * s, w4, lane);
+      as = mma(tfrag<TK16>(smem + B_XIN, 32 * s, 0, lane), yd, as);
+      bd = mma(one, yd, bd);
+    }
+#ifdef TF2_LEAD_LATE_MASKS
+    {  // the next step's dropout masks: the leaders' slack before barrier 1 (beside the laggards' MFMA-bound unit)
+      uint32_t m0, m1;
+      br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), 16 * wave + (lane & 15), g, m0, m1);
+      mka0 = awu(m0);
+      mka1 = awu(m1);
+    }
+#endif
   }
+  (void)seed; (void)mka0; (void)mka1;
   // LayerNorm gradient sums out of the fp64 accumulators (complete: counter B; DBL aliases CS, written back below)
   const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
   const f4v cm = mom_ld(rm, 0, tid), cv = mom_ld(rm, 1, tid), cmv = mom_ld(rm, 2, tid);
@@ -807,17 +824,16 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
         if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = a3[i];
         if (i16 < FF) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
       }
-      if (g == 0) {
-        cs[VS_F2B * 64 + 16 * w4 + i16] = b3[0];
-        if (wave == 0 && i16 < FF) cs[VS_F1B + i16] = b1[0];
-      }
-    } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int k = 4 * g + i;
         if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as[i];
       }
-      if (g == 0) cs[VS_DB * 64 + 16 * w4 + i16] = bd[0];
+      if (g == 0) {
+        cs[VS_F2B * 64 + 16 * w4 + i16] = b3[0];
+        cs[VS_DB * 64 + 16 * w4 + i16] = bd[0];
+        if (wave == 0 && i16 < FF) cs[VS_F1B + i16] = b1[0];
+      }
     }
   }
   lds_bar();
@@ -1018,6 +1034,9 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
+#ifdef TF2_LEAD_LATE_MASKS
+    if (wave >= 4)  // (leaders hash theirs before barrier 1 of the update, see br_update)
+#endif
     {  // the next step's dropout masks, while the head works (this wave would only spin)
       uint32_t m0, m1;
       br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), 16 * wave + (lane & 15), g, m0, m1);
@@ -1028,7 +1047,12 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     u32x4 du[2];
     const int go[1] = {gr_off(1, BR, wave, lane)};
     const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
+#ifdef TF2_BWD_PRIO_SPLIT  // A/B variant: the leaders' backward (started first) below the laggards' on the same SIMD
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
+    else prio_hi();
+#else
     prio_hi();
+#endif
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) {  // timed out: abort the step for every wave (they wait on this wave's progress)
       if (lane == 0) abort_w[wave] = 1u;
@@ -1053,7 +1077,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     asm volatile(";MARK upd");
     // (false: the head saw a NaN loss somewhere in the batch — the client's round fails and this step's update is
     // not applied — or a wave stopped making progress)
-    const bool upd_ok = br_update<BR>(smem, st, K, lane, wave, tid, step, rm, stp, sync + XF_TMO);
+    const bool upd_ok = br_update<BR>(smem, st, K, lane, wave, tid, step, rm, stp, sync + XF_TMO, seed, mka0, mka1);
     asm volatile(";MARK upd_end");
     if (!upd_ok) {
       failed = true;
@@ -1153,7 +1177,12 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       timed_out = failed = true;
       break;
     }
+#ifdef TF2_HEAD_PRIO_SPLIT  // A/B variant: head waves 0-3 (their rows arrive first) below waves 4-7
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
+    else prio_hi();
+#else
     prio_hi();
+#endif
     stp(10, tid);
     // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
     // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
