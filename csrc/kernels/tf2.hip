@@ -5,9 +5,10 @@
 //
 // What differs from transformer.hip: after the prologue NOTHING of a client's model lives in global
 // memory.  Per workgroup:
-//   * fp32 master weights and both Adam moments stay in REGISTERS for the whole round: every lane owns
-//     the elements of the weight-gradient tiles it computes (4 per 16x16 tile, <= 6 tiles per lane) and
-//     one or two bias / LayerNorm entries; the optimizer never touches memory;
+//   * the head's fp32 master weights and the branches' compact entries (biases, LayerNorm, the small dense /
+//     ffn weights) stay in REGISTERS (AGPRs) for the whole round; their Adam moments, and the branches'
+//     64 x 64 v / out_proj blocks (weights AND moments), sit in a per-workgroup workspace slab that each
+//     update phase loads ahead of its arithmetic (L2-resident; see br_update for why the blocks moved there);
 //   * bf16 weight images (the MFMA operands) and an fp32 copy of the bias / LayerNorm vectors live in
 //     LDS; Adam rewrites them in place;
 //   * activations chain in registers: every GEMM is computed transposed, Y^T = W . X^T, so the
@@ -16,8 +17,10 @@
 //     the matching permuted order (pcol below).  The forward and the d(input) backward of a wave never
 //     leave its registers and need no barrier; LayerNorm row sums are in-lane + two permlane swaps;
 //   * the activations the weight gradients need (X and dY of every dW = dY^T X) are written to
-//     XOR-swizzled LDS tiles as they are produced and read back with ds_read_b64_tr_b16 in ONE dW phase
-//     per step (the only two workgroup barriers of a step bracket it);
+//     XOR-swizzled LDS tiles as they are produced and read back with ds_read_b64_tr_b16; each wave starts
+//     the weight-gradient work its inputs allow as soon as its own backward is done, tracked by LDS progress
+//     counters instead of a barrier (br_update), so the waves that finish the backward first work while the
+//     rest are still in theirs;
 //   * the only global traffic in the step loop is the next batch's input rows (prefetched during the
 //     hand-off wait) and the hand-offs themselves: per wave 2 KB of bf16 rows as {value, step tag}
 //     granules in 16-byte write-through (sc1) stores, swept with sc1 loads until every tag matches — the
@@ -106,7 +109,7 @@ constexpr int H_DZ2 = H_DZ1 + 16384;               // tile32:  d(fc2 pre-activat
 constexpr int H_NVEC = 132;                        // fc1.b 64 | fc2.b 32 | output.w 32 | output.b 1
 constexpr int H_VEC = H_DZ2 + 8192;
 constexpr int H_PART = H_VEC + H_NVEC * 4;         // fp32 [8 waves][132] per-wave column sums (their gradients)
-constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss partials
+constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss partials, then u32 [8] their abort flags
 constexpr int H_TOTAL = H_LOSS + 64;
 enum { HV_B1 = 0, HV_B2 = 64, HV_WO = 96, HV_BO = 128 };
 
@@ -1166,6 +1169,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const uint32_t key = afl_hash32(seed, (uint32_t)step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
+    const float inv_bn = 1.f / (float)Bn;  // (before the wait: the division is off the critical path)
     // fc1 dropout mask before the wait (the wave would only spin there)
     const uint32_t mh = mask16(key, L_HEAD, r, g, THR_P03);
     sb();
@@ -1215,7 +1219,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     }
     // ---- fc2 + GELU, output layer, sigmoid, BCE (log clamped at -100)
     float dz2[8], gw[8];
-    float lrow = 0.f, dy3 = 0.f;
+    float dy3 = 0.f, pl = 0.f;
     {
       const s8v b0 = bfrag(a1, 0), b1 = bfrag(a1, 1);
       f4v acc[2];
@@ -1245,24 +1249,22 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
       const float p = sigmoidf_(y3);
       if (valid) {
-        // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
-        float lg, lg1;
-        bce_logs(p, lg, lg1);
-        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
-        lrow = -(lab * lp + (1.f - lab) * l1p);
+        // torch's BCELoss gradient (p - y) / max(p (1 - p), 1e-12) times the sigmoid's p (1 - p), as one factor
+        // without a division (1 unless the sigmoid saturates; NaN propagates through the compare's false branch)
         const float pq = p * (1.f - p);
-        dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
+        dy3 = (p - lab) * (pq >= 1e-12f ? 1.f : pq * 1e12f) * inv_bn;
       }
+      pl = p;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         dz2[j] = dy3 * wo[j] * gp2[j];
         gw[j] = dy3 * g2[j];
       }
     }
-    // per-wave loss partial (each row counted once: lane group 0); its NaN test rides on the hand-off flag
-    float lsum = wave_sum(g == 0 ? lrow : 0.f);
-    if (lane == 0) lossw[wave] = lsum;
-    const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
+    // the NaN-loss abort rides on the hand-off tag: a row's loss is NaN exactly where its gradient factor dy3 is
+    // not finite (p or the label NaN; labels are 0 / 1), so the flag needs no loss on the critical path — the loss
+    // VALUE (logs, wave sum) is computed after the hand-off, and the head aborts on the same flags
+    const uint32_t wave_nan = __builtin_amdgcn_ballot_w64(!(fabsf(dy3) <= 3.402823466e38f)) != 0 ? 1u : 0u;
     // ---- d a1 = dz2 . W2 -> d z1 = d a1 * drop'(.) * gelu'(z1)
     float dz1[16];
     {
@@ -1294,6 +1296,21 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       }
     }
     prio_lo();
+    {  // per-wave loss partial (each row counted once: lane group 0) and the abort flag, for the loss barrier
+      float lrow = 0.f;
+      if (valid) {
+        // clamp like torch.clamp: NaN must propagate (fmaxf would swallow it)
+        float lg, lg1;
+        bce_logs(pl, lg, lg1);
+        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
+        lrow = -(lab * lp + (1.f - lab) * l1p);
+      }
+      const float lsum = wave_sum(g == 0 ? lrow : 0.f);
+      if (lane == 0) {
+        lossw[wave] = lsum;
+        lossw[8 + wave] = __uint_as_float(wave_nan);
+      }
+    }
     // ---- deferred: dW operand tiles and column sums of this wave's rows (read after the loss barrier)
     {
       sb();
@@ -1338,10 +1355,14 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     lds_bar();
     {
       float tot = 0.f;
+      uint32_t any = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) tot += lossw[i];
+      for (int i = 0; i < 8; ++i) {
+        tot += lossw[i];
+        any |= __float_as_uint(lossw[8 + i]);
+      }
       const float loss = tot / (float)Bn;
-      if (loss != loss) {  // uniform across the workgroup; the branches see the per-wave NaN flags
+      if (any) {  // a NaN loss (uniform across the workgroup; the branches abort on the same per-wave flags)
         failed = true;
         break;
       }
