@@ -97,7 +97,7 @@ constexpr int H_DZ2 = H_DZ1 + 8192;                // tile16:  d(fc2 pre-activat
 constexpr int H_NVEC = 68;                         // fc1.b 32 | fc2.b 16 | output.w 16 | output.b 1 (| pad)
 constexpr int H_VEC = H_DZ2 + 4096;
 constexpr int H_PART = H_VEC + H_NVEC * 4;         // fp32 [8 waves][68] per-wave column sums
-constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss partials
+constexpr int H_LOSS = H_PART + 8 * H_NVEC * 4;    // fp32 [8] per-wave loss partials, then u32 [8] abort flags
 constexpr int H_TOTAL = H_LOSS + 64;
 enum { HV_B1 = 0, HV_B2 = 32, HV_WO = 48, HV_BO = 64, HV_N = 65 };
 
@@ -905,6 +905,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     const AdamK K = adam_k(a, step);
     const int Bn = min(BS, nd - w.b0);
     const bool valid = r < Bn;
+    const float inv_bn = 1.f / (float)Bn;  // (before the wait: the division is off the critical path)
     sb();
     u32x4 cv[4];  // vitals rows (cv[0..1]) | labs rows (cv[2..3])
     const int go[2] = {gr_off(0, 0, wave, lane), gr_off(0, 1, wave, lane)};
@@ -938,7 +939,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     }
     // ---- fc2 + ReLU, output layer, sigmoid, BCE (log clamped at -100)
     float dz2[4], gw[4], f2[4];
-    float lrow = 0.f, dy3 = 0.f;
+    float dy3 = 0.f, pl = 0.f;
     {
       const f4v acc = mma(wfrag(smem + H_IMG_W2, HLD2, 0, 0, lane), bfrag(a1, 0), Z4);
       const f4v b2 = *(const LDS_AS f4v*)(vec + (HV_B2 + 4 * g) * 4), wo = *(const LDS_AS f4v*)(vec + (HV_WO + 4 * g) * 4);
@@ -950,23 +951,20 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       }
       const float y3 = fk::rsum4(dot) + *(const LDS_AS float*)(vec + HV_BO * 4);
       const float p = __builtin_amdgcn_rcpf(1.f + __expf(-y3));
-      if (valid) {
-        float lg, lg1;
-        bce_logs(p, lg, lg1);
-        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
-        lrow = -(lab * lp + (1.f - lab) * l1p);
+      if (valid) {  // (torch's BCE gradient times the sigmoid's, without a division: tf2.hip head)
         const float pq = p * (1.f - p);
-        dy3 = (p - lab) * (pq / fmaxf(pq, 1e-12f)) / (float)Bn;
+        dy3 = (p - lab) * (pq >= 1e-12f ? 1.f : pq * 1e12f) * inv_bn;
       }
+      pl = p;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         dz2[i] = f2[i] > 0.f ? dy3 * wo[i] : 0.f;
         gw[i] = dy3 * f2[i];
       }
     }
-    const float lsum = wave_sum(g == 0 ? lrow : 0.f);
-    if (lane == 0) lossw[wave] = lsum;
-    const uint32_t wave_nan = __builtin_amdgcn_readfirstlane(lsum != lsum ? 1u : 0u);
+    // NaN-loss abort flag from the gradient factor (NaN loss <=> non-finite dy3 for 0 / 1 labels, tf2.hip head);
+    // the loss value is computed after the hand-off
+    const uint32_t wave_nan = __builtin_amdgcn_ballot_w64(!(fabsf(dy3) <= 3.402823466e38f)) != 0 ? 1u : 0u;
     // ---- d a1 = dz2 . W2 -> d z1
     float dz1[8];
     {
@@ -996,6 +994,20 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       }
     }
     prio_lo();
+    {  // per-wave loss partial (lane group 0: each row once) and the abort flag, for the loss barrier
+      float lrow = 0.f;
+      if (valid) {
+        float lg, lg1;
+        bce_logs(pl, lg, lg1);
+        const float lp = lg < -100.f ? -100.f : lg, l1p = lg1 < -100.f ? -100.f : lg1;
+        lrow = -(lab * lp + (1.f - lab) * l1p);
+      }
+      const float lsum = wave_sum(g == 0 ? lrow : 0.f);
+      if (lane == 0) {
+        lossw[wave] = lsum;
+        lossw[8 + wave] = __uint_as_float(wave_nan);
+      }
+    }
     stp(1, tid);
     // ---- deferred: dW operand tiles and column sums of this wave's rows
     {
@@ -1039,10 +1051,14 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
     lds_bar();
     {
       float tot = 0.f;
+      uint32_t any = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) tot += lossw[i];
+      for (int i = 0; i < 8; ++i) {
+        tot += lossw[i];
+        any |= __float_as_uint(lossw[8 + i]);
+      }
       const float loss = tot / (float)Bn;
-      if (loss != loss) {
+      if (any) {  // (the same per-wave flags the branches abort on)
         failed = true;
         break;
       }
