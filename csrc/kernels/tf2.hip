@@ -714,8 +714,7 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
 // before B, so the leaders' two units became the tail; profiles/ab_tf2_r6_update.log.)
 template <int BR>
 __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid, int step,
-                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo, uint32_t seed, float& mka0,
-                                          float& mka1) {
+                                          __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo) {
   using B = BrK<BR>;
   using C = Cmp<BR>;
   opq(lane, wave);
@@ -795,16 +794,7 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
       as = mma(tfrag<TK16>(smem + B_XIN, 32 * s, 0, lane), yd, as);
       bd = mma(one, yd, bd);
     }
-#ifdef TF2_LEAD_LATE_MASKS
-    {  // the next step's dropout masks: the leaders' slack before barrier 1 (beside the laggards' MFMA-bound unit)
-      uint32_t m0, m1;
-      br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), 16 * wave + (lane & 15), g, m0, m1);
-      mka0 = awu(m0);
-      mka1 = awu(m1);
-    }
-#endif
   }
-  (void)seed; (void)mka0; (void)mka1;
   // LayerNorm gradient sums out of the fp64 accumulators (complete: counter B; DBL aliases CS, written back below)
   const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
   const f4v cm = mom_ld(rm, 0, tid), cv = mom_ld(rm, 1, tid), cmv = mom_ld(rm, 2, tid);
@@ -1037,9 +1027,6 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     w.b0 += BS;  // prefetch the next batch's inputs while the head works
     more = walk_valid(w, nd, BS, E);
     if (more) load_x<BR>(xin, a, cid, w, 16 * wave + (lane & 15), g);
-#ifdef TF2_LEAD_LATE_MASKS
-    if (wave >= 4)  // (leaders hash theirs before barrier 1 of the update, see br_update)
-#endif
     {  // the next step's dropout masks, while the head works (this wave would only spin)
       uint32_t m0, m1;
       br_masks<BR>(afl_hash32(seed, (uint32_t)(step + 1)), 16 * wave + (lane & 15), g, m0, m1);
@@ -1080,7 +1067,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     asm volatile(";MARK upd");
     // (false: the head saw a NaN loss somewhere in the batch — the client's round fails and this step's update is
     // not applied — or a wave stopped making progress)
-    const bool upd_ok = br_update<BR>(smem, st, K, lane, wave, tid, step, rm, stp, sync + XF_TMO, seed, mka0, mka1);
+    const bool upd_ok = br_update<BR>(smem, st, K, lane, wave, tid, step, rm, stp, sync + XF_TMO);
     asm volatile(";MARK upd_end");
     if (!upd_ok) {
       failed = true;
