@@ -704,7 +704,8 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
 //             out_proj image no longer read): their out_proj unit — dW over the 128 rows, Adam on the workspace
 //             copy (p, m, v), image, bias sums; then counter B (every wave's dense dY rows): the dense tile w4
 //             and its bias sums;
-//   laggards  counter B (the whole backward: the v image no longer read): their in_proj.v unit.
+//   laggards  counter A (the v unit's dY rows): their in_proj.v unit, whose new bf16 weights wait for counter B (the
+//             v image is read until the end of every wave's backward).
 // The small tiles' gradients and the bias sums are held in registers until barrier 1; then the LayerNorm sums
 // (fixed-point accumulators DBL, aliasing CS), the bias sums and the small gradients (staging GS, aliasing the dead
 // XIN / F2 tiles) are stored; barrier 2; every thread runs Adam on its compact entries (U3).  The abort decision
@@ -760,7 +761,9 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
     }
     prio_hi();
   } else {
-    if (!lds_wait(smem, B_CNT_B, all)) {
+    // (the v unit's operands are complete at A — only its image write waits for B, the end of every wave's
+    // backward — so the laggards' weight-gradient MFMAs overlap the last laggard's v backward)
+    if (!lds_wait(smem, B_CNT_A, all)) {
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
@@ -779,6 +782,10 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
     if (!ABL(K, ABL_UADAM)) unit_adam(U, acc, K);
     u32x2v w[4];
     unit_pack(U, w);
+    if (!lead && !lds_wait(smem, B_CNT_B, all)) {  // (the v image is read until the end of every wave's backward)
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
     unit_img(smem, B::vo(!lead), Ta, Tb, lane, w);
 #pragma unroll
     for (int j = 0; j < 12; ++j) unit_st(rm, ui, j, lane, U[j]);
