@@ -44,13 +44,9 @@ using namespace oc;
 
 // ----------------------------------------------------------------------------------- LDS maps (bytes)
 // branch workgroup
-#ifndef TF2_NO_BPAD
 // dense image compact (k unpermuted: the K <= 16 MFMA reads k = 4g .. 4g + 3 at byte 8g), which pays for 32-byte
 // padding of the v / out_proj images (ds_read_b128 fragment reads conflict-free in gfx950 banking)
 constexpr int LDDN = 24 * 2, LDVO = LD64 + 16;
-#else
-constexpr int LDDN = LD32, LDVO = LD64;
-#endif
 constexpr int B_IMG_D = 0;                         // [64][32]  dense (K = din padded to 32)
 constexpr int B_IMG_V = B_IMG_D + 64 * LDDN;       // [64][64]  in_proj rows 128..191 (v)
 constexpr int B_IMG_O = B_IMG_V + 64 * LDVO;       // [64][64]  out_proj
@@ -134,9 +130,12 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 constexpr int MOM_SLOTS = 11;
 constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
-constexpr int CMP_SLOTS = 3;
+constexpr int CMP_SLOTS = 1;
 constexpr long BR_UNITS = (long)CMP_SLOTS * NTH * 16;
-constexpr long BR_WG_BYTES = BR_UNITS + 8L * 12 * 64 * 16;
+// then the leaders' SMALL units: leader w4's dense / ffn.3 / ffn.0 weight tiles (4 elements per lane each), [w4][9]
+// [lane] float4 = m of the three tiles, v, then p
+constexpr long BR_SMALL = BR_UNITS + 8L * 12 * 64 * 16;
+constexpr long BR_WG_BYTES = BR_SMALL + 4L * 9 * 64 * 16;
 constexpr long WS_BYTES = WS_MOM + MOM_WG_BYTES + 2 * BR_WG_BYTES;  // head, vitals branch, labs branch
 
 // branch LayerNorm column sums -> fp64 accumulator k of DBL (order G1 B1 G2 B2 G3 B3)
@@ -224,7 +223,7 @@ struct BrK {
   static constexpr BrOff o = BR == 0 ? OV : OL;
   static constexpr int din = BR == 0 ? D_V : D_L;
   static constexpr int xoff = BR == 0 ? 0 : D_V;
-  // (the dense, ffn.0 and ffn.3 weights are compact entries: their image positions come from cmp_img, not a Mat)
+  // (the dense, ffn.0 and ffn.3 weights are the leaders' small units: smu_elem gives their image positions)
   static constexpr Mat MV{o.inproj_w + 128 * 64, 64, 64, B_IMG_V, LDVO};
   static constexpr Mat MO{o.out_w, 64, 64, B_IMG_O, LDVO};
   // the v (lo) or out_proj block matrix, built from constants (a `lo ? MV : MO` lvalue select would
@@ -265,27 +264,16 @@ __device__ __forceinline__ void load16(float (&x)[16], const uint32_t (&d)[8]) {
 
 // Optimizer state of one branch lane (AGPR-resident, see ar/aw; the v / out_proj blocks' weights and moments live
 // in the workspace units, see br_update):
-//  * cmp: up to NCMP "compact" entries: the bias / LayerNorm vectors (VEC index e < 648), then the real
-//    elements of the dense, ffn.0 and ffn.3 weights (padding-free: their gradient tiles are mostly padding,
-//    so they are staged through LDS and owned element-wise instead of tile-wise).  Entry e belongs to thread
-//    e % 512, slot e / 512.
+//  * cmp: NCMP "compact" entries, the bias / LayerNorm vectors (VEC index e < 648): entry e belongs to thread
+//    e % 512, slot e / 512.  (The dense, ffn.0 and ffn.3 weights were compact entries too, staged through LDS and
+//    updated by every thread after the staging barrier; since round 6 the leaders update them as tiles in their
+//    slack before barrier 1 — br_update, small units — and the compact pass is 2 entries per thread, not 5.)
+constexpr int NCMP = 2;
 struct BrState {
-  VS cmp[5];
-  float dst[5];  // AGPR: where compact entry h's new value goes (cmp_dst), fixed for the round
+  VS cmp[NCMP];
+  float dst[NCMP];  // AGPR: where compact entry h's new value goes (cmp_dst), fixed for the round
 };
-constexpr int NCMP = 5;
-template <int BR>
-struct Cmp {
-  static constexpr int din = BR == 0 ? D_V : D_L;
-  static constexpr int E_D = B_NVEC;             // dense weight [64][din]
-  static constexpr int E_F1 = E_D + 64 * din;    // ffn.0 weight [6][64]
-  static constexpr int E_F2 = E_F1 + FF * 64;    // ffn.3 weight [64][6]
-  static constexpr int N = E_F2 + 64 * FF;
-  static_assert(N <= NCMP * NTH, "compact entries");
-};
-// compact weight-gradient staging (fp32 [N - 648]) in the XIN / F2 / DF0 tiles, dead by then
-constexpr int B_GS = B_XIN;
-static_assert(B_GS + (Cmp<1>::N - B_NVEC) * 4 <= B_VEC, "compact gradient staging fits");
+static_assert(B_NVEC <= NCMP * NTH, "compact entries");
 
 // Every dropout keep-bit of a branch wave's forward for one step, packed into two words:
 //   mk0 = m1 (out_proj dropout, 16 bits) | m2 (ffn.3 dropout) << 16;
@@ -326,12 +314,8 @@ __device__ __forceinline__ void br_forward(uchar* smem, const float (&xin)[4], u
     const s4v bx = bfrag4(xin);
     f4v acc[4];
 #pragma unroll
-#ifndef TF2_NO_BPAD
     for (int T = 0; T < 4; ++T)
       acc[T] = mma16(*(const LDS_AS s4v*)(smem + B_IMG_D + (16 * T + (lane & 15)) * LDDN + 8 * (lane >> 4)), bx, Z4);
-#else
-    for (int T = 0; T < 4; ++T) acc[T] = mma16(wfrag4(smem + B_IMG_D, LD32, T, lane), bx, Z4);
-#endif
     float bd[16], gp[16];
     vec16g(bd, vg + VS_DB * 256);
 #pragma unroll
@@ -557,54 +541,17 @@ __device__ __forceinline__ void br_backward(uchar* smem, const float (&dout)[16]
 }
 
 
-// compact entry e of branch BR: flat parameter index (or -1), where the new value goes
+// compact entry e (< 648: a bias / LayerNorm vector element) of branch BR: flat parameter index (or -1)
 template <int BR>
 __device__ __forceinline__ int cmp_param(int e) {
-  using C = Cmp<BR>;
-  using B = BrK<BR>;
-  if (e < B_NVEC) return B::vec_param(e);
-  if (e < C::E_F1) {  // dense [64][din]: entries k-major (i = 64 k + n), so no division by din
-    const int i = e - C::E_D;
-    return B::o.dense_w + (i & 63) * C::din + (i >> 6);
-  }
-  if (e < C::E_F2) return B::o.ff0_w + (e - C::E_F1);
-  if (e < C::N) {  // ffn.3 [64][6]: k-major too
-    const int i = e - C::E_F2;
-    return B::o.ff3_w + (i & 63) * FF + (i >> 6);
-  }
-  return -1;
+  return e < B_NVEC ? BrK<BR>::vec_param(e) : -1;
 }
-// store descriptor of compact entry e for U3: bit 31 set = fp32 store at VEC (bias / LayerNorm entries),
-// clear = bf16 store into a weight image; padding entries and entries past the end point at this lane's
-// dummy word (DF0 tile) instead
-template <int BR>
-__device__ __forceinline__ int cmp_img(int e);
+// store descriptor of compact entry e for U3 (fp32 store into VEC); padding entries and entries past the end point
+// at this lane's dummy word (DF0 tile) instead
 template <int BR>
 __device__ __forceinline__ uint32_t cmp_dst(int e, int lane) {
-  using C = Cmp<BR>;
   const uint32_t dmy = B_DF0 + 768 + 4 * lane;
-  if (e >= C::N) return dmy;
-  if (e < B_NVEC) return cmp_param<BR>(e) >= 0 ? (0x80000000u | (uint32_t)(B_VEC + 4 * e)) : (0x80000000u | dmy);
-  return (uint32_t)cmp_img<BR>(e);
-}
-// bf16 image byte offset of compact weight entry e (>= 648)
-template <int BR>
-__device__ __forceinline__ int cmp_img(int e) {
-  using C = Cmp<BR>;
-  if (e < C::E_F1) {
-    const int i = e - C::E_D;
-#ifndef TF2_NO_BPAD
-    return B_IMG_D + (i & 63) * LDDN + (i >> 6) * 2;
-#else
-    return B_IMG_D + (i & 63) * LD32 + pcol(i >> 6) * 2;
-#endif
-  }
-  if (e < C::E_F2) {
-    const int i = e - C::E_F1, n = i >> 6, k = i & 63;
-    return B_IMG_F1 + n * LD64 + pcol(k) * 2;
-  }
-  const int i = e - C::E_F2;
-  return B_IMG_F2 + (i & 63) * LD32 + pcol(i >> 6) * 2;
+  return cmp_param<BR>(e) >= 0 ? (0x80000000u | (uint32_t)(B_VEC + 4 * e)) : (0x80000000u | dmy);
 }
 
 // ------------------------------------------------------------------------------ branch weight update
@@ -693,6 +640,83 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
   }
 }
 
+// Small units: leader w4 owns its dense tile (k 0..15, n tile w4), ffn.3 tile (n tile w4, k 0..15) and ffn.0 k tile
+// w4 (n 0..15) — the weight-gradient tiles it computes (lane element (k = 16 T + 4g + i, n = 16 Tn + i16)); tile s
+// of the unit: 0 dense, 1 ffn.3, 2 ffn.0; slots s (m), 3 + s (v), 6 + s (p).  Padding elements (k >= din, ffn k >= 6,
+// ffn.0 n >= 6) keep p = 0: their inputs / gradients are exactly zero, so Adam leaves them there.
+__device__ __forceinline__ f4v smu_ld(__amdgpu_buffer_rsrc_t rm, int w4, int j, int lane) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rm, (int)BR_SMALL + ((w4 * 9 + j) * 64 + lane) * 16,
+                                                                        0, 16));
+}
+__device__ __forceinline__ void smu_st(__amdgpu_buffer_rsrc_t rm, int w4, int j, int lane, f4v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rm, (int)BR_SMALL + ((w4 * 9 + j) * 64 + lane) * 16,
+                                         0, 0);
+  store_guard();
+}
+// (flat parameter index, bf16 image byte offset) of element i of small tile s of leader w4's lane, or pi = -1
+template <int BR>
+__device__ __forceinline__ void smu_elem(int s, int w4, int lane, int i, int& pi, int& img) {
+  using B = BrK<BR>;
+  constexpr int din = BrK<BR>::din;
+  const int g = lane >> 4, i16 = lane & 15;
+  if (s == 0) {  // dense W[n][k], n = 16 w4 + i16, k = 4g + i; image compact, k unpermuted
+    const int n = 16 * w4 + i16, k = 4 * g + i;
+    pi = k < din ? B::o.dense_w + n * din + k : -1;
+    img = B_IMG_D + n * LDDN + k * 2;
+  } else if (s == 1) {  // ffn.3 W[n][k], n = 16 w4 + i16, k = 4g + i < 6
+    const int n = 16 * w4 + i16, k = 4 * g + i;
+    pi = k < FF ? B::o.ff3_w + n * FF + k : -1;
+    img = B_IMG_F2 + n * LD32 + pcol(k) * 2;
+  } else {  // ffn.0 W[n][k], n = i16 < 6, k = 16 w4 + 4g + i
+    const int n = i16, k = 16 * w4 + 4 * g + i;
+    pi = n < FF ? B::o.ff0_w + n * 64 + k : -1;
+    img = B_IMG_F1 + n * LD64 + pcol(k) * 2;
+  }
+}
+// Adam on the 12 elements of a small unit (S = {m0 m1 m2, v0 v1 v2, p0 p1 p2}), gradients g[3]; new bf16 images
+__device__ __forceinline__ void smu_adam(f4v (&S)[9], const f4v (&gs)[3], const AdamK& K) {
+  float p[12], mm[12], vv[12], g[12], den[12];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mm[4 * s + i] = S[s][i];
+      vv[4 * s + i] = S[3 + s][i];
+      p[4 * s + i] = S[6 + s][i];
+      g[4 * s + i] = gs[s][i];
+    }
+#pragma unroll
+  for (int e = 0; e < 12; ++e) {
+    const float mk = mm[e] * K.keep;
+    mm[e] = mk + K.c1 * (g[e] - mk);
+    vv[e] = fk::B2 * vv[e] + (1.f - fk::B2) * g[e] * g[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 12; ++e) den[e] = __builtin_amdgcn_sqrtf(vv[e]);
+#pragma unroll
+  for (int e = 0; e < 12; ++e) den[e] = __builtin_amdgcn_rcpf(den[e] * K.rsqrt_bc2 + K.eps);
+#pragma unroll
+  for (int e = 0; e < 12; ++e) p[e] -= K.lr_bc1 * mm[e] * den[e];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      S[s][i] = mm[4 * s + i];
+      S[3 + s][i] = vv[4 * s + i];
+      S[6 + s][i] = p[4 * s + i];
+    }
+}
+// the small unit's new weights into the three images (4 consecutive (permuted) k per lane: one 8-byte store each)
+template <int BR>
+__device__ __forceinline__ void smu_img(uchar* smem, const f4v (&S)[9], int w4, int lane) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    int pi, img;
+    smu_elem<BR>(s, w4, lane, 0, pi, img);
+    *(LDS_AS u32x2v*)(smem + img) = u32x2v{pk2(S[6 + s][0], S[6 + s][1]), pk2(S[6 + s][2], S[6 + s][3])};
+  }
+}
+
 // Weight gradients + Adam for one step, started by each wave as soon as its own backward is done — no barrier
 // between the backward and the weight-gradient work.  The waves of a SIMD pair run the same chain and the arbiter
 // favours the older one, so waves 0-3 ("leaders") reach this point ~2.5 us before waves 4-7 ("laggards", the
@@ -706,9 +730,11 @@ __device__ __forceinline__ void unit_dw(const uchar* X, const uchar* DY, int Ta,
 //             and its bias sums;
 //   laggards  counter A (the v unit's dY rows): their in_proj.v unit, whose new bf16 weights wait for counter B (the
 //             v image is read until the end of every wave's backward).
-// The small tiles' gradients and the bias sums are held in registers until barrier 1; then the LayerNorm sums
-// (fixed-point accumulators DBL, aliasing CS), the bias sums and the small gradients (staging GS, aliasing the dead
-// XIN / F2 tiles) are stored; barrier 2; every thread runs Adam on its compact entries (U3).  The abort decision
+// The leaders then run Adam on their small unit (the dense / ffn.3 / ffn.0 tiles, workspace-resident like the
+// blocks) and write its images — in their slack while the laggards finish the v block.  The bias sums are held in
+// registers until barrier 1; then they and the LayerNorm sums (fixed-point accumulators DBL, aliasing CS) are
+// stored; barrier 2; every thread runs Adam on its compact entries (U3: the 648 bias / LayerNorm elements, 2 per
+// thread — 5 when the small weights were compact entries too: +3.6 %, profiles/ab_tf2_r6_update.log).  The abort decision
 // (a NaN loss anywhere in the batch) is taken by every wave after counter A or B — every abort word is written
 // before its wave signals — before anything is updated.  Returns false on abort.
 // (Measured first: the leaders taking both units after counter A was 1 % slower — A is reached only ~0.2 us
@@ -717,7 +743,6 @@ template <int BR>
 __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK& K, int lane, int wave, int tid, int step,
                                           __amdgpu_buffer_rsrc_t rm, Stamp& stp, gu32* tmo) {
   using B = BrK<BR>;
-  using C = Cmp<BR>;
   opq(lane, wave);
   asm volatile("" : "+v"(tid));
   const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
@@ -791,6 +816,9 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
     for (int j = 0; j < 12; ++j) unit_st(rm, ui, j, lane, U[j]);
   }
   if (lead) {
+    f4v S[9];  // the small unit (issued here: its loads overlap the wait for B and the dense MFMAs)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) S[j] = smu_ld(rm, w4, j, lane);
     if (!lds_wait(smem, B_CNT_B, all)) {  // (the dense dY rows and the LayerNorm sums below are complete at B)
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
@@ -801,34 +829,28 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
       as = mma(tfrag<TK16>(smem + B_XIN, 32 * s, 0, lane), yd, as);
       bd = mma(one, yd, bd);
     }
+    // Adam on the small unit (dense, ffn.3, ffn.0 tiles); their images are free: the dense one is read only by the
+    // forward, the ffn ones by the backward before counters C / A
+    const f4v gs3[3] = {as, a3, af1};
+    if (!ABL(K, ABL_U3)) smu_adam(S, gs3, K);
+    smu_img<BR>(smem, S, w4, lane);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) smu_st(rm, w4, j, lane, S[j]);
   }
   // LayerNorm gradient sums out of the fp64 accumulators (complete: counter B; DBL aliases CS, written back below)
   const float lnsum = tid < B_NLN ? lds_getq(smem + B_DBL, tid) : 0.f;
-  const f4v cm = mom_ld(rm, 0, tid), cv = mom_ld(rm, 1, tid), cmv = mom_ld(rm, 2, tid);
+  const f4v cmom = mom_ld(rm, 0, tid);  // compact entries' m0 m1 v0 v1
   stp(5, tid);
   prio_hi();
   lds_bar();
   {
     LDS_AS float* cs = ldsf(smem, B_CS);
     if (tid < B_NLN) cs[ln_seg(tid >> 6) * 64 + (tid & 63)] = lnsum;
-    LDS_AS float* gs = ldsf(smem, B_GS);  // small gradients -> compact staging (dW^T tile element (k = 16T + 4g + i,
-    const int n = 16 * w4 + i16;          // n = 16 Tn + i16))
     if (do_bias && g == 0) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) cs[(lead ? VS_OB : VS_VB) * 64 + 16 * (Tb + b) + i16] = bsu[b][0];
     }
     if (lead) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 4 * g + i;
-        if (k < FF) gs[C::E_F2 - B_NVEC + k * 64 + n] = a3[i];
-        if (i16 < FF) gs[C::E_F1 - B_NVEC + i16 * 64 + 16 * w4 + 4 * g + i] = af1[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 4 * g + i;
-        if (k < C::din) gs[C::E_D - B_NVEC + k * 64 + n] = as[i];
-      }
       if (g == 0) {
         cs[VS_F2B * 64 + 16 * w4 + i16] = b3[0];
         cs[VS_DB * 64 + 16 * w4 + i16] = bd[0];
@@ -844,15 +866,14 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
   // (dead until the next backward).  Entries past the end or padding compute on garbage that only
   // reaches the dummies.  (The divergent if / else version was ~1,200 instructions, 1.4 us per step.)
   if (tid < (B_DBL_BYTES - B_NVEC * 4) / 4) ldsf(smem, B_CS)[B_NVEC + tid] = 0.f;
-  float mm[NCMP] = {cm[0], cm[1], cm[2], cm[3], cmv[0]}, vv[NCMP] = {cv[0], cv[1], cv[2], cv[3], cmv[1]};
+  float mm[NCMP] = {cmom[0], cmom[1]}, vv[NCMP] = {cmom[2], cmom[3]};
   if (!ABL(K, ABL_U3)) {
     const int dmy = B_DF0 + 4 * (tid & 63);
     float gr[NCMP], pn[NCMP];
 #pragma unroll
     for (int h = 0; h < NCMP; ++h) {
       const int e = tid + NTH * h;
-      const bool vec = e < B_NVEC;  // gradient in CS (bias / LayerNorm sums) or GS (staged small dW)
-      gr[h] = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
+      gr[h] = e < B_NVEC ? *(const LDS_AS float*)(smem + B_CS + 4 * e) : 0.f;  // (past the end: dummies only)
     }
     adam_staged<NCMP>(st.cmp, mm, vv, gr, pn, K);
 #pragma unroll
@@ -867,9 +888,7 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
       *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 512 : off)) = fk::f2bf(pn[h]);
     }
   }
-  mom_st(rm, 0, tid, f4v{mm[0], mm[1], mm[2], mm[3]});
-  mom_st(rm, 1, tid, f4v{vv[0], vv[1], vv[2], vv[3]});
-  mom_st(rm, 2, tid, f4v{mm[4], vv[4], 0.f, 0.f});
+  mom_st(rm, 0, tid, f4v{mm[0], mm[1], vv[0], vv[1]});
   return true;
 }
 
@@ -883,7 +902,6 @@ template <int BR>
 __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P, __amdgpu_buffer_rsrc_t rm, int lane,
                                         int wave, int tid) {
   using B = BrK<BR>;
-  using C = Cmp<BR>;
 #pragma unroll
   for (int k = 0; k < CMP_SLOTS; ++k) mom_st(rm, k, tid, Z4);
   {  // wave w: unit 2 (w & 3) + (w >> 2) (every unit once): p from the parameters -> workspace + bf16 image, m = v = 0
@@ -901,19 +919,31 @@ __device__ __forceinline__ void br_init(uchar* smem, BrState& st, const float* P
       *(LDS_AS u32x2v*)(smem + M.img + n * M.ld + pcol(k0) * 2) = u32x2v{pk2(p[0], p[1]), pk2(p[2], p[3])};
     }
   }
+  if (wave < 4) {  // leader w4's small unit: p from the parameters (0 for padding) -> workspace + images, m = v = 0
+    f4v S[9];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      S[s] = S[3 + s] = Z4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int pi, img;
+        smu_elem<BR>(s, wave, lane, i, pi, img);
+        S[6 + s][i] = pi >= 0 ? P[pi] : 0.f;
+      }
+    }
+    smu_img<BR>(smem, S, wave, lane);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) smu_st(rm, wave, j, lane, S[j]);
+  }
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
     float p0 = 0.f;
-    if (e < C::N) {
+    if (e < B_NVEC) {
       const int pi = cmp_param<BR>(e);
       p0 = pi >= 0 ? P[pi] : 0.f;
-      if (e < B_NVEC) {
-        ldsf(smem, B_VEC)[e] = p0;
-        ldsf(smem, B_CS)[e] = 0.f;
-      } else {
-        *(LDS_AS unsigned short*)(smem + cmp_img<BR>(e)) = fk::f2bf(p0);
-      }
+      ldsf(smem, B_VEC)[e] = p0;
+      ldsf(smem, B_CS)[e] = 0.f;
     }
     st.cmp[h] = VS{aw(p0)};
     st.dst[h] = awu(cmp_dst<BR>(e, lane));
@@ -924,7 +954,6 @@ template <int BR>
 __device__ __forceinline__ void br_fini(const BrState& st, float* P, __amdgpu_buffer_rsrc_t rm, int lane, int wave,
                                         int tid) {
   using B = BrK<BR>;
-  using C = Cmp<BR>;
   {  // the units' weights (stored by the waves that updated them: wait for every store before reading back)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -940,10 +969,22 @@ __device__ __forceinline__ void br_fini(const BrState& st, float* P, __amdgpu_bu
       for (int i = 0; i < 4; ++i) dst[i] = p[i];
     }
   }
+  if (wave < 4) {  // leader w4's small unit (its own stores)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const f4v p = smu_ld(rm, wave, 6 + s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int pi, img;
+        smu_elem<BR>(s, wave, lane, i, pi, img);
+        if (pi >= 0) P[pi] = p[i];
+      }
+    }
+  }
 #pragma unroll
   for (int h = 0; h < NCMP; ++h) {
     const int e = tid + NTH * h;
-    if (e < C::N) {
+    if (e < B_NVEC) {
       const int pi = cmp_param<BR>(e);
       if (pi >= 0) P[pi] = ar(st.cmp[h].p);
     }
