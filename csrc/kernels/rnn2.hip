@@ -23,8 +23,9 @@
 //   backward layer by layer: gate backward -> d(gate pre-activations) tile in LDS -> d(layer input)
 //     through the transposed image (before that layer's Adam) -> barrier -> dW = dG^T X with Adam fused
 //     (tile-owned weights) and bias sums (MFMA with an all-ones operand) -> barrier (the dG tile is reused);
-//   the layer-1 weights, biases and LayerNorm vectors are "compact" entries (one element per thread slot)
-//     updated in one branch-free pass at the end of the step.
+//   the layer-1 weights are tile-owned as well (Adam fused into dW1, 12 tiles: waves 0-3 own two, 4-7 one);
+//   the biases and LayerNorm vectors are "compact" entries (one element per thread slot) updated in one
+//     branch-free pass at the end of the step.
 // LDS is the binding budget (bf16 images 63 KB, h1 / h2 tiles 32 KB, one dG tile 48 KB), hence one dG tile
 // and two barriers per layer.
 //
@@ -63,7 +64,7 @@ constexpr int B_W1 = 0;                            // [192][24] layer 1 combined
 constexpr int B_W2 = B_W1 + 192 * LDW1;            // [192][72] layer 2 (K permuted, pcol)
 constexpr int B_W3 = B_W2 + 192 * LDW2;            // [192][72] layer 3
 constexpr int B_X2 = B_W3 + 192 * LDW3;            // tile64: h1 (X of dW2); after dW2: tile16 xin (X of dW1)
-constexpr int B_X3 = B_X2 + 16384;                 // tile64: h2 (X of dW3); after dW3: layer-1 gradient staging
+constexpr int B_X3 = B_X2 + 16384;                 // tile64: h2 (X of dW3)
 constexpr int B_DG = B_X3 + 16384;                 // 3 x tile64: d(gate pre-activations) [128][192] of one layer
 constexpr int B_NVEC = 1280;                       // 6 x (b_ih 96 | b_hh 96) in (layer, direction) order, LN w | b
 constexpr int B_VEC = B_DG + 3 * 16384;            // fp32 [1280] bias / LayerNorm parameters
@@ -72,12 +73,12 @@ constexpr int B_CS = B_VEC + B_NVEC * 4;           // fp32 [1280] their gradient
 // 8-wave sums are independent of the wave order by construction, as tf2.hip): LN weight / bias (0..127), then
 // per layer the d(b_hn) sums of both directions (128 + 64 (l - 1) + 32 d + j)
 // The fp64 slots live in the layer-1 image's row padding (bytes 32..47 of each 48-byte row: the forward reads
-// bytes 0..31 of a row, the compact update writes only real entries k < din <= 16), two slots per row (dbl_slot).
+// bytes 0..31 of a row, the dW1 update writes bytes 0..31 only), two slots per row (dbl_slot).
 constexpr int B_NDBL = 128 + 3 * 64;
 static_assert(B_NDBL <= 2 * 192 && LDW1 == 48, "fp64 column-sum slots fit the layer-1 image padding");
 constexpr int B_MISC = B_CS + B_NVEC * 4;          // u32 [8] per-wave abort words (+ pad)
 constexpr int B_TOTAL = B_MISC + 64;
-constexpr int B_X1 = B_X2, B_GS = B_X3;
+constexpr int B_X1 = B_X2;
 __device__ __forceinline__ uchar* dbl_slot(uchar* smem, int idx) { return smem + B_W1 + (idx >> 1) * LDW1 + 32 + 8 * (idx & 1); }
 enum { VL_LNW = 1152, VL_LNB = 1216 };
 
@@ -109,12 +110,11 @@ constexpr int SMEM = ST_OFF + ST_N * 8;
 constexpr int SMEM = SMEM_CORE;
 #endif
 static_assert(SMEM <= 160 * 1024, "LDS budget");
-static_assert(192 * 16 * 4 <= 16384, "layer-1 gradient staging fits the h2 tile");
 
 // ------------------------------------------------------------------- per-client workspace (bytes)
 // (hand-off payloads travel as tagged granules in the per-call zeroed sync block: onchip.h gr_put / gr_get)
 // Adam moment slab per workgroup [slot][thread] of float4.  Branch: W3 tiles m 0-5 / v 6-11, W2 tiles m 12-17
-// / v 18-23, compact entries m 24-26 / v 27-29.  Head: fc1 tiles m 0-1 / v 2-3, fc2 tile m 4 / v 5, vector 6.
+// / v 18-23, compact entries m 24 / v 25, layer-1 tiles (m, v) 26-27 and 28-29.  Head: fc1 tiles m 0-1 / v 2-3, fc2 tile m 4 / v 5, vector 6.
 constexpr int MOM_SLOTS = 30;
 constexpr long WS_MOM = 0;
 constexpr long MOM_WG_BYTES = (long)MOM_SLOTS * NTH * 16;
@@ -216,13 +216,13 @@ __device__ __forceinline__ of2v gru_unit2(of2v ar, of2v az, of2v an, of2v bhn, u
 // ------------------------------------------------------------------------------ branch workgroup
 // One code path serves both branches (runtime branch index, wave-uniform): the vitals and labs branches differ
 // only in din and their parameter offsets, and a single instantiation halves the kernel's code size.
-constexpr int NC = (B_NVEC + 192 * DL + NTH - 1) / NTH;   // compact slots per thread (labs; vitals pads)
+constexpr int NC = (B_NVEC + NTH - 1) / NTH;   // compact slots per thread
 // VEC segment of (layer l, direction d): b_ih at +0, b_hh at +96
 __host__ __device__ constexpr int v0(int l, int d) { return ((l - 1) * 2 + d) * 192; }
 struct RB {
   int base, din, xoff, N;
   __device__ __forceinline__ explicit RB(int br)
-      : base(br ? BASE_L : BASE_V), din(br ? DL : DV), xoff(br ? DV : 0), N(B_NVEC + 192 * (br ? DL : DV)) {}
+      : base(br ? BASE_L : BASE_V), din(br ? DL : DV), xoff(br ? DV : 0), N(B_NVEC) {}
   // flat offsets (rnn_common.h Br<>, with din at run time): W_ih of (layer l, direction d), b_ih, LN weight
   __device__ __forceinline__ int wih(int l, int d) const {
     return base + (l == 1 ? d * dir_block(din) : 2 * dir_block(din) + ((l - 2) * 2 + d) * dir_block(64));
@@ -239,19 +239,10 @@ struct RB {
       const int ld = e / 192, w = e - 192 * ld;               // (layer, direction) block, entry in it
       return bih(ld / 2 + 1, ld & 1) + w;                     // b_hh follows b_ih in the flat layout
     }
-    if (e < B_NVEC) return ln_w() + (e - VL_LNW);             // ln_b follows ln_w
-    const int i = e - B_NVEC, n = i % 192, k = i / 192;       // layer-1 weights, k-major
-    return wih(1, n / 96) + (n % 96) * din + k;
+    return ln_w() + (e - VL_LNW);                             // ln_b follows ln_w
   }
-  // store descriptor: bit 31 = fp32 store at VEC, else bf16 store into the layer-1 image; entries past the
-  // end point at this lane's dummy word (the dG tile, dead while the compact entries are updated)
-  __device__ __forceinline__ uint32_t cmp_dst(int e, int lane) const {
-    const uint32_t dmy = B_DG + 4 * lane;
-    if (e >= N) return 0x80000000u | dmy;
-    if (e < B_NVEC) return 0x80000000u | (uint32_t)(B_VEC + 4 * e);
-    const int i = e - B_NVEC;
-    return (uint32_t)(B_W1 + (i % 192) * LDW1 + (i / 192) * 2);
-  }
+  // layer-1 weight (row n of the combined [192][din] gate matrix, column k) -> flat parameter index
+  __device__ __forceinline__ int w1_param(int n, int k) const { return wih(1, n / 96) + (n % 96) * din + k; }
 };
 static_assert(Br<1>::ln_b == Br<1>::ln_w + 64 && Br<0>::bhh(2, 1) == Br<0>::bih(2, 1) + G3, "contiguous vectors");
 
@@ -264,6 +255,7 @@ struct Saved {
 };
 struct BrState {
   TS w3[6], w2[6];  // tiles of the layer-3 / layer-2 weight gradients (k tiles 2(w&1)+a, n tiles 3(w>>1)+b)
+  TS l1[2];         // layer-1 tiles wave + 8 t (n rows 16 (wave + 8 t) + lane % 16, k = 4 (lane / 16) + i)
   VS cmp[NC];       // compact entries e = tid + 512 h
 };
 
@@ -545,29 +537,84 @@ __device__ __forceinline__ void layer_dw(uchar* smem, const RB& R, TS (&wt)[6], 
   }
 }
 
-// layer 1: dW (staged, compact entries) and bias sums; the fp64 sums -> CS
-__device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wave, int tid) {
+// layer 1: dW tiles with Adam fused (weights in AGPRs, moments in slots 26-29, bf16 -> the layer-1 image, whose
+// bytes 0..31 of a row the backward does not read) and bias sums; the fp64 sums -> CS.  Columns k >= din are
+// zero-gradient (their weights stay 0, the image's zero columns).
+template <int NT>
+__device__ __forceinline__ void l1_tiles(uchar* smem, BrState& st, f4v (&um)[4], const f4v (&acc)[2], int din,
+                                         int wave, int lane, const AdamK& K) {
+  constexpr int N = 4 * NT;
+  const int g4 = 4 * (lane >> 4);
+  float p[N], mm[N], vv[N], g[N], den[N];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p[4 * t + i] = ar(st.l1[t].p[i]);
+      mm[4 * t + i] = um[2 * t][i];
+      vv[4 * t + i] = um[2 * t + 1][i];
+      g[4 * t + i] = g4 + i < din ? acc[t][i] : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float mk = mm[i] * K.keep;
+    mm[i] = mk + K.c1 * (g[i] - mk);
+    vv[i] = fk::B2 * vv[i] + (1.f - fk::B2) * g[i] * g[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_sqrtf(vv[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) den[i] = __builtin_amdgcn_rcpf(den[i] * K.rsqrt_bc2 + K.eps);
+#pragma unroll
+  for (int i = 0; i < N; ++i) p[i] -= K.lr_bc1 * mm[i] * den[i];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      st.l1[t].p[i] = aw(p[4 * t + i]);
+      um[2 * t][i] = mm[4 * t + i];
+      um[2 * t + 1][i] = vv[4 * t + i];
+    }
+    const int n = 16 * (wave + 8 * t) + (lane & 15);
+    *(LDS_AS u32x2v*)(smem + B_W1 + n * LDW1 + 2 * g4) =
+        u32x2v{pk2(p[4 * t], p[4 * t + 1]), pk2(p[4 * t + 2], p[4 * t + 3])};
+  }
+}
+__device__ __forceinline__ void layer1_mom_ld(__amdgpu_buffer_rsrc_t rm, int tid, f4v (&um)[4]) {
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) um[k] = slot_ld(rm, 26 + k, 16 * tid);
+}
+__device__ __forceinline__ void layer1_dw(uchar* smem, BrState& st, f4v (&um)[4], __amdgpu_buffer_rsrc_t rm, int din,
+                                          const AdamK& K, int lane, int wave, int tid) {
   opq(lane, wave);
-  const int i16 = lane & 15, g = lane >> 4;
-  LDS_AS float* gs = ldsf(smem, B_GS);
+  const int i16 = lane & 15;
+  const int nt = wave < 4 ? 2 : 1;
+  f4v acc[2] = {Z4, Z4};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (h == 1 && wave >= 4) break;
     const int Tn = wave + 8 * h;
-    f4v acc = Z4, bs = Z4;
+    f4v bs = Z4;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const s8v y = tfrag<TK64>(smem + B_DG + (Tn >> 2) * 16384, 32 * s, Tn & 3, lane);
-      acc = mma(tfrag<TK16>(smem + B_X1, 32 * s, 0, lane), y, acc);
+      acc[h] = mma(tfrag<TK16>(smem + B_X1, 32 * s, 0, lane), y, acc[h]);
       bs = mma(ones8(), y, bs);
     }
-    const int n = 16 * Tn + i16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = 4 * g + i;
-      if (k < din) gs[192 * k + n] = acc[i];
+    if ((lane >> 4) == 0) bias_cs(smem, 1, Tn, i16, bs[0]);
+  }
+  if (!ABL(ABL_TADAM)) {
+    if (nt == 2) l1_tiles<2>(smem, st, um, acc, din, wave, lane, K);
+    else l1_tiles<1>(smem, st, um, acc, din, wave, lane, K);
+  }
+  if (!ABL(ABL_MOM)) {
+    slot_st(rm, 26, 16 * tid, um[0]);
+    slot_st(rm, 27, 16 * tid, um[1]);
+    if (nt == 2) {
+      slot_st(rm, 28, 16 * tid, um[2]);
+      slot_st(rm, 29, 16 * tid, um[3]);
     }
-    if (g == 0) bias_cs(smem, 1, Tn, i16, bs[0]);
   }
   if (tid < B_NDBL) {
     const float s = lds_getq(dbl_slot(smem, tid), 0);
@@ -583,48 +630,40 @@ __device__ __forceinline__ void layer1_dw(uchar* smem, int din, int lane, int wa
   }
 }
 
-// compact entries, branch-free (tf2.hip U3): gradient from CS or GS, Adam, fp32 -> VEC or bf16 -> layer-1 image;
-// the store descriptors are recomputed here (cheaper than keeping NC of them live through the step)
-__device__ __forceinline__ void compact_mom_ld(__amdgpu_buffer_rsrc_t rm, int tid, f4v (&c)[6]) {
+// compact entries, branch-free (tf2.hip U3): gradient from CS, Adam, fp32 -> VEC (entries past the end write
+// this lane's dummy word in the dG tile, dead while the compact entries are updated)
+__device__ __forceinline__ void compact_mom_ld(__amdgpu_buffer_rsrc_t rm, int tid, f4v (&c)[2]) {
   asm volatile("" : "+v"(tid));
-#pragma unroll
-  for (int k = 0; k < 6; ++k) c[k] = slot_ld(rm, 24 + k, 16 * tid);
+  c[0] = slot_ld(rm, 24, 16 * tid);
+  c[1] = slot_ld(rm, 25, 16 * tid);
 }
-__device__ __forceinline__ void compact_update(uchar* smem, const RB& R, BrState& st, __amdgpu_buffer_rsrc_t rm,
-                                               const f4v (&c)[6], const AdamK& K, int lane, int tid) {
+__device__ __forceinline__ void compact_update(uchar* smem, BrState& st, __amdgpu_buffer_rsrc_t rm, const f4v (&c)[2],
+                                               const AdamK& K, int tid) {
+  static_assert(NC <= 4, "compact moments fit one slot each");
   asm volatile("" : "+v"(tid));
-  lane = tid & 63;
-  const f4v cm0 = c[0], cm1 = c[1], cm2 = c[2], cv0 = c[3], cv1 = c[4], cv2 = c[5];
-  float mmc[12] = {cm0[0], cm0[1], cm0[2], cm0[3], cm1[0], cm1[1], cm1[2], cm1[3], cm2[0], cm2[1], cm2[2], cm2[3]};
-  float vvc[12] = {cv0[0], cv0[1], cv0[2], cv0[3], cv1[0], cv1[1], cv1[2], cv1[3], cv2[0], cv2[1], cv2[2], cv2[3]};
-  const int dmy = B_DG + 256 + 4 * lane;
+  const int dmy = B_DG + 256 + 4 * (tid & 63);
   float gr[NC], mh[NC], vh[NC], pn[NC];
 #pragma unroll
   for (int h = 0; h < NC; ++h) {
     const int e = tid + NTH * h;
-    const bool vec = e < B_NVEC;
-    gr[h] = *(const LDS_AS float*)(smem + (vec ? B_CS + 4 * e : B_GS + 4 * (e - B_NVEC)));
-    if (ABL(ABL_HALF) && !vec) gr[h] = 0.f;  // (ablation: waves 4-7 stage no layer-1 tiles; the rest is stale h2 data)
-    mh[h] = mmc[h];
-    vh[h] = vvc[h];
+    gr[h] = ldsf(smem, B_CS)[min(e, B_NVEC - 1)];  // (entries past the end: any finite value)
+    mh[h] = c[0][h];
+    vh[h] = c[1][h];
   }
   adam_staged<NC>(st.cmp, mh, vh, gr, pn, K);
 #pragma unroll
   for (int h = 0; h < NC; ++h) {
-    const uint32_t dd = R.cmp_dst(tid + NTH * h, lane);
-    const bool f32 = dd >> 31;
-    const int off = (int)(dd & 0x7FFFFFFFu);
-    *(LDS_AS float*)(smem + (f32 ? off : dmy)) = pn[h];
-    *(LDS_AS unsigned short*)(smem + (f32 ? dmy + 256 : off)) = fk::f2bf(pn[h]);
-    mmc[h] = mh[h];
-    vvc[h] = vh[h];
+    const int e = tid + NTH * h;
+    *(LDS_AS float*)(smem + (e < B_NVEC ? B_VEC + 4 * e : dmy)) = pn[h];
   }
-  slot_st(rm, 24, 16 * tid, f4v{mmc[0], mmc[1], mmc[2], mmc[3]});
-  slot_st(rm, 25, 16 * tid, f4v{mmc[4], mmc[5], mmc[6], mmc[7]});
-  slot_st(rm, 26, 16 * tid, f4v{mmc[8], mmc[9], mmc[10], mmc[11]});
-  slot_st(rm, 27, 16 * tid, f4v{vvc[0], vvc[1], vvc[2], vvc[3]});
-  slot_st(rm, 28, 16 * tid, f4v{vvc[4], vvc[5], vvc[6], vvc[7]});
-  slot_st(rm, 29, 16 * tid, f4v{vvc[8], vvc[9], vvc[10], vvc[11]});
+  f4v m4 = Z4, v4 = Z4;
+#pragma unroll
+  for (int h = 0; h < NC; ++h) {
+    m4[h] = mh[h];
+    v4[h] = vh[h];
+  }
+  slot_st(rm, 24, 16 * tid, m4);
+  slot_st(rm, 25, 16 * tid, v4);
 }
 
 __device__ __forceinline__ void load_x(float (&x)[4], const AflTfTrainArgs& a, const RB& R, int cid, const Walk& w, int r,
@@ -667,13 +706,25 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
         tile_load(st.w2[3 * a2 + b], R.mat(2, d), Ta + a2, Tn0 + b - 6 * d, lane, P, smem);
       }
 #pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = 16 * (wave + 8 * t) + (lane & 15);
+      float p0[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * g + i;
+        p0[i] = (t == 0 || wave < 4) && k < R.din ? P[R.w1_param(n, k)] : 0.f;
+        st.l1[t].p[i] = aw(p0[i]);
+      }
+      if (t == 0 || wave < 4)
+        *(LDS_AS u32x2v*)(smem + B_W1 + n * LDW1 + 8 * g) = u32x2v{pk2(p0[0], p0[1]), pk2(p0[2], p0[3])};
+    }
+#pragma unroll
     for (int h = 0; h < NC; ++h) {
       const int e = tid + NTH * h;
       float p0 = 0.f;
       if (e < R.N) {
         p0 = P[R.cmp_param(e)];
-        if (e < B_NVEC) ldsf(smem, B_VEC)[e] = p0;
-        else *(LDS_AS unsigned short*)(smem + R.cmp_dst(e, lane)) = fk::f2bf(p0);
+        ldsf(smem, B_VEC)[e] = p0;
       }
       st.cmp[h] = VS{aw(p0)};
     }
@@ -802,16 +853,18 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
       dnr_colsum(smem, 1, dnr, ln);
       *(LDS_AS u32x2v*)(smem + B_X1 + toff<TK16>(rr, ln >> 4)) = u32x2v{xpk[0], xpk[1]};
     }
+    f4v um[4];
+    layer1_mom_ld(rm, tid, um);
     lds_bar();  // A1
     stp(8, tid);
     asm volatile(";MARK dw1");
-    if (!half_idle) layer1_dw(smem, R.din, lane, wave, tid);
-    f4v cmom[6];
+    if (!half_idle) layer1_dw(smem, st, um, rm, R.din, K, lane, wave, tid);
+    f4v cmom[2];
     compact_mom_ld(rm, tid, cmom);
     lds_bar();  // C: every gradient of the compact entries in CS / GS
     stp(9, tid);
     asm volatile(";MARK u3");
-    compact_update(smem, R, st, rm, cmom, K, lane, tid);
+    compact_update(smem, st, rm, cmom, K, tid);
     stp(10, tid);
     lds_bar();
     stp(11, tid);
@@ -827,6 +880,13 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
         tile_store(st.w3[3 * a2 + b], R.mat(3, d), Ta + a2, Tn0 + b - 6 * d, lane, P);
         tile_store(st.w2[3 * a2 + b], R.mat(2, d), Ta + a2, Tn0 + b - 6 * d, lane, P);
       }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = 16 * (wave + 8 * t) + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((t == 0 || wave < 4) && 4 * g + i < R.din) P[R.w1_param(n, 4 * g + i)] = ar(st.l1[t].p[i]);
+    }
 #pragma unroll
     for (int h = 0; h < NC; ++h) {
       const int e = tid + NTH * h;
