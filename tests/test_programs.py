@@ -165,6 +165,31 @@ def test_attention_rc_mask_statistics():
     assert abs(agree - (0.9 * 0.9 + 0.1 * 0.1)) < 0.01  # independent draws
 
 
+def test_attention_rc_keep_rate_within_3_sigma():
+    """Keep rate of the attention dropout draw over >= 1e6 draws (two 16-bit decisions per 32-bit mix, threshold
+    round(p * 2^16)) is within 3 sigma of 1 - p, for the whole draw and for each 16-bit half (even / odd columns)."""
+    import numpy as np
+
+    from attackfl_amd.ops import masks
+
+    p = 0.1
+    rows, cols = np.arange(1024)[:, None], np.arange(1040)[None, :]
+    k = np.concatenate([masks.keep_rc(masks.step_key(11, s), 10 + s, rows, cols, p).numpy().ravel()
+                        for s in range(2)]).astype(np.float64)
+    n = k.size
+    assert n >= 2_000_000
+    q = 1 - round(p * 65536) / 65536  # the exact keep probability of a 16-bit threshold
+    assert abs(q - (1 - p)) < 2 ** -16
+    sig = np.sqrt(q * (1 - q) / n)
+    assert abs(k.mean() - q) < 3 * sig, (k.mean(), q, sig)
+    halves = k.reshape(-1, 2)  # (even, odd) column pairs = low / high halves of one mix
+    for h in range(2):
+        assert abs(halves[:, h].mean() - q) < 3 * np.sqrt(2) * sig
+    # the two halves of one mix are independent decisions
+    both = (halves[:, 0] * halves[:, 1]).mean()
+    assert abs(both - q * q) < 3 * np.sqrt(q * q * (1 - q * q) / (n / 2))
+
+
 def test_client_chunks_balanced():
     from attackfl_amd.ops.transformer import client_chunks
 
