@@ -188,6 +188,19 @@ def test_attention_rc_keep_rate_within_3_sigma():
     # the two halves of one mix are independent decisions
     both = (halves[:, 0] * halves[:, 1]).mean()
     assert abs(both - q * q) < 3 * np.sqrt(q * q * (1 - q * q) / (n / 2))
+    # no xor structure from hr ^ hc: the four corners of random (row pair, column pair) rectangles, whose mix
+    # inputs xor to zero, are independent draws (all kept: q^4; odd count kept: the binomial parity)
+    km = k[: 1024 * 1040].reshape(1024, 1040)
+    rs = np.random.RandomState(5)
+    i1, i2, j1, j2 = rs.randint(0, 1024, 400000), rs.randint(0, 1024, 400000), rs.randint(0, 1040, 400000), \
+        rs.randint(0, 1040, 400000)
+    ok = (i1 != i2) & (j1 != j2)
+    corners = np.stack([km[i1, j1], km[i1, j2], km[i2, j1], km[i2, j2]])[:, ok]
+    m = corners.shape[1]
+    all4, par = corners.prod(axis=0).mean(), (corners.sum(axis=0) % 2).mean()
+    par_q = 4 * q * (1 - q) ** 3 + 4 * q ** 3 * (1 - q)
+    assert abs(all4 - q ** 4) < 4 * np.sqrt(q ** 4 * (1 - q ** 4) / m), all4
+    assert abs(par - par_q) < 4 * np.sqrt(par_q * (1 - par_q) / m), par
 
 
 def test_client_chunks_balanced():
