@@ -87,7 +87,7 @@ def _hash4(key: int, layer: int, r, c) -> np.ndarray:
 
 def keep_rc(key: int, layer: int, rows, cols, p: float) -> torch.Tensor:
     """Attention-probability dropout of the bf16 HAR kernels (``har.hip`` ``attn_keep``): a strong hash per
-    ROW and one per column PAIR, combined by xor and two multiply-xorshift rounds; the 32-bit result gives the
+    ROW and one per column PAIR, combined by xor and one multiply-xorshift round; the 32-bit result gives the
     16-bit uniforms of the pair's two columns.  The per-row and per-column hashes are computed once per
     workgroup (registers / an LDS table), so a probability costs half a 2-round mix instead of half a full
     hash4 — the attention kernels are VALU-bound and the full hash was most of their work."""
@@ -98,8 +98,6 @@ def keep_rc(key: int, layer: int, rows, cols, p: float) -> torch.Tensor:
     hc = _hash4(key ^ 0xA5A5A5A5, layer, 0, col >> np.uint64(1))
     x = (hr ^ hc) & m
     x = (x * np.uint64(0x7FEB352D)) & m
-    x ^= x >> np.uint64(15)
-    x = (x * np.uint64(0x846CA68B)) & m
     x ^= x >> np.uint64(16)
     u16 = (x >> ((col & np.uint64(1)) << np.uint64(4))) & np.uint64(0xFFFF)
     return torch.from_numpy(np.ascontiguousarray(u16 >= np.uint64(thr16(p))))

@@ -421,7 +421,7 @@ __device__ __forceinline__ float sum_x16_x32(float a) {
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
 // Probability dropout (masks.keep_rc): a strong hash per row (attn_hr) and per column pair (attn_hc, an LDS
-// table per workgroup) combined by xor and two multiply-xorshift rounds; 16 bits per column.  Only the forward
+// table per workgroup) combined by xor and one multiply-xorshift round; 16 bits per column.  Only the forward
 // hashes: it stores the flags as 64-bit ballot words (AflHarAttn::mask) that the backward kernels read back.
 // Kept probabilities are NOT scaled here: 1/(1-p) is folded into O (forward), dV and dP (backward).
 __device__ __forceinline__ uint32_t attn_hr(uint32_t key, uint32_t layer, uint32_t r) {
@@ -430,13 +430,13 @@ __device__ __forceinline__ uint32_t attn_hr(uint32_t key, uint32_t layer, uint32
 __device__ __forceinline__ uint32_t attn_hc(uint32_t key, uint32_t layer, uint32_t cp) {
   return afl_hash4(key ^ 0xA5A5A5A5u, layer, 0u, cp);
 }
+// One multiply-xorshift round (3 vector instructions per mix: xor, v_mul_lo_u32, xor with the high half):
+// the draw is VALU-issue-bound and a second round measured as pure cost.  hr and hc are full-avalanche hashes;
+// the product's carries break the xor structure of hr ^ hc (every output bit's four-corner parity is balanced,
+// keep rate / halves / rectangles pinned by tests/test_programs.py).
 __device__ __forceinline__ uint32_t attn_mix(uint32_t hr, uint32_t hc) {
-  uint32_t x = hr ^ hc;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
+  uint32_t x = (hr ^ hc) * 0x7FEB352Du;
+  return x ^ (x >> 16);
 }
 // keep flags of keys kb .. kb+3 (kb even) of the row with hash hr: pairs kb/2, kb/2 + 1 from the LDS table
 __device__ __forceinline__ void keep4(const LDS_AS uint32_t* HC, uint32_t hr, int kb, uint32_t thr, bool* k) {
