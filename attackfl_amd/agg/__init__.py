@@ -155,9 +155,11 @@ def _gmm_md2(Lc, r, x, mu):
     return s
 
 
-def gmm_filter_ref(G: np.ndarray, att: np.ndarray):
+def gmm_filter_ref(G: np.ndarray, att: np.ndarray, rank: Optional[int] = None):
     """Host mirror of ``agg.hip`` ``k_gmm_filter`` (same algorithm and operation order, fp64): returns
-    (keep [n] bool, threshold, kept, ok).  See the kernel for the algorithm and its reference mapping."""
+    (keep [n] bool, threshold, kept, ok).  See the kernel for the algorithm and its reference mapping.
+    ``rank`` overrides the PCA rank r = max(1, min(4, n // 2 - 1)) (1..4; the sensitivity study
+    tools/dbg/gmm_rank_study.py)."""
     n = G.shape[0]
     A = [list(map(float, row)) for row in G]
     V = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
@@ -185,7 +187,7 @@ def gmm_filter_ref(G: np.ndarray, att: np.ndarray):
                     V[k][q] = sn * vkp + c * vkq
     order = sorted(range(n), key=lambda i: -A[i][i])  # stable: ties keep index order (as the insertion sort)
     ev = [A[i][i] for i in order]
-    r = max(1, min(4, n // 2 - 1))
+    r = max(1, min(4, n // 2 - 1)) if rank is None else max(1, min(4, int(rank)))
     Z = [[V[i][order[k]] * math.sqrt(max(ev[k], 1e-30)) for k in range(r)] for i in range(n)]
     zmax = max(1e-30, max(abs(z) for row in Z for z in row))
     Z = [[z / zmax for z in row] for row in Z]
