@@ -158,8 +158,8 @@ def _gmm_md2(Lc, r, x, mu):
 def gmm_filter_ref(G: np.ndarray, att: np.ndarray, rank: Optional[int] = None):
     """Host mirror of ``agg.hip`` ``k_gmm_filter`` (same algorithm and operation order, fp64): returns
     (keep [n] bool, threshold, kept, ok).  See the kernel for the algorithm and its reference mapping.
-    ``rank`` overrides the PCA rank r = max(1, min(4, n // 2 - 1)) (1..4; the sensitivity study
-    tools/dbg/gmm_rank_study.py)."""
+    ``rank`` > 0 sets the PCA rank r = min(rank, 4, n); None / 0: r = max(1, min(4, n // 2 - 1)) (the
+    sensitivity study: profiles/gmm_rank_study_r6.md)."""
     n = G.shape[0]
     A = [list(map(float, row)) for row in G]
     V = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
@@ -187,7 +187,7 @@ def gmm_filter_ref(G: np.ndarray, att: np.ndarray, rank: Optional[int] = None):
                     V[k][q] = sn * vkp + c * vkq
     order = sorted(range(n), key=lambda i: -A[i][i])  # stable: ties keep index order (as the insertion sort)
     ev = [A[i][i] for i in order]
-    r = max(1, min(4, n // 2 - 1)) if rank is None else max(1, min(4, int(rank)))
+    r = min(int(rank), 4, n) if rank else max(1, min(4, n // 2 - 1))
     Z = [[V[i][order[k]] * math.sqrt(max(ev[k], 1e-30)) for k in range(r)] for i in range(n)]
     zmax = max(1e-30, max(abs(z) for row in Z for z in row))
     Z = [[z / zmax for z in row] for row in Z]
@@ -287,22 +287,25 @@ def gmm_filter_ref(G: np.ndarray, att: np.ndarray, rank: Optional[int] = None):
     return keep, thr, int(keep.sum()), st["ok"]
 
 
-def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, seed: int = 0, **_) -> AggResult:
+def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, seed: int = 0,
+        gmm_rank: Optional[int] = None, **_) -> AggResult:
     """GMM gradient filter (reference server.py:352-370; its full-covariance fit on raw P-dim updates crashes, A-8):
     a 2-component GMM on the updates' leading PCA scores, deterministic (agg.hip ``k_gmm_filter``, one fused
     launch on the device; ``gmm_filter_ref`` on the host).  The mean of the kept rows; the round fails when no
-    row is kept (reference ``round_result = False``) — the only host read of the mode, one byte after the kernel."""
+    row is kept (reference ``round_result = False``) — the only host read of the mode, one byte after the kernel.
+    ``gmm_rank``: the PCA rank (engine ``gmm-rank``; None / 0 = max(1, min(4, n // 2 - 1)))."""
     n = U.shape[0]
     att = attackers.bool() if attackers is not None else torch.zeros(n, dtype=torch.bool)
     G = _centred_gram(U)
     if U.is_cuda and n <= 64:
-        keep_d, inf_d = ops.native().gmm_filter(G.contiguous(), att.to(U.device, torch.uint8).contiguous())
+        keep_d, inf_d = ops.native().gmm_filter(G.contiguous(), att.to(U.device, torch.uint8).contiguous(),
+                                                int(gmm_rank or 0))
         keep = keep_d.bool()
         thr = inf_d[0]
         if not bool(inf_d[1] > 0):  # (the one synchronising read)
             return AggResult(None, False, {"kept": keep, "threshold": thr})
         return AggResult(_masked_mean(U, keep), True, {"kept": keep, "threshold": thr})
-    keep, thr, kept, _ = gmm_filter_ref(G.cpu().numpy(), att.cpu().numpy())
+    keep, thr, kept, _ = gmm_filter_ref(G.cpu().numpy(), att.cpu().numpy(), rank=gmm_rank)
     if not kept:
         return AggResult(None, False, {"kept": []})
     return AggResult(mean_of(U[torch.from_numpy(np.nonzero(keep)[0]).to(U.device)]), True,

@@ -41,6 +41,8 @@ Extensions (all optional, defaults keep reference behaviour):
   compat-fedavg-alias: bool         (True = reproduce reference A-13: FedAvg writes the aggregate into the
                                     first client's stored update, which attackers may receive as "genuine")
   fault-inject: [{client, round}]   (NaN-poison a client's model before that training round)
+  gmm-rank: int                     (gmm mode's PCA rank, default 1; 0 = max(1, min(4, n // 2 - 1)), the
+                                    round-5 rule: profiles/gmm_rank_study_r6.md)
   save-state: bool                  (write {model}.state.pt + {model}.clients.r{rank}.pt every round)
   resume: bool                      (continue from those files: counters, RNGs, optimizer moments)
 """
@@ -89,7 +91,7 @@ EXTENSION_DEFAULTS: Dict[str, Any] = {
     "engine": {"trainer": "auto", "distance": "spectral", "seed": 0, "metrics": "", "checkpoint-dir": ".",
                "async-checkpoint": True, "compat-hyper-resume": False, "compat-fltrust": False, "max-retries": 50, "trace": False,
                "phase-sync": False, "fault-inject": [], "save-state": False, "resume": False,
-               "speculative": True, "compat-har-train": False, "compat-fedavg-alias": False},
+               "speculative": True, "compat-har-train": False, "compat-fedavg-alias": False, "gmm-rank": 1},
 }
 
 

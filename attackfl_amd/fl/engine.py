@@ -20,11 +20,13 @@ this round's validation at any world size (speculative launch, ``run_round``).
 """
 from __future__ import annotations
 
+import atexit
 import contextlib
 import os
 import random
 import time
 import uuid
+import weakref
 import zlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -142,10 +144,25 @@ def build_client_table(cfg: Config, world: int, attackers: Optional[Dict[int, At
     return table
 
 
+_LIVE: "weakref.WeakSet[FLEngine]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_engines():
+    """Interpreter exit: close every engine its script did not close (a pending speculative launch and the
+    checkpoint writer thread would otherwise still run while the runtime tears down: abort at exit)."""
+    for eng in list(_LIVE):
+        try:
+            eng.close()
+        except Exception:  # noqa: BLE001 (best effort at exit)
+            pass
+
+
 class FLEngine:
     def __init__(self, cfg: Config, comm: Optional[Comm] = None, table: Optional[List[ClientInfo]] = None,
                  device=None, leader: Optional[bool] = None, verbose: bool = True, train_dataset=None,
                  test_dataset=None):
+        _LIVE.add(self)
         self.cfg = cfg
         self.comm = comm or LoopbackComm(device or "cpu")
         self.device = torch.device(device) if device is not None else self.comm.device
@@ -751,7 +768,8 @@ class FLEngine:
             info["n"] = int(U.shape[0])
             return info
         fn = AGGREGATORS[mode]
-        res: AggResult = fn(U, sizes, attackers=attackers, seed=self.seed * 13 + self.round_no)
+        res: AggResult = fn(U, sizes, attackers=attackers, seed=self.seed * 13 + self.round_no,
+                            gmm_rank=int(self.cfg.engine.get("gmm-rank", 1)))
         info.update({k: v for k, v in res.info.items() if k != "scores"})
         if not res.ok:
             info["agg_failed"] = True
@@ -1242,6 +1260,9 @@ class FLEngine:
         return self.history
 
     def close(self):
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
         if self._spec is not None:
             # a speculative launch nobody consumed (bench.py drives run_round itself): wait for the GPU work,
             # skip the block / meta bookkeeping.  Client state (local_params, training_round, client RNGs) is

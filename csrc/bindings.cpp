@@ -82,7 +82,7 @@ torch::Tensor pairwise_sqdist_gram(torch::Tensor G) {
 }
 
 // GMM filter (agg.gmm): G = centred Gram [n, n] fp64, att [n] uint8 -> (keep [n] uint8, info [3] fp64)
-std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
+std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att, int64_t rank) {
   check_dev(G, "G", torch::kFloat64);
   check_dev(att, "att", torch::kUInt8);
   const int64_t n = G.size(0);
@@ -90,7 +90,7 @@ std::vector<torch::Tensor> gmm_filter(torch::Tensor G, torch::Tensor att) {
   auto keep = torch::zeros({n}, att.options());
   auto info = torch::zeros({3}, G.options());
   TORCH_CHECK(afl_gmm_filter(G.data_ptr<double>(), (int)n, att.data_ptr<uint8_t>(), keep.data_ptr<uint8_t>(),
-                             info.data_ptr<double>(), cur()) == 0, "gmm_filter launch failed");
+                             info.data_ptr<double>(), (int)rank, cur()) == 0, "gmm_filter launch failed");
   AFL_CHECK_LAUNCH();
   return {keep, info};
 }
@@ -754,7 +754,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weighted_rows", &weighted_rows);
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
-  m.def("gmm_filter", &gmm_filter);
+  m.def("gmm_filter", &gmm_filter, pybind11::arg("G"), pybind11::arg("att"), pybind11::arg("rank") = 0);
   m.def("top_pc", &top_pc);
   m.def("fxsum_test", &fxsum_test);
   m.def("gram_centred", &gram_centred);

@@ -422,7 +422,8 @@ int afl_attn_bwd(const AflAttn& a, hipStream_t s);
 int afl_gram_partials(int K, long P);  // doubles of scratch afl_pair_sqdist_gram needs
 int afl_pair_sqdist_gram(const float* G, int K, long P, double* partial, double* D, hipStream_t s);
 // GMM gradient filter on the centred Gram matrix (agg.hip k_gmm_filter): keep[n] (0/1), info = {threshold, kept, ok}
-int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, hipStream_t s);
+int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, int rank,
+                   hipStream_t s);
 // FLTracer PCA(1) scores from the centred Gram [n][n] fp64 (n <= 64): Jacobi eigen-decomposition, z [n] fp64
 int afl_top_pc(const double* G, int n, int sweeps, double* z, hipStream_t s);
 void afl_noise_philox(const float* own, float* out, long P, float sigma, uint64_t seed, hipStream_t s);

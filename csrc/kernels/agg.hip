@@ -480,7 +480,7 @@ void afl_adam_flat(float* p, const float* g, float* m, float* v, long n, int ste
 // ============================================================================ gmm_filter
 // GMM gradient filter (reference server.py:352-370, src/Utils.py:257-323), all decisions on the device so the
 // round needs no host round trip: input the centred Gram matrix G = Xc Xc^T [n][n] (fp64) of the client updates.
-//   1. PCA scores in r = max(1, min(4, n/2 - 1)) dims: cyclic Jacobi eigen-decomposition of G (12 sweeps),
+//   1. PCA scores in r dims (rank > 0: min(rank, 4, n); 0: max(1, min(4, n/2 - 1))): cyclic Jacobi eigen-decomposition of G (12 sweeps),
 //      eigenvalues in descending order, Z = V_r sqrt(lambda_r), scaled by 1 / max |Z|;
 //   2. rows ordered benign then malicious (train_gmm_model's vstack), a 2-component full-covariance GMM
 //      (reg_covar 1e-6, tol 1e-3, <= 100 EM iterations, sklearn's M / E steps) initialised by a deterministic
@@ -518,7 +518,7 @@ __device__ __host__ inline double gmm_md2(const double (&Lc)[GMM_R][GMM_R], int 
 }
 
 __global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G, int n, const unsigned char* __restrict__ att,
-                                                   unsigned char* __restrict__ keep, double* __restrict__ info) {
+                                                   unsigned char* __restrict__ keep, double* __restrict__ info, int rank) {
   __shared__ double A[GMM_MAXN * GMM_MAXN], V[GMM_MAXN * GMM_MAXN], Z[GMM_MAXN * GMM_R], X[GMM_MAXN * GMM_R];
   __shared__ double resp[GMM_MAXN * 2], ev[GMM_MAXN];
   __shared__ int ord[GMM_MAXN], evi[GMM_MAXN];
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G,
     ev[j + 1] = v;
     evi[j + 1] = ix;
   }
-  const int r = max(1, min(GMM_R, n / 2 - 1));
+  const int r = rank > 0 ? min(min(rank, GMM_R), n) : max(1, min(GMM_R, n / 2 - 1));
   double zmax = 0.0;
   for (int i = 0; i < n; ++i)
     for (int k = 0; k < r; ++k) {
@@ -700,9 +700,10 @@ __global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G,
   info[2] = okc ? 1.0 : 0.0;
 }
 
-int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, hipStream_t s) {
-  if (n < 1 || n > GMM_MAXN) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_gmm_filter, dim3(1), dim3(64), 0, s, G, n, att, keep, info);
+int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, int rank,
+                   hipStream_t s) {
+  if (n < 1 || n > GMM_MAXN || rank < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gmm_filter, dim3(1), dim3(64), 0, s, G, n, att, keep, info, rank);
   return (int)hipGetLastError();
 }
 

@@ -175,8 +175,8 @@ def _gmm_case(n, seed):
     return U, att
 
 
-@pytest.mark.parametrize("n,seed", [(8, 0), (10, 1), (12, 2)])
-def test_gmm_filter_em_matches_sklearn_from_the_same_init(n, seed):
+@pytest.mark.parametrize("n,seed,rank", [(8, 0, None), (10, 1, None), (12, 2, None), (8, 0, 1), (10, 1, 2)])
+def test_gmm_filter_em_matches_sklearn_from_the_same_init(n, seed, rank):
     """The mirror's EM (after its deterministic k-means init) equals sklearn's GaussianMixture started from the
     same weights / means / precisions (reference train_gmm_model, src/Utils.py:257-262)."""
     import math as m_
@@ -185,11 +185,11 @@ def test_gmm_filter_em_matches_sklearn_from_the_same_init(n, seed):
 
     U, att = _gmm_case(n, seed)
     G = agg._centred_gram(U).numpy()
-    keep, thr, kept, ok = agg.gmm_filter_ref(G, att.numpy())
+    keep, thr, kept, ok = agg.gmm_filter_ref(G, att.numpy(), rank=rank)
     assert ok and 0 < kept <= n
     # independent PCA scores (eigh) and the same k-means init
     ev, V = np.linalg.eigh(G)
-    r = max(1, min(4, n // 2 - 1))
+    r = rank or max(1, min(4, n // 2 - 1))
     Z = V[:, ::-1][:, :r] * np.sqrt(np.maximum(ev[::-1][:r], 1e-30))
     Z = Z / np.abs(Z).max()
     X = np.vstack([Z[~att.numpy()], Z[att.numpy()]])

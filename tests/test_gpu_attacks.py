@@ -37,8 +37,8 @@ def test_fused_bisection_matches_generic_and_cpu(gpu, name, mode, fn, scale, mon
     assert torch.equal(fused.params, gen.params)
 
 
-@pytest.mark.parametrize("n,seed", [(8, 0), (10, 1), (12, 2), (5, 3)])
-def test_gmm_filter_kernel_matches_host_mirror(gpu, n, seed):
+@pytest.mark.parametrize("n,seed,rank", [(8, 0, 0), (10, 1, 0), (12, 2, 0), (5, 3, 0), (8, 0, 1), (12, 2, 2), (6, 4, 4)])
+def test_gmm_filter_kernel_matches_host_mirror(gpu, n, seed, rank):
     """agg.hip k_gmm_filter (the whole GMM decision in one launch) vs its fp64 host mirror."""
     from attackfl_amd import agg
     from attackfl_amd.ops import native
@@ -49,13 +49,15 @@ def test_gmm_filter_kernel_matches_host_mirror(gpu, n, seed):
     att = torch.zeros(n, dtype=torch.bool)
     att[n - 2:] = True
     G = agg._centred_gram(U)
-    keep, thr, kept, ok = agg.gmm_filter_ref(G.numpy(), att.numpy())
-    kd, info = native().gmm_filter(G.to(gpu), att.to(gpu, torch.uint8))
+    keep, thr, kept, ok = agg.gmm_filter_ref(G.numpy(), att.numpy(), rank=rank)
+    kd, info = native().gmm_filter(G.to(gpu), att.to(gpu, torch.uint8), rank)
     assert kd.bool().cpu().numpy().tolist() == keep.tolist()
     assert info[0].item() == pytest.approx(thr, rel=1e-9, abs=1e-12)
     assert int(info[1].item()) == kept and bool(info[2].item()) == ok
-    res = agg.gmm(U.to(gpu), torch.ones(n), attackers=att)
-    assert res.ok and torch.allclose(res.params.cpu(), U[torch.from_numpy(keep)].mean(0), atol=1e-6)
+    res = agg.gmm(U.to(gpu), torch.ones(n), attackers=att, gmm_rank=rank)
+    assert res.ok == (kept > 0)  # (nothing kept: the round fails)
+    if kept:
+        assert torch.allclose(res.params.cpu(), U[torch.from_numpy(keep)].mean(0), atol=1e-6)
 
 
 def test_gram_centred_matches_fp64_reference(gpu):

@@ -54,6 +54,7 @@ def run(rank: int, rounds: int = 12):
         print(json.dumps({"rank": rank, "round": rec.get("round"), "ok": rec.get("ok"), "metric": rec.get("metric"),
                           "kept_by_rank": seen.get("sets")}), flush=True)
     print(json.dumps({"rank": rank, "final_metric": eng.validation.last_metric}), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":
