@@ -18,6 +18,7 @@ computed locally and no scatter is needed.
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Optional, Dict, Sequence
 
@@ -25,6 +26,9 @@ import torch
 
 from .. import ops
 from ..models import PackedHyperNet
+
+# diagnostic A/B switch: generate_many through the torch MLP (7 small launches) instead of the native features
+_TORCH_GEN = bool(os.environ.get("AFL_HYPER_TORCH_GEN"))
 
 
 class HyperServer:
@@ -67,7 +71,14 @@ class HyperServer:
         c = self._gen_cache
         if c is not None and c[0] == key:
             return c[1]
-        out = self.hnet.generate_many(key)
+        if self._native_ok() and not _TORCH_GEN:
+            # MLP features of every client in one native launch, then one GEMM over the packed heads (the torch
+            # MLP was 7 small launches issued one by one on the round boundary)
+            h = self.hnet
+            feat = ops.hyper_features(h.arena, key, self.layout_vec())
+            out = torch.addmm(h.b[None, :], feat, h.W.t())
+        else:
+            out = self.hnet.generate_many(key)
         self._gen_cache = (key, out)
         return out
 

@@ -649,12 +649,35 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
   }
 }
 
+// MLP features of up to HF_MAXC clients in ONE launch (the START / validation models of a round: one workgroup
+// stages the embedding-MLP parameters once and runs hs_forward per client; was one k_hyper_small per client)
+constexpr int HF_MAXC = 64;
+struct HyClients {
+  int c[HF_MAXC];
+};
+__global__ void __launch_bounds__(HS_NT) k_hyper_feat_many(const float* __restrict__ A, HySmallDesc d, long nmlp,
+                                                           HyClients cl, int n, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];
+  __shared__ float acts[HS_LMAX + 1][HS_HMAX];
+  const int tid = threadIdx.x;
+  const long base = d.w[0];
+  for (long e = tid; e < nmlp; e += HS_NT) sm[e] = A[base + e];
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    hs_forward(A, sm, d, cl.c[k], acts);  // (its first barrier also orders the previous client's reads of acts)
+    if (tid < d.H) out[(long)k * d.H + tid] = acts[d.L][tid];
+    __syncthreads();
+  }
+}
+
 void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const int* clients, int n, float* out,
                         hipStream_t s) {
-  for (int k = 0; k < n; ++k)
-    hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, const_cast<float*>(A), nullptr, nullptr, nullptr, 0,
-                       -1, clients[k], out + (long)k * d.H, nullptr, d, offW - d.w[0], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
-                       nullptr);
+  for (int k0 = 0; k0 < n; k0 += HF_MAXC) {
+    HyClients cl{};
+    const int m = n - k0 < HF_MAXC ? n - k0 : HF_MAXC;
+    for (int k = 0; k < m; ++k) cl.c[k] = clients[k0 + k];
+    hipLaunchKernelGGL(k_hyper_feat_many, dim3(1), dim3(HS_NT), 0, s, A, d, offW - d.w[0], cl, m, out + (long)k0 * d.H);
+  }
 }
 
 long afl_hyper_small_capacity() { return HS_SMEM; }

@@ -228,6 +228,10 @@ def test_hyper_server_update_matches_composite(gpu, model, clip):
     cpu.hnet.arena.copy_(a)  # same parameters on both sides
     ref = torch.stack([cpu.hnet.features(i)[1] for i in (0, 2, 4)])
     assert torch.allclose(feats, ref, rtol=1e-4, atol=1e-5)
+    # the round's START models: native features + one GEMM (HyperServer.generate_many) vs the torch MLP path
+    many = dev.generate_many([4, 0, 2, 1]).cpu()
+    ref_many = dev.hnet.generate_many([4, 0, 2, 1]).cpu()
+    assert torch.allclose(many, ref_many, rtol=1e-4, atol=1e-5), float((many - ref_many).abs().max())
 
 
 @pytest.mark.gpu
