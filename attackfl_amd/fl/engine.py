@@ -438,18 +438,21 @@ class FLEngine:
         return out
 
     def _take_rows(self, pool: torch.Tensor, idx: List[int]) -> torch.Tensor:
-        """``pool[idx]`` with the index list on the device through a small cache: indexing a device tensor
-        with a Python list makes a pageable host -> device copy, which synchronises the stream (the host
-        would wait for the training launch already enqueued — the early launch's whole point)."""
+        """``pool[idx]`` with the index list on the device through a small cache and a pinned, non-blocking
+        upload: indexing a device tensor with a Python list (or a pageable ``.to``) makes a pageable host ->
+        device copy, which synchronises the stream — the host would wait for the training launch already
+        enqueued, the early launch's whole point (a random genuine sample misses the cache most rounds)."""
         if pool.device.type != "cuda":
             return pool[idx]
+        from ..ops.layers import upload
+
         key = tuple(idx)
         cache = self.__dict__.setdefault("_rows_idx", {})
         ix = cache.get(key)
         if ix is None:
             if len(cache) > 1024:
                 cache.clear()
-            ix = cache[key] = torch.tensor(idx, dtype=torch.long).to(pool.device)
+            ix = cache[key] = upload(torch.tensor(idx, dtype=torch.long), pool.device)
         return pool.index_select(0, ix)
 
     # ------------------------------------------------------------------------------------------
@@ -939,7 +942,7 @@ class FLEngine:
         # ---- genuine pool for the next START (non-attacker rows stored this round; only attackers read it) ----
         if self._has_attackers and attackers is not None and esl is None:
             keep = [k for k in range(stored) if not bool(attackers[k])]
-            self.genuine_pool = U[keep].clone() if keep else None
+            self.genuine_pool = self._take_rows(U, keep) if keep else None  # (index_select: a new tensor)
             if (keep and keep[0] == 0 and round_ok and self.mode == "fedavg" and self.global_params is not None
                     and self.cfg.engine.get("compat-fedavg-alias", False)):
                 # A-13: the reference averages INTO the first stored update's dict, which is also the first
@@ -1074,7 +1077,7 @@ class FLEngine:
         keep = None
         if self._has_attackers:  # the pool of a fully stored round (before the next START overwrites U)
             keep = [k for k, i in enumerate(self.selected) if self.table[i].attack is None]
-            self.genuine_pool = U[keep].clone() if keep else None
+            self.genuine_pool = self._take_rows(U, keep) if keep else None  # (index_select: a new tensor)
         self.global_params = g
         if self.mode != "hyper":
             self._prefetch_validation(g)
