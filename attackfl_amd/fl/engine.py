@@ -517,6 +517,26 @@ class FLEngine:
         self._stage(prep, self._attack_decisions(prep))
         return prep
 
+    def _prepare_staged(self) -> dict:
+        """``_prepare_local`` with its device half (the upload and the plan kernel) on a staging stream: those
+        depend on nothing the running training writes, and on the compute stream they sat behind it, in the gap
+        between two training kernels.  The launch waits for the staging event (``_enqueue_local``)."""
+        dev = self.device
+        if dev.type != "cuda":
+            return self._prepare_local()
+        if getattr(self, "_stage_stream", None) is None:
+            self._stage_stream = torch.cuda.Stream(device=dev)
+        main = torch.cuda.current_stream(dev)
+        with torch.cuda.stream(self._stage_stream):
+            prep = self._prepare_local()
+            ev = torch.cuda.Event()
+            ev.record(self._stage_stream)
+        plan = prep.get("plan")
+        if plan is not None and plan.order.is_cuda:
+            plan.order.record_stream(main)  # (allocated on the staging stream, read by the launch on main)
+        prep["staged_ev"] = ev
+        return prep
+
     @staticmethod
     def _attack_decisions(prep: dict) -> tuple:
         return tuple(lc.info.attack is not None and lc.training_round >= lc.info.attack.round
@@ -577,6 +597,8 @@ class FLEngine:
         cfg = self.cfg
         dev = self.device
         tq = time.perf_counter()
+        if prep.get("staged_ev") is not None:  # uploads / plan staged on the staging stream (_prepare_staged)
+            torch.cuda.current_stream(dev).wait_event(prep["staged_ev"])
         for j, i, lc, _ in prep["clients"]:
             g = genuine.get(i)
             if lc.info.attack is not None and g is not None and g.shape[0] > 0:
@@ -857,7 +879,7 @@ class FLEngine:
             if self._speculative and self.rounds_left > 1 and not last and self._next_prep is None:
                 # the next launch's host half (draws, uploads, plan) while this round's training runs: after
                 # it, only the aggregate, START and the launch itself separate two training kernels
-                self._next_prep = self._prepare_local()
+                self._next_prep = self._prepare_staged()
             esl = self._early_launch(st, last)
             block = self._finish_local(st)
             if self.phase_sync:  # stream-ordered otherwise: the timing-only sync is skipped
@@ -1056,10 +1078,12 @@ class FLEngine:
                 return None
             n = len(self.selected)
             U = self.local_params[:n]
-            ok_all = (st["pending"].ok_device()[:n] > 0).all()
+            ok_n = st["pending"].ok_device()[:n]
+            ok_all = None if self.mode != "hyper" else (ok_n > 0).all()  # (FedAvg: decided inside the aggregate)
             w = st["fedavg_w"]
         else:  # several ranks: called on the gathered rows (device), before the host reads their meta
             P = self.P
+            ok_n = None
             ok_all = ((sel[:, P] > 0.5) & (sel[:, P + 1] > 0.5)).all()
             s = sel[:, P + 2].double()
             w = s / s.sum()
@@ -1073,7 +1097,12 @@ class FLEngine:
                              enable=ok_all.to(torch.int32).reshape(1))
             g = g_old
         else:
-            g = torch.where(ok_all, ops.weighted_rows(U, w), g_old)
+            if ok_n is not None and ok_n.dtype == torch.int32 and g_old is not None:
+                g = ops.weighted_rows(U, w, ok_n, g_old)  # (the success check fused into the aggregate's pass)
+            else:
+                if ok_all is None:
+                    ok_all = (ok_n > 0).all()
+                g = torch.where(ok_all, ops.weighted_rows(U, w), g_old)
         keep = None
         if self._has_attackers:  # the pool of a fully stored round (before the next START overwrites U)
             keep = [k for k, i in enumerate(self.selected) if self.table[i].attack is None]

@@ -342,9 +342,7 @@ class FusedTrainer:
         # (two blocking .cpu() reads cost two host round trips between the round's training and its aggregate)
         C, E = losses.shape
         buf = self._pinned(C, E)
-        buf.copy_(torch.cat([ok.to(torch.float32)[:, None], losses], 1), non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(self.device))
+        done = self._readback(ok, losses, buf)
 
         def fin():
             # poll instead of a blocking wait: the host then wakes within microseconds of the launch's end
@@ -357,6 +355,33 @@ class FusedTrainer:
             return [bool(x) for x in okh.tolist()], buf[:, 1:].clone()
 
         return Pending(fin, ok, losses)
+
+    def _readback(self, ok: torch.Tensor, losses: torch.Tensor, buf: torch.Tensor) -> torch.cuda.Event:
+        """Enqueue the result copy; returns its event.  When the launch leaves most CUs free (the on-chip trainers
+        at a few clients per rank) the copy goes on a read-back stream that waits for the training: the compute
+        stream then runs the round's aggregate and the next launch right away instead of three small kernels
+        later.  A launch that fills the GPU keeps the copy on the compute stream (on another stream the copy
+        could wait behind the NEXT launch's persistent workgroups)."""
+        dev = self.device
+        main = torch.cuda.current_stream(dev)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        side = 3 * ok.shape[0] * 2 <= cus
+        if side:
+            rs = getattr(self, "_rb_stream", None)
+            if rs is None:
+                rs = self._rb_stream = torch.cuda.Stream(device=dev)
+            trained = torch.cuda.Event()
+            trained.record(main)
+            rs.wait_event(trained)
+            ok.record_stream(rs)
+            losses.record_stream(rs)
+        else:
+            rs = main
+        with torch.cuda.stream(rs):
+            buf.copy_(torch.cat([ok.to(torch.float32)[:, None], losses], 1), non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(rs)
+        return done
 
     def _pinned(self, C: int, E: int) -> torch.Tensor:
         """Pinned [C, 1 + E] result buffers, a ring of 3 (a launch's result is read before the launch after

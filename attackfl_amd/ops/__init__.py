@@ -271,10 +271,16 @@ def attack_coeffs_segments(G: torch.Tensor, mean: torch.Tensor, dev: torch.Tenso
 
 
 # ---------------------------------------------------------------- aggregation
-def weighted_rows(U: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def weighted_rows(U: torch.Tensor, w: torch.Tensor, ok: Optional[torch.Tensor] = None,
+                  fallback: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """sum_i w_i U_i; with ``ok`` / ``fallback``: ``fallback`` unless every ``ok`` > 0 (one pass on the device)."""
     if _dev(U):
+        if ok is not None:
+            return native().weighted_rows(U.contiguous(), w.to(device=U.device, dtype=torch.float64).contiguous(),
+                                          ok.to(torch.int32).contiguous(), fallback.contiguous())
         return native().weighted_rows(U.contiguous(), w.to(device=U.device, dtype=torch.float64).contiguous())
-    return composite.weighted_rows(U, w)
+    out = composite.weighted_rows(U, w)
+    return out if ok is None else torch.where((ok > 0).all(), out, fallback)
 
 
 def fedavg(U: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:

@@ -310,14 +310,25 @@ torch::Tensor spectral_norm_slots(torch::Tensor D, torch::Tensor tab, int64_t ma
   return out;
 }
 
-torch::Tensor weighted_rows(torch::Tensor U, torch::Tensor w) {
+torch::Tensor weighted_rows(torch::Tensor U, torch::Tensor w, c10::optional<torch::Tensor> ok,
+                            c10::optional<torch::Tensor> fallback) {
   check_dev(U, "U", torch::kFloat32);
   check_dev(w, "w", torch::kFloat64);
   const int N = U.size(0);
   const long P = U.size(1);
   TORCH_CHECK(w.numel() == N, "w must have N entries");
+  TORCH_CHECK(ok.has_value() == fallback.has_value(), "weighted_rows: ok and fallback go together");
+  const int* okp = nullptr;
+  const float* fb = nullptr;
+  if (ok.has_value()) {
+    check_dev(*ok, "ok", torch::kInt32);
+    check_dev(*fallback, "fallback", torch::kFloat32);
+    TORCH_CHECK(ok->numel() == N && fallback->numel() == P, "weighted_rows: ok [N], fallback [P]");
+    okp = ok->data_ptr<int>();
+    fb = fallback->data_ptr<float>();
+  }
   auto out = torch::empty({P}, U.options());
-  afl_weighted_rows(U.data_ptr<float>(), w.data_ptr<double>(), N, P, out.data_ptr<float>(), cur());
+  afl_weighted_rows(U.data_ptr<float>(), w.data_ptr<double>(), N, P, out.data_ptr<float>(), cur(), okp, fb);
   AFL_CHECK_LAUNCH();
   return out;
 }
@@ -751,7 +762,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spec_eval", &spec_eval);
   m.def("spec_bisect", &spec_bisect);
   m.def("bisect_vec", &bisect_vec);
-  m.def("weighted_rows", &weighted_rows);
+  m.def("weighted_rows", &weighted_rows, pybind11::arg("U"), pybind11::arg("w"), pybind11::arg("ok") = pybind11::none(),
+        pybind11::arg("fallback") = pybind11::none());
   m.def("coord_select", &coord_select);
   m.def("row_dots", &row_dots);
   m.def("gmm_filter", &gmm_filter, pybind11::arg("G"), pybind11::arg("att"), pybind11::arg("rank") = 0);

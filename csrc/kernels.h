@@ -7,7 +7,8 @@
 // agg.hip
 void afl_colstats(const float* G, int K, long P, float* mean, float* stdv, float* out, float z, int mode,
                   hipStream_t s);
-void afl_weighted_rows(const float* U, const double* w, int N, long P, float* out, hipStream_t s);
+void afl_weighted_rows(const float* U, const double* w, int N, long P, float* out, hipStream_t s,
+                       const int* ok = nullptr, const float* fallback = nullptr);
 int afl_pair_sqdist_nblocks(long P);
 void afl_pair_sqdist(const float* G, int K, long P, double* partial, double* D, hipStream_t s);
 void afl_seg_reduce(int mode, const float* X, long P, int rows, const float* mean, const float* dev, const int* tiles,

@@ -42,17 +42,28 @@ void afl_colstats(const float* G, int K, long P, float* mean, float* stdv, float
 }
 
 // ============================================================================ weighted rows
+// ok (optional, int32 [N]): every entry > 0 -> the weighted sum, else out = fallback (FedAvg keeps the previous global
+// model when a client failed: the early-launch aggregate, decided on the device in the same pass)
 __global__ void __launch_bounds__(256) k_weighted_rows(const float* __restrict__ U, const double* __restrict__ w, int N,
-                                                       long P, float* __restrict__ out) {
+                                                       long P, float* __restrict__ out, const int* __restrict__ ok,
+                                                       const float* __restrict__ fallback) {
   long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P) return;
+  bool all_ok = true;
+  if (ok != nullptr)
+    for (int i = 0; i < N; ++i) all_ok = all_ok && ok[i] > 0;
+  if (!all_ok) {
+    out[c] = fallback[c];
+    return;
+  }
   double acc = 0.0;
   for (int i = 0; i < N; ++i) acc += w[i] * (double)U[(long)i * P + c];
   out[c] = (float)acc;
 }
 
-void afl_weighted_rows(const float* U, const double* w, int N, long P, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_weighted_rows, dim3(afl_cdiv(P, 256)), dim3(256), 0, s, U, w, N, P, out);
+void afl_weighted_rows(const float* U, const double* w, int N, long P, float* out, hipStream_t s, const int* ok,
+                       const float* fallback) {
+  hipLaunchKernelGGL(k_weighted_rows, dim3(afl_cdiv(P, 256)), dim3(256), 0, s, U, w, N, P, out, ok, fallback);
 }
 
 // ============================================================================ pairwise sq-dist

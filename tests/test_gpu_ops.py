@@ -281,3 +281,25 @@ def test_philox_noise_matches_cpu_mirror(gpu, P):
         ref = ops.noise(own, 0.3, seed)
         assert torch.allclose(got, ref, atol=2e-6, rtol=0)
         assert torch.equal(ops.noise(own.cuda(), 0.3, seed).cpu(), got)   # deterministic
+
+
+@pytest.mark.gpu
+def test_weighted_rows_with_success_check(gpu):
+    """FedAvg's early-launch aggregate: the weighted sum when every client succeeded, the fallback (previous
+    global model) otherwise — decided inside the same pass (agg.hip k_weighted_rows ok / fallback)."""
+    from attackfl_amd import ops
+
+    g = torch.Generator().manual_seed(3)
+    U = torch.randn(7, 5003, generator=g)
+    w = torch.rand(7, generator=g, dtype=torch.float64)
+    w = w / w.sum()
+    old = torch.randn(5003, generator=g)
+    ref = (w[:, None] * U.double()).sum(0).float()
+    Ud, wd, oldd = U.to(gpu), w.to(gpu), old.to(gpu)
+    ok = torch.ones(7, dtype=torch.int32, device=gpu)
+    assert torch.allclose(ops.weighted_rows(Ud, wd, ok, oldd).cpu(), ref, atol=1e-6)
+    assert torch.equal(ops.weighted_rows(Ud, wd).cpu(), ops.weighted_rows(Ud, wd, ok, oldd).cpu())
+    ok[4] = 0
+    assert torch.equal(ops.weighted_rows(Ud, wd, ok, oldd).cpu(), old)
+    # CPU composite: same decision
+    assert torch.equal(ops.weighted_rows(U, w, ok.cpu(), old), old)
