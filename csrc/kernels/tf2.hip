@@ -763,11 +763,7 @@ __device__ __forceinline__ bool br_update(uchar* smem, BrState& st, const AdamK&
   if (lead) {
     // the leaders' ffn tiles run below the laggards' backward on the same SIMD (priority 0: +1.9 % against 2,
     // +1.7 % at 1; profiles/ab_tf2_r6_update.log), the out_proj unit after A at the critical priority again
-#ifndef TF2_LEAD_PRIO
     prio_lo();
-#else  // A/B variant
-    __builtin_amdgcn_s_setprio(TF2_LEAD_PRIO);
-#endif
     if (!lds_wait(smem, B_CNT_C, all)) {
       if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
@@ -1087,12 +1083,7 @@ __device__ __forceinline__ void branch_main(const AflTfTrainArgs& a, int cid, uc
     u32x4 du[2];
     const int go[1] = {gr_off(1, BR, wave, lane)};
     const uint32_t fv = gr_get<1>(rg, go, du, (uint32_t)step, 1, sync + XF_TMO, lane);  // d(out) of this wave's rows
-#ifdef TF2_BWD_PRIO_SPLIT  // A/B variant: the leaders' backward (started first) below the laggards' on the same SIMD
-    if (wave < 4) __builtin_amdgcn_s_setprio(1);
-    else prio_hi();
-#else
-    prio_hi();
-#endif
+    prio_hi();  // (the leaders' backward below the laggards' measured -0.5 %: profiles/ab_tf2_r6_update.log)
     stp(2, tid);
     if (fv == 0xFFFFFFFFu) {  // timed out: abort the step for every wave (they wait on this wave's progress)
       if (lane == 0) abort_w[wave] = 1u;
@@ -1218,12 +1209,7 @@ __device__ __forceinline__ void head_main(const AflTfTrainArgs& a, int cid, ucha
       timed_out = failed = true;
       break;
     }
-#ifdef TF2_HEAD_PRIO_SPLIT  // A/B variant: head waves 0-3 (their rows arrive first) below waves 4-7
-    if (wave < 4) __builtin_amdgcn_s_setprio(1);
-    else prio_hi();
-#else
-    prio_hi();
-#endif
+    prio_hi();  // (head waves 0-3 below 4-7 measured -7 %: profiles/ab_tf2_r6_update.log)
     stp(10, tid);
     // (the dW operands of this step — cat, a1, dz1, dz2 tiles — and the head's column sums are written
     // only AFTER the d(cat) hand-off below: they are off the branches' critical path)
