@@ -210,6 +210,46 @@ constexpr int HS_LMAX = 8;
 constexpr int HS_NT = 1024;          // threads of the small-net workgroup (16 waves)
 constexpr int HS_SMEM = 28 * 1024;   // floats of MLP parameters staged in LDS (112 KB)
 
+// stage n floats (16-byte aligned source and destination when n4 mode) into LDS with every load of a thread in
+// flight: clamped indices (a conditional load per slot made the compiler keep the batch in scratch and wait for
+// each load in turn: 8 serial round trips per batch)
+__device__ __forceinline__ void hs_stage(float* __restrict__ dst, const float* __restrict__ src, long n) {
+  const int tid = threadIdx.x;
+  if (n <= 0) return;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && (n & 3) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const long n4 = n / 4;
+    for (long e0 = tid; e0 < n4; e0 += 8 * HS_NT) {
+      float4 t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const long e = e0 + q * HS_NT;
+        t[q] = s4[e < n4 ? e : n4 - 1];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const long e = e0 + q * HS_NT;
+        if (e < n4) d4[e] = t[q];
+      }
+    }
+  } else {
+    for (long e0 = tid; e0 < n; e0 += 8 * HS_NT) {
+      float t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const long e = e0 + q * HS_NT;
+        t[q] = src[e < n ? e : n - 1];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const long e = e0 + q * HS_NT;
+        if (e < n) dst[e] = t[q];
+      }
+    }
+  }
+}
+
 // relu that keeps NaN like torch.relu
 __device__ __forceinline__ float hs_relu(float z) { return z < 0.f ? 0.f : z; }
 
@@ -278,32 +318,26 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = d.H, L = d.L, E = d.E;
   const long base = d.w[0];
-  // stage the MLP parameters (contiguous [w_0 .. b_{L-1}]) in LDS, float4 when aligned
-  if ((base & 3) == 0 && (nmlp & 3) == 0) {
-    const float4* src = reinterpret_cast<const float4*>(A + base);
-    float4* dst = reinterpret_cast<float4*>(sm);
-    const long n4 = nmlp / 4;
-    for (long e0 = tid; e0 < n4; e0 += 8 * HS_NT) {  // 8 loads in flight per thread
-      float4 t[8];
+  // the rows kernel's per-block partials (nb <= 256): 8 lanes per column, all 32 loads of a lane in flight and
+  // issued ahead of the staging loads below (the two latencies overlap; summed in the same order as before)
+  float pt[32];
+  {
+    const int c = tid >> 3, sub = tid & 7;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (e0 + q * HS_NT < n4) t[q] = src[e0 + q * HS_NT];
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (e0 + q * HS_NT < n4) dst[e0 + q * HS_NT] = t[q];
+    for (int k = 0; k < 32; ++k) {
+      const int bb = sub + 8 * k;
+      pt[k] = (ci >= 0 && c <= H && bb < nb) ? partial[(long)bb * (H + 1) + c] : 0.f;
     }
-  } else {
-    for (long e = tid; e < nmlp; e += HS_NT) sm[e] = A[base + e];
   }
+  // stage the MLP parameters (contiguous [w_0 .. b_{L-1}]) in LDS
+  hs_stage(sm, A + base, nmlp);
   if (ci >= 0) {
-    const int P1 = H + 1;
     // reduce the rows kernel's per-block partials: 8 lanes per column (W^T delta [H] and |delta|^2)
     {
       const int c = tid >> 3, sub = tid & 7;
       float s = 0.f;
-      if (c <= H)
-#pragma unroll 8
-        for (int bb = sub; bb < nb; bb += 8) s += partial[(long)bb * P1 + c];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) s += pt[k];  // (zeros past nb: adding +0.0 leaves every partial sum unchanged)
       s = hs_sum8(s);
       if (c <= H && sub == 0) {
         if (c < H) dz[L - 1][c] = s;
@@ -380,11 +414,11 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
         for (long e0 = tid; e0 < n4; e0 += 4 * HS_NT) {
           float4 mm[4], vv[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (e0 + q * HS_NT < n4) {
-              mm[q] = m4[e0 + q * HS_NT];
-              vv[q] = v4[e0 + q * HS_NT];
-            }
+          for (int q = 0; q < 4; ++q) {  // (clamped: every load of the batch in flight, see hs_stage)
+            const long e = e0 + q * HS_NT < n4 ? e0 + q * HS_NT : n4 - 1;
+            mm[q] = m4[e];
+            vv[q] = v4[e];
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const long e4 = e0 + q * HS_NT;
@@ -661,7 +695,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_feat_many(const float* __restri
   __shared__ float acts[HS_LMAX + 1][HS_HMAX];
   const int tid = threadIdx.x;
   const long base = d.w[0];
-  for (long e = tid; e < nmlp; e += HS_NT) sm[e] = A[base + e];
+  hs_stage(sm, A + base, nmlp);
   __syncthreads();
   for (int k = 0; k < n; ++k) {
     hs_forward(A, sm, d, cl.c[k], acts);  // (its first barrier also orders the previous client's reads of acts)
