@@ -499,7 +499,8 @@ void afl_adam_flat(float* p, const float* g, float* m, float* v, long n, int ste
 //      draws from an unseeded RNG in the reference, so any fixed init is one of its possible runs;
 //   3. threshold = 3 x population std of the benign rows' Mahalanobis distances to component 0; a row is kept
 //      when its distance to its most probable component is <= threshold.
-// One lane does the O(n^3 + 100 n r^2) work (n <= 64); agg.gmm_filter_ref in Python is the bit-level mirror.
+// One wave: the Jacobi rotations are applied by lane k to row / column k, the E-step and the decisions run one lane
+// per row, every sum stays on lane 0 in row order; agg.gmm_filter_ref in Python is the bit-level mirror.
 constexpr int GMM_MAXN = 64, GMM_R = 4;
 
 __device__ __host__ inline bool gmm_chol(const double (&S)[GMM_R][GMM_R], int r, double (&Lc)[GMM_R][GMM_R]) {
@@ -538,133 +539,147 @@ __global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G,
     V[e] = (e / n == e % n) ? 1.0 : 0.0;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  // ---- 1. Jacobi eigen-decomposition (cyclic sweeps, fixed count)
+  // ---- 1. Jacobi eigen-decomposition (cyclic sweeps, fixed count): every lane derives the rotation, lane k applies
+  //      it to row / column k (the same element operations in the same order as the single-lane form and the host
+  //      mirror; one lane walking the n^2 updates serially through LDS took ~0.6 ms for n = 8)
+  const int k = threadIdx.x;
   for (int sweep = 0; sweep < 12; ++sweep)
     for (int p = 0; p < n - 1; ++p)
       for (int q = p + 1; q < n; ++q) {
         const double apq = A[p * n + q];
-        if (fabs(apq) < 1e-300) continue;
+        if (fabs(apq) < 1e-300) continue;  // (uniform: every lane read the same word)
         const double th = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
         const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
         const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-        for (int k = 0; k < n; ++k) {  // columns p, q
+        __syncthreads();  // every lane has read A[p][p], A[q][q], A[p][q] before they change
+        if (k < n) {  // columns p, q
           const double akp = A[k * n + p], akq = A[k * n + q];
           A[k * n + p] = c * akp - s * akq;
           A[k * n + q] = s * akp + c * akq;
         }
-        for (int k = 0; k < n; ++k) {  // rows p, q
+        __syncthreads();
+        if (k < n) {  // rows p, q; eigenvectors
           const double apk = A[p * n + k], aqk = A[q * n + k];
           A[p * n + k] = c * apk - s * aqk;
           A[q * n + k] = s * apk + c * aqk;
-        }
-        for (int k = 0; k < n; ++k) {
           const double vkp = V[k * n + p], vkq = V[k * n + q];
           V[k * n + p] = c * vkp - s * vkq;
           V[k * n + q] = s * vkp + c * vkq;
         }
+        __syncthreads();
       }
-  for (int i = 0; i < n; ++i) {
-    ev[i] = A[i * n + i];
-    evi[i] = i;
-  }
-  for (int i = 1; i < n; ++i) {  // stable insertion sort, descending
-    const double v = ev[i];
-    const int ix = evi[i];
-    int j = i - 1;
-    while (j >= 0 && ev[j] < v) {
-      ev[j + 1] = ev[j];
-      evi[j + 1] = evi[j];
-      --j;
+  // ---- the rest: one lane, except the E-step and the decisions (lane i = row i; the sums stay on lane 0 in row
+  //      order, so every value equals the single-lane form's and the host mirror's)
+  __shared__ double mu[2][GMM_R], w[2], cov[2][GMM_R][GMM_R], Lc[2][GMM_R][GMM_R], logdet[2], lse_row[GMM_MAXN];
+  __shared__ int sh_r, sh_m, sh_nb, sh_K, sh_okc, sh_stop;
+  __shared__ double sh_thr;
+  if (k == 0) {
+    for (int i = 0; i < n; ++i) {
+      ev[i] = A[i * n + i];
+      evi[i] = i;
     }
-    ev[j + 1] = v;
-    evi[j + 1] = ix;
-  }
-  const int r = rank > 0 ? min(min(rank, GMM_R), n) : max(1, min(GMM_R, n / 2 - 1));
-  double zmax = 0.0;
-  for (int i = 0; i < n; ++i)
-    for (int k = 0; k < r; ++k) {
-      const double z = V[i * n + evi[k]] * sqrt(fmax(ev[k], 1e-30));
-      Z[i * GMM_R + k] = z;
-      zmax = fmax(zmax, fabs(z));
-    }
-  zmax = fmax(zmax, 1e-30);
-  int m = 0, nb = 0;
-  for (int i = 0; i < n; ++i)
-    if (!att[i]) ord[m++] = i;
-  nb = m;
-  for (int i = 0; i < n; ++i)
-    if (att[i]) ord[m++] = i;
-  for (int i = 0; i < n; ++i)
-    for (int k = 0; k < r; ++k) Z[i * GMM_R + k] /= zmax;
-  for (int i = 0; i < m; ++i)
-    for (int k = 0; k < r; ++k) X[i * GMM_R + k] = Z[ord[i] * GMM_R + k];
-  const int K = m >= 2 ? 2 : 1;
-  // ---- 2a. deterministic k-means initialisation
-  double mu[2][GMM_R];
-  for (int k = 0; k < r; ++k) mu[0][k] = mu[1][k] = X[k];
-  if (K == 2) {
-    int far = 0;
-    double best = -1.0;
-    for (int i = 0; i < m; ++i) {
-      double d = 0.0;
-      for (int k = 0; k < r; ++k) d += (X[i * GMM_R + k] - X[k]) * (X[i * GMM_R + k] - X[k]);
-      if (d > best) {
-        best = d;
-        far = i;
+    for (int i = 1; i < n; ++i) {  // stable insertion sort, descending
+      const double v = ev[i];
+      const int ix = evi[i];
+      int j = i - 1;
+      while (j >= 0 && ev[j] < v) {
+        ev[j + 1] = ev[j];
+        evi[j + 1] = evi[j];
+        --j;
       }
+      ev[j + 1] = v;
+      evi[j + 1] = ix;
     }
-    for (int k = 0; k < r; ++k) mu[1][k] = X[far * GMM_R + k];
-    for (int it = 0; it < 10; ++it) {
-      double s[2][GMM_R] = {}, cnt[2] = {0.0, 0.0};
+    const int r = rank > 0 ? min(min(rank, GMM_R), n) : max(1, min(GMM_R, n / 2 - 1));
+    double zmax = 0.0;
+    for (int i = 0; i < n; ++i)
+      for (int kk = 0; kk < r; ++kk) {
+        const double z = V[i * n + evi[kk]] * sqrt(fmax(ev[kk], 1e-30));
+        Z[i * GMM_R + kk] = z;
+        zmax = fmax(zmax, fabs(z));
+      }
+    zmax = fmax(zmax, 1e-30);
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+      if (!att[i]) ord[m++] = i;
+    const int nb = m;
+    for (int i = 0; i < n; ++i)
+      if (att[i]) ord[m++] = i;
+    for (int i = 0; i < n; ++i)
+      for (int kk = 0; kk < r; ++kk) Z[i * GMM_R + kk] /= zmax;
+    for (int i = 0; i < m; ++i)
+      for (int kk = 0; kk < r; ++kk) X[i * GMM_R + kk] = Z[ord[i] * GMM_R + kk];
+    const int K = m >= 2 ? 2 : 1;
+    // ---- 2a. deterministic k-means initialisation
+    for (int kk = 0; kk < r; ++kk) mu[0][kk] = mu[1][kk] = X[kk];
+    if (K == 2) {
+      int far = 0;
+      double best = -1.0;
       for (int i = 0; i < m; ++i) {
-        double d0 = 0.0, d1 = 0.0;
-        for (int k = 0; k < r; ++k) {
-          d0 += (X[i * GMM_R + k] - mu[0][k]) * (X[i * GMM_R + k] - mu[0][k]);
-          d1 += (X[i * GMM_R + k] - mu[1][k]) * (X[i * GMM_R + k] - mu[1][k]);
+        double d = 0.0;
+        for (int kk = 0; kk < r; ++kk) d += (X[i * GMM_R + kk] - X[kk]) * (X[i * GMM_R + kk] - X[kk]);
+        if (d > best) {
+          best = d;
+          far = i;
         }
-        const int l = d1 < d0 ? 1 : 0;
-        resp[i * 2 + 0] = l == 0 ? 1.0 : 0.0;
-        resp[i * 2 + 1] = l == 1 ? 1.0 : 0.0;
-        cnt[l] += 1.0;
-        for (int k = 0; k < r; ++k) s[l][k] += X[i * GMM_R + k];
       }
-      for (int c = 0; c < 2; ++c)
-        if (cnt[c] > 0.0)
-          for (int k = 0; k < r; ++k) mu[c][k] = s[c][k] / cnt[c];
+      for (int kk = 0; kk < r; ++kk) mu[1][kk] = X[far * GMM_R + kk];
+      for (int it = 0; it < 10; ++it) {
+        double sm[2][GMM_R] = {}, cnt[2] = {0.0, 0.0};
+        for (int i = 0; i < m; ++i) {
+          double d0 = 0.0, d1 = 0.0;
+          for (int kk = 0; kk < r; ++kk) {
+            d0 += (X[i * GMM_R + kk] - mu[0][kk]) * (X[i * GMM_R + kk] - mu[0][kk]);
+            d1 += (X[i * GMM_R + kk] - mu[1][kk]) * (X[i * GMM_R + kk] - mu[1][kk]);
+          }
+          const int l = d1 < d0 ? 1 : 0;
+          resp[i * 2 + 0] = l == 0 ? 1.0 : 0.0;
+          resp[i * 2 + 1] = l == 1 ? 1.0 : 0.0;
+          cnt[l] += 1.0;
+          for (int kk = 0; kk < r; ++kk) sm[l][kk] += X[i * GMM_R + kk];
+        }
+        for (int c = 0; c < 2; ++c)
+          if (cnt[c] > 0.0)
+            for (int kk = 0; kk < r; ++kk) mu[c][kk] = sm[c][kk] / cnt[c];
+      }
+    } else {
+      for (int i = 0; i < m; ++i) {
+        resp[i * 2] = 1.0;
+        resp[i * 2 + 1] = 0.0;
+      }
     }
-  } else {
-    for (int i = 0; i < m; ++i) {
-      resp[i * 2] = 1.0;
-      resp[i * 2 + 1] = 0.0;
-    }
+    sh_r = r;
+    sh_m = m;
+    sh_nb = nb;
+    sh_K = K;
+    sh_okc = 1;
   }
+  __syncthreads();
+  const int r = sh_r, m = sh_m, nb = sh_nb, K = sh_K;
   // ---- 2b. EM (sklearn GaussianMixture, covariance_type "full")
   const double eps10 = 10.0 * 2.220446049250313e-16, reg = 1e-6, LOG2PI = 1.8378770664093453;
-  double w[2], cov[2][GMM_R][GMM_R], Lc[2][GMM_R][GMM_R], logdet[2];
-  bool okc = true;
-  auto mstep = [&]() {
+  auto mstep = [&]() {  // (lane 0)
     double nks = 0.0;
     for (int c = 0; c < K; ++c) {
       double nk = eps10;
       for (int i = 0; i < m; ++i) nk += resp[i * 2 + c];
-      for (int k = 0; k < r; ++k) {
-        double s = 0.0;
-        for (int i = 0; i < m; ++i) s += resp[i * 2 + c] * X[i * GMM_R + k];
-        mu[c][k] = s / nk;
+      for (int kk = 0; kk < r; ++kk) {
+        double sv = 0.0;
+        for (int i = 0; i < m; ++i) sv += resp[i * 2 + c] * X[i * GMM_R + kk];
+        mu[c][kk] = sv / nk;
       }
       for (int a = 0; a < r; ++a)
         for (int b = 0; b < r; ++b) {
-          double s = 0.0;
+          double sv = 0.0;
           for (int i = 0; i < m; ++i)
-            s += resp[i * 2 + c] * (X[i * GMM_R + a] - mu[c][a]) * (X[i * GMM_R + b] - mu[c][b]);
-          cov[c][a][b] = s / nk + (a == b ? reg : 0.0);
+            sv += resp[i * 2 + c] * (X[i * GMM_R + a] - mu[c][a]) * (X[i * GMM_R + b] - mu[c][b]);
+          cov[c][a][b] = sv / nk + (a == b ? reg : 0.0);
         }
       w[c] = nk;
       nks += nk;
-      okc = okc && gmm_chol(cov[c], r, Lc[c]);
+      sh_okc = sh_okc && gmm_chol(cov[c], r, Lc[c]);
       double ld = 0.0;
-      for (int k = 0; k < r; ++k) ld += log(Lc[c][k][k]);
+      for (int kk = 0; kk < r; ++kk) ld += log(Lc[c][kk][kk]);
       logdet[c] = 2.0 * ld;
     }
     for (int c = 0; c < K; ++c) w[c] /= nks;
@@ -672,43 +687,62 @@ __global__ void __launch_bounds__(64) k_gmm_filter(const double* __restrict__ G,
   auto wlogp = [&](const double* x, int c) {
     return log(w[c]) - 0.5 * (r * LOG2PI + gmm_md2(Lc[c], r, x, mu[c]) + logdet[c]);
   };
-  mstep();
-  double lb = -INFINITY;
-  for (int it = 0; it < 100 && okc; ++it) {
-    const double prev = lb;
-    double tot = 0.0;
-    for (int i = 0; i < m; ++i) {
-      double lp[2] = {wlogp(X + i * GMM_R, 0), K == 2 ? wlogp(X + i * GMM_R, 1) : -INFINITY};
+  if (k == 0) {
+    mstep();
+    sh_stop = sh_okc ? 0 : 1;
+  }
+  __syncthreads();
+  double lb = -INFINITY;  // (lane 0's copy is the one that decides)
+  for (int it = 0; it < 100 && !sh_stop; ++it) {
+    if (k < m) {  // E-step, lane k = row k
+      const double* x = X + k * GMM_R;
+      double lp[2] = {wlogp(x, 0), K == 2 ? wlogp(x, 1) : -INFINITY};
       const double mx = fmax(lp[0], lp[1]);
       const double lse = mx + log(exp(lp[0] - mx) + exp(lp[1] - mx));
-      tot += lse;
-      resp[i * 2] = exp(lp[0] - lse);
-      resp[i * 2 + 1] = K == 2 ? exp(lp[1] - lse) : 0.0;
+      lse_row[k] = lse;
+      resp[k * 2] = exp(lp[0] - lse);
+      resp[k * 2 + 1] = K == 2 ? exp(lp[1] - lse) : 0.0;
     }
-    mstep();
-    lb = tot / m;
-    if (fabs(lb - prev) < 1e-3) break;
+    __syncthreads();
+    if (k == 0) {
+      const double prev = lb;
+      double tot = 0.0;
+      for (int i = 0; i < m; ++i) tot += lse_row[i];
+      mstep();
+      lb = tot / m;
+      sh_stop = (!sh_okc || fabs(lb - prev) < 1e-3) ? 1 : 0;
+    }
+    __syncthreads();
   }
   // ---- 3. threshold and decisions
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < nb; ++i) s1 += sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0]));
-  const double meanb = nb ? s1 / nb : 0.0;
-  for (int i = 0; i < nb; ++i) {
-    const double d = sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0])) - meanb;
-    s2 += d * d;
+  if (k == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < nb; ++i) s1 += sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0]));
+    const double meanb = nb ? s1 / nb : 0.0;
+    for (int i = 0; i < nb; ++i) {
+      const double d = sqrt(gmm_md2(Lc[0], r, X + i * GMM_R, mu[0])) - meanb;
+      s2 += d * d;
+    }
+    sh_thr = nb ? 3.0 * sqrt(s2 / nb) : INFINITY;
   }
-  const double thr = nb ? 3.0 * sqrt(s2 / nb) : INFINITY;
-  int kept = 0;
-  for (int i = 0; i < n; ++i) {
-    const double* x = Z + i * GMM_R;
+  __syncthreads();
+  const double thr = sh_thr;
+  const bool okc = sh_okc != 0;
+  if (k < n) {  // lane k = client k
+    const double* x = Z + k * GMM_R;
     const int c = (K == 2 && wlogp(x, 1) > wlogp(x, 0)) ? 1 : 0;
-    const bool k = okc && sqrt(gmm_md2(Lc[c], r, x, mu[c])) <= thr;
-    keep[i] = k ? 1 : 0;
-    kept += k ? 1 : 0;
+    const bool kp = okc && sqrt(gmm_md2(Lc[c], r, x, mu[c])) <= thr;
+    keep[k] = kp ? 1 : 0;
+    lse_row[k] = kp ? 1.0 : 0.0;
   }
-  info[0] = thr;
-  info[1] = (double)kept;
-  info[2] = okc ? 1.0 : 0.0;
+  __syncthreads();
+  if (k == 0) {
+    int kept = 0;
+    for (int i = 0; i < n; ++i) kept += lse_row[i] > 0.5 ? 1 : 0;
+    info[0] = thr;
+    info[1] = (double)kept;
+    info[2] = okc ? 1.0 : 0.0;
+  }
 }
 
 int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned char* keep, double* info, int rank,
