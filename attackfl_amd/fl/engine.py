@@ -1093,8 +1093,10 @@ class FLEngine:
         if self.mode == "hyper":  # the update runs, or leaves the hypernetwork untouched, as the device decides
             hyper_step = self.hyper.step
             self.ckpt_writer.fence()  # the previous round's checkpoint copy of the arena, updated in place below
+            nxt = self._next_prep  # (staged ahead: its START models come out of the update's last launches)
             self.hyper.train(self.selected, {i: U[k] for k, i in enumerate(self.selected)},
-                             enable=ok_all.to(torch.int32).reshape(1))
+                             enable=ok_all.to(torch.int32).reshape(1),
+                             gen_key=[i for _, i, _, _ in nxt["clients"]] if nxt and nxt.get("clients") else None)
             g = g_old
         else:
             if ok_n is not None and ok_n.dtype == torch.int32 and g_old is not None:

@@ -72,11 +72,10 @@ class HyperServer:
         if c is not None and c[0] == key:
             return c[1]
         if self._native_ok() and not _TORCH_GEN:
-            # MLP features of every client in one native launch, then one GEMM over the packed heads (the torch
-            # MLP was 7 small launches issued one by one on the round boundary)
-            h = self.hnet
-            feat = ops.hyper_features(h.arena, key, self.layout_vec())
-            out = torch.addmm(h.b[None, :], feat, h.W.t())
+            # MLP features of every client in one native launch, then one sweep over the packed heads for all of
+            # them (the same arithmetic as the generation fused into the update; was a library GEMM, and before
+            # that the torch MLP: 7 small launches issued one by one on the round boundary)
+            out = ops.hyper_generate_many(self.hnet.arena, key, self.layout_vec())
         else:
             out = self.hnet.generate_many(key)
         self._gen_cache = (key, out)
@@ -142,13 +141,15 @@ class HyperServer:
         return h.slots["W"][0] - h.slots["mlp0.W"][0] <= ops.native().hyper_small_capacity()
 
     def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor],
-              enable: Optional[torch.Tensor] = None) -> None:
+              enable: Optional[torch.Tensor] = None, gen_key: Optional[Sequence[int]] = None) -> None:
         """One round of the sequential server update over ``selected`` (client order kept).
 
         On GPU the whole round is enqueued by ``ops.hyper_server_update`` (three launches per client,
         no host synchronisation, ``last_info`` read lazily); on CPU the composite path below is the oracle.
         ``enable`` (GPU only): device int32 word decided on the device — 0 leaves the hypernetwork and its
-        moments untouched (the caller then rolls ``step`` back)."""
+        moments untouched (the caller then rolls ``step`` back).  ``gen_key`` (GPU only): the clients of the next
+        ``generate_many``; their models come out of the update's own last launches (the features in the last
+        small-net launch, the heads sweep fused with the last head Adam) and are memoised for that call."""
         h = self.hnet
         selected = list(selected)
         if not selected:
@@ -164,10 +165,15 @@ class HyperServer:
             else:
                 U = torch.stack([r.contiguous() for r in rows])
                 urows = list(range(len(rows)))
-            info = ops.hyper_server_update(h.arena, self.m, self.v, U, urows, selected, self.layout_vec(), self.step,
-                                           self.lr, self.clip, enable=enable)
+            gen = tuple(int(i) for i in gen_key) if gen_key is not None and not _TORCH_GEN else ()
+            if len(gen) > 32:
+                gen = ()
+            info, out = ops.hyper_server_update(h.arena, self.m, self.v, U, urows, selected, self.layout_vec(),
+                                                self.step, self.lr, self.clip, enable=enable, gen=gen)
             self.step += len(selected)
             self._info_dev = info[-1]  # no host sync here (see last_info)
+            if gen:
+                self._gen_cache = (gen, out)
             return
         if enable is not None:
             raise RuntimeError("a device-decided hypernetwork update needs the native server kernels")

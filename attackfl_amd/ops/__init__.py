@@ -372,16 +372,26 @@ def hyper_adam_outer(W, b, m_wb, v_wb, delta, feat, step: int, lr: float, scale:
 
 
 def hyper_server_update(arena, m, v, U, urows, clients, layout, step0: int, lr: float, clip: float,
-                        beta1=0.9, beta2=0.999, eps=1e-8, enable: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Sequential pFedHN server update of a whole round on the device (no host sync); info [n, 2].
-    ``enable``: optional device int32 word; 0 leaves arena / moments untouched (decided on the device)."""
-    return native().hyper_server_update(arena, m, v, U.contiguous(), [int(r) for r in urows],
-                                        [int(c) for c in clients], [int(x) for x in layout], int(step0), float(lr),
-                                        float(clip), float(beta1), float(beta2), float(eps), enable)
+                        beta1=0.9, beta2=0.999, eps=1e-8, enable: Optional[torch.Tensor] = None, gen=()):
+    """Sequential pFedHN server update of a whole round on the device (no host sync) -> (info [n, 2],
+    generated [len(gen), P]).  ``enable``: optional device int32 word; 0 leaves arena / moments untouched (decided
+    on the device).  ``gen``: clients whose models the updated hypernetwork generates inside the update's last
+    launches (the next START; <= 32)."""
+    info, out = native().hyper_server_update(arena, m, v, U.contiguous(), [int(r) for r in urows],
+                                             [int(c) for c in clients], [int(x) for x in layout], int(step0),
+                                             float(lr), float(clip), float(beta1), float(beta2), float(eps), enable,
+                                             [int(c) for c in gen])
+    return info, out
 
 
 def hyper_features(arena, clients, layout) -> torch.Tensor:
     return native().hyper_features(arena, [int(c) for c in clients], [int(x) for x in layout])
+
+
+def hyper_generate_many(arena, clients, layout) -> torch.Tensor:
+    """Models [n, P] of ``clients`` generated from the packed hypernetwork arena (device; the same per-row
+    arithmetic as the generation fused into ``hyper_server_update``)."""
+    return native().hyper_generate_many(arena, [int(c) for c in clients], [int(x) for x in layout])
 
 
 def hyper_generate(W: torch.Tensor, b: torch.Tensor, feat: torch.Tensor) -> torch.Tensor:

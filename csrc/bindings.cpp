@@ -473,11 +473,14 @@ HySmallDesc hy_desc(const std::vector<int64_t>& lay, long& offW, long& offB, lon
 }
 
 // Whole sequential hypernetwork server update of one round (every selected client in order), enqueued
-// without a host synchronisation.  Returns info [n, 2] = (grad norm, clip scale) per client (device).
-torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::Tensor v, torch::Tensor U,
-                                  std::vector<int64_t> urows, std::vector<int64_t> clients, std::vector<int64_t> lay,
-                                  int64_t step0, double lr, double clip, double b1, double b2, double eps,
-                                  c10::optional<torch::Tensor> enable) {
+// without a host synchronisation.  Returns {info [n, 2] = (grad norm, clip scale) per client, gen [ngen, P]}
+// (device): gen = the models of the clients ``gen`` generated by the updated hypernetwork (by the unchanged one
+// when ``enable`` is 0), produced inside the update's last launches (empty when no client is asked for).
+std::vector<torch::Tensor> hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::Tensor v, torch::Tensor U,
+                                               std::vector<int64_t> urows, std::vector<int64_t> clients,
+                                               std::vector<int64_t> lay, int64_t step0, double lr, double clip,
+                                               double b1, double b2, double eps, c10::optional<torch::Tensor> enable,
+                                               std::vector<int64_t> gen) {
   for (auto* t : {&arena, &m, &v, &U}) check_dev(*t, "hyper tensor", torch::kFloat32);
   const int* en = nullptr;
   if (enable.has_value() && enable->defined()) {
@@ -496,9 +499,15 @@ torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::T
     TORCH_CHECK(urows[k] >= 0 && urows[k] < U.size(0), "hyper: update row out of range");
     TORCH_CHECK(clients[k] >= 0 && clients[k] < d.n_nodes, "hyper: client index out of range");
   }
+  const int ng = (int)gen.size();
+  TORCH_CHECK(ng <= 32, "hyper: at most 32 generated clients per update");
+  for (int k = 0; k < ng; ++k) TORCH_CHECK(gen[k] >= 0 && gen[k] < d.n_nodes, "hyper: generated client out of range");
   std::vector<int> cl(clients.begin(), clients.end());
+  std::vector<int> gl(gen.begin(), gen.end());
   std::vector<long> ur(urows.begin(), urows.end());
   auto opt = arena.options();
+  auto gfeat = torch::empty({std::max(ng, 1) * (long)d.H}, opt);
+  auto gout = torch::empty({ng, P}, opt);
   auto delta = torch::empty({2 * P}, opt);  // (two: the fused head Adam reads client k's, writes client k+1's)
   auto partial = torch::empty({(long)afl_hyper_nblocks(P) * (d.H + 1)}, opt);
   auto feat = torch::empty({2 * 128}, opt);
@@ -506,9 +515,30 @@ torch::Tensor hyper_server_update(torch::Tensor arena, torch::Tensor m, torch::T
   afl_hyper_server_update(arena.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), U.data_ptr<float>(),
                           ur.data(), cl.data(), n, d, offW, offB, P, (int)step0, (float)lr, (float)clip, (float)b1,
                           (float)b2, (float)eps, delta.data_ptr<float>(), partial.data_ptr<float>(),
-                          feat.data_ptr<float>(), info.data_ptr<float>(), en, cur());
+                          feat.data_ptr<float>(), info.data_ptr<float>(), en, gl.data(), ng, gfeat.data_ptr<float>(),
+                          gout.data_ptr<float>(), cur());
   AFL_CHECK_LAUNCH();
-  return info;
+  return {info, gout};
+}
+
+// models of several clients generated by the hypernetwork (features launch + one sweep over the heads): [n, P]
+torch::Tensor hyper_generate_many(torch::Tensor arena, std::vector<int64_t> clients, std::vector<int64_t> lay) {
+  check_dev(arena, "arena", torch::kFloat32);
+  long offW, offB, P;
+  HySmallDesc d = hy_desc(lay, offW, offB, P);
+  TORCH_CHECK(d.H % 4 == 0 && offW % 4 == 0 && arena.numel() == offB + P, "hyper: head block must be float4-aligned");
+  const int n = (int)clients.size();
+  for (int k = 0; k < n; ++k) TORCH_CHECK(clients[k] >= 0 && clients[k] < d.n_nodes, "hyper: client out of range");
+  std::vector<int> cl(clients.begin(), clients.end());
+  auto feat = torch::empty({n, d.H}, arena.options());
+  auto out = torch::empty({n, P}, arena.options());
+  if (n) {
+    afl_hyper_features(arena.data_ptr<float>(), d, offW, cl.data(), n, feat.data_ptr<float>(), cur());
+    afl_hyper_generate(arena.data_ptr<float>(), d, offW, offB, P, feat.data_ptr<float>(), n, out.data_ptr<float>(),
+                       cur());
+  }
+  AFL_CHECK_LAUNCH();
+  return out;
 }
 
 // hypernetwork features (embedding -> MLP output) of several clients -> [n, H]
@@ -782,6 +812,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("make_plan", &make_plan);
   m.def("step_tables", &step_tables);
   m.def("hyper_features", &hyper_features);
+  m.def("hyper_generate_many", &hyper_generate_many);
   m.def("hyper_small_capacity", &afl_hyper_small_capacity);
   m.def("tf_train", &tf_train, py::arg("params"), py::arg("rows"), py::arg("order"), py::arg("nd"),
         py::arg("seeds"), py::arg("epochs"), py::arg("batch"), py::arg("lr"), py::arg("opt_mode") = 0,

@@ -38,7 +38,11 @@ struct HySmallDesc {
 void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
                              int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
                              float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
-                             float* info, const int* enable, hipStream_t s);
+                             float* info, const int* enable, const int* gen, int ngen, float* gen_feat,
+                             float* gen_out, hipStream_t s);
+// W f_c + b of n clients (feat [n, H]) -> out [n, P]: one sweep over the heads per 32 clients
+void afl_hyper_generate(const float* A, const HySmallDesc& d, long offW, long offB, long P, const float* feat, int n,
+                        float* out, hipStream_t s);
 void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const int* clients, int n, float* out,
                         hipStream_t s);
 long afl_hyper_small_capacity();  // max floats of embedding-MLP parameters the small-net kernel stages in LDS

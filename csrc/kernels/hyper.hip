@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(256) k_hyper_rows(const float* __restrict__ W,
 // float4 variant (H % 4 == 0, H <= 128, 16-B aligned W): no LDS staging.  A half-wave owns one row at a
 // time (lane j holds columns 4j..4j+3 and the matching f in registers), dots reduce inside the half,
 // each lane accumulates its 4 columns of W^T delta in registers; 4 rows per half in flight.
-constexpr int HR4_NT = 512;
+constexpr int HR4_NT = 1024;  // 16 waves: 4 per SIMD over the 256-block grid (the partials layout caps the grid)
 constexpr int HR4_U = 4;
 __global__ void __launch_bounds__(HR4_NT) k_hyper_rows4(const float* __restrict__ W, const float* __restrict__ b,
                                                         const float* __restrict__ f, const float* __restrict__ u,
@@ -250,6 +250,12 @@ __device__ __forceinline__ void hs_stage(float* __restrict__ dst, const float* _
   }
 }
 
+// a list of client indices passed by value (the generation / feature kernels)
+constexpr int HF_MAXC = 64;
+struct HyClients {
+  int c[HF_MAXC];
+};
+
 // relu that keeps NaN like torch.relu
 __device__ __forceinline__ float hs_relu(float z) { return z < 0.f ? 0.f : z; }
 
@@ -292,12 +298,15 @@ __device__ void hs_forward(const float* __restrict__ A, const float* sm, const H
   }
 }
 
-// Adam on one element (gradient already scaled)
+// Adam on one element (gradient already scaled).  Every fused multiply-add is spelled out: the head update runs
+// in three kernels (k_hyper_adam_v, k_hyper_adam_rows4, k_hyper_gen4) that must agree bitwise, which the
+// compiler's own contraction choices do not promise across differently shaped kernels.
 __device__ __forceinline__ float hs_adam(float p, float g, float& mm, float& vv, float lr_bc1, float rsqrt_bc2,
                                          float b1, float b2, float eps) {
-  mm = mm + (1.f - b1) * (g - mm);
-  vv = b2 * vv + (1.f - b2) * g * g;
-  return p - lr_bc1 * mm / (sqrtf(vv) * rsqrt_bc2 + eps);
+#pragma clang fp contract(off)  // (g - mm must not absorb the caller's product that formed g)
+  mm = __builtin_fmaf(1.f - b1, g - mm, mm);
+  vv = __builtin_fmaf((1.f - b2) * g, g, b2 * vv);
+  return p - (lr_bc1 * mm) / __builtin_fmaf(__builtin_sqrtf(vv), rsqrt_bc2, eps);
 }
 
 __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, float* __restrict__ m,
@@ -305,10 +314,13 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
                                                        int nb, int ci, int cj, float* __restrict__ feat_j,
                                                        float* __restrict__ info, HySmallDesc d, long nmlp,
                                                        float clip, float lr_bc1, float rsqrt_bc2, float b1, float b2,
-                                                       float eps, const int* __restrict__ enable) {
+                                                       float eps, const int* __restrict__ enable, HyClients gen,
+                                                       int ngen, float* __restrict__ gen_feat) {
   // enable (device word, optional): 0 = the round failed, leave the hypernetwork untouched (the engine enqueues
-  // the update before it knows; FLEngine._early_launch)
-  if (enable != nullptr && *enable == 0) return;
+  // the update before it knows; FLEngine._early_launch).  gen / ngen: after the update, the MLP features of the
+  // next generation's clients -> gen_feat [ngen, H] (from the untouched MLP when the update is disabled)
+  const bool upd = enable == nullptr || *enable != 0;
+  if (!upd && ngen == 0) return;
   __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];
   __shared__ float acts[HS_LMAX + 1][HS_HMAX];
   __shared__ float dz[HS_LMAX][HS_HMAX];  // dL/d(output of layer l)
@@ -331,7 +343,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
   }
   // stage the MLP parameters (contiguous [w_0 .. b_{L-1}]) in LDS
   hs_stage(sm, A + base, nmlp);
-  if (ci >= 0) {
+  if (ci >= 0 && upd) {
     // reduce the rows kernel's per-block partials: 8 lanes per column (W^T delta [H] and |delta|^2)
     {
       const int c = tid >> 3, sub = tid & 7;
@@ -461,9 +473,13 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
     }
     __syncthreads();  // updated embedding (global, this workgroup's writes) and LDS MLP visible
   }
-  if (cj >= 0) {
+  if (cj >= 0 && upd) {
     hs_forward(A, sm, d, cj, acts);
     if (tid < H) feat_j[tid] = acts[L][tid];
+  }
+  for (int k = 0; k < ngen; ++k) {
+    hs_forward(A, sm, d, gen.c[k], acts);  // (its first barrier also orders the previous reads of acts)
+    if (tid < H) gen_feat[(long)k * H + tid] = acts[L][tid];
   }
 }
 
@@ -473,6 +489,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
 // 19.5 MB for TransformerModel; the rows pass needs the updated rows, which this thread holds in registers).
 // Same row mapping as k_hyper_rows4, same partial layout (k_hyper_small reduces it), same arithmetic as the
 // two kernels it replaces.
+constexpr int HA_U = 2;  // rows per half-wave in flight (4 spilled at the 128-VGPR cap of 16-wave blocks)
 __global__ void __launch_bounds__(HR4_NT) k_hyper_adam_rows4(float* __restrict__ W, float* __restrict__ b,
                                                              float* __restrict__ m, float* __restrict__ v,
                                                              const float* __restrict__ delta_k,
@@ -500,34 +517,28 @@ __global__ void __launch_bounds__(HR4_NT) k_hyper_adam_rows4(float* __restrict__
   float dsq = 0.f;
   const long nslots = 2L * gridDim.x * (HR4_NT / 64);
   const long slot = 2L * ((long)blockIdx.x * (HR4_NT / 64) + wv) + half;
-  for (long r0 = slot; r0 < P; r0 += HR4_U * nslots) {
-    float4 w[HR4_U], mm[HR4_U], vv[HR4_U];
+  for (long r0 = slot; r0 < P; r0 += HA_U * nslots) {
+    float4 w[HA_U], mm[HA_U], vv[HA_U];
 #pragma unroll
-    for (int q = 0; q < HR4_U; ++q) {
-      const long r = r0 + q * nslots;
-      const bool ok = act && r < P;
-      w[q] = ok ? W4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      mm[q] = ok ? m4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      vv[q] = ok ? v4[r * H4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < HA_U; ++q) {  // (clamped rows / columns: every load of the batch in flight, no scratch)
+      const long r = r0 + q * nslots < P ? r0 + q * nslots : P - 1;
+      const long e = r * H4 + (act ? j : 0);
+      w[q] = W4[e];
+      mm[q] = m4[e];
+      vv[q] = v4[e];
     }
 #pragma unroll
-    for (int q = 0; q < HR4_U; ++q) {
+    for (int q = 0; q < HA_U; ++q) {
       const long r = r0 + q * nslots;
       const bool rv = r < P;  // (no early exit: the half-wave reduction below needs every lane of the half)
-      const long rr = rv ? r : 0;
+      const long rr = rv ? r : P - 1;
+      if (!act) w[q] = make_float4(0.f, 0.f, 0.f, 0.f);
       const float dr = gs * delta_k[rr];
       {  // head Adam on this lane's 4 columns (k_hyper_adam_v)
-        float* pp = &w[q].x;
-        float* mp = &mm[q].x;
-        float* vp = &vv[q].x;
-        const float* fp = &fk.x;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float g = dr * fp[c];
-          mp[c] = mp[c] + (1.f - b1) * (g - mp[c]);
-          vp[c] = b2 * vp[c] + (1.f - b2) * g * g;
-          pp[c] -= lr_bc1 * mp[c] / (sqrtf(vp[c]) * rsqrt_bc2 + eps);
-        }
+        w[q].x = hs_adam(w[q].x, dr * fk.x, mm[q].x, vv[q].x, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].y = hs_adam(w[q].y, dr * fk.y, mm[q].y, vv[q].y, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].z = hs_adam(w[q].z, dr * fk.z, mm[q].z, vv[q].z, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].w = hs_adam(w[q].w, dr * fk.w, mm[q].w, vv[q].w, lr_bc1, rsqrt_bc2, b1, b2, eps);
         if (act && rv) {
           W4[r * H4 + j] = w[q];
           m4[r * H4 + j] = mm[q];
@@ -535,9 +546,8 @@ __global__ void __launch_bounds__(HR4_NT) k_hyper_adam_rows4(float* __restrict__
         }
       }
       // bias Adam (every lane of the half computes it, lane 0 stores)
-      const float bm = m[nW + rr] + (1.f - b1) * (dr - m[nW + rr]);
-      const float bv = b2 * v[nW + rr] + (1.f - b2) * dr * dr;
-      const float bn = b[rr] - lr_bc1 * bm / (sqrtf(bv) * rsqrt_bc2 + eps);
+      float bm = m[nW + rr], bv = v[nW + rr];
+      const float bn = hs_adam(b[rr], dr, bm, bv, lr_bc1, rsqrt_bc2, b1, b2, eps);
       // client k+1's rows pass on the updated row
       float d = w[q].x * fn.x + w[q].y * fn.y + w[q].z * fn.z + w[q].w * fn.w;
 #pragma unroll
@@ -608,16 +618,10 @@ __global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, flo
     const int h = (int)(e - r * H);
     const float dr = gs * delta[r];
     float4 p = W4[i], mm = m4[i], vv = v4[i];
-    float* pp = &p.x;
-    float* mp = &mm.x;
-    float* vp = &vv.x;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float g = dr * fs[h + q];
-      mp[q] = mp[q] + (1.f - b1) * (g - mp[q]);
-      vp[q] = b2 * vp[q] + (1.f - b2) * g * g;
-      pp[q] -= lr_bc1 * mp[q] / (sqrtf(vp[q]) * rsqrt_bc2 + eps);
-    }
+    p.x = hs_adam(p.x, dr * fs[h], mm.x, vv.x, lr_bc1, rsqrt_bc2, b1, b2, eps);
+    p.y = hs_adam(p.y, dr * fs[h + 1], mm.y, vv.y, lr_bc1, rsqrt_bc2, b1, b2, eps);
+    p.z = hs_adam(p.z, dr * fs[h + 2], mm.z, vv.z, lr_bc1, rsqrt_bc2, b1, b2, eps);
+    p.w = hs_adam(p.w, dr * fs[h + 3], mm.w, vv.w, lr_bc1, rsqrt_bc2, b1, b2, eps);
     W4[i] = p;
     m4[i] = mm;
     v4[i] = vv;
@@ -626,25 +630,159 @@ __global__ void __launch_bounds__(256) k_hyper_adam_v(float* __restrict__ W, flo
   for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < P; r += stride) {
     const float g = gs * delta[r];
     const long e = nW + r;
-    const float mi = m[e] + (1.f - b1) * (g - m[e]);
-    const float vi = b2 * v[e] + (1.f - b2) * g * g;
+    float mi = m[e], vi = v[e];
+    bvec[r] = hs_adam(bvec[r], g, mi, vi, lr_bc1, rsqrt_bc2, b1, b2, eps);
     m[e] = mi;
     v[e] = vi;
-    bvec[r] -= lr_bc1 * mi / (sqrtf(vi) * rsqrt_bc2 + eps);
+  }
+}
+
+// Generation W f_c + b for up to HG_MAXC clients in ONE sweep over the packed heads (was a library GEMM after
+// the features launch), optionally FUSED with the last client's head Adam (ADAM: the row is updated in registers
+// and the generation reads the updated row; the two-kernel sequence wrote and re-read the 39 MB heads of
+// RNNModel).  Row mapping of k_hyper_rows4 (a half-wave per row, lane j owns columns 4j..4j+3).  The per-client
+// dots of a row reduce as one transpose-reduction over the half-wave: 8 clients in 9 shuffles (a shuffle tree
+// per client would be 40), lane j ends with the total of client (j >> 2) of its group of 8.  The fused and the
+// plain kernel run the same arithmetic, so a START generated inside the update equals a later plain generation.
+constexpr int HG_MAXC = 32;
+template <bool ADAM>
+__global__ void __launch_bounds__(HR4_NT) k_hyper_gen4(float* __restrict__ W, float* __restrict__ b,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       const float* __restrict__ delta_k,
+                                                       const float* __restrict__ f_k, const float* __restrict__ gsp,
+                                                       const float* __restrict__ gfeat, int ngen,
+                                                       float* __restrict__ out, long P, int H, float lr_bc1,
+                                                       float rsqrt_bc2, float b1, float b2, float eps,
+                                                       const int* __restrict__ enable) {
+  __shared__ float4 fs[HG_MAXC][HR_HMAX / 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = lane & 31, half = lane >> 5, H4 = H >> 2;
+  const bool act = j < H4;
+  const bool upd = ADAM && (enable == nullptr || *enable != 0);
+  const int ng8 = (ngen + 7) & ~7;  // clients padded to groups of 8 (zero features)
+  for (int e = tid; e < ng8 * (HR_HMAX / 4); e += HR4_NT) {
+    const int c = e / (HR_HMAX / 4), q = e - c * (HR_HMAX / 4);
+    fs[c][q] = (c < ngen && q < H4) ? reinterpret_cast<const float4*>(gfeat + (long)c * H)[q]
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  float4 fk = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gs = 0.f;
+  if (upd) {
+    if (act) fk = reinterpret_cast<const float4*>(f_k)[j];
+    gs = *gsp;
+  }
+  float4* W4 = reinterpret_cast<float4*>(W);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const long nW = P * H;
+  const long nslots = 2L * gridDim.x * (HR4_NT / 64);
+  const long slot = 2L * ((long)blockIdx.x * (HR4_NT / 64) + wv) + half;
+  const bool b4 = (j & 16) != 0, b3 = (j & 8) != 0, b2s = (j & 4) != 0;
+  for (long r0 = slot; r0 < P; r0 += HR4_U * nslots) {
+    float4 w[HR4_U], mm[HR4_U], vv[HR4_U];
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {  // (clamped rows: every load of the batch in flight)
+      const long r = r0 + q * nslots < P ? r0 + q * nslots : P - 1;
+      const long e = r * H4 + (act ? j : 0);
+      w[q] = W4[e];
+      if (upd) {
+        mm[q] = m4[e];
+        vv[q] = v4[e];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < HR4_U; ++q) {
+      const long r = r0 + q * nslots;
+      const bool rv = r < P;  // (no early exit: the half-wave reduction needs every lane of the half)
+      const long rr = rv ? r : P - 1;
+      if (!act) w[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float bn;
+      if (upd) {
+        const float dr = gs * delta_k[rr];
+        // head Adam on this lane's 4 columns (k_hyper_adam_v's arithmetic)
+        w[q].x = hs_adam(w[q].x, dr * fk.x, mm[q].x, vv[q].x, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].y = hs_adam(w[q].y, dr * fk.y, mm[q].y, vv[q].y, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].z = hs_adam(w[q].z, dr * fk.z, mm[q].z, vv[q].z, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        w[q].w = hs_adam(w[q].w, dr * fk.w, mm[q].w, vv[q].w, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        if (act && rv) {
+          W4[r * H4 + j] = w[q];
+          m4[r * H4 + j] = mm[q];
+          v4[r * H4 + j] = vv[q];
+        }
+        float bm = m[nW + rr], bvv = v[nW + rr];
+        bn = hs_adam(b[rr], dr, bm, bvv, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        if (rv && j == 0) {
+          m[nW + r] = bm;
+          v[nW + r] = bvv;
+          b[r] = bn;
+        }
+      } else {
+        bn = b[rr];
+      }
+      for (int c0 = 0; c0 < ng8; c0 += 8) {
+        float dv[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float4 f = fs[c0 + c][j];
+          dv[c] = __builtin_fmaf(w[q].w, f.w, __builtin_fmaf(w[q].z, f.z, __builtin_fmaf(w[q].y, f.y, w[q].x * f.x)));
+        }
+        // transpose-reduction: xor 16 halves the client set (bit 4 keeps the upper four), xor 8 and xor 4 again,
+        // then xor 2 / xor 1 finish the sum over the lanes that share bits 4..2
+        float d4[4], d2[2], d1;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float keep = b4 ? dv[c + 4] : dv[c], send = b4 ? dv[c] : dv[c + 4];
+          d4[c] = keep + __shfl_xor(send, 16, 64);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float keep = b3 ? d4[c + 2] : d4[c], send = b3 ? d4[c] : d4[c + 2];
+          d2[c] = keep + __shfl_xor(send, 8, 64);
+        }
+        {
+          const float keep = b2s ? d2[1] : d2[0], send = b2s ? d2[0] : d2[1];
+          d1 = keep + __shfl_xor(send, 4, 64);
+        }
+        d1 += __shfl_xor(d1, 2, 64);
+        d1 += __shfl_xor(d1, 1, 64);
+        // lane j holds client c0 + 4*b4 + 2*b3 + b2s
+        const int c = c0 + (b4 ? 4 : 0) + (b3 ? 2 : 0) + (b2s ? 1 : 0);
+        if (rv && (j & 3) == 0 && c < ngen) out[(long)c * P + r] = d1 + bn;
+      }
+    }
+  }
+}
+
+void afl_hyper_generate(const float* A, const HySmallDesc& d, long offW, long offB, long P, const float* feat,
+                        int n, float* out, hipStream_t s) {
+  const int nb = afl_hyper_nblocks(P);
+  float* W = const_cast<float*>(A) + offW;
+  float* bv = const_cast<float*>(A) + offB;
+  for (int c0 = 0; c0 < n; c0 += HG_MAXC) {
+    const int m = n - c0 < HG_MAXC ? n - c0 : HG_MAXC;
+    hipLaunchKernelGGL(k_hyper_gen4<false>, dim3(nb), dim3(HR4_NT), 0, s, W, bv, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, feat + (long)c0 * d.H, m, out + (long)c0 * P, P, d.H, 0.f, 0.f, 0.f, 0.f, 0.f,
+                       nullptr);
   }
 }
 
 void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
                              int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
                              float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
-                             float* info, const int* enable, hipStream_t s) {
+                             float* info, const int* enable, const int* gen, int ngen, float* gen_feat,
+                             float* gen_out, hipStream_t s) {
+  // gen (optional, ngen <= HG_MAXC): the clients whose models the updated hypernetwork generates next; the last
+  // client's small-net launch computes their features and the last head Adam writes gen_out [ngen, P]
   const int H = d.H;
+  HyClients gl{};
+  for (int k = 0; k < ngen; ++k) gl.c[k] = gen[k];
   const int nb = afl_hyper_nblocks(P);
   float* W = A + offW;
   float* bv = A + offB;
   const long nmlp = offW - d.w[0];
   hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, -1, clients[0], feat, info, d,
-                     nmlp, clip, 0.f, 0.f, b1, b2, eps, enable);
+                     nmlp, clip, 0.f, 0.f, b1, b2, eps, enable, gl, 0, gen_feat);
   const long nW4 = P * H / 4;
   const int nba = (int)min(4096L, (nW4 + 255) / 256);
   // the rows pass of client k + 1 rides in client k's head Adam (k_hyper_adam_rows4) when the heads are
@@ -670,25 +808,26 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
         hipLaunchKernelGGL(k_hyper_rows, dim3(nb), dim3(256), 0, s, W, bv, fk, U + urow[k] * P, P, H, dk, partial,
                            H + 1);
     }
+    const bool last = k + 1 == n;
     hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
-                       k + 1 < n ? clients[k + 1] : -1, fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps,
-                       enable);
-    if (fused && k + 1 < n)
+                       last ? -1 : clients[k + 1], fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps,
+                       enable, gl, last ? ngen : 0, gen_feat);
+    if (fused && !last)
       hipLaunchKernelGGL(k_hyper_adam_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, m + offW, v + offW, dk, fk,
                          info + 2 * k + 1, fn, U + urow[k + 1] * P, dn, partial, P, H, lr_bc1, rbc2, b1, b2, eps,
                          enable);
+    else if (fused && ngen > 0)  // the last head Adam with the next generation in the same sweep
+      hipLaunchKernelGGL(k_hyper_gen4<true>, dim3(nb), dim3(HR4_NT), 0, s, W, bv, m + offW, v + offW, dk, fk,
+                         info + 2 * k + 1, gen_feat, ngen, gen_out, P, H, lr_bc1, rbc2, b1, b2, eps, enable);
     else
       hipLaunchKernelGGL(k_hyper_adam_v, dim3(nba), dim3(256), 0, s, W, bv, m + offW, v + offW, dk, fk, P, H,
                          lr_bc1, rbc2, b1, b2, eps, info + 2 * k + 1, enable);
   }
+  if (ngen > 0 && !fused) afl_hyper_generate(A, d, offW, offB, P, gen_feat, ngen, gen_out, s);
 }
 
 // MLP features of up to HF_MAXC clients in ONE launch (the START / validation models of a round: one workgroup
 // stages the embedding-MLP parameters once and runs hs_forward per client; was one k_hyper_small per client)
-constexpr int HF_MAXC = 64;
-struct HyClients {
-  int c[HF_MAXC];
-};
 __global__ void __launch_bounds__(HS_NT) k_hyper_feat_many(const float* __restrict__ A, HySmallDesc d, long nmlp,
                                                            HyClients cl, int n, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];

@@ -228,10 +228,45 @@ def test_hyper_server_update_matches_composite(gpu, model, clip):
     cpu.hnet.arena.copy_(a)  # same parameters on both sides
     ref = torch.stack([cpu.hnet.features(i)[1] for i in (0, 2, 4)])
     assert torch.allclose(feats, ref, rtol=1e-4, atol=1e-5)
-    # the round's START models: native features + one GEMM (HyperServer.generate_many) vs the torch MLP path
+    # the round's START models: native features + one heads sweep (HyperServer.generate_many) vs the torch MLP
     many = dev.generate_many([4, 0, 2, 1]).cpu()
     ref_many = dev.hnet.generate_many([4, 0, 2, 1]).cpu()
     assert torch.allclose(many, ref_many, rtol=1e-4, atol=1e-5), float((many - ref_many).abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["TransformerModel", "RNNModel"])
+@pytest.mark.parametrize("ngen", [3, 8, 11])
+def test_hyper_update_fused_generation(gpu, model, ngen):
+    """The next START generated inside the update's last launches (features in the last small-net launch, the
+    heads sweep fused with the last head Adam) equals a plain generate_many from the updated arena BITWISE, the
+    update itself equals the unfused one bitwise, and a device-disabled update generates from the unchanged arena."""
+    from attackfl_amd.fl.hyper_server import HyperServer
+    from attackfl_amd.models import build_model
+
+    sd = build_model(model, seed=0).state_dict()
+    n = 12
+    srv = [HyperServer(sd, n, 0.01, 0.05, gpu, seed=3) for _ in range(2)]
+    g = torch.Generator().manual_seed(2)
+    sel = [3, 0, 4, 1, 7]
+    gen = [(5 * k + 1) % n for k in range(ngen)]
+    r = torch.randn(len(sel), srv[0].hnet.P, generator=g).to(gpu)
+    U = torch.stack([srv[0].generate(i) for i in sel]) - 0.1 * torch.sign(r) * (0.5 + r.abs())
+    on = torch.ones(1, dtype=torch.int32, device=gpu)
+    srv[0].train(sel, {i: U[k] for k, i in enumerate(sel)}, enable=on, gen_key=gen)
+    fused = srv[0].generate_many(gen)  # (memoised by the update)
+    srv[1].train(sel, {i: U[k] for k, i in enumerate(sel)}, enable=on)
+    assert torch.equal(srv[0].hnet.arena, srv[1].hnet.arena)
+    assert torch.equal(srv[0].m, srv[1].m) and torch.equal(srv[0].v, srv[1].v)
+    plain = srv[1].generate_many(gen)
+    assert torch.equal(fused, plain), float((fused - plain).abs().max())
+    ref = srv[1].hnet.generate_many(gen)  # torch MLP + GEMM
+    assert torch.allclose(plain, ref, rtol=1e-4, atol=1e-5), float((plain - ref).abs().max())
+    # a disabled update: arena, moments untouched, START generated from the unchanged hypernetwork
+    before = (srv[0].hnet.arena.clone(), srv[0].m.clone(), srv[0].v.clone())
+    srv[0].train(sel, {i: U[k] for k, i in enumerate(sel)}, enable=torch.zeros_like(on), gen_key=gen)
+    assert all(torch.equal(a, b) for a, b in zip((srv[0].hnet.arena, srv[0].m, srv[0].v), before))
+    assert torch.equal(srv[0].generate_many(gen), ops.hyper_generate_many(before[0], gen, srv[0].layout_vec()))
 
 
 @pytest.mark.gpu
