@@ -50,6 +50,11 @@ from ..utils.log import Logger, MetricsWriter, NullLogger, print_with_color
 from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
 
+# rules that run on the device without a host read: with one of them the aggregate and the next round's launch
+# are enqueued before the host waits for the training, as for FedAvg (FLEngine._early_launch); gmm reads one
+# byte (its success), FLTrust trains a server model first
+EARLY_AGGREGATORS = ("trimmed_mean", "median", "krum", "shieldfl", "scionfl", "fltracer", "byzantine")
+
 META = 5  # valid, result, size, is_attacker, decision word; then the client's per-epoch losses (E columns)
 DECISION = 4  # column of the sender's decision word (``FLEngine._decision_word``)
 
@@ -262,6 +267,7 @@ class FLEngine:
         self._spec = None
         self._next_prep = None  # the next launch's host half, staged while the current training runs
         self._fedavg_w = None
+        self._early_agg_info: dict = {}  # a robust rule's info of the last early launch (_early_info)
         self._val_stream = None
         self._start_ready = None
         self._sel_cache = None
@@ -590,6 +596,7 @@ class FLEngine:
                      "attack_rows": [j for j, _ in attack_rows], "js": js, "meta_d": meta_d, "js_d": js_d,
                      "rows_d": rows_d, "tseed_d": tseed_d, "plan": plan,
                      "fedavg_w": fw_d if sel_nd is not None and fw.size == len(self.selected) else None,
+                     "sizes_h": torch.from_numpy(sel_nd) if sel_nd is not None else None,
                      "tq1": tq1, "tq2": tq2})
 
     def _enqueue_local(self, prep: dict, genuine: Dict[int, Optional[torch.Tensor]]) -> dict:
@@ -656,7 +663,7 @@ class FLEngine:
         tp1 = time.perf_counter()
         return {"block": block, "attack_jobs": attack_jobs, "ready": ready, "pending": pending, "params": params,
                 "in_place": in_place, "rows_d": rows_d, "n_local": n_local, "meta": prep["meta"],
-                "train_rows": train_rows, "fedavg_w": prep["fedavg_w"], "plain": plain,
+                "train_rows": train_rows, "fedavg_w": prep["fedavg_w"], "sizes_h": prep.get("sizes_h"), "plain": plain,
                 "t": (prep["tq"], prep["tq1"], prep["tq2"], tp0, tp1), "t_enqueue": tp0 - tq}
 
     def _finish_attacks(self, st: dict) -> None:
@@ -1056,7 +1063,8 @@ class FLEngine:
         if self.mode == "hyper":
             mode_ok = self.device.type == "cuda" and self.hyper._native_ok()
         else:
-            mode_ok = (self.mode == "fedavg" and not self.fast_fedavg and self.global_params is not None
+            mode_ok = ((self.mode == "fedavg" or self.mode in EARLY_AGGREGATORS) and not self.fast_fedavg
+                       and self.global_params is not None
                        and not self.cfg.engine.get("compat-fedavg-alias", False))
         return self._speculative and mode_ok and self.rounds_left > 1 and not last
 
@@ -1079,14 +1087,16 @@ class FLEngine:
             n = len(self.selected)
             U = self.local_params[:n]
             ok_n = st["pending"].ok_device()[:n]
-            ok_all = None if self.mode != "hyper" else (ok_n > 0).all()  # (FedAvg: decided inside the aggregate)
+            ok_all = None if self.mode == "fedavg" else (ok_n > 0).all()  # (FedAvg: decided inside the aggregate)
             w = st["fedavg_w"]
+            sizes = st["sizes_h"]
         else:  # several ranks: called on the gathered rows (device), before the host reads their meta
             P = self.P
             ok_n = None
             ok_all = ((sel[:, P] > 0.5) & (sel[:, P + 1] > 0.5)).all()
             s = sel[:, P + 2].double()
             w = s / s.sum()
+            sizes = s
         snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
                 self.server_rng.getstate(), self.genuine_pool)
         g_old, hyper_step = self.global_params, None
@@ -1098,6 +1108,12 @@ class FLEngine:
                              enable=ok_all.to(torch.int32).reshape(1),
                              gen_key=[i for _, i, _, _ in nxt["clients"]] if nxt and nxt.get("clients") else None)
             g = g_old
+        elif self.mode != "fedavg":
+            # a robust rule, all on the device (no host read): its result kept only when every client succeeded
+            res = AGGREGATORS[self.mode](U, sizes, attackers=None, seed=self.seed * 13 + self.round_no,
+                                        gmm_rank=int(self.cfg.engine.get("gmm-rank", 1)))
+            g = torch.where(ok_all, res.params.to(torch.float32), g_old)  # (a new tensor: never a row of U)
+            self._early_agg_info = {k: v for k, v in res.info.items() if k != "scores"}
         else:
             if ok_n is not None and ok_n.dtype == torch.int32 and g_old is not None:
                 g = ops.weighted_rows(U, w, ok_n, g_old)  # (the success check fused into the aggregate's pass)
@@ -1124,6 +1140,8 @@ class FLEngine:
             return {}
         if self.mode == "hyper":
             return {"path": "early-launch", "_lazy": lambda: self.hyper.last_info}  # (as _aggregate)
+        if self.mode != "fedavg":
+            return {**self._early_agg_info, "path": "early-launch"}
         return {"n": len(self.selected), "path": "early-launch"}
 
     def _early_launch_failed(self, esl: dict, results: np.ndarray) -> None:

@@ -138,7 +138,7 @@ class HyperServer:
         if not (self.device.type == "cuda" and h.H % 4 == 0 and h.slots["W"][0] % 4 == 0 and h.H <= 127
                 and h.E <= 128 and h.n_hidden + 1 <= 8):
             return False
-        return h.slots["W"][0] - h.slots["mlp0.W"][0] <= ops.native().hyper_small_capacity()
+        return h.slots["W"][0] - h.slots["emb"][0] <= ops.native().hyper_small_capacity()
 
     def train(self, selected: Sequence[int], updates: Dict[int, torch.Tensor],
               enable: Optional[torch.Tensor] = None, gen_key: Optional[Sequence[int]] = None) -> None:

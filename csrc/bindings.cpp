@@ -468,7 +468,8 @@ HySmallDesc hy_desc(const std::vector<int64_t>& lay, long& offW, long& offB, lon
   offB = lay[t + 5];
   P = lay[t + 6];
   TORCH_CHECK(d.E >= 1 && d.E <= 128 && d.H >= 1 && d.H <= 127, "hyper: embedding size must be <= 128, hidden <= 127");
-  TORCH_CHECK(offW - d.w[0] <= afl_hyper_small_capacity(), "hyper: MLP too large for the small-net kernel");
+  TORCH_CHECK(d.w[0] == d.emb + (long)d.n_nodes * d.E, "hyper: the embedding must precede the MLP in the arena");
+  TORCH_CHECK(offW - d.emb <= afl_hyper_small_capacity(), "hyper: embedding + MLP too large for the small-net kernel");
   return d;
 }
 

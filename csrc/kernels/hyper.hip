@@ -208,7 +208,8 @@ void afl_hyper_adam(float* W, float* bvec, float* m, float* v, const float* delt
 constexpr int HS_HMAX = 128;
 constexpr int HS_LMAX = 8;
 constexpr int HS_NT = 1024;          // threads of the small-net workgroup (16 waves)
-constexpr int HS_SMEM = 28 * 1024;   // floats of MLP parameters staged in LDS (112 KB)
+constexpr int HS_SMEM = 28 * 1024;   // floats of embedding + MLP parameters staged in LDS (112 KB)
+constexpr int HS_PF = 6;             // float4 moment chunks per thread held for the flat Adam (24 K floats)
 
 // stage n floats (16-byte aligned source and destination when n4 mode) into LDS with every load of a thread in
 // flight: clamped indices (a conditional load per slot made the compiler keep the batch in scratch and wait for
@@ -272,14 +273,14 @@ __device__ __forceinline__ float hs_wave_sum(float x) {
   return x;
 }
 
-// MLP forward of client c from the LDS copy (sm = parameters from d.w[0] on) -> acts[0..L]
-// 8 lanes per output neuron.
-__device__ void hs_forward(const float* __restrict__ A, const float* sm, const HySmallDesc& d, int c,
-                           float (*acts)[HS_HMAX]) {
+// MLP forward of client c from the LDS copy (sm = the arena from d.emb on) -> acts[0..L]
+// 8 lanes per output neuron.  sm holds the whole small region [d.emb, offW): embedding table and MLP (the
+// embedding row came from global memory before, one load round trip per forward)
+__device__ void hs_forward(const float* sm, const HySmallDesc& d, int c, float (*acts)[HS_HMAX]) {
   const int tid = threadIdx.x;
-  if (tid < d.E) acts[0][tid] = A[d.emb + (long)c * d.E + tid];
+  if (tid < d.E) acts[0][tid] = sm[(long)c * d.E + tid];
   __syncthreads();
-  const long base = d.w[0];
+  const long base = d.emb;
   const int o = tid >> 3, sub = tid & 7;
   int din = d.E;
   for (int l = 0; l < d.L; ++l) {
@@ -309,10 +310,11 @@ __device__ __forceinline__ float hs_adam(float p, float g, float& mm, float& vv,
   return p - (lr_bc1 * mm) / __builtin_fmaf(__builtin_sqrtf(vv), rsqrt_bc2, eps);
 }
 
+template <bool FLAT>
 __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, float* __restrict__ m,
                                                        float* __restrict__ v, const float* __restrict__ partial,
                                                        int nb, int ci, int cj, float* __restrict__ feat_j,
-                                                       float* __restrict__ info, HySmallDesc d, long nmlp,
+                                                       float* __restrict__ info, HySmallDesc d, long nsmall,
                                                        float clip, float lr_bc1, float rsqrt_bc2, float b1, float b2,
                                                        float eps, const int* __restrict__ enable, HyClients gen,
                                                        int ngen, float* __restrict__ gen_feat) {
@@ -329,7 +331,7 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
   __shared__ float sc;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = d.H, L = d.L, E = d.E;
-  const long base = d.w[0];
+  const long base = d.emb;  // sm = [emb | mlp0.W | mlp0.b | ...] (nsmall floats)
   // the rows kernel's per-block partials (nb <= 256): 8 lanes per column, all 32 loads of a lane in flight and
   // issued ahead of the staging loads below (the two latencies overlap; summed in the same order as before)
   float pt[32];
@@ -341,8 +343,15 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
       pt[k] = (ci >= 0 && c <= H && bb < nb) ? partial[(long)bb * (H + 1) + c] : 0.f;
     }
   }
-  // stage the MLP parameters (contiguous [w_0 .. b_{L-1}]) in LDS
-  hs_stage(sm, A + base, nmlp);
+  // stage the embedding table and the MLP parameters (contiguous [emb, w_0 .. b_{L-1}]) in LDS
+  hs_stage(sm, A + base, nsmall);
+  // flat Adam over the whole small region (float4 chunks, every segment a multiple of 4 floats): the moments of
+  // this thread's chunks are loaded ahead of the forward / backward passes (the per-segment loops waited for
+  // seven load round trips after them)
+  const long nemb = (long)d.n_nodes * E;
+  const long n4s = nsmall / 4;
+  constexpr bool flat = FLAT;  // (hs_flat_ok on the host)
+  float4 pm[HS_PF], pv[HS_PF];
   if (ci >= 0 && upd) {
     // reduce the rows kernel's per-block partials: 8 lanes per column (W^T delta [H] and |delta|^2)
     {
@@ -356,7 +365,17 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
         else sc = s;  // |delta|^2 (sc is rewritten with the clip scale below)
       }
     }
-    hs_forward(A, sm, d, ci, acts);  // its barriers publish sm, dz[L-1] and sc
+    if (flat) {  // (after the partials are summed: their registers are free again)
+      const float4* m4 = reinterpret_cast<const float4*>(m + base);
+      const float4* v4 = reinterpret_cast<const float4*>(v + base);
+#pragma unroll
+      for (int i = 0; i < HS_PF; ++i) {
+        const long c = tid + (long)i * HS_NT < n4s ? tid + (long)i * HS_NT : n4s - 1;  // (clamped: all in flight)
+        pm[i] = m4[c];
+        pv[i] = v4[c];
+      }
+    }
+    hs_forward(sm, d, ci, acts);  // its barriers publish sm, dz[L-1] and sc
     const float dd = sc;
     for (int l = L - 1; l >= 0; --l) {
       const int din = l == 0 ? E : H;
@@ -402,15 +421,64 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
     }
     __syncthreads();
     const float gs = red[0][0];
+    if (flat) {
+      // one float4 chunk of [emb | mlp0.W | mlp0.b | ...] per step: parameters from LDS, moments from the
+      // registers loaded above; the global arena, the moments and the LDS copy (the next forward) written back
+      float4* m4 = reinterpret_cast<float4*>(m + base);
+      float4* v4 = reinterpret_cast<float4*>(v + base);
+      float4* A4 = reinterpret_cast<float4*>(A + base);
+      float4* s4 = reinterpret_cast<float4*>(sm);
+#pragma unroll
+      for (int i = 0; i < HS_PF; ++i) {
+        const long c = tid + (long)i * HS_NT;
+        if (c >= n4s) continue;
+        const long x = 4 * c;
+        float4 g;
+        if (x < nemb) {  // embedding (zero-gradient rows still move: torch's dense Embedding grad)
+          const int row = (int)(x / E), col = (int)(x - (long)row * E);
+          g = row == ci ? make_float4(gs * gemb[col], gs * gemb[col + 1], gs * gemb[col + 2], gs * gemb[col + 3])
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          int l = 0;
+          long ow = d.w[0] - base, ob = d.b[0] - base;
+#pragma unroll
+          for (int q = 1; q < HS_LMAX; ++q)  // (unrolled: no dynamic index into the by-value descriptor)
+            if (q < L && x >= d.w[q] - base) {
+              l = q;
+              ow = d.w[q] - base;
+              ob = d.b[q] - base;
+            }
+          if (x < ob) {  // W of layer l: row o, columns k..k+3 (din % 4 == 0)
+            const int din = l == 0 ? E : H;
+            const int o = (int)((x - ow) / din), k = (int)(x - ow - (long)o * din);
+            const float go = gs * dz[l][o];
+            g = make_float4(go * acts[l][k], go * acts[l][k + 1], go * acts[l][k + 2], go * acts[l][k + 3]);
+          } else {  // bias of layer l
+            const int o = (int)(x - ob);
+            g = make_float4(gs * dz[l][o], gs * dz[l][o + 1], gs * dz[l][o + 2], gs * dz[l][o + 3]);
+          }
+        }
+        float4 p = s4[c];
+        p.x = hs_adam(p.x, g.x, pm[i].x, pv[i].x, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        p.y = hs_adam(p.y, g.y, pm[i].y, pv[i].y, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        p.z = hs_adam(p.z, g.z, pm[i].z, pv[i].z, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        p.w = hs_adam(p.w, g.w, pm[i].w, pv[i].w, lr_bc1, rsqrt_bc2, b1, b2, eps);
+        m4[c] = pm[i];
+        v4[c] = pv[i];
+        A4[c] = p;
+        s4[c] = p;
+      }
+      __syncthreads();  // the LDS copy updated for the next forward
+    } else {
     // Adam over the embedding table (zero-gradient rows still move: torch's dense Embedding grad)
-    const long nemb = (long)d.n_nodes * E;
     for (long e = tid; e < nemb; e += HS_NT) {
       const int row = (int)(e / E), col = (int)(e - (long)row * E);
       float mm = m[d.emb + e], vv = v[d.emb + e];
-      const float p = hs_adam(A[d.emb + e], row == ci ? gs * gemb[col] : 0.f, mm, vv, lr_bc1, rsqrt_bc2, b1, b2, eps);
+      const float p = hs_adam(sm[e], row == ci ? gs * gemb[col] : 0.f, mm, vv, lr_bc1, rsqrt_bc2, b1, b2, eps);
       m[d.emb + e] = mm;
       v[d.emb + e] = vv;
       A[d.emb + e] = p;
+      sm[e] = p;
     }
     // Adam over the MLP (params from LDS, moments streamed; the LDS copy is updated for the next forward)
     for (int l = 0; l < L; ++l) {
@@ -471,14 +539,15 @@ __global__ void __launch_bounds__(HS_NT) k_hyper_small(float* __restrict__ A, fl
         sm[ob + o] = p;
       }
     }
-    __syncthreads();  // updated embedding (global, this workgroup's writes) and LDS MLP visible
+    __syncthreads();  // updated LDS embedding and MLP visible
+    }
   }
   if (cj >= 0 && upd) {
-    hs_forward(A, sm, d, cj, acts);
+    hs_forward(sm, d, cj, acts);
     if (tid < H) feat_j[tid] = acts[L][tid];
   }
   for (int k = 0; k < ngen; ++k) {
-    hs_forward(A, sm, d, gen.c[k], acts);  // (its first barrier also orders the previous reads of acts)
+    hs_forward(sm, d, gen.c[k], acts);  // (its first barrier also orders the previous reads of acts)
     if (tid < H) gen_feat[(long)k * H + tid] = acts[L][tid];
   }
 }
@@ -767,6 +836,12 @@ void afl_hyper_generate(const float* A, const HySmallDesc& d, long offW, long of
   }
 }
 
+// the flat small-net Adam applies: float4 segments, and the moment chunks fit the per-thread registers
+static bool hs_flat_ok(const HySmallDesc& d, long nsmall) {
+  const long nemb = (long)d.n_nodes * d.E;
+  return ((d.emb | nsmall | nemb | d.E) & 3) == 0 && nsmall / 4 <= (long)HS_PF * HS_NT;
+}
+
 void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const long* urow, const int* clients,
                              int n, const HySmallDesc& d, long offW, long offB, long P, int step0, float lr,
                              float clip, float b1, float b2, float eps, float* delta, float* partial, float* feat,
@@ -780,9 +855,10 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
   const int nb = afl_hyper_nblocks(P);
   float* W = A + offW;
   float* bv = A + offB;
-  const long nmlp = offW - d.w[0];
-  hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, -1, clients[0], feat, info, d,
-                     nmlp, clip, 0.f, 0.f, b1, b2, eps, enable, gl, 0, gen_feat);
+  const long nsmall = offW - d.emb;
+  const auto small = hs_flat_ok(d, nsmall) ? k_hyper_small<true> : k_hyper_small<false>;
+  hipLaunchKernelGGL(small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, -1, clients[0], feat, info, d,
+                     nsmall, clip, 0.f, 0.f, b1, b2, eps, enable, gl, 0, gen_feat);
   const long nW4 = P * H / 4;
   const int nba = (int)min(4096L, (nW4 + 255) / 256);
   // the rows pass of client k + 1 rides in client k's head Adam (k_hyper_adam_rows4) when the heads are
@@ -809,8 +885,8 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
                            H + 1);
     }
     const bool last = k + 1 == n;
-    hipLaunchKernelGGL(k_hyper_small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
-                       last ? -1 : clients[k + 1], fn, info + 2 * k, d, nmlp, clip, lr_bc1, rbc2, b1, b2, eps,
+    hipLaunchKernelGGL(small, dim3(1), dim3(HS_NT), 0, s, A, m, v, partial, nb, clients[k],
+                       last ? -1 : clients[k + 1], fn, info + 2 * k, d, nsmall, clip, lr_bc1, rbc2, b1, b2, eps,
                        enable, gl, last ? ngen : 0, gen_feat);
     if (fused && !last)
       hipLaunchKernelGGL(k_hyper_adam_rows4, dim3(nb), dim3(HR4_NT), 0, s, W, bv, m + offW, v + offW, dk, fk,
@@ -828,16 +904,15 @@ void afl_hyper_server_update(float* A, float* m, float* v, const float* U, const
 
 // MLP features of up to HF_MAXC clients in ONE launch (the START / validation models of a round: one workgroup
 // stages the embedding-MLP parameters once and runs hs_forward per client; was one k_hyper_small per client)
-__global__ void __launch_bounds__(HS_NT) k_hyper_feat_many(const float* __restrict__ A, HySmallDesc d, long nmlp,
+__global__ void __launch_bounds__(HS_NT) k_hyper_feat_many(const float* __restrict__ A, HySmallDesc d, long nsmall,
                                                            HyClients cl, int n, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float sm[HS_SMEM];
   __shared__ float acts[HS_LMAX + 1][HS_HMAX];
   const int tid = threadIdx.x;
-  const long base = d.w[0];
-  hs_stage(sm, A + base, nmlp);
+  hs_stage(sm, A + d.emb, nsmall);
   __syncthreads();
   for (int k = 0; k < n; ++k) {
-    hs_forward(A, sm, d, cl.c[k], acts);  // (its first barrier also orders the previous client's reads of acts)
+    hs_forward(sm, d, cl.c[k], acts);  // (its first barrier also orders the previous client's reads of acts)
     if (tid < d.H) out[(long)k * d.H + tid] = acts[d.L][tid];
     __syncthreads();
   }
@@ -849,7 +924,7 @@ void afl_hyper_features(const float* A, const HySmallDesc& d, long offW, const i
     HyClients cl{};
     const int m = n - k0 < HF_MAXC ? n - k0 : HF_MAXC;
     for (int k = 0; k < m; ++k) cl.c[k] = clients[k0 + k];
-    hipLaunchKernelGGL(k_hyper_feat_many, dim3(1), dim3(HS_NT), 0, s, A, d, offW - d.w[0], cl, m, out + (long)k0 * d.H);
+    hipLaunchKernelGGL(k_hyper_feat_many, dim3(1), dim3(HS_NT), 0, s, A, d, offW - d.emb, cl, m, out + (long)k0 * d.H);
   }
 }
 

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from attackfl_amd.config import from_dict
-from attackfl_amd.fl.engine import FLEngine, build_client_table
+from attackfl_amd.fl.engine import EARLY_AGGREGATORS, FLEngine, build_client_table
 from launch import parse_attackers
 
 pytestmark = pytest.mark.gpu
@@ -156,7 +156,12 @@ def test_deferred_checkpoint_copies_the_submitted_state(gpu, tmp_path):
 @pytest.mark.parametrize("model,attackers,mode", [("TransformerModel", False, "fedavg"),
                                                   ("TransformerModel", True, "fedavg"),
                                                   ("TransformerModel", True, "hyper"), ("RNNModel", True, "hyper"),
-                                                  ("CNNModel", False, "fedavg")])
+                                                  ("CNNModel", False, "fedavg"),
+                                                  ("TransformerModel", True, "krum"),
+                                                  ("TransformerModel", True, "scionfl"),
+                                                  ("TransformerModel", True, "fltracer"),
+                                                  ("TransformerModel", False, "shieldfl"),
+                                                  ("TransformerModel", True, "trimmed_mean")])
 def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode):
     """The next round's training enqueued before this round's validation (engine.speculative) gives the
     same rounds bit for bit as the serial schedule — including a round whose validation fails (the retry
@@ -176,12 +181,12 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
         if attackers:  # client 2 runs Min-Max from its 2nd training round (pool drawn before the launch)
             d["server"]["random-seed"] = 11
         cfg = from_dict(d)
-        atk = "2:Min-Max:2" if mode == "fedavg" else "2:Opt-Fang:2"
+        atk = "2:Opt-Fang:2" if mode == "hyper" else "2:Min-Max:2"
         table = build_client_table(cfg, 1, parse_attackers(atk) if attackers else None)
         eng = FLEngine(cfg, device="cuda", table=table, verbose=False)
         assert eng._speculative == spec
         calls = {"n": 0}
-        name = "test" if mode == "fedavg" else "test_hyper"
+        name = "test_hyper" if mode == "hyper" else "test"
         test = getattr(eng.validation, name)
 
         def flaky(*a):  # the second validation fails once: that round is retried
@@ -191,7 +196,9 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
 
         setattr(eng.validation, name, flaky)
         hist = eng.run()
-        out = (eng.global_params if mode == "fedavg" else eng.hyper.hnet.arena).detach().cpu().clone()
+        out = (eng.hyper.hnet.arena if mode == "hyper" else eng.global_params).detach().cpu().clone()
+        # (the robust rules run in the early launch too: aggregate + next launch before the host wait)
+        assert not spec or mode not in EARLY_AGGREGATORS or any(r.get("path") == "early-launch" for r in hist)
         eng.close()
         return [(r["ok"], None if r["metric"] != r["metric"] else r["metric"]) for r in hist], out
 
@@ -209,9 +216,11 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
 @pytest.mark.parametrize("mode", ["trimmed_mean", "median", "krum", "shieldfl", "scionfl", "gmm", "FLTrust",
                                   "fltracer", "byzantine"])
 @pytest.mark.parametrize("attack", ["Min-Max", "LIE"])
-def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
+def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
     """Every robust server mode on the native path (fused TransformerModel trainer, device aggregators,
-    device validation) with one attacker of 5 from round 2 (reference server.py:286-494)."""
+    device validation) with one attacker of 5 from round 2 (reference server.py:286-494).  The rules in
+    EARLY_AGGREGATORS run inside the early launch from round 2 on (aggregate + next launch before the host wait):
+    the rule itself is captured, on whichever path calls it."""
     d = {
         "server": {"num-round": 3, "clients": 5, "mode": mode, "model": "TransformerModel", "data-name": "ICU",
                    "genuine-rate": 1.0, "data-distribution": {"num-data-range": [300, 500]}},
@@ -225,16 +234,19 @@ def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
     eng = FLEngine(cfg, device="cuda", table=build_client_table(cfg, 1, parse_attackers(spec)), verbose=False)
     assert eng.trainer.kind == "fused"
     # every round's device aggregate against the CPU composite of the same rule on the same gathered rows
+    from attackfl_amd.agg import AGGREGATORS
     seen = []
-    orig = eng._aggregate
+    orig_fn = AGGREGATORS.get(mode)
 
-    def capture(U, sizes, attackers, round_ok):
+    def capture(U, sizes, attackers=None, seed=0, **kw):
         rows = U.detach().cpu().clone()
-        info = orig(U, sizes, attackers, round_ok)
-        seen.append((rows, sizes.clone(), attackers.clone(), eng.global_params.detach().cpu().clone(), eng.round_no))
-        return info
+        res = orig_fn(U, sizes, attackers=attackers, seed=seed, **kw)
+        seen.append((rows, sizes.detach().cpu().clone(), None if attackers is None else attackers.clone(),
+                     res.params.detach().cpu().clone(), seed))
+        return res
 
-    eng._aggregate = capture
+    if orig_fn is not None:
+        monkeypatch.setitem(AGGREGATORS, mode, capture)
     fl_seen = []
     if mode == "FLTrust":  # the rows, g_0 and the server model around every device FLTrust aggregate
         orig_fl = eng._fltrust
@@ -250,7 +262,9 @@ def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
     hist = eng.run()
     eng.close()
     assert [r["ok"] for r in hist] == [True, True, True]
-    assert len(seen) == 3
+    assert len(seen) == (0 if mode == "FLTrust" else 3)
+    if mode in EARLY_AGGREGATORS:
+        assert any(r.get("path") == "early-launch" for r in hist)  # (the last round never launches early)
     if mode == "FLTrust":
         # the trust / rescale math of server.py:714-740 in fp64 on the captured rows and server delta
         assert len(fl_seen) == 3
@@ -265,11 +279,11 @@ def test_robust_modes_end_to_end(gpu, tmp_path, mode, attack):
             assert (out.double() - ref).abs().max().item() <= 2e-5 * max(1.0, ref.abs().max().item())
             assert bool((trust > 0).any())  # (some clients trusted: the check is not vacuous)
     if mode != "FLTrust":  # (FLTrust trains a server model: its composite would need the CPU trainer)
-        from attackfl_amd.agg import AGGREGATORS
-        for rows, sizes, att, got, rnd in seen:
-            ref = AGGREGATORS[mode](rows, sizes, attackers=att, seed=eng.seed * 13 + rnd).params
+        for k, (rows, sizes, att, got, seed) in enumerate(seen):
+            assert seed == eng.seed * 13 + k + 1
+            ref = orig_fn(rows, sizes, attackers=att, seed=seed).params
             tol = 1e-6 if mode in ("median", "trimmed_mean", "krum") else 2e-5
-            assert (got - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (mode, rnd)
+            assert (got - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (mode, k)
     assert all(0.0 <= r["metric"] <= 1.0 for r in hist)
     assert "attack" in hist[1] and "attack" in hist[2]
     if mode == "FLTrust":
