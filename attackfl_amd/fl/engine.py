@@ -52,7 +52,8 @@ from .trainers import Plan, make_plan, make_trainer
 
 # rules that run on the device without a host read: with one of them the aggregate and the next round's launch
 # are enqueued before the host waits for the training, as for FedAvg (FLEngine._early_launch); gmm reads one
-# byte (its success), FLTrust trains a server model first
+# byte (its success) and stays on the ordinary path; FLTrust (server-model training + trust weights, device work
+# too) takes the early launch through its own branch
 EARLY_AGGREGATORS = ("trimmed_mean", "median", "krum", "shieldfl", "scionfl", "fltracer", "byzantine")
 
 META = 5  # valid, result, size, is_attacker, decision word; then the client's per-epoch losses (E columns)
@@ -844,7 +845,15 @@ class FLEngine:
         params = g0.clone()[None]
         # kept and read at the round's host synchronisation (_finish_round): a NaN result is ignored like the
         # reference's train_on_device return value, a cross-workgroup timeout still raises
-        self._fl_pending = trainer.launch(params, plan, self.cfg.lr, 100, [self.seed + self.round_no])
+        seed = self.seed + self.round_no
+        ds = getattr(trainer, "device_seed", None)
+        seeds_dev = None
+        if ds is not None and self.device.type == "cuda":
+            # a pinned, non-blocking upload: the trainer's own upload of a host list is a pageable copy, which
+            # waits for the clients' training (the early launch enqueues this before that ends)
+            from ..ops.layers import upload
+            seeds_dev = upload(torch.tensor([ds(seed)], dtype=torch.int32), self.device)
+        self._fl_pending = trainer.launch(params, plan, self.cfg.lr, 100, [seed], seeds_dev=seeds_dev)
         server_new = params[0]
         g0_delta = server_new - g0
         if compat and self.global_params is None:
@@ -1063,7 +1072,7 @@ class FLEngine:
         if self.mode == "hyper":
             mode_ok = self.device.type == "cuda" and self.hyper._native_ok()
         else:
-            mode_ok = ((self.mode == "fedavg" or self.mode in EARLY_AGGREGATORS) and not self.fast_fedavg
+            mode_ok = ((self.mode in ("fedavg", "FLTrust") or self.mode in EARLY_AGGREGATORS) and not self.fast_fedavg
                        and self.global_params is not None
                        and not self.cfg.engine.get("compat-fedavg-alias", False))
         return self._speculative and mode_ok and self.rounds_left > 1 and not last
@@ -1099,7 +1108,7 @@ class FLEngine:
             sizes = s
         snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
                 self.server_rng.getstate(), self.genuine_pool)
-        g_old, hyper_step = self.global_params, None
+        g_old, hyper_step, fl_old = self.global_params, None, None
         if self.mode == "hyper":  # the update runs, or leaves the hypernetwork untouched, as the device decides
             hyper_step = self.hyper.step
             self.ckpt_writer.fence()  # the previous round's checkpoint copy of the arena, updated in place below
@@ -1108,6 +1117,11 @@ class FLEngine:
                              enable=ok_all.to(torch.int32).reshape(1),
                              gen_key=[i for _, i, _, _ in nxt["clients"]] if nxt and nxt.get("clients") else None)
             g = g_old
+        elif self.mode == "FLTrust":
+            # the server model's training and the trust-weighted sum, all enqueued on the device (_fltrust); the
+            # server model and the trust scores are rolled back if a client failed (_early_launch_failed)
+            fl_old = self.fltrust_model
+            g = torch.where(ok_all, self._fltrust(U), g_old)
         elif self.mode != "fedavg":
             # a robust rule, all on the device (no host read): its result kept only when every client succeeded
             res = AGGREGATORS[self.mode](U, sizes, attackers=None, seed=self.seed * 13 + self.round_no,
@@ -1133,19 +1147,25 @@ class FLEngine:
         prep = self._next_prep  # (staged ahead: the snapshot above already includes its draws)
         self._spec = self._launch_local(self._genuine_for_attackers())
         return {"g_old": g_old, "snap": snap, "keep": keep, "pool": self.genuine_pool, "agg_done": agg_done,
-                "prep": prep, "hyper_step": hyper_step}
+                "prep": prep, "hyper_step": hyper_step, "fl_old": fl_old}
 
     def _early_info(self, round_ok: bool) -> dict:
         if not round_ok:
             return {}
         if self.mode == "hyper":
             return {"path": "early-launch", "_lazy": lambda: self.hyper.last_info}  # (as _aggregate)
+        if self.mode == "FLTrust":
+            return {"path": "early-launch"}  # (the trust scores join the record in _finish_round, as ever)
         if self.mode != "fedavg":
             return {**self._early_agg_info, "path": "early-launch"}
         return {"n": len(self.selected), "path": "early-launch"}
 
     def _early_launch_failed(self, esl: dict, results: np.ndarray) -> None:
         self.global_params = esl["g_old"]  # (the device selected the same values: the launch's START)
+        if esl.get("fl_old") is not None:  # FLTrust: no server-model step and no trust scores for a failed round
+            self.fltrust_model = esl["fl_old"]
+            self._trust = None
+            self._fl_pending = None
         if esl["hyper_step"] is not None:  # the device skipped the hypernetwork update: its step count too
             self.hyper.step = esl["hyper_step"]
             self.hyper._info_dev = None

@@ -161,7 +161,8 @@ def test_deferred_checkpoint_copies_the_submitted_state(gpu, tmp_path):
                                                   ("TransformerModel", True, "scionfl"),
                                                   ("TransformerModel", True, "fltracer"),
                                                   ("TransformerModel", False, "shieldfl"),
-                                                  ("TransformerModel", True, "trimmed_mean")])
+                                                  ("TransformerModel", True, "trimmed_mean"),
+                                                  ("TransformerModel", True, "FLTrust")])
 def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode):
     """The next round's training enqueued before this round's validation (engine.speculative) gives the
     same rounds bit for bit as the serial schedule — including a round whose validation fails (the retry
@@ -198,7 +199,8 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
         hist = eng.run()
         out = (eng.hyper.hnet.arena if mode == "hyper" else eng.global_params).detach().cpu().clone()
         # (the robust rules run in the early launch too: aggregate + next launch before the host wait)
-        assert not spec or mode not in EARLY_AGGREGATORS or any(r.get("path") == "early-launch" for r in hist)
+        assert not spec or mode not in EARLY_AGGREGATORS + ("FLTrust",) or \
+            any(r.get("path") == "early-launch" for r in hist)
         eng.close()
         return [(r["ok"], None if r["metric"] != r["metric"] else r["metric"]) for r in hist], out
 
@@ -263,7 +265,7 @@ def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
     eng.close()
     assert [r["ok"] for r in hist] == [True, True, True]
     assert len(seen) == (0 if mode == "FLTrust" else 3)
-    if mode in EARLY_AGGREGATORS:
+    if mode in EARLY_AGGREGATORS + ("FLTrust",):
         assert any(r.get("path") == "early-launch" for r in hist)  # (the last round never launches early)
     if mode == "FLTrust":
         # the trust / rescale math of server.py:714-740 in fp64 on the captured rows and server delta
