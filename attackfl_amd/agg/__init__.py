@@ -312,6 +312,20 @@ def gmm(U: torch.Tensor, sizes=None, attackers: Optional[torch.Tensor] = None, s
                      {"kept": np.nonzero(keep)[0].tolist(), "threshold": float(thr)})
 
 
+def gmm_early(U: torch.Tensor, attackers: torch.Tensor, gmm_rank: Optional[int] = None):
+    """``gmm`` without its host read, for the engine's early launch (device U, n <= 64): (mean of the kept
+    rows, device bool "some row kept" = the rule's success, info).  ``attackers``: bool, host or device (a host
+    tensor goes up pinned, never through a pageable copy that would wait for the stream)."""
+    from ..ops.layers import upload
+
+    att = attackers.to(torch.uint8)
+    att = upload(att, U.device) if att.device.type == "cpu" else att
+    G = _centred_gram(U)
+    keep_d, inf_d = ops.native().gmm_filter(G.contiguous(), att.contiguous(), int(gmm_rank or 0))
+    keep = keep_d.bool()
+    return _masked_mean(U, keep), inf_d[1] > 0, {"kept": keep, "threshold": inf_d[0]}
+
+
 def scionfl(U: torch.Tensor, sizes: torch.Tensor, seed: int = 0, **_) -> AggResult:
     """All on the device: quantisation, L2-from-counts, the 3x-mean clip, the cosine-distance threshold
     (the int(0.5 n)-th largest score) and the size-weighted FedAvg of the kept originals."""

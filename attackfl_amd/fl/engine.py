@@ -35,7 +35,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..agg import AGGREGATORS, AggResult
+from ..agg import AGGREGATORS, AggResult, gmm_early
 from ..agg import host_info as agg_host_info
 from ..attacks import DistanceEngine, host_info, run_attack
 from ..config import AttackSpec, Config
@@ -51,9 +51,9 @@ from .hyper_server import HyperServer
 from .trainers import Plan, make_plan, make_trainer
 
 # rules that run on the device without a host read: with one of them the aggregate and the next round's launch
-# are enqueued before the host waits for the training, as for FedAvg (FLEngine._early_launch); gmm reads one
-# byte (its success) and stays on the ordinary path; FLTrust (server-model training + trust weights, device work
-# too) takes the early launch through its own branch
+# are enqueued before the host waits for the training, as for FedAvg (FLEngine._early_launch).  gmm (whose
+# success the host reads after its wait, from a copy queued before the next launch) and FLTrust (server-model
+# training + trust weights, device work too) take the early launch through branches of their own
 EARLY_AGGREGATORS = ("trimmed_mean", "median", "krum", "shieldfl", "scionfl", "fltracer", "byzantine")
 
 META = 5  # valid, result, size, is_attacker, decision word; then the client's per-epoch losses (E columns)
@@ -269,6 +269,7 @@ class FLEngine:
         self._next_prep = None  # the next launch's host half, staged while the current training runs
         self._fedavg_w = None
         self._early_agg_info: dict = {}  # a robust rule's info of the last early launch (_early_info)
+        self._early_agg_ok = None  # gmm: (pinned bool, event) of the early launch's filter success
         self._val_stream = None
         self._start_ready = None
         self._sel_cache = None
@@ -912,6 +913,9 @@ class FLEngine:
             results = meta.numpy()[:, 1] > 0.5
             round_ok = bool(results.all())
             info = self._early_info(round_ok)
+            if not self._early_agg_done() and round_ok:
+                round_ok = False
+                info = {**self._early_agg_info, "agg_failed": True}
             if not round_ok:
                 self._early_launch_failed(esl, results)
             t2 = t3 = time.perf_counter()
@@ -966,6 +970,9 @@ class FLEngine:
                 else None
             if esl is not None:  # (several ranks: the aggregate and the next launch are in already)
                 info = self._early_info(round_ok)
+                if not self._early_agg_done() and round_ok:
+                    round_ok = False
+                    info = {**self._early_agg_info, "agg_failed": True}
                 if not round_ok:
                     self._early_launch_failed(esl, results)
             else:
@@ -1072,7 +1079,8 @@ class FLEngine:
         if self.mode == "hyper":
             mode_ok = self.device.type == "cuda" and self.hyper._native_ok()
         else:
-            mode_ok = ((self.mode in ("fedavg", "FLTrust") or self.mode in EARLY_AGGREGATORS) and not self.fast_fedavg
+            mode_ok = ((self.mode in ("fedavg", "FLTrust", "gmm") or self.mode in EARLY_AGGREGATORS)
+                       and not (self.mode == "gmm" and len(self.selected) > 64) and not self.fast_fedavg
                        and self.global_params is not None
                        and not self.cfg.engine.get("compat-fedavg-alias", False))
         return self._speculative and mode_ok and self.rounds_left > 1 and not last
@@ -1099,6 +1107,7 @@ class FLEngine:
             ok_all = None if self.mode == "fedavg" else (ok_n > 0).all()  # (FedAvg: decided inside the aggregate)
             w = st["fedavg_w"]
             sizes = st["sizes_h"]
+            attackers = torch.from_numpy(st["meta"][self._local_rows(), 3] > 0.5)
         else:  # several ranks: called on the gathered rows (device), before the host reads their meta
             P = self.P
             ok_n = None
@@ -1106,6 +1115,7 @@ class FLEngine:
             s = sel[:, P + 2].double()
             w = s / s.sum()
             sizes = s
+            attackers = sel[:, P + 3] > 0.5
         snap = ([(lc.rng.getstate(), lc.training_round, lc.genuine) for lc in self.local],
                 self.server_rng.getstate(), self.genuine_pool)
         g_old, hyper_step, fl_old = self.global_params, None, None
@@ -1117,6 +1127,16 @@ class FLEngine:
                              enable=ok_all.to(torch.int32).reshape(1),
                              gen_key=[i for _, i, _, _ in nxt["clients"]] if nxt and nxt.get("clients") else None)
             g = g_old
+        elif self.mode == "gmm":
+            # the filter's success (some row kept) joins the clients' on the device; the host reads it after
+            # its wait from a pinned copy queued BEFORE the next launch (run_round)
+            params, ok_agg, self._early_agg_info = gmm_early(U, attackers, int(self.cfg.engine.get("gmm-rank", 1)))
+            g = torch.where(ok_all & ok_agg, params, g_old)
+            okh = torch.empty(1, dtype=torch.bool, pin_memory=True)
+            okh.copy_(ok_agg.reshape(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._early_agg_ok = (okh, ev)
         elif self.mode == "FLTrust":
             # the server model's training and the trust-weighted sum, all enqueued on the device (_fltrust); the
             # server model and the trust scores are rolled back if a client failed (_early_launch_failed)
@@ -1160,6 +1180,15 @@ class FLEngine:
             return {**self._early_agg_info, "path": "early-launch"}
         return {"n": len(self.selected), "path": "early-launch"}
 
+    def _early_agg_done(self) -> bool:
+        """gmm's filter success of the early launch (True for every other rule): its pinned copy was queued before
+        the next launch, so this waits for the filter only, not for the training queued behind it."""
+        ok, self._early_agg_ok = self._early_agg_ok, None
+        if ok is None:
+            return True
+        ok[1].synchronize()
+        return bool(ok[0][0])
+
     def _early_launch_failed(self, esl: dict, results: np.ndarray) -> None:
         self.global_params = esl["g_old"]  # (the device selected the same values: the launch's START)
         if esl.get("fl_old") is not None:  # FLTrust: no server-model step and no trust scores for a failed round
@@ -1172,7 +1201,8 @@ class FLEngine:
         if esl["keep"] is None:
             return  # no attackers: the launch in flight is this round's retry
         # attackers sample the stored prefix's genuine rows: discard the launch, restore what it consumed
-        stored = int(np.nonzero(~results)[0][0])
+        # (every row is stored when only the aggregate failed: gmm kept no row)
+        stored = int(np.nonzero(~results)[0][0]) if not results.all() else len(results)
         pos = [esl["keep"].index(k) for k in range(stored) if k in esl["keep"]]
         pool = esl["pool"][pos] if pos else None
         states, srng, _ = esl["snap"]

@@ -162,7 +162,8 @@ def test_deferred_checkpoint_copies_the_submitted_state(gpu, tmp_path):
                                                   ("TransformerModel", True, "fltracer"),
                                                   ("TransformerModel", False, "shieldfl"),
                                                   ("TransformerModel", True, "trimmed_mean"),
-                                                  ("TransformerModel", True, "FLTrust")])
+                                                  ("TransformerModel", True, "FLTrust"),
+                                                  ("TransformerModel", True, "gmm")])
 def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode):
     """The next round's training enqueued before this round's validation (engine.speculative) gives the
     same rounds bit for bit as the serial schedule — including a round whose validation fails (the retry
@@ -199,7 +200,7 @@ def test_speculative_launch_matches_serial(gpu, tmp_path, model, attackers, mode
         hist = eng.run()
         out = (eng.hyper.hnet.arena if mode == "hyper" else eng.global_params).detach().cpu().clone()
         # (the robust rules run in the early launch too: aggregate + next launch before the host wait)
-        assert not spec or mode not in EARLY_AGGREGATORS + ("FLTrust",) or \
+        assert not spec or mode not in EARLY_AGGREGATORS + ("FLTrust", "gmm") or \
             any(r.get("path") == "early-launch" for r in hist)
         eng.close()
         return [(r["ok"], None if r["metric"] != r["metric"] else r["metric"]) for r in hist], out
@@ -249,6 +250,18 @@ def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
 
     if orig_fn is not None:
         monkeypatch.setitem(AGGREGATORS, mode, capture)
+    if mode == "gmm":  # (the early launch calls the filter without its host read)
+        import attackfl_amd.fl.engine as engine_mod
+        orig_early = engine_mod.gmm_early
+
+        def capture_early(U, attackers, gmm_rank=None):
+            rows = U.detach().cpu().clone()
+            params, ok, info = orig_early(U, attackers, gmm_rank)
+            seen.append((rows, torch.ones(U.shape[0]), attackers.detach().cpu().clone(), params.detach().cpu().clone(),
+                         eng.seed * 13 + len(seen) + 1))
+            return params, ok, info
+
+        monkeypatch.setattr(engine_mod, "gmm_early", capture_early)
     fl_seen = []
     if mode == "FLTrust":  # the rows, g_0 and the server model around every device FLTrust aggregate
         orig_fl = eng._fltrust
@@ -265,7 +278,7 @@ def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
     eng.close()
     assert [r["ok"] for r in hist] == [True, True, True]
     assert len(seen) == (0 if mode == "FLTrust" else 3)
-    if mode in EARLY_AGGREGATORS + ("FLTrust",):
+    if mode in EARLY_AGGREGATORS + ("FLTrust", "gmm"):
         assert any(r.get("path") == "early-launch" for r in hist)  # (the last round never launches early)
     if mode == "FLTrust":
         # the trust / rescale math of server.py:714-740 in fp64 on the captured rows and server delta
@@ -283,7 +296,7 @@ def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
     if mode != "FLTrust":  # (FLTrust trains a server model: its composite would need the CPU trainer)
         for k, (rows, sizes, att, got, seed) in enumerate(seen):
             assert seed == eng.seed * 13 + k + 1
-            ref = orig_fn(rows, sizes, attackers=att, seed=seed).params
+            ref = orig_fn(rows, sizes, attackers=att, seed=seed, gmm_rank=1).params
             tol = 1e-6 if mode in ("median", "trimmed_mean", "krum") else 2e-5
             assert (got - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (mode, k)
     assert all(0.0 <= r["metric"] <= 1.0 for r in hist)
