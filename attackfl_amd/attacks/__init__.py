@@ -218,7 +218,7 @@ def _bisect_fused(cd: "_CandidateDistances", threshold: torch.Tensor, kind: str,
         vA, vB, vC = (cd.A, cd.B, cd.C) if cd.vec else (None, None, None)
     vA, vB, vC = [None if t is None else t.to(torch.float64).contiguous() for t in (vA, vB, vC)]
     st = torch.zeros(40, dtype=torch.float64, device=dev)
-    st[0] = float(gamma)
+    st[:1].fill_(float(gamma))  # (st[0] = x is a pageable scalar copy: a host wait for the side stream)
     thr = threshold.to(device=dev, dtype=torch.float64).reshape(1)
     k = 1 if kind == "sum" else 0
     nat = ops.native()

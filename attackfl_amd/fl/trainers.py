@@ -286,6 +286,9 @@ class EagerTrainer:
         return True
 
 
+_RB_STREAMS: dict = {}  # device -> the shared read-back stream (FusedTrainer._readback)
+
+
 def _nd(plan: Plan):
     return plan.nd_dev if plan.nd_dev is not None else plan.nd
 
@@ -367,9 +370,13 @@ class FusedTrainer:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         side = 3 * ok.shape[0] * 2 <= cus
         if side:
-            rs = getattr(self, "_rb_stream", None)
+            # ONE read-back stream per device for every trainer (FLTrust's server-model trainer too): a stream
+            # waiting for a training blocks the hardware queue it is mapped to (GPU_MAX_HW_QUEUES = 4), and one
+            # more stream moved the attack's side stream onto that queue, behind the wait (FLTrust + Min-Max: the
+            # attack math started only after the clients' training, -10 %)
+            rs = _RB_STREAMS.get(dev)
             if rs is None:
-                rs = self._rb_stream = torch.cuda.Stream(device=dev)
+                rs = _RB_STREAMS[dev] = torch.cuda.Stream(device=dev)
             trained = torch.cuda.Event()
             trained.record(main)
             rs.wait_event(trained)
