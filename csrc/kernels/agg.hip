@@ -754,43 +754,90 @@ int afl_gmm_filter(const double* G, int n, const unsigned char* att, unsigned ch
 
 // ============================================================================ top_pc
 // First principal-component scores of n <= 64 rows from their centred Gram G = Xc Xc^T (fp64 [n][n]), the
-// FLTracer PCA(1) (reference src/Utils.py:359-369): cyclic Jacobi eigen-decomposition with a fixed sweep count,
-// one wave, lane k applying each rotation to row / column k (the rotations themselves are sequential);
-// z = v_max sqrt(lambda_max).  (Repeated squaring of G, the previous form, let the second eigenvector leak in
-// at (lambda_2 / lambda_1)^(2^squarings): 2 % at a 0.999 ratio, 66 % at 0.9999 — nearly iid updates.)
+// FLTracer PCA(1) (reference src/Utils.py:359-369): Jacobi eigen-decomposition on one wave (at most ``sweeps``
+// sweeps, fewer once the off-diagonal mass is at fp64 rounding); z = v_max sqrt(lambda_max).  Parallel (round-robin) ordering: each step rotates m / 2 DISJOINT pairs at
+// once (m = n rounded up to even; m - 1 steps cover every pair once per sweep), their (c, s) computed by one lane
+// each, then one lane per (pair, row / column) applies them — 7 dependent steps per sweep at n = 8 instead of 28
+// sequential rotations (the rotation's fp64 divide / square-root chain and three barriers were the kernel's whole
+// time: 158 us per call).  (Repeated squaring of G, the round-4 form, let the second eigenvector leak in at
+// (lambda_2 / lambda_1)^(2^squarings): 2 % at a 0.999 ratio, 66 % at 0.9999 — nearly iid updates.)
 __global__ void __launch_bounds__(64) k_top_pc(const double* __restrict__ G, int n, int sweeps, double* __restrict__ z) {
   __shared__ double A[GMM_MAXN * GMM_MAXN], V[GMM_MAXN * GMM_MAXN];
+  __shared__ double cs_c[GMM_MAXN / 2], cs_s[GMM_MAXN / 2];
+  __shared__ int cs_p[GMM_MAXN / 2], cs_q[GMM_MAXN / 2];
   const int k = threadIdx.x;
   for (int e = k; e < n * n; e += blockDim.x) {
     A[e] = G[e];
     V[e] = (e / n == e % n) ? 1.0 : 0.0;
   }
+  const int m = n + (n & 1);  // (an odd n pairs one index with the dummy index n each step: skipped)
+  const int half = m / 2;
   __syncthreads();
-  for (int sweep = 0; sweep < sweeps; ++sweep)
-    for (int p = 0; p < n - 1; ++p)
-      for (int q = p + 1; q < n; ++q) {
-        const double apq = A[p * n + q];
-        if (fabs(apq) < 1e-300) continue;  // (uniform: every lane read the same word)
-        const double th = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
-        const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
-        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-        __syncthreads();
-        if (k < n) {  // columns p, q
-          const double akp = A[k * n + p], akq = A[k * n + q];
-          A[k * n + p] = c * akp - s * akq;
-          A[k * n + q] = s * akp + c * akq;
-          const double vkp = V[k * n + p], vkq = V[k * n + q];
-          V[k * n + p] = c * vkp - s * vkq;
-          V[k * n + q] = s * vkp + c * vkq;
-        }
-        __syncthreads();
-        if (k < n) {  // rows p, q
-          const double apk = A[p * n + k], aqk = A[q * n + k];
-          A[p * n + k] = c * apk - s * aqk;
-          A[q * n + k] = s * apk + c * aqk;
-        }
-        __syncthreads();
+  for (int sweep = 0; sweep < sweeps; ++sweep) {
+    {  // converged to fp64 precision (off-diagonal mass <= 1e-32 of the diagonal's): the remaining rotations
+       // would be identities up to rounding, so the sweep count is an upper bound (uniform decision)
+      double off = 0.0, dia = 0.0;
+      if (k < n) {
+        dia = A[k * n + k] * A[k * n + k];
+        for (int j = k + 1; j < n; ++j) off += A[k * n + j] * A[k * n + j];
       }
+      for (int o = 32; o > 0; o >>= 1) {
+        off += __shfl_xor(off, o, 64);
+        dia += __shfl_xor(dia, o, 64);
+      }
+      if (off <= 1e-32 * dia) break;
+    }
+    for (int r = 0; r < m - 1; ++r) {
+      if (k < half) {  // pair k of step r: (r, m - 1) and ((r + k) % (m - 1), (r - k + m - 1) % (m - 1))
+        int p = k == 0 ? r : (r + k) % (m - 1);
+        int q = k == 0 ? m - 1 : (r - k + m - 1) % (m - 1);
+        if (p > q) {
+          const int t = p;
+          p = q;
+          q = t;
+        }
+        double c = 1.0, sn = 0.0;
+        if (q < n) {
+          const double apq = A[p * n + q];
+          if (fabs(apq) >= 1e-300) {
+            const double th = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+            c = 1.0 / sqrt(t * t + 1.0);
+            sn = t * c;
+          }
+        }
+        cs_p[k] = p;
+        cs_q[k] = q < n ? q : p;  // (identity on the dummy pair: c = 1, s = 0 on column p alone)
+        cs_c[k] = c;
+        cs_s[k] = sn;
+      }
+      __syncthreads();
+      // one lane per (pair t, row / column i): every pair's rotation applied at once (disjoint pairs)
+      for (int e = k; e < half * n; e += 64) {  // columns p, q
+        const int t = e / n, i = e - t * n;
+        const int p = cs_p[t], q = cs_q[t];
+        if (p == q) continue;
+        const double c = cs_c[t], sn = cs_s[t];
+        const double aip = A[i * n + p], aiq = A[i * n + q];
+        const double vip = V[i * n + p], viq = V[i * n + q];
+        A[i * n + p] = c * aip - sn * aiq;
+        A[i * n + q] = sn * aip + c * aiq;
+        V[i * n + p] = c * vip - sn * viq;
+        V[i * n + q] = sn * vip + c * viq;
+      }
+      __syncthreads();
+      for (int e = k; e < half * n; e += 64) {  // rows p, q
+        const int t = e / n, i = e - t * n;
+        const int p = cs_p[t], q = cs_q[t];
+        if (p == q) continue;
+        const double c = cs_c[t], sn = cs_s[t];
+        const double api = A[p * n + i], aqi = A[q * n + i];
+        A[p * n + i] = c * api - sn * aqi;
+        A[q * n + i] = sn * api + c * aqi;
+      }
+      __syncthreads();
+    }
+  }
   int top = 0;
   for (int i = 1; i < n; ++i)
     if (A[i * n + i] > A[top * n + top]) top = i;
