@@ -368,8 +368,9 @@ std::vector<torch::Tensor> stoch_quant(torch::Tensor U, int64_t seed) {
   auto sigma = torch::empty_like(U);
   auto smin = torch::empty({N}, U.options());
   auto smax = torch::empty({N}, U.options());
+  auto ws = torch::empty({afl_stoch_quant_ws(N)}, U.options());
   afl_stoch_quant(U.data_ptr<float>(), N, P, (uint64_t)seed, sigma.data_ptr<float>(), smin.data_ptr<float>(),
-                  smax.data_ptr<float>(), cur());
+                  smax.data_ptr<float>(), ws.data_ptr<float>(), cur());
   AFL_CHECK_LAUNCH();
   return {sigma, smin, smax};
 }

@@ -17,8 +17,9 @@ void afl_coord_select(const float* U, int N, long P, int mode, int trim, float* 
 int afl_row_dots_nchunks(long P);
 void afl_row_dots(const float* U, const float* ref, int N, long P, int mode, double* partial, double* out,
                   hipStream_t s);
+long afl_stoch_quant_ws(int N);  // floats of workspace afl_stoch_quant needs
 void afl_stoch_quant(const float* U, int N, long P, uint64_t seed, float* sigma, float* smin, float* smax,
-                     hipStream_t s);
+                     float* ws, hipStream_t s);
 void afl_adam_flat(float* p, const float* g, float* m, float* v, long n, int step, float lr, float b1, float b2,
                    float eps, float gscale, hipStream_t s);
 

@@ -417,52 +417,94 @@ void afl_row_dots(const float* U, const float* ref, int N, long P, int mode, dou
 }
 
 // ============================================================================ ScionFL quantisation
-__global__ void __launch_bounds__(256) k_row_minmax(const float* __restrict__ U, long P, float* __restrict__ smin,
-                                                    float* __restrict__ smax) {
+// Row min / max over SQ_NB chunks per row (one workgroup per row kept 8 CUs busy for 49 us at 8 x 47.7 k), the
+// chunk partials reduced by the quantisation kernel's blocks themselves (min / max: any order gives the same
+// values, so the bits are those of the one-pass form).
+constexpr int SQ_NB = 32;
+__global__ void __launch_bounds__(256) k_row_minmax(const float* __restrict__ U, long P, float* __restrict__ part) {
   __shared__ float smn[4], smx[4];
-  const float* u = U + (long)blockIdx.x * P;
+  const int r = blockIdx.y, b = blockIdx.x;
+  const long c0 = P * b / SQ_NB, c1 = P * (b + 1) / SQ_NB;
+  const float* u = U + (long)r * P;
   float mn = __int_as_float(0x7f800000), mx = -mn;
-  for (long c = threadIdx.x; c < P; c += blockDim.x) {
-    float a = u[c];
+  for (long c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+    const float a = u[c];
     mn = fminf(mn, a);
     mx = fmaxf(mx, a);
   }
   mn = wave_min(mn);
   mx = wave_max(mx);
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
     smn[w] = mn;
     smx[w] = mx;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+    for (int i = 1; i < 4; ++i) {
       mn = fminf(mn, smn[i]);
       mx = fmaxf(mx, smx[i]);
     }
-    mn = fminf(mn, smn[0]);
-    mx = fmaxf(mx, smx[0]);
-    smin[blockIdx.x] = mn;
-    smax[blockIdx.x] = mx;
+    part[((long)r * SQ_NB + b) * 2] = mn;
+    part[((long)r * SQ_NB + b) * 2 + 1] = mx;
   }
 }
 
 __global__ void __launch_bounds__(256) k_stoch_quant(const float* __restrict__ U, long P, long total,
-                                                     const float* __restrict__ smin, const float* __restrict__ smax,
-                                                     uint64_t seed, float* __restrict__ sigma) {
-  long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+                                                     const float* __restrict__ part, float* __restrict__ smin,
+                                                     float* __restrict__ smax, uint64_t seed,
+                                                     float* __restrict__ sigma) {
+  __shared__ float lo_s[2], hi_s[2];
+  const long id0 = (long)blockIdx.x * blockDim.x;
+  const long r0 = id0 / P;  // a block spans at most two rows (P >= 256) or several (P < 256: handled per row)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w < 2) {  // wave w reduces the partials of row r0 + w
+    const long r = r0 + w;
+    const long nrows = total / P;
+    float mn = __int_as_float(0x7f800000), mx = -mn;
+    if (r < nrows && lane < SQ_NB) {
+      mn = part[(r * SQ_NB + lane) * 2];
+      mx = part[(r * SQ_NB + lane) * 2 + 1];
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) {
+      lo_s[w] = mn;
+      hi_s[w] = mx;
+    }
+  }
+  __syncthreads();
+  const long id = id0 + threadIdx.x;
   if (id >= total) return;
-  long r = id / P;
-  float lo = smin[r], hi = smax[r];
-  float p = (U[id] - lo) / (hi - lo + 1e-6f);
+  const long r = id / P;
+  float lo, hi;
+  if (r - r0 < 2) {
+    lo = lo_s[r - r0];
+    hi = hi_s[r - r0];
+  } else {  // (rows shorter than a block: reduce this row's partials directly)
+    lo = __int_as_float(0x7f800000);
+    hi = -lo;
+    for (int b = 0; b < SQ_NB; ++b) {
+      lo = fminf(lo, part[(r * SQ_NB + b) * 2]);
+      hi = fmaxf(hi, part[(r * SQ_NB + b) * 2 + 1]);
+    }
+  }
+  if (id == r * P) {  // the row's first element publishes its min / max
+    smin[r] = lo;
+    smax[r] = hi;
+  }
+  const float p = (U[id] - lo) / (hi - lo + 1e-6f);
   sigma[id] = afl_uniform(seed, (uint64_t)id) < p ? 1.f : 0.f;
 }
 
+long afl_stoch_quant_ws(int N) { return (long)N * SQ_NB * 2; }
+
 void afl_stoch_quant(const float* U, int N, long P, uint64_t seed, float* sigma, float* smin, float* smax,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(k_row_minmax, dim3(N), dim3(256), 0, s, U, P, smin, smax);
-  long total = (long)N * P;
-  hipLaunchKernelGGL(k_stoch_quant, dim3(afl_cdiv(total, 256)), dim3(256), 0, s, U, P, total, smin, smax, seed, sigma);
+                     float* ws, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_minmax, dim3(SQ_NB, N), dim3(256), 0, s, U, P, ws);
+  const long total = (long)N * P;
+  hipLaunchKernelGGL(k_stoch_quant, dim3(afl_cdiv(total, 256)), dim3(256), 0, s, U, P, total, ws, smin, smax, seed,
+                     sigma);
 }
 
 // ============================================================================ Adam (flat)

@@ -306,12 +306,15 @@ def test_robust_modes_end_to_end(gpu, tmp_path, monkeypatch, mode, attack):
     assert os.path.exists(os.path.join(tmp_path, "TransformerModel.pth"))
 
 
-def test_stoch_quant_matches_cpu_mirror(gpu):
-    """k_stoch_quant's Bernoulli draws are the counter-based afl_uniform the CPU composite mirrors bit for bit."""
+@pytest.mark.parametrize("shape", [(6, 5000), (8, 47693), (37, 100), (3, 7), (5, 257)])
+def test_stoch_quant_matches_cpu_mirror(gpu, shape):
+    """k_stoch_quant's Bernoulli draws are the counter-based afl_uniform the CPU composite mirrors bit for bit;
+    the chunked row min / max (32 partials per row, reduced by the quantisation blocks) at row lengths above and
+    below one block, and at a block straddling rows."""
     from attackfl_amd import ops
     from attackfl_amd.ops import composite as C
 
-    U = torch.randn(6, 5000, generator=torch.Generator().manual_seed(0))
+    U = torch.randn(*shape, generator=torch.Generator().manual_seed(0))
     s_d, lo_d, hi_d = ops.stochastic_quantize(U.to(gpu), 1234)
     s_c, lo_c, hi_c = C.stochastic_quantize(U, 1234)
     assert torch.equal(lo_d.cpu(), lo_c) and torch.equal(hi_d.cpu(), hi_c)
