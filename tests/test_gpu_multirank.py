@@ -38,6 +38,11 @@ CASES = {
     # the on-chip CNN trainer needs all 32 workgroups of a client co-resident: ranks sharing the GPU size their
     # launches to CUs / sharers (parallel.launcher.gpu_sharers) instead of spinning on absent workgroups
     "cnn-fedavg": ("CNNModel", "fedavg", {}),
+    # robust rules in the early launch at world > 1 (device sizes / attacker flags from the gathered meta):
+    # a plain device rule, gmm (filter success read after the wait) and FLTrust (replicated server-model step)
+    "tf-krum-minmax": ("TransformerModel", "krum", {5: {"mode": "Min-Max", "round": 2}}),
+    "tf-gmm-minmax": ("TransformerModel", "gmm", {5: {"mode": "Min-Max", "round": 2}}),
+    "tf-fltrust-minmax": ("TransformerModel", "FLTrust", {5: {"mode": "Min-Max", "round": 2}}),
 }
 
 
